@@ -1,0 +1,383 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of the reference's render-and-optimise hot path:
+  octree export → ray/octree intersection → sort/trim → inverse-CDF sampling
+  → trilinear interpolation → NRGBD decoder → SDF-weight compositing →
+  Criterion loss → (torch-CPU autograd) backward.
+
+Kernels come from svo_oracle.c (ctypes); the host-side logic is restated in
+torch-CPU fp32 here, each function citing the reference lines it follows.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  The product package never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libsvo_oracle.so")
+_lib = None
+
+MAX_DEPTH = 10.0  # voxel_helpers.py:24
+N_MAX_HITS = 50   # voxel_helpers.py:561 (max_voxel_hit is ignored by the reference)
+SAMPLER_G = 200   # voxel_helpers.py:300
+SAMPLER_CHUNK = 4 * SAMPLER_G  # voxel_helpers.py:331
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i64, f32, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_int
+        L.oracle_octree_new.restype = vp
+        L.oracle_octree_new.argtypes = [i32]
+        L.oracle_octree_free.argtypes = [vp]
+        L.oracle_octree_insert.argtypes = [vp, vp, i64]
+        L.oracle_octree_count.restype = i64
+        L.oracle_octree_count.argtypes = [vp]
+        L.oracle_octree_export.argtypes = [vp, vp, vp, vp]
+        L.oracle_svo_intersect.restype = i64
+        L.oracle_svo_intersect.argtypes = [i64, vp, vp, vp, vp, f32, i32, vp, vp, vp]
+        L.oracle_inverse_cdf.argtypes = [i32, i32, i32, i32, f32] + [vp] * 9
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# --------------------------------------------------------------------------
+# Octree build / export — octree.cpp:104-294, :561-687; mapping.py:300-406
+# --------------------------------------------------------------------------
+class OracleOctree:
+    def __init__(self, grid_dim: int):
+        self._h = lib().oracle_octree_new(int(grid_dim))
+
+    def insert(self, vox: np.ndarray):
+        v = np.ascontiguousarray(vox, dtype=np.int32)
+        lib().oracle_octree_insert(self._h, _ptr(v), int(v.shape[0]))
+
+    def count(self) -> int:
+        return int(lib().oracle_octree_count(self._h))
+
+    def export(self):
+        n = self.count()
+        voxels = np.zeros((n, 4), np.float32)
+        children = np.zeros((n, 8), np.float32)
+        features = np.zeros((n, 8), np.int32)
+        lib().oracle_octree_export(self._h, _ptr(voxels), _ptr(children), _ptr(features))
+        return voxels, children, features
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.oracle_octree_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def map_states_from_export(voxels, children, features, voxel_size, embeddings):
+    """mapping.py:328-377 — centres, [N,9] structure, vertex ids."""
+    vox = torch.from_numpy(np.asarray(voxels, np.float32))
+    ch = torch.from_numpy(np.asarray(children, np.float32))
+    centres = (vox[:, :3] + vox[:, -1:] / 2) * voxel_size
+    structure = torch.cat([ch, vox[:, -1:]], -1).int()
+    return {
+        "voxel_vertex_idx": torch.from_numpy(np.asarray(features, np.int32)),
+        "voxel_center_xyz": centres.float(),
+        "voxel_structure": structure,
+        "voxel_vertex_emb": embeddings,
+    }
+
+
+# --------------------------------------------------------------------------
+# Intersection — voxel_helpers.py:110-166 (kernel) + :557-595 (sort/trim)
+# --------------------------------------------------------------------------
+def svo_intersect_flat(ray_start, ray_dir, centres, structure, voxel_size, n_max=N_MAX_HITS):
+    """Per-ray DFS hits in emission order; returns (idx, t_in, t_out, visits)."""
+    rs = np.ascontiguousarray(ray_start, np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(ray_dir, np.float32).reshape(-1, 3)
+    pts = np.ascontiguousarray(centres, np.float32)
+    ch = np.ascontiguousarray(structure, np.int32)
+    n = rs.shape[0]
+    idx = np.empty((n, n_max), np.int32)
+    t0 = np.empty((n, n_max), np.float32)
+    t1 = np.empty((n, n_max), np.float32)
+    visits = lib().oracle_svo_intersect(n, _ptr(rs), _ptr(rd), _ptr(pts), _ptr(ch), float(voxel_size), int(n_max),
+                                        _ptr(idx), _ptr(t0), _ptr(t1))
+    if visits < 0:
+        raise RuntimeError("oracle DFS stack overflow")
+    return idx, t0, t1, int(visits)
+
+
+def ray_intersect_vox(rays_o, rays_d, centres, structure, voxel_size, max_distance=10.0):
+    """voxel_helpers.py:557-595 with a stable sort on DFS emission order."""
+    S, N = rays_o.shape[:2]
+    idx, t0, t1, _ = svo_intersect_flat(rays_o.detach().reshape(-1, 3).numpy(), rays_d.detach().reshape(-1, 3).numpy(),
+                                        centres.detach().numpy(), structure.numpy(), voxel_size)
+    pts_idx = torch.from_numpy(idx).reshape(S, N, -1)
+    min_depth = torch.from_numpy(t0).reshape(S, N, -1)
+    max_depth = torch.from_numpy(t1).reshape(S, N, -1)
+    miss = pts_idx.eq(-1)
+    min_depth = min_depth.masked_fill(miss, max_distance)
+    max_depth = max_depth.masked_fill(miss, max_distance)
+    min_depth, order = torch.sort(min_depth, dim=-1, stable=True)
+    max_depth = max_depth.gather(-1, order)
+    pts_idx = pts_idx.gather(-1, order)
+    pts_idx[min_depth > max_distance] = -1
+    miss = pts_idx.eq(-1)
+    min_depth = min_depth.masked_fill(miss, max_distance)
+    max_depth = max_depth.masked_fill(miss, max_distance)
+    P = int(pts_idx.ne(-1).sum(-1).max())
+    out = {
+        "min_depth": min_depth[..., :P],
+        "max_depth": max_depth[..., :P],
+        "intersected_voxel_idx": pts_idx[..., :P],
+    }
+    hits = out["intersected_voxel_idx"].ne(-1).any(-1)
+    return out, hits
+
+
+# --------------------------------------------------------------------------
+# Sampling — voxel_helpers.py:288-374 (host wrapper) + :637-663 (ray_sample)
+# --------------------------------------------------------------------------
+def sampler_layout(n_rays):
+    """K' (rays per sampler slot block) and the padded ray count H."""
+    kp = int(math.ceil(n_rays / SAMPLER_G))
+    return kp, kp * SAMPLER_G
+
+
+def inverse_cdf_sampling(pts_idx, min_depth, max_depth, probs, steps, fixed_step_size=-1.0, noise=None,
+                         deterministic=False, generator=None):
+    """Returns (sampled_idx, depth, dists, noise_used) as the reference host
+    wrapper does; `noise` (shape [200, K', max_steps]) may be injected."""
+    N, P = pts_idx.shape
+    kp, H = sampler_layout(N)
+    if H > N:  # pad with copies of row 0 (voxel_helpers.py:303-310)
+        pad = H - N
+        pts_idx = torch.cat([pts_idx, pts_idx[:1].expand(pad, P)], 0)
+        min_depth = torch.cat([min_depth, min_depth[:1].expand(pad, P)], 0)
+        max_depth = torch.cat([max_depth, max_depth[:1].expand(pad, P)], 0)
+        probs = torch.cat([probs, probs[:1].expand(pad, P)], 0)
+        steps = torch.cat([steps, steps[:1].expand(pad)], 0)
+    pts_idx = pts_idx.reshape(SAMPLER_G, kp, P).int().contiguous()
+    min_depth = min_depth.reshape(SAMPLER_G, kp, P).float().contiguous()
+    max_depth = max_depth.reshape(SAMPLER_G, kp, P).float().contiguous()
+    probs = probs.reshape(SAMPLER_G, kp, P).float().contiguous()
+    steps = steps.reshape(SAMPLER_G, kp).float().contiguous()
+    max_steps = int(steps.ceil().long().max()) + P
+    if noise is None:
+        if deterministic:
+            noise = torch.full((SAMPLER_G, kp, max_steps), 0.5)
+        else:
+            noise = torch.rand((SAMPLER_G, kp, max_steps), generator=generator).clamp(min=0.001, max=0.999)
+    assert tuple(noise.shape) == (SAMPLER_G, kp, max_steps), (noise.shape, (SAMPLER_G, kp, max_steps))
+    noise = noise.float().contiguous()
+    parts = []
+    for c0 in range(0, kp, SAMPLER_CHUNK):  # voxel_helpers.py:331-343
+        c1 = min(kp, c0 + SAMPLER_CHUNK)
+        w = c1 - c0
+        a_idx = pts_idx[:, c0:c1].contiguous().numpy()
+        a_lo = min_depth[:, c0:c1].contiguous().numpy()
+        a_hi = max_depth[:, c0:c1].contiguous().numpy()
+        a_nz = noise[:, c0:c1].contiguous().numpy()
+        a_pr = probs[:, c0:c1].contiguous().numpy()
+        a_st = steps[:, c0:c1].contiguous().numpy()
+        o_idx = np.full((SAMPLER_G, w, max_steps), -1, np.int32)
+        o_dep = np.zeros((SAMPLER_G, w, max_steps), np.float32)
+        o_dis = np.zeros((SAMPLER_G, w, max_steps), np.float32)
+        lib().oracle_inverse_cdf(SAMPLER_G, w, P, max_steps, float(fixed_step_size), _ptr(a_idx), _ptr(a_lo),
+                                 _ptr(a_hi), _ptr(a_nz), _ptr(a_pr), _ptr(a_st), _ptr(o_idx), _ptr(o_dep),
+                                 _ptr(o_dis))
+        parts.append((torch.from_numpy(o_idx), torch.from_numpy(o_dep), torch.from_numpy(o_dis)))
+    s_idx, s_dep, s_dis = [torch.cat([p[i] for p in parts], 1).reshape(H, -1)[:N] for i in range(3)]
+    max_len = int(s_idx.ne(-1).sum(-1).max())
+    return s_idx[:, :max_len], s_dep[:, :max_len], s_dis[:, :max_len], noise
+
+
+def ray_sample(intersection, step_size, noise=None, deterministic=False, generator=None):
+    """voxel_helpers.py:637-663."""
+    idx = intersection["intersected_voxel_idx"]
+    dists = (intersection["max_depth"] - intersection["min_depth"]).masked_fill(idx.eq(-1), 0)
+    probs = dists / dists.sum(dim=-1, keepdim=True)
+    steps = dists.sum(-1) / step_size
+    s_idx, s_dep, s_dis, noise = inverse_cdf_sampling(idx, intersection["min_depth"], intersection["max_depth"],
+                                                      probs, steps, -1.0, noise, deterministic, generator)
+    s_dis = s_dis.clamp(min=0.0)
+    s_dep = s_dep.masked_fill(s_idx.eq(-1), MAX_DEPTH)
+    s_dis = s_dis.masked_fill(s_idx.eq(-1), 0.0)
+    return {"sampled_point_depth": s_dep, "sampled_point_distance": s_dis, "sampled_point_voxel_idx": s_idx}, noise
+
+
+# --------------------------------------------------------------------------
+# Interpolation — render_helpers.py:46-156
+# --------------------------------------------------------------------------
+_CORNERS = torch.tensor([[(k >> 2) & 1, (k >> 1) & 1, k & 1] for k in range(8)], dtype=torch.float32)
+
+
+def interp_features(xyz, leaf_idx, centres, vertex_idx, embeddings, voxel_size):
+    """feats[M,16] = Σ_k w_k(p) E[vertex_idx[leaf, k]], p = (x-c)/voxel + 0.5."""
+    li = leaf_idx.long()
+    c = centres[li]
+    e = embeddings[vertex_idx[li].long()]            # [M,8,D]
+    p = ((xyz - c) / voxel_size + 0.5).unsqueeze(1)  # [M,1,3]
+    q = _CORNERS.unsqueeze(0)
+    w = (p * q + (1 - p) * (1 - q)).prod(dim=-1, keepdim=True)
+    return (w * e).sum(1)
+
+
+# --------------------------------------------------------------------------
+# Decoder — nrgbd.py:80-146 for depth 2, embedder 'none', skips [] (all configs)
+# --------------------------------------------------------------------------
+def decoder_params_init(width=128, in_dim=16, sdf_dim=128, seed=0):
+    """Same shapes/order as nrgbd.Decoder.state_dict(); nn.Linear default init."""
+    g = torch.Generator().manual_seed(seed)
+
+    def lin(i, o):
+        bound = 1.0 / math.sqrt(i)
+        w = (torch.rand((o, i), generator=g) * 2 - 1) * bound
+        b = (torch.rand((o,), generator=g) * 2 - 1) * bound
+        return w, b
+
+    p = {}
+    p["pts_linears.0.weight"], p["pts_linears.0.bias"] = lin(in_dim, width)
+    p["pts_linears.1.weight"], p["pts_linears.1.bias"] = lin(width, width)
+    p["sdf_out.weight"], p["sdf_out.bias"] = lin(width, 1 + sdf_dim)
+    p["color_out.0.weight"], p["color_out.0.bias"] = lin(sdf_dim + in_dim, width)
+    p["color_out.2.weight"], p["color_out.2.bias"] = lin(width, 3)
+    return p
+
+
+def decoder_forward(params, x):
+    """nrgbd.py:116-146 → (color [M,3], sdf [M])."""
+    F = torch.nn.functional
+    h = F.relu(F.linear(x, params["pts_linears.0.weight"], params["pts_linears.0.bias"]))
+    h = F.relu(F.linear(h, params["pts_linears.1.weight"], params["pts_linears.1.bias"]))
+    o = F.linear(h, params["sdf_out.weight"], params["sdf_out.bias"])
+    sdf, feat = o[:, :1], o[:, 1:]
+    hc = F.relu(F.linear(torch.cat([feat, x], -1), params["color_out.0.weight"], params["color_out.0.bias"]))
+    rgb = torch.sigmoid(F.linear(hc, params["color_out.2.weight"], params["color_out.2.bias"]))
+    return rgb, sdf[:, 0]
+
+
+# --------------------------------------------------------------------------
+# render_rays — render_helpers.py:351-556
+# --------------------------------------------------------------------------
+def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_size, truncation, max_distance,
+                noise=None, deterministic=False, generator=None):
+    intersection, hits = ray_intersect_vox(rays_o, rays_d, map_states["voxel_center_xyz"],
+                                           map_states["voxel_structure"], voxel_size, max_distance)
+    assert hits.sum() > 0
+    ray_mask = hits.view(1, -1)
+    intersection = {k: v[ray_mask].reshape(-1, v.size(-1)) for k, v in intersection.items()}
+    ro = rays_o[ray_mask].reshape(-1, 3)
+    rd = rays_d[ray_mask].reshape(-1, 3)
+    samples, noise = ray_sample(intersection, step_size, noise, deterministic, generator)
+    depth = samples["sampled_point_depth"]
+    sidx = samples["sampled_point_voxel_idx"].long()
+    mask = sidx.ne(-1)
+    xyz = ro.unsqueeze(1) + rd.unsqueeze(1) * depth.unsqueeze(2)
+    feats = interp_features(xyz[mask], sidx[mask], map_states["voxel_center_xyz"], map_states["voxel_vertex_idx"],
+                            map_states["voxel_vertex_emb"], voxel_size)
+    rgb_s, sdf_s = decoder_forward(decoder_params, feats)
+    R, S = mask.shape
+    sdf = torch.ones(R, S).masked_scatter(mask, sdf_s)
+    colour = torch.zeros(R, S, 3).masked_scatter(mask.unsqueeze(-1).expand(R, S, 3), rgb_s)
+    valid = mask.float()
+    z = depth
+    w = torch.sigmoid(sdf / truncation) * torch.sigmoid(-sdf / truncation)
+    sign = sdf[:, 1:] * sdf[:, :-1]
+    first = torch.argmax((sign < 0.0).float(), dim=1)[..., None]
+    z_min = torch.gather(z, 1, first)
+    w = w * (z < z_min + truncation).float() * valid
+    w = w / (w.sum(dim=-1, keepdim=True) + 1e-8)
+    return {
+        "weights": w,
+        "color": (w[..., None] * colour).sum(-2),
+        "depth": (w * z).sum(-1),
+        "z_vals": z,
+        "sdf": sdf,
+        "ray_mask": ray_mask,
+        "samples": samples,
+        "sampled_xyz": xyz,
+        "intersection": intersection,
+        "noise": noise,
+        "n_samples": int(mask.sum()),
+    }
+
+
+# --------------------------------------------------------------------------
+# Criterion — criterion.py:16-116 (weight_depth_loss=False path + median path)
+# --------------------------------------------------------------------------
+def criterion(outputs, rgb_gt, depth_gt, weights_cfg, truncation, max_depth, weight_depth_loss=False):
+    ray_mask = outputs["ray_mask"]
+    gt_depth = depth_gt[ray_mask]
+    gt_color = rgb_gt[ray_mask]
+    z = outputs["z_vals"]
+    sdf = outputs["sdf"]
+    color_loss = (gt_color - outputs["color"]).abs().mean()
+    valid = (gt_depth > 0.01) & (gt_depth < max_depth)
+    dl = (gt_depth - outputs["depth"]).abs()
+    if weight_depth_loss:
+        var = (outputs["weights"] * ((outputs["depth"].unsqueeze(-1) - z) ** 2)).sum(-1)
+        tmp = dl / torch.sqrt(var + 1e-10)
+        valid = (tmp < 10 * tmp.median()) & valid
+    depth_loss = dl[valid].mean()
+    d = gt_depth.unsqueeze(-1).expand(*z.shape)
+    front = (z < d - truncation).float()
+    back = (z > d + truncation).float()
+    dmask = ((d > 0.0) & (d < max_depth)).float()
+    sdf_mask = (1.0 - front) * (1.0 - back) * dmask
+    n_fs = torch.count_nonzero(front).float()
+    n_sdf = torch.count_nonzero(sdf_mask).float()
+    fs_w = 1.0 - n_fs / (n_fs + n_sdf)
+    sdf_w = 1.0 - n_sdf / (n_fs + n_sdf)
+    fs_loss = torch.mean(torch.square(sdf * front - front)) * fs_w
+    sdf_loss = torch.mean(torch.square((z + sdf * truncation) * sdf_mask - d * sdf_mask)) * sdf_w
+    loss = (weights_cfg["rgb_weight"] * color_loss + weights_cfg["depth_weight"] * depth_loss
+            + weights_cfg["fs_weight"] * fs_loss + weights_cfg["sdf_weight"] * sdf_loss)
+    return loss, {"color_loss": color_loss, "depth_loss": depth_loss, "fs_loss": fs_loss, "sdf_loss": sdf_loss}
+
+
+REPLICA_CRITERIA = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+SCANNET_CRITERIA = {"rgb_weight": 1.0, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+
+
+def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_params, step_size, voxel_size,
+                        truncation=0.1, max_distance=10.0, criteria=REPLICA_CRITERIA, noise=None,
+                        deterministic=False, generator=None, rays_require_grad=True):
+    """One bundle-adjust iteration's differentiable part (render_helpers.py:648-671).
+
+    Returns outputs, loss and grads for embeddings, decoder params, rays_o, rays_d."""
+    emb = map_states["voxel_vertex_emb"].detach().clone().requires_grad_(True)
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in decoder_params.items()}
+    ro = rays_o.detach().clone().requires_grad_(rays_require_grad)
+    rd = rays_d.detach().clone().requires_grad_(rays_require_grad)
+    ms = dict(map_states)
+    ms["voxel_vertex_emb"] = emb
+    out = render_rays(ro, rd, ms, params, step_size, voxel_size, truncation, max_distance, noise, deterministic,
+                      generator)
+    loss, parts = criterion(out, rgb_gt, depth_gt, criteria, truncation, max_distance)
+    loss.backward()
+    grads = {"embeddings": emb.grad, "rays_o": ro.grad, "rays_d": rd.grad}
+    for k, v in params.items():
+        grads[k] = v.grad
+    return out, loss.detach(), parts, grads

@@ -1,0 +1,239 @@
+"""Generate golden fixtures from the REFERENCE Python path (container only).
+
+Runs /root/reference/src/variations/render_helpers.render_rays, the
+reference Criterion and loss.backward() on small seeded inputs and stores
+inputs, intermediates, outputs and gradients as .npz files in this directory.
+
+The reference's `grid` CUDA extension cannot be built in this image (it needs
+cuda.h / ATen-CUDA headers), so a stand-in `grid` module backed by the
+oracle's C restatement (oracle/svo_oracle.c) is installed in sys.modules;
+everything ABOVE the two kernels — batching/padding, sort/trim, probs/steps,
+sampler host wrapper, interpolation, decoder, compositing, loss, autograd —
+is the reference's own code.  Modules the path does not use (open3d, annoy,
+tensorboardX) are replaced by empty stubs, torch.Tensor.cuda by identity
+(CPU-only torch), and the reference's per-call np.savetxt debug dumps land in
+a temp dir.  Noise drawn inside InverseCDFRaySampling is recorded so the
+build can inject the same noise.
+
+Usage:  python tests/golden/make_golden.py     (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True  # never write into /root/reference
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "proud-slam_amd"))
+
+from oracle import oracle as O  # noqa: E402
+from psvo import synthetic as syn  # noqa: E402
+
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---------------------------------------------------------------- stubs
+def _install_stubs(noise_log):
+    for name in ("open3d", "tensorboardX", "annoy"):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+    sys.modules["annoy"].AnnoyIndex = object
+    sys.modules["tensorboardX"].SummaryWriter = object
+
+    grid = types.ModuleType("grid")
+
+    def svo_intersect(ray_start, ray_dir, points, children, voxelsize, n_max):
+        B, K, _ = ray_start.shape
+        # the reference replicates the tree B times; every copy is identical
+        idx, t0, t1, _ = O.svo_intersect_flat(ray_start.reshape(-1, 3).numpy(), ray_dir.reshape(-1, 3).numpy(),
+                                              points[0].contiguous().numpy(), children[0].contiguous().numpy(),
+                                              voxelsize, n_max)
+        return (torch.from_numpy(idx).reshape(B, K, n_max), torch.from_numpy(t0).reshape(B, K, n_max),
+                torch.from_numpy(t1).reshape(B, K, n_max))
+
+    def inverse_cdf_sampling(pts_idx, min_depth, max_depth, noise, probs, steps, fixed_step_size):
+        b, k, p = pts_idx.shape
+        ms = noise.shape[-1]
+        noise_log.append(noise.clone())
+        o_idx = np.full((b, k, ms), -1, np.int32)
+        o_dep = np.zeros((b, k, ms), np.float32)
+        o_dis = np.zeros((b, k, ms), np.float32)
+        c = lambda t, dt: np.ascontiguousarray(t.numpy(), dtype=dt)
+        O.lib().oracle_inverse_cdf(b, k, p, ms, float(fixed_step_size), O._ptr(c(pts_idx, np.int32)),
+                                   O._ptr(c(min_depth, np.float32)), O._ptr(c(max_depth, np.float32)),
+                                   O._ptr(c(noise, np.float32)), O._ptr(c(probs, np.float32)),
+                                   O._ptr(c(steps, np.float32)), O._ptr(o_idx), O._ptr(o_dep), O._ptr(o_dis))
+        return torch.from_numpy(o_idx), torch.from_numpy(o_dep), torch.from_numpy(o_dis)
+
+    grid.svo_intersect = svo_intersect
+    grid.inverse_cdf_sampling = inverse_cdf_sampling
+    sys.modules["grid"] = grid
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    sys.path.insert(0, os.path.join(REF, "src"))
+
+
+def _reference_modules():
+    import importlib
+    rh = importlib.import_module("variations.render_helpers")
+    nrgbd = importlib.import_module("variations.nrgbd")
+    crit = importlib.import_module("criterion")
+    return rh, nrgbd, crit
+
+
+# ---------------------------------------------------------------- cases
+def _octree(vox, grid_dim):
+    t = O.OracleOctree(grid_dim)
+    t.insert(vox)
+    v, c, f = t.export()
+    t.close()
+    return v, c, f
+
+
+def case_inputs(name):
+    """Seeded inputs for each golden case."""
+    g = np.random.default_rng(0)
+    if name == "A_voxels_center":
+        # the reference's only data fixture (875 real voxel centres, +10 m
+        # offset) translated into a depth-6 (grid 64) octree — SURVEY §8d A.
+        pts = np.loadtxt(os.path.join(REF, "src/variations/voxels_center.txt"))
+        key = np.round(pts / 0.2).astype(np.int64)
+        key = key - key.min(0) + 1
+        vox, grid_dim = key.astype(np.int32), 64
+        centre = (key.mean(0) + 0.5) * 0.2
+        eye = centre + np.array([-2.5, -0.6, 0.4])
+        T = syn.look_at(eye, centre)
+        scene = syn.Scene([], grid_dim=grid_dim)
+        K = scene.intrinsics
+        gen = torch.Generator().manual_seed(0)
+        pix = syn.gumbel_topk_pixels(K["H"], K["W"], 1024, gen).numpy()
+        u, v = (pix % K["W"]).astype(np.float64), (pix // K["W"]).astype(np.float64)
+        d = np.stack([(u - K["cx"]) / K["fx"], (v - K["cy"]) / K["fy"], np.ones_like(u)], -1).astype(np.float32)
+        rd = d @ T[:3, :3].astype(np.float32).T
+        ro = np.broadcast_to(T[:3, 3].astype(np.float32), rd.shape).copy()
+        depth = g.uniform(1.5, 4.0, (1, 1024)).astype(np.float32)
+        rgb = g.uniform(0, 1, (1, 1024, 3)).astype(np.float32)
+        return dict(vox=vox, grid_dim=grid_dim, rays_o=ro[None], rays_d=rd[None], rgb=rgb, depth=depth,
+                    step=0.02, width=128, emb_std=0.3, crit="replica", deterministic=False)
+    if name in ("B_room0_small", "B_room0_det"):
+        w = syn.make_workload("room0", n_frames=1, rays_per_frame=384, seed=3)
+        ro, rd = w.rays_o.numpy(), w.rays_d.numpy()
+        # grazing rays inside the floor voxel layer: > 50 leaf hits, DFS-order truncation
+        n_graze = 8
+        o = np.array([10.05, 10.07, 10.1], np.float32) + np.linspace(0, 0.06, n_graze)[:, None].astype(np.float32)
+        dd = np.array([0.8, 0.6, 0.0], np.float32)[None].repeat(n_graze, 0)
+        dd[:, 1] += np.linspace(0, 0.04, n_graze).astype(np.float32)
+        ro = np.concatenate([ro, o[None]], 1)
+        rd = np.concatenate([rd, dd[None]], 1)
+        rgb = np.concatenate([w.rgb.numpy(), g.uniform(0, 1, (1, n_graze, 3)).astype(np.float32)], 1)
+        depth = np.concatenate([w.depth.numpy(), np.full((1, n_graze), 3.0, np.float32)], 1)
+        return dict(vox=w.voxels, grid_dim=256, rays_o=ro, rays_d=rd, rgb=rgb, depth=depth,
+                    step=0.02 if name == "B_room0_small" else 0.012, width=128, emb_std=0.3, crit="replica",
+                    deterministic=(name == "B_room0_det"))
+    if name == "C_scannet_small":
+        w = syn.make_workload("scannet0000", n_frames=1, rays_per_frame=256, seed=5)
+        return dict(vox=w.voxels, grid_dim=256, rays_o=w.rays_o.numpy(), rays_d=w.rays_d.numpy(),
+                    rgb=w.rgb.numpy(), depth=w.depth.numpy(), step=0.02, width=256, emb_std=0.3, crit="scannet",
+                    deterministic=False)
+    raise KeyError(name)
+
+
+CASES = ["A_voxels_center", "B_room0_small", "B_room0_det", "C_scannet_small"]
+
+
+def run_case(name, rh, nrgbd, crit_mod, noise_log):
+    inp = case_inputs(name)
+    voxels, children, features = _octree(inp["vox"], inp["grid_dim"])
+    n_nodes = voxels.shape[0]
+    torch.manual_seed(1234)
+    emb = (torch.randn(n_nodes, 16) * inp["emb_std"]).requires_grad_(True)
+    dec = nrgbd.Decoder(depth=2, width=inp["width"], in_dim=16, skips=[], embedder="none", multires=0)
+    # map_states exactly as Mapping.update_grid_pcd_features builds them (mapping.py:328-377)
+    vt = torch.from_numpy(voxels)
+    centres = (vt[:, :3] + vt[:, -1:] / 2) * 0.2
+    structure = torch.cat([torch.from_numpy(children), vt[:, -1:]], -1).int()
+    map_states = {"voxel_vertex_idx": torch.from_numpy(features), "voxel_center_xyz": centres.float(),
+                  "voxel_structure": structure, "voxel_vertex_emb": emb}
+    ro = torch.from_numpy(np.ascontiguousarray(inp["rays_o"], np.float32)).requires_grad_(True)
+    rd = torch.from_numpy(np.ascontiguousarray(inp["rays_d"], np.float32)).requires_grad_(True)
+    args = types.SimpleNamespace(
+        criteria={**(O.REPLICA_CRITERIA if inp["crit"] == "replica" else O.SCANNET_CRITERIA), "sdf_truncation": 0.1},
+        data_specs={"max_depth": 10.0 if inp["crit"] == "replica" else 5.0})
+    criterion = crit_mod.Criterion(args)
+    noise_log.clear()
+    torch.manual_seed(99)
+    # deterministic=True is not reachable through render_rays (ray_sample passes
+    # fixed=False); the det case calls the same path with noise forced to 0.5.
+    if inp["deterministic"]:
+        orig = torch.Tensor.uniform_
+        torch.Tensor.uniform_ = lambda self, *a, **k: self.fill_(0.5)
+    try:
+        out = rh.render_rays(ro, rd, map_states, dec, None, inp["step"], 0.2, 0.1, 10, args.data_specs["max_depth"])
+    finally:
+        if inp["deterministic"]:
+            torch.Tensor.uniform_ = orig
+    rgb_gt = torch.from_numpy(inp["rgb"])
+    depth_gt = torch.from_numpy(inp["depth"])
+    loss, parts = criterion(out, (rgb_gt, depth_gt))
+    loss.backward()
+    noise = torch.cat(noise_log, 1).numpy() if len(noise_log) > 1 else noise_log[0].numpy()
+    # also record the raw DFS hits and sorted/trimmed intersection
+    from variations import voxel_helpers as vh
+    inter, hits = vh.ray_intersect_vox(ro.detach(), rd.detach(), centres, structure, 0.2, 10, 10.0)
+    raw_idx, raw_t0, raw_t1, visits = O.svo_intersect_flat(inp["rays_o"], inp["rays_d"], centres.numpy(),
+                                                           structure.numpy(), 0.2)
+    rec = dict(
+        grid_dim=np.int64(inp["grid_dim"]), vox=inp["vox"], voxels=voxels, children=children, features=features,
+        centres=centres.numpy(), structure=structure.numpy(), embeddings=emb.detach().numpy(),
+        rays_o=inp["rays_o"], rays_d=inp["rays_d"], rgb=inp["rgb"], depth_gt=inp["depth"],
+        step_size=np.float32(inp["step"]), voxel_size=np.float32(0.2), truncation=np.float32(0.1),
+        max_distance=np.float32(10.0), max_depth=np.float32(args.data_specs["max_depth"]),
+        crit=np.array([args.criteria[k] for k in ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight")],
+                      np.float32),
+        width=np.int64(inp["width"]), noise=noise,
+        raw_idx=raw_idx, raw_t0=raw_t0, raw_t1=raw_t1, visits=np.int64(visits),
+        hit_idx=inter["intersected_voxel_idx"].numpy(), hit_min=inter["min_depth"].numpy(),
+        hit_max=inter["max_depth"].numpy(), hits=hits.numpy(),
+        z_vals=out["z_vals"].detach().numpy(), sdf=out["sdf"].detach().numpy(),
+        weights=out["weights"].detach().numpy(), color=out["color"].detach().numpy(),
+        depth=out["depth"].detach().numpy(), ray_mask=out["ray_mask"].numpy(),
+        loss=np.float32(loss.item()),
+        loss_parts=np.array([parts[k] for k in ("color_loss", "depth_loss", "fs_loss", "sdf_loss")], np.float32),
+        grad_embeddings=emb.grad.numpy(), grad_rays_o=ro.grad.numpy(), grad_rays_d=rd.grad.numpy(),
+    )
+    for k, v in dec.state_dict().items():
+        rec["dec." + k] = v.numpy()
+    for k, p in dec.named_parameters():
+        rec["grad_dec." + k] = p.grad.numpy()
+    return rec
+
+
+def main():
+    noise_log = []
+    _install_stubs(noise_log)
+    rh, nrgbd, crit_mod = _reference_modules()
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)  # render_rays np.savetxt()s every call (render_helpers.py:403-404)
+        try:
+            for name in CASES:
+                rec = run_case(name, rh, nrgbd, crit_mod, noise_log)
+                path = os.path.join(OUT_DIR, f"{name}.npz")
+                np.savez_compressed(path, **rec)
+                print(f"{name}: nodes={rec['voxels'].shape[0]} rays={rec['rays_o'].shape[1]} "
+                      f"R_hit={int(rec['hits'].sum())} P={rec['hit_idx'].shape[-1]} S={rec['z_vals'].shape[-1]} "
+                      f"loss={float(rec['loss']):.6f} -> {os.path.relpath(path, REPO)} "
+                      f"({os.path.getsize(path) // 1024} KiB)")
+        finally:
+            os.chdir(cwd)
+
+
+if __name__ == "__main__":
+    main()

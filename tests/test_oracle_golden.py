@@ -1,0 +1,113 @@
+"""Pin the CPU oracle to golden vectors produced by the reference's own Python
+path (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import torch
+
+from oracle import oracle as O
+
+
+def _decoder_params(g):
+    return {k[len("dec."):]: torch.from_numpy(v) for k, v in g.items() if k.startswith("dec.")}
+
+
+def _run_oracle(g):
+    ms = O.map_states_from_export(g["voxels"], g["children"], g["features"], float(g["voxel_size"]),
+                                  torch.from_numpy(g["embeddings"]))
+    crit = dict(zip(("rgb_weight", "depth_weight", "fs_weight", "sdf_weight"), g["crit"].tolist()))
+    return O.render_and_backward(torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"]),
+                                 torch.from_numpy(g["rgb"]), torch.from_numpy(g["depth_gt"]), ms, _decoder_params(g),
+                                 float(g["step_size"]), float(g["voxel_size"]), float(g["truncation"]),
+                                 float(g["max_depth"]), crit, noise=torch.from_numpy(g["noise"]))
+
+
+def test_octree_export_matches_golden(golden):
+    _, g = golden
+    t = O.OracleOctree(int(g["grid_dim"]))
+    t.insert(g["vox"])
+    v, c, f = t.export()
+    np.testing.assert_array_equal(v, g["voxels"])
+    np.testing.assert_array_equal(c, g["children"])
+    np.testing.assert_array_equal(f, g["features"])
+
+
+def test_map_states_match_golden(golden):
+    _, g = golden
+    ms = O.map_states_from_export(g["voxels"], g["children"], g["features"], 0.2, None)
+    np.testing.assert_array_equal(ms["voxel_center_xyz"].numpy(), g["centres"])
+    np.testing.assert_array_equal(ms["voxel_structure"].numpy(), g["structure"])
+
+
+def test_intersection_matches_golden(golden):
+    _, g = golden
+    out, hits = O.ray_intersect_vox(torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"]),
+                                    torch.from_numpy(g["centres"]), torch.from_numpy(g["structure"]), 0.2, 10.0)
+    np.testing.assert_array_equal(out["intersected_voxel_idx"].numpy(), g["hit_idx"])
+    np.testing.assert_array_equal(out["min_depth"].numpy(), g["hit_min"])
+    np.testing.assert_array_equal(out["max_depth"].numpy(), g["hit_max"])
+    np.testing.assert_array_equal(hits.numpy(), g["hits"])
+
+
+def test_render_and_grads_match_golden(golden):
+    name, g = golden
+    out, loss, parts, grads = _run_oracle(g)
+    # integer / index work and the sampler are bit-exact
+    np.testing.assert_array_equal(out["ray_mask"].numpy(), g["ray_mask"])
+    np.testing.assert_array_equal(out["z_vals"].detach().numpy(), g["z_vals"])
+    # fp32 paths: same torch-CPU ops, only reduction order may differ
+    tol = dict(rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(out["sdf"].detach().numpy(), g["sdf"], **tol)
+    np.testing.assert_allclose(out["weights"].detach().numpy(), g["weights"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(out["color"].detach().numpy(), g["color"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(out["depth"].detach().numpy(), g["depth"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(float(loss), float(g["loss"]), rtol=1e-5)
+    for k, ref in (("embeddings", g["grad_embeddings"]), ("rays_o", g["grad_rays_o"]), ("rays_d", g["grad_rays_d"])):
+        got = grads[k].numpy()
+        scale = np.abs(ref).max() + 1e-12
+        assert np.abs(got - ref).max() <= 1e-4 * scale, (name, k, np.abs(got - ref).max(), scale)
+    for k in [k for k in g if k.startswith("grad_dec.")]:
+        got = grads[k[len("grad_dec."):]].numpy()
+        ref = g[k]
+        scale = np.abs(ref).max() + 1e-12
+        assert np.abs(got - ref).max() <= 1e-4 * scale, (name, k, np.abs(got - ref).max(), scale)
+
+
+def test_sampler_known_answer_slot_quirk():
+    """SURVEY §8a-8, measured on the reference kernel: eight identical 2-hit
+    rays launched as one K'=8 block give 10 valid samples in slots 0-3 and 9
+    in the later slots (the trailing segment is only emitted when
+    j*P + bin < K')."""
+    b, k, p = 1, 8, 2
+    idx = np.tile(np.array([5, 9], np.int32), (b, k, 1))
+    lo = np.tile(np.array([1.0, 1.4], np.float32), (b, k, 1))
+    hi = np.tile(np.array([1.2, 1.6], np.float32), (b, k, 1))
+    probs = np.tile(np.array([0.5, 0.5], np.float32), (b, k, 1))
+    steps = np.full((b, k), 8.0, np.float32)
+    ms = 8 + p
+    noise = np.full((b, k, ms), 0.5, np.float32)
+    o_idx = np.full((b, k, ms), -1, np.int32)
+    o_dep = np.zeros((b, k, ms), np.float32)
+    o_dis = np.zeros((b, k, ms), np.float32)
+    O.lib().oracle_inverse_cdf(b, k, p, ms, -1.0, *(O._ptr(a) for a in (idx, lo, hi, noise, probs, steps,
+                                                                         o_idx, o_dep, o_dis)))
+    counts = (o_idx[0] != -1).sum(-1)
+    assert counts.tolist() == [10, 10, 10, 10, 9, 9, 9, 9]
+
+
+def test_sampler_done_case_reads_next_slot():
+    """When a ray's hits fill all P columns and its bins run out inside the
+    main loop, the trailing emission takes pts_idx[H + P] = the NEXT slot's
+    first voxel id (sample_gpu.cu:224-226), only while j*P + P < K'."""
+    b, k, p = 1, 4, 1
+    idx = np.array([[[3], [7], [11], [13]]], np.int32)
+    lo = np.full((b, k, p), 1.0, np.float32)
+    hi = np.full((b, k, p), 1.1, np.float32)
+    probs = np.ones((b, k, p), np.float32)
+    steps = np.full((b, k), 3.5, np.float32)   # ceil → 4 steps; the 4th cdf > 1 exhausts the bins
+    ms = 4 + p
+    noise = np.full((b, k, ms), 0.999, np.float32)
+    o_idx = np.full((b, k, ms), -1, np.int32)
+    o_dep = np.zeros((b, k, ms), np.float32)
+    o_dis = np.zeros((b, k, ms), np.float32)
+    O.lib().oracle_inverse_cdf(b, k, p, ms, -1.0, *(O._ptr(a) for a in (idx, lo, hi, noise, probs, steps,
+                                                                         o_idx, o_dep, o_dis)))
+    assert o_idx[0].tolist() == [[3, 3, 3, 3, 7], [7, 7, 7, 7, 11], [11, 11, 11, 11, 13], [13, 13, 13, 13, -1]]
