@@ -1,0 +1,288 @@
+"""Benchmark: rays/s for render + loss + backward (+ optimiser step) of the
+Proud-SLAM mapping render-and-optimise iteration (render_helpers.py:609-676)
+on synthetic Replica room0-shaped input (BASELINE.json configs[1]: 4096
+rays/iter = 4 keyframes x 1024 rays, 1x MI355X; ~64 samples/ray).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One process per GPU; every rank renders its own 4096 rays against the
+replicated octree (weak scaling) and the embedding + decoder gradients are
+summed over ranks with one RCCL all-reduce per step.  Rank 0 prints one JSON
+line.  Inputs (octree, embeddings, decoder, a pool of ray batches with GT)
+are resident in HBM before timing starts.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "proud-slam_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "rays/sec render+backward, Replica room0, 64 samples/ray, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scene", default="room0")
+    ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--rays-per-frame", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=128)
+    ap.add_argument("--samples-per-ray", type=float, default=64.0)
+    ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def build_scene(args, device, rank):
+    from psvo import synthetic as syn
+    from psvo.octree import Octree, map_states
+    from psvo.decoder import Decoder
+    scene_fn = {"room0": syn.room0, "office0": syn.office0, "scannet0000": syn.scannet0000,
+                "multiroom": syn.multiroom}[args.scene]
+    scene = scene_fn()
+    vox = syn.surface_voxels(scene, seed=0)
+    tree = Octree()
+    tree.init(scene.grid_dim, 16, scene.voxel_size, 8)
+    tree.insert(vox)
+    n_nodes = tree.count_nodes()
+    num_embeddings = max(20000, n_nodes)  # replica.yaml:38 num_embeddings
+    g = torch.Generator().manual_seed(0)
+    emb = (torch.randn(num_embeddings, 16, generator=g) * 0.01).to(device).requires_grad_(True)  # mapping.py:80
+    ms = map_states(tree, emb, scene.voxel_size, device=device)
+    torch.manual_seed(0)
+    dec = Decoder(depth=2, width=args.width, in_dim=16, skips=[], embedder="none").to(device)
+    batches = []
+    for i in range(args.pool):
+        poses = syn.camera_poses(scene, args.frames, seed=1000 * rank + i)
+        ro, rd, rgb, depth = syn.rays_for_frames(scene, poses, args.rays_per_frame, seed=1000 * rank + i)
+        batches.append(tuple(x.to(device) for x in (ro, rd, rgb, depth)))
+    return scene, tree, ms, emb, dec, batches
+
+
+def calibrate_step(ms, batches, target, voxel_size):
+    """step_size so that the mean valid samples per hit ray ≈ target."""
+    from psvo.render_helpers import query_samples
+
+    def mean_samples(step):
+        s = query_samples(batches[0][0], batches[0][1], ms, step, voxel_size, 10.0, seed=1)
+        return s.m / s.r_hit
+    lo, hi = 0.001, 0.05
+    for _ in range(18):
+        mid = math.sqrt(lo * hi)
+        if mean_samples(mid) > target:
+            lo = mid
+        else:
+            hi = mid
+    step = math.sqrt(lo * hi)
+    return step, mean_samples(step)
+
+
+class KernelTimer:
+    """HIP events around chosen launches on the launching stream."""
+
+    def __init__(self):
+        self.events = {}
+        self.enabled = False
+
+    def __call__(self, name):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if timer.enabled:
+                    s = torch.cuda.Event(enable_timing=True)
+                    s.record(torch.cuda.current_stream())
+                    self_.s = s
+
+            def __exit__(self_, *exc):
+                if timer.enabled:
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(torch.cuda.current_stream())
+                    timer.events.setdefault(name, []).append((self_.s, e))
+        return _Ctx()
+
+    def mean_ms(self, name):
+        ev = self.events.get(name, [])
+        if not ev:
+            return float("nan")
+        return float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+
+def cpu_baseline(args, scene, tree, step_size, seconds):
+    """Oracle (reference algorithm restated: C kernels + torch-CPU render /
+    loss / autograd) on the host cores, bounded sample of the same workload."""
+    from oracle import oracle as O
+    from psvo import synthetic as syn
+    voxels, children, features = tree.export_arrays()
+    g = torch.Generator().manual_seed(0)
+    emb = torch.randn(voxels.shape[0], 16, generator=g) * 0.01
+    ms = O.map_states_from_export(voxels, children, features, scene.voxel_size, emb)
+    params = O.decoder_params_init(args.width)
+    poses = syn.camera_poses(scene, args.frames, seed=0)
+    ro, rd, rgb, depth = syn.rays_for_frames(scene, poses, args.rays_per_frame, seed=0)
+    t0 = time.time()
+    n_it = 0
+    while True:
+        O.render_and_backward(ro, rd, rgb, depth, ms, params, step_size, scene.voxel_size,
+                              generator=torch.Generator().manual_seed(n_it))
+        n_it += 1
+        if time.time() - t0 >= seconds or n_it >= 50:
+            break
+    dt = time.time() - t0
+    rays = n_it * ro.shape[1]
+    return {"value": rays / dt, "unit": "rays/s", "cores": int(torch.get_num_threads()), "kind": "port",
+            "sample": f"{n_it} iterations x {ro.shape[1]} rays ({args.scene}, {args.frames}x{args.rays_per_frame}), "
+                      f"oracle C kernels single-thread + torch-CPU render/loss/backward, {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from psvo import _lib
+    from psvo import render_helpers as RH
+    from psvo.criterion import Criterion
+    import types
+    _lib.lib()
+
+    scene, tree, ms, emb, dec, batches = build_scene(args, device, rank)
+    step_size, spr = calibrate_step(ms, batches, args.samples_per_ray, scene.voxel_size)
+    crit_args = types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0,
+                                                "fs_weight": 10.0, "sdf_truncation": 0.1},
+                                      data_specs={"max_depth": 10.0})
+    criterion = Criterion(crit_args)
+    embed_optim = torch.optim.Adam([emb], lr=5e-3)
+    model_optim = torch.optim.Adam(dec.parameters(), lr=5e-3)
+    params = [emb] + list(dec.parameters())
+    timer = KernelTimer()
+    RH.KERNEL_TIMER = timer
+    stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
+
+    def step(i, record=False):
+        ro, rd, rgb, depth = batches[i % len(batches)]
+        out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True)
+        loss, _ = criterion(out, (rgb, depth))
+        embed_optim.zero_grad(set_to_none=False)
+        model_optim.zero_grad(set_to_none=False)
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)
+            off = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p))
+                off += n
+        embed_optim.step()
+        model_optim.step()
+        if record:
+            s = out["samples"]
+            stats["m"] += s.m
+            stats["r_hit"] += s.r_hit
+            stats["visits"] += s.visits
+            stats["s_max"] = max(stats["s_max"], s.s_max)
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rays_per_step = args.frames * args.rays_per_frame
+    total_rays = rays_per_step * args.steps * world
+    value = total_rays / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # roofline of the dominant HBM-class kernel pair (query+interp backward):
+    # algorithmic bytes per launch from SURVEY §8d per-sample figures
+    m_avg = stats["m"] / args.steps
+    r_avg = stats["r_hit"] / args.steps
+    v_avg = stats["visits"] / args.steps
+    bwd_ms = timer.mean_ms("interp_bwd")
+    fwd_ms = timer.mean_ms("interp_fwd")
+    bytes_bwd = 1664.0 * m_avg
+    bytes_fwd = 628.0 * m_avg
+    achieved = bytes_bwd / (bwd_ms * 1e-3) / 1e9 if bwd_ms == bwd_ms else None
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("interp_bwd_bytes_per_launch")
+        except Exception:
+            traffic = None
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (room0-shaped octree + Replica pinhole rays, analytic GT; random-init embeddings/decoder)",
+        "config": {"workload": f"{args.scene}: {args.frames} keyframes x {args.rays_per_frame} rays/iter per GPU, "
+                               f"{tree.count_nodes()} octree nodes, decoder W={args.width}, "
+                               f"{m_avg / max(r_avg, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
+                   "rays_per_step_per_gpu": rays_per_step, "samples_per_step": m_avg, "hit_rays_per_step": r_avg,
+                   "aabb_tests_per_step": v_avg, "parallelism": f"dp{world} (ray-sharded, RCCL grad all-reduce)"},
+        "roofline": {"kernel": "interp_bwd (embedding scatter + d_xyz)", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
+        "kernels_ms": {"interp_fwd": fwd_ms, "interp_bwd": bwd_ms,
+                       "interp_fwd_GBs": bytes_fwd / (fwd_ms * 1e-3) / 1e9 if fwd_ms == fwd_ms else None},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, scene, tree, step_size, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

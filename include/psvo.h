@@ -1,0 +1,157 @@
+/*
+ * psvo — MI355X-native sparse-voxel-octree renderer: C ABI.
+ *
+ * Plain pointers and sizes only; every device pointer is HBM memory owned by
+ * the caller; every call is asynchronous on `stream` (a hipStream_t passed as
+ * void*) and returns PSVO_OK or an error code (psvo_last_error() gives the
+ * message).  No call allocates, frees or synchronises, so callers may capture
+ * sequences into a hipGraph.
+ *
+ * Reference interfaces replaced (DARYL-GWZ/Proud-SLAM):
+ *   psvo_svo_intersect            grid.svo_intersect
+ *                                 third_party/sparse_voxels/src/intersect.cpp:83-112,
+ *                                 intersect_gpu.cu:191-270, :415-426
+ *   psvo_inverse_cdf_sampling     grid.inverse_cdf_sampling
+ *                                 third_party/sparse_voxels/src/sample.cpp:56-95,
+ *                                 sample_gpu.cu:133-239, :255-269
+ *   psvo_ray_intersect_sorted     voxel_helpers.ray_intersect_vox (voxel_helpers.py:557-595)
+ *                                 + SparseVoxelOctreeRayIntersect (:110-166), fused
+ *   psvo_hit_rank / psvo_sample_rays / psvo_sample_points
+ *                                 render_helpers.render_rays ray/sample compaction
+ *                                 (render_helpers.py:390-460) + voxel_helpers.ray_sample
+ *                                 (voxel_helpers.py:637-663) + InverseCDFRaySampling (:288-374)
+ *   psvo_interp_fwd / _bwd        render_helpers.get_features_vox (render_helpers.py:104-156)
+ *                                 forward and its autograd backward
+ *   psvo_composite_fwd / _bwd     render_helpers.render_rays compositing (render_helpers.py:504-556)
+ *   psvo_loss_*                   criterion.Criterion.forward (criterion.py:16-116)
+ *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
+ *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
+ */
+#ifndef PSVO_H
+#define PSVO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    PSVO_OK = 0,
+    PSVO_E_INVALID = 1,   /* bad argument (shape / size / null pointer) */
+    PSVO_E_LAUNCH = 2,    /* HIP launch or runtime error */
+    PSVO_E_OVERFLOW = 3   /* DFS stack overflow (reference: assert(ptr < 256)) */
+};
+
+const char *psvo_last_error(void);
+const char *psvo_version(void);
+
+/* ---- drop-in `grid` kernels (reference layouts) ----------------------- */
+
+/* ray_start/ray_dir f32[b,m,3]; points f32[b,n,3]; children i32[b,n,9];
+ * outputs idx i32 / min_depth f32 / max_depth f32 [b,m,n_max] (idx -1 when
+ * unused; depths 0 there).  Hits in DFS emission order, children popped 7→0. */
+int psvo_svo_intersect(void *stream, int b, int n, int m, float voxelsize, int n_max, const float *ray_start,
+                       const float *ray_dir, const float *points, const int *children, int *idx, float *min_depth,
+                       float *max_depth);
+
+/* One reference launch over a contiguous [b, num_rays, max_hits] chunk; the
+ * outputs [b, num_rays, max_steps] must be pre-filled (-1 / 0 / 0). */
+int psvo_inverse_cdf_sampling(void *stream, int b, int num_rays, int max_hits, int max_steps,
+                              float fixed_step_size, const int *pts_idx, const float *min_depth,
+                              const float *max_depth, const float *uniform_noise, const float *probs,
+                              const float *steps, int *sampled_idx, float *sampled_depth, float *sampled_dists);
+
+/* ---- fused render path ------------------------------------------------ */
+
+/* Device-side statistics written by the query stages (int32 words).       */
+enum {
+    PSVO_STAT_P = 0,         /* max valid hits over rays (voxel_helpers.py:582) */
+    PSVO_STAT_R_HIT = 1,     /* rays with >= 1 hit */
+    PSVO_STAT_MAX_CEIL = 2,  /* max ceil(steps) over hit rays (voxel_helpers.py:320) */
+    PSVO_STAT_S_MAX = 3,     /* max valid samples per ray (voxel_helpers.py:359) */
+    PSVO_STAT_M = 4,         /* total valid samples */
+    PSVO_STAT_VISITS = 5,    /* AABB tests performed (traffic accounting) */
+    PSVO_STAT_WORDS = 8
+};
+
+/* DFS + stable sort by t_in + max_distance trim for R rays.  hit_* are
+ * [R, 50] (sorted valid prefix, then -1 / max_distance fills); ray_nv[R]
+ * valid-hit count; ray_dsum[R] = Σ(t_out - t_in) in sorted order.
+ * `stats` (PSVO_STAT_WORDS int32, zeroed by the caller) receives P, R_hit,
+ * max ceil(Σ/step) and the visit count. */
+int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const float *rays_o, const float *rays_d,
+                              const float *centres, const int *structure, float voxel_size, float max_distance,
+                              float step_size, int *hit_idx, float *hit_t0, float *hit_t1, int *ray_nv,
+                              float *ray_dsum, int *stats);
+
+/* ray_rank[R] = rank among hit rays or -1; rank_ray[R_hit] = original ray. */
+int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray);
+
+/* Inverse-CDF sampling of the R_hit hit rays with the reference's logical
+ * [200, K', P] layout (K' = ceil(R_hit/200), 800-slot launch chunks): P,
+ * R_hit and max_steps are read from `stats` on the device.  noise is either
+ * NULL (counter-based uniform from `seed`, clamped to [0.001, 0.999]) or
+ * f32[200, K', max_steps].  Outputs [R_hit, max_steps_cap] with
+ * max_steps_cap >= stats[P] + stats[MAX_CEIL]; per-ray valid counts to
+ * ray_ns[R_hit]; S_max / M into stats. */
+int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                     const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
+                     const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
+                     int *ray_ns);
+
+/* Exclusive scan of per-ray sample counts → sample offsets. */
+int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets);
+
+/* Compact valid samples (ray-major): leaf[M], t[M], ray[M]; z_vals and mask
+ * [R_hit, S_max] (z = 10 where invalid, render_helpers.py:418-460). */
+int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int max_steps_cap, const int *s_idx,
+                       const float *s_depth, const int *ray_ns, const int *offsets, int *leaf, float *t,
+                       int *ray_of_sample, float *z_vals, uint8_t *mask);
+
+/* Trilinear interpolation of vertex embeddings at x = o[ray] + d[ray]*t.
+ * centres f32[N,3]; vertex_idx i32[N,8]; emb f32[E,D] with D == 16. */
+int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size, const int *leaf, const float *t,
+                    const int *ray_of_sample, const float *rays_o, const float *rays_d, const float *centres,
+                    const int *vertex_idx, const float *emb, float *feat);
+
+/* Backward of psvo_interp_fwd given grad_feat[M,D]: accumulates into
+ * grad_emb[E,D] (float atomics, caller zeroes) and per-ray grad_o/grad_d
+ * [R_hit,3] (caller zeroes).  Samples must be ray-major (offsets[R_hit+1]). */
+int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets, const int *leaf,
+                    const float *t, const float *rays_o, const float *rays_d, const float *centres,
+                    const int *vertex_idx, const float *emb, const float *grad_feat, float *grad_emb,
+                    float *grad_o, float *grad_d);
+
+/* SDF-to-weight compositing (render_helpers.py:504-556) per hit ray.
+ * sdf_s[M], rgb_s[M,3] per valid sample; outputs sdf/weights [R_hit,S_max]
+ * (sdf padded with 1), color [R_hit,3], depth [R_hit]. */
+int psvo_composite_fwd(void *stream, int64_t r_hit, int s_max, float truncation, const int *offsets,
+                       const int *ray_ns, const float *z_vals, const float *sdf_s, const float *rgb_s,
+                       float *sdf, float *weights, float *color, float *depth, float *z_min);
+
+/* Backward of psvo_composite_fwd: given grad_color[R_hit,3], grad_depth[R_hit],
+ * grad_weights[R_hit,S_max] (may be NULL) and grad_sdf[R_hit,S_max] (may be
+ * NULL), writes grad_sdf_s[M] and grad_rgb_s[M,3]. */
+int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation, const int *offsets,
+                       const int *ray_ns, const float *z_vals, const float *sdf, const float *weights,
+                       const float *rgb_s, const float *grad_color, const float *grad_depth,
+                       const float *grad_weights, const float *grad_sdf, float *grad_sdf_s, float *grad_rgb_s);
+
+/* ---- octree builder (CPU, host memory) -------------------------------- */
+void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);
+void psvo_octree_free(void *tree);
+int psvo_octree_insert(void *tree, const int *vox, int64_t n);
+int64_t psvo_octree_count(void *tree);
+int64_t psvo_octree_count_leaves(void *tree);
+/* voxels f32[N,4], children f32[N,8], features i32[N,8] as
+ * Octree::get_centres_and_children (octree.cpp:561-687) */
+int psvo_octree_export(void *tree, float *voxels, float *children, int *features);
+int psvo_octree_has_voxel(void *tree, int x, int y, int z);
+double psvo_octree_try_insert(void *tree, const int *vox, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PSVO_H */

@@ -1,0 +1,191 @@
+// SDF-to-weight compositing per hit ray (forward + backward) on gfx950.
+//
+// Reference: render_helpers.py:504-556 —
+//   sdf    = masked_scatter_ones(mask, sdf_s)        [R_hit, S]  (pad 1)
+//   colour = masked_scatter(mask, rgb_s)              [R_hit, S, 3] (pad 0)
+//   u      = σ(sdf/tr)·σ(-sdf/tr)
+//   ind    = argmax(sdf[:,1:]·sdf[:,:-1] < 0)  (first sign change, 0 if none)
+//   z_min  = z[ind];  w = u · [z < z_min + tr] · valid;  w /= Σw + 1e-8
+//   rgb    = Σ w·colour;  depth = Σ w·z
+// and the backward torch autograd derives for it (ind / the masks carry no
+// gradient; padded sdf entries are constants).
+//
+// One wave per ray: a ray's S_max (≈100–600) samples stream through the 64
+// lanes in strides; reductions are wave shuffles, so no LDS and no atomics.
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+__device__ __forceinline__ int wmin(int v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v = min(v, __shfl_xor(v, s, 64));
+    return v;
+}
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void k_composite_fwd(int64_t r_hit, int s_max, float tr,
+                                                       const int *__restrict__ offsets,
+                                                       const int *__restrict__ ray_ns,
+                                                       const float *__restrict__ z_vals,
+                                                       const float *__restrict__ sdf_s,
+                                                       const float *__restrict__ rgb_s, float *__restrict__ sdf,
+                                                       float *__restrict__ weights, float *__restrict__ color,
+                                                       float *__restrict__ depth, float *__restrict__ z_min_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int off = offsets[r], ns = ray_ns[r];
+    const float *z = z_vals + r * s_max;
+    float *sd = sdf + r * s_max;
+    float *wt = weights + r * s_max;
+    // pass 1: padded sdf row + first sign change
+    int first = s_max;
+    for (int s = lane; s < s_max; s += 64) {
+        const float v = s < ns ? sdf_s[off + s] : 1.0f;
+        sd[s] = v;
+        if (s + 1 < s_max) {
+            const float v1 = (s + 1) < ns ? sdf_s[off + s + 1] : 1.0f;
+            if (v1 * v < 0.0f) first = min(first, s);
+        }
+    }
+    first = wmin(first);
+    const int ind = first == s_max ? 0 : first;
+    const float zmin = z[ind];
+    // pass 2: unnormalised weights and their sum
+    float tot = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float v = sd[s];
+        const float a = v / tr;
+        float w = sigm(a) * sigm(-a);
+        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        w = keep ? w : 0.0f;
+        wt[s] = w;
+        tot += w;
+    }
+    tot = wsum(tot) + 1e-8f;
+    float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float w = wt[s] / tot;
+        wt[s] = w;
+        if (s < ns) {
+            const float *c = rgb_s + (int64_t)(off + s) * 3;
+            cr += w * c[0];
+            cg += w * c[1];
+            cb += w * c[2];
+        }
+        dd += w * z[s];
+    }
+    cr = wsum(cr);
+    cg = wsum(cg);
+    cb = wsum(cb);
+    dd = wsum(dd);
+    if (lane == 0) {
+        color[r * 3 + 0] = cr;
+        color[r * 3 + 1] = cg;
+        color[r * 3 + 2] = cb;
+        depth[r] = dd;
+        if (z_min_out) z_min_out[r] = zmin;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_composite_bwd(int64_t r_hit, int s_max, float tr,
+                                                       const int *__restrict__ offsets,
+                                                       const int *__restrict__ ray_ns,
+                                                       const float *__restrict__ z_vals,
+                                                       const float *__restrict__ sdf,
+                                                       const float *__restrict__ weights,
+                                                       const float *__restrict__ rgb_s,
+                                                       const float *__restrict__ g_color,
+                                                       const float *__restrict__ g_depth,
+                                                       const float *__restrict__ g_weights,
+                                                       const float *__restrict__ g_sdf,
+                                                       float *__restrict__ g_sdf_s, float *__restrict__ g_rgb_s) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int off = offsets[r], ns = ray_ns[r];
+    const float *z = z_vals + r * s_max;
+    const float *sd = sdf + r * s_max;
+    const float *wt = weights + r * s_max;
+    const float gr = g_color ? g_color[r * 3 + 0] : 0.f;
+    const float gg = g_color ? g_color[r * 3 + 1] : 0.f;
+    const float gb = g_color ? g_color[r * 3 + 2] : 0.f;
+    const float gdp = g_depth ? g_depth[r] : 0.f;
+    // dL/dW_s and Σ_s dL/dW_s · W_s
+    float dot = 0.f, tot = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        float gw = gdp * z[s] + (g_weights ? g_weights[r * s_max + s] : 0.f);
+        if (s < ns) {
+            const float *c = rgb_s + (int64_t)(off + s) * 3;
+            gw += gr * c[0] + gg * c[1] + gb * c[2];
+        }
+        dot += gw * wt[s];
+    }
+    dot = wsum(dot);
+    // T = Σ_kept u + 1e-8, the forward's normaliser (W_s = w_s / T); the
+    // kept set is recomputed from the padded sdf row exactly as the forward.
+    int first = s_max;
+    for (int s = lane; s < s_max; s += 64) {
+        if (s + 1 < s_max && sd[s + 1] * sd[s] < 0.0f) first = min(first, s);
+    }
+    first = wmin(first);
+    const float zmin = z[first == s_max ? 0 : first];
+    for (int s = lane; s < s_max; s += 64) {
+        const float a = sd[s] / tr;
+        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        tot += keep ? sigm(a) * sigm(-a) : 0.f;
+    }
+    tot = wsum(tot) + 1e-8f;
+    for (int s = lane; s < ns; s += 64) {
+        const float *c = rgb_s + (int64_t)(off + s) * 3;
+        const float W = wt[s];
+        float gw = gdp * z[s] + (g_weights ? g_weights[r * s_max + s] : 0.f) + gr * c[0] + gg * c[1] + gb * c[2];
+        const float a = sd[s] / tr;
+        const float sp = sigm(a), sn = sigm(-a);
+        const bool keep = z[s] < zmin + tr;
+        const float gu = keep ? (gw - dot) / tot : 0.f;
+        const float du = sp * sn * (sn - sp) / tr;
+        float gs = gu * du + (g_sdf ? g_sdf[r * s_max + s] : 0.f);
+        g_sdf_s[off + s] = gs;
+        float *gc = g_rgb_s + (int64_t)(off + s) * 3;
+        gc[0] = W * gr;
+        gc[1] = W * gg;
+        gc[2] = W * gb;
+    }
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int psvo_composite_fwd(void *stream, int64_t r_hit, int s_max, float truncation, const int *offsets,
+                                  const int *ray_ns, const float *z_vals, const float *sdf_s, const float *rgb_s,
+                                  float *sdf, float *weights, float *color, float *depth, float *z_min) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_fwd: bad sizes");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_composite_fwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+                       truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf, weights, color, depth, z_min);
+    return check_launch("composite_fwd");
+}
+
+extern "C" int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation, const int *offsets,
+                                  const int *ray_ns, const float *z_vals, const float *sdf, const float *weights,
+                                  const float *rgb_s, const float *grad_color, const float *grad_depth,
+                                  const float *grad_weights, const float *grad_sdf, float *grad_sdf_s,
+                                  float *grad_rgb_s) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_bwd: bad sizes");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_composite_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+                       truncation, offsets, ray_ns, z_vals, sdf, weights, rgb_s, grad_color, grad_depth,
+                       grad_weights, grad_sdf, grad_sdf_s, grad_rgb_s);
+    return check_launch("composite_bwd");
+}

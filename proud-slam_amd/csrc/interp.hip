@@ -1,0 +1,216 @@
+// Trilinear interpolation of per-vertex embeddings at ray samples, forward
+// and backward, on gfx950.
+//
+// Reference: render_helpers.py:104-156 (get_features_vox) with :86-99
+// (get_embeddings_vox), :67-83 (offset_points) and :46-59 (trilinear_interp);
+// the backward is what torch autograd derives for that graph
+// (embedding_dense_backward scatter + d/dx of the weights), plus the
+// broadcast backward of sampled_xyz = rays_o + rays_d * depth
+// (render_helpers.py:436-437).
+//
+//   x = o[ray] + d[ray] * t            (per valid sample, ray-major order)
+//   p = (x - centre[leaf]) / voxel + 0.5
+//   w_k = Π_a (q_ka ? p_a : 1 - p_a),   k = 4 ix + 2 iy + iz  (meshgrid 'ij')
+//   feat = Σ_k w_k E[vertex_idx[leaf, k]]
+//
+// Layout: embeddings are [E, 16] f32 = one 64-B row; four lanes own one
+// sample and each moves 16 B (dims 4q..4q+3), so a wave-instruction reads
+// sixteen 64-B rows — whole rows, never split across instructions.  The
+// backward runs one wave per ray: the ray's samples are contiguous, the
+// dL/dx reduction to d_o / d_d stays in registers (no atomics on rays), and
+// the embedding scatter uses global f32 atomics shaped as 64-B row segments.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+struct Corner {
+    float w[8];
+    float px, py, pz;
+};
+
+__device__ __forceinline__ void corner_weights(float px, float py, float pz, float w[8]) {
+    const float ax[2] = {1.0f - px, px};
+    const float ay[2] = {1.0f - py, py};
+    const float az[2] = {1.0f - pz, pz};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = (ax[(k >> 2) & 1] * ay[(k >> 1) & 1]) * az[k & 1];
+}
+
+__global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size, const int *__restrict__ leaf,
+                                                    const float *__restrict__ t,
+                                                    const int *__restrict__ ray_of_sample,
+                                                    const float *__restrict__ rays_o,
+                                                    const float *__restrict__ rays_d,
+                                                    const float *__restrict__ centres,
+                                                    const int *__restrict__ vertex_idx,
+                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = g >> 2;
+    const int q = (int)(g & 3);
+    if (s >= m) return;
+    const int lf = leaf[s];
+    const int r = ray_of_sample[s];
+    const float ts = t[s];
+    float p[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float x = rays_o[(int64_t)r * 3 + a] + rays_d[(int64_t)r * 3 + a] * ts;
+        p[a] = __fdiv_rn(x - centres[(int64_t)lf * 3 + a], voxel_size) + 0.5f;
+    }
+    float w[8];
+    corner_weights(p[0], p[1], p[2], w);
+    const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8);
+    const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8 + 4);
+    const int vid[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float4 e = emb[(int64_t)vid[k] * 4 + q];
+        acc.x = acc.x + w[k] * e.x;
+        acc.y = acc.y + w[k] * e.y;
+        acc.z = acc.z + w[k] * e.z;
+        acc.w = acc.w + w[k] * e.w;
+    }
+    feat[s * 4 + q] = acc;
+}
+
+// One wave per ray; 16 samples per pass, 4 lanes per sample.
+__global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
+                                                    const int *__restrict__ leaf, const float *__restrict__ t,
+                                                    const float *__restrict__ rays_o,
+                                                    const float *__restrict__ rays_d,
+                                                    const float *__restrict__ centres,
+                                                    const int *__restrict__ vertex_idx,
+                                                    const float4 *__restrict__ emb,
+                                                    const float4 *__restrict__ grad_feat,
+                                                    float *__restrict__ grad_emb, float *__restrict__ grad_o,
+                                                    float *__restrict__ grad_d) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int beg = offsets[r], end = offsets[r + 1];
+    const int q = lane & 3;
+    const int sub = lane >> 2;
+    float o[3], d[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        o[a] = rays_o[r * 3 + a];
+        d[a] = rays_d[r * 3 + a];
+    }
+    float go[3] = {0.f, 0.f, 0.f}, gd[3] = {0.f, 0.f, 0.f};
+    for (int base = beg; base < end; base += 16) {
+        const int s = base + sub;
+        const bool active = s < end;
+        float p[3] = {0.f, 0.f, 0.f};
+        float w[8];
+        int vid[8];
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        float ts = 0.f;
+        if (active) {
+            const int lf = leaf[s];
+            ts = t[s];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float x = o[a] + d[a] * ts;
+                p[a] = __fdiv_rn(x - centres[(int64_t)lf * 3 + a], voxel_size) + 0.5f;
+            }
+            const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8);
+            const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8 + 4);
+            vid[0] = v0.x; vid[1] = v0.y; vid[2] = v0.z; vid[3] = v0.w;
+            vid[4] = v1.x; vid[5] = v1.y; vid[6] = v1.z; vid[7] = v1.w;
+            g = grad_feat[(int64_t)s * 4 + q];
+        }
+        corner_weights(p[0], p[1], p[2], w);
+        // e_k · g over this lane's 4 dims, then reduced over the sample's 4 lanes
+        float eg[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float acc = 0.f;
+            if (active) {
+                const float4 e = emb[(int64_t)vid[k] * 4 + q];
+                acc = e.x * g.x + e.y * g.y + e.z * g.z + e.w * g.w;
+                float *dst = grad_emb + (int64_t)vid[k] * 16 + q * 4;
+                atomicAdd(dst + 0, w[k] * g.x);
+                atomicAdd(dst + 1, w[k] * g.y);
+                atomicAdd(dst + 2, w[k] * g.z);
+                atomicAdd(dst + 3, w[k] * g.w);
+            }
+            acc += __shfl_xor(acc, 1, 64);
+            acc += __shfl_xor(acc, 2, 64);
+            eg[k] = acc;
+        }
+        if (active && q == 0) {
+            const float ax[2] = {1.0f - p[0], p[0]};
+            const float ay[2] = {1.0f - p[1], p[1]};
+            const float az[2] = {1.0f - p[2], p[2]};
+            float dp[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int ix = (k >> 2) & 1, iy = (k >> 1) & 1, iz = k & 1;
+                const float sx = ix ? 1.f : -1.f, sy = iy ? 1.f : -1.f, sz = iz ? 1.f : -1.f;
+                dp[0] += sx * ay[iy] * az[iz] * eg[k];
+                dp[1] += sy * ax[ix] * az[iz] * eg[k];
+                dp[2] += sz * ax[ix] * ay[iy] * eg[k];
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float gx = __fdiv_rn(dp[a], voxel_size);
+                go[a] += gx;
+                gd[a] += gx * ts;
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float x = go[a], y = gd[a];
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            x += __shfl_xor(x, sh, 64);
+            y += __shfl_xor(y, sh, 64);
+        }
+        go[a] = x;
+        gd[a] = y;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            grad_o[r * 3 + a] = go[a];
+            grad_d[r * 3 + a] = gd[a];
+        }
+    }
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size, const int *leaf, const float *t,
+                               const int *ray_of_sample, const float *rays_o, const float *rays_d,
+                               const float *centres, const int *vertex_idx, const float *emb, float *feat) {
+    PSVO_REQUIRE(d == 16, "interp_fwd: embedding dim %d unsupported (16 only)", d);
+    PSVO_REQUIRE(m >= 0 && voxel_size > 0.f, "interp_fwd: bad sizes");
+    if (m == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
+                       t, ray_of_sample, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
+                       reinterpret_cast<float4 *>(feat));
+    return check_launch("interp_fwd");
+}
+
+extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets,
+                               const int *leaf, const float *t, const float *rays_o, const float *rays_d,
+                               const float *centres, const int *vertex_idx, const float *emb,
+                               const float *grad_feat, float *grad_emb, float *grad_o, float *grad_d) {
+    PSVO_REQUIRE(d == 16, "interp_bwd: embedding dim %d unsupported (16 only)", d);
+    PSVO_REQUIRE(r_hit >= 0 && voxel_size > 0.f, "interp_bwd: bad sizes");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_interp_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, voxel_size,
+                       offsets, leaf, t, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
+                       reinterpret_cast<const float4 *>(grad_feat), grad_emb, grad_o, grad_d);
+    return check_launch("interp_bwd");
+}

@@ -1,0 +1,33 @@
+// Internal helpers shared by the psvo HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/psvo.h"
+
+namespace psvo {
+
+// Set the thread-local error message; returns `code` for tail calls.
+int set_error(int code, const char *fmt, ...);
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Check the most recent launch.  Never exits the process (the reference's
+// CUDA_CHECK_ERRORS calls exit(-1), cuda_utils.h:37-48): the binding raises.
+int check_launch(const char *what);
+
+constexpr int kWave = 64;
+constexpr int kMaxHits = 50;        // voxel_helpers.py:561 (n_max hard-coded)
+constexpr int kSamplerG = 200;      // voxel_helpers.py:300
+constexpr int kSamplerChunk = 800;  // voxel_helpers.py:331 (4 * G)
+constexpr float kMaxDepthFill = 10.0f;  // voxel_helpers.py:24 MAX_DEPTH
+
+inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace psvo
+
+#define PSVO_REQUIRE(cond, ...)                                       \
+    do {                                                              \
+        if (!(cond)) return ::psvo::set_error(PSVO_E_INVALID, __VA_ARGS__); \
+    } while (0)

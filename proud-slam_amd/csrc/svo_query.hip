@@ -1,0 +1,603 @@
+// Ray / sparse-voxel-octree query on gfx950: DFS intersection, stable
+// depth sort, hit-ray ranking, inverse-CDF sampling and sample compaction.
+//
+// Reference behaviour restated (DARYL-GWZ/Proud-SLAM):
+//   intersect_gpu.cu:75-140   slab AABB test
+//   intersect_gpu.cu:191-270  DFS from node 0, children popped 7→0, ≤ n_max leaf hits
+//   voxel_helpers.py:557-595  sort by t_in, max_distance trim, P = max valid hits
+//   voxel_helpers.py:288-374  sampler host wrapper: G = 200 blocks × K' slots, 800-slot chunks
+//   sample_gpu.cu:133-239     inverse-CDF kernel incl. its layout-dependent trailing segment
+//   voxel_helpers.py:637-663  probs / steps, clamp + MAX_DEPTH fill
+//   render_helpers.py:390-460 ray and sample compaction
+//
+// MI355X design: one lane per ray (rays are independent and divergent); the
+// DFS keeps a per-level (node, remaining-children bitmask) stack and the
+// ≤50-entry hit list in LDS, laid out [slot][lane] so the 64 lanes of a wave
+// hit 64 distinct banks.  Per-launch statistics (P, R_hit, max steps, S_max,
+// M) are wave-reduced and published with one atomic per wave, so the host
+// reads them back once instead of the reference's sequence of host syncs.
+//
+// Arithmetic: traversal and sampler are compiled with FP contraction off and
+// IEEE division so hit indices and sample depths reproduce the CPU oracle
+// bit for bit (the reference CUDA uses __fdividef and nvcc's default FMA
+// contraction; see DESIGN.md "parity").
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+constexpr int kLevels = 16;  // octree depth <= 15 (grid_dim <= 32768)
+
+__device__ __forceinline__ bool ray_aabb(const float o[3], const float inv[3], float cx, float cy, float cz,
+                                         float half, float &t_lo, float &t_hi) {
+    float lo_all = 0.0f, hi_all = 100000.0f;
+    const float c[3] = {cx, cy, cz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float lo = (c[a] - half - o[a]) * inv[a];
+        float hi = (c[a] + half - o[a]) * inv[a];
+        if (hi < lo) {
+            const float tmp = lo;
+            lo = hi;
+            hi = tmp;
+        }
+        if (hi < lo_all) return false;
+        if (lo > hi_all) return false;
+        lo_all = (lo > lo_all) ? lo : lo_all;
+        hi_all = (hi < hi_all) ? hi : hi_all;
+        if (lo_all > hi_all) return false;
+    }
+    t_lo = lo_all;
+    t_hi = hi_all;
+    return true;
+}
+
+__device__ __forceinline__ int child_mask(const int *__restrict__ children, int node) {
+    const int *row = children + (int64_t)node * 9;
+    int m = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m |= (row[u] > -1) ? (1 << u) : 0;
+    return m;
+}
+
+// DFS of one ray over the flattened octree, emitting ≤ n_max leaf hits in
+// the reference order into the LDS-resident list (stride kWave).
+// Returns the number of AABB tests; *cnt the number of hits; *overflow if
+// the level stack would exceed kLevels.
+__device__ int dfs_ray(const float o[3], const float d[3], const float *__restrict__ points,
+                       const int *__restrict__ children, float half_voxel, int n_max, int *l_node, int *l_mask,
+                       int *h_idx, float *h_t0, float *h_t1, int *cnt_out, bool *overflow) {
+    float inv[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, d[a]);
+    int cnt = 0, visits = 0;
+    int lvl = -1;
+    {
+        float t0, t1;
+        const int side = children[8];
+        ++visits;
+        if (ray_aabb(o, inv, points[0], points[1], points[2], half_voxel * (float)side, t0, t1)) {
+            if (side == 1) {
+                h_idx[0] = 0;
+                h_t0[0] = t0;
+                h_t1[0] = t1;
+                cnt = 1;
+            } else {
+                lvl = 0;
+                l_node[0] = 0;
+                l_mask[0] = child_mask(children, 0);
+            }
+        }
+    }
+    while (lvl >= 0 && cnt < n_max) {
+        int m = l_mask[lvl * kWave];
+        if (m == 0) {
+            --lvl;
+            continue;
+        }
+        const int u = 31 - __clz(m);
+        l_mask[lvl * kWave] = m & ~(1 << u);
+        const int k = children[(int64_t)l_node[lvl * kWave] * 9 + u];
+        const float *pc = points + (int64_t)k * 3;
+        const int side = children[(int64_t)k * 9 + 8];
+        float t0, t1;
+        ++visits;
+        if (!ray_aabb(o, inv, pc[0], pc[1], pc[2], half_voxel * (float)side, t0, t1)) continue;
+        if (side == 1) {
+            h_idx[cnt * kWave] = k;
+            h_t0[cnt * kWave] = t0;
+            h_t1[cnt * kWave] = t1;
+            ++cnt;
+            continue;
+        }
+        if (lvl + 1 >= kLevels) {
+            *overflow = true;
+            break;
+        }
+        ++lvl;
+        l_node[lvl * kWave] = k;
+        l_mask[lvl * kWave] = child_mask(children, k);
+    }
+    *cnt_out = cnt;
+    return visits;
+}
+
+// ---------------------------------------------------------------------------
+// drop-in grid.svo_intersect: [b, m] rays against [b, n] trees.
+__global__ __launch_bounds__(64) void k_svo_intersect_raw(int b, int n, int m, float voxelsize, int n_max,
+                                                          const float *__restrict__ ray_start,
+                                                          const float *__restrict__ ray_dir,
+                                                          const float *__restrict__ points,
+                                                          const int *__restrict__ children, int *__restrict__ idx,
+                                                          float *__restrict__ min_depth,
+                                                          float *__restrict__ max_depth) {
+    __shared__ int l_node[kLevels * kWave];
+    __shared__ int l_mask[kLevels * kWave];
+    __shared__ int h_idx[kMaxHits * kWave];
+    __shared__ float h_t0[kMaxHits * kWave];
+    __shared__ float h_t1[kMaxHits * kWave];
+    const int lane = threadIdx.x;
+    const int64_t gid = (int64_t)blockIdx.x * kWave + lane;
+    if (gid >= (int64_t)b * m) return;
+    const int bi = (int)(gid / m);
+    const float o[3] = {ray_start[gid * 3 + 0], ray_start[gid * 3 + 1], ray_start[gid * 3 + 2]};
+    const float d[3] = {ray_dir[gid * 3 + 0], ray_dir[gid * 3 + 1], ray_dir[gid * 3 + 2]};
+    int cnt = 0;
+    bool overflow = false;
+    const int nm = n_max < kMaxHits ? n_max : kMaxHits;
+    dfs_ray(o, d, points + (int64_t)bi * n * 3, children + (int64_t)bi * n * 9, voxelsize * 0.5f, nm,
+            l_node + lane, l_mask + lane, h_idx + lane, h_t0 + lane, h_t1 + lane, &cnt, &overflow);
+    int *oi = idx + gid * n_max;
+    float *omin = min_depth + gid * n_max;
+    float *omax = max_depth + gid * n_max;
+    for (int l = 0; l < n_max; ++l) {
+        const bool v = l < cnt;
+        oi[l] = v ? h_idx[l * kWave + lane] : -1;
+        omin[l] = v ? h_t0[l * kWave + lane] : 0.0f;
+        omax[l] = v ? h_t1[l * kWave + lane] : 0.0f;
+    }
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v = max(v, __shfl_xor(v, s, kWave));
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, kWave);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// fused ray_intersect_vox: DFS → stable sort by t_in → max_distance trim,
+// plus per-ray Σ(t_out - t_in) for the sampler's probs / steps.
+__global__ __launch_bounds__(64) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
+                                                         const float *__restrict__ rays_d,
+                                                         const float *__restrict__ centres,
+                                                         const int *__restrict__ structure, float voxel_size,
+                                                         float max_distance, float step_size,
+                                                         int *__restrict__ hit_idx, float *__restrict__ hit_t0,
+                                                         float *__restrict__ hit_t1, int *__restrict__ ray_nv,
+                                                         float *__restrict__ ray_dsum, int *__restrict__ stats) {
+    __shared__ int l_node[kLevels * kWave];
+    __shared__ int l_mask[kLevels * kWave];
+    __shared__ int h_idx[kMaxHits * kWave];
+    __shared__ float h_t0[kMaxHits * kWave];
+    __shared__ float h_t1[kMaxHits * kWave];
+    const int lane = threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kWave + lane;
+    int nv = 0, visits = 0, ceil_steps = 0;
+    bool overflow = false;
+    if (r < n_rays) {
+        const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
+        const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
+        int *hi = h_idx + lane;
+        float *ha = h_t0 + lane;
+        float *hb = h_t1 + lane;
+        int cnt = 0;
+        visits = dfs_ray(o, d, centres, structure, voxel_size * 0.5f, kMaxHits, l_node + lane, l_mask + lane, hi,
+                         ha, hb, &cnt, &overflow);
+        // stable insertion sort by t_in (DFS emission order breaks ties)
+        for (int i = 1; i < cnt; ++i) {
+            const int ki = hi[i * kWave];
+            const float ka = ha[i * kWave], kb = hb[i * kWave];
+            int j = i - 1;
+            while (j >= 0 && ha[j * kWave] > ka) {
+                hi[(j + 1) * kWave] = hi[j * kWave];
+                ha[(j + 1) * kWave] = ha[j * kWave];
+                hb[(j + 1) * kWave] = hb[j * kWave];
+                --j;
+            }
+            hi[(j + 1) * kWave] = ki;
+            ha[(j + 1) * kWave] = ka;
+            hb[(j + 1) * kWave] = kb;
+        }
+        while (nv < cnt && !(ha[nv * kWave] > max_distance)) ++nv;
+        float dsum = 0.0f;
+        int *oi = hit_idx + r * kMaxHits;
+        float *oa = hit_t0 + r * kMaxHits;
+        float *ob = hit_t1 + r * kMaxHits;
+        for (int l = 0; l < kMaxHits; ++l) {
+            const bool v = l < nv;
+            const float a = v ? ha[l * kWave] : max_distance;
+            const float bb = v ? hb[l * kWave] : max_distance;
+            if (v) dsum = dsum + (bb - a);
+            oi[l] = v ? hi[l * kWave] : -1;
+            oa[l] = a;
+            ob[l] = bb;
+        }
+        ray_nv[r] = nv;
+        ray_dsum[r] = dsum;
+        if (nv > 0) ceil_steps = (int)ceilf(__fdiv_rn(dsum, step_size));
+    }
+    const int wmax_nv = wave_max(nv);
+    const int whit = wave_sum(nv > 0 ? 1 : 0);
+    const int wceil = wave_max(ceil_steps);
+    const int wvis = wave_sum(visits);
+    const int wov = wave_max(overflow ? 1 : 0);
+    if (lane == 0) {
+        atomicMax(stats + PSVO_STAT_P, wmax_nv);
+        atomicAdd(stats + PSVO_STAT_R_HIT, whit);
+        atomicMax(stats + PSVO_STAT_MAX_CEIL, wceil);
+        atomicAdd(stats + PSVO_STAT_VISITS, wvis);
+        if (wov) atomicOr(stats + 7, 1);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Single-workgroup exclusive scan (n ≲ 10^6): each thread owns a contiguous
+// run; run totals scanned in LDS.
+template <typename F>
+__device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *total) {
+    __shared__ int s_sum[1024];
+    const int tid = threadIdx.x;
+    const int nt = blockDim.x;
+    const int64_t per = (n + nt - 1) / nt;
+    const int64_t beg = tid * per;
+    const int64_t end = beg + per < n ? beg + per : n;
+    int local = 0;
+    for (int64_t i = beg; i < end; ++i) local += value(i);
+    s_sum[tid] = local;
+    __syncthreads();
+    for (int off = 1; off < nt; off <<= 1) {
+        const int v = tid >= off ? s_sum[tid - off] : 0;
+        __syncthreads();
+        s_sum[tid] += v;
+        __syncthreads();
+    }
+    int run = s_sum[tid] - local;
+    for (int64_t i = beg; i < end; ++i) {
+        out[i] = run;
+        run += value(i);
+    }
+    if (tid == nt - 1) *total = s_sum[tid];
+}
+
+__global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restrict__ ray_nv,
+                                                   int *__restrict__ ray_rank, int *__restrict__ rank_ray) {
+    __shared__ int total;
+    block_scan_runs(n, [&](int64_t i) { return ray_nv[i] > 0 ? 1 : 0; }, ray_rank, &total);
+    __syncthreads();
+    const int tid = threadIdx.x;
+    for (int64_t i = tid; i < n; i += blockDim.x) {
+        if (ray_nv[i] > 0) {
+            rank_ray[ray_rank[i]] = (int)i;
+        } else {
+            ray_rank[i] = -1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_counts(int64_t n, const int *__restrict__ counts,
+                                                      int *__restrict__ offsets) {
+    __shared__ int total;
+    block_scan_runs(n, [&](int64_t i) { return counts[i]; }, offsets, &total);
+    __syncthreads();
+    if (threadIdx.x == 0) offsets[n] = total;
+}
+
+// ---------------------------------------------------------------------------
+// Sampler core shared by the drop-in launch and the fused path.  `Rows`
+// abstracts where row elements come from: the drop-in kernel indexes a
+// contiguous chunk exactly like the reference; the fused kernel maps the
+// reference's logical [200, K', P] layout onto the compacted hit rays.
+struct RawRows {
+    const int *pts_idx;
+    const float *min_depth, *max_depth, *probs;
+    int H;
+    __device__ int idx_at(int elem_from_H) const { return pts_idx[H + elem_from_H]; }
+    __device__ int idx_slot0(int col) const { return pts_idx[col]; }
+    __device__ float lo_at(int e) const { return min_depth[H + e]; }
+    __device__ float hi_at(int e) const { return max_depth[H + e]; }
+    __device__ float prob_at(int e) const { return probs[H + e]; }
+};
+
+struct FusedRows {
+    const int *rank_ray;
+    const int *hit_idx;
+    const float *hit_t0, *hit_t1, *dsum;
+    int P, r_hit;
+    int own_row;   // logical row of this ray
+    int base_row;  // logical row of slot 0 of this chunk of this block
+    int jj;        // slot within the launch chunk
+    __device__ int real(int lrow) const { return lrow < r_hit ? lrow : 0; }
+    __device__ int64_t at(int elem_from_H) const {
+        const int e = jj * P + elem_from_H;
+        const int lrow = base_row + e / P;
+        const int col = e % P;
+        return (int64_t)rank_ray[real(lrow)] * kMaxHits + col;
+    }
+    __device__ int idx_at(int e) const { return hit_idx[at(e)]; }
+    __device__ int idx_slot0(int col) const { return hit_idx[(int64_t)rank_ray[real(base_row)] * kMaxHits + col]; }
+    __device__ float lo_at(int e) const { return hit_t0[at(e)]; }
+    __device__ float hi_at(int e) const { return hit_t1[at(e)]; }
+    __device__ float prob_at(int e) const {
+        const int64_t a = at(e);
+        const float dd = hit_idx[a] != -1 ? hit_t1[a] - hit_t0[a] : 0.0f;
+        return __fdiv_rn(dd, dsum[rank_ray[real(own_row)]]);
+    }
+};
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// inverse-CDF sampling of one ray; writes ≤ max_steps samples, returns count s.
+template <typename Rows, typename Noise, typename Emit>
+__device__ int sample_one(const Rows &rows, float steps_j, float fixed_step_size, int max_hits, int num_rays,
+                          int H, int max_steps, Noise noise, Emit emit) {
+    int bin = 0, s = 0;
+    float lo_depth = rows.lo_at(0);
+    float hi_depth = rows.hi_at(0);
+    float lo_cdf = 0.0f;
+    float hi_cdf = rows.prob_at(0);
+    float step = (float)(1.0 / (double)steps_j);
+    float z_low = lo_depth;
+    const int total_steps = (int)ceilf(steps_j);
+    bool done = false;
+    if (fixed_step_size > 0.0f) step = fixed_step_size;
+    for (int cs = 0; cs < total_steps; ++cs) {
+        const float cdf = ((float)cs + noise(cs)) * step;
+        while (cdf > hi_cdf) {
+            if (s < max_steps) emit(s, rows.idx_at(bin), (hi_depth + z_low) * 0.5f, hi_depth - z_low);
+            ++bin;
+            ++s;
+            if (bin >= max_hits || rows.idx_at(bin) == -1) {
+                done = true;
+                break;
+            }
+            lo_depth = rows.lo_at(bin);
+            hi_depth = rows.hi_at(bin);
+            lo_cdf = hi_cdf;
+            hi_cdf = hi_cdf + rows.prob_at(bin);
+            z_low = lo_depth;
+        }
+        if (done) break;
+        const float u = __fdiv_rn(cdf - lo_cdf, hi_cdf - lo_cdf);
+        const float z = lo_depth + u * (hi_depth - lo_depth);
+        if (s < max_steps) emit(s, rows.idx_at(bin), (z + z_low) * 0.5f, z - z_low);
+        z_low = z;
+        ++s;
+    }
+    // sample_gpu.cu:224-237 verbatim semantics (see svo_oracle.c)
+    while ((z_low < hi_depth) && (num_rays > (H + bin))) {
+        if (s < max_steps) emit(s, rows.idx_at(bin), (hi_depth + z_low) * 0.5f, hi_depth - z_low);
+        ++bin;
+        ++s;
+        if (bin >= max_hits || rows.idx_slot0(bin) == -1) break;
+        lo_depth = rows.lo_at(bin);
+        hi_depth = rows.hi_at(bin);
+        z_low = lo_depth;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(64) void k_sample_raw(int b, int num_rays, int max_hits, int max_steps,
+                                                   float fixed_step_size, const int *__restrict__ pts_idx,
+                                                   const float *__restrict__ min_depth,
+                                                   const float *__restrict__ max_depth,
+                                                   const float *__restrict__ noise, const float *__restrict__ probs,
+                                                   const float *__restrict__ steps, int *__restrict__ s_idx,
+                                                   float *__restrict__ s_depth, float *__restrict__ s_dist) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)b * num_rays) return;
+    const int bi = (int)(gid / num_rays);
+    const int j = (int)(gid % num_rays);
+    const int64_t blk_h = (int64_t)bi * num_rays * max_hits;
+    const int64_t blk_s = (int64_t)bi * num_rays * max_steps;
+    RawRows rows{pts_idx + blk_h, min_depth + blk_h, max_depth + blk_h, probs + blk_h, j * max_hits};
+    const int K = j * max_steps;
+    const float *nz = noise + blk_s + K;
+    int *oi = s_idx + blk_s + K;
+    float *od = s_depth + blk_s + K;
+    float *os = s_dist + blk_s + K;
+    sample_one(
+        rows, steps[(int64_t)bi * num_rays + j], fixed_step_size, max_hits, num_rays, j * max_hits, max_steps,
+        [&](int cs) { return nz[cs]; },
+        [&](int s, int v, float dep, float dis) {
+            oi[s] = v;
+            od[s] = dep;
+            os[s] = dis;
+        });
+}
+
+__global__ __launch_bounds__(64) void k_sample_fused(int64_t r_hit_cap, int max_steps_cap,
+                                                     const int *__restrict__ rank_ray,
+                                                     const int *__restrict__ hit_idx,
+                                                     const float *__restrict__ hit_t0,
+                                                     const float *__restrict__ hit_t1,
+                                                     const float *__restrict__ ray_dsum, float step_size,
+                                                     const float *__restrict__ noise, uint64_t seed,
+                                                     int *__restrict__ stats, int *__restrict__ s_idx,
+                                                     float *__restrict__ s_depth, float *__restrict__ s_dist,
+                                                     int *__restrict__ ray_ns) {
+    const int P = stats[PSVO_STAT_P];
+    const int r_hit = stats[PSVO_STAT_R_HIT];
+    const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * kWave + lane;
+    int count = 0;
+    if (i < r_hit && i < r_hit_cap && P > 0) {
+        if (max_steps > max_steps_cap && lane == 0) atomicOr(stats + 7, 2);
+        const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
+        const int b = i / kp;
+        const int j = i - b * kp;
+        const int c = j / kSamplerChunk;
+        const int jj = j - c * kSamplerChunk;
+        const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
+        FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj};
+        const float dsum = ray_dsum[rank_ray[i]];
+        const float steps_j = __fdiv_rn(dsum, step_size);
+        const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
+        int *oi = s_idx + (int64_t)i * max_steps_cap;
+        float *od = s_depth + (int64_t)i * max_steps_cap;
+        float *os = s_dist + (int64_t)i * max_steps_cap;
+        const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
+        const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
+        const int s_end = sample_one(
+            rows, steps_j, -1.0f, P, nr, jj * P, cap,
+            [&](int cs) {
+                if (nz) return nz[cs];
+                const float u = (float)(mix32(key + (uint64_t)cs) >> 8) * (1.0f / 16777216.0f);
+                return fminf(fmaxf(u, 0.001f), 0.999f);
+            },
+            [&](int s, int v, float dep, float dis) {
+                // voxel_helpers.py:654-656: clamp dists, MAX_DEPTH / 0 where idx == -1
+                oi[s] = v;
+                od[s] = v == -1 ? kMaxDepthFill : dep;
+                os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
+                count += (v != -1);
+            });
+        const int s_written = s_end < cap ? s_end : cap;
+        for (int s = s_written; s < max_steps_cap; ++s) {
+            oi[s] = -1;
+            od[s] = kMaxDepthFill;
+            os[s] = 0.0f;
+        }
+        ray_ns[i] = count;
+    }
+    const int wmax = wave_max(count);
+    const int wsum = wave_sum(count);
+    if (lane == 0) {
+        atomicMax(stats + PSVO_STAT_S_MAX, wmax);
+        atomicAdd(stats + PSVO_STAT_M, wsum);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// z_vals / mask [R_hit, S_max] and ray-major compacted samples.
+__global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__restrict__ s_idx,
+                                const float *__restrict__ s_depth, const int *__restrict__ ray_ns,
+                                const int *__restrict__ offsets, int *__restrict__ leaf, float *__restrict__ t,
+                                int *__restrict__ ray_of_sample, float *__restrict__ z_vals,
+                                uint8_t *__restrict__ mask) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= r_hit * s_max) return;
+    const int64_t r = e / s_max;
+    const int s = (int)(e - r * s_max);
+    const int v = s_idx[r * cap + s];
+    const float z = s_depth[r * cap + s];
+    z_vals[e] = z;
+    mask[e] = v != -1;
+    if (v != -1) {
+        const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
+        leaf[o] = v;
+        t[o] = z;
+        ray_of_sample[o] = (int)r;
+    }
+}
+
+}  // namespace
+
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int psvo_svo_intersect(void *stream, int b, int n, int m, float voxelsize, int n_max,
+                                  const float *ray_start, const float *ray_dir, const float *points,
+                                  const int *children, int *idx, float *min_depth, float *max_depth) {
+    PSVO_REQUIRE(b >= 0 && n > 0 && m >= 0 && n_max > 0, "svo_intersect: bad sizes b=%d n=%d m=%d n_max=%d", b, n, m,
+                 n_max);
+    PSVO_REQUIRE(n_max <= kMaxHits, "svo_intersect: n_max=%d exceeds %d", n_max, kMaxHits);
+    const int64_t total = (int64_t)b * m;
+    if (total == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_svo_intersect_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, n, m,
+                       voxelsize, n_max, ray_start, ray_dir, points, children, idx, min_depth, max_depth);
+    return check_launch("svo_intersect");
+}
+
+extern "C" int psvo_inverse_cdf_sampling(void *stream, int b, int num_rays, int max_hits, int max_steps,
+                                         float fixed_step_size, const int *pts_idx, const float *min_depth,
+                                         const float *max_depth, const float *uniform_noise, const float *probs,
+                                         const float *steps, int *sampled_idx, float *sampled_depth,
+                                         float *sampled_dists) {
+    PSVO_REQUIRE(b >= 0 && num_rays >= 0 && max_hits > 0 && max_steps > 0,
+                 "inverse_cdf_sampling: bad sizes b=%d num_rays=%d max_hits=%d max_steps=%d", b, num_rays, max_hits,
+                 max_steps);
+    const int64_t total = (int64_t)b * num_rays;
+    if (total == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_sample_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, num_rays,
+                       max_hits, max_steps, fixed_step_size, pts_idx, min_depth, max_depth, uniform_noise, probs,
+                       steps, sampled_idx, sampled_depth, sampled_dists);
+    return check_launch("inverse_cdf_sampling");
+}
+
+extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const float *rays_o, const float *rays_d,
+                                         const float *centres, const int *structure, float voxel_size,
+                                         float max_distance, float step_size, int *hit_idx, float *hit_t0,
+                                         float *hit_t1, int *ray_nv, float *ray_dsum, int *stats) {
+    PSVO_REQUIRE(n_rays >= 0, "ray_intersect_sorted: n_rays < 0");
+    PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
+    if (n_rays == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kWave)), dim3(kWave), 0, as_stream(stream), n_rays,
+                       rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
+                       ray_nv, ray_dsum, stats);
+    return check_launch("ray_intersect_sorted");
+}
+
+extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray) {
+    PSVO_REQUIRE(n_rays >= 0, "hit_rank: n_rays < 0");
+    if (n_rays == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_hit_rank, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_rank, rank_ray);
+    return check_launch("hit_rank");
+}
+
+extern "C" int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray,
+                                const int *hit_idx, const float *hit_t0, const float *hit_t1, const float *ray_dsum,
+                                float step_size, const float *noise, uint64_t seed, int *stats, int *s_idx,
+                                float *s_depth, float *s_dist, int *ray_ns) {
+    PSVO_REQUIRE(r_hit_cap >= 0 && max_steps_cap > 0, "sample_rays: bad caps");
+    if (r_hit_cap == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, kWave)), dim3(kWave), 0, as_stream(stream), r_hit_cap,
+                       max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
+                       s_idx, s_depth, s_dist, ray_ns);
+    return check_launch("sample_rays");
+}
+
+extern "C" int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets) {
+    PSVO_REQUIRE(n >= 0, "scan_counts: n < 0");
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, as_stream(stream), n, counts, offsets);
+    return check_launch("scan_counts");
+}
+
+extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int max_steps_cap, const int *s_idx,
+                                  const float *s_depth, const int *ray_ns, const int *offsets, int *leaf, float *t,
+                                  int *ray_of_sample, float *z_vals, uint8_t *mask) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max >= 0 && s_max <= max_steps_cap, "sample_points: bad sizes");
+    const int64_t total = r_hit * (int64_t)s_max;
+    if (total == 0) return PSVO_OK;
+    (void)ray_ns;
+    hipLaunchKernelGGL(k_sample_points, dim3(div_up(total, 256)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+                       max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask);
+    return check_launch("sample_points");
+}

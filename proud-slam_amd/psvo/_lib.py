@@ -1,0 +1,100 @@
+"""ctypes binding of libpsvo.so (include/psvo.h).
+
+The library is built in-tree (proud-slam_amd/lib/libpsvo.so, see
+csrc/Makefile).  There is NO fallback: if the library is missing or fails to
+load, every psvo entry point raises — the product path never silently runs
+PyTorch or CPU code in place of the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpsvo.so")
+
+_vp, _i32, _i64, _f32, _f64, _u64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float,
+                                      ctypes.c_double, ctypes.c_uint64)
+
+# name -> (restype, argtypes); mirrors include/psvo.h
+_SIGNATURES = {
+    "psvo_last_error": (ctypes.c_char_p, []),
+    "psvo_version": (ctypes.c_char_p, []),
+    "psvo_svo_intersect": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32] + [_vp] * 7),
+    "psvo_inverse_cdf_sampling": (_i32, [_vp, _i32, _i32, _i32, _i32, _f32] + [_vp] * 9),
+    "psvo_ray_intersect_sorted": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32] + [_vp] * 6),
+    "psvo_hit_rank": (_i32, [_vp, _i64, _vp, _vp, _vp]),
+    "psvo_sample_rays": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _u64, _vp, _vp, _vp, _vp,
+                                _vp]),
+    "psvo_scan_counts": (_i32, [_vp, _i64, _vp, _vp]),
+    "psvo_sample_points": (_i32, [_vp, _i64, _i32, _i32] + [_vp] * 9),
+    "psvo_interp_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 8),
+    "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 11),
+    "psvo_composite_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 10),
+    "psvo_composite_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
+    "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
+    "psvo_octree_free": (None, [_vp]),
+    "psvo_octree_insert": (_i32, [_vp, _vp, _i64]),
+    "psvo_octree_count": (_i64, [_vp]),
+    "psvo_octree_count_leaves": (_i64, [_vp]),
+    "psvo_octree_export": (_i32, [_vp, _vp, _vp, _vp]),
+    "psvo_octree_has_voxel": (_i32, [_vp, _i32, _i32, _i32]),
+    "psvo_octree_try_insert": (_f64, [_vp, _vp, _i64]),
+}
+
+_lib = None
+
+
+class PsvoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpsvo.so (after torch, so the HIP runtime is torch's)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PsvoError(f"libpsvo.so not built: {LIB_PATH} is missing (run `make -C proud-slam_amd/csrc` or "
+                            f"__graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().psvo_last_error().decode(errors="replace")
+        raise PsvoError(f"{name} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Device/host pointer of a tensor (None → NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    """Raw hipStream_t of torch's current stream on `device`."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device_tensor(t, name, dtype=None):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be a contiguous tensor")
+    if dtype is not None and t.dtype != dtype:
+        kind = {torch.float32: "float", torch.int32: "int"}.get(dtype, str(dtype))
+        raise RuntimeError(f"{name} must be a {kind} tensor")

@@ -1,0 +1,135 @@
+"""`svo.Octree` equivalent (torch.classes.svo.Octree, bindings.cpp:11-35) over
+libpsvo's C++ builder.
+
+Method names, argument meaning and outputs follow octree.cpp: node ids are
+creation order (root 0), get_centres_and_children() returns
+(voxels f32[N,4], children f32[N,8], features i32[N,8], pcd_xyz, pcd_color).
+Per-node point samples (octree.cpp:198-239, read only by the disabled
+get_features_pcd path, render_helpers.py:481) are not stored: the last two
+outputs are zero tensors of the reference's shapes.  Pickling replays the
+inserts like the reference's def_pickle (bindings.cpp:27-35).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+class Octree:
+    def __init__(self):
+        self._h = None
+        self._inserted = []
+        self.size = self.feat_dim = self.max_num = 0
+        self.voxel_size = 0.0
+
+    # octree.cpp:46-67
+    def init(self, grid_dim, feat_dim, voxel_size, max_num=8):
+        self.close()
+        h = L.lib().psvo_octree_new(int(grid_dim), int(feat_dim), float(voxel_size), int(max_num))
+        if not h:
+            raise RuntimeError(f"Octree.init: grid_dim must be a power of two >= 2 (got {grid_dim})")
+        self._h = h
+        self.size, self.feat_dim, self.voxel_size, self.max_num = int(grid_dim), int(feat_dim), float(voxel_size), int(max_num)
+        self._inserted = []
+
+    def _check(self):
+        if not self._h:
+            raise RuntimeError("Octree not initialized!")
+
+    @staticmethod
+    def _as_int3(pts):
+        a = pts.detach().cpu().numpy() if isinstance(pts, torch.Tensor) else np.asarray(pts)
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        if a.ndim != 2 or a.shape[1] != 3:
+            raise RuntimeError(f"Point dimensions mismatch: inputs are {a.shape[-1] if a.ndim else 0} expect 3")
+        return a
+
+    # octree.cpp:104-294
+    def insert(self, pts, color=None, pcd=None):
+        self._check()
+        a = self._as_int3(pts)
+        self._inserted.append(a)
+        L.call("psvo_octree_insert", self._h, a.ctypes.data_as(L._vp), int(a.shape[0]))
+
+    def try_insert(self, pts):
+        self._check()
+        a = self._as_int3(pts)
+        return float(L.lib().psvo_octree_try_insert(self._h, a.ctypes.data_as(L._vp), int(a.shape[0])))
+
+    def count_nodes(self):
+        self._check()
+        return int(L.lib().psvo_octree_count(self._h))
+
+    def count_leaf_nodes(self):
+        self._check()
+        return int(L.lib().psvo_octree_count_leaves(self._h))
+
+    def has_voxel(self, pts):
+        self._check()
+        p = pts.tolist() if isinstance(pts, torch.Tensor) else list(pts)
+        if len(p) != 3:
+            return False
+        return bool(L.lib().psvo_octree_has_voxel(self._h, int(p[0]), int(p[1]), int(p[2])))
+
+    def export_arrays(self):
+        """(voxels, children, features) as numpy arrays (host)."""
+        self._check()
+        n = self.count_nodes()
+        voxels = np.empty((n, 4), np.float32)
+        children = np.empty((n, 8), np.float32)
+        features = np.empty((n, 8), np.int32)
+        L.call("psvo_octree_export", self._h, voxels.ctypes.data_as(L._vp), children.ctypes.data_as(L._vp),
+               features.ctypes.data_as(L._vp))
+        return voxels, children, features
+
+    # octree.cpp:561-687
+    def get_centres_and_children(self):
+        v, c, f = self.export_arrays()
+        n = v.shape[0]
+        return (torch.from_numpy(v), torch.from_numpy(c), torch.from_numpy(f),
+                torch.zeros((n, self.max_num, 4), dtype=torch.float32),
+                torch.zeros((n, self.max_num, 3), dtype=torch.float32))
+
+    def get_leaf_voxels(self):
+        v, _, f = self.export_arrays()
+        return torch.from_numpy(v[f[:, 0] >= 0, :3].copy())
+
+    def close(self):
+        if self._h:
+            L.lib().psvo_octree_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __getstate__(self):
+        return (self.size, self.feat_dim, self.voxel_size, [a.copy() for a in self._inserted], self.max_num)
+
+    def __setstate__(self, state):
+        self._h = None
+        size, feat_dim, voxel_size, inserted, max_num = state
+        self.init(size, feat_dim, voxel_size, max_num)
+        for a in inserted:
+            self.insert(a)
+
+
+def map_states(tree: Octree, embeddings: torch.Tensor, voxel_size: float, device=None):
+    """Mapping.update_grid_pcd_features (mapping.py:300-406) without the
+    pointcloud fields: centres, [N,9] structure, vertex ids on `device`."""
+    voxels, children, features, pcd_xyz, pcd_color = tree.get_centres_and_children()
+    centres = (voxels[:, :3] + voxels[:, -1:] / 2) * voxel_size
+    structure = torch.cat([children, voxels[:, -1:]], -1).int()
+    dev = device if device is not None else embeddings.device
+    return {
+        "voxel_vertex_idx": features.to(dev),
+        "voxel_center_xyz": centres.float().to(dev),
+        "voxel_structure": structure.to(dev),
+        "voxel_vertex_emb": embeddings,
+        "pointclouds_xyz": pcd_xyz,
+        "pointclouds_color": pcd_color,
+    }

@@ -1,0 +1,371 @@
+"""MI355X render path with the reference's render_helpers API
+(src/variations/render_helpers.py): render_rays, get_features_vox,
+bundle_adjust_frames, track_frame, get_scores/eval_points helpers.
+
+render_rays (render_helpers.py:351-556) runs as:
+
+  ray_intersect_sorted  DFS + stable t_in sort + max_distance trim   (1 kernel)
+  hit_rank              compaction order of hit rays                  (1 kernel)
+  ── read back P, R_hit, max ceil(steps)  (sync 1; sizes the outputs) ──
+  sample_rays           inverse-CDF sampling, reference [200,K',P] layout
+  scan_counts           per-ray sample offsets
+  ── read back S_max, M  (sync 2; output shapes [R_hit, S_max]) ──
+  sample_points         z_vals / mask and ray-major compact samples
+  interp  (autograd)    x = o + d t, trilinear embedding gather   HIP fwd/bwd
+  decoder               the caller's sdf_network (MLP)
+  composite (autograd)  sdf→weights, rgb/depth                    HIP fwd/bwd
+
+The reference needs ~10 host syncs per call and copies the
+octree 256× per intersection; this path syncs twice and copies nothing.
+"""
+from __future__ import annotations
+
+import contextlib
+from copy import deepcopy
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _lib as L
+from .voxel_helpers import MAX_DEPTH, N_MAX_HITS, _intersect_sorted
+
+D_EMB = 16
+
+# Optional per-kernel HIP-event timer (bench.py installs one); called as a
+# context manager around individual launches on the current stream.
+KERNEL_TIMER = None
+
+
+def _timed(name):
+    if KERNEL_TIMER is None:
+        return contextlib.nullcontext()
+    return KERNEL_TIMER(name)
+
+
+def ray(ray_start, ray_dir, depths):
+    return ray_start + ray_dir * depths
+
+
+def fill_in(shape, mask, input, initial=1.0):
+    if isinstance(initial, torch.Tensor):
+        output = initial.expand(*shape)
+    else:
+        output = input.new_ones(*shape) * initial
+    return output.masked_scatter(mask.unsqueeze(-1).expand(*shape), input)
+
+
+def masked_scatter(mask, x):
+    B, K = mask.size()
+    if x.dim() == 1:
+        return x.new_zeros(B, K).masked_scatter(mask, x)
+    return x.new_zeros(B, K, x.size(-1)).masked_scatter(mask.unsqueeze(-1).expand(B, K, x.size(-1)), x)
+
+
+def masked_scatter_ones(mask, x):
+    B, K = mask.size()
+    if x.dim() == 1:
+        return x.new_ones(B, K).masked_scatter(mask, x)
+    return x.new_ones(B, K, x.size(-1)).masked_scatter(mask.unsqueeze(-1).expand(B, K, x.size(-1)), x)
+
+
+# --------------------------------------------------------------------------
+# autograd Functions over the HIP kernels
+# --------------------------------------------------------------------------
+class InterpSamples(Function):
+    """feat[M,16] = trilinear(E, x = o[ray] + d[ray] t) — get_features_vox
+    (render_helpers.py:104-156) fused with sampled_xyz (:436-437).
+    Backward: d_emb (float atomics), d_o / d_d per ray (wave reductions)."""
+
+    @staticmethod
+    def forward(ctx, ro_hit, rd_hit, emb, leaf, t, ray_of_sample, offsets, centres, vertex_idx, voxel_size):
+        M = leaf.numel()
+        feat = torch.empty((M, D_EMB), dtype=torch.float32, device=leaf.device)
+        with _timed("interp_fwd"):
+            L.call("psvo_interp_fwd", L.stream_of(leaf.device), M, D_EMB, float(voxel_size), L.ptr(leaf), L.ptr(t),
+                   L.ptr(ray_of_sample), L.ptr(ro_hit), L.ptr(rd_hit), L.ptr(centres), L.ptr(vertex_idx),
+                   L.ptr(emb), L.ptr(feat))
+        ctx.save_for_backward(ro_hit, rd_hit, emb, leaf, t, offsets, centres, vertex_idx)
+        ctx.voxel_size = float(voxel_size)
+        return feat
+
+    @staticmethod
+    def backward(ctx, grad_feat):
+        ro_hit, rd_hit, emb, leaf, t, offsets, centres, vertex_idx = ctx.saved_tensors
+        dev = leaf.device
+        r_hit = ro_hit.shape[0]
+        grad_feat = grad_feat.contiguous().float()
+        grad_emb = torch.zeros_like(emb)
+        grad_o = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
+        grad_d = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
+        with _timed("interp_bwd"):
+            L.call("psvo_interp_bwd", L.stream_of(dev), r_hit, D_EMB, ctx.voxel_size, L.ptr(offsets), L.ptr(leaf),
+                   L.ptr(t), L.ptr(ro_hit), L.ptr(rd_hit), L.ptr(centres), L.ptr(vertex_idx), L.ptr(emb),
+                   L.ptr(grad_feat), L.ptr(grad_emb), L.ptr(grad_o), L.ptr(grad_d))
+        return (grad_o if ctx.needs_input_grad[0] else None, grad_d if ctx.needs_input_grad[1] else None,
+                grad_emb if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None)
+
+
+class CompositeRays(Function):
+    """render_helpers.py:504-556: (sdf_s[M], rgb_s[M,3]) → padded sdf,
+    weights [R_hit,S_max], color [R_hit,3], depth [R_hit], z_min [R_hit,1]."""
+
+    @staticmethod
+    def forward(ctx, sdf_s, rgb_s, z_vals, offsets, ray_ns, truncation):
+        r_hit, s_max = z_vals.shape
+        dev = z_vals.device
+        sdf_s = sdf_s.contiguous().float()
+        rgb_s = rgb_s.contiguous().float()
+        sdf = torch.empty((r_hit, s_max), dtype=torch.float32, device=dev)
+        weights = torch.empty((r_hit, s_max), dtype=torch.float32, device=dev)
+        color = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
+        depth = torch.empty((r_hit,), dtype=torch.float32, device=dev)
+        z_min = torch.empty((r_hit, 1), dtype=torch.float32, device=dev)
+        L.call("psvo_composite_fwd", L.stream_of(dev), r_hit, s_max, float(truncation), L.ptr(offsets), L.ptr(ray_ns),
+               L.ptr(z_vals), L.ptr(sdf_s), L.ptr(rgb_s), L.ptr(sdf), L.ptr(weights), L.ptr(color), L.ptr(depth),
+               L.ptr(z_min))
+        ctx.save_for_backward(offsets, ray_ns, z_vals, sdf, weights, rgb_s)
+        ctx.truncation = float(truncation)
+        ctx.m = sdf_s.shape[0]
+        ctx.mark_non_differentiable(z_min)
+        return sdf, weights, color, depth, z_min
+
+    @staticmethod
+    def backward(ctx, g_sdf, g_weights, g_color, g_depth, g_zmin):
+        offsets, ray_ns, z_vals, sdf, weights, rgb_s = ctx.saved_tensors
+        r_hit, s_max = z_vals.shape
+        dev = z_vals.device
+        c = lambda g: None if g is None else g.contiguous().float()
+        g_sdf_s = torch.empty((ctx.m,), dtype=torch.float32, device=dev)
+        g_rgb_s = torch.empty((ctx.m, 3), dtype=torch.float32, device=dev)
+        L.call("psvo_composite_bwd", L.stream_of(dev), r_hit, s_max, ctx.truncation, L.ptr(offsets), L.ptr(ray_ns),
+               L.ptr(z_vals), L.ptr(sdf), L.ptr(weights), L.ptr(rgb_s), L.ptr(c(g_color)), L.ptr(c(g_depth)),
+               L.ptr(c(g_weights)), L.ptr(c(g_sdf)), L.ptr(g_sdf_s), L.ptr(g_rgb_s))
+        return g_sdf_s, g_rgb_s, None, None, None, None
+
+
+# --------------------------------------------------------------------------
+# query stages (no grad)
+# --------------------------------------------------------------------------
+class RaySamples:
+    """Everything the differentiable part needs about one ray batch."""
+
+    __slots__ = ("ray_mask", "rank_ray", "r_hit", "P", "s_max", "m", "z_vals", "sample_mask", "leaf", "t",
+                 "ray_of_sample", "offsets", "ray_ns", "s_idx", "s_depth", "s_dist", "visits", "max_steps")
+
+
+@torch.no_grad()
+def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise=None, seed=None):
+    """Intersection → sampling → compaction for rays_o/rays_d [1, R, 3]."""
+    dev = rays_o.device
+    q = _intersect_sorted(rays_o, rays_d, map_states["voxel_center_xyz"], map_states["voxel_structure"],
+                          voxel_size, max_distance, step_size)
+    R = q["R"]
+    ray_rank = torch.empty((R,), dtype=torch.int32, device=dev)
+    rank_ray = torch.empty((R,), dtype=torch.int32, device=dev)
+    stream = L.stream_of(dev)
+    L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
+    st = q["stats"].cpu()  # sync 1
+    P, r_hit, max_ceil, visits = int(st[0]), int(st[1]), int(st[2]), int(st[5])
+    if int(st[7]) & 1:
+        raise RuntimeError("octree deeper than the DFS level stack (15)")
+    assert r_hit > 0, "no ray hits the octree (render_helpers.py:388)"
+    max_steps = max_ceil + P
+    s_idx = torch.empty((r_hit, max_steps), dtype=torch.int32, device=dev)
+    s_depth = torch.empty((r_hit, max_steps), dtype=torch.float32, device=dev)
+    s_dist = torch.empty((r_hit, max_steps), dtype=torch.float32, device=dev)
+    ray_ns = torch.empty((r_hit,), dtype=torch.int32, device=dev)
+    offsets = torch.empty((r_hit + 1,), dtype=torch.int32, device=dev)
+    if noise is not None:
+        noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+        kp = (r_hit + 199) // 200
+        if tuple(noise.shape) != (200, kp, max_steps):
+            raise ValueError(f"noise must be [200, {kp}, {max_steps}], got {tuple(noise.shape)}")
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    L.call("psvo_sample_rays", stream, r_hit, max_steps, L.ptr(rank_ray), L.ptr(q["hit_idx"]), L.ptr(q["hit_t0"]),
+           L.ptr(q["hit_t1"]), L.ptr(q["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(q["stats"]),
+           L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns))
+    L.call("psvo_scan_counts", stream, r_hit, L.ptr(ray_ns), L.ptr(offsets))
+    st = q["stats"].cpu()  # sync 2
+    s_max, m = int(st[3]), int(st[4])
+    if int(st[7]) & 2:
+        raise RuntimeError("sampler exceeded max_steps")
+    leaf = torch.empty((m,), dtype=torch.int32, device=dev)
+    t = torch.empty((m,), dtype=torch.float32, device=dev)
+    ray_of_sample = torch.empty((m,), dtype=torch.int32, device=dev)
+    z_vals = torch.empty((r_hit, s_max), dtype=torch.float32, device=dev)
+    mask = torch.empty((r_hit, s_max), dtype=torch.uint8, device=dev)
+    L.call("psvo_sample_points", stream, r_hit, s_max, max_steps, L.ptr(s_idx), L.ptr(s_depth), L.ptr(ray_ns),
+           L.ptr(offsets), L.ptr(leaf), L.ptr(t), L.ptr(ray_of_sample), L.ptr(z_vals), L.ptr(mask))
+    out = RaySamples()
+    out.ray_mask = (ray_rank >= 0).view(1, R)
+    out.rank_ray = rank_ray[:r_hit].long()
+    out.r_hit, out.P, out.s_max, out.m, out.visits, out.max_steps = r_hit, P, s_max, m, visits, max_steps
+    out.z_vals, out.sample_mask = z_vals, mask.bool()
+    out.leaf, out.t, out.ray_of_sample, out.offsets, out.ray_ns = leaf, t, ray_of_sample, offsets, ray_ns
+    out.s_idx, out.s_depth, out.s_dist = s_idx, s_depth, s_dist
+    return out
+
+
+def render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxel_size, truncation, max_voxel_hit,
+                max_distance, chunk_size=10000, profiler=None, return_raw=False, noise=None, seed=None,
+                return_samples=False):
+    """render_helpers.py:351-556.  `noise` ([200, K', max_steps]) / `seed`
+    select the sampler's uniform noise; by default it is drawn on the device
+    from a seed taken from torch's CPU generator."""
+    if profiler is not None:
+        profiler.tick("ray_intersect")
+    smp = query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise, seed)
+    if profiler is not None:
+        profiler.tok("ray_intersect")
+    ro = rays_o.reshape(-1, 3)
+    rd = rays_d.reshape(-1, 3)
+    ro_hit = ro.index_select(0, smp.rank_ray).float().contiguous()
+    rd_hit = rd.index_select(0, smp.rank_ray).float().contiguous()
+    if smp.m == 0:
+        return None, 0
+    emb = map_states["voxel_vertex_emb"]
+    feats = InterpSamples.apply(ro_hit, rd_hit, emb, smp.leaf, smp.t, smp.ray_of_sample, smp.offsets,
+                                map_states["voxel_center_xyz"].float().contiguous(),
+                                map_states["voxel_vertex_idx"].int().contiguous(), voxel_size)
+    if profiler is not None:
+        profiler.tick("render_core")
+    field = sdf_network({"emb": feats, "dists": None})
+    if profiler is not None:
+        profiler.tok("render_core")
+    sdf, weights, color, depth, z_min = CompositeRays.apply(field["sdf"], field["color"], smp.z_vals, smp.offsets,
+                                                            smp.ray_ns, truncation)
+    out = {
+        "weights": weights,
+        "color": color,
+        "depth": depth,
+        "z_vals": smp.z_vals,
+        "sdf": sdf,
+        "ray_mask": smp.ray_mask,
+        "raw": z_min if return_raw else None,
+    }
+    if return_samples:
+        out["samples"] = smp
+    return out
+
+
+@torch.enable_grad()
+def get_features_vox(samples, map_states, voxel_size):
+    """render_helpers.py:104-156 for arbitrary sample points (mesh / eval).
+    sampled_point_xyz [M,3] is treated as o + 1·t with o = xyz, t = 0."""
+    xyz = samples["sampled_point_xyz"].float().contiguous()
+    idx = samples["sampled_point_voxel_idx"].int().contiguous()
+    M = xyz.shape[0]
+    dev = xyz.device
+    zeros = torch.zeros((M,), dtype=torch.float32, device=dev)
+    ray_of_sample = torch.arange(M, dtype=torch.int32, device=dev)
+    offsets = torch.arange(M + 1, dtype=torch.int32, device=dev)
+    feats = InterpSamples.apply(xyz, torch.ones_like(xyz), map_states["voxel_vertex_emb"], idx, zeros,
+                                ray_of_sample, offsets, map_states["voxel_center_xyz"].float().contiguous(),
+                                map_states["voxel_vertex_idx"].int().contiguous(), voxel_size)
+    return {"dists": samples.get("sampled_point_distance"), "emb": feats}
+
+
+@torch.no_grad()
+def get_scores(sdf_network, map_states, voxel_size, bits=8):
+    """render_helpers.py:243-294: decoder outputs on a bits³ grid per voxel."""
+    feats = map_states["voxel_vertex_idx"]
+    points = map_states["voxel_center_xyz"]
+    values = map_states["voxel_vertex_emb"]
+    chunk_size = 32
+    res = bits
+    lin = torch.linspace(-0.5, 0.5, res, device=points.device)
+    xx, yy, zz = torch.meshgrid(lin, lin, lin, indexing="ij")
+    grid_pts = torch.stack([xx, yy, zz], -1).float().reshape(1, -1, 3) * voxel_size
+    outs = []
+    for i in range(0, points.size(0), chunk_size):
+        p = points[i:i + chunk_size]
+        xyz = (grid_pts + p.unsqueeze(1)).reshape(-1, 3)
+        idx = torch.arange(i, i + p.size(0), device=points.device)[:, None].expand(p.size(0), res ** 3).reshape(-1)
+        fi = get_features_vox({"sampled_point_xyz": xyz, "sampled_point_voxel_idx": idx},
+                              {"voxel_vertex_idx": feats, "voxel_center_xyz": points, "voxel_vertex_emb": values},
+                              voxel_size)
+        outs.append(sdf_network.get_values(fi["emb"]).reshape(-1, res ** 3, 4).detach().cpu())
+    return torch.cat(outs, 0).view(-1, res, res, res, 4)
+
+
+@torch.no_grad()
+def eval_points(sdf_network, map_states, sampled_xyz, sampled_idx, voxel_size):
+    """render_helpers.py:297-328."""
+    sampled_idx = sampled_idx.reshape(-1)
+    sampled_xyz = sampled_xyz.reshape(-1, 3)
+    if sampled_xyz.shape[0] == 0:
+        return None
+    fi = get_features_vox({"sampled_point_xyz": sampled_xyz, "sampled_point_voxel_idx": sampled_idx}, map_states,
+                          voxel_size)
+    return sdf_network.get_values(fi["emb"]).reshape(-1, 4)[:, :3].detach().cpu()
+
+
+def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, voxel_size, step_size,
+                         N_rays=512, num_iterations=10, truncation=0.1, max_voxel_hit=10, max_distance=10,
+                         learning_rate=[1e-2, 5e-3], embed_optim=None, model_optim=None, resnet_optim=None,
+                         update_pose=True):
+    """render_helpers.py:559-676 — mapping's render-and-optimise loop."""
+    optimizers = [embed_optim]
+    if model_optim is not None:
+        optimizers += [model_optim]
+    if resnet_optim is not None:
+        optimizers += [resnet_optim]
+    for keyframe in keyframe_graph:
+        if keyframe.stamp != 0 and update_pose:
+            optimizers += [keyframe.optim]
+    for _ in range(num_iterations):
+        rays_o, rays_d, rgb_samples, depth_samples = [], [], [], []
+        for frame in keyframe_graph:
+            pose = frame.get_pose().cuda()
+            frame.sample_rays(N_rays)
+            sample_mask = frame.sample_mask.cuda()
+            sampled_rays_d = frame.rays_d[sample_mask].cuda()
+            R = pose[:3, :3].transpose(-1, -2)
+            sampled_rays_d = sampled_rays_d @ R
+            sampled_rays_o = pose[:3, 3].reshape(1, -1).expand_as(sampled_rays_d)
+            rays_d += [sampled_rays_d]
+            rays_o += [sampled_rays_o]
+            rgb_samples += [frame.rgb.cuda()[sample_mask]]
+            depth_samples += [frame.depth.cuda()[sample_mask]]
+        rays_d = torch.cat(rays_d, dim=0).unsqueeze(0)
+        rays_o = torch.cat(rays_o, dim=0).unsqueeze(0)
+        rgb_samples = torch.cat(rgb_samples, dim=0).unsqueeze(0)
+        depth_samples = torch.cat(depth_samples, dim=0).unsqueeze(0)
+        final_outputs = render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxel_size,
+                                    truncation, max_voxel_hit, max_distance)
+        loss, _ = loss_criteria(final_outputs, (rgb_samples, depth_samples))
+        for optim in optimizers:
+            optim.zero_grad()
+        loss.backward()
+        for optim in optimizers:
+            optim.step()
+
+
+def track_frame(frame_pose, curr_frame, map_states, sdf_network, resnet, loss_criteria, voxel_size, N_rays=512,
+                step_size=0.05, num_iterations=10, truncation=0.1, learning_rate=1e-3, max_voxel_hit=10,
+                max_distance=10, profiler=None, depth_variance=False):
+    """render_helpers.py:679-761 — pose-only optimisation of one frame."""
+    init_pose = deepcopy(frame_pose).cuda()
+    init_pose.requires_grad_(True)
+    optim = torch.optim.Adam(init_pose.parameters(), lr=learning_rate)
+    hit_mask = None
+    for it in range(num_iterations):
+        curr_frame.sample_rays(N_rays)
+        sample_mask = curr_frame.sample_mask
+        ray_dirs = curr_frame.rays_d[sample_mask].unsqueeze(0).cuda()
+        rgb = curr_frame.rgb[sample_mask].cuda()
+        depth = curr_frame.depth[sample_mask].cuda()
+        ray_dirs_iter = (ray_dirs.squeeze(0) @ init_pose.rotation().transpose(-1, -2)).unsqueeze(0)
+        ray_start_iter = init_pose.translation().reshape(1, 1, -1).expand_as(ray_dirs_iter).cuda().contiguous()
+        final_outputs = render_rays(ray_start_iter, ray_dirs_iter, map_states, sdf_network, resnet, step_size,
+                                    voxel_size, truncation, max_voxel_hit, max_distance,
+                                    profiler=profiler if it == 0 else None)
+        hit_mask = final_outputs["ray_mask"].view(N_rays)
+        final_outputs["ray_mask"] = hit_mask
+        loss, _ = loss_criteria(final_outputs, (rgb, depth), weight_depth_loss=depth_variance)
+        optim.zero_grad()
+        loss.backward()
+        optim.step()
+    return init_pose, optim, hit_mask

@@ -1,0 +1,93 @@
+"""CPU-side checks of the product library: it loads, exports every symbol
+include/psvo.h declares, and its CPU octree builder reproduces the oracle /
+golden node numbering and export exactly.  No GPU compute calls."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from psvo import _lib as L
+from psvo.octree import Octree, map_states
+from oracle import oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, "include", "psvo.h")).read()
+    return sorted(set(re.findall(r"\b(psvo_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.lib()
+    declared = _header_symbols()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(L.exported_symbols())
+    assert lib.psvo_version().decode().startswith("psvo")
+
+
+def test_library_links_torch_hip_runtime():
+    maps = open("/proc/self/maps").read()
+    libs = set(re.findall(r"\S*libamdhip64\S*", maps))
+    assert len(libs) <= 1, libs
+
+
+def test_octree_matches_golden(golden):
+    name, g = golden
+    t = Octree()
+    t.init(int(g["grid_dim"]), 16, 0.2, 8)
+    t.insert(torch.from_numpy(g["vox"]), None, None)
+    v, c, f = t.export_arrays()
+    np.testing.assert_array_equal(v, g["voxels"])
+    np.testing.assert_array_equal(c, g["children"])
+    np.testing.assert_array_equal(f, g["features"])
+    assert t.count_nodes() == g["voxels"].shape[0]
+    ms = map_states(t, torch.zeros(1), 0.2, device="cpu")
+    np.testing.assert_array_equal(ms["voxel_center_xyz"].numpy(), g["centres"])
+    np.testing.assert_array_equal(ms["voxel_structure"].numpy(), g["structure"])
+
+
+@pytest.mark.parametrize("grid_dim,n,seed", [(16, 40, 0), (64, 600, 1), (256, 3000, 2), (1024, 2000, 3)])
+def test_octree_matches_oracle_incremental(grid_dim, n, seed):
+    """Several insert() calls with duplicates and FEATURE→SURFACE promotion."""
+    rng = np.random.default_rng(seed)
+    vox = rng.integers(0, grid_dim - 1, size=(n, 3)).astype(np.int32)
+    vox = np.concatenate([vox, vox[: n // 4] + 1], 0).clip(0, grid_dim - 2).astype(np.int32)
+    t, o = Octree(), O.OracleOctree(grid_dim)
+    t.init(grid_dim, 16, 0.2, 8)
+    for part in np.array_split(vox, 3):
+        t.insert(part)
+        o.insert(part)
+    a, b = t.export_arrays(), o.export()
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert t.count_leaf_nodes() == int((b[2][:, 0] >= 0).sum())
+    assert t.has_voxel(vox[0].tolist())
+    assert 0.99 <= t.try_insert(vox[:10]) <= 1.0
+
+
+def test_octree_pickle_replays_inserts():
+    import pickle
+    rng = np.random.default_rng(5)
+    vox = rng.integers(0, 60, size=(200, 3)).astype(np.int32)
+    t = Octree()
+    t.init(64, 16, 0.2, 8)
+    t.insert(vox)
+    t2 = pickle.loads(pickle.dumps(t))
+    for x, y in zip(t.export_arrays(), t2.export_arrays()):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_grid_module_rejects_host_tensors():
+    import grid
+    x = torch.zeros(1, 4, 3)
+    with pytest.raises(RuntimeError, match="CUDA"):
+        grid.svo_intersect(x, x, torch.zeros(1, 2, 3), torch.zeros(1, 2, 9, dtype=torch.int32), 0.2, 50)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        grid.svo_intersect(x.transpose(1, 2), x, x, x, 0.2, 50)
+    with pytest.raises(NotImplementedError):
+        grid.ball_intersect(x, x, x, 0.1, 4)
