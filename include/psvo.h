@@ -23,7 +23,8 @@
  *   psvo_interp_fwd / _bwd        render_helpers.get_features_vox (render_helpers.py:104-156)
  *                                 forward and its autograd backward
  *   psvo_composite_fwd / _bwd     render_helpers.render_rays compositing (render_helpers.py:504-556)
- *   psvo_loss_*                   criterion.Criterion.forward (criterion.py:16-116)
+ *   psvo_mlp_fwd / _bwd           variations/nrgbd.Decoder forward + autograd backward
+ *                                 (nrgbd.py:80-146), fused fp32 MFMA
  *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
  *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
  */
@@ -137,6 +138,26 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
                        const int *ray_ns, const float *z_vals, const float *sdf, const float *weights,
                        const float *rgb_s, const float *grad_color, const float *grad_depth,
                        const float *grad_weights, const float *grad_sdf, float *grad_sdf_s, float *grad_rgb_s);
+
+/* ---- NRGBD decoder (nrgbd.py:80-146; width 128, in 16, depth 2) ------- */
+/* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
+ * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
+ * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied). */
+int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                 const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                 const float *b4, const float *w5, const float *b5, float *sdf, float *rgb);
+
+/* Floats of device workspace psvo_mlp_bwd needs for m samples. */
+int64_t psvo_mlp_workspace_floats(int64_t m, int n_split);
+
+/* Backward given g_sdf[M], g_rgb[M,3]: writes dfeat[M,16] and the 10
+ * parameter gradients (overwrite, or add when `accumulate`); split-K over
+ * n_split sample ranges with a deterministic slab reduction. */
+int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                 const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                 const float *b4, const float *w5, const float *b5, const float *g_sdf, const float *g_rgb,
+                 float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4,
+                 float *gb4, float *gw5, float *gb5, int accumulate, int n_split, float *workspace);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

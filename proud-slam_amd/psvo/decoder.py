@@ -5,14 +5,51 @@ embedder 'none', skips []:
   h = ReLU(L0(x)); h = ReLU(L1(h)); o = sdf_out(h) = [sdf | f(128)]
   rgb = σ(L5(ReLU(L4([f, x]))))
 
-forward/get_values run the layers with PyTorch-ROCm GEMMs (hipBLASLt);
-the render path calls forward({'emb': feats}) on all valid samples at once.
+On a GPU with width 128 (every Replica config) forward() runs the fused
+fp32-MFMA kernels of libpsvo (csrc/mlp.hip) through DecoderMLP; other widths
+(ScanNet/ARKit W=256) run the same layers as PyTorch-ROCm GEMMs.
+get_values() (mesh extraction, no grad) uses the PyTorch layers.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _lib as L
+
+
+class DecoderMLP(Function):
+    """(feat[M,16], W1,b1,...,W5,b5) → (sdf[M], rgb[M,3]) on libpsvo's fused
+    MFMA kernels; backward gives dfeat and all ten parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, feat, *params):
+        feat = feat.contiguous().float()
+        m = feat.shape[0]
+        dev = feat.device
+        sdf = torch.empty((m,), dtype=torch.float32, device=dev)
+        rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
+        ps = [p.contiguous() for p in params]
+        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb))
+        ctx.save_for_backward(feat, *ps)
+        return sdf, rgb
+
+    @staticmethod
+    def backward(ctx, g_sdf, g_rgb):
+        feat, *ps = ctx.saved_tensors
+        m = feat.shape[0]
+        dev = feat.device
+        g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
+        g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
+        n_split = max(1, min(256, (m + 2047) // 2048))
+        ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
+        dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
+        grads = [torch.empty_like(p) for p in ps]
+        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(g_sdf),
+               L.ptr(g_rgb), L.ptr(dfeat), *[L.ptr(g) for g in grads], 0, n_split, L.ptr(ws))
+        return (dfeat, *grads)
 
 
 class _Same(nn.Module):
@@ -54,6 +91,19 @@ class Decoder(nn.Module):
     def get_sdf(self, inputs):
         return self.get_values(inputs["emb"])[:, 3]
 
+    def fused_params(self):
+        l0, l1 = self.pts_linears
+        return [l0.weight, l0.bias, l1.weight, l1.bias, self.sdf_out.weight, self.sdf_out.bias,
+                self.color_out[0].weight, self.color_out[0].bias, self.color_out[2].weight, self.color_out[2].bias]
+
+    def can_fuse(self, x):
+        return (x.is_cuda and self.W == 128 and self.D == 2 and not self.skips and x.shape[-1] == 16
+                and self.sdf_out.out_features == 129)
+
     def forward(self, inputs):
-        out = self.get_values(inputs["emb"])
+        x = inputs["emb"]
+        if self.can_fuse(x):
+            sdf, rgb = DecoderMLP.apply(x, *self.fused_params())
+            return {"color": rgb, "sdf": sdf}
+        out = self.get_values(x)
         return {"color": out[:, :3], "sdf": out[:, 3]}

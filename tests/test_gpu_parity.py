@@ -183,13 +183,20 @@ def test_interp_matches_torch_fp32_reference():
     centres = (torch.rand(n_nodes, 3, device=DEV) * 4).float()
     vidx = torch.randint(0, 900, (n_nodes, 8), device=DEV, dtype=torch.int32)
     emb = torch.randn(900, 16, device=DEV, requires_grad=True)
-    ro = torch.rand(n_rays, 3, device=DEV, requires_grad=True)
-    rd = torch.rand(n_rays, 3, device=DEV, requires_grad=True)
     M = n_rays * per
     ray = torch.arange(n_rays, device=DEV, dtype=torch.int32).repeat_interleave(per)
     offsets = torch.arange(0, M + 1, per, device=DEV, dtype=torch.int32)
-    leaf = torch.randint(0, n_nodes, (M,), device=DEV, dtype=torch.int32)
+    # each ray crosses runs of samples inside 3 voxels (points stay inside
+    # their voxel: trilinear weights in [0, 1] as on the render path)
+    leaf = torch.randint(0, n_nodes, (n_rays, 3), device=DEV, dtype=torch.int32)
+    leaf = leaf.repeat_interleave(torch.tensor([12, 13, 12], device=DEV), dim=1).reshape(-1).contiguous()
+    ro = (centres[leaf.view(n_rays, per)[:, 0].long()] - 0.05).detach().requires_grad_(True)
+    rd = (torch.rand(n_rays, 3, device=DEV) * 0.02).requires_grad_(True)
     t = torch.rand(M, device=DEV) * 3
+    # move each sample's leaf centre so that x = o + d t sits inside it
+    x_s = (ro[ray.long()] + rd[ray.long()] * t[:, None]).detach()
+    centres = centres.clone()
+    centres[leaf.long()] = x_s + (torch.rand(M, 3, device=DEV) - 0.5) * 0.15
     feat = InterpSamples.apply(ro, rd, emb, leaf, t, ray, offsets, centres, vidx, 0.2)
     gout = torch.randn_like(feat)
     (feat * gout).sum().backward()
