@@ -142,22 +142,27 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
 /* ---- NRGBD decoder (nrgbd.py:80-146; width 128, in 16, depth 2) ------- */
 /* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
  * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
- * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied). */
+ * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
+ * Training mode: act f32[4][M][128] (h1, h2, f, c1) and masks u64[M][2][3]
+ * (ReLU masks) are written for psvo_mlp_bwd; pass NULL for both otherwise. */
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                 const float *b4, const float *w5, const float *b5, float *sdf, float *rgb);
+                 const float *b4, const float *w5, const float *b5, float *sdf, float *rgb, float *act,
+                 uint64_t *masks);
 
 /* Floats of device workspace psvo_mlp_bwd needs for m samples. */
 int64_t psvo_mlp_workspace_floats(int64_t m, int n_split);
 
-/* Backward given g_sdf[M], g_rgb[M,3]: writes dfeat[M,16] and the 10
- * parameter gradients (overwrite, or add when `accumulate`); split-K over
- * n_split sample ranges with a deterministic slab reduction. */
+/* Backward given g_sdf[M], g_rgb[M,3] and the training forward's rgb / act /
+ * masks: writes dfeat[M,16] and the 10 parameter gradients (overwrite, or
+ * add when `accumulate`); split-K over ~n_split sample ranges with a
+ * deterministic slab reduction. */
 int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                 const float *b4, const float *w5, const float *b5, const float *g_sdf, const float *g_rgb,
-                 float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4,
-                 float *gb4, float *gw5, float *gb5, int accumulate, int n_split, float *workspace);
+                 const float *b4, const float *w5, const float *b5, const float *rgb, const float *act,
+                 const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1,
+                 float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5,
+                 int accumulate, int n_split, float *workspace);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

@@ -218,9 +218,14 @@ __device__ __forceinline__ void load_x(const float *__restrict__ feat, int64_t s
 }
 
 // ---------------------------------------------------------------------------
-// forward: feat[M,16] → sdf[M], rgb[M,3]
+// forward: feat[M,16] → sdf[M], rgb[M,3].  Training mode (act != null) also
+// stores the row-major activations the weight gradients need
+// (act = [h1 | h2 | f | c1], each [M][128]) and the ReLU masks of h1, h2, c1
+// (masks [M][2][3] u64: lane-half h of sample s holds bits of its 64
+// features), so the backward never re-runs the forward.
 __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float *__restrict__ feat, MlpParams p,
-                                                         float *__restrict__ sdf_out, float *__restrict__ rgb_out) {
+                                                         float *__restrict__ sdf_out, float *__restrict__ rgb_out,
+                                                         float *__restrict__ act, uint64_t *__restrict__ masks) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *wl = lds + kOffW;
     const int lane = threadIdx.x & 63;
@@ -228,6 +233,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     const int h = lane >> 5;
     const int64_t s = (int64_t)blockIdx.x * kTile + wave * 32 + (lane & 31);
     const bool valid = s < m;
+    const bool save = act != nullptr;
     float x[8];
     load_x(feat, s, valid, h, x);
     stage_vectors(lds, p);
@@ -236,26 +242,38 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     f32x16 a[kNB], bacc[kNB];
     init_bias(a, lds + kOffB1, h);
     gemm_x(wl, x, a, lane);
-    relu(a);  // h1
+    const uint64_t m1 = relu(a);  // h1
+    if (save) store_rows(act, s, valid, 128, a, h);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w2, 128, 128, 0, 128);
     __syncthreads();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    relu(bacc);  // h2
+    const uint64_t m2 = relu(bacc);  // h2
+    if (save) store_rows(act + m * 128, s, valid, 128, bacc, h);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w3, 128, 128, 1, 128);  // rows 1..128 → f
     __syncthreads();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
+    if (save) store_rows(act + 2 * m * 128, s, valid, 128, a, h);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w4, 128, 144, 0, 128);  // [f | x]
     __syncthreads();
     init_bias(bacc, lds + kOffB4, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
-    relu(bacc);  // c1
+    const uint64_t m4 = relu(bacc);  // c1
+    if (save) {
+        store_rows(act + 3 * m * 128, s, valid, 128, bacc, h);
+        if (valid) {
+            uint64_t *mk = masks + (s * 2 + h) * 3;
+            mk[0] = m1;
+            mk[1] = m2;
+            mk[2] = m4;
+        }
+    }
     float rgb[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
@@ -268,20 +286,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
 }
 
 // ---------------------------------------------------------------------------
-// backward (data): recompute the forward, then chain the δ's down to dx.
-// Writes the row-major operands of the weight gradients:
-//   A1 = h1, A2 = h2, A3 = f, A4 = c1           [M][128]
-//   D1 = δh1, D2 = δh2, D3 = δf, D4 = δc1       [M][128]   (post-ReLU-mask)
-//   D5 = δ(rgb logits) [M][3];  dfeat [M][16]
+// backward (data): chain the δ's from (g_sdf, g_rgb) down to dx using the
+// forward's rgb and ReLU masks.  Writes the row-major δ operands of the
+// weight gradients: D1 = δh1, D2 = δh2, D3 = δf, D4 = δc1 [M][128] (post
+// mask), D5 = δ(rgb logits) [M][3], and dfeat [M][16].
 struct BwdOut {
-    float *a1, *a2, *a3, *a4, *d1, *d2, *d3, *d4, *d5, *dfeat;
+    float *d1, *d2, *d3, *d4, *d5, *dfeat;
 };
 
 constexpr int kThreadsBwd = 512;
 constexpr int kTileBwd = 256;
 
-__global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, const float *__restrict__ feat,
-                                                                 MlpParams p, const float *__restrict__ g_sdf,
+__global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpParams p,
+                                                                 const float *__restrict__ rgb_in,
+                                                                 const uint64_t *__restrict__ masks,
+                                                                 const float *__restrict__ g_sdf,
                                                                  const float *__restrict__ g_rgb, BwdOut o) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *wl = lds + kOffW;
@@ -290,51 +309,31 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, cons
     const int h = lane >> 5;
     const int64_t s = (int64_t)blockIdx.x * kTileBwd + wave * 32 + (lane & 31);
     const bool valid = s < m;
-    float x[8];
-    load_x(feat, s, valid, h, x);
-    stage_vectors(lds, p);
-    // ---- recompute forward
-    stage_fwd<kThreadsBwd>(wl, p.w1, 128, 16, 0, 0);
-    __syncthreads();
-    f32x16 a[kNB], bacc[kNB];
-    init_bias(a, lds + kOffB1, h);
-    gemm_x(wl, x, a, lane);
-    const uint64_t m1 = relu(a);
-    store_rows(o.a1, s, valid, 128, a, h);
-    __syncthreads();
-    stage_fwd<kThreadsBwd>(wl, p.w2, 128, 128, 0, 128);
-    __syncthreads();
-    init_bias(bacc, lds + kOffB2, h);
-    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    const uint64_t m2 = relu(bacc);
-    store_rows(o.a2, s, valid, 128, bacc, h);
-    __syncthreads();
-    stage_fwd<kThreadsBwd>(wl, p.w3, 128, 128, 1, 128);
-    __syncthreads();
-    init_bias(a, lds + kOffB3 + 1, h);
-    gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    store_rows(o.a3, s, valid, 128, a, h);
-    __syncthreads();
-    stage_fwd<kThreadsBwd>(wl, p.w4, 128, 144, 0, 128);
-    __syncthreads();
-    init_bias(bacc, lds + kOffB4, h);
-    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
-    const uint64_t m4 = relu(bacc);  // c1
-    store_rows(o.a4, s, valid, 128, bacc, h);
-    float d5[3];
+    uint64_t m1 = 0, m2 = 0, m4 = 0;
+    float d5[3] = {0.f, 0.f, 0.f};
+    float dsdf = 0.0f;
+    if (valid) {
+        const uint64_t *mk = masks + (s * 2 + h) * 3;
+        m1 = mk[0];
+        m2 = mk[1];
+        m4 = mk[2];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float y = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
-        const float g = valid ? g_rgb[s * 3 + c] : 0.0f;
-        d5[c] = g * (y * (1.0f - y));
+        for (int c = 0; c < 3; ++c) {
+            const float y = rgb_in[s * 3 + c];
+            d5[c] = g_rgb[s * 3 + c] * (y * (1.0f - y));  // sigmoid backward
+        }
+        dsdf = g_sdf[s];
     }
     if (valid && h == 0) {
         o.d5[s * 3 + 0] = d5[0];
         o.d5[s * 3 + 1] = d5[1];
         o.d5[s * 3 + 2] = d5[2];
     }
-    // ---- δc1 = W5ᵀ δ5 ⊙ mask   (VALU)
+    stage_vectors(lds, p);
+    // ---- δc1 = W5ᵀ δ5 ⊙ mask (VALU); overlap with the W4ᵀ staging
+    stage_bwd<kThreadsBwd>(wl, p.w4, 128, 144, 0, 5);
+    __syncthreads();
+    f32x16 a[kNB], bacc[kNB];
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
@@ -345,9 +344,6 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, cons
         }
     store_rows(o.d4, s, valid, 128, bacc, h);
     // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
-    __syncthreads();
-    stage_bwd<kThreadsBwd>(wl, p.w4, 128, 144, 0, 5);
-    __syncthreads();
     f32x16 t5[5];
     zero(t5);
     gemm_acc<kNB, 5>(wl, bacc, t5, lane);
@@ -357,7 +353,6 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, cons
 #pragma unroll
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
     store_rows(o.d3, s, valid, 128, a, h);
-    const float dsdf = valid ? g_sdf[s] : 0.0f;
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w3, 128, 128, 1, 4);
@@ -396,118 +391,169 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, cons
 
 // ---------------------------------------------------------------------------
 // backward (weights): dW[rows][cols] = Σ_s D[s][row] · A[s][col], db = Σ_s D[s].
-// Split-K over samples; each workgroup writes a private slab (fixed-order,
-// deterministic reduction in k_mlp_dw_reduce).
-struct DwLayer {
-    const float *D;   // [M][ldD], rows [d_row0, rows)
-    const float *D0;  // optional row 0 column (δsdf) → D rows start at 1
-    int ldD, rows;
-    const float *A;   // [M][ldA], first a_cols columns
-    const float *A2;  // [M][16] extra columns (x)
-    int ldA, a_cols, cols;
-    int slab_off;     // offset of this layer's (rows*cols + rows) in a slab
-};
-struct DwArgs {
-    DwLayer L[5];
-    int slab_stride;
+// One workgroup = one (layer, sample-range); 64-sample chunks of D and A are
+// staged into LDS with 16-B loads (two workgroups per CU overlap one's loads
+// with the other's MFMAs); each wave accumulates its 32x32 blocks of C across
+// the whole range in registers and writes them once to a private slab, which
+// k_mlp_dw_reduce sums in a fixed order (bitwise reproducible).
+//
+// Layers (C rows x cols; D and A sources):
+//   0: W1 128x16   D1 | feat          3: W4 128x144  D4 | [f, feat]
+//   1: W2 128x128  D2 | h1            4: W5 3x128    D5 | c1
+//   2: W3 129x128  [g_sdf, D3] | h2   (C row 0 = sdf row: LDS block 4)
+struct DwSrc {
+    const float *D[5];
+    const float *A[5];
+    const float *feat, *g_sdf;
 };
 
-constexpr int kDwChunk = 32;
-constexpr int kDwLd = 160;  // padded LDS row (5 blocks)
+constexpr int kDwS = 64;         // samples per staged chunk
+constexpr int kDwLd = 160;       // LDS row pitch (5 blocks of 32)
 
-__global__ __launch_bounds__(256) void k_mlp_dw(int64_t m, DwArgs args, int n_split, float *__restrict__ slabs) {
-    __shared__ __attribute__((aligned(16))) float Dl[kDwChunk * kDwLd];
-    __shared__ __attribute__((aligned(16))) float Al[kDwChunk * kDwLd];
-    const DwLayer &L = args.L[blockIdx.y];
-    const int split = blockIdx.x;
+template <int RB, int CB>
+__device__ __forceinline__ void dw_mfma(const float *Dl, const float *Al, f32x16 (&acc)[5], int wave, int h, int i) {
+#pragma unroll
+    for (int t = 0; t < kDwS / 2; ++t) {
+        const int row = (2 * t + h) * kDwLd;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int bid = wave + 4 * j;
+            if (bid < RB * CB) {
+                const int rb = bid / CB, cb = bid % CB;
+                acc[j] = mfma(Dl[row + 32 * rb + i], Al[row + 32 * cb + i], acc[j]);
+            }
+        }
+    }
+}
+
+// rows [s0, s0 + kDwS) of a row-major [M][ld] source, columns [0, n) (n % 4
+// == 0, ld % 4 == 0) → LDS rows at column offset `col0`; zero beyond M.
+__device__ __forceinline__ void stage_v4(float *dst, int col0, const float *__restrict__ src, int ld, int n,
+                                         int64_t s0, int64_t m) {
+    const int per_row = n >> 2;
+    for (int e = threadIdx.x; e < kDwS * per_row; e += 256) {
+        const int ss = e / per_row, c4 = e - ss * per_row;
+        const int64_t sg = s0 + ss;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (sg < m) v = *reinterpret_cast<const float4 *>(src + sg * ld + 4 * c4);
+        *reinterpret_cast<float4 *>(dst + ss * kDwLd + col0 + 4 * c4) = v;
+    }
+}
+__device__ __forceinline__ void stage_scalar(float *dst, int col0, const float *__restrict__ src, int ld, int n,
+                                             int64_t s0, int64_t m) {
+    for (int e = threadIdx.x; e < kDwS * n; e += 256) {
+        const int ss = e / n, c = e - ss * n;
+        const int64_t sg = s0 + ss;
+        dst[ss * kDwLd + col0 + c] = sg < m ? src[sg * ld + c] : 0.0f;
+    }
+}
+// zero columns [c0, c1) of every staged row
+__device__ __forceinline__ void zero_cols(float *dst, int c0, int c1) {
+    const int w = c1 - c0;
+    for (int e = threadIdx.x; e < kDwS * w; e += 256) dst[(e / w) * kDwLd + c0 + e % w] = 0.0f;
+}
+
+template <int L>
+__device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab, float *Dl,
+                                         float *Al) {
+    constexpr int RB = (L == 2) ? 5 : (L == 4 ? 1 : 4);
+    constexpr int CB = (L == 0) ? 1 : (L == 3 ? 5 : 4);
+    constexpr int ROWS = (L == 2) ? 129 : (L == 4 ? 3 : 128);
+    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
-    const int RB = (L.rows + 31) >> 5, CB = (L.cols + 31) >> 5;
-    const int nblk = RB * CB;
-    const int64_t n_chunks = (m + kDwChunk - 1) / kDwChunk;
+    const int64_t n_chunks = (m + kDwS - 1) / kDwS;
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
     f32x16 acc[5];
     zero(acc);
     float bias = 0.0f;
-    const int d_shift = L.D0 ? 1 : 0;
+    // one-time zero of padding columns that staging never writes
+    if (L == 0) zero_cols(Al, 16, 32);
+    if (L == 2) zero_cols(Dl, 129, 160);
+    if (L == 3) zero_cols(Al, 144, 160);
+    if (L == 4) zero_cols(Dl, 3, 32);
     for (int64_t c = c_beg; c < c_end; ++c) {
-        const int64_t s0 = c * kDwChunk;
+        const int64_t s0 = c * kDwS;
         __syncthreads();
-        for (int e = threadIdx.x; e < kDwChunk * kDwLd; e += 256) {
-            const int ss = e / kDwLd, col = e - ss * kDwLd;
-            const int64_t sg = s0 + ss;
-            float dv = 0.0f, av = 0.0f;
-            if (sg < m) {
-                if (col < L.rows) {
-                    if (d_shift && col == 0)
-                        dv = L.D0[sg];
-                    else
-                        dv = L.D[sg * L.ldD + col - d_shift];
-                }
-                if (col < L.a_cols)
-                    av = L.A[sg * L.ldA + col];
-                else if (col < L.cols)
-                    av = L.A2[sg * 16 + (col - L.a_cols)];
-            }
-            Dl[e] = dv;
-            Al[e] = av;
-        }
+        if (L == 4) stage_scalar(Dl, 0, src.D[4], 3, 3, s0, m);
+        else stage_v4(Dl, 0, src.D[L], 128, 128, s0, m);
+        if (L == 2) stage_scalar(Dl, 128, src.g_sdf, 1, 1, s0, m);
+        if (L == 0) stage_v4(Al, 0, src.feat, 16, 16, s0, m);
+        else stage_v4(Al, 0, src.A[L], 128, 128, s0, m);
+        if (L == 3) stage_v4(Al, 128, src.feat, 16, 16, s0, m);
         __syncthreads();
-        if (threadIdx.x < L.rows) {
+        if (threadIdx.x < ROWS) {
+            // C row r ← LDS column (layer 2: row 0 is column 128, rows 1.. are 0..)
+            const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
 #pragma unroll 8
-            for (int ss = 0; ss < kDwChunk; ++ss) bias += Dl[ss * kDwLd + threadIdx.x];
+            for (int ss = 0; ss < kDwS; ++ss) bias += Dl[ss * kDwLd + col];
         }
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int bid = wave + 4 * j;
-            if (bid < nblk) {
-                const int rb = bid / CB, cb = bid - rb * CB;
-#pragma unroll 4
-                for (int t = 0; t < kDwChunk / 2; ++t) {
-                    const int row = 2 * t + h;
-                    acc[j] = mfma(Dl[row * kDwLd + 32 * rb + i], Al[row * kDwLd + 32 * cb + i], acc[j]);
-                }
-            }
-        }
+        dw_mfma<RB, CB>(Dl, Al, acc, wave, h, i);
     }
-    float *slab = slabs + (int64_t)split * args.slab_stride + L.slab_off;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const int bid = wave + 4 * j;
-        if (bid < nblk) {
-            const int rb = bid / CB, cb = bid - rb * CB;
+        if (bid < RB * CB) {
+            const int rb = bid / CB, cb = bid % CB;
             const int col = 32 * cb + i;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = 32 * rb + phi(r, h);
-                if (row < L.rows && col < L.cols) slab[row * L.cols + col] = acc[j][r];
+                const int lr = 32 * rb + phi(r, h);  // LDS column of D
+                int row;
+                if (L == 2) row = lr == 128 ? 0 : (lr < 128 ? lr + 1 : -1);
+                else row = lr < ROWS ? lr : -1;
+                if (row >= 0 && col < COLS) slab[row * COLS + col] = acc[j][r];
             }
         }
     }
-    if (threadIdx.x < L.rows) slab[L.rows * L.cols + threadIdx.x] = bias;
+    if (threadIdx.x < ROWS) slab[ROWS * COLS + threadIdx.x] = bias;
 }
 
-// grads[e] = Σ_split slabs[split][e], e over the packed (W, b) of all layers,
-// scattered to the five (weight, bias) gradient buffers.
-struct DwDst {
-    float *w[5], *b[5];
-    int off[5], rows[5], cols[5];
+struct DwGrid {
+    int wg_begin[6];  // prefix over layers of split counts
+    int slab_off[5];  // float offset of layer l's first slab
+    int slab_len[5];  // rows*cols + rows
 };
 
-__global__ void k_mlp_dw_reduce(int n_split, int slab_stride, const float *__restrict__ slabs, DwDst dst,
-                                int accumulate) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= slab_stride) return;
-    float v = 0.0f;
-    for (int sp = 0; sp < n_split; ++sp) v += slabs[(int64_t)sp * slab_stride + e];
+__global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * kDwS * kDwLd];
+    float *Dl = lds, *Al = lds + kDwS * kDwLd;
+    const int wg = blockIdx.x;
+    int L = 0;
 #pragma unroll
-    for (int l = 0; l < 5; ++l) {
-        const int rel = e - dst.off[l];
-        const int nw = dst.rows[l] * dst.cols[l];
-        if (rel >= 0 && rel < nw + dst.rows[l]) {
-            float *p = rel < nw ? dst.w[l] + rel : dst.b[l] + (rel - nw);
-            *p = accumulate ? *p + v : v;
-        }
+    for (int l = 1; l < 5; ++l) L += (wg >= g.wg_begin[l]);
+    const int split = wg - g.wg_begin[L];
+    const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
+    float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
+    switch (L) {
+        case 0: dw_layer<0>(m, src, split, n_split, slab, Dl, Al); break;
+        case 1: dw_layer<1>(m, src, split, n_split, slab, Dl, Al); break;
+        case 2: dw_layer<2>(m, src, split, n_split, slab, Dl, Al); break;
+        case 3: dw_layer<3>(m, src, split, n_split, slab, Dl, Al); break;
+        default: dw_layer<4>(m, src, split, n_split, slab, Dl, Al); break;
     }
+}
+
+// grads of layer l = Σ over its splits (fixed order); one thread per element.
+struct DwDst {
+    float *w[5], *b[5];
+    int rows[5], cols[5];
+    int elem_begin[6];
+};
+
+__global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst dst, int accumulate) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= dst.elem_begin[5]) return;
+    int L = 0;
+#pragma unroll
+    for (int l = 1; l < 5; ++l) L += (e >= dst.elem_begin[l]);
+    const int rel = e - dst.elem_begin[L];
+    const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
+    const float *p = slabs + g.slab_off[L] + rel;
+    float v = 0.0f;
+    for (int sp = 0; sp < n_split; ++sp) v += p[(int64_t)sp * g.slab_len[L]];
+    const int nw = dst.rows[L] * dst.cols[L];
+    float *out = rel < nw ? dst.w[L] + rel : dst.b[L] + (rel - nw);
+    *out = accumulate ? *out + v : v;
 }
 
 }  // namespace
@@ -517,9 +563,11 @@ using namespace psvo;
 
 extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                            const float *b4, const float *w5, const float *b5, float *sdf, float *rgb) {
+                            const float *b4, const float *w5, const float *b5, float *sdf, float *rgb, float *act,
+                            uint64_t *masks) {
     PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
+    PSVO_REQUIRE((act == nullptr) == (masks == nullptr), "mlp_fwd: act and masks go together");
     if (m == 0) return PSVO_OK;
     static bool attr = false;
     if (!attr) {
@@ -529,55 +577,62 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     }
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
     hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, as_stream(stream), m, feat, p,
-                       sdf, rgb);
+                       sdf, rgb, act, masks);
     return check_launch("mlp_fwd");
 }
 
-// Packed slab layout (floats): per layer rows*cols weights then rows biases.
-static void dw_layout(int off[5], int rows[5], int cols[5], int *stride) {
-    const int R[5] = {128, 128, 129, 128, 3}, C[5] = {16, 128, 128, 144, 128};
-    int o = 0;
+static const int kDwRows[5] = {128, 128, 129, 128, 3};
+static const int kDwCols[5] = {16, 128, 128, 144, 128};
+static const int kDwBlocks[5] = {4, 16, 20, 20, 4};
+
+// split counts per layer ∝ MFMA blocks, ≈ 2 workgroups per CU in total
+static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
+    const int64_t chunks = (m + kDwS - 1) / kDwS;
+    int wg = 0, off = 0;
     for (int l = 0; l < 5; ++l) {
-        rows[l] = R[l];
-        cols[l] = C[l];
-        off[l] = o;
-        o += R[l] * C[l] + R[l];
+        int sp = (int)((int64_t)n_split * kDwBlocks[l] / 20);
+        if (sp < 1) sp = 1;
+        if (sp > chunks) sp = (int)(chunks > 0 ? chunks : 1);
+        g->wg_begin[l] = wg;
+        g->slab_off[l] = off;
+        g->slab_len[l] = kDwRows[l] * kDwCols[l] + kDwRows[l];
+        wg += sp;
+        off += sp * g->slab_len[l];
     }
-    *stride = (o + 63) & ~63;
+    g->wg_begin[5] = wg;
+    *slab_floats = off;
 }
 
 extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
-    int off[5], rows[5], cols[5], stride;
-    dw_layout(off, rows, cols, &stride);
-    return m * (8 * 128 + 3 + 16) + (int64_t)n_split * stride;
+    DwGrid g;
+    int slab;
+    dw_grid(m, n_split, &g, &slab);
+    return m * (4 * 128 + 3) + slab;
 }
 
 // Full decoder backward: grads of the 10 parameters (overwritten, or added
-// to when `accumulate`) and dfeat [M,16].  `workspace` holds the row-major
-// activations / deltas and the split-K slabs (psvo_mlp_workspace_floats).
+// to when `accumulate`) and dfeat [M,16], from the training forward's rgb,
+// activations and masks.  `workspace`: δ operands + split-K slabs
+// (psvo_mlp_workspace_floats).
 extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                            const float *b4, const float *w5, const float *b5, const float *g_sdf,
-                            const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
-                            float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5,
-                            int accumulate, int n_split, float *workspace) {
+                            const float *b4, const float *w5, const float *b5, const float *rgb, const float *act,
+                            const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1,
+                            float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4,
+                            float *gw5, float *gb5, int accumulate, int n_split, float *workspace) {
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
     hipStream_t st = as_stream(stream);
-    int off[5], rows[5], cols[5], stride;
-    dw_layout(off, rows, cols, &stride);
+    DwGrid g;
+    int slab_floats;
+    dw_grid(m, n_split, &g, &slab_floats);
     float *ws = workspace;
     BwdOut o;
-    o.a1 = ws; ws += m * 128;
-    o.a2 = ws; ws += m * 128;
-    o.a3 = ws; ws += m * 128;
-    o.a4 = ws; ws += m * 128;
     o.d1 = ws; ws += m * 128;
     o.d2 = ws; ws += m * 128;
     o.d3 = ws; ws += m * 128;
     o.d4 = ws; ws += m * 128;
     o.d5 = ws; ws += m * 3;
-    ws += m * 16;  // reserved
     float *slabs = ws;
     o.dfeat = dfeat;
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
@@ -588,31 +643,32 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd);
             attr = true;
         }
-        hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, feat, p,
-                           g_sdf, g_rgb, o);
+        hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p, rgb,
+                           masks, g_sdf, g_rgb, o);
         int rc = check_launch("mlp_bwd_data");
         if (rc) return rc;
     }
-    DwArgs a;
-    a.slab_stride = stride;
-    a.L[0] = DwLayer{o.d1, nullptr, 128, 128, feat, nullptr, 16, 16, 16, off[0]};
-    a.L[1] = DwLayer{o.d2, nullptr, 128, 128, o.a1, nullptr, 128, 128, 128, off[1]};
-    a.L[2] = DwLayer{o.d3, g_sdf, 128, 129, o.a2, nullptr, 128, 128, 128, off[2]};
-    a.L[3] = DwLayer{o.d4, nullptr, 128, 128, o.a3, feat, 128, 128, 144, off[3]};
-    a.L[4] = DwLayer{o.d5, nullptr, 3, 3, o.a4, nullptr, 128, 128, 128, off[4]};
-    hipLaunchKernelGGL(k_mlp_dw, dim3(n_split, 5), dim3(256), 0, st, m, a, n_split, slabs);
+    DwSrc src;
+    src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4; src.D[4] = o.d5;
+    src.A[0] = feat; src.A[1] = act; src.A[2] = act + m * 128; src.A[3] = act + 2 * m * 128;
+    src.A[4] = act + 3 * m * 128;
+    src.feat = feat;
+    src.g_sdf = g_sdf;
+    hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs);
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
     DwDst d;
     float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
+    int e = 0;
     for (int l = 0; l < 5; ++l) {
         d.w[l] = gw[l];
         d.b[l] = gb[l];
-        d.off[l] = off[l];
-        d.rows[l] = rows[l];
-        d.cols[l] = cols[l];
+        d.rows[l] = kDwRows[l];
+        d.cols[l] = kDwCols[l];
+        d.elem_begin[l] = e;
+        e += kDwRows[l] * kDwCols[l] + kDwRows[l];
     }
-    hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(stride, 256)), dim3(256), 0, st, n_split, stride, slabs, d,
-                       accumulate);
+    d.elem_begin[5] = e;
+    hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, st, g, slabs, d, accumulate);
     return check_launch("mlp_dw_reduce");
 }

@@ -22,7 +22,9 @@ from . import _lib as L
 
 class DecoderMLP(Function):
     """(feat[M,16], W1,b1,...,W5,b5) → (sdf[M], rgb[M,3]) on libpsvo's fused
-    MFMA kernels; backward gives dfeat and all ten parameter gradients."""
+    MFMA kernels; backward gives dfeat and all ten parameter gradients.  The
+    training forward keeps the activations the weight gradients need
+    (2 KB/sample) so the backward never re-runs the forward."""
 
     @staticmethod
     def forward(ctx, feat, *params):
@@ -32,23 +34,29 @@ class DecoderMLP(Function):
         sdf = torch.empty((m,), dtype=torch.float32, device=dev)
         rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
         ps = [p.contiguous() for p in params]
-        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb))
-        ctx.save_for_backward(feat, *ps)
+        training = torch.is_grad_enabled() and (feat.requires_grad or any(p.requires_grad for p in ps))
+        act = torch.empty((4, m, 128), dtype=torch.float32, device=dev) if training else None
+        masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
+        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb),
+               L.ptr(act), L.ptr(masks))
+        if training:
+            ctx.save_for_backward(feat, rgb, act, masks, *ps)
         return sdf, rgb
 
     @staticmethod
     def backward(ctx, g_sdf, g_rgb):
-        feat, *ps = ctx.saved_tensors
+        feat, rgb, act, masks, *ps = ctx.saved_tensors
         m = feat.shape[0]
         dev = feat.device
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
         g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
-        n_split = max(1, min(256, (m + 2047) // 2048))
+        n_split = 256
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
-        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(g_sdf),
-               L.ptr(g_rgb), L.ptr(dfeat), *[L.ptr(g) for g in grads], 0, n_split, L.ptr(ws))
+        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(rgb), L.ptr(act),
+               L.ptr(masks), L.ptr(g_sdf), L.ptr(g_rgb), L.ptr(dfeat), *[L.ptr(g) for g in grads], 0, n_split,
+               L.ptr(ws))
         return (dfeat, *grads)
 
 

@@ -188,11 +188,11 @@ def test_interp_matches_torch_fp32_reference():
     offsets = torch.arange(0, M + 1, per, device=DEV, dtype=torch.int32)
     # each ray crosses runs of samples inside 3 voxels (points stay inside
     # their voxel: trilinear weights in [0, 1] as on the render path)
-    leaf = torch.randint(0, n_nodes, (n_rays, 3), device=DEV, dtype=torch.int32)
+    leaf = torch.randperm(n_nodes, device=DEV)[: n_rays * 3].to(torch.int32).view(n_rays, 3)  # distinct runs
     leaf = leaf.repeat_interleave(torch.tensor([12, 13, 12], device=DEV), dim=1).reshape(-1).contiguous()
     ro = (centres[leaf.view(n_rays, per)[:, 0].long()] - 0.05).detach().requires_grad_(True)
     rd = (torch.rand(n_rays, 3, device=DEV) * 0.02).requires_grad_(True)
-    t = torch.rand(M, device=DEV) * 3
+    t = torch.sort(torch.rand(n_rays, per, device=DEV) * 3, dim=1).values.reshape(-1)
     # move each sample's leaf centre so that x = o + d t sits inside it
     x_s = (ro[ray.long()] + rd[ray.long()] * t[:, None]).detach()
     centres = centres.clone()
