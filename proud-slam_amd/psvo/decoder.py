@@ -34,7 +34,7 @@ class DecoderMLP(Function):
         sdf = torch.empty((m,), dtype=torch.float32, device=dev)
         rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
         ps = [p.contiguous() for p in params]
-        training = torch.is_grad_enabled() and (feat.requires_grad or any(p.requires_grad for p in ps))
+        training = any(ctx.needs_input_grad)  # grad mode is off inside Function.forward
         act = torch.empty((4, m, 128), dtype=torch.float32, device=dev) if training else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
         L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb),
