@@ -143,7 +143,7 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
 /* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
  * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
  * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
- * Training mode: act f32[4][M][128] (h1, h2, f, c1) and masks u64[M][2][3]
+ * Training mode: act f32[4][ceil(M/32)*32*128] (h1, h2, f, c1; tile-major) and masks u64[M][2][3]
  * (ReLU masks) are written for psvo_mlp_bwd; pass NULL for both otherwise. */
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,

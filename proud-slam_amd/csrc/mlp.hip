@@ -162,6 +162,20 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
                 make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
 }
 
+// Store an activation in TILE-MAJOR form — the accumulator registers as
+// they stand: [tile = s/32][block b][rg][lane][4] — one fully contiguous
+// 1-KB write per wave-instruction.  Element (s, f) lives at
+// tm_index(s, f) below; the weight-gradient kernel re-layouts on staging.
+__device__ __forceinline__ void store_tile(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane) {
+    float *base = dst + tile * (kNB * 4 * 64 * 4);
+#pragma unroll
+    for (int b = 0; b < kNB; ++b)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+            *reinterpret_cast<float4 *>(base + ((b * 4 + rg) * 64 + lane) * 4) =
+                make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
+}
+
 // Forward image of W[rows][cols] (global row-major, first row `row0`):
 // columns < acc_cols come from accumulator blocks, the rest from x.
 template <int NT>
@@ -243,21 +257,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     init_bias(a, lds + kOffB1, h);
     gemm_x(wl, x, a, lane);
     const uint64_t m1 = relu(a);  // h1
-    if (save) store_rows(act, s, valid, 128, a, h);
+    const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
+    const int64_t tstride = ((m + 31) / 32) * 32 * 128;  // floats per tile-major matrix
+    if (save) store_tile(act, tile, a, lane);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w2, 128, 128, 0, 128);
     __syncthreads();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
-    if (save) store_rows(act + m * 128, s, valid, 128, bacc, h);
+    if (save) store_tile(act + tstride, tile, bacc, lane);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w3, 128, 128, 1, 128);  // rows 1..128 → f
     __syncthreads();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    if (save) store_rows(act + 2 * m * 128, s, valid, 128, a, h);
+    if (save) store_tile(act + 2 * tstride, tile, a, lane);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w4, 128, 144, 0, 128);  // [f | x]
     __syncthreads();
@@ -266,7 +282,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
     if (save) {
-        store_rows(act + 3 * m * 128, s, valid, 128, bacc, h);
+        store_tile(act + 3 * tstride, tile, bacc, lane);
         if (valid) {
             uint64_t *mk = masks + (s * 2 + h) * 3;
             mk[0] = m1;
@@ -309,6 +325,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     const int h = lane >> 5;
     const int64_t s = (int64_t)blockIdx.x * kTileBwd + wave * 32 + (lane & 31);
     const bool valid = s < m;
+    const int64_t tile = (int64_t)blockIdx.x * (kTileBwd / 32) + wave;
     uint64_t m1 = 0, m2 = 0, m4 = 0;
     float d5[3] = {0.f, 0.f, 0.f};
     float dsdf = 0.0f;
@@ -342,7 +359,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
             const float v = lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
             bacc[b][r] = ((m4 >> (16 * b + r)) & 1) ? v : 0.0f;
         }
-    store_rows(o.d4, s, valid, 128, bacc, h);
+    store_tile(o.d4, tile, bacc, lane);
     // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
     f32x16 t5[5];
     zero(t5);
@@ -352,7 +369,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-    store_rows(o.d3, s, valid, 128, a, h);
+    store_tile(o.d3, tile, a, lane);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w3, 128, 128, 1, 4);
@@ -363,7 +380,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
         for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     apply_mask(bacc, m2);
-    store_rows(o.d2, s, valid, 128, bacc, h);
+    store_tile(o.d2, tile, bacc, lane);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w2, 128, 128, 0, 4);
@@ -371,7 +388,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
     apply_mask(a, m1);
-    store_rows(o.d1, s, valid, 128, a, h);
+    store_tile(o.d1, tile, a, lane);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w1, 128, 16, 0, 1);
@@ -413,16 +430,29 @@ constexpr int kDwLd = 160;       // LDS row pitch (5 blocks of 32)
 template <int RB, int CB>
 __device__ __forceinline__ void dw_mfma(const float *Dl, const float *Al, f32x16 (&acc)[5], int wave, int h, int i) {
 #pragma unroll
-    for (int t = 0; t < kDwS / 2; ++t) {
-        const int row = (2 * t + h) * kDwLd;
+    for (int j = 0; j < 5; ++j) {
+        const int bid = wave + 4 * j;
+        if (bid < RB * CB) {  // wave-uniform; the k-loop below is branch-free
+            const int rb = bid / CB, cb = bid % CB;
+            const float *dp = Dl + h * kDwLd + 32 * rb + i;
+            const float *ap = Al + h * kDwLd + 32 * cb + i;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int bid = wave + 4 * j;
-            if (bid < RB * CB) {
-                const int rb = bid / CB, cb = bid % CB;
-                acc[j] = mfma(Dl[row + 32 * rb + i], Al[row + 32 * cb + i], acc[j]);
-            }
+            for (int t = 0; t < kDwS / 2; ++t) acc[j] = mfma(dp[2 * t * kDwLd], ap[2 * t * kDwLd], acc[j]);
         }
+    }
+}
+
+// tile-major [M/32][4][4][64][4] chunk (two tiles = 64 samples) → LDS rows
+// [s][col0 + f]; rows past M are zero.
+__device__ __forceinline__ void stage_tm(float *dst, int col0, const float *__restrict__ src, int64_t s0, int64_t m) {
+    const int64_t t0 = s0 >> 5;
+    for (int e = threadIdx.x; e < 2 * 4 * 4 * 64; e += 256) {
+        const int lane = e & 63, rg = (e >> 6) & 3, b = (e >> 8) & 3, tl = e >> 10;
+        const int sl = (tl << 5) + (lane & 31);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s0 + sl < m) v = *reinterpret_cast<const float4 *>(src + (t0 + tl) * (4 * 4 * 64 * 4) + (int64_t)e * 4 -
+                                                                (int64_t)tl * (4 * 4 * 64 * 4));
+        *reinterpret_cast<float4 *>(dst + sl * kDwLd + col0 + 32 * b + 8 * rg + 4 * (lane >> 5)) = v;
     }
 }
 
@@ -475,10 +505,10 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
         const int64_t s0 = c * kDwS;
         __syncthreads();
         if (L == 4) stage_scalar(Dl, 0, src.D[4], 3, 3, s0, m);
-        else stage_v4(Dl, 0, src.D[L], 128, 128, s0, m);
+        else stage_tm(Dl, 0, src.D[L], s0, m);
         if (L == 2) stage_scalar(Dl, 128, src.g_sdf, 1, 1, s0, m);
         if (L == 0) stage_v4(Al, 0, src.feat, 16, 16, s0, m);
-        else stage_v4(Al, 0, src.A[L], 128, 128, s0, m);
+        else stage_tm(Al, 0, src.A[L], s0, m);
         if (L == 3) stage_v4(Al, 128, src.feat, 16, 16, s0, m);
         __syncthreads();
         if (threadIdx.x < ROWS) {
@@ -549,8 +579,17 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
     const int rel = e - dst.elem_begin[L];
     const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
     const float *p = slabs + g.slab_off[L] + rel;
+    const int64_t stride = g.slab_len[L];
     float v = 0.0f;
-    for (int sp = 0; sp < n_split; ++sp) v += p[(int64_t)sp * g.slab_len[L]];
+    int sp = 0;
+    for (; sp + 8 <= n_split; sp += 8) {
+        float q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = p[(sp + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += q[u];
+    }
+    for (; sp < n_split; ++sp) v += p[sp * stride];
     const int nw = dst.rows[L] * dst.cols[L];
     float *out = rel < nw ? dst.w[L] + rel : dst.b[L] + (rel - nw);
     *out = accumulate ? *out + v : v;
@@ -607,7 +646,8 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
     dw_grid(m, n_split, &g, &slab);
-    return m * (4 * 128 + 3) + slab;
+    const int64_t mp = (m + 31) / 32 * 32;
+    return mp * 4 * 128 + m * 3 + slab;
 }
 
 // Full decoder backward: grads of the 10 parameters (overwritten, or added
@@ -627,11 +667,12 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     int slab_floats;
     dw_grid(m, n_split, &g, &slab_floats);
     float *ws = workspace;
+    const int64_t mp = (m + 31) / 32 * 32;  // tile-major matrices are padded to whole tiles
     BwdOut o;
-    o.d1 = ws; ws += m * 128;
-    o.d2 = ws; ws += m * 128;
-    o.d3 = ws; ws += m * 128;
-    o.d4 = ws; ws += m * 128;
+    o.d1 = ws; ws += mp * 128;
+    o.d2 = ws; ws += mp * 128;
+    o.d3 = ws; ws += mp * 128;
+    o.d4 = ws; ws += mp * 128;
     o.d5 = ws; ws += m * 3;
     float *slabs = ws;
     o.dfeat = dfeat;
@@ -650,8 +691,8 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     }
     DwSrc src;
     src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4; src.D[4] = o.d5;
-    src.A[0] = feat; src.A[1] = act; src.A[2] = act + m * 128; src.A[3] = act + 2 * m * 128;
-    src.A[4] = act + 3 * m * 128;
+    src.A[0] = feat; src.A[1] = act; src.A[2] = act + mp * 128; src.A[3] = act + 2 * mp * 128;
+    src.A[4] = act + 3 * mp * 128;
     src.feat = feat;
     src.g_sdf = g_sdf;
     hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs);

@@ -35,7 +35,8 @@ class DecoderMLP(Function):
         rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
         ps = [p.contiguous() for p in params]
         training = any(ctx.needs_input_grad)  # grad mode is off inside Function.forward
-        act = torch.empty((4, m, 128), dtype=torch.float32, device=dev) if training else None
+        mp = (m + 31) // 32 * 32  # tile-major activations: whole 32-sample tiles
+        act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if training else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
         L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb),
                L.ptr(act), L.ptr(masks))
@@ -50,7 +51,7 @@ class DecoderMLP(Function):
         dev = feat.device
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
         g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
-        n_split = 256
+        n_split = 128
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
