@@ -166,7 +166,8 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
 // they stand: [tile = s/32][block b][rg][lane][4] — one fully contiguous
 // 1-KB write per wave-instruction.  Element (s, f) lives at
 // tm_index(s, f) below; the weight-gradient kernel re-layouts on staging.
-__device__ __forceinline__ void store_tile(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane) {
+__device__ __forceinline__ void store_tile(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane, int64_t m) {
+    if (tile * 32 >= m) return;  // wave-uniform: tiles wholly past M are not allocated
     float *base = dst + tile * (kNB * 4 * 64 * 4);
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
@@ -259,21 +260,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     const uint64_t m1 = relu(a);  // h1
     const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
     const int64_t tstride = ((m + 31) / 32) * 32 * 128;  // floats per tile-major matrix
-    if (save) store_tile(act, tile, a, lane);
+    if (save) store_tile(act, tile, a, lane, m);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w2, 128, 128, 0, 128);
     __syncthreads();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
-    if (save) store_tile(act + tstride, tile, bacc, lane);
+    if (save) store_tile(act + tstride, tile, bacc, lane, m);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w3, 128, 128, 1, 128);  // rows 1..128 → f
     __syncthreads();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    if (save) store_tile(act + 2 * tstride, tile, a, lane);
+    if (save) store_tile(act + 2 * tstride, tile, a, lane, m);
     __syncthreads();
     stage_fwd<kThreads>(wl, p.w4, 128, 144, 0, 128);  // [f | x]
     __syncthreads();
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
     if (save) {
-        store_tile(act + 3 * tstride, tile, bacc, lane);
+        store_tile(act + 3 * tstride, tile, bacc, lane, m);
         if (valid) {
             uint64_t *mk = masks + (s * 2 + h) * 3;
             mk[0] = m1;
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
             const float v = lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
             bacc[b][r] = ((m4 >> (16 * b + r)) & 1) ? v : 0.0f;
         }
-    store_tile(o.d4, tile, bacc, lane);
+    store_tile(o.d4, tile, bacc, lane, m);
     // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
     f32x16 t5[5];
     zero(t5);
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-    store_tile(o.d3, tile, a, lane);
+    store_tile(o.d3, tile, a, lane, m);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w3, 128, 128, 1, 4);
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
         for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     apply_mask(bacc, m2);
-    store_tile(o.d2, tile, bacc, lane);
+    store_tile(o.d2, tile, bacc, lane, m);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w2, 128, 128, 0, 4);
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
     apply_mask(a, m1);
-    store_tile(o.d1, tile, a, lane);
+    store_tile(o.d1, tile, a, lane, m);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
     __syncthreads();
     stage_bwd<kThreadsBwd>(wl, p.w1, 128, 16, 0, 1);
@@ -483,6 +484,31 @@ __device__ __forceinline__ void zero_cols(float *dst, int c0, int c1) {
     for (int e = threadIdx.x; e < kDwS * w; e += 256) dst[(e / w) * kDwLd + c0 + e % w] = 0.0f;
 }
 
+// Register prefetch of one tile-major 64-sample chunk (8 float4 / thread).
+struct TmRegs {
+    float4 v[8];
+};
+__device__ __forceinline__ void tm_load(TmRegs &r, const float *__restrict__ src, int64_t s0, int64_t m) {
+    const int64_t t0 = s0 >> 5;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int lane = e & 63, tl = e >> 10;
+        const int sl = (tl << 5) + (lane & 31);
+        r.v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s0 + sl < m) r.v[u] = *reinterpret_cast<const float4 *>(src + t0 * (4 * 4 * 64 * 4) + (int64_t)e * 4);
+    }
+}
+__device__ __forceinline__ void tm_store(float *dst, int col0, const TmRegs &r) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int lane = e & 63, rg = (e >> 6) & 3, b = (e >> 8) & 3, tl = e >> 10;
+        const int sl = (tl << 5) + (lane & 31);
+        *reinterpret_cast<float4 *>(dst + sl * kDwLd + col0 + 32 * b + 8 * rg + 4 * (lane >> 5)) = r.v[u];
+    }
+}
+
 template <int L>
 __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab, float *Dl,
                                          float *Al) {
@@ -490,27 +516,37 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     constexpr int CB = (L == 0) ? 1 : (L == 3 ? 5 : 4);
     constexpr int ROWS = (L == 2) ? 129 : (L == 4 ? 3 : 128);
     constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
+    constexpr bool D_TM = (L != 4);  // D staged from tile-major
+    constexpr bool A_TM = (L != 0);  // A staged from tile-major
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
     const int64_t n_chunks = (m + kDwS - 1) / kDwS;
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
     f32x16 acc[5];
     zero(acc);
     float bias = 0.0f;
-    // one-time zero of padding columns that staging never writes
     if (L == 0) zero_cols(Al, 16, 32);
     if (L == 2) zero_cols(Dl, 129, 160);
     if (L == 3) zero_cols(Al, 144, 160);
     if (L == 4) zero_cols(Dl, 3, 32);
+    TmRegs rd, ra;
+    if (c_beg < c_end) {
+        if (D_TM) tm_load(rd, src.D[L], c_beg * kDwS, m);
+        if (A_TM) tm_load(ra, src.A[L], c_beg * kDwS, m);
+    }
     for (int64_t c = c_beg; c < c_end; ++c) {
         const int64_t s0 = c * kDwS;
-        __syncthreads();
-        if (L == 4) stage_scalar(Dl, 0, src.D[4], 3, 3, s0, m);
-        else stage_tm(Dl, 0, src.D[L], s0, m);
+        __syncthreads();  // previous chunk's MFMAs are done with the LDS image
+        if (D_TM) tm_store(Dl, 0, rd);
+        else stage_scalar(Dl, 0, src.D[4], 3, 3, s0, m);
         if (L == 2) stage_scalar(Dl, 128, src.g_sdf, 1, 1, s0, m);
-        if (L == 0) stage_v4(Al, 0, src.feat, 16, 16, s0, m);
-        else stage_tm(Al, 0, src.A[L], s0, m);
+        if (A_TM) tm_store(Al, 0, ra);
+        else stage_v4(Al, 0, src.feat, 16, 16, s0, m);
         if (L == 3) stage_v4(Al, 128, src.feat, 16, 16, s0, m);
         __syncthreads();
+        if (c + 1 < c_end) {  // next chunk in flight during this chunk's MFMAs
+            if (D_TM) tm_load(rd, src.D[L], s0 + kDwS, m);
+            if (A_TM) tm_load(ra, src.A[L], s0 + kDwS, m);
+        }
         if (threadIdx.x < ROWS) {
             // C row r ← LDS column (layer 2: row 0 is column 128, rows 1.. are 0..)
             const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
