@@ -69,21 +69,28 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// acc[ob] += image(`wl`: NOUT x NIN blocks) · in[kb]
+// acc[ob] += image(`wl`: NOUT x NIN blocks) · in[kb].  Per (kb, rg) the NOUT
+// operand groups are read first, then the 4·NOUT MFMAs run with the
+// independent accumulators interleaved (ob innermost), so no MFMA waits on
+// its predecessor and the next group's ds_reads overlap these MFMAs.
 template <int NIN, int NOUT>
 __device__ __forceinline__ void gemm_acc(const float *wl, const f32x16 (&in)[NIN], f32x16 (&acc)[NOUT], int lane) {
 #pragma unroll
     for (int kb = 0; kb < NIN; ++kb) {
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
+            float4 a[NOUT];
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob) {
-                const float4 a = *reinterpret_cast<const float4 *>(wl + ((((ob * NIN + kb) * 4 + rg) * 64 + lane) << 2));
-                acc[ob] = mfma(a.x, in[kb][4 * rg + 0], acc[ob]);
-                acc[ob] = mfma(a.y, in[kb][4 * rg + 1], acc[ob]);
-                acc[ob] = mfma(a.z, in[kb][4 * rg + 2], acc[ob]);
-                acc[ob] = mfma(a.w, in[kb][4 * rg + 3], acc[ob]);
-            }
+            for (int ob = 0; ob < NOUT; ++ob)
+                a[ob] = *reinterpret_cast<const float4 *>(wl + ((((ob * NIN + kb) * 4 + rg) * 64 + lane) << 2));
+#pragma unroll
+            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].x, in[kb][4 * rg + 0], acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].y, in[kb][4 * rg + 1], acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].z, in[kb][4 * rg + 2], acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].w, in[kb][4 * rg + 3], acc[ob]);
         }
     }
 }
@@ -92,14 +99,17 @@ __device__ __forceinline__ void gemm_acc(const float *wl, const f32x16 (&in)[NIN
 __device__ __forceinline__ void gemm_x(const float *wl, const float (&x)[8], f32x16 (&acc)[kNB], int lane) {
 #pragma unroll
     for (int tg = 0; tg < 2; ++tg) {
+        float4 a[kNB];
 #pragma unroll
-        for (int ob = 0; ob < kNB; ++ob) {
-            const float4 a = *reinterpret_cast<const float4 *>(wl + (((ob * 2 + tg) * 64 + lane) << 2));
-            acc[ob] = mfma(a.x, x[4 * tg + 0], acc[ob]);
-            acc[ob] = mfma(a.y, x[4 * tg + 1], acc[ob]);
-            acc[ob] = mfma(a.z, x[4 * tg + 2], acc[ob]);
-            acc[ob] = mfma(a.w, x[4 * tg + 3], acc[ob]);
-        }
+        for (int ob = 0; ob < kNB; ++ob) a[ob] = *reinterpret_cast<const float4 *>(wl + (((ob * 2 + tg) * 64 + lane) << 2));
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].x, x[4 * tg + 0], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].y, x[4 * tg + 1], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].z, x[4 * tg + 2], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].w, x[4 * tg + 3], acc[ob]);
     }
 }
 
@@ -428,18 +438,22 @@ struct DwSrc {
 constexpr int kDwS = 64;         // samples per staged chunk
 constexpr int kDwLd = 160;       // LDS row pitch (5 blocks of 32)
 
-template <int RB, int CB>
+// Each wave owns NBW blocks of C that share one operand block: either a
+// fixed column block (cb = wave, rb = 0..NBW-1) or a fixed row block
+// (rb = wave, cb = 0..NBW-1).  Per 2-sample k-step: 1 shared + NBW other
+// operand reads, then NBW independent MFMAs.
+template <int NBW, bool FIX_CB>
 __device__ __forceinline__ void dw_mfma(const float *Dl, const float *Al, f32x16 (&acc)[5], int wave, int h, int i) {
+    const float *sp = (FIX_CB ? Al : Dl) + h * kDwLd + 32 * wave + i;
+    const float *op = (FIX_CB ? Dl : Al) + h * kDwLd + i;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const int bid = wave + 4 * j;
-        if (bid < RB * CB) {  // wave-uniform; the k-loop below is branch-free
-            const int rb = bid / CB, cb = bid % CB;
-            const float *dp = Dl + h * kDwLd + 32 * rb + i;
-            const float *ap = Al + h * kDwLd + 32 * cb + i;
+    for (int t = 0; t < kDwS / 2; ++t) {
+        const float sh = sp[2 * t * kDwLd];
+        float ot[NBW];
 #pragma unroll
-            for (int t = 0; t < kDwS / 2; ++t) acc[j] = mfma(dp[2 * t * kDwLd], ap[2 * t * kDwLd], acc[j]);
-        }
+        for (int j = 0; j < NBW; ++j) ot[j] = op[2 * t * kDwLd + 32 * j];
+#pragma unroll
+        for (int j = 0; j < NBW; ++j) acc[j] = FIX_CB ? mfma(ot[j], sh, acc[j]) : mfma(sh, ot[j], acc[j]);
     }
 }
 
@@ -516,6 +530,11 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     constexpr int CB = (L == 0) ? 1 : (L == 3 ? 5 : 4);
     constexpr int ROWS = (L == 2) ? 129 : (L == 4 ? 3 : 128);
     constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
+    // block ownership: W1 (4x1) and W4 (4x5) fix rb = wave; W2 (4x4), W3 (5x4)
+    // and W5 (1x4) fix cb = wave
+    constexpr bool FIX_CB = (L == 1 || L == 2 || L == 4);
+    constexpr int NBW = FIX_CB ? RB : CB;
+    constexpr int kBiasCols = (L == 2) ? 129 : ROWS;  // D columns holding bias sums
     constexpr bool D_TM = (L != 4);  // D staged from tile-major
     constexpr bool A_TM = (L != 0);  // A staged from tile-major
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
@@ -547,31 +566,37 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
             if (D_TM) tm_load(rd, src.D[L], s0 + kDwS, m);
             if (A_TM) tm_load(ra, src.A[L], s0 + kDwS, m);
         }
-        if (threadIdx.x < ROWS) {
-            // C row r ← LDS column (layer 2: row 0 is column 128, rows 1.. are 0..)
-            const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
+        if (threadIdx.x < 2 * kBiasCols) {
+            // thread → (LDS column, half of the chunk); summed in fixed order
+            const int col = threadIdx.x % kBiasCols, hs = threadIdx.x / kBiasCols;
+            float part = 0.0f;
 #pragma unroll 8
-            for (int ss = 0; ss < kDwS; ++ss) bias += Dl[ss * kDwLd + col];
+            for (int ss = 0; ss < kDwS / 2; ++ss) part += Dl[(hs * (kDwS / 2) + ss) * kDwLd + col];
+            bias += part;
         }
-        dw_mfma<RB, CB>(Dl, Al, acc, wave, h, i);
+        dw_mfma<NBW, FIX_CB>(Dl, Al, acc, wave, h, i);
     }
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const int bid = wave + 4 * j;
-        if (bid < RB * CB) {
-            const int rb = bid / CB, cb = bid % CB;
-            const int col = 32 * cb + i;
+    for (int j = 0; j < NBW; ++j) {
+        const int rb = FIX_CB ? j : wave, cb = FIX_CB ? wave : j;
+        const int col = 32 * cb + i;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lr = 32 * rb + phi(r, h);  // LDS column of D
-                int row;
-                if (L == 2) row = lr == 128 ? 0 : (lr < 128 ? lr + 1 : -1);
-                else row = lr < ROWS ? lr : -1;
-                if (row >= 0 && col < COLS) slab[row * COLS + col] = acc[j][r];
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int lr = 32 * rb + phi(r, h);  // LDS column of D
+            int row;
+            if (L == 2) row = lr == 128 ? 0 : (lr < 128 ? lr + 1 : -1);
+            else row = lr < ROWS ? lr : -1;
+            if (row >= 0 && col < COLS) slab[row * COLS + col] = acc[j][r];
         }
     }
-    if (threadIdx.x < ROWS) slab[ROWS * COLS + threadIdx.x] = bias;
+    // combine the two half-chunk partial sums of each column (fixed order)
+    __syncthreads();
+    if (threadIdx.x < 2 * kBiasCols) Dl[threadIdx.x] = bias;
+    __syncthreads();
+    if (threadIdx.x < ROWS) {
+        const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
+        slab[ROWS * COLS + threadIdx.x] = Dl[col] + Dl[kBiasCols + col];
+    }
 }
 
 struct DwGrid {
