@@ -542,7 +542,7 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
     f32x16 acc[5];
     zero(acc);
-    float bias = 0.0f;
+    float bias[2] = {0.0f, 0.0f};
     if (L == 0) zero_cols(Al, 16, 32);
     if (L == 2) zero_cols(Dl, 129, 160);
     if (L == 3) zero_cols(Al, 144, 160);
@@ -566,13 +566,17 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
             if (D_TM) tm_load(rd, src.D[L], s0 + kDwS, m);
             if (A_TM) tm_load(ra, src.A[L], s0 + kDwS, m);
         }
-        if (threadIdx.x < 2 * kBiasCols) {
-            // thread → (LDS column, half of the chunk); summed in fixed order
-            const int col = threadIdx.x % kBiasCols, hs = threadIdx.x / kBiasCols;
-            float part = 0.0f;
+        // bias partial sums: slot q = (half, LDS column), thread t owns q = t and t + 256
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int q = threadIdx.x + 256 * k;
+            if (q < 2 * kBiasCols) {
+                const int col = q % kBiasCols, hs = q / kBiasCols;
+                float part = 0.0f;
 #pragma unroll 8
-            for (int ss = 0; ss < kDwS / 2; ++ss) part += Dl[(hs * (kDwS / 2) + ss) * kDwLd + col];
-            bias += part;
+                for (int ss = 0; ss < kDwS / 2; ++ss) part += Dl[(hs * (kDwS / 2) + ss) * kDwLd + col];
+                bias[k] += part;
+            }
         }
         dw_mfma<NBW, FIX_CB>(Dl, Al, acc, wave, h, i);
     }
@@ -591,7 +595,9 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     }
     // combine the two half-chunk partial sums of each column (fixed order)
     __syncthreads();
-    if (threadIdx.x < 2 * kBiasCols) Dl[threadIdx.x] = bias;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (threadIdx.x + 256 * k < 2 * kBiasCols) Dl[threadIdx.x + 256 * k] = bias[k];
     __syncthreads();
     if (threadIdx.x < ROWS) {
         const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
