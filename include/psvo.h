@@ -25,6 +25,8 @@
  *   psvo_composite_fwd / _bwd     render_helpers.render_rays compositing (render_helpers.py:504-556)
  *   psvo_mlp_fwd / _bwd           variations/nrgbd.Decoder forward + autograd backward
  *                                 (nrgbd.py:80-146), fused fp32 MFMA
+ *   psvo_criterion_*              criterion.Criterion.forward + autograd backward
+ *                                 (criterion.py:17-116)
  *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
  *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
  */
@@ -163,6 +165,41 @@ int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const fl
                  const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1,
                  float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5,
                  int accumulate, int n_split, float *workspace);
+
+/* ---- mapping loss (criterion.py:17-116) ------------------------------ */
+/* out[] words written by psvo_criterion_finalize */
+enum {
+    PSVO_CRIT_LOSS = 0, PSVO_CRIT_COLOR = 1, PSVO_CRIT_DEPTH = 2, PSVO_CRIT_FS = 3, PSVO_CRIT_SDF = 4,
+    PSVO_CRIT_FS_WEIGHT = 5, PSVO_CRIT_SDF_WEIGHT = 6, /* 7..10: backward coefficients */
+    PSVO_CRIT_OUT_WORDS = 16
+};
+enum { PSVO_CRIT_USE_COLOR = 1, PSVO_CRIT_USE_DEPTH = 2, PSVO_CRIT_USE_SDF = 4 };
+
+/* Floats of workspace psvo_criterion_sums needs. */
+int64_t psvo_criterion_workspace_floats(int64_t r_hit);
+
+/* Loss sums over the R_hit hit rays: gt_rgb f32[R,3] / gt_depth f32[R] are
+ * indexed through rank_ray[R_hit]; colour [R_hit,3], depth [R_hit], sdf and
+ * z_vals [R_hit,S_max] as psvo_composite_fwd / psvo_sample_points produce.
+ * sums f64[8] = {Σ|Δrgb|, Σ_valid |Δd|, n_valid, n_front, n_sdf, Σ fs², Σ sdf², 0}
+ * (fixed-order, deterministic).  pad_extra > 0 adds that many padded samples
+ * (z = 10, sdf = 1) per ray — for a shard whose S_max is below the global
+ * one, so that all-reduced sums equal the single-GPU sums. */
+int psvo_criterion_sums(void *stream, int64_t r_hit, int s_max, int pad_extra, float truncation, float max_depth,
+                        const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *color,
+                        const float *depth, const float *sdf, const float *z_vals, float *workspace, double *sums);
+
+/* Loss and its parts from (possibly all-reduced) sums over n_hit rays ×
+ * s_max columns; flags = PSVO_CRIT_USE_* terms; out f32[PSVO_CRIT_OUT_WORDS]. */
+int psvo_criterion_finalize(void *stream, const double *sums, int64_t n_hit, int s_max, float rgb_w, float depth_w,
+                            float fs_w, float sdf_w, float truncation, int flags, float *out);
+
+/* Backward given g_loss (device scalar): g_color [R_hit,3], g_depth [R_hit],
+ * g_sdf [R_hit,S_max]. */
+int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
+                       const float *gt_rgb, const float *gt_depth, const float *color, const float *depth,
+                       const float *sdf, const float *z_vals, const float *out, const float *g_loss, float *g_color,
+                       float *g_depth, float *g_sdf);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

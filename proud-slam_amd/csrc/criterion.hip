@@ -1,0 +1,229 @@
+// Mapping loss (Criterion) on the device, forward + backward, no host syncs.
+//
+// Reference: src/criterion.py:17-116 (forward :17-68, get_masks :78-101,
+// get_sdf_loss :103-116).  With d = gt depth of the hit ray, z/p the padded
+// [R_hit, S_max] z_vals / sdf rows:
+//   colour = mean |gt_rgb − rgb|                          over R_hit·3
+//   depth  = mean_{valid} |gt_d − depth|,  valid = 0.01 < d < max_depth
+//   f  = [z < d − tr],  b = [z > d + tr],  dm = [0 < d < max_depth]
+//   sm = (1−f)(1−b)dm
+//   fs  = mean (p·f − f)²           · (1 − n_f/(n_f+n_s))   over R_hit·S_max
+//   sdf = mean ((z + p·tr)·sm − d·sm)² · (1 − n_s/(n_f+n_s))
+//   loss = rgb_w·colour + depth_w·depth + fs_w·fs + sdf_w·sdf
+// The torch version needs three host syncs (boolean indexing) and ~40
+// launches; here it is per-ray partial sums (one wave per ray), a fixed-order
+// double reduction (deterministic), a one-thread finalise, and one backward
+// pass.  The eight sums are exactly what a data-parallel run all-reduces to
+// form the single-GPU loss of the global batch.
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+#pragma clang fp contract(off)
+
+namespace psvo {
+namespace {
+
+enum { kSumColor = 0, kSumDepth, kNValid, kNFront, kNSdf, kSqFs, kSqSdf, kNSums = 8 };
+enum { kFlagColor = 1, kFlagDepth = 2, kFlagSdf = 4 };
+// out[] layout (PSVO_CRIT_* in psvo.h)
+enum { kOutLoss = 0, kOutColor, kOutDepth, kOutFs, kOutSdf, kOutFsW, kOutSdfW, kOutCColor, kOutCDepth, kOutCFs,
+       kOutCSdf };
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+
+struct SampleTerms {
+    float f, sm, xfs, ysdf;
+};
+
+__device__ __forceinline__ SampleTerms sample_terms(float z, float p, float d, float tr, float max_depth) {
+    SampleTerms o;
+    o.f = z < (d - tr) ? 1.0f : 0.0f;
+    const float b = z > (d + tr) ? 1.0f : 0.0f;
+    const float dm = (d > 0.0f && d < max_depth) ? 1.0f : 0.0f;
+    o.sm = (1.0f - o.f) * (1.0f - b) * dm;
+    o.xfs = p * o.f - o.f;
+    o.ysdf = (z + p * tr) * o.sm - d * o.sm;
+    return o;
+}
+
+// one wave per hit ray → part[r][8]
+__global__ __launch_bounds__(256) void k_crit_rays(int64_t r_hit, int s_max, int pad_extra, float tr, float max_depth,
+                                                   const int *__restrict__ rank_ray, const float *__restrict__ gt_rgb,
+                                                   const float *__restrict__ gt_depth, const float *__restrict__ color,
+                                                   const float *__restrict__ depth, const float *__restrict__ sdf,
+                                                   const float *__restrict__ z_vals, float *__restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int64_t orig = rank_ray[r];
+    const float d = gt_depth[orig];
+    float nf = 0.f, ns = 0.f, qfs = 0.f, qsdf = 0.f;
+    const float *z = z_vals + r * s_max;
+    const float *p = sdf + r * s_max;
+    for (int s = lane; s < s_max; s += 64) {
+        const SampleTerms t = sample_terms(z[s], p[s], d, tr, max_depth);
+        nf += t.f;
+        ns += t.sm;
+        qfs += t.xfs * t.xfs;
+        qsdf += t.ysdf * t.ysdf;
+    }
+    nf = wsum(nf);
+    ns = wsum(ns);
+    qfs = wsum(qfs);
+    qsdf = wsum(qsdf);
+    if (lane == 0) {
+        float ac = 0.f;
+        for (int c = 0; c < 3; ++c) ac += fabsf(gt_rgb[orig * 3 + c] - color[r * 3 + c]);
+        const bool valid = d > 0.01f && d < max_depth;
+        if (pad_extra > 0) {  // padded samples of the global [R_hit, S_max] layout: z = 10, sdf = 1
+            const SampleTerms t = sample_terms(10.0f, 1.0f, d, tr, max_depth);
+            nf += t.f * pad_extra;
+            ns += t.sm * pad_extra;
+            qsdf += t.ysdf * t.ysdf * pad_extra;
+        }
+        float *o = part + r * kNSums;
+        o[kSumColor] = ac;
+        o[kSumDepth] = valid ? fabsf(d - depth[r]) : 0.0f;
+        o[kNValid] = valid ? 1.0f : 0.0f;
+        o[kNFront] = nf;
+        o[kNSdf] = ns;
+        o[kSqFs] = qfs;
+        o[kSqSdf] = qsdf;
+        o[7] = 0.0f;
+    }
+}
+
+// fixed-order reduction of part[r_hit][8] → sums[8] (double)
+__global__ __launch_bounds__(256) void k_crit_reduce(int64_t r_hit, const float *__restrict__ part,
+                                                     double *__restrict__ sums) {
+    __shared__ double red[kNSums][256];
+    double acc[kNSums];
+#pragma unroll
+    for (int k = 0; k < kNSums; ++k) acc[k] = 0.0;
+    for (int64_t r = threadIdx.x; r < r_hit; r += 256) {
+#pragma unroll
+        for (int k = 0; k < kNSums; ++k) acc[k] += (double)part[r * kNSums + k];
+    }
+#pragma unroll
+    for (int k = 0; k < kNSums; ++k) red[k][threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int k = 0; k < kNSums; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < kNSums) sums[threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void k_crit_finalize(const double *__restrict__ sums, double n_hit, double n_cols, float rgb_w,
+                                float depth_w, float fs_w, float sdf_w, float tr, int flags, float *__restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const double n_el = n_hit * n_cols;
+    const float color_loss = (float)(sums[kSumColor] / (3.0 * n_hit));
+    const float n_valid = (float)sums[kNValid];
+    const float depth_loss = (float)(sums[kSumDepth] / sums[kNValid]);  // 0/0 = NaN as torch's empty mean
+    const float n_f = (float)sums[kNFront], n_s = (float)sums[kNSdf];
+    const float n_tot = n_s + n_f;
+    const float fs_weight = 1.0f - n_f / n_tot;
+    const float sdf_weight = 1.0f - n_s / n_tot;
+    const float fs_loss = (float)(sums[kSqFs] / n_el) * fs_weight;
+    const float sdf_loss = (float)(sums[kSqSdf] / n_el) * sdf_weight;
+    float loss = 0.0f;
+    if (flags & kFlagColor) loss += rgb_w * color_loss;
+    if (flags & kFlagDepth) loss += depth_w * depth_loss;
+    if (flags & kFlagSdf) {
+        loss += fs_w * fs_loss;
+        loss += sdf_w * sdf_loss;
+    }
+    out[kOutLoss] = loss;
+    out[kOutColor] = color_loss;
+    out[kOutDepth] = depth_loss;
+    out[kOutFs] = fs_loss;
+    out[kOutSdf] = sdf_loss;
+    out[kOutFsW] = fs_weight;
+    out[kOutSdfW] = sdf_weight;
+    // backward coefficients (d loss / d term per element, before the sign / residual factor)
+    out[kOutCColor] = (flags & kFlagColor) ? (float)(rgb_w / (3.0 * n_hit)) : 0.0f;
+    out[kOutCDepth] = (flags & kFlagDepth) ? depth_w / n_valid : 0.0f;
+    out[kOutCFs] = (flags & kFlagSdf) ? (float)(2.0 * (double)(fs_w * fs_weight) / n_el) : 0.0f;
+    out[kOutCSdf] = (flags & kFlagSdf) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
+}
+
+__device__ __forceinline__ float sgn(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+
+__global__ __launch_bounds__(256) void k_crit_bwd(int64_t r_hit, int s_max, float tr, float max_depth,
+                                                  const int *__restrict__ rank_ray, const float *__restrict__ gt_rgb,
+                                                  const float *__restrict__ gt_depth, const float *__restrict__ color,
+                                                  const float *__restrict__ depth, const float *__restrict__ sdf,
+                                                  const float *__restrict__ z_vals, const float *__restrict__ coef,
+                                                  const float *__restrict__ g_loss, float *__restrict__ g_color,
+                                                  float *__restrict__ g_depth, float *__restrict__ g_sdf) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const float g = g_loss[0];
+    const int64_t orig = rank_ray[r];
+    const float d = gt_depth[orig];
+    const float cfs = g * coef[kOutCFs], csdf = g * coef[kOutCSdf];
+    const float *z = z_vals + r * s_max;
+    const float *p = sdf + r * s_max;
+    float *gs = g_sdf + r * s_max;
+    for (int s = lane; s < s_max; s += 64) {
+        const SampleTerms t = sample_terms(z[s], p[s], d, tr, max_depth);
+        gs[s] = cfs * t.xfs * t.f + csdf * t.ysdf * t.sm;
+    }
+    if (lane < 3) {
+        g_color[r * 3 + lane] = -(g * coef[kOutCColor]) * sgn(gt_rgb[orig * 3 + lane] - color[r * 3 + lane]);
+    } else if (lane == 3) {
+        const bool valid = d > 0.01f && d < max_depth;
+        g_depth[r] = valid ? -(g * coef[kOutCDepth]) * sgn(d - depth[r]) : 0.0f;
+    }
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int64_t psvo_criterion_workspace_floats(int64_t r_hit) { return r_hit * kNSums; }
+
+extern "C" int psvo_criterion_sums(void *stream, int64_t r_hit, int s_max, int pad_extra, float truncation,
+                                   float max_depth, const int *rank_ray, const float *gt_rgb, const float *gt_depth,
+                                   const float *color, const float *depth, const float *sdf, const float *z_vals,
+                                   float *workspace, double *sums) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0 && pad_extra >= 0, "criterion_sums: bad sizes");
+    PSVO_REQUIRE(rank_ray && gt_rgb && gt_depth && color && depth && sdf && z_vals && workspace && sums,
+                 "criterion_sums: null pointer");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
+                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, workspace);
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    return check_launch("criterion_sums");
+}
+
+extern "C" int psvo_criterion_finalize(void *stream, const double *sums, int64_t n_hit, int s_max, float rgb_w,
+                                       float depth_w, float fs_w, float sdf_w, float truncation, int flags,
+                                       float *out) {
+    PSVO_REQUIRE(n_hit > 0 && s_max > 0, "criterion_finalize: bad sizes");
+    hipLaunchKernelGGL(k_crit_finalize, dim3(1), dim3(64), 0, as_stream(stream), sums, (double)n_hit, (double)s_max,
+                       rgb_w, depth_w, fs_w, sdf_w, truncation, flags, out);
+    return check_launch("criterion_finalize");
+}
+
+extern "C" int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                                  const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *color,
+                                  const float *depth, const float *sdf, const float *z_vals, const float *out,
+                                  const float *g_loss, float *g_color, float *g_depth, float *g_sdf) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_bwd: bad sizes");
+    hipLaunchKernelGGL(k_crit_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
+                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, out, g_loss, g_color,
+                       g_depth, g_sdf);
+    return check_launch("criterion_bwd");
+}

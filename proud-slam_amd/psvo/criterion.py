@@ -5,11 +5,70 @@ and the same padded-mean semantics over [R_hit, S_max].  loss_dict values
 are converted to Python floats lazily (on first access) instead of five
 `.item()` host syncs per call (criterion.py:39-67); bundle_adjust_frames and
 track_frame discard the dict.
+
+When `outputs` comes from psvo.render_helpers.render_rays (it carries the
+hit-ray order `rank_ray`), the loss runs as libpsvo's criterion kernels
+(csrc/criterion.hip): no boolean indexing, so no host syncs, and a
+deterministic reduction.  weight_depth_loss (tracking's median filter) and
+foreign output dicts use the PyTorch formulation below.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
+from torch.autograd import Function
+
+from . import _lib as L
+
+CRIT_OUT_WORDS = 16
+_USE_COLOR, _USE_DEPTH, _USE_SDF = 1, 2, 4
+
+
+class CriterionLoss(Function):
+    """(colour, depth, sdf) of the hit rays → scalar loss; the parts and the
+    fs/sdf balance weights (f32[16], PSVO_CRIT_* words) are appended to `sink`.
+    `reduce_sums` (optional) is applied to the f64[8] sums in place before the
+    loss is formed — the data-parallel hook (all-reduce) of SURVEY §8e."""
+
+    @staticmethod
+    def forward(ctx, color, depth, sdf, z_vals, gt_rgb, gt_depth, rank_ray, cfg, reduce_sums=None, sink=None):
+        tr, max_depth, rgb_w, depth_w, fs_w, sdf_w, flags = cfg
+        r_hit, s_max = z_vals.shape
+        dev = z_vals.device
+        n_hit, s_cols, pad_extra = r_hit, s_max, 0
+        if reduce_sums is not None:
+            n_hit, s_cols = reduce_sums.global_shape(r_hit, s_max)
+            pad_extra = s_cols - s_max
+        ws = torch.empty((int(L.lib().psvo_criterion_workspace_floats(r_hit)),), dtype=torch.float32, device=dev)
+        sums = torch.empty((8,), dtype=torch.float64, device=dev)
+        out = torch.empty((CRIT_OUT_WORDS,), dtype=torch.float32, device=dev)
+        stream = L.stream_of(dev)
+        L.call("psvo_criterion_sums", stream, r_hit, s_max, pad_extra, tr, max_depth, L.ptr(rank_ray), L.ptr(gt_rgb),
+               L.ptr(gt_depth), L.ptr(color), L.ptr(depth), L.ptr(sdf), L.ptr(z_vals), L.ptr(ws), L.ptr(sums))
+        if reduce_sums is not None:
+            reduce_sums(sums)
+        L.call("psvo_criterion_finalize", stream, L.ptr(sums), n_hit, s_cols, rgb_w, depth_w, fs_w, sdf_w, tr, flags,
+               L.ptr(out))
+        ctx.save_for_backward(color, depth, sdf, z_vals, gt_rgb, gt_depth, rank_ray, out)
+        ctx.cfg = cfg
+        if sink is not None:
+            sink.append(out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        color, depth, sdf, z_vals, gt_rgb, gt_depth, rank_ray, out = ctx.saved_tensors
+        tr, max_depth = ctx.cfg[0], ctx.cfg[1]
+        r_hit, s_max = z_vals.shape
+        dev = z_vals.device
+        g = g_loss.detach().float().contiguous()
+        g_color = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
+        g_depth = torch.empty((r_hit,), dtype=torch.float32, device=dev)
+        g_sdf = torch.empty((r_hit, s_max), dtype=torch.float32, device=dev)
+        L.call("psvo_criterion_bwd", L.stream_of(dev), r_hit, s_max, tr, max_depth, L.ptr(rank_ray), L.ptr(gt_rgb),
+               L.ptr(gt_depth), L.ptr(color), L.ptr(depth), L.ptr(sdf), L.ptr(z_vals), L.ptr(out), L.ptr(g),
+               L.ptr(g_color), L.ptr(g_depth), L.ptr(g_sdf))
+        return g_color, g_depth, g_sdf, None, None, None, None, None, None, None
 
 
 class LazyLossDict(dict):
@@ -41,7 +100,9 @@ class Criterion(nn.Module):
         self.max_dpeth = args.data_specs["max_depth"]
 
     def forward(self, outputs, obs, use_color_loss=True, use_depth_loss=True, compute_sdf_loss=True,
-                weight_depth_loss=False):
+                weight_depth_loss=False, reduce_sums=None):
+        if outputs.get("rank_ray") is not None and not weight_depth_loss and outputs["z_vals"].is_cuda:
+            return self._forward_fused(outputs, obs, use_color_loss, use_depth_loss, compute_sdf_loss, reduce_sums)
         img, depth = obs
         loss = 0
         loss_dict = LazyLossDict()
@@ -76,6 +137,30 @@ class Criterion(nn.Module):
             loss_dict["sdf_loss"] = sdf_loss
         loss_dict["loss"] = loss.detach() if isinstance(loss, torch.Tensor) else loss
         return loss, loss_dict
+
+    def _forward_fused(self, outputs, obs, use_color, use_depth, use_sdf, reduce_sums):
+        img, depth = obs
+        flags = (_USE_COLOR if use_color else 0) | (_USE_DEPTH if use_depth else 0) | (_USE_SDF if use_sdf else 0)
+        cfg = (float(self.truncation), float(self.max_dpeth), float(self.rgb_weight), float(self.depth_weight),
+               float(self.fs_weight), float(self.sdf_weight), flags)
+        dev = outputs["z_vals"].device
+        gt_rgb = img.reshape(-1, 3).to(device=dev, dtype=torch.float32).contiguous()
+        gt_depth = depth.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
+        f = lambda t: t.float().contiguous()
+        sink = []
+        loss = CriterionLoss.apply(f(outputs["color"]), f(outputs["depth"]), f(outputs["sdf"]), f(outputs["z_vals"]),
+                                   gt_rgb, gt_depth, outputs["rank_ray"], cfg, reduce_sums, sink)
+        out = sink[0]
+        parts = LazyLossDict()
+        if use_color:
+            parts["color_loss"] = out[1]
+        if use_depth:
+            parts["depth_loss"] = out[2]
+        if use_sdf:
+            parts["fs_loss"] = out[3]
+            parts["sdf_loss"] = out[4]
+        parts["loss"] = loss.detach()
+        return loss, parts
 
     def compute_loss(self, x, y, mask=None, loss_type="l2"):
         if mask is None:

@@ -151,7 +151,7 @@ class RaySamples:
     """Everything the differentiable part needs about one ray batch."""
 
     __slots__ = ("ray_mask", "rank_ray", "r_hit", "P", "s_max", "m", "z_vals", "sample_mask", "leaf", "t",
-                 "ray_of_sample", "offsets", "ray_ns", "s_idx", "s_depth", "s_dist", "visits", "max_steps")
+                 "ray_of_sample", "offsets", "ray_ns", "rank_ray32", "s_idx", "s_depth", "s_dist", "visits", "max_steps")
 
 
 @torch.no_grad()
@@ -200,7 +200,8 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
            L.ptr(offsets), L.ptr(leaf), L.ptr(t), L.ptr(ray_of_sample), L.ptr(z_vals), L.ptr(mask))
     out = RaySamples()
     out.ray_mask = (ray_rank >= 0).view(1, R)
-    out.rank_ray = rank_ray[:r_hit].long()
+    out.rank_ray32 = rank_ray[:r_hit]
+    out.rank_ray = out.rank_ray32.long()
     out.r_hit, out.P, out.s_max, out.m, out.visits, out.max_steps = r_hit, P, s_max, m, visits, max_steps
     out.z_vals, out.sample_mask = z_vals, mask.bool()
     out.leaf, out.t, out.ray_of_sample, out.offsets, out.ray_ns = leaf, t, ray_of_sample, offsets, ray_ns
@@ -244,6 +245,7 @@ def render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxe
         "sdf": sdf,
         "ray_mask": smp.ray_mask,
         "raw": z_min if return_raw else None,
+        "rank_ray": smp.rank_ray32,  # hit-ray order for the fused Criterion (not in the reference dict)
     }
     if return_samples:
         out["samples"] = smp
