@@ -191,8 +191,8 @@ def main():
         ro, rd, rgb, depth = batches[i % len(batches)]
         out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True)
         loss, _ = criterion(out, (rgb, depth))
-        embed_optim.zero_grad(set_to_none=False)
-        model_optim.zero_grad(set_to_none=False)
+        embed_optim.zero_grad()  # set_to_none, as optim.zero_grad() in render_helpers.py:668
+        model_optim.zero_grad()
         loss.backward()
         if world > 1:
             flat = torch.cat([p.grad.reshape(-1) for p in params])
