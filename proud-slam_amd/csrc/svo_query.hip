@@ -431,66 +431,188 @@ __global__ __launch_bounds__(64) void k_sample_raw(int b, int num_rays, int max_
         });
 }
 
-__global__ __launch_bounds__(64) void k_sample_fused(int64_t r_hit_cap, int max_steps_cap,
-                                                     const int *__restrict__ rank_ray,
-                                                     const int *__restrict__ hit_idx,
-                                                     const float *__restrict__ hit_t0,
-                                                     const float *__restrict__ hit_t1,
-                                                     const float *__restrict__ ray_dsum, float step_size,
-                                                     const float *__restrict__ noise, uint64_t seed,
-                                                     int *__restrict__ stats, int *__restrict__ s_idx,
-                                                     float *__restrict__ s_depth, float *__restrict__ s_dist,
-                                                     int *__restrict__ ray_ns) {
+// Wave-parallel restatement of sample_one for one ray (one wave), valid when
+// the cdf sequence ((cs + noise) * step) is non-decreasing — noise in [0, 1)
+// and probs >= 0, which the fused path guarantees (probs are interval
+// lengths / their sum; noise is clamped to [0.001, 0.999] or caller-given in
+// [0, 1)).  The serial loop's output is a merge of two sorted streams:
+//   interior sample cs in bin b(cs)   at position cs + b(cs)
+//   end of bin b (bins it passed)     at position C_b + b
+// with C_b = #{cs : !(cdf_cs > hcdf_b)} (first cs beyond bin b) and
+// b(cs) = #{b : C_b <= cs}.  The trailing segment (sample_gpu.cu:224-237) is a
+// run of consecutive bins whose first failing predicate a ballot finds.
+// Every value is computed with the same float expressions as sample_one, so
+// outputs are bit-identical to it.  Lane b owns bin b (max_hits <= 64).
+template <typename Rows, typename Noise, typename Emit>
+__device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int num_rays, int H, Noise noise, Emit emit,
+                           int lane) {
+    const bool own = lane < max_hits;
+    const int idx_b = own ? rows.idx_at(lane) : -1;
+    const float lo_b = own ? rows.lo_at(lane) : 0.0f;
+    const float hi_b = own ? rows.hi_at(lane) : 0.0f;
+    const float prob_b = own ? rows.prob_at(lane) : 0.0f;
+    // valid bins [0, nb): the serial loop stops at the first bin >= 1 with idx -1
+    const uint64_t inval = __ballot(own && lane >= 1 && idx_b == -1);
+    const int nb = inval ? min(__ffsll((unsigned long long)inval) - 1, max_hits) : max_hits;
+    // hcdf_b: the serial running sum, same order of float additions
+    float acc = 0.0f, hcdf_b = 0.0f;
+    for (int k = 0; k < nb; ++k) {
+        const float pk = __shfl(prob_b, k, kWave);
+        acc = (k == 0) ? pk : acc + pk;
+        if (k == lane) hcdf_b = acc;
+    }
+    const float step = (float)(1.0 / (double)steps_j);
+    const int total_steps = (int)ceilf(steps_j);
+    auto cdf_at = [&](int cs) { return ((float)cs + noise(cs)) * step; };
+    // C_b = first cs in [0, total_steps) with cdf_cs > hcdf_b (total_steps if none)
+    int c_b = total_steps;
+    if (lane < nb) {
+        int lo = 0, hi = total_steps;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cdf_at(mid) > hcdf_b) hi = mid; else lo = mid + 1;
+        }
+        c_b = lo;
+    } else {
+        c_b = 0x7fffffff;  // bins past nb never end by cdf
+    }
+    const int cs_end = __shfl(c_b, nb - 1, kWave);  // first cs past the last valid bin
+    const bool done = cs_end < total_steps;
+    const int cs_lim = done ? cs_end : total_steps;
+    // b(cs) = #{b < nb : C_b <= cs}; C_b is non-decreasing in b
+    auto bin_of = [&](int cs) {
+        int lo = 0, hi = nb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (__shfl(c_b, mid, kWave) <= cs) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    // z of interior sample c lying in bin b (sample_one: u, z)
+    auto z_at = [&](int c, int b) {
+        const float hc = __shfl(hcdf_b, b, kWave);
+        const float lc = b == 0 ? 0.0f : __shfl(hcdf_b, b > 0 ? b - 1 : 0, kWave);
+        const float lo = __shfl(lo_b, b, kWave), hi = __shfl(hi_b, b, kWave);
+        const float u = __fdiv_rn(cdf_at(c) - lc, hc - lc);
+        return lo + u * (hi - lo);
+    };
+    // interior samples.  The shuffles inside bin_of / z_at need every lane, so
+    // the loop runs to a wave-uniform bound and masks the tail.
+    for (int base = 0; base < cs_lim; base += kWave) {
+        const int cs = base + lane;
+        const bool act = cs < cs_lim;
+        const int b = bin_of(act ? cs : 0);
+        const int c_prev = b == 0 ? 0 : __shfl(c_b, b > 0 ? b - 1 : 0, kWave);
+        const bool first = cs == c_prev;
+        const float z = z_at(act ? cs : 0, b);
+        const float zp = z_at(act && !first ? cs - 1 : (act ? cs : 0), b);
+        const float z_low = first ? __shfl(lo_b, b, kWave) : zp;
+        const int vb = __shfl(idx_b, b, kWave);
+        if (act) emit(cs + b, vb, (z + z_low) * 0.5f, z - z_low);
+    }
+    // ends of the bins the main loop passed
+    const int b_last = total_steps > 0 && !done ? bin_of(total_steps - 1) : 0;
+    const int n_ends = done ? nb : b_last;
+    const int c_prev_own = lane == 0 ? 0 : __shfl(c_b, lane > 0 ? lane - 1 : 0, kWave);
+    {
+        const bool has = lane < nb && c_b > c_prev_own;  // interior samples in my bin
+        const float zl_last = z_at(has ? c_b - 1 : 0, lane < nb ? lane : 0);
+        const float z_low = has ? zl_last : lo_b;
+        if (lane < n_ends) emit(c_b + lane, idx_b, (hi_b + z_low) * 0.5f, hi_b - z_low);
+    }
+    int s = cs_lim + n_ends;
+    // trailing segment
+    int bin0;
+    float zl, hi_d;
+    if (done) {
+        bin0 = nb;
+        const int bl = nb - 1;
+        const int cl = __shfl(c_b, bl, kWave), cp = bl == 0 ? 0 : __shfl(c_b, bl > 0 ? bl - 1 : 0, kWave);
+        const float zz = z_at(cl > cp ? cl - 1 : 0, bl);
+        zl = cl > cp ? zz : __shfl(lo_b, bl, kWave);
+        hi_d = __shfl(hi_b, bl, kWave);
+    } else if (total_steps == 0) {
+        bin0 = 0;
+        zl = __shfl(lo_b, 0, kWave);
+        hi_d = __shfl(hi_b, 0, kWave);
+    } else {
+        bin0 = b_last;
+        zl = z_at(total_steps - 1, b_last);
+        hi_d = __shfl(hi_b, b_last, kWave);
+    }
+    if (zl < hi_d && num_rays > H + bin0) {
+        const int v0 = bin0 < max_hits ? __shfl(idx_b, bin0 < kWave ? bin0 : 0, kWave) : rows.idx_at(bin0);
+        if (lane == 0) emit(s, v0, (hi_d + zl) * 0.5f, hi_d - zl);
+        // bins k > bin0 continue while idx_slot0(k) != -1 && lo < hi && num_rays > H + k
+        const bool cont = own && lane > bin0 && rows.idx_slot0(lane) != -1 && lo_b < hi_b && num_rays > H + lane;
+        const uint64_t fail = ~__ballot(cont) & (~0ull << (bin0 + 1 < 64 ? bin0 + 1 : 63));
+        const int k_end = bin0 + 1 >= 64 ? bin0 + 1 : (fail ? __ffsll((unsigned long long)fail) - 1 : 64);
+        if (lane > bin0 && lane < k_end) emit(s + (lane - bin0), idx_b, (hi_b + lo_b) * 0.5f, hi_b - lo_b);
+        s += k_end - bin0;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max_steps_cap,
+                                                      const int *__restrict__ rank_ray,
+                                                      const int *__restrict__ hit_idx,
+                                                      const float *__restrict__ hit_t0,
+                                                      const float *__restrict__ hit_t1,
+                                                      const float *__restrict__ ray_dsum, float step_size,
+                                                      const float *__restrict__ noise, uint64_t seed,
+                                                      int *__restrict__ stats, int *__restrict__ s_idx,
+                                                      float *__restrict__ s_depth, float *__restrict__ s_dist,
+                                                      int *__restrict__ ray_ns) {
     const int P = stats[PSVO_STAT_P];
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
-    const int lane = threadIdx.x;
-    const int i = blockIdx.x * kWave + lane;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int i = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    if (i >= r_hit || i >= r_hit_cap || P <= 0) return;
+    if (max_steps > max_steps_cap && lane == 0 && i == 0) atomicOr(stats + 7, 2);
+    const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
+    const int b = i / kp;
+    const int j = i - b * kp;
+    const int c = j / kSamplerChunk;
+    const int jj = j - c * kSamplerChunk;
+    const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
+    FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj};
+    const float dsum = ray_dsum[rank_ray[i]];
+    const float steps_j = __fdiv_rn(dsum, step_size);
+    const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
+    int *oi = s_idx + (int64_t)i * max_steps_cap;
+    float *od = s_depth + (int64_t)i * max_steps_cap;
+    float *os = s_dist + (int64_t)i * max_steps_cap;
+    const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
+    const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
     int count = 0;
-    if (i < r_hit && i < r_hit_cap && P > 0) {
-        if (max_steps > max_steps_cap && lane == 0) atomicOr(stats + 7, 2);
-        const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
-        const int b = i / kp;
-        const int j = i - b * kp;
-        const int c = j / kSamplerChunk;
-        const int jj = j - c * kSamplerChunk;
-        const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
-        FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj};
-        const float dsum = ray_dsum[rank_ray[i]];
-        const float steps_j = __fdiv_rn(dsum, step_size);
-        const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
-        int *oi = s_idx + (int64_t)i * max_steps_cap;
-        float *od = s_depth + (int64_t)i * max_steps_cap;
-        float *os = s_dist + (int64_t)i * max_steps_cap;
-        const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
-        const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
-        const int s_end = sample_one(
-            rows, steps_j, -1.0f, P, nr, jj * P, cap,
-            [&](int cs) {
-                if (nz) return nz[cs];
-                const float u = (float)(mix32(key + (uint64_t)cs) >> 8) * (1.0f / 16777216.0f);
-                return fminf(fmaxf(u, 0.001f), 0.999f);
-            },
-            [&](int s, int v, float dep, float dis) {
-                // voxel_helpers.py:654-656: clamp dists, MAX_DEPTH / 0 where idx == -1
-                oi[s] = v;
-                od[s] = v == -1 ? kMaxDepthFill : dep;
-                os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
-                count += (v != -1);
-            });
-        const int s_written = s_end < cap ? s_end : cap;
-        for (int s = s_written; s < max_steps_cap; ++s) {
-            oi[s] = -1;
-            od[s] = kMaxDepthFill;
-            os[s] = 0.0f;
-        }
-        ray_ns[i] = count;
+    const int s_end = sample_wave(
+        rows, steps_j, P, nr, jj * P,
+        [&](int cs) {
+            if (nz) return nz[cs];
+            const float u = (float)(mix32(key + (uint64_t)cs) >> 8) * (1.0f / 16777216.0f);
+            return fminf(fmaxf(u, 0.001f), 0.999f);
+        },
+        [&](int s, int v, float dep, float dis) {
+            if (s >= cap) return;
+            // voxel_helpers.py:654-656: clamp dists, MAX_DEPTH / 0 where idx == -1
+            oi[s] = v;
+            od[s] = v == -1 ? kMaxDepthFill : dep;
+            os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
+            count += (v != -1);
+        },
+        lane);
+    const int s_written = s_end < cap ? s_end : cap;
+    for (int s = s_written + lane; s < max_steps_cap; s += kWave) {
+        oi[s] = -1;
+        od[s] = kMaxDepthFill;
+        os[s] = 0.0f;
     }
-    const int wmax = wave_max(count);
-    const int wsum = wave_sum(count);
+    count = wave_sum(count);
     if (lane == 0) {
-        atomicMax(stats + PSVO_STAT_S_MAX, wmax);
-        atomicAdd(stats + PSVO_STAT_M, wsum);
+        ray_ns[i] = count;
+        atomicMax(stats + PSVO_STAT_S_MAX, count);
+        atomicAdd(stats + PSVO_STAT_M, count);
     }
 }
 
@@ -578,7 +700,7 @@ extern "C" int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_c
                                 float *s_depth, float *s_dist, int *ray_ns) {
     PSVO_REQUIRE(r_hit_cap >= 0 && max_steps_cap > 0, "sample_rays: bad caps");
     if (r_hit_cap == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, kWave)), dim3(kWave), 0, as_stream(stream), r_hit_cap,
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, as_stream(stream), r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns);
     return check_launch("sample_rays");

@@ -79,7 +79,10 @@ def exported_symbols():
 
 
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    """Call a psvo entry point; tensor arguments are passed as their data
+    pointers and stay referenced (alive) until the call returns."""
+    cargs = [ctypes.c_void_p(a.data_ptr()) if isinstance(a, torch.Tensor) else a for a in args]
+    rc = getattr(lib(), name)(*cargs)
     if rc != 0:
         msg = lib().psvo_last_error().decode(errors="replace")
         raise PsvoError(f"{name} failed (code {rc}): {msg}")

@@ -139,8 +139,8 @@ class CompositeRays(Function):
         g_sdf_s = torch.empty((ctx.m,), dtype=torch.float32, device=dev)
         g_rgb_s = torch.empty((ctx.m, 3), dtype=torch.float32, device=dev)
         L.call("psvo_composite_bwd", L.stream_of(dev), r_hit, s_max, ctx.truncation, L.ptr(offsets), L.ptr(ray_ns),
-               L.ptr(z_vals), L.ptr(sdf), L.ptr(weights), L.ptr(rgb_s), L.ptr(c(g_color)), L.ptr(c(g_depth)),
-               L.ptr(c(g_weights)), L.ptr(c(g_sdf)), L.ptr(g_sdf_s), L.ptr(g_rgb_s))
+               L.ptr(z_vals), L.ptr(sdf), L.ptr(weights), L.ptr(rgb_s), c(g_color), c(g_depth), c(g_weights),
+               c(g_sdf), L.ptr(g_sdf_s), L.ptr(g_rgb_s))
         return g_sdf_s, g_rgb_s, None, None, None, None
 
 

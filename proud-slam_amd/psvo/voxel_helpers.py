@@ -118,8 +118,8 @@ def _intersect_sorted(rays_o, rays_d, centres, structure, voxel_size, max_distan
     ray_nv = torch.empty((R,), dtype=torch.int32, device=dev)
     ray_dsum = torch.empty((R,), dtype=torch.float32, device=dev)
     stats = torch.zeros((STAT_WORDS,), dtype=torch.int32, device=dev)
-    L.call("psvo_ray_intersect_sorted", L.stream_of(dev), R, L.ptr(ro), L.ptr(rd), L.ptr(centres.float().contiguous()),
-           L.ptr(structure.int().contiguous()), float(voxel_size), float(max_distance), float(step_size),
+    L.call("psvo_ray_intersect_sorted", L.stream_of(dev), R, L.ptr(ro), L.ptr(rd), centres.float().contiguous(),
+           structure.int().contiguous(), float(voxel_size), float(max_distance), float(step_size),
            L.ptr(hit_idx), L.ptr(hit_t0), L.ptr(hit_t1), L.ptr(ray_nv), L.ptr(ray_dsum), L.ptr(stats))
     return dict(ro=ro, rd=rd, hit_idx=hit_idx, hit_t0=hit_t0, hit_t1=hit_t1, ray_nv=ray_nv, ray_dsum=ray_dsum,
                 stats=stats, R=R)

@@ -261,3 +261,47 @@ def test_full_size_properties():
     loss = out["color"].sum() + out["depth"].sum() + out["sdf"].sum()
     loss.backward()
     assert torch.isfinite(emb.grad).all()
+
+
+@pytest.mark.parametrize("step", [0.0078, 0.05])
+def test_fused_sampler_matches_oracle_full_size(step):
+    """The wave-parallel fused sampler (one wave per hit ray) against the C
+    oracle's serial restatement of sample_gpu.cu on BASELINE config B
+    (room0, 4096 rays), fed the same intersections, probs and noise: sample
+    indices, depths and distances bit-identical."""
+    from psvo import synthetic as syn
+    from psvo.octree import Octree, map_states
+    from psvo.render_helpers import query_samples
+    from psvo.voxel_helpers import _intersect_sorted
+    w = syn.make_workload("room0", 4, 1024, seed=3)
+    tree = Octree()
+    tree.init(256, 16, 0.2, 8)
+    tree.insert(w.voxels)
+    ms = map_states(tree, torch.zeros(tree.count_nodes(), 16, device=DEV), 0.2, device=DEV)
+    ro, rd = w.rays_o.to(DEV), w.rays_d.to(DEV)
+    q = _intersect_sorted(ro, rd, ms["voxel_center_xyz"], ms["voxel_structure"], 0.2, 10.0, step)
+    st = q["stats"].cpu()
+    P, r_hit, max_ceil = int(st[0]), int(st[1]), int(st[2])
+    hit = torch.nonzero(q["ray_nv"].cpu() > 0).squeeze(1)
+    idx = q["hit_idx"].cpu()[hit, :P]
+    t0 = q["hit_t0"].cpu()[hit, :P]
+    t1 = q["hit_t1"].cpu()[hit, :P]
+    dsum = q["ray_dsum"].cpu()[hit]
+    dd = torch.where(idx != -1, t1 - t0, torch.zeros_like(t0))
+    probs = torch.from_numpy(dd.numpy() / dsum.numpy()[:, None])
+    steps = torch.from_numpy(dsum.numpy() / np.float32(step))
+    kp = (r_hit + 199) // 200
+    max_steps = max_ceil + P
+    noise = torch.rand((200, kp, max_steps), generator=torch.Generator().manual_seed(5)).clamp(0.001, 0.999)
+    o_idx, o_dep, o_dis, _ = O.inverse_cdf_sampling(idx, t0, t1, probs, steps, -1.0, noise)
+    o_dis = o_dis.clamp(min=0.0)
+    o_dep = o_dep.masked_fill(o_idx.eq(-1), O.MAX_DEPTH)
+    o_dis = o_dis.masked_fill(o_idx.eq(-1), 0.0)
+    smp = query_samples(ro, rd, ms, step, 0.2, 10.0, noise=noise)
+    n = o_idx.shape[1]
+    g_idx, g_dep, g_dis = smp.s_idx.cpu(), smp.s_depth.cpu(), smp.s_dist.cpu()
+    assert smp.r_hit == r_hit and g_idx.shape[0] == o_idx.shape[0]
+    np.testing.assert_array_equal(g_idx[:, :n].numpy(), o_idx.numpy())
+    np.testing.assert_array_equal(g_dep[:, :n].numpy(), o_dep.numpy())
+    np.testing.assert_array_equal(g_dis[:, :n].numpy(), o_dis.numpy())
+    assert bool((g_idx[:, n:] == -1).all())
