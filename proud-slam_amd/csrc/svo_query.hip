@@ -176,68 +176,153 @@ __device__ __forceinline__ int wave_sum(int v) {
 // ---------------------------------------------------------------------------
 // fused ray_intersect_vox: DFS → stable sort by t_in → max_distance trim,
 // plus per-ray Σ(t_out - t_in) for the sampler's probs / steps.
-__global__ __launch_bounds__(64) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
-                                                         const float *__restrict__ rays_d,
-                                                         const float *__restrict__ centres,
-                                                         const int *__restrict__ structure, float voxel_size,
-                                                         float max_distance, float step_size,
-                                                         int *__restrict__ hit_idx, float *__restrict__ hit_t0,
-                                                         float *__restrict__ hit_t1, int *__restrict__ ray_nv,
-                                                         float *__restrict__ ray_dsum, int *__restrict__ stats) {
-    __shared__ int l_node[kLevels * kWave];
-    __shared__ int l_mask[kLevels * kWave];
-    __shared__ int h_idx[kMaxHits * kWave];
-    __shared__ float h_t0[kMaxHits * kWave];
-    __shared__ float h_t1[kMaxHits * kWave];
-    const int lane = threadIdx.x;
-    const int64_t r = (int64_t)blockIdx.x * kWave + lane;
-    int nv = 0, visits = 0, ceil_steps = 0;
+//
+// Eight lanes per ray (lane u of the group owns child slot u), eight rays per
+// wave.  Expanding a node tests its ≤8 children in parallel and records, per
+// level, the hit / leaf bitmasks and each child's (id, t_in, t_out) in LDS;
+// the DFS then pops hit children highest slot first — the reference's 7→0
+// order — so leaf hits are emitted in exactly the serial order and the
+// ≤ n_max cap cuts the same list.  The dependent-load chain per ray shrinks
+// from one per AABB test to one per internal node on the path.  The stable
+// sort is a rank sort (rank = #{t_j < t_i} + #{t_j == t_i, j < i}).
+constexpr int kGrp = 8;                 // lanes per ray
+constexpr int kRaysPerWave = kWave / kGrp;
+constexpr int kIsWaves = 4;             // waves per block
+
+struct IsLds {
+    float t0[kLevels][kWave];
+    float t1[kLevels][kWave];
+    int kid[kLevels][kWave];
+    int mask[kLevels][kWave];  // bits 0-7 hit children left, bits 8-15 leaf children
+    int h_idx[kRaysPerWave][kMaxHits];
+    float h_t0[kRaysPerWave][kMaxHits];
+    float h_t1[kRaysPerWave][kMaxHits];
+    float h_d[kRaysPerWave][kMaxHits];  // t_out - t_in in sorted order
+};
+
+__global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
+                                                          const float *__restrict__ rays_d,
+                                                          const float *__restrict__ centres,
+                                                          const int *__restrict__ structure, float voxel_size,
+                                                          float max_distance, float step_size,
+                                                          int *__restrict__ hit_idx, float *__restrict__ hit_t0,
+                                                          float *__restrict__ hit_t1, int *__restrict__ ray_nv,
+                                                          float *__restrict__ ray_dsum, int *__restrict__ stats) {
+    __shared__ IsLds lds_all[kIsWaves];
+    IsLds &S = lds_all[threadIdx.x / kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / kGrp, u = lane & (kGrp - 1);
+    const int64_t r = ((int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave) * kRaysPerWave + g;
+    const float half = voxel_size * 0.5f;
+    int nv = 0, visits = 0, ceil_steps = 0, cnt = 0;
     bool overflow = false;
     if (r < n_rays) {
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
         const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
-        int *hi = h_idx + lane;
-        float *ha = h_t0 + lane;
-        float *hb = h_t1 + lane;
-        int cnt = 0;
-        visits = dfs_ray(o, d, centres, structure, voxel_size * 0.5f, kMaxHits, l_node + lane, l_mask + lane, hi,
-                         ha, hb, &cnt, &overflow);
-        // stable insertion sort by t_in (DFS emission order breaks ties)
-        for (int i = 1; i < cnt; ++i) {
-            const int ki = hi[i * kWave];
-            const float ka = ha[i * kWave], kb = hb[i * kWave];
-            int j = i - 1;
-            while (j >= 0 && ha[j * kWave] > ka) {
-                hi[(j + 1) * kWave] = hi[j * kWave];
-                ha[(j + 1) * kWave] = ha[j * kWave];
-                hb[(j + 1) * kWave] = hb[j * kWave];
-                --j;
+        float inv[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, d[a]);
+        // test the children of `node` into level `lvl` (all 8 lanes of the group)
+        auto expand = [&](int node, int lvl) {
+            const int k = structure[(int64_t)node * 9 + u];
+            bool hit = false, leaf = false;
+            float a = 0.0f, b = 0.0f;
+            if (k > -1) {
+                const int side = structure[(int64_t)k * 9 + 8];
+                const float *pc = centres + (int64_t)k * 3;
+                hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                leaf = side == 1;
+                ++visits;
             }
-            hi[(j + 1) * kWave] = ki;
-            ha[(j + 1) * kWave] = ka;
-            hb[(j + 1) * kWave] = kb;
+            S.t0[lvl][lane] = a;
+            S.t1[lvl][lane] = b;
+            S.kid[lvl][lane] = k;
+            const uint64_t hb = __ballot(hit), lb = __ballot(hit && leaf);
+            S.mask[lvl][lane] = (int)((hb >> (g * kGrp)) & 0xff) | ((int)((lb >> (g * kGrp)) & 0xff) << 8);
+        };
+        int lvl = -1;
+        {
+            float a = 0.0f, b = 0.0f;
+            const int side = structure[8];
+            const bool hit = ray_aabb(o, inv, centres[0], centres[1], centres[2], half * (float)side, a, b);
+            if (u == 0) ++visits;
+            if (hit) {
+                if (side == 1) {
+                    if (u == 0) {
+                        S.h_idx[g][0] = 0;
+                        S.h_t0[g][0] = a;
+                        S.h_t1[g][0] = b;
+                    }
+                    cnt = 1;
+                } else {
+                    lvl = 0;
+                    expand(0, 0);
+                }
+            }
         }
-        while (nv < cnt && !(ha[nv * kWave] > max_distance)) ++nv;
-        float dsum = 0.0f;
-        int *oi = hit_idx + r * kMaxHits;
-        float *oa = hit_t0 + r * kMaxHits;
-        float *ob = hit_t1 + r * kMaxHits;
-        for (int l = 0; l < kMaxHits; ++l) {
-            const bool v = l < nv;
-            const float a = v ? ha[l * kWave] : max_distance;
-            const float bb = v ? hb[l * kWave] : max_distance;
-            if (v) dsum = dsum + (bb - a);
-            oi[l] = v ? hi[l * kWave] : -1;
-            oa[l] = a;
-            ob[l] = bb;
+        while (lvl >= 0 && cnt < kMaxHits) {
+            const int mm = S.mask[lvl][lane];
+            const int m = mm & 0xff;
+            if (m == 0) {
+                --lvl;
+                continue;
+            }
+            const int ub = 31 - __clz(m);
+            S.mask[lvl][lane] = mm & ~(1 << ub);
+            if ((mm >> 8) & (1 << ub)) {  // leaf hit: emitted by the lane that tested it
+                if (u == ub) {
+                    S.h_idx[g][cnt] = S.kid[lvl][lane];
+                    S.h_t0[g][cnt] = S.t0[lvl][lane];
+                    S.h_t1[g][cnt] = S.t1[lvl][lane];
+                }
+                ++cnt;
+                continue;
+            }
+            if (lvl + 1 >= kLevels) {
+                overflow = true;
+                break;
+            }
+            const int k = S.kid[lvl][g * kGrp + ub];
+            ++lvl;
+            expand(k, lvl);
         }
-        ray_nv[r] = nv;
-        ray_dsum[r] = dsum;
-        if (nv > 0) ceil_steps = (int)ceilf(__fdiv_rn(dsum, step_size));
+        // stable rank sort by t_in, then the max_distance trim (a prefix after sorting)
+        for (int i = u; i < cnt; i += kGrp) {
+            const float ti = S.h_t0[g][i];
+            int rank = 0;
+            for (int j = 0; j < cnt; ++j) {
+                const float tj = S.h_t0[g][j];
+                rank += (tj < ti) || (tj == ti && j < i);
+            }
+            nv += !(ti > max_distance);
+            const float bi = S.h_t1[g][i];
+            S.h_d[g][rank] = bi - ti;
+            if (!(ti > max_distance)) {
+                hit_idx[r * kMaxHits + rank] = S.h_idx[g][i];
+                hit_t0[r * kMaxHits + rank] = ti;
+                hit_t1[r * kMaxHits + rank] = bi;
+            }
+        }
+        // group-reduce nv (each lane counted its own entries)
+#pragma unroll
+        for (int sh = 1; sh < kGrp; sh <<= 1) nv += __shfl_xor(nv, sh, kWave);
+        for (int l = nv + u; l < kMaxHits; l += kGrp) {
+            hit_idx[r * kMaxHits + l] = -1;
+            hit_t0[r * kMaxHits + l] = max_distance;
+            hit_t1[r * kMaxHits + l] = max_distance;
+        }
+        if (u == 0) {
+            float dsum = 0.0f;
+            for (int l = 0; l < nv; ++l) dsum = dsum + S.h_d[g][l];
+            ray_nv[r] = nv;
+            ray_dsum[r] = dsum;
+            if (nv > 0) ceil_steps = (int)ceilf(__fdiv_rn(dsum, step_size));
+        }
     }
-    const int wmax_nv = wave_max(nv);
-    const int whit = wave_sum(nv > 0 ? 1 : 0);
-    const int wceil = wave_max(ceil_steps);
+    const bool lead = u == 0 && r < n_rays;
+    const int wmax_nv = wave_max(lead ? nv : 0);
+    const int whit = wave_sum(lead && nv > 0 ? 1 : 0);
+    const int wceil = wave_max(lead ? ceil_steps : 0);
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow ? 1 : 0);
     if (lane == 0) {
@@ -443,9 +528,20 @@ __global__ __launch_bounds__(64) void k_sample_raw(int b, int num_rays, int max_
 // run of consecutive bins whose first failing predicate a ballot finds.
 // Every value is computed with the same float expressions as sample_one, so
 // outputs are bit-identical to it.  Lane b owns bin b (max_hits <= 64).
+struct WaveBins {  // per-wave LDS: bin b written by lane b, read by any lane
+    float hc[kWave], lo[kWave], hi[kWave];
+    int idx[kWave], c[kWave];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <typename Rows, typename Noise, typename Emit>
 __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int num_rays, int H, Noise noise, Emit emit,
-                           int lane) {
+                           int lane, WaveBins &W) {
     const bool own = lane < max_hits;
     const int idx_b = own ? rows.idx_at(lane) : -1;
     const float lo_b = own ? rows.lo_at(lane) : 0.0f;
@@ -465,7 +561,7 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
     const int total_steps = (int)ceilf(steps_j);
     auto cdf_at = [&](int cs) { return ((float)cs + noise(cs)) * step; };
     // C_b = first cs in [0, total_steps) with cdf_cs > hcdf_b (total_steps if none)
-    int c_b = total_steps;
+    int c_b = 0x7fffffff;  // bins past nb never end by cdf
     if (lane < nb) {
         int lo = 0, hi = total_steps;
         while (lo < hi) {
@@ -473,10 +569,14 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
             if (cdf_at(mid) > hcdf_b) hi = mid; else lo = mid + 1;
         }
         c_b = lo;
-    } else {
-        c_b = 0x7fffffff;  // bins past nb never end by cdf
     }
-    const int cs_end = __shfl(c_b, nb - 1, kWave);  // first cs past the last valid bin
+    W.hc[lane] = hcdf_b;
+    W.lo[lane] = lo_b;
+    W.hi[lane] = hi_b;
+    W.idx[lane] = idx_b;
+    W.c[lane] = c_b;
+    wave_lds_sync();
+    const int cs_end = W.c[nb - 1];  // first cs past the last valid bin
     const bool done = cs_end < total_steps;
     const int cs_lim = done ? cs_end : total_steps;
     // b(cs) = #{b < nb : C_b <= cs}; C_b is non-decreasing in b
@@ -484,64 +584,51 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
         int lo = 0, hi = nb;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (__shfl(c_b, mid, kWave) <= cs) lo = mid + 1; else hi = mid;
+            if (W.c[mid] <= cs) lo = mid + 1; else hi = mid;
         }
         return lo;
     };
+    auto c_before = [&](int b) { return b == 0 ? 0 : W.c[b - 1]; };
     // z of interior sample c lying in bin b (sample_one: u, z)
     auto z_at = [&](int c, int b) {
-        const float hc = __shfl(hcdf_b, b, kWave);
-        const float lc = b == 0 ? 0.0f : __shfl(hcdf_b, b > 0 ? b - 1 : 0, kWave);
-        const float lo = __shfl(lo_b, b, kWave), hi = __shfl(hi_b, b, kWave);
+        const float hc = W.hc[b];
+        const float lc = b == 0 ? 0.0f : W.hc[b - 1];
+        const float lo = W.lo[b], hi = W.hi[b];
         const float u = __fdiv_rn(cdf_at(c) - lc, hc - lc);
         return lo + u * (hi - lo);
     };
-    // interior samples.  The shuffles inside bin_of / z_at need every lane, so
-    // the loop runs to a wave-uniform bound and masks the tail.
-    for (int base = 0; base < cs_lim; base += kWave) {
-        const int cs = base + lane;
-        const bool act = cs < cs_lim;
-        const int b = bin_of(act ? cs : 0);
-        const int c_prev = b == 0 ? 0 : __shfl(c_b, b > 0 ? b - 1 : 0, kWave);
-        const bool first = cs == c_prev;
-        const float z = z_at(act ? cs : 0, b);
-        const float zp = z_at(act && !first ? cs - 1 : (act ? cs : 0), b);
-        const float z_low = first ? __shfl(lo_b, b, kWave) : zp;
-        const int vb = __shfl(idx_b, b, kWave);
-        if (act) emit(cs + b, vb, (z + z_low) * 0.5f, z - z_low);
+    // interior samples
+    for (int cs = lane; cs < cs_lim; cs += kWave) {
+        const int b = bin_of(cs);
+        const float z = z_at(cs, b);
+        const float z_low = cs == c_before(b) ? W.lo[b] : z_at(cs - 1, b);
+        emit(cs + b, W.idx[b], (z + z_low) * 0.5f, z - z_low);
     }
     // ends of the bins the main loop passed
     const int b_last = total_steps > 0 && !done ? bin_of(total_steps - 1) : 0;
     const int n_ends = done ? nb : b_last;
-    const int c_prev_own = lane == 0 ? 0 : __shfl(c_b, lane > 0 ? lane - 1 : 0, kWave);
-    {
-        const bool has = lane < nb && c_b > c_prev_own;  // interior samples in my bin
-        const float zl_last = z_at(has ? c_b - 1 : 0, lane < nb ? lane : 0);
-        const float z_low = has ? zl_last : lo_b;
-        if (lane < n_ends) emit(c_b + lane, idx_b, (hi_b + z_low) * 0.5f, hi_b - z_low);
-    }
+    // z_low at the end of bin b: its last interior sample, or lo_b if it has none
+    auto end_z_low = [&](int b) { return W.c[b] > c_before(b) ? z_at(W.c[b] - 1, b) : W.lo[b]; };
+    if (lane < n_ends) emit(c_b + lane, idx_b, (hi_b + end_z_low(lane)) * 0.5f, hi_b - end_z_low(lane));
     int s = cs_lim + n_ends;
     // trailing segment
     int bin0;
     float zl, hi_d;
     if (done) {
         bin0 = nb;
-        const int bl = nb - 1;
-        const int cl = __shfl(c_b, bl, kWave), cp = bl == 0 ? 0 : __shfl(c_b, bl > 0 ? bl - 1 : 0, kWave);
-        const float zz = z_at(cl > cp ? cl - 1 : 0, bl);
-        zl = cl > cp ? zz : __shfl(lo_b, bl, kWave);
-        hi_d = __shfl(hi_b, bl, kWave);
+        zl = end_z_low(nb - 1);
+        hi_d = W.hi[nb - 1];
     } else if (total_steps == 0) {
         bin0 = 0;
-        zl = __shfl(lo_b, 0, kWave);
-        hi_d = __shfl(hi_b, 0, kWave);
+        zl = W.lo[0];
+        hi_d = W.hi[0];
     } else {
         bin0 = b_last;
         zl = z_at(total_steps - 1, b_last);
-        hi_d = __shfl(hi_b, b_last, kWave);
+        hi_d = W.hi[b_last];
     }
     if (zl < hi_d && num_rays > H + bin0) {
-        const int v0 = bin0 < max_hits ? __shfl(idx_b, bin0 < kWave ? bin0 : 0, kWave) : rows.idx_at(bin0);
+        const int v0 = bin0 < max_hits ? W.idx[bin0] : rows.idx_at(bin0);
         if (lane == 0) emit(s, v0, (hi_d + zl) * 0.5f, hi_d - zl);
         // bins k > bin0 continue while idx_slot0(k) != -1 && lo < hi && num_rays > H + k
         const bool cont = own && lane > bin0 && rows.idx_slot0(lane) != -1 && lo_b < hi_b && num_rays > H + lane;
@@ -568,6 +655,8 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
     const int lane = threadIdx.x & (kWave - 1);
     const int i = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    __shared__ WaveBins bins_all[4];
+    WaveBins &W = bins_all[threadIdx.x / kWave];
     if (i >= r_hit || i >= r_hit_cap || P <= 0) return;
     if (max_steps > max_steps_cap && lane == 0 && i == 0) atomicOr(stats + 7, 2);
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
@@ -601,7 +690,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
             os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
             count += (v != -1);
         },
-        lane);
+        lane, W);
     const int s_written = s_end < cap ? s_end : cap;
     for (int s = s_written + lane; s < max_steps_cap; s += kWave) {
         oi[s] = -1;
@@ -681,7 +770,8 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     PSVO_REQUIRE(n_rays >= 0, "ray_intersect_sorted: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kWave)), dim3(kWave), 0, as_stream(stream), n_rays,
+    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves * kRaysPerWave)), dim3(kIsWaves * kWave), 0,
+                       as_stream(stream), n_rays,
                        rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
                        ray_nv, ray_dsum, stats);
     return check_launch("ray_intersect_sorted");
