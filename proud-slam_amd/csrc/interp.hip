@@ -18,7 +18,8 @@
 // sixteen 64-B rows — whole rows, never split across instructions.  The
 // backward runs one wave per ray: the ray's samples are contiguous, the
 // dL/dx reduction to d_o / d_d stays in registers (no atomics on rays), and
-// the embedding scatter uses global f32 atomics shaped as 64-B row segments.
+// the embedding scatter sums each leaf run first and then adds whole 64-B
+// rows with global f32 atomics (one request per row and run).
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -74,24 +75,27 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
     feat[s * 4 + q] = acc;
 }
 
-// Lane-group helpers: 16 sample slots × 4 lanes; shifting by one slot is a
-// 4-lane shuffle.
-__device__ __forceinline__ float slot_up(float v, int n, int lane) {
-    const int src = lane - 4 * n;
-    const float o = __shfl(v, src < 0 ? lane : src, 64);
-    return o;
-}
-__device__ __forceinline__ int slot_up_i(int v, int n, int lane) {
-    const int src = lane - 4 * n;
-    return __shfl(v, src < 0 ? lane : src, 64);
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave per ray; 16 samples per pass, 4 lanes per sample (dims 4q..4q+3).
-// Consecutive samples of a ray mostly share a leaf, hence the same 8 vertex
-// rows: the per-corner contributions w_k·g are summed over each run of equal
-// leaves inside the pass (segmented scan over the 16 slots) and only the run's
-// last slot issues the atomics — ~8x fewer atomics and no same-address
-// collisions inside one atomic instruction.
+struct BwdPass {  // per-wave LDS: one 16-sample pass
+    float w[16][8];    // trilinear weights per slot
+    float g[16][16];   // grad_feat rows
+    int vid[16][8];    // vertex rows of the slot's leaf
+    int leaf[16];
+};
+
+// One wave per ray; 16 samples per pass, 4 lanes per sample (dims 4q..4q+3)
+// for the gathers and dL/dx.  The embedding gradient is summed per leaf RUN
+// (consecutive samples of the ray in the same voxel share the 8 vertex rows):
+// lane j owns (corner j/16 + 4i, dim j%16), i = 0, 1, accumulates the run in
+// registers across passes and flushes it when the leaf changes with two
+// atomic instructions, each covering four whole 64-B rows — one memory-side
+// request per row, the shape global f32 atomics run at full rate with
+// (MI355X_MICROARCH.md, global float atomics).
 __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
                                                     const int *__restrict__ leaf, const float *__restrict__ t,
                                                     const float *__restrict__ rays_o,
@@ -102,12 +106,15 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
                                                     const float4 *__restrict__ grad_feat,
                                                     float *__restrict__ grad_emb, float *__restrict__ grad_o,
                                                     float *__restrict__ grad_d) {
+    __shared__ BwdPass pass_all[4];
+    BwdPass &B = pass_all[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const int beg = offsets[r], end = offsets[r + 1];
     const int q = lane & 3;
     const int sub = lane >> 2;
+    const int ek0 = lane >> 4, ed = lane & 15;  // run accumulator slots: corners ek0, ek0 + 4; dim ed
     float o[3], d[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -115,6 +122,8 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         d[a] = rays_d[r * 3 + a];
     }
     float go[3] = {0.f, 0.f, 0.f}, gd[3] = {0.f, 0.f, 0.f};
+    int cur_leaf = -1, cur_v0 = 0, cur_v1 = 0;
+    float acc0 = 0.f, acc1 = 0.f;
     for (int base = beg; base < end; base += 16) {
         const int s = base + sub;
         const bool active = s < end;
@@ -123,7 +132,7 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         int vid[8];
         float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
         float ts = 0.f;
-        int lf = -1 - sub;  // distinct per inactive slot: never joins a run
+        int lf = -1;
         if (active) {
             lf = leaf[s];
             ts = t[s];
@@ -142,44 +151,29 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
             for (int k = 0; k < 8; ++k) vid[k] = 0;
         }
         corner_weights(p[0], p[1], p[2], w);
-        // run structure over the 16 slots: seg_start = first slot of my run
-        const int prev_lf = slot_up_i(lf, 1, lane);
-        const bool head = (sub == 0) || (prev_lf != lf);
-        int seg_start = head ? sub : 0;
+        // stage this pass for the run sums
+        wave_lds_sync();  // the previous pass's readers are done
+        *reinterpret_cast<float4 *>(&B.g[sub][4 * q]) = g;
+        if (q == 0) {
 #pragma unroll
-        for (int n = 1; n < 16; n <<= 1) seg_start = max(seg_start, slot_up_i(seg_start, n, lane));
-        const int next_start = __shfl(seg_start, lane + 4 < 64 ? lane + 4 : lane, 64);
-        const bool tail = active && ((sub == 15) || (next_start != seg_start) || (base + sub + 1 >= end));
+            for (int k = 0; k < 8; ++k) {
+                B.w[sub][k] = w[k];
+                B.vid[sub][k] = vid[k];
+            }
+            B.leaf[sub] = lf;
+        }
+        // dL/dx for this lane's sample: eg_k = E[vid_k] · g
         float eg[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            float acc = 0.f;
+            float a = 0.f;
             if (active) {
                 const float4 e = emb[(int64_t)vid[k] * 4 + q];
-                acc = e.x * g.x + e.y * g.y + e.z * g.z + e.w * g.w;
+                a = e.x * g.x + e.y * g.y + e.z * g.z + e.w * g.w;
             }
-            float cx = w[k] * g.x, cy = w[k] * g.y, cz = w[k] * g.z, cw = w[k] * g.w;
-#pragma unroll
-            for (int n = 1; n < 16; n <<= 1) {
-                const float ux = slot_up(cx, n, lane), uy = slot_up(cy, n, lane);
-                const float uz = slot_up(cz, n, lane), uw = slot_up(cw, n, lane);
-                if (sub - n >= seg_start) {
-                    cx += ux;
-                    cy += uy;
-                    cz += uz;
-                    cw += uw;
-                }
-            }
-            if (tail) {
-                float *dst = grad_emb + (int64_t)vid[k] * 16 + q * 4;
-                atomicAdd(dst + 0, cx);
-                atomicAdd(dst + 1, cy);
-                atomicAdd(dst + 2, cz);
-                atomicAdd(dst + 3, cw);
-            }
-            acc += __shfl_xor(acc, 1, 64);
-            acc += __shfl_xor(acc, 2, 64);
-            eg[k] = acc;
+            a += __shfl_xor(a, 1, 64);
+            a += __shfl_xor(a, 2, 64);
+            eg[k] = a;
         }
         if (active && q == 0) {
             const float ax[2] = {1.0f - p[0], p[0]};
@@ -201,6 +195,30 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
                 gd[a] += gx * ts;
             }
         }
+        wave_lds_sync();
+        // run sums over the pass's valid slots (wave-uniform loop)
+        const int n_slots = min(16, end - base);
+        for (int sl = 0; sl < n_slots; ++sl) {
+            const int lf_s = B.leaf[sl];
+            if (lf_s != cur_leaf) {
+                if (cur_leaf >= 0) {
+                    atomicAdd(grad_emb + (int64_t)cur_v0 * 16 + ed, acc0);
+                    atomicAdd(grad_emb + (int64_t)cur_v1 * 16 + ed, acc1);
+                }
+                cur_leaf = lf_s;
+                cur_v0 = B.vid[sl][ek0];
+                cur_v1 = B.vid[sl][ek0 + 4];
+                acc0 = 0.f;
+                acc1 = 0.f;
+            }
+            const float gv = B.g[sl][ed];
+            acc0 += B.w[sl][ek0] * gv;
+            acc1 += B.w[sl][ek0 + 4] * gv;
+        }
+    }
+    if (cur_leaf >= 0) {
+        atomicAdd(grad_emb + (int64_t)cur_v0 * 16 + ed, acc0);
+        atomicAdd(grad_emb + (int64_t)cur_v1 * 16 + ed, acc1);
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a) {

@@ -400,6 +400,11 @@ struct RawRows {
     __device__ float lo_at(int e) const { return min_depth[H + e]; }
     __device__ float hi_at(int e) const { return max_depth[H + e]; }
     __device__ float prob_at(int e) const { return probs[H + e]; }
+    // bins of the ray's own row (e < max_hits)
+    __device__ int own_idx(int e) const { return idx_at(e); }
+    __device__ float own_lo(int e) const { return lo_at(e); }
+    __device__ float own_hi(int e) const { return hi_at(e); }
+    __device__ float own_prob(int e) const { return prob_at(e); }
 };
 
 struct FusedRows {
@@ -425,6 +430,17 @@ struct FusedRows {
         const int64_t a = at(e);
         const float dd = hit_idx[a] != -1 ? hit_t1[a] - hit_t0[a] : 0.0f;
         return __fdiv_rn(dd, dsum[rank_ray[real(own_row)]]);
+    }
+    // bins of the ray's own row (e < P): logical row own_row = i < r_hit, no division
+    int64_t own_base;  // rank_ray[own_row] * kMaxHits
+    float own_dsum;
+    __device__ int own_idx(int e) const { return hit_idx[own_base + e]; }
+    __device__ float own_lo(int e) const { return hit_t0[own_base + e]; }
+    __device__ float own_hi(int e) const { return hit_t1[own_base + e]; }
+    __device__ float own_prob(int e) const {
+        const int64_t a = own_base + e;
+        const float dd = hit_idx[a] != -1 ? hit_t1[a] - hit_t0[a] : 0.0f;
+        return __fdiv_rn(dd, own_dsum);
     }
 };
 
@@ -543,10 +559,10 @@ template <typename Rows, typename Noise, typename Emit>
 __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int num_rays, int H, Noise noise, Emit emit,
                            int lane, WaveBins &W) {
     const bool own = lane < max_hits;
-    const int idx_b = own ? rows.idx_at(lane) : -1;
-    const float lo_b = own ? rows.lo_at(lane) : 0.0f;
-    const float hi_b = own ? rows.hi_at(lane) : 0.0f;
-    const float prob_b = own ? rows.prob_at(lane) : 0.0f;
+    const int idx_b = own ? rows.own_idx(lane) : -1;
+    const float lo_b = own ? rows.own_lo(lane) : 0.0f;
+    const float hi_b = own ? rows.own_hi(lane) : 0.0f;
+    const float prob_b = own ? rows.own_prob(lane) : 0.0f;
     // valid bins [0, nb): the serial loop stops at the first bin >= 1 with idx -1
     const uint64_t inval = __ballot(own && lane >= 1 && idx_b == -1);
     const int nb = inval ? min(__ffsll((unsigned long long)inval) - 1, max_hits) : max_hits;
@@ -597,12 +613,21 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
         const float u = __fdiv_rn(cdf_at(c) - lc, hc - lc);
         return lo + u * (hi - lo);
     };
-    // interior samples
-    for (int cs = lane; cs < cs_lim; cs += kWave) {
-        const int b = bin_of(cs);
-        const float z = z_at(cs, b);
-        const float z_low = cs == c_before(b) ? W.lo[b] : z_at(cs - 1, b);
-        emit(cs + b, W.idx[b], (z + z_low) * 0.5f, z - z_low);
+    // interior samples; z(cs - 1) comes from the neighbouring lane (the loop
+    // bound is wave-uniform, so every lane takes part in the shuffles)
+    float carry = 0.0f;
+    for (int base = 0; base < cs_lim; base += kWave) {
+        const int cs = base + lane;
+        const bool act = cs < cs_lim;
+        const int b = act ? bin_of(cs) : 0;
+        const float z = act ? z_at(cs, b) : 0.0f;
+        float zp = __shfl(z, lane > 0 ? lane - 1 : 0, kWave);
+        if (lane == 0) zp = carry;
+        carry = __shfl(z, kWave - 1, kWave);
+        if (act) {
+            const float z_low = cs == c_before(b) ? W.lo[b] : zp;
+            emit(cs + b, W.idx[b], (z + z_low) * 0.5f, z - z_low);
+        }
     }
     // ends of the bins the main loop passed
     const int b_last = total_steps > 0 && !done ? bin_of(total_steps - 1) : 0;
@@ -665,8 +690,10 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
     const int c = j / kSamplerChunk;
     const int jj = j - c * kSamplerChunk;
     const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
-    FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj};
-    const float dsum = ray_dsum[rank_ray[i]];
+    const int orig = rank_ray[i];
+    const float dsum = ray_dsum[orig];
+    FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj,
+                   (int64_t)orig * kMaxHits, dsum};
     const float steps_j = __fdiv_rn(dsum, step_size);
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
     int *oi = s_idx + (int64_t)i * max_steps_cap;
