@@ -95,13 +95,14 @@ int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank
  * [200, K', P] layout (K' = ceil(R_hit/200), 800-slot launch chunks): P,
  * R_hit and max_steps are read from `stats` on the device.  noise is either
  * NULL (counter-based uniform from `seed`, clamped to [0.001, 0.999]) or
- * f32[200, K', max_steps].  Outputs [R_hit, max_steps_cap] with
- * max_steps_cap >= stats[P] + stats[MAX_CEIL]; per-ray valid counts to
- * ray_ns[R_hit]; S_max / M into stats. */
+ * f32[200, K', max_steps] with values in [0, 1).  Outputs [R_hit,
+ * max_steps_cap] with max_steps_cap >= stats[P] + stats[MAX_CEIL]; per-ray
+ * valid counts to ray_ns[R_hit], their exclusive scan to offsets[R_hit+1];
+ * S_max / M into stats. */
 int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                      const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                      const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                     int *ray_ns);
+                     int *ray_ns, int *offsets);
 
 /* Exclusive scan of per-ray sample counts → sample offsets. */
 int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets);

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     const int g = lane / kGrp, u = lane & (kGrp - 1);
     const int64_t r = ((int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave) * kRaysPerWave + g;
     const float half = voxel_size * 0.5f;
-    int nv = 0, visits = 0, ceil_steps = 0, cnt = 0;
+    int nv = 0, visits = 0, cnt = 0;
     bool overflow = false;
     if (r < n_rays) {
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
@@ -316,21 +316,61 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             for (int l = 0; l < nv; ++l) dsum = dsum + S.h_d[g][l];
             ray_nv[r] = nv;
             ray_dsum[r] = dsum;
-            if (nv > 0) ceil_steps = (int)ceilf(__fdiv_rn(dsum, step_size));
         }
     }
-    const bool lead = u == 0 && r < n_rays;
-    const int wmax_nv = wave_max(lead ? nv : 0);
-    const int whit = wave_sum(lead && nv > 0 ? 1 : 0);
-    const int wceil = wave_max(lead ? ceil_steps : 0);
+    // visits / overflow: one atomic per block (per-ray P, R_hit and max ceil
+    // are reduced by k_ray_stats: thousands of same-address atomics serialise
+    // at the memory side)
+    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow ? 1 : 0);
     if (lane == 0) {
-        atomicMax(stats + PSVO_STAT_P, wmax_nv);
-        atomicAdd(stats + PSVO_STAT_R_HIT, whit);
-        atomicMax(stats + PSVO_STAT_MAX_CEIL, wceil);
-        atomicAdd(stats + PSVO_STAT_VISITS, wvis);
-        if (wov) atomicOr(stats + 7, 1);
+        blk_vis[threadIdx.x / kWave] = wvis;
+        blk_ov[threadIdx.x / kWave] = wov;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int v = 0, ov = 0;
+        for (int w = 0; w < kIsWaves; ++w) {
+            v += blk_vis[w];
+            ov |= blk_ov[w];
+        }
+        atomicAdd(stats + PSVO_STAT_VISITS, v);
+        if (ov) atomicOr(stats + 7, 1);
+    }
+}
+
+// P (max valid hits), R_hit and max ceil(Σ/step) over the rays — one block.
+__global__ __launch_bounds__(1024) void k_ray_stats(int64_t n, const int *__restrict__ ray_nv,
+                                                    const float *__restrict__ ray_dsum, float step_size,
+                                                    int *__restrict__ stats) {
+    int p = 0, hits = 0, mc = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int nv = ray_nv[i];
+        p = max(p, nv);
+        hits += nv > 0;
+        if (nv > 0) mc = max(mc, (int)ceilf(__fdiv_rn(ray_dsum[i], step_size)));
+    }
+    p = wave_max(p);
+    hits = wave_sum(hits);
+    mc = wave_max(mc);
+    __shared__ int sp[16], sh[16], sm[16];
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        sp[w] = p;
+        sh[w] = hits;
+        sm[w] = mc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x / kWave); ++k) {
+            p = max(p, sp[k]);
+            hits += sh[k];
+            mc = max(mc, sm[k]);
+        }
+        stats[PSVO_STAT_P] = p;
+        stats[PSVO_STAT_R_HIT] = hits;
+        stats[PSVO_STAT_MAX_CEIL] = mc;
     }
 }
 
@@ -725,10 +765,26 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
         os[s] = 0.0f;
     }
     count = wave_sum(count);
-    if (lane == 0) {
-        ray_ns[i] = count;
-        atomicMax(stats + PSVO_STAT_S_MAX, count);
-        atomicAdd(stats + PSVO_STAT_M, count);
+    if (lane == 0) ray_ns[i] = count;
+}
+
+// offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.
+__global__ __launch_bounds__(1024) void k_scan_samples(int64_t r_hit_cap, const int *__restrict__ ray_ns,
+                                                       int *__restrict__ offsets, int *__restrict__ stats) {
+    __shared__ int total;
+    __shared__ int smax[16];
+    const int64_t n = min((int64_t)stats[PSVO_STAT_R_HIT], r_hit_cap);
+    block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total);
+    int mx = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mx = max(mx, ray_ns[i]);
+    mx = wave_max(mx);
+    if ((threadIdx.x & (kWave - 1)) == 0) smax[threadIdx.x / kWave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x / kWave); ++k) mx = max(mx, smax[k]);
+        offsets[n] = total;
+        stats[PSVO_STAT_S_MAX] = mx;
+        stats[PSVO_STAT_M] = total;
     }
 }
 
@@ -797,10 +853,12 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     PSVO_REQUIRE(n_rays >= 0, "ray_intersect_sorted: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
+    hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves * kRaysPerWave)), dim3(kIsWaves * kWave), 0,
-                       as_stream(stream), n_rays,
+                       st, n_rays,
                        rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
                        ray_nv, ray_dsum, stats);
+    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
 
@@ -814,12 +872,15 @@ extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, in
 extern "C" int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray,
                                 const int *hit_idx, const float *hit_t0, const float *hit_t1, const float *ray_dsum,
                                 float step_size, const float *noise, uint64_t seed, int *stats, int *s_idx,
-                                float *s_depth, float *s_dist, int *ray_ns) {
+                                float *s_depth, float *s_dist, int *ray_ns, int *offsets) {
     PSVO_REQUIRE(r_hit_cap >= 0 && max_steps_cap > 0, "sample_rays: bad caps");
+    PSVO_REQUIRE(offsets != nullptr && ray_ns != nullptr, "sample_rays: ray_ns / offsets required");
     if (r_hit_cap == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, as_stream(stream), r_hit_cap,
-                       max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
-                       s_idx, s_depth, s_dist, ray_ns);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, r_hit_cap, max_steps_cap,
+                       rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
+                       s_dist, ray_ns);
+    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, r_hit_cap, ray_ns, offsets, stats);
     return check_launch("sample_rays");
 }
 

@@ -7,8 +7,8 @@ render_rays (render_helpers.py:351-556) runs as:
   ray_intersect_sorted  DFS + stable t_in sort + max_distance trim   (1 kernel)
   hit_rank              compaction order of hit rays                  (1 kernel)
   ── read back P, R_hit, max ceil(steps)  (sync 1; sizes the outputs) ──
-  sample_rays           inverse-CDF sampling, reference [200,K',P] layout
-  scan_counts           per-ray sample offsets
+  sample_rays           inverse-CDF sampling, reference [200,K',P] layout,
+                        + per-ray sample offsets, S_max, M
   ── read back S_max, M  (sync 2; output shapes [R_hit, S_max]) ──
   sample_points         z_vals / mask and ray-major compact samples
   interp  (autograd)    x = o + d t, trilinear embedding gather   HIP fwd/bwd
@@ -185,8 +185,7 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     L.call("psvo_sample_rays", stream, r_hit, max_steps, L.ptr(rank_ray), L.ptr(q["hit_idx"]), L.ptr(q["hit_t0"]),
            L.ptr(q["hit_t1"]), L.ptr(q["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(q["stats"]),
-           L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns))
-    L.call("psvo_scan_counts", stream, r_hit, L.ptr(ray_ns), L.ptr(offsets))
+           L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns), L.ptr(offsets))
     st = q["stats"].cpu()  # sync 2
     s_max, m = int(st[3]), int(st[4])
     if int(st[7]) & 2:
