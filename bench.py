@@ -180,8 +180,9 @@ def main():
                                                 "fs_weight": 10.0, "sdf_truncation": 0.1},
                                       data_specs={"max_depth": 10.0})
     criterion = Criterion(crit_args)
-    embed_optim = torch.optim.Adam([emb], lr=5e-3, fused=True)  # one multi-tensor launch per step
-    model_optim = torch.optim.Adam(dec.parameters(), lr=5e-3, fused=True)
+    from psvo.optim import Adam  # torch.optim.Adam semantics, one HIP launch per step per optimiser
+    embed_optim = Adam([emb], lr=5e-3)
+    model_optim = Adam(dec.parameters(), lr=5e-3)
     params = [emb] + list(dec.parameters())
     timer = KernelTimer()
     RH.KERNEL_TIMER = timer

@@ -27,6 +27,8 @@
  *                                 (nrgbd.py:80-146), fused fp32 MFMA
  *   psvo_criterion_*              criterion.Criterion.forward + autograd backward
  *                                 (criterion.py:17-116)
+ *   psvo_adam_step                torch.optim.Adam.step of the mapping loop
+ *                                 (render_helpers.py:581-596, :668-672)
  *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
  *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
  */
@@ -113,19 +115,21 @@ int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int max_steps_cap
                        const float *s_depth, const int *ray_ns, const int *offsets, int *leaf, float *t,
                        int *ray_of_sample, float *z_vals, uint8_t *mask);
 
-/* Trilinear interpolation of vertex embeddings at x = o[ray] + d[ray]*t.
+/* Trilinear interpolation of vertex embeddings at x = o[row] + d[row]*t with
+ * row = ray_index[ray_of_sample] (ray_index NULL: row = ray_of_sample).
  * centres f32[N,3]; vertex_idx i32[N,8]; emb f32[E,D] with D == 16. */
 int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size, const int *leaf, const float *t,
-                    const int *ray_of_sample, const float *rays_o, const float *rays_d, const float *centres,
-                    const int *vertex_idx, const float *emb, float *feat);
+                    const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
+                    const float *centres, const int *vertex_idx, const float *emb, float *feat);
 
 /* Backward of psvo_interp_fwd given grad_feat[M,D]: accumulates into
- * grad_emb[E,D] (float atomics, caller zeroes) and per-ray grad_o/grad_d
- * [R_hit,3] (caller zeroes).  Samples must be ray-major (offsets[R_hit+1]). */
-int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets, const int *leaf,
-                    const float *t, const float *rays_o, const float *rays_d, const float *centres,
-                    const int *vertex_idx, const float *emb, const float *grad_feat, float *grad_emb,
-                    float *grad_o, float *grad_d);
+ * grad_emb[E,D] (float atomics, caller zeroes) and writes grad_o / grad_d at
+ * the rows ray_index[r] (or r) of the R_hit hit rays (other rows untouched).
+ * Samples must be ray-major (offsets[R_hit+1]). */
+int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets, const int *ray_index,
+                    const int *leaf, const float *t, const float *rays_o, const float *rays_d, const float *centres,
+                    const int *vertex_idx, const float *emb, const float *grad_feat, float *grad_emb, float *grad_o,
+                    float *grad_d);
 
 /* SDF-to-weight compositing (render_helpers.py:504-556) per hit ray.
  * sdf_s[M], rgb_s[M,3] per valid sample; outputs sdf/weights [R_hit,S_max]
@@ -201,6 +205,14 @@ int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
                        const float *gt_rgb, const float *gt_depth, const float *color, const float *depth,
                        const float *sdf, const float *z_vals, const float *out, const float *g_loss, float *g_color,
                        float *g_depth, float *g_sdf);
+
+/* ---- optimiser ------------------------------------------------------- */
+/* One Adam step (torch.optim.Adam, amsgrad off) over n_tensors f32 tensors:
+ * host arrays of device pointers and element counts; `step` is the step
+ * number after increment (bias corrections 1 - beta^step). */
+int psvo_adam_step(void *stream, int n_tensors, float *const *params, const float *const *grads,
+                   float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, int64_t step);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

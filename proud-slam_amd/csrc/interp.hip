@@ -40,6 +40,7 @@ __device__ __forceinline__ void corner_weights(float px, float py, float pz, flo
 __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size, const int *__restrict__ leaf,
                                                     const float *__restrict__ t,
                                                     const int *__restrict__ ray_of_sample,
+                                                    const int *__restrict__ ray_index,
                                                     const float *__restrict__ rays_o,
                                                     const float *__restrict__ rays_d,
                                                     const float *__restrict__ centres,
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
     const int q = (int)(g & 3);
     if (s >= m) return;
     const int lf = leaf[s];
-    const int r = ray_of_sample[s];
+    const int r = ray_index ? ray_index[ray_of_sample[s]] : ray_of_sample[s];
     const float ts = t[s];
     float p[3];
 #pragma unroll
@@ -97,6 +98,7 @@ struct BwdPass {  // per-wave LDS: one 16-sample pass
 // request per row, the shape global f32 atomics run at full rate with
 // (MI355X_MICROARCH.md, global float atomics).
 __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
+                                                    const int *__restrict__ ray_index,
                                                     const int *__restrict__ leaf, const float *__restrict__ t,
                                                     const float *__restrict__ rays_o,
                                                     const float *__restrict__ rays_d,
@@ -112,14 +114,15 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const int beg = offsets[r], end = offsets[r + 1];
+    const int64_t ro_row = ray_index ? ray_index[r] : r;  // row of rays_o / rays_d / grad_o / grad_d
     const int q = lane & 3;
     const int sub = lane >> 2;
     const int ek0 = lane >> 4, ed = lane & 15;  // run accumulator slots: corners ek0, ek0 + 4; dim ed
     float o[3], d[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        o[a] = rays_o[r * 3 + a];
-        d[a] = rays_d[r * 3 + a];
+        o[a] = rays_o[ro_row * 3 + a];
+        d[a] = rays_d[ro_row * 3 + a];
     }
     float go[3] = {0.f, 0.f, 0.f}, gd[3] = {0.f, 0.f, 0.f};
     int cur_leaf = -1, cur_v0 = 0, cur_v1 = 0;
@@ -234,8 +237,8 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
     if (lane == 0) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            grad_o[r * 3 + a] = go[a];
-            grad_d[r * 3 + a] = gd[a];
+            grad_o[ro_row * 3 + a] = go[a];
+            grad_d[ro_row * 3 + a] = gd[a];
         }
     }
 }
@@ -246,26 +249,28 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
 using namespace psvo;
 
 extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size, const int *leaf, const float *t,
-                               const int *ray_of_sample, const float *rays_o, const float *rays_d,
+                               const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
                                const float *centres, const int *vertex_idx, const float *emb, float *feat) {
     PSVO_REQUIRE(d == 16, "interp_fwd: embedding dim %d unsupported (16 only)", d);
     PSVO_REQUIRE(m >= 0 && voxel_size > 0.f, "interp_fwd: bad sizes");
     if (m == 0) return PSVO_OK;
     hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
-                       t, ray_of_sample, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
+                       t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
+                       reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<float4 *>(feat));
     return check_launch("interp_fwd");
 }
 
 extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets,
-                               const int *leaf, const float *t, const float *rays_o, const float *rays_d,
+                               const int *ray_index, const int *leaf, const float *t, const float *rays_o, const float *rays_d,
                                const float *centres, const int *vertex_idx, const float *emb,
                                const float *grad_feat, float *grad_emb, float *grad_o, float *grad_d) {
     PSVO_REQUIRE(d == 16, "interp_bwd: embedding dim %d unsupported (16 only)", d);
     PSVO_REQUIRE(r_hit >= 0 && voxel_size > 0.f, "interp_bwd: bad sizes");
     if (r_hit == 0) return PSVO_OK;
     hipLaunchKernelGGL(k_interp_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, voxel_size,
-                       offsets, leaf, t, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
+                       offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
+                       reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<const float4 *>(grad_feat), grad_emb, grad_o, grad_d);
     return check_launch("interp_bwd");
 }

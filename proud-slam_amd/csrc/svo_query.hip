@@ -187,7 +187,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // sort is a rank sort (rank = #{t_j < t_i} + #{t_j == t_i, j < i}).
 constexpr int kGrp = 8;                 // lanes per ray
 constexpr int kRaysPerWave = kWave / kGrp;
-constexpr int kIsWaves = 4;             // waves per block
+constexpr int kIsWaves = 1;             // waves per block (512 blocks for 4096 rays: every CU busy)
 
 struct IsLds {
     float t0[kLevels][kWave];

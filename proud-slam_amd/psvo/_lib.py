@@ -30,8 +30,8 @@ _SIGNATURES = {
                                 _vp, _vp]),
     "psvo_scan_counts": (_i32, [_vp, _i64, _vp, _vp]),
     "psvo_sample_points": (_i32, [_vp, _i64, _i32, _i32] + [_vp] * 9),
-    "psvo_interp_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 8),
-    "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 11),
+    "psvo_interp_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 9),
+    "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
     "psvo_composite_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 10),
     "psvo_composite_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
     "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 15),
@@ -41,6 +41,7 @@ _SIGNATURES = {
     "psvo_criterion_sums": (_i32, [_vp, _i64, _i32, _i32, _f32, _f32] + [_vp] * 9),
     "psvo_criterion_finalize": (_i32, [_vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "psvo_criterion_bwd": (_i32, [_vp, _i64, _i32, _f32, _f32] + [_vp] * 12),
+    "psvo_adam_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _f64, _i64]),
     "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
     "psvo_octree_free": (None, [_vp]),
     "psvo_octree_insert": (_i32, [_vp, _vp, _i64]),

@@ -73,37 +73,41 @@ def masked_scatter_ones(mask, x):
 # autograd Functions over the HIP kernels
 # --------------------------------------------------------------------------
 class InterpSamples(Function):
-    """feat[M,16] = trilinear(E, x = o[ray] + d[ray] t) — get_features_vox
-    (render_helpers.py:104-156) fused with sampled_xyz (:436-437).
-    Backward: d_emb (float atomics), d_o / d_d per ray (wave reductions)."""
+    """feat[M,16] = trilinear(E, x = o[row] + d[row] t) — get_features_vox
+    (render_helpers.py:104-156) fused with sampled_xyz (:436-437) and the
+    hit-ray gather of rays_o / rays_d (row = ray_index[ray_of_sample], or
+    ray_of_sample when ray_index is None).  Backward: d_emb (float atomics on
+    whole 64-B rows), d_o / d_d per ray (wave reductions) at the rays' rows."""
 
     @staticmethod
-    def forward(ctx, ro_hit, rd_hit, emb, leaf, t, ray_of_sample, offsets, centres, vertex_idx, voxel_size):
+    def forward(ctx, rays_o, rays_d, emb, leaf, t, ray_of_sample, offsets, centres, vertex_idx, voxel_size,
+                ray_index=None):
         M = leaf.numel()
         feat = torch.empty((M, D_EMB), dtype=torch.float32, device=leaf.device)
         with _timed("interp_fwd"):
-            L.call("psvo_interp_fwd", L.stream_of(leaf.device), M, D_EMB, float(voxel_size), L.ptr(leaf), L.ptr(t),
-                   L.ptr(ray_of_sample), L.ptr(ro_hit), L.ptr(rd_hit), L.ptr(centres), L.ptr(vertex_idx),
-                   L.ptr(emb), L.ptr(feat))
-        ctx.save_for_backward(ro_hit, rd_hit, emb, leaf, t, offsets, centres, vertex_idx)
+            L.call("psvo_interp_fwd", L.stream_of(leaf.device), M, D_EMB, float(voxel_size), leaf, t, ray_of_sample,
+                   ray_index, rays_o, rays_d, centres, vertex_idx, emb, feat)
+        ctx.save_for_backward(rays_o, rays_d, emb, leaf, t, offsets, centres, vertex_idx, ray_index)
         ctx.voxel_size = float(voxel_size)
         return feat
 
     @staticmethod
     def backward(ctx, grad_feat):
-        ro_hit, rd_hit, emb, leaf, t, offsets, centres, vertex_idx = ctx.saved_tensors
+        rays_o, rays_d, emb, leaf, t, offsets, centres, vertex_idx, ray_index = ctx.saved_tensors
         dev = leaf.device
-        r_hit = ro_hit.shape[0]
+        r_hit = offsets.numel() - 1
         grad_feat = grad_feat.contiguous().float()
         grad_emb = torch.zeros_like(emb)
-        grad_o = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
-        grad_d = torch.empty((r_hit, 3), dtype=torch.float32, device=dev)
+        need_od = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        # rows of rays that hit nothing get zero gradient
+        god = (torch.zeros if ray_index is not None else torch.empty)((2,) + tuple(rays_o.shape), dtype=torch.float32,
+                                                                      device=dev)
         with _timed("interp_bwd"):
-            L.call("psvo_interp_bwd", L.stream_of(dev), r_hit, D_EMB, ctx.voxel_size, L.ptr(offsets), L.ptr(leaf),
-                   L.ptr(t), L.ptr(ro_hit), L.ptr(rd_hit), L.ptr(centres), L.ptr(vertex_idx), L.ptr(emb),
-                   L.ptr(grad_feat), L.ptr(grad_emb), L.ptr(grad_o), L.ptr(grad_d))
-        return (grad_o if ctx.needs_input_grad[0] else None, grad_d if ctx.needs_input_grad[1] else None,
-                grad_emb if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None)
+            L.call("psvo_interp_bwd", L.stream_of(dev), r_hit, D_EMB, ctx.voxel_size, offsets, ray_index, leaf, t,
+                   rays_o, rays_d, centres, vertex_idx, emb, grad_feat, grad_emb, god[0], god[1])
+        return (god[0] if need_od and ctx.needs_input_grad[0] else None,
+                god[1] if need_od and ctx.needs_input_grad[1] else None,
+                grad_emb if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None)
 
 
 class CompositeRays(Function):
@@ -150,7 +154,7 @@ class CompositeRays(Function):
 class RaySamples:
     """Everything the differentiable part needs about one ray batch."""
 
-    __slots__ = ("ray_mask", "rank_ray", "r_hit", "P", "s_max", "m", "z_vals", "sample_mask", "leaf", "t",
+    __slots__ = ("ray_mask", "r_hit", "P", "s_max", "m", "z_vals", "sample_mask", "leaf", "t",
                  "ray_of_sample", "offsets", "ray_ns", "rank_ray32", "s_idx", "s_depth", "s_dist", "visits", "max_steps")
 
 
@@ -200,9 +204,8 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
     out = RaySamples()
     out.ray_mask = (ray_rank >= 0).view(1, R)
     out.rank_ray32 = rank_ray[:r_hit]
-    out.rank_ray = out.rank_ray32.long()
     out.r_hit, out.P, out.s_max, out.m, out.visits, out.max_steps = r_hit, P, s_max, m, visits, max_steps
-    out.z_vals, out.sample_mask = z_vals, mask.bool()
+    out.z_vals, out.sample_mask = z_vals, mask  # uint8 [R_hit, S_max]
     out.leaf, out.t, out.ray_of_sample, out.offsets, out.ray_ns = leaf, t, ray_of_sample, offsets, ray_ns
     out.s_idx, out.s_depth, out.s_dist = s_idx, s_depth, s_dist
     return out
@@ -219,16 +222,14 @@ def render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxe
     smp = query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise, seed)
     if profiler is not None:
         profiler.tok("ray_intersect")
-    ro = rays_o.reshape(-1, 3)
-    rd = rays_d.reshape(-1, 3)
-    ro_hit = ro.index_select(0, smp.rank_ray).float().contiguous()
-    rd_hit = rd.index_select(0, smp.rank_ray).float().contiguous()
+    ro = rays_o.reshape(-1, 3).float().contiguous()
+    rd = rays_d.reshape(-1, 3).float().contiguous()
     if smp.m == 0:
         return None, 0
     emb = map_states["voxel_vertex_emb"]
-    feats = InterpSamples.apply(ro_hit, rd_hit, emb, smp.leaf, smp.t, smp.ray_of_sample, smp.offsets,
+    feats = InterpSamples.apply(ro, rd, emb, smp.leaf, smp.t, smp.ray_of_sample, smp.offsets,
                                 map_states["voxel_center_xyz"].float().contiguous(),
-                                map_states["voxel_vertex_idx"].int().contiguous(), voxel_size)
+                                map_states["voxel_vertex_idx"].int().contiguous(), voxel_size, smp.rank_ray32)
     if profiler is not None:
         profiler.tick("render_core")
     field = sdf_network({"emb": feats, "dists": None})
