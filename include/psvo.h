@@ -150,12 +150,15 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
 /* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
  * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
  * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
+ * `images` (psvo_mlp_image_floats() floats) receives the weights' LDS operand
+ * images, rebuilt by every call; psvo_mlp_bwd reuses them (same weights).
  * Training mode: act f32[4][ceil(M/32)*32*128] (h1, h2, f, c1; tile-major) and masks u64[M][2][3]
  * (ReLU masks) are written for psvo_mlp_bwd; pass NULL for both otherwise. */
+int64_t psvo_mlp_image_floats(void);
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                 const float *b4, const float *w5, const float *b5, float *sdf, float *rgb, float *act,
-                 uint64_t *masks);
+                 const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
+                 float *act, uint64_t *masks);
 
 /* Floats of device workspace psvo_mlp_bwd needs for m samples. */
 int64_t psvo_mlp_workspace_floats(int64_t m, int n_split);
@@ -166,8 +169,8 @@ int64_t psvo_mlp_workspace_floats(int64_t m, int n_split);
  * deterministic slab reduction. */
 int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                 const float *b4, const float *w5, const float *b5, const float *rgb, const float *act,
-                 const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1,
+                 const float *b4, const float *w5, const float *b5, const float *images, const float *rgb,
+                 const float *act, const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1,
                  float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5,
                  int accumulate, int n_split, float *workspace);
 

@@ -187,33 +187,78 @@ __device__ __forceinline__ void store_tile(float *dst, int64_t tile, const f32x1
                 make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
 }
 
-// Forward image of W[rows][cols] (global row-major, first row `row0`):
-// columns < acc_cols come from accumulator blocks, the rest from x.
-template <int NT>
-__device__ __forceinline__ void stage_fwd(float *wl, const float *__restrict__ W, int rows, int cols, int row0,
-                                          int acc_cols) {
-    const int n = rows * cols;
-    const int xbase = (rows >> 5) * (acc_cols >> 5) * 16 * 64;
-    for (int e = threadIdx.x; e < n; e += NT) {
-        const int o = e / cols, k = e - o * cols;
-        const float v = W[(int64_t)(o + row0) * cols + k];
-        wl[k < acc_cols ? perm_acc(o, k, acc_cols >> 5) : xbase + perm_x(o, k - acc_cols)] = v;
-    }
+// ---------------------------------------------------------------------------
+// Weight images: every layer's LDS operand image, laid out exactly as the
+// kernels read it, built once per weight update by k_mlp_prep (a gather,
+// coalesced writes) so that staging is a straight 16-B copy.
+//   fwd: W1 (perm_x), W2, W3 rows 1..128 (perm_acc), W4 ([f | x])
+//   bwd: W4ᵀ (5 product blocks), W3ᵀ rows 1..128, W2ᵀ, W1ᵀ (1 block)
+constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF4 = kImgF3 + 16384,
+              kImgB4 = kImgF4 + 18432, kImgB3 = kImgB4 + 20480, kImgB2 = kImgB3 + 16384, kImgB1 = kImgB2 + 16384,
+              kImgTotal = kImgB1 + 4096;  // 110,592 floats
+
+__device__ __forceinline__ void inv_perm_acc(int pos, int nkb, int &i, int &k) {
+    const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
+    const int rg = rest & 3, blk = rest >> 2;
+    const int kb = blk % nkb, ib = blk / nkb;
+    const int h = lane >> 5;
+    i = ib * 32 + (lane & 31);
+    k = kb * 32 + c + 4 * h + 8 * rg;
+}
+__device__ __forceinline__ void inv_perm_x(int pos, int &i, int &k) {
+    const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
+    const int tg = rest & 1, ib = rest >> 1;
+    i = ib * 32 + (lane & 31);
+    k = 2 * (tg * 4 + c) + (lane >> 5);
 }
 
-// Backward (transposed) image of W[rows][cols]: product rows = columns of W
-// (padded to `out_blocks` x 32), reduction over W's rows (from δ blocks).
-template <int NT>
-__device__ __forceinline__ void stage_bwd(float *wl, const float *__restrict__ W, int rows, int cols, int row0,
-                                          int out_blocks) {
-    const int nimg = out_blocks * (rows >> 5) * 1024;
-    for (int e = threadIdx.x; e < nimg; e += NT) wl[e] = 0.0f;
-    __syncthreads();
-    const int n = rows * cols;
-    for (int e = threadIdx.x; e < n; e += NT) {
-        const int o = e / cols, k = e - o * cols;
-        wl[perm_acc(k, o, rows >> 5)] = W[(int64_t)(o + row0) * cols + k];
+__global__ __launch_bounds__(256) void k_mlp_prep(const float *__restrict__ w1, const float *__restrict__ w2,
+                                                  const float *__restrict__ w3, const float *__restrict__ w4,
+                                                  float *__restrict__ img) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kImgTotal) return;
+    int i, k;
+    float v = 0.0f;
+    if (e < kImgF2) {
+        inv_perm_x(e - kImgF1, i, k);
+        v = w1[i * 16 + k];
+    } else if (e < kImgF3) {
+        inv_perm_acc(e - kImgF2, 4, i, k);
+        v = w2[i * 128 + k];
+    } else if (e < kImgF4) {
+        inv_perm_acc(e - kImgF3, 4, i, k);
+        v = w3[(i + 1) * 128 + k];
+    } else if (e < kImgB4) {
+        const int pos = e - kImgF4;
+        if (pos < 16384) {
+            inv_perm_acc(pos, 4, i, k);
+            v = w4[i * 144 + k];
+        } else {
+            inv_perm_x(pos - 16384, i, k);
+            v = w4[i * 144 + 128 + k];
+        }
+    } else if (e < kImgB3) {  // W4ᵀ: product row i = column of W4 (< 144), reduction k = row of W4
+        inv_perm_acc(e - kImgB4, 4, i, k);
+        v = i < 144 ? w4[k * 144 + i] : 0.0f;
+    } else if (e < kImgB2) {
+        inv_perm_acc(e - kImgB3, 4, i, k);
+        v = w3[(k + 1) * 128 + i];
+    } else if (e < kImgB1) {
+        inv_perm_acc(e - kImgB2, 4, i, k);
+        v = w2[k * 128 + i];
+    } else {
+        inv_perm_acc(e - kImgB1, 4, i, k);
+        v = i < 16 ? w1[k * 16 + i] : 0.0f;
     }
+    img[e] = v;
+}
+
+// n floats (n % 4 == 0) of a prepared image → LDS, 16 B per lane
+template <int NT>
+__device__ __forceinline__ void copy_img(float *wl, const float *__restrict__ img, int n) {
+    const float4 *src = reinterpret_cast<const float4 *>(img);
+    float4 *dst = reinterpret_cast<float4 *>(wl);
+    for (int e = threadIdx.x; e < (n >> 2); e += NT) dst[e] = src[e];
 }
 
 struct MlpParams {
@@ -249,6 +294,7 @@ __device__ __forceinline__ void load_x(const float *__restrict__ feat, int64_t s
 // (masks [M][2][3] u64: lane-half h of sample s holds bits of its 64
 // features), so the backward never re-runs the forward.
 __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float *__restrict__ feat, MlpParams p,
+                                                         const float *__restrict__ img,
                                                          float *__restrict__ sdf_out, float *__restrict__ rgb_out,
                                                          float *__restrict__ act, uint64_t *__restrict__ masks) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -262,7 +308,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     float x[8];
     load_x(feat, s, valid, h, x);
     stage_vectors(lds, p);
-    stage_fwd<kThreads>(wl, p.w1, 128, 16, 0, 0);
+    copy_img<kThreads>(wl, img + kImgF1, 2048);
     __syncthreads();
     f32x16 a[kNB], bacc[kNB];
     init_bias(a, lds + kOffB1, h);
@@ -272,21 +318,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     const int64_t tstride = ((m + 31) / 32) * 32 * 128;  // floats per tile-major matrix
     if (save) store_tile(act, tile, a, lane, m);
     __syncthreads();
-    stage_fwd<kThreads>(wl, p.w2, 128, 128, 0, 128);
+    copy_img<kThreads>(wl, img + kImgF2, 16384);
     __syncthreads();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
     if (save) store_tile(act + tstride, tile, bacc, lane, m);
     __syncthreads();
-    stage_fwd<kThreads>(wl, p.w3, 128, 128, 1, 128);  // rows 1..128 → f
+    copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
     __syncthreads();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
     if (save) store_tile(act + 2 * tstride, tile, a, lane, m);
     __syncthreads();
-    stage_fwd<kThreads>(wl, p.w4, 128, 144, 0, 128);  // [f | x]
+    copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
     __syncthreads();
     init_bias(bacc, lds + kOffB4, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
@@ -325,6 +371,7 @@ constexpr int kThreadsBwd = 512;
 constexpr int kTileBwd = 256;
 
 __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpParams p,
+                                                                 const float *__restrict__ img,
                                                                  const float *__restrict__ rgb_in,
                                                                  const uint64_t *__restrict__ masks,
                                                                  const float *__restrict__ g_sdf,
@@ -359,7 +406,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     }
     stage_vectors(lds, p);
     // ---- δc1 = W5ᵀ δ5 ⊙ mask (VALU); overlap with the W4ᵀ staging
-    stage_bwd<kThreadsBwd>(wl, p.w4, 128, 144, 0, 5);
+    copy_img<kThreadsBwd>(wl, img + kImgB4, 20480);
     __syncthreads();
     f32x16 a[kNB], bacc[kNB];
 #pragma unroll
@@ -383,7 +430,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     store_tile(o.d3, tile, a, lane, m);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     __syncthreads();
-    stage_bwd<kThreadsBwd>(wl, p.w3, 128, 128, 1, 4);
+    copy_img<kThreadsBwd>(wl, img + kImgB3, 16384);
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
@@ -394,7 +441,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     store_tile(o.d2, tile, bacc, lane, m);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
     __syncthreads();
-    stage_bwd<kThreadsBwd>(wl, p.w2, 128, 128, 0, 4);
+    copy_img<kThreadsBwd>(wl, img + kImgB2, 16384);
     __syncthreads();
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
@@ -402,7 +449,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     store_tile(o.d1, tile, a, lane, m);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
     __syncthreads();
-    stage_bwd<kThreadsBwd>(wl, p.w1, 128, 16, 0, 1);
+    copy_img<kThreadsBwd>(wl, img + kImgB1, 4096);
     __syncthreads();
     f32x16 t1[1];
     zero(t1);
@@ -667,12 +714,15 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
 
 using namespace psvo;
 
+extern "C" int64_t psvo_mlp_image_floats(void) { return kImgTotal; }
+
 extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                            const float *b4, const float *w5, const float *b5, float *sdf, float *rgb, float *act,
-                            uint64_t *masks) {
+                            const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
+                            float *act, uint64_t *masks) {
     PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
+    PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats floats)");
     PSVO_REQUIRE((act == nullptr) == (masks == nullptr), "mlp_fwd: act and masks go together");
     if (m == 0) return PSVO_OK;
     static bool attr = false;
@@ -681,9 +731,11 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd);
         attr = true;
     }
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, w1, w2, w3, w4, images);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, as_stream(stream), m, feat, p,
-                       sdf, rgb, act, masks);
+    hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf, rgb,
+                       act, masks);
     return check_launch("mlp_fwd");
 }
 
@@ -723,12 +775,13 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
 // (psvo_mlp_workspace_floats).
 extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                            const float *b4, const float *w5, const float *b5, const float *rgb, const float *act,
-                            const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1,
+                            const float *b4, const float *w5, const float *b5, const float *images, const float *rgb,
+                            const float *act, const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1,
                             float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4,
                             float *gw5, float *gb5, int accumulate, int n_split, float *workspace) {
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
+    PSVO_REQUIRE(images != nullptr, "mlp_bwd: images of the training forward required");
     hipStream_t st = as_stream(stream);
     DwGrid g;
     int slab_floats;
@@ -751,8 +804,8 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd);
             attr = true;
         }
-        hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p, rgb,
-                           masks, g_sdf, g_rgb, o);
+        hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p, images,
+                           rgb, masks, g_sdf, g_rgb, o);
         int rc = check_launch("mlp_bwd_data");
         if (rc) return rc;
     }

@@ -34,9 +34,10 @@ _SIGNATURES = {
     "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
     "psvo_composite_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 10),
     "psvo_composite_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
-    "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 15),
+    "psvo_mlp_image_floats": (_i64, []),
+    "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 16),
     "psvo_mlp_workspace_floats": (_i64, [_i64, _i32]),
-    "psvo_mlp_bwd": (_i32, [_vp, _i64, _i32] + [_vp] * 27 + [_i32, _i32, _vp]),
+    "psvo_mlp_bwd": (_i32, [_vp, _i64, _i32] + [_vp] * 28 + [_i32, _i32, _vp]),
     "psvo_criterion_workspace_floats": (_i64, [_i64]),
     "psvo_criterion_sums": (_i32, [_vp, _i64, _i32, _i32, _f32, _f32] + [_vp] * 9),
     "psvo_criterion_finalize": (_i32, [_vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i32, _vp]),

@@ -38,15 +38,15 @@ class DecoderMLP(Function):
         mp = (m + 31) // 32 * 32  # tile-major activations: whole 32-sample tiles
         act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if training else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
-        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(sdf), L.ptr(rgb),
-               L.ptr(act), L.ptr(masks))
+        images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=dev)
+        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, feat, *ps, images, sdf, rgb, act, masks)
         if training:
-            ctx.save_for_backward(feat, rgb, act, masks, *ps)
+            ctx.save_for_backward(feat, rgb, act, masks, images, *ps)
         return sdf, rgb
 
     @staticmethod
     def backward(ctx, g_sdf, g_rgb):
-        feat, rgb, act, masks, *ps = ctx.saved_tensors
+        feat, rgb, act, masks, images, *ps = ctx.saved_tensors
         m = feat.shape[0]
         dev = feat.device
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
@@ -55,9 +55,8 @@ class DecoderMLP(Function):
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
-        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, L.ptr(feat), *[L.ptr(p) for p in ps], L.ptr(rgb), L.ptr(act),
-               L.ptr(masks), L.ptr(g_sdf), L.ptr(g_rgb), L.ptr(dfeat), *[L.ptr(g) for g in grads], 0, n_split,
-               L.ptr(ws))
+        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb, dfeat, *grads,
+               0, n_split, ws)
         return (dfeat, *grads)
 
 
