@@ -152,7 +152,8 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
  * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
  * `images` (psvo_mlp_image_floats() floats) receives the weights' LDS operand
  * images, rebuilt by every call; psvo_mlp_bwd reuses them (same weights).
- * Training mode: act f32[4][ceil(M/32)*32*128] (h1, h2, f, c1; tile-major) and masks u64[M][2][3]
+ * Training mode: act f32[4][ceil(M/64)*64*128] (h1, h2, f, c1; chunk-feature-major, see mlp.hip) and
+ * masks u64[M][2][3]
  * (ReLU masks) are written for psvo_mlp_bwd; pass NULL for both otherwise. */
 int64_t psvo_mlp_image_floats(void);
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,

@@ -172,19 +172,33 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
                 make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
 }
 
-// Store an activation in TILE-MAJOR form — the accumulator registers as
-// they stand: [tile = s/32][block b][rg][lane][4] — one fully contiguous
-// 1-KB write per wave-instruction.  Element (s, f) lives at
-// tm_index(s, f) below; the weight-gradient kernel re-layouts on staging.
-__device__ __forceinline__ void store_tile(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane, int64_t m) {
-    if (tile * 32 >= m) return;  // wave-uniform: tiles wholly past M are not allocated
-    float *base = dst + tile * (kNB * 4 * 64 * 4);
+// Activations and δ's the weight gradients consume are stored CHUNK-FEATURE
+// major ("CF"): per 64-sample chunk a [128 feature][64 slot] block in which
+// sample s sits at permuted position p = (s&1)·32 + s/2 (so that the two
+// samples of one f32 MFMA k-step pair, 2t and 2t+1, sit at t and 32 + t) and
+// 16-B groups are XOR-swizzled by feature (g ^ f%16), which makes the
+// weight-gradient kernel's 4-k-step ds_read_b128 operand reads bank-conflict
+// free while its LDS image stays a straight copy of the chunk (global_load_lds).
+// A wave stores its 32-sample tile register by register: each store is two
+// feature rows × two 64-B runs.
+constexpr int kCh = 64;              // samples per CF chunk
+constexpr int kCfChunk = 128 * kCh;  // floats per CF chunk
+
+__device__ __forceinline__ int cf_slot(int f, int s) {
+    const int p = (s & 1) * 32 + (s >> 1);
+    return f * kCh + ((((p >> 2) ^ (f & 15)) << 2) | (p & 3));
+}
+
+// tile = global 32-sample tile index (wave-uniform); n_tiles = allocated tiles
+__device__ __forceinline__ void store_cf(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane, int64_t n_tiles) {
+    if (tile >= n_tiles) return;
+    float *base = dst + (tile >> 1) * kCfChunk;
+    const int sc = (int)(tile & 1) * 32 + (lane & 31);
+    const int hh = lane >> 5;
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg)
-            *reinterpret_cast<float4 *>(base + ((b * 4 + rg) * 64 + lane) * 4) =
-                make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
+        for (int r = 0; r < 16; ++r) base[cf_slot(32 * b + phi(r, hh), sc)] = v[b][r];
 }
 
 // ---------------------------------------------------------------------------
@@ -315,22 +329,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_x(wl, x, a, lane);
     const uint64_t m1 = relu(a);  // h1
     const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
-    const int64_t tstride = ((m + 31) / 32) * 32 * 128;  // floats per tile-major matrix
-    if (save) store_tile(act, tile, a, lane, m);
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
+    const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
+    if (save) store_cf(act, tile, a, lane, n_tiles);
     __syncthreads();
     copy_img<kThreads>(wl, img + kImgF2, 16384);
     __syncthreads();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
-    if (save) store_tile(act + tstride, tile, bacc, lane, m);
+    if (save) store_cf(act + tstride, tile, bacc, lane, n_tiles);
     __syncthreads();
     copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
     __syncthreads();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    if (save) store_tile(act + 2 * tstride, tile, a, lane, m);
+    if (save) store_cf(act + 2 * tstride, tile, a, lane, n_tiles);
     __syncthreads();
     copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
     __syncthreads();
@@ -339,7 +354,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
     if (save) {
-        store_tile(act + 3 * tstride, tile, bacc, lane, m);
+        store_cf(act + 3 * tstride, tile, bacc, lane, n_tiles);
         if (valid) {
             uint64_t *mk = masks + (s * 2 + h) * 3;
             mk[0] = m1;
@@ -384,6 +399,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     const int64_t s = (int64_t)blockIdx.x * kTileBwd + wave * 32 + (lane & 31);
     const bool valid = s < m;
     const int64_t tile = (int64_t)blockIdx.x * (kTileBwd / 32) + wave;
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
     uint64_t m1 = 0, m2 = 0, m4 = 0;
     float d5[3] = {0.f, 0.f, 0.f};
     float dsdf = 0.0f;
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
             const float v = lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
             bacc[b][r] = ((m4 >> (16 * b + r)) & 1) ? v : 0.0f;
         }
-    store_tile(o.d4, tile, bacc, lane, m);
+    store_cf(o.d4, tile, bacc, lane, n_tiles);
     // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
     f32x16 t5[5];
     zero(t5);
@@ -427,7 +443,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-    store_tile(o.d3, tile, a, lane, m);
+    store_cf(o.d3, tile, a, lane, n_tiles);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     __syncthreads();
     copy_img<kThreadsBwd>(wl, img + kImgB3, 16384);
@@ -438,7 +454,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
         for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     apply_mask(bacc, m2);
-    store_tile(o.d2, tile, bacc, lane, m);
+    store_cf(o.d2, tile, bacc, lane, n_tiles);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
     __syncthreads();
     copy_img<kThreadsBwd>(wl, img + kImgB2, 16384);
@@ -446,7 +462,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
     apply_mask(a, m1);
-    store_tile(o.d1, tile, a, lane, m);
+    store_cf(o.d1, tile, a, lane, n_tiles);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
     __syncthreads();
     copy_img<kThreadsBwd>(wl, img + kImgB1, 4096);
@@ -466,190 +482,229 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
 
 // ---------------------------------------------------------------------------
 // backward (weights): dW[rows][cols] = Σ_s D[s][row] · A[s][col], db = Σ_s D[s].
-// One workgroup = one (layer, sample-range); 64-sample chunks of D and A are
-// staged into LDS with 16-B loads (two workgroups per CU overlap one's loads
-// with the other's MFMAs); each wave accumulates its 32x32 blocks of C across
-// the whole range in registers and writes them once to a private slab, which
-// k_mlp_dw_reduce sums in a fixed order (bitwise reproducible).
-//
-// Layers (C rows x cols; D and A sources):
-//   0: W1 128x16   D1 | feat          3: W4 128x144  D4 | [f, feat]
-//   1: W2 128x128  D2 | h1            4: W5 3x128    D5 | c1
-//   2: W3 129x128  [g_sdf, D3] | h2   (C row 0 = sdf row: LDS block 4)
+// Split-K over 64-sample CF chunks: a workgroup owns (layer, chunk range),
+// copies each chunk's D and A blocks into LDS with global_load_lds (no
+// registers, no re-layout), and its 4 waves accumulate their 32x32 blocks
+// of C across the range in registers (f32 MFMA, 4 k-steps per ds_read_b128
+// operand read); per-layer private slabs are summed by k_mlp_dw_reduce in a
+// fixed order (bitwise reproducible).  Thin pieces run on the VALU from the
+// same LDS images: bias sums, W3's sdf row (g_sdf ⊗ h2) and W5 (δ5 ⊗ c1).
+//   L0: W1 128x16   D = δh1 | A = x (16 rows from feat, 16 zero rows)
+//   L1: W2 128x128  D = δh2 | A = h1        2x2 blocks per wave
+//   L2: W3 rows 1..128 D = δf | A = h2      2x2 blocks per wave (+ sdf row, db3)
+//   L3: W4 128x144  D = δc1 | A = [f | x]   2x2 blocks + one x block per wave
+//   L4: W5 3x128    VALU: δ5 [M][3] ⊗ c1
 struct DwSrc {
-    const float *D[5];
-    const float *A[5];
-    const float *feat, *g_sdf;
+    const float *D[4];  // CF: δh1, δh2, δf, δc1
+    const float *A[4];  // CF: (unused), h1, h2, f
+    const float *c1;    // CF
+    const float *d5;    // [M][3]
+    const float *feat;  // [M][16]
+    const float *g_sdf; // [M]
 };
 
-constexpr int kDwS = 64;         // samples per staged chunk
-constexpr int kDwLd = 160;       // LDS row pitch (5 blocks of 32)
+constexpr int kDwA = 160;  // A image rows (W4: 128 f + 16 x + 16 zero)
 
-// Each wave owns NBW blocks of C that share one operand block: either a
-// fixed column block (cb = wave, rb = 0..NBW-1) or a fixed row block
-// (rb = wave, cb = 0..NBW-1).  Per 2-sample k-step: 1 shared + NBW other
-// operand reads, then NBW independent MFMAs.
-template <int NBW, bool FIX_CB>
-__device__ __forceinline__ void dw_mfma(const float *Dl, const float *Al, f32x16 (&acc)[5], int wave, int h, int i) {
-    const float *sp = (FIX_CB ? Al : Dl) + h * kDwLd + 32 * wave + i;
-    const float *op = (FIX_CB ? Dl : Al) + h * kDwLd + i;
+__device__ __forceinline__ void glds16(const float *g, float *l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+}
+
+// one CF chunk (128 x 64 floats, 32 KB) → LDS, lane-linear 16-B copies
+__device__ __forceinline__ void copy_cf(float *dst, const float *__restrict__ src) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int t = 0; t < kDwS / 2; ++t) {
-        const float sh = sp[2 * t * kDwLd];
-        float ot[NBW];
-#pragma unroll
-        for (int j = 0; j < NBW; ++j) ot[j] = op[2 * t * kDwLd + 32 * j];
-#pragma unroll
-        for (int j = 0; j < NBW; ++j) acc[j] = FIX_CB ? mfma(ot[j], sh, acc[j]) : mfma(sh, ot[j], acc[j]);
+    for (int u = 0; u < kCfChunk / (256 * 4); ++u) {
+        const int blk = u * 4 + wave;  // 1-KB piece of this wave-instruction
+        glds16(src + (blk * 64 + lane) * 4, dst + blk * 256);
     }
 }
 
-// tile-major [M/32][4][4][64][4] chunk (two tiles = 64 samples) → LDS rows
-// [s][col0 + f]; rows past M are zero.
-__device__ __forceinline__ void stage_tm(float *dst, int col0, const float *__restrict__ src, int64_t s0, int64_t m) {
-    const int64_t t0 = s0 >> 5;
-    for (int e = threadIdx.x; e < 2 * 4 * 4 * 64; e += 256) {
-        const int lane = e & 63, rg = (e >> 6) & 3, b = (e >> 8) & 3, tl = e >> 10;
-        const int sl = (tl << 5) + (lane & 31);
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (s0 + sl < m) v = *reinterpret_cast<const float4 *>(src + (t0 + tl) * (4 * 4 * 64 * 4) + (int64_t)e * 4 -
-                                                                (int64_t)tl * (4 * 4 * 64 * 4));
-        *reinterpret_cast<float4 *>(dst + sl * kDwLd + col0 + 32 * b + 8 * rg + 4 * (lane >> 5)) = v;
+// x rows of a chunk (feat [M][16]) into an A image at rows row0..row0+15
+__device__ __forceinline__ void stage_x(float *Al, int row0, const float *__restrict__ feat, int64_t s0, int64_t m) {
+    const int t = threadIdx.x;  // 256 threads: sample t/4, features 4(t%4)..+3
+    const int sl = t >> 2, k4 = (t & 3) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s0 + sl < m) v = *reinterpret_cast<const float4 *>(feat + (s0 + sl) * 16 + k4);
+    Al[cf_slot(row0 + k4 + 0, sl)] = v.x;
+    Al[cf_slot(row0 + k4 + 1, sl)] = v.y;
+    Al[cf_slot(row0 + k4 + 2, sl)] = v.z;
+    Al[cf_slot(row0 + k4 + 3, sl)] = v.w;
+}
+
+// operand of feature row f for k-steps 4·t4 .. 4·t4+3 of lane half h
+__device__ __forceinline__ float4 cf_op(const float *img, int f, int h, int t4) {
+    const int g = 8 * h + t4;
+    return *reinterpret_cast<const float4 *>(img + f * kCh + (((g ^ (f & 15)) << 2)));
+}
+
+// sample of LDS slot q in feature row f (inverse of cf_slot within the chunk)
+__device__ __forceinline__ int cf_sample(int f, int q) {
+    const int p = ((((q >> 2) ^ (f & 15)) << 2) | (q & 3));
+    return p < 32 ? 2 * p : 2 * (p - 32) + 1;
+}
+
+// Σ over the chunk of row f of a CF image (rotated float4 reads: conflict free)
+__device__ __forceinline__ float cf_row_sum(const float *img, int f) {
+    float acc = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int g = (i + f) & 15;
+        const float4 v = *reinterpret_cast<const float4 *>(img + f * kCh + 4 * g);
+        acc += (v.x + v.y) + (v.z + v.w);
+    }
+    return acc;
+}
+// Σ_s w[s] · row f (w indexed by chunk sample)
+__device__ __forceinline__ float cf_row_dot(const float *img, int f, const float *w) {
+    float acc = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int g = (i + f) & 15;
+        const float4 v = *reinterpret_cast<const float4 *>(img + f * kCh + 4 * g);
+        acc += v.x * w[cf_sample(f, 4 * g + 0)] + v.y * w[cf_sample(f, 4 * g + 1)] +
+               v.z * w[cf_sample(f, 4 * g + 2)] + v.w * w[cf_sample(f, 4 * g + 3)];
+    }
+    return acc;
+}
+
+// One chunk (32 k-steps) of MFMAs for a wave's NR x NC blocks; with XBLK an
+// extra block (D row block rb[xsel], A rows 128..159 = x) shares the D reads.
+template <int NR, int NC, bool XBLK>
+__device__ __forceinline__ void dw_chunk(const float *Dl, const float *Al, const int (&rb)[NR], const int (&cb)[NC],
+                                         f32x16 (&acc)[NR][NC], f32x16 &accx, int xsel, int lane) {
+    const int x = lane & 31, h = lane >> 5;
+#pragma unroll 2
+    for (int t4 = 0; t4 < 8; ++t4) {
+        float4 dv[NR], av[NC], ax;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) dv[i] = cf_op(Dl, 32 * rb[i] + x, h, t4);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) av[j] = cf_op(Al, 32 * cb[j] + x, h, t4);
+        if (XBLK) ax = cf_op(Al, 128 + x, h, t4);
+        const float4 dx = (XBLK && NR > 1 && xsel) ? dv[NR - 1] : dv[0];
+#define PSVO_DW_K(c)                                                                       \
+        _Pragma("unroll") for (int i = 0; i < NR; ++i)                                     \
+            _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(dv[i].c, av[j].c, acc[i][j]); \
+        if (XBLK) accx = mfma(dx.c, ax.c, accx);
+        PSVO_DW_K(x)
+        PSVO_DW_K(y)
+        PSVO_DW_K(z)
+        PSVO_DW_K(w)
+#undef PSVO_DW_K
     }
 }
 
-// rows [s0, s0 + kDwS) of a row-major [M][ld] source, columns [0, n) (n % 4
-// == 0, ld % 4 == 0) → LDS rows at column offset `col0`; zero beyond M.
-__device__ __forceinline__ void stage_v4(float *dst, int col0, const float *__restrict__ src, int ld, int n,
-                                         int64_t s0, int64_t m) {
-    const int per_row = n >> 2;
-    for (int e = threadIdx.x; e < kDwS * per_row; e += 256) {
-        const int ss = e / per_row, c4 = e - ss * per_row;
-        const int64_t sg = s0 + ss;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (sg < m) v = *reinterpret_cast<const float4 *>(src + sg * ld + 4 * c4);
-        *reinterpret_cast<float4 *>(dst + ss * kDwLd + col0 + 4 * c4) = v;
-    }
-}
-__device__ __forceinline__ void stage_scalar(float *dst, int col0, const float *__restrict__ src, int ld, int n,
-                                             int64_t s0, int64_t m) {
-    for (int e = threadIdx.x; e < kDwS * n; e += 256) {
-        const int ss = e / n, c = e - ss * n;
-        const int64_t sg = s0 + ss;
-        dst[ss * kDwLd + col0 + c] = sg < m ? src[sg * ld + c] : 0.0f;
-    }
-}
-// zero columns [c0, c1) of every staged row
-__device__ __forceinline__ void zero_cols(float *dst, int c0, int c1) {
-    const int w = c1 - c0;
-    for (int e = threadIdx.x; e < kDwS * w; e += 256) dst[(e / w) * kDwLd + c0 + e % w] = 0.0f;
-}
-
-// Register prefetch of one tile-major 64-sample chunk (8 float4 / thread).
-struct TmRegs {
-    float4 v[8];
-};
-__device__ __forceinline__ void tm_load(TmRegs &r, const float *__restrict__ src, int64_t s0, int64_t m) {
-    const int64_t t0 = s0 >> 5;
+// write C blocks to the slab (rows offset `row_off` in the layer's matrix)
+template <int NR, int NC>
+__device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int max_col, const int (&rb)[NR],
+                                         const int (&cb)[NC], const f32x16 (&acc)[NR][NC], int lane) {
+    const int x = lane & 31, h = lane >> 5;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        const int e = threadIdx.x + 256 * u;
-        const int lane = e & 63, tl = e >> 10;
-        const int sl = (tl << 5) + (lane & 31);
-        r.v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (s0 + sl < m) r.v[u] = *reinterpret_cast<const float4 *>(src + t0 * (4 * 4 * 64 * 4) + (int64_t)e * 4);
-    }
-}
-__device__ __forceinline__ void tm_store(float *dst, int col0, const TmRegs &r) {
+    for (int i = 0; i < NR; ++i)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        const int e = threadIdx.x + 256 * u;
-        const int lane = e & 63, rg = (e >> 6) & 3, b = (e >> 8) & 3, tl = e >> 10;
-        const int sl = (tl << 5) + (lane & 31);
-        *reinterpret_cast<float4 *>(dst + sl * kDwLd + col0 + 32 * b + 8 * rg + 4 * (lane >> 5)) = r.v[u];
-    }
+        for (int j = 0; j < NC; ++j) {
+            const int col = 32 * cb[j] + x;
+            if (col >= max_col) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) slab[(row_off + 32 * rb[i] + phi(r, h)) * cols + col] = acc[i][j][r];
+        }
 }
 
 template <int L>
 __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab, float *Dl,
-                                         float *Al) {
-    constexpr int RB = (L == 2) ? 5 : (L == 4 ? 1 : 4);
-    constexpr int CB = (L == 0) ? 1 : (L == 3 ? 5 : 4);
-    constexpr int ROWS = (L == 2) ? 129 : (L == 4 ? 3 : 128);
-    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
-    // block ownership: W1 (4x1) and W4 (4x5) fix rb = wave; W2 (4x4), W3 (5x4)
-    // and W5 (1x4) fix cb = wave
-    constexpr bool FIX_CB = (L == 1 || L == 2 || L == 4);
-    constexpr int NBW = FIX_CB ? RB : CB;
-    constexpr int kBiasCols = (L == 2) ? 129 : ROWS;  // D columns holding bias sums
-    constexpr bool D_TM = (L != 4);  // D staged from tile-major
-    constexpr bool A_TM = (L != 0);  // A staged from tile-major
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
-    const int64_t n_chunks = (m + kDwS - 1) / kDwS;
+                                         float *Al, float *aux) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n_chunks = (m + kCh - 1) / kCh;
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
-    f32x16 acc[5];
-    zero(acc);
-    float bias[2] = {0.0f, 0.0f};
-    if (L == 0) zero_cols(Al, 16, 32);
-    if (L == 2) zero_cols(Dl, 129, 160);
-    if (L == 3) zero_cols(Al, 144, 160);
-    if (L == 4) zero_cols(Dl, 3, 32);
-    TmRegs rd, ra;
-    if (c_beg < c_end) {
-        if (D_TM) tm_load(rd, src.D[L], c_beg * kDwS, m);
-        if (A_TM) tm_load(ra, src.A[L], c_beg * kDwS, m);
+    // block ownership: W1 one block per wave (rb = wave); others 2x2 per wave
+    constexpr int NR = (L == 0) ? 1 : 2;
+    constexpr int NC = (L == 0) ? 1 : 2;
+    constexpr bool XBLK = (L == 3);  // W4's x columns: block (rb = wave, cb = 4)
+    int rb[NR], cb[NC];
+    if (L == 0) {
+        rb[0] = wave;
+        cb[0] = 0;
+    } else {
+        rb[0] = 2 * (wave >> 1);
+        rb[NR - 1] = 2 * (wave >> 1) + 1;
+        cb[0] = 2 * (wave & 1);
+        cb[NC - 1] = 2 * (wave & 1) + 1;
     }
+    const int xsel = wave & 1;  // rb[xsel] == wave
+    f32x16 acc[NR][NC];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) zero(acc[i]);
+    f32x16 accx[1];
+    zero(accx);
+    float vsum0 = 0.f, vsum1 = 0.f;  // VALU partials (bias / sdf row / W5)
+    // zero A rows that no chunk overwrites
+    if (L == 0)
+        for (int e = threadIdx.x; e < 16 * kCh; e += 256) Al[16 * kCh + e] = 0.f;
+    if (L == 3)
+        for (int e = threadIdx.x; e < 16 * kCh; e += 256) Al[144 * kCh + e] = 0.f;
     for (int64_t c = c_beg; c < c_end; ++c) {
-        const int64_t s0 = c * kDwS;
-        __syncthreads();  // previous chunk's MFMAs are done with the LDS image
-        if (D_TM) tm_store(Dl, 0, rd);
-        else stage_scalar(Dl, 0, src.D[4], 3, 3, s0, m);
-        if (L == 2) stage_scalar(Dl, 128, src.g_sdf, 1, 1, s0, m);
-        if (A_TM) tm_store(Al, 0, ra);
-        else stage_v4(Al, 0, src.feat, 16, 16, s0, m);
-        if (L == 3) stage_v4(Al, 128, src.feat, 16, 16, s0, m);
-        __syncthreads();
-        if (c + 1 < c_end) {  // next chunk in flight during this chunk's MFMAs
-            if (D_TM) tm_load(rd, src.D[L], s0 + kDwS, m);
-            if (A_TM) tm_load(ra, src.A[L], s0 + kDwS, m);
-        }
-        // bias partial sums: slot q = (half, LDS column), thread t owns q = t and t + 256
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int q = threadIdx.x + 256 * k;
-            if (q < 2 * kBiasCols) {
-                const int col = q % kBiasCols, hs = q / kBiasCols;
-                float part = 0.0f;
-#pragma unroll 8
-                for (int ss = 0; ss < kDwS / 2; ++ss) part += Dl[(hs * (kDwS / 2) + ss) * kDwLd + col];
-                bias[k] += part;
+        const int64_t s0 = c * kCh;
+        __syncthreads();  // previous chunk's readers are done with the images
+        if (L == 4) {
+            copy_cf(Al, src.c1 + c * kCfChunk);
+            if (threadIdx.x < kCh * 3) {
+                const int sl = threadIdx.x / 3, cc = threadIdx.x - 3 * sl;
+                aux[cc * kCh + sl] = (s0 + sl < m) ? src.d5[(s0 + sl) * 3 + cc] : 0.f;
             }
+        } else {
+            copy_cf(Dl, src.D[L] + c * kCfChunk);
+            if (L == 0) stage_x(Al, 0, src.feat, s0, m);
+            else copy_cf(Al, src.A[L] + c * kCfChunk);
+            if (L == 3) stage_x(Al, 128, src.feat, s0, m);
+            if (L == 2 && threadIdx.x < kCh) aux[threadIdx.x] = (s0 + threadIdx.x < m) ? src.g_sdf[s0 + threadIdx.x] : 0.f;
         }
-        dw_mfma<NBW, FIX_CB>(Dl, Al, acc, wave, h, i);
-    }
-#pragma unroll
-    for (int j = 0; j < NBW; ++j) {
-        const int rb = FIX_CB ? j : wave, cb = FIX_CB ? wave : j;
-        const int col = 32 * cb + i;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int lr = 32 * rb + phi(r, h);  // LDS column of D
-            int row;
-            if (L == 2) row = lr == 128 ? 0 : (lr < 128 ? lr + 1 : -1);
-            else row = lr < ROWS ? lr : -1;
-            if (row >= 0 && col < COLS) slab[row * COLS + col] = acc[j][r];
+        __builtin_amdgcn_s_waitcnt(0);  // this thread's global_load_lds have landed
+        __syncthreads();
+        // VALU pieces
+        if (L == 4) {
+            const int j = threadIdx.x & 127;
+            const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
+            vsum0 += cf_row_dot(Al, j, aux + c0 * kCh);
+            if (c0 == 0) vsum1 += cf_row_dot(Al, j, aux + 2 * kCh);
+        } else {
+            if (threadIdx.x < 128) vsum0 += cf_row_sum(Dl, threadIdx.x);  // bias partial of D row
+            if (L == 2) {
+                if (threadIdx.x >= 128) vsum1 += cf_row_dot(Al, threadIdx.x - 128, aux);  // W3 sdf row
+                if (threadIdx.x == 0) {
+                    float gs = 0.f;
+                    for (int q = 0; q < kCh; ++q) gs += aux[q];
+                    vsum1 += gs;  // db3[0]
+                }
+            }
+            dw_chunk<NR, NC, XBLK>(Dl, Al, rb, cb, acc, accx[0], xsel, lane);
         }
     }
-    // combine the two half-chunk partial sums of each column (fixed order)
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (threadIdx.x + 256 * k < 2 * kBiasCols) Dl[threadIdx.x + 256 * k] = bias[k];
-    __syncthreads();
-    if (threadIdx.x < ROWS) {
-        const int col = (L == 2) ? (threadIdx.x == 0 ? 128 : threadIdx.x - 1) : threadIdx.x;
-        slab[ROWS * COLS + threadIdx.x] = Dl[col] + Dl[kBiasCols + col];
+    // ---- write the slab: [rows][cols] weights, then [rows] bias
+    if (L == 4) {
+        const int j = threadIdx.x & 127, c0 = threadIdx.x >> 7;
+        slab[c0 * 128 + j] = vsum0;
+        if (c0 == 0) slab[2 * 128 + j] = vsum1;
+        if (threadIdx.x < 3) {  // Σ δ5 over the range, fixed order
+            float b = 0.f;
+            for (int64_t sg = c_beg * kCh; sg < c_end * kCh && sg < m; ++sg) b += src.d5[sg * 3 + threadIdx.x];
+            slab[3 * 128 + threadIdx.x] = b;
+        }
+        return;
     }
+    constexpr int ROWS = (L == 2) ? 129 : 128;
+    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
+    constexpr int ROW_OFF = (L == 2) ? 1 : 0;
+    dw_store<NR, NC>(slab, COLS, ROW_OFF, COLS, rb, cb, acc, lane);
+    if (XBLK) {
+        const int rbx[1] = {wave}, cbx[1] = {4};
+        const f32x16 tmp[1][1] = {{accx[0]}};
+        dw_store<1, 1>(slab, COLS, 0, COLS, rbx, cbx, tmp, lane);
+    }
+    if (L == 2 && threadIdx.x >= 128) slab[threadIdx.x - 128] = vsum1;  // sdf row = row 0
+    float *bias = slab + ROWS * COLS;
+    if (threadIdx.x < 128) bias[ROW_OFF + threadIdx.x] = vsum0;
+    if (L == 2 && threadIdx.x == 0) bias[0] = vsum1;
 }
 
 struct DwGrid {
@@ -658,9 +713,11 @@ struct DwGrid {
     int slab_len[5];  // rows*cols + rows
 };
 
+constexpr int kDwLds = (128 + kDwA) * kCh + 3 * kCh;  // D image, A image, aux (g_sdf / δ5)
+
 __global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs) {
-    __shared__ __attribute__((aligned(16))) float lds[2 * kDwS * kDwLd];
-    float *Dl = lds, *Al = lds + kDwS * kDwLd;
+    __shared__ __attribute__((aligned(16))) float lds[kDwLds];
+    float *Dl = lds, *Al = lds + 128 * kCh, *aux = lds + (128 + kDwA) * kCh;
     const int wg = blockIdx.x;
     int L = 0;
 #pragma unroll
@@ -669,11 +726,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid 
     const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
     float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
     switch (L) {
-        case 0: dw_layer<0>(m, src, split, n_split, slab, Dl, Al); break;
-        case 1: dw_layer<1>(m, src, split, n_split, slab, Dl, Al); break;
-        case 2: dw_layer<2>(m, src, split, n_split, slab, Dl, Al); break;
-        case 3: dw_layer<3>(m, src, split, n_split, slab, Dl, Al); break;
-        default: dw_layer<4>(m, src, split, n_split, slab, Dl, Al); break;
+        case 0: dw_layer<0>(m, src, split, n_split, slab, Dl, Al, aux); break;
+        case 1: dw_layer<1>(m, src, split, n_split, slab, Dl, Al, aux); break;
+        case 2: dw_layer<2>(m, src, split, n_split, slab, Dl, Al, aux); break;
+        case 3: dw_layer<3>(m, src, split, n_split, slab, Dl, Al, aux); break;
+        default: dw_layer<4>(m, src, split, n_split, slab, Dl, Al, aux); break;
     }
 }
 
@@ -741,14 +798,16 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-static const int kDwBlocks[5] = {4, 16, 20, 20, 4};
+static const int kDwWeight[5] = {3, 10, 11, 13, 3};  // relative per-chunk cost (MFMA + staging)
 
-// split counts per layer ∝ MFMA blocks, ≈ 2 workgroups per CU in total
+// split counts per layer ∝ cost, ≈ 2 workgroups per CU in total for n_split = 512
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
-    const int64_t chunks = (m + kDwS - 1) / kDwS;
+    const int64_t chunks = (m + kCh - 1) / kCh;
+    int wsum = 0;
+    for (int l = 0; l < 5; ++l) wsum += kDwWeight[l];
     int wg = 0, off = 0;
     for (int l = 0; l < 5; ++l) {
-        int sp = (int)((int64_t)n_split * kDwBlocks[l] / 20);
+        int sp = (int)((int64_t)n_split * kDwWeight[l] / wsum);
         if (sp < 1) sp = 1;
         if (sp > chunks) sp = (int)(chunks > 0 ? chunks : 1);
         g->wg_begin[l] = wg;
@@ -765,7 +824,7 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
     dw_grid(m, n_split, &g, &slab);
-    const int64_t mp = (m + 31) / 32 * 32;
+    const int64_t mp = (m + kCh - 1) / kCh * kCh;
     return mp * 4 * 128 + m * 3 + slab;
 }
 
@@ -787,7 +846,7 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     int slab_floats;
     dw_grid(m, n_split, &g, &slab_floats);
     float *ws = workspace;
-    const int64_t mp = (m + 31) / 32 * 32;  // tile-major matrices are padded to whole tiles
+    const int64_t mp = (m + kCh - 1) / kCh * kCh;  // CF matrices hold whole 64-sample chunks
     BwdOut o;
     o.d1 = ws; ws += mp * 128;
     o.d2 = ws; ws += mp * 128;
@@ -810,9 +869,10 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
         if (rc) return rc;
     }
     DwSrc src;
-    src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4; src.D[4] = o.d5;
-    src.A[0] = feat; src.A[1] = act; src.A[2] = act + mp * 128; src.A[3] = act + 2 * mp * 128;
-    src.A[4] = act + 3 * mp * 128;
+    src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4;
+    src.A[0] = nullptr; src.A[1] = act; src.A[2] = act + mp * 128; src.A[3] = act + 2 * mp * 128;
+    src.c1 = act + 3 * mp * 128;
+    src.d5 = o.d5;
     src.feat = feat;
     src.g_sdf = g_sdf;
     hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs);

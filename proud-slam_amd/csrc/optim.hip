@@ -12,8 +12,9 @@
 //   m  = β1 m + (1 − β1) g'
 //   v  = β2 v + (1 − β2) g'²
 //   p  = p − (lr / bc1) · m / (sqrt(v) / sqrt(bc2) + eps)
-// with bc1 = 1 − β1^t, bc2 = 1 − β2^t (host, double) — torch's _fused_adam
-// formulation (FusedAdamKernel), f32 arithmetic.
+// with bc1 = 1 − β1^t, bc2 = 1 − β2^t and 1 − β (host, double, as torch
+// forms them from Python floats) — torch's _fused_adam formulation
+// (FusedAdamKernel), f32 arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -37,7 +38,7 @@ struct AdamTable {
 };
 
 __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float lr_bc1, float bc2_sqrt, float beta1,
-                                              float beta2, float eps, float wd) {
+                                              float beta2, float omb1, float omb2, float eps, float wd) {
     int ti = 0;
     while (ti + 1 < tab.count && (int)blockIdx.x >= tab.block_begin[ti + 1]) ++ti;
     const int64_t base = (int64_t)(blockIdx.x - tab.block_begin[ti]) * kAdamSlice;
@@ -46,7 +47,6 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float lr_bc1, float
     const float *__restrict__ g = tab.g[ti];
     float *__restrict__ m = tab.m[ti];
     float *__restrict__ v = tab.v[ti];
-    const float omb1 = 1.0f - beta1, omb2 = 1.0f - beta2;
     for (int64_t i = base + threadIdx.x; i < base + kAdamSlice && i < n; i += 256) {
         float gi = g[i];
         float pi = p[i];
@@ -95,7 +95,8 @@ extern "C" int psvo_adam_step(void *stream, int n_tensors, float *const *params,
         tab.block_begin[tab.count] = blocks;
         if (blocks == 0) continue;
         hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, as_stream(stream), tab, lr_bc1, bc2_sqrt,
-                           (float)beta1, (float)beta2, (float)eps, (float)weight_decay);
+                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
+                           (float)weight_decay);
         const int rc = check_launch("adam_step");
         if (rc) return rc;
     }

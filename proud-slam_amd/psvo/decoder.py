@@ -35,7 +35,7 @@ class DecoderMLP(Function):
         rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
         ps = [p.contiguous() for p in params]
         training = any(ctx.needs_input_grad)  # grad mode is off inside Function.forward
-        mp = (m + 31) // 32 * 32  # tile-major activations: whole 32-sample tiles
+        mp = (m + 63) // 64 * 64  # CF activations: whole 64-sample chunks
         act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if training else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
         images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=dev)
@@ -51,7 +51,7 @@ class DecoderMLP(Function):
         dev = feat.device
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
         g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
-        n_split = 128
+        n_split = 512  # split-K workgroups of the weight gradients (~2 per CU)
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
