@@ -538,11 +538,8 @@ __device__ __forceinline__ float4 cf_op(const float *img, int f, int h, int t4) 
     return *reinterpret_cast<const float4 *>(img + f * kCh + (((g ^ (f & 15)) << 2)));
 }
 
-// sample of LDS slot q in feature row f (inverse of cf_slot within the chunk)
-__device__ __forceinline__ int cf_sample(int f, int q) {
-    const int p = ((((q >> 2) ^ (f & 15)) << 2) | (q & 3));
-    return p < 32 ? 2 * p : 2 * (p - 32) + 1;
-}
+// chunk-local sample at permuted position p (inverse of p = (s&1)·32 + s/2)
+__device__ __forceinline__ int p_sample(int p) { return p < 32 ? 2 * p : 2 * (p - 32) + 1; }
 
 // Σ over the chunk of row f of a CF image (rotated float4 reads: conflict free)
 __device__ __forceinline__ float cf_row_sum(const float *img, int f) {
@@ -555,15 +552,16 @@ __device__ __forceinline__ float cf_row_sum(const float *img, int f) {
     }
     return acc;
 }
-// Σ_s w[s] · row f (w indexed by chunk sample)
-__device__ __forceinline__ float cf_row_dot(const float *img, int f, const float *w) {
+// Σ_s w[s] · row f, with w stored in permuted order (wp[p] = w[p_sample(p)]):
+// slot group g of row f holds positions 4(g ^ f%16) .. +3
+__device__ __forceinline__ float cf_row_dot(const float *img, int f, const float *wp) {
     float acc = 0.f;
 #pragma unroll 4
     for (int i = 0; i < 16; ++i) {
         const int g = (i + f) & 15;
         const float4 v = *reinterpret_cast<const float4 *>(img + f * kCh + 4 * g);
-        acc += v.x * w[cf_sample(f, 4 * g + 0)] + v.y * w[cf_sample(f, 4 * g + 1)] +
-               v.z * w[cf_sample(f, 4 * g + 2)] + v.w * w[cf_sample(f, 4 * g + 3)];
+        const float4 w = *reinterpret_cast<const float4 *>(wp + 4 * (g ^ (f & 15)));
+        acc += (v.x * w.x + v.y * w.y) + (v.z * w.z + v.w * w.w);
     }
     return acc;
 }
@@ -648,16 +646,20 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
         __syncthreads();  // previous chunk's readers are done with the images
         if (L == 4) {
             copy_cf(Al, src.c1 + c * kCfChunk);
-            if (threadIdx.x < kCh * 3) {
-                const int sl = threadIdx.x / 3, cc = threadIdx.x - 3 * sl;
-                aux[cc * kCh + sl] = (s0 + sl < m) ? src.d5[(s0 + sl) * 3 + cc] : 0.f;
+            if (threadIdx.x < kCh * 3) {  // δ5 channels in permuted sample order
+                const int cc = threadIdx.x / kCh, pp = threadIdx.x - cc * kCh;
+                const int64_t sg = s0 + p_sample(pp);
+                aux[cc * kCh + pp] = sg < m ? src.d5[sg * 3 + cc] : 0.f;
             }
         } else {
             copy_cf(Dl, src.D[L] + c * kCfChunk);
             if (L == 0) stage_x(Al, 0, src.feat, s0, m);
             else copy_cf(Al, src.A[L] + c * kCfChunk);
             if (L == 3) stage_x(Al, 128, src.feat, s0, m);
-            if (L == 2 && threadIdx.x < kCh) aux[threadIdx.x] = (s0 + threadIdx.x < m) ? src.g_sdf[s0 + threadIdx.x] : 0.f;
+            if (L == 2 && threadIdx.x < kCh) {  // g_sdf in permuted sample order
+                const int64_t sg = s0 + p_sample(threadIdx.x);
+                aux[threadIdx.x] = sg < m ? src.g_sdf[sg] : 0.f;
+            }
         }
         __builtin_amdgcn_s_waitcnt(0);  // this thread's global_load_lds have landed
         __syncthreads();
@@ -798,7 +800,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-static const int kDwWeight[5] = {3, 10, 11, 13, 3};  // relative per-chunk cost (MFMA + staging)
+static const int kDwWeight[5] = {4, 11, 11, 13, 4};  // relative per-chunk time (MFMA vs staging bound)
 
 // split counts per layer ∝ cost, ≈ 2 workgroups per CU in total for n_split = 512
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
