@@ -21,6 +21,8 @@
 // chains, no TF32-like rounding): the numerics class of the reference.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "psvo_common.h"
 
 namespace psvo {
@@ -717,10 +719,11 @@ struct DwGrid {
 
 constexpr int kDwLds = (128 + kDwA) * kCh + 3 * kCh;  // D image, A image, aux (g_sdf / δ5)
 
-__global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs) {
+__global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs,
+                                                   int wg_offset) {
     __shared__ __attribute__((aligned(16))) float lds[kDwLds];
     float *Dl = lds, *Al = lds + 128 * kCh, *aux = lds + (128 + kDwA) * kCh;
-    const int wg = blockIdx.x;
+    const int wg = blockIdx.x + wg_offset;
     int L = 0;
 #pragma unroll
     for (int l = 1; l < 5; ++l) L += (wg >= g.wg_begin[l]);
@@ -877,7 +880,15 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     src.d5 = o.d5;
     src.feat = feat;
     src.g_sdf = g_sdf;
-    hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs);
+    // PSVO_DW_LAYER=l (profiling aid): launch layer l's workgroups as their own dispatch
+    static const char *only = getenv("PSVO_DW_LAYER");
+    if (only && *only) {
+        for (int l = 0; l < 5; ++l)
+            hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[l + 1] - g.wg_begin[l]), dim3(256), 0, st, m, src, g, slabs,
+                               g.wg_begin[l]);
+    } else {
+        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs, 0);
+    }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
     DwDst d;
