@@ -507,9 +507,27 @@ struct DwSrc {
 
 constexpr int kDwA = 160;  // A image rows (W4: 128 f + 16 x + 16 zero)
 
+// global → LDS copies (global_load_lds_*): LDS destination = wave-uniform
+// base (M0) + lane × size.  Issued through inline asm so that the compiler's
+// wait insertion does not treat them as LDS writes aliasing every ds_read
+// (it would drain the prefetch with vmcnt(0) before each operand read); the
+// kernel counts them itself (wait_vm).
+__device__ __forceinline__ uint32_t lds_addr(const float *l) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)l;
+}
 __device__ __forceinline__ void glds16(const float *g, float *l) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(l)))
+                 : "memory");
+}
+__device__ __forceinline__ void glds4(const float *g, float *l) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(l)))
+                 : "memory");
 }
 
 // one CF chunk (128 x 64 floats, 32 KB) → LDS, lane-linear 16-B copies
@@ -520,18 +538,6 @@ __device__ __forceinline__ void copy_cf(float *dst, const float *__restrict__ sr
         const int blk = u * 4 + wave;  // 1-KB piece of this wave-instruction
         glds16(src + (blk * 64 + lane) * 4, dst + blk * 256);
     }
-}
-
-// x rows of a chunk (feat [M][16]) into an A image at rows row0..row0+15
-__device__ __forceinline__ void stage_x(float *Al, int row0, const float *__restrict__ feat, int64_t s0, int64_t m) {
-    const int t = threadIdx.x;  // 256 threads: sample t/4, features 4(t%4)..+3
-    const int sl = t >> 2, k4 = (t & 3) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (s0 + sl < m) v = *reinterpret_cast<const float4 *>(feat + (s0 + sl) * 16 + k4);
-    Al[cf_slot(row0 + k4 + 0, sl)] = v.x;
-    Al[cf_slot(row0 + k4 + 1, sl)] = v.y;
-    Al[cf_slot(row0 + k4 + 2, sl)] = v.z;
-    Al[cf_slot(row0 + k4 + 3, sl)] = v.w;
 }
 
 // operand of feature row f for k-steps 4·t4 .. 4·t4+3 of lane half h
@@ -611,13 +617,79 @@ __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int
         }
 }
 
+// Double-buffered stage: D [128][64], A [160][64] CF images, raw x rows
+// [64][16] and raw per-sample scalars (g_sdf or δ5 [64][3]), all filled by
+// global_load_lds; the raw pieces are re-laid out LDS→LDS after landing.
+constexpr int kStD = 0, kStA = kStD + 128 * kCh, kStX = kStA + kDwA * kCh, kStS = kStX + kCh * 16,
+              kStage = kStS + kCh * 3;                        // 19,648 floats per stage
+constexpr int kDwLds = 2 * kStage + 4 * kCh;                  // + permuted per-sample weights
+static_assert(kDwLds * 4 <= 160 * 1024, "dW LDS budget");
+
+// issue the global_load_lds of chunk c into stage `st`; returns this wave's instruction count
 template <int L>
-__device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab, float *Dl,
-                                         float *Al, float *aux) {
+__device__ __forceinline__ int dw_issue(const DwSrc &src, int64_t c, int64_t m, float *st) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int n = 0;
+    if (L == 4) {
+        copy_cf(st + kStA, src.c1 + c * kCfChunk);
+        n += 8;
+    } else {
+        copy_cf(st + kStD, src.D[L] + c * kCfChunk);
+        n += 8;
+        if (L >= 1 && L <= 3) {
+            copy_cf(st + kStA, src.A[L] + c * kCfChunk);
+            n += 8;
+        }
+    }
+    const int64_t s0 = c * kCh;
+    if (L == 0 || L == 3) {  // x rows [64][16] = 4 KB: one 16-B piece per thread; rows past M clamp to row 0
+        const int e = threadIdx.x;  // float4 index: sample e/4, features 4(e%4)..
+        const int64_t sg = s0 + (e >> 2);
+        glds16(src.feat + (sg < m ? sg : 0) * 16 + (e & 3) * 4, st + kStX + wave * 256);
+        n += 1;
+    }
+    if (L == 2 && wave == 0) {  // g_sdf [64]
+        const int64_t sg = s0 + lane;
+        glds4(src.g_sdf + (sg < m ? sg : 0), st + kStS);
+        n += 1;
+    }
+    if (L == 4 && wave < 3) {  // δ5 [64][3] = 192 floats
+        const int64_t e = s0 * 3 + wave * 64 + lane;
+        glds4(src.d5 + (e < m * 3 ? e : 0), st + kStS + wave * 64);
+        n += 1;
+    }
+    return n;
+}
+
+__device__ __forceinline__ void wait_vm(int n) {
+    // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima); n <= 63
+    asm volatile("" ::: "memory");
+    switch (n) {
+        case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+        case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+        case 8: __builtin_amdgcn_s_waitcnt(0x0F78); break;
+        case 9: __builtin_amdgcn_s_waitcnt(0x0F79); break;
+        case 16: __builtin_amdgcn_s_waitcnt(0x4F70); break;
+        case 17: __builtin_amdgcn_s_waitcnt(0x4F71); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0F70); break;  // conservative: everything
+    }
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS ops done (vmcnt left as is)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int L>
+__device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab,
+                                         float *lds) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n_chunks = (m + kCh - 1) / kCh;
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
-    // block ownership: W1 one block per wave (rb = wave); others 2x2 per wave
+    float *wperm = lds + 2 * kStage;  // per-sample weights in permuted order: [4][64]
     constexpr int NR = (L == 0) ? 1 : 2;
     constexpr int NC = (L == 0) ? 1 : 2;
     constexpr bool XBLK = (L == 3);  // W4's x columns: block (rb = wave, cb = 4)
@@ -637,63 +709,77 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     for (int i = 0; i < NR; ++i) zero(acc[i]);
     f32x16 accx[1];
     zero(accx);
-    float vsum0 = 0.f, vsum1 = 0.f;  // VALU partials (bias / sdf row / W5)
-    // zero A rows that no chunk overwrites
-    if (L == 0)
-        for (int e = threadIdx.x; e < 16 * kCh; e += 256) Al[16 * kCh + e] = 0.f;
-    if (L == 3)
-        for (int e = threadIdx.x; e < 16 * kCh; e += 256) Al[144 * kCh + e] = 0.f;
+    float vsum0 = 0.f, vsum1 = 0.f, vbias = 0.f;  // VALU partials (bias / sdf row / W5)
+    // A rows no chunk writes: W1 rows 16..31, W4 rows 144..159 (both stages)
+    if (L == 0 || L == 3) {
+        const int r0 = (L == 0) ? 16 : 144;
+        for (int e = threadIdx.x; e < 16 * kCh; e += 256) {
+            lds[kStA + r0 * kCh + e] = 0.f;
+            lds[kStage + kStA + r0 * kCh + e] = 0.f;
+        }
+    }
+    __syncthreads();
+    int n_next = 0;
+    if (c_beg < c_end) n_next = dw_issue<L>(src, c_beg, m, lds);
     for (int64_t c = c_beg; c < c_end; ++c) {
+        float *st = lds + ((c - c_beg) & 1) * kStage;
+        float *nx = lds + ((c - c_beg + 1) & 1) * kStage;
+        // prefetch chunk c+1 into the other stage (its readers finished before the last barrier)
+        int n_after = 0;
+        if (c + 1 < c_end) n_after = dw_issue<L>(src, c + 1, m, nx);
+        wait_vm(n_after);  // chunk c has landed for this wave
+        raw_barrier();     // ... and for every wave
         const int64_t s0 = c * kCh;
-        __syncthreads();  // previous chunk's readers are done with the images
-        if (L == 4) {
-            copy_cf(Al, src.c1 + c * kCfChunk);
-            if (threadIdx.x < kCh * 3) {  // δ5 channels in permuted sample order
-                const int cc = threadIdx.x / kCh, pp = threadIdx.x - cc * kCh;
-                const int64_t sg = s0 + p_sample(pp);
-                aux[cc * kCh + pp] = sg < m ? src.d5[sg * 3 + cc] : 0.f;
-            }
-        } else {
-            copy_cf(Dl, src.D[L] + c * kCfChunk);
-            if (L == 0) stage_x(Al, 0, src.feat, s0, m);
-            else copy_cf(Al, src.A[L] + c * kCfChunk);
-            if (L == 3) stage_x(Al, 128, src.feat, s0, m);
-            if (L == 2 && threadIdx.x < kCh) {  // g_sdf in permuted sample order
-                const int64_t sg = s0 + p_sample(threadIdx.x);
-                aux[threadIdx.x] = sg < m ? src.g_sdf[sg] : 0.f;
+        // raw pieces → layouts (samples past M zeroed)
+        if (L == 0 || L == 3) {
+            const int row0 = (L == 0) ? 0 : 128;
+            for (int e = threadIdx.x; e < kCh * 16; e += 256) {
+                const int sl = e >> 4, k = e & 15;
+                st[kStA + cf_slot(row0 + k, sl)] = (s0 + sl < m) ? st[kStX + e] : 0.f;
             }
         }
-        __builtin_amdgcn_s_waitcnt(0);  // this thread's global_load_lds have landed
-        __syncthreads();
+        if (L == 2 && threadIdx.x < kCh) {
+            const int sl = p_sample(threadIdx.x);
+            wperm[threadIdx.x] = (s0 + sl < m) ? st[kStS + sl] : 0.f;
+        }
+        if (L == 4 && threadIdx.x < 3 * kCh) {
+            const int cc = threadIdx.x / kCh, pp = threadIdx.x - cc * kCh, sl = p_sample(pp);
+            wperm[cc * kCh + pp] = (s0 + sl < m) ? st[kStS + sl * 3 + cc] : 0.f;
+        }
+        if (L != 1) raw_barrier();
         // VALU pieces
         if (L == 4) {
             const int j = threadIdx.x & 127;
             const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
-            vsum0 += cf_row_dot(Al, j, aux + c0 * kCh);
-            if (c0 == 0) vsum1 += cf_row_dot(Al, j, aux + 2 * kCh);
+            vsum0 += cf_row_dot(st + kStA, j, wperm + c0 * kCh);
+            if (c0 == 0) vsum1 += cf_row_dot(st + kStA, j, wperm + 2 * kCh);
+            if (threadIdx.x >= 253) {  // db5: threads 253..255 sum channel t-253 of the chunk
+                float b = 0.f;
+                for (int q = 0; q < kCh; ++q) b += wperm[(threadIdx.x - 253) * kCh + q];
+                vbias += b;
+            }
         } else {
-            if (threadIdx.x < 128) vsum0 += cf_row_sum(Dl, threadIdx.x);  // bias partial of D row
+            if (threadIdx.x < 128) vsum0 += cf_row_sum(st + kStD, threadIdx.x);  // bias partial of D row
             if (L == 2) {
-                if (threadIdx.x >= 128) vsum1 += cf_row_dot(Al, threadIdx.x - 128, aux);  // W3 sdf row
+                if (threadIdx.x >= 128) vsum1 += cf_row_dot(st + kStA, threadIdx.x - 128, wperm);  // W3 sdf row
                 if (threadIdx.x == 0) {
                     float gs = 0.f;
-                    for (int q = 0; q < kCh; ++q) gs += aux[q];
+                    for (int q = 0; q < kCh; ++q) gs += wperm[q];
                     vsum1 += gs;  // db3[0]
                 }
             }
-            dw_chunk<NR, NC, XBLK>(Dl, Al, rb, cb, acc, accx[0], xsel, lane);
+            dw_chunk<NR, NC, XBLK>(st + kStD, st + kStA, rb, cb, acc, accx[0], xsel, lane);
         }
+        n_next = n_after;
+        raw_barrier();  // everyone is done reading stage `st` (and wperm) before it is refilled
     }
+    (void)n_next;
     // ---- write the slab: [rows][cols] weights, then [rows] bias
     if (L == 4) {
         const int j = threadIdx.x & 127, c0 = threadIdx.x >> 7;
         slab[c0 * 128 + j] = vsum0;
         if (c0 == 0) slab[2 * 128 + j] = vsum1;
-        if (threadIdx.x < 3) {  // Σ δ5 over the range, fixed order
-            float b = 0.f;
-            for (int64_t sg = c_beg * kCh; sg < c_end * kCh && sg < m; ++sg) b += src.d5[sg * 3 + threadIdx.x];
-            slab[3 * 128 + threadIdx.x] = b;
-        }
+        if (threadIdx.x >= 253) slab[3 * 128 + (threadIdx.x - 253)] = vbias;  // Σ δ5 per channel
         return;
     }
     constexpr int ROWS = (L == 2) ? 129 : 128;
@@ -717,12 +803,9 @@ struct DwGrid {
     int slab_len[5];  // rows*cols + rows
 };
 
-constexpr int kDwLds = (128 + kDwA) * kCh + 3 * kCh;  // D image, A image, aux (g_sdf / δ5)
-
-__global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs,
+__global__ __launch_bounds__(256, 1) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs,
                                                    int wg_offset) {
-    __shared__ __attribute__((aligned(16))) float lds[kDwLds];
-    float *Dl = lds, *Al = lds + 128 * kCh, *aux = lds + (128 + kDwA) * kCh;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wg = blockIdx.x + wg_offset;
     int L = 0;
 #pragma unroll
@@ -731,11 +814,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp_dw(int64_t m, DwSrc src, DwGrid 
     const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
     float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
     switch (L) {
-        case 0: dw_layer<0>(m, src, split, n_split, slab, Dl, Al, aux); break;
-        case 1: dw_layer<1>(m, src, split, n_split, slab, Dl, Al, aux); break;
-        case 2: dw_layer<2>(m, src, split, n_split, slab, Dl, Al, aux); break;
-        case 3: dw_layer<3>(m, src, split, n_split, slab, Dl, Al, aux); break;
-        default: dw_layer<4>(m, src, split, n_split, slab, Dl, Al, aux); break;
+        case 0: dw_layer<0>(m, src, split, n_split, slab, lds); break;
+        case 1: dw_layer<1>(m, src, split, n_split, slab, lds); break;
+        case 2: dw_layer<2>(m, src, split, n_split, slab, lds); break;
+        case 3: dw_layer<3>(m, src, split, n_split, slab, lds); break;
+        default: dw_layer<4>(m, src, split, n_split, slab, lds); break;
     }
 }
 
@@ -803,7 +886,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-static const int kDwWeight[5] = {4, 11, 11, 13, 4};  // relative per-chunk time (MFMA vs staging bound)
+static const int kDwWeight[5] = {3, 10, 10, 12, 3};  // relative per-chunk time (MFMA vs staging bound)
 
 // split counts per layer ∝ cost, ≈ 2 workgroups per CU in total for n_split = 512
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
@@ -880,14 +963,20 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     src.d5 = o.d5;
     src.feat = feat;
     src.g_sdf = g_sdf;
-    // PSVO_DW_LAYER=l (profiling aid): launch layer l's workgroups as their own dispatch
+    static bool dw_attr = false;
+    if (!dw_attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_dw),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwLds * 4);
+        dw_attr = true;
+    }
+    // PSVO_DW_LAYER=1 (profiling aid): launch each layer's workgroups as their own dispatch
     static const char *only = getenv("PSVO_DW_LAYER");
     if (only && *only) {
         for (int l = 0; l < 5; ++l)
-            hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[l + 1] - g.wg_begin[l]), dim3(256), 0, st, m, src, g, slabs,
-                               g.wg_begin[l]);
+            hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[l + 1] - g.wg_begin[l]), dim3(256), kDwLds * 4, st, m, src,
+                               g, slabs, g.wg_begin[l]);
     } else {
-        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), 0, st, m, src, g, slabs, 0);
+        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), kDwLds * 4, st, m, src, g, slabs, 0);
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;

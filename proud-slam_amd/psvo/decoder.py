@@ -51,7 +51,7 @@ class DecoderMLP(Function):
         dev = feat.device
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
         g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
-        n_split = 512  # split-K workgroups of the weight gradients (~2 per CU)
+        n_split = 256  # split-K workgroups of the weight gradients (one per CU)
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
