@@ -495,7 +495,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
 //   L1: W2 128x128  D = δh2 | A = h1        2x2 blocks per wave
 //   L2: W3 rows 1..128 D = δf | A = h2      2x2 blocks per wave (+ sdf row, db3)
 //   L3: W4 128x144  D = δc1 | A = [f | x]   2x2 blocks + one x block per wave
-//   L4: W5 3x128    VALU: δ5 [M][3] ⊗ c1
+//   W5 3x128 (VALU, δ5 [M][3] ⊗ c1) runs in the W1 workgroups
 struct DwSrc {
     const float *D[4];  // CF: δh1, δh2, δf, δc1
     const float *A[4];  // CF: (unused), h1, h2, f
@@ -630,17 +630,10 @@ template <int L>
 __device__ __forceinline__ int dw_issue(const DwSrc &src, int64_t c, int64_t m, float *st) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int n = 0;
-    if (L == 4) {
-        copy_cf(st + kStA, src.c1 + c * kCfChunk);
-        n += 8;
-    } else {
-        copy_cf(st + kStD, src.D[L] + c * kCfChunk);
-        n += 8;
-        if (L >= 1 && L <= 3) {
-            copy_cf(st + kStA, src.A[L] + c * kCfChunk);
-            n += 8;
-        }
-    }
+    copy_cf(st + kStD, src.D[L] + c * kCfChunk);
+    if (L == 0) copy_cf(st + kStA + 32 * kCh, src.c1 + c * kCfChunk);  // c1 → A rows 32..159
+    else copy_cf(st + kStA, src.A[L] + c * kCfChunk);
+    n += 16;
     const int64_t s0 = c * kCh;
     if (L == 0 || L == 3) {  // x rows [64][16] = 4 KB: one 16-B piece per thread; rows past M clamp to row 0
         const int e = threadIdx.x;  // float4 index: sample e/4, features 4(e%4)..
@@ -653,7 +646,7 @@ __device__ __forceinline__ int dw_issue(const DwSrc &src, int64_t c, int64_t m, 
         glds4(src.g_sdf + (sg < m ? sg : 0), st + kStS);
         n += 1;
     }
-    if (L == 4 && wave < 3) {  // δ5 [64][3] = 192 floats
+    if (L == 0 && wave < 3) {  // δ5 [64][3] = 192 floats
         const int64_t e = s0 * 3 + wave * 64 + lane;
         glds4(src.d5 + (e < m * 3 ? e : 0), st + kStS + wave * 64);
         n += 1;
@@ -671,6 +664,7 @@ __device__ __forceinline__ void wait_vm(int n) {
         case 9: __builtin_amdgcn_s_waitcnt(0x0F79); break;
         case 16: __builtin_amdgcn_s_waitcnt(0x4F70); break;
         case 17: __builtin_amdgcn_s_waitcnt(0x4F71); break;
+        case 18: __builtin_amdgcn_s_waitcnt(0x4F72); break;
         default: __builtin_amdgcn_s_waitcnt(0x0F70); break;  // conservative: everything
     }
     asm volatile("" ::: "memory");
@@ -683,9 +677,11 @@ __device__ __forceinline__ void raw_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// L = 0: W1 (MFMA) and W5 (VALU) share a workgroup (both are light: one
+// 32x32 block per wave / three row dots); L = 1..3: W2, W3, W4.
 template <int L>
 __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab,
-                                         float *lds) {
+                                         float *slab5, float *lds) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n_chunks = (m + kCh - 1) / kCh;
     const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
@@ -709,7 +705,8 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     for (int i = 0; i < NR; ++i) zero(acc[i]);
     f32x16 accx[1];
     zero(accx);
-    float vsum0 = 0.f, vsum1 = 0.f, vbias = 0.f;  // VALU partials (bias / sdf row / W5)
+    float vsum0 = 0.f, vsum1 = 0.f;              // VALU partials: bias, W3 sdf row / db3[0]
+    float w5a = 0.f, w5b = 0.f, vbias5 = 0.f;    // W5 row dots and db5
     // A rows no chunk writes: W1 rows 16..31, W4 rows 144..159 (both stages)
     if (L == 0 || L == 3) {
         const int r0 = (L == 0) ? 16 : 144;
@@ -742,23 +739,25 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
             const int sl = p_sample(threadIdx.x);
             wperm[threadIdx.x] = (s0 + sl < m) ? st[kStS + sl] : 0.f;
         }
-        if (L == 4 && threadIdx.x < 3 * kCh) {
+        if (L == 0 && threadIdx.x < 3 * kCh) {
             const int cc = threadIdx.x / kCh, pp = threadIdx.x - cc * kCh, sl = p_sample(pp);
             wperm[cc * kCh + pp] = (s0 + sl < m) ? st[kStS + sl * 3 + cc] : 0.f;
         }
         if (L != 1) raw_barrier();
         // VALU pieces
-        if (L == 4) {
-            const int j = threadIdx.x & 127;
-            const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
-            vsum0 += cf_row_dot(st + kStA, j, wperm + c0 * kCh);
-            if (c0 == 0) vsum1 += cf_row_dot(st + kStA, j, wperm + 2 * kCh);
-            if (threadIdx.x >= 253) {  // db5: threads 253..255 sum channel t-253 of the chunk
-                float b = 0.f;
-                for (int q = 0; q < kCh; ++q) b += wperm[(threadIdx.x - 253) * kCh + q];
-                vbias += b;
+        {
+            if (L == 0) {  // W5 = δ5 ⊗ c1 (c1 in A rows 32..159), db5
+                const float *c1l = st + kStA + 32 * kCh;
+                const int j = threadIdx.x & 127;
+                const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
+                w5a += cf_row_dot(c1l, j, wperm + c0 * kCh);
+                if (c0 == 0) w5b += cf_row_dot(c1l, j, wperm + 2 * kCh);
+                if (threadIdx.x >= 253) {  // threads 253..255 sum channel t-253 of the chunk
+                    float b = 0.f;
+                    for (int q = 0; q < kCh; ++q) b += wperm[(threadIdx.x - 253) * kCh + q];
+                    vbias5 += b;
+                }
             }
-        } else {
             if (threadIdx.x < 128) vsum0 += cf_row_sum(st + kStD, threadIdx.x);  // bias partial of D row
             if (L == 2) {
                 if (threadIdx.x >= 128) vsum1 += cf_row_dot(st + kStA, threadIdx.x - 128, wperm);  // W3 sdf row
@@ -775,12 +774,11 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
     }
     (void)n_next;
     // ---- write the slab: [rows][cols] weights, then [rows] bias
-    if (L == 4) {
+    if (L == 0) {
         const int j = threadIdx.x & 127, c0 = threadIdx.x >> 7;
-        slab[c0 * 128 + j] = vsum0;
-        if (c0 == 0) slab[2 * 128 + j] = vsum1;
-        if (threadIdx.x >= 253) slab[3 * 128 + (threadIdx.x - 253)] = vbias;  // Σ δ5 per channel
-        return;
+        slab5[c0 * 128 + j] = w5a;
+        if (c0 == 0) slab5[2 * 128 + j] = w5b;
+        if (threadIdx.x >= 253) slab5[3 * 128 + (threadIdx.x - 253)] = vbias5;
     }
     constexpr int ROWS = (L == 2) ? 129 : 128;
     constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
@@ -798,8 +796,9 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
 }
 
 struct DwGrid {
-    int wg_begin[6];  // prefix over layers of split counts
-    int slab_off[5];  // float offset of layer l's first slab
+    int wg_begin[5];  // prefix over workgroup types (0: W1+W5, 1: W2, 2: W3, 3: W4) of split counts
+    int n_split[5];   // slabs per weight matrix (W5 has W1's)
+    int slab_off[5];  // float offset of matrix l's first slab
     int slab_len[5];  // rows*cols + rows
 };
 
@@ -809,16 +808,16 @@ __global__ __launch_bounds__(256, 1) void k_mlp_dw(int64_t m, DwSrc src, DwGrid 
     const int wg = blockIdx.x + wg_offset;
     int L = 0;
 #pragma unroll
-    for (int l = 1; l < 5; ++l) L += (wg >= g.wg_begin[l]);
+    for (int l = 1; l < 4; ++l) L += (wg >= g.wg_begin[l]);
     const int split = wg - g.wg_begin[L];
     const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
     float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
+    float *slab5 = slabs + g.slab_off[4] + (int64_t)split * g.slab_len[4];
     switch (L) {
-        case 0: dw_layer<0>(m, src, split, n_split, slab, lds); break;
-        case 1: dw_layer<1>(m, src, split, n_split, slab, lds); break;
-        case 2: dw_layer<2>(m, src, split, n_split, slab, lds); break;
-        case 3: dw_layer<3>(m, src, split, n_split, slab, lds); break;
-        default: dw_layer<4>(m, src, split, n_split, slab, lds); break;
+        case 0: dw_layer<0>(m, src, split, n_split, slab, slab5, lds); break;
+        case 1: dw_layer<1>(m, src, split, n_split, slab, slab5, lds); break;
+        case 2: dw_layer<2>(m, src, split, n_split, slab, slab5, lds); break;
+        default: dw_layer<3>(m, src, split, n_split, slab, slab5, lds); break;
     }
 }
 
@@ -836,7 +835,7 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
 #pragma unroll
     for (int l = 1; l < 5; ++l) L += (e >= dst.elem_begin[l]);
     const int rel = e - dst.elem_begin[L];
-    const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
+    const int n_split = g.n_split[L];
     const float *p = slabs + g.slab_off[L] + rel;
     const int64_t stride = g.slab_len[L];
     float v = 0.0f;
@@ -886,25 +885,31 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-static const int kDwWeight[5] = {3, 10, 10, 12, 3};  // relative per-chunk time (MFMA vs staging bound)
+// relative per-chunk time of the workgroup types (W1+W5, W2, W3, W4), measured standalone
+static const int kDwWeight[4] = {5, 10, 11, 13};
 
-// split counts per layer ∝ cost, ≈ 2 workgroups per CU in total for n_split = 512
+// split counts per workgroup type ∝ cost, n_split ≈ number of CUs in total
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
     const int64_t chunks = (m + kCh - 1) / kCh;
     int wsum = 0;
-    for (int l = 0; l < 5; ++l) wsum += kDwWeight[l];
-    int wg = 0, off = 0;
-    for (int l = 0; l < 5; ++l) {
+    for (int l = 0; l < 4; ++l) wsum += kDwWeight[l];
+    int wg = 0;
+    for (int l = 0; l < 4; ++l) {
         int sp = (int)((int64_t)n_split * kDwWeight[l] / wsum);
         if (sp < 1) sp = 1;
         if (sp > chunks) sp = (int)(chunks > 0 ? chunks : 1);
         g->wg_begin[l] = wg;
+        g->n_split[l] = sp;
+        wg += sp;
+    }
+    g->wg_begin[4] = wg;
+    g->n_split[4] = g->n_split[0];  // W5 slabs come from the W1 workgroups
+    int off = 0;
+    for (int l = 0; l < 5; ++l) {
         g->slab_off[l] = off;
         g->slab_len[l] = kDwRows[l] * kDwCols[l] + kDwRows[l];
-        wg += sp;
-        off += sp * g->slab_len[l];
+        off += g->n_split[l] * g->slab_len[l];
     }
-    g->wg_begin[5] = wg;
     *slab_floats = off;
 }
 
@@ -972,11 +977,11 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     // PSVO_DW_LAYER=1 (profiling aid): launch each layer's workgroups as their own dispatch
     static const char *only = getenv("PSVO_DW_LAYER");
     if (only && *only) {
-        for (int l = 0; l < 5; ++l)
+        for (int l = 0; l < 4; ++l)
             hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[l + 1] - g.wg_begin[l]), dim3(256), kDwLds * 4, st, m, src,
                                g, slabs, g.wg_begin[l]);
     } else {
-        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[5]), dim3(256), kDwLds * 4, st, m, src, g, slabs, 0);
+        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[4]), dim3(256), kDwLds * 4, st, m, src, g, slabs, 0);
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
