@@ -752,19 +752,21 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
                 const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
                 w5a += cf_row_dot(c1l, j, wperm + c0 * kCh);
                 if (c0 == 0) w5b += cf_row_dot(c1l, j, wperm + 2 * kCh);
-                if (threadIdx.x >= 253) {  // threads 253..255 sum channel t-253 of the chunk
-                    float b = 0.f;
-                    for (int q = 0; q < kCh; ++q) b += wperm[(threadIdx.x - 253) * kCh + q];
+                if (wave < 3) {  // db5: wave c sums channel c of the chunk (one sample per lane)
+                    float b = wperm[wave * kCh + lane];
+#pragma unroll
+                    for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
                     vbias5 += b;
                 }
             }
             if (threadIdx.x < 128) vsum0 += cf_row_sum(st + kStD, threadIdx.x);  // bias partial of D row
             if (L == 2) {
                 if (threadIdx.x >= 128) vsum1 += cf_row_dot(st + kStA, threadIdx.x - 128, wperm);  // W3 sdf row
-                if (threadIdx.x == 0) {
-                    float gs = 0.f;
-                    for (int q = 0; q < kCh; ++q) gs += wperm[q];
-                    vsum1 += gs;  // db3[0]
+                if (wave == 0) {  // db3[0] = Σ g_sdf: one sample per lane, wave reduction
+                    float gs = wperm[lane];
+#pragma unroll
+                    for (int sh = 32; sh > 0; sh >>= 1) gs += __shfl_xor(gs, sh, 64);
+                    vsum1 += gs;
                 }
             }
             dw_chunk<NR, NC, XBLK>(st + kStD, st + kStA, rb, cb, acc, accx[0], xsel, lane);
@@ -778,7 +780,7 @@ __device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split,
         const int j = threadIdx.x & 127, c0 = threadIdx.x >> 7;
         slab5[c0 * 128 + j] = w5a;
         if (c0 == 0) slab5[2 * 128 + j] = w5b;
-        if (threadIdx.x >= 253) slab5[3 * 128 + (threadIdx.x - 253)] = vbias5;
+        if (wave < 3 && lane == 0) slab5[3 * 128 + wave] = vbias5;
     }
     constexpr int ROWS = (L == 2) ? 129 : 128;
     constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
