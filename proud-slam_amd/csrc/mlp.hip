@@ -888,7 +888,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
 // relative per-chunk time of the workgroup types (W1+W5, W2, W3, W4), measured standalone
-static const int kDwWeight[4] = {5, 10, 11, 13};
+static const int kDwWeight[4] = {46, 50, 58, 68};
 
 // split counts per workgroup type ∝ cost, n_split ≈ number of CUs in total
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
