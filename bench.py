@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact-global-loss", action="store_true",
+                    help="N>1: loss of the union of all ranks' rays (all-reduced criterion sums)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -56,8 +58,15 @@ def setup_dist():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # RCCL over xGMI; PSVO_DIST_BACKEND=gloo rehearses the N>1 path with
+        # several ranks sharing one GPU (the device index wraps around)
+        backend = os.environ.get("PSVO_DIST_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -188,21 +197,21 @@ def main():
     RH.KERNEL_TIMER = timer
     stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
 
+    from psvo.dist import GlobalLossSums, GradBucket
+    # one flat RCCL all-reduce of all gradients per step; exact mode forms the
+    # loss of the union of the ranks' rays (global normalisers) and sums
+    bucket = GradBucket(params, op="sum" if args.exact_global_loss else "mean")
+    reducer = GlobalLossSums() if (args.exact_global_loss and world > 1) else None
+
     def step(i, record=False):
         ro, rd, rgb, depth = batches[i % len(batches)]
         out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True)
-        loss, _ = criterion(out, (rgb, depth))
+        loss, _ = criterion(out, (rgb, depth), reduce_sums=reducer)
         embed_optim.zero_grad()  # set_to_none, as optim.zero_grad() in render_helpers.py:668
         model_optim.zero_grad()
         loss.backward()
         if world > 1:
-            flat = torch.cat([p.grad.reshape(-1) for p in params])
-            dist.all_reduce(flat)
-            off = 0
-            for p in params:
-                n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p))
-                off += n
+            bucket.allreduce()
         embed_optim.step()
         model_optim.step()
         if record:

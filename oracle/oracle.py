@@ -357,6 +357,45 @@ def criterion(outputs, rgb_gt, depth_gt, weights_cfg, truncation, max_depth, wei
     return loss, {"color_loss": color_loss, "depth_loss": depth_loss, "fs_loss": fs_loss, "sdf_loss": sdf_loss}
 
 
+def criterion_sums(color, depth, sdf, z, gt_rgb_hit, gt_depth_hit, truncation, max_depth, pad_extra=0):
+    """The eight additive partial sums the loss of criterion() decomposes into
+    (csrc/criterion.hip layout): Σ|Δrgb|, Σ_valid|Δd|, n_valid, n_front,
+    n_sdf, Σ fs², Σ sdf², 0 — differentiable torch ops.  pad_extra counts
+    extra padded samples (z = 10, sdf = 1) per ray, as a shard with a smaller
+    S_max than the global batch has them (criterion.py:70-116)."""
+    d = gt_depth_hit.unsqueeze(-1).expand(*z.shape)
+    front = (z < d - truncation).float()
+    back = (z > d + truncation).float()
+    dmask = ((d > 0.0) & (d < max_depth)).float()
+    sm = (1.0 - front) * (1.0 - back) * dmask
+    valid = ((gt_depth_hit > 0.01) & (gt_depth_hit < max_depth)).float()
+    zero = color.new_zeros(())
+    s = [(gt_rgb_hit - color).abs().sum(), ((gt_depth_hit - depth).abs() * valid).sum(), valid.sum(),
+         front.sum(), sm.sum(), torch.square(sdf * front - front).sum(),
+         torch.square((z + sdf * truncation) * sm - d * sm).sum(), zero]
+    if pad_extra:
+        zp = torch.full_like(gt_depth_hit, 10.0)
+        fp = (zp < gt_depth_hit - truncation).float()
+        bp = (zp > gt_depth_hit + truncation).float()
+        smp = (1.0 - fp) * (1.0 - bp) * ((gt_depth_hit > 0.0) & (gt_depth_hit < max_depth)).float()
+        s[3] = s[3] + pad_extra * fp.sum()
+        s[4] = s[4] + pad_extra * smp.sum()
+        s[6] = s[6] + pad_extra * torch.square((zp + truncation) * smp - gt_depth_hit * smp).sum()
+    return torch.stack(s)
+
+
+def criterion_from_sums(sums, n_hit, s_cols, weights_cfg):
+    """Loss of criterion() from (all-reduced) sums over n_hit rays x s_cols columns."""
+    color_loss = sums[0] / (3 * n_hit)
+    depth_loss = sums[1] / sums[2]
+    n_f, n_s = sums[3], sums[4]
+    fs_loss = sums[5] / (n_hit * s_cols) * (1.0 - n_f / (n_f + n_s))
+    sdf_loss = sums[6] / (n_hit * s_cols) * (1.0 - n_s / (n_f + n_s))
+    loss = (weights_cfg["rgb_weight"] * color_loss + weights_cfg["depth_weight"] * depth_loss
+            + weights_cfg["fs_weight"] * fs_loss + weights_cfg["sdf_weight"] * sdf_loss)
+    return loss, {"color_loss": color_loss, "depth_loss": depth_loss, "fs_loss": fs_loss, "sdf_loss": sdf_loss}
+
+
 REPLICA_CRITERIA = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
 SCANNET_CRITERIA = {"rgb_weight": 1.0, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
 

@@ -1,0 +1,109 @@
+"""Data-parallel path on CPU (gloo, world_size 2): psvo.dist.GlobalLossSums
+makes the sharded loss equal the single-process loss of the concatenated
+batch (criterion.py's batch-global normalisers, padded to the global S_max),
+and psvo.dist.GradBucket's one flat all-reduce makes the per-rank decoder
+gradients sum to the single-process gradients."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+R_HIT, S_MAX, TR, MAX_D = 96, 40, 0.05, 5.0
+
+
+def _batch(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    feats = torch.randn(R_HIT, S_MAX, 8, generator=g)
+    ns = torch.randint(5, S_MAX + 1, (R_HIT,), generator=g)
+    ns[:R_HIT // 2] = torch.clamp(ns[:R_HIT // 2], max=25)  # shard 0 has a smaller S_max
+    z = torch.sort(torch.rand(R_HIT, S_MAX, generator=g) * 6, dim=1).values
+    valid = torch.arange(S_MAX)[None, :] < ns[:, None]
+    z = torch.where(valid, z, torch.full_like(z, 10.0))
+    gt_rgb = torch.rand(R_HIT, 3, generator=g)
+    gt_d = torch.rand(R_HIT, generator=g) * 5.5
+    return feats, valid, z, gt_rgb, gt_d, ns
+
+
+def _model():
+    torch.manual_seed(1)
+    return torch.nn.Linear(8, 4)
+
+
+def _render(model, feats, valid, z):
+    out = model(feats)
+    sdf = torch.where(valid, out[..., 0], torch.ones_like(z))
+    w = torch.softmax(torch.where(valid, -sdf.abs(), torch.full_like(z, -1e4)), dim=1)
+    color = (w.unsqueeze(-1) * torch.sigmoid(out[..., 1:])).sum(1)
+    depth = (w * z).sum(1)
+    return color, depth, sdf
+
+
+def _single():
+    feats, valid, z, gt_rgb, gt_d, _ = _batch()
+    model = _model()
+    color, depth, sdf = _render(model, feats, valid, z)
+    out = {"ray_mask": torch.ones(R_HIT, dtype=torch.bool), "z_vals": z, "sdf": sdf, "color": color, "depth": depth}
+    loss, _ = O.criterion(out, gt_rgb, gt_d, O.REPLICA_CRITERIA, TR, MAX_D)
+    loss.backward()
+    return loss.detach(), [p.grad.clone() for p in model.parameters()]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from psvo.dist import GlobalLossSums, GradBucket, shard
+        feats, valid, z, gt_rgb, gt_d, ns = _batch()
+        b, e = shard(R_HIT, rank, world)
+        s_loc = int(ns[b:e].max())  # this shard's own S_max
+        feats, valid, z = feats[b:e, :s_loc], valid[b:e, :s_loc], z[b:e, :s_loc]
+        model = _model()
+        color, depth, sdf = _render(model, feats, valid, z)
+        red = GlobalLossSums()
+        n_hit, s_cols = red.global_shape(e - b, s_loc)
+        sums = O.criterion_sums(color, depth, sdf, z, gt_rgb[b:e], gt_d[b:e], TR, MAX_D, pad_extra=s_cols - s_loc)
+        tot = sums.detach().double().clone()
+        red(tot)
+        sums_g = sums + (tot.to(sums.dtype) - sums).detach()  # global values, local gradient paths
+        loss, _ = O.criterion_from_sums(sums_g, n_hit, s_cols, O.REPLICA_CRITERIA)
+        loss.backward()
+        GradBucket(model.parameters(), op="sum").allreduce()
+        q.put((rank, float(loss), n_hit, s_cols, [p.grad.clone() for p in model.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_global_loss_and_grad_bucket_match_single_process():
+    loss1, grads1 = _single()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, loss, n_hit, s_cols, grads in res:
+        assert (n_hit, s_cols) == (R_HIT, S_MAX)
+        assert abs(loss - float(loss1)) <= 1e-5 * abs(float(loss1))
+        for a, b in zip(grads, grads1):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * float(b.abs().max()))
+    # replicas stay identical
+    for a, b in zip(res[0][4], res[1][4]):
+        assert torch.equal(a, b)
