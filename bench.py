@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec render+backward, Replica room0, 64 samples/ray, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (v_mfma_f32_32x32x2_f32) dense peak
 
 
 def parse():
@@ -194,7 +195,7 @@ def main():
     model_optim = Adam(dec.parameters(), lr=5e-3)
     params = [emb] + list(dec.parameters())
     timer = KernelTimer()
-    RH.KERNEL_TIMER = timer
+    _lib.KERNEL_TIMER = timer
     stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
 
     from psvo.dist import GlobalLossSums, GradBucket
@@ -245,22 +246,31 @@ def main():
     value = total_rays / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # roofline of the dominant HBM-class kernel pair (query+interp backward):
-    # algorithmic bytes per launch from SURVEY §8d per-sample figures
+    # Rooflines.  Dominant by time: the NRGBD decoder — fwd, the
+    # δ chain and the weight gradients are each 53,760 MAC/sample (W=128):
+    # 3 x 107,520 FLOP per sample, MFMA-bound at the f32 matrix peak; timed
+    # with HIP events around its two libpsvo calls (mlp_fwd = prep + fwd,
+    # mlp_bwd = δ chain + dW + slab reduce).  Secondary: interp backward,
+    # HBM-bound, 1,664 algorithmic B/sample.
     m_avg = stats["m"] / args.steps
     r_avg = stats["r_hit"] / args.steps
     v_avg = stats["visits"] / args.steps
     bwd_ms = timer.mean_ms("interp_bwd")
     fwd_ms = timer.mean_ms("interp_fwd")
+    mlp_f_ms = timer.mean_ms("mlp_fwd")
+    mlp_b_ms = timer.mean_ms("mlp_bwd")
+    mlp_ms = mlp_f_ms + mlp_b_ms
+    flops_mlp = 3 * 107520.0 * m_avg
+    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms == mlp_ms else None
     bytes_bwd = 1664.0 * m_avg
     bytes_fwd = 628.0 * m_avg
     achieved = bytes_bwd / (bwd_ms * 1e-3) / 1e9 if bwd_ms == bwd_ms else None
-    traffic = None
+    traffic = {}
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("interp_bwd_bytes_per_launch")
+            traffic = json.load(open(args.traffic_json))
         except Exception:
-            traffic = None
+            traffic = {}
     result = {
         "metric": METRIC,
         "value": value,
@@ -279,11 +289,18 @@ def main():
                                f"{m_avg / max(r_avg, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
                    "rays_per_step_per_gpu": rays_per_step, "samples_per_step": m_avg, "hit_rays_per_step": r_avg,
                    "aabb_tests_per_step": v_avg, "parallelism": f"dp{world} (ray-sharded, RCCL grad all-reduce)"},
-        "roofline": {"kernel": "interp_bwd (embedding scatter + d_xyz)", "bound": "hbm",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                     "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
-        "kernels_ms": {"interp_fwd": fwd_ms, "interp_bwd": bwd_ms,
+        "roofline": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd/bwd_data/dw/dw_reduce)", "bound": "mfma",
+                     "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
+                     "traffic": traffic.get("mlp_bytes_per_step"),
+                     "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
+                     "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
+        "roofline_hbm": {"kernel": "k_interp_bwd (embedding scatter + d_xyz)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic.get("interp_bwd_bytes_per_launch"),
+                         "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
+        "kernels_ms": {"interp_fwd": fwd_ms, "interp_bwd": bwd_ms, "mlp_fwd": mlp_f_ms, "mlp_bwd": mlp_b_ms,
                        "interp_fwd_GBs": bytes_fwd / (fwd_ms * 1e-3) / 1e9 if fwd_ms == fwd_ms else None},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -55,6 +55,28 @@ _SIGNATURES = {
 
 _lib = None
 
+# Optional per-launch HIP-event timer (bench.py installs one): a callable
+# name -> context manager recording events around launches on the current
+# stream.  None (the default) costs nothing.
+KERNEL_TIMER = None
+
+
+def timed(name):
+    if KERNEL_TIMER is None:
+        return _NULL
+    return KERNEL_TIMER(name)
+
+
+class _Null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _Null()
+
 
 class PsvoError(RuntimeError):
     pass

@@ -39,7 +39,8 @@ class DecoderMLP(Function):
         act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if training else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
         images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=dev)
-        L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, feat, *ps, images, sdf, rgb, act, masks)
+        with L.timed("mlp_fwd"):
+            L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, feat, *ps, images, sdf, rgb, act, masks)
         if training:
             ctx.save_for_backward(feat, rgb, act, masks, images, *ps)
         return sdf, rgb
@@ -55,8 +56,9 @@ class DecoderMLP(Function):
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps]
-        L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb, dfeat, *grads,
-               0, n_split, ws)
+        with L.timed("mlp_bwd"):
+            L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb, dfeat,
+                   *grads, 0, n_split, ws)
         return (dfeat, *grads)
 
 

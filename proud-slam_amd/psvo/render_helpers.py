@@ -20,7 +20,6 @@ octree 256× per intersection; this path syncs twice and copies nothing.
 """
 from __future__ import annotations
 
-import contextlib
 from copy import deepcopy
 
 import torch
@@ -32,15 +31,7 @@ from .voxel_helpers import MAX_DEPTH, N_MAX_HITS, _intersect_sorted
 
 D_EMB = 16
 
-# Optional per-kernel HIP-event timer (bench.py installs one); called as a
-# context manager around individual launches on the current stream.
-KERNEL_TIMER = None
-
-
-def _timed(name):
-    if KERNEL_TIMER is None:
-        return contextlib.nullcontext()
-    return KERNEL_TIMER(name)
+_timed = L.timed  # per-launch HIP-event timer hook (psvo._lib.KERNEL_TIMER)
 
 
 def ray(ray_start, ray_dir, depths):
