@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--autograd", action="store_true",
+                    help="headline number from the drop-in autograd path instead of the native engine")
     ap.add_argument("--exact-global-loss", action="store_true",
                     help="N>1: loss of the union of all ranks' rays (all-reduced criterion sums)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -199,12 +201,22 @@ def main():
     stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
 
     from psvo.dist import GlobalLossSums, GradBucket
+    from psvo.engine import MappingEngine
     # one flat RCCL all-reduce of all gradients per step; exact mode forms the
     # loss of the union of the ranks' rays (global normalisers) and sums
     bucket = GradBucket(params, op="sum" if args.exact_global_loss else "mean")
     reducer = GlobalLossSums() if (args.exact_global_loss and world > 1) else None
+    engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
+                           criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
 
-    def step(i, record=False):
+    def record_stats(m, r_hit, visits, s_max):
+        stats["m"] += m
+        stats["r_hit"] += r_hit
+        stats["visits"] += visits
+        stats["s_max"] = max(stats["s_max"], s_max)
+
+    def step_autograd(i, record=False):
+        """The drop-in path: render_rays + Criterion + backward + Adam steps."""
         ro, rd, rgb, depth = batches[i % len(batches)]
         out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True)
         loss, _ = criterion(out, (rgb, depth), reduce_sums=reducer)
@@ -217,30 +229,68 @@ def main():
         model_optim.step()
         if record:
             s = out["samples"]
-            stats["m"] += s.m
-            stats["r_hit"] += s.r_hit
-            stats["visits"] += s.visits
-            stats["s_max"] = max(stats["s_max"], s.s_max)
+            record_stats(s.m, s.r_hit, s.visits, s.s_max)
         return loss
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    timer.enabled = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, record=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    timer.enabled = False
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def step_engine(i, record=False):
+        """The same iteration as one native call (psvo_map_step); with N > 1 the
+        flat gradient bucket is all-reduced (RCCL) before the Adam steps."""
+        ro, rd, rgb, depth = batches[i % len(batches)]
+        loss = engine.step(ro, rd, rgb, depth, seed=1000003 * rank + i, apply_adam=(world == 1))
+        if world > 1:
+            dist.all_reduce(engine.grad_flat)
+            engine.grad_flat.div_(world)
+            engine.adam()
+        if record:
+            st = engine.last_stats
+            record_stats(st[4], st[1], st[5], st[3])
+        return loss
+
+    def run(step_fn, steps, warmup, timed_hook=None):
+        for i in range(warmup):
+            step_fn(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if timed_hook:
+            timed_hook(True)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step_fn(warmup + i, record=timed_hook is not None)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if timed_hook:
+            timed_hook(False)
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    if args.autograd:
+        def hook(on):
+            timer.enabled = on
+        elapsed = run(step_autograd, args.steps, args.warmup, hook)
+        kt = {k: timer.mean_ms(k) for k in ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd")}
+    else:
+        def hook(on):
+            if on:
+                engine.set_timing(True)
+        elapsed = run(step_engine, args.steps, args.warmup, hook)
+        kt = engine.timing()
+        engine.set_timing(False)
+    # the other path, for reference (not the headline number)
+    other_steps = max(5, min(args.steps, 20))
+    if args.autograd:
+        el2 = run(step_engine, other_steps, 2)
+        other = {"path": "native engine (psvo_map_step)"}
+    else:
+        el2 = run(step_autograd, other_steps, 2)
+        other = {"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"}
+    other.update(value=args.frames * args.rays_per_frame * other_steps * world / el2,
+                 ms_per_step=1000.0 * el2 / other_steps)
     rays_per_step = args.frames * args.rays_per_frame
     total_rays = rays_per_step * args.steps * world
     value = total_rays / elapsed
@@ -255,10 +305,8 @@ def main():
     m_avg = stats["m"] / args.steps
     r_avg = stats["r_hit"] / args.steps
     v_avg = stats["visits"] / args.steps
-    bwd_ms = timer.mean_ms("interp_bwd")
-    fwd_ms = timer.mean_ms("interp_fwd")
-    mlp_f_ms = timer.mean_ms("mlp_fwd")
-    mlp_b_ms = timer.mean_ms("mlp_bwd")
+    bwd_ms, fwd_ms = kt["interp_bwd"], kt["interp_fwd"]
+    mlp_f_ms, mlp_b_ms = kt["mlp_fwd"], kt["mlp_bwd"]
     mlp_ms = mlp_f_ms + mlp_b_ms
     flops_mlp = 3 * 107520.0 * m_avg
     mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms == mlp_ms else None
@@ -300,6 +348,8 @@ def main():
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic.get("interp_bwd_bytes_per_launch"),
                          "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
+        "path": "drop-in autograd path" if args.autograd else "native engine (psvo_map_step: one call per iteration)",
+        "other_path": other,
         "kernels_ms": {"interp_fwd": fwd_ms, "interp_bwd": bwd_ms, "mlp_fwd": mlp_f_ms, "mlp_bwd": mlp_b_ms,
                        "interp_fwd_GBs": bytes_fwd / (fwd_ms * 1e-3) / 1e9 if fwd_ms == fwd_ms else None},
     }

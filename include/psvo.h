@@ -29,6 +29,8 @@
  *                                 (criterion.py:17-116)
  *   psvo_adam_step                torch.optim.Adam.step of the mapping loop
  *                                 (render_helpers.py:581-596, :668-672)
+ *   psvo_map_step                 one bundle_adjust_frames iteration (render_helpers.py:609-672):
+ *                                 render_rays + Criterion + backward + both Adam steps
  *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
  *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
  */
@@ -217,6 +219,59 @@ int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
 int psvo_adam_step(void *stream, int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, double lr, double beta1,
                    double beta2, double eps, double weight_decay, int64_t step);
+
+/* ---- native mapping iteration ---------------------------------------- */
+typedef struct psvo_engine psvo_engine;  /* owns a device workspace arena */
+
+typedef struct psvo_map_desc {
+    /* map (device): centres f32[N,3], structure i32[N,9], vertex_idx i32[N,8] */
+    int64_t n_nodes;
+    const float *centres;
+    const int *structure;
+    const int *vertex_idx;
+    /* embeddings f32[n_emb,16] and their Adam moments (updated in place) */
+    float *emb;
+    int64_t n_emb;
+    float *emb_m, *emb_v;
+    /* decoder W1,b1,...,W5,b5 (psvo_mlp_fwd layout) and Adam moments */
+    float *dec[10];
+    float *dec_m[10];
+    float *dec_v[10];
+    int width; /* 128 */
+    float voxel_size, step_size, max_distance, truncation, max_depth;
+    float w_rgb, w_depth, w_fs, w_sdf; /* Criterion weights (criterion.py:8-13) */
+    double lr_emb, lr_dec, beta1, beta2, eps;
+    /* optional flat gradient buffer f32[psvo_map_grad_floats(n_emb)]:
+     * [embeddings | W1, b1, ..., W5, b5]; NULL = engine-owned */
+    float *grad_flat;
+} psvo_map_desc;
+
+enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
+
+int64_t psvo_map_grad_floats(int64_t n_emb);
+
+psvo_engine *psvo_engine_new(void);
+void psvo_engine_free(psvo_engine *e);
+
+/* Optional HIP-event timing of the roofline regions (on the launch stream). */
+enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
+       PSVO_TIME_REGIONS = 4 };
+int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators */
+int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
+
+/* One iteration on n_rays rays (rays_o/rays_d f32[R,3], gt_rgb f32[R,3],
+ * gt_depth f32[R]): sampler noise from `seed`; Adam bias corrections for
+ * step number `adam_step`; flags PSVO_STEP_NO_ADAM stops after the
+ * gradients (into desc->grad_flat) so that ranks can all-reduce them and
+ * then call psvo_map_adam.  loss_out: device f32[PSVO_CRIT_OUT_WORDS]
+ * (PSVO_CRIT_* words); stats_out: host int[PSVO_STAT_WORDS] or NULL.  Two
+ * stats read-backs synchronise the stream; everything else is queued. */
+int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
+                  const float *rays_d, const float *gt_rgb, const float *gt_depth, uint64_t seed, int64_t adam_step,
+                  int flags, float *loss_out, int *stats_out);
+
+/* Both Adam steps of the iteration from desc->grad_flat. */
+int psvo_map_adam(void *stream, const psvo_map_desc *d, int64_t adam_step);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

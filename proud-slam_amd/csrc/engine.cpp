@@ -1,0 +1,316 @@
+// Native mapping-iteration engine: one C call runs a whole render-and-optimise
+// iteration of the mapping loop (render_helpers.py:609-672 — render_rays,
+// Criterion, loss.backward(), Adam(embeddings).step(), Adam(decoder).step())
+// on one HIP stream: 24 kernel launches, two 32-byte stats read-backs that
+// size the sample buffers, no host allocation after warm-up.  It strings
+// together the same C-ABI entry points the PyTorch autograd path calls, so
+// the two paths compute the same numbers; what it removes is the Python /
+// autograd / allocator time between launches, which otherwise leaves the GPU
+// idle behind every read-back.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+enum Slot {
+    kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
+    kOffsets, kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
+    kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
+    kGradEmb, kGradOD, kSlots
+};
+
+struct Arena {
+    void *p[kSlots] = {};
+    size_t cap[kSlots] = {};
+};
+
+}  // namespace
+}  // namespace psvo
+
+// optional HIP-event timing of the roofline regions (PSVO_TIME_*)
+struct EngineTimer {
+    bool on = false;
+    bool pending = false;  // events of the last step not yet read
+    hipEvent_t ev[PSVO_TIME_REGIONS][2] = {};
+    double ms[PSVO_TIME_REGIONS] = {};
+    int64_t n[PSVO_TIME_REGIONS] = {};
+};
+
+struct psvo_engine {
+    psvo::Arena a;
+    int *host_stats = nullptr;  // pinned, PSVO_STAT_WORDS ints
+    EngineTimer tm;
+};
+
+using namespace psvo;
+
+#define ENG_CALL(x)                     \
+    do {                                \
+        const int _rc = (x);            \
+        if (_rc != PSVO_OK) return _rc; \
+    } while (0)
+
+namespace {
+
+// device buffer of at least `bytes` for `slot`; growing synchronises the
+// stream first (the old buffer may still be read by queued kernels)
+void *slot_buf(psvo_engine *e, hipStream_t st, int slot, size_t bytes, int *rc) {
+    if (bytes == 0) bytes = 16;
+    if (e->a.cap[slot] >= bytes) return e->a.p[slot];
+    if (e->a.p[slot]) {
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(e->a.p[slot]);
+        e->a.p[slot] = nullptr;
+        e->a.cap[slot] = 0;
+    }
+    const size_t cap = bytes + bytes / 4;  // headroom against per-step size jitter
+    if (hipMalloc(&e->a.p[slot], cap) != hipSuccess) {
+        *rc = set_error(PSVO_E_LAUNCH, "engine: hipMalloc(%zu) failed", cap);
+        return nullptr;
+    }
+    e->a.cap[slot] = cap;
+    return e->a.p[slot];
+}
+
+void timer_collect(psvo_engine *e) {
+    EngineTimer &t = e->tm;
+    if (!t.pending) return;
+    for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
+        float ms = 0.f;
+        if (hipEventSynchronize(t.ev[r][1]) == hipSuccess && hipEventElapsedTime(&ms, t.ev[r][0], t.ev[r][1]) == hipSuccess) {
+            t.ms[r] += ms;
+            t.n[r] += 1;
+        }
+    }
+    t.pending = false;
+}
+
+inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
+    if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
+}
+
+int read_stats(psvo_engine *e, hipStream_t st, const int *dstats) {
+    if (hipMemcpyAsync(e->host_stats, dstats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) !=
+        hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: stats read-back failed");
+    if (hipStreamSynchronize(st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: stream sync failed");
+    return PSVO_OK;
+}
+
+}  // namespace
+
+extern "C" psvo_engine *psvo_engine_new(void) {
+    psvo_engine *e = new psvo_engine();
+    if (hipHostMalloc(reinterpret_cast<void **>(&e->host_stats), PSVO_STAT_WORDS * sizeof(int),
+                      hipHostMallocDefault) != hipSuccess) {
+        delete e;
+        return nullptr;
+    }
+    return e;
+}
+
+extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
+    PSVO_REQUIRE(e, "engine_set_timing: null engine");
+    if (on && !e->tm.ev[0][0])
+        for (int r = 0; r < PSVO_TIME_REGIONS; ++r)
+            for (int k = 0; k < 2; ++k)
+                if (hipEventCreate(&e->tm.ev[r][k]) != hipSuccess)
+                    return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
+    timer_collect(e);
+    e->tm.on = on != 0;
+    for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
+        e->tm.ms[r] = 0.0;
+        e->tm.n[r] = 0;
+    }
+    return PSVO_OK;
+}
+
+extern "C" int psvo_engine_timing(psvo_engine *e, double *mean_ms) {
+    PSVO_REQUIRE(e && mean_ms, "engine_timing: null argument");
+    timer_collect(e);
+    for (int r = 0; r < PSVO_TIME_REGIONS; ++r) mean_ms[r] = e->tm.n[r] ? e->tm.ms[r] / (double)e->tm.n[r] : -1.0;
+    return PSVO_OK;
+}
+
+extern "C" void psvo_engine_free(psvo_engine *e) {
+    if (!e) return;
+    (void)hipDeviceSynchronize();
+    for (int r = 0; r < PSVO_TIME_REGIONS; ++r)
+        for (int k = 0; k < 2; ++k)
+            if (e->tm.ev[r][k]) (void)hipEventDestroy(e->tm.ev[r][k]);
+    for (int s = 0; s < kSlots; ++s)
+        if (e->a.p[s]) (void)hipFree(e->a.p[s]);
+    if (e->host_stats) (void)hipHostFree(e->host_stats);
+    delete e;
+}
+
+#define ENG_BUF(T, name, slot, bytes)                                        \
+    T *name = reinterpret_cast<T *>(slot_buf(e, st, slot, (bytes), &rc));   \
+    if (!name) return rc;
+
+static const int64_t kDecSizes[10] = {128 * 16, 128, 128 * 128, 128, 129 * 128, 129, 128 * 144, 128, 3 * 128, 3};
+static const int64_t kDecTotal = 128 * 16 + 128 + 128 * 128 + 128 + 129 * 128 + 129 + 128 * 144 + 128 + 3 * 128 + 3;
+
+extern "C" int64_t psvo_map_grad_floats(int64_t n_emb) { return n_emb * 16 + kDecTotal; }
+
+// grads: [embeddings (n_emb x 16) | W1, b1, ..., W5, b5]
+static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_t adam_step) {
+    float *p[1] = {d->emb};
+    const float *g[1] = {grads};
+    float *m[1] = {d->emb_m};
+    float *v[1] = {d->emb_v};
+    const int64_t n[1] = {d->n_emb * 16};
+    ENG_CALL(psvo_adam_step(st, 1, p, g, m, v, n, d->lr_emb, d->beta1, d->beta2, d->eps, 0.0, adam_step));
+    const float *gd[10];
+    int64_t off = d->n_emb * 16;
+    for (int i = 0; i < 10; ++i) {
+        gd[i] = grads + off;
+        off += kDecSizes[i];
+    }
+    ENG_CALL(psvo_adam_step(st, 10, d->dec, gd, d->dec_m, d->dec_v, kDecSizes, d->lr_dec, d->beta1, d->beta2,
+                            d->eps, 0.0, adam_step));
+    return PSVO_OK;
+}
+
+extern "C" int psvo_map_adam(void *stream, const psvo_map_desc *d, int64_t adam_step) {
+    PSVO_REQUIRE(d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
+    return map_adam(as_stream(stream), d, d->grad_flat, adam_step);
+}
+
+extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
+                             const float *rays_o, const float *rays_d, const float *gt_rgb, const float *gt_depth,
+                             uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
+    PSVO_REQUIRE(e && d && rays_o && rays_d && gt_rgb && gt_depth && loss_out, "map_step: null argument");
+    PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "map_step: bad sizes");
+    PSVO_REQUIRE(d->width == 128, "map_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
+    hipStream_t st = as_stream(stream);
+    int rc = PSVO_OK;
+    const int64_t R = n_rays;
+    // ---- query: intersection, hit ranks, statistics
+    ENG_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
+    if (hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    ENG_BUF(int, hit_idx, kHitIdx, R * kMaxHits * sizeof(int));
+    ENG_BUF(float, hit_t0, kHitT0, R * kMaxHits * sizeof(float));
+    ENG_BUF(float, hit_t1, kHitT1, R * kMaxHits * sizeof(float));
+    ENG_BUF(int, ray_nv, kRayNv, R * sizeof(int));
+    ENG_BUF(float, ray_dsum, kRayDsum, R * sizeof(float));
+    ENG_BUF(int, ray_rank, kRayRank, R * sizeof(int));
+    ENG_BUF(int, rank_ray, kRankRay, R * sizeof(int));
+    ENG_CALL(psvo_ray_intersect_sorted(stream, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
+                                       d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum,
+                                       stats));
+    ENG_CALL(psvo_hit_rank(stream, R, ray_nv, ray_rank, rank_ray));
+    ENG_CALL(read_stats(e, st, stats));
+    timer_collect(e);  // the previous step's events completed before this read-back
+    const int P = e->host_stats[PSVO_STAT_P], r_hit = e->host_stats[PSVO_STAT_R_HIT];
+    const int max_steps = e->host_stats[PSVO_STAT_MAX_CEIL] + P;
+    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "map_step: octree deeper than the DFS stack");
+    if (r_hit == 0) return set_error(PSVO_E_INVALID, "map_step: no ray hits the octree (render_helpers.py:388)");
+    // ---- sampling
+    ENG_BUF(int, s_idx, kSIdx, (size_t)r_hit * max_steps * sizeof(int));
+    ENG_BUF(float, s_depth, kSDepth, (size_t)r_hit * max_steps * sizeof(float));
+    ENG_BUF(float, s_dist, kSDist, (size_t)r_hit * max_steps * sizeof(float));
+    ENG_BUF(int, ray_ns, kRayNs, (size_t)r_hit * sizeof(int));
+    ENG_BUF(int, offsets, kOffsets, (size_t)(r_hit + 1) * sizeof(int));
+    ENG_CALL(psvo_sample_rays(stream, r_hit, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
+                              nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
+    ENG_CALL(read_stats(e, st, stats));
+    const int s_max = e->host_stats[PSVO_STAT_S_MAX];
+    const int64_t M = e->host_stats[PSVO_STAT_M];
+    if (e->host_stats[7] & 2) return set_error(PSVO_E_OVERFLOW, "map_step: sampler exceeded max_steps");
+    if (stats_out) memcpy(stats_out, e->host_stats, PSVO_STAT_WORDS * sizeof(int));
+    if (M == 0) return set_error(PSVO_E_INVALID, "map_step: no valid samples");
+    const size_t RS = (size_t)r_hit * s_max;
+    ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
+    ENG_BUF(float, tt, kT, M * sizeof(float));
+    ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
+    ENG_BUF(float, z_vals, kZ, RS * sizeof(float));
+    ENG_BUF(uint8_t, smask, kMask, RS);
+    ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
+                                z_vals, smask));
+    // ---- forward: interpolation, decoder, compositing, loss
+    ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
+    mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+    ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
+                             d->vertex_idx, d->emb, feat));
+    mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+    const int64_t mp = (M + 63) / 64 * 64;
+    ENG_BUF(float, images, kImages, psvo_mlp_image_floats() * sizeof(float));
+    ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
+    ENG_BUF(float, rgb_s, kRgbS, M * 3 * sizeof(float));
+    ENG_BUF(float, act, kAct, (size_t)4 * mp * 128 * sizeof(float));
+    ENG_BUF(uint64_t, masks, kMasks, (size_t)M * 6 * sizeof(uint64_t));
+    float *const *W = d->dec;
+    mark(e, st, PSVO_TIME_MLP_FWD, 0);
+    ENG_CALL(psvo_mlp_fwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images,
+                          sdf_s, rgb_s, act, masks));
+    mark(e, st, PSVO_TIME_MLP_FWD, 1);
+    ENG_BUF(float, sdf, kSdf, RS * sizeof(float));
+    ENG_BUF(float, weights, kWeights, RS * sizeof(float));
+    ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
+    ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
+    ENG_BUF(float, z_min, kZmin, (size_t)r_hit * sizeof(float));
+    ENG_CALL(psvo_composite_fwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf,
+                                weights, color, depth, z_min));
+    ENG_BUF(float, crit_ws, kCritWs, psvo_criterion_workspace_floats(r_hit) * sizeof(float));
+    ENG_BUF(double, sums, kSums, 8 * sizeof(double));
+    ENG_CALL(psvo_criterion_sums(stream, r_hit, s_max, 0, d->truncation, d->max_depth, rank_ray, gt_rgb, gt_depth,
+                                 color, depth, sdf, z_vals, crit_ws, sums));
+    ENG_CALL(psvo_criterion_finalize(stream, sums, r_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
+                                     d->truncation, PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF,
+                                     loss_out));
+    // ---- backward (d loss = 1)
+    ENG_BUF(float, g_loss, kGLoss, sizeof(float));
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g_loss), 0x3F800000 /* 1.0f */, 1, st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: g_loss fill failed");
+    ENG_BUF(float, g_color, kGColor, (size_t)r_hit * 3 * sizeof(float));
+    ENG_BUF(float, g_depth, kGDepth, (size_t)r_hit * sizeof(float));
+    ENG_BUF(float, g_sdf, kGSdf, RS * sizeof(float));
+    ENG_CALL(psvo_criterion_bwd(stream, r_hit, s_max, d->truncation, d->max_depth, rank_ray, gt_rgb, gt_depth, color,
+                                depth, sdf, z_vals, loss_out, g_loss, g_color, g_depth, g_sdf));
+    ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
+    ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
+    ENG_CALL(psvo_composite_bwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf, weights, rgb_s,
+                                g_color, g_depth, nullptr, g_sdf, g_sdf_s, g_rgb_s));
+    const int n_split = 256;
+    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
+    ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
+    // gradients: the caller's flat buffer (data-parallel all-reduce) or the arena
+    float *grads = d->grad_flat;
+    if (!grads) {
+        ENG_BUF(float, gbuf, kDecGrad, psvo_map_grad_floats(d->n_emb) * sizeof(float));
+        grads = gbuf;
+    }
+    float *grad_emb = grads;
+    float *G[10];
+    {
+        int64_t off = d->n_emb * 16;
+        for (int i = 0; i < 10; ++i) {
+            G[i] = grads + off;
+            off += kDecSizes[i];
+        }
+    }
+    mark(e, st, PSVO_TIME_MLP_BWD, 0);
+    ENG_CALL(psvo_mlp_bwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images,
+                          rgb_s, act, masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
+                          G[8], G[9], 0, n_split, mlp_ws));
+    mark(e, st, PSVO_TIME_MLP_BWD, 1);
+    ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
+    if (hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    mark(e, st, PSVO_TIME_INTERP_BWD, 0);
+    ENG_CALL(psvo_interp_bwd(stream, r_hit, 16, d->voxel_size, offsets, rank_ray, leaf, tt, rays_o, rays_d,
+                             d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
+    mark(e, st, PSVO_TIME_INTERP_BWD, 1);
+    e->tm.pending = e->tm.on;
+    // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
+    if (!(flags & PSVO_STEP_NO_ADAM)) ENG_CALL(map_adam(st, d, grads, adam_step));
+    return PSVO_OK;
+}

@@ -43,6 +43,13 @@ _SIGNATURES = {
     "psvo_criterion_finalize": (_i32, [_vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "psvo_criterion_bwd": (_i32, [_vp, _i64, _i32, _f32, _f32] + [_vp] * 12),
     "psvo_adam_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _f64, _i64]),
+    "psvo_engine_new": (_vp, []),
+    "psvo_engine_free": (None, [_vp]),
+    "psvo_engine_set_timing": (_i32, [_vp, _i32]),
+    "psvo_engine_timing": (_i32, [_vp, _vp]),
+    "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
+    "psvo_map_adam": (_i32, [_vp, _vp, _i64]),
+    "psvo_map_grad_floats": (_i64, [_i64]),
     "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
     "psvo_octree_free": (None, [_vp]),
     "psvo_octree_insert": (_i32, [_vp, _vp, _i64]),

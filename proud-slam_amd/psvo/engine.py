@@ -1,0 +1,130 @@
+"""Native mapping iteration (csrc/engine.cpp): one libpsvo call per
+bundle_adjust_frames iteration (render_helpers.py:609-672): render_rays →
+Criterion → backward → Adam(embeddings).step() + Adam(decoder).step().
+
+Same kernels and numbers as the autograd path (render_rays + Criterion +
+loss.backward() + psvo.optim.Adam), without the Python/autograd time between
+launches.  Embeddings and decoder parameters are updated in place; the Adam
+moments live here (state_dict-compatible with psvo.optim.Adam / torch Adam:
+exp_avg / exp_avg_sq / step).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+_vp, _i32, _i64, _f32, _f64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double
+
+
+class MapDesc(ctypes.Structure):
+    """Mirror of psvo_map_desc (include/psvo.h)."""
+    _fields_ = [("n_nodes", _i64), ("centres", _vp), ("structure", _vp), ("vertex_idx", _vp),
+                ("emb", _vp), ("n_emb", _i64), ("emb_m", _vp), ("emb_v", _vp),
+                ("dec", _vp * 10), ("dec_m", _vp * 10), ("dec_v", _vp * 10), ("width", _i32),
+                ("voxel_size", _f32), ("step_size", _f32), ("max_distance", _f32), ("truncation", _f32),
+                ("max_depth", _f32), ("w_rgb", _f32), ("w_depth", _f32), ("w_fs", _f32), ("w_sdf", _f32),
+                ("lr_emb", _f64), ("lr_dec", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
+                ("grad_flat", _vp)]
+
+
+def _lib():
+    return L.lib()
+
+
+class MappingEngine:
+    """map_states: psvo.octree.map_states dict (device); decoder: psvo.decoder.Decoder
+    (width 128); criteria: dict of rgb/depth/fs/sdf weights (Criterion args.criteria)."""
+
+    def __init__(self, map_states, decoder, voxel_size, step_size, truncation=0.1, max_distance=10.0,
+                 criteria=None, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3, betas=(0.9, 0.999), eps=1e-8):
+        crit = criteria or {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+        self.ms = map_states
+        self.emb = map_states["voxel_vertex_emb"]
+        self.params = decoder.fused_params()
+        for t in [self.emb] + self.params:
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise RuntimeError("MappingEngine: embeddings / decoder parameters must be contiguous f32 CUDA")
+        self.centres = map_states["voxel_center_xyz"].float().contiguous()
+        self.structure = map_states["voxel_structure"].int().contiguous()
+        self.vertex_idx = map_states["voxel_vertex_idx"].int().contiguous()
+        self.emb_m = torch.zeros_like(self.emb)
+        self.emb_v = torch.zeros_like(self.emb)
+        self.dec_m = [torch.zeros_like(p) for p in self.params]
+        self.dec_v = [torch.zeros_like(p) for p in self.params]
+        self.step_no = 0
+        self.loss_out = torch.empty(16, dtype=torch.float32, device=self.emb.device)
+        self.stats = (ctypes.c_int * 8)()
+        d = MapDesc()
+        d.n_nodes = self.centres.shape[0]
+        d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
+                                                                        self.vertex_idx))
+        d.emb, d.n_emb = self.emb.data_ptr(), self.emb.shape[0]
+        d.emb_m, d.emb_v = self.emb_m.data_ptr(), self.emb_v.data_ptr()
+        for i in range(10):
+            d.dec[i] = self.params[i].data_ptr()
+            d.dec_m[i] = self.dec_m[i].data_ptr()
+            d.dec_v[i] = self.dec_v[i].data_ptr()
+        d.width = decoder.W
+        d.voxel_size, d.step_size, d.max_distance, d.truncation = voxel_size, step_size, max_distance, truncation
+        d.max_depth = max_depth
+        d.w_rgb, d.w_depth = crit["rgb_weight"], crit["depth_weight"]
+        d.w_fs, d.w_sdf = crit["fs_weight"], crit["sdf_weight"]
+        d.lr_emb, d.lr_dec, d.beta1, d.beta2, d.eps = lr_emb, lr_dec, betas[0], betas[1], eps
+        # flat gradient bucket [embeddings | decoder]: what data-parallel ranks all-reduce
+        self.grad_flat = torch.zeros(int(_lib().psvo_map_grad_floats(self.emb.shape[0])), dtype=torch.float32,
+                                     device=self.emb.device)
+        d.grad_flat = self.grad_flat.data_ptr()
+        self.desc = d
+        h = _lib().psvo_engine_new()
+        if not h:
+            raise L.PsvoError("psvo_engine_new failed")
+        self.handle = _vp(h)
+
+    def step(self, rays_o, rays_d, rgb, depth, seed, apply_adam=True):
+        """One iteration; returns the loss (0-dim device tensor, not synchronised;
+        the buffer is reused by the next step).  apply_adam=False stops after the
+        gradients (self.grad_flat) — all-reduce them, then call adam()."""
+        ro = rays_o.reshape(-1, 3).float().contiguous()
+        rd = rays_d.reshape(-1, 3).float().contiguous()
+        gt_rgb = rgb.reshape(-1, 3).float().contiguous()
+        gt_d = depth.reshape(-1).float().contiguous()
+        self.step_no += 1
+        rc = _lib().psvo_map_step(self.handle, L.stream_of(ro.device), ctypes.addressof(self.desc), ro.shape[0],
+                                  ro.data_ptr(), rd.data_ptr(), gt_rgb.data_ptr(), gt_d.data_ptr(), int(seed),
+                                  self.step_no, 0 if apply_adam else 1, self.loss_out.data_ptr(),
+                                  ctypes.addressof(self.stats))
+        if rc != 0:
+            raise L.PsvoError(f"psvo_map_step failed (code {rc}): {_lib().psvo_last_error().decode()}")
+        return self.loss_out[0]
+
+    def adam(self):
+        """Both Adam steps from self.grad_flat (after a step(apply_adam=False))."""
+        L.call("psvo_map_adam", L.stream_of(self.emb.device), ctypes.addressof(self.desc), self.step_no)
+
+    def set_timing(self, on):
+        """HIP events around the decoder fwd / bwd and interp fwd / bwd launches."""
+        L.call("psvo_engine_set_timing", self.handle, int(bool(on)))
+
+    def timing(self):
+        """Mean ms per step of {mlp_fwd, mlp_bwd, interp_fwd, interp_bwd} since set_timing(True)."""
+        out = (ctypes.c_double * 4)()
+        L.call("psvo_engine_timing", self.handle, ctypes.cast(out, ctypes.c_void_p))
+        return dict(zip(("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd"), list(out)))
+
+    @property
+    def last_stats(self):
+        return list(self.stats)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None:
+            _lib().psvo_engine_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -21,3 +21,11 @@ if [ "${PROFILE:-1}" = "1" ]; then
   echo "rocprof rc=$rc"
   find gpurun_out/prof -name "*stats*" | head
 fi
+if [ "${DIST:-0}" = "1" ]; then
+  # N>1 rehearsal: two ranks sharing the one GPU over gloo (the driver runs RCCL on 8 GPUs)
+  PSVO_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 \
+      > gpurun_out/bench_dist2.json 2> gpurun_out/bench_dist2.err
+  rc=$?
+  echo "dist2 rc=$rc"; cat gpurun_out/bench_dist2.json; tail -5 gpurun_out/bench_dist2.err
+fi

@@ -15,7 +15,8 @@ def per_kernel(path, counter):
 
 
 def short(name):
-    return name.split("(")[0].split("::")[-1]
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0].split("<")[0].split("::")[-1].strip() or name[:40]
 
 
 fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
