@@ -269,12 +269,32 @@ __global__ __launch_bounds__(256) void k_mlp_prep(const float *__restrict__ w1, 
     img[e] = v;
 }
 
-// n floats (n % 4 == 0) of a prepared image → LDS, 16 B per lane
+// Barrier for LDS hazards only: waits for this wave's LDS operations, not for
+// its global stores (__syncthreads' fence would also drain every outstanding
+// activation store and glds before each layer).
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS ops done (vmcnt left as is)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// n floats (n % (4 NT) == 0 up to a tail) of a prepared image → LDS: batches
+// of 8 16-B loads in flight per thread before their LDS writes
 template <int NT>
 __device__ __forceinline__ void copy_img(float *wl, const float *__restrict__ img, int n) {
     const float4 *src = reinterpret_cast<const float4 *>(img);
     float4 *dst = reinterpret_cast<float4 *>(wl);
-    for (int e = threadIdx.x; e < (n >> 2); e += NT) dst[e] = src[e];
+    const int n4 = n >> 2;
+    int e = threadIdx.x;
+    for (; e + 7 * NT < n4; e += 8 * NT) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[e + u * NT];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[e + u * NT] = v[u];
+    }
+    for (; e < n4; e += NT) dst[e] = src[e];
 }
 
 struct MlpParams {
@@ -325,7 +345,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     load_x(feat, s, valid, h, x);
     stage_vectors(lds, p);
     copy_img<kThreads>(wl, img + kImgF1, 2048);
-    __syncthreads();
+    raw_barrier();
     f32x16 a[kNB], bacc[kNB];
     init_bias(a, lds + kOffB1, h);
     gemm_x(wl, x, a, lane);
@@ -334,23 +354,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
     const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
     if (save) store_cf(act, tile, a, lane, n_tiles);
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreads>(wl, img + kImgF2, 16384);
-    __syncthreads();
+    raw_barrier();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
     if (save) store_cf(act + tstride, tile, bacc, lane, n_tiles);
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
-    __syncthreads();
+    raw_barrier();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
     if (save) store_cf(act + 2 * tstride, tile, a, lane, n_tiles);
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
-    __syncthreads();
+    raw_barrier();
     init_bias(bacc, lds + kOffB4, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
@@ -425,7 +445,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     stage_vectors(lds, p);
     // ---- δc1 = W5ᵀ δ5 ⊙ mask (VALU); overlap with the W4ᵀ staging
     copy_img<kThreadsBwd>(wl, img + kImgB4, 20480);
-    __syncthreads();
+    raw_barrier();
     f32x16 a[kNB], bacc[kNB];
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
@@ -447,9 +467,9 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
     store_cf(o.d3, tile, a, lane, n_tiles);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB3, 16384);
-    __syncthreads();
+    raw_barrier();
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
@@ -458,17 +478,17 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     apply_mask(bacc, m2);
     store_cf(o.d2, tile, bacc, lane, n_tiles);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB2, 16384);
-    __syncthreads();
+    raw_barrier();
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
     apply_mask(a, m1);
     store_cf(o.d1, tile, a, lane, n_tiles);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
-    __syncthreads();
+    raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB1, 4096);
-    __syncthreads();
+    raw_barrier();
     f32x16 t1[1];
     zero(t1);
     gemm_acc<kNB, 1>(wl, a, t1, lane);
@@ -670,12 +690,6 @@ __device__ __forceinline__ void wait_vm(int n) {
     asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ void raw_barrier() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS ops done (vmcnt left as is)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // L = 0: W1 (MFMA) and W5 (VALU) share a workgroup (both are light: one
 // 32x32 block per wave / three row dots); L = 1..3: W2, W3, W4.
