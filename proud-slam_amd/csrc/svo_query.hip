@@ -68,6 +68,7 @@ __device__ __forceinline__ int child_mask(const int *__restrict__ children, int 
 // the reference order into the LDS-resident list (stride kWave).
 // Returns the number of AABB tests; *cnt the number of hits; *overflow if
 // the level stack would exceed kLevels.
+template <int STRIDE = kWave>
 __device__ int dfs_ray(const float o[3], const float d[3], const float *__restrict__ points,
                        const int *__restrict__ children, float half_voxel, int n_max, int *l_node, int *l_mask,
                        int *h_idx, float *h_t0, float *h_t1, int *cnt_out, bool *overflow) {
@@ -94,23 +95,23 @@ __device__ int dfs_ray(const float o[3], const float d[3], const float *__restri
         }
     }
     while (lvl >= 0 && cnt < n_max) {
-        int m = l_mask[lvl * kWave];
+        int m = l_mask[lvl * STRIDE];
         if (m == 0) {
             --lvl;
             continue;
         }
         const int u = 31 - __clz(m);
-        l_mask[lvl * kWave] = m & ~(1 << u);
-        const int k = children[(int64_t)l_node[lvl * kWave] * 9 + u];
+        l_mask[lvl * STRIDE] = m & ~(1 << u);
+        const int k = children[(int64_t)l_node[lvl * STRIDE] * 9 + u];
         const float *pc = points + (int64_t)k * 3;
         const int side = children[(int64_t)k * 9 + 8];
         float t0, t1;
         ++visits;
         if (!ray_aabb(o, inv, pc[0], pc[1], pc[2], half_voxel * (float)side, t0, t1)) continue;
         if (side == 1) {
-            h_idx[cnt * kWave] = k;
-            h_t0[cnt * kWave] = t0;
-            h_t1[cnt * kWave] = t1;
+            h_idx[cnt * STRIDE] = k;
+            h_t0[cnt * STRIDE] = t0;
+            h_t1[cnt * STRIDE] = t1;
             ++cnt;
             continue;
         }
@@ -119,8 +120,8 @@ __device__ int dfs_ray(const float o[3], const float d[3], const float *__restri
             break;
         }
         ++lvl;
-        l_node[lvl * kWave] = k;
-        l_mask[lvl * kWave] = child_mask(children, k);
+        l_node[lvl * STRIDE] = k;
+        l_mask[lvl * STRIDE] = child_mask(children, k);
     }
     *cnt_out = cnt;
     return visits;
@@ -162,6 +163,12 @@ __global__ __launch_bounds__(64) void k_svo_intersect_raw(int b, int n, int m, f
     }
 }
 
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) v = max(v, __shfl_xor(v, s, kWave));
@@ -174,31 +181,55 @@ __device__ __forceinline__ int wave_sum(int v) {
 }
 
 // ---------------------------------------------------------------------------
-// fused ray_intersect_vox: DFS → stable sort by t_in → max_distance trim,
-// plus per-ray Σ(t_out - t_in) for the sampler's probs / steps.
+// fused ray_intersect_vox: octree query → stable sort by t_in → max_distance
+// trim, plus per-ray Σ(t_out - t_in) for the sampler's probs / steps.
 //
-// Eight lanes per ray (lane u of the group owns child slot u), eight rays per
-// wave.  Expanding a node tests its ≤8 children in parallel and records, per
-// level, the hit / leaf bitmasks and each child's (id, t_in, t_out) in LDS;
-// the DFS then pops hit children highest slot first — the reference's 7→0
-// order — so leaf hits are emitted in exactly the serial order and the
-// ≤ n_max cap cuts the same list.  The dependent-load chain per ray shrinks
-// from one per AABB test to one per internal node on the path.  The stable
-// sort is a rank sort (rank = #{t_j < t_i} + #{t_j == t_i, j < i}).
-constexpr int kGrp = 8;                 // lanes per ray
-constexpr int kRaysPerWave = kWave / kGrp;
-constexpr int kIsWaves = 1;             // waves per block (512 blocks for 4096 rays: every CU busy)
+// One wave per ray, LEVEL-SYNCHRONOUS instead of depth-first: each pass
+// tests the children of 8 frontier nodes on the 64 lanes (lane = node slot ×
+// child slot), so a ray needs one dependent load pair per level instead of
+// one per AABB test, and all lanes of a wave follow one ray (no divergence
+// between rays).  The reference's depth-first emission order (children
+// popped 7→0, intersect_gpu.cu:191-270) is the lexicographic order of the
+// path keys Σ_d (7 − u_d)·8^(15−d); the first n_max = 50 leaves in that
+// order are the 50 smallest keys, so once 50 leaves are known every leaf or
+// subtree whose key exceeds the 50th is pruned (the DFS would never have
+// reached it).  The stable sort by t_in breaks ties by key = DFS order.  If
+// a level's frontier or leaf list would overflow LDS the wave falls back to
+// the serial DFS on lane 0 (same results).
+constexpr int kBfsF = 128;   // frontier capacity per level
+constexpr int kBfsL = 128;   // leaf list capacity (≤ 50 after pruning + one level)
+constexpr int kIsWaves = 4;  // waves (rays) per block
 
-struct IsLds {
-    float t0[kLevels][kWave];
-    float t1[kLevels][kWave];
-    int kid[kLevels][kWave];
-    int mask[kLevels][kWave];  // bits 0-7 hit children left, bits 8-15 leaf children
-    int h_idx[kRaysPerWave][kMaxHits];
-    float h_t0[kRaysPerWave][kMaxHits];
-    float h_t1[kRaysPerWave][kMaxHits];
-    float h_d[kRaysPerWave][kMaxHits];  // t_out - t_in in sorted order
+struct BfsLds {
+    uint64_t fkey[2][kBfsF];
+    int fnode[2][kBfsF];
+    uint64_t lkey[kBfsL];
+    int lidx[kBfsL];
+    float lt0[kBfsL], lt1[kBfsL];
+    float hd[kMaxHits];  // t_out - t_in in sorted order
+    int dfs_node[kLevels], dfs_mask[kLevels];
 };
+
+__device__ __forceinline__ uint64_t key_digit(int u, int depth) {
+    return (uint64_t)(7 - u) << (3 * (kLevels - depth));
+}
+
+// 50th smallest key of the leaf list (keys unique): the threshold of the prune
+__device__ uint64_t kth_key(const BfsLds &S, int n, int kth, int lane) {
+    uint64_t found = ~0ull;
+    for (int i = lane; i < n; i += kWave) {
+        const uint64_t ki = S.lkey[i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += S.lkey[j] < ki;
+        if (rank == kth) found = ki;
+    }
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const uint64_t o = __shfl_xor(found, sh, kWave);
+        found = o < found ? o : found;
+    }
+    return found;
+}
 
 __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
                                                           const float *__restrict__ rays_d,
@@ -208,112 +239,199 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           int *__restrict__ hit_idx, float *__restrict__ hit_t0,
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
                                                           float *__restrict__ ray_dsum, int *__restrict__ stats) {
-    __shared__ IsLds lds_all[kIsWaves];
-    IsLds &S = lds_all[threadIdx.x / kWave];
+    __shared__ BfsLds lds_all[kIsWaves];
+    BfsLds &S = lds_all[threadIdx.x / kWave];
     const int lane = threadIdx.x & (kWave - 1);
-    const int g = lane / kGrp, u = lane & (kGrp - 1);
-    const int64_t r = ((int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave) * kRaysPerWave + g;
+    const int64_t r = (int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave;
     const float half = voxel_size * 0.5f;
-    int nv = 0, visits = 0, cnt = 0;
-    bool overflow = false;
+    int visits = 0;
+    bool overflow_stack = false;
     if (r < n_rays) {
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
         const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
         float inv[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, d[a]);
-        // test the children of `node` into level `lvl` (all 8 lanes of the group)
-        auto expand = [&](int node, int lvl) {
-            const int k = structure[(int64_t)node * 9 + u];
-            bool hit = false, leaf = false;
-            float a = 0.0f, b = 0.0f;
-            if (k > -1) {
-                const int side = structure[(int64_t)k * 9 + 8];
-                const float *pc = centres + (int64_t)k * 3;
-                hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
-                leaf = side == 1;
-                ++visits;
-            }
-            S.t0[lvl][lane] = a;
-            S.t1[lvl][lane] = b;
-            S.kid[lvl][lane] = k;
-            const uint64_t hb = __ballot(hit), lb = __ballot(hit && leaf);
-            S.mask[lvl][lane] = (int)((hb >> (g * kGrp)) & 0xff) | ((int)((lb >> (g * kGrp)) & 0xff) << 8);
-        };
-        int lvl = -1;
-        {
-            float a = 0.0f, b = 0.0f;
+        int nl = 0, nf = 0, cur = 0;
+        bool spill = false;
+        {  // root (every lane computes the same test)
+            float a = 0.f, b = 0.f;
             const int side = structure[8];
             const bool hit = ray_aabb(o, inv, centres[0], centres[1], centres[2], half * (float)side, a, b);
-            if (u == 0) ++visits;
+            visits += lane == 0;
             if (hit) {
                 if (side == 1) {
-                    if (u == 0) {
-                        S.h_idx[g][0] = 0;
-                        S.h_t0[g][0] = a;
-                        S.h_t1[g][0] = b;
+                    if (lane == 0) {
+                        S.lkey[0] = 0;
+                        S.lidx[0] = 0;
+                        S.lt0[0] = a;
+                        S.lt1[0] = b;
                     }
-                    cnt = 1;
+                    nl = 1;
                 } else {
-                    lvl = 0;
-                    expand(0, 0);
+                    if (lane == 0) {
+                        S.fkey[0][0] = 0;
+                        S.fnode[0][0] = 0;
+                    }
+                    nf = 1;
                 }
             }
         }
-        while (lvl >= 0 && cnt < kMaxHits) {
-            const int mm = S.mask[lvl][lane];
-            const int m = mm & 0xff;
-            if (m == 0) {
-                --lvl;
-                continue;
-            }
-            const int ub = 31 - __clz(m);
-            S.mask[lvl][lane] = mm & ~(1 << ub);
-            if ((mm >> 8) & (1 << ub)) {  // leaf hit: emitted by the lane that tested it
-                if (u == ub) {
-                    S.h_idx[g][cnt] = S.kid[lvl][lane];
-                    S.h_t0[g][cnt] = S.t0[lvl][lane];
-                    S.h_t1[g][cnt] = S.t1[lvl][lane];
-                }
-                ++cnt;
-                continue;
-            }
-            if (lvl + 1 >= kLevels) {
-                overflow = true;
+        wave_lds_sync();
+        bool bounded = false;
+        uint64_t kbound = ~0ull;
+        for (int depth = 0; nf > 0 && !spill; ++depth) {
+            if (depth + 1 > kLevels) {
+                overflow_stack = true;
                 break;
             }
-            const int k = S.kid[lvl][g * kGrp + ub];
-            ++lvl;
-            expand(k, lvl);
-        }
-        // stable rank sort by t_in, then the max_distance trim (a prefix after sorting)
-        for (int i = u; i < cnt; i += kGrp) {
-            const float ti = S.h_t0[g][i];
-            int rank = 0;
-            for (int j = 0; j < cnt; ++j) {
-                const float tj = S.h_t0[g][j];
-                rank += (tj < ti) || (tj == ti && j < i);
+            int nn = 0;  // next frontier size
+            for (int base = 0; base < nf; base += kWave / 8) {
+                const int fi = base + (lane >> 3), u = lane & 7;
+                bool hit = false, leaf = false;
+                int k = -1;
+                float a = 0.f, b = 0.f;
+                uint64_t ck = 0;
+                if (fi < nf) {
+                    const int node = S.fnode[cur][fi];
+                    ck = S.fkey[cur][fi] | key_digit(u, depth + 1);
+                    k = structure[(int64_t)node * 9 + u];
+                    if (k > -1) {
+                        const int side = structure[(int64_t)k * 9 + 8];
+                        const float *pc = centres + (int64_t)k * 3;
+                        hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                        leaf = side == 1;
+                        ++visits;
+                        if (bounded && ck > kbound) hit = false;  // beyond the first 50 in DFS order
+                    }
+                }
+                const uint64_t lb = __ballot(hit && leaf), ib = __ballot(hit && !leaf);
+                const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                const int nlb = __popcll(lb), nib = __popcll(ib);
+                if (nl + nlb > kBfsL || nn + nib > kBfsF) {
+                    spill = true;
+                    break;
+                }
+                if (hit && leaf) {
+                    const int pos = nl + __popcll(lb & below);
+                    S.lkey[pos] = ck;
+                    S.lidx[pos] = k;
+                    S.lt0[pos] = a;
+                    S.lt1[pos] = b;
+                }
+                if (hit && !leaf) {
+                    const int pos = nn + __popcll(ib & below);
+                    S.fkey[cur ^ 1][pos] = ck;
+                    S.fnode[cur ^ 1][pos] = k;
+                }
+                nl += nlb;
+                nn += nib;
             }
-            nv += !(ti > max_distance);
-            const float bi = S.h_t1[g][i];
-            S.h_d[g][rank] = bi - ti;
-            if (!(ti > max_distance)) {
-                hit_idx[r * kMaxHits + rank] = S.h_idx[g][i];
+            wave_lds_sync();
+            if (spill) break;
+            if (nl >= kMaxHits) {  // keep the 50 smallest keys; prune the next frontier
+                kbound = kth_key(S, nl, kMaxHits - 1, lane);
+                bounded = true;
+                wave_lds_sync();
+                // compact leaves (order irrelevant: sorted by (t_in, key) below)
+                const uint64_t keep_all = 0;
+                (void)keep_all;
+                int w = 0;
+                for (int i0 = 0; i0 < nl; i0 += kWave) {
+                    const int i = i0 + lane;
+                    uint64_t kk = 0;
+                    int ix = 0;
+                    float ta = 0.f, tb = 0.f;
+                    const bool keep = i < nl && (kk = S.lkey[i]) <= kbound;
+                    if (i < nl) {
+                        ix = S.lidx[i];
+                        ta = S.lt0[i];
+                        tb = S.lt1[i];
+                    }
+                    const uint64_t kb = __ballot(keep);
+                    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                    wave_lds_sync();
+                    if (keep) {
+                        const int pos = w + __popcll(kb & below);
+                        S.lkey[pos] = kk;
+                        S.lidx[pos] = ix;
+                        S.lt0[pos] = ta;
+                        S.lt1[pos] = tb;
+                    }
+                    w += __popcll(kb);
+                    wave_lds_sync();
+                }
+                nl = w;
+                // prune the next frontier by the same bound
+                int wn = 0;
+                for (int i0 = 0; i0 < nn; i0 += kWave) {
+                    const int i = i0 + lane;
+                    uint64_t kk = 0;
+                    int nd = 0;
+                    if (i < nn) {
+                        kk = S.fkey[cur ^ 1][i];
+                        nd = S.fnode[cur ^ 1][i];
+                    }
+                    const bool keep = i < nn && kk <= kbound;
+                    const uint64_t kb = __ballot(keep);
+                    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                    wave_lds_sync();
+                    if (keep) {
+                        const int pos = wn + __popcll(kb & below);
+                        S.fkey[cur ^ 1][pos] = kk;
+                        S.fnode[cur ^ 1][pos] = nd;
+                    }
+                    wn += __popcll(kb);
+                    wave_lds_sync();
+                }
+                nn = wn;
+            }
+            cur ^= 1;
+            nf = nn;
+        }
+        if (spill) {  // serial DFS on lane 0 (reference order by construction; key = emission index)
+            int cnt = 0;
+            bool ov = false;
+            if (lane == 0) {
+                visits += dfs_ray<1>(o, d, centres, structure, half, kMaxHits, S.dfs_node, S.dfs_mask, S.lidx, S.lt0,
+                                     S.lt1, &cnt, &ov);
+                for (int i = 0; i < cnt; ++i) S.lkey[i] = (uint64_t)i;
+            }
+            cnt = __shfl(cnt, 0, kWave);
+            overflow_stack = overflow_stack || __shfl((int)ov, 0, kWave);
+            nl = cnt;
+            wave_lds_sync();
+        }
+        // stable sort by t_in (ties: DFS order = key), trim at max_distance
+        int nv = 0;
+        for (int i = lane; i < nl; i += kWave) {
+            const float ti = S.lt0[i];
+            const uint64_t ki = S.lkey[i];
+            int rank = 0;
+            for (int j = 0; j < nl; ++j) {
+                const float tj = S.lt0[j];
+                rank += (tj < ti) || (tj == ti && S.lkey[j] < ki);
+            }
+            const bool in = !(ti > max_distance);
+            nv += in;
+            const float bi = S.lt1[i];
+            S.hd[rank] = bi - ti;
+            if (in) {
+                hit_idx[r * kMaxHits + rank] = S.lidx[i];
                 hit_t0[r * kMaxHits + rank] = ti;
                 hit_t1[r * kMaxHits + rank] = bi;
             }
         }
-        // group-reduce nv (each lane counted its own entries)
-#pragma unroll
-        for (int sh = 1; sh < kGrp; sh <<= 1) nv += __shfl_xor(nv, sh, kWave);
-        for (int l = nv + u; l < kMaxHits; l += kGrp) {
+        nv = wave_sum(nv);
+        for (int l = nv + lane; l < kMaxHits; l += kWave) {
             hit_idx[r * kMaxHits + l] = -1;
             hit_t0[r * kMaxHits + l] = max_distance;
             hit_t1[r * kMaxHits + l] = max_distance;
         }
-        if (u == 0) {
+        wave_lds_sync();
+        if (lane == 0) {
             float dsum = 0.0f;
-            for (int l = 0; l < nv; ++l) dsum = dsum + S.h_d[g][l];
+            for (int l = 0; l < nv; ++l) dsum = dsum + S.hd[l];
             ray_nv[r] = nv;
             ray_dsum[r] = dsum;
         }
@@ -323,7 +441,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     // at the memory side)
     __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves];
     const int wvis = wave_sum(visits);
-    const int wov = wave_max(overflow ? 1 : 0);
+    const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
         blk_vis[threadIdx.x / kWave] = wvis;
         blk_ov[threadIdx.x / kWave] = wov;
@@ -589,11 +707,6 @@ struct WaveBins {  // per-wave LDS: bin b written by lane b, read by any lane
     int idx[kWave], c[kWave];
 };
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <typename Rows, typename Noise, typename Emit>
 __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int num_rays, int H, Noise noise, Emit emit,
@@ -854,8 +967,7 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves * kRaysPerWave)), dim3(kIsWaves * kWave), 0,
-                       st, n_rays,
+    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st, n_rays,
                        rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
                        ray_nv, ray_dsum, stats);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
