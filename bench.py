@@ -273,7 +273,7 @@ def main():
         def hook(on):
             timer.enabled = on
         elapsed = run(step_autograd, args.steps, args.warmup, hook)
-        kt = {k: timer.mean_ms(k) for k in ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd")}
+        kt = {k: timer.mean_ms(k) for k in MappingEngine.REGIONS}
     else:
         def hook(on):
             if on:
@@ -296,23 +296,30 @@ def main():
     value = total_rays / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # Rooflines.  Dominant by time: the NRGBD decoder — fwd, the
-    # δ chain and the weight gradients are each 53,760 MAC/sample (W=128):
-    # 3 x 107,520 FLOP per sample, MFMA-bound at the f32 matrix peak; timed
-    # with HIP events around its two libpsvo calls (mlp_fwd = prep + fwd,
-    # mlp_bwd = δ chain + dW + slab reduce).  Secondary: interp backward,
-    # HBM-bound, 1,664 algorithmic B/sample.
+    # Rooflines.  Primary — the north star's "octree query+interp
+    # kernel", HBM-bound: algorithmic bytes per step = per ray 24 B + 48 B per
+    # AABB-tested node (V measured by the kernel) + per valid sample 12 B
+    # (sampler output) + 628 B (interp fwd) + 1,664 B (interp bwd), over the
+    # summed HIP-event time of its launches (intersect + stats + hit rank,
+    # sampler + scan, sample compaction, interp fwd, interp bwd).  Secondary —
+    # the decoder (dominant by time): fwd, δ chain and weight gradients are
+    # each 53,760 MAC/sample (W=128) = 3 x 107,520 FLOP/sample, MFMA-bound.
     m_avg = stats["m"] / args.steps
     r_avg = stats["r_hit"] / args.steps
     v_avg = stats["visits"] / args.steps
+    rays_step = args.frames * args.rays_per_frame
     bwd_ms, fwd_ms = kt["interp_bwd"], kt["interp_fwd"]
     mlp_f_ms, mlp_b_ms = kt["mlp_fwd"], kt["mlp_bwd"]
+    q_parts = {k: kt[k] for k in ("intersect", "sample", "points", "interp_fwd", "interp_bwd")}
+    q_ms = sum(q_parts.values())
+    bytes_query = rays_step * 24.0 + v_avg * 48.0 + m_avg * 12.0
+    bytes_qi = bytes_query + m_avg * (628.0 + 1664.0)
+    qi_gbs = bytes_qi / (q_ms * 1e-3) / 1e9 if q_ms > 0 else None
     mlp_ms = mlp_f_ms + mlp_b_ms
     flops_mlp = 3 * 107520.0 * m_avg
-    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms == mlp_ms else None
+    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
     bytes_bwd = 1664.0 * m_avg
-    bytes_fwd = 628.0 * m_avg
-    achieved = bytes_bwd / (bwd_ms * 1e-3) / 1e9 if bwd_ms == bwd_ms else None
+    achieved_bwd = bytes_bwd / (bwd_ms * 1e-3) / 1e9 if bwd_ms > 0 else None
     traffic = {}
     if os.path.exists(args.traffic_json):
         try:
@@ -337,21 +344,28 @@ def main():
                                f"{m_avg / max(r_avg, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
                    "rays_per_step_per_gpu": rays_per_step, "samples_per_step": m_avg, "hit_rays_per_step": r_avg,
                    "aabb_tests_per_step": v_avg, "parallelism": f"dp{world} (ray-sharded, RCCL grad all-reduce)"},
-        "roofline": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd/bwd_data/dw/dw_reduce)", "bound": "mfma",
-                     "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
-                     "traffic": traffic.get("mlp_bytes_per_step"),
-                     "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
-                     "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
-        "roofline_hbm": {"kernel": "k_interp_bwd (embedding scatter + d_xyz)", "bound": "hbm",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic.get("interp_bwd_bytes_per_launch"),
-                         "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
+        "roofline": {"kernel": "octree query+interp (k_intersect_sorted+k_ray_stats+k_hit_rank, k_sample_fused+"
+                               "k_scan_samples, k_sample_points, k_interp_fwd, k_interp_bwd)",
+                     "bound": "hbm", "achieved": qi_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (qi_gbs / HBM_PEAK_GBS) if qi_gbs else None,
+                     "traffic": traffic.get("query_interp_bytes_per_step"),
+                     "algorithmic_bytes_per_launch": bytes_qi, "avg_launch_ms": q_ms,
+                     "parts_ms": q_parts, "visits_per_ray": v_avg / max(rays_step, 1),
+                     "samples_per_hit_ray": m_avg / max(r_avg, 1)},
+        "roofline_mfma": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd/bwd_data/dw/dw_reduce)",
+                          "bound": "mfma", "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
+                          "traffic": traffic.get("mlp_bytes_per_step"),
+                          "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
+                          "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
+        "roofline_interp_bwd": {"kernel": "k_interp_bwd", "bound": "hbm", "achieved": achieved_bwd,
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": (achieved_bwd / HBM_PEAK_GBS) if achieved_bwd else None,
+                                "traffic": traffic.get("interp_bwd_bytes_per_launch"),
+                                "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
         "path": "drop-in autograd path" if args.autograd else "native engine (psvo_map_step: one call per iteration)",
         "other_path": other,
-        "kernels_ms": {"interp_fwd": fwd_ms, "interp_bwd": bwd_ms, "mlp_fwd": mlp_f_ms, "mlp_bwd": mlp_b_ms,
-                       "interp_fwd_GBs": bytes_fwd / (fwd_ms * 1e-3) / 1e9 if fwd_ms == fwd_ms else None},
+        "kernels_ms": kt,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, scene, tree, step_size, args.cpu_baseline_seconds)

@@ -255,7 +255,7 @@ void psvo_engine_free(psvo_engine *e);
 
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
-       PSVO_TIME_REGIONS = 4 };
+       PSVO_TIME_INTERSECT = 4, PSVO_TIME_SAMPLE = 5, PSVO_TIME_POINTS = 6, PSVO_TIME_REGIONS = 7 };
 int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators */
 int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
 

@@ -203,10 +203,12 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(float, ray_dsum, kRayDsum, R * sizeof(float));
     ENG_BUF(int, ray_rank, kRayRank, R * sizeof(int));
     ENG_BUF(int, rank_ray, kRankRay, R * sizeof(int));
+    mark(e, st, PSVO_TIME_INTERSECT, 0);
     ENG_CALL(psvo_ray_intersect_sorted(stream, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                        d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum,
                                        stats));
     ENG_CALL(psvo_hit_rank(stream, R, ray_nv, ray_rank, rank_ray));
+    mark(e, st, PSVO_TIME_INTERSECT, 1);
     ENG_CALL(read_stats(e, st, stats));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int P = e->host_stats[PSVO_STAT_P], r_hit = e->host_stats[PSVO_STAT_R_HIT];
@@ -219,8 +221,10 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(float, s_dist, kSDist, (size_t)r_hit * max_steps * sizeof(float));
     ENG_BUF(int, ray_ns, kRayNs, (size_t)r_hit * sizeof(int));
     ENG_BUF(int, offsets, kOffsets, (size_t)(r_hit + 1) * sizeof(int));
+    mark(e, st, PSVO_TIME_SAMPLE, 0);
     ENG_CALL(psvo_sample_rays(stream, r_hit, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
                               nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
+    mark(e, st, PSVO_TIME_SAMPLE, 1);
     ENG_CALL(read_stats(e, st, stats));
     const int s_max = e->host_stats[PSVO_STAT_S_MAX];
     const int64_t M = e->host_stats[PSVO_STAT_M];
@@ -233,8 +237,10 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
     ENG_BUF(float, z_vals, kZ, RS * sizeof(float));
     ENG_BUF(uint8_t, smask, kMask, RS);
+    mark(e, st, PSVO_TIME_POINTS, 0);
     ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
                                 z_vals, smask));
+    mark(e, st, PSVO_TIME_POINTS, 1);
     // ---- forward: interpolation, decoder, compositing, loss
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
     mark(e, st, PSVO_TIME_INTERP_FWD, 0);

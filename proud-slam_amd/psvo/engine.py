@@ -108,11 +108,13 @@ class MappingEngine:
         """HIP events around the decoder fwd / bwd and interp fwd / bwd launches."""
         L.call("psvo_engine_set_timing", self.handle, int(bool(on)))
 
+    REGIONS = ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd", "intersect", "sample", "points")
+
     def timing(self):
-        """Mean ms per step of {mlp_fwd, mlp_bwd, interp_fwd, interp_bwd} since set_timing(True)."""
-        out = (ctypes.c_double * 4)()
+        """Mean ms per step of each PSVO_TIME_* region since set_timing(True)."""
+        out = (ctypes.c_double * len(self.REGIONS))()
         L.call("psvo_engine_timing", self.handle, ctypes.cast(out, ctypes.c_void_p))
-        return dict(zip(("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd"), list(out)))
+        return dict(zip(self.REGIONS, list(out)))
 
     @property
     def last_stats(self):

@@ -153,13 +153,14 @@ class RaySamples:
 def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise=None, seed=None):
     """Intersection → sampling → compaction for rays_o/rays_d [1, R, 3]."""
     dev = rays_o.device
-    q = _intersect_sorted(rays_o, rays_d, map_states["voxel_center_xyz"], map_states["voxel_structure"],
-                          voxel_size, max_distance, step_size)
-    R = q["R"]
+    R = rays_o.numel() // 3
     ray_rank = torch.empty((R,), dtype=torch.int32, device=dev)
     rank_ray = torch.empty((R,), dtype=torch.int32, device=dev)
     stream = L.stream_of(dev)
-    L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
+    with _timed("intersect"):
+        q = _intersect_sorted(rays_o, rays_d, map_states["voxel_center_xyz"], map_states["voxel_structure"],
+                              voxel_size, max_distance, step_size)
+        L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
     st = q["stats"].cpu()  # sync 1
     P, r_hit, max_ceil, visits = int(st[0]), int(st[1]), int(st[2]), int(st[5])
     if int(st[7]) & 1:
@@ -178,9 +179,10 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
             raise ValueError(f"noise must be [200, {kp}, {max_steps}], got {tuple(noise.shape)}")
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    L.call("psvo_sample_rays", stream, r_hit, max_steps, L.ptr(rank_ray), L.ptr(q["hit_idx"]), L.ptr(q["hit_t0"]),
-           L.ptr(q["hit_t1"]), L.ptr(q["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(q["stats"]),
-           L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns), L.ptr(offsets))
+    with _timed("sample"):
+        L.call("psvo_sample_rays", stream, r_hit, max_steps, L.ptr(rank_ray), L.ptr(q["hit_idx"]), L.ptr(q["hit_t0"]),
+               L.ptr(q["hit_t1"]), L.ptr(q["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(q["stats"]),
+               L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns), L.ptr(offsets))
     st = q["stats"].cpu()  # sync 2
     s_max, m = int(st[3]), int(st[4])
     if int(st[7]) & 2:
@@ -190,8 +192,9 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
     ray_of_sample = torch.empty((m,), dtype=torch.int32, device=dev)
     z_vals = torch.empty((r_hit, s_max), dtype=torch.float32, device=dev)
     mask = torch.empty((r_hit, s_max), dtype=torch.uint8, device=dev)
-    L.call("psvo_sample_points", stream, r_hit, s_max, max_steps, L.ptr(s_idx), L.ptr(s_depth), L.ptr(ray_ns),
-           L.ptr(offsets), L.ptr(leaf), L.ptr(t), L.ptr(ray_of_sample), L.ptr(z_vals), L.ptr(mask))
+    with _timed("points"):
+        L.call("psvo_sample_points", stream, r_hit, s_max, max_steps, L.ptr(s_idx), L.ptr(s_depth), L.ptr(ray_ns),
+               L.ptr(offsets), L.ptr(leaf), L.ptr(t), L.ptr(ray_of_sample), L.ptr(z_vals), L.ptr(mask))
     out = RaySamples()
     out.ray_mask = (ray_rank >= 0).view(1, R)
     out.rank_ray32 = rank_ray[:r_hit]
