@@ -329,86 +329,51 @@ __device__ __forceinline__ void load_x(const float *__restrict__ feat, int64_t s
 // (act = [h1 | h2 | f | c1], each [M][128]) and the ReLU masks of h1, h2, c1
 // (masks [M][2][3] u64: lane-half h of sample s holds bits of its 64
 // features), so the backward never re-runs the forward.
-// Register-staged prefetch of a prepared weight image: the global loads of
-// layer l+1's image are issued before layer l's MFMAs and written to the
-// other LDS buffer after them, so staging never stalls the MFMA chain.
-template <int NT, int NMAX>
-struct ImgRegs {
-    float4 v[NMAX];
-    template <int N>
-    __device__ __forceinline__ void load(const float *__restrict__ img) {
-        static_assert(N / 4 <= NT * NMAX, "image larger than the prefetch registers");
-        const float4 *src = reinterpret_cast<const float4 *>(img);
-#pragma unroll
-        for (int u = 0; u < NMAX; ++u) {
-            const int e = threadIdx.x + u * NT;
-            if (e < N / 4) v[u] = src[e];
-        }
-    }
-    template <int N>
-    __device__ __forceinline__ void store(float *dst) const {
-        float4 *d = reinterpret_cast<float4 *>(dst);
-#pragma unroll
-        for (int u = 0; u < NMAX; ++u) {
-            const int e = threadIdx.x + u * NT;
-            if (e < N / 4) d[e] = v[u];
-        }
-    }
-};
-
-// forward: 8 waves = 256 samples per workgroup, one workgroup per CU, two
-// LDS image buffers (layer l computes from one while layer l+1's image is
-// written into the other).
-constexpr int kThreadsF = 512;
-constexpr int kTileF = 256;
-constexpr int kLdsFwd2 = (kOffW + 2 * kImgFwd) * 4;  // 151,584 B
-
-__global__ __launch_bounds__(kThreadsF, 1) void k_mlp_fwd(int64_t m, const float *__restrict__ feat, MlpParams p,
-                                                          const float *__restrict__ img,
-                                                          float *__restrict__ sdf_out, float *__restrict__ rgb_out,
-                                                          float *__restrict__ act, uint64_t *__restrict__ masks) {
+__global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float *__restrict__ feat, MlpParams p,
+                                                         const float *__restrict__ img,
+                                                         float *__restrict__ sdf_out, float *__restrict__ rgb_out,
+                                                         float *__restrict__ act, uint64_t *__restrict__ masks) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *buf0 = lds + kOffW, *buf1 = buf0 + kImgFwd;
+    float *wl = lds + kOffW;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const int64_t s = (int64_t)blockIdx.x * kTileF + wave * 32 + (lane & 31);
+    const int64_t s = (int64_t)blockIdx.x * kTile + wave * 32 + (lane & 31);
     const bool valid = s < m;
     const bool save = act != nullptr;
-    const int64_t tile = (int64_t)blockIdx.x * (kTileF / 32) + wave;
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
-    const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
     float x[8];
     load_x(feat, s, valid, h, x);
     stage_vectors(lds, p);
-    copy_img<kThreadsF>(buf0, img + kImgF1, 2048);
-    ImgRegs<kThreadsF, 9> pf;
-    pf.load<16384>(img + kImgF2);
+    copy_img<kThreads>(wl, img + kImgF1, 2048);
     raw_barrier();
     f32x16 a[kNB], bacc[kNB];
     init_bias(a, lds + kOffB1, h);
-    gemm_x(buf0, x, a, lane);
+    gemm_x(wl, x, a, lane);
     const uint64_t m1 = relu(a);  // h1
-    pf.store<16384>(buf1);        // W2 image
-    pf.load<16384>(img + kImgF3);
+    const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
+    const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
     if (save) store_cf(act, tile, a, lane, n_tiles);
     raw_barrier();
+    copy_img<kThreads>(wl, img + kImgF2, 16384);
+    raw_barrier();
     init_bias(bacc, lds + kOffB2, h);
-    gemm_acc<kNB, kNB>(buf1, a, bacc, lane);
+    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
-    pf.store<16384>(buf0);           // W3 rows 1..128 image
-    pf.load<18432>(img + kImgF4);
     if (save) store_cf(act + tstride, tile, bacc, lane, n_tiles);
+    raw_barrier();
+    copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
     raw_barrier();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
-    gemm_acc<kNB, kNB>(buf0, bacc, a, lane);  // f
-    pf.store<18432>(buf1);                    // W4 image: [f | x]
+    gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
     if (save) store_cf(act + 2 * tstride, tile, a, lane, n_tiles);
     raw_barrier();
+    copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
+    raw_barrier();
     init_bias(bacc, lds + kOffB4, h);
-    gemm_acc<kNB, kNB>(buf1, a, bacc, lane);
-    gemm_x(buf1 + kNB * kNB * 16 * 64, x, bacc, lane);
+    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
+    gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
     if (save) {
         store_cf(act + 3 * tstride, tile, bacc, lane, n_tiles);
@@ -923,14 +888,14 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd);
         attr = true;
     }
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, w1, w2, w3, w4, images);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTileF)), dim3(kThreadsF), kLdsFwd2, st, m, feat, p, images, sdf,
-                       rgb, act, masks);
+    hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf, rgb,
+                       act, masks);
     return check_launch("mlp_fwd");
 }
 
