@@ -270,8 +270,9 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
                   const float *rays_d, const float *gt_rgb, const float *gt_depth, uint64_t seed, int64_t adam_step,
                   int flags, float *loss_out, int *stats_out);
 
-/* Both Adam steps of the iteration from desc->grad_flat. */
-int psvo_map_adam(void *stream, const psvo_map_desc *d, int64_t adam_step);
+/* Both Adam steps of the iteration from desc->grad_flat (one launch; the
+ * embedding gradient is zeroed as it is consumed). */
+int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step);
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

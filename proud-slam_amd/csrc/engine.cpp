@@ -11,6 +11,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <cmath>
+
 #include <vector>
 
 #include "psvo_common.h"
@@ -46,6 +48,9 @@ struct psvo_engine {
     psvo::Arena a;
     int *host_stats = nullptr;  // pinned, PSVO_STAT_WORDS ints
     EngineTimer tm;
+    hipEvent_t ready = nullptr;     // read-back completion (spin-polled)
+    bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
+    const float *clean_buf = nullptr;  // ... and which buffer that is
 };
 
 using namespace psvo;
@@ -95,11 +100,20 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
     if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
 }
 
+// 32-byte read-back of the device statistics; the host spins on an event
+// (instead of a blocking stream sync) so it resumes launching within ~1 µs
+// of the copy completing.
 int read_stats(psvo_engine *e, hipStream_t st, const int *dstats) {
     if (hipMemcpyAsync(e->host_stats, dstats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) !=
         hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: stats read-back failed");
-    if (hipStreamSynchronize(st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: stream sync failed");
+    if (!e->ready && hipEventCreateWithFlags(&e->ready, hipEventDisableTiming) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: hipEventCreate failed");
+    if (hipEventRecord(e->ready, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
+    hipError_t q;
+    while ((q = hipEventQuery(e->ready)) == hipErrorNotReady) {
+    }
+    if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: stats read-back: %s", hipGetErrorString(q));
     return PSVO_OK;
 }
 
@@ -147,6 +161,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     for (int s = 0; s < kSlots; ++s)
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
     if (e->host_stats) (void)hipHostFree(e->host_stats);
+    if (e->ready) (void)hipEventDestroy(e->ready);
     delete e;
 }
 
@@ -160,27 +175,41 @@ static const int64_t kDecTotal = 128 * 16 + 128 + 128 * 128 + 128 + 129 * 128 + 
 extern "C" int64_t psvo_map_grad_floats(int64_t n_emb) { return n_emb * 16 + kDecTotal; }
 
 // grads: [embeddings (n_emb x 16) | W1, b1, ..., W5, b5]
+// one launch for both optimisers (lr per tensor); the embedding gradient is
+// zeroed as it is consumed — the next iteration's atomics accumulate into it
 static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_t adam_step) {
-    float *p[1] = {d->emb};
-    const float *g[1] = {grads};
-    float *m[1] = {d->emb_m};
-    float *v[1] = {d->emb_v};
-    const int64_t n[1] = {d->n_emb * 16};
-    ENG_CALL(psvo_adam_step(st, 1, p, g, m, v, n, d->lr_emb, d->beta1, d->beta2, d->eps, 0.0, adam_step));
-    const float *gd[10];
+    float *p[11];
+    const float *g[11];
+    float *m[11], *v[11];
+    int64_t n[11];
+    double lr[11];
+    int zero[11];
+    p[0] = d->emb;
+    g[0] = grads;
+    m[0] = d->emb_m;
+    v[0] = d->emb_v;
+    n[0] = d->n_emb * 16;
+    lr[0] = d->lr_emb;
+    zero[0] = 1;
     int64_t off = d->n_emb * 16;
     for (int i = 0; i < 10; ++i) {
-        gd[i] = grads + off;
+        p[1 + i] = d->dec[i];
+        g[1 + i] = grads + off;
+        m[1 + i] = d->dec_m[i];
+        v[1 + i] = d->dec_v[i];
+        n[1 + i] = kDecSizes[i];
+        lr[1 + i] = d->lr_dec;
+        zero[1 + i] = 0;  // overwritten by the decoder backward
         off += kDecSizes[i];
     }
-    ENG_CALL(psvo_adam_step(st, 10, d->dec, gd, d->dec_m, d->dec_v, kDecSizes, d->lr_dec, d->beta1, d->beta2,
-                            d->eps, 0.0, adam_step));
-    return PSVO_OK;
+    return adam_launch(st, 11, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero);
 }
 
-extern "C" int psvo_map_adam(void *stream, const psvo_map_desc *d, int64_t adam_step) {
-    PSVO_REQUIRE(d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
-    return map_adam(as_stream(stream), d, d->grad_flat, adam_step);
+extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
+    PSVO_REQUIRE(e && d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
+    ENG_CALL(map_adam(as_stream(stream), d, d->grad_flat, adam_step));
+    e->grads_clean = true;
+    return PSVO_OK;
 }
 
 extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
@@ -209,23 +238,27 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
                                        stats));
     ENG_CALL(psvo_hit_rank(stream, R, ray_nv, ray_rank, rank_ray));
     mark(e, st, PSVO_TIME_INTERSECT, 1);
-    ENG_CALL(read_stats(e, st, stats));
-    timer_collect(e);  // the previous step's events completed before this read-back
-    const int P = e->host_stats[PSVO_STAT_P], r_hit = e->host_stats[PSVO_STAT_R_HIT];
-    const int max_steps = e->host_stats[PSVO_STAT_MAX_CEIL] + P;
-    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "map_step: octree deeper than the DFS stack");
-    if (r_hit == 0) return set_error(PSVO_E_INVALID, "map_step: no ray hits the octree (render_helpers.py:388)");
-    // ---- sampling
-    ENG_BUF(int, s_idx, kSIdx, (size_t)r_hit * max_steps * sizeof(int));
-    ENG_BUF(float, s_depth, kSDepth, (size_t)r_hit * max_steps * sizeof(float));
-    ENG_BUF(float, s_dist, kSDist, (size_t)r_hit * max_steps * sizeof(float));
-    ENG_BUF(int, ray_ns, kRayNs, (size_t)r_hit * sizeof(int));
-    ENG_BUF(int, offsets, kOffsets, (size_t)(r_hit + 1) * sizeof(int));
+    // ---- sampling, without a read-back: the sampler reads P, R_hit and
+    // max ⌈steps⌉ from `stats` on the device; its buffers are [R, cap] with
+    // cap ≥ max_steps = max ⌈Σ(t_out − t_in)/step⌉ + P, bounded by 50 leaf
+    // intervals of at most a voxel diagonal (rows are written only up to
+    // max_steps; an overflow is flagged and reported below)
+    const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
+                          kMaxHits + 1;
+    ENG_BUF(int, s_idx, kSIdx, (size_t)R * max_steps * sizeof(int));
+    ENG_BUF(float, s_depth, kSDepth, (size_t)R * max_steps * sizeof(float));
+    ENG_BUF(float, s_dist, kSDist, (size_t)R * max_steps * sizeof(float));
+    ENG_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
+    ENG_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
     mark(e, st, PSVO_TIME_SAMPLE, 0);
-    ENG_CALL(psvo_sample_rays(stream, r_hit, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
+    ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
                               nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
     mark(e, st, PSVO_TIME_SAMPLE, 1);
     ENG_CALL(read_stats(e, st, stats));
+    timer_collect(e);  // the previous step's events completed before this read-back
+    const int r_hit = e->host_stats[PSVO_STAT_R_HIT];
+    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "map_step: octree deeper than the DFS stack");
+    if (r_hit == 0) return set_error(PSVO_E_INVALID, "map_step: no ray hits the octree (render_helpers.py:388)");
     const int s_max = e->host_stats[PSVO_STAT_S_MAX];
     const int64_t M = e->host_stats[PSVO_STAT_M];
     if (e->host_stats[7] & 2) return set_error(PSVO_E_OVERFLOW, "map_step: sampler exceeded max_steps");
@@ -309,14 +342,20 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
                           G[8], G[9], 0, n_split, mlp_ws));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
-    if (hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
+    if (!(e->grads_clean && e->clean_buf == grad_emb) &&
+        hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    e->grads_clean = false;
+    e->clean_buf = grad_emb;
     mark(e, st, PSVO_TIME_INTERP_BWD, 0);
     ENG_CALL(psvo_interp_bwd(stream, r_hit, 16, d->voxel_size, offsets, rank_ray, leaf, tt, rays_o, rays_d,
                              d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
     mark(e, st, PSVO_TIME_INTERP_BWD, 1);
     e->tm.pending = e->tm.on;
     // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
-    if (!(flags & PSVO_STEP_NO_ADAM)) ENG_CALL(map_adam(st, d, grads, adam_step));
+    if (!(flags & PSVO_STEP_NO_ADAM)) {
+        ENG_CALL(map_adam(st, d, grads, adam_step));
+        e->grads_clean = true;
+    }
     return PSVO_OK;
 }

@@ -25,7 +25,7 @@ namespace psvo {
 namespace {
 
 constexpr int kAdamMaxTensors = 24;
-constexpr int kAdamSlice = 4096;  // elements per block
+constexpr int kAdamSlice = 1024;  // elements per block (4 per thread)
 
 struct AdamTable {
     float *p[kAdamMaxTensors];
@@ -33,18 +33,22 @@ struct AdamTable {
     float *m[kAdamMaxTensors];
     float *v[kAdamMaxTensors];
     int64_t n[kAdamMaxTensors];
+    float lr_bc1[kAdamMaxTensors];  // lr / (1 - β1^t) per tensor
+    int zero_grad[kAdamMaxTensors]; // write 0 into the gradient after use
     int block_begin[kAdamMaxTensors + 1];
     int count;
 };
 
-__global__ __launch_bounds__(256) void k_adam(AdamTable tab, float lr_bc1, float bc2_sqrt, float beta1,
-                                              float beta2, float omb1, float omb2, float eps, float wd) {
+__global__ __launch_bounds__(256) void k_adam(AdamTable tab, float bc2_sqrt, float beta1, float beta2, float omb1,
+                                              float omb2, float eps, float wd) {
     int ti = 0;
     while (ti + 1 < tab.count && (int)blockIdx.x >= tab.block_begin[ti + 1]) ++ti;
     const int64_t base = (int64_t)(blockIdx.x - tab.block_begin[ti]) * kAdamSlice;
     const int64_t n = tab.n[ti];
     float *__restrict__ p = tab.p[ti];
-    const float *__restrict__ g = tab.g[ti];
+    float *__restrict__ g = const_cast<float *>(tab.g[ti]);
+    const float lr_bc1 = tab.lr_bc1[ti];
+    const bool zg = tab.zero_grad[ti] != 0;
     float *__restrict__ m = tab.m[ti];
     float *__restrict__ v = tab.v[ti];
     for (int64_t i = base + threadIdx.x; i < base + kAdamSlice && i < n; i += 256) {
@@ -57,6 +61,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float lr_bc1, float
         p[i] = pi - lr_bc1 * mi / denom;
         m[i] = mi;
         v[i] = vi;
+        if (zg) g[i] = 0.0f;
     }
 }
 
@@ -65,14 +70,17 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float lr_bc1, float
 
 using namespace psvo;
 
-extern "C" int psvo_adam_step(void *stream, int n_tensors, float *const *params, const float *const *grads,
-                              float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, double lr,
-                              double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+// One launch over n_tensors tensors (chunks of kAdamMaxTensors); per-tensor
+// learning rate and optional gradient zeroing (the engine's accumulation
+// buffer is left zeroed for the next iteration's float atomics).
+int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads,
+                      float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, const double *lr,
+                      double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                      const int *zero_grad) {
     PSVO_REQUIRE(n_tensors >= 0 && step >= 1, "adam_step: bad arguments (n_tensors=%d step=%lld)", n_tensors,
                  (long long)step);
     const double bc1 = 1.0 - std::pow(beta1, (double)step);
     const double bc2 = 1.0 - std::pow(beta2, (double)step);
-    const float lr_bc1 = (float)(lr / bc1);
     const float bc2_sqrt = (float)std::sqrt(bc2);
     int t = 0;
     while (t < n_tensors) {
@@ -89,16 +97,27 @@ extern "C" int psvo_adam_step(void *stream, int n_tensors, float *const *params,
             tab.m[k] = exp_avg[t];
             tab.v[k] = exp_avg_sq[t];
             tab.n[k] = numel[t];
+            tab.lr_bc1[k] = (float)(lr[t] / bc1);
+            tab.zero_grad[k] = zero_grad ? zero_grad[t] : 0;
             tab.block_begin[k] = blocks;
             blocks += (int)div_up(numel[t], kAdamSlice);
         }
         tab.block_begin[tab.count] = blocks;
         if (blocks == 0) continue;
-        hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, as_stream(stream), tab, lr_bc1, bc2_sqrt,
-                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
-                           (float)weight_decay);
+        hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, st, tab, bc2_sqrt, (float)beta1, (float)beta2,
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
         const int rc = check_launch("adam_step");
         if (rc) return rc;
     }
     return PSVO_OK;
+}
+
+extern "C" int psvo_adam_step(void *stream, int n_tensors, float *const *params, const float *const *grads,
+                              float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, double lr,
+                              double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+    PSVO_REQUIRE(n_tensors >= 0 && n_tensors <= 4096, "adam_step: bad n_tensors=%d", n_tensors);
+    double lrs[4096];
+    for (int i = 0; i < n_tensors; ++i) lrs[i] = lr;
+    return adam_launch(as_stream(stream), n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lrs, beta1, beta2,
+                       eps, weight_decay, step, nullptr);
 }

@@ -872,7 +872,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
         },
         lane, W);
     const int s_written = s_end < cap ? s_end : cap;
-    for (int s = s_written + lane; s < max_steps_cap; s += kWave) {
+    for (int s = s_written + lane; s < cap; s += kWave) {  // up to max_steps: readers stop at S_max <= max_steps
         oi[s] = -1;
         od[s] = kMaxDepthFill;
         os[s] = 0.0f;

@@ -48,7 +48,7 @@ _SIGNATURES = {
     "psvo_engine_set_timing": (_i32, [_vp, _i32]),
     "psvo_engine_timing": (_i32, [_vp, _vp]),
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
-    "psvo_map_adam": (_i32, [_vp, _vp, _i64]),
+    "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
     "psvo_map_grad_floats": (_i64, [_i64]),
     "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
     "psvo_octree_free": (None, [_vp]),

@@ -102,7 +102,7 @@ class MappingEngine:
 
     def adam(self):
         """Both Adam steps from self.grad_flat (after a step(apply_adam=False))."""
-        L.call("psvo_map_adam", L.stream_of(self.emb.device), ctypes.addressof(self.desc), self.step_no)
+        L.call("psvo_map_adam", self.handle, L.stream_of(self.emb.device), ctypes.addressof(self.desc), self.step_no)
 
     def set_timing(self, on):
         """HIP events around the decoder fwd / bwd and interp fwd / bwd launches."""
