@@ -85,8 +85,10 @@ def scannet0000(offset=10.0) -> Scene:
     return s
 
 
-def multiroom(n_x=6, n_y=6, offset=10.0) -> Scene:
-    """ARKit-style large scene: a grid of furnished rooms in a depth-10 tree."""
+def multiroom(n_x=15, n_y=15, offset=10.0) -> Scene:
+    """ARKit-style large scene (config E): a 15 x 15 grid of furnished rooms in
+    a depth-10 tree (grid 1024) — > 1M SURFACE leaves, ~2.7M nodes, a ~170 MB
+    embedding table."""
     boxes = []
     rng = np.random.default_rng(7)
     for i in range(n_x):
@@ -117,11 +119,13 @@ def _face_points(box: Box, spacing: float):
     return np.concatenate(pts, 0)
 
 
-def surface_voxels(scene: Scene, spacing=0.05, seed=0) -> np.ndarray:
+def surface_voxels(scene: Scene, spacing=None, seed=0) -> np.ndarray:
     """Integer voxel coords floor(p / voxel) of surface samples (mapping.py:264),
     de-duplicated in first-seen order (a mapping run inserts per frame; the
     octree's node numbering follows insertion order)."""
     rng = np.random.default_rng(seed)
+    if spacing is None:  # 5 cm faces; half a voxel for the big multi-room scene
+        spacing = 0.05 if scene.grid_dim <= 256 else scene.voxel_size * 0.5
     pts = np.concatenate([_face_points(b, spacing) for b in scene.boxes], 0)
     if scene.depth_noise > 0:
         pts = pts + rng.normal(0.0, scene.depth_noise, pts.shape)

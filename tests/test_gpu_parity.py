@@ -305,3 +305,62 @@ def test_fused_sampler_matches_oracle_full_size(step):
     np.testing.assert_array_equal(g_dep[:, :n].numpy(), o_dep.numpy())
     np.testing.assert_array_equal(g_dis[:, :n].numpy(), o_dis.numpy())
     assert bool((g_idx[:, n:] == -1).all())
+
+
+def test_config_e_multiroom_properties():
+    """SURVEY §8 config E (multi-room scene, 1024³ grid, >1M surface leaves,
+    depth-10 tree): hit sets contain every brute-force SURFACE leaf (rays with
+    < 50 hits), indices are deterministic, one engine iteration over the
+    2.7M-row embedding table gives a finite loss and touches only the rows the
+    rays reach."""
+    from psvo import synthetic as syn
+    from psvo.octree import Octree, map_states
+    from psvo.decoder import Decoder
+    from psvo.engine import MappingEngine
+    from psvo.render_helpers import query_samples
+    from psvo.voxel_helpers import _intersect_sorted
+    w = syn.make_workload("multiroom", 2, 512, seed=3)
+    tree = Octree()
+    tree.init(w.scene.grid_dim, 16, w.scene.voxel_size, 8)
+    tree.insert(w.voxels)
+    n_nodes = tree.count_nodes()
+    assert n_nodes > 2_000_000
+    emb = torch.randn(n_nodes, 16, device=DEV) * 0.1
+    ms = map_states(tree, emb, w.scene.voxel_size, device=DEV)
+    assert int((ms["voxel_structure"][:, 8] == 1).sum()) > 1_000_000
+    ro, rd = w.rays_o.to(DEV), w.rays_d.to(DEV)
+    vs = w.scene.voxel_size
+    s1 = query_samples(ro, rd, ms, 0.008, vs, 10.0, seed=7)
+    s2 = query_samples(ro, rd, ms, 0.008, vs, 10.0, seed=7)
+    assert torch.equal(s1.s_idx, s2.s_idx) and torch.equal(s1.z_vals, s2.z_vals)
+    q = _intersect_sorted(ro, rd, ms["voxel_center_xyz"], ms["voxel_structure"], vs, 10.0, 0.008)
+    nv, idx = q["ray_nv"].cpu(), q["hit_idx"].cpu()
+    leaves = torch.nonzero(ms["voxel_structure"][:, 8] == 1).squeeze(1)
+    c = ms["voxel_center_xyz"][leaves].double().cpu()
+    checked = 0
+    for r in range(0, ro.shape[1], 61):
+        if nv[r] >= 50:
+            continue
+        o64, d64 = ro[0, r].double().cpu(), rd[0, r].double().cpu()
+        inv = 1.0 / d64
+        t0 = ((c - vs / 2) - o64) * inv
+        t1 = ((c + vs / 2) - o64) * inv
+        tlo = torch.minimum(t0, t1).amax(-1).clamp(min=0)
+        thi = torch.maximum(t0, t1).amin(-1)
+        exp = set(int(leaves[j]) for j in torch.nonzero(tlo < thi - 1e-5).squeeze(1).tolist())
+        mine = set(int(v) for v in idx[r, : nv[r]].tolist())
+        assert exp <= mine, (r, exp - mine)
+        checked += 1
+    assert checked > 0
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    emb0 = emb.clone()
+    eng = MappingEngine(ms, dec, vs, 0.008, truncation=0.1, max_distance=10.0, max_depth=10.0)
+    loss = float(eng.step(ro, rd, w.rgb.to(DEV), w.depth.to(DEV), seed=5))
+    assert loss == loss and abs(loss) < 1e30
+    touched = (emb - emb0).abs().amax(-1) > 0
+    reached = torch.zeros(n_nodes, dtype=torch.bool, device=DEV)
+    hit = idx[torch.arange(idx.shape[1])[None, :] < nv[:, None]].unique().long().to(DEV)
+    reached[ms["voxel_vertex_idx"][hit].reshape(-1).long()] = True
+    assert int(touched.sum()) > 0
+    assert not bool((touched & ~reached).any())
+    eng.close()
