@@ -79,6 +79,7 @@ enum {
     PSVO_STAT_S_MAX = 3,     /* max valid samples per ray (voxel_helpers.py:359) */
     PSVO_STAT_M = 4,         /* total valid samples */
     PSVO_STAT_VISITS = 5,    /* AABB tests performed (traffic accounting) */
+    PSVO_STAT_SPILLS = 6,    /* rays that fell back to the serial DFS (diagnostic) */
     PSVO_STAT_WORDS = 8
 };
 

@@ -184,25 +184,32 @@ __device__ __forceinline__ int wave_sum(int v) {
 // fused ray_intersect_vox: octree query → stable sort by t_in → max_distance
 // trim, plus per-ray Σ(t_out - t_in) for the sampler's probs / steps.
 //
-// One wave per ray, LEVEL-SYNCHRONOUS instead of depth-first: each pass
-// tests the children of 8 frontier nodes on the 64 lanes (lane = node slot ×
-// child slot), so a ray needs one dependent load pair per level instead of
-// one per AABB test, and all lanes of a wave follow one ray (no divergence
-// between rays).  The reference's depth-first emission order (children
-// popped 7→0, intersect_gpu.cu:191-270) is the lexicographic order of the
-// path keys Σ_d (7 − u_d)·8^(15−d); the first n_max = 50 leaves in that
-// order are the 50 smallest keys, so once 50 leaves are known every leaf or
-// subtree whose key exceeds the 50th is pruned (the DFS would never have
-// reached it).  The stable sort by t_in breaks ties by key = DFS order.  If
-// a level's frontier or leaf list would overflow LDS the wave falls back to
-// the serial DFS on lane 0 (same results).
-constexpr int kBfsF = 128;   // frontier capacity per level
-constexpr int kBfsL = 128;   // leaf list capacity (≤ 50 after pruning + one level)
+// One wave per ray, KEY-ORDERED CHUNKED traversal instead of one-node-at-a-
+// time DFS.  Every node has a path key Σ_d (7 − u_d)·8^(16−d); the
+// reference's depth-first emission order (children popped 7→0,
+// intersect_gpu.cu:191-270) is ascending key order, and the first n_max = 50
+// leaves it emits are the 50 smallest leaf keys.  The wave keeps an LDS stack
+// of untested candidates sorted by key (smallest on top) and each round pops
+// up to 64 of them — one per lane — and tests them together: one dependent
+// memory round trip per round (the candidate's centre and its whole
+// structure row, children included, are independent loads), instead of one
+// per AABB test.  Hit internal nodes push their existing children (keys
+// ascending toward the top, so every child precedes every remaining
+// candidate: preorder keys).  Once 50 leaves are known the 50th key bounds
+// the search and every candidate beyond it is dropped (the DFS would never
+// have reached it).  The stable sort by t_in breaks ties by key = DFS order.
+// A round whose children would overflow the stack re-queues its tail lanes;
+// a ray that cannot progress at all, or a tree deeper than the reference's
+// 16-level stack, falls back to the serial DFS on lane 0 (same results,
+// counted in stats[PSVO_STAT_SPILLS]).
+constexpr int kStk = 512;    // candidate stack entries per ray
+constexpr int kBfsL = 128;   // leaf list capacity (≤ 49 + 64 between compactions)
 constexpr int kIsWaves = 4;  // waves (rays) per block
 
-struct BfsLds {
-    uint64_t fkey[2][kBfsF];
-    int fnode[2][kBfsF];
+struct KeyLds {
+    uint64_t skey[kStk];
+    int snode[kStk];
+    uint8_t sdep[kStk];
     uint64_t lkey[kBfsL];
     int lidx[kBfsL];
     float lt0[kBfsL], lt1[kBfsL];
@@ -214,8 +221,17 @@ __device__ __forceinline__ uint64_t key_digit(int u, int depth) {
     return (uint64_t)(7 - u) << (3 * (kLevels - depth));
 }
 
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int s = 1; s < kWave; s <<= 1) {
+        const int t = __shfl_up(v, s, kWave);
+        if (lane >= s) v += t;
+    }
+    return v;
+}
+
 // 50th smallest key of the leaf list (keys unique): the threshold of the prune
-__device__ uint64_t kth_key(const BfsLds &S, int n, int kth, int lane) {
+__device__ uint64_t kth_key(const KeyLds &S, int n, int kth, int lane) {
     uint64_t found = ~0ull;
     for (int i = lane; i < n; i += kWave) {
         const uint64_t ki = S.lkey[i];
@@ -239,103 +255,115 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           int *__restrict__ hit_idx, float *__restrict__ hit_t0,
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
                                                           float *__restrict__ ray_dsum, int *__restrict__ stats) {
-    __shared__ BfsLds lds_all[kIsWaves];
-    BfsLds &S = lds_all[threadIdx.x / kWave];
+    __shared__ KeyLds lds_all[kIsWaves];
+    KeyLds &S = lds_all[threadIdx.x / kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t r = (int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave;
     const float half = voxel_size * 0.5f;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int visits = 0;
-    bool overflow_stack = false;
+    bool overflow_stack = false, spill = false;
     if (r < n_rays) {
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
         const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
         float inv[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, d[a]);
-        int nl = 0, nf = 0, cur = 0;
-        bool spill = false;
-        {  // root (every lane computes the same test)
-            float a = 0.f, b = 0.f;
-            const int side = structure[8];
-            const bool hit = ray_aabb(o, inv, centres[0], centres[1], centres[2], half * (float)side, a, b);
-            visits += lane == 0;
-            if (hit) {
-                if (side == 1) {
-                    if (lane == 0) {
-                        S.lkey[0] = 0;
-                        S.lidx[0] = 0;
-                        S.lt0[0] = a;
-                        S.lt1[0] = b;
-                    }
-                    nl = 1;
-                } else {
-                    if (lane == 0) {
-                        S.fkey[0][0] = 0;
-                        S.fnode[0][0] = 0;
-                    }
-                    nf = 1;
-                }
-            }
-        }
-        wave_lds_sync();
+        int nl = 0, sp = 1;
         bool bounded = false;
         uint64_t kbound = ~0ull;
-        for (int depth = 0; nf > 0 && !spill; ++depth) {
-            if (depth + 1 > kLevels) {
-                overflow_stack = true;
+        if (lane == 0) {  // the root is the first candidate
+            S.skey[0] = 0;
+            S.snode[0] = 0;
+            S.sdep[0] = 0;
+        }
+        wave_lds_sync();
+        while (sp > 0) {  // wave-uniform trip count
+            const int n = min(sp, kWave);
+            uint64_t key = 0;
+            int node = 0, dep = 0;
+            if (lane < n) {
+                const int e = sp - 1 - lane;
+                key = S.skey[e];
+                node = S.snode[e];
+                dep = S.sdep[e];
+            }
+            // popped keys ascend with the lane: the live lanes are a prefix
+            const bool live = lane < n && !(bounded && key > kbound);
+            const int n_eff = __popcll(__ballot(live));
+            int row[8];
+            int side = 0;
+            float a = 0.f, b = 0.f;
+            bool hit = false;
+            if (live) {
+                const int *rw = structure + (int64_t)node * 9;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) row[u] = rw[u];
+                side = rw[8];
+                const float *pc = centres + (int64_t)node * 3;
+                hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+            }
+            const bool leaf = hit && side == 1;
+            const bool inner = hit && side != 1;
+            if (__ballot(inner && dep >= kLevels)) {  // deeper than the reference's stack
+                spill = true;
                 break;
             }
-            int nn = 0;  // next frontier size
-            for (int base = 0; base < nf; base += kWave / 8) {
-                const int fi = base + (lane >> 3), u = lane & 7;
-                bool hit = false, leaf = false;
-                int k = -1;
-                float a = 0.f, b = 0.f;
-                uint64_t ck = 0;
-                if (fi < nf) {
-                    const int node = S.fnode[cur][fi];
-                    ck = S.fkey[cur][fi] | key_digit(u, depth + 1);
-                    k = structure[(int64_t)node * 9 + u];
-                    if (k > -1) {
-                        const int side = structure[(int64_t)k * 9 + 8];
-                        const float *pc = centres + (int64_t)k * 3;
-                        hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
-                        leaf = side == 1;
-                        ++visits;
-                        if (bounded && ck > kbound) hit = false;  // beyond the first 50 in DFS order
+            int c = 0;
+            if (inner) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c += row[u] > -1;
+            }
+            const int incl = wave_incl_scan(c, lane);
+            // a prune drops everything below the popped chunk (all keys > kbound)
+            const int floor_ = (n_eff < n) ? 0 : sp - n;
+            const bool ok = !live || floor_ + (n_eff - 1 - lane) + incl <= kStk;
+            const uint64_t bad = __ballot(!ok);
+            const int J = bad ? (int)__ffsll((unsigned long long)bad) - 1 : n_eff;  // accepted lanes [0, J)
+            if (J == 0 && n_eff > 0) {
+                spill = true;
+                break;
+            }
+            const int T = J > 0 ? __shfl(incl, J - 1, kWave) : 0;
+            const bool acc = lane < J;
+            wave_lds_sync();  // every lane has read its candidate before the stack is rewritten
+            if (live && !acc) {  // re-queued tail keeps its order on top of the floor
+                const int pos = floor_ + (n_eff - 1 - lane);
+                S.skey[pos] = key;
+                S.snode[pos] = node;
+                S.sdep[pos] = (uint8_t)dep;
+            }
+            const int base = floor_ + (n_eff - J);
+            if (acc && inner) {
+                int g = incl - c;  // rank of this lane's first (smallest-key) child
+                const int cd = dep + 1;
+#pragma unroll
+                for (int u = 7; u >= 0; --u) {
+                    if (row[u] > -1) {
+                        const int pos = base + (T - 1 - g);
+                        S.skey[pos] = key | key_digit(u, cd);
+                        S.snode[pos] = row[u];
+                        S.sdep[pos] = (uint8_t)cd;
+                        ++g;
                     }
                 }
-                const uint64_t lb = __ballot(hit && leaf), ib = __ballot(hit && !leaf);
-                const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-                const int nlb = __popcll(lb), nib = __popcll(ib);
-                if (nl + nlb > kBfsL || nn + nib > kBfsF) {
-                    spill = true;
-                    break;
-                }
-                if (hit && leaf) {
-                    const int pos = nl + __popcll(lb & below);
-                    S.lkey[pos] = ck;
-                    S.lidx[pos] = k;
-                    S.lt0[pos] = a;
-                    S.lt1[pos] = b;
-                }
-                if (hit && !leaf) {
-                    const int pos = nn + __popcll(ib & below);
-                    S.fkey[cur ^ 1][pos] = ck;
-                    S.fnode[cur ^ 1][pos] = k;
-                }
-                nl += nlb;
-                nn += nib;
             }
+            const uint64_t lb = __ballot(acc && leaf);
+            if (acc && leaf) {
+                const int pos = nl + __popcll(lb & below);
+                S.lkey[pos] = key;
+                S.lidx[pos] = node;
+                S.lt0[pos] = a;
+                S.lt1[pos] = b;
+            }
+            visits += acc ? 1 : 0;
+            nl += __popcll(lb);
+            sp = base + T;
             wave_lds_sync();
-            if (spill) break;
-            if (nl >= kMaxHits) {  // keep the 50 smallest keys; prune the next frontier
+            if (nl >= kMaxHits) {  // keep the 50 smallest keys; later candidates beyond them are dropped
                 kbound = kth_key(S, nl, kMaxHits - 1, lane);
                 bounded = true;
                 wave_lds_sync();
-                // compact leaves (order irrelevant: sorted by (t_in, key) below)
-                const uint64_t keep_all = 0;
-                (void)keep_all;
                 int w = 0;
                 for (int i0 = 0; i0 < nl; i0 += kWave) {
                     const int i = i0 + lane;
@@ -349,7 +377,6 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                         tb = S.lt1[i];
                     }
                     const uint64_t kb = __ballot(keep);
-                    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
                     wave_lds_sync();
                     if (keep) {
                         const int pos = w + __popcll(kb & below);
@@ -362,32 +389,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     wave_lds_sync();
                 }
                 nl = w;
-                // prune the next frontier by the same bound
-                int wn = 0;
-                for (int i0 = 0; i0 < nn; i0 += kWave) {
-                    const int i = i0 + lane;
-                    uint64_t kk = 0;
-                    int nd = 0;
-                    if (i < nn) {
-                        kk = S.fkey[cur ^ 1][i];
-                        nd = S.fnode[cur ^ 1][i];
-                    }
-                    const bool keep = i < nn && kk <= kbound;
-                    const uint64_t kb = __ballot(keep);
-                    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-                    wave_lds_sync();
-                    if (keep) {
-                        const int pos = wn + __popcll(kb & below);
-                        S.fkey[cur ^ 1][pos] = kk;
-                        S.fnode[cur ^ 1][pos] = nd;
-                    }
-                    wn += __popcll(kb);
-                    wave_lds_sync();
-                }
-                nn = wn;
             }
-            cur ^= 1;
-            nf = nn;
         }
         if (spill) {  // serial DFS on lane 0 (reference order by construction; key = emission index)
             int cnt = 0;
@@ -439,21 +441,24 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     // visits / overflow: one atomic per block (per-ray P, R_hit and max ceil
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
     // at the memory side)
-    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves];
+    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
         blk_vis[threadIdx.x / kWave] = wvis;
         blk_ov[threadIdx.x / kWave] = wov;
+        blk_sp[threadIdx.x / kWave] = spill ? 1 : 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int v = 0, ov = 0;
+        int v = 0, ov = 0, sps = 0;
         for (int w = 0; w < kIsWaves; ++w) {
             v += blk_vis[w];
             ov |= blk_ov[w];
+            sps += blk_sp[w];
         }
         atomicAdd(stats + PSVO_STAT_VISITS, v);
+        if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
 }
