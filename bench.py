@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--autograd", action="store_true",
                     help="headline number from the drop-in autograd path instead of the native engine")
     ap.add_argument("--exact-global-loss", action="store_true",
-                    help="N>1: loss of the union of all ranks' rays (all-reduced criterion sums)")
+                    help="N>1: sharded == single-GPU on the global batch (global sampler layout, all-reduced "
+                         "criterion sums; runs the autograd path)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -200,12 +201,15 @@ def main():
     _lib.KERNEL_TIMER = timer
     stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
 
-    from psvo.dist import GlobalLossSums, GradBucket
+    from psvo.dist import GlobalBatch, GlobalLossSums, GradBucket
     from psvo.engine import MappingEngine
     # one flat RCCL all-reduce of all gradients per step; exact mode forms the
     # loss of the union of the ranks' rays (global normalisers) and sums
     bucket = GradBucket(params, op="sum" if args.exact_global_loss else "mean")
     reducer = GlobalLossSums() if (args.exact_global_loss and world > 1) else None
+    gbatch = GlobalBatch() if (args.exact_global_loss and world > 1) else None
+    if gbatch is not None:
+        args.autograd = True  # the engine samples per rank; exactness runs the drop-in path
     engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
                            criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
 
@@ -218,7 +222,8 @@ def main():
     def step_autograd(i, record=False):
         """The drop-in path: render_rays + Criterion + backward + Adam steps."""
         ro, rd, rgb, depth = batches[i % len(batches)]
-        out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True)
+        out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True,
+                             seed=(7919 * i + 1) if gbatch is not None else None, batch=gbatch)
         loss, _ = criterion(out, (rgb, depth), reduce_sums=reducer)
         embed_optim.zero_grad()  # set_to_none, as optim.zero_grad() in render_helpers.py:668
         model_optim.zero_grad()

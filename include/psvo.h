@@ -109,6 +109,23 @@ int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const i
                      const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                      int *ray_ns, int *offsets);
 
+/* psvo_sample_rays for the logical hit rows [row_begin, row_begin + n_rows)
+ * (n_rows < 0: through R_hit), outputs at row - row_begin.  rank_ray,
+ * hit_*, ray_dsum and stats (P / R_hit / max ceil) describe the GLOBAL ray
+ * batch (all ranks' rays concatenated): a data-parallel rank samples its own
+ * rays inside the single-GPU [200, K', P] layout — the sampler quirks of
+ * voxel_helpers.py:300-317 / sample_gpu.cu:224-237 and the noise depend on
+ * the global slot.  S_max / M of the range go to stats. */
+int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n_rows, int64_t r_hit_cap, int max_steps_cap,
+                           const int *rank_ray, const int *hit_idx, const float *hit_t0, const float *hit_t1,
+                           const float *ray_dsum, float step_size, const float *noise, uint64_t seed, int *stats,
+                           int *s_idx, float *s_depth, float *s_dist, int *ray_ns, int *offsets);
+
+/* P, R_hit and max ceil(Σ(t_out - t_in) / step) of n_rays intersected rays
+ * into stats (the reduction psvo_ray_intersect_sorted ends with). */
+int psvo_ray_stats(void *stream, int64_t n_rays, const int *ray_nv, const float *ray_dsum, float step_size,
+                   int *stats);
+
 /* Exclusive scan of per-ray sample counts → sample offsets. */
 int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets);
 

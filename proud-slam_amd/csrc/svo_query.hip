@@ -823,7 +823,13 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
     return s;
 }
 
-__global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max_steps_cap,
+// Rows [row_begin, row_begin + n_rows) of the logical hit-ray order (n_rows <
+// 0: through R_hit); ray i's outputs go to row i - row_begin.  A data-
+// parallel rank samples its own rays inside the GLOBAL [200, K', P] layout
+// this way: rank_ray / hit_* / dsum / stats then describe
+// the all-gathered batch, and the noise key is the global logical index.
+__global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                      int max_steps_cap,
                                                       const int *__restrict__ rank_ray,
                                                       const int *__restrict__ hit_idx,
                                                       const float *__restrict__ hit_t0,
@@ -837,11 +843,13 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
     const int lane = threadIdx.x & (kWave - 1);
-    const int i = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    const int il = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    const int i = (int)row_begin + il;                                        // logical row
     __shared__ WaveBins bins_all[4];
     WaveBins &W = bins_all[threadIdx.x / kWave];
-    if (i >= r_hit || i >= r_hit_cap || P <= 0) return;
-    if (max_steps > max_steps_cap && lane == 0 && i == 0) atomicOr(stats + 7, 2);
+    const int64_t n_own = n_rows < 0 ? (int64_t)r_hit - row_begin : n_rows;
+    if (i >= r_hit || il >= n_own || il >= r_hit_cap || P <= 0) return;
+    if (max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + 7, 2);
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
     const int b = i / kp;
     const int j = i - b * kp;
@@ -854,9 +862,9 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
                    (int64_t)orig * kMaxHits, dsum};
     const float steps_j = __fdiv_rn(dsum, step_size);
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
-    int *oi = s_idx + (int64_t)i * max_steps_cap;
-    float *od = s_depth + (int64_t)i * max_steps_cap;
-    float *os = s_dist + (int64_t)i * max_steps_cap;
+    int *oi = s_idx + (int64_t)il * max_steps_cap;
+    float *od = s_depth + (int64_t)il * max_steps_cap;
+    float *os = s_dist + (int64_t)il * max_steps_cap;
     const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
     const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
     int count = 0;
@@ -883,15 +891,17 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t r_hit_cap, int max
         os[s] = 0.0f;
     }
     count = wave_sum(count);
-    if (lane == 0) ray_ns[i] = count;
+    if (lane == 0) ray_ns[il] = count;
 }
 
 // offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.
-__global__ __launch_bounds__(1024) void k_scan_samples(int64_t r_hit_cap, const int *__restrict__ ray_ns,
-                                                       int *__restrict__ offsets, int *__restrict__ stats) {
+__global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                       const int *__restrict__ ray_ns, int *__restrict__ offsets,
+                                                       int *__restrict__ stats) {
     __shared__ int total;
     __shared__ int smax[16];
-    const int64_t n = min((int64_t)stats[PSVO_STAT_R_HIT], r_hit_cap);
+    const int64_t n_own = n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
+    const int64_t n = max((int64_t)0, min(n_own, r_hit_cap));
     block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total);
     int mx = 0;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mx = max(mx, ray_ns[i]);
@@ -986,19 +996,39 @@ extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, in
     return check_launch("hit_rank");
 }
 
+extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                      int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                                      const float *hit_t0, const float *hit_t1, const float *ray_dsum,
+                                      float step_size, const float *noise, uint64_t seed, int *stats, int *s_idx,
+                                      float *s_depth, float *s_dist, int *ray_ns, int *offsets) {
+    PSVO_REQUIRE(r_hit_cap >= 0 && max_steps_cap > 0, "sample_rays: bad caps");
+    PSVO_REQUIRE(row_begin >= 0, "sample_rays: row_begin < 0");
+    PSVO_REQUIRE(offsets != nullptr && ray_ns != nullptr, "sample_rays: ray_ns / offsets required");
+    if (r_hit_cap == 0) return PSVO_OK;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
+                       max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
+                       s_idx, s_depth, s_dist, ray_ns);
+    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
+                       stats);
+    return check_launch("sample_rays");
+}
+
 extern "C" int psvo_sample_rays(void *stream, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray,
                                 const int *hit_idx, const float *hit_t0, const float *hit_t1, const float *ray_dsum,
                                 float step_size, const float *noise, uint64_t seed, int *stats, int *s_idx,
                                 float *s_depth, float *s_dist, int *ray_ns, int *offsets) {
-    PSVO_REQUIRE(r_hit_cap >= 0 && max_steps_cap > 0, "sample_rays: bad caps");
-    PSVO_REQUIRE(offsets != nullptr && ray_ns != nullptr, "sample_rays: ray_ns / offsets required");
-    if (r_hit_cap == 0) return PSVO_OK;
-    hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, r_hit_cap, max_steps_cap,
-                       rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
-                       s_dist, ray_ns);
-    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, r_hit_cap, ray_ns, offsets, stats);
-    return check_launch("sample_rays");
+    return psvo_sample_rays_range(stream, 0, -1, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
+                                  ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets);
+}
+
+extern "C" int psvo_ray_stats(void *stream, int64_t n_rays, const int *ray_nv, const float *ray_dsum,
+                              float step_size, int *stats) {
+    PSVO_REQUIRE(n_rays >= 0 && step_size > 0.0f, "ray_stats: bad arguments");
+    if (n_rays == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_dsum, step_size,
+                       stats);
+    return check_launch("ray_stats");
 }
 
 extern "C" int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets) {

@@ -28,6 +28,9 @@ _SIGNATURES = {
     "psvo_hit_rank": (_i32, [_vp, _i64, _vp, _vp, _vp]),
     "psvo_sample_rays": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _u64, _vp, _vp, _vp, _vp,
                                 _vp, _vp]),
+    "psvo_sample_rays_range": (_i32, [_vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _u64, _vp,
+                                      _vp, _vp, _vp, _vp, _vp]),
+    "psvo_ray_stats": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp]),
     "psvo_scan_counts": (_i32, [_vp, _i64, _vp, _vp]),
     "psvo_sample_points": (_i32, [_vp, _i64, _i32, _i32] + [_vp] * 9),
     "psvo_interp_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 9),

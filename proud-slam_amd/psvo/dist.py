@@ -80,8 +80,7 @@ class GlobalLossSums:
     def global_shape(self, r_hit, s_max):
         if world() == 1:
             return r_hit, s_max
-        dev = torch.device("cuda", torch.cuda.current_device()) if _backend(self.group) == "nccl" else "cpu"
-        t = torch.tensor([r_hit, -s_max], dtype=torch.int64, device=dev)
+        t = torch.tensor([r_hit, -s_max], dtype=torch.int64, device=_coll_device(self.group))
         r = t.clone()
         dist.all_reduce(r[:1], op=dist.ReduceOp.SUM, group=self.group)
         dist.all_reduce(r[1:], op=dist.ReduceOp.MIN, group=self.group)  # max via min of negatives
@@ -91,6 +90,60 @@ class GlobalLossSums:
     def __call__(self, sums):
         if world() > 1:
             dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
+
+
+class GlobalBatch:
+    """Exact data-parallel sampling: each rank samples
+    its own hit rays inside the [200, K', P] layout of the CONCATENATED batch
+    (ranks in order), with the global P / max_steps and noise keyed by the
+    global logical index, so its samples equal the matching rows of a
+    single-GPU run on the whole batch.  query_samples all-gathers the
+    per-ray hit lists (idx / t_in / t_out / count / Σ) through gather_cat —
+    P·12 B per ray, an exactness mode rather than the throughput path."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    @property
+    def world(self):
+        return world()
+
+    @property
+    def rank(self):
+        return dist.get_rank(self.group) if world() > 1 else 0
+
+    def sizes(self, n):
+        if world() == 1:
+            return [int(n)]
+        t = torch.tensor([int(n)], dtype=torch.int64, device=_coll_device(self.group))
+        out = [torch.zeros_like(t) for _ in range(world())]
+        dist.all_gather(out, t, group=self.group)
+        return [int(x) for x in out]
+
+    def max_int(self, v):
+        if world() == 1:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=_coll_device(self.group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t)
+
+    def gather_cat(self, t, sizes):
+        """Concatenate every rank's `t` (first dims `sizes`) in rank order."""
+        if world() == 1:
+            return t
+        dev = t.device
+        stage = "cpu" if _backend(self.group) == "gloo" else dev
+        n_max = max(sizes)
+        pad = torch.zeros((n_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=stage)
+        pad[: t.shape[0]].copy_(t)
+        out = [torch.empty_like(pad) for _ in range(world())]
+        dist.all_gather(out, pad, group=self.group)
+        return torch.cat([o[:k] for o, k in zip(out, sizes)], 0).to(dev)
+
+
+def _coll_device(group=None):
+    """Where small host-side collective operands live: the GPU for RCCL, the CPU for gloo."""
+    return torch.device("cuda", torch.cuda.current_device()) if _backend(group) == "nccl" else torch.device("cpu")
 
 
 def _backend(group=None):

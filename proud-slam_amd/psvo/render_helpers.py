@@ -149,21 +149,61 @@ class RaySamples:
                  "ray_of_sample", "offsets", "ray_ns", "rank_ray32", "s_idx", "s_depth", "s_dist", "visits", "max_steps")
 
 
+def _global_rows(q, R, step_size, batch):
+    """All-gather the per-ray hit lists and rank the global batch (dist.GlobalBatch):
+    returns the global rank_ray / ray_rank / stats / hit arrays, this rank's
+    first ray and first logical hit row, and the local hit count."""
+    dev = q["ray_nv"].device
+    sizes = batch.sizes(R)
+    ray_off = sum(sizes[: batch.rank])
+    g = {k: batch.gather_cat(q[k], sizes) for k in ("hit_idx", "hit_t0", "hit_t1", "ray_nv", "ray_dsum")}
+    rg = sum(sizes)
+    g["stats"] = torch.zeros_like(q["stats"])
+    g["ray_rank"] = torch.empty((rg,), dtype=torch.int32, device=dev)
+    g["rank_ray"] = torch.empty((rg,), dtype=torch.int32, device=dev)
+    stream = L.stream_of(dev)
+    L.call("psvo_ray_stats", stream, rg, L.ptr(g["ray_nv"]), L.ptr(g["ray_dsum"]), float(step_size), L.ptr(g["stats"]))
+    L.call("psvo_hit_rank", stream, rg, L.ptr(g["ray_nv"]), L.ptr(g["ray_rank"]), L.ptr(g["rank_ray"]))
+    counts = torch.stack([(g["ray_nv"][:ray_off] > 0).sum(), (q["ray_nv"] > 0).sum()]).to(torch.int32)
+    return g, ray_off, counts
+
+
 @torch.no_grad()
-def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise=None, seed=None):
-    """Intersection → sampling → compaction for rays_o/rays_d [1, R, 3]."""
+def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise=None, seed=None,
+                  batch=None):
+    """Intersection → sampling → compaction for rays_o/rays_d [1, R, 3].
+
+    batch (psvo.dist.GlobalBatch, optional): sample inside the layout of all
+    ranks' rays concatenated — the samples then equal the matching rows of a
+    single-GPU run on the whole batch with the same seed / noise."""
     dev = rays_o.device
     R = rays_o.numel() // 3
     ray_rank = torch.empty((R,), dtype=torch.int32, device=dev)
     rank_ray = torch.empty((R,), dtype=torch.int32, device=dev)
     stream = L.stream_of(dev)
+    exact = batch is not None and batch.world > 1
     with _timed("intersect"):
         q = _intersect_sorted(rays_o, rays_d, map_states["voxel_center_xyz"], map_states["voxel_structure"],
                               voxel_size, max_distance, step_size)
-        L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
-    st = q["stats"].cpu()  # sync 1
-    P, r_hit, max_ceil, visits = int(st[0]), int(st[1]), int(st[2]), int(st[5])
-    if int(st[7]) & 1:
+        if exact:
+            g, ray_off, counts = _global_rows(q, R, step_size, batch)
+        else:
+            L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
+    if exact:
+        st = torch.cat([g["stats"], counts, q["stats"][5:8]]).cpu()  # sync 1
+        P, rg_hit, max_ceil = int(st[0]), int(st[1]), int(st[2])
+        row_begin, r_hit, visits, flags = int(st[8]), int(st[9]), int(st[10]), int(st[12])
+        stats = g["stats"]
+        rank_ray_s, hit_src = g["rank_ray"], g
+        ray_rank = g["ray_rank"][ray_off:ray_off + R].clone()
+        ray_rank = torch.where(ray_rank >= 0, ray_rank - row_begin, ray_rank)
+        rank_ray[:r_hit] = g["rank_ray"][row_begin:row_begin + r_hit] - ray_off
+        assert rg_hit > 0, "no ray hits the octree (render_helpers.py:388)"
+    else:
+        st = q["stats"].cpu()  # sync 1
+        P, r_hit, max_ceil, visits, flags = int(st[0]), int(st[1]), int(st[2]), int(st[5]), int(st[7])
+        row_begin, rg_hit, stats, rank_ray_s, hit_src = 0, r_hit, q["stats"], rank_ray, q
+    if flags & 1:
         raise RuntimeError("octree deeper than the DFS level stack (15)")
     assert r_hit > 0, "no ray hits the octree (render_helpers.py:388)"
     max_steps = max_ceil + P
@@ -174,17 +214,22 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
     offsets = torch.empty((r_hit + 1,), dtype=torch.int32, device=dev)
     if noise is not None:
         noise = noise.to(device=dev, dtype=torch.float32).contiguous()
-        kp = (r_hit + 199) // 200
+        kp = (rg_hit + 199) // 200
         if tuple(noise.shape) != (200, kp, max_steps):
             raise ValueError(f"noise must be [200, {kp}, {max_steps}], got {tuple(noise.shape)}")
     if seed is None:
+        if exact:
+            raise ValueError("query_samples: a GlobalBatch needs the same explicit seed (or noise) on every rank")
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     with _timed("sample"):
-        L.call("psvo_sample_rays", stream, r_hit, max_steps, L.ptr(rank_ray), L.ptr(q["hit_idx"]), L.ptr(q["hit_t0"]),
-               L.ptr(q["hit_t1"]), L.ptr(q["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(q["stats"]),
-               L.ptr(s_idx), L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns), L.ptr(offsets))
-    st = q["stats"].cpu()  # sync 2
+        L.call("psvo_sample_rays_range", stream, row_begin, r_hit, r_hit, max_steps, L.ptr(rank_ray_s),
+               L.ptr(hit_src["hit_idx"]), L.ptr(hit_src["hit_t0"]), L.ptr(hit_src["hit_t1"]),
+               L.ptr(hit_src["ray_dsum"]), float(step_size), L.ptr(noise), seed, L.ptr(stats), L.ptr(s_idx),
+               L.ptr(s_depth), L.ptr(s_dist), L.ptr(ray_ns), L.ptr(offsets))
+    st = stats.cpu()  # sync 2
     s_max, m = int(st[3]), int(st[4])
+    if exact:  # pad to the global S_max: the composite's first sign change sees the sdf = 1 padding
+        s_max = batch.max_int(s_max)
     if int(st[7]) & 2:
         raise RuntimeError("sampler exceeded max_steps")
     leaf = torch.empty((m,), dtype=torch.int32, device=dev)
@@ -207,13 +252,13 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
 
 def render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxel_size, truncation, max_voxel_hit,
                 max_distance, chunk_size=10000, profiler=None, return_raw=False, noise=None, seed=None,
-                return_samples=False):
+                return_samples=False, batch=None):
     """render_helpers.py:351-556.  `noise` ([200, K', max_steps]) / `seed`
     select the sampler's uniform noise; by default it is drawn on the device
     from a seed taken from torch's CPU generator."""
     if profiler is not None:
         profiler.tick("ray_intersect")
-    smp = query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise, seed)
+    smp = query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distance, noise, seed, batch)
     if profiler is not None:
         profiler.tok("ray_intersect")
     ro = rays_o.reshape(-1, 3).float().contiguous()
