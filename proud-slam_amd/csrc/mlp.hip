@@ -130,25 +130,39 @@ __device__ __forceinline__ void init_bias(f32x16 (&acc)[kNB], const float *b, in
         for (int r = 0; r < 16; ++r) acc[ob][r] = b[32 * ob + phi(r, h)];
 }
 
-// ReLU in place; returns the (value > 0) mask, bit 16b + r.
+// ReLU in place; returns the (value > 0) mask, bit 16b + r.  No compares:
+// y = max(v, 0), and t = (−u) & ~u (u = bits of y) has its sign bit set
+// exactly for positive non-zero patterns (±0 clear), so no per-element
+// compare results pile up in SGPR pairs (the compare form spilled ~300 SGPRs).
 __device__ __forceinline__ uint64_t relu(f32x16 (&v)[kNB]) {
-    uint64_t m = 0;
+    uint32_t half[2] = {0u, 0u};
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const bool pos = v[b][r] > 0.0f;
-            v[b][r] = pos ? v[b][r] : 0.0f;
-            m |= (uint64_t)pos << (16 * b + r);
+            // pinned in program order: the scheduler would otherwise hoist all
+            // 64 element computations and keep them live at once
+            float y = v[b][r];
+            asm volatile("" : "+v"(y));
+            y = fmaxf(y, 0.0f);
+            v[b][r] = y;
+            const uint32_t u = __float_as_uint(y);
+            const uint32_t t = (0u - u) & ~u;
+            half[b >> 1] |= (t >> 31) << (16 * (b & 1) + r);
+            asm volatile("" : "+v"(half[b >> 1]));
         }
-    return m;
+    return (uint64_t)half[0] | ((uint64_t)half[1] << 32);
 }
 
 __device__ __forceinline__ void apply_mask(f32x16 (&v)[kNB], uint64_t m) {
+    const uint32_t half[2] = {(uint32_t)m, (uint32_t)(m >> 32)};
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[b][r] = ((m >> (16 * b + r)) & 1) ? v[b][r] : 0.0f;
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t keep = 0u - ((half[b >> 1] >> (16 * (b & 1) + r)) & 1u);
+            v[b][r] = __uint_as_float(__float_as_uint(v[b][r]) & keep);
+        }
 }
 
 // Σ_k w[k] · v[k][sample] over this lane's 64 features (other half via partner lane)
@@ -185,6 +199,7 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
 // feature rows × two 64-B runs.
 constexpr int kCh = 64;              // samples per CF chunk
 constexpr int kCfChunk = 128 * kCh;  // floats per CF chunk
+constexpr int64_t kMaxSamples = (int64_t)65535 * kCh;  // one CF matrix < 2 GiB (buffer offsets)
 
 __device__ __forceinline__ int cf_slot(int f, int s) {
     const int p = (s & 1) * 32 + (s >> 1);
@@ -203,6 +218,41 @@ __device__ __forceinline__ void store_cf(float *dst, int64_t tile, const f32x16 
         for (int r = 0; r < 16; ++r) base[cf_slot(32 * b + phi(r, hh), sc)] = v[b][r];
 }
 
+// The same stores as buffer stores whose addresses need no VALU: element
+// (b, r) of the tile lands at byte
+//   chunk + f·256 + 4·((((p>>2) ^ (f&15)) << 2) | (p&3)),  f = 32b + phi(r, h)
+// and f&15 = (r&3) + 8((r>>2)&1) + 4h, so with the 8 per-lane XOR offsets
+// voff[(r&3) + 4((r>>2)&1)] (chunk and 1024h folded in) the rest is
+// 8192b + 2048(r>>2) (an SGPR soffset) + 256(r&3) (the immediate offset).
+struct CfStore {
+    int voff[8];
+    bool ok;
+    __device__ CfStore(int64_t tile, int lane, int64_t n_tiles) {
+        ok = tile < n_tiles;
+        const int sc = (int)(tile & 1) * 32 + (lane & 31);
+        const int p = (sc & 1) * 32 + (sc >> 1);
+        const int hh = lane >> 5;
+        const int chunk = (int)((tile >> 1) * kCfChunk * 4);
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) {
+            const int x = (c8 & 3) + 8 * (c8 >> 2) + 4 * hh;
+            voff[c8] = chunk + 1024 * hh + 4 * ((((p >> 2) ^ x) << 2) | (p & 3));
+        }
+    }
+    __device__ __forceinline__ void store(const float *matrix, int64_t bytes, const f32x16 (&v)[kNB]) const {
+        if (!ok) return;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(matrix), 0, (int)bytes, 0x00020000);
+#pragma unroll
+        for (int b = 0; b < kNB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[b][r]), rs,
+                                                      voff[(r & 3) + 4 * ((r >> 2) & 1)] + 256 * (r & 3),
+                                                      8192 * b + 2048 * (r >> 2), 0);
+    }
+};
+
 // ---------------------------------------------------------------------------
 // Weight images: every layer's LDS operand image, laid out exactly as the
 // kernels read it, built once per weight update by k_mlp_prep (a gather,
@@ -211,7 +261,9 @@ __device__ __forceinline__ void store_cf(float *dst, int64_t tile, const f32x16 
 //   bwd: W4ᵀ (5 product blocks), W3ᵀ rows 1..128, W2ᵀ, W1ᵀ (1 block)
 constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF4 = kImgF3 + 16384,
               kImgB4 = kImgF4 + 18432, kImgB3 = kImgB4 + 20480, kImgB2 = kImgB3 + 16384, kImgB1 = kImgB2 + 16384,
-              kImgTotal = kImgB1 + 4096;  // 110,592 floats
+              kImgVec = kImgB1 + 4096,    // the small vectors in their LDS layout (kOffB1..kOffW), padded
+              kVecPad = 1280,             // to whole 1-KB glds pieces
+              kImgTotal = kImgVec + kVecPad;  // 111,872 floats
 
 __device__ __forceinline__ void inv_perm_acc(int pos, int nkb, int &i, int &k) {
     const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
@@ -228,13 +280,32 @@ __device__ __forceinline__ void inv_perm_x(int pos, int &i, int &k) {
     k = 2 * (tg * 4 + c) + (lane >> 5);
 }
 
-__global__ __launch_bounds__(256) void k_mlp_prep(const float *__restrict__ w1, const float *__restrict__ w2,
-                                                  const float *__restrict__ w3, const float *__restrict__ w4,
-                                                  float *__restrict__ img) {
+struct MlpParams {
+    const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4, *w5, *b5;
+};
+
+// element e (< kVecPad) of the vector image = LDS float e of stage_vectors' carve
+__device__ __forceinline__ float vec_elem(const MlpParams &p, int e) {
+    if (e < kOffB2) return p.b1[e - kOffB1];
+    if (e < kOffB3) return p.b2[e - kOffB2];
+    if (e < kOffB4) return e - kOffB3 < 129 ? p.b3[e - kOffB3] : 0.0f;
+    if (e < kOffB5) return p.b4[e - kOffB4];
+    if (e < kOffW3r0) return e - kOffB5 < 3 ? p.b5[e - kOffB5] : 0.0f;
+    if (e < kOffW5) return p.w3[e - kOffW3r0];
+    if (e < kOffW) return p.w5[e - kOffW5];
+    return 0.0f;
+}
+
+__global__ __launch_bounds__(256) void k_mlp_prep(MlpParams p, float *__restrict__ img) {
+    const float *w1 = p.w1, *w2 = p.w2, *w3 = p.w3, *w4 = p.w4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kImgTotal) return;
     int i, k;
     float v = 0.0f;
+    if (e >= kImgVec) {
+        img[e] = vec_elem(p, e - kImgVec);
+        return;
+    }
     if (e < kImgF2) {
         inv_perm_x(e - kImgF1, i, k);
         v = w1[i * 16 + k];
@@ -297,10 +368,6 @@ __device__ __forceinline__ void copy_img(float *wl, const float *__restrict__ im
     for (; e < n4; e += NT) dst[e] = src[e];
 }
 
-struct MlpParams {
-    const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4, *w5, *b5;
-};
-
 __device__ __forceinline__ void stage_vectors(float *lds, const MlpParams &p) {
     for (int e = threadIdx.x; e < 128; e += kThreads) {
         lds[kOffB1 + e] = p.b1[e];
@@ -353,21 +420,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
     const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
-    if (save) store_cf(act, tile, a, lane, n_tiles);
+    const int64_t tbytes = tstride * 4;                // < 2^31 (psvo_mlp_fwd checks m)
+    const CfStore cfs(tile, lane, n_tiles);
+    if (save) cfs.store(act, tbytes, a);
     raw_barrier();
     copy_img<kThreads>(wl, img + kImgF2, 16384);
     raw_barrier();
     init_bias(bacc, lds + kOffB2, h);
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     const uint64_t m2 = relu(bacc);  // h2
-    if (save) store_cf(act + tstride, tile, bacc, lane, n_tiles);
+    if (save) cfs.store(act + tstride, tbytes, bacc);
     raw_barrier();
     copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
     raw_barrier();
     const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    if (save) store_cf(act + 2 * tstride, tile, a, lane, n_tiles);
+    if (save) cfs.store(act + 2 * tstride, tbytes, a);
     raw_barrier();
     copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
     raw_barrier();
@@ -376,7 +445,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
     if (save) {
-        store_cf(act + 3 * tstride, tile, bacc, lane, n_tiles);
+        cfs.store(act + 3 * tstride, tbytes, bacc);
         if (valid) {
             uint64_t *mk = masks + (s * 2 + h) * 3;
             mk[0] = m1;
@@ -422,6 +491,8 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     const bool valid = s < m;
     const int64_t tile = (int64_t)blockIdx.x * (kTileBwd / 32) + wave;
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
+    const int64_t tbytes = n_tiles * 32 * 128 * 4;
+    const CfStore cfs(tile, lane, n_tiles);
     uint64_t m1 = 0, m2 = 0, m4 = 0;
     float d5[3] = {0.f, 0.f, 0.f};
     float dsdf = 0.0f;
@@ -453,9 +524,9 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
         for (int r = 0; r < 16; ++r) {
             const int k = 32 * b + phi(r, h);
             const float v = lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
-            bacc[b][r] = ((m4 >> (16 * b + r)) & 1) ? v : 0.0f;
+            bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
         }
-    store_cf(o.d4, tile, bacc, lane, n_tiles);
+    cfs.store(o.d4, tbytes, bacc);
     // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
     f32x16 t5[5];
     zero(t5);
@@ -465,7 +536,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
 #pragma unroll
     for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-    store_cf(o.d3, tile, a, lane, n_tiles);
+    cfs.store(o.d3, tbytes, a);
     // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
     raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB3, 16384);
@@ -476,7 +547,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
         for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     apply_mask(bacc, m2);
-    store_cf(o.d2, tile, bacc, lane, n_tiles);
+    cfs.store(o.d2, tbytes, bacc);
     // ---- δh1 = W2ᵀ δh2 ⊙ mask
     raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB2, 16384);
@@ -484,7 +555,7 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
     zero(a);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);
     apply_mask(a, m1);
-    store_cf(o.d1, tile, a, lane, n_tiles);
+    cfs.store(o.d1, tbytes, a);
     // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
     raw_barrier();
     copy_img<kThreadsBwd>(wl, img + kImgB1, 4096);
@@ -869,6 +940,137 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
     *out = accumulate ? *out + v : v;
 }
 
+// ---------------------------------------------------------------------------
+// forward, persistent + double-buffered: one 512-thread workgroup per CU
+// loops over 256-sample tiles (8 waves × 32 samples, the chain of k_mlp_fwd
+// per wave).  The vectors and W1 stay resident in LDS; W2, W3, W4 stream
+// through two 72-KB buffers with global_load_lds issued one layer ahead
+// (W2 of the next tile during W4 of this one), so no wave waits for weight
+// staging; each layer's activation stores are issued after the barrier that
+// opens the next layer and drain behind its MFMAs.  LDS: 5 + 8 + 2 × 72 KB.
+constexpr int kF2Waves = 8, kF2Threads = kF2Waves * 64, kF2Tile = kF2Waves * 32;
+constexpr int kF2W1 = kVecPad, kF2Buf0 = kF2W1 + 2048, kF2Buf1 = kF2Buf0 + kImgFwd;
+constexpr int kLdsFwd2 = (kF2Buf1 + kImgFwd) * 4;  // 160,768 B
+static_assert(kLdsFwd2 <= 160 * 1024, "fwd2 LDS budget");
+static_assert(kOffW <= kVecPad, "vector image");
+
+__device__ __forceinline__ void stage8(float *dst, const float *img, int n_floats, int wave, int lane) {
+    for (int c = wave; c < n_floats / 256; c += kF2Waves) glds16(img + (c * 64 + lane) * 4, dst + c * 256);
+}
+
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const float *__restrict__ feat,
+                                                            const float *__restrict__ img,
+                                                            float *__restrict__ sdf_out, float *__restrict__ rgb_out,
+                                                            float *__restrict__ act, uint64_t *__restrict__ masks) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const bool save = act != nullptr;
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF 32-sample tiles
+    const int64_t tstride = n_tiles * 32 * 128;
+    const int64_t tbytes = tstride * 4;
+    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    auto buf = [&](int i) { return lds + ((i & 1) ? kF2Buf1 : kF2Buf0); };
+    int seq = 0;  // staged layers so far: W(seq) sits in buf(seq)
+    int64_t t = blockIdx.x;
+    float xn[8];
+    {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        load_x(feat, s, s < m, h, xn);
+    }
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
+    stage8(buf(0), img + kImgF2, 16384, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    for (; t < n_wg_tiles; t += gridDim.x) {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        const bool valid = s < m;
+        const bool more = t + gridDim.x < n_wg_tiles;
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = xn[i];
+        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
+        f32x16 a[kNB], bacc[kNB];
+        // h1 = relu(W1 x + b1): resident W1
+        init_bias(a, lds + kOffB1, h);
+        gemm_x(lds + kF2W1, x, a, lane);
+        const uint64_t m1 = relu(a);
+        // h2 = relu(W2 h1 + b2)
+        wait_vm(0);
+        raw_barrier();
+        stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
+        if (save) cfs.store(act, tbytes, a);
+        init_bias(bacc, lds + kOffB2, h);
+        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane);
+        ++seq;
+        const uint64_t m2 = relu(bacc);
+        // [sdf | f] = W3 h2 + b3
+        wait_vm(0);
+        raw_barrier();
+        stage8(buf(seq + 1), img + kImgF4, 18432, wave, lane);
+        if (save) cfs.store(act + tstride, tbytes, bacc);
+        const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
+        init_bias(a, lds + kOffB3 + 1, h);
+        gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane);
+        ++seq;
+        // c1 = relu(W4 [f; x] + b4); the next tile's W2 and x start loading
+        wait_vm(0);
+        raw_barrier();
+        if (more) {
+            stage8(buf(seq + 1), img + kImgF2, 16384, wave, lane);
+            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+            load_x(feat, sn, sn < m, h, xn);
+        }
+        if (save) cfs.store(act + 2 * tstride, tbytes, a);
+        init_bias(bacc, lds + kOffB4, h);
+        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane);
+        gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
+        ++seq;
+        const uint64_t m4 = relu(bacc);
+        if (save) {
+            cfs.store(act + 3 * tstride, tbytes, bacc);
+            if (valid) {
+                uint64_t *mk = masks + (s * 2 + h) * 3;
+                mk[0] = m1;
+                mk[1] = m2;
+                mk[2] = m4;
+            }
+        }
+        float rgb[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
+        if (valid && h == 0) {
+            sdf_out[s] = sdf;
+            rgb_out[s * 3 + 0] = rgb[0];
+            rgb_out[s * 3 + 1] = rgb[1];
+            rgb_out[s * 3 + 2] = rgb[2];
+        }
+    }
+    wait_vm(0);
+}
+
+static int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+static bool use_fwd2() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PSVO_MLP_FWD");
+        v = (e && e[0] == '1') ? 0 : 1;  // PSVO_MLP_FWD=1: the per-tile kernel (A/B)
+    }
+    return v == 1;
+}
+
 }  // namespace
 }  // namespace psvo
 
@@ -884,6 +1086,8 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
     PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats floats)");
     PSVO_REQUIRE((act == nullptr) == (masks == nullptr), "mlp_fwd: act and masks go together");
+    PSVO_REQUIRE(m <= kMaxSamples, "mlp_fwd: m = %lld > %lld (32-bit CF offsets)", (long long)m,
+                 (long long)kMaxSamples);
     if (m == 0) return PSVO_OK;
     static bool attr = false;
     if (!attr) {
@@ -892,10 +1096,23 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
         attr = true;
     }
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, w1, w2, w3, w4, images);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf, rgb,
-                       act, masks);
+    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
+    if (use_fwd2()) {
+        static bool attr2 = false;
+        if (!attr2) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
+            attr2 = true;
+        }
+        const int64_t tiles = div_up(m, kF2Tile);
+        const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
+        hipLaunchKernelGGL(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
+                           masks);
+    } else {
+        hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf,
+                           rgb, act, masks);
+    }
     return check_launch("mlp_fwd");
 }
 
