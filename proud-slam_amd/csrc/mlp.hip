@@ -71,28 +71,55 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// acc[ob] += image(`wl`: NOUT x NIN blocks) · in[kb].  Per (kb, rg) the NOUT
-// operand groups are read first, then the 4·NOUT MFMAs run with the
-// independent accumulators interleaved (ob innermost), so no MFMA waits on
-// its predecessor and the next group's ds_reads overlap these MFMAs.
-template <int NIN, int NOUT>
-__device__ __forceinline__ void gemm_acc(const float *wl, const f32x16 (&in)[NIN], f32x16 (&acc)[NOUT], int lane) {
+// acc[ob] += image(`wl`: NOUT x NIN blocks) · in[kb].  Software-pipelined:
+// the NOUT operand groups of step (kb, rg) + 1 are read from LDS before the
+// 4·NOUT MFMAs of step (kb, rg) issue (ob innermost, independent
+// accumulators), and scheduling barriers per step keep the compiler from
+// pulling those reads back next to their first use — so the LDS latency
+// hides behind a step of MFMAs instead of stalling every 4 of them.  `st`
+// (St::kN stores per step) drains a pending store queue between the reads
+// and the MFMAs of each step — spread over the GEMM instead of a burst that
+// fills the TA command FIFO and stalls the wave.
+struct NoStore {
+    static constexpr int kN = 0;
+    __device__ __forceinline__ void operator()(int, int) const {}
+};
+
+template <int NIN, int NOUT, typename St = NoStore>
+__device__ __forceinline__ void gemm_acc(const float *wl, const f32x16 (&in)[NIN], f32x16 (&acc)[NOUT], int lane,
+                                         const St &st = St()) {
+    constexpr int kSteps = NIN * 4;
+    auto opnd = [&](int step, int ob) {
+        const int kb = step >> 2, rg = step & 3;
+        return *reinterpret_cast<const float4 *>(wl + ((((ob * NIN + kb) * 4 + rg) * 64 + lane) << 2));
+    };
+    float4 cur[NOUT];
 #pragma unroll
-    for (int kb = 0; kb < NIN; ++kb) {
+    for (int ob = 0; ob < NOUT; ++ob) cur[ob] = opnd(0, ob);
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-            float4 a[NOUT];
+    for (int step = 0; step < kSteps; ++step) {
+        const int kb = step >> 2, rg = step & 3;
+        float4 nxt[NOUT];
+        if (step + 1 < kSteps) {
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob)
-                a[ob] = *reinterpret_cast<const float4 *>(wl + ((((ob * NIN + kb) * 4 + rg) * 64 + lane) << 2));
+            for (int ob = 0; ob < NOUT; ++ob) nxt[ob] = opnd(step + 1, ob);
+        }
+        st(kb, rg);
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].x, in[kb][4 * rg + 0], acc[ob]);
+        for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(cur[ob].x, in[kb][4 * rg + 0], acc[ob]);
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].y, in[kb][4 * rg + 1], acc[ob]);
+        for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(cur[ob].y, in[kb][4 * rg + 1], acc[ob]);
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].z, in[kb][4 * rg + 2], acc[ob]);
+        for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(cur[ob].z, in[kb][4 * rg + 2], acc[ob]);
 #pragma unroll
-            for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(a[ob].w, in[kb][4 * rg + 3], acc[ob]);
+        for (int ob = 0; ob < NOUT; ++ob) acc[ob] = mfma(cur[ob].w, in[kb][4 * rg + 3], acc[ob]);
+        if (step + 1 < kSteps) __builtin_amdgcn_sched_group_barrier(0x100, NOUT, 0);  // the next step's reads
+        if (St::kN > 0) __builtin_amdgcn_sched_group_barrier(0x040, St::kN, 0);      // queued stores
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NOUT, 0);                     // this step's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        if (step + 1 < kSteps) {
+#pragma unroll
+            for (int ob = 0; ob < NOUT; ++ob) cur[ob] = nxt[ob];
         }
     }
 }
@@ -247,9 +274,32 @@ struct CfStore {
         for (int b = 0; b < kNB; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[b][r]), rs,
-                                                      voff[(r & 3) + 4 * ((r >> 2) & 1)] + 256 * (r & 3),
-                                                      8192 * b + 2048 * (r >> 2), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[b][r]), rs, voff[(r & 3) + 4 * ((r >> 2) & 1)],
+                                                      8192 * b + 2048 * (r >> 2) + 256 * (r & 3), 0);
+    }
+};
+
+// Pending-store queue for gemm_acc: the tile `v` (the GEMM's input) into a CF
+// matrix, 4 registers per GEMM step.  A disabled queue (or a tile past the
+// allocation) gets an empty buffer range, so the hardware drops its stores
+// without a branch in the MFMA stream.
+struct CfQueue {
+    static constexpr int kN = 4;
+    const CfStore &c;
+    const f32x16 (&v)[kNB];
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ CfQueue(const CfStore &cs, const float *matrix, int64_t bytes, bool on, const f32x16 (&vv)[kNB])
+        : c(cs), v(vv),
+          rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(matrix), 0,
+                                               __builtin_amdgcn_readfirstlane((on && cs.ok) ? (int)bytes : 0),
+                                               0x00020000)) {}
+    __device__ __forceinline__ void operator()(int kb, int rg) const {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = 4 * rg + j;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[kb][r]), rs, c.voff[(r & 3) + 4 * ((r >> 2) & 1)],
+                                                  8192 * kb + 2048 * (r >> 2) + 256 * (r & 3), 0);
+        }
     }
 };
 
@@ -1001,19 +1051,17 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
         wait_vm(0);
         raw_barrier();
         stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
-        if (save) cfs.store(act, tbytes, a);
         init_bias(bacc, lds + kOffB2, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane);
+        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
         ++seq;
         const uint64_t m2 = relu(bacc);
         // [sdf | f] = W3 h2 + b3
         wait_vm(0);
         raw_barrier();
         stage8(buf(seq + 1), img + kImgF4, 18432, wave, lane);
-        if (save) cfs.store(act + tstride, tbytes, bacc);
         const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
         init_bias(a, lds + kOffB3 + 1, h);
-        gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane);
+        gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane, CfQueue(cfs, act + tstride, tbytes, save, bacc));  // + h2
         ++seq;
         // c1 = relu(W4 [f; x] + b4); the next tile's W2 and x start loading
         wait_vm(0);
@@ -1023,9 +1071,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
             const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
             load_x(feat, sn, sn < m, h, xn);
         }
-        if (save) cfs.store(act + 2 * tstride, tbytes, a);
         init_bias(bacc, lds + kOffB4, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane);
+        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act + 2 * tstride, tbytes, save, a));  // + f
         gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
         ++seq;
         const uint64_t m4 = relu(bacc);
@@ -1051,6 +1098,136 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     wait_vm(0);
 }
 
+// ---------------------------------------------------------------------------
+// backward (data), persistent + double-buffered like k_mlp_fwd2: 8 waves ×
+// 32 samples per tile; W4ᵀ / W2ᵀ stream through an 80-KB buffer and W3ᵀ /
+// W1ᵀ through a 64-KB one, each image issued (global_load_lds) one layer
+// ahead; each δ is stored from inside the GEMM that consumes it; the next
+// tile's per-sample inputs load during the W1ᵀ layer.
+constexpr int kB2BufA = kVecPad, kB2BufB = kB2BufA + 20480;
+constexpr int kLdsBwd2 = (kB2BufB + 16384) * 4;  // 152,576 B
+static_assert(kLdsBwd2 <= 160 * 1024, "bwd2 LDS budget");
+
+struct BwdIn {
+    uint64_t mk[3];
+    float y[3], g[3], gs;
+};
+
+__device__ __forceinline__ void load_bwd_in(const float *__restrict__ rgb_in, const uint64_t *__restrict__ masks,
+                                            const float *__restrict__ g_sdf, const float *__restrict__ g_rgb,
+                                            int64_t s, bool valid, int h, BwdIn &in) {
+    const int64_t q = valid ? s : 0;
+    const uint64_t *mk = masks + (q * 2 + h) * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        in.mk[i] = mk[i];
+        in.y[i] = rgb_in[q * 3 + i];
+        in.g[i] = g_rgb[q * 3 + i];
+    }
+    in.gs = g_sdf[q];
+}
+
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const float *__restrict__ img,
+                                                            const float *__restrict__ rgb_in,
+                                                            const uint64_t *__restrict__ masks,
+                                                            const float *__restrict__ g_sdf,
+                                                            const float *__restrict__ g_rgb, BwdOut o) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *bufA = lds + kB2BufA, *bufB = lds + kB2BufB;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
+    const int64_t tbytes = n_tiles * 32 * 128 * 4;
+    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    int64_t t = blockIdx.x;
+    BwdIn nin;
+    {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, s < m, h, nin);
+    }
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    stage8(bufA, img + kImgB4, 20480, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    for (; t < n_wg_tiles; t += gridDim.x) {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        const bool valid = s < m;
+        const bool more = t + gridDim.x < n_wg_tiles;
+        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
+        const BwdIn in = nin;
+        float d5[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d5[c] = valid ? in.g[c] * (in.y[c] * (1.0f - in.y[c])) : 0.0f;  // sigmoid bwd
+        const float dsdf = valid ? in.gs : 0.0f;
+        const uint64_t m1 = valid ? in.mk[0] : 0, m2 = valid ? in.mk[1] : 0, m4 = valid ? in.mk[2] : 0;
+        if (valid && h == 0) {
+            o.d5[s * 3 + 0] = d5[0];
+            o.d5[s * 3 + 1] = d5[1];
+            o.d5[s * 3 + 2] = d5[2];
+        }
+        // ---- W4ᵀ layer (bufA); W3ᵀ → bufB
+        wait_vm(0);
+        raw_barrier();
+        stage8(bufB, img + kImgB3, 16384, wave, lane);
+        f32x16 a[kNB], bacc[kNB];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
+                const int k = 32 * b + phi(r, h);
+                const float v =
+                    lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
+                bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
+            }
+        f32x16 t5[5];
+        zero(t5);
+        gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, true, bacc));  // + δc1 stores
+        float dxc[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
+        // ---- W3ᵀ layer (bufB); W2ᵀ → bufA
+        wait_vm(0);
+        raw_barrier();
+        stage8(bufA, img + kImgB2, 16384, wave, lane);
+#pragma unroll
+        for (int b = 0; b < kNB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
+        gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, true, a));  // + δf stores
+        apply_mask(bacc, m2);
+        // ---- W2ᵀ layer (bufA); W1ᵀ → bufB
+        wait_vm(0);
+        raw_barrier();
+        stage8(bufB, img + kImgB1, 4096, wave, lane);
+        zero(a);
+        gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, true, bacc));  // + δh2 stores
+        apply_mask(a, m1);
+        // ---- W1ᵀ layer (bufB); next tile's W4ᵀ → bufA and its inputs
+        wait_vm(0);
+        raw_barrier();
+        if (more) {
+            stage8(bufA, img + kImgB4, 20480, wave, lane);
+            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, sn < m, h, nin);
+        }
+        f32x16 t1[1];
+        zero(t1);
+        gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, true, a));  // + δh1 stores
+        if (valid) {
+            float *dst = o.dfeat + s * kIn;
+#pragma unroll
+            for (int rg = 0; rg < 2; ++rg)
+                *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
+                    make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
+                                t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
+        }
+    }
+    wait_vm(0);
+}
+
 static int device_cus() {
     static int cus = 0;
     if (cus == 0) {
@@ -1066,7 +1243,7 @@ static bool use_fwd2() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("PSVO_MLP_FWD");
-        v = (e && e[0] == '1') ? 0 : 1;  // PSVO_MLP_FWD=1: the per-tile kernel (A/B)
+        v = (e && e[0] == '1') ? 0 : 1;  // PSVO_MLP_FWD=1: the per-tile fwd / bwd_data kernels (A/B)
     }
     return v == 1;
 }
@@ -1189,8 +1366,21 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd);
             attr = true;
         }
-        hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p, images,
-                           rgb, masks, g_sdf, g_rgb, o);
+        if (use_fwd2()) {
+            static bool attr2 = false;
+            if (!attr2) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd2),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd2);
+                attr2 = true;
+            }
+            const int64_t tiles = div_up(m, kF2Tile);
+            const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
+            hipLaunchKernelGGL(k_mlp_bwd2, dim3(grid), dim3(kF2Threads), kLdsBwd2, st, m, images, rgb, masks, g_sdf,
+                               g_rgb, o);
+        } else {
+            hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p,
+                               images, rgb, masks, g_sdf, g_rgb, o);
+        }
         int rc = check_launch("mlp_bwd_data");
         if (rc) return rc;
     }
