@@ -720,25 +720,41 @@ __device__ __forceinline__ float cf_row_dot(const float *img, int f, const float
 template <int NR, int NC, bool XBLK>
 __device__ __forceinline__ void dw_chunk(const float *Dl, const float *Al, const int (&rb)[NR], const int (&cb)[NC],
                                          f32x16 (&acc)[NR][NC], f32x16 &accx, int xsel, int lane) {
+    // software-pipelined like gemm_acc: the operands of k-group t4 + 1 are
+    // read before the MFMAs of k-group t4 issue (one wave per SIMD here, so
+    // an exposed LDS latency is an idle MFMA pipe)
     const int x = lane & 31, h = lane >> 5;
-#pragma unroll 2
+    constexpr int NOP = NR + NC + (XBLK ? 1 : 0);
+    auto load = [&](int t4, float4 (&o)[NOP]) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) o[i] = cf_op(Dl, 32 * rb[i] + x, h, t4);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) o[NR + j] = cf_op(Al, 32 * cb[j] + x, h, t4);
+        if (XBLK) o[NOP - 1] = cf_op(Al, 128 + x, h, t4);
+    };
+    float4 cur[NOP];
+    load(0, cur);
+#pragma unroll
     for (int t4 = 0; t4 < 8; ++t4) {
-        float4 dv[NR], av[NC], ax;
-#pragma unroll
-        for (int i = 0; i < NR; ++i) dv[i] = cf_op(Dl, 32 * rb[i] + x, h, t4);
-#pragma unroll
-        for (int j = 0; j < NC; ++j) av[j] = cf_op(Al, 32 * cb[j] + x, h, t4);
-        if (XBLK) ax = cf_op(Al, 128 + x, h, t4);
-        const float4 dx = (XBLK && NR > 1 && xsel) ? dv[NR - 1] : dv[0];
-#define PSVO_DW_K(c)                                                                       \
-        _Pragma("unroll") for (int i = 0; i < NR; ++i)                                     \
-            _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(dv[i].c, av[j].c, acc[i][j]); \
-        if (XBLK) accx = mfma(dx.c, ax.c, accx);
+        float4 nxt[NOP];
+        if (t4 + 1 < 8) load(t4 + 1, nxt);
+        const float4 dx = (XBLK && NR > 1 && xsel) ? cur[NR - 1] : cur[0];
+#define PSVO_DW_K(c)                                                                                          \
+        _Pragma("unroll") for (int i = 0; i < NR; ++i)                                                        \
+            _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(cur[i].c, cur[NR + j].c, acc[i][j]); \
+        if (XBLK) accx = mfma(dx.c, cur[NOP - 1].c, accx);
         PSVO_DW_K(x)
         PSVO_DW_K(y)
         PSVO_DW_K(z)
         PSVO_DW_K(w)
 #undef PSVO_DW_K
+        if (t4 + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, NOP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * (NR * NC + (XBLK ? 1 : 0)), 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t4 + 1 < 8) {
+#pragma unroll
+            for (int i = 0; i < NOP; ++i) cur[i] = nxt[i];
+        }
     }
 }
 
