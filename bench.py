@@ -357,7 +357,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_qi, "avg_launch_ms": q_ms,
                      "parts_ms": q_parts, "visits_per_ray": v_avg / max(rays_step, 1),
                      "samples_per_hit_ray": m_avg / max(r_avg, 1)},
-        "roofline_mfma": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd/bwd_data/dw/dw_reduce)",
+        "roofline_mfma": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd2/bwd2/dw/dw_reduce)",
                           "bound": "mfma", "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
                           "traffic": traffic.get("mlp_bytes_per_step"),
