@@ -233,10 +233,9 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(int, ray_rank, kRayRank, R * sizeof(int));
     ENG_BUF(int, rank_ray, kRankRay, R * sizeof(int));
     mark(e, st, PSVO_TIME_INTERSECT, 0);
-    ENG_CALL(psvo_ray_intersect_sorted(stream, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
-                                       d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum,
-                                       stats));
-    ENG_CALL(psvo_hit_rank(stream, R, ray_nv, ray_rank, rank_ray));
+    ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
+                                    d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
+                                    ray_rank, rank_ray));
     mark(e, st, PSVO_TIME_INTERSECT, 1);
     // ---- sampling, without a read-back: the sampler reads P, R_hit and
     // max ⌈steps⌉ from `stats` on the device; its buffers are [R, cap] with

@@ -30,6 +30,11 @@ constexpr float kMaxDepthFill = 10.0f;  // voxel_helpers.py:24 MAX_DEPTH
 
 inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
+                     const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
+                     float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
+                     int *rank_ray);
+
 }  // namespace psvo
 
 #define PSVO_REQUIRE(cond, ...)                                       \

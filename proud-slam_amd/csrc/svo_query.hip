@@ -464,9 +464,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
 }
 
 // P (max valid hits), R_hit and max ceil(Σ/step) over the rays — one block.
-__global__ __launch_bounds__(1024) void k_ray_stats(int64_t n, const int *__restrict__ ray_nv,
-                                                    const float *__restrict__ ray_dsum, float step_size,
-                                                    int *__restrict__ stats) {
+__device__ void ray_stats_body(int64_t n, const int *__restrict__ ray_nv, const float *__restrict__ ray_dsum,
+                               float step_size, int *__restrict__ stats) {
     int p = 0, hits = 0, mc = 0;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
         const int nv = ray_nv[i];
@@ -497,37 +496,57 @@ __global__ __launch_bounds__(1024) void k_ray_stats(int64_t n, const int *__rest
     }
 }
 
+__global__ __launch_bounds__(1024) void k_ray_stats(int64_t n, const int *__restrict__ ray_nv,
+                                                    const float *__restrict__ ray_dsum, float step_size,
+                                                    int *__restrict__ stats) {
+    ray_stats_body(n, ray_nv, ray_dsum, step_size, stats);
+}
+
 // ---------------------------------------------------------------------------
 // Single-workgroup exclusive scan (n ≲ 10^6): each thread owns a contiguous
 // run; run totals scanned in LDS.
 template <typename F>
 __device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *total) {
-    __shared__ int s_sum[1024];
+    // thread t scans the run [t·per, (t+1)·per); the run totals are scanned
+    // with wave shuffles and one LDS pass over the ≤ 16 wave totals
+    // (2 barriers instead of a 2·log2(1024)-barrier Hillis–Steele pass)
+    __shared__ int s_wave[16];
     const int tid = threadIdx.x;
     const int nt = blockDim.x;
+    const int lane = tid & (kWave - 1), w = tid / kWave, nw = nt / kWave;
     const int64_t per = (n + nt - 1) / nt;
     const int64_t beg = tid * per;
     const int64_t end = beg + per < n ? beg + per : n;
     int local = 0;
     for (int64_t i = beg; i < end; ++i) local += value(i);
-    s_sum[tid] = local;
-    __syncthreads();
-    for (int off = 1; off < nt; off <<= 1) {
-        const int v = tid >= off ? s_sum[tid - off] : 0;
-        __syncthreads();
-        s_sum[tid] += v;
-        __syncthreads();
+    int incl = local;
+#pragma unroll
+    for (int sh = 1; sh < kWave; sh <<= 1) {
+        const int t = __shfl_up(incl, sh, kWave);
+        if (lane >= sh) incl += t;
     }
-    int run = s_sum[tid] - local;
+    if (lane == kWave - 1) s_wave[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        int v = lane < nw ? s_wave[lane] : 0;
+#pragma unroll
+        for (int sh = 1; sh < 16; sh <<= 1) {
+            const int t = __shfl_up(v, sh, kWave);
+            if (lane >= sh) v += t;
+        }
+        if (lane < nw) s_wave[lane] = v;  // inclusive wave prefix
+    }
+    __syncthreads();
+    int run = (w > 0 ? s_wave[w - 1] : 0) + incl - local;
     for (int64_t i = beg; i < end; ++i) {
         out[i] = run;
         run += value(i);
     }
-    if (tid == nt - 1) *total = s_sum[tid];
+    if (tid == nt - 1) *total = s_wave[nw - 1];
 }
 
-__global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restrict__ ray_nv,
-                                                   int *__restrict__ ray_rank, int *__restrict__ rank_ray) {
+__device__ void hit_rank_body(int64_t n, const int *__restrict__ ray_nv, int *__restrict__ ray_rank,
+                              int *__restrict__ rank_ray) {
     __shared__ int total;
     block_scan_runs(n, [&](int64_t i) { return ray_nv[i] > 0 ? 1 : 0; }, ray_rank, &total);
     __syncthreads();
@@ -539,6 +558,21 @@ __global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restr
             ray_rank[i] = -1;
         }
     }
+}
+
+__global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restrict__ ray_nv,
+                                                   int *__restrict__ ray_rank, int *__restrict__ rank_ray) {
+    hit_rank_body(n, ray_nv, ray_rank, rank_ray);
+}
+
+// k_ray_stats + k_hit_rank in one launch (the engine's path)
+__global__ __launch_bounds__(1024) void k_ray_stats_rank(int64_t n, const int *__restrict__ ray_nv,
+                                                         const float *__restrict__ ray_dsum, float step_size,
+                                                         int *__restrict__ stats, int *__restrict__ ray_rank,
+                                                         int *__restrict__ rank_ray) {
+    ray_stats_body(n, ray_nv, ray_dsum, step_size, stats);
+    __syncthreads();
+    hit_rank_body(n, ray_nv, ray_rank, rank_ray);
 }
 
 __global__ __launch_bounds__(1024) void k_scan_counts(int64_t n, const int *__restrict__ counts,
@@ -988,6 +1022,25 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
+
+namespace psvo {
+// psvo_ray_intersect_sorted + psvo_hit_rank with the two single-block
+// reductions fused into one launch (engine.cpp)
+int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
+                     const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
+                     float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
+                     int *rank_ray) {
+    PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
+    PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
+    if (n_rays == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st, n_rays,
+                       rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
+                       ray_nv, ray_dsum, stats);
+    hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
+                       ray_rank, rank_ray);
+    return check_launch("intersect_ranked");
+}
+}  // namespace psvo
 
 extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray) {
     PSVO_REQUIRE(n_rays >= 0, "hit_rank: n_rays < 0");
