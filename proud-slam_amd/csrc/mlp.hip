@@ -215,55 +215,42 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
                 make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
 }
 
-// Activations and δ's the weight gradients consume are stored CHUNK-FEATURE
-// major ("CF"): per 64-sample chunk a [128 feature][64 slot] block in which
-// sample s sits at permuted position p = (s&1)·32 + s/2 (so that the two
-// samples of one f32 MFMA k-step pair, 2t and 2t+1, sit at t and 32 + t) and
-// 16-B groups are XOR-swizzled by feature (g ^ f%16), which makes the
-// weight-gradient kernel's 4-k-step ds_read_b128 operand reads bank-conflict
-// free while its LDS image stays a straight copy of the chunk (global_load_lds).
-// A wave stores its 32-sample tile register by register: each store is two
-// feature rows × two 64-B runs.
-constexpr int kCh = 64;              // samples per CF chunk
-constexpr int kCfChunk = 128 * kCh;  // floats per CF chunk
-constexpr int64_t kMaxSamples = (int64_t)65535 * kCh;  // one CF matrix < 2 GiB (buffer offsets)
+// Activations and δ's the weight gradients consume are stored TILE-FEATURE
+// major ("CF"): per 32-sample tile a [128 feature][32 slot] block (16 KB) in
+// which tile-local sample c sits at position p = (c&1)·16 + c/2 (the two
+// samples of one f32 MFMA k-step pair, 2t and 2t+1, at t and 16 + t) and the
+// 8 16-B groups of a row are XOR-swizzled by feature (slot = g ^ (f/2)%8: any
+// 16 consecutive rows then cover all 64 banks once per 16-B column).  That
+// is exactly the weight-gradient kernel's LDS operand image (conflict-free
+// 4-k-step ds_read_b128), so a tile lands there by straight 1-KB
+// global_load_lds copies.  The producing wave writes its 32-sample tile
+// register by register with buffer stores: each covers two 64-B runs of two
+// feature rows.
+constexpr int kCh = 64;                 // allocation granule: CF buffers hold whole 64-sample pairs of tiles
+constexpr int kTileS = 32;              // samples per CF tile
+constexpr int kCfTile = 128 * kTileS;   // floats per CF tile
+constexpr int64_t kMaxSamples = (int64_t)131071 * kTileS;  // one CF matrix < 2 GiB (buffer offsets)
 
-__device__ __forceinline__ int cf_slot(int f, int s) {
-    const int p = (s & 1) * 32 + (s >> 1);
-    return f * kCh + ((((p >> 2) ^ (f & 15)) << 2) | (p & 3));
-}
+__device__ __forceinline__ int cf_row_slot(int row, int g) { return row * kTileS + ((g ^ ((row >> 1) & 7)) << 2); }
 
-// tile = global 32-sample tile index (wave-uniform); n_tiles = allocated tiles
-__device__ __forceinline__ void store_cf(float *dst, int64_t tile, const f32x16 (&v)[kNB], int lane, int64_t n_tiles) {
-    if (tile >= n_tiles) return;
-    float *base = dst + (tile >> 1) * kCfChunk;
-    const int sc = (int)(tile & 1) * 32 + (lane & 31);
-    const int hh = lane >> 5;
-#pragma unroll
-    for (int b = 0; b < kNB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) base[cf_slot(32 * b + phi(r, hh), sc)] = v[b][r];
-}
-
-// The same stores as buffer stores whose addresses need no VALU: element
-// (b, r) of the tile lands at byte
-//   chunk + f·256 + 4·((((p>>2) ^ (f&15)) << 2) | (p&3)),  f = 32b + phi(r, h)
-// and f&15 = (r&3) + 8((r>>2)&1) + 4h, so with the 8 per-lane XOR offsets
-// voff[(r&3) + 4((r>>2)&1)] (chunk and 1024h folded in) the rest is
-// 8192b + 2048(r>>2) (an SGPR soffset) + 256(r&3) (the immediate offset).
+// Element (b, r) of a wave's accumulator tile lands at byte
+//   tile·16384 + f·128 + 4·((((p>>2) ^ X) << 2) | (p&3)),  f = 32b + phi(r, h)
+// with X = (f/2)%8 = 4((r>>2)&1) + 2h + ((r>>1)&1): per lane 4 XOR variants
+// voff[((r>>1)&1) + 2((r>>2)&1)] (tile and 512h folded in) and a
+// wave-uniform rest 4096b + 1024(r>>2) + 128(r&3) (soffset).
 struct CfStore {
-    int voff[8];
+    int voff[4];
     bool ok;
     __device__ CfStore(int64_t tile, int lane, int64_t n_tiles) {
         ok = tile < n_tiles;
-        const int sc = (int)(tile & 1) * 32 + (lane & 31);
-        const int p = (sc & 1) * 32 + (sc >> 1);
+        const int c = lane & 31;
+        const int p = (c & 1) * 16 + (c >> 1);
         const int hh = lane >> 5;
-        const int chunk = (int)((tile >> 1) * kCfChunk * 4);
+        const int base = (int)(tile * kCfTile * 4) + 512 * hh;
 #pragma unroll
-        for (int c8 = 0; c8 < 8; ++c8) {
-            const int x = (c8 & 3) + 8 * (c8 >> 2) + 4 * hh;
-            voff[c8] = chunk + 1024 * hh + 4 * ((((p >> 2) ^ x) << 2) | (p & 3));
+        for (int v = 0; v < 4; ++v) {
+            const int xr = 4 * (v >> 1) + 2 * hh + (v & 1);
+            voff[v] = base + 4 * ((((p >> 2) ^ xr) << 2) | (p & 3));
         }
     }
     __device__ __forceinline__ void store(const float *matrix, int64_t bytes, const f32x16 (&v)[kNB]) const {
@@ -274,8 +261,8 @@ struct CfStore {
         for (int b = 0; b < kNB; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[b][r]), rs, voff[(r & 3) + 4 * ((r >> 2) & 1)],
-                                                      8192 * b + 2048 * (r >> 2) + 256 * (r & 3), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[b][r]), rs, voff[((r >> 1) & 1) + 2 * ((r >> 2) & 1)],
+                                                      4096 * b + 1024 * (r >> 2) + 128 * (r & 3), 0);
     }
 };
 
@@ -297,8 +284,8 @@ struct CfQueue {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int r = 4 * rg + j;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[kb][r]), rs, c.voff[(r & 3) + 4 * ((r >> 2) & 1)],
-                                                  8192 * kb + 2048 * (r >> 2) + 256 * (r & 3), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[kb][r]), rs, c.voff[((r >> 1) & 1) + 2 * ((r >> 2) & 1)],
+                                                  4096 * kb + 1024 * (r >> 2) + 128 * (r & 3), 0);
         }
     }
 };
@@ -624,19 +611,11 @@ __global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpP
 }
 
 // ---------------------------------------------------------------------------
-// backward (weights): dW[rows][cols] = Σ_s D[s][row] · A[s][col], db = Σ_s D[s].
-// Split-K over 64-sample CF chunks: a workgroup owns (layer, chunk range),
-// copies each chunk's D and A blocks into LDS with global_load_lds (no
-// registers, no re-layout), and its 4 waves accumulate their 32x32 blocks
-// of C across the range in registers (f32 MFMA, 4 k-steps per ds_read_b128
-// operand read); per-layer private slabs are summed by k_mlp_dw_reduce in a
-// fixed order (bitwise reproducible).  Thin pieces run on the VALU from the
-// same LDS images: bias sums, W3's sdf row (g_sdf ⊗ h2) and W5 (δ5 ⊗ c1).
-//   L0: W1 128x16   D = δh1 | A = x (16 rows from feat, 16 zero rows)
-//   L1: W2 128x128  D = δh2 | A = h1        2x2 blocks per wave
-//   L2: W3 rows 1..128 D = δf | A = h2      2x2 blocks per wave (+ sdf row, db3)
-//   L3: W4 128x144  D = δc1 | A = [f | x]   2x2 blocks + one x block per wave
-//   W5 3x128 (VALU, δ5 [M][3] ⊗ c1) runs in the W1 workgroups
+// backward (weights) operands (k_mlp_dw2 below):
+//   L0: W1 128x16   D = δh1 | A = x (16 rows from feat, 16 zero rows); W5 3x128 = δ5 ⊗ c1
+//   L1: W2 128x128  D = δh2 | A = h1
+//   L2: W3 rows 1..128 D = δf | A = h2 (+ the sdf row g_sdf ⊗ h2, db3)
+//   L3: W4 128x144  D = δc1 | A = [f | x]
 struct DwSrc {
     const float *D[4];  // CF: δh1, δh2, δf, δc1
     const float *A[4];  // CF: (unused), h1, h2, f
@@ -671,93 +650,6 @@ __device__ __forceinline__ void glds4(const float *g, float *l) {
                  : "memory");
 }
 
-// one CF chunk (128 x 64 floats, 32 KB) → LDS, lane-linear 16-B copies
-__device__ __forceinline__ void copy_cf(float *dst, const float *__restrict__ src) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int u = 0; u < kCfChunk / (256 * 4); ++u) {
-        const int blk = u * 4 + wave;  // 1-KB piece of this wave-instruction
-        glds16(src + (blk * 64 + lane) * 4, dst + blk * 256);
-    }
-}
-
-// operand of feature row f for k-steps 4·t4 .. 4·t4+3 of lane half h
-__device__ __forceinline__ float4 cf_op(const float *img, int f, int h, int t4) {
-    const int g = 8 * h + t4;
-    return *reinterpret_cast<const float4 *>(img + f * kCh + (((g ^ (f & 15)) << 2)));
-}
-
-// chunk-local sample at permuted position p (inverse of p = (s&1)·32 + s/2)
-__device__ __forceinline__ int p_sample(int p) { return p < 32 ? 2 * p : 2 * (p - 32) + 1; }
-
-// Σ over the chunk of row f of a CF image (rotated float4 reads: conflict free)
-__device__ __forceinline__ float cf_row_sum(const float *img, int f) {
-    float acc = 0.f;
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int g = (i + f) & 15;
-        const float4 v = *reinterpret_cast<const float4 *>(img + f * kCh + 4 * g);
-        acc += (v.x + v.y) + (v.z + v.w);
-    }
-    return acc;
-}
-// Σ_s w[s] · row f, with w stored in permuted order (wp[p] = w[p_sample(p)]):
-// slot group g of row f holds positions 4(g ^ f%16) .. +3
-__device__ __forceinline__ float cf_row_dot(const float *img, int f, const float *wp) {
-    float acc = 0.f;
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int g = (i + f) & 15;
-        const float4 v = *reinterpret_cast<const float4 *>(img + f * kCh + 4 * g);
-        const float4 w = *reinterpret_cast<const float4 *>(wp + 4 * (g ^ (f & 15)));
-        acc += (v.x * w.x + v.y * w.y) + (v.z * w.z + v.w * w.w);
-    }
-    return acc;
-}
-
-// One chunk (32 k-steps) of MFMAs for a wave's NR x NC blocks; with XBLK an
-// extra block (D row block rb[xsel], A rows 128..159 = x) shares the D reads.
-template <int NR, int NC, bool XBLK>
-__device__ __forceinline__ void dw_chunk(const float *Dl, const float *Al, const int (&rb)[NR], const int (&cb)[NC],
-                                         f32x16 (&acc)[NR][NC], f32x16 &accx, int xsel, int lane) {
-    // software-pipelined like gemm_acc: the operands of k-group t4 + 1 are
-    // read before the MFMAs of k-group t4 issue (one wave per SIMD here, so
-    // an exposed LDS latency is an idle MFMA pipe)
-    const int x = lane & 31, h = lane >> 5;
-    constexpr int NOP = NR + NC + (XBLK ? 1 : 0);
-    auto load = [&](int t4, float4 (&o)[NOP]) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i) o[i] = cf_op(Dl, 32 * rb[i] + x, h, t4);
-#pragma unroll
-        for (int j = 0; j < NC; ++j) o[NR + j] = cf_op(Al, 32 * cb[j] + x, h, t4);
-        if (XBLK) o[NOP - 1] = cf_op(Al, 128 + x, h, t4);
-    };
-    float4 cur[NOP];
-    load(0, cur);
-#pragma unroll
-    for (int t4 = 0; t4 < 8; ++t4) {
-        float4 nxt[NOP];
-        if (t4 + 1 < 8) load(t4 + 1, nxt);
-        const float4 dx = (XBLK && NR > 1 && xsel) ? cur[NR - 1] : cur[0];
-#define PSVO_DW_K(c)                                                                                          \
-        _Pragma("unroll") for (int i = 0; i < NR; ++i)                                                        \
-            _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(cur[i].c, cur[NR + j].c, acc[i][j]); \
-        if (XBLK) accx = mfma(dx.c, cur[NOP - 1].c, accx);
-        PSVO_DW_K(x)
-        PSVO_DW_K(y)
-        PSVO_DW_K(z)
-        PSVO_DW_K(w)
-#undef PSVO_DW_K
-        if (t4 + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, NOP, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4 * (NR * NC + (XBLK ? 1 : 0)), 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t4 + 1 < 8) {
-#pragma unroll
-            for (int i = 0; i < NOP; ++i) cur[i] = nxt[i];
-        }
-    }
-}
-
 // write C blocks to the slab (rows offset `row_off` in the layer's matrix)
 template <int NR, int NC>
 __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int max_col, const int (&rb)[NR],
@@ -777,40 +669,6 @@ __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int
 // Double-buffered stage: D [128][64], A [160][64] CF images, raw x rows
 // [64][16] and raw per-sample scalars (g_sdf or δ5 [64][3]), all filled by
 // global_load_lds; the raw pieces are re-laid out LDS→LDS after landing.
-constexpr int kStD = 0, kStA = kStD + 128 * kCh, kStX = kStA + kDwA * kCh, kStS = kStX + kCh * 16,
-              kStage = kStS + kCh * 3;                        // 19,648 floats per stage
-constexpr int kDwLds = 2 * kStage + 4 * kCh;                  // + permuted per-sample weights
-static_assert(kDwLds * 4 <= 160 * 1024, "dW LDS budget");
-
-// issue the global_load_lds of chunk c into stage `st`; returns this wave's instruction count
-template <int L>
-__device__ __forceinline__ int dw_issue(const DwSrc &src, int64_t c, int64_t m, float *st) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int n = 0;
-    copy_cf(st + kStD, src.D[L] + c * kCfChunk);
-    if (L == 0) copy_cf(st + kStA + 32 * kCh, src.c1 + c * kCfChunk);  // c1 → A rows 32..159
-    else copy_cf(st + kStA, src.A[L] + c * kCfChunk);
-    n += 16;
-    const int64_t s0 = c * kCh;
-    if (L == 0 || L == 3) {  // x rows [64][16] = 4 KB: one 16-B piece per thread; rows past M clamp to row 0
-        const int e = threadIdx.x;  // float4 index: sample e/4, features 4(e%4)..
-        const int64_t sg = s0 + (e >> 2);
-        glds16(src.feat + (sg < m ? sg : 0) * 16 + (e & 3) * 4, st + kStX + wave * 256);
-        n += 1;
-    }
-    if (L == 2 && wave == 0) {  // g_sdf [64]
-        const int64_t sg = s0 + lane;
-        glds4(src.g_sdf + (sg < m ? sg : 0), st + kStS);
-        n += 1;
-    }
-    if (L == 0 && wave < 3) {  // δ5 [64][3] = 192 floats
-        const int64_t e = s0 * 3 + wave * 64 + lane;
-        glds4(src.d5 + (e < m * 3 ? e : 0), st + kStS + wave * 64);
-        n += 1;
-    }
-    return n;
-}
-
 __device__ __forceinline__ void wait_vm(int n) {
     // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima); n <= 63
     asm volatile("" ::: "memory");
@@ -830,124 +688,6 @@ __device__ __forceinline__ void wait_vm(int n) {
 
 // L = 0: W1 (MFMA) and W5 (VALU) share a workgroup (both are light: one
 // 32x32 block per wave / three row dots); L = 1..3: W2, W3, W4.
-template <int L>
-__device__ __forceinline__ void dw_layer(int64_t m, const DwSrc &src, int split, int n_split, float *slab,
-                                         float *slab5, float *lds) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t n_chunks = (m + kCh - 1) / kCh;
-    const int64_t c_beg = n_chunks * split / n_split, c_end = n_chunks * (split + 1) / n_split;
-    float *wperm = lds + 2 * kStage;  // per-sample weights in permuted order: [4][64]
-    constexpr int NR = (L == 0) ? 1 : 2;
-    constexpr int NC = (L == 0) ? 1 : 2;
-    constexpr bool XBLK = (L == 3);  // W4's x columns: block (rb = wave, cb = 4)
-    int rb[NR], cb[NC];
-    if (L == 0) {
-        rb[0] = wave;
-        cb[0] = 0;
-    } else {
-        rb[0] = 2 * (wave >> 1);
-        rb[NR - 1] = 2 * (wave >> 1) + 1;
-        cb[0] = 2 * (wave & 1);
-        cb[NC - 1] = 2 * (wave & 1) + 1;
-    }
-    const int xsel = wave & 1;  // rb[xsel] == wave
-    f32x16 acc[NR][NC];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) zero(acc[i]);
-    f32x16 accx[1];
-    zero(accx);
-    float vsum0 = 0.f, vsum1 = 0.f;              // VALU partials: bias, W3 sdf row / db3[0]
-    float w5a = 0.f, w5b = 0.f, vbias5 = 0.f;    // W5 row dots and db5
-    // A rows no chunk writes: W1 rows 16..31, W4 rows 144..159 (both stages)
-    if (L == 0 || L == 3) {
-        const int r0 = (L == 0) ? 16 : 144;
-        for (int e = threadIdx.x; e < 16 * kCh; e += 256) {
-            lds[kStA + r0 * kCh + e] = 0.f;
-            lds[kStage + kStA + r0 * kCh + e] = 0.f;
-        }
-    }
-    __syncthreads();
-    int n_next = 0;
-    if (c_beg < c_end) n_next = dw_issue<L>(src, c_beg, m, lds);
-    for (int64_t c = c_beg; c < c_end; ++c) {
-        float *st = lds + ((c - c_beg) & 1) * kStage;
-        float *nx = lds + ((c - c_beg + 1) & 1) * kStage;
-        // prefetch chunk c+1 into the other stage (its readers finished before the last barrier)
-        int n_after = 0;
-        if (c + 1 < c_end) n_after = dw_issue<L>(src, c + 1, m, nx);
-        wait_vm(n_after);  // chunk c has landed for this wave
-        raw_barrier();     // ... and for every wave
-        const int64_t s0 = c * kCh;
-        // raw pieces → layouts (samples past M zeroed)
-        if (L == 0 || L == 3) {
-            const int row0 = (L == 0) ? 0 : 128;
-            for (int e = threadIdx.x; e < kCh * 16; e += 256) {
-                const int sl = e >> 4, k = e & 15;
-                st[kStA + cf_slot(row0 + k, sl)] = (s0 + sl < m) ? st[kStX + e] : 0.f;
-            }
-        }
-        if (L == 2 && threadIdx.x < kCh) {
-            const int sl = p_sample(threadIdx.x);
-            wperm[threadIdx.x] = (s0 + sl < m) ? st[kStS + sl] : 0.f;
-        }
-        if (L == 0 && threadIdx.x < 3 * kCh) {
-            const int cc = threadIdx.x / kCh, pp = threadIdx.x - cc * kCh, sl = p_sample(pp);
-            wperm[cc * kCh + pp] = (s0 + sl < m) ? st[kStS + sl * 3 + cc] : 0.f;
-        }
-        if (L != 1) raw_barrier();
-        // VALU pieces
-        {
-            if (L == 0) {  // W5 = δ5 ⊗ c1 (c1 in A rows 32..159), db5
-                const float *c1l = st + kStA + 32 * kCh;
-                const int j = threadIdx.x & 127;
-                const int c0 = threadIdx.x >> 7;  // channel 0 or 1; threads < 128 also take channel 2
-                w5a += cf_row_dot(c1l, j, wperm + c0 * kCh);
-                if (c0 == 0) w5b += cf_row_dot(c1l, j, wperm + 2 * kCh);
-                if (wave < 3) {  // db5: wave c sums channel c of the chunk (one sample per lane)
-                    float b = wperm[wave * kCh + lane];
-#pragma unroll
-                    for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
-                    vbias5 += b;
-                }
-            }
-            if (threadIdx.x < 128) vsum0 += cf_row_sum(st + kStD, threadIdx.x);  // bias partial of D row
-            if (L == 2) {
-                if (threadIdx.x >= 128) vsum1 += cf_row_dot(st + kStA, threadIdx.x - 128, wperm);  // W3 sdf row
-                if (wave == 0) {  // db3[0] = Σ g_sdf: one sample per lane, wave reduction
-                    float gs = wperm[lane];
-#pragma unroll
-                    for (int sh = 32; sh > 0; sh >>= 1) gs += __shfl_xor(gs, sh, 64);
-                    vsum1 += gs;
-                }
-            }
-            dw_chunk<NR, NC, XBLK>(st + kStD, st + kStA, rb, cb, acc, accx[0], xsel, lane);
-        }
-        n_next = n_after;
-        raw_barrier();  // everyone is done reading stage `st` (and wperm) before it is refilled
-    }
-    (void)n_next;
-    // ---- write the slab: [rows][cols] weights, then [rows] bias
-    if (L == 0) {
-        const int j = threadIdx.x & 127, c0 = threadIdx.x >> 7;
-        slab5[c0 * 128 + j] = w5a;
-        if (c0 == 0) slab5[2 * 128 + j] = w5b;
-        if (wave < 3 && lane == 0) slab5[3 * 128 + wave] = vbias5;
-    }
-    constexpr int ROWS = (L == 2) ? 129 : 128;
-    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
-    constexpr int ROW_OFF = (L == 2) ? 1 : 0;
-    dw_store<NR, NC>(slab, COLS, ROW_OFF, COLS, rb, cb, acc, lane);
-    if (XBLK) {
-        const int rbx[1] = {wave}, cbx[1] = {4};
-        const f32x16 tmp[1][1] = {{accx[0]}};
-        dw_store<1, 1>(slab, COLS, 0, COLS, rbx, cbx, tmp, lane);
-    }
-    if (L == 2 && threadIdx.x >= 128) slab[threadIdx.x - 128] = vsum1;  // sdf row = row 0
-    float *bias = slab + ROWS * COLS;
-    if (threadIdx.x < 128) bias[ROW_OFF + threadIdx.x] = vsum0;
-    if (L == 2 && threadIdx.x == 0) bias[0] = vsum1;
-}
-
 struct DwGrid {
     int wg_begin[5];  // prefix over workgroup types (0: W1+W5, 1: W2, 2: W3, 3: W4) of split counts
     int n_split[5];   // slabs per weight matrix (W5 has W1's)
@@ -955,8 +695,262 @@ struct DwGrid {
     int slab_len[5];  // rows*cols + rows
 };
 
-__global__ __launch_bounds__(256, 1) void k_mlp_dw(int64_t m, DwSrc src, DwGrid g, float *__restrict__ slabs,
-                                                   int wg_offset) {
+// ---------------------------------------------------------------------------
+// weight gradients: dW_L = Σ_s δ_L[:, s] ⊗ a_{L-1}[:, s] (+ biases, the W3 sdf
+// row, W5), split-K over 32-sample CF tiles: workgroup (layer L, split) sums
+// a contiguous range of tiles into its slab; k_mlp_dw_reduce adds the slabs.
+// Tiles stream through a ring of 4 LDS stages with three in flight while one
+// is consumed (straight 1-KB global_load_lds copies: the CF tile IS the
+// operand image; the x rows and per-sample weights come by 4-B gathers whose
+// out-of-range samples read a zero block), so the copy engine, not a layout
+// pass, sits between HBM and the MFMAs.  8 waves (2 per SIMD): L1..L3 wave w
+// owns rows {2(w>>2), 2(w>>2)+1} × column w&3 (32 × 32 blocks), the x
+// columns of W4 on waves with (w&3) < 2; L0 (W1, 4 row blocks) runs its MFMAs
+// on waves 0..3 and W5 = δ5 ⊗ c1 on waves 4..7.  Bias sums and the W3 sdf row
+// ride on the MFMA operands already in registers.  One barrier per tile;
+// per-wave copy counts are uniform, so the wait is a compile-time vmcnt.
+constexpr int kDw2Waves = 8;
+constexpr int kS2D = 0, kS2A = 128 * kTileS, kS2S = kS2A + kDwA * kTileS, kStage2 = kS2S + 64 * kDw2Waves;
+constexpr int kDw2Stages = 4;
+constexpr int kDw2Lds = kDw2Stages * kStage2;  // 155,648 B
+static_assert(kDw2Lds * 4 <= 160 * 1024, "dw2 LDS budget");
+
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+    asm volatile("" ::: "memory");
+}
+
+// rows [r0, r0+8) of a CF tile → stage rows [dr0, dr0+8): one 1-KB copy
+// (dr0 ≡ r0 mod 16, so the row swizzle carries over)
+__device__ __forceinline__ void s2_rows(float *stage, const float *tile, int r0, int dr0, int lane) {
+    glds16(tile + r0 * kTileS + lane * 4, stage + dr0 * kTileS);
+}
+
+// tile-local sample of logical group g (= h·4 + t4), element e
+__device__ __forceinline__ int s2_sample(int g, int e) { return 2 * (4 * (g & 3) + e) + (g >> 2); }
+
+// x features k0, k0+1 → A rows arow0, arow0+1 (2 rows × 32 floats per wave instruction)
+__device__ __forceinline__ void s2_x(float *stage, const float *feat, const float *zblk, int64_t s0, int64_t m, int k0,
+                                     int arow0, int lane) {
+    const int dr = arow0 + (lane >> 5), q = lane & 31, k = k0 + (lane >> 5);
+    const int g = (q >> 2) ^ ((dr >> 1) & 7), e = q & 3;
+    const int64_t sg = s0 + s2_sample(g, e);
+    glds4(sg < m ? feat + sg * 16 + k : zblk, stage + kS2A + arow0 * kTileS);
+}
+
+template <int L>
+__device__ __forceinline__ void dw2_issue(const DwSrc &src, const float *zblk, int64_t t, int64_t m, float *stage,
+                                          int wave, int lane) {
+    const float *dt = src.D[L] + t * kCfTile;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) s2_rows(stage + kS2D, dt, (8 * i + wave) * 8, (8 * i + wave) * 8, lane);
+    if (L == 1 || L == 2 || L == 3) {
+        const float *at = src.A[L] + t * kCfTile;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) s2_rows(stage + kS2A, at, (8 * i + wave) * 8, (8 * i + wave) * 8, lane);
+    }
+    if (L == 0) {  // c1 → A rows 32..159
+        const float *at = src.c1 + t * kCfTile;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) s2_rows(stage + kS2A, at, (8 * i + wave) * 8, 32 + (8 * i + wave) * 8, lane);
+    }
+    const int64_t s0 = t * kTileS;
+    if (L == 0 || L == 3) {  // x: 16 rows, one 2-row instruction per wave
+        const int rbase = (L == 0) ? 0 : 128;
+        s2_x(stage, src.feat, zblk, s0, m, 2 * wave, rbase + 2 * wave, lane);
+    }
+    if (L == 0 || L == 2) {  // per-sample weights [ch][h][16] (δ5 for L0, g_sdf for L2)
+        const int idx = wave * 64 + lane;
+        const int nch = (L == 0) ? 3 : 1;
+        const float *srcp = zblk;
+        if (idx < 32 * nch) {
+            const int ch = idx >> 5, q = idx & 31;
+            const int64_t sg = s0 + 2 * (q & 15) + (q >> 4);
+            if (sg < m) srcp = (L == 0) ? src.d5 + sg * 3 + ch : src.g_sdf + sg;
+        }
+        glds4(srcp, stage + kS2S + wave * 64);
+    }
+}
+
+template <int L>
+constexpr int dw2_count() { return 2 + ((L == 0) ? 2 + 1 + 1 : (L == 3) ? 2 + 1 : (L == 2) ? 2 + 1 : 2); }
+
+template <int L>
+__device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const float *zblk, int split, int n_split,
+                                          float *slab, float *slab5, float *lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = lane & 31, h = lane >> 5;
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u_beg = n_units * split / n_split, u_end = n_units * (split + 1) / n_split;
+    constexpr int NR = (L == 0) ? 1 : 2;
+    constexpr int NC = 1;
+    constexpr bool XBLK = (L == 3);
+    constexpr int NOP = NR + NC + (XBLK ? 1 : 0);
+    constexpr int NI = dw2_count<L>();
+    int rb[NR], cb[NC];
+    if (L == 0) {
+        rb[0] = wave & 3;
+        cb[0] = 0;
+    } else {
+        rb[0] = 2 * (wave >> 2);
+        rb[NR - 1] = 2 * (wave >> 2) + 1;
+        cb[0] = wave & 3;
+    }
+    const bool mfma_wave = (L != 0) || wave < 4;
+    const bool xwave = XBLK && (wave & 3) < 2;
+    const int xsel = wave & 1;
+    const bool own_bias = (L == 0) ? wave < 4 : ((wave & 3) == 0);  // D rows summed once
+    const bool own_sdf = (L == 2) && ((wave >> 2) == 0);             // A columns dotted once
+    f32x16 acc[NR][NC];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) zero(acc[i]);
+    f32x16 accx[1];
+    zero(accx);
+    float bsum[NR], sdfp[NC];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) bsum[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) sdfp[j] = 0.f;
+    float w5[3] = {0.f, 0.f, 0.f}, vb = 0.f;  // L0: W5 partials; db5 (L0) / db3[0] (L2) partials
+    // rows no copy writes: W1 rows 16..31, W4 rows 144..159
+    if (L == 0 || L == 3) {
+        const int r0 = (L == 0) ? 16 : 144;
+        for (int e = threadIdx.x; e < 16 * kTileS; e += 64 * kDw2Waves)
+#pragma unroll
+            for (int st = 0; st < kDw2Stages; ++st) lds[st * kStage2 + kS2A + r0 * kTileS + e] = 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kDw2Stages - 1; ++k)
+        if (u_beg + k < u_end) dw2_issue<L>(src, zblk, u_beg + k, m, lds + k * kStage2, wave, lane);
+    for (int64_t u = u_beg; u < u_end; ++u) {
+        float *st = lds + ((int)((u - u_beg) & (kDw2Stages - 1))) * kStage2;
+        // tile u landed for this wave: only the newer in-flight tiles may still be outstanding
+        const int64_t ahead = (u_end - 1 - u) < (kDw2Stages - 2) ? (u_end - 1 - u) : (kDw2Stages - 2);
+        if (ahead >= 2) wait_vm_c<2 * NI>();
+        else if (ahead == 1) wait_vm_c<NI>();
+        else wait_vm_c<0>();
+        raw_barrier();  // ... for every wave; and every wave is done with tile u-1's stage
+        if (u + kDw2Stages - 1 < u_end)
+            dw2_issue<L>(src, zblk, u + kDw2Stages - 1, m,
+                         lds + ((int)((u + kDw2Stages - 1 - u_beg) & (kDw2Stages - 1))) * kStage2, wave, lane);
+        const float *Dl = st + kS2D, *Al = st + kS2A, *Sl = st + kS2S;
+        if (L == 0 && wave >= 4) {  // W5 = δ5 ⊗ c1 (A rows 32..159): thread = (c1 row, k-half); db5
+            const int tw = threadIdx.x - 256;
+            const int row = 32 + (tw & 127), hh = tw >> 7;
+#pragma unroll
+            for (int t4 = 0; t4 < 4; ++t4) {
+                const float4 a = *reinterpret_cast<const float4 *>(Al + cf_row_slot(row, hh * 4 + t4));
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float4 w = *reinterpret_cast<const float4 *>(Sl + ch * 32 + hh * 16 + 4 * t4);
+                    w5[ch] += (a.x * w.x + a.y * w.y) + (a.z * w.z + a.w * w.w);
+                }
+            }
+            if (wave < 7 && lane < 32) vb += Sl[(wave - 4) * 32 + lane];
+        }
+        if (L == 2 && wave == 0 && lane < 32) vb += Sl[lane];  // db3[0] = Σ g_sdf
+        if (mfma_wave) {
+            // MFMAs; the operands of k-group t4+1 are read before the MFMAs of t4
+            auto load = [&](int t4, float4 (&o)[NOP]) {
+#pragma unroll
+                for (int i = 0; i < NR; ++i)
+                    o[i] = *reinterpret_cast<const float4 *>(Dl + cf_row_slot(32 * rb[i] + x, h * 4 + t4));
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    o[NR + j] = *reinterpret_cast<const float4 *>(Al + cf_row_slot(32 * cb[j] + x, h * 4 + t4));
+                if (XBLK) o[NOP - 1] = *reinterpret_cast<const float4 *>(Al + cf_row_slot(128 + x, h * 4 + t4));
+            };
+            float4 cur[NOP];
+            load(0, cur);
+#pragma unroll
+            for (int t4 = 0; t4 < 4; ++t4) {
+                float4 nxt[NOP];
+                if (t4 + 1 < 4) load(t4 + 1, nxt);
+                const float4 dx = (XBLK && NR > 1 && xsel) ? cur[NR - 1] : cur[0];
+#define PSVO_DW2_K(c)                                                                                         \
+                _Pragma("unroll") for (int i = 0; i < NR; ++i)                                                \
+                    _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(cur[i].c, cur[NR + j].c, acc[i][j]); \
+                if (xwave) accx[0] = mfma(dx.c, cur[NOP - 1].c, accx[0]);
+                PSVO_DW2_K(x)
+                PSVO_DW2_K(y)
+                PSVO_DW2_K(z)
+                PSVO_DW2_K(w)
+#undef PSVO_DW2_K
+                if (own_bias) {
+#pragma unroll
+                    for (int i = 0; i < NR; ++i) bsum[i] += (cur[i].x + cur[i].y) + (cur[i].z + cur[i].w);
+                }
+                if (L == 2 && own_sdf) {
+                    const float4 w = *reinterpret_cast<const float4 *>(Sl + h * 16 + 4 * t4);
+#pragma unroll
+                    for (int j = 0; j < NC; ++j)
+                        sdfp[j] += (cur[NR + j].x * w.x + cur[NR + j].y * w.y) +
+                                   (cur[NR + j].z * w.z + cur[NR + j].w * w.w);
+                }
+                if (t4 + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, NOP, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4 * NR * NC, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t4 + 1 < 4) {
+#pragma unroll
+                    for (int i = 0; i < NOP; ++i) cur[i] = nxt[i];
+                }
+            }
+        }
+    }
+    wait_vm_c<0>();
+    // ---- the slab: [rows][cols] weights, then [rows] bias
+    constexpr int ROWS = (L == 2) ? 129 : 128;
+    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
+    constexpr int ROW_OFF = (L == 2) ? 1 : 0;
+    if (mfma_wave) dw_store<NR, NC>(slab, COLS, ROW_OFF, COLS, rb, cb, acc, lane);
+    if (xwave) {
+        const int rbx[1] = {rb[xsel]}, cbx[1] = {4};
+        const f32x16 tmp[1][1] = {{accx[0]}};
+        dw_store<1, 1>(slab, COLS, 0, COLS, rbx, cbx, tmp, lane);
+    }
+    float *bias = slab + ROWS * COLS;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+        if (own_bias && h == 0) bias[ROW_OFF + 32 * rb[i] + x] = v;
+    }
+    if (L == 2) {
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const float v = sdfp[j] + __shfl_xor(sdfp[j], 32, 64);
+            if (own_sdf && h == 0) slab[32 * cb[j] + x] = v;  // sdf row = row 0
+        }
+        float b = vb;  // lanes 0..31 of wave 0: partial Σ g_sdf
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
+        if (wave == 0 && lane == 0) bias[0] = b;
+    }
+    if (L == 0) {
+        __syncthreads();  // the stages are free: combine the two k-halves of W5 through LDS
+        float *red = lds;
+        const int tw = threadIdx.x - 256;
+        if (tw >= 128) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) red[ch * 128 + (tw - 128)] = w5[ch];
+        }
+        __syncthreads();
+        if (tw >= 0 && tw < 128) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) slab5[ch * 128 + tw] = w5[ch] + red[ch * 128 + tw];
+        }
+        float b = vb;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
+        if (wave >= 4 && wave < 7 && lane == 0) slab5[3 * 128 + (wave - 4)] = b;
+    }
+}
+
+__global__ __launch_bounds__(64 * kDw2Waves, 1) void k_mlp_dw2(int64_t m, DwSrc src, const float *__restrict__ zblk,
+                                                               DwGrid g, float *__restrict__ slabs, int wg_offset) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wg = blockIdx.x + wg_offset;
     int L = 0;
@@ -967,14 +961,13 @@ __global__ __launch_bounds__(256, 1) void k_mlp_dw(int64_t m, DwSrc src, DwGrid 
     float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
     float *slab5 = slabs + g.slab_off[4] + (int64_t)split * g.slab_len[4];
     switch (L) {
-        case 0: dw_layer<0>(m, src, split, n_split, slab, slab5, lds); break;
-        case 1: dw_layer<1>(m, src, split, n_split, slab, slab5, lds); break;
-        case 2: dw_layer<2>(m, src, split, n_split, slab, slab5, lds); break;
-        default: dw_layer<3>(m, src, split, n_split, slab, slab5, lds); break;
+        case 0: dw2_layer<0>(m, src, zblk, split, n_split, slab, slab5, lds); break;
+        case 1: dw2_layer<1>(m, src, zblk, split, n_split, slab, slab5, lds); break;
+        case 2: dw2_layer<2>(m, src, zblk, split, n_split, slab, slab5, lds); break;
+        default: dw2_layer<3>(m, src, zblk, split, n_split, slab, slab5, lds); break;
     }
 }
 
-// grads of layer l = Σ over its splits (fixed order); one thread per element.
 struct DwDst {
     float *w[5], *b[5];
     int rows[5], cols[5];
@@ -1311,17 +1304,17 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-// relative per-chunk time of the workgroup types (W1+W5, W2, W3, W4), measured standalone
-static const int kDwWeight[4] = {46, 50, 58, 68};
+// relative per-tile time of the workgroup types (W1+W5, W2, W3, W4), measured standalone
+static const int kDw2Weight[4] = {29, 53, 56, 79};
 
-// split counts per workgroup type ∝ cost, n_split ≈ number of CUs in total
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
-    const int64_t chunks = (m + kCh - 1) / kCh;
+    const int64_t chunks = (m + kTileS - 1) / kTileS;  // split units: CF tiles
+    const int *kDwWeightSel = kDw2Weight;
     int wsum = 0;
-    for (int l = 0; l < 4; ++l) wsum += kDwWeight[l];
+    for (int l = 0; l < 4; ++l) wsum += kDwWeightSel[l];
     int wg = 0;
     for (int l = 0; l < 4; ++l) {
-        int sp = (int)((int64_t)n_split * kDwWeight[l] / wsum);
+        int sp = (int)((int64_t)n_split * kDwWeightSel[l] / wsum);
         if (sp < 1) sp = 1;
         if (sp > chunks) sp = (int)(chunks > 0 ? chunks : 1);
         g->wg_begin[l] = wg;
@@ -1409,18 +1402,18 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     src.g_sdf = g_sdf;
     static bool dw_attr = false;
     if (!dw_attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_dw),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwLds * 4);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_dw2),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDw2Lds * 4);
         dw_attr = true;
     }
+    const float *zblk = images + kImgVec + kOffW;  // zero floats of the vector image (k_mlp_prep)
     // PSVO_DW_LAYER=1 (profiling aid): launch each layer's workgroups as their own dispatch
     static const char *only = getenv("PSVO_DW_LAYER");
-    if (only && *only) {
-        for (int l = 0; l < 4; ++l)
-            hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[l + 1] - g.wg_begin[l]), dim3(256), kDwLds * 4, st, m, src,
-                               g, slabs, g.wg_begin[l]);
-    } else {
-        hipLaunchKernelGGL(k_mlp_dw, dim3(g.wg_begin[4]), dim3(256), kDwLds * 4, st, m, src, g, slabs, 0);
+    const int n_launch = (only && *only) ? 4 : 1;
+    for (int l = 0; l < n_launch; ++l) {
+        const int wg0 = n_launch == 1 ? 0 : g.wg_begin[l];
+        const int nwg = n_launch == 1 ? g.wg_begin[4] : g.wg_begin[l + 1] - g.wg_begin[l];
+        hipLaunchKernelGGL(k_mlp_dw2, dim3(nwg), dim3(64 * kDw2Waves), kDw2Lds * 4, st, m, src, zblk, g, slabs, wg0);
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
