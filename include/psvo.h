@@ -292,6 +292,27 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * embedding gradient is zeroed as it is consumed). */
 int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step);
 
+/* ---- octree builder on the device (csrc/octree_gpu.hip) ----------------
+ * The same tree as psvo_octree_* (Octree::insert, octree.cpp:104-294: ids in
+ * creation order, root 0, SURFACE leaf + 7 FEATURE corner leaves per voxel)
+ * built in HBM by a hash-and-scan construction, incrementally across
+ * inserts; export writes get_centres_and_children (octree.cpp:561-687) and /
+ * or the renderer's map_states arrays (mapping.py:328-372) on the device.
+ * vox / hit / outputs are device pointers; rows = psvo_dtree_count(). */
+void *psvo_dtree_new(void *stream, int grid_dim, int64_t capacity);
+void psvo_dtree_free(void *tree);
+int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64_t n);
+int64_t psvo_dtree_count(void *tree);
+int64_t psvo_dtree_count_leaves(void *tree, void *stream);
+/* any output may be NULL: voxels f32[N,4], children f32[N,8], features i32[N,8]
+ * (get_centres_and_children), centres f32[N,3] = (xyz + side/2)·voxel_size,
+ * structure i32[N,9] = [children | side] (map_states) */
+int psvo_dtree_export(void *tree, void *stream, float voxel_size, float *voxels, float *children, int *features,
+                      float *centres, int *structure);
+/* hit[i·corners + j] = leaf at voxel i's corner j exists (corners 1: has_voxel,
+ * 8: the corner keys try_insert counts, octree.cpp:381-474) */
+int psvo_dtree_probe(void *tree, void *stream, const int *vox, int64_t n, int corners, int *hit);
+
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);
 void psvo_octree_free(void *tree);

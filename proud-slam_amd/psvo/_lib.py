@@ -53,6 +53,13 @@ _SIGNATURES = {
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
     "psvo_map_grad_floats": (_i64, [_i64]),
+    "psvo_dtree_new": (_vp, [_vp, _i32, _i64]),
+    "psvo_dtree_free": (None, [_vp]),
+    "psvo_dtree_insert": (_i32, [_vp, _vp, _vp, _i64]),
+    "psvo_dtree_count": (_i64, [_vp]),
+    "psvo_dtree_count_leaves": (_i64, [_vp, _vp]),
+    "psvo_dtree_export": (_i32, [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
+    "psvo_dtree_probe": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
     "psvo_octree_free": (None, [_vp]),
     "psvo_octree_insert": (_i32, [_vp, _vp, _i64]),
