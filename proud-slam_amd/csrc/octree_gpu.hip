@@ -89,10 +89,14 @@ struct DtTable {
     uint64_t mask;  // capacity - 1 (power of two)
 };
 
-// slot of `k`, inserting it if absent
+constexpr int kDtMaxProbe = 256;
+constexpr uint64_t kDtNoSlot = ~0ull;
+
+// slot of `k`, inserting it if absent; kDtNoSlot if the probe run exceeds
+// kDtMaxProbe (the host grows the table and redoes the batch)
 __device__ __forceinline__ uint64_t dt_insert(const DtTable &t, uint64_t k) {
     uint64_t s = dt_hash(k) & t.mask;
-    for (;;) {
+    for (int probe = 0; probe < kDtMaxProbe; ++probe) {
         const unsigned long long cur = t.key[s];
         if (cur == k) return s;
         if (cur == kEmptyKey) {
@@ -101,15 +105,17 @@ __device__ __forceinline__ uint64_t dt_insert(const DtTable &t, uint64_t k) {
         }
         s = (s + 1) & t.mask;
     }
+    return kDtNoSlot;
 }
 __device__ __forceinline__ int64_t dt_find(const DtTable &t, uint64_t k) {
     uint64_t s = dt_hash(k) & t.mask;
-    for (;;) {
+    for (int probe = 0; probe < kDtMaxProbe; ++probe) {
         const unsigned long long cur = t.key[s];
         if (cur == k) return (int64_t)s;
         if (cur == kEmptyKey) return -1;
         s = (s + 1) & t.mask;
     }
+    return -1;
 }
 
 __constant__ int kDtIncX[8] = {0, 0, 0, 0, 1, 1, 1, 1};
@@ -147,12 +153,14 @@ __global__ void k_dt_rehash(DtTable t, DtNodes nd, int64_t n, int D) {
     const int x = (int)dt_squeeze3(c), y = (int)dt_squeeze3(c >> 1), z = (int)dt_squeeze3(c >> 2);
     const int d = D - (31 - __clz(nd.side[i]));  // side = size >> d
     const uint64_t s = dt_insert(t, dt_key(x, y, z, d, D));
+    if (s == kDtNoSlot) return;  // cannot happen below load 1/2 (the table holds >= 2 slots per node)
     t.id[s] = (int)i;
     if (nd.type[i] == kDtSurface) t.flags[s] = 1u;
 }
 
 // 1. keys + min walk + SURFACE flags
-__global__ void k_dt_walk(DtTable t, const int *__restrict__ vox, int64_t n_walks, int D, unsigned w_base) {
+__global__ void k_dt_walk(DtTable t, const int *__restrict__ vox, int64_t n_walks, int D, unsigned w_base,
+                          int *__restrict__ overflow) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_walks * D) return;
     const int64_t w = e / D;
@@ -161,8 +169,15 @@ __global__ void k_dt_walk(DtTable t, const int *__restrict__ vox, int64_t n_walk
     const int j = (int)(w & 7);
     const int x = vox[3 * i] + kDtIncX[j], y = vox[3 * i + 1] + kDtIncY[j], z = vox[3 * i + 2] + kDtIncZ[j];
     const uint64_t s = dt_insert(t, dt_key(x, y, z, d, D));
-    atomicMin(t.minw + s, w_base + (unsigned)w);
-    if (d == D && j == 0) atomicOr(t.flags + s, 1u);
+    if (s == kDtNoSlot) {
+        *overflow = 1;
+        return;
+    }
+    // the shallow keys are shared by nearly every walk: a plain read first
+    // keeps the same-address atomics (which serialise) to the few that can win
+    const unsigned wv = w_base + (unsigned)w;
+    if (wv < __atomic_load_n(t.minw + s, __ATOMIC_RELAXED)) atomicMin(t.minw + s, wv);
+    if (d == D && j == 0 && !(__atomic_load_n(t.flags + s, __ATOMIC_RELAXED) & 1u)) atomicOr(t.flags + s, 1u);
 }
 
 // 2. creator flags (w, d order)
@@ -349,7 +364,7 @@ struct psvo_dtree {
     unsigned w_next = 0;  // walk counter across inserts (min-walk order stays global)
     DtTable t{};
     DtNodes nd{};
-    int *scratch = nullptr;  // flags | ranks | totals | sum
+    int *scratch = nullptr;  // flags | ranks | totals | sum | overflow
     int64_t scratch_n = 0;
 };
 
@@ -381,9 +396,9 @@ int dt_alloc_nodes(psvo_dtree *tr, int64_t cap, hipStream_t st) {
     return PSVO_OK;
 }
 
-int dt_alloc_table(psvo_dtree *tr, hipStream_t st) {
+int dt_alloc_table(psvo_dtree *tr, hipStream_t st, uint64_t min_slots) {
     uint64_t slots = 1024;
-    while (slots < (uint64_t)tr->cap * 2) slots <<= 1;
+    while (slots < min_slots || slots < (uint64_t)tr->count * 2) slots <<= 1;
     DtTable t{};
     if (hipMalloc(&t.key, slots * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&t.minw, slots * sizeof(unsigned)) != hipSuccess || hipMalloc(&t.id, slots * sizeof(int)) != hipSuccess ||
@@ -418,7 +433,8 @@ extern "C" void *psvo_dtree_new(void *stream, int grid_dim, int64_t capacity) {
     while ((1 << D) < grid_dim) ++D;
     tr->D = D;
     tr->shift = kDtMaxBits - D - 1;
-    if (dt_alloc_nodes(tr, capacity > 1024 ? capacity : 1024, st) != PSVO_OK || dt_alloc_table(tr, st) != PSVO_OK) {
+    const int64_t cap0 = capacity > 1024 ? capacity : 1024;
+    if (dt_alloc_nodes(tr, cap0, st) != PSVO_OK || dt_alloc_table(tr, st, (uint64_t)cap0 * 2) != PSVO_OK) {
         delete tr;
         return nullptr;
     }
@@ -463,17 +479,8 @@ extern "C" int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64
     const int64_t n_walks = n * 8, ne = n_walks * tr->D;
     PSVO_REQUIRE(ne < (int64_t)1 << 31 && (uint64_t)tr->w_next + (uint64_t)n_walks < 0xffffffffull,
                  "dtree_insert: batch too large (%lld voxels)", (long long)n);
-    // capacity: every (walk, depth) could create a node
-    if (tr->count + ne > tr->cap) {
-        int64_t cap = tr->cap;
-        while (cap < tr->count + ne) cap *= 2;
-        int rc = dt_alloc_nodes(tr, cap, st);
-        if (rc) return rc;
-        rc = dt_alloc_table(tr, st);
-        if (rc) return rc;
-    }
     const int64_t nb = div_up(ne, 1024);
-    const int64_t need = 2 * ne + nb + 1;
+    const int64_t need = 2 * ne + nb + 2;
     if (need > tr->scratch_n) {
         (void)hipStreamSynchronize(st);
         (void)hipFree(tr->scratch);
@@ -481,20 +488,46 @@ extern "C" int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64
             return set_error(PSVO_E_LAUNCH, "dtree_insert: out of device memory");
         tr->scratch_n = need;
     }
-    int *flag = tr->scratch, *rank = flag + ne, *totals = rank + ne, *sum = totals + nb;
+    int *flag = tr->scratch, *rank = flag + ne, *totals = rank + ne, *sum = totals + nb, *overflow = sum + 1;
     const dim3 g(div_up(ne, 256)), b(256);
-    hipLaunchKernelGGL(k_dt_walk, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next);
+    // table: about 2.4 new nodes per voxel on surface scans; keep load <= 1/2
+    // for that and grow (rehash from the node arrays, batch redone) if a
+    // probe run still overflows
+    uint64_t want = 2 * (uint64_t)(tr->count + 3 * n);
+    for (int attempt = 0;; ++attempt) {
+        if (want > tr->t.mask + 1) {
+            int rc = dt_alloc_table(tr, st, want);
+            if (rc) return rc;
+        }
+        int ov = 0;
+        (void)hipMemsetAsync(overflow, 0, sizeof(int), st);
+        hipLaunchKernelGGL(k_dt_walk, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, overflow);
+        if (hipMemcpyAsync(&ov, overflow, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "dtree_insert: walk failed (%s)", hipGetErrorString(hipGetLastError()));
+        if (!ov) break;
+        if (attempt >= 6) return set_error(PSVO_E_OVERFLOW, "dtree_insert: hash table overflow");
+        want = 4 * (tr->t.mask + 1);
+        int rc = dt_alloc_table(tr, st, want);
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(k_dt_flag, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, flag);
     hipLaunchKernelGGL(k_dt_scan_local, dim3(nb), dim3(1024), 0, st, flag, ne, rank, totals);
     hipLaunchKernelGGL(k_dt_scan_totals, dim3(1), dim3(1024), 0, st, totals, nb, sum);
     hipLaunchKernelGGL(k_dt_scan_add, dim3(nb), dim3(1024), 0, st, rank, ne, totals);
-    hipLaunchKernelGGL(k_dt_create, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->shift, tr->size, flag, rank,
-                       tr->count);
-    hipLaunchKernelGGL(k_dt_link, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->size, flag);
     int created = 0;
     if (hipMemcpyAsync(&created, sum, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "dtree_insert: launch failed (%s)", hipGetErrorString(hipGetLastError()));
+        return set_error(PSVO_E_LAUNCH, "dtree_insert: scan failed (%s)", hipGetErrorString(hipGetLastError()));
+    if (tr->count + created > tr->cap) {  // node arrays: exactly what this batch creates
+        int64_t cap = tr->cap;
+        while (cap < tr->count + created) cap *= 2;
+        int rc = dt_alloc_nodes(tr, cap, st);
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_dt_create, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->shift, tr->size, flag, rank,
+                       tr->count);
+    hipLaunchKernelGGL(k_dt_link, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->size, flag);
     tr->count += created;
     tr->w_next += (unsigned)n_walks;
     return check_launch("dtree_insert");

@@ -17,6 +17,12 @@ import torch
 from . import _lib as L
 
 
+def _zeros_view(n, k, c, device="cpu"):
+    """[n, k, c] zeros without the memory: the per-node point samples the
+    reference exports (octree.cpp:641-655) feed only disabled paths."""
+    return torch.zeros((1, 1, 1), dtype=torch.float32, device=device).expand(n, k, c)
+
+
 class Octree:
     def __init__(self):
         self._h = None
@@ -88,9 +94,8 @@ class Octree:
     def get_centres_and_children(self):
         v, c, f = self.export_arrays()
         n = v.shape[0]
-        return (torch.from_numpy(v), torch.from_numpy(c), torch.from_numpy(f),
-                torch.zeros((n, self.max_num, 4), dtype=torch.float32),
-                torch.zeros((n, self.max_num, 3), dtype=torch.float32))
+        return (torch.from_numpy(v), torch.from_numpy(c), torch.from_numpy(f), _zeros_view(n, self.max_num, 4),
+                _zeros_view(n, self.max_num, 3))
 
     def get_leaf_voxels(self):
         v, _, f = self.export_arrays()
@@ -202,8 +207,7 @@ class DeviceOctree:
     def get_centres_and_children(self):
         v, c, f = self.export_arrays()
         n = v.shape[0]
-        return (v, c, f, torch.zeros((n, self.max_num, 4), dtype=torch.float32, device=self.device),
-                torch.zeros((n, self.max_num, 3), dtype=torch.float32, device=self.device))
+        return (v, c, f, _zeros_view(n, self.max_num, 4, self.device), _zeros_view(n, self.max_num, 3, self.device))
 
     def render_arrays(self, voxel_size):
         """map_states' (voxel_center_xyz f32[N,3], voxel_structure i32[N,9],
@@ -242,8 +246,8 @@ def map_states(tree: Octree, embeddings: torch.Tensor, voxel_size: float, device
             "voxel_center_xyz": centres.to(dev),
             "voxel_structure": structure.to(dev),
             "voxel_vertex_emb": embeddings,
-            "pointclouds_xyz": torch.zeros((n, tree.max_num, 4), dtype=torch.float32),
-            "pointclouds_color": torch.zeros((n, tree.max_num, 3), dtype=torch.float32),
+            "pointclouds_xyz": _zeros_view(n, tree.max_num, 4),
+            "pointclouds_color": _zeros_view(n, tree.max_num, 3),
         }
     voxels, children, features, pcd_xyz, pcd_color = tree.get_centres_and_children()
     centres = (voxels[:, :3] + voxels[:, -1:] / 2) * voxel_size
