@@ -172,9 +172,10 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
  * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
  * `images` (psvo_mlp_image_floats() floats) receives the weights' LDS operand
  * images, rebuilt by every call; psvo_mlp_bwd reuses them (same weights).
- * Training mode: act f32[4][ceil(M/64)*64*128] (h1, h2, f, c1; chunk-feature-major, see mlp.hip) and
- * masks u64[M][2][3]
- * (ReLU masks) are written for psvo_mlp_bwd; pass NULL for both otherwise. */
+ * Training mode: masks u64[M][2][3] (ReLU masks, needed by any psvo_mlp_bwd)
+ * and act f32[4][ceil(M/64)*64*128] (h1, h2, f, c1 in 32-sample CF tiles, see
+ * mlp.hip; needed only for weight gradients) are written when non-NULL;
+ * act requires masks.  Inference: both NULL. */
 int64_t psvo_mlp_image_floats(void);
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
@@ -187,7 +188,9 @@ int64_t psvo_mlp_workspace_floats(int64_t m, int n_split);
 /* Backward given g_sdf[M], g_rgb[M,3] and the training forward's rgb / act /
  * masks: writes dfeat[M,16] and the 10 parameter gradients (overwrite, or
  * add when `accumulate`); split-K over ~n_split sample ranges with a
- * deterministic slab reduction. */
+ * deterministic slab reduction.  gw1 == NULL (frozen decoder, e.g.
+ * tracking): dfeat only — act may then be NULL and the other gradient
+ * pointers are ignored. */
 int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                  const float *b4, const float *w5, const float *b5, const float *images, const float *rgb,

@@ -97,6 +97,8 @@ struct BwdPass {  // per-wave LDS: one 16-sample pass
 // atomic instructions, each covering four whole 64-B rows — one memory-side
 // request per row, the shape global f32 atomics run at full rate with
 // (MI355X_MICROARCH.md, global float atomics).
+// EMB = false: pose-only backward (tracking, frozen embeddings): d_o / d_d only
+template <bool EMB>
 __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
                                                     const int *__restrict__ ray_index,
                                                     const int *__restrict__ leaf, const float *__restrict__ t,
@@ -156,8 +158,8 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         corner_weights(p[0], p[1], p[2], w);
         // stage this pass for the run sums
         wave_lds_sync();  // the previous pass's readers are done
-        *reinterpret_cast<float4 *>(&B.g[sub][4 * q]) = g;
-        if (q == 0) {
+        if (EMB) *reinterpret_cast<float4 *>(&B.g[sub][4 * q]) = g;
+        if (EMB && q == 0) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 B.w[sub][k] = w[k];
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         }
         wave_lds_sync();
         // run sums over the pass's valid slots (wave-uniform loop)
-        const int n_slots = min(16, end - base);
+        const int n_slots = EMB ? min(16, end - base) : 0;
         for (int sl = 0; sl < n_slots; ++sl) {
             const int lf_s = B.leaf[sl];
             if (lf_s != cur_leaf) {
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
             acc1 += B.w[sl][ek0 + 4] * gv;
         }
     }
-    if (cur_leaf >= 0) {
+    if (EMB && cur_leaf >= 0) {
         atomicAdd(grad_emb + (int64_t)cur_v0 * 16 + ed, acc0);
         atomicAdd(grad_emb + (int64_t)cur_v1 * 16 + ed, acc1);
     }
@@ -267,10 +269,17 @@ extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_s
                                const float *grad_feat, float *grad_emb, float *grad_o, float *grad_d) {
     PSVO_REQUIRE(d == 16, "interp_bwd: embedding dim %d unsupported (16 only)", d);
     PSVO_REQUIRE(r_hit >= 0 && voxel_size > 0.f, "interp_bwd: bad sizes");
+    PSVO_REQUIRE(grad_o != nullptr && grad_d != nullptr, "interp_bwd: grad_o / grad_d required");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_interp_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, voxel_size,
-                       offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
-                       reinterpret_cast<const float4 *>(emb),
-                       reinterpret_cast<const float4 *>(grad_feat), grad_emb, grad_o, grad_d);
+    if (grad_emb)
+        hipLaunchKernelGGL(k_interp_bwd<true>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+                           voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
+                           reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
+                           grad_emb, grad_o, grad_d);
+    else
+        hipLaunchKernelGGL(k_interp_bwd<false>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+                           voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
+                           reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
+                           nullptr, grad_o, grad_d);
     return check_launch("interp_bwd");
 }

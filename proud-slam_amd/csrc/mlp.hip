@@ -481,14 +481,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     gemm_acc<kNB, kNB>(wl, a, bacc, lane);
     gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
     const uint64_t m4 = relu(bacc);  // c1
-    if (save) {
-        cfs.store(act + 3 * tstride, tbytes, bacc);
-        if (valid) {
-            uint64_t *mk = masks + (s * 2 + h) * 3;
-            mk[0] = m1;
-            mk[1] = m2;
-            mk[2] = m4;
-        }
+    if (save) cfs.store(act + 3 * tstride, tbytes, bacc);
+    if (masks != nullptr && valid) {
+        uint64_t *mk = masks + (s * 2 + h) * 3;
+        mk[0] = m1;
+        mk[1] = m2;
+        mk[2] = m4;
     }
     float rgb[3];
 #pragma unroll
@@ -1025,7 +1023,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const bool save = act != nullptr;
+    const bool save = act != nullptr;         // CF activations (weight gradients)
+    const bool save_mask = masks != nullptr;  // ReLU masks (δ chain)
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF 32-sample tiles
     const int64_t tstride = n_tiles * 32 * 128;
     const int64_t tbytes = tstride * 4;
@@ -1085,14 +1084,12 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
         gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
         ++seq;
         const uint64_t m4 = relu(bacc);
-        if (save) {
-            cfs.store(act + 3 * tstride, tbytes, bacc);
-            if (valid) {
-                uint64_t *mk = masks + (s * 2 + h) * 3;
-                mk[0] = m1;
-                mk[1] = m2;
-                mk[2] = m4;
-            }
+        if (save) cfs.store(act + 3 * tstride, tbytes, bacc);
+        if (save_mask && valid) {
+            uint64_t *mk = masks + (s * 2 + h) * 3;
+            mk[0] = m1;
+            mk[1] = m2;
+            mk[2] = m4;
         }
         float rgb[3];
 #pragma unroll
@@ -1191,7 +1188,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
             }
         f32x16 t5[5];
         zero(t5);
-        gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, true, bacc));  // + δc1 stores
+        gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1 stores
         float dxc[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
@@ -1205,14 +1202,14 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
         for (int b = 0; b < kNB; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
-        gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, true, a));  // + δf stores
+        gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
         apply_mask(bacc, m2);
         // ---- W2ᵀ layer (bufA); W1ᵀ → bufB
         wait_vm(0);
         raw_barrier();
         stage8(bufB, img + kImgB1, 4096, wave, lane);
         zero(a);
-        gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, true, bacc));  // + δh2 stores
+        gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2 stores
         apply_mask(a, m1);
         // ---- W1ᵀ layer (bufB); next tile's W4ᵀ → bufA and its inputs
         wait_vm(0);
@@ -1224,7 +1221,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
         }
         f32x16 t1[1];
         zero(t1);
-        gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, true, a));  // + δh1 stores
+        gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
         if (valid) {
             float *dst = o.dfeat + s * kIn;
 #pragma unroll
@@ -1271,7 +1268,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
     PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats floats)");
-    PSVO_REQUIRE((act == nullptr) == (masks == nullptr), "mlp_fwd: act and masks go together");
+    PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd: act needs masks");
     PSVO_REQUIRE(m <= kMaxSamples, "mlp_fwd: m = %lld > %lld (32-bit CF offsets)", (long long)m,
                  (long long)kMaxSamples);
     if (m == 0) return PSVO_OK;
@@ -1353,6 +1350,8 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
     PSVO_REQUIRE(images != nullptr, "mlp_bwd: images of the training forward required");
+    const bool want_w = gw1 != nullptr;  // NULL weight gradients: δ chain / dfeat only (frozen decoder)
+    PSVO_REQUIRE(!want_w || act != nullptr, "mlp_bwd: weight gradients need the forward's activations");
     hipStream_t st = as_stream(stream);
     DwGrid g;
     int slab_floats;
@@ -1367,6 +1366,7 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     o.d5 = ws; ws += m * 3;
     float *slabs = ws;
     o.dfeat = dfeat;
+    if (!want_w) o.d1 = o.d2 = o.d3 = o.d4 = nullptr;  // δ feeds only the weight gradients
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
     if (m > 0) {
         static bool attr = false;
@@ -1393,6 +1393,7 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
         int rc = check_launch("mlp_bwd_data");
         if (rc) return rc;
     }
+    if (!want_w) return PSVO_OK;
     DwSrc src;
     src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4;
     src.A[0] = nullptr; src.A[1] = act; src.A[2] = act + mp * 128; src.A[3] = act + 2 * mp * 128;

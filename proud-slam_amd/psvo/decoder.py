@@ -34,15 +34,18 @@ class DecoderMLP(Function):
         sdf = torch.empty((m,), dtype=torch.float32, device=dev)
         rgb = torch.empty((m, 3), dtype=torch.float32, device=dev)
         ps = [p.contiguous() for p in params]
-        training = any(ctx.needs_input_grad)  # grad mode is off inside Function.forward
+        # grad mode is off inside Function.forward: needs_input_grad tells what backward will want
+        need_w = any(ctx.needs_input_grad[1:])           # weight gradients need the activations
+        training = need_w or ctx.needs_input_grad[0]     # dfeat alone (frozen decoder) needs only the masks
         mp = (m + 63) // 64 * 64  # CF activations: whole 64-sample chunks
-        act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if training else None
+        act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if need_w else None
         masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
         images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=dev)
         with L.timed("mlp_fwd"):
             L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, feat, *ps, images, sdf, rgb, act, masks)
         if training:
             ctx.save_for_backward(feat, rgb, act, masks, images, *ps)
+            ctx.need_w = need_w
         return sdf, rgb
 
     @staticmethod
@@ -55,11 +58,11 @@ class DecoderMLP(Function):
         n_split = 256  # split-K workgroups of the weight gradients (one per CU)
         ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
-        grads = [torch.empty_like(p) for p in ps]
+        grads = [torch.empty_like(p) for p in ps] if ctx.need_w else [None] * len(ps)
         with L.timed("mlp_bwd"):
             L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb, dfeat,
                    *grads, 0, n_split, ws)
-        return (dfeat, *grads)
+        return (dfeat if ctx.needs_input_grad[0] else None, *grads)
 
 
 class _Same(nn.Module):

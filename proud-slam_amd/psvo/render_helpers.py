@@ -88,7 +88,8 @@ class InterpSamples(Function):
         dev = leaf.device
         r_hit = offsets.numel() - 1
         grad_feat = grad_feat.contiguous().float()
-        grad_emb = torch.zeros_like(emb)
+        # frozen embeddings (tracking): the kernel skips the scatter-add
+        grad_emb = torch.zeros_like(emb) if ctx.needs_input_grad[2] else None
         need_od = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         # rows of rays that hit nothing get zero gradient
         god = (torch.zeros if ray_index is not None else torch.empty)((2,) + tuple(rays_o.shape), dtype=torch.float32,

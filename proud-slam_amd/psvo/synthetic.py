@@ -217,6 +217,40 @@ def rays_for_frames(scene: Scene, poses, n_per_frame: int, seed=0):
     return cat(R_o).unsqueeze(0), cat(R_d).unsqueeze(0), cat(GT_c).unsqueeze(0), cat(GT_d).unsqueeze(0)
 
 
+class SyntheticFrame:
+    """An RGBDFrame stand-in (frame.py:10-96 fields track_frame reads): camera
+    ray directions rays_d [H, W, 3] (frame.py:48-58), analytic rgb / depth
+    [H, W] of `scene` seen from pose T, and sample_rays(n) → sample_mask
+    (gumbel top-k over the pixels, sample_util.py:4-20).  `scale` shrinks the
+    Replica intrinsics to keep the frame small."""
+
+    def __init__(self, scene: Scene, T, scale=0.25, seed=0, device="cuda"):
+        K = scene.intrinsics
+        H, W = int(K["H"] * scale), int(K["W"] * scale)
+        fx, fy, cx, cy = K["fx"] * scale, K["fy"] * scale, K["cx"] * scale, K["cy"] * scale
+        iy, ix = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+        d_cam = np.stack([(ix - cx) / fx, (iy - cy) / fy, np.ones_like(ix, dtype=np.float64)], -1).astype(np.float32)
+        Rm = np.asarray(T, np.float64)[:3, :3]
+        d_world = d_cam.reshape(-1, 3).astype(np.float64) @ Rm.T
+        o_world = np.broadcast_to(np.asarray(T, np.float64)[:3, 3], d_world.shape)
+        t, hb = _ray_boxes(o_world, d_world, scene.boxes)
+        t = np.where(np.isfinite(t), t, 0.0)
+        p = o_world + d_world * t[:, None]
+        col = 0.5 + 0.5 * np.sin(np.stack([1.3 * p[:, 0] + 0.7 * hb, 1.7 * p[:, 1], 2.1 * p[:, 2] + 0.3 * hb], -1))
+        self.h, self.w = H, W
+        self.rays_d = torch.from_numpy(d_cam).to(device)
+        self.rgb = torch.from_numpy(col.reshape(H, W, 3).astype(np.float32)).to(device)
+        self.depth = torch.from_numpy(t.reshape(H, W).astype(np.float32)).to(device)
+        self.gen = torch.Generator().manual_seed(seed)
+        self.sample_mask = None
+
+    def sample_rays(self, n):
+        pix = gumbel_topk_pixels(self.h, self.w, n, self.gen)
+        mask = torch.zeros(self.h * self.w, dtype=torch.bool)
+        mask[pix] = True
+        self.sample_mask = mask.view(self.h, self.w).to(self.depth.device)
+
+
 @dataclass
 class Workload:
     scene: Scene

@@ -1,0 +1,135 @@
+"""Tracking path (render_helpers.py:679-761): pose-only
+gradients through the ray → sample → trilinear chain (d_o / d_d of
+k_interp_bwd), with and without tracking's median-filtered depth loss
+(criterion.py:45-50), against the oracle (CPU restatement + torch autograd)
+on the same rays and noise; the frozen-map fast path (no embedding /
+decoder gradients: no scatter-add, no activations, no dW) gives the same
+pose gradient bit for bit; track_frame runs end to end."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CRIT = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+
+
+def _setup():
+    from psvo import synthetic as syn
+    from psvo.octree import Octree
+    scene = syn.room0()
+    tree = Octree()
+    tree.init(scene.grid_dim, 16, scene.voxel_size, 8)
+    tree.insert(syn.surface_voxels(scene, seed=0))
+    v, c, f = tree.export_arrays()
+    g = torch.Generator().manual_seed(3)
+    emb = torch.randn(max(20000, v.shape[0]), 16, generator=g) * 0.2
+    ms_cpu = O.map_states_from_export(v, c, f, scene.voxel_size, emb)
+    T = syn.camera_poses(scene, 1, seed=5)[0]
+    frame = syn.SyntheticFrame(scene, T, scale=0.2, seed=1)
+    return scene, ms_cpu, emb, T, frame
+
+
+def _perturbed(T):
+    from psvo.pose import OptimizablePose
+    from scipy.spatial.transform import Rotation as Rr
+    dT = np.eye(4)
+    dT[:3, :3] = Rr.from_rotvec([0.01, -0.02, 0.015]).as_matrix()
+    dT[:3, 3] = [0.02, -0.01, 0.03]
+    return OptimizablePose.from_matrix(T @ dT)
+
+
+def _rays(pose, frame, mask):
+    dirs = frame.rays_d[mask].to(pose.data.device)
+    rd = (dirs @ pose.rotation().transpose(-1, -2)).unsqueeze(0)
+    ro = pose.translation().reshape(1, 1, -1).expand_as(rd).contiguous()
+    return ro, rd
+
+
+@pytest.mark.parametrize("depth_variance", [False, True])
+def test_pose_gradient_matches_oracle(depth_variance):
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    from psvo.render_helpers import render_rays
+    scene, ms_cpu, emb, T, frame = _setup()
+    frame.sample_rays(1024)
+    mask = frame.sample_mask
+    rgb, depth = frame.rgb[mask], frame.depth[mask]
+    params = O.decoder_params_init(128, seed=2)
+    # oracle (CPU): deterministic noise, returned for the product run
+    pose_o = _perturbed(T)
+    ro, rd = _rays(pose_o, frame, mask.cpu())
+    out_o = O.render_rays(ro, rd, ms_cpu, params, 0.01, scene.voxel_size, 0.1, 10.0, deterministic=True)
+    loss_o, _ = O.criterion(out_o, rgb.cpu().view(1, -1, 3), depth.cpu().view(1, -1), O.REPLICA_CRITERIA, 0.1, 10.0,
+                            weight_depth_loss=depth_variance)
+    loss_o.backward()
+    # product (HIP)
+    pose = _perturbed(T).to(DEV)
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec.load_state_dict(params)
+    ms = {"voxel_center_xyz": ms_cpu["voxel_center_xyz"].to(DEV), "voxel_structure": ms_cpu["voxel_structure"].to(DEV),
+          "voxel_vertex_idx": ms_cpu["voxel_vertex_idx"].to(DEV), "voxel_vertex_emb": emb.to(DEV)}
+    ro, rd = _rays(pose, frame, mask)
+    out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, noise=out_o["noise"])
+    crit = Criterion(types.SimpleNamespace(criteria=dict(CRIT, sdf_truncation=0.1), data_specs={"max_depth": 10.0}))
+    out["ray_mask"] = out["ray_mask"].view(-1)
+    loss, _ = crit(out, (rgb, depth), weight_depth_loss=depth_variance)
+    loss.backward()
+    np.testing.assert_allclose(float(loss), float(loss_o), rtol=1e-4)
+    g, g_o = pose.data.grad.cpu(), pose_o.data.grad
+    assert float((g - g_o).abs().max()) <= 2e-3 * float(g_o.abs().max()), (g, g_o)
+
+
+def test_frozen_map_pose_gradient_is_identical():
+    """requires_grad=False on embeddings / decoder: the pose gradient is the
+    same, bit for bit, as with the full backward."""
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    from psvo.render_helpers import render_rays
+    scene, ms_cpu, emb, T, frame = _setup()
+    frame.sample_rays(1024)
+    mask = frame.sample_mask
+    rgb, depth = frame.rgb[mask], frame.depth[mask]
+    crit = Criterion(types.SimpleNamespace(criteria=dict(CRIT, sdf_truncation=0.1), data_specs={"max_depth": 10.0}))
+    torch.manual_seed(0)
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    grads = []
+    for frozen in (False, True):
+        e = emb.to(DEV).requires_grad_(not frozen)
+        for p in dec.parameters():
+            p.requires_grad_(not frozen)
+            p.grad = None
+        ms = {"voxel_center_xyz": ms_cpu["voxel_center_xyz"].to(DEV),
+              "voxel_structure": ms_cpu["voxel_structure"].to(DEV),
+              "voxel_vertex_idx": ms_cpu["voxel_vertex_idx"].to(DEV), "voxel_vertex_emb": e}
+        pose = _perturbed(T).to(DEV)
+        ro, rd = _rays(pose, frame, mask)
+        out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, seed=11)
+        out["ray_mask"] = out["ray_mask"].view(-1)
+        loss, _ = crit(out, (rgb, depth), weight_depth_loss=True)
+        loss.backward()
+        grads.append(pose.data.grad.clone())
+        if frozen:
+            assert e.grad is None and all(p.grad is None for p in dec.parameters())
+    assert torch.equal(grads[0], grads[1])
+
+
+def test_track_frame_runs():
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    from psvo.render_helpers import track_frame
+    scene, ms_cpu, emb, T, frame = _setup()
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    ms = {"voxel_center_xyz": ms_cpu["voxel_center_xyz"].to(DEV), "voxel_structure": ms_cpu["voxel_structure"].to(DEV),
+          "voxel_vertex_idx": ms_cpu["voxel_vertex_idx"].to(DEV), "voxel_vertex_emb": emb.to(DEV)}
+    crit = Criterion(types.SimpleNamespace(criteria=dict(CRIT, sdf_truncation=0.1), data_specs={"max_depth": 10.0}))
+    pose0 = _perturbed(T)
+    pose, optim, hit = track_frame(pose0, frame, ms, dec, None, crit, scene.voxel_size, N_rays=1024, step_size=0.01,
+                                   num_iterations=5, depth_variance=True)
+    assert torch.isfinite(pose.data).all()
+    assert hit.dtype == torch.bool and int(hit.sum()) > 0
+    assert float((pose.data.detach().cpu() - pose0.data).abs().max()) > 0  # the pose moved
