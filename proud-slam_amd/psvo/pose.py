@@ -15,13 +15,19 @@ import torch.nn as nn
 
 
 def _series(x, first_denom, step, nth=10):
-    """Σ_{i≤nth} (−1)^i x^{2i} / d_i with d_0 = first_denom, d_i = d_{i−1}·step(i)."""
-    out = torch.zeros_like(x)
+    """Σ_{i≤nth} (−1)^i x^{2i} / d_i with d_0 = first_denom, d_i = d_{i−1}·step(i),
+    by Horner's rule in y = x² (coefficients folded on the host: nth
+    multiply-adds on the device instead of a power, divide and add per term)."""
+    coef = []
     denom = float(first_denom)
     for i in range(nth + 1):
         if i > 0:
             denom *= step(i)
-        out = out + (-1.0) ** i * x ** (2 * i) / denom
+        coef.append((-1.0) ** i / denom)
+    y = x * x
+    out = torch.full_like(x, coef[-1])
+    for c in reversed(coef[:-1]):
+        out = torch.addcmul(torch.full_like(x, c), out, y)
     return out
 
 

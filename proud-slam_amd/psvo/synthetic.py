@@ -241,14 +241,16 @@ class SyntheticFrame:
         self.rays_d = torch.from_numpy(d_cam).to(device)
         self.rgb = torch.from_numpy(col.reshape(H, W, 3).astype(np.float32)).to(device)
         self.depth = torch.from_numpy(t.reshape(H, W).astype(np.float32)).to(device)
-        self.gen = torch.Generator().manual_seed(seed)
+        self.gen = torch.Generator(device=device).manual_seed(seed)
         self.sample_mask = None
 
     def sample_rays(self, n):
-        pix = gumbel_topk_pixels(self.h, self.w, n, self.gen)
-        mask = torch.zeros(self.h * self.w, dtype=torch.bool)
-        mask[pix] = True
-        self.sample_mask = mask.view(self.h, self.w).to(self.depth.device)
+        """gumbel top-k over a uniform pixel distribution, on the frame's device"""
+        u = torch.rand(self.h * self.w, generator=self.gen, device=self.depth.device)
+        g = -torch.log(-torch.log(u + 1e-7) + 1e-7)
+        mask = torch.zeros(self.h * self.w, dtype=torch.bool, device=self.depth.device)
+        mask[torch.topk(g, n).indices] = True
+        self.sample_mask = mask.view(self.h, self.w)
 
 
 @dataclass

@@ -1,0 +1,58 @@
+"""track_frame throughput (render_helpers.py:679-761 shape: 1024 rays per
+iteration, median depth loss, Adam on the pose): ms per iteration with the
+map requiring gradients (as the reference's tracker) and frozen (fast path)."""
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "proud-slam_amd"))
+from psvo import synthetic as syn  # noqa: E402
+from psvo.criterion import Criterion  # noqa: E402
+from psvo.decoder import Decoder  # noqa: E402
+from psvo.octree import Octree, map_states  # noqa: E402
+from psvo.pose import OptimizablePose  # noqa: E402
+from psvo.render_helpers import track_frame  # noqa: E402
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    scene = syn.room0()
+    tree = Octree()
+    tree.init(scene.grid_dim, 16, scene.voxel_size, 8)
+    tree.insert(syn.surface_voxels(scene, seed=0))
+    g = torch.Generator().manual_seed(0)
+    emb = (torch.randn(max(20000, tree.count_nodes()), 16, generator=g) * 0.01).cuda()
+    T = syn.camera_poses(scene, 1, seed=5)[0]
+    frame = syn.SyntheticFrame(scene, T, scale=0.5, seed=1)
+    crit = Criterion(types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0,
+                                                     "fs_weight": 10.0, "sdf_truncation": 0.1},
+                                           data_specs={"max_depth": 10.0}))
+    out = {}
+    for frozen in (False, True):
+        dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").cuda()
+        e = emb.clone().requires_grad_(not frozen)
+        for p in dec.parameters():
+            p.requires_grad_(not frozen)
+        ms = map_states(tree, e, scene.voxel_size, device="cuda")
+        pose0 = OptimizablePose.from_matrix(T)
+        track_frame(pose0, frame, ms, dec, None, crit, scene.voxel_size, N_rays=1024, step_size=0.0078,
+                    num_iterations=3, depth_variance=True)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        track_frame(pose0, frame, ms, dec, None, crit, scene.voxel_size, N_rays=1024, step_size=0.0078,
+                    num_iterations=iters, depth_variance=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out["frozen_map" if frozen else "map_requires_grad"] = {"ms_per_iteration": 1e3 * el / iters,
+                                                                "rays_per_s": 1024 * iters / el}
+    print(json.dumps({"track_frame": out, "iterations": iters, "rays_per_iteration": 1024}))
+
+
+if __name__ == "__main__":
+    main()
