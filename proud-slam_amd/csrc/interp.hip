@@ -82,9 +82,9 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-struct BwdPass {  // per-wave LDS: one 16-sample pass
-    float w[16][8];    // trilinear weights per slot
-    float g[16][16];   // grad_feat rows
+struct BwdPass {  // per-wave LDS: one 16-sample pass, slot-minor so a lane reads 4 slots per ds_read_b128
+    float w[8][16];    // trilinear weights [corner][slot]
+    float g[16][16];   // grad_feat [dim][slot]
     int vid[16][8];    // vertex rows of the slot's leaf
     int leaf[16];
 };
@@ -156,16 +156,18 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
             for (int k = 0; k < 8; ++k) vid[k] = 0;
         }
         corner_weights(p[0], p[1], p[2], w);
-        // stage this pass for the run sums
+        // stage this pass for the run sums (each of the sample's 4 lanes writes a quarter)
         wave_lds_sync();  // the previous pass's readers are done
-        if (EMB) *reinterpret_cast<float4 *>(&B.g[sub][4 * q]) = g;
-        if (EMB && q == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                B.w[sub][k] = w[k];
-                B.vid[sub][k] = vid[k];
-            }
-            B.leaf[sub] = lf;
+        if (EMB) {
+            B.g[4 * q + 0][sub] = g.x;
+            B.g[4 * q + 1][sub] = g.y;
+            B.g[4 * q + 2][sub] = g.z;
+            B.g[4 * q + 3][sub] = g.w;
+            B.w[2 * q][sub] = w[2 * q];
+            B.w[2 * q + 1][sub] = w[2 * q + 1];
+            B.vid[sub][2 * q] = vid[2 * q];
+            B.vid[sub][2 * q + 1] = vid[2 * q + 1];
+            if (q == 0) B.leaf[sub] = lf;
         }
         // dL/dx for this lane's sample: eg_k = E[vid_k] · g
         float eg[8];
@@ -201,24 +203,42 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
             }
         }
         wave_lds_sync();
-        // run sums over the pass's valid slots (wave-uniform loop)
-        const int n_slots = EMB ? min(16, end - base) : 0;
-        for (int sl = 0; sl < n_slots; ++sl) {
-            const int lf_s = B.leaf[sl];
-            if (lf_s != cur_leaf) {
-                if (cur_leaf >= 0) {
-                    atomicAdd(grad_emb + (int64_t)cur_v0 * 16 + ed, acc0);
-                    atomicAdd(grad_emb + (int64_t)cur_v1 * 16 + ed, acc1);
-                }
-                cur_leaf = lf_s;
-                cur_v0 = B.vid[sl][ek0];
-                cur_v1 = B.vid[sl][ek0 + 4];
-                acc0 = 0.f;
-                acc1 = 0.f;
+        if (EMB) {
+            // run sums over the pass's valid slots: the pass's weights, gradients
+            // and leaves come into registers with 16 vector LDS reads, then the
+            // slot loop is register-only (the leaf compare is wave-uniform)
+            const int n_slots = min(16, end - base);
+            float wa[16], wb[16], gv[16];
+            int lfs[16];
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const float4 a = *reinterpret_cast<const float4 *>(&B.w[ek0][4 * c4]);
+                const float4 b = *reinterpret_cast<const float4 *>(&B.w[ek0 + 4][4 * c4]);
+                const float4 gg = *reinterpret_cast<const float4 *>(&B.g[ed][4 * c4]);
+                const int4 l4 = *reinterpret_cast<const int4 *>(&B.leaf[4 * c4]);
+                wa[4 * c4] = a.x; wa[4 * c4 + 1] = a.y; wa[4 * c4 + 2] = a.z; wa[4 * c4 + 3] = a.w;
+                wb[4 * c4] = b.x; wb[4 * c4 + 1] = b.y; wb[4 * c4 + 2] = b.z; wb[4 * c4 + 3] = b.w;
+                gv[4 * c4] = gg.x; gv[4 * c4 + 1] = gg.y; gv[4 * c4 + 2] = gg.z; gv[4 * c4 + 3] = gg.w;
+                lfs[4 * c4] = l4.x; lfs[4 * c4 + 1] = l4.y; lfs[4 * c4 + 2] = l4.z; lfs[4 * c4 + 3] = l4.w;
             }
-            const float gv = B.g[sl][ed];
-            acc0 += B.w[sl][ek0] * gv;
-            acc1 += B.w[sl][ek0 + 4] * gv;
+#pragma unroll
+            for (int sl = 0; sl < 16; ++sl) {
+                if (sl < n_slots) {
+                    if (lfs[sl] != cur_leaf) {
+                        if (cur_leaf >= 0) {
+                            atomicAdd(grad_emb + (int64_t)cur_v0 * 16 + ed, acc0);
+                            atomicAdd(grad_emb + (int64_t)cur_v1 * 16 + ed, acc1);
+                        }
+                        cur_leaf = lfs[sl];
+                        cur_v0 = B.vid[sl][ek0];
+                        cur_v1 = B.vid[sl][ek0 + 4];
+                        acc0 = 0.f;
+                        acc1 = 0.f;
+                    }
+                    acc0 += wa[sl] * gv[sl];
+                    acc1 += wb[sl] * gv[sl];
+                }
+            }
         }
     }
     if (EMB && cur_leaf >= 0) {
