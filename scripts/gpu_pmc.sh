@@ -11,7 +11,7 @@ IFS=';' read -ra SETS <<< "${PMC_SETS}"
 for set in "${SETS[@]}"; do
   i=$((i + 1))
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_$i -o pmc --pmc $set -- \
-      python3 scripts/mlp_bench.py --iters 3 > gpurun_out/pmc_$i.log 2>&1
+      ${PMC_CMD:-python3 scripts/mlp_bench.py --iters 3} > gpurun_out/pmc_$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
