@@ -233,6 +233,34 @@ int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
                        const float *sdf, const float *z_vals, const float *out, const float *g_loss, float *g_color,
                        float *g_depth, float *g_sdf);
 
+/* Tracking's weight_depth_loss filter (criterion.py:45-49) over the R_hit
+ * hit rays (R_hit ≤ 16384): dtmp f32[R_hit] = |gt_d − depth| /
+ * sqrt(Σ_s w·(depth − z)² + 1e-10) from psvo_composite_fwd's weights, and
+ * dthr f32[1] = 10 · torch.median(dtmp) (lower middle element). */
+int psvo_criterion_depth_filter(void *stream, int64_t r_hit, int s_max, const int *rank_ray, const float *gt_depth,
+                                const float *depth, const float *weights, const float *z_vals, float *dtmp,
+                                float *dthr);
+/* psvo_criterion_sums / _bwd with the depth filter: a ray's depth term is
+ * valid only if also dtmp[r] < dthr[0] (both NULL: no filter). */
+int psvo_criterion_sums_ex(void *stream, int64_t r_hit, int s_max, int pad_extra, float truncation, float max_depth,
+                           const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *color,
+                           const float *depth, const float *sdf, const float *z_vals, const float *dtmp,
+                           const float *dthr, float *workspace, double *sums);
+int psvo_criterion_bwd_ex(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                          const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *color,
+                          const float *depth, const float *sdf, const float *z_vals, const float *out,
+                          const float *g_loss, const float *dtmp, const float *dthr, float *g_color, float *g_depth,
+                          float *g_sdf);
+
+/* ---- camera pose (tracking, csrc/pose.hip) ---------------------------- */
+/* pose f32[6] = [t | w] (se3pose.py:8-98, R = I + A·[w]× + B·[w]×², Taylor
+ * A/B): rays_o[r] = t, rays_d[r] = R·dirs[r] (render_helpers.py:714-716). */
+int psvo_pose_rays(void *stream, int64_t n, const float *pose, const float *dirs, float *rays_o, float *rays_d);
+/* grad f32[6] = dL/d[t | w] from per-ray grad_o / grad_d of the R_hit hit
+ * rays at rows rank_ray[r] (psvo_interp_bwd's output), through rotation(). */
+int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,
+                   const float *g_d, const float *pose, float *grad);
+
 /* ---- optimiser ------------------------------------------------------- */
 /* One Adam step (torch.optim.Adam, amsgrad off) over n_tensors f32 tensors:
  * host arrays of device pointers and element counts; `step` is the step
@@ -290,6 +318,19 @@ int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region
 int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
                   const float *rays_d, const float *gt_rgb, const float *gt_depth, uint64_t seed, int64_t adam_step,
                   int flags, float *loss_out, int *stats_out);
+
+/* One tracking iteration (track_frame's loop body, render_helpers.py:
+ * 708-722): world rays from pose f32[6] (device) and camera-frame dirs_cam
+ * f32[R,3], render against the frozen map / decoder of `d` (emb, dec read
+ * only), Criterion (+ the median depth filter with PSVO_TRACK_DEPTH_FILTER),
+ * backward to the pose only, and torch.optim.Adam on the pose (lr, d->beta1,
+ * d->beta2, d->eps; moments pose_m / pose_v f32[6]) unless
+ * PSVO_STEP_NO_ADAM.  pose_grad: device f32[6] out or NULL.  One stats
+ * read-back; loss_out / stats_out as psvo_map_step. */
+enum { PSVO_TRACK_DEPTH_FILTER = 2 };
+int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *dirs_cam,
+                    const float *gt_rgb, const float *gt_depth, float *pose, float *pose_m, float *pose_v, double lr,
+                    uint64_t seed, int64_t adam_step, int flags, float *pose_grad, float *loss_out, int *stats_out);
 
 /* Both Adam steps of the iteration from desc->grad_flat (one launch; the
  * embedding gradient is zeroed as it is consumed). */

@@ -15,6 +15,9 @@
 // double reduction (deterministic), a one-thread finalise, and one backward
 // pass.  The eight sums are exactly what a data-parallel run all-reduces to
 // form the single-GPU loss of the global batch.
+// Tracking's weight_depth_loss filter (criterion.py:45-49: valid &= tmp <
+// 10·median(tmp)) is two more launches: per-ray tmp, and a one-block bitonic
+// sort for the median; sums / bwd then take tmp and the threshold.
 #include <hip/hip_runtime.h>
 
 #include "psvo_common.h"
@@ -56,7 +59,8 @@ __global__ __launch_bounds__(256) void k_crit_rays(int64_t r_hit, int s_max, int
                                                    const int *__restrict__ rank_ray, const float *__restrict__ gt_rgb,
                                                    const float *__restrict__ gt_depth, const float *__restrict__ color,
                                                    const float *__restrict__ depth, const float *__restrict__ sdf,
-                                                   const float *__restrict__ z_vals, float *__restrict__ part) {
+                                                   const float *__restrict__ z_vals, const float *__restrict__ dtmp,
+                                                   const float *__restrict__ dthr, float *__restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256) void k_crit_rays(int64_t r_hit, int s_max, int
     if (lane == 0) {
         float ac = 0.f;
         for (int c = 0; c < 3; ++c) ac += fabsf(gt_rgb[orig * 3 + c] - color[r * 3 + c]);
-        const bool valid = d > 0.01f && d < max_depth;
+        const bool valid = d > 0.01f && d < max_depth && (!dtmp || dtmp[r] < dthr[0]);
         if (pad_extra > 0) {  // padded samples of the global [R_hit, S_max] layout: z = 10, sdf = 1
             const SampleTerms t = sample_terms(10.0f, 1.0f, d, tr, max_depth);
             nf += t.f * pad_extra;
@@ -163,7 +167,8 @@ __global__ __launch_bounds__(256) void k_crit_bwd(int64_t r_hit, int s_max, floa
                                                   const float *__restrict__ gt_depth, const float *__restrict__ color,
                                                   const float *__restrict__ depth, const float *__restrict__ sdf,
                                                   const float *__restrict__ z_vals, const float *__restrict__ coef,
-                                                  const float *__restrict__ g_loss, float *__restrict__ g_color,
+                                                  const float *__restrict__ g_loss, const float *__restrict__ dtmp,
+                                                  const float *__restrict__ dthr, float *__restrict__ g_color,
                                                   float *__restrict__ g_depth, float *__restrict__ g_sdf) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -182,9 +187,58 @@ __global__ __launch_bounds__(256) void k_crit_bwd(int64_t r_hit, int s_max, floa
     if (lane < 3) {
         g_color[r * 3 + lane] = -(g * coef[kOutCColor]) * sgn(gt_rgb[orig * 3 + lane] - color[r * 3 + lane]);
     } else if (lane == 3) {
-        const bool valid = d > 0.01f && d < max_depth;
+        const bool valid = d > 0.01f && d < max_depth && (!dtmp || dtmp[r] < dthr[0]);
         g_depth[r] = valid ? -(g * coef[kOutCDepth]) * sgn(d - depth[r]) : 0.0f;
     }
+}
+
+// tracking's depth filter (criterion.py:45-50): per hit ray
+//   tmp = |d − depth| / sqrt(Σ_s w_s (depth − z_s)² + 1e-10)
+__global__ __launch_bounds__(256) void k_crit_depth_tmp(int64_t r_hit, int s_max, const int *__restrict__ rank_ray,
+                                                        const float *__restrict__ gt_depth,
+                                                        const float *__restrict__ depth,
+                                                        const float *__restrict__ weights,
+                                                        const float *__restrict__ z_vals, float *__restrict__ dtmp) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const float pd = depth[r];
+    float v = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float e = pd - z_vals[r * s_max + s];
+        v += weights[r * s_max + s] * (e * e);
+    }
+    v = wsum(v);
+    if (lane == 0) dtmp[r] = fabsf(gt_depth[rank_ray[r]] - pd) / sqrtf(v + 1e-10f);
+}
+
+// threshold = 10 · median(tmp) (torch.median: the lower middle element,
+// index (n−1)/2 of the sorted values): one block, bitonic sort in LDS
+constexpr int kMedianMax = 16384;
+__global__ __launch_bounds__(1024) void k_crit_depth_thr(int64_t r_hit, const float *__restrict__ dtmp,
+                                                         float *__restrict__ dthr) {
+    extern __shared__ float v[];
+    int n2 = 1;
+    while (n2 < r_hit) n2 <<= 1;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) v[i] = i < r_hit ? dtmp[i] : __int_as_float(0x7f800000);
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+                const int ij = i ^ j;
+                if (ij > i) {
+                    const float a = v[i], b = v[ij];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        v[i] = b;
+                        v[ij] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) dthr[0] = 10.0f * v[(r_hit - 1) / 2];
 }
 
 }  // namespace
@@ -194,18 +248,42 @@ using namespace psvo;
 
 extern "C" int64_t psvo_criterion_workspace_floats(int64_t r_hit) { return r_hit * kNSums; }
 
+extern "C" int psvo_criterion_depth_filter(void *stream, int64_t r_hit, int s_max, const int *rank_ray,
+                                           const float *gt_depth, const float *depth, const float *weights,
+                                           const float *z_vals, float *dtmp, float *dthr) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_depth_filter: bad sizes");
+    PSVO_REQUIRE(r_hit <= kMedianMax, "criterion_depth_filter: %lld hit rays > %d (single-block median)",
+                 (long long)r_hit, kMedianMax);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_crit_depth_tmp, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, rank_ray, gt_depth,
+                       depth, weights, z_vals, dtmp);
+    int n2 = 1;
+    while (n2 < r_hit) n2 <<= 1;
+    hipLaunchKernelGGL(k_crit_depth_thr, dim3(1), dim3(1024), n2 * sizeof(float), st, r_hit, dtmp, dthr);
+    return check_launch("criterion_depth_filter");
+}
+
+extern "C" int psvo_criterion_sums_ex(void *stream, int64_t r_hit, int s_max, int pad_extra, float truncation,
+                                      float max_depth, const int *rank_ray, const float *gt_rgb, const float *gt_depth,
+                                      const float *color, const float *depth, const float *sdf, const float *z_vals,
+                                      const float *dtmp, const float *dthr, float *workspace, double *sums) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0 && pad_extra >= 0, "criterion_sums: bad sizes");
+    PSVO_REQUIRE(rank_ray && gt_rgb && gt_depth && color && depth && sdf && z_vals && workspace && sums,
+                 "criterion_sums: null pointer");
+    PSVO_REQUIRE((dtmp == nullptr) == (dthr == nullptr), "criterion_sums: depth filter needs tmp and threshold");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
+                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, dtmp, dthr, workspace);
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    return check_launch("criterion_sums");
+}
+
 extern "C" int psvo_criterion_sums(void *stream, int64_t r_hit, int s_max, int pad_extra, float truncation,
                                    float max_depth, const int *rank_ray, const float *gt_rgb, const float *gt_depth,
                                    const float *color, const float *depth, const float *sdf, const float *z_vals,
                                    float *workspace, double *sums) {
-    PSVO_REQUIRE(r_hit > 0 && s_max > 0 && pad_extra >= 0, "criterion_sums: bad sizes");
-    PSVO_REQUIRE(rank_ray && gt_rgb && gt_depth && color && depth && sdf && z_vals && workspace && sums,
-                 "criterion_sums: null pointer");
-    hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
-                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, workspace);
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
-    return check_launch("criterion_sums");
+    return psvo_criterion_sums_ex(stream, r_hit, s_max, pad_extra, truncation, max_depth, rank_ray, gt_rgb, gt_depth,
+                                  color, depth, sdf, z_vals, nullptr, nullptr, workspace, sums);
 }
 
 extern "C" int psvo_criterion_finalize(void *stream, const double *sums, int64_t n_hit, int s_max, float rgb_w,
@@ -217,13 +295,23 @@ extern "C" int psvo_criterion_finalize(void *stream, const double *sums, int64_t
     return check_launch("criterion_finalize");
 }
 
+extern "C" int psvo_criterion_bwd_ex(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                                     const int *rank_ray, const float *gt_rgb, const float *gt_depth,
+                                     const float *color, const float *depth, const float *sdf, const float *z_vals,
+                                     const float *out, const float *g_loss, const float *dtmp, const float *dthr,
+                                     float *g_color, float *g_depth, float *g_sdf) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_bwd: bad sizes");
+    PSVO_REQUIRE((dtmp == nullptr) == (dthr == nullptr), "criterion_bwd: depth filter needs tmp and threshold");
+    hipLaunchKernelGGL(k_crit_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
+                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, out, g_loss, dtmp, dthr,
+                       g_color, g_depth, g_sdf);
+    return check_launch("criterion_bwd");
+}
+
 extern "C" int psvo_criterion_bwd(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
                                   const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *color,
                                   const float *depth, const float *sdf, const float *z_vals, const float *out,
                                   const float *g_loss, float *g_color, float *g_depth, float *g_sdf) {
-    PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_bwd: bad sizes");
-    hipLaunchKernelGGL(k_crit_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
-                       max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, out, g_loss, g_color,
-                       g_depth, g_sdf);
-    return check_launch("criterion_bwd");
+    return psvo_criterion_bwd_ex(stream, r_hit, s_max, truncation, max_depth, rank_ray, gt_rgb, gt_depth, color, depth,
+                                 sdf, z_vals, out, g_loss, nullptr, nullptr, g_color, g_depth, g_sdf);
 }

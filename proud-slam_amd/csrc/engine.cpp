@@ -24,7 +24,7 @@ enum Slot {
     kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
     kOffsets, kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
-    kGradEmb, kGradOD, kSlots
+    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSlots
 };
 
 struct Arena {
@@ -212,19 +212,29 @@ extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *
     return PSVO_OK;
 }
 
-extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
-                             const float *rays_o, const float *rays_d, const float *gt_rgb, const float *gt_depth,
-                             uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
-    PSVO_REQUIRE(e && d && rays_o && rays_d && gt_rgb && gt_depth && loss_out, "map_step: null argument");
-    PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "map_step: bad sizes");
-    PSVO_REQUIRE(d->width == 128, "map_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
-    hipStream_t st = as_stream(stream);
+namespace {
+
+// what one render (query + forward) leaves for the loss and the backward
+struct Render {
+    int64_t r_hit = 0, m = 0;
+    int s_max = 0;
+    int *rank_ray, *ray_ns, *offsets, *leaf, *ray_of;
+    float *tt, *z_vals, *feat, *images, *sdf_s, *rgb_s, *act, *sdf, *weights, *color, *depth;
+    uint64_t *masks;
+};
+
+// render_rays (render_helpers.py:363-556) on the device: intersection, hit
+// ranks, sampling (one stats read-back sizes the sample buffers),
+// interpolation, decoder, compositing.  want_act: keep the decoder
+// activations for weight gradients (mapping); tracking keeps only the masks.
+int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, const float *rays_o,
+           const float *rays_d, uint64_t seed, bool want_act, int *stats_out, const char *who, Render &o) {
     int rc = PSVO_OK;
-    const int64_t R = n_rays;
+    void *stream = st;
     // ---- query: intersection, hit ranks, statistics
     ENG_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+        return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
     ENG_BUF(int, hit_idx, kHitIdx, R * kMaxHits * sizeof(int));
     ENG_BUF(float, hit_t0, kHitT0, R * kMaxHits * sizeof(float));
     ENG_BUF(float, hit_t1, kHitT1, R * kMaxHits * sizeof(float));
@@ -256,13 +266,13 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_CALL(read_stats(e, st, stats));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int r_hit = e->host_stats[PSVO_STAT_R_HIT];
-    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "map_step: octree deeper than the DFS stack");
-    if (r_hit == 0) return set_error(PSVO_E_INVALID, "map_step: no ray hits the octree (render_helpers.py:388)");
+    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
+    if (r_hit == 0) return set_error(PSVO_E_INVALID, "%s: no ray hits the octree (render_helpers.py:388)", who);
     const int s_max = e->host_stats[PSVO_STAT_S_MAX];
     const int64_t M = e->host_stats[PSVO_STAT_M];
-    if (e->host_stats[7] & 2) return set_error(PSVO_E_OVERFLOW, "map_step: sampler exceeded max_steps");
+    if (e->host_stats[7] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
     if (stats_out) memcpy(stats_out, e->host_stats, PSVO_STAT_WORDS * sizeof(int));
-    if (M == 0) return set_error(PSVO_E_INVALID, "map_step: no valid samples");
+    if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
@@ -273,7 +283,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
                                 z_vals, smask));
     mark(e, st, PSVO_TIME_POINTS, 1);
-    // ---- forward: interpolation, decoder, compositing, loss
+    // ---- forward: interpolation, decoder, compositing
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
     mark(e, st, PSVO_TIME_INTERP_FWD, 0);
     ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
@@ -283,7 +293,11 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(float, images, kImages, psvo_mlp_image_floats() * sizeof(float));
     ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
     ENG_BUF(float, rgb_s, kRgbS, M * 3 * sizeof(float));
-    ENG_BUF(float, act, kAct, (size_t)4 * mp * 128 * sizeof(float));
+    float *act = nullptr;
+    if (want_act) {
+        ENG_BUF(float, abuf, kAct, (size_t)4 * mp * 128 * sizeof(float));
+        act = abuf;
+    }
     ENG_BUF(uint64_t, masks, kMasks, (size_t)M * 6 * sizeof(uint64_t));
     float *const *W = d->dec;
     mark(e, st, PSVO_TIME_MLP_FWD, 0);
@@ -297,26 +311,81 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(float, z_min, kZmin, (size_t)r_hit * sizeof(float));
     ENG_CALL(psvo_composite_fwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf,
                                 weights, color, depth, z_min));
+    o.r_hit = r_hit;
+    o.m = M;
+    o.s_max = s_max;
+    o.rank_ray = rank_ray;
+    o.ray_ns = ray_ns;
+    o.offsets = offsets;
+    o.leaf = leaf;
+    o.ray_of = ray_of;
+    o.tt = tt;
+    o.z_vals = z_vals;
+    o.feat = feat;
+    o.images = images;
+    o.sdf_s = sdf_s;
+    o.rgb_s = rgb_s;
+    o.act = act;
+    o.masks = masks;
+    o.sdf = sdf;
+    o.weights = weights;
+    o.color = color;
+    o.depth = depth;
+    return PSVO_OK;
+}
+
+// Criterion forward + backward to the per-sample decoder gradients (d loss =
+// 1); dtmp/dthr: tracking's median depth filter or NULL.
+int loss_backward(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const Render &q, const float *gt_rgb,
+                  const float *gt_depth, const float *dtmp, const float *dthr, float *loss_out, float **g_sdf_s_out,
+                  float **g_rgb_s_out) {
+    int rc = PSVO_OK;
+    void *stream = st;
+    const int64_t r_hit = q.r_hit, M = q.m;
+    const int s_max = q.s_max;
+    const size_t RS = (size_t)r_hit * s_max;
     ENG_BUF(float, crit_ws, kCritWs, psvo_criterion_workspace_floats(r_hit) * sizeof(float));
     ENG_BUF(double, sums, kSums, 8 * sizeof(double));
-    ENG_CALL(psvo_criterion_sums(stream, r_hit, s_max, 0, d->truncation, d->max_depth, rank_ray, gt_rgb, gt_depth,
-                                 color, depth, sdf, z_vals, crit_ws, sums));
+    ENG_CALL(psvo_criterion_sums_ex(stream, r_hit, s_max, 0, d->truncation, d->max_depth, q.rank_ray, gt_rgb,
+                                    gt_depth, q.color, q.depth, q.sdf, q.z_vals, dtmp, dthr, crit_ws, sums));
     ENG_CALL(psvo_criterion_finalize(stream, sums, r_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
                                      d->truncation, PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF,
                                      loss_out));
-    // ---- backward (d loss = 1)
     ENG_BUF(float, g_loss, kGLoss, sizeof(float));
     if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g_loss), 0x3F800000 /* 1.0f */, 1, st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: g_loss fill failed");
+        return set_error(PSVO_E_LAUNCH, "engine: g_loss fill failed");
     ENG_BUF(float, g_color, kGColor, (size_t)r_hit * 3 * sizeof(float));
     ENG_BUF(float, g_depth, kGDepth, (size_t)r_hit * sizeof(float));
     ENG_BUF(float, g_sdf, kGSdf, RS * sizeof(float));
-    ENG_CALL(psvo_criterion_bwd(stream, r_hit, s_max, d->truncation, d->max_depth, rank_ray, gt_rgb, gt_depth, color,
-                                depth, sdf, z_vals, loss_out, g_loss, g_color, g_depth, g_sdf));
+    ENG_CALL(psvo_criterion_bwd_ex(stream, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_rgb, gt_depth,
+                                   q.color, q.depth, q.sdf, q.z_vals, loss_out, g_loss, dtmp, dthr, g_color, g_depth,
+                                   g_sdf));
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
     ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
-    ENG_CALL(psvo_composite_bwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf, weights, rgb_s,
-                                g_color, g_depth, nullptr, g_sdf, g_sdf_s, g_rgb_s));
+    ENG_CALL(psvo_composite_bwd(stream, r_hit, s_max, d->truncation, q.offsets, q.ray_ns, q.z_vals, q.sdf, q.weights,
+                                q.rgb_s, g_color, g_depth, nullptr, g_sdf, g_sdf_s, g_rgb_s));
+    *g_sdf_s_out = g_sdf_s;
+    *g_rgb_s_out = g_rgb_s;
+    return PSVO_OK;
+}
+
+}  // namespace
+
+extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
+                             const float *rays_o, const float *rays_d, const float *gt_rgb, const float *gt_depth,
+                             uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
+    PSVO_REQUIRE(e && d && rays_o && rays_d && gt_rgb && gt_depth && loss_out, "map_step: null argument");
+    PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "map_step: bad sizes");
+    PSVO_REQUIRE(d->width == 128, "map_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
+    hipStream_t st = as_stream(stream);
+    int rc = PSVO_OK;
+    const int64_t R = n_rays;
+    Render q;
+    ENG_CALL(render(e, st, d, R, rays_o, rays_d, seed, true, stats_out, "map_step", q));
+    const int64_t M = q.m;
+    // ---- loss and backward (d loss = 1)
+    float *g_sdf_s, *g_rgb_s;
+    ENG_CALL(loss_backward(e, st, d, q, gt_rgb, gt_depth, nullptr, nullptr, loss_out, &g_sdf_s, &g_rgb_s));
     const int n_split = 256;
     ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
@@ -335,10 +404,11 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
             off += kDecSizes[i];
         }
     }
+    float *const *W = d->dec;
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(psvo_mlp_bwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images,
-                          rgb_s, act, masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
-                          G[8], G[9], 0, n_split, mlp_ws));
+    ENG_CALL(psvo_mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                          q.images, q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4],
+                          G[5], G[6], G[7], G[8], G[9], 0, n_split, mlp_ws));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
     if (!(e->grads_clean && e->clean_buf == grad_emb) &&
@@ -347,7 +417,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     e->grads_clean = false;
     e->clean_buf = grad_emb;
     mark(e, st, PSVO_TIME_INTERP_BWD, 0);
-    ENG_CALL(psvo_interp_bwd(stream, r_hit, 16, d->voxel_size, offsets, rank_ray, leaf, tt, rays_o, rays_d,
+    ENG_CALL(psvo_interp_bwd(stream, q.r_hit, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt, rays_o, rays_d,
                              d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
     mark(e, st, PSVO_TIME_INTERP_BWD, 1);
     e->tm.pending = e->tm.on;
@@ -355,6 +425,68 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step));
         e->grads_clean = true;
+    }
+    return PSVO_OK;
+}
+
+extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
+                               const float *dirs_cam, const float *gt_rgb, const float *gt_depth, float *pose,
+                               float *pose_m, float *pose_v, double lr, uint64_t seed, int64_t adam_step, int flags,
+                               float *pose_grad, float *loss_out, int *stats_out) {
+    PSVO_REQUIRE(e && d && dirs_cam && gt_rgb && gt_depth && pose && loss_out, "track_step: null argument");
+    PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "track_step: bad sizes");
+    PSVO_REQUIRE(d->width == 128, "track_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
+    PSVO_REQUIRE((flags & PSVO_STEP_NO_ADAM) || (pose_m && pose_v), "track_step: Adam needs pose_m / pose_v");
+    hipStream_t st = as_stream(stream);
+    int rc = PSVO_OK;
+    const int64_t R = n_rays;
+    // ---- world rays from the pose (render_helpers.py:714-716)
+    ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
+    ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
+    ENG_CALL(psvo_pose_rays(stream, R, pose, dirs_cam, rays_o, rays_d));
+    Render q;
+    ENG_CALL(render(e, st, d, R, rays_o, rays_d, seed, false, stats_out, "track_step", q));
+    // ---- loss (optionally with the median depth filter) and backward
+    float *dtmp = nullptr, *dthr = nullptr;
+    if (flags & PSVO_TRACK_DEPTH_FILTER) {
+        ENG_BUF(float, tbuf, kDTmp, (size_t)q.r_hit * sizeof(float) + 64);
+        dtmp = tbuf;
+        dthr = tbuf + ((q.r_hit + 15) / 16) * 16;
+        ENG_CALL(psvo_criterion_depth_filter(stream, q.r_hit, q.s_max, q.rank_ray, gt_depth, q.depth, q.weights,
+                                             q.z_vals, dtmp, dthr));
+    }
+    float *g_sdf_s, *g_rgb_s;
+    ENG_CALL(loss_backward(e, st, d, q, gt_rgb, gt_depth, dtmp, dthr, loss_out, &g_sdf_s, &g_rgb_s));
+    // frozen map: decoder backward to the features only, interpolation
+    // backward to the rays only (no embedding scatter)
+    const int64_t M = q.m;
+    ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
+    const int n_split = 256;
+    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
+    float *const *W = d->dec;
+    mark(e, st, PSVO_TIME_MLP_BWD, 0);
+    ENG_CALL(psvo_mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                          q.images, q.rgb_s, nullptr, q.masks, g_sdf_s, g_rgb_s, dfeat, nullptr, nullptr, nullptr,
+                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, n_split, mlp_ws));
+    mark(e, st, PSVO_TIME_MLP_BWD, 1);
+    ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
+    mark(e, st, PSVO_TIME_INTERP_BWD, 0);
+    ENG_CALL(psvo_interp_bwd(stream, q.r_hit, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt, rays_o, rays_d,
+                             d->centres, d->vertex_idx, d->emb, dfeat, nullptr, grad_od, grad_od + R * 3));
+    mark(e, st, PSVO_TIME_INTERP_BWD, 1);
+    e->tm.pending = e->tm.on;
+    // ---- pose gradient through rotation() and the pose's Adam step
+    if (!pose_grad) {
+        ENG_BUF(float, gbuf, kPoseGrad, 8 * sizeof(float));
+        pose_grad = gbuf;
+    }
+    ENG_CALL(psvo_pose_grad(stream, q.r_hit, q.rank_ray, dirs_cam, grad_od, grad_od + R * 3, pose, pose_grad));
+    if (!(flags & PSVO_STEP_NO_ADAM)) {
+        int64_t n6 = 6;
+        int zero = 0;
+        const float *g = pose_grad;
+        ENG_CALL(adam_launch(st, 1, &pose, &g, &pose_m, &pose_v, &n6, &lr, d->beta1, d->beta2, d->eps, 0.0, adam_step,
+                             &zero));
     }
     return PSVO_OK;
 }

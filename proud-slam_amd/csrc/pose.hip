@@ -1,0 +1,161 @@
+// Camera pose of the tracking loop on the device.
+//
+// Reference: track_frame (render_helpers.py:679-761) optimises an SE(3) pose
+// (se3pose.py:8-98; parameters [t | w], w axis-angle) through
+//   rays_d = dirs_cam @ R(w)ᵀ,  rays_o = t           (render_helpers.py:714-716)
+//   R = I + A(θ²)·W + B(θ²)·W²,  W = [w]×,  A = sin θ/θ,  B = (1 − cos θ)/θ²
+// with A, B as 10th-order Taylor series in θ² (se3pose.py:27-44).  Two
+// kernels: the world rays from the pose (one thread per ray, R recomputed per
+// thread from the six parameters — 11 multiply-adds), and the pose gradient
+// from the interpolation backward's per-ray grad_o / grad_d:
+//   dL/dt   = Σ_r grad_o[r]
+//   G_jk    = dL/dR_jk = Σ_r grad_d[r]_j · dir[r]_k
+//   dL/dw_k = Σ_jk G_jk · (2w_k A′·W + A·E_k + 2w_k B′·W² + B·(E_k W + W E_k))_jk
+// (E_k = [e_k]×, A′ = dA/d(θ²)), i.e. what autograd derives through
+// rotation() — one block, a fixed-order reduction.
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+constexpr int kSeriesN = 10;
+
+// Horner evaluation of Σ_i (−1)^i y^i / d_i (d_0 = d0, d_i = d_{i−1}·step(i))
+// and its derivative in y; `a` selects sin θ/θ (step (2i)(2i+1), d0 = 1) or
+// (1 − cos θ)/θ² (step (2i+1)(2i+2), d0 = 2).
+__device__ __forceinline__ void series(float y, bool a, float &p, float &dp) {
+    float c[kSeriesN + 1];
+    double den = a ? 1.0 : 2.0;
+    for (int i = 0; i <= kSeriesN; ++i) {
+        if (i > 0) den *= a ? (double)(2 * i) * (2 * i + 1) : (double)(2 * i + 1) * (2 * i + 2);
+        c[i] = (float)((i & 1 ? -1.0 : 1.0) / den);
+    }
+    p = c[kSeriesN];
+    dp = 0.f;
+    for (int i = kSeriesN - 1; i >= 0; --i) {
+        dp = dp * y + p;
+        p = p * y + c[i];
+    }
+}
+
+struct Rot {
+    float w[3], W[3][3], W2[3][3], A, B, dA, dB;
+    float R[3][3];
+};
+
+__device__ __forceinline__ void rotation(const float *__restrict__ pose, Rot &q) {
+    q.w[0] = pose[3];
+    q.w[1] = pose[4];
+    q.w[2] = pose[5];
+    const float y = q.w[0] * q.w[0] + q.w[1] * q.w[1] + q.w[2] * q.w[2];
+    series(y, true, q.A, q.dA);
+    series(y, false, q.B, q.dB);
+    const float(&w)[3] = q.w;
+    float W[3][3] = {{0.f, -w[2], w[1]}, {w[2], 0.f, -w[0]}, {-w[1], w[0], 0.f}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            q.W[i][j] = W[i][j];
+            q.W2[i][j] = W[i][0] * W[0][j] + W[i][1] * W[1][j] + W[i][2] * W[2][j];
+        }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) q.R[i][j] = (i == j ? 1.f : 0.f) + q.A * q.W[i][j] + q.B * q.W2[i][j];
+}
+
+__global__ __launch_bounds__(256) void k_pose_rays(int64_t n, const float *__restrict__ pose,
+                                                   const float *__restrict__ dirs, float *__restrict__ rays_o,
+                                                   float *__restrict__ rays_d) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    Rot q;
+    rotation(pose, q);
+    const float d0 = dirs[r * 3 + 0], d1 = dirs[r * 3 + 1], d2 = dirs[r * 3 + 2];
+    for (int j = 0; j < 3; ++j) {
+        rays_d[r * 3 + j] = d0 * q.R[j][0] + d1 * q.R[j][1] + d2 * q.R[j][2];
+        rays_o[r * 3 + j] = pose[j];
+    }
+}
+
+constexpr int kGradThreads = 1024;
+
+__global__ __launch_bounds__(kGradThreads) void k_pose_grad(int64_t r_hit, const int *__restrict__ rank_ray,
+                                                            const float *__restrict__ dirs,
+                                                            const float *__restrict__ g_o,
+                                                            const float *__restrict__ g_d,
+                                                            const float *__restrict__ pose, float *__restrict__ grad) {
+    __shared__ float part[kGradThreads / 64][12];
+    float acc[12] = {};
+    for (int64_t r = threadIdx.x; r < r_hit; r += kGradThreads) {
+        const int64_t row = rank_ray ? rank_ray[r] : r;
+        float dir[3], gd[3];
+        for (int j = 0; j < 3; ++j) {
+            acc[j] += g_o[row * 3 + j];
+            gd[j] = g_d[row * 3 + j];
+            dir[j] = dirs[row * 3 + j];
+        }
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) acc[3 + j * 3 + k] += gd[j] * dir[k];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = 0; i < 12; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+        if (lane == 0) part[wv][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float tot[12] = {};
+    for (int w = 0; w < kGradThreads / 64; ++w)
+        for (int i = 0; i < 12; ++i) tot[i] += part[w][i];
+    Rot q;
+    rotation(pose, q);
+    const float(&G)[3][3] = *reinterpret_cast<const float(*)[3][3]>(tot + 3);
+    // Σ G∘W, Σ G∘W² and, per k, Σ G∘E_k, Σ G∘(E_k W + W E_k)
+    float gw = 0.f, gw2 = 0.f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            gw += G[i][j] * q.W[i][j];
+            gw2 += G[i][j] * q.W2[i][j];
+        }
+    for (int k = 0; k < 3; ++k) {
+        float e[3] = {0.f, 0.f, 0.f};
+        e[k] = 1.f;
+        const float E[3][3] = {{0.f, -e[2], e[1]}, {e[2], 0.f, -e[0]}, {-e[1], e[0], 0.f}};
+        float ge = 0.f, gs = 0.f;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                ge += G[i][j] * E[i][j];
+                float s = 0.f;
+                for (int l = 0; l < 3; ++l) s += E[i][l] * q.W[l][j] + q.W[i][l] * E[l][j];
+                gs += G[i][j] * s;
+            }
+        const float dy = 2.f * q.w[k];
+        grad[3 + k] = dy * q.dA * gw + q.A * ge + dy * q.dB * gw2 + q.B * gs;
+    }
+    for (int j = 0; j < 3; ++j) grad[j] = tot[j];
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int psvo_pose_rays(void *stream, int64_t n, const float *pose, const float *dirs, float *rays_o,
+                              float *rays_d) {
+    PSVO_REQUIRE(n > 0, "pose_rays: bad size");
+    PSVO_REQUIRE(pose && dirs && rays_o && rays_d, "pose_rays: null pointer");
+    hipLaunchKernelGGL(k_pose_rays, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, pose, dirs, rays_o,
+                       rays_d);
+    return check_launch("pose_rays");
+}
+
+extern "C" int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,
+                              const float *g_d, const float *pose, float *grad) {
+    PSVO_REQUIRE(r_hit >= 0, "pose_grad: bad size");
+    PSVO_REQUIRE(dirs && g_o && g_d && pose && grad, "pose_grad: null pointer");
+    hipLaunchKernelGGL(k_pose_grad, dim3(1), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray, dirs, g_o,
+                       g_d, pose, grad);
+    return check_launch("pose_grad");
+}

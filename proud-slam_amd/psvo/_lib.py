@@ -52,6 +52,13 @@ _SIGNATURES = {
     "psvo_engine_timing": (_i32, [_vp, _vp]),
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
+    "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _u64, _i64, _i32, _vp, _vp,
+                               _vp]),
+    "psvo_pose_rays": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "psvo_pose_grad": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "psvo_criterion_depth_filter": (_i32, [_vp, _i64, _i32] + [_vp] * 7),
+    "psvo_criterion_sums_ex": (_i32, [_vp, _i64, _i32, _i32, _f32, _f32] + [_vp] * 11),
+    "psvo_criterion_bwd_ex": (_i32, [_vp, _i64, _i32, _f32, _f32] + [_vp] * 14),
     "psvo_map_grad_floats": (_i64, [_i64]),
     "psvo_dtree_new": (_vp, [_vp, _i32, _i64]),
     "psvo_dtree_free": (None, [_vp]),

@@ -1,4 +1,4 @@
-"""Native mapping iteration (csrc/engine.cpp): one libpsvo call per
+"""Native mapping / tracking iterations (csrc/engine.cpp): one libpsvo call per
 bundle_adjust_frames iteration (render_helpers.py:609-672): render_rays →
 Criterion → backward → Adam(embeddings).step() + Adam(decoder).step().
 
@@ -115,6 +115,112 @@ class MappingEngine:
         out = (ctypes.c_double * len(self.REGIONS))()
         L.call("psvo_engine_timing", self.handle, ctypes.cast(out, ctypes.c_void_p))
         return dict(zip(self.REGIONS, list(out)))
+
+    @property
+    def last_stats(self):
+        return list(self.stats)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None:
+            _lib().psvo_engine_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TrackingEngine:
+    """Native tracking iteration (psvo_track_step): track_frame's loop body
+    (render_helpers.py:708-722) — world rays from the pose, render_rays
+    against the frozen map, Criterion (weight_depth_loss = the median depth
+    filter), backward to the pose only and torch.optim.Adam on the pose — as
+    one libpsvo call with a single stats read-back.  The map (map_states) and
+    decoder are read, never written."""
+
+    def __init__(self, map_states, decoder, voxel_size, step_size, truncation=0.1, max_distance=10.0,
+                 criteria=None, max_depth=10.0, betas=(0.9, 0.999), eps=1e-8):
+        crit = criteria or {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+        emb = map_states["voxel_vertex_emb"].detach()
+        self.params = [p.detach() for p in decoder.fused_params()]
+        for t in [emb] + self.params:
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise RuntimeError("TrackingEngine: embeddings / decoder parameters must be contiguous f32 CUDA")
+        self.dev = emb.device
+        self.emb = emb
+        self.centres = map_states["voxel_center_xyz"].float().contiguous()
+        self.structure = map_states["voxel_structure"].int().contiguous()
+        self.vertex_idx = map_states["voxel_vertex_idx"].int().contiguous()
+        d = MapDesc()
+        d.n_nodes = self.centres.shape[0]
+        d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
+                                                                        self.vertex_idx))
+        d.emb, d.n_emb = emb.data_ptr(), emb.shape[0]
+        for i in range(10):
+            d.dec[i] = self.params[i].data_ptr()
+        d.width = decoder.W
+        d.voxel_size, d.step_size, d.max_distance, d.truncation = voxel_size, step_size, max_distance, truncation
+        d.max_depth = max_depth
+        d.w_rgb, d.w_depth = crit["rgb_weight"], crit["depth_weight"]
+        d.w_fs, d.w_sdf = crit["fs_weight"], crit["sdf_weight"]
+        d.beta1, d.beta2, d.eps = betas[0], betas[1], eps
+        self.desc = d
+        # pose [t | w] and its Adam state; pose_grad / loss of the last step
+        self.pose = torch.zeros(6, dtype=torch.float32, device=self.dev)
+        self.pose_m = torch.zeros(6, dtype=torch.float32, device=self.dev)
+        self.pose_v = torch.zeros(6, dtype=torch.float32, device=self.dev)
+        self.pose_grad = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        self.loss_out = torch.empty(16, dtype=torch.float32, device=self.dev)
+        self.stats = (ctypes.c_int * 8)()
+        self.step_no = 0
+        h = _lib().psvo_engine_new()
+        if not h:
+            raise L.PsvoError("psvo_engine_new failed")
+        self.handle = _vp(h)
+
+    def reset(self, pose_data):
+        """Start a frame from pose parameters [t | w] (a fresh torch.optim.Adam)."""
+        self.pose.copy_(torch.as_tensor(pose_data, dtype=torch.float32).reshape(6))
+        self.pose_m.zero_()
+        self.pose_v.zero_()
+        self.step_no = 0
+
+    def step(self, dirs_cam, rgb, depth, seed, lr=1e-3, depth_variance=False, apply_adam=True):
+        """One iteration on camera-frame directions [R,3] with their gt rgb
+        [R,3] / depth [R]; returns the loss (0-dim device tensor, reused)."""
+        dirs = dirs_cam.reshape(-1, 3).float().contiguous()
+        gt_rgb = rgb.reshape(-1, 3).float().contiguous()
+        gt_d = depth.reshape(-1).float().contiguous()
+        self.step_no += 1
+        flags = (0 if apply_adam else 1) | (2 if depth_variance else 0)
+        rc = _lib().psvo_track_step(self.handle, L.stream_of(self.dev), ctypes.addressof(self.desc), dirs.shape[0],
+                                    dirs.data_ptr(), gt_rgb.data_ptr(), gt_d.data_ptr(), self.pose.data_ptr(),
+                                    self.pose_m.data_ptr(), self.pose_v.data_ptr(), float(lr), int(seed),
+                                    self.step_no, flags, self.pose_grad.data_ptr(), self.loss_out.data_ptr(),
+                                    ctypes.addressof(self.stats))
+        if rc != 0:
+            raise L.PsvoError(f"psvo_track_step failed (code {rc}): {_lib().psvo_last_error().decode()}")
+        return self.loss_out[0]
+
+    def track_frame(self, frame_pose, curr_frame, N_rays=512, num_iterations=10, learning_rate=1e-3,
+                    depth_variance=False, seed=None):
+        """track_frame (render_helpers.py:679-761) on the native step: samples
+        N_rays pixels per iteration from curr_frame (sample_rays → sample_idx)
+        and returns an OptimizablePose holding the optimised parameters."""
+        from .pose import OptimizablePose
+        self.reset(frame_pose.data.detach())
+        dirs_all = curr_frame.rays_d.reshape(-1, 3)
+        rgb_all = curr_frame.rgb.reshape(-1, 3)
+        depth_all = curr_frame.depth.reshape(-1)
+        base = int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed)
+        for it in range(num_iterations):
+            curr_frame.sample_rays(N_rays)
+            idx = curr_frame.sample_idx
+            self.step(dirs_all.index_select(0, idx), rgb_all.index_select(0, idx), depth_all.index_select(0, idx),
+                      base + it, learning_rate, depth_variance)
+        return OptimizablePose(self.pose.detach().clone())
 
     @property
     def last_stats(self):

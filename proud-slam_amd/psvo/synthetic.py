@@ -248,9 +248,11 @@ class SyntheticFrame:
         """gumbel top-k over a uniform pixel distribution, on the frame's device"""
         u = torch.rand(self.h * self.w, generator=self.gen, device=self.depth.device)
         g = -torch.log(-torch.log(u + 1e-7) + 1e-7)
+        idx = torch.topk(g, n).indices.sort().values
         mask = torch.zeros(self.h * self.w, dtype=torch.bool, device=self.depth.device)
-        mask[torch.topk(g, n).indices] = True
+        mask[idx] = True
         self.sample_mask = mask.view(self.h, self.w)
+        self.sample_idx = idx  # the mask's pixels in row-major order (no host sync to gather them)
 
 
 @dataclass

@@ -51,6 +51,36 @@ def main():
         el = time.perf_counter() - t0
         out["frozen_map" if frozen else "map_requires_grad"] = {"ms_per_iteration": 1e3 * el / iters,
                                                                 "rays_per_s": 1024 * iters / el}
+    # native step (psvo_track_step): one libpsvo call per iteration
+    from psvo.engine import TrackingEngine  # noqa: E402
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").cuda()
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    ms = map_states(tree, emb.clone(), scene.voxel_size, device="cuda")
+    eng = TrackingEngine(ms, dec, scene.voxel_size, 0.0078, 0.1, 10.0)
+    pose0 = OptimizablePose.from_matrix(T)
+    eng.track_frame(pose0, frame, N_rays=1024, num_iterations=3, depth_variance=True, seed=0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.track_frame(pose0, frame, N_rays=1024, num_iterations=iters, depth_variance=True, seed=1)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["native_track_step"] = {"ms_per_iteration": 1e3 * el / iters, "rays_per_s": 1024 * iters / el}
+    # the step alone (rays already gathered: no frame sampling between steps)
+    frame.sample_rays(1024)
+    idx = frame.sample_idx
+    dirs = frame.rays_d.reshape(-1, 3)[idx]
+    rgb = frame.rgb.reshape(-1, 3)[idx]
+    dep = frame.depth.reshape(-1)[idx]
+    eng.reset(pose0.data)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(iters):
+        eng.step(dirs, rgb, dep, seed=it, depth_variance=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["native_step_only"] = {"ms_per_iteration": 1e3 * el / iters, "rays_per_s": 1024 * iters / el}
+    eng.close()
     print(json.dumps({"track_frame": out, "iterations": iters, "rays_per_iteration": 1024}))
 
 

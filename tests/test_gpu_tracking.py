@@ -133,3 +133,118 @@ def test_track_frame_runs():
     assert torch.isfinite(pose.data).all()
     assert hit.dtype == torch.bool and int(hit.sum()) > 0
     assert float((pose.data.detach().cpu() - pose0.data).abs().max()) > 0  # the pose moved
+
+
+def _native_setup():
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    scene, ms_cpu, emb, T, _ = _setup()
+    torch.manual_seed(0)
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    ms = {"voxel_center_xyz": ms_cpu["voxel_center_xyz"].to(DEV), "voxel_structure": ms_cpu["voxel_structure"].to(DEV),
+          "voxel_vertex_idx": ms_cpu["voxel_vertex_idx"].to(DEV), "voxel_vertex_emb": emb.to(DEV)}
+    crit = Criterion(types.SimpleNamespace(criteria=dict(CRIT, sdf_truncation=0.1), data_specs={"max_depth": 10.0}))
+    return scene, ms, dec, crit, T
+
+
+@pytest.mark.parametrize("depth_variance", [False, True])
+def test_native_track_step_matches_autograd(depth_variance):
+    """psvo_track_step (one call: pose → rays → render → loss with the
+    on-device median filter → pose gradient → Adam) against the drop-in
+    autograd iteration on the same rays and sampler seed: same loss, pose
+    gradient and updated pose."""
+    from psvo.engine import TrackingEngine
+    from psvo.render_helpers import render_rays
+    from psvo import synthetic as syn
+    scene, ms, dec, crit, T = _native_setup()
+    frame = syn.SyntheticFrame(scene, T, scale=0.2, seed=1)
+    frame.sample_rays(1024)
+    mask = frame.sample_mask
+    dirs, rgb, depth = frame.rays_d[mask], frame.rgb[mask], frame.depth[mask]
+    # drop-in: render_rays + Criterion + autograd + torch Adam
+    pose = _perturbed(T).to(DEV)
+    opt = torch.optim.Adam(pose.parameters(), lr=1e-3)
+    ro, rd = _rays(pose, frame, mask)
+    out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, seed=11)
+    out["ray_mask"] = out["ray_mask"].view(-1)
+    loss, _ = crit(out, (rgb, depth), weight_depth_loss=depth_variance)
+    opt.zero_grad()
+    loss.backward()
+    g_ref = pose.data.grad.clone()
+    opt.step()
+    # native
+    eng = TrackingEngine(ms, dec, scene.voxel_size, 0.01, 0.1, 10.0, CRIT, 10.0)
+    eng.reset(_perturbed(T).data)
+    loss_n = eng.step(dirs, rgb, depth, seed=11, lr=1e-3, depth_variance=depth_variance)
+    torch.cuda.synchronize()
+    assert eng.last_stats[0] > 0
+    np.testing.assert_allclose(float(loss_n), float(loss), rtol=2e-5)
+    g = eng.pose_grad[:6]
+    assert float((g - g_ref).abs().max()) <= 1e-3 * float(g_ref.abs().max()), (g, g_ref)
+    torch.testing.assert_close(eng.pose, pose.data.detach(), rtol=0, atol=2e-6)
+    eng.close()
+
+
+def test_pose_rays_and_grad_kernels():
+    """psvo_pose_rays / psvo_pose_grad against torch autograd through
+    OptimizablePose.rotation() (se3pose.py:23-31) for random poses, including
+    the identity rotation (w = 0)."""
+    from psvo import _lib as L
+    from psvo.pose import OptimizablePose
+    g = torch.Generator().manual_seed(4)
+    n = 777
+    for w_scale in (0.0, 0.05, 1.3):
+        data = torch.cat([torch.randn(3, generator=g), torch.randn(3, generator=g) * w_scale])
+        pose = OptimizablePose(data).to(DEV)
+        dirs = torch.randn(n, 3, generator=g).to(DEV)
+        rd_ref = dirs @ pose.rotation().transpose(-1, -2)
+        ro_ref = pose.translation().expand_as(rd_ref)
+        go, gd = torch.randn(n, 3, generator=g).to(DEV), torch.randn(n, 3, generator=g).to(DEV)
+        ((ro_ref * go).sum() + (rd_ref * gd).sum()).backward()
+        ro, rd = torch.empty_like(dirs), torch.empty_like(dirs)
+        p = pose.data.detach().contiguous()
+        L.call("psvo_pose_rays", L.stream_of(dirs.device), n, p, dirs, ro, rd)
+        torch.testing.assert_close(ro, ro_ref.detach(), rtol=0, atol=0)
+        torch.testing.assert_close(rd, rd_ref.detach(), rtol=1e-5, atol=1e-5)
+        # only the first 500 "hit" rays, at rows given by rank_ray
+        rank = torch.randperm(n, generator=g)[:500].int().to(DEV)
+        grad = torch.empty(6, device=DEV)
+        L.call("psvo_pose_grad", L.stream_of(dirs.device), 500, rank, dirs, go, gd, p, grad)
+        sel = rank.long()
+        pose.data.grad = None
+        rd_ref = dirs[sel] @ pose.rotation().transpose(-1, -2)
+        ((pose.translation().expand_as(rd_ref) * go[sel]).sum() + (rd_ref * gd[sel]).sum()).backward()
+        ref = pose.data.grad
+        assert float((grad - ref).abs().max()) <= 1e-4 * float(ref.abs().max()), (w_scale, grad, ref)
+
+
+def test_native_track_frame_matches_dropin_trajectory():
+    """Three iterations of TrackingEngine.track_frame against the drop-in
+    loop (same frame sampling and per-iteration sampler seeds): same pose."""
+    from psvo.engine import TrackingEngine
+    from psvo.render_helpers import render_rays
+    from psvo import synthetic as syn
+    scene, ms, dec, crit, T = _native_setup()
+    iters, base = 3, 1234
+    frame = syn.SyntheticFrame(scene, T, scale=0.2, seed=7)
+    pose = _perturbed(T).to(DEV)
+    opt = torch.optim.Adam(pose.parameters(), lr=1e-3)
+    for it in range(iters):
+        frame.sample_rays(1024)
+        mask = frame.sample_mask
+        ro, rd = _rays(pose, frame, mask)
+        out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, seed=base + it)
+        out["ray_mask"] = out["ray_mask"].view(-1)
+        loss, _ = crit(out, (frame.rgb[mask], frame.depth[mask]), weight_depth_loss=True)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    eng = TrackingEngine(ms, dec, scene.voxel_size, 0.01, 0.1, 10.0, CRIT, 10.0)
+    frame2 = syn.SyntheticFrame(scene, T, scale=0.2, seed=7)
+    out_pose = eng.track_frame(_perturbed(T), frame2, N_rays=1024, num_iterations=iters, depth_variance=True,
+                               seed=base)
+    torch.testing.assert_close(out_pose.data, pose.data.detach(), rtol=0, atol=1e-5)
+    assert float((out_pose.data.cpu() - _perturbed(T).data).abs().max()) > 1e-4
+    eng.close()
