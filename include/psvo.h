@@ -175,7 +175,8 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
  * Training mode: masks u64[M][2][3] (ReLU masks, needed by any psvo_mlp_bwd)
  * and act f32[4][ceil(M/64)*64*128] (h1, h2, f, c1 in 32-sample CF tiles, see
  * mlp.hip; needed only for weight gradients) are written when non-NULL;
- * act requires masks.  Inference: both NULL. */
+ * act requires masks.  Inference: both NULL; rgb NULL as well: the sdf
+ * alone (Decoder.get_sdf, mesh lattices — h1, h2 and W3's sdf row only). */
 int64_t psvo_mlp_image_floats(void);
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
@@ -260,6 +261,38 @@ int psvo_pose_rays(void *stream, int64_t n, const float *pose, const float *dirs
  * rays at rows rank_ray[r] (psvo_interp_bwd's output), through rotation(). */
 int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,
                    const float *g_d, const float *pose, float *grad);
+
+/* ---- mesh extraction (csrc/mesh.hip; mesh_util.py:80-169) -------------
+ * On the SURFACE voxels (centres f32[n,3], vertex_idx i32[n,8]) of
+ * Mapping.extract_mesh (mapping.py:420-431). */
+/* The marching-cubes case table (host copy): ntri[256], tri[256][36] cube
+ * edge ids (edge = axis·4 + o1 + 2·o2; corner b = (b&1, b>>1&1, b>>2&1)). */
+int psvo_mesh_case_table(int8_t *ntri, int8_t *tri);
+/* torch.linspace(-0.5, 0.5, res) as the CPU computes it (host call). */
+int psvo_mesh_linspace(int res, float *out);
+/* get_scores' lattice features (render_helpers.py:243-294): feat f32[n·res³,16],
+ * voxel-major, lattice (i,j,k) row-major, x = lin[i,j,k]·voxel + centre. */
+int psvo_mesh_grid_feat(void *stream, int64_t n_vox, int res, float voxel_size, const float *centres,
+                        const int *vertex_idx, const float *emb, float *feat);
+/* eval_points' features (render_helpers.py:297-328) at xyz f32[n,3] in voxel
+ * rows row i32[n] (row < 0: zero features). */
+int psvo_mesh_point_feat(void *stream, int64_t n, float voxel_size, const float *xyz, const int *row,
+                         const float *centres, const int *vertex_idx, const float *emb, float *feat);
+/* Marching cubes over sdf f32[n·res³] (res ≤ 16), per voxel, skipping voxels
+ * without a sign change (mesh_util.py:149-169): count vertices nv / triangles
+ * nt i32[n], exclusive offsets vbase / tbase i64[n] and totals i64[2] = {V, F}
+ * (device); then emit verts f32[V,3] = ((lattice pos)/(res−1) − ½)·voxel +
+ * centre and faces i32[F,3] (vertex ids, voxel-major, normals towards sdf > 0). */
+int psvo_mesh_mc_count(void *stream, int64_t n_vox, int res, const float *sdf, int *nv, int *nt, int64_t *vbase,
+                       int64_t *tbase, int64_t *totals);
+int psvo_mesh_mc_emit(void *stream, int64_t n_vox, int res, float voxel_size, const float *sdf, const float *centres,
+                      const int *nv, const int64_t *vbase, const int64_t *tbase, float *verts, int *faces);
+/* Vertex colours' voxel lookup (mesh_util.py:112-125): row[v] = the row of
+ * voxels f32[n,4] whose min corner equals verts[v] // voxel (torch floor
+ * division), −1 if none; table: i32[4·psvo_mesh_vox_map_slots(n)] scratch. */
+int64_t psvo_mesh_vox_map_slots(int64_t n_vox);
+int psvo_mesh_vertex_rows(void *stream, int64_t n_vox, const float *voxels, int64_t n_verts, const float *verts,
+                          float voxel_size, int *table, int *row);
 
 /* ---- optimiser ------------------------------------------------------- */
 /* One Adam step (torch.optim.Adam, amsgrad off) over n_tensors f32 tensors:

@@ -1104,6 +1104,55 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     wait_vm(0);
 }
 
+// sdf only (Decoder.get_sdf; mesh lattices): h1, h2 and the sdf row of W3 —
+// 18.3 of the 53.7 k MACs per sample.  W1 and W2 stay resident (77 KB of
+// LDS, no staging in the loop); the same instruction sequence as
+// k_mlp_fwd2's first two layers, so the sdf is bit-identical to its output.
+constexpr int kLdsSdf2 = (kF2Buf0 + 16384) * 4;
+
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m, const float *__restrict__ feat,
+                                                            const float *__restrict__ img,
+                                                            float *__restrict__ sdf_out) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    float *w2 = lds + kF2Buf0;
+    int64_t t = blockIdx.x;
+    float xn[8];
+    {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        load_x(feat, s, s < m, h, xn);
+    }
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
+    stage8(w2, img + kImgF2, 16384, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    for (; t < n_wg_tiles; t += gridDim.x) {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        const bool valid = s < m;
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = xn[i];
+        if (t + gridDim.x < n_wg_tiles) {
+            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+            load_x(feat, sn, sn < m, h, xn);
+        }
+        f32x16 a[kNB], bacc[kNB];
+        init_bias(a, lds + kOffB1, h);
+        gemm_x(lds + kF2W1, x, a, lane);
+        (void)relu(a);
+        init_bias(bacc, lds + kOffB2, h);
+        gemm_acc<kNB, kNB>(w2, a, bacc, lane);
+        (void)relu(bacc);
+        const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
+        if (valid && h == 0) sdf_out[s] = sdf;
+    }
+    wait_vm(0);
+}
+
 // ---------------------------------------------------------------------------
 // backward (data), persistent + double-buffered like k_mlp_fwd2: 8 waves ×
 // 32 samples per tile; W4ᵀ / W2ᵀ stream through an 80-KB buffer and W3ᵀ /
@@ -1281,6 +1330,19 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     hipStream_t st = as_stream(stream);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
     hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
+    if (rgb == nullptr) {  // sdf only (inference)
+        PSVO_REQUIRE(act == nullptr && masks == nullptr, "mlp_fwd: the sdf-only forward is inference only");
+        static bool attr_s = false;
+        if (!attr_s) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_sdf2),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSdf2);
+            attr_s = true;
+        }
+        const int64_t tiles = div_up(m, kF2Tile);
+        const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
+        hipLaunchKernelGGL(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf);
+        return check_launch("mlp_fwd");
+    }
     if (use_fwd2()) {
         static bool attr2 = false;
         if (!attr2) {

@@ -55,6 +55,14 @@ _SIGNATURES = {
     "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _u64, _i64, _i32, _vp, _vp,
                                _vp]),
     "psvo_pose_rays": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "psvo_mesh_linspace": (_i32, [_i32, _vp]),
+    "psvo_mesh_case_table": (_i32, [_vp, _vp]),
+    "psvo_mesh_grid_feat": (_i32, [_vp, _i64, _i32, _f32, _vp, _vp, _vp, _vp]),
+    "psvo_mesh_point_feat": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "psvo_mesh_mc_count": (_i32, [_vp, _i64, _i32] + [_vp] * 6),
+    "psvo_mesh_mc_emit": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 7),
+    "psvo_mesh_vox_map_slots": (_i64, [_i64]),
+    "psvo_mesh_vertex_rows": (_i32, [_vp, _i64, _vp, _i64, _vp, _f32, _vp, _vp]),
     "psvo_pose_grad": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "psvo_criterion_depth_filter": (_i32, [_vp, _i64, _i32] + [_vp] * 7),
     "psvo_criterion_sums_ex": (_i32, [_vp, _i64, _i32, _i32, _f32, _f32] + [_vp] * 11),

@@ -15,6 +15,9 @@ tensorboardX) are replaced by empty stubs, torch.Tensor.cuda by identity
 a temp dir.  Noise drawn inside InverseCDFRaySampling is recorded so the
 build can inject the same noise.
 
+M_mesh_A.npz: the reference's get_scores / eval_points (mesh extraction's
+lattice scores and vertex colours) on the A octree's first 40 SURFACE voxels.
+
 Usage:  python tests/golden/make_golden.py     (writes tests/golden/*.npz)
 """
 from __future__ import annotations
@@ -215,6 +218,34 @@ def run_case(name, rh, nrgbd, crit_mod, noise_log):
     return rec
 
 
+def run_mesh_case(rh, nrgbd):
+    """get_scores / eval_points (render_helpers.py:243-328) on the SURFACE
+    voxels Mapping.extract_mesh selects (mapping.py:420-431), for the first
+    40 of them (two of get_scores' 32-voxel chunks)."""
+    inp = case_inputs("A_voxels_center")
+    voxels, children, features = _octree(inp["vox"], inp["grid_dim"])
+    torch.manual_seed(4321)
+    emb = torch.randn(voxels.shape[0], 16) * 0.3
+    dec = nrgbd.Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none", multires=0)
+    vt, ft = torch.from_numpy(voxels), torch.from_numpy(features)
+    keep = ~ft.eq(-1).any(-1)
+    sv, sf = vt[keep][:40], ft[keep][:40]
+    centres = (sv[:, :3] + sv[:, -1:] / 2) * 0.2
+    states = {"voxel_vertex_idx": sf, "voxel_center_xyz": centres, "voxel_vertex_emb": emb}
+    with torch.no_grad():
+        scores = rh.get_scores(dec, states, 0.2, bits=8)
+        g = torch.Generator().manual_seed(7)
+        idx = torch.randint(0, sv.shape[0], (300,), generator=g)
+        pts = centres[idx] + (torch.rand(300, 3, generator=g) - 0.5) * 0.2
+        colours = rh.eval_points(dec, states, pts, idx, 0.2)
+    rec = dict(voxels=sv.numpy(), features=sf.numpy(), centres=centres.numpy(), embeddings=emb.numpy(),
+               voxel_size=np.float32(0.2), res=np.int64(8), scores=scores.numpy(), points=pts.numpy(),
+               point_idx=idx.numpy().astype(np.int64), point_rgb=colours.numpy())
+    for k, v in dec.state_dict().items():
+        rec["dec." + k] = v.numpy()
+    return rec
+
+
 def main():
     noise_log = []
     _install_stubs(noise_log)
@@ -231,6 +262,11 @@ def main():
                       f"R_hit={int(rec['hits'].sum())} P={rec['hit_idx'].shape[-1]} S={rec['z_vals'].shape[-1]} "
                       f"loss={float(rec['loss']):.6f} -> {os.path.relpath(path, REPO)} "
                       f"({os.path.getsize(path) // 1024} KiB)")
+            rec = run_mesh_case(rh, nrgbd)
+            path = os.path.join(OUT_DIR, "M_mesh_A.npz")
+            np.savez_compressed(path, **rec)
+            print(f"M_mesh_A: voxels={rec['voxels'].shape[0]} scores={tuple(rec['scores'].shape)} "
+                  f"-> {os.path.relpath(path, REPO)} ({os.path.getsize(path) // 1024} KiB)")
         finally:
             os.chdir(cwd)
 
