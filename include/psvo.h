@@ -31,6 +31,9 @@
  *                                 (render_helpers.py:581-596, :668-672)
  *   psvo_map_step                 one bundle_adjust_frames iteration (render_helpers.py:609-672):
  *                                 render_rays + Criterion + backward + both Adam steps
+ *   psvo_share_*                  share.ShareData (src/share.py:27-166) served by a BaseManager
+ *                                 (voxslam.py:28-33): update_share_data (mapping.py:236-248) /
+ *                                 do_tracking (tracking.py:114-125) state exchange, device-resident
  *   psvo_octree_*                 torch.classes.svo.Octree (third_party/sparse_octree/src/bindings.cpp:4-35,
  *                                 octree.cpp:104-294, :561-687) — CPU builder, host memory
  */
@@ -47,7 +50,9 @@ enum {
     PSVO_OK = 0,
     PSVO_E_INVALID = 1,   /* bad argument (shape / size / null pointer) */
     PSVO_E_LAUNCH = 2,    /* HIP launch or runtime error */
-    PSVO_E_OVERFLOW = 3   /* DFS stack overflow (reference: assert(ptr < 256)) */
+    PSVO_E_OVERFLOW = 3,  /* DFS stack overflow (reference: assert(ptr < 256)) */
+    PSVO_E_BUSY = 4,      /* share channel: no free slot within the timeout */
+    PSVO_E_SYSTEM = 5     /* share channel: shared-memory / OS error */
 };
 
 const char *psvo_last_error(void);
@@ -389,6 +394,42 @@ int psvo_dtree_export(void *tree, void *stream, float voxel_size, float *voxels,
 /* hit[i·corners + j] = leaf at voxel i's corner j exists (corners 1: has_voxel,
  * 8: the corner keys try_insert counts, octree.cpp:381-474) */
 int psvo_dtree_probe(void *tree, void *stream, const int *vox, int64_t n, int corners, int *hit);
+
+/* ---- tracker <-> mapper state exchange (csrc/share.cpp) ----------------
+ * A POSIX shared-memory block `name` ("/…") holds a robust process-shared
+ * mutex, PSVO_SHARE_FLAGS int flags (stop_mapping / stop_tracking), the
+ * tracked trajectory and PSVO_SHARE_CHANNELS channels of 3 device slots.  A
+ * slot is a device allocation of the publishing process exported with
+ * hipIpcGetMemHandle; publish copies D2D into a slot no reader holds and makes
+ * it the latest (one stream sync); readers pin the latest slot, copy D2D into
+ * their own buffers and unpin.  Unlike the kernels above, publish / read
+ * synchronise `stream` (the snapshot must be complete before it is visible). */
+#define PSVO_SHARE_CHANNELS 8
+#define PSVO_SHARE_FLAGS 8
+#define PSVO_SHARE_META_CAP 65536
+#define PSVO_SHARE_TRAJ_CAP 65536
+#define PSVO_SHARE_POSE_DIM 8   /* trajectory row = [n, pose[0..n), 0...], n <= 7 */
+int64_t psvo_share_block_bytes(void);
+void *psvo_share_create(const char *name);  /* NULL on error (psvo_last_error) */
+void *psvo_share_attach(const char *name);
+void psvo_share_detach(void *share);        /* frees this process's slots, closes its IPC mappings */
+int psvo_share_unlink(const char *name);
+int psvo_share_set_flag(void *share, int i, int value);
+int psvo_share_get_flag(void *share, int i);   /* -1 on bad arguments */
+int psvo_share_push_pose(void *share, const double *pose, int n);
+int64_t psvo_share_trajectory(void *share, double *out, int64_t cap);  /* rows [cap, 8]; returns the pose count */
+/* writer: n device buffers -> a free slot of `channel` at 256-B aligned
+ * offsets (written to offsets[n]) + opaque meta; *version = new version */
+int psvo_share_publish(void *share, void *stream, int channel, int n, const void *const *srcs, const int64_t *bytes,
+                       const void *meta, int64_t meta_len, int timeout_ms, int64_t *offsets, uint64_t *version);
+/* reader: 1 = pinned the latest snapshot newer than `after` (slot, version,
+ * meta, used bytes, device base pointer filled), 0 = nothing newer, < 0 = -error */
+int psvo_share_acquire(void *share, int channel, uint64_t after, int *slot, uint64_t *version, void *meta,
+                       int64_t meta_cap, int64_t *meta_len, int64_t *used, void **base);
+int psvo_share_read(void *share, void *stream, int channel, int slot, int n, void *const *dsts,
+                    const int64_t *offsets, const int64_t *bytes, const void *base);
+int psvo_share_release(void *share, int channel, int slot);
+uint64_t psvo_share_version(void *share, int channel);   /* latest version, 0 = none */
 
 /* ---- octree builder (CPU, host memory) -------------------------------- */
 void *psvo_octree_new(int grid_dim, int feat_dim, double voxel_size, int max_points_per_leaf);

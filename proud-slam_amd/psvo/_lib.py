@@ -75,6 +75,20 @@ _SIGNATURES = {
     "psvo_dtree_count_leaves": (_i64, [_vp, _vp]),
     "psvo_dtree_export": (_i32, [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "psvo_dtree_probe": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "psvo_share_block_bytes": (_i64, []),
+    "psvo_share_create": (_vp, [ctypes.c_char_p]),
+    "psvo_share_attach": (_vp, [ctypes.c_char_p]),
+    "psvo_share_detach": (None, [_vp]),
+    "psvo_share_unlink": (_i32, [ctypes.c_char_p]),
+    "psvo_share_set_flag": (_i32, [_vp, _i32, _i32]),
+    "psvo_share_get_flag": (_i32, [_vp, _i32]),
+    "psvo_share_push_pose": (_i32, [_vp, _vp, _i32]),
+    "psvo_share_trajectory": (_i64, [_vp, _vp, _i64]),
+    "psvo_share_publish": (_i32, [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
+    "psvo_share_acquire": (_i32, [_vp, _i32, _u64, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "psvo_share_read": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "psvo_share_release": (_i32, [_vp, _i32, _i32]),
+    "psvo_share_version": (_u64, [_vp, _i32]),
     "psvo_octree_new": (_vp, [_i32, _i32, _f64, _i32]),
     "psvo_octree_free": (None, [_vp]),
     "psvo_octree_insert": (_i32, [_vp, _vp, _i64]),
