@@ -237,11 +237,24 @@ def main():
             record_stats(s.m, s.r_hit, s.visits, s.s_max)
         return loss
 
+    eng_it = [0]  # engine iterations so far: the next batch is always the one already queued
+
+    def eng_batch(it):
+        return batches[it % len(batches)], 1000003 * rank + it
+
     def step_engine(i, record=False):
-        """The same iteration as one native call (psvo_map_step); with N > 1 the
+        """The same iteration as one native call (psvo_map_step); the next
+        batch's ray query is queued first (psvo_map_query, side stream: it
+        reads only rays + octree, so it overlaps this step).  With N > 1 the
         flat gradient bucket is all-reduced (RCCL) before the Adam steps."""
-        ro, rd, rgb, depth = batches[i % len(batches)]
-        loss = engine.step(ro, rd, rgb, depth, seed=1000003 * rank + i, apply_adam=(world == 1))
+        it = eng_it[0]
+        eng_it[0] += 1
+        (ro, rd, rgb, depth), seed = eng_batch(it)
+        if not engine._queued:
+            engine.query(ro, rd, seed)
+        (nro, nrd, _, _), nseed = eng_batch(it + 1)
+        engine.query(nro, nrd, nseed)
+        loss = engine.step(ro, rd, rgb, depth, seed=seed, apply_adam=(world == 1))
         if world > 1:
             dist.all_reduce(engine.grad_flat)
             engine.grad_flat.div_(world)

@@ -353,6 +353,14 @@ int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region
  * then call psvo_map_adam.  loss_out: device f32[PSVO_CRIT_OUT_WORDS]
  * (PSVO_CRIT_* words); stats_out: host int[PSVO_STAT_WORDS] or NULL.  Two
  * stats read-backs synchronise the stream; everything else is queued. */
+/* Queue the query (intersection + sampling + statistics read-back) of the
+ * NEXT batch on the engine's side stream, ordered after `stream`'s current
+ * position: the step that consumes it (psvo_map_step with the same rays,
+ * n_rays and seed) then starts without a read-back stall, and the query runs
+ * beside the current step's decoder kernels.  At most two queued; the rays
+ * must stay valid until the consuming step. */
+int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
+                   const float *rays_d, uint64_t seed);
 int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
                   const float *rays_d, const float *gt_rgb, const float *gt_depth, uint64_t seed, int64_t adam_step,
                   int flags, float *loss_out, int *stats_out);

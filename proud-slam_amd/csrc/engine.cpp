@@ -20,9 +20,12 @@
 namespace psvo {
 namespace {
 
+// buffers of one query (intersection + sampling of a ray batch): a query set
+enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
+             kOffsets, kQSlots };
+// buffers of the rest of a step
 enum Slot {
-    kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-    kOffsets, kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
+    kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
     kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSlots
 };
@@ -30,6 +33,24 @@ enum Slot {
 struct Arena {
     void *p[kSlots] = {};
     size_t cap[kSlots] = {};
+};
+
+// One ray batch's query: its buffers, the pinned statistics it reads back
+// and the events that order it against the steps.  psvo_map_query runs a
+// query on the engine's side stream one step ahead (the query depends only on
+// the rays and the octree, not on the embeddings / decoder the running step
+// updates), so the step that consumes it finds its sizes already on the host.
+struct QuerySet {
+    Arena a;                      // slots kStats..kOffsets
+    int *host_stats = nullptr;    // pinned, PSVO_STAT_WORDS
+    hipEvent_t done = nullptr;    // statistics landed (after the sampler)
+    hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
+    bool freed_recorded = false;
+    bool pending = false;
+    int64_t R = 0;
+    const float *ro = nullptr, *rd = nullptr;
+    uint64_t seed = 0;
+    int max_steps = 0;
 };
 
 }  // namespace
@@ -46,9 +67,11 @@ struct EngineTimer {
 
 struct psvo_engine {
     psvo::Arena a;
-    int *host_stats = nullptr;  // pinned, PSVO_STAT_WORDS ints
+    psvo::QuerySet qs[2];           // FIFO of queries: head = the next step's
+    int q_head = 0, q_count = 0;
+    hipStream_t side = nullptr;     // psvo_map_query's stream
+    hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
     EngineTimer tm;
-    hipEvent_t ready = nullptr;     // read-back completion (spin-polled)
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
 };
@@ -65,22 +88,26 @@ namespace {
 
 // device buffer of at least `bytes` for `slot`; growing synchronises the
 // stream first (the old buffer may still be read by queued kernels)
-void *slot_buf(psvo_engine *e, hipStream_t st, int slot, size_t bytes, int *rc) {
+void *arena_buf(Arena &a, hipStream_t st, int slot, size_t bytes, int *rc) {
     if (bytes == 0) bytes = 16;
-    if (e->a.cap[slot] >= bytes) return e->a.p[slot];
-    if (e->a.p[slot]) {
+    if (a.cap[slot] >= bytes) return a.p[slot];
+    if (a.p[slot]) {
         (void)hipStreamSynchronize(st);
-        (void)hipFree(e->a.p[slot]);
-        e->a.p[slot] = nullptr;
-        e->a.cap[slot] = 0;
+        (void)hipFree(a.p[slot]);
+        a.p[slot] = nullptr;
+        a.cap[slot] = 0;
     }
     const size_t cap = bytes + bytes / 4;  // headroom against per-step size jitter
-    if (hipMalloc(&e->a.p[slot], cap) != hipSuccess) {
+    if (hipMalloc(&a.p[slot], cap) != hipSuccess) {
         *rc = set_error(PSVO_E_LAUNCH, "engine: hipMalloc(%zu) failed", cap);
         return nullptr;
     }
-    e->a.cap[slot] = cap;
-    return e->a.p[slot];
+    a.cap[slot] = cap;
+    return a.p[slot];
+}
+
+void *slot_buf(psvo_engine *e, hipStream_t st, int slot, size_t bytes, int *rc) {
+    return arena_buf(e->a, st, slot, bytes, rc);
 }
 
 void timer_collect(psvo_engine *e) {
@@ -100,32 +127,43 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
     if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
 }
 
-// 32-byte read-back of the device statistics; the host spins on an event
-// (instead of a blocking stream sync) so it resumes launching within ~1 µs
-// of the copy completing.
-int read_stats(psvo_engine *e, hipStream_t st, const int *dstats) {
-    if (hipMemcpyAsync(e->host_stats, dstats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) !=
-        hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "engine: stats read-back failed");
-    if (!e->ready && hipEventCreateWithFlags(&e->ready, hipEventDisableTiming) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "engine: hipEventCreate failed");
-    if (hipEventRecord(e->ready, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
+// The host spins on an event (instead of a blocking sync) so it resumes
+// launching within ~1 µs of the read-back completing.
+int spin_wait(hipEvent_t ev, const char *who) {
     hipError_t q;
-    while ((q = hipEventQuery(e->ready)) == hipErrorNotReady) {
+    while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
     }
-    if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: stats read-back: %s", hipGetErrorString(q));
+    if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
     return PSVO_OK;
+}
+
+int query_set_init(QuerySet &s) {
+    if (s.host_stats) return PSVO_OK;
+    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_stats), PSVO_STAT_WORDS * sizeof(int), hipHostMallocDefault) !=
+            hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s.freed, hipEventDisableTiming) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: query set allocation failed");
+    return PSVO_OK;
+}
+
+void query_set_free(QuerySet &s) {
+    for (int k = 0; k < kQSlots; ++k)
+        if (s.a.p[k]) (void)hipFree(s.a.p[k]);
+    if (s.host_stats) (void)hipHostFree(s.host_stats);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.freed) (void)hipEventDestroy(s.freed);
 }
 
 }  // namespace
 
 extern "C" psvo_engine *psvo_engine_new(void) {
     psvo_engine *e = new psvo_engine();
-    if (hipHostMalloc(reinterpret_cast<void **>(&e->host_stats), PSVO_STAT_WORDS * sizeof(int),
-                      hipHostMallocDefault) != hipSuccess) {
-        delete e;
-        return nullptr;
-    }
+    for (auto &q : e->qs)
+        if (query_set_init(q) != PSVO_OK) {
+            psvo_engine_free(e);
+            return nullptr;
+        }
     return e;
 }
 
@@ -160,8 +198,9 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
             if (e->tm.ev[r][k]) (void)hipEventDestroy(e->tm.ev[r][k]);
     for (int s = 0; s < kSlots; ++s)
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
-    if (e->host_stats) (void)hipHostFree(e->host_stats);
-    if (e->ready) (void)hipEventDestroy(e->ready);
+    for (auto &q : e->qs) query_set_free(q);
+    if (e->side) (void)hipStreamDestroy(e->side);
+    if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
 
@@ -223,55 +262,115 @@ struct Render {
     uint64_t *masks;
 };
 
-// render_rays (render_helpers.py:363-556) on the device: intersection, hit
-// ranks, sampling (one stats read-back sizes the sample buffers),
-// interpolation, decoder, compositing.  want_act: keep the decoder
-// activations for weight gradients (mapping); tracking keeps only the masks.
-int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, const float *rays_o,
-           const float *rays_d, uint64_t seed, bool want_act, int *stats_out, const char *who, Render &o) {
+#define Q_BUF(T, name, slot, bytes)                                              \
+    T *name = reinterpret_cast<T *>(arena_buf(q.a, st, slot, (bytes), &rc));    \
+    if (!name) return rc;
+
+// The query half of render_rays (render_helpers.py:363-413): intersection,
+// hit ranks and sampling of one ray batch into query set `q` on stream `st`,
+// then the 32-byte statistics read-back (event q.done).  The sampler reads P,
+// R_hit and max ⌈steps⌉ from `stats` on the device; its buffers are [R, cap]
+// with cap ≥ max_steps = max ⌈Σ(t_out − t_in)/step⌉ + P, bounded by 50 leaf
+// intervals of at most a voxel diagonal (rows are written only up to
+// max_steps; an overflow is flagged and reported by the consumer).
+int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_desc *d, int64_t R,
+                  const float *rays_o, const float *rays_d, uint64_t seed, const char *who) {
     int rc = PSVO_OK;
     void *stream = st;
-    // ---- query: intersection, hit ranks, statistics
-    ENG_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
+    Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
-    ENG_BUF(int, hit_idx, kHitIdx, R * kMaxHits * sizeof(int));
-    ENG_BUF(float, hit_t0, kHitT0, R * kMaxHits * sizeof(float));
-    ENG_BUF(float, hit_t1, kHitT1, R * kMaxHits * sizeof(float));
-    ENG_BUF(int, ray_nv, kRayNv, R * sizeof(int));
-    ENG_BUF(float, ray_dsum, kRayDsum, R * sizeof(float));
-    ENG_BUF(int, ray_rank, kRayRank, R * sizeof(int));
-    ENG_BUF(int, rank_ray, kRankRay, R * sizeof(int));
+    Q_BUF(int, hit_idx, kHitIdx, R * kMaxHits * sizeof(int));
+    Q_BUF(float, hit_t0, kHitT0, R * kMaxHits * sizeof(float));
+    Q_BUF(float, hit_t1, kHitT1, R * kMaxHits * sizeof(float));
+    Q_BUF(int, ray_nv, kRayNv, R * sizeof(int));
+    Q_BUF(float, ray_dsum, kRayDsum, R * sizeof(float));
+    Q_BUF(int, ray_rank, kRayRank, R * sizeof(int));
+    Q_BUF(int, rank_ray, kRankRay, R * sizeof(int));
     mark(e, st, PSVO_TIME_INTERSECT, 0);
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
                                     ray_rank, rank_ray));
     mark(e, st, PSVO_TIME_INTERSECT, 1);
-    // ---- sampling, without a read-back: the sampler reads P, R_hit and
-    // max ⌈steps⌉ from `stats` on the device; its buffers are [R, cap] with
-    // cap ≥ max_steps = max ⌈Σ(t_out − t_in)/step⌉ + P, bounded by 50 leaf
-    // intervals of at most a voxel diagonal (rows are written only up to
-    // max_steps; an overflow is flagged and reported below)
     const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
                           kMaxHits + 1;
-    ENG_BUF(int, s_idx, kSIdx, (size_t)R * max_steps * sizeof(int));
-    ENG_BUF(float, s_depth, kSDepth, (size_t)R * max_steps * sizeof(float));
-    ENG_BUF(float, s_dist, kSDist, (size_t)R * max_steps * sizeof(float));
-    ENG_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
-    ENG_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
+    Q_BUF(int, s_idx, kSIdx, (size_t)R * max_steps * sizeof(int));
+    Q_BUF(float, s_depth, kSDepth, (size_t)R * max_steps * sizeof(float));
+    Q_BUF(float, s_dist, kSDist, (size_t)R * max_steps * sizeof(float));
+    Q_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
+    Q_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
     mark(e, st, PSVO_TIME_SAMPLE, 0);
     ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
                               nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
     mark(e, st, PSVO_TIME_SAMPLE, 1);
-    ENG_CALL(read_stats(e, st, stats));
+    if (hipMemcpyAsync(q.host_stats, stats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord(q.done, st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "%s: stats read-back failed", who);
+    q.R = R;
+    q.ro = rays_o;
+    q.rd = rays_d;
+    q.seed = seed;
+    q.max_steps = max_steps;
+    return PSVO_OK;
+}
+
+// A query set for a step on `st` over (R, rays, seed): the queued one
+// psvo_map_query prepared for exactly this batch, or a fresh query enqueued
+// on `st` itself.
+int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, const float *rays_o,
+               const float *rays_d, uint64_t seed, const char *who, QuerySet **out) {
+    if (e->q_count > 0) {
+        QuerySet &q = e->qs[e->q_head];
+        if (q.R != R || q.ro != rays_o || q.rd != rays_d || q.seed != seed)
+            return set_error(PSVO_E_INVALID, "%s: rays / seed differ from the batch queued by psvo_map_query", who);
+        // the step's kernels read the query's outputs: order the streams
+        if (hipStreamWaitEvent(st, q.done, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        *out = &q;
+        return PSVO_OK;
+    }
+    QuerySet &q = e->qs[e->q_head];
+    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, seed, who));
+    *out = &q;
+    return PSVO_OK;
+}
+
+// Give back the head query set once the step's kernels are queued.
+int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
+    if (hipEventRecord(q->freed, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
+    q->freed_recorded = true;
+    if (e->q_count > 0 && q == &e->qs[e->q_head]) {
+        q->pending = false;
+        e->q_head ^= 1;
+        e->q_count--;
+    }
+    return PSVO_OK;
+}
+
+// render_rays (render_helpers.py:363-556) on the device, after the query:
+// sample compaction (sized by the query's read-back), interpolation, decoder,
+// compositing.  want_act: keep the decoder activations for weight gradients
+// (mapping); tracking keeps only the masks.
+int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qset, const float *rays_o,
+           const float *rays_d, bool want_act, int *stats_out, const char *who, Render &o) {
+    int rc = PSVO_OK;
+    void *stream = st;
+    const int max_steps = qset.max_steps;
+    const int *rank_ray = static_cast<const int *>(qset.a.p[kRankRay]);
+    const int *s_idx = static_cast<const int *>(qset.a.p[kSIdx]);
+    const float *s_depth = static_cast<const float *>(qset.a.p[kSDepth]);
+    const int *ray_ns = static_cast<const int *>(qset.a.p[kRayNs]);
+    const int *offsets = static_cast<const int *>(qset.a.p[kOffsets]);
+    ENG_CALL(spin_wait(qset.done, who));
     timer_collect(e);  // the previous step's events completed before this read-back
-    const int r_hit = e->host_stats[PSVO_STAT_R_HIT];
-    if (e->host_stats[7] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
+    const int *hs = qset.host_stats;
+    const int r_hit = hs[PSVO_STAT_R_HIT];
+    if (hs[7] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
     if (r_hit == 0) return set_error(PSVO_E_INVALID, "%s: no ray hits the octree (render_helpers.py:388)", who);
-    const int s_max = e->host_stats[PSVO_STAT_S_MAX];
-    const int64_t M = e->host_stats[PSVO_STAT_M];
-    if (e->host_stats[7] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
-    if (stats_out) memcpy(stats_out, e->host_stats, PSVO_STAT_WORDS * sizeof(int));
+    const int s_max = hs[PSVO_STAT_S_MAX];
+    const int64_t M = hs[PSVO_STAT_M];
+    if (hs[7] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
+    if (stats_out) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
@@ -314,9 +413,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, co
     o.r_hit = r_hit;
     o.m = M;
     o.s_max = s_max;
-    o.rank_ray = rank_ray;
-    o.ray_ns = ray_ns;
-    o.offsets = offsets;
+    o.rank_ray = const_cast<int *>(rank_ray);
+    o.ray_ns = const_cast<int *>(ray_ns);
+    o.offsets = const_cast<int *>(offsets);
     o.leaf = leaf;
     o.ray_of = ray_of;
     o.tt = tt;
@@ -381,7 +480,9 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     int rc = PSVO_OK;
     const int64_t R = n_rays;
     Render q;
-    ENG_CALL(render(e, st, d, R, rays_o, rays_d, seed, true, stats_out, "map_step", q));
+    QuerySet *qset = nullptr;
+    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset));
+    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q));
     const int64_t M = q.m;
     // ---- loss and backward (d loss = 1)
     float *g_sdf_s, *g_rgb_s;
@@ -421,11 +522,35 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
                              d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
     mark(e, st, PSVO_TIME_INTERP_BWD, 1);
     e->tm.pending = e->tm.on;
+    ENG_CALL(release_query(e, st, qset));
     // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step));
         e->grads_clean = true;
     }
+    return PSVO_OK;
+}
+
+extern "C" int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
+                              const float *rays_o, const float *rays_d, uint64_t seed) {
+    PSVO_REQUIRE(e && d && rays_o && rays_d && n_rays > 0, "map_query: bad arguments");
+    PSVO_REQUIRE(e->q_count < 2, "map_query: two queries already queued (run psvo_map_step)");
+    hipStream_t st = as_stream(stream);
+    if (!e->side) {
+        if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->in_ready, hipEventDisableTiming) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_query: side stream creation failed");
+    }
+    QuerySet &q = e->qs[(e->q_head + e->q_count) & 1];
+    // the rays were produced on the caller's stream; the set's buffers may
+    // still be read by the step that consumed it last
+    if (hipEventRecord(e->in_ready, st) != hipSuccess || hipStreamWaitEvent(e->side, e->in_ready, 0) != hipSuccess ||
+        (q.freed_recorded && hipStreamWaitEvent(e->side, q.freed, 0) != hipSuccess))
+        return set_error(PSVO_E_LAUNCH, "map_query: stream ordering failed");
+    // (a buffer that must grow syncs the side stream first, which includes that wait)
+    ENG_CALL(query_enqueue(e, e->side, q, d, n_rays, rays_o, rays_d, seed, "map_query"));
+    q.pending = true;
+    e->q_count++;
     return PSVO_OK;
 }
 
@@ -445,7 +570,10 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
     ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
     ENG_CALL(psvo_pose_rays(stream, R, pose, dirs_cam, rays_o, rays_d));
     Render q;
-    ENG_CALL(render(e, st, d, R, rays_o, rays_d, seed, false, stats_out, "track_step", q));
+    PSVO_REQUIRE(e->q_count == 0, "track_step: the engine has queued mapping queries");
+    QuerySet *qset = nullptr;
+    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "track_step", &qset));
+    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, false, stats_out, "track_step", q));
     // ---- loss (optionally with the median depth filter) and backward
     float *dtmp = nullptr, *dthr = nullptr;
     if (flags & PSVO_TRACK_DEPTH_FILTER) {
@@ -475,6 +603,7 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
                              d->centres, d->vertex_idx, d->emb, dfeat, nullptr, grad_od, grad_od + R * 3));
     mark(e, st, PSVO_TIME_INTERP_BWD, 1);
     e->tm.pending = e->tm.on;
+    ENG_CALL(release_query(e, st, qset));
     // ---- pose gradient through rotation() and the pose's Adam step
     if (!pose_grad) {
         ENG_BUF(float, gbuf, kPoseGrad, 8 * sizeof(float));

@@ -52,6 +52,7 @@ _SIGNATURES = {
     "psvo_engine_timing": (_i32, [_vp, _vp]),
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
+    "psvo_map_query": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _u64]),
     "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _u64, _i64, _i32, _vp, _vp,
                                _vp]),
     "psvo_pose_rays": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),

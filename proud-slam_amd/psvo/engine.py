@@ -78,17 +78,38 @@ class MappingEngine:
                                      device=self.emb.device)
         d.grad_flat = self.grad_flat.data_ptr()
         self.desc = d
+        self._queued = []
         h = _lib().psvo_engine_new()
         if not h:
             raise L.PsvoError("psvo_engine_new failed")
         self.handle = _vp(h)
 
+    def query(self, rays_o, rays_d, seed):
+        """Queue the next iteration's ray query (intersection + sampling) on the
+        engine's side stream, so that it overlaps the current step and the next
+        step() with the same rays / seed starts without a read-back stall
+        (the query reads only the rays and the octree, which the step does not
+        change)."""
+        ro = rays_o.reshape(-1, 3).float().contiguous()
+        rd = rays_d.reshape(-1, 3).float().contiguous()
+        rc = _lib().psvo_map_query(self.handle, L.stream_of(ro.device), ctypes.addressof(self.desc), ro.shape[0],
+                                   ro.data_ptr(), rd.data_ptr(), int(seed))
+        if rc != 0:
+            raise L.PsvoError(f"psvo_map_query failed (code {rc}): {_lib().psvo_last_error().decode()}")
+        self._queued.append((ro, rd))   # alive until the consuming step has run
+
     def step(self, rays_o, rays_d, rgb, depth, seed, apply_adam=True):
         """One iteration; returns the loss (0-dim device tensor, not synchronised;
         the buffer is reused by the next step).  apply_adam=False stops after the
-        gradients (self.grad_flat) — all-reduce them, then call adam()."""
-        ro = rays_o.reshape(-1, 3).float().contiguous()
-        rd = rays_d.reshape(-1, 3).float().contiguous()
+        gradients (self.grad_flat) — all-reduce them, then call adam().  If
+        query() queued this batch, its results are used."""
+        if self._queued:
+            ro, rd = self._queued[0]
+            if ro.data_ptr() != rays_o.reshape(-1, 3).data_ptr() and rays_o.is_contiguous():
+                raise RuntimeError("MappingEngine.step: rays differ from the queued query")
+        else:
+            ro = rays_o.reshape(-1, 3).float().contiguous()
+            rd = rays_d.reshape(-1, 3).float().contiguous()
         gt_rgb = rgb.reshape(-1, 3).float().contiguous()
         gt_d = depth.reshape(-1).float().contiguous()
         self.step_no += 1
@@ -97,7 +118,10 @@ class MappingEngine:
                                   self.step_no, 0 if apply_adam else 1, self.loss_out.data_ptr(),
                                   ctypes.addressof(self.stats))
         if rc != 0:
+            self.step_no -= 1
             raise L.PsvoError(f"psvo_map_step failed (code {rc}): {_lib().psvo_last_error().decode()}")
+        if self._queued:
+            self._queued.pop(0)   # consumed (the step's kernels are stream-ordered after their last use)
         return self.loss_out[0]
 
     def adam(self):

@@ -6,6 +6,7 @@ order; the decoder gradients are deterministic); embeddings agree up to the
 order of the float atomics in the interpolation backward."""
 import types
 
+import numpy as np
 import pytest
 import torch
 
@@ -80,3 +81,56 @@ def test_engine_matches_autograd_path():
     st = eng.last_stats
     assert st[1] > 0 and st[4] > 0  # R_hit, M
     eng.close()
+
+
+def test_engine_query_ahead_matches_inline():
+    """psvo_map_query (next batch's intersection + sampling on the side stream,
+    one step ahead) gives the same iterations as queries inline in the step."""
+    from psvo import _lib as L
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ro, rd, rgb, dep = (t.reshape(-1, t.shape[-1]) if t.dim() == 3 else t.reshape(-1)
+                        for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
+    R = ro.shape[0]
+    halves = [(ro[s].to(DEV).contiguous(), rd[s].to(DEV).contiguous(), rgb[s].to(DEV).contiguous(),
+               dep[s].to(DEV).contiguous()) for s in (slice(0, R // 2), slice(R // 2, R))]
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    engines, embs, decs = [], [], []
+    for _ in range(2):
+        from copy import deepcopy
+        d = deepcopy(dec)
+        e = emb0.clone().to(DEV)
+        engines.append(MappingEngine(map_states(tree, e, 0.2, device=DEV), d, 0.2, 0.01, truncation=0.1,
+                                     max_distance=10.0, criteria=crit, max_depth=10.0))
+        embs.append(e)
+        decs.append(d)
+    inline, ahead = engines
+    n_it = 5
+    la, lb = [], []
+    for it in range(n_it):
+        b = halves[it % 2]
+        la.append(float(inline.step(*b, seed=50 + it)))
+    stats_inline = inline.last_stats
+    for it in range(n_it):
+        b = halves[it % 2]
+        if not ahead._queued:
+            ahead.query(b[0], b[1], 50 + it)
+        if it + 1 < n_it:
+            nb = halves[(it + 1) % 2]
+            ahead.query(nb[0], nb[1], 50 + it + 1)
+        lb.append(float(ahead.step(*b, seed=50 + it)))
+    assert ahead.last_stats == stats_inline
+    assert la[0] == lb[0]
+    np.testing.assert_allclose(lb, la, rtol=1e-4)
+    for p, q in zip(decs[0].fused_params(), decs[1].fused_params()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(embs[0], embs[1], rtol=1e-4, atol=1e-6)
+    # a step whose batch is not the queued one is refused
+    ahead.query(halves[0][0], halves[0][1], 7)
+    with pytest.raises(RuntimeError):
+        ahead.step(*halves[1], seed=7)
+    with pytest.raises(L.PsvoError):   # same rays, other seed: the C side refuses it
+        ahead.step(*halves[0], seed=8)
+    for e in engines:
+        e.close()
