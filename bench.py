@@ -105,8 +105,14 @@ def calibrate_step(ms, batches, target, voxel_size):
     from psvo.render_helpers import query_samples
 
     def mean_samples(step):
-        s = query_samples(batches[0][0], batches[0][1], ms, step, voxel_size, 10.0, seed=1)
-        return s.m / s.r_hit
+        # pooled over every batch the timed loop cycles through, so the timed
+        # workload (not just batch 0) averages `target` samples per hit ray
+        m = r = 0
+        for i, b in enumerate(batches):
+            s = query_samples(b[0], b[1], ms, step, voxel_size, 10.0, seed=1 + i)
+            m += s.m
+            r += s.r_hit
+        return m / r
     lo, hi = 0.001, 0.05
     for _ in range(18):
         mid = math.sqrt(lo * hi)

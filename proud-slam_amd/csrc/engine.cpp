@@ -9,6 +9,7 @@
 // idle behind every read-back.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <cmath>
@@ -71,6 +72,10 @@ struct psvo_engine {
     int q_head = 0, q_count = 0;
     hipStream_t side = nullptr;     // psvo_map_query's stream
     hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
+    // the embedding backward runs on `aux` beside the decoder's weight
+    // gradients (k_interp_bwd's 8-KB workgroups fit next to k_mlp_dw2's 152 KB)
+    hipStream_t aux = nullptr;
+    hipEvent_t dfeat_ready = nullptr, emb_done = nullptr;
     EngineTimer tm;
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
@@ -200,6 +205,9 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
     for (auto &q : e->qs) query_set_free(q);
     if (e->side) (void)hipStreamDestroy(e->side);
+    if (e->aux) (void)hipStreamDestroy(e->aux);
+    if (e->dfeat_ready) (void)hipEventDestroy(e->dfeat_ready);
+    if (e->emb_done) (void)hipEventDestroy(e->emb_done);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
@@ -506,21 +514,36 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
         }
     }
     float *const *W = d->dec;
-    mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(psvo_mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                          q.images, q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4],
-                          G[5], G[6], G[7], G[8], G[9], 0, n_split, mlp_ws));
-    mark(e, st, PSVO_TIME_MLP_BWD, 1);
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
+    // PSVO_SERIAL_BWD=1 (A/B aid): the embedding backward after the weight gradients on one stream
+    static const bool serial = getenv("PSVO_SERIAL_BWD") && *getenv("PSVO_SERIAL_BWD") == '1';
+    const bool overlap = !serial && !e->tm.on;  // timed runs keep the regions apart
+    if (overlap && !e->aux) {
+        if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->dfeat_ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->emb_done, hipEventDisableTiming) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: aux stream creation failed");
+    }
+    mark(e, st, PSVO_TIME_MLP_BWD, 0);
+    ENG_CALL(mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
+                     q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
+                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr));
+    mark(e, st, PSVO_TIME_MLP_BWD, 1);
+    // embedding backward: after dfeat (k_mlp_bwd2), beside k_mlp_dw2 / reduce
+    hipStream_t eb = overlap ? e->aux : st;
+    if (overlap && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     if (!(e->grads_clean && e->clean_buf == grad_emb) &&
-        hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
+        hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), eb) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     e->grads_clean = false;
     e->clean_buf = grad_emb;
-    mark(e, st, PSVO_TIME_INTERP_BWD, 0);
-    ENG_CALL(psvo_interp_bwd(stream, q.r_hit, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt, rays_o, rays_d,
+    mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
+    ENG_CALL(psvo_interp_bwd(eb, q.r_hit, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt, rays_o, rays_d,
                              d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
-    mark(e, st, PSVO_TIME_INTERP_BWD, 1);
+    mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
+    if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
+        return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
     ENG_CALL(release_query(e, st, qset));
     // ---- optimiser steps (skipped when the caller all-reduces the gradients first)

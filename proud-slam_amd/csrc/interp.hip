@@ -86,8 +86,7 @@ struct BwdPass {  // per-wave LDS: one 16-sample pass, slot-minor so a lane read
     float w[8][16];    // trilinear weights [corner][slot]
     float g[16][16];   // grad_feat [dim][slot]
     int vid[16][8];    // vertex rows of the slot's leaf
-    int leaf[16];
-};
+};  // 8 KB per 4-wave workgroup: fits beside k_mlp_dw2 (152 KB) on one CU
 
 // One wave per ray; 16 samples per pass, 4 lanes per sample (dims 4q..4q+3)
 // for the gathers and dL/dx.  The embedding gradient is summed per leaf RUN
@@ -115,7 +114,9 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
-    const int beg = offsets[r], end = offsets[r + 1];
+    // wave-uniform (one wave per ray): scalar registers for the run loop
+    const int beg = __builtin_amdgcn_readfirstlane(offsets[r]);
+    const int end = __builtin_amdgcn_readfirstlane(offsets[r + 1]);
     const int64_t ro_row = ray_index ? ray_index[r] : r;  // row of rays_o / rays_d / grad_o / grad_d
     const int q = lane & 3;
     const int sub = lane >> 2;
@@ -167,7 +168,6 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
             B.w[2 * q + 1][sub] = w[2 * q + 1];
             B.vid[sub][2 * q] = vid[2 * q];
             B.vid[sub][2 * q + 1] = vid[2 * q + 1];
-            if (q == 0) B.leaf[sub] = lf;
         }
         // dL/dx for this lane's sample: eg_k = E[vid_k] · g
         float eg[8];
@@ -204,22 +204,23 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         }
         wave_lds_sync();
         if (EMB) {
-            // run sums over the pass's valid slots: the pass's weights, gradients
-            // and leaves come into registers with 16 vector LDS reads, then the
-            // slot loop is register-only (the leaf compare is wave-uniform)
+            // run sums over the pass's valid slots: the pass's weights and
+            // gradients come into registers with 12 vector LDS reads, the
+            // leaves as wave-uniform (scalar) loads, then the slot loop is
+            // register-only (the leaf compare is wave-uniform)
             const int n_slots = min(16, end - base);
             float wa[16], wb[16], gv[16];
             int lfs[16];
+#pragma unroll
+            for (int sl = 0; sl < 16; ++sl) lfs[sl] = leaf[base + (sl < n_slots ? sl : 0)];
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
                 const float4 a = *reinterpret_cast<const float4 *>(&B.w[ek0][4 * c4]);
                 const float4 b = *reinterpret_cast<const float4 *>(&B.w[ek0 + 4][4 * c4]);
                 const float4 gg = *reinterpret_cast<const float4 *>(&B.g[ed][4 * c4]);
-                const int4 l4 = *reinterpret_cast<const int4 *>(&B.leaf[4 * c4]);
                 wa[4 * c4] = a.x; wa[4 * c4 + 1] = a.y; wa[4 * c4 + 2] = a.z; wa[4 * c4 + 3] = a.w;
                 wb[4 * c4] = b.x; wb[4 * c4 + 1] = b.y; wb[4 * c4 + 2] = b.z; wb[4 * c4 + 3] = b.w;
                 gv[4 * c4] = gg.x; gv[4 * c4 + 1] = gg.y; gv[4 * c4 + 2] = gg.z; gv[4 * c4 + 3] = gg.w;
-                lfs[4 * c4] = l4.x; lfs[4 * c4 + 1] = l4.y; lfs[4 * c4 + 2] = l4.z; lfs[4 * c4 + 3] = l4.w;
             }
 #pragma unroll
             for (int sl = 0; sl < 16; ++sl) {

@@ -25,6 +25,10 @@
 
 #include "psvo_common.h"
 
+#ifdef PSVO_STAMPS
+__device__ unsigned long long psvo_g_stamps[2][256][8][8][16];  // diagnostic build only
+#endif
+
 namespace psvo {
 namespace {
 
@@ -124,21 +128,32 @@ __device__ __forceinline__ void gemm_acc(const float *wl, const f32x16 (&in)[NIN
     }
 }
 
-// acc[ob] += image(perm_x) · x  (x[t] = x feature 2t + h)
-__device__ __forceinline__ void gemm_x(const float *wl, const float (&x)[8], f32x16 (&acc)[kNB], int lane) {
+// acc[ob] += image(perm_x) · x  (x[t] = x feature 2t + h).  `st` (a store
+// queue of 16 slots, e.g. CfQueue: one 16-KB CF tile) drains 2 slots per k
+// sub-step, between that sub-step's 4 MFMAs.
+template <typename St = NoStore>
+__device__ __forceinline__ void gemm_x(const float *wl, const float (&x)[8], f32x16 (&acc)[kNB], int lane,
+                                       const St &st = St()) {
 #pragma unroll
     for (int tg = 0; tg < 2; ++tg) {
         float4 a[kNB];
 #pragma unroll
         for (int ob = 0; ob < kNB; ++ob) a[ob] = *reinterpret_cast<const float4 *>(wl + (((ob * 2 + tg) * 64 + lane) << 2));
 #pragma unroll
-        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].x, x[4 * tg + 0], acc[ob]);
+        for (int c = 0; c < 4; ++c) {
+            if (St::kN > 0) {
+                const int q = 2 * (4 * tg + c);
+                st(q >> 2, q & 3);
+                st((q + 1) >> 2, (q + 1) & 3);
+            }
 #pragma unroll
-        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].y, x[4 * tg + 1], acc[ob]);
-#pragma unroll
-        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].z, x[4 * tg + 2], acc[ob]);
-#pragma unroll
-        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].w, x[4 * tg + 3], acc[ob]);
+            for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob][c], x[4 * tg + c], acc[ob]);
+            if (St::kN > 0) {
+                __builtin_amdgcn_sched_group_barrier(0x040, 2 * St::kN, 0);  // the queued stores
+                __builtin_amdgcn_sched_group_barrier(0x008, kNB, 0);         // then this sub-step's MFMAs
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
     }
 }
 
@@ -997,6 +1012,28 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
     *out = accumulate ? *out + v : v;
 }
 
+// Diagnostic build only (-DPSVO_STAMPS, `make stamps`: lib/diag/): per-wave
+// s_memtime stamps at the layer boundaries of k_mlp_fwd2 / k_mlp_bwd2, read
+// through psvo_debug_stamps.  In the product library every PSVO_STAMP is empty.
+#ifdef PSVO_STAMPS
+constexpr int kStampIters = 8, kStampWgs = 256;  // psvo_g_stamps[2][256][8][8][16]
+#define PSVO_STAMP_DECL int stit_ = 0
+#define PSVO_STAMP(i)                                                                               \
+    do {                                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        unsigned long long t_;                                                                      \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        if ((threadIdx.x & 63) == 0 && stit_ < kStampIters && blockIdx.x < kStampWgs)               \
+            psvo_g_stamps[kStampK][blockIdx.x][threadIdx.x >> 6][stit_][i] = t_;                         \
+    } while (0)
+#define PSVO_STAMP_FLUSH(k) ++stit_
+#else
+#define PSVO_STAMP_DECL
+#define PSVO_STAMP(i)
+#define PSVO_STAMP_FLUSH(k)
+#endif
+
 // ---------------------------------------------------------------------------
 // forward, persistent + double-buffered: one 512-thread workgroup per CU
 // loops over 256-sample tiles (8 waves × 32 samples, the chain of k_mlp_fwd
@@ -1021,85 +1058,134 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
                                                             float *__restrict__ act, uint64_t *__restrict__ masks) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const bool save = act != nullptr;         // CF activations (weight gradients)
     const bool save_mask = masks != nullptr;  // ReLU masks (δ chain)
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF 32-sample tiles
     const int64_t tstride = n_tiles * 32 * 128;
     const int64_t tbytes = tstride * 4;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    // Balanced split: workgroup b owns the 32-sample units [u0, u1) — every
+    // wave slot of the chip gets floor or ceil of n_units / (8 · grid), so the
+    // last iteration is a partial one (waves past u1 skip their MFMAs but keep
+    // staging and barriers) instead of a whole extra 256-sample round.
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int n_it = (int)((u1 - u0 + kF2Waves - 1) / kF2Waves);
     auto buf = [&](int i) { return lds + ((i & 1) ? kF2Buf1 : kF2Buf0); };
     int seq = 0;  // staged layers so far: W(seq) sits in buf(seq)
-    int64_t t = blockIdx.x;
+    [[maybe_unused]] constexpr int kStampK = 0;
     float xn[8];
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_x(feat, s, s < m, h, xn);
+        const int64_t u = u0 + wave;
+        const int64_t s = u * kTileS + (lane & 31);
+        load_x(feat, s, u < u1 && s < m, h, xn);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
     stage8(buf(0), img + kImgF2, 16384, wave, lane);
     wait_vm(0);
     raw_barrier();
-    for (; t < n_wg_tiles; t += gridDim.x) {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        const bool valid = s < m;
-        const bool more = t + gridDim.x < n_wg_tiles;
+    // c1 (the W4 layer's activation) of iteration i is stored from inside
+    // iteration i+1's W1 layer (bacc is untouched until the W2 layer): the
+    // 64 stores drain behind MFMAs instead of stalling the epilogue
+    f32x16 bacc[kNB];
+    CfStore c1_cfs(0, lane, 0);
+    bool c1_pending = false;
+    PSVO_STAMP_DECL;
+    for (int it = 0; it < n_it; ++it) {
+        PSVO_STAMP(0);
+        const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
+        const bool active = u < u1;  // wave-uniform
+        const int64_t s = u * kTileS + (lane & 31);
+        const bool valid = active && s < m;
+        const bool more = it + 1 < n_it;
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = xn[i];
-        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
-        f32x16 a[kNB], bacc[kNB];
-        // h1 = relu(W1 x + b1): resident W1
-        init_bias(a, lds + kOffB1, h);
-        gemm_x(lds + kF2W1, x, a, lane);
-        const uint64_t m1 = relu(a);
+        const CfStore cfs(u, lane, n_tiles);
+        f32x16 a[kNB];
+        uint64_t m1 = 0, m2 = 0;
+        float sdf = 0.f;
+        // h1 = relu(W1 x + b1): resident W1 (+ the previous iteration's c1 stores)
+        if (active) {
+            init_bias(a, lds + kOffB1, h);
+            gemm_x(lds + kF2W1, x, a, lane, CfQueue(c1_cfs, act + 3 * tstride, tbytes, save && c1_pending, bacc));
+            m1 = relu(a);
+        } else if (save && c1_pending) {
+            c1_cfs.store(act + 3 * tstride, tbytes, bacc);
+        }
+        c1_pending = false;
+        PSVO_STAMP(1);
         // h2 = relu(W2 h1 + b2)
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(2);
         stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
-        init_bias(bacc, lds + kOffB2, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
+        if (active) {
+            init_bias(bacc, lds + kOffB2, h);
+            gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
+            m2 = relu(bacc);
+        }
         ++seq;
-        const uint64_t m2 = relu(bacc);
+        PSVO_STAMP(3);
         // [sdf | f] = W3 h2 + b3
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(4);
         stage8(buf(seq + 1), img + kImgF4, 18432, wave, lane);
-        const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
-        init_bias(a, lds + kOffB3 + 1, h);
-        gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane, CfQueue(cfs, act + tstride, tbytes, save, bacc));  // + h2
+        if (active) {
+            sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
+            init_bias(a, lds + kOffB3 + 1, h);
+            gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane, CfQueue(cfs, act + tstride, tbytes, save, bacc));  // + h2
+        }
         ++seq;
-        // c1 = relu(W4 [f; x] + b4); the next tile's W2 and x start loading
+        PSVO_STAMP(5);
+        // c1 = relu(W4 [f; x] + b4); the next iteration's W2 and x start loading
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(6);
         if (more) {
             stage8(buf(seq + 1), img + kImgF2, 16384, wave, lane);
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
-            load_x(feat, sn, sn < m, h, xn);
+            const int64_t un = u + kF2Waves;
+            const int64_t sn = un * kTileS + (lane & 31);
+            load_x(feat, sn, un < u1 && sn < m, h, xn);
         }
-        init_bias(bacc, lds + kOffB4, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act + 2 * tstride, tbytes, save, a));  // + f
-        gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
+        if (active) {
+            init_bias(bacc, lds + kOffB4, h);
+            gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act + 2 * tstride, tbytes, save, a));  // + f
+            gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
+        }
         ++seq;
-        const uint64_t m4 = relu(bacc);
-        if (save) cfs.store(act + 3 * tstride, tbytes, bacc);
-        if (save_mask && valid) {
-            uint64_t *mk = masks + (s * 2 + h) * 3;
-            mk[0] = m1;
-            mk[1] = m2;
-            mk[2] = m4;
-        }
-        float rgb[3];
+        PSVO_STAMP(7);
+        if (active) {
+            const uint64_t m4 = relu(bacc);
+            if (save) {
+                if (more) {
+                    c1_cfs = cfs;
+                    c1_pending = true;
+                } else {
+                    cfs.store(act + 3 * tstride, tbytes, bacc);
+                }
+            }
+            if (save_mask && valid) {
+                uint64_t *mk = masks + (s * 2 + h) * 3;
+                mk[0] = m1;
+                mk[1] = m2;
+                mk[2] = m4;
+            }
+            float rgb[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
-        if (valid && h == 0) {
-            sdf_out[s] = sdf;
-            rgb_out[s * 3 + 0] = rgb[0];
-            rgb_out[s * 3 + 1] = rgb[1];
-            rgb_out[s * 3 + 2] = rgb[2];
+            for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
+            if (valid && h == 0) {
+                sdf_out[s] = sdf;
+                rgb_out[s * 3 + 0] = rgb[0];
+                rgb_out[s * 3 + 1] = rgb[1];
+                rgb_out[s * 3 + 2] = rgb[2];
+            }
         }
+        PSVO_STAMP(8);
+        PSVO_STAMP_FLUSH(0);
     }
     wait_vm(0);
 }
@@ -1190,26 +1276,33 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *bufA = lds + kB2BufA, *bufB = lds + kB2BufB;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
     const int64_t tbytes = n_tiles * 32 * 128 * 4;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
-    int64_t t = blockIdx.x;
+    // balanced split of the 32-sample units, as k_mlp_fwd2
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int n_it = (int)((u1 - u0 + kF2Waves - 1) / kF2Waves);
+    [[maybe_unused]] constexpr int kStampK = 1;
     BwdIn nin;
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, s < m, h, nin);
+        const int64_t u = u0 + wave;
+        const int64_t s = u * kTileS + (lane & 31);
+        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, u < u1 && s < m, h, nin);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(bufA, img + kImgB4, 20480, wave, lane);
     wait_vm(0);
     raw_barrier();
-    for (; t < n_wg_tiles; t += gridDim.x) {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        const bool valid = s < m;
-        const bool more = t + gridDim.x < n_wg_tiles;
-        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
+    PSVO_STAMP_DECL;
+    for (int it = 0; it < n_it; ++it) {
+        const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
+        const bool active = u < u1;  // wave-uniform
+        const int64_t s = u * kTileS + (lane & 31);
+        const bool valid = active && s < m;
+        const bool more = it + 1 < n_it;
+        const CfStore cfs(u, lane, n_tiles);
         const BwdIn in = nin;
         float d5[3];
 #pragma unroll
@@ -1222,63 +1315,82 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
             o.d5[s * 3 + 2] = d5[2];
         }
         // ---- W4ᵀ layer (bufA); W3ᵀ → bufB
+        PSVO_STAMP(1);
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(2);
         stage8(bufB, img + kImgB3, 16384, wave, lane);
         f32x16 a[kNB], bacc[kNB];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
-                const int k = 32 * b + phi(r, h);
-                const float v =
-                    lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
-                bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
-            }
-        f32x16 t5[5];
-        zero(t5);
-        gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1 stores
         float dxc[8];
+        if (active) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
+            for (int b = 0; b < kNB; ++b)
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
+                for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
+                    const int k = 32 * b + phi(r, h);
+                    const float v =
+                        lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
+                    bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
+                }
+            f32x16 t5[5];
+            zero(t5);
+            gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1
+#pragma unroll
+            for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
+        }
         // ---- W3ᵀ layer (bufB); W2ᵀ → bufA
+        PSVO_STAMP(3);
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(4);
         stage8(bufA, img + kImgB2, 16384, wave, lane);
+        if (active) {
 #pragma unroll
-        for (int b = 0; b < kNB; ++b)
+            for (int b = 0; b < kNB; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
-        gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
-        apply_mask(bacc, m2);
+                for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
+            gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
+            apply_mask(bacc, m2);
+        }
         // ---- W2ᵀ layer (bufA); W1ᵀ → bufB
+        PSVO_STAMP(5);
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(6);
         stage8(bufB, img + kImgB1, 4096, wave, lane);
-        zero(a);
-        gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2 stores
-        apply_mask(a, m1);
-        // ---- W1ᵀ layer (bufB); next tile's W4ᵀ → bufA and its inputs
+        if (active) {
+            zero(a);
+            gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2
+            apply_mask(a, m1);
+        }
+        // ---- W1ᵀ layer (bufB); next iteration's W4ᵀ → bufA and its inputs
+        PSVO_STAMP(7);
         wait_vm(0);
         raw_barrier();
+        PSVO_STAMP(8);
         if (more) {
             stage8(bufA, img + kImgB4, 20480, wave, lane);
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
-            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, sn < m, h, nin);
+            const int64_t un = u + kF2Waves;
+            const int64_t sn = un * kTileS + (lane & 31);
+            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, un < u1 && sn < m, h, nin);
         }
-        f32x16 t1[1];
-        zero(t1);
-        gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
-        if (valid) {
-            float *dst = o.dfeat + s * kIn;
+        if (active) {
+            f32x16 t1[1];
+            zero(t1);
+            gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
+            if (valid) {
+                float *dst = o.dfeat + s * kIn;
 #pragma unroll
-            for (int rg = 0; rg < 2; ++rg)
-                *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
-                    make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
-                                t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
+                for (int rg = 0; rg < 2; ++rg)
+                    *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
+                        make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
+                                    t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
+            }
         }
+        PSVO_STAMP(9);
+        PSVO_STAMP_FLUSH(1);
     }
     wait_vm(0);
 }
@@ -1305,6 +1417,14 @@ static bool use_fwd2() {
 
 }  // namespace
 }  // namespace psvo
+
+#ifdef PSVO_STAMPS
+// copies the stamp array ([2 kernels][256 wg][8 waves][8 tiles][16 points] u64)
+extern "C" int psvo_debug_stamps(void *dst, int64_t bytes) {
+    if (bytes < (int64_t)sizeof(psvo_g_stamps)) return -1;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(psvo_g_stamps), sizeof(psvo_g_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 using namespace psvo;
 
@@ -1350,7 +1470,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
             attr2 = true;
         }
-        const int64_t tiles = div_up(m, kF2Tile);
+        const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
         hipLaunchKernelGGL(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
                            masks);
@@ -1403,12 +1523,13 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
 // to when `accumulate`) and dfeat [M,16], from the training forward's rgb,
 // activations and masks.  `workspace`: δ operands + split-K slabs
 // (psvo_mlp_workspace_floats).
-extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
-                            const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
-                            const float *b4, const float *w5, const float *b5, const float *images, const float *rgb,
-                            const float *act, const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1,
-                            float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4,
-                            float *gw5, float *gb5, int accumulate, int n_split, float *workspace) {
+namespace psvo {
+int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
+            const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
+            const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
+            const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
+            float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
+            float *workspace, hipEvent_t dfeat_ready) {
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
     PSVO_REQUIRE(images != nullptr, "mlp_bwd: images of the training forward required");
@@ -1455,6 +1576,8 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
         int rc = check_launch("mlp_bwd_data");
         if (rc) return rc;
     }
+    if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
     if (!want_w) return PSVO_OK;
     DwSrc src;
     src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4;
@@ -1494,4 +1617,16 @@ extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *fea
     d.elem_begin[5] = e;
     hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, st, g, slabs, d, accumulate);
     return check_launch("mlp_dw_reduce");
+}
+}  // namespace psvo
+
+extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                            const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                            const float *b4, const float *w5, const float *b5, const float *images, const float *rgb,
+                            const float *act, const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1,
+                            float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, float *gw4, float *gb4,
+                            float *gw5, float *gb5, int accumulate, int n_split, float *workspace) {
+    return psvo::mlp_bwd(stream, m, width, feat, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images, rgb, act, masks,
+                         g_sdf, g_rgb, dfeat, gw1, gb1, gw2, gb2, gw3, gb3, gw4, gb4, gw5, gb5, accumulate, n_split,
+                         workspace, nullptr);
 }

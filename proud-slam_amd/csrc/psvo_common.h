@@ -35,6 +35,15 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray);
 
+// psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
+// dfeat is written, before the weight-gradient kernels are queued
+int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
+            const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
+            const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
+            const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
+            float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
+            float *workspace, hipEvent_t dfeat_ready);
+
 }  // namespace psvo
 
 #define PSVO_REQUIRE(cond, ...)                                       \

@@ -1,0 +1,69 @@
+"""Diagnostic: where k_mlp_fwd2 / k_mlp_bwd2 spend a tile (s_memtime stamps of
+the lib/diag/libpsvo_stamps.so build, `make -C proud-slam_amd/csrc stamps`).
+Read the SHARES of the segments, not the absolute time (the stamps fence the
+code).  Prints per-segment mean cycles over (workgroup, wave, tile)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "proud-slam_amd"))
+from psvo import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_stamps.so")
+from psvo.decoder import Decoder  # noqa: E402
+
+FWD = ["L1", "bar1", "L2", "bar2", "L3(+sdf)", "bar3(+stage,x)", "L4", "epilogue"]
+BWD = ["bar1", "W4T", "bar2", "W3T", "bar3", "W2T", "bar4", "W1T+dfeat"]
+
+
+def main():
+    m = int(sys.argv[1]) if len(sys.argv) > 1 else 262963
+    torch.manual_seed(0)
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").cuda()
+    x = (torch.randn(m, 16, device="cuda") * 0.3).requires_grad_(True)
+    for _ in range(4):
+        out = dec({"emb": x})
+        (out["sdf"].sum() + out["color"].sum()).backward()
+    torch.cuda.synchronize()
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    shape = (2, 256, 8, 8, 16)
+    buf = np.zeros(shape, dtype=np.uint64)
+    rc = L.psvo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(buf.nbytes))
+    assert rc == 0, rc
+    n_wg_tiles = (m + 255) // 256
+    for k, names in ((0, FWD), (1, BWD)):
+        st = buf[k].astype(np.int64)
+        npts = len(names) + 1
+        p0 = 0 if k == 0 else 1  # bwd2 has no point 0 (diagnostic-build compiler issue)
+        st = st[..., p0:]
+        rows, spans = [], []
+        for wg in range(256):
+            n_it = len(range(wg, n_wg_tiles, 256))
+            for w in range(8):
+                for it in range(min(n_it, 8)):
+                    v = st[wg, w, it, :npts]
+                    if v[0] == 0 or v[-1] == 0:
+                        continue
+                    rows.append(np.diff(v))
+                    spans.append(v[-1] - v[0])
+            # per-WG: first tile start .. last tile end
+        d = np.array(rows, dtype=np.float64)
+        tot = d.sum(1).mean()
+        print(f"{'fwd2' if k == 0 else 'bwd2'}: {len(rows)} wave-tiles, mean tile {tot:.0f} cycles")
+        for i, nm in enumerate(names):
+            print(f"   {nm:16s} {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot:5.1f}%)  p90 {np.percentile(d[:, i], 90):9.0f}")
+        # workgroup-level: iterations per WG and the tail
+        first = st[:, :, 0, 0]
+        its = np.array([len(range(wg, n_wg_tiles, 256)) for wg in range(256)])
+        last_end = np.array([st[wg, :, min(its[wg], 8) - 1, npts - 1].max() for wg in range(256)])
+        t0 = first[first > 0].min()
+        print(f"   kernel span (stamps) {(last_end.max() - t0):.0f} cycles; WG end spread "
+              f"{np.percentile(last_end - t0, [0, 50, 90, 100]).round()}; tiles/WG {np.bincount(its)}")
+
+
+if __name__ == "__main__":
+    main()
