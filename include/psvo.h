@@ -171,6 +171,20 @@ int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float truncation,
                        const float *rgb_s, const float *grad_color, const float *grad_depth,
                        const float *grad_weights, const float *grad_sdf, float *grad_sdf_s, float *grad_rgb_s);
 
+/* Mapping-step fusion of psvo_composite_fwd, psvo_criterion_sums' per-ray
+ * partials, psvo_criterion_bwd (d loss = 1) and psvo_composite_bwd
+ * (grad_weights = 0) in one pass per hit ray — same arithmetic.  coef f32[4]
+ * = the backward coefficients from psvo_criterion_coef; workspace as
+ * psvo_criterion_sums' (the count slots already filled by
+ * psvo_criterion_coef; this fills the others, so psvo_criterion_reduce +
+ * psvo_criterion_finalize then give the loss).  Writes color [R_hit,3],
+ * depth [R_hit], grad_sdf_s [M], grad_rgb_s [M,3]. */
+int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                        const int *offsets, const int *ray_ns, const float *z_vals, const int *rank_ray,
+                        const float *gt_rgb, const float *gt_depth, const float *sdf_s, const float *rgb_s,
+                        const float *coef, float *workspace, float *color, float *depth, float *grad_sdf_s,
+                        float *grad_rgb_s);
+
 /* ---- NRGBD decoder (nrgbd.py:80-146; width 128, in 16, depth 2) ------- */
 /* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
  * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
@@ -231,6 +245,17 @@ int psvo_criterion_sums(void *stream, int64_t r_hit, int s_max, int pad_extra, f
  * s_max columns; flags = PSVO_CRIT_USE_* terms; out f32[PSVO_CRIT_OUT_WORDS]. */
 int psvo_criterion_finalize(void *stream, const double *sums, int64_t n_hit, int s_max, float rgb_w, float depth_w,
                             float fs_w, float sdf_w, float truncation, int flags, float *out);
+
+/* The Criterion's normalisers depend only on z_vals and the GT depth
+ * (criterion.py:78-101): counts n_valid / n_front / n_sdf into workspace's
+ * count slots, their sums into sums f64[8], and the backward coefficients
+ * coef f32[4] = {c_colour, c_depth, c_fs, c_sdf} exactly as
+ * psvo_criterion_finalize derives them — before the decoder has run. */
+int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                        const int *rank_ray, const float *gt_depth, const float *z_vals, float rgb_w, float depth_w,
+                        float fs_w, float sdf_w, int flags, float *workspace, double *sums, float *coef);
+/* Fixed-order reduction of the workspace's per-ray partials into sums f64[8]. */
+int psvo_criterion_reduce(void *stream, int64_t r_hit, const float *workspace, double *sums);
 
 /* Backward given g_loss (device scalar): g_color [R_hit,3], g_depth [R_hit],
  * g_sdf [R_hit,S_max]. */

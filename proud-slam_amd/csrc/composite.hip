@@ -31,6 +31,23 @@ __device__ __forceinline__ int wmin(int v) {
 }
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Backward per-sample pieces shared by k_composite_bwd and k_composite_loss,
+// with the roundings spelled out (fmaf), so both kernels produce the same
+// bits whatever the compiler would contract in either context.
+// dL/dW_s = g_depth·z_s + g_w,s (+ g_colour·c_s for a valid sample)
+__device__ __forceinline__ float comp_gw(float gdp, float z, float gwx, const float *c, float gr, float gg, float gb) {
+    const float g = fmaf(gdp, z, gwx);
+    return c ? fmaf(gb, c[2], fmaf(gg, c[1], fmaf(gr, c[0], g))) : g;
+}
+// dL/dsdf_s through the weights (kept samples) plus the direct term g
+__device__ __forceinline__ float comp_gsdf(float gw, float dot, float tot, bool keep, float sdf, float tr, float g) {
+    const float a = sdf / tr;
+    const float sp = sigm(a), sn = sigm(-a);
+    const float gu = keep ? (gw - dot) / tot : 0.f;
+    const float du = sp * sn * (sn - sp) / tr;
+    return fmaf(gu, du, g);
+}
+
 __global__ __launch_bounds__(256) void k_composite_fwd(int64_t r_hit, int s_max, float tr,
                                                        const int *__restrict__ offsets,
                                                        const int *__restrict__ ray_ns,
@@ -122,12 +139,9 @@ __global__ __launch_bounds__(256) void k_composite_bwd(int64_t r_hit, int s_max,
     // dL/dW_s and Σ_s dL/dW_s · W_s
     float dot = 0.f, tot = 0.f;
     for (int s = lane; s < s_max; s += 64) {
-        float gw = gdp * z[s] + (g_weights ? g_weights[r * s_max + s] : 0.f);
-        if (s < ns) {
-            const float *c = rgb_s + (int64_t)(off + s) * 3;
-            gw += gr * c[0] + gg * c[1] + gb * c[2];
-        }
-        dot += gw * wt[s];
+        const float gw = comp_gw(gdp, z[s], g_weights ? g_weights[r * s_max + s] : 0.f,
+                                 s < ns ? rgb_s + (int64_t)(off + s) * 3 : nullptr, gr, gg, gb);
+        dot = fmaf(gw, wt[s], dot);
     }
     dot = wsum(dot);
     // T = Σ_kept u + 1e-8, the forward's normaliser (W_s = w_s / T); the
@@ -147,18 +161,157 @@ __global__ __launch_bounds__(256) void k_composite_bwd(int64_t r_hit, int s_max,
     for (int s = lane; s < ns; s += 64) {
         const float *c = rgb_s + (int64_t)(off + s) * 3;
         const float W = wt[s];
-        float gw = gdp * z[s] + (g_weights ? g_weights[r * s_max + s] : 0.f) + gr * c[0] + gg * c[1] + gb * c[2];
-        const float a = sd[s] / tr;
-        const float sp = sigm(a), sn = sigm(-a);
-        const bool keep = z[s] < zmin + tr;
-        const float gu = keep ? (gw - dot) / tot : 0.f;
-        const float du = sp * sn * (sn - sp) / tr;
-        float gs = gu * du + (g_sdf ? g_sdf[r * s_max + s] : 0.f);
-        g_sdf_s[off + s] = gs;
+        const float gw = comp_gw(gdp, z[s], g_weights ? g_weights[r * s_max + s] : 0.f, c, gr, gg, gb);
+        g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, z[s] < zmin + tr, sd[s], tr, g_sdf ? g_sdf[r * s_max + s] : 0.f);
         float *gc = g_rgb_s + (int64_t)(off + s) * 3;
         gc[0] = W * gr;
         gc[1] = W * gg;
         gc[2] = W * gb;
+    }
+}
+
+// Mapping step: compositing (k_composite_fwd), the Criterion's per-ray
+// partial sums (k_crit_rays' colour / depth / fs / sdf slots; the count
+// slots come from k_crit_counts), its backward with the precomputed
+// coefficients (k_crit_bwd at d loss = 1) and the compositing backward
+// (k_composite_bwd) in one wave per ray — the same arithmetic, four launches
+// and the padded [R_hit, S_max] sdf / weight rows fewer.
+//   coef = {c_colour, c_depth, c_fs, c_sdf} (k_crit_coef)
+constexpr int kPartColor = 0, kPartDepth = 1, kPartQFs = 5, kPartQSdf = 6, kPartN = 8;
+
+// criterion.hip's sample_terms, with its no-contraction arithmetic
+struct CritTerms {
+    float f, sm, xfs, ysdf;
+};
+__device__ __forceinline__ CritTerms crit_terms(float z, float p, float d, float tr, float max_depth) {
+#pragma clang fp contract(off)
+    CritTerms o;
+    o.f = z < (d - tr) ? 1.0f : 0.0f;
+    const float b = z > (d + tr) ? 1.0f : 0.0f;
+    const float dm = (d > 0.0f && d < max_depth) ? 1.0f : 0.0f;
+    o.sm = (1.0f - o.f) * (1.0f - b) * dm;
+    o.xfs = p * o.f - o.f;
+    o.ysdf = (z + p * tr) * o.sm - d * o.sm;
+    return o;
+}
+__device__ __forceinline__ float crit_sq_add(float acc, float x) {
+#pragma clang fp contract(off)
+    return acc + x * x;
+}
+__device__ __forceinline__ float crit_grad(float cfs, float csdf, const CritTerms &t) {
+#pragma clang fp contract(off)
+    return cfs * t.xfs * t.f + csdf * t.ysdf * t.sm;
+}
+
+__global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max, float tr, float max_depth,
+                                                        const int *__restrict__ offsets,
+                                                        const int *__restrict__ ray_ns,
+                                                        const float *__restrict__ z_vals,
+                                                        const int *__restrict__ rank_ray,
+                                                        const float *__restrict__ gt_rgb,
+                                                        const float *__restrict__ gt_depth,
+                                                        const float *__restrict__ sdf_s,
+                                                        const float *__restrict__ rgb_s,
+                                                        const float *__restrict__ coef, float *__restrict__ part,
+                                                        float *__restrict__ color, float *__restrict__ depth,
+                                                        float *__restrict__ g_sdf_s, float *__restrict__ g_rgb_s) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int off = offsets[r], ns = ray_ns[r];
+    const float *z = z_vals + r * s_max;
+    auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
+    // ---- forward (k_composite_fwd)
+    int first = s_max;
+    for (int s = lane; s < s_max; s += 64) {
+        const float v = sdf_at(s);
+        if (s + 1 < s_max && sdf_at(s + 1) * v < 0.0f) first = min(first, s);
+    }
+    first = wmin(first);
+    const float zmin = z[first == s_max ? 0 : first];
+    float tot = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float a = sdf_at(s) / tr;
+        float w = sigm(a) * sigm(-a);
+        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        tot += keep ? w : 0.0f;
+    }
+    tot = wsum(tot) + 1e-8f;
+    auto weight_at = [&](int s) {  // normalised weight W_s (0 outside the kept set)
+        const float a = sdf_at(s) / tr;
+        const float w = sigm(a) * sigm(-a);
+        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        return (keep ? w : 0.0f) / tot;
+    };
+    float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float w = weight_at(s);
+        if (s < ns) {
+            const float *c = rgb_s + (int64_t)(off + s) * 3;
+            cr += w * c[0];
+            cg += w * c[1];
+            cb += w * c[2];
+        }
+        dd += w * z[s];
+    }
+    cr = wsum(cr);
+    cg = wsum(cg);
+    cb = wsum(cb);
+    dd = wsum(dd);
+    // ---- loss partials (k_crit_rays) and d loss / d {colour, depth} (k_crit_bwd)
+    const int64_t orig = rank_ray[r];
+    const float d = gt_depth[orig];
+    const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
+    float qfs = 0.f, qsdf = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const CritTerms t = crit_terms(z[s], sdf_at(s), d, tr, max_depth);
+        qfs = crit_sq_add(qfs, t.xfs);
+        qsdf = crit_sq_add(qsdf, t.ysdf);
+    }
+    qfs = wsum(qfs);
+    qsdf = wsum(qsdf);
+    const float rgb[3] = {cr, cg, cb};
+    float gcol[3], ac = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float e = gt_rgb[orig * 3 + c] - rgb[c];
+        ac += fabsf(e);
+        gcol[c] = -ccol * (e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f));
+    }
+    const bool valid = d > 0.01f && d < max_depth;
+    const float ed = d - dd;
+    const float gdp = valid ? -cdep * (ed > 0.0f ? 1.0f : (ed < 0.0f ? -1.0f : 0.0f)) : 0.0f;
+    if (lane == 0) {
+        color[r * 3 + 0] = cr;
+        color[r * 3 + 1] = cg;
+        color[r * 3 + 2] = cb;
+        depth[r] = dd;
+        float *o = part + r * kPartN;
+        o[kPartColor] = ac;
+        o[kPartDepth] = valid ? fabsf(ed) : 0.0f;
+        o[kPartQFs] = qfs;
+        o[kPartQSdf] = qsdf;
+        o[7] = 0.0f;
+    }
+    // ---- compositing backward (k_composite_bwd, g_weights = 0)
+    float dot = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const float gw = comp_gw(gdp, z[s], 0.f, s < ns ? rgb_s + (int64_t)(off + s) * 3 : nullptr, gcol[0], gcol[1],
+                                 gcol[2]);
+        dot = fmaf(gw, weight_at(s), dot);
+    }
+    dot = wsum(dot);
+    for (int s = lane; s < ns; s += 64) {
+        const float *c = rgb_s + (int64_t)(off + s) * 3;
+        const float W = weight_at(s);
+        const float gw = comp_gw(gdp, z[s], 0.f, c, gcol[0], gcol[1], gcol[2]);
+        const float p = sdf_s[off + s];
+        const float gsdf = crit_grad(cfs, csdf, crit_terms(z[s], p, d, tr, max_depth));  // k_crit_bwd's term
+        g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, z[s] < zmin + tr, p, tr, gsdf);
+        float *gc = g_rgb_s + (int64_t)(off + s) * 3;
+        gc[0] = W * gcol[0];
+        gc[1] = W * gcol[1];
+        gc[2] = W * gcol[2];
     }
 }
 
@@ -188,4 +341,20 @@ extern "C" int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float 
                        truncation, offsets, ray_ns, z_vals, sdf, weights, rgb_s, grad_color, grad_depth,
                        grad_weights, grad_sdf, grad_sdf_s, grad_rgb_s);
     return check_launch("composite_bwd");
+}
+
+extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                                   const int *offsets, const int *ray_ns, const float *z_vals, const int *rank_ray,
+                                   const float *gt_rgb, const float *gt_depth, const float *sdf_s,
+                                   const float *rgb_s, const float *coef, float *workspace, float *color,
+                                   float *depth, float *grad_sdf_s, float *grad_rgb_s) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_loss: bad sizes");
+    PSVO_REQUIRE(offsets && ray_ns && z_vals && rank_ray && gt_rgb && gt_depth && sdf_s && rgb_s && coef &&
+                     workspace && color && depth && grad_sdf_s && grad_rgb_s,
+                 "composite_loss: null pointer");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_composite_loss, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+                       truncation, max_depth, offsets, ray_ns, z_vals, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
+                       workspace, color, depth, grad_sdf_s, grad_rgb_s);
+    return check_launch("composite_loss");
 }

@@ -192,6 +192,57 @@ __global__ __launch_bounds__(256) void k_crit_bwd(int64_t r_hit, int s_max, floa
     }
 }
 
+// ---- mapping step, split by what each part depends on -------------------
+// The loss's normalisers (n_valid, n_front, n_sdf) and hence every backward
+// coefficient depend only on z_vals and the GT depth, not on the decoder: the
+// engine counts them beside the decoder forward (k_crit_counts → reduce →
+// k_crit_coef), and k_composite_loss (composite.hip) then runs compositing,
+// the loss partials and the whole per-ray backward in one pass; the loss
+// value itself (reduce + finalize) is off the critical path.
+
+// one wave per hit ray: the count slots of part[r] (kNValid, kNFront, kNSdf)
+__global__ __launch_bounds__(256) void k_crit_counts(int64_t r_hit, int s_max, float tr, float max_depth,
+                                                     const int *__restrict__ rank_ray,
+                                                     const float *__restrict__ gt_depth,
+                                                     const float *__restrict__ z_vals, float *__restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const float d = gt_depth[rank_ray[r]];
+    const float *z = z_vals + r * s_max;
+    float nf = 0.f, ns = 0.f;
+    for (int s = lane; s < s_max; s += 64) {
+        const SampleTerms t = sample_terms(z[s], 1.0f, d, tr, max_depth);
+        nf += t.f;
+        ns += t.sm;
+    }
+    nf = wsum(nf);
+    ns = wsum(ns);
+    if (lane == 0) {
+        float *o = part + r * kNSums;
+        o[kNValid] = (d > 0.01f && d < max_depth) ? 1.0f : 0.0f;
+        o[kNFront] = nf;
+        o[kNSdf] = ns;
+    }
+}
+
+// the backward coefficients of k_crit_finalize from the count sums alone
+// (same arithmetic, so the two agree bit for bit)
+__global__ void k_crit_coef(const double *__restrict__ sums, double n_hit, double n_cols, float rgb_w, float depth_w,
+                            float fs_w, float sdf_w, float tr, int flags, float *__restrict__ coef) {
+    if (threadIdx.x != 0) return;
+    const double n_el = n_hit * n_cols;
+    const float n_valid = (float)sums[kNValid];
+    const float n_f = (float)sums[kNFront], n_s = (float)sums[kNSdf];
+    const float n_tot = n_s + n_f;
+    const float fs_weight = 1.0f - n_f / n_tot;
+    const float sdf_weight = 1.0f - n_s / n_tot;
+    coef[0] = (flags & kFlagColor) ? (float)(rgb_w / (3.0 * n_hit)) : 0.0f;
+    coef[1] = (flags & kFlagDepth) ? depth_w / n_valid : 0.0f;
+    coef[2] = (flags & kFlagSdf) ? (float)(2.0 * (double)(fs_w * fs_weight) / n_el) : 0.0f;
+    coef[3] = (flags & kFlagSdf) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
+}
+
 // tracking's depth filter (criterion.py:45-50): per hit ray
 //   tmp = |d − depth| / sqrt(Σ_s w_s (depth − z_s)² + 1e-10)
 __global__ __launch_bounds__(256) void k_crit_depth_tmp(int64_t r_hit, int s_max, const int *__restrict__ rank_ray,
@@ -284,6 +335,27 @@ extern "C" int psvo_criterion_sums(void *stream, int64_t r_hit, int s_max, int p
                                    float *workspace, double *sums) {
     return psvo_criterion_sums_ex(stream, r_hit, s_max, pad_extra, truncation, max_depth, rank_ray, gt_rgb, gt_depth,
                                   color, depth, sdf, z_vals, nullptr, nullptr, workspace, sums);
+}
+
+extern "C" int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                                   const int *rank_ray, const float *gt_depth, const float *z_vals, float rgb_w,
+                                   float depth_w, float fs_w, float sdf_w, int flags, float *workspace, double *sums,
+                                   float *coef) {
+    PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_coef: bad sizes");
+    PSVO_REQUIRE(rank_ray && gt_depth && z_vals && workspace && sums && coef, "criterion_coef: null pointer");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
+                       rank_ray, gt_depth, z_vals, workspace);
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
+                       fs_w, sdf_w, truncation, flags, coef);
+    return check_launch("criterion_coef");
+}
+
+extern "C" int psvo_criterion_reduce(void *stream, int64_t r_hit, const float *workspace, double *sums) {
+    PSVO_REQUIRE(r_hit > 0 && workspace && sums, "criterion_reduce: bad arguments");
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, as_stream(stream), r_hit, workspace, sums);
+    return check_launch("criterion_reduce");
 }
 
 extern "C" int psvo_criterion_finalize(void *stream, const double *sums, int64_t n_hit, int s_max, float rgb_w,

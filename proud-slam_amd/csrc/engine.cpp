@@ -28,7 +28,7 @@ enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankR
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
-    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSlots
+    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kSlots
 };
 
 struct Arena {
@@ -74,8 +74,11 @@ struct psvo_engine {
     hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
     // the embedding backward runs on `aux` beside the decoder's weight
     // gradients (k_interp_bwd's 8-KB workgroups fit next to k_mlp_dw2's 152 KB)
+    // (and the loss normalisers beside the decoder forward, the loss value
+    // beside the decoder backward)
     hipStream_t aux = nullptr;
-    hipEvent_t dfeat_ready = nullptr, emb_done = nullptr;
+    hipEvent_t dfeat_ready = nullptr, emb_done = nullptr, z_ready = nullptr, coef_ready = nullptr,
+               grads_ready = nullptr;
     EngineTimer tm;
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
@@ -208,6 +211,9 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->aux) (void)hipStreamDestroy(e->aux);
     if (e->dfeat_ready) (void)hipEventDestroy(e->dfeat_ready);
     if (e->emb_done) (void)hipEventDestroy(e->emb_done);
+    if (e->z_ready) (void)hipEventDestroy(e->z_ready);
+    if (e->coef_ready) (void)hipEventDestroy(e->coef_ready);
+    if (e->grads_ready) (void)hipEventDestroy(e->grads_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
@@ -357,10 +363,35 @@ int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
 
 // render_rays (render_helpers.py:363-556) on the device, after the query:
 // sample compaction (sized by the query's read-back), interpolation, decoder,
+// Work beside the main stream on `aux` (PSVO_SERIAL_BWD=1 or timed runs:
+// everything on the caller's stream, in dependency order).
+bool engine_overlap(psvo_engine *e) {
+    static const bool serial = getenv("PSVO_SERIAL_BWD") && *getenv("PSVO_SERIAL_BWD") == '1';
+    return !serial && !e->tm.on;
+}
+int ensure_aux(psvo_engine *e) {
+    if (e->aux) return PSVO_OK;
+    hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready};
+    if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
+    for (hipEvent_t *ev : evs)
+        if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "engine: event creation failed");
+    return PSVO_OK;
+}
+// `st` waits for `ev` recorded on `from` now (no-op when from == st)
+int fork_join(hipStream_t from, hipStream_t st, hipEvent_t ev) {
+    if (from == st) return PSVO_OK;
+    if (hipEventRecord(ev, from) != hipSuccess || hipStreamWaitEvent(st, ev, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: stream ordering failed");
+    return PSVO_OK;
+}
+
 // compositing.  want_act: keep the decoder activations for weight gradients
 // (mapping); tracking keeps only the masks.
 int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qset, const float *rays_o,
-           const float *rays_d, bool want_act, int *stats_out, const char *who, Render &o) {
+           const float *rays_d, bool want_act, int *stats_out, const char *who, Render &o,
+           bool fused_loss = false) {
     int rc = PSVO_OK;
     void *stream = st;
     const int max_steps = qset.max_steps;
@@ -390,6 +421,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
                                 z_vals, smask));
     mark(e, st, PSVO_TIME_POINTS, 1);
+    // the loss normalisers can start now (psvo_map_step, on aux)
+    if (fused_loss && engine_overlap(e)) ENG_CALL(fork_join(st, e->aux, e->z_ready));
     // ---- forward: interpolation, decoder, compositing
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
     mark(e, st, PSVO_TIME_INTERP_FWD, 0);
@@ -411,13 +444,6 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_CALL(psvo_mlp_fwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images,
                           sdf_s, rgb_s, act, masks));
     mark(e, st, PSVO_TIME_MLP_FWD, 1);
-    ENG_BUF(float, sdf, kSdf, RS * sizeof(float));
-    ENG_BUF(float, weights, kWeights, RS * sizeof(float));
-    ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
-    ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
-    ENG_BUF(float, z_min, kZmin, (size_t)r_hit * sizeof(float));
-    ENG_CALL(psvo_composite_fwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf,
-                                weights, color, depth, z_min));
     o.r_hit = r_hit;
     o.m = M;
     o.s_max = s_max;
@@ -434,6 +460,14 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.rgb_s = rgb_s;
     o.act = act;
     o.masks = masks;
+    if (fused_loss) return PSVO_OK;  // compositing is part of psvo_composite_loss
+    ENG_BUF(float, sdf, kSdf, RS * sizeof(float));
+    ENG_BUF(float, weights, kWeights, RS * sizeof(float));
+    ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
+    ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
+    ENG_BUF(float, z_min, kZmin, (size_t)r_hit * sizeof(float));
+    ENG_CALL(psvo_composite_fwd(stream, r_hit, s_max, d->truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf,
+                                weights, color, depth, z_min));
     o.sdf = sdf;
     o.weights = weights;
     o.color = color;
@@ -490,11 +524,35 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     Render q;
     QuerySet *qset = nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset));
-    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q));
+    const bool overlap = engine_overlap(e);
+    if (overlap) ENG_CALL(ensure_aux(e));
+    hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward
+    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
     const int64_t M = q.m;
-    // ---- loss and backward (d loss = 1)
-    float *g_sdf_s, *g_rgb_s;
-    ENG_CALL(loss_backward(e, st, d, q, gt_rgb, gt_depth, nullptr, nullptr, loss_out, &g_sdf_s, &g_rgb_s));
+    const int64_t r_hit = q.r_hit;
+    const int s_max = q.s_max;
+    // ---- loss and backward (d loss = 1): normalisers on aux (after the
+    // sampler, beside the decoder forward), then one fused per-ray pass
+    ENG_BUF(float, crit_ws, kCritWs, psvo_criterion_workspace_floats(r_hit) * sizeof(float));
+    ENG_BUF(double, sums_c, kSumsC, 8 * sizeof(double));
+    ENG_BUF(double, sums, kSums, 8 * sizeof(double));
+    ENG_BUF(float, coef, kCoef, 4 * sizeof(float));
+    ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
+    ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
+    ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
+    ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
+    const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
+    ENG_CALL(psvo_criterion_coef(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth, q.z_vals,
+                                 d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
+    ENG_CALL(fork_join(ax, st, e->coef_ready));
+    ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
+                                 q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
+                                 g_sdf_s, g_rgb_s));
+    // the loss value (not on the gradient path): aux, beside the decoder backward
+    ENG_CALL(fork_join(st, ax, e->grads_ready));
+    ENG_CALL(psvo_criterion_reduce(ax, r_hit, crit_ws, sums));
+    ENG_CALL(psvo_criterion_finalize(ax, sums, r_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
+                                     d->truncation, crit_flags, loss_out));
     const int n_split = 256;
     ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
@@ -515,22 +573,13 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     }
     float *const *W = d->dec;
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
-    // PSVO_SERIAL_BWD=1 (A/B aid): the embedding backward after the weight gradients on one stream
-    static const bool serial = getenv("PSVO_SERIAL_BWD") && *getenv("PSVO_SERIAL_BWD") == '1';
-    const bool overlap = !serial && !e->tm.on;  // timed runs keep the regions apart
-    if (overlap && !e->aux) {
-        if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&e->dfeat_ready, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->emb_done, hipEventDisableTiming) != hipSuccess)
-            return set_error(PSVO_E_LAUNCH, "map_step: aux stream creation failed");
-    }
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
     ENG_CALL(mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     // embedding backward: after dfeat (k_mlp_bwd2), beside k_mlp_dw2 / reduce
-    hipStream_t eb = overlap ? e->aux : st;
+    hipStream_t eb = ax;
     if (overlap && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     if (!(e->grads_clean && e->clean_buf == grad_emb) &&

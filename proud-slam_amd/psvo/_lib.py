@@ -37,6 +37,10 @@ _SIGNATURES = {
     "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
     "psvo_composite_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 10),
     "psvo_composite_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
+    "psvo_composite_loss": (_i32, [_vp, _i64, _i32, _f32, _f32] + [_vp] * 14),
+    "psvo_criterion_coef": (_i32, [_vp, _i64, _i32, _f32, _f32, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _i32, _vp,
+                                   _vp, _vp]),
+    "psvo_criterion_reduce": (_i32, [_vp, _i64, _vp, _vp]),
     "psvo_mlp_image_floats": (_i64, []),
     "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 16),
     "psvo_mlp_workspace_floats": (_i64, [_i64, _i32]),

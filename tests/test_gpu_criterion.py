@@ -147,3 +147,66 @@ def test_fused_criterion_deterministic():
     assert float(a[0]) == float(b[0])
     for x, y in zip(a[2:], b[2:]):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_composite_loss_matches_kernel_chain(seed):
+    """psvo_composite_loss (+ psvo_criterion_coef / _reduce) == composite_fwd →
+    criterion_sums → finalize → criterion_bwd → composite_bwd, bit for bit."""
+    from psvo import _lib as L
+    c = _case(seed)
+    r_hit, s_max = c["z"].shape
+    g = torch.Generator().manual_seed(100 + seed)
+    ns = (c["z"] < 10.0).sum(1).to(torch.int32)
+    offsets = torch.zeros(r_hit + 1, dtype=torch.int32)
+    offsets[1:] = torch.cumsum(ns, 0)
+    M = int(offsets[-1])
+    sdf_s = (torch.randn(M, generator=g) * 0.3).to(DEV)
+    rgb_s = torch.rand(M, 3, generator=g).to(DEV)
+    z = c["z"].contiguous().to(DEV)
+    rank_ray = c["hit"].to(torch.int32).to(DEV)
+    gt_rgb, gt_depth = c["gt_rgb"].to(DEV), c["gt_depth"].to(DEV)
+    offsets, ns = offsets.to(DEV), ns.to(DEV)
+    tr, md = 0.05, 5.0
+    w = (0.5, 1.0, 10.0, 5000.0)
+    st = L.stream_of(DEV)
+    f32 = dict(dtype=torch.float32, device=DEV)
+    # the chain
+    sdf, wts = torch.empty(r_hit, s_max, **f32), torch.empty(r_hit, s_max, **f32)
+    col, dep, zmin = torch.empty(r_hit, 3, **f32), torch.empty(r_hit, **f32), torch.empty(r_hit, **f32)
+    L.call("psvo_composite_fwd", st, r_hit, s_max, tr, L.ptr(offsets), L.ptr(ns), L.ptr(z), L.ptr(sdf_s),
+           L.ptr(rgb_s), L.ptr(sdf), L.ptr(wts), L.ptr(col), L.ptr(dep), L.ptr(zmin))
+    ws = torch.empty(r_hit * 8, **f32)
+    sums = torch.empty(8, dtype=torch.float64, device=DEV)
+    out = torch.zeros(16, **f32)
+    L.call("psvo_criterion_sums", st, r_hit, s_max, 0, tr, md, L.ptr(rank_ray), L.ptr(gt_rgb), L.ptr(gt_depth),
+           L.ptr(col), L.ptr(dep), L.ptr(sdf), L.ptr(z), L.ptr(ws), L.ptr(sums))
+    L.call("psvo_criterion_finalize", st, L.ptr(sums), r_hit, s_max, *w, tr, 7, L.ptr(out))
+    g_loss = torch.ones(1, **f32)
+    gc, gd, gs = torch.empty(r_hit, 3, **f32), torch.empty(r_hit, **f32), torch.empty(r_hit, s_max, **f32)
+    L.call("psvo_criterion_bwd", st, r_hit, s_max, tr, md, L.ptr(rank_ray), L.ptr(gt_rgb), L.ptr(gt_depth),
+           L.ptr(col), L.ptr(dep), L.ptr(sdf), L.ptr(z), L.ptr(out), L.ptr(g_loss), L.ptr(gc), L.ptr(gd), L.ptr(gs))
+    g_sdf_a, g_rgb_a = torch.empty(M, **f32), torch.empty(M, 3, **f32)
+    L.call("psvo_composite_bwd", st, r_hit, s_max, tr, L.ptr(offsets), L.ptr(ns), L.ptr(z), L.ptr(sdf), L.ptr(wts),
+           L.ptr(rgb_s), L.ptr(gc), L.ptr(gd), None, L.ptr(gs), L.ptr(g_sdf_a), L.ptr(g_rgb_a))
+    # the fused pass
+    ws2 = torch.full((r_hit * 8,), float("nan"), **f32)
+    sums_c, sums2 = torch.empty(8, dtype=torch.float64, device=DEV), torch.empty(8, dtype=torch.float64, device=DEV)
+    coef = torch.empty(4, **f32)
+    out2 = torch.zeros(16, **f32)
+    L.call("psvo_criterion_coef", st, r_hit, s_max, tr, md, L.ptr(rank_ray), L.ptr(gt_depth), L.ptr(z), *w, 7,
+           L.ptr(ws2), L.ptr(sums_c), L.ptr(coef))
+    col2, dep2 = torch.empty(r_hit, 3, **f32), torch.empty(r_hit, **f32)
+    g_sdf_b, g_rgb_b = torch.empty(M, **f32), torch.empty(M, 3, **f32)
+    L.call("psvo_composite_loss", st, r_hit, s_max, tr, md, L.ptr(offsets), L.ptr(ns), L.ptr(z), L.ptr(rank_ray),
+           L.ptr(gt_rgb), L.ptr(gt_depth), L.ptr(sdf_s), L.ptr(rgb_s), L.ptr(coef), L.ptr(ws2), L.ptr(col2),
+           L.ptr(dep2), L.ptr(g_sdf_b), L.ptr(g_rgb_b))
+    L.call("psvo_criterion_reduce", st, r_hit, L.ptr(ws2), L.ptr(sums2))
+    L.call("psvo_criterion_finalize", st, L.ptr(sums2), r_hit, s_max, *w, tr, 7, L.ptr(out2))
+    torch.cuda.synchronize()
+    assert torch.equal(coef, out[7:11]), (coef, out[7:11])
+    assert torch.equal(col2, col) and torch.equal(dep2, dep)
+    assert torch.equal(sums2, sums)
+    assert torch.equal(out2, out)
+    assert torch.equal(g_rgb_b, g_rgb_a)
+    assert torch.equal(g_sdf_b, g_sdf_a), float((g_sdf_b - g_sdf_a).abs().max())
