@@ -26,7 +26,7 @@
 #include "psvo_common.h"
 
 #ifdef PSVO_STAMPS
-__device__ unsigned long long psvo_g_stamps[2][256][8][8][16];  // diagnostic build only
+__device__ unsigned long long psvo_g_stamps[3][256][8][8][16];  // diagnostic build only
 #endif
 
 namespace psvo {
@@ -718,7 +718,7 @@ struct DwGrid {
 // out-of-range samples read a zero block), so the copy engine, not a layout
 // pass, sits between HBM and the MFMAs.  8 waves (2 per SIMD): L1..L3 wave w
 // owns rows {2(w>>2), 2(w>>2)+1} × column w&3 (32 × 32 blocks), the x
-// columns of W4 on waves with (w&3) < 2; L0 (W1, 4 row blocks) runs its MFMAs
+// columns of W4 on waves 0, 1, 6, 7 (one per SIMD); L0 (W1, 4 row blocks) runs its MFMAs
 // on waves 0..3 and W5 = δ5 ⊗ c1 on waves 4..7.  Bias sums and the W3 sdf row
 // ride on the MFMA operands already in registers.  One barrier per tile;
 // per-wave copy counts are uniform, so the wait is a compile-time vmcnt.
@@ -813,7 +813,8 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
         cb[0] = wave & 3;
     }
     const bool mfma_wave = (L != 0) || wave < 4;
-    const bool xwave = XBLK && (wave & 3) < 2;
+    // the 4 x row blocks on waves 0, 1, 6, 7: one per SIMD (waves w and w+4 share SIMD w&3)
+    const bool xwave = XBLK && ((wave >> 2) == 0 ? (wave & 3) < 2 : (wave & 3) >= 2);
     const int xsel = wave & 1;
     const bool own_bias = (L == 0) ? wave < 4 : ((wave & 3) == 0);  // D rows summed once
     const bool own_sdf = (L == 2) && ((wave >> 2) == 0);             // A columns dotted once
@@ -839,6 +840,26 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
 #pragma unroll
     for (int k = 0; k < kDw2Stages - 1; ++k)
         if (u_beg + k < u_end) dw2_issue<L>(src, zblk, u_beg + k, m, lds + k * kStage2, wave, lane);
+#ifdef PSVO_STAMPS
+    unsigned long long dws_[8] = {};  // start, end, wait, barrier, issue, mfma, units
+    auto dw_now = []() {
+        unsigned long long t_;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return t_;
+    };
+    dws_[0] = dw_now();
+    unsigned long long t_a_ = dws_[0];
+#define PSVO_DW_SEG(k)                     \
+    do {                                   \
+        const unsigned long long t_b_ = dw_now(); \
+        dws_[k] += t_b_ - t_a_;            \
+        t_a_ = t_b_;                       \
+    } while (0)
+#else
+#define PSVO_DW_SEG(k)
+#endif
     for (int64_t u = u_beg; u < u_end; ++u) {
         float *st = lds + ((int)((u - u_beg) & (kDw2Stages - 1))) * kStage2;
         // tile u landed for this wave: only the newer in-flight tiles may still be outstanding
@@ -846,10 +867,13 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
         if (ahead >= 2) wait_vm_c<2 * NI>();
         else if (ahead == 1) wait_vm_c<NI>();
         else wait_vm_c<0>();
+        PSVO_DW_SEG(2);
         raw_barrier();  // ... for every wave; and every wave is done with tile u-1's stage
+        PSVO_DW_SEG(3);
         if (u + kDw2Stages - 1 < u_end)
             dw2_issue<L>(src, zblk, u + kDw2Stages - 1, m,
                          lds + ((int)((u + kDw2Stages - 1 - u_beg) & (kDw2Stages - 1))) * kStage2, wave, lane);
+        PSVO_DW_SEG(4);
         const float *Dl = st + kS2D, *Al = st + kS2A, *Sl = st + kS2S;
         if (L == 0 && wave >= 4) {  // W5 = δ5 ⊗ c1 (A rows 32..159): thread = (c1 row, k-half); db5
             const int tw = threadIdx.x - 256;
@@ -913,8 +937,20 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
                 }
             }
         }
+        PSVO_DW_SEG(5);
     }
     wait_vm_c<0>();
+#ifdef PSVO_STAMPS
+    dws_[1] = dw_now();
+    dws_[6] = (unsigned long long)(u_end - u_beg);
+    dws_[7] = (unsigned long long)L;
+    {
+        const int wg_ = blockIdx.x + 0;
+        if (lane == 0 && wg_ < 256)
+            for (int i_ = 0; i_ < 8; ++i_) psvo_g_stamps[2][wg_][wave][0][i_] = dws_[i_];
+    }
+#endif
+#undef PSVO_DW_SEG
     // ---- the slab: [rows][cols] weights, then [rows] bias
     constexpr int ROWS = (L == 2) ? 129 : 128;
     constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
@@ -1361,7 +1397,7 @@ static bool use_fwd2() {
 }  // namespace psvo
 
 #ifdef PSVO_STAMPS
-// copies the stamp array ([2 kernels][256 wg][8 waves][8 tiles][16 points] u64)
+// copies the stamp array ([3 kernels][256 wg][8 waves][8 tiles][16 points] u64)
 extern "C" int psvo_debug_stamps(void *dst, int64_t bytes) {
     if (bytes < (int64_t)sizeof(psvo_g_stamps)) return -1;
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(psvo_g_stamps), sizeof(psvo_g_stamps)) == hipSuccess ? 0 : -2;
@@ -1425,8 +1461,9 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-// relative per-tile time of the workgroup types (W1+W5, W2, W3, W4), measured standalone
-static const int kDw2Weight[4] = {29, 53, 56, 79};
+// relative per-tile time of the workgroup types (W1+W5, W2, W3, W4): s_memtime stamps
+// (scripts/mlp_stamps.py) at the bench size, 3010 / 5713 / 5929 / 7258 cycles per wave
+static const int kDw2Weight[4] = {28, 53, 55, 67};
 
 static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
     const int64_t chunks = (m + kTileS - 1) / kTileS;  // split units: CF tiles

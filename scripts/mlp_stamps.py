@@ -30,7 +30,7 @@ def main():
         (out["sdf"].sum() + out["color"].sum()).backward()
     torch.cuda.synchronize()
     L = ctypes.CDLL(_lib.LIB_PATH)
-    shape = (2, 256, 8, 8, 16)
+    shape = (3, 256, 8, 8, 16)
     buf = np.zeros(shape, dtype=np.uint64)
     rc = L.psvo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(buf.nbytes))
     assert rc == 0, rc
@@ -63,6 +63,26 @@ def main():
         t0 = first[first > 0].min()
         print(f"   kernel span (stamps) {(last_end.max() - t0):.0f} cycles; WG end spread "
               f"{np.percentile(last_end - t0, [0, 50, 90, 100]).round()}; tiles/WG {np.bincount(its)}")
+    dw_report(buf)
+
+
+def dw_report(buf):
+    """k_mlp_dw2: per-workgroup span and per-wave segment shares, by layer type."""
+    st = buf[2, :, :, 0, :8].astype(np.int64)  # [wg][wave][start,end,wait,bar,issue,mfma,units,L]
+    used = st[:, 0, 0] > 0
+    t0 = st[used, :, 0].min()
+    print("dw2: per layer type (0: W1+W5, 1: W2, 2: W3, 3: W4)")
+    for L in range(4):
+        sel = used & (st[:, 0, 7] == L)
+        if not sel.any():
+            continue
+        span = (st[sel, :, 1].max(1) - t0)
+        seg = st[sel][:, :, 2:6].sum(axis=(0, 1)).astype(np.float64)
+        tot = seg.sum()
+        units = st[sel, 0, 6]
+        print(f"  L{L}: {int(sel.sum())} wgs, units/wg {units.min()}-{units.max()}, end {span.min()}-{span.max()} cycles, "
+              f"wait {100 * seg[0] / tot:.1f}% bar {100 * seg[1] / tot:.1f}% issue {100 * seg[2] / tot:.1f}% "
+              f"mfma {100 * seg[3] / tot:.1f}%  per-unit {tot / units.sum() / 8:.0f} cyc/wave")
 
 
 if __name__ == "__main__":
