@@ -1070,6 +1070,76 @@ constexpr int kStampIters = 8, kStampWgs = 256;  // psvo_g_stamps[2][256][8][8][
 #define PSVO_STAMP_FLUSH(k)
 #endif
 
+// ---- k_mlp_fwd2's W4 layer, one 32-row output block at a time ----------
+// Block OB's MFMAs carry the CF stores of f (its block OB, the layer input)
+// and of c1 block OB-1 (finished, ReLU'd) — one store each per k-step — so
+// the c1 tile no longer leaves in one 64-store burst that, issued by every
+// wave of the chip at once, stalled the epilogue on HBM write drain; block
+// OB's ReLU and mask bits run under block OB+1's MFMAs.  Per accumulator the
+// MFMA order is unchanged: the same bits.
+template <int OB>
+struct L4Queue {
+    static constexpr int kN = OB > 0 ? 2 : 1;
+    const CfStore &c;
+    const f32x16 (&f)[kNB];
+    const f32x16 (&c1)[kNB];
+    __amdgpu_buffer_rsrc_t rf, rc;
+    __device__ L4Queue(const CfStore &cs, const float *fm, const float *cm, int64_t bytes, bool on,
+                       const f32x16 (&ff)[kNB], const f32x16 (&cc)[kNB])
+        : c(cs), f(ff), c1(cc),
+          rf(__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fm), 0,
+                                               __builtin_amdgcn_readfirstlane((on && cs.ok) ? (int)bytes : 0),
+                                               0x00020000)),
+          rc(__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(cm), 0,
+                                               __builtin_amdgcn_readfirstlane((on && cs.ok) ? (int)bytes : 0),
+                                               0x00020000)) {}
+    __device__ __forceinline__ void operator()(int kb, int rg) const {
+        const int r = 4 * kb + rg;
+        const int vo = c.voff[((r >> 1) & 1) + 2 * ((r >> 2) & 1)];
+        const int so = 1024 * (r >> 2) + 128 * (r & 3);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f[OB][r]), rf, vo, 4096 * OB + so, 0);
+        if (OB > 0)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c1[OB - 1][r]), rc, vo, 4096 * (OB - 1) + so, 0);
+    }
+};
+
+// relu() restricted to block OB (same per-element sequence and mask bits)
+template <int OB>
+__device__ __forceinline__ void relu_block(f32x16 &v, uint32_t (&half)[2]) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float y = v[r];
+        asm volatile("" : "+v"(y));
+        y = fmaxf(y, 0.0f);
+        v[r] = y;
+        const uint32_t u = __float_as_uint(y);
+        const uint32_t t = (0u - u) & ~u;
+        half[OB >> 1] |= (t >> 31) << (16 * (OB & 1) + r);
+        asm volatile("" : "+v"(half[OB >> 1]));
+    }
+}
+
+// bacc[OB] += W4 block OB · [f; x] (bias already in bacc), then its ReLU and
+// mask bits (the rgb head's dots wait for all four blocks: until then f is
+// live as the layer input and the registers are spoken for)
+template <int OB>
+__device__ __forceinline__ void l4_block(const float *wl, const f32x16 (&a)[kNB], const float (&x)[8],
+                                         f32x16 (&bacc)[kNB], int lane, const L4Queue<OB> &q,
+                                         uint32_t (&half)[2]) {
+    f32x16 (&acc)[1] = *reinterpret_cast<f32x16(*)[1]>(&bacc[OB]);
+    gemm_acc<kNB, 1>(wl + OB * kNB * 4 * 64 * 4, a, acc, lane, q);
+    const float *wx = wl + kNB * kNB * 16 * 64;
+#pragma unroll
+    for (int tg = 0; tg < 2; ++tg) {
+        const float4 w4 = *reinterpret_cast<const float4 *>(wx + (((OB * 2 + tg) * 64 + lane) << 2));
+        acc[0] = mfma(w4.x, x[4 * tg + 0], acc[0]);
+        acc[0] = mfma(w4.y, x[4 * tg + 1], acc[0]);
+        acc[0] = mfma(w4.z, x[4 * tg + 2], acc[0]);
+        acc[0] = mfma(w4.w, x[4 * tg + 3], acc[0]);
+    }
+    relu_block<OB>(bacc[OB], half);
+}
+
 // ---------------------------------------------------------------------------
 // forward, persistent + double-buffered: one 512-thread workgroup per CU
 // loops over 256-sample tiles (8 waves × 32 samples, the chain of k_mlp_fwd
@@ -1156,11 +1226,26 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
             load_x(feat, sn, sn < m, h, xn);
         }
         init_bias(bacc, lds + kOffB4, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act + 2 * tstride, tbytes, save, a));  // + f
-        gemm_x(buf(seq) + kNB * kNB * 16 * 64, x, bacc, lane);
+        uint32_t half4[2] = {0u, 0u};
+        {
+            const float *wl4 = buf(seq);
+            const float *fm = act + 2 * tstride, *cm = act + 3 * tstride;
+            l4_block<0>(wl4, a, x, bacc, lane, L4Queue<0>(cfs, fm, cm, tbytes, save, a, bacc), half4);
+            l4_block<1>(wl4, a, x, bacc, lane, L4Queue<1>(cfs, fm, cm, tbytes, save, a, bacc), half4);
+            l4_block<2>(wl4, a, x, bacc, lane, L4Queue<2>(cfs, fm, cm, tbytes, save, a, bacc), half4);
+            l4_block<3>(wl4, a, x, bacc, lane, L4Queue<3>(cfs, fm, cm, tbytes, save, a, bacc), half4);
+            if (save && cfs.ok) {  // c1 block 3
+                const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<float *>(cm), 0, __builtin_amdgcn_readfirstlane((int)tbytes), 0x00020000);
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bacc[3][r]), rc,
+                                                          cfs.voff[((r >> 1) & 1) + 2 * ((r >> 2) & 1)],
+                                                          4096 * 3 + 1024 * (r >> 2) + 128 * (r & 3), 0);
+            }
+        }
         ++seq;
-        const uint64_t m4 = relu(bacc);
-        if (save) cfs.store(act + 3 * tstride, tbytes, bacc);
+        const uint64_t m4 = (uint64_t)half4[0] | ((uint64_t)half4[1] << 32);
         if (save_mask && valid) {
             uint64_t *mk = masks + (s * 2 + h) * 3;
             mk[0] = m1;
