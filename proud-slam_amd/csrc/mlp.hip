@@ -724,8 +724,8 @@ struct DwGrid {
 // per-wave copy counts are uniform, so the wait is a compile-time vmcnt.
 constexpr int kDw2Waves = 8;
 constexpr int kS2D = 0, kS2A = 128 * kTileS, kS2S = kS2A + kDwA * kTileS, kStage2 = kS2S + 64 * kDw2Waves;
-constexpr int kDw2Stages = 4;
-constexpr int kDw2Lds = kDw2Stages * kStage2;  // 155,648 B
+constexpr int kDw2Stages = 3;
+constexpr int kDw2Lds = kDw2Stages * kStage2;  // 116,736 B: room beside it for 2 k_interp_bwd workgroups
 static_assert(kDw2Lds * 4 <= 160 * 1024, "dw2 LDS budget");
 
 template <int N>
@@ -861,7 +861,7 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
 #define PSVO_DW_SEG(k)
 #endif
     for (int64_t u = u_beg; u < u_end; ++u) {
-        float *st = lds + ((int)((u - u_beg) & (kDw2Stages - 1))) * kStage2;
+        float *st = lds + ((int)((u - u_beg) % kDw2Stages)) * kStage2;
         // tile u landed for this wave: only the newer in-flight tiles may still be outstanding
         const int64_t ahead = (u_end - 1 - u) < (kDw2Stages - 2) ? (u_end - 1 - u) : (kDw2Stages - 2);
         if (ahead >= 2) wait_vm_c<2 * NI>();
@@ -872,7 +872,7 @@ __device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const flo
         PSVO_DW_SEG(3);
         if (u + kDw2Stages - 1 < u_end)
             dw2_issue<L>(src, zblk, u + kDw2Stages - 1, m,
-                         lds + ((int)((u + kDw2Stages - 1 - u_beg) & (kDw2Stages - 1))) * kStage2, wave, lane);
+                         lds + ((int)((u + kDw2Stages - 1 - u_beg) % kDw2Stages)) * kStage2, wave, lane);
         PSVO_DW_SEG(4);
         const float *Dl = st + kS2D, *Al = st + kS2A, *Sl = st + kS2S;
         if (L == 0 && wave >= 4) {  // W5 = δ5 ⊗ c1 (A rows 32..159): thread = (c1 row, k-half); db5
