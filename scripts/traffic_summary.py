@@ -32,9 +32,9 @@ K = out["kernels"]
 if "k_interp_bwd" in K:
     out["interp_bwd_bytes_per_launch"] = K["k_interp_bwd"]["total"]
 mlp = [n for n in ("k_mlp_prep", "k_mlp_fwd", "k_mlp_fwd2", "k_mlp_bwd_data", "k_mlp_bwd2", "k_mlp_dw",
-                    "k_mlp_dw_reduce") if n in K]
+                    "k_mlp_dw2", "k_mlp_dw_reduce") if n in K]
 out["mlp_bytes_per_step"] = sum(K[n]["total"] for n in mlp)
-qi = [n for n in ("k_intersect_sorted", "k_ray_stats", "k_hit_rank", "k_sample_fused", "k_scan_samples",
+qi = [n for n in ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples",
                   "k_sample_points", "k_interp_fwd", "k_interp_bwd") if n in K]
 out["query_interp_bytes_per_step"] = sum(K[n]["total"] for n in qi)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
