@@ -218,6 +218,8 @@ def main():
         args.autograd = True  # the engine samples per rank; exactness runs the drop-in path
     engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
                            criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
+    from psvo.dist import EngineGradExchange
+    exchange = EngineGradExchange(engine)
 
     def record_stats(m, r_hit, visits, s_max):
         stats["m"] += m
@@ -262,8 +264,7 @@ def main():
         engine.query(nro, nrd, nseed)
         loss = engine.step(ro, rd, rgb, depth, seed=seed, apply_adam=(world == 1))
         if world > 1:
-            dist.all_reduce(engine.grad_flat)
-            engine.grad_flat.div_(world)
+            exchange()  # flat RCCL all-reduce (row-sparse exchange for ≥ 32 MB tables), mean over ranks
             engine.adam()
         if record:
             st = engine.last_stats
@@ -352,6 +353,8 @@ def main():
         try:
             traffic = json.load(open(args.traffic_json))
         except Exception:
+            traffic = {}
+        if traffic.get("scene", "room0") != args.scene:  # PMC passes of another scene: not this workload's bytes
             traffic = {}
     result = {
         "metric": METRIC,

@@ -362,6 +362,20 @@ enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
 
 int64_t psvo_map_grad_floats(int64_t n_emb);
 
+/* ---- row-sparse gradient exchange (data parallel on large maps, §8e) ---- */
+/* Ints of workspace psvo_rows_compact needs for n_rows rows. */
+int64_t psvo_rows_workspace_ints(int64_t n_rows);
+/* Pack the rows of grad f32[n_rows, width] with a non-zero element: ids
+ * i32[count] ascending, rows f32[count, width]; count → device int.  Replaces
+ * the dense all-reduce of the embedding gradient (GradBucket / the engine's
+ * flat bucket) when a step touches few rows of a large table. */
+int psvo_rows_compact(void *stream, int64_t n_rows, int width, const float *grad, int *workspace, int *ids,
+                      float *rows, int *count);
+/* grad[ids[i]] += rows[i] for i < n_list (ids unique within the list; ids < 0
+ * are padding and skipped).  Applying every rank's list in rank order gives
+ * every rank the same sums, bit for bit. */
+int psvo_rows_scatter_add(void *stream, int64_t n_list, int width, const int *ids, const float *rows, float *grad);
+
 psvo_engine *psvo_engine_new(void);
 void psvo_engine_free(psvo_engine *e);
 

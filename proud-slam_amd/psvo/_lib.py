@@ -41,6 +41,9 @@ _SIGNATURES = {
     "psvo_criterion_coef": (_i32, [_vp, _i64, _i32, _f32, _f32, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _i32, _vp,
                                    _vp, _vp]),
     "psvo_criterion_reduce": (_i32, [_vp, _i64, _vp, _vp]),
+    "psvo_rows_workspace_ints": (_i64, [_i64]),
+    "psvo_rows_compact": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "psvo_rows_scatter_add": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "psvo_mlp_image_floats": (_i64, []),
     "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 16),
     "psvo_mlp_workspace_floats": (_i64, [_i64, _i32]),

@@ -158,3 +158,115 @@ def shard(n_total, rank, world_size):
     per = (n_total + world_size - 1) // world_size
     b = min(n_total, rank * per)
     return b, min(n_total, b + per)
+
+
+class DeviceRowOps:
+    """psvo_rows_compact / psvo_rows_scatter_add on the tensor's device (HIP)."""
+
+    def __init__(self):
+        from psvo import _lib as L
+        self.L = L
+
+    def compact(self, grad2d, ids, rows, count, workspace):
+        self.L.call("psvo_rows_compact", self.L.stream_of(grad2d.device), grad2d.shape[0], grad2d.shape[1], grad2d,
+                    workspace, ids, rows, count)
+
+    def scatter_add(self, ids, rows, grad2d):
+        self.L.call("psvo_rows_scatter_add", self.L.stream_of(grad2d.device), ids.shape[0], grad2d.shape[1], ids,
+                    rows, grad2d)
+
+    def workspace_ints(self, n_rows):
+        return int(self.L.lib().psvo_rows_workspace_ints(n_rows))
+
+
+class SparseRowSum:
+    """In-place all-reduce (sum) of a row-sparse gradient grad2d [n_rows, width]
+    that exchanges only the rows a rank touched (a step's
+    rays reach a few hundred thousand embedding rows of a multi-million-row
+    table, so (id, row) pairs are a small fraction of the dense bytes a ring
+    all-reduce moves).
+
+    Protocol: compact the non-zero rows on the device (ascending ids), one
+    host read of the count, all-gather the counts, all-gather the padded
+    (id, row) lists, zero grad2d and scatter-add the lists in rank order — the
+    same additions in the same order on every rank, so replicas stay
+    bit-identical.  Falls back to a dense all-reduce when the padded lists
+    would move more bytes than the table.  Returns "sparse" or "dense"."""
+
+    def __init__(self, n_rows, width, device, group=None, ops=None):
+        self.group = group
+        self.ops = ops if ops is not None else DeviceRowOps()
+        self.ids = torch.empty(n_rows, dtype=torch.int32, device=device)
+        self.rows = torch.empty(n_rows, width, dtype=torch.float32, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.workspace = torch.empty(max(1, self.ops.workspace_ints(n_rows)), dtype=torch.int32, device=device)
+
+    def __call__(self, grad2d):
+        n_rows, width = grad2d.shape
+        ws = world()
+        if ws == 1:
+            return "dense"
+        self.ops.compact(grad2d, self.ids, self.rows, self.count, self.workspace)
+        stage = torch.device("cpu") if _backend(self.group) == "gloo" else grad2d.device
+        cnt = self.count.to(stage, torch.int64)
+        counts = [torch.empty_like(cnt) for _ in range(ws)]
+        dist.all_gather(counts, cnt, group=self.group)
+        counts = [int(c) for c in counts]
+        n_max = max(counts)
+        if ws * n_max * (width + 1) >= n_rows * width:
+            flat = grad2d if stage == grad2d.device else grad2d.to(stage)
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            if flat is not grad2d:
+                grad2d.copy_(flat)
+            return "dense"
+        if n_max == 0:  # no rank touched a row: the sum is zero (and gloo rejects empty gathers)
+            grad2d.zero_()
+            return "sparse"
+        mine = int(counts[dist.get_rank(self.group) if self.group is not None else dist.get_rank()])
+        ids = torch.full((n_max,), -1, dtype=torch.int32, device=stage)
+        rows = torch.zeros((n_max, width), dtype=torch.float32, device=stage)
+        ids[:mine].copy_(self.ids[:mine])
+        rows[:mine].copy_(self.rows[:mine])
+        all_ids = [torch.empty_like(ids) for _ in range(ws)]
+        all_rows = [torch.empty_like(rows) for _ in range(ws)]
+        dist.all_gather(all_ids, ids, group=self.group)
+        dist.all_gather(all_rows, rows, group=self.group)
+        grad2d.zero_()
+        for r in range(ws):
+            k = counts[r]
+            if k:
+                self.ops.scatter_add(all_ids[r][:k].to(grad2d.device), all_rows[r][:k].to(grad2d.device), grad2d)
+        return "sparse"
+
+
+class EngineGradExchange:
+    """The engine's per-step gradient exchange (MappingEngine.grad_flat =
+    [embedding rows | decoder]): one flat all-reduce while the table is small
+    (config B/D: 0.9 MB of embeddings — latency-bound, one collective is best),
+    SparseRowSum on the embedding rows + a dense all-reduce of the decoder
+    tail once the table reaches `sparse_min_bytes` (config E's multi-million-
+    row table, where a step touches a small fraction of the rows).  The
+    result is averaged over ranks (op "mean", as GradBucket)."""
+
+    def __init__(self, engine, sparse_min_bytes=32 << 20, group=None, ops=None):
+        self.engine = engine
+        self.group = group
+        self.n_emb = int(engine.emb.shape[0])
+        self.sparse = None
+        if self.n_emb * 16 * 4 >= sparse_min_bytes:
+            self.sparse = SparseRowSum(self.n_emb, 16, engine.grad_flat.device, group=group, ops=ops)
+        self.last_mode = "dense"
+
+    def __call__(self):
+        ws = world()
+        if ws == 1:
+            return
+        flat = self.engine.grad_flat
+        if self.sparse is None:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.last_mode = "dense"
+        else:
+            n = self.n_emb * 16
+            self.last_mode = self.sparse(flat[:n].view(self.n_emb, 16))
+            dist.all_reduce(flat[n:], op=dist.ReduceOp.SUM, group=self.group)
+        flat.div_(ws)

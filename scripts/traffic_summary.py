@@ -37,5 +37,6 @@ out["mlp_bytes_per_step"] = sum(K[n]["total"] for n in mlp)
 qi = [n for n in ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples",
                   "k_sample_points", "k_interp_fwd", "k_interp_bwd") if n in K]
 out["query_interp_bytes_per_step"] = sum(K[n]["total"] for n in qi)
+out["scene"] = sys.argv[4] if len(sys.argv) > 4 else "room0"  # the bench scene the passes ran (gpu_traffic.sh: default)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps({k: round(v["total"] / 1e6, 2) for k, v in K.items()}, indent=0))

@@ -107,3 +107,67 @@ def test_sharded_global_loss_and_grad_bucket_match_single_process():
     # replicas stay identical
     for a, b in zip(res[0][4], res[1][4]):
         assert torch.equal(a, b)
+
+
+class _TorchRowOps:
+    """Test-only stand-in for psvo_rows_compact / psvo_rows_scatter_add on CPU
+    tensors, to check SparseRowSum's exchange protocol over gloo (the device
+    kernels themselves are checked in tests/test_gpu_rows.py)."""
+
+    def workspace_ints(self, n_rows):
+        return 1
+
+    def compact(self, grad2d, ids, rows, count, workspace):
+        nz = (grad2d != 0).any(1).nonzero().flatten()
+        ids[: nz.numel()] = nz.to(torch.int32)
+        rows[: nz.numel()] = grad2d[nz]
+        count[0] = nz.numel()
+
+    def scatter_add(self, ids, rows, grad2d):
+        keep = ids >= 0
+        grad2d[ids[keep].long()] += rows[keep]
+
+
+def _sparse_grad(rank, n_rows, touched, seed):
+    g = torch.Generator().manual_seed(seed + rank)
+    grad = torch.zeros(n_rows, 16)
+    idx = torch.randperm(n_rows, generator=g)[:touched]
+    grad[idx] = torch.randn(touched, 16, generator=g)
+    return grad
+
+
+def _sparse_worker(rank, world, port, q, n_rows, touched):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from psvo.dist import SparseRowSum
+        grad = _sparse_grad(rank, n_rows, touched, 7)
+        mode = SparseRowSum(n_rows, 16, "cpu", ops=_TorchRowOps())(grad)
+        q.put((rank, mode, grad.numpy().copy()))  # by value: the worker may exit before the get
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("touched,expect", [(40, "sparse"), (0, "sparse"), (900, "dense")])
+def test_sparse_row_sum_protocol(touched, expect):
+    """Row-sparse exchange (config E data parallelism): every rank ends with
+    the sum of all ranks' gradients, bit-identical across ranks; the dense
+    fallback when the lists would outweigh the table."""
+    n_rows, world = 1000, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sparse_worker, args=(r, world, port, q, n_rows, touched)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = sum(_sparse_grad(r, n_rows, touched, 7) for r in range(world))
+    got = [torch.from_numpy(r[2]) for r in res]
+    for (rank, mode, _), grad in zip(res, got):
+        assert mode == expect
+        torch.testing.assert_close(grad, want, rtol=1e-6, atol=1e-6)
+    assert torch.equal(got[0], got[1]) and torch.equal(got[0], got[2])
