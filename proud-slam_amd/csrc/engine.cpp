@@ -78,7 +78,7 @@ struct psvo_engine {
     // beside the decoder backward)
     hipStream_t aux = nullptr;
     hipEvent_t dfeat_ready = nullptr, emb_done = nullptr, z_ready = nullptr, coef_ready = nullptr,
-               grads_ready = nullptr;
+               grads_ready = nullptr, prep_fork = nullptr, prep_done = nullptr;
     EngineTimer tm;
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
@@ -214,6 +214,8 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->z_ready) (void)hipEventDestroy(e->z_ready);
     if (e->coef_ready) (void)hipEventDestroy(e->coef_ready);
     if (e->grads_ready) (void)hipEventDestroy(e->grads_ready);
+    if (e->prep_fork) (void)hipEventDestroy(e->prep_fork);
+    if (e->prep_done) (void)hipEventDestroy(e->prep_done);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
@@ -371,7 +373,8 @@ bool engine_overlap(psvo_engine *e) {
 }
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
-    hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready};
+    hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
+                         &e->prep_fork, &e->prep_done};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
     for (hipEvent_t *ev : evs)
@@ -412,6 +415,15 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     if (stats_out) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
+    float *const *W = d->dec;
+    ENG_BUF(float, images, kImages, psvo_mlp_image_floats() * sizeof(float));
+    // the decoder's operand images depend only on the weights: built on aux
+    // beside the sampler compaction and the interpolation (psvo_map_step)
+    const bool early_images = fused_loss && engine_overlap(e);
+    if (early_images) {
+        ENG_CALL(fork_join(st, e->aux, e->prep_fork));
+        ENG_CALL(mlp_images(e->aux, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+    }
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
     ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
@@ -430,7 +442,6 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
                              d->vertex_idx, d->emb, feat));
     mark(e, st, PSVO_TIME_INTERP_FWD, 1);
     const int64_t mp = (M + 63) / 64 * 64;
-    ENG_BUF(float, images, kImages, psvo_mlp_image_floats() * sizeof(float));
     ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
     ENG_BUF(float, rgb_s, kRgbS, M * 3 * sizeof(float));
     float *act = nullptr;
@@ -439,10 +450,15 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         act = abuf;
     }
     ENG_BUF(uint64_t, masks, kMasks, (size_t)M * 6 * sizeof(uint64_t));
-    float *const *W = d->dec;
     mark(e, st, PSVO_TIME_MLP_FWD, 0);
-    ENG_CALL(psvo_mlp_fwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images,
-                          sdf_s, rgb_s, act, masks));
+    if (early_images) {
+        ENG_CALL(fork_join(e->aux, st, e->prep_done));
+        ENG_CALL(mlp_fwd_prepared(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                                  images, sdf_s, rgb_s, act, masks));
+    } else {
+        ENG_CALL(psvo_mlp_fwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                              images, sdf_s, rgb_s, act, masks));
+    }
     mark(e, st, PSVO_TIME_MLP_FWD, 1);
     o.r_hit = r_hit;
     o.m = M;

@@ -1493,10 +1493,10 @@ using namespace psvo;
 
 extern "C" int64_t psvo_mlp_image_floats(void) { return kImgTotal; }
 
-extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                             const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                            float *act, uint64_t *masks) {
+                            float *act, uint64_t *masks, bool images_ready) {
     PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused path is width 128)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
     PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats floats)");
@@ -1512,7 +1512,7 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
     }
     hipStream_t st = as_stream(stream);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
+    if (!images_ready) hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
     if (rgb == nullptr) {  // sdf only (inference)
         PSVO_REQUIRE(act == nullptr && masks == nullptr, "mlp_fwd: the sdf-only forward is inference only");
         static bool attr_s = false;
@@ -1542,6 +1542,30 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
                            rgb, act, masks);
     }
     return check_launch("mlp_fwd");
+}
+
+namespace psvo {
+int mlp_images(void *stream, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+               const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images) {
+    MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
+    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, as_stream(stream), p, images);
+    return check_launch("mlp_images");
+}
+int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                     const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                     const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
+                     float *act, uint64_t *masks) {
+    return mlp_fwd_impl(stream, m, width, feat, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images, sdf, rgb, act, masks,
+                        true);
+}
+}  // namespace psvo
+
+extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                            const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                            const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
+                            float *act, uint64_t *masks) {
+    return mlp_fwd_impl(stream, m, width, feat, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images, sdf, rgb, act, masks,
+                        false);
 }
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};

@@ -44,6 +44,16 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready);
 
+// the decoder's LDS operand images (k_mlp_prep) on their own, and
+// psvo_mlp_fwd without rebuilding them (the engine prepares them on its aux
+// stream beside the sampler / interpolation kernels)
+int mlp_images(void *stream, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+               const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
+int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
+                     const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
+                     const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
+                     float *act, uint64_t *masks);
+
 }  // namespace psvo
 
 #define PSVO_REQUIRE(cond, ...)                                       \
