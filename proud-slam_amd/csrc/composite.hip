@@ -35,9 +35,14 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 // with the roundings spelled out (fmaf), so both kernels produce the same
 // bits whatever the compiler would contract in either context.
 // dL/dW_s = g_depth·z_s + g_w,s (+ g_colour·c_s for a valid sample)
-__device__ __forceinline__ float comp_gw(float gdp, float z, float gwx, const float *c, float gr, float gg, float gb) {
+__device__ __forceinline__ float comp_gw3(float gdp, float z, float gwx, bool has_c, float c0, float c1, float c2,
+                                          float gr, float gg, float gb) {
     const float g = fmaf(gdp, z, gwx);
-    return c ? fmaf(gb, c[2], fmaf(gg, c[1], fmaf(gr, c[0], g))) : g;
+    return has_c ? fmaf(gb, c2, fmaf(gg, c1, fmaf(gr, c0, g))) : g;
+}
+__device__ __forceinline__ float comp_gw(float gdp, float z, float gwx, const float *c, float gr, float gg, float gb) {
+    return c ? comp_gw3(gdp, z, gwx, true, c[0], c[1], c[2], gr, gg, gb) : comp_gw3(gdp, z, gwx, false, 0.f, 0.f,
+                                                                                   0.f, gr, gg, gb);
 }
 // dL/dsdf_s through the weights (kept samples) plus the direct term g
 __device__ __forceinline__ float comp_gsdf(float gw, float dot, float tot, bool keep, float sdf, float tr, float g) {
@@ -203,6 +208,10 @@ __device__ __forceinline__ float crit_grad(float cfs, float csdf, const CritTerm
     return cfs * t.xfs * t.f + csdf * t.ysdf * t.sm;
 }
 
+// J > 0: a ray's samples (s_max ≤ 64·J) are read once into registers —
+// sample s = lane + 64j in slot j — and every pass runs from them; J = 0
+// re-reads memory per pass (any s_max).  Same operations in the same order.
+template <int J>
 __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max, float tr, float max_depth,
                                                         const int *__restrict__ offsets,
                                                         const int *__restrict__ ray_ns,
@@ -221,38 +230,63 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const int off = offsets[r], ns = ray_ns[r];
     const float *z = z_vals + r * s_max;
     auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
+    constexpr int JR = J > 0 ? J : 1;
+    float zr[JR], pr[JR], c0r[JR], c1r[JR], c2r[JR];
+    if constexpr (J > 0) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int s = lane + 64 * j;
+            zr[j] = s < s_max ? z[s] : 0.f;
+            pr[j] = sdf_at(s);
+            const bool v = s < ns;
+            const float *c = rgb_s + (int64_t)(off + (v ? s : 0)) * 3;
+            c0r[j] = v ? c[0] : 0.f;
+            c1r[j] = v ? c[1] : 0.f;
+            c2r[j] = v ? c[2] : 0.f;
+        }
+    }
+    auto Z = [&](int j, int s) {
+        if constexpr (J > 0) return zr[j]; else return z[s];
+    };
+    auto P = [&](int j, int s) {
+        if constexpr (J > 0) return pr[j]; else return sdf_at(s);
+    };
+    auto C = [&](int j, int s, int k) {
+        if constexpr (J > 0) return k == 0 ? c0r[j] : (k == 1 ? c1r[j] : c2r[j]);
+        else return rgb_s[(int64_t)(off + s) * 3 + k];
+    };
+#define PSVO_FOR_S(lim) for (int j = 0, s = lane; (J == 0 || j < J) && s < (lim); ++j, s += 64)
     // ---- forward (k_composite_fwd)
     int first = s_max;
-    for (int s = lane; s < s_max; s += 64) {
-        const float v = sdf_at(s);
+    PSVO_FOR_S(s_max) {
+        const float v = P(j, s);
         if (s + 1 < s_max && sdf_at(s + 1) * v < 0.0f) first = min(first, s);
     }
     first = wmin(first);
     const float zmin = z[first == s_max ? 0 : first];
     float tot = 0.f;
-    for (int s = lane; s < s_max; s += 64) {
-        const float a = sdf_at(s) / tr;
+    PSVO_FOR_S(s_max) {
+        const float a = P(j, s) / tr;
         float w = sigm(a) * sigm(-a);
-        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        const bool keep = (Z(j, s) < zmin + tr) && (s < ns);
         tot += keep ? w : 0.0f;
     }
     tot = wsum(tot) + 1e-8f;
-    auto weight_at = [&](int s) {  // normalised weight W_s (0 outside the kept set)
-        const float a = sdf_at(s) / tr;
+    auto weight_at = [&](int j, int s) {  // normalised weight W_s (0 outside the kept set)
+        const float a = P(j, s) / tr;
         const float w = sigm(a) * sigm(-a);
-        const bool keep = (z[s] < zmin + tr) && (s < ns);
+        const bool keep = (Z(j, s) < zmin + tr) && (s < ns);
         return (keep ? w : 0.0f) / tot;
     };
     float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f;
-    for (int s = lane; s < s_max; s += 64) {
-        const float w = weight_at(s);
+    PSVO_FOR_S(s_max) {
+        const float w = weight_at(j, s);
         if (s < ns) {
-            const float *c = rgb_s + (int64_t)(off + s) * 3;
-            cr += w * c[0];
-            cg += w * c[1];
-            cb += w * c[2];
+            cr += w * C(j, s, 0);
+            cg += w * C(j, s, 1);
+            cb += w * C(j, s, 2);
         }
-        dd += w * z[s];
+        dd += w * Z(j, s);
     }
     cr = wsum(cr);
     cg = wsum(cg);
@@ -263,8 +297,8 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const float d = gt_depth[orig];
     const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
     float qfs = 0.f, qsdf = 0.f;
-    for (int s = lane; s < s_max; s += 64) {
-        const CritTerms t = crit_terms(z[s], sdf_at(s), d, tr, max_depth);
+    PSVO_FOR_S(s_max) {
+        const CritTerms t = crit_terms(Z(j, s), P(j, s), d, tr, max_depth);
         qfs = crit_sq_add(qfs, t.xfs);
         qsdf = crit_sq_add(qsdf, t.ysdf);
     }
@@ -295,24 +329,26 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     }
     // ---- compositing backward (k_composite_bwd, g_weights = 0)
     float dot = 0.f;
-    for (int s = lane; s < s_max; s += 64) {
-        const float gw = comp_gw(gdp, z[s], 0.f, s < ns ? rgb_s + (int64_t)(off + s) * 3 : nullptr, gcol[0], gcol[1],
-                                 gcol[2]);
-        dot = fmaf(gw, weight_at(s), dot);
+    PSVO_FOR_S(s_max) {
+        const bool v = s < ns;
+        const float gw = comp_gw3(gdp, Z(j, s), 0.f, v, v ? C(j, s, 0) : 0.f, v ? C(j, s, 1) : 0.f,
+                                  v ? C(j, s, 2) : 0.f, gcol[0], gcol[1], gcol[2]);
+        dot = fmaf(gw, weight_at(j, s), dot);
     }
     dot = wsum(dot);
-    for (int s = lane; s < ns; s += 64) {
-        const float *c = rgb_s + (int64_t)(off + s) * 3;
-        const float W = weight_at(s);
-        const float gw = comp_gw(gdp, z[s], 0.f, c, gcol[0], gcol[1], gcol[2]);
-        const float p = sdf_s[off + s];
-        const float gsdf = crit_grad(cfs, csdf, crit_terms(z[s], p, d, tr, max_depth));  // k_crit_bwd's term
-        g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, z[s] < zmin + tr, p, tr, gsdf);
+    PSVO_FOR_S(ns) {
+        const float W = weight_at(j, s);
+        const float zs = Z(j, s);
+        const float gw = comp_gw3(gdp, zs, 0.f, true, C(j, s, 0), C(j, s, 1), C(j, s, 2), gcol[0], gcol[1], gcol[2]);
+        const float p = P(j, s);
+        const float gsdf = crit_grad(cfs, csdf, crit_terms(zs, p, d, tr, max_depth));  // k_crit_bwd's term
+        g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, zs < zmin + tr, p, tr, gsdf);
         float *gc = g_rgb_s + (int64_t)(off + s) * 3;
         gc[0] = W * gcol[0];
         gc[1] = W * gcol[1];
         gc[2] = W * gcol[2];
     }
+#undef PSVO_FOR_S
 }
 
 }  // namespace
@@ -353,8 +389,10 @@ extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float
                      workspace && color && depth && grad_sdf_s && grad_rgb_s,
                  "composite_loss: null pointer");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_composite_loss, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
-                       truncation, max_depth, offsets, ray_ns, z_vals, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
-                       workspace, color, depth, grad_sdf_s, grad_rgb_s);
+    // samples cached in registers up to 64·4 per ray (room0: S_max ≈ 100–200)
+    auto kern = s_max <= 128 ? k_composite_loss<2> : s_max <= 256 ? k_composite_loss<4> : k_composite_loss<0>;
+    hipLaunchKernelGGL(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
+                       max_depth, offsets, ray_ns, z_vals, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace,
+                       color, depth, grad_sdf_s, grad_rgb_s);
     return check_launch("composite_loss");
 }

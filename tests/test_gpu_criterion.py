@@ -149,12 +149,13 @@ def test_fused_criterion_deterministic():
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_composite_loss_matches_kernel_chain(seed):
+@pytest.mark.parametrize("seed,s_max", [(0, 77), (1, 77), (2, 77), (3, 128), (4, 200), (5, 300)])
+def test_composite_loss_matches_kernel_chain(seed, s_max):
     """psvo_composite_loss (+ psvo_criterion_coef / _reduce) == composite_fwd →
-    criterion_sums → finalize → criterion_bwd → composite_bwd, bit for bit."""
+    criterion_sums → finalize → criterion_bwd → composite_bwd, bit for bit —
+    for each of its register-cached (S_max ≤ 128, ≤ 256) and memory variants."""
     from psvo import _lib as L
-    c = _case(seed)
+    c = _case(seed, s_max=s_max)
     r_hit, s_max = c["z"].shape
     g = torch.Generator().manual_seed(100 + seed)
     ns = (c["z"] < 10.0).sum(1).to(torch.int32)
