@@ -156,6 +156,17 @@ int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const 
                     const int *vertex_idx, const float *emb, const float *grad_feat, float *grad_emb, float *grad_o,
                     float *grad_d);
 
+/* psvo_interp_bwd with each ray's samples split into 64-sample work units
+ * (one wave each), so the launch is not serialised behind the longest rays;
+ * the per-unit d_o / d_d partials (workspace f32[psvo_interp_bwd_workspace_
+ * floats(r_hit, s_max)]) are summed per ray in unit order (deterministic).
+ * Same embedding gradient; d_o / d_d equal up to fp32 summation order. */
+int64_t psvo_interp_bwd_workspace_floats(int64_t r_hit, int s_max);
+int psvo_interp_bwd_chunked(void *stream, int64_t r_hit, int s_max, int d, float voxel_size, const int *offsets,
+                            const int *ray_index, const int *leaf, const float *t, const float *rays_o,
+                            const float *rays_d, const float *centres, const int *vertex_idx, const float *emb,
+                            const float *grad_feat, float *grad_emb, float *grad_o, float *grad_d, float *workspace);
+
 /* SDF-to-weight compositing (render_helpers.py:504-556) per hit ray.
  * sdf_s[M], rgb_s[M,3] per valid sample; outputs sdf/weights [R_hit,S_max]
  * (sdf padded with 1), color [R_hit,3], depth [R_hit]. */

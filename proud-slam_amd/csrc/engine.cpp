@@ -28,7 +28,7 @@ enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankR
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
-    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kSlots
+    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kIbWs, kSlots
 };
 
 struct Arena {
@@ -603,9 +603,11 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     e->grads_clean = false;
     e->clean_buf = grad_emb;
+    ENG_BUF(float, ib_ws, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
     mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
-    ENG_CALL(psvo_interp_bwd(eb, q.r_hit, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt, rays_o, rays_d,
-                             d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od, grad_od + R * 3));
+    ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt,
+                                     rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od,
+                                     grad_od + R * 3, ib_ws));
     mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");

@@ -82,6 +82,8 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+constexpr int kInterpChunk = 64;  // samples per work unit of the chunked backward (4 passes)
+
 struct BwdPass {  // per-wave LDS: one 16-sample pass, slot-minor so a lane reads 4 slots per ds_read_b128
     float w[8][16];    // trilinear weights [corner][slot]
     float g[16][16];   // grad_feat [dim][slot]
@@ -108,15 +110,23 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
                                                     const float4 *__restrict__ emb,
                                                     const float4 *__restrict__ grad_feat,
                                                     float *__restrict__ grad_emb, float *__restrict__ grad_o,
-                                                    float *__restrict__ grad_d) {
+                                                    float *__restrict__ grad_d, int chunk, int c_max,
+                                                    float *__restrict__ part) {
     __shared__ BwdPass pass_all[4];
     BwdPass &B = pass_all[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // unit = one ray (chunk == 0) or chunk c of ray r (chunk samples each, c < c_max):
+    // a long ray's samples spread over several waves instead of serialising
+    // the launch behind its passes; partial d_o / d_d go to part[unit]
+    const int64_t u = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t r = chunk ? u / c_max : u;
     if (r >= r_hit) return;
-    // wave-uniform (one wave per ray): scalar registers for the run loop
-    const int beg = __builtin_amdgcn_readfirstlane(offsets[r]);
-    const int end = __builtin_amdgcn_readfirstlane(offsets[r + 1]);
+    // wave-uniform: scalar registers for the run loop
+    const int rbeg = __builtin_amdgcn_readfirstlane(offsets[r]);
+    const int rend = __builtin_amdgcn_readfirstlane(offsets[r + 1]);
+    const int cidx = chunk ? (int)(u - r * c_max) : 0;
+    const int beg = chunk ? min(rend, rbeg + cidx * chunk) : rbeg;
+    const int end = chunk ? min(rend, beg + chunk) : rend;
     const int64_t ro_row = ray_index ? ray_index[r] : r;  // row of rays_o / rays_d / grad_o / grad_d
     const int q = lane & 3;
     const int sub = lane >> 2;
@@ -258,12 +268,35 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
         gd[a] = y;
     }
     if (lane == 0) {
+        if (chunk) {
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            grad_o[ro_row * 3 + a] = go[a];
-            grad_d[ro_row * 3 + a] = gd[a];
+            for (int a = 0; a < 3; ++a) {
+                part[u * 6 + a] = go[a];
+                part[u * 6 + 3 + a] = gd[a];
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                grad_o[ro_row * 3 + a] = go[a];
+                grad_d[ro_row * 3 + a] = gd[a];
+            }
         }
     }
+}
+
+// d_o / d_d of each ray = its chunks' partials summed in chunk order
+__global__ __launch_bounds__(256) void k_interp_bwd_rays(int64_t r_hit, int c_max, const int *__restrict__ ray_index,
+                                                         const float *__restrict__ part, float *__restrict__ grad_o,
+                                                         float *__restrict__ grad_d) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= r_hit * 6) return;
+    const int64_t r = e / 6;
+    const int k = (int)(e - r * 6);
+    float v = 0.f;
+    for (int c = 0; c < c_max; ++c) v += part[(r * c_max + c) * 6 + k];
+    const int64_t row = ray_index ? ray_index[r] : r;
+    if (k < 3) grad_o[row * 3 + k] = v;
+    else grad_d[row * 3 + k - 3] = v;
 }
 
 }  // namespace
@@ -296,11 +329,43 @@ extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_s
         hipLaunchKernelGGL(k_interp_bwd<true>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
-                           grad_emb, grad_o, grad_d);
+                           grad_emb, grad_o, grad_d, 0, 1, nullptr);
     else
         hipLaunchKernelGGL(k_interp_bwd<false>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
-                           nullptr, grad_o, grad_d);
+                           nullptr, grad_o, grad_d, 0, 1, nullptr);
     return check_launch("interp_bwd");
+}
+
+extern "C" int64_t psvo_interp_bwd_workspace_floats(int64_t r_hit, int s_max) {
+    return r_hit * ((s_max + kInterpChunk - 1) / kInterpChunk) * 6;
+}
+
+extern "C" int psvo_interp_bwd_chunked(void *stream, int64_t r_hit, int s_max, int d, float voxel_size,
+                                       const int *offsets, const int *ray_index, const int *leaf, const float *t,
+                                       const float *rays_o, const float *rays_d, const float *centres,
+                                       const int *vertex_idx, const float *emb, const float *grad_feat,
+                                       float *grad_emb, float *grad_o, float *grad_d, float *workspace) {
+    PSVO_REQUIRE(d == 16, "interp_bwd: embedding dim %d unsupported (16 only)", d);
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && voxel_size > 0.f, "interp_bwd: bad sizes");
+    PSVO_REQUIRE(grad_o != nullptr && grad_d != nullptr && workspace != nullptr,
+                 "interp_bwd: grad_o / grad_d / workspace required");
+    if (r_hit == 0) return PSVO_OK;
+    const int c_max = (s_max + kInterpChunk - 1) / kInterpChunk;
+    const int64_t units = r_hit * c_max;
+    hipStream_t st = as_stream(stream);
+    if (grad_emb)
+        hipLaunchKernelGGL(k_interp_bwd<true>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+                           ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
+                           reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
+                           grad_emb, grad_o, grad_d, kInterpChunk, c_max, workspace);
+    else
+        hipLaunchKernelGGL(k_interp_bwd<false>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+                           ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
+                           reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
+                           nullptr, grad_o, grad_d, kInterpChunk, c_max, workspace);
+    hipLaunchKernelGGL(k_interp_bwd_rays, dim3(div_up(r_hit * 6, 256)), dim3(256), 0, st, r_hit, c_max, ray_index,
+                       workspace, grad_o, grad_d);
+    return check_launch("interp_bwd_chunked");
 }

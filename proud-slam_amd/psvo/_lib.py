@@ -35,6 +35,8 @@ _SIGNATURES = {
     "psvo_sample_points": (_i32, [_vp, _i64, _i32, _i32] + [_vp] * 9),
     "psvo_interp_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 9),
     "psvo_interp_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
+    "psvo_interp_bwd_workspace_floats": (_i64, [_i64, _i32]),
+    "psvo_interp_bwd_chunked": (_i32, [_vp, _i64, _i32, _i32, _f32] + [_vp] * 13),
     "psvo_composite_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 10),
     "psvo_composite_bwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 12),
     "psvo_composite_loss": (_i32, [_vp, _i64, _i32, _f32, _f32] + [_vp] * 14),
