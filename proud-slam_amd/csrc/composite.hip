@@ -389,8 +389,11 @@ extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float
                      workspace && color && depth && grad_sdf_s && grad_rgb_s,
                  "composite_loss: null pointer");
     if (r_hit == 0) return PSVO_OK;
-    // samples cached in registers up to 64·4 per ray (room0: S_max ≈ 100–200)
-    auto kern = s_max <= 128 ? k_composite_loss<2> : s_max <= 256 ? k_composite_loss<4> : k_composite_loss<0>;
+    // samples cached in registers up to 64·8 per ray (room0 bench batches: S_max ≈ 200–300)
+    auto kern = s_max <= 128   ? k_composite_loss<2>
+                : s_max <= 256 ? k_composite_loss<4>
+                : s_max <= 512 ? k_composite_loss<8>
+                               : k_composite_loss<0>;
     hipLaunchKernelGGL(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
                        max_depth, offsets, ray_ns, z_vals, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace,
                        color, depth, grad_sdf_s, grad_rgb_s);

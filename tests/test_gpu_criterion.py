@@ -149,7 +149,7 @@ def test_fused_criterion_deterministic():
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("seed,s_max", [(0, 77), (1, 77), (2, 77), (3, 128), (4, 200), (5, 300)])
+@pytest.mark.parametrize("seed,s_max", [(0, 77), (1, 77), (2, 77), (3, 128), (4, 200), (5, 300), (6, 600)])
 def test_composite_loss_matches_kernel_chain(seed, s_max):
     """psvo_composite_loss (+ psvo_criterion_coef / _reduce) == composite_fwd →
     criterion_sums → finalize → criterion_bwd → composite_bwd, bit for bit —
