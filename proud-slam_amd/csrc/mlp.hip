@@ -208,13 +208,16 @@ __device__ __forceinline__ void apply_mask(f32x16 (&v)[kNB], uint64_t m) {
 }
 
 // Σ_k w[k] · v[k][sample] over this lane's 64 features (other half via partner lane)
+// (roundings spelled out — an fmaf chain and one add — so every kernel that
+// uses it, e.g. the sdf-only and the training forward, gives the same bits
+// whatever the compiler would contract around it)
 __device__ __forceinline__ float row_dot(const float *w, const f32x16 (&v)[kNB], int h) {
     float s = 0.f;
 #pragma unroll
     for (int b = 0; b < kNB; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s += w[32 * b + phi(r, h)] * v[b][r];
-    return s + __shfl_xor(s, 32, 64);
+        for (int r = 0; r < 16; ++r) s = fmaf(w[32 * b + phi(r, h)], v[b][r], s);
+    return __fadd_rn(s, __shfl_xor(s, 32, 64));
 }
 
 // Store an activation held in accumulator form as rows of a row-major
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float 
     raw_barrier();
     copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
     raw_barrier();
-    const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
+    const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
     init_bias(a, lds + kOffB3 + 1, h);
     gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
     if (save) cfs.store(act + 2 * tstride, tbytes, a);
@@ -1164,21 +1167,28 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
                                                             float *__restrict__ act, uint64_t *__restrict__ masks) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const bool save = act != nullptr;         // CF activations (weight gradients)
     const bool save_mask = masks != nullptr;  // ReLU masks (δ chain)
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF 32-sample tiles
     const int64_t tstride = n_tiles * 32 * 128;
     const int64_t tbytes = tstride * 4;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    // Balanced split: workgroup b owns the 32-sample units [u0, u1), so every
+    // wave slot gets floor or ceil of n_units / (8 · grid) and the last
+    // iteration is a partial one (waves past u1 skip their MFMAs but keep the
+    // staging and barriers) instead of a whole extra 256-sample round on a
+    // few CUs while the rest of the chip waits at the kernel boundary.
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int n_it = (int)((u1 - u0 + kF2Waves - 1) / kF2Waves);
     auto buf = [&](int i) { return lds + ((i & 1) ? kF2Buf1 : kF2Buf0); };
     int seq = 0;  // staged layers so far: W(seq) sits in buf(seq)
-    int64_t t = blockIdx.x;
     float xn[8];
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_x(feat, s, s < m, h, xn);
+        const int64_t u = u0 + wave;
+        const int64_t s = u * kTileS + (lane & 31);
+        load_x(feat, s, u < u1 && s < m, h, xn);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
@@ -1187,43 +1197,60 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     raw_barrier();
     [[maybe_unused]] constexpr int kStampK = 0;
     PSVO_STAMP_DECL;
-    for (; t < n_wg_tiles; t += gridDim.x) {
+    for (int it = 0; it < n_it; ++it) {
         PSVO_STAMP(0);
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        const bool valid = s < m;
-        const bool more = t + gridDim.x < n_wg_tiles;
+        const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
+        const bool active = u < u1;  // wave-uniform
+        const int64_t s = u * kTileS + (lane & 31);
+        const bool valid = active && s < m;
+        const bool more = it + 1 < n_it;
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = xn[i];
-        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
+        const CfStore cfs(u, lane, n_tiles);
         f32x16 a[kNB], bacc[kNB];
+        uint64_t m1 = 0, m2 = 0;
+        float sdf = 0.f;
         // h1 = relu(W1 x + b1): resident W1
-        init_bias(a, lds + kOffB1, h);
-        gemm_x(lds + kF2W1, x, a, lane);
-        const uint64_t m1 = relu(a);
+        if (active) {
+            init_bias(a, lds + kOffB1, h);
+            gemm_x(lds + kF2W1, x, a, lane);
+            m1 = relu(a);
+        }
         // h2 = relu(W2 h1 + b2)
         wait_vm(0);
         raw_barrier();
         stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
-        init_bias(bacc, lds + kOffB2, h);
-        gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
+        if (active) {
+            init_bias(bacc, lds + kOffB2, h);
+            gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
+            m2 = relu(bacc);
+        }
         ++seq;
-        const uint64_t m2 = relu(bacc);
         // [sdf | f] = W3 h2 + b3
         wait_vm(0);
         raw_barrier();
         stage8(buf(seq + 1), img + kImgF4, 18432, wave, lane);
-        const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
-        init_bias(a, lds + kOffB3 + 1, h);
-        gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane, CfQueue(cfs, act + tstride, tbytes, save, bacc));  // + h2
+        if (active) {
+            sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
+            init_bias(a, lds + kOffB3 + 1, h);
+            gemm_acc<kNB, kNB>(buf(seq), bacc, a, lane, CfQueue(cfs, act + tstride, tbytes, save, bacc));  // + h2
+        }
         ++seq;
         // c1 = relu(W4 [f; x] + b4); the next tile's W2 and x start loading
         wait_vm(0);
         raw_barrier();
         if (more) {
             stage8(buf(seq + 1), img + kImgF2, 16384, wave, lane);
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
-            load_x(feat, sn, sn < m, h, xn);
+            const int64_t un = u + kF2Waves;
+            const int64_t sn = un * kTileS + (lane & 31);
+            load_x(feat, sn, un < u1 && sn < m, h, xn);
+        }
+        if (!active) {
+            ++seq;
+            PSVO_STAMP(8);
+            PSVO_STAMP_FLUSH(0);
+            continue;
         }
         init_bias(bacc, lds + kOffB4, h);
         uint32_t half4[2] = {0u, 0u};
@@ -1310,7 +1337,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m, const flo
         init_bias(bacc, lds + kOffB2, h);
         gemm_acc<kNB, kNB>(w2, a, bacc, lane);
         (void)relu(bacc);
-        const float sdf = lds[kOffB3] + row_dot(lds + kOffW3r0, bacc, h);
+        const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
         if (valid && h == 0) sdf_out[s] = sdf;
     }
     wait_vm(0);
@@ -1353,28 +1380,33 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *bufA = lds + kB2BufA, *bufB = lds + kB2BufB;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
     const int64_t tbytes = n_tiles * 32 * 128 * 4;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
-    int64_t t = blockIdx.x;
+    // balanced split of the 32-sample units, as k_mlp_fwd2
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int n_it = (int)((u1 - u0 + kF2Waves - 1) / kF2Waves);
+    [[maybe_unused]] constexpr int kStampK = 1;
     BwdIn nin;
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, s < m, h, nin);
+        const int64_t u = u0 + wave;
+        const int64_t s = u * kTileS + (lane & 31);
+        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, u < u1 && s < m, h, nin);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(bufA, img + kImgB4, 20480, wave, lane);
     wait_vm(0);
     raw_barrier();
-    [[maybe_unused]] constexpr int kStampK = 1;
     PSVO_STAMP_DECL;
-    for (; t < n_wg_tiles; t += gridDim.x) {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        const bool valid = s < m;
-        const bool more = t + gridDim.x < n_wg_tiles;
-        const CfStore cfs(t * kF2Waves + wave, lane, n_tiles);
+    for (int it = 0; it < n_it; ++it) {
+        const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
+        const bool active = u < u1;  // wave-uniform
+        const int64_t s = u * kTileS + (lane & 31);
+        const bool valid = active && s < m;
+        const bool more = it + 1 < n_it;
+        const CfStore cfs(u, lane, n_tiles);
         const BwdIn in = nin;
         float d5[3];
 #pragma unroll
@@ -1393,64 +1425,73 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
         PSVO_STAMP(2);
         stage8(bufB, img + kImgB3, 16384, wave, lane);
         f32x16 a[kNB], bacc[kNB];
-#pragma unroll
-        for (int b = 0; b < kNB; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
-                const int k = 32 * b + phi(r, h);
-                const float v =
-                    lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
-                bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
-            }
-        f32x16 t5[5];
-        zero(t5);
-        gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1 stores
         float dxc[8];
+        if (active) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
+            for (int b = 0; b < kNB; ++b)
 #pragma unroll
-        for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
+                for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
+                    const int k = 32 * b + phi(r, h);
+                    const float v =
+                        lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
+                    bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
+                }
+            f32x16 t5[5];
+            zero(t5);
+            gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1
+#pragma unroll
+            for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
+#pragma unroll
+            for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
+        }
         // ---- W3ᵀ layer (bufB); W2ᵀ → bufA
         PSVO_STAMP(3);
         wait_vm(0);
         raw_barrier();
         PSVO_STAMP(4);
         stage8(bufA, img + kImgB2, 16384, wave, lane);
+        if (active) {
 #pragma unroll
-        for (int b = 0; b < kNB; ++b)
+            for (int b = 0; b < kNB; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
-        gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
-        apply_mask(bacc, m2);
+                for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
+            gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
+            apply_mask(bacc, m2);
+        }
         // ---- W2ᵀ layer (bufA); W1ᵀ → bufB
         PSVO_STAMP(5);
         wait_vm(0);
         raw_barrier();
         PSVO_STAMP(6);
         stage8(bufB, img + kImgB1, 4096, wave, lane);
-        zero(a);
-        gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2 stores
-        apply_mask(a, m1);
-        // ---- W1ᵀ layer (bufB); next tile's W4ᵀ → bufA and its inputs
+        if (active) {
+            zero(a);
+            gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2
+            apply_mask(a, m1);
+        }
+        // ---- W1ᵀ layer (bufB); next iteration's W4ᵀ → bufA and its inputs
         PSVO_STAMP(7);
         wait_vm(0);
         raw_barrier();
         PSVO_STAMP(8);
         if (more) {
             stage8(bufA, img + kImgB4, 20480, wave, lane);
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
-            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, sn < m, h, nin);
+            const int64_t un = u + kF2Waves;
+            const int64_t sn = un * kTileS + (lane & 31);
+            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, un < u1 && sn < m, h, nin);
         }
-        f32x16 t1[1];
-        zero(t1);
-        gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
-        if (valid) {
-            float *dst = o.dfeat + s * kIn;
+        if (active) {
+            f32x16 t1[1];
+            zero(t1);
+            gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
+            if (valid) {
+                float *dst = o.dfeat + s * kIn;
 #pragma unroll
-            for (int rg = 0; rg < 2; ++rg)
-                *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
-                    make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
-                                t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
+                for (int rg = 0; rg < 2; ++rg)
+                    *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
+                        make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
+                                    t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
+            }
         }
         PSVO_STAMP(9);
         PSVO_STAMP_FLUSH(1);
