@@ -311,14 +311,17 @@ def main():
         engine.set_timing(False)
     # the other path, for reference (not the headline number)
     other_steps = max(5, min(args.steps, 20))
-    if args.autograd:
-        el2 = run(step_engine, other_steps, 2)
-        other = {"path": "native engine (psvo_map_step)"}
+    if args.autograd and args.width != 128:
+        other = {"path": "native engine: not run (its fused decoder is width 128)"}
     else:
-        el2 = run(step_autograd, other_steps, 2)
-        other = {"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"}
-    other.update(value=args.frames * args.rays_per_frame * other_steps * world / el2,
-                 ms_per_step=1000.0 * el2 / other_steps)
+        if args.autograd:
+            el2 = run(step_engine, other_steps, 2)
+            other = {"path": "native engine (psvo_map_step)"}
+        else:
+            el2 = run(step_autograd, other_steps, 2)
+            other = {"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"}
+        other.update(value=args.frames * args.rays_per_frame * other_steps * world / el2,
+                     ms_per_step=1000.0 * el2 / other_steps)
     rays_per_step = args.frames * args.rays_per_frame
     total_rays = rays_per_step * args.steps * world
     value = total_rays / elapsed
