@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec render+backward, Replica room0, 64 samples/ray, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: aggregate L2 (8 x 4 MiB) ≈34.5 TB/s
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (v_mfma_f32_32x32x2_f32) dense peak
 
 
@@ -51,16 +52,32 @@ def parse():
     ap.add_argument("--autograd", action="store_true",
                     help="headline number from the drop-in autograd path instead of the native engine")
     ap.add_argument("--exact-global-loss", action="store_true",
-                    help="N>1: sharded == single-GPU on the global batch (global sampler layout, all-reduced "
-                         "criterion sums; runs the autograd path)")
+                    help="(kept for compatibility: N>1 always computes the union-batch loss)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
 
-def setup_dist():
+def launch_workers(args):
+    """`python bench.py --gpus N` (N > 1) without a torch.distributed launcher:
+    start N ranks under torch.distributed.run as a child process (this parent
+    never touches the GPU) and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         # RCCL over xGMI; PSVO_DIST_BACKEND=gloo rehearses the N>1 path with
         # several ranks sharing one GPU (the device index wraps around)
@@ -155,6 +172,16 @@ class KernelTimer:
         return float(np.mean([s.elapsed_time(e) for s, e in ev]))
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args, scene, tree, step_size, seconds):
     """Oracle (reference algorithm restated: C kernels + torch-CPU render /
     loss / autograd) on the host cores, bounded sample of the same workload."""
@@ -178,13 +205,17 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
     dt = time.time() - t0
     rays = n_it * ro.shape[1]
     return {"value": rays / dt, "unit": "rays/s", "cores": int(torch.get_num_threads()), "kind": "port",
+            "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count(),
+            "process_cpu_share": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
             "sample": f"{n_it} iterations x {ro.shape[1]} rays ({args.scene}, {args.frames}x{args.rays_per_frame}), "
                       f"oracle C kernels single-thread + torch-CPU render/loss/backward, {dt:.1f}s"}
 
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args))
+    world, rank, local = setup_dist(args)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     from psvo import _lib
@@ -209,17 +240,26 @@ def main():
 
     from psvo.dist import GlobalBatch, GlobalLossSums, GradBucket
     from psvo.engine import MappingEngine
-    # one flat RCCL all-reduce of all gradients per step; exact mode forms the
-    # loss of the union of the ranks' rays (global normalisers) and sums
-    bucket = GradBucket(params, op="sum" if args.exact_global_loss else "mean")
-    reducer = GlobalLossSums() if (args.exact_global_loss and world > 1) else None
-    gbatch = GlobalBatch() if (args.exact_global_loss and world > 1) else None
-    if gbatch is not None:
-        args.autograd = True  # the engine samples per rank; exactness runs the drop-in path
-    engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
-                           criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
-    from psvo.dist import EngineGradExchange
-    exchange = EngineGradExchange(engine)
+    # N > 1: both paths form the loss of the union of the ranks' rays (global
+    # sampler layout and normalisers) and sum the gradients with one flat
+    # all-reduce per step
+    bucket = GradBucket(params, op="sum")
+    reducer = GlobalLossSums() if world > 1 else None
+    gbatch = GlobalBatch() if world > 1 else None
+    if not args.autograd and args.width != 128:
+        # the fused decoder and the native engine are width 128: W=256
+        # (ScanNet / ARKit configs) runs the drop-in path, recorded in "path"
+        args.autograd = True
+    engine = exchange = None
+    if args.width == 128:
+        engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
+                               criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
+        from psvo.dist import EngineExchange, EngineGradExchange
+        if world > 1:
+            # the loss of the union of all ranks' rays: union-batch
+            # sampler layout and normalisers, gradients summed over ranks
+            engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
+        exchange = EngineGradExchange(engine, op="sum")
 
     def record_stats(m, r_hit, visits, s_max):
         stats["m"] += m
@@ -231,7 +271,7 @@ def main():
         """The drop-in path: render_rays + Criterion + backward + Adam steps."""
         ro, rd, rgb, depth = batches[i % len(batches)]
         out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True,
-                             seed=(7919 * i + 1) if gbatch is not None else None, batch=gbatch)
+                             seed=7919 * i + 1, batch=gbatch)
         loss, _ = criterion(out, (rgb, depth), reduce_sums=reducer)
         embed_optim.zero_grad()  # set_to_none, as optim.zero_grad() in render_helpers.py:668
         model_optim.zero_grad()
@@ -248,7 +288,8 @@ def main():
     eng_it = [0]  # engine iterations so far: the next batch is always the one already queued
 
     def eng_batch(it):
-        return batches[it % len(batches)], 1000003 * rank + it
+        # one seed for all ranks: the sampler noise is keyed by the union batch's logical row
+        return batches[it % len(batches)], 1000003 + it
 
     def step_engine(i, record=False):
         """The same iteration as one native call (psvo_map_step); the next
@@ -268,7 +309,7 @@ def main():
             engine.adam()
         if record:
             st = engine.last_stats
-            record_stats(st[4], st[1], st[5], st[3])
+            record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3])  # this rank's hit rays
         return loss
 
     def run(step_fn, steps, warmup, timed_hook=None):
@@ -297,6 +338,7 @@ def main():
     # the headline steps run without HIP-event markers (each costs a few µs of
     # GPU idle); the per-region breakdown comes from a separate marked run
     n_mark = max(5, min(args.steps, 20))
+    kt_overlap = None
     if args.autograd:
         elapsed = run(step_autograd, args.steps, args.warmup, lambda on: None)
         timer.enabled = True
@@ -305,14 +347,19 @@ def main():
         kt = {k: timer.mean_ms(k) for k in MappingEngine.REGIONS}
     else:
         elapsed = run(step_engine, args.steps, args.warmup, lambda on: None)
-        engine.set_timing(True)
+        engine.set_timing(True)      # regions serialised on one stream
         run(step_engine, n_mark, 0)
         kt = engine.timing()
+        engine.set_timing("overlap")  # the same regions as the headline steps run them
+        run(step_engine, n_mark, 0)
+        kt_overlap = engine.timing()
         engine.set_timing(False)
     # the other path, for reference (not the headline number)
     other_steps = max(5, min(args.steps, 20))
     if args.autograd and args.width != 128:
         other = {"path": "native engine: not run (its fused decoder is width 128)"}
+    elif world > 1:
+        other = {"path": "not run at N > 1 (the headline path only)"}
     else:
         if args.autograd:
             el2 = run(step_engine, other_steps, 2)
@@ -328,29 +375,29 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     # Rooflines.  Primary — the north star's "octree query+interp
-    # kernel", HBM-bound: algorithmic bytes per step = per ray 24 B + 48 B per
-    # AABB-tested node (V measured by the kernel) + per valid sample 12 B
-    # (sampler output) + 628 B (interp fwd) + 1,664 B (interp bwd), over the
-    # summed HIP-event time of its launches (intersect + stats + hit rank,
-    # sampler + scan, sample compaction, interp fwd, interp bwd).  Secondary —
-    # the decoder (dominant by time): fwd, δ chain and weight gradients are
-    # each 53,760 MAC/sample (W=128) = 3 x 107,520 FLOP/sample, MFMA-bound.
+    # kernel": algorithmic bytes per step = per ray 24 B + 48 B per AABB-tested
+    # node (V counted by the kernel) + per valid sample 12 B (sampler output)
+    # + 628 B (interp fwd) + 1,664 B (interp bwd), over the summed HIP-event
+    # time of its launches (intersect + stats + hit rank, sampler + scan,
+    # sample compaction, interp fwd, interp bwd).  Three fractions: the
+    # algorithmic bytes against HBM (the contract's `frac`; > 1 would mean the
+    # gathers are served from L2, and the bound is then reported as L2), the
+    # same against the L2's ≈34.5 TB/s, and the PMC-counted HBM bytes
+    # (FETCH_SIZE x 2 + WRITE_SIZE, profiles/traffic.json) against HBM.  Times
+    # from the serialised marked run (`time_ms`) and as the headline steps
+    # overlap them (`time_ms_overlapped`).  Secondary — the decoder (dominant
+    # by time): fwd, δ chain and weight gradients are each W-dependent MACs per
+    # sample (3 x 2 x MACs FLOP/sample), MFMA-bound.
     m_avg = stats["m"] / args.steps
     r_avg = stats["r_hit"] / args.steps
     v_avg = stats["visits"] / args.steps
     rays_step = args.frames * args.rays_per_frame
-    bwd_ms, fwd_ms = kt["interp_bwd"], kt["interp_fwd"]
-    mlp_f_ms, mlp_b_ms = kt["mlp_fwd"], kt["mlp_bwd"]
-    q_parts = {k: kt[k] for k in ("intersect", "sample", "points", "interp_fwd", "interp_bwd")}
+    q_keys = ("intersect", "sample", "points", "interp_fwd", "interp_bwd")
+    q_parts = {k: kt[k] for k in q_keys}
     q_ms = sum(q_parts.values())
+    q_ms_ov = sum(kt_overlap[k] for k in q_keys) if kt_overlap else None
     bytes_query = rays_step * 24.0 + v_avg * 48.0 + m_avg * 12.0
     bytes_qi = bytes_query + m_avg * (628.0 + 1664.0)
-    qi_gbs = bytes_qi / (q_ms * 1e-3) / 1e9 if q_ms > 0 else None
-    mlp_ms = mlp_f_ms + mlp_b_ms
-    flops_mlp = 3 * 107520.0 * m_avg
-    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
-    bytes_bwd = 1664.0 * m_avg
-    achieved_bwd = bytes_bwd / (bwd_ms * 1e-3) / 1e9 if bwd_ms > 0 else None
     traffic = {}
     if os.path.exists(args.traffic_json):
         try:
@@ -359,6 +406,42 @@ def main():
             traffic = {}
         if traffic.get("scene", "room0") != args.scene:  # PMC passes of another scene: not this workload's bytes
             traffic = {}
+
+    def bw_roof(kernel, alg_bytes, ms, ms_ov, counter_bytes, extra=None):
+        gbs = alg_bytes / (ms * 1e-3) / 1e9 if ms and ms > 0 else None
+        frac_hbm = gbs / HBM_PEAK_GBS if gbs else None
+        bound, peak = ("hbm", HBM_PEAK_GBS) if (frac_hbm is None or frac_hbm <= 1.0) else ("l2", L2_PEAK_GBS)
+        r = {"kernel": kernel, "bound": bound, "achieved": gbs, "peak": peak, "unit": "GB/s",
+             "frac": gbs / peak if gbs else None, "traffic": counter_bytes,
+             "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": ms, "time_ms_overlapped": ms_ov,
+             "frac_hbm_algorithmic": frac_hbm,
+             "frac_l2_algorithmic": gbs / L2_PEAK_GBS if gbs else None,
+             "frac_hbm_counters": (counter_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if (counter_bytes and ms) else None,
+             "frac_hbm_algorithmic_overlapped": (alg_bytes / (ms_ov * 1e-3) / 1e9 / HBM_PEAK_GBS)
+             if ms_ov and ms_ov > 0 else None}
+        if extra:
+            r.update(extra)
+        for k, v in r.items():
+            if k.startswith("frac") and v is not None and k != "frac_hbm_algorithmic" and \
+                    k != "frac_hbm_algorithmic_overlapped":
+                assert v <= 1.0, (kernel, k, v)
+        return r
+
+    roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, "
+                      "k_sample_points, k_interp_fwd, k_interp_bwd)", bytes_qi, q_ms, q_ms_ov,
+                      traffic.get("query_interp_bytes_per_step"),
+                      {"parts_ms": q_parts, "parts_ms_overlapped": {k: kt_overlap[k] for k in q_keys}
+                       if kt_overlap else None, "visits_per_ray": v_avg / max(rays_step, 1),
+                       "samples_per_hit_ray": m_avg / max(r_avg, 1)})
+    roof_ib = bw_roof("k_interp_bwd", 1664.0 * m_avg, kt["interp_bwd"],
+                      kt_overlap["interp_bwd"] if kt_overlap else None,
+                      traffic.get("interp_bwd_bytes_per_launch"))
+    mlp_f_ms, mlp_b_ms = kt["mlp_fwd"], kt["mlp_bwd"]
+    mlp_ms = mlp_f_ms + mlp_b_ms
+    w = args.width
+    macs = 16 * w + w * w + w * 129 + 144 * w + w * 3  # nrgbd.py:80-146, depth 2, sdf_dim 128, in_dim 16
+    flops_mlp = 3 * 2.0 * macs * m_avg
+    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
     result = {
         "metric": METRIC,
         "value": value,
@@ -377,28 +460,18 @@ def main():
                                f"{m_avg / max(r_avg, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
                    "rays_per_step_per_gpu": rays_per_step, "samples_per_step": m_avg, "hit_rays_per_step": r_avg,
                    "aabb_tests_per_step": v_avg, "parallelism": f"dp{world} (ray-sharded, RCCL grad all-reduce)"},
-        "roofline": {"kernel": "octree query+interp (k_intersect_sorted+k_ray_stats+k_hit_rank, k_sample_fused+"
-                               "k_scan_samples, k_sample_points, k_interp_fwd, k_interp_bwd)",
-                     "bound": "hbm", "achieved": qi_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (qi_gbs / HBM_PEAK_GBS) if qi_gbs else None,
-                     "traffic": traffic.get("query_interp_bytes_per_step"),
-                     "algorithmic_bytes_per_launch": bytes_qi, "avg_launch_ms": q_ms,
-                     "parts_ms": q_parts, "visits_per_ray": v_avg / max(rays_step, 1),
-                     "samples_per_hit_ray": m_avg / max(r_avg, 1)},
-        "roofline_mfma": {"kernel": "NRGBD decoder MLP fwd+bwd (k_mlp_prep/fwd2/bwd2/dw/dw_reduce)",
+        "roofline": roof_qi,
+        "roofline_mfma": {"kernel": f"NRGBD decoder MLP W={w} fwd+bwd (fwd, δ chain, weight gradients)",
                           "bound": "mfma", "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
                           "traffic": traffic.get("mlp_bytes_per_step"),
                           "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
-        "roofline_interp_bwd": {"kernel": "k_interp_bwd", "bound": "hbm", "achieved": achieved_bwd,
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": (achieved_bwd / HBM_PEAK_GBS) if achieved_bwd else None,
-                                "traffic": traffic.get("interp_bwd_bytes_per_launch"),
-                                "algorithmic_bytes_per_launch": bytes_bwd, "avg_launch_ms": bwd_ms},
+        "roofline_interp_bwd": roof_ib,
         "path": "drop-in autograd path" if args.autograd else "native engine (psvo_map_step: one call per iteration)",
         "other_path": other,
         "kernels_ms": kt,
+        "kernels_ms_overlapped": kt_overlap,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, scene, tree, step_size, args.cpu_baseline_seconds)

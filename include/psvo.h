@@ -85,7 +85,15 @@ enum {
     PSVO_STAT_M = 4,         /* total valid samples */
     PSVO_STAT_VISITS = 5,    /* AABB tests performed (traffic accounting) */
     PSVO_STAT_SPILLS = 6,    /* rays that fell back to the serial DFS (diagnostic) */
-    PSVO_STAT_WORDS = 8
+    PSVO_STAT_FLAGS = 7,     /* bit 0: DFS stack overflow; bit 1: sampler exceeded max_steps */
+    /* data-parallel engine (psvo_engine_set_exchange): words 0..3 then describe
+     * the GLOBAL batch (P, R_hit, max ceil, S_max over all ranks) and these the
+     * rank's own rows */
+    PSVO_STAT_ROW_BEGIN = 8,     /* first global logical hit row of this rank */
+    PSVO_STAT_R_HIT_LOCAL = 9,   /* this rank's hit rays */
+    PSVO_STAT_NEXT_COL0 = 10,    /* first voxel id of the global row after this rank's last */
+    PSVO_STAT_S_MAX_LOCAL = 11,  /* this rank's max valid samples per ray */
+    PSVO_STAT_WORDS = 16
 };
 
 /* DFS + stable sort by t_in + max_distance trim for R rays.  hit_* are
@@ -389,11 +397,35 @@ int psvo_rows_scatter_add(void *stream, int64_t n_list, int width, const int *id
 
 psvo_engine *psvo_engine_new(void);
 void psvo_engine_free(psvo_engine *e);
+/* Data-parallel mapping: one process per GPU, each rank steps
+ * its own shard of the ray batch and the engine computes the loss of the
+ * UNION batch — the single-GPU result on all ranks' rays concatenated in rank
+ * order.  The engine calls `fn` for each collective, on the stream the
+ * operands were produced on (the collective must be ordered on it):
+ *   PSVO_XCH_GATHER_I32: xi32[out + r·count + k] = rank r's xi32[in + k]
+ *   PSVO_XCH_SUM_I32 / _F64: in-place sum of xi32 / xf64 [in, in + count)
+ * PSVO_XCH_QUERY is or-ed into ops issued by psvo_map_query (they may run
+ * concurrently with the previous step's: use a separate communicator).
+ * xi32: psvo_engine_exchange_words(world, max_rays_global) device int32;
+ * xf64: 16 device doubles.  Returns non-zero on failure.  Exchanged per step:
+ * 8 + 1 words per rank (all-gathered), a [200, 50] int32 table of the
+ * sampler's slot-0 voxel ids, 16 doubles; then the caller sums grad_flat
+ * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam. */
+enum { PSVO_XCH_GATHER_I32 = 1, PSVO_XCH_SUM_I32 = 2, PSVO_XCH_SUM_F64 = 3, PSVO_XCH_QUERY = 0x100 };
+typedef int (*psvo_exchange_fn)(void *user, int op, int64_t in_off, int64_t out_off, int64_t count, void *stream);
+int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global);
+int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_rays_global, psvo_exchange_fn fn,
+                             void *user, int *xi32, double *xf64);
+
+/* Queries psvo_map_query queued and no step has consumed yet (0..2).  A step
+ * that fails after picking up its queued query still consumes it. */
+int psvo_engine_queued(psvo_engine *e);
 
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
        PSVO_TIME_INTERSECT = 4, PSVO_TIME_SAMPLE = 5, PSVO_TIME_POINTS = 6, PSVO_TIME_REGIONS = 7 };
-int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators */
+int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators; on = 1: regions serialised
+                                                           on one stream, 2: as run (side streams overlap) */
 int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
 
 /* One iteration on n_rays rays (rays_o/rays_d f32[R,3], gt_rgb f32[R,3],

@@ -213,12 +213,25 @@ def inverse_cdf_sampling(pts_idx, min_depth, max_depth, probs, steps, fixed_step
     return s_idx[:, :max_len], s_dep[:, :max_len], s_dis[:, :max_len], noise
 
 
-def ray_sample(intersection, step_size, noise=None, deterministic=False, generator=None):
-    """voxel_helpers.py:637-663."""
+def sequential_row_sums(dists):
+    """Σ over the last dim, accumulated left to right in fp32 (the depth-sorted
+    hit order).  torch leaves a reduction's order unspecified (CPU: vectorised
+    cascade; CUDA: tree); this is the order the HIP kernel fixes."""
+    d = dists.detach().numpy()
+    acc = np.zeros(d.shape[:-1], np.float32)
+    for j in range(d.shape[-1]):
+        acc = (acc + d[..., j]).astype(np.float32)
+    return torch.from_numpy(acc)
+
+
+def ray_sample(intersection, step_size, noise=None, deterministic=False, generator=None, sum_order="torch"):
+    """voxel_helpers.py:637-663.  sum_order "torch": dists.sum(-1) as the
+    reference writes it (torch-CPU order); "sequential": sequential_row_sums."""
     idx = intersection["intersected_voxel_idx"]
     dists = (intersection["max_depth"] - intersection["min_depth"]).masked_fill(idx.eq(-1), 0)
-    probs = dists / dists.sum(dim=-1, keepdim=True)
-    steps = dists.sum(-1) / step_size
+    dsum = dists.sum(dim=-1) if sum_order == "torch" else sequential_row_sums(dists)
+    probs = dists / dsum.unsqueeze(-1)
+    steps = dsum / step_size
     s_idx, s_dep, s_dis, noise = inverse_cdf_sampling(idx, intersection["min_depth"], intersection["max_depth"],
                                                       probs, steps, -1.0, noise, deterministic, generator)
     s_dis = s_dis.clamp(min=0.0)
@@ -282,7 +295,7 @@ def decoder_forward(params, x):
 # render_rays — render_helpers.py:351-556
 # --------------------------------------------------------------------------
 def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_size, truncation, max_distance,
-                noise=None, deterministic=False, generator=None):
+                noise=None, deterministic=False, generator=None, sum_order="torch"):
     intersection, hits = ray_intersect_vox(rays_o, rays_d, map_states["voxel_center_xyz"],
                                            map_states["voxel_structure"], voxel_size, max_distance)
     assert hits.sum() > 0
@@ -290,7 +303,7 @@ def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_siz
     intersection = {k: v[ray_mask].reshape(-1, v.size(-1)) for k, v in intersection.items()}
     ro = rays_o[ray_mask].reshape(-1, 3)
     rd = rays_d[ray_mask].reshape(-1, 3)
-    samples, noise = ray_sample(intersection, step_size, noise, deterministic, generator)
+    samples, noise = ray_sample(intersection, step_size, noise, deterministic, generator, sum_order)
     depth = samples["sampled_point_depth"]
     sidx = samples["sampled_point_voxel_idx"].long()
     mask = sidx.ne(-1)
@@ -402,7 +415,8 @@ SCANNET_CRITERIA = {"rgb_weight": 1.0, "depth_weight": 1.0, "sdf_weight": 5000.0
 
 def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_params, step_size, voxel_size,
                         truncation=0.1, max_distance=10.0, criteria=REPLICA_CRITERIA, noise=None,
-                        deterministic=False, generator=None, rays_require_grad=True):
+                        deterministic=False, generator=None, rays_require_grad=True, sum_order="torch",
+                        max_depth=None):
     """One bundle-adjust iteration's differentiable part (render_helpers.py:648-671).
 
     Returns outputs, loss and grads for embeddings, decoder params, rays_o, rays_d."""
@@ -413,8 +427,9 @@ def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_pa
     ms = dict(map_states)
     ms["voxel_vertex_emb"] = emb
     out = render_rays(ro, rd, ms, params, step_size, voxel_size, truncation, max_distance, noise, deterministic,
-                      generator)
-    loss, parts = criterion(out, rgb_gt, depth_gt, criteria, truncation, max_distance)
+                      generator, sum_order)
+    loss, parts = criterion(out, rgb_gt, depth_gt, criteria, truncation,
+                            max_distance if max_depth is None else max_depth)  # data_specs max_depth
     loss.backward()
     grads = {"embeddings": emb.grad, "rays_o": ro.grad, "rays_d": rd.grad}
     for k, v in params.items():

@@ -352,6 +352,25 @@ extern "C" int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float
     return check_launch("criterion_coef");
 }
 
+namespace psvo {
+// psvo_criterion_coef in two halves, so that a data-parallel engine can
+// all-reduce the count sums (union-batch normalisers) between them
+int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
+                     const float *gt_depth, const float *z_vals, float *workspace, double *sums) {
+    if (r_hit > 0)
+        hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
+                           max_depth, rank_ray, gt_depth, z_vals, workspace);
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    return check_launch("criterion_counts");
+}
+int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
+                             float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef) {
+    hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)n_hit, (double)n_cols, rgb_w, depth_w,
+                       fs_w, sdf_w, truncation, flags, coef);
+    return check_launch("criterion_coef");
+}
+}  // namespace psvo
+
 extern "C" int psvo_criterion_reduce(void *stream, int64_t r_hit, const float *workspace, double *sums) {
     PSVO_REQUIRE(r_hit > 0 && workspace && sums, "criterion_reduce: bad arguments");
     hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, as_stream(stream), r_hit, workspace, sums);

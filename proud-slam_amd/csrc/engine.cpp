@@ -60,13 +60,39 @@ struct QuerySet {
 // optional HIP-event timing of the roofline regions (PSVO_TIME_*)
 struct EngineTimer {
     bool on = false;
+    bool overlap = false;  // mode 2: events on the streams the regions run on, side streams kept
     bool pending = false;  // events of the last step not yet read
     hipEvent_t ev[PSVO_TIME_REGIONS][2] = {};
     double ms[PSVO_TIME_REGIONS] = {};
     int64_t n[PSVO_TIME_REGIONS] = {};
 };
 
+// Data-parallel exchange (psvo_engine_set_exchange): the caller's collective
+// callback and the device buffers it operates on.
+struct EngineExchange {
+    psvo_exchange_fn fn = nullptr;
+    void *user = nullptr;
+    int rank = 0, world = 1;
+    int nch = 1;               // launch chunks the slot-0 table covers
+    int *xi32 = nullptr;       // psvo_engine_exchange_words(world, max_rays_global) int32
+    double *xf64 = nullptr;    // 16 doubles: [0, 8) count sums, [8, 16) loss sums
+    bool on() const { return fn != nullptr && world > 1; }
+    // int32 word offsets
+    int64_t in_off() const { return 0; }
+    int64_t all_off() const { return psvo::kDistWordsPerRank; }
+    int64_t smax_in_off() const { return all_off() + (int64_t)world * psvo::kDistWordsPerRank; }
+    int64_t smax_all_off() const { return smax_in_off() + 8; }
+    int64_t table_off() const { return (smax_all_off() + world + 63) / 64 * 64; }
+    int64_t table_words() const { return (int64_t)psvo::kSamplerG * nch * psvo::kMaxHits; }
+    int call(int op, int64_t in, int64_t out, int64_t count, hipStream_t st, const char *what) const {
+        const int rc = fn(user, op, in, out, count, st);
+        if (rc != 0) return psvo::set_error(PSVO_E_LAUNCH, "exchange (%s) failed with %d", what, rc);
+        return PSVO_OK;
+    }
+};
+
 struct psvo_engine {
+    EngineExchange x;
     psvo::Arena a;
     psvo::QuerySet qs[2];           // FIFO of queries: head = the next step's
     int q_head = 0, q_count = 0;
@@ -175,6 +201,35 @@ extern "C" psvo_engine *psvo_engine_new(void) {
     return e;
 }
 
+extern "C" int psvo_engine_queued(psvo_engine *e) { return e ? e->q_count : 0; }
+
+extern "C" int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global) {
+    if (world < 1 || max_rays_global < 1) return -1;
+    EngineExchange x;
+    x.world = world;
+    x.nch = dist_slot0_rows(max_rays_global) / kSamplerG;
+    return x.table_off() + x.table_words();
+}
+
+extern "C" int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_rays_global,
+                                        psvo_exchange_fn fn, void *user, int *xi32, double *xf64) {
+    PSVO_REQUIRE(e, "engine_set_exchange: null engine");
+    PSVO_REQUIRE(world >= 1 && rank >= 0 && rank < world && max_rays_global >= 1,
+                 "engine_set_exchange: bad rank %d / world %d / max_rays_global %lld", rank, world,
+                 (long long)max_rays_global);
+    PSVO_REQUIRE(e->q_count == 0, "engine_set_exchange: queries are queued");
+    PSVO_REQUIRE(!fn || (xi32 && xf64), "engine_set_exchange: exchange buffers required");
+    e->x = EngineExchange();
+    e->x.fn = fn;
+    e->x.user = user;
+    e->x.rank = rank;
+    e->x.world = world;
+    e->x.nch = dist_slot0_rows(max_rays_global) / kSamplerG;
+    e->x.xi32 = xi32;
+    e->x.xf64 = xf64;
+    return PSVO_OK;
+}
+
 extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
     PSVO_REQUIRE(e, "engine_set_timing: null engine");
     if (on && !e->tm.ev[0][0])
@@ -184,6 +239,7 @@ extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
                     return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
     timer_collect(e);
     e->tm.on = on != 0;
+    e->tm.overlap = on == 2;
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
         e->tm.ms[r] = 0.0;
         e->tm.n[r] = 0;
@@ -307,6 +363,16 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
                                     ray_rank, rank_ray));
+    const EngineExchange &x = e->x;
+    if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced
+        ENG_CALL(dist_pack(st, stats, rank_ray, hit_idx, x.xi32 + x.in_off()));
+        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), kDistWordsPerRank, st,
+                        "query stats"));
+        ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, stats, rank_ray, hit_idx, x.nch,
+                             x.xi32 + x.table_off()));
+        ENG_CALL(x.call(PSVO_XCH_SUM_I32 | PSVO_XCH_QUERY, x.table_off(), x.table_off(), x.table_words(), st,
+                        "slot-0 table"));
+    }
     mark(e, st, PSVO_TIME_INTERSECT, 1);
     const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
                           kMaxHits + 1;
@@ -316,8 +382,17 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     Q_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
     Q_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
     mark(e, st, PSVO_TIME_SAMPLE, 0);
-    ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
-                              nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
+    if (x.on()) {
+        ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
+                             x.xi32 + x.table_off(), x.nch, s_idx, s_depth, s_dist, ray_ns, offsets));
+        // S_max of the union: every rank pads its [R_hit, S_max] blocks to it
+        ENG_CALL(dist_pack_smax(st, stats, x.xi32 + x.smax_in_off()));
+        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.smax_in_off(), x.smax_all_off(), 1, st, "S_max"));
+        ENG_CALL(dist_smax(st, x.xi32 + x.smax_all_off(), x.world, stats));
+    } else {
+        ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
+                                  nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
+    }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
     if (hipMemcpyAsync(q.host_stats, stats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord(q.done, st) != hipSuccess)
@@ -352,6 +427,25 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
 }
 
 // Give back the head query set once the step's kernels are queued.
+int release_query(psvo_engine *e, hipStream_t st, QuerySet *q);
+
+// Drops the step's query set if the step fails after take_query: without it a
+// failed batch (no hit ray, sampler overflow) would stay at the FIFO head and
+// every later step would be refused as "rays differ from the queued batch".
+struct QueryGuard {
+    psvo_engine *e;
+    hipStream_t st;
+    QuerySet *q = nullptr;
+    ~QueryGuard() {
+        if (q) (void)release_query(e, st, q);
+    }
+    int release() {
+        QuerySet *x = q;
+        q = nullptr;
+        return release_query(e, st, x);
+    }
+};
+
 int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
     if (hipEventRecord(q->freed, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
     q->freed_recorded = true;
@@ -369,7 +463,7 @@ int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
 // everything on the caller's stream, in dependency order).
 bool engine_overlap(psvo_engine *e) {
     static const bool serial = getenv("PSVO_SERIAL_BWD") && *getenv("PSVO_SERIAL_BWD") == '1';
-    return !serial && !e->tm.on;
+    return !serial && (!e->tm.on || e->tm.overlap);
 }
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
@@ -406,13 +500,21 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_CALL(spin_wait(qset.done, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
-    const int r_hit = hs[PSVO_STAT_R_HIT];
-    if (hs[7] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
-    if (r_hit == 0) return set_error(PSVO_E_INVALID, "%s: no ray hits the octree (render_helpers.py:388)", who);
+    // data-parallel: this rank's hit rays, padded to the union's S_max
+    const bool dist = e->x.on();
+    const int r_hit = dist ? hs[PSVO_STAT_R_HIT_LOCAL] : hs[PSVO_STAT_R_HIT];
+    if (hs[PSVO_STAT_FLAGS] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
+    if (hs[PSVO_STAT_FLAGS] & 4) return set_error(PSVO_E_OVERFLOW, "%s: union batch exceeds max_rays_global", who);
+    if (hs[PSVO_STAT_R_HIT] == 0)
+        return set_error(PSVO_E_INVALID, "%s: no ray hits the octree (render_helpers.py:388)", who);
     const int s_max = hs[PSVO_STAT_S_MAX];
     const int64_t M = hs[PSVO_STAT_M];
-    if (hs[7] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
+    if (hs[PSVO_STAT_FLAGS] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
     if (stats_out) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
+    o.r_hit = r_hit;
+    o.m = M;
+    o.s_max = s_max;
+    if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
     float *const *W = d->dec;
@@ -540,6 +642,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     Render q;
     QuerySet *qset = nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset));
+    QueryGuard guard{e, st, qset};
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
     hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward
@@ -547,27 +650,54 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     const int64_t M = q.m;
     const int64_t r_hit = q.r_hit;
     const int s_max = q.s_max;
+    // data-parallel: the loss of the union batch (criterion.py:70-101 normalise
+    // by batch-global counts and the padded [R_hit, S_max] size): count sums
+    // and loss sums are all-reduced, the rank's gradients are its part of the
+    // union-batch gradient (the caller sums them over ranks)
+    const EngineExchange &x = e->x;
+    const bool dist = x.on();
+    const bool empty = dist && (r_hit == 0 || M == 0);
+    const int64_t n_hit = dist ? qset->host_stats[PSVO_STAT_R_HIT] : r_hit;
     // ---- loss and backward (d loss = 1): normalisers on aux (after the
     // sampler, beside the decoder forward), then one fused per-ray pass
     ENG_BUF(float, crit_ws, kCritWs, psvo_criterion_workspace_floats(r_hit) * sizeof(float));
-    ENG_BUF(double, sums_c, kSumsC, 8 * sizeof(double));
-    ENG_BUF(double, sums, kSums, 8 * sizeof(double));
+    double *sums_c = x.xf64, *sums = x.xf64 ? x.xf64 + 8 : nullptr;
+    if (!dist) {
+        ENG_BUF(double, sc, kSumsC, 8 * sizeof(double));
+        ENG_BUF(double, sl, kSums, 8 * sizeof(double));
+        sums_c = sc;
+        sums = sl;
+    }
     ENG_BUF(float, coef, kCoef, 4 * sizeof(float));
     ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
     ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
     ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
-    ENG_CALL(psvo_criterion_coef(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth, q.z_vals,
-                                 d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
+    if (dist) {
+        ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
+                                  q.z_vals, crit_ws, sums_c));
+        ENG_CALL(x.call(PSVO_XCH_SUM_F64, 0, 0, 8, ax, "loss normalisers"));
+        ENG_CALL(criterion_coef_from_sums(ax, sums_c, n_hit, s_max, d->truncation, d->w_rgb, d->w_depth, d->w_fs,
+                                          d->w_sdf, crit_flags, coef));
+    } else {
+        ENG_CALL(psvo_criterion_coef(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth, q.z_vals,
+                                     d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
+    }
     ENG_CALL(fork_join(ax, st, e->coef_ready));
-    ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
-                                 q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
-                                 g_sdf_s, g_rgb_s));
+    if (!empty)
+        ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
+                                     q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
+                                     g_sdf_s, g_rgb_s));
     // the loss value (not on the gradient path): aux, beside the decoder backward
     ENG_CALL(fork_join(st, ax, e->grads_ready));
-    ENG_CALL(psvo_criterion_reduce(ax, r_hit, crit_ws, sums));
-    ENG_CALL(psvo_criterion_finalize(ax, sums, r_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
+    if (!empty) {
+        ENG_CALL(psvo_criterion_reduce(ax, r_hit, crit_ws, sums));
+    } else if (hipMemsetAsync(sums, 0, 8 * sizeof(double), ax) != hipSuccess) {
+        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    }
+    if (dist) ENG_CALL(x.call(PSVO_XCH_SUM_F64, 8, 8, 8, ax, "loss sums"));
+    ENG_CALL(psvo_criterion_finalize(ax, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
                                      d->truncation, crit_flags, loss_out));
     const int n_split = 256;
     ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
@@ -589,6 +719,15 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     }
     float *const *W = d->dec;
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
+    if (empty) {  // no samples on this rank: its part of the gradient is zero
+        ENG_CALL(fork_join(ax, st, e->emb_done));
+        if (hipMemsetAsync(grads, 0, (size_t)psvo_map_grad_floats(d->n_emb) * sizeof(float), st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+        e->grads_clean = false;
+        ENG_CALL(guard.release());
+        if (!(flags & PSVO_STEP_NO_ADAM)) ENG_CALL(map_adam(st, d, grads, adam_step));
+        return PSVO_OK;
+    }
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
     ENG_CALL(mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
@@ -612,7 +751,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
-    ENG_CALL(release_query(e, st, qset));
+    ENG_CALL(guard.release());
     // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step));
@@ -661,8 +800,10 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
     ENG_CALL(psvo_pose_rays(stream, R, pose, dirs_cam, rays_o, rays_d));
     Render q;
     PSVO_REQUIRE(e->q_count == 0, "track_step: the engine has queued mapping queries");
+    PSVO_REQUIRE(!e->x.on(), "track_step: tracking runs on one GPU (SURVEY §8e: its median filter is global)");
     QuerySet *qset = nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "track_step", &qset));
+    QueryGuard guard{e, st, qset};
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, false, stats_out, "track_step", q));
     // ---- loss (optionally with the median depth filter) and backward
     float *dtmp = nullptr, *dthr = nullptr;
@@ -693,7 +834,7 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
                              d->centres, d->vertex_idx, d->emb, dfeat, nullptr, grad_od, grad_od + R * 3));
     mark(e, st, PSVO_TIME_INTERP_BWD, 1);
     e->tm.pending = e->tm.on;
-    ENG_CALL(release_query(e, st, qset));
+    ENG_CALL(guard.release());
     // ---- pose gradient through rotation() and the pose's Adam step
     if (!pose_grad) {
         ENG_BUF(float, gbuf, kPoseGrad, 8 * sizeof(float));

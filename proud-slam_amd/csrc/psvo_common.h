@@ -35,6 +35,28 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray);
 
+// data-parallel query (svo_query.hip): rows of the exchanged slot-0 table for
+// a union batch of at most max_rays_global rays; pack this rank's 8 words;
+// union statistics + slot-0 table from the gathered words; the sampler over
+// the rank's rows; S_max of the union
+constexpr int kDistWordsPerRank = 8;
+int dist_slot0_rows(int64_t max_rays_global);
+int dist_pack(hipStream_t st, const int *stats, const int *rank_ray, const int *hit_idx, int *out);
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int *stats, const int *rank_ray,
+                const int *hit_idx, int nch, int *table);
+int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
+                int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
+                int *offsets);
+int dist_pack_smax(hipStream_t st, const int *stats, int *out);
+int dist_smax(hipStream_t st, const int *all, int world, int *stats);
+
+// psvo_criterion_coef split at the count sums (criterion.hip)
+int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
+                     const float *gt_depth, const float *z_vals, float *workspace, double *sums);
+int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
+                             float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef);
+
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
 // dfeat is written, before the weight-gradient kernels are queued
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,

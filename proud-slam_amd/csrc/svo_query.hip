@@ -617,10 +617,19 @@ struct FusedRows {
         const int e = jj * P + elem_from_H;
         const int lrow = base_row + e / P;
         const int col = e % P;
-        return (int64_t)rank_ray[real(lrow)] * kMaxHits + col;
+        return (int64_t)rank_ray[real(lrow) - row_begin] * kMaxHits + col;
     }
-    __device__ int idx_at(int e) const { return hit_idx[at(e)]; }
-    __device__ int idx_slot0(int col) const { return hit_idx[(int64_t)rank_ray[real(base_row)] * kMaxHits + col]; }
+    __device__ int idx_at(int e) const {
+        if (slot0) {
+            const int lrow = base_row + (jj * P + e) / P;
+            if (lrow < row_begin || lrow >= row_end) return next_col0;  // only (own row + 1, col 0) is read
+        }
+        return hit_idx[at(e)];
+    }
+    __device__ int idx_slot0(int col) const {
+        if (slot0) return slot0[(int64_t)slot0_row * kMaxHits + col];
+        return hit_idx[(int64_t)rank_ray[real(base_row)] * kMaxHits + col];
+    }
     __device__ float lo_at(int e) const { return hit_t0[at(e)]; }
     __device__ float hi_at(int e) const { return hit_t1[at(e)]; }
     __device__ float prob_at(int e) const {
@@ -639,6 +648,13 @@ struct FusedRows {
         const float dd = hit_idx[a] != -1 ? hit_t1[a] - hit_t0[a] : 0.0f;
         return __fdiv_rn(dd, own_dsum);
     }
+    // data-parallel engine: this rank holds only the logical rows
+    // [row_begin, row_end) (rank_ray / hit_* are local); the sampler reads
+    // other rows only as slot 0's voxel ids (the exchanged slot-0 table) and
+    // as the first voxel id of the row after its own (next_col0)
+    const int *slot0 = nullptr;  // [200 · nch][kMaxHits]
+    int slot0_row = 0;           // table row of (block, chunk)
+    int row_begin = 0, row_end = 0, next_col0 = -1;
 };
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
@@ -872,10 +888,15 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
                                                       const float *__restrict__ noise, uint64_t seed,
                                                       int *__restrict__ stats, int *__restrict__ s_idx,
                                                       float *__restrict__ s_depth, float *__restrict__ s_dist,
-                                                      int *__restrict__ ray_ns) {
+                                                      int *__restrict__ ray_ns, const int *__restrict__ slot0,
+                                                      int slot0_nch) {
     const int P = stats[PSVO_STAT_P];
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
+    if (slot0) {  // data-parallel engine: the rank's rows, local rank_ray / hit arrays
+        row_begin = stats[PSVO_STAT_ROW_BEGIN];
+        n_rows = stats[PSVO_STAT_R_HIT_LOCAL];
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int il = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
     const int i = (int)row_begin + il;                                        // logical row
@@ -883,17 +904,28 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     WaveBins &W = bins_all[threadIdx.x / kWave];
     const int64_t n_own = n_rows < 0 ? (int64_t)r_hit - row_begin : n_rows;
     if (i >= r_hit || il >= n_own || il >= r_hit_cap || P <= 0) return;
-    if (max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + 7, 2);
+    if (max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + PSVO_STAT_FLAGS, 2);
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
     const int b = i / kp;
     const int j = i - b * kp;
     const int c = j / kSamplerChunk;
     const int jj = j - c * kSamplerChunk;
     const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
-    const int orig = rank_ray[i];
+    const int orig = slot0 ? rank_ray[il] : rank_ray[i];
     const float dsum = ray_dsum[orig];
     FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj,
                    (int64_t)orig * kMaxHits, dsum};
+    if (slot0) {
+        if (c >= slot0_nch) {  // the exchanged table covers slot0_nch launch chunks
+            if (lane == 0) atomicOr(stats + PSVO_STAT_FLAGS, 4);
+            return;
+        }
+        rows.slot0 = slot0;
+        rows.slot0_row = b * slot0_nch + c;
+        rows.row_begin = (int)row_begin;
+        rows.row_end = (int)(row_begin + n_rows);
+        rows.next_col0 = stats[PSVO_STAT_NEXT_COL0];
+    }
     const float steps_j = __fdiv_rn(dsum, step_size);
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
     int *oi = s_idx + (int64_t)il * max_steps_cap;
@@ -931,10 +963,11 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
 // offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
-                                                       int *__restrict__ stats) {
+                                                       int *__restrict__ stats, int dist) {
     __shared__ int total;
     __shared__ int smax[16];
-    const int64_t n_own = n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
+    const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
+                               : n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
     const int64_t n = max((int64_t)0, min(n_own, r_hit_cap));
     block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total);
     int mx = 0;
@@ -971,6 +1004,84 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
         t[o] = z;
         ray_of_sample[o] = (int)r;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Data-parallel query (engine.cpp): each rank samples
+// its own hit rays inside the [200, K', P] layout of the union batch (ranks
+// in order).  Besides P / R_hit / max ceil(steps) of the union, the sampler
+// reads other ranks' rows in two places only (sample_gpu.cu:224-237): the
+// voxel ids of each launch block's slot-0 row (idx_slot0) and the first voxel
+// id of the row after a ray's own (a ray with exactly P bins).  So a rank
+// exchanges 8 words (all-gather), then a [200 · nch, 50] slot-0 table
+// (all-reduce sum: each row is written by its owner, zeros elsewhere) — not
+// its hit lists.
+constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id of its first hit row
+
+__global__ void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
+                            const int *__restrict__ hit_idx, int *__restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const int r_hit = stats[PSVO_STAT_R_HIT];
+    out[0] = r_hit;
+    out[1] = stats[PSVO_STAT_P];
+    out[2] = stats[PSVO_STAT_MAX_CEIL];
+    out[3] = r_hit > 0 ? hit_idx[(int64_t)rank_ray[0] * kMaxHits] : -1;
+    for (int k = 4; k < kDistWords; ++k) out[k] = 0;
+}
+
+// union-batch statistics from the gathered words (world x kDistWords)
+__global__ void k_dist_layout(const int *__restrict__ all, int world, int rank, int *__restrict__ stats) {
+    if (threadIdx.x != 0) return;
+    int r_hit = 0, p = 0, mc = 0, begin = 0;
+    for (int r = 0; r < world; ++r) {
+        const int *w = all + r * kDistWords;
+        if (r < rank) begin += w[0];
+        r_hit += w[0];
+        p = max(p, w[1]);
+        mc = max(mc, w[2]);
+    }
+    // the logical row after this rank's last: the next rank holding hit rows,
+    // or (past the union's last row) row 0, as the reference's row-0 padding
+    int next = -1;
+    for (int r = rank + 1; r < world && next < 0; ++r)
+        if (all[r * kDistWords] > 0) next = r;
+    for (int r = 0; r < world && next < 0; ++r)
+        if (all[r * kDistWords] > 0) next = r;
+    stats[PSVO_STAT_R_HIT_LOCAL] = all[rank * kDistWords];
+    stats[PSVO_STAT_ROW_BEGIN] = begin;
+    stats[PSVO_STAT_NEXT_COL0] = next >= 0 ? all[next * kDistWords + 3] : -1;
+    stats[PSVO_STAT_P] = p;
+    stats[PSVO_STAT_R_HIT] = r_hit;
+    stats[PSVO_STAT_MAX_CEIL] = mc;
+}
+
+// table row (b, c) = the voxel ids of logical row b·K' + c·800 (row 0 past the
+// union's end) if this rank holds it, else zeros
+__global__ void k_dist_slot0(const int *__restrict__ stats, const int *__restrict__ rank_ray,
+                             const int *__restrict__ hit_idx, int nch, int *__restrict__ table) {
+    const int r_hit = stats[PSVO_STAT_R_HIT];
+    const int begin = stats[PSVO_STAT_ROW_BEGIN];
+    const int n_loc = stats[PSVO_STAT_R_HIT_LOCAL];
+    const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
+    const int row = blockIdx.x;  // b * nch + c
+    const int b = row / nch, c = row - b * nch;
+    int lrow = b * kp + c * kSamplerChunk;
+    if (lrow >= r_hit) lrow = 0;
+    const bool mine = lrow >= begin && lrow < begin + n_loc;
+    for (int col = threadIdx.x; col < kMaxHits; col += blockDim.x)
+        table[(int64_t)row * kMaxHits + col] = mine ? hit_idx[(int64_t)rank_ray[lrow - begin] * kMaxHits + col] : 0;
+}
+
+__global__ void k_dist_pack_smax(const int *__restrict__ stats, int *__restrict__ out) {
+    if (threadIdx.x == 0) out[0] = stats[PSVO_STAT_S_MAX];
+}
+
+__global__ void k_dist_smax(const int *__restrict__ all, int world, int *__restrict__ stats) {
+    if (threadIdx.x != 0) return;
+    int mx = 0;
+    for (int r = 0; r < world; ++r) mx = max(mx, all[r]);
+    stats[PSVO_STAT_S_MAX_LOCAL] = stats[PSVO_STAT_S_MAX];
+    stats[PSVO_STAT_S_MAX] = mx;
 }
 
 }  // namespace
@@ -1042,6 +1153,43 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
 }
 }  // namespace psvo
 
+namespace psvo {
+int dist_slot0_rows(int64_t max_rays_global) {
+    const int64_t kp = (max_rays_global + kSamplerG - 1) / kSamplerG;
+    return kSamplerG * (int)((kp + kSamplerChunk - 1) / kSamplerChunk);
+}
+int dist_pack(hipStream_t st, const int *stats, const int *rank_ray, const int *hit_idx, int *out) {
+    hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(64), 0, st, stats, rank_ray, hit_idx, out);
+    return check_launch("dist_pack");
+}
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int *stats, const int *rank_ray,
+                const int *hit_idx, int nch, int *table) {
+    hipLaunchKernelGGL(k_dist_layout, dim3(1), dim3(64), 0, st, all, world, rank, stats);
+    hipLaunchKernelGGL(k_dist_slot0, dim3(kSamplerG * nch), dim3(64), 0, st, stats, rank_ray, hit_idx, nch, table);
+    return check_launch("dist_layout");
+}
+// the fused sampler + scan over this rank's rows (stats from dist_layout)
+int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
+                int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
+                int *offsets) {
+    if (r_hit_cap == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
+                       rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
+                       s_dist, ray_ns, table, nch);
+    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1);
+    return check_launch("dist_sample");
+}
+int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
+    hipLaunchKernelGGL(k_dist_pack_smax, dim3(1), dim3(64), 0, st, stats, out);
+    return check_launch("dist_pack_smax");
+}
+int dist_smax(hipStream_t st, const int *all, int world, int *stats) {
+    hipLaunchKernelGGL(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats);
+    return check_launch("dist_smax");
+}
+}  // namespace psvo
+
 extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray) {
     PSVO_REQUIRE(n_rays >= 0, "hit_rank: n_rays < 0");
     if (n_rays == 0) return PSVO_OK;
@@ -1061,9 +1209,9 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
-                       s_idx, s_depth, s_dist, ray_ns);
+                       s_idx, s_depth, s_dist, ray_ns, nullptr, 0);
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
-                       stats);
+                       stats, 0);
     return check_launch("sample_rays");
 }
 

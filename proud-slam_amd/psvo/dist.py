@@ -239,6 +239,107 @@ class SparseRowSum:
         return "sparse"
 
 
+XCH_GATHER_I32, XCH_SUM_I32, XCH_SUM_F64, XCH_QUERY = 1, 2, 3, 0x100
+
+
+class EngineExchange:
+    """The collectives of the data-parallel native engine (psvo_engine_set_exchange,
+    include/psvo.h): the engine computes the loss of the UNION of all ranks'
+    rays — bit-identical sample layout and normalisers to one GPU rendering the
+    concatenated batch — and calls back here for four small collectives per
+    step (8 + 1 words all-gathered and a 40-KB slot-0 table summed in the
+    query phase, 16 doubles summed in the step), each on the HIP stream the
+    engine produced the operand on.
+
+    With RCCL ("nccl") the query-phase collectives run on their own
+    communicator (they are issued one step ahead, concurrently with the
+    previous step's), so neither phase queues behind the other on one NCCL
+    stream; with gloo (CPU rehearsal / tests) operands are staged through the
+    host.  `apply` is the whole protocol and works on CPU tensors too."""
+
+    def __init__(self, max_rays_global, device=None, group=None, query_group=None):
+        self.world = world()
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.max_rays_global = int(max_rays_global)
+        self.group = group
+        self.nccl = self.world > 1 and _backend(group) == "nccl"
+        if query_group is None and self.nccl:
+            query_group = dist.new_group(list(range(self.world)), backend="nccl")
+        self.query_group = query_group if query_group is not None else group
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.xi32 = None
+        self.xf64 = torch.zeros(16, dtype=torch.float64, device=self.device)
+        self.error = None
+        self._cb = None
+
+    def buffers(self, n_words):
+        self.xi32 = torch.zeros(int(n_words), dtype=torch.int32, device=self.device)
+        return self.xi32, self.xf64
+
+    def apply(self, op, in_off, out_off, count, stream=None):
+        """One collective of the engine protocol on xi32 / xf64 (see psvo.h)."""
+        grp = self.query_group if (op & XCH_QUERY) else self.group
+        op &= 0xFF
+        buf = self.xf64 if op == XCH_SUM_F64 else self.xi32
+        if op == XCH_GATHER_I32:
+            src = buf[in_off:in_off + count]
+            dst = buf[out_off:out_off + count * self.world]
+        else:
+            src = dst = buf[in_off:in_off + count]
+        if self.world == 1:
+            if op == XCH_GATHER_I32:
+                dst.copy_(src)
+            return
+        if self.nccl:
+            ctx = torch.cuda.stream(torch.cuda.ExternalStream(stream)) if stream else _nullctx()
+            with ctx:
+                if op == XCH_GATHER_I32:
+                    dist.all_gather_into_tensor(dst, src, group=grp)
+                else:
+                    dist.all_reduce(dst, op=dist.ReduceOp.SUM, group=grp)
+            return
+        # gloo: stage through the host, ordered on the engine's stream
+        if stream and src.is_cuda:
+            torch.cuda.ExternalStream(stream).synchronize()
+        h = src.cpu().clone()
+        if op == XCH_GATHER_I32:
+            parts = [torch.empty_like(h) for _ in range(self.world)]
+            dist.all_gather(parts, h, group=grp)
+            h = torch.cat(parts)
+        else:
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=grp)
+        if stream and dst.is_cuda:
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
+                dst.copy_(h)
+        else:
+            dst.copy_(h)
+
+    def callback(self):
+        """The psvo_exchange_fn handed to the engine (kept alive here)."""
+        import ctypes
+        if self._cb is None:
+            proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_void_p)
+
+            def fn(user, op, in_off, out_off, count, stream):
+                try:
+                    self.apply(op, in_off, out_off, count, stream)
+                    return 0
+                except BaseException as exc:  # noqa: BLE001 — reported through the engine's error
+                    self.error = exc
+                    return 1
+            self._cb = proto(fn)
+        return self._cb
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
 class EngineGradExchange:
     """The engine's per-step gradient exchange (MappingEngine.grad_flat =
     [embedding rows | decoder]): one flat all-reduce while the table is small
@@ -248,9 +349,10 @@ class EngineGradExchange:
     row table, where a step touches a small fraction of the rows).  The
     result is averaged over ranks (op "mean", as GradBucket)."""
 
-    def __init__(self, engine, sparse_min_bytes=32 << 20, group=None, ops=None):
+    def __init__(self, engine, sparse_min_bytes=32 << 20, group=None, ops=None, op="mean"):
         self.engine = engine
         self.group = group
+        self.op = op  # "sum": the engine's union-batch loss (EngineExchange) — gradients add up
         self.n_emb = int(engine.emb.shape[0])
         self.sparse = None
         if self.n_emb * 16 * 4 >= sparse_min_bytes:
@@ -269,4 +371,5 @@ class EngineGradExchange:
             n = self.n_emb * 16
             self.last_mode = self.sparse(flat[:n].view(self.n_emb, 16))
             dist.all_reduce(flat[n:], op=dist.ReduceOp.SUM, group=self.group)
-        flat.div_(ws)
+        if self.op == "mean":
+            flat.div_(ws)

@@ -56,7 +56,7 @@ class MappingEngine:
         self.dec_v = [torch.zeros_like(p) for p in self.params]
         self.step_no = 0
         self.loss_out = torch.empty(16, dtype=torch.float32, device=self.emb.device)
-        self.stats = (ctypes.c_int * 8)()
+        self.stats = (ctypes.c_int * 16)()
         d = MapDesc()
         d.n_nodes = self.centres.shape[0]
         d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
@@ -78,11 +78,38 @@ class MappingEngine:
                                      device=self.emb.device)
         d.grad_flat = self.grad_flat.data_ptr()
         self.desc = d
-        self._queued = []
+        self._queued = []   # (caller's rays_o, rays_d, seed, converted ro, rd) per queued query
+        self.exchange = None
         h = _lib().psvo_engine_new()
         if not h:
             raise L.PsvoError("psvo_engine_new failed")
         self.handle = _vp(h)
+
+    def set_exchange(self, exchange):
+        """Data-parallel mode (psvo.dist.EngineExchange): every step computes
+        the loss of the union of all ranks' rays; sum grad_flat over ranks
+        (psvo.dist.EngineGradExchange(op="sum")) before adam()."""
+        n = int(_lib().psvo_engine_exchange_words(exchange.world, exchange.max_rays_global))
+        xi32, xf64 = exchange.buffers(n)
+        if xi32.device != self.emb.device:
+            raise RuntimeError("EngineExchange buffers must live on the engine's device")
+        L.call("psvo_engine_set_exchange", self.handle, exchange.rank, exchange.world, exchange.max_rays_global,
+               ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
+        self.exchange = exchange
+
+    def _error(self, name, rc):
+        msg = _lib().psvo_last_error().decode()
+        if self.exchange is not None and self.exchange.error is not None:
+            msg += f" ({type(self.exchange.error).__name__}: {self.exchange.error})"
+            self.exchange.error = None
+        return L.PsvoError(f"{name} failed (code {rc}): {msg}")
+
+    def _sync_queue(self):
+        """Drop the Python records of queries the engine consumed (a failed
+        step consumes its query too)."""
+        n = int(_lib().psvo_engine_queued(self.handle))
+        while len(self._queued) > n:
+            self._queued.pop(0)
 
     def query(self, rays_o, rays_d, seed):
         """Queue the next iteration's ray query (intersection + sampling) on the
@@ -95,8 +122,8 @@ class MappingEngine:
         rc = _lib().psvo_map_query(self.handle, L.stream_of(ro.device), ctypes.addressof(self.desc), ro.shape[0],
                                    ro.data_ptr(), rd.data_ptr(), int(seed))
         if rc != 0:
-            raise L.PsvoError(f"psvo_map_query failed (code {rc}): {_lib().psvo_last_error().decode()}")
-        self._queued.append((ro, rd))   # alive until the consuming step has run
+            raise self._error("psvo_map_query", rc)
+        self._queued.append((rays_o, rays_d, int(seed), ro, rd))   # alive until the consuming step has run
 
     def step(self, rays_o, rays_d, rgb, depth, seed, apply_adam=True):
         """One iteration; returns the loss (0-dim device tensor, not synchronised;
@@ -104,9 +131,10 @@ class MappingEngine:
         gradients (self.grad_flat) — all-reduce them, then call adam().  If
         query() queued this batch, its results are used."""
         if self._queued:
-            ro, rd = self._queued[0]
-            if ro.data_ptr() != rays_o.reshape(-1, 3).data_ptr() and rays_o.is_contiguous():
-                raise RuntimeError("MappingEngine.step: rays differ from the queued query")
+            q_o, q_d, q_seed, ro, rd = self._queued[0]
+            if q_o is not rays_o or q_d is not rays_d or q_seed != int(seed):
+                raise RuntimeError("MappingEngine.step: rays / seed differ from the batch query() queued "
+                                   "(pass the same tensor objects and seed)")
         else:
             ro = rays_o.reshape(-1, 3).float().contiguous()
             rd = rays_d.reshape(-1, 3).float().contiguous()
@@ -117,11 +145,12 @@ class MappingEngine:
                                   ro.data_ptr(), rd.data_ptr(), gt_rgb.data_ptr(), gt_d.data_ptr(), int(seed),
                                   self.step_no, 0 if apply_adam else 1, self.loss_out.data_ptr(),
                                   ctypes.addressof(self.stats))
+        # queued records the engine consumed (the step's kernels are
+        # stream-ordered after their last use of the rays)
+        self._sync_queue()
         if rc != 0:
             self.step_no -= 1
-            raise L.PsvoError(f"psvo_map_step failed (code {rc}): {_lib().psvo_last_error().decode()}")
-        if self._queued:
-            self._queued.pop(0)   # consumed (the step's kernels are stream-ordered after their last use)
+            raise self._error("psvo_map_step", rc)
         return self.loss_out[0]
 
     def adam(self):
@@ -129,8 +158,10 @@ class MappingEngine:
         L.call("psvo_map_adam", self.handle, L.stream_of(self.emb.device), ctypes.addressof(self.desc), self.step_no)
 
     def set_timing(self, on):
-        """HIP events around the decoder fwd / bwd and interp fwd / bwd launches."""
-        L.call("psvo_engine_set_timing", self.handle, int(bool(on)))
+        """HIP events around the decoder fwd / bwd and interp fwd / bwd launches.
+        on=True: regions serialised on one stream; on="overlap": as the
+        untimed step runs them (side streams overlapping the main stream)."""
+        L.call("psvo_engine_set_timing", self.handle, 2 if on == "overlap" else int(bool(on)))
 
     REGIONS = ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd", "intersect", "sample", "points")
 
@@ -197,7 +228,7 @@ class TrackingEngine:
         self.pose_v = torch.zeros(6, dtype=torch.float32, device=self.dev)
         self.pose_grad = torch.zeros(8, dtype=torch.float32, device=self.dev)
         self.loss_out = torch.empty(16, dtype=torch.float32, device=self.dev)
-        self.stats = (ctypes.c_int * 8)()
+        self.stats = (ctypes.c_int * 16)()
         self.step_no = 0
         h = _lib().psvo_engine_new()
         if not h:

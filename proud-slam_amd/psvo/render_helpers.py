@@ -191,7 +191,7 @@ def query_samples(rays_o, rays_d, map_states, step_size, voxel_size, max_distanc
         else:
             L.call("psvo_hit_rank", stream, R, L.ptr(q["ray_nv"]), L.ptr(ray_rank), L.ptr(rank_ray))
     if exact:
-        st = torch.cat([g["stats"], counts, q["stats"][5:8]]).cpu()  # sync 1
+        st = torch.cat([g["stats"][:8], counts, q["stats"][5:8]]).cpu()  # sync 1
         P, rg_hit, max_ceil = int(st[0]), int(st[1]), int(st[2])
         row_begin, r_hit, visits, flags = int(st[8]), int(st[9]), int(st[10]), int(st[12])
         stats = g["stats"]

@@ -24,7 +24,7 @@ MAX_DEPTH = 10.0        # voxel_helpers.py:24
 N_MAX_HITS = 50         # voxel_helpers.py:561
 SAMPLER_G = 200         # voxel_helpers.py:300
 SAMPLER_CHUNK = 4 * SAMPLER_G
-STAT_WORDS = 8
+STAT_WORDS = 16
 
 
 class SparseVoxelOctreeRayIntersect(Function):

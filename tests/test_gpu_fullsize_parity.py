@@ -1,0 +1,167 @@
+"""HIP path bit-exact against the C oracle at every BASELINE config size
+(VERDICT r1 item 1).  The oracle's intersection (svo_oracle.c: the DFS of
+intersect_gpu.cu:191-270 + voxel_helpers.py:557-595's sort / trim) and its
+sampler (sample_gpu.cu:133-239 + voxel_helpers.py:288-374's [200, K', P]
+wrapper), fed the ORACLE's own intersection, against k_intersect_sorted /
+k_sample_fused on the same rays and noise:
+
+  * hit ids, t_in, t_out, per-ray valid counts: bit-exact, every ray;
+  * sample voxel ids, depths, distances: bit-exact, every ray.  The one
+    order-dependent input, Σ(t_out − t_in) per ray (a torch .sum(-1) in the
+    reference, whose order torch leaves unspecified), is accumulated left to
+    right on both sides (oracle.sequential_row_sums); that the sample COUNT
+    does not depend on the order is checked separately: ⌈Σ/step⌉ agrees
+    between torch's CPU order and the sequential one on every ray;
+  * the whole render + Criterion + backward chain at configs B (W=128) and
+    C (W=256): z_vals bit-exact, fp32 outputs rtol 1e-4 / atol 1e-5, loss
+    rtol 1e-4, gradients ≤ 2e-3 · max|ref| (float-atomic / GEMM order).
+
+Configs (BASELINE.json): B room0 4 x 1024 rays; C scannet0000 8 x 1024 rays
+(W = 256, max_depth 5); D office0 32 x 1024 rays (the whole global batch of
+the 8-GPU config on one GPU); E multiroom (>1M SURFACE leaves, depth-10 tree)
+4 x 1024 rays."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CONFIGS = {
+    "B": dict(scene="room0", frames=4, rays=1024, step=0.0078, width=128, max_depth=10.0),
+    "C": dict(scene="scannet0000", frames=8, rays=1024, step=0.008, width=256, max_depth=5.0),
+    "D": dict(scene="office0", frames=32, rays=1024, step=0.008, width=128, max_depth=10.0),
+    "E": dict(scene="multiroom", frames=4, rays=1024, step=0.008, width=128, max_depth=10.0),
+}
+_CACHE = {}
+
+
+def _setup(name):
+    if name in _CACHE:
+        return _CACHE[name]
+    from psvo import synthetic as syn
+    from psvo.octree import Octree, map_states
+    c = CONFIGS[name]
+    w = syn.make_workload(c["scene"], c["frames"], c["rays"], seed=21)
+    tree = Octree()
+    tree.init(w.scene.grid_dim, 16, w.scene.voxel_size, 8)
+    tree.insert(w.voxels)
+    n = tree.count_nodes()
+    emb = torch.randn(max(20000, n), 16, generator=torch.Generator().manual_seed(3)) * 0.1
+    ms = map_states(tree, emb.to(DEV), w.scene.voxel_size, device=DEV)
+    ms_cpu = {k: v.cpu() for k, v in ms.items()}
+    _CACHE.clear()  # one scene at a time (config E's tree is large)
+    _CACHE[name] = (c, w, ms, ms_cpu)
+    return _CACHE[name]
+
+
+def _oracle_intersection(w, ms_cpu, vs):
+    return O.ray_intersect_vox(w.rays_o, w.rays_d, ms_cpu["voxel_center_xyz"], ms_cpu["voxel_structure"], vs, 10.0)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_intersect_bit_exact_full_size(name):
+    from psvo.voxel_helpers import _intersect_sorted
+    c, w, ms, ms_cpu = _setup(name)
+    vs = w.scene.voxel_size
+    o_out, o_hits = _oracle_intersection(w, ms_cpu, vs)
+    P = o_out["intersected_voxel_idx"].shape[-1]
+    q = _intersect_sorted(w.rays_o.to(DEV), w.rays_d.to(DEV), ms["voxel_center_xyz"], ms["voxel_structure"], vs, 10.0,
+                          c["step"])
+    st = q["stats"].cpu()
+    assert int(st[0]) == P and int(st[1]) == int(o_hits.sum())
+    assert int(st[7]) == 0  # no DFS-stack overflow
+    o_idx = o_out["intersected_voxel_idx"][0]
+    nv = q["ray_nv"].cpu()
+    assert torch.equal(nv, o_idx.ne(-1).sum(-1).int())
+    assert torch.equal(q["hit_idx"].cpu()[:, :P], o_idx)
+    assert torch.equal(q["hit_t0"].cpu()[:, :P], o_out["min_depth"][0])
+    assert torch.equal(q["hit_t1"].cpu()[:, :P], o_out["max_depth"][0])
+    assert (q["hit_idx"].cpu()[:, P:] == -1).all()
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_sampler_bit_exact_full_size(name):
+    from psvo.render_helpers import query_samples
+    c, w, ms, ms_cpu = _setup(name)
+    vs = w.scene.voxel_size
+    o_out, o_hits = _oracle_intersection(w, ms_cpu, vs)
+    hit = o_hits.view(-1)
+    inter = {k: v[0][hit] for k, v in o_out.items()}
+    idx = inter["intersected_voxel_idx"]
+    P = idx.shape[-1]
+    dists = (inter["max_depth"] - inter["min_depth"]).masked_fill(idx.eq(-1), 0)
+    seq = O.sequential_row_sums(dists)
+    tor = dists.sum(-1)
+    step = np.float32(c["step"])
+    # the sample count per ray does not depend on the summation order
+    assert torch.equal(torch.ceil(seq / step), torch.ceil(tor / step))
+    r_hit = int(hit.sum())
+    kp = (r_hit + 199) // 200
+    max_steps = int(torch.ceil(seq / step).max()) + P
+    noise = torch.rand((200, kp, max_steps), generator=torch.Generator().manual_seed(9)).clamp(0.001, 0.999)
+    o_smp, _ = O.ray_sample(inter, c["step"], noise=noise, sum_order="sequential")
+    smp = query_samples(w.rays_o.to(DEV), w.rays_d.to(DEV), ms, c["step"], vs, 10.0, noise=noise)
+    assert smp.r_hit == r_hit and smp.P == P
+    o_idx = o_smp["sampled_point_voxel_idx"]
+    n = o_idx.shape[1]
+    assert smp.s_max == n
+    assert torch.equal(smp.s_idx.cpu()[:, :n], o_idx)
+    assert torch.equal(smp.s_depth.cpu()[:, :n], o_smp["sampled_point_depth"])
+    assert torch.equal(smp.s_dist.cpu()[:, :n], o_smp["sampled_point_distance"])
+    assert (smp.s_idx.cpu()[:, n:] == -1).all()
+    assert smp.m == int(o_idx.ne(-1).sum())
+    if name == "B":
+        assert 60 < smp.m / smp.r_hit < 70  # the metric's ~64 samples per hit ray
+
+
+@pytest.mark.parametrize("name", ["B", "C"])
+def test_render_loss_grads_full_size(name):
+    import types
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    from psvo.render_helpers import render_rays
+    c, w, ms, ms_cpu = _setup(name)
+    vs = w.scene.voxel_size
+    crit_w = O.SCANNET_CRITERIA if c["scene"] == "scannet0000" else O.REPLICA_CRITERIA
+    params = O.decoder_params_init(c["width"], seed=4)
+    o_out, o_hits = _oracle_intersection(w, ms_cpu, vs)
+    hit = o_hits.view(-1)
+    inter = {k: v[0][hit] for k, v in o_out.items()}
+    dists = (inter["max_depth"] - inter["min_depth"]).masked_fill(inter["intersected_voxel_idx"].eq(-1), 0)
+    P = dists.shape[-1]
+    max_steps = int(torch.ceil(O.sequential_row_sums(dists) / np.float32(c["step"])).max()) + P
+    kp = (int(hit.sum()) + 199) // 200
+    noise = torch.rand((200, kp, max_steps), generator=torch.Generator().manual_seed(13)).clamp(0.001, 0.999)
+    rgb, depth = w.rgb.reshape(1, -1, 3), w.depth.reshape(1, -1)
+    o_res, o_loss, _, o_grads = O.render_and_backward(w.rays_o, w.rays_d, rgb, depth, ms_cpu, params, c["step"], vs,
+                                                      0.1, 10.0, crit_w, noise=noise, sum_order="sequential",
+                                                      max_depth=c["max_depth"])
+    dec = Decoder(depth=2, width=c["width"], in_dim=16, skips=[], embedder="none").to(DEV)
+    dec.load_state_dict(params)
+    emb = ms["voxel_vertex_emb"].clone().requires_grad_(True)
+    ms2 = dict(ms, voxel_vertex_emb=emb)
+    ro = w.rays_o.to(DEV).requires_grad_(True)
+    rd = w.rays_d.to(DEV).requires_grad_(True)
+    out = render_rays(ro, rd, ms2, dec, None, c["step"], vs, 0.1, 10, 10.0, noise=noise)
+    crit = Criterion(types.SimpleNamespace(criteria={**crit_w, "sdf_truncation": 0.1},
+                                           data_specs={"max_depth": c["max_depth"]}))
+    loss, _ = crit(out, (rgb.to(DEV), depth.to(DEV)))
+    loss.backward()
+    assert torch.equal(out["ray_mask"].cpu(), o_res["ray_mask"])
+    assert torch.equal(out["z_vals"].cpu(), o_res["z_vals"])
+    tol = dict(rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(out["sdf"].detach().cpu(), o_res["sdf"].detach(), **tol)
+    torch.testing.assert_close(out["color"].detach().cpu(), o_res["color"].detach(), **tol)
+    torch.testing.assert_close(out["depth"].detach().cpu(), o_res["depth"].detach(), **tol)
+    assert abs(float(loss) - float(o_loss)) <= 1e-4 * abs(float(o_loss))
+    pairs = [(emb.grad, o_grads["embeddings"]), (ro.grad, o_grads["rays_o"]), (rd.grad, o_grads["rays_d"])]
+    for k, p in dec.named_parameters():
+        pairs.append((p.grad, o_grads[k]))
+    for a, b in pairs:
+        scale = float(b.abs().max()) + 1e-12
+        assert float((a.detach().cpu() - b).abs().max()) <= 2e-3 * scale
