@@ -42,9 +42,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scene", default="room0")
-    ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--frames", type=int, default=None,
+                    help="keyframes x rays-per-frame = rays per iteration per GPU (default: 8 for scannet0000, else 4)")
     ap.add_argument("--rays-per-frame", type=int, default=1024)
-    ap.add_argument("--width", type=int, default=128)
+    ap.add_argument("--width", type=int, default=None,
+                    help="decoder width (default: the scene's config — 256 for scannet0000 / multiroom (ARKit), "
+                         "else 128)")
     ap.add_argument("--samples-per-ray", type=float, default=64.0)
     ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -54,7 +57,22 @@ def parse():
     ap.add_argument("--exact-global-loss", action="store_true",
                     help="(kept for compatibility: N>1 always computes the union-batch loss)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    big = a.scene in ("scannet0000", "multiroom")  # configs/scannet/scannet.yaml:17, configs/arkit/arkit.yaml:17
+    if a.width is None:
+        a.width = 256 if big else 128
+    if a.frames is None:
+        a.frames = 8 if a.scene == "scannet0000" else 4
+    return a
+
+
+# per-scene Criterion / data specs (configs/replica/replica.yaml, configs/scannet/scannet.yaml:8-13)
+SCENE_CRITERIA = {
+    "scannet0000": ({"rgb_weight": 1.0, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0,
+                     "sdf_truncation": 0.1}, 5.0),
+}
+DEFAULT_CRITERIA = ({"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0,
+                     "sdf_truncation": 0.1}, 10.0)
 
 
 def launch_workers(args):
@@ -226,9 +244,8 @@ def main():
 
     scene, tree, ms, emb, dec, batches = build_scene(args, device, rank)
     step_size, spr = calibrate_step(ms, batches, args.samples_per_ray, scene.voxel_size)
-    crit_args = types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0,
-                                                "fs_weight": 10.0, "sdf_truncation": 0.1},
-                                      data_specs={"max_depth": 10.0})
+    crit_cfg, max_depth = SCENE_CRITERIA.get(args.scene, DEFAULT_CRITERIA)
+    crit_args = types.SimpleNamespace(criteria=dict(crit_cfg), data_specs={"max_depth": max_depth})
     criterion = Criterion(crit_args)
     from psvo.optim import Adam  # torch.optim.Adam semantics, one HIP launch per step per optimiser
     embed_optim = Adam([emb], lr=5e-3)
@@ -246,20 +263,14 @@ def main():
     bucket = GradBucket(params, op="sum")
     reducer = GlobalLossSums() if world > 1 else None
     gbatch = GlobalBatch() if world > 1 else None
-    if not args.autograd and args.width != 128:
-        # the fused decoder and the native engine are width 128: W=256
-        # (ScanNet / ARKit configs) runs the drop-in path, recorded in "path"
-        args.autograd = True
-    engine = exchange = None
-    if args.width == 128:
-        engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
-                               criteria=crit_args.criteria, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
-        from psvo.dist import EngineExchange, EngineGradExchange
-        if world > 1:
-            # the loss of the union of all ranks' rays: union-batch
-            # sampler layout and normalisers, gradients summed over ranks
-            engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
-        exchange = EngineGradExchange(engine, op="sum")
+    engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
+                           criteria=crit_args.criteria, max_depth=max_depth, lr_emb=5e-3, lr_dec=5e-3)
+    from psvo.dist import EngineExchange, EngineGradExchange
+    if world > 1:
+        # the loss of the union of all ranks' rays: union-batch
+        # sampler layout and normalisers, gradients summed over ranks
+        engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
+    exchange = EngineGradExchange(engine, op="sum")
 
     def record_stats(m, r_hit, visits, s_max):
         stats["m"] += m
@@ -356,9 +367,7 @@ def main():
         engine.set_timing(False)
     # the other path, for reference (not the headline number)
     other_steps = max(5, min(args.steps, 20))
-    if args.autograd and args.width != 128:
-        other = {"path": "native engine: not run (its fused decoder is width 128)"}
-    elif world > 1:
+    if world > 1:
         other = {"path": "not run at N > 1 (the headline path only)"}
     else:
         if args.autograd:

@@ -204,7 +204,7 @@ int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation
                         const float *coef, float *workspace, float *color, float *depth, float *grad_sdf_s,
                         float *grad_rgb_s);
 
-/* ---- NRGBD decoder (nrgbd.py:80-146; width 128, in 16, depth 2) ------- */
+/* ---- NRGBD decoder (nrgbd.py:80-146; width 128 or 256, in 16, depth 2) -- */
 /* Weights in torch nn.Linear layout ([out][in] row-major): W1[128,16],
  * W2[128,128], W3[129,128] (row 0 = sdf), W4[128,144] ([f | x] columns),
  * W5[3,128].  Forward: feat[M,16] → sdf[M], rgb[M,3] (sigmoid applied).
@@ -214,8 +214,19 @@ int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation
  * and act f32[4][ceil(M/64)*64*128] (h1, h2, f, c1 in 32-sample CF tiles, see
  * mlp.hip; needed only for weight gradients) are written when non-NULL;
  * act requires masks.  Inference: both NULL; rgb NULL as well: the sdf
- * alone (Decoder.get_sdf, mesh lattices — h1, h2 and W3's sdf row only). */
+ * alone (Decoder.get_sdf, mesh lattices — h1, h2 and W3's sdf row only).
+ * Width 256 (W1[256,16], W2[256,256], W3[129,256], W4[256,144], W5[3,256];
+ * mlp256.hip): images psvo_mlp_image_floats_w(256), act / masks as sized by
+ * psvo_mlp_act_floats / psvo_mlp_mask_words (16-sample tiles); rgb NULL
+ * skips only the rgb stores. */
 int64_t psvo_mlp_image_floats(void);
+/* width-aware sizes (width 128 or 256; -1 otherwise): operand images, the
+ * training forward's activations (act) and ReLU masks (u64 words), the
+ * backward's workspace */
+int64_t psvo_mlp_image_floats_w(int width);
+int64_t psvo_mlp_act_floats(int64_t m, int width);
+int64_t psvo_mlp_mask_words(int64_t m, int width);
+int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split);
 int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                  const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                  const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
@@ -368,7 +379,7 @@ typedef struct psvo_map_desc {
     float *dec[10];
     float *dec_m[10];
     float *dec_v[10];
-    int width; /* 128 */
+    int width; /* 128 (Replica) or 256 (ScanNet / ARKit) */
     float voxel_size, step_size, max_distance, truncation, max_depth;
     float w_rgb, w_depth, w_fs, w_sdf; /* Criterion weights (criterion.py:8-13) */
     double lr_emb, lr_dec, beta1, beta2, eps;
@@ -379,7 +390,8 @@ typedef struct psvo_map_desc {
 
 enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
 
-int64_t psvo_map_grad_floats(int64_t n_emb);
+int64_t psvo_map_grad_floats(int64_t n_emb);                 /* width 128 */
+int64_t psvo_map_grad_floats_w(int64_t n_emb, int width);
 
 /* ---- row-sparse gradient exchange (data parallel on large maps, §8e) ---- */
 /* Ints of workspace psvo_rows_compact needs for n_rows rows. */

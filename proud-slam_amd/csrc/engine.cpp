@@ -280,10 +280,21 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     T *name = reinterpret_cast<T *>(slot_buf(e, st, slot, (bytes), &rc));   \
     if (!name) return rc;
 
-static const int64_t kDecSizes[10] = {128 * 16, 128, 128 * 128, 128, 129 * 128, 129, 128 * 144, 128, 3 * 128, 3};
-static const int64_t kDecTotal = 128 * 16 + 128 + 128 * 128 + 128 + 129 * 128 + 129 + 128 * 144 + 128 + 3 * 128 + 3;
+// decoder parameter sizes (nrgbd.py:98-108, depth 2, in 16, sdf_dim 128) for width W
+static void dec_sizes(int W, int64_t (&n)[10]) {
+    const int64_t w = W;
+    const int64_t v[10] = {w * 16, w, w * w, w, 129 * w, 129, w * 144, w, 3 * w, 3};
+    for (int i = 0; i < 10; ++i) n[i] = v[i];
+}
+static int64_t dec_total(int W) {
+    int64_t n[10], t = 0;
+    dec_sizes(W, n);
+    for (int i = 0; i < 10; ++i) t += n[i];
+    return t;
+}
 
-extern "C" int64_t psvo_map_grad_floats(int64_t n_emb) { return n_emb * 16 + kDecTotal; }
+extern "C" int64_t psvo_map_grad_floats(int64_t n_emb) { return n_emb * 16 + dec_total(128); }
+extern "C" int64_t psvo_map_grad_floats_w(int64_t n_emb, int width) { return n_emb * 16 + dec_total(width); }
 
 // grads: [embeddings (n_emb x 16) | W1, b1, ..., W5, b5]
 // one launch for both optimisers (lr per tensor); the embedding gradient is
@@ -303,6 +314,8 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
     lr[0] = d->lr_emb;
     zero[0] = 1;
     int64_t off = d->n_emb * 16;
+    int64_t kDecSizes[10];
+    dec_sizes(d->width, kDecSizes);
     for (int i = 0; i < 10; ++i) {
         p[1 + i] = d->dec[i];
         g[1 + i] = grads + off;
@@ -518,13 +531,14 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
     float *const *W = d->dec;
-    ENG_BUF(float, images, kImages, psvo_mlp_image_floats() * sizeof(float));
+    const int width = d->width;
+    ENG_BUF(float, images, kImages, psvo_mlp_image_floats_w(width) * sizeof(float));
     // the decoder's operand images depend only on the weights: built on aux
     // beside the sampler compaction and the interpolation (psvo_map_step)
     const bool early_images = fused_loss && engine_overlap(e);
     if (early_images) {
         ENG_CALL(fork_join(st, e->aux, e->prep_fork));
-        ENG_CALL(mlp_images(e->aux, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+        ENG_CALL(mlp_images(e->aux, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
     }
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
@@ -543,22 +557,21 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
                              d->vertex_idx, d->emb, feat));
     mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-    const int64_t mp = (M + 63) / 64 * 64;
     ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
     ENG_BUF(float, rgb_s, kRgbS, M * 3 * sizeof(float));
     float *act = nullptr;
     if (want_act) {
-        ENG_BUF(float, abuf, kAct, (size_t)4 * mp * 128 * sizeof(float));
+        ENG_BUF(float, abuf, kAct, (size_t)psvo_mlp_act_floats(M, width) * sizeof(float));
         act = abuf;
     }
-    ENG_BUF(uint64_t, masks, kMasks, (size_t)M * 6 * sizeof(uint64_t));
+    ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
     mark(e, st, PSVO_TIME_MLP_FWD, 0);
     if (early_images) {
         ENG_CALL(fork_join(e->aux, st, e->prep_done));
-        ENG_CALL(mlp_fwd_prepared(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+        ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                                   images, sdf_s, rgb_s, act, masks));
     } else {
-        ENG_CALL(psvo_mlp_fwd(stream, M, 128, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+        ENG_CALL(psvo_mlp_fwd(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                               images, sdf_s, rgb_s, act, masks));
     }
     mark(e, st, PSVO_TIME_MLP_FWD, 1);
@@ -635,7 +648,8 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
                              uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && rays_o && rays_d && gt_rgb && gt_depth && loss_out, "map_step: null argument");
     PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "map_step: bad sizes");
-    PSVO_REQUIRE(d->width == 128, "map_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
+    PSVO_REQUIRE(d->width == 128 || d->width == 256, "map_step: decoder width %d unsupported (fused: 128, 256)",
+                 d->width);
     hipStream_t st = as_stream(stream);
     int rc = PSVO_OK;
     const int64_t R = n_rays;
@@ -700,17 +714,19 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_CALL(psvo_criterion_finalize(ax, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
                                      d->truncation, crit_flags, loss_out));
     const int n_split = 256;
-    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
+    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats_w(M, d->width, n_split) * sizeof(float));
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
     // gradients: the caller's flat buffer (data-parallel all-reduce) or the arena
     float *grads = d->grad_flat;
     if (!grads) {
-        ENG_BUF(float, gbuf, kDecGrad, psvo_map_grad_floats(d->n_emb) * sizeof(float));
+        ENG_BUF(float, gbuf, kDecGrad, psvo_map_grad_floats_w(d->n_emb, d->width) * sizeof(float));
         grads = gbuf;
     }
     float *grad_emb = grads;
     float *G[10];
     {
+        int64_t kDecSizes[10];
+        dec_sizes(d->width, kDecSizes);
         int64_t off = d->n_emb * 16;
         for (int i = 0; i < 10; ++i) {
             G[i] = grads + off;
@@ -721,7 +737,8 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
     if (empty) {  // no samples on this rank: its part of the gradient is zero
         ENG_CALL(fork_join(ax, st, e->emb_done));
-        if (hipMemsetAsync(grads, 0, (size_t)psvo_map_grad_floats(d->n_emb) * sizeof(float), st) != hipSuccess)
+        if (hipMemsetAsync(grads, 0, (size_t)psvo_map_grad_floats_w(d->n_emb, d->width) * sizeof(float), st) !=
+            hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
         e->grads_clean = false;
         ENG_CALL(guard.release());
@@ -729,7 +746,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
         return PSVO_OK;
     }
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
+    ENG_CALL(mlp_bwd(stream, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
@@ -789,7 +806,8 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
                                float *pose_grad, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && dirs_cam && gt_rgb && gt_depth && pose && loss_out, "track_step: null argument");
     PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "track_step: bad sizes");
-    PSVO_REQUIRE(d->width == 128, "track_step: decoder width %d unsupported (fused decoder is width 128)", d->width);
+    PSVO_REQUIRE(d->width == 128 || d->width == 256, "track_step: decoder width %d unsupported (fused: 128, 256)",
+                 d->width);
     PSVO_REQUIRE((flags & PSVO_STEP_NO_ADAM) || (pose_m && pose_v), "track_step: Adam needs pose_m / pose_v");
     hipStream_t st = as_stream(stream);
     int rc = PSVO_OK;
@@ -821,10 +839,10 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
     const int64_t M = q.m;
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
     const int n_split = 256;
-    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats(M, n_split) * sizeof(float));
+    ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats_w(M, d->width, n_split) * sizeof(float));
     float *const *W = d->dec;
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(psvo_mlp_bwd(stream, M, 128, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+    ENG_CALL(psvo_mlp_bwd(stream, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                           q.images, q.rgb_s, nullptr, q.masks, g_sdf_s, g_rgb_s, dfeat, nullptr, nullptr, nullptr,
                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, n_split, mlp_ws));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);

@@ -1534,11 +1534,35 @@ using namespace psvo;
 
 extern "C" int64_t psvo_mlp_image_floats(void) { return kImgTotal; }
 
+// width-aware sizes (width 128: the CF layout above; width 256: mlp256.hip)
+extern "C" int64_t psvo_mlp_image_floats_w(int width) {
+    return width == 128 ? kImgTotal : width == 256 ? dec256_image_floats() : -1;
+}
+extern "C" int64_t psvo_mlp_act_floats(int64_t m, int width) {
+    const int64_t mp = (m + kCh - 1) / kCh * kCh;
+    return width == 128 ? mp * 4 * 128 : width == 256 ? dec256_act_floats(m) : -1;
+}
+extern "C" int64_t psvo_mlp_mask_words(int64_t m, int width) {
+    return width == 128 ? m * 6 : width == 256 ? dec256_mask_words(m) : -1;
+}
+
 static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                             const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
                             float *act, uint64_t *masks, bool images_ready) {
-    PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused path is width 128)", width);
+    if (width == 256) {
+        PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
+        PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats_w floats)");
+        PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd: act needs masks");
+        PSVO_REQUIRE(m <= ((int64_t)1 << 31) / 256, "mlp_fwd: m = %lld too large", (long long)m);
+        hipStream_t st = as_stream(stream);
+        if (!images_ready) {
+            const int rc = dec256_images(st, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images);
+            if (rc) return rc;
+        }
+        return dec256_fwd(st, m, feat, images, sdf, rgb, act, masks);
+    }
+    PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
     PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats floats)");
     PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd: act needs masks");
@@ -1586,8 +1610,10 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
 }
 
 namespace psvo {
-int mlp_images(void *stream, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
-               const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images) {
+int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
+               const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
+               float *images) {
+    if (width == 256) return dec256_images(as_stream(stream), w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
     hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, as_stream(stream), p, images);
     return check_launch("mlp_images");
@@ -1640,12 +1666,18 @@ static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
     *slab_floats = off;
 }
 
+extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split);
+
 extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
     dw_grid(m, n_split, &g, &slab);
     const int64_t mp = (m + kCh - 1) / kCh * kCh;
     return mp * 4 * 128 + m * 3 + slab;
+}
+
+extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split) {
+    return width == 128 ? psvo_mlp_workspace_floats(m, n_split) : width == 256 ? dec256_workspace_floats(m) : -1;
 }
 
 // Full decoder backward: grads of the 10 parameters (overwritten, or added
@@ -1659,7 +1691,15 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready) {
-    PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused path is width 128)", width);
+    if (width == 256) {
+        PSVO_REQUIRE(m >= 0, "mlp_bwd: bad sizes");
+        PSVO_REQUIRE(images != nullptr && masks != nullptr, "mlp_bwd: images / masks of the training forward required");
+        PSVO_REQUIRE(gw1 == nullptr || act != nullptr, "mlp_bwd: weight gradients need the forward's activations");
+        float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
+        return dec256_bwd(as_stream(stream), m, feat, images, rgb, act, masks, g_sdf, g_rgb, dfeat, gw, gb, accumulate,
+                          workspace, dfeat_ready);
+    }
+    PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
     PSVO_REQUIRE(images != nullptr, "mlp_bwd: images of the training forward required");
     const bool want_w = gw1 != nullptr;  // NULL weight gradients: δ chain / dfeat only (frozen decoder)

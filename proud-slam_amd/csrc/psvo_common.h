@@ -57,6 +57,21 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef);
 
+// width-256 decoder (mlp256.hip): sizes, operand images, forward (act /
+// masks NULL: inference), backward (gw[0] NULL: δ chain to dfeat only)
+int64_t dec256_tiles16(int64_t m);
+int64_t dec256_image_floats();
+int64_t dec256_act_floats(int64_t m);
+int64_t dec256_mask_words(int64_t m);
+int64_t dec256_workspace_floats(int64_t m);
+int dec256_images(hipStream_t st, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+                  const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
+int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images, float *sdf, float *rgb, float *act,
+               uint64_t *masks);
+int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
+               const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
+               float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready);
+
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
 // dfeat is written, before the weight-gradient kernels are queued
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
@@ -69,8 +84,9 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
 // the decoder's LDS operand images (k_mlp_prep) on their own, and
 // psvo_mlp_fwd without rebuilding them (the engine prepares them on its aux
 // stream beside the sampler / interpolation kernels)
-int mlp_images(void *stream, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
-               const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
+int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
+               const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
+               float *images);
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,

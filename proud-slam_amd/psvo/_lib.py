@@ -47,6 +47,11 @@ _SIGNATURES = {
     "psvo_rows_compact": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_scatter_add": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "psvo_mlp_image_floats": (_i64, []),
+    "psvo_mlp_image_floats_w": (_i64, [_i32]),
+    "psvo_mlp_act_floats": (_i64, [_i64, _i32]),
+    "psvo_mlp_mask_words": (_i64, [_i64, _i32]),
+    "psvo_mlp_workspace_floats_w": (_i64, [_i64, _i32, _i32]),
+    "psvo_map_grad_floats_w": (_i64, [_i64, _i32]),
     "psvo_mlp_fwd": (_i32, [_vp, _i64, _i32] + [_vp] * 16),
     "psvo_mlp_workspace_floats": (_i64, [_i64, _i32]),
     "psvo_mlp_bwd": (_i32, [_vp, _i64, _i32] + [_vp] * 28 + [_i32, _i32, _vp]),

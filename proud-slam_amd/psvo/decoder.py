@@ -5,9 +5,9 @@ embedder 'none', skips []:
   h = ReLU(L0(x)); h = ReLU(L1(h)); o = sdf_out(h) = [sdf | f(128)]
   rgb = σ(L5(ReLU(L4([f, x]))))
 
-On a GPU with width 128 (every Replica config) forward() runs the fused
-fp32-MFMA kernels of libpsvo (csrc/mlp.hip) through DecoderMLP; other widths
-(ScanNet/ARKit W=256) run the same layers as PyTorch-ROCm GEMMs.
+On a GPU forward() runs the fused fp32-MFMA kernels of libpsvo through
+DecoderMLP: width 128 (every Replica config, csrc/mlp.hip) and width 256
+(ScanNet / ARKit, configs/scannet/scannet.yaml:17, csrc/mlp256.hip).
 get_values() (mesh extraction, no grad) uses the PyTorch layers.
 """
 from __future__ import annotations
@@ -37,15 +37,19 @@ class DecoderMLP(Function):
         # grad mode is off inside Function.forward: needs_input_grad tells what backward will want
         need_w = any(ctx.needs_input_grad[1:])           # weight gradients need the activations
         training = need_w or ctx.needs_input_grad[0]     # dfeat alone (frozen decoder) needs only the masks
-        mp = (m + 63) // 64 * 64  # CF activations: whole 64-sample chunks
-        act = torch.empty((4, mp, 128), dtype=torch.float32, device=dev) if need_w else None
-        masks = torch.empty((m, 2, 3), dtype=torch.int64, device=dev) if training else None
-        images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=dev)
+        width = ps[0].shape[0]
+        lib = L.lib()
+        act = torch.empty((int(lib.psvo_mlp_act_floats(m, width)),), dtype=torch.float32,
+                          device=dev) if need_w else None
+        masks = torch.empty((int(lib.psvo_mlp_mask_words(m, width)),), dtype=torch.int64,
+                            device=dev) if training else None
+        images = torch.empty((int(lib.psvo_mlp_image_floats_w(width)),), dtype=torch.float32, device=dev)
         with L.timed("mlp_fwd"):
-            L.call("psvo_mlp_fwd", L.stream_of(dev), m, 128, feat, *ps, images, sdf, rgb, act, masks)
+            L.call("psvo_mlp_fwd", L.stream_of(dev), m, width, feat, *ps, images, sdf, rgb, act, masks)
         if training:
             ctx.save_for_backward(feat, rgb, act, masks, images, *ps)
             ctx.need_w = need_w
+            ctx.width = width
         return sdf, rgb
 
     @staticmethod
@@ -56,12 +60,13 @@ class DecoderMLP(Function):
         g_sdf = torch.zeros((m,), device=dev) if g_sdf is None else g_sdf.contiguous().float()
         g_rgb = torch.zeros((m, 3), device=dev) if g_rgb is None else g_rgb.contiguous().float()
         n_split = 256  # split-K workgroups of the weight gradients (one per CU)
-        ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats(m, n_split)),), dtype=torch.float32, device=dev)
+        ws = torch.empty((int(L.lib().psvo_mlp_workspace_floats_w(m, ctx.width, n_split)),), dtype=torch.float32,
+                         device=dev)
         dfeat = torch.empty((m, 16), dtype=torch.float32, device=dev)
         grads = [torch.empty_like(p) for p in ps] if ctx.need_w else [None] * len(ps)
         with L.timed("mlp_bwd"):
-            L.call("psvo_mlp_bwd", L.stream_of(dev), m, 128, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb, dfeat,
-                   *grads, 0, n_split, ws)
+            L.call("psvo_mlp_bwd", L.stream_of(dev), m, ctx.width, feat, *ps, images, rgb, act, masks, g_sdf, g_rgb,
+                   dfeat, *grads, 0, n_split, ws)
         return (dfeat if ctx.needs_input_grad[0] else None, *grads)
 
 
@@ -110,7 +115,7 @@ class Decoder(nn.Module):
                 self.color_out[0].weight, self.color_out[0].bias, self.color_out[2].weight, self.color_out[2].bias]
 
     def can_fuse(self, x):
-        return (x.is_cuda and self.W == 128 and self.D == 2 and not self.skips and x.shape[-1] == 16
+        return (x.is_cuda and self.W in (128, 256) and self.D == 2 and not self.skips and x.shape[-1] == 16
                 and self.sdf_out.out_features == 129)
 
     def forward(self, inputs):

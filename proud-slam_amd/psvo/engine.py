@@ -36,7 +36,7 @@ def _lib():
 
 class MappingEngine:
     """map_states: psvo.octree.map_states dict (device); decoder: psvo.decoder.Decoder
-    (width 128); criteria: dict of rgb/depth/fs/sdf weights (Criterion args.criteria)."""
+    (width 128 or 256); criteria: dict of rgb/depth/fs/sdf weights (Criterion args.criteria)."""
 
     def __init__(self, map_states, decoder, voxel_size, step_size, truncation=0.1, max_distance=10.0,
                  criteria=None, max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3, betas=(0.9, 0.999), eps=1e-8):
@@ -74,8 +74,8 @@ class MappingEngine:
         d.w_fs, d.w_sdf = crit["fs_weight"], crit["sdf_weight"]
         d.lr_emb, d.lr_dec, d.beta1, d.beta2, d.eps = lr_emb, lr_dec, betas[0], betas[1], eps
         # flat gradient bucket [embeddings | decoder]: what data-parallel ranks all-reduce
-        self.grad_flat = torch.zeros(int(_lib().psvo_map_grad_floats(self.emb.shape[0])), dtype=torch.float32,
-                                     device=self.emb.device)
+        self.grad_flat = torch.zeros(int(_lib().psvo_map_grad_floats_w(self.emb.shape[0], decoder.W)),
+                                     dtype=torch.float32, device=self.emb.device)
         d.grad_flat = self.grad_flat.data_ptr()
         self.desc = d
         self._queued = []   # (caller's rays_o, rays_d, seed, converted ro, rd) per queued query

@@ -33,9 +33,10 @@ def _decode_sdf(sdf_network, feat, out):
     if not sdf_network.can_fuse(feat):
         out.copy_(sdf_network.get_values(feat)[:, 3])
         return
-    images = torch.empty((int(L.lib().psvo_mlp_image_floats()),), dtype=torch.float32, device=feat.device)
+    w = sdf_network.W
+    images = torch.empty((int(L.lib().psvo_mlp_image_floats_w(w)),), dtype=torch.float32, device=feat.device)
     ps = [p.detach() for p in sdf_network.fused_params()]
-    L.call("psvo_mlp_fwd", L.stream_of(feat.device), feat.shape[0], 128, feat, *ps, images, out, None, None, None)
+    L.call("psvo_mlp_fwd", L.stream_of(feat.device), feat.shape[0], w, feat, *ps, images, out, None, None, None)
 
 
 def surface_states(voxels, features, embeddings, voxel_size):

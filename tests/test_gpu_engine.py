@@ -130,7 +130,36 @@ def test_engine_query_ahead_matches_inline():
     ahead.query(halves[0][0], halves[0][1], 7)
     with pytest.raises(RuntimeError):
         ahead.step(*halves[1], seed=7)
-    with pytest.raises(L.PsvoError):   # same rays, other seed: the C side refuses it
+    with pytest.raises(RuntimeError, match="differ"):   # same rays, other seed: refused
         ahead.step(*halves[0], seed=8)
     for e in engines:
         e.close()
+
+
+def test_failed_step_does_not_wedge_the_engine():
+    """a queued batch whose step fails (here: no ray hits the
+    octree) is consumed by the failed step; the next queued batch steps
+    normally, and a step with other rays than the queued ones is refused."""
+    from psvo._lib import PsvoError
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ms = map_states(tree, emb0.clone().to(DEV), 0.2, device=DEV)
+    eng = MappingEngine(ms, dec, 0.2, 0.01)
+    ro, rd = w.rays_o.to(DEV), w.rays_d.to(DEV)
+    rgb, depth = w.rgb.to(DEV), w.depth.to(DEV)
+    miss_o = torch.full_like(ro, -50.0)   # far outside the scene, pointing away
+    miss_d = torch.zeros_like(rd)
+    miss_d[..., 0] = -1.0
+    eng.query(miss_o, miss_d, 1)
+    eng.query(ro, rd, 2)
+    with pytest.raises(PsvoError, match="no ray hits"):
+        eng.step(miss_o, miss_d, rgb, depth, seed=1)
+    with pytest.raises(RuntimeError, match="differ"):
+        eng.step(ro, rd, rgb, depth, seed=3)  # wrong seed for the queued batch
+    loss = float(eng.step(ro, rd, rgb, depth, seed=2))
+    assert np.isfinite(loss)
+    assert int(eng.last_stats[1]) > 0
+    loss2 = float(eng.step(ro, rd, rgb, depth, seed=4))  # nothing queued: fresh query
+    assert np.isfinite(loss2)
+    eng.close()

@@ -7,11 +7,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.mark.parametrize("width", [128, 256])
 @pytest.mark.parametrize("m", [1, 77, 1000, 4099])
-def test_decoder_fused_matches_torch(m):
+def test_decoder_fused_matches_torch(m, width):
     from psvo.decoder import Decoder, DecoderMLP
     torch.manual_seed(m)
-    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec = Decoder(depth=2, width=width, in_dim=16, skips=[], embedder="none").to(DEV)
     with torch.no_grad():
         for p in dec.parameters():
             p.mul_(3.0)  # wider pre-activations: exercise both ReLU sides and sigmoid tails
@@ -42,10 +43,11 @@ def test_decoder_fused_matches_torch(m):
         assert err <= 2e-4 * scale, (k, err, scale)
 
 
-def test_decoder_fused_is_deterministic():
+@pytest.mark.parametrize("width", [128, 256])
+def test_decoder_fused_is_deterministic(width):
     from psvo.decoder import Decoder, DecoderMLP
     torch.manual_seed(0)
-    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec = Decoder(depth=2, width=width, in_dim=16, skips=[], embedder="none").to(DEV)
     x = torch.randn(20000, 16, device=DEV, requires_grad=True)
     outs = []
     for _ in range(2):
@@ -57,3 +59,27 @@ def test_decoder_fused_is_deterministic():
             p.grad = None
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("width", [128, 256])
+def test_decoder_frozen_and_inference(width):
+    """Frozen decoder (tracking: dfeat only, no activations kept) and the
+    inference forward (no grad) give the training path's numbers."""
+    from psvo.decoder import Decoder, DecoderMLP
+    torch.manual_seed(5)
+    dec = Decoder(depth=2, width=width, in_dim=16, skips=[], embedder="none").to(DEV)
+    x = torch.randn(3001, 16, device=DEV)
+    g_sdf = torch.randn(3001, device=DEV)
+    g_rgb = torch.randn(3001, 3, device=DEV)
+    xa = x.clone().requires_grad_(True)
+    sdf, rgb = DecoderMLP.apply(xa, *dec.fused_params())
+    ((sdf * g_sdf).sum() + (rgb * g_rgb).sum()).backward()
+    xb = x.clone().requires_grad_(True)
+    frozen = [p.detach() for p in dec.fused_params()]
+    sdf2, rgb2 = DecoderMLP.apply(xb, *frozen)
+    ((sdf2 * g_sdf).sum() + (rgb2 * g_rgb).sum()).backward()
+    assert torch.equal(sdf, sdf2) and torch.equal(rgb, rgb2)
+    assert torch.equal(xa.grad, xb.grad)
+    with torch.no_grad():
+        sdf3, rgb3 = DecoderMLP.apply(x, *frozen)
+    assert torch.equal(sdf3, sdf2) and torch.equal(rgb3, rgb2)
