@@ -13,7 +13,8 @@ import os
 import torch
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpsvo.so")
+# PSVO_LIB_PATH: a diagnostic build of the same sources (A/B experiments); never set on the product path
+LIB_PATH = os.environ.get("PSVO_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libpsvo.so")
 
 _vp, _i32, _i64, _f32, _f64, _u64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float,
                                       ctypes.c_double, ctypes.c_uint64)

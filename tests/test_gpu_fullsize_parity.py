@@ -159,9 +159,11 @@ def test_render_loss_grads_full_size(name):
     torch.testing.assert_close(out["color"].detach().cpu(), o_res["color"].detach(), **tol)
     torch.testing.assert_close(out["depth"].detach().cpu(), o_res["depth"].detach(), **tol)
     assert abs(float(loss) - float(o_loss)) <= 1e-4 * abs(float(o_loss))
-    pairs = [(emb.grad, o_grads["embeddings"]), (ro.grad, o_grads["rays_o"]), (rd.grad, o_grads["rays_d"])]
+    pairs = [("embeddings", emb.grad, o_grads["embeddings"]), ("rays_o", ro.grad, o_grads["rays_o"]),
+             ("rays_d", rd.grad, o_grads["rays_d"])]
     for k, p in dec.named_parameters():
-        pairs.append((p.grad, o_grads[k]))
-    for a, b in pairs:
+        pairs.append((k, p.grad, o_grads[k]))
+    for k, a, b in pairs:
         scale = float(b.abs().max()) + 1e-12
-        assert float((a.detach().cpu() - b).abs().max()) <= 2e-3 * scale
+        err = float((a.detach().cpu() - b).abs().max())
+        assert err <= 2e-3 * scale, (k, err, scale)
