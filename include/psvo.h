@@ -319,6 +319,13 @@ int psvo_criterion_bwd_ex(void *stream, int64_t r_hit, int s_max, float truncati
 int psvo_pose_rays(void *stream, int64_t n, const float *pose, const float *dirs, float *rays_o, float *rays_d);
 /* grad f32[6] = dL/d[t | w] from per-ray grad_o / grad_d of the R_hit hit
  * rays at rows rank_ray[r] (psvo_interp_bwd's output), through rotation(). */
+/* Several keyframes (bundle_adjust_frames, render_helpers.py:620-640): poses
+ * f32[F][6], frame f owns rays [f·rays_per_frame, (f+1)·rays_per_frame);
+ * grads f32[F][8] ([dL/dt | dL/dw | 0 0]) over each frame's hit rays. */
+int psvo_pose_rays_frames(void *stream, int64_t n, int64_t rays_per_frame, const float *poses, const float *dirs,
+                          float *rays_o, float *rays_d);
+int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_per_frame, int64_t r_hit, const int *rank_ray,
+                          const float *dirs, const float *g_o, const float *g_d, const float *poses, float *grads);
 int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,
                    const float *g_d, const float *pose, float *grad);
 
@@ -467,6 +474,30 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * d->beta2, d->eps; moments pose_m / pose_v f32[6]) unless
  * PSVO_STEP_NO_ADAM.  pose_grad: device f32[6] out or NULL.  One stats
  * read-back; loss_out / stats_out as psvo_map_step. */
+/* bundle_adjust_frames with update_pose (render_helpers.py:559-676): the
+ * iteration's rays come from the keyframes' current poses — frame f's rays
+ * are [f·rays_per_frame, (f+1)·rays_per_frame): rays_o = t_f, rays_d =
+ * dirs_cam @ R(w_f)ᵀ (:620-640) — and after the backward every keyframe with
+ * pose_step[f] ≥ 1 takes its pose Adam step (its own step number, lr_pose;
+ * frame.py:27 keyframe.optim) beside Adam(embeddings) / Adam(decoder).
+ * poses / pose_m / pose_v: device f32[F][6], updated in place; pose_step:
+ * host int64[F] (0: the frame's pose is fixed — stamp 0 or update_pose
+ * False); pose_grad: device f32[F][8] output or NULL.  noise: the sampler's
+ * uniform noise f32[200, K', max_steps] (voxel_helpers.py:323-328) or NULL
+ * (drawn from seed).  No queued psvo_map_query may be pending. */
+typedef struct psvo_map_frames {
+    int n_frames;
+    int64_t rays_per_frame;
+    const float *dirs_cam;
+    float *poses, *pose_m, *pose_v;
+    const int64_t *pose_step;
+    double lr_pose;
+    float *pose_grad;
+} psvo_map_frames;
+int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *frames,
+                         const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,
+                         int64_t adam_step, int flags, float *loss_out, int *stats_out);
+
 enum { PSVO_TRACK_DEPTH_FILTER = 2 };
 int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *dirs_cam,
                     const float *gt_rgb, const float *gt_depth, float *pose, float *pose_m, float *pose_v, double lr,

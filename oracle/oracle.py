@@ -435,3 +435,66 @@ def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_pa
     for k, v in params.items():
         grads[k] = v.grad
     return out, loss.detach(), parts, grads
+
+
+# --------------------------------------------------------------------------
+# bundle_adjust_frames — render_helpers.py:559-676 with keyframe poses
+# (se3pose.py:8-98 restated below: [t | w], R = I + A[w]x + B[w]x^2, A / B as
+# 10th-order Taylor series in theta)
+# --------------------------------------------------------------------------
+def _taylor(theta, first, step, nth=10):
+    ans = torch.zeros_like(theta)
+    denom = 1.0
+    for i in range(nth + 1):
+        if i > 0:
+            denom *= step(i)
+        ans = ans + (-1) ** i * theta ** (2 * i) / (denom * first)
+    return ans
+
+
+def se3_rotation(data):
+    """se3pose.py:24-33 (rotation of pose parameters [t | w])."""
+    w = data[3:]
+    wx = torch.stack([torch.stack([torch.zeros(()), -w[2], w[1]]), torch.stack([w[2], torch.zeros(()), -w[0]]),
+                      torch.stack([-w[1], w[0], torch.zeros(())])])
+    theta = w.norm(dim=-1)[..., None, None]
+    A = _taylor(theta, 1.0, lambda i: (2 * i) * (2 * i + 1))
+    B = _taylor(theta, 2.0, lambda i: (2 * i + 1) * (2 * i + 2))
+    return torch.eye(3) + A * wx + B * (wx @ wx)
+
+
+def bundle_adjust(frames, picks, noises, map_states, decoder_params, poses0, stamps, step_size, voxel_size,
+                  n_iters, lr_map=5e-3, lr_pose=1e-3, criteria=REPLICA_CRITERIA, truncation=0.1, max_distance=10.0):
+    """frames: [(rays_d [H,W,3], rgb [H,W,3], depth [H,W])]; picks[it][f]:
+    sorted pixel ids; noises[it]: the sampler noise of iteration it.  Adam
+    (torch, CPU) on embeddings, decoder and the poses of frames with stamp != 0.
+    Returns (losses, embeddings, decoder params, poses)."""
+    emb = map_states["voxel_vertex_emb"].detach().clone().requires_grad_(True)
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in decoder_params.items()}
+    poses = [torch.tensor(p, dtype=torch.float32).requires_grad_(True) for p in poses0]
+    opts = [torch.optim.Adam([emb], lr=lr_map), torch.optim.Adam(list(params.values()), lr=lr_map)]
+    opts += [torch.optim.Adam([poses[f]], lr=lr_pose) for f in range(len(frames)) if stamps[f] != 0]
+    ms = dict(map_states)
+    ms["voxel_vertex_emb"] = emb
+    losses = []
+    for it in range(n_iters):
+        ro, rd, rgb, dep = [], [], [], []
+        for f, (rays_d, rgb_f, depth_f) in enumerate(frames):
+            idx = torch.as_tensor(picks[it][f]).long()
+            R = se3_rotation(poses[f])
+            d = rays_d.reshape(-1, 3)[idx] @ R.transpose(-1, -2)
+            ro.append(poses[f][:3].reshape(1, -1).expand_as(d))
+            rd.append(d)
+            rgb.append(rgb_f.reshape(-1, 3)[idx])
+            dep.append(depth_f.reshape(-1)[idx])
+        rays_o, rays_d_w = torch.cat(ro)[None], torch.cat(rd)[None]
+        out = render_rays(rays_o, rays_d_w, ms, params, step_size, voxel_size, truncation, max_distance,
+                          noise=torch.as_tensor(noises[it]))
+        loss, _ = criterion(out, torch.cat(rgb)[None], torch.cat(dep)[None], criteria, truncation, max_distance)
+        for o in opts:
+            o.zero_grad()
+        loss.backward()
+        for o in opts:
+            o.step()
+        losses.append(float(loss.detach()))
+    return losses, emb.detach(), {k: v.detach() for k, v in params.items()}, torch.stack([p.detach() for p in poses])

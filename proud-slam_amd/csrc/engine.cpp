@@ -359,7 +359,8 @@ struct Render {
 // intervals of at most a voxel diagonal (rows are written only up to
 // max_steps; an overflow is flagged and reported by the consumer).
 int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_desc *d, int64_t R,
-                  const float *rays_o, const float *rays_d, uint64_t seed, const char *who) {
+                  const float *rays_o, const float *rays_d, uint64_t seed, const char *who,
+                  const float *noise = nullptr) {
     int rc = PSVO_OK;
     void *stream = st;
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
@@ -377,6 +378,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
                                     ray_rank, rank_ray));
     const EngineExchange &x = e->x;
+    if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced
         ENG_CALL(dist_pack(st, stats, rank_ray, hit_idx, x.xi32 + x.in_off()));
         ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), kDistWordsPerRank, st,
@@ -404,7 +406,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         ENG_CALL(dist_smax(st, x.xi32 + x.smax_all_off(), x.world, stats));
     } else {
         ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
-                                  nullptr, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
+                                  noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
     if (hipMemcpyAsync(q.host_stats, stats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -422,7 +424,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
 // psvo_map_query prepared for exactly this batch, or a fresh query enqueued
 // on `st` itself.
 int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, const float *rays_o,
-               const float *rays_d, uint64_t seed, const char *who, QuerySet **out) {
+               const float *rays_d, uint64_t seed, const char *who, QuerySet **out, const float *noise = nullptr) {
     if (e->q_count > 0) {
         QuerySet &q = e->qs[e->q_head];
         if (q.R != R || q.ro != rays_o || q.rd != rays_d || q.seed != seed)
@@ -434,7 +436,7 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
         return PSVO_OK;
     }
     QuerySet &q = e->qs[e->q_head];
-    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, seed, who));
+    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, seed, who, noise));
     *out = &q;
     return PSVO_OK;
 }
@@ -643,19 +645,47 @@ int loss_backward(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
 
 }  // namespace
 
-extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
-                             const float *rays_o, const float *rays_d, const float *gt_rgb, const float *gt_depth,
-                             uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
+namespace {
+// the keyframe poses' part of an iteration (psvo_map_step_frames): per-frame
+// gradient from the rays' grad_o / grad_d, then each optimised pose's Adam
+int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const psvo_map_frames *fr,
+                  const Render &q, const float *grad_od, int64_t R) {
+    int rc = PSVO_OK;
+    float *pg = fr->pose_grad;
+    if (!pg) {
+        ENG_BUF(float, gbuf, kPoseGrad, (size_t)fr->n_frames * 8 * sizeof(float));
+        pg = gbuf;
+    }
+    ENG_CALL(psvo_pose_grad_frames(st, fr->n_frames, fr->rays_per_frame, q.r_hit, q.rank_ray, fr->dirs_cam, grad_od,
+                                   grad_od + R * 3, fr->poses, pg));
+    for (int f = 0; f < fr->n_frames; ++f) {
+        if (fr->pose_step[f] < 1) continue;  // stamp 0 / update_pose False: no optimiser (render_helpers.py:594-596)
+        float *p = fr->poses + f * 6;
+        float *m = fr->pose_m + f * 6;
+        float *v = fr->pose_v + f * 6;
+        const float *g = pg + f * 8;
+        int64_t n6 = 6;
+        int zero = 0;
+        double lr = fr->lr_pose;
+        ENG_CALL(adam_launch(st, 1, &p, &g, &m, &v, &n6, &lr, d->beta1, d->beta2, d->eps, 0.0, fr->pose_step[f], &zero));
+    }
+    return PSVO_OK;
+}
+}  // namespace
+
+static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
+                         const float *rays_d, const float *gt_rgb, const float *gt_depth, const float *noise,
+                         uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out,
+                         const psvo_map_frames *fr) {
     PSVO_REQUIRE(e && d && rays_o && rays_d && gt_rgb && gt_depth && loss_out, "map_step: null argument");
     PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "map_step: bad sizes");
     PSVO_REQUIRE(d->width == 128 || d->width == 256, "map_step: decoder width %d unsupported (fused: 128, 256)",
                  d->width);
-    hipStream_t st = as_stream(stream);
     int rc = PSVO_OK;
     const int64_t R = n_rays;
     Render q;
     QuerySet *qset = nullptr;
-    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset));
+    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise));
     QueryGuard guard{e, st, qset};
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
@@ -746,7 +776,7 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
         return PSVO_OK;
     }
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(mlp_bwd(stream, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
+    ENG_CALL(mlp_bwd(st, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
@@ -769,12 +799,39 @@ extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
     ENG_CALL(guard.release());
+    if (fr) ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R));
     // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step));
         e->grads_clean = true;
     }
     return PSVO_OK;
+}
+
+extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
+                             const float *rays_o, const float *rays_d, const float *gt_rgb, const float *gt_depth,
+                             uint64_t seed, int64_t adam_step, int flags, float *loss_out, int *stats_out) {
+    return map_step_impl(e, as_stream(stream), d, n_rays, rays_o, rays_d, gt_rgb, gt_depth, nullptr, seed, adam_step,
+                         flags, loss_out, stats_out, nullptr);
+}
+
+extern "C" int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *fr,
+                                    const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,
+                                    int64_t adam_step, int flags, float *loss_out, int *stats_out) {
+    PSVO_REQUIRE(e && d && fr && fr->dirs_cam && fr->poses && fr->pose_step, "map_step_frames: null argument");
+    PSVO_REQUIRE(fr->n_frames > 0 && fr->rays_per_frame > 0, "map_step_frames: bad sizes");
+    PSVO_REQUIRE(!e->x.on(), "map_step_frames: keyframe pose updates are single-GPU");
+    PSVO_REQUIRE(e->q_count == 0, "map_step_frames: rays come from this step's poses (no queued query)");
+    for (int f = 0; f < fr->n_frames; ++f)
+        PSVO_REQUIRE(fr->pose_step[f] < 1 || (fr->pose_m && fr->pose_v), "map_step_frames: pose Adam needs m / v");
+    hipStream_t st = as_stream(stream);
+    int rc = PSVO_OK;
+    const int64_t R = (int64_t)fr->n_frames * fr->rays_per_frame;
+    ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
+    ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
+    ENG_CALL(psvo_pose_rays_frames(st, R, fr->rays_per_frame, fr->poses, fr->dirs_cam, rays_o, rays_d));
+    return map_step_impl(e, st, d, R, rays_o, rays_d, gt_rgb, gt_depth, noise, seed, adam_step, flags, loss_out,
+                         stats_out, fr);
 }
 
 extern "C" int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,

@@ -79,6 +79,64 @@ __global__ __launch_bounds__(256) void k_pose_rays(int64_t n, const float *__res
 
 constexpr int kGradThreads = 1024;
 
+// bundle_adjust_frames (render_helpers.py:620-640): frame f's rays are
+// [f·rpf, (f+1)·rpf), rays_d = dirs @ R(w_f)ᵀ, rays_o = t_f
+__global__ __launch_bounds__(256) void k_pose_rays_frames(int64_t n, int64_t rpf, const float *__restrict__ poses,
+                                                          const float *__restrict__ dirs, float *__restrict__ rays_o,
+                                                          float *__restrict__ rays_d) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float *pose = poses + (r / rpf) * 6;
+    Rot q;
+    rotation(pose, q);
+    const float d0 = dirs[r * 3 + 0], d1 = dirs[r * 3 + 1], d2 = dirs[r * 3 + 2];
+    for (int j = 0; j < 3; ++j) {
+        rays_d[r * 3 + j] = d0 * q.R[j][0] + d1 * q.R[j][1] + d2 * q.R[j][2];
+        rays_o[r * 3 + j] = pose[j];
+    }
+}
+
+// dL/d[t | w] of one pose from Σ grad_o (tot[0..2]) and G = Σ grad_d ⊗ dir (tot[3..11])
+__device__ void pose_chain(const float *__restrict__ pose, const float (&tot)[12], float *__restrict__ grad);
+
+// Σ over the hit rays of ray range [ray_lo, ray_hi) (hit ranks keep ray order,
+// so they are one contiguous run of rank_ray) → pose gradient; block = frame
+__global__ __launch_bounds__(kGradThreads) void k_pose_grad_frames(int64_t r_hit, const int *__restrict__ rank_ray,
+                                                                   int64_t rpf, const float *__restrict__ dirs,
+                                                                   const float *__restrict__ g_o,
+                                                                   const float *__restrict__ g_d,
+                                                                   const float *__restrict__ poses,
+                                                                   float *__restrict__ grads) {
+    __shared__ float part[kGradThreads / 64][12];
+    const int64_t lo = blockIdx.x * rpf, hi = lo + rpf;
+    float acc[12] = {};
+    for (int64_t r = threadIdx.x; r < r_hit; r += kGradThreads) {
+        const int64_t row = rank_ray[r];
+        if (row < lo || row >= hi) continue;
+        float dir[3], gd[3];
+        for (int j = 0; j < 3; ++j) {
+            acc[j] += g_o[row * 3 + j];
+            gd[j] = g_d[row * 3 + j];
+            dir[j] = dirs[row * 3 + j];
+        }
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) acc[3 + j * 3 + k] += gd[j] * dir[k];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = 0; i < 12; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+        if (lane == 0) part[wv][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float tot[12] = {};
+    for (int w = 0; w < kGradThreads / 64; ++w)
+        for (int i = 0; i < 12; ++i) tot[i] += part[w][i];
+    pose_chain(poses + blockIdx.x * 6, tot, grads + blockIdx.x * 8);
+}
+
 __global__ __launch_bounds__(kGradThreads) void k_pose_grad(int64_t r_hit, const int *__restrict__ rank_ray,
                                                             const float *__restrict__ dirs,
                                                             const float *__restrict__ g_o,
@@ -109,6 +167,10 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_grad(int64_t r_hit, const
     float tot[12] = {};
     for (int w = 0; w < kGradThreads / 64; ++w)
         for (int i = 0; i < 12; ++i) tot[i] += part[w][i];
+    pose_chain(pose, tot, grad);
+}
+
+__device__ void pose_chain(const float *__restrict__ pose, const float (&tot)[12], float *__restrict__ grad) {
     Rot q;
     rotation(pose, q);
     const float(&G)[3][3] = *reinterpret_cast<const float(*)[3][3]>(tot + 3);
@@ -149,6 +211,25 @@ extern "C" int psvo_pose_rays(void *stream, int64_t n, const float *pose, const 
     hipLaunchKernelGGL(k_pose_rays, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, pose, dirs, rays_o,
                        rays_d);
     return check_launch("pose_rays");
+}
+
+extern "C" int psvo_pose_rays_frames(void *stream, int64_t n, int64_t rays_per_frame, const float *poses,
+                                     const float *dirs, float *rays_o, float *rays_d) {
+    PSVO_REQUIRE(n > 0 && rays_per_frame > 0 && n % rays_per_frame == 0, "pose_rays_frames: bad sizes");
+    PSVO_REQUIRE(poses && dirs && rays_o && rays_d, "pose_rays_frames: null pointer");
+    hipLaunchKernelGGL(k_pose_rays_frames, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, rays_per_frame,
+                       poses, dirs, rays_o, rays_d);
+    return check_launch("pose_rays_frames");
+}
+
+extern "C" int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_per_frame, int64_t r_hit,
+                                     const int *rank_ray, const float *dirs, const float *g_o, const float *g_d,
+                                     const float *poses, float *grads) {
+    PSVO_REQUIRE(n_frames > 0 && rays_per_frame > 0 && r_hit >= 0, "pose_grad_frames: bad sizes");
+    PSVO_REQUIRE(rank_ray && dirs && g_o && g_d && poses && grads, "pose_grad_frames: null pointer");
+    hipLaunchKernelGGL(k_pose_grad_frames, dim3(n_frames), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray,
+                       rays_per_frame, dirs, g_o, g_d, poses, grads);
+    return check_launch("pose_grad_frames");
 }
 
 extern "C" int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,

@@ -71,6 +71,9 @@ _SIGNATURES = {
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
     "psvo_map_query": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _u64]),
+    "psvo_map_step_frames": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
+    "psvo_pose_rays_frames": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "psvo_pose_grad_frames": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _u64, _i64, _i32, _vp, _vp,
                                _vp]),
     "psvo_pose_rays": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),

@@ -30,6 +30,12 @@ class MapDesc(ctypes.Structure):
                 ("grad_flat", _vp)]
 
 
+class MapFrames(ctypes.Structure):
+    """Mirror of psvo_map_frames (include/psvo.h)."""
+    _fields_ = [("n_frames", _i32), ("rays_per_frame", _i64), ("dirs_cam", _vp), ("poses", _vp), ("pose_m", _vp),
+                ("pose_v", _vp), ("pose_step", _vp), ("lr_pose", _f64), ("pose_grad", _vp)]
+
+
 def _lib():
     return L.lib()
 
@@ -84,6 +90,83 @@ class MappingEngine:
         if not h:
             raise L.PsvoError("psvo_engine_new failed")
         self.handle = _vp(h)
+
+    def bind_adam(self, emb_m, emb_v, dec_m, dec_v):
+        """Use external Adam moments (e.g. the state tensors of the caller's
+        torch / psvo Adam optimisers, so that the engine continues their
+        state): f32 tensors shaped like the embeddings / fused decoder params."""
+        for t, ref in zip([emb_m, emb_v] + list(dec_m) + list(dec_v), [self.emb] * 2 + self.params * 2):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.shape == ref.shape):
+                raise RuntimeError("MappingEngine.bind_adam: moments must match the parameters (contiguous f32 CUDA)")
+        self.emb_m, self.emb_v, self.dec_m, self.dec_v = emb_m, emb_v, list(dec_m), list(dec_v)
+        d = self.desc
+        d.emb_m, d.emb_v = emb_m.data_ptr(), emb_v.data_ptr()
+        for i in range(10):
+            d.dec_m[i] = self.dec_m[i].data_ptr()
+            d.dec_v[i] = self.dec_v[i].data_ptr()
+
+    def set_lr(self, lr_emb=None, lr_dec=None):
+        if lr_emb is not None:
+            self.desc.lr_emb = float(lr_emb)
+        if lr_dec is not None:
+            self.desc.lr_dec = float(lr_dec)
+
+    def step_frames(self, dirs_cam, rays_per_frame, poses, pose_m, pose_v, pose_steps, lr_pose, rgb, depth, seed,
+                    noise=None, adam_step=None, apply_adam=True, pose_grad=None):
+        """One bundle_adjust_frames iteration with keyframe pose updates
+        (psvo_map_step_frames): rays from the current poses [F, 6] (frame f
+        owns rows [f·rays_per_frame, (f+1)·rays_per_frame) of dirs_cam),
+        render + loss + backward, Adam on embeddings / decoder and on every
+        pose with pose_steps[f] ≥ 1 (its Adam step number; 0 = fixed pose).
+        poses / pose_m / pose_v are updated in place.  Returns the loss."""
+        if self._queued:
+            raise RuntimeError("MappingEngine.step_frames: a query() is queued (rays here come from the poses)")
+        dirs = dirs_cam.reshape(-1, 3).float().contiguous()
+        n_f = poses.shape[0]
+        for t in (poses, pose_m, pose_v):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == (n_f, 6)):
+                raise RuntimeError("MappingEngine.step_frames: poses / moments must be contiguous f32 CUDA [F, 6]")
+        if dirs.shape[0] != n_f * int(rays_per_frame):
+            raise RuntimeError("MappingEngine.step_frames: dirs_cam must hold F x rays_per_frame rows")
+        gt_rgb = rgb.reshape(-1, 3).float().contiguous()
+        gt_d = depth.reshape(-1).float().contiguous()
+        steps = (ctypes.c_int64 * n_f)(*[int(x) for x in pose_steps])
+        fr = MapFrames()
+        fr.n_frames, fr.rays_per_frame = n_f, int(rays_per_frame)
+        fr.dirs_cam, fr.poses, fr.pose_m, fr.pose_v = dirs.data_ptr(), poses.data_ptr(), pose_m.data_ptr(), \
+            pose_v.data_ptr()
+        fr.pose_step = ctypes.cast(steps, ctypes.c_void_p)
+        fr.lr_pose = float(lr_pose)
+        fr.pose_grad = pose_grad.data_ptr() if pose_grad is not None else None
+        nz = None
+        if noise is not None:
+            nz = noise.to(device=dirs.device, dtype=torch.float32).contiguous()
+            self._check_noise(nz, dirs, int(rays_per_frame), poses)
+        self.step_no = self.step_no + 1 if adam_step is None else int(adam_step)
+        rc = _lib().psvo_map_step_frames(self.handle, L.stream_of(dirs.device), ctypes.addressof(self.desc),
+                                         ctypes.addressof(fr), gt_rgb.data_ptr(), gt_d.data_ptr(),
+                                         nz.data_ptr() if nz is not None else None, int(seed), self.step_no,
+                                         0 if apply_adam else 1, self.loss_out.data_ptr(),
+                                         ctypes.addressof(self.stats))
+        if rc != 0:
+            raise self._error("psvo_map_step_frames", rc)
+        return self.loss_out[0]
+
+    def _check_noise(self, nz, dirs, rpf, poses):
+        """Injected sampler noise must have the layout this batch's sampler
+        reads ([200, K', max_steps], voxel_helpers.py:303-328): one synchronous
+        intersection of the batch's rays (a test / replay path only)."""
+        from .voxel_helpers import _intersect_sorted
+        ro = torch.empty_like(dirs)
+        rd = torch.empty_like(dirs)
+        L.call("psvo_pose_rays_frames", L.stream_of(dirs.device), dirs.shape[0], rpf, poses, dirs, ro, rd)
+        d = self.desc
+        q = _intersect_sorted(ro, rd, self.centres, self.structure, d.voxel_size, d.max_distance, d.step_size)
+        st = q["stats"].cpu()
+        P, r_hit, max_ceil = int(st[0]), int(st[1]), int(st[2])
+        want = (200, (r_hit + 199) // 200, max_ceil + P)
+        if tuple(nz.shape) != want:
+            raise ValueError(f"step_frames: noise must be {list(want)} for this batch, got {list(nz.shape)}")
 
     def set_exchange(self, exchange):
         """Data-parallel mode (psvo.dist.EngineExchange): every step computes

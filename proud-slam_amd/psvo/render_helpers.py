@@ -344,11 +344,168 @@ def eval_points(sdf_network, map_states, sampled_xyz, sampled_idx, voxel_size):
     return sdf_network.get_values(fi["emb"]).reshape(-1, 4)[:, :3].detach().cpu()
 
 
+# ---------------------------------------------------------------------------
+# bundle_adjust_frames on the native engine (psvo_map_step_frames): one C
+# call per iteration — rays from the keyframes' current poses, render, loss,
+# backward, Adam(embeddings), Adam(decoder) and every keyframe's pose Adam —
+# continuing the caller's optimisers' state (exp_avg / exp_avg_sq / step are
+# read from and written back to them), so the drop-in loop and this path are
+# interchangeable mid-run.
+_ENGINES = {}
+
+
+def _is_adam(opt):
+    from .optim import Adam as PsvoAdam
+    if not isinstance(opt, (torch.optim.Adam, PsvoAdam)) or len(opt.param_groups) != 1:
+        return False
+    g = opt.param_groups[0]
+    return (not g.get("amsgrad", False) and g.get("weight_decay", 0.0) == 0.0 and not g.get("maximize", False)
+            and not g.get("capturable", False) and not g.get("differentiable", False))
+
+
+def _adam_state(opt, p):
+    st = opt.state[p]
+    if len(st) == 0:  # as Adam's lazy init
+        st["step"] = torch.tensor(0.0)
+        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    return st
+
+
+def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim, model_optim,
+                resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays):
+    """The cached MappingEngine for this map / decoder, or None when the
+    call is outside what the native iteration covers (then the autograd loop
+    below runs — the same kernels)."""
+    from .engine import MappingEngine
+    emb = map_states.get("voxel_vertex_emb")
+    if resnet is not None or resnet_optim is not None or model_optim is None or embed_optim is None:
+        return None
+    if not (_is_adam(embed_optim) and _is_adam(model_optim)):
+        return None
+    if not (isinstance(emb, torch.Tensor) and emb.is_cuda and emb.dtype == torch.float32 and emb.is_contiguous()):
+        return None
+    if [p for p in embed_optim.param_groups[0]["params"]] != [emb]:
+        return None
+    params = sdf_network.fused_params() if hasattr(sdf_network, "fused_params") else None
+    if params is None or not sdf_network.can_fuse(emb[:1]) or list(model_optim.param_groups[0]["params"]) != params:
+        return None
+    ge, gm = embed_optim.param_groups[0], model_optim.param_groups[0]
+    if tuple(ge["betas"]) != tuple(gm["betas"]) or ge["eps"] != gm["eps"]:
+        return None
+    if not all(hasattr(loss_criteria, a) for a in ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight",
+                                                   "truncation", "max_dpeth")):
+        return None
+    for kf in keyframe_graph:
+        if not (hasattr(kf, "sample_rays") and hasattr(kf, "rays_d") and getattr(kf, "pose", None) is not None):
+            return None
+    key = (emb.data_ptr(), emb.shape[0], id(sdf_network), map_states["voxel_center_xyz"].data_ptr(),
+           map_states["voxel_center_xyz"].shape[0], map_states["voxel_structure"].data_ptr(),
+           map_states["voxel_vertex_idx"].data_ptr(), float(voxel_size), float(step_size), float(truncation),
+           float(max_distance))
+    eng = _ENGINES.get(key)
+    if eng is None:
+        if len(_ENGINES) > 4:
+            _ENGINES.clear()
+        crit = {"rgb_weight": loss_criteria.rgb_weight, "depth_weight": loss_criteria.depth_weight,
+                "fs_weight": loss_criteria.fs_weight, "sdf_weight": loss_criteria.sdf_weight}
+        eng = MappingEngine(map_states, sdf_network, voxel_size, step_size, truncation=loss_criteria.truncation,
+                            max_distance=max_distance, criteria=crit, max_depth=loss_criteria.max_dpeth,
+                            betas=tuple(ge["betas"]), eps=ge["eps"])
+        _ENGINES[key] = eng
+    return eng
+
+
+def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays, num_iterations, update_pose,
+                          noise):
+    emb = eng.emb
+    params = eng.params
+    st_e = _adam_state(embed_optim, emb)
+    st_d = [_adam_state(model_optim, p) for p in params]
+    steps = {int(st_e["step"].item())} | {int(st["step"].item()) for st in st_d}
+    if len(steps) != 1:
+        return False  # parameters at different Adam steps: the engine steps them together
+    eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
+                  [st["exp_avg_sq"] for st in st_d])
+    eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
+    adam_step = steps.pop()
+    dev = emb.device
+    # keyframe poses [F, 6] and their Adam state on the device
+    kfs = list(keyframe_graph)
+    upd = [bool(kf.stamp != 0 and update_pose and getattr(kf, "optim", None) is not None) for kf in kfs]
+    pose_params = [kf.pose.data for kf in kfs]
+    poses = torch.stack([p.detach().to(dev, torch.float32) for p in pose_params]).contiguous()
+    pm = torch.zeros_like(poses)
+    pv = torch.zeros_like(poses)
+    pstep = [0] * len(kfs)
+    lr_pose = None
+    for f, kf in enumerate(kfs):
+        if not upd[f]:
+            continue
+        if not _is_adam(kf.optim):
+            return False
+        st = _adam_state(kf.optim, pose_params[f])
+        pm[f].copy_(st["exp_avg"].reshape(6))
+        pv[f].copy_(st["exp_avg_sq"].reshape(6))
+        pstep[f] = int(st["step"].item())
+        lr = kf.optim.param_groups[0]["lr"]
+        if lr_pose is not None and lr != lr_pose:
+            return False
+        lr_pose = lr
+        if tuple(kf.optim.param_groups[0]["betas"]) != tuple(embed_optim.param_groups[0]["betas"]):
+            return False
+    for it in range(num_iterations):
+        dirs, rgbs, depths = [], [], []
+        for kf in kfs:
+            kf.sample_rays(N_rays)
+            idx = getattr(kf, "sample_idx", None)
+            if idx is None:
+                idx = kf.sample_mask.reshape(-1).nonzero().squeeze(1)
+            idx = idx.to(dev)
+            if idx.numel() != N_rays:
+                raise RuntimeError("bundle_adjust_frames: sample_rays gave %d rays, expected %d" % (idx.numel(), N_rays))
+            dirs.append(kf.rays_d.reshape(-1, 3).to(dev)[idx])
+            rgbs.append(kf.rgb.reshape(-1, 3).to(dev)[idx])
+            depths.append(kf.depth.reshape(-1).to(dev)[idx])
+        nz = noise(it) if callable(noise) else None
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if nz is None else 0
+        adam_step += 1
+        cur = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
+        eng.step_frames(torch.cat(dirs), N_rays, poses, pm, pv, cur, lr_pose or 0.0, torch.cat(rgbs),
+                        torch.cat(depths), seed, noise=nz, adam_step=adam_step)
+        pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur)]
+    # write back: optimiser steps, pose parameters and their Adam state
+    with torch.no_grad():
+        for st in [st_e] + st_d:
+            st["step"].fill_(float(adam_step))
+        for f, kf in enumerate(kfs):
+            if not upd[f]:
+                continue
+            pose_params[f].copy_(poses[f].to(pose_params[f].device).reshape(pose_params[f].shape))
+            st = kf.optim.state[pose_params[f]]
+            st["exp_avg"].copy_(pm[f].to(st["exp_avg"].device).reshape(st["exp_avg"].shape))
+            st["exp_avg_sq"].copy_(pv[f].to(st["exp_avg_sq"].device).reshape(st["exp_avg_sq"].shape))
+            st["step"].fill_(float(pstep[f]))
+    return True
+
+
 def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, voxel_size, step_size,
                          N_rays=512, num_iterations=10, truncation=0.1, max_voxel_hit=10, max_distance=10,
                          learning_rate=[1e-2, 5e-3], embed_optim=None, model_optim=None, resnet_optim=None,
-                         update_pose=True):
-    """render_helpers.py:559-676 — mapping's render-and-optimise loop."""
+                         update_pose=True, noise=None, use_engine=True):
+    """render_helpers.py:559-676 — mapping's render-and-optimise loop.
+
+    Runs on the native engine (one psvo_map_step_frames call per iteration)
+    whenever the optimisers are plain Adam over the map embeddings / fused
+    decoder and no point-feature network is attached; otherwise the autograd
+    loop below (same kernels).  `noise` (not in the reference signature): a
+    callable iteration → sampler noise [200, K', max_steps], for parity tests."""
+    if use_engine:
+        eng = _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim, model_optim,
+                          resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays)
+        if eng is not None and _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
+                                                     num_iterations, update_pose, noise):
+            return
     optimizers = [embed_optim]
     if model_optim is not None:
         optimizers += [model_optim]
@@ -376,7 +533,8 @@ def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_c
         rgb_samples = torch.cat(rgb_samples, dim=0).unsqueeze(0)
         depth_samples = torch.cat(depth_samples, dim=0).unsqueeze(0)
         final_outputs = render_rays(rays_o, rays_d, map_states, sdf_network, resnet, step_size, voxel_size,
-                                    truncation, max_voxel_hit, max_distance)
+                                    truncation, max_voxel_hit, max_distance,
+                                    noise=noise(_) if callable(noise) else None)
         loss, _ = loss_criteria(final_outputs, (rgb_samples, depth_samples))
         for optim in optimizers:
             optim.zero_grad()

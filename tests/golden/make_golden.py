@@ -15,6 +15,9 @@ tensorboardX) are replaced by empty stubs, torch.Tensor.cuda by identity
 a temp dir.  Noise drawn inside InverseCDFRaySampling is recorded so the
 build can inject the same noise.
 
+BA_room0.npz: the reference's bundle_adjust_frames (3 keyframes, 3
+iterations, pose Adam on the non-first keyframes) — see run_ba_case.
+
 M_mesh_A.npz: the reference's get_scores / eval_points (mesh extraction's
 lattice scores and vertex colours) on the A octree's first 40 SURFACE voxels.
 
@@ -246,6 +249,97 @@ def run_mesh_case(rh, nrgbd):
     return rec
 
 
+def run_ba_case(rh, nrgbd, crit_mod, noise_log):
+    """The reference bundle_adjust_frames (render_helpers.py:559-676): 3
+    keyframes (stamps 0, 5, 9 — the first pose stays fixed, :594-596) of a
+    room0-shaped scene at a reduced resolution, 160 rays per frame, 3
+    iterations, Adam(embeddings) / Adam(decoder) lr 5e-3 and each keyframe's
+    pose Adam lr 1e-3 (frame.py:27).  Stub keyframes carry the reference's own
+    se3pose.OptimizablePose and replay recorded pixel samples; the sampler
+    noise of every iteration is recorded."""
+    import importlib
+    se3 = importlib.import_module("se3pose")
+    scene = syn.room0()
+    vox = syn.surface_voxels(scene, seed=0)
+    voxels, children, features = _octree(vox, 256)
+    n_nodes = voxels.shape[0]
+    Ts = syn.camera_poses(scene, 3, seed=17)
+    frames = [syn.SyntheticFrame(scene, T, scale=0.06, seed=100 + i, device="cpu") for i, T in enumerate(Ts)]
+    n_rays, iters = 160, 3
+    gen = torch.Generator().manual_seed(5)
+    picks = [[torch.randperm(f.h * f.w, generator=gen)[:n_rays].sort().values for f in frames] for _ in range(iters)]
+
+    class KF:
+        def __init__(self, i, fr, T, stamp):
+            self.stamp = stamp
+            self.rays_d, self.rgb, self.depth = fr.rays_d, fr.rgb, fr.depth
+            self.h, self.w = fr.h, fr.w
+            self.pose = se3.OptimizablePose.from_matrix(torch.tensor(T, dtype=torch.float32))
+            self.optim = torch.optim.Adam(self.pose.parameters(), lr=1e-3)
+            self.i, self.calls = i, 0
+
+        def get_pose(self):
+            return self.pose.matrix()
+
+        def sample_rays(self, n):
+            idx = picks[self.calls][self.i]
+            self.calls += 1
+            m = torch.zeros(self.h * self.w, dtype=torch.bool)
+            m[idx] = True
+            self.sample_mask = m.view(self.h, self.w)
+
+    kfs = [KF(i, fr, T, st) for i, (fr, T, st) in enumerate(zip(frames, Ts, (0, 5, 9)))]
+    pose0 = np.stack([kf.pose.data.detach().numpy().copy() for kf in kfs])
+    torch.manual_seed(77)
+    emb0 = torch.randn(n_nodes, 16) * 0.3
+    emb = emb0.clone().requires_grad_(True)
+    dec = nrgbd.Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none", multires=0)
+    dec0 = {k: v.detach().clone().numpy() for k, v in dec.state_dict().items()}
+    vt = torch.from_numpy(voxels)
+    centres = (vt[:, :3] + vt[:, -1:] / 2) * 0.2
+    structure = torch.cat([torch.from_numpy(children), vt[:, -1:]], -1).int()
+    map_states = {"voxel_vertex_idx": torch.from_numpy(features), "voxel_center_xyz": centres.float(),
+                  "voxel_structure": structure, "voxel_vertex_emb": emb}
+    args = types.SimpleNamespace(criteria={**O.REPLICA_CRITERIA, "sdf_truncation": 0.1},
+                                 data_specs={"max_depth": 10.0})
+    crit = crit_mod.Criterion(args)
+    losses = []
+
+    def loss_rec(outputs, obs, **kw):
+        loss, parts = crit(outputs, obs, **kw)
+        losses.append(float(loss))
+        return loss, parts
+    embed_optim = torch.optim.Adam([emb], lr=5e-3)
+    model_optim = torch.optim.Adam(dec.parameters(), lr=5e-3)
+    noise_log.clear()
+    torch.manual_seed(31)
+    rh.bundle_adjust_frames(kfs, map_states, dec, None, loss_rec, 0.2, 0.02, N_rays=n_rays, num_iterations=iters,
+                            embed_optim=embed_optim, model_optim=model_optim, update_pose=True)
+    assert len(noise_log) == iters, len(noise_log)
+    emb1 = emb.detach()
+    changed = torch.nonzero((emb1 != emb0).any(-1)).squeeze(1)
+    rec = dict(voxels=voxels, children=children, features=features, centres=centres.numpy(),
+               structure=structure.numpy(), n_nodes=np.int64(n_nodes), emb_seed=np.int64(77), emb_std=np.float32(0.3),
+               emb0_checksum=np.float64(emb0.double().sum()), pose0=pose0, stamps=np.array([0, 5, 9], np.int64),
+               poses1=np.stack([kf.pose.data.detach().numpy() for kf in kfs]),
+               step_size=np.float32(0.02), n_rays=np.int64(n_rays), iters=np.int64(iters),
+               losses=np.array(losses, np.float32), emb_changed_rows=changed.numpy().astype(np.int64),
+               emb1_changed=emb1[changed].numpy())
+    for i, fr in enumerate(frames):
+        rec[f"frame{i}.rays_d"] = fr.rays_d.numpy()
+        rec[f"frame{i}.rgb"] = fr.rgb.numpy()
+        rec[f"frame{i}.depth"] = fr.depth.numpy()
+    for it in range(iters):
+        rec[f"noise{it}"] = noise_log[it].numpy()
+        for i in range(len(frames)):
+            rec[f"pick{it}.{i}"] = picks[it][i].numpy()
+    for k, v in dec0.items():
+        rec["dec0." + k] = v
+    for k, v in dec.state_dict().items():
+        rec["dec1." + k] = v.numpy()
+    return rec
+
+
 def main():
     noise_log = []
     _install_stubs(noise_log)
@@ -262,6 +356,11 @@ def main():
                       f"R_hit={int(rec['hits'].sum())} P={rec['hit_idx'].shape[-1]} S={rec['z_vals'].shape[-1]} "
                       f"loss={float(rec['loss']):.6f} -> {os.path.relpath(path, REPO)} "
                       f"({os.path.getsize(path) // 1024} KiB)")
+            rec = run_ba_case(rh, nrgbd, crit_mod, noise_log)
+            path = os.path.join(OUT_DIR, "BA_room0.npz")
+            np.savez_compressed(path, **rec)
+            print(f"BA_room0: nodes={int(rec['n_nodes'])} losses={rec['losses'].tolist()} "
+                  f"-> {os.path.relpath(path, REPO)} ({os.path.getsize(path) // 1024} KiB)")
             rec = run_mesh_case(rh, nrgbd)
             path = os.path.join(OUT_DIR, "M_mesh_A.npz")
             np.savez_compressed(path, **rec)

@@ -1,0 +1,92 @@
+"""bundle_adjust_frames (render_helpers.py:559-676) against the reference's
+own run (tests/golden/BA_room0.npz): 3 keyframes (stamp 0
+fixed, two pose-optimised), 160 rays each, 3 iterations with the recorded
+pixel picks and sampler noise, torch Adam on embeddings / decoder / poses.
+Both the native engine path (psvo_map_step_frames, one call per iteration,
+pose Adam on the device) and the autograd loop are checked: final keyframe
+poses, embedding rows and decoder parameters (tolerance for Adam's
+amplification of ulp-level gradient differences: tests/test_oracle_golden.py
+adam_close), and the optimisers' state written back (step counts)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from test_oracle_golden import adam_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class _KF:
+    """Keyframe stand-in with the fields bundle_adjust_frames reads (frame.py:10-96)."""
+
+    def __init__(self, i, g, picks, stamp):
+        from psvo.pose import OptimizablePose
+        self.stamp = int(stamp)
+        self.rays_d = torch.from_numpy(g[f"frame{i}.rays_d"]).to(DEV)
+        self.rgb = torch.from_numpy(g[f"frame{i}.rgb"]).to(DEV)
+        self.depth = torch.from_numpy(g[f"frame{i}.depth"]).to(DEV)
+        self.h, self.w = self.depth.shape
+        self.pose = OptimizablePose(torch.from_numpy(g["pose0"][i]).to(DEV))
+        self.optim = torch.optim.Adam(self.pose.parameters(), lr=1e-3)
+        self.i, self.picks, self.calls = i, picks, 0
+
+    def get_pose(self):
+        return self.pose.matrix()
+
+    def sample_rays(self, n):
+        idx = torch.from_numpy(self.picks[self.calls][self.i]).to(DEV)
+        self.calls += 1
+        m = torch.zeros(self.h * self.w, dtype=torch.bool, device=DEV)
+        m[idx] = True
+        self.sample_mask = m.view(self.h, self.w)
+
+
+@pytest.mark.parametrize("use_engine", [True, False])
+def test_bundle_adjust_matches_reference(use_engine):
+    import types
+    from psvo import render_helpers as RH
+    from psvo.criterion import Criterion
+    from psvo.decoder import Decoder
+    g = load_golden("BA_room0")
+    n = int(g["n_nodes"])
+    torch.manual_seed(int(g["emb_seed"]))
+    emb0 = torch.randn(n, 16) * float(g["emb_std"])
+    emb = emb0.clone().to(DEV).requires_grad_(True)
+    ms = {"voxel_vertex_idx": torch.from_numpy(g["features"]).to(DEV),
+          "voxel_center_xyz": torch.from_numpy(g["centres"]).to(DEV),
+          "voxel_structure": torch.from_numpy(g["structure"]).to(DEV), "voxel_vertex_emb": emb}
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("dec0.")})
+    iters = int(g["iters"])
+    picks = [[g[f"pick{it}.{i}"] for i in range(3)] for it in range(iters)]
+    noises = [torch.from_numpy(g[f"noise{it}"]) for it in range(iters)]
+    kfs = [_KF(i, g, picks, st) for i, st in enumerate(g["stamps"])]
+    crit = Criterion(types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0,
+                                                     "fs_weight": 10.0, "sdf_truncation": 0.1},
+                                           data_specs={"max_depth": 10.0}))
+    eo = torch.optim.Adam([emb], lr=5e-3)
+    mo = torch.optim.Adam(dec.parameters(), lr=5e-3)
+    RH._ENGINES.clear()
+    RH.bundle_adjust_frames(kfs, ms, dec, None, crit, 0.2, float(g["step_size"]), N_rays=int(g["n_rays"]),
+                            num_iterations=iters, embed_optim=eo, model_optim=mo, update_pose=True,
+                            noise=lambda it: noises[it], use_engine=use_engine)
+    torch.cuda.synchronize()
+    assert (len(RH._ENGINES) == 1) == use_engine  # the native path ran (or not)
+    poses = np.stack([kf.pose.data.detach().cpu().numpy() for kf in kfs])
+    np.testing.assert_allclose(poses, g["poses1"], rtol=0, atol=1e-5)
+    assert np.array_equal(poses[0], g["pose0"][0])  # stamp 0: no pose optimiser
+    rows = torch.from_numpy(g["emb_changed_rows"])
+    e1 = emb.detach().cpu()
+    adam_close(e1[rows].numpy(), g["emb1_changed"], tight=1e-5)
+    untouched = torch.ones(n, dtype=torch.bool)
+    untouched[rows] = False
+    assert torch.equal(e1[untouched], emb0[untouched])
+    for k, v in dec.state_dict().items():
+        adam_close(v.cpu().numpy(), g["dec1." + k], tight=1e-5)
+    # the optimisers' state continues from where the loop left it
+    assert int(eo.state[emb]["step"]) == iters
+    assert all(int(mo.state[p]["step"]) == iters for p in dec.parameters())
+    assert int(kfs[1].optim.state[kfs[1].pose.data]["step"]) == iters
+    assert len(kfs[0].optim.state) == 0
