@@ -52,12 +52,18 @@ def parse():
     ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--autograd", action="store_true",
-                    help="headline number from the drop-in autograd path instead of the native engine")
+    ap.add_argument("--path", choices=("ba", "step", "autograd"), default="ba",
+                    help="headline: ba = the reference's bundle_adjust_frames API (keyframe poses optimised too; "
+                         "dispatches to the native engine), step = the engine's psvo_map_step on pre-built "
+                         "world-space ray batches, autograd = render_rays + Criterion + backward + Adam")
+    ap.add_argument("--autograd", action="store_true", help="same as --path autograd")
     ap.add_argument("--exact-global-loss", action="store_true",
                     help="(kept for compatibility: N>1 always computes the union-batch loss)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     a = ap.parse_args()
+    if a.autograd:
+        a.path = "autograd"
+    a.autograd = a.path == "autograd"
     big = a.scene in ("scannet0000", "multiroom")  # configs/scannet/scannet.yaml:17, configs/arkit/arkit.yaml:17
     if a.width is None:
         a.width = 256 if big else 128
@@ -253,7 +259,7 @@ def main():
     params = [emb] + list(dec.parameters())
     timer = KernelTimer()
     _lib.KERNEL_TIMER = timer
-    stats = {"m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
+    stats = {"n": 0, "m": 0, "r_hit": 0, "visits": 0, "s_max": 0}
 
     from psvo.dist import GlobalBatch, GlobalLossSums, GradBucket
     from psvo.engine import MappingEngine
@@ -273,6 +279,7 @@ def main():
     exchange = EngineGradExchange(engine, op="sum")
 
     def record_stats(m, r_hit, visits, s_max):
+        stats["n"] += 1
         stats["m"] += m
         stats["r_hit"] += r_hit
         stats["visits"] += visits
@@ -346,38 +353,103 @@ def main():
             el = float(t.item())
         return el
 
+    # ---- bundle_adjust_frames (the reference's mapping API, render_helpers.py:
+    # 559-676): this rank's keyframes — full-resolution synthetic RGB-D frames
+    # with their own poses (optimised, lr 1e-3, frame.py:27) — each iteration
+    # samples rays_per_frame pixels per keyframe (gumbel top-k on the device),
+    # renders, back-propagates and steps every optimiser.  K steps = one call
+    # with num_iterations = K (how Mapping calls it).
+    kfs = None
+    ba_calls = [0]
+
+    def build_keyframes():
+        from psvo.pose import OptimizablePose
+        from psvo.synthetic import SyntheticFrame, camera_poses
+        out = []
+        for f, T in enumerate(camera_poses(scene, args.frames, seed=1000 * rank + 77)):
+            fr = SyntheticFrame(scene, T, scale=1.0, seed=7 * (rank * args.frames + f) + 1, device=device)
+            fr.stamp = rank * args.frames + f  # the union batch's first keyframe (stamp 0) keeps its pose
+            fr.pose = OptimizablePose.from_matrix(T).to(device)
+            fr.optim = torch.optim.Adam(fr.pose.parameters(), lr=1e-3)
+            fr.get_pose = fr.pose.matrix
+            out.append(fr)
+        return out
+
+    def run_ba(steps):
+        engine.discard_queued()  # a look-ahead query of the engine-step runs
+        call = ba_calls[0]
+        ba_calls[0] += 1
+        RH.bundle_adjust_frames(kfs, ms, dec, None, criterion, scene.voxel_size, step_size,
+                                N_rays=args.rays_per_frame, num_iterations=steps, embed_optim=embed_optim,
+                                model_optim=model_optim, update_pose=True, engine=engine,
+                                seed_fn=lambda it: 1000003 * (call + 1) + it)  # same on every rank
+
+    def timed_ba(steps, warmup):
+        if warmup:
+            run_ba(warmup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        run_ba(steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     # the headline steps run without HIP-event markers (each costs a few µs of
-    # GPU idle); the per-region breakdown comes from a separate marked run
+    # GPU idle); the per-region breakdown comes from separate marked runs of
+    # the engine step (pre-built ray batches, the same kernels)
     n_mark = max(5, min(args.steps, 20))
     kt_overlap = None
-    if args.autograd:
-        elapsed = run(step_autograd, args.steps, args.warmup, lambda on: None)
+    others = []
+    if args.path == "ba":
+        kfs = build_keyframes()
+        elapsed = timed_ba(args.steps, args.warmup)
+        path_desc = ("bundle_adjust_frames (drop-in API: per-iteration gumbel pixel sampling on the device, "
+                     "keyframe poses optimised; dispatched to psvo_map_step_frames)")
+    elif args.path == "autograd":
+        elapsed = run(step_autograd, args.steps, args.warmup)
+        path_desc = "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"
+    else:
+        elapsed = run(step_engine, args.steps, args.warmup)
+        path_desc = "native engine (psvo_map_step on pre-built world-space ray batches, next query one step ahead)"
+    if args.path == "autograd":
         timer.enabled = True
-        run(step_autograd, n_mark, 0)
+        run(step_autograd, n_mark, 0, lambda on: None)
         timer.enabled = False
         kt = {k: timer.mean_ms(k) for k in MappingEngine.REGIONS}
     else:
-        elapsed = run(step_engine, args.steps, args.warmup, lambda on: None)
         engine.set_timing(True)      # regions serialised on one stream
-        run(step_engine, n_mark, 0)
+        run(step_engine, n_mark, 2, lambda on: None)
         kt = engine.timing()
         engine.set_timing("overlap")  # the same regions as the headline steps run them
         run(step_engine, n_mark, 0)
         kt_overlap = engine.timing()
         engine.set_timing(False)
-    # the other path, for reference (not the headline number)
+    # the other paths, for reference (not the headline number)
     other_steps = max(5, min(args.steps, 20))
-    if world > 1:
-        other = {"path": "not run at N > 1 (the headline path only)"}
-    else:
-        if args.autograd:
+    rays_step = args.frames * args.rays_per_frame
+    if world == 1:
+        if args.path != "step":
             el2 = run(step_engine, other_steps, 2)
-            other = {"path": "native engine (psvo_map_step)"}
-        else:
+            others.append({"path": "native engine step (psvo_map_step, fixed poses, pre-built rays)",
+                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
+        if args.path != "autograd":
             el2 = run(step_autograd, other_steps, 2)
-            other = {"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"}
-        other.update(value=args.frames * args.rays_per_frame * other_steps * world / el2,
-                     ms_per_step=1000.0 * el2 / other_steps)
+            others.append({"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)",
+                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
+        if args.path != "ba":
+            kfs = build_keyframes()
+            el2 = timed_ba(other_steps, 2)
+            others.append({"path": "bundle_adjust_frames (native engine, poses optimised)",
+                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
+    other = others if others else {"path": "not run at N > 1 (the headline path only)"}
     rays_per_step = args.frames * args.rays_per_frame
     total_rays = rays_per_step * args.steps * world
     value = total_rays / elapsed
@@ -397,10 +469,10 @@ def main():
     # overlap them (`time_ms_overlapped`).  Secondary — the decoder (dominant
     # by time): fwd, δ chain and weight gradients are each W-dependent MACs per
     # sample (3 x 2 x MACs FLOP/sample), MFMA-bound.
-    m_avg = stats["m"] / args.steps
-    r_avg = stats["r_hit"] / args.steps
-    v_avg = stats["visits"] / args.steps
-    rays_step = args.frames * args.rays_per_frame
+    n_rec = max(stats["n"], 1)
+    m_avg = stats["m"] / n_rec
+    r_avg = stats["r_hit"] / n_rec
+    v_avg = stats["visits"] / n_rec
     q_keys = ("intersect", "sample", "points", "interp_fwd", "interp_bwd")
     q_parts = {k: kt[k] for k in q_keys}
     q_ms = sum(q_parts.values())
@@ -477,7 +549,7 @@ def main():
                           "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
         "roofline_interp_bwd": roof_ib,
-        "path": "drop-in autograd path" if args.autograd else "native engine (psvo_map_step: one call per iteration)",
+        "path": path_desc,
         "other_path": other,
         "kernels_ms": kt,
         "kernels_ms_overlapped": kt_overlap,

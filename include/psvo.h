@@ -426,7 +426,8 @@ void psvo_engine_free(psvo_engine *e);
  * PSVO_XCH_QUERY is or-ed into ops issued by psvo_map_query (they may run
  * concurrently with the previous step's: use a separate communicator).
  * xi32: psvo_engine_exchange_words(world, max_rays_global) device int32;
- * xf64: 16 device doubles.  Returns non-zero on failure.  Exchanged per step:
+ * xf64: 16 + 8 x 64 device doubles (count sums, loss sums, the keyframe pose
+ * gradients of psvo_map_step_frames, summed over ranks).  Returns non-zero on failure.  Exchanged per step:
  * 8 + 1 words per rank (all-gathered), a [200, 50] int32 table of the
  * sampler's slot-0 voxel ids, 16 doubles; then the caller sums grad_flat
  * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam. */
@@ -439,6 +440,8 @@ int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_ra
 /* Queries psvo_map_query queued and no step has consumed yet (0..2).  A step
  * that fails after picking up its queued query still consumes it. */
 int psvo_engine_queued(psvo_engine *e);
+/* Drop the queued queries (e.g. the look-ahead query of a loop that ended). */
+int psvo_map_discard(psvo_engine *e);
 
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
@@ -484,7 +487,9 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * host int64[F] (0: the frame's pose is fixed — stamp 0 or update_pose
  * False); pose_grad: device f32[F][8] output or NULL.  noise: the sampler's
  * uniform noise f32[200, K', max_steps] (voxel_helpers.py:323-328) or NULL
- * (drawn from seed).  No queued psvo_map_query may be pending. */
+ * (drawn from seed).  No queued psvo_map_query may be pending.  Data parallel
+ * (psvo_engine_set_exchange): each rank passes the keyframes of its part of
+ * the union batch; pose gradients are summed over ranks (≤ 64 keyframes). */
 typedef struct psvo_map_frames {
     int n_frames;
     int64_t rays_per_frame;

@@ -203,6 +203,22 @@ extern "C" psvo_engine *psvo_engine_new(void) {
 
 extern "C" int psvo_engine_queued(psvo_engine *e) { return e ? e->q_count : 0; }
 
+// Drop every queued query (their buffers are reused only after their side-
+// stream work completed: the next query waits on the stream).
+extern "C" int psvo_map_discard(psvo_engine *e) {
+    PSVO_REQUIRE(e, "map_discard: null engine");
+    while (e->q_count > 0) {
+        QuerySet &q = e->qs[e->q_head];
+        if (e->side && hipEventRecord(q.freed, e->side) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_discard: event record failed");
+        q.freed_recorded = e->side != nullptr;
+        q.pending = false;
+        e->q_head ^= 1;
+        e->q_count--;
+    }
+    return PSVO_OK;
+}
+
 extern "C" int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global) {
     if (world < 1 || max_rays_global < 1) return -1;
     EngineExchange x;
@@ -658,6 +674,13 @@ int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
     }
     ENG_CALL(psvo_pose_grad_frames(st, fr->n_frames, fr->rays_per_frame, q.r_hit, q.rank_ray, fr->dirs_cam, grad_od,
                                    grad_od + R * 3, fr->poses, pg));
+    const EngineExchange &x = e->x;
+    if (x.on()) {  // a keyframe's rays may sit on several ranks: the pose gradient is their sum
+        const int64_t nw = (int64_t)fr->n_frames * 8;
+        ENG_CALL(pose_grads_to_f64(st, nw, pg, x.xf64 + kXchF64Base));
+        ENG_CALL(x.call(PSVO_XCH_SUM_F64, kXchF64Base, kXchF64Base, nw, st, "pose gradients"));
+        ENG_CALL(pose_grads_from_f64(st, nw, pg, x.xf64 + kXchF64Base));
+    }
     for (int f = 0; f < fr->n_frames; ++f) {
         if (fr->pose_step[f] < 1) continue;  // stamp 0 / update_pose False: no optimiser (render_helpers.py:594-596)
         float *p = fr->poses + f * 6;
@@ -820,7 +843,8 @@ extern "C" int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map
                                     int64_t adam_step, int flags, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && fr && fr->dirs_cam && fr->poses && fr->pose_step, "map_step_frames: null argument");
     PSVO_REQUIRE(fr->n_frames > 0 && fr->rays_per_frame > 0, "map_step_frames: bad sizes");
-    PSVO_REQUIRE(!e->x.on(), "map_step_frames: keyframe pose updates are single-GPU");
+    PSVO_REQUIRE(!e->x.on() || fr->n_frames <= kXchMaxFrames, "map_step_frames: at most %d keyframes per rank",
+                 kXchMaxFrames);
     PSVO_REQUIRE(e->q_count == 0, "map_step_frames: rays come from this step's poses (no queued query)");
     for (int f = 0; f < fr->n_frames; ++f)
         PSVO_REQUIRE(fr->pose_step[f] < 1 || (fr->pose_m && fr->pose_v), "map_step_frames: pose Adam needs m / v");

@@ -86,6 +86,7 @@ class MappingEngine:
         self.desc = d
         self._queued = []   # (caller's rays_o, rays_d, seed, converted ro, rd) per queued query
         self.exchange = None
+        self.grad_exchange = None
         h = _lib().psvo_engine_new()
         if not h:
             raise L.PsvoError("psvo_engine_new failed")
@@ -179,6 +180,8 @@ class MappingEngine:
         L.call("psvo_engine_set_exchange", self.handle, exchange.rank, exchange.world, exchange.max_rays_global,
                ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
         self.exchange = exchange
+        from .dist import EngineGradExchange
+        self.grad_exchange = EngineGradExchange(self, op="sum")  # the union-batch loss: rank gradients add up
 
     def _error(self, name, rc):
         msg = _lib().psvo_last_error().decode()
@@ -186,6 +189,11 @@ class MappingEngine:
             msg += f" ({type(self.exchange.error).__name__}: {self.exchange.error})"
             self.exchange.error = None
         return L.PsvoError(f"{name} failed (code {rc}): {msg}")
+
+    def discard_queued(self):
+        """Drop queries queued by query() that no step will consume."""
+        L.call("psvo_map_discard", self.handle)
+        self._queued.clear()
 
     def _sync_queue(self):
         """Drop the Python records of queries the engine consumed (a failed

@@ -417,7 +417,7 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
 
 
 def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays, num_iterations, update_pose,
-                          noise):
+                          noise, seed_fn=None):
     emb = eng.emb
     params = eng.params
     st_e = _adam_state(embed_optim, emb)
@@ -468,11 +468,18 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             rgbs.append(kf.rgb.reshape(-1, 3).to(dev)[idx])
             depths.append(kf.depth.reshape(-1).to(dev)[idx])
         nz = noise(it) if callable(noise) else None
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if nz is None else 0
+        if seed_fn is not None:
+            seed = int(seed_fn(it))
+        else:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if nz is None else 0
         adam_step += 1
         cur = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
+        dp = eng.grad_exchange is not None
         eng.step_frames(torch.cat(dirs), N_rays, poses, pm, pv, cur, lr_pose or 0.0, torch.cat(rgbs),
-                        torch.cat(depths), seed, noise=nz, adam_step=adam_step)
+                        torch.cat(depths), seed, noise=nz, adam_step=adam_step, apply_adam=not dp)
+        if dp:  # data parallel: sum the union-batch gradient over ranks, then the same Adam everywhere
+            eng.grad_exchange()
+            eng.adam()
         pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur)]
     # write back: optimiser steps, pose parameters and their Adam state
     with torch.no_grad():
@@ -492,20 +499,28 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
 def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, voxel_size, step_size,
                          N_rays=512, num_iterations=10, truncation=0.1, max_voxel_hit=10, max_distance=10,
                          learning_rate=[1e-2, 5e-3], embed_optim=None, model_optim=None, resnet_optim=None,
-                         update_pose=True, noise=None, use_engine=True):
+                         update_pose=True, noise=None, use_engine=True, engine=None, seed_fn=None):
     """render_helpers.py:559-676 — mapping's render-and-optimise loop.
 
     Runs on the native engine (one psvo_map_step_frames call per iteration)
     whenever the optimisers are plain Adam over the map embeddings / fused
     decoder and no point-feature network is attached; otherwise the autograd
-    loop below (same kernels).  `noise` (not in the reference signature): a
-    callable iteration → sampler noise [200, K', max_steps], for parity tests."""
+    loop below (same kernels).  Keywords beyond the reference signature:
+    `noise` — a callable iteration → sampler noise [200, K', max_steps]
+    (parity tests); `engine` — a prepared psvo.engine.MappingEngine to use
+    (e.g. one with a data-parallel EngineExchange: every rank passes the
+    keyframes of its share of the union batch); `seed_fn` — iteration →
+    sampler seed (must agree across ranks when data parallel)."""
     if use_engine:
-        eng = _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim, model_optim,
-                          resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays)
+        eng = engine
+        if eng is None:
+            eng = _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim,
+                              model_optim, resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays)
         if eng is not None and _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
-                                                     num_iterations, update_pose, noise):
+                                                     num_iterations, update_pose, noise, seed_fn):
             return
+        if engine is not None:
+            raise RuntimeError("bundle_adjust_frames: the given engine cannot run this call (optimiser state)")
     optimizers = [embed_optim]
     if model_optim is not None:
         optimizers += [model_optim]

@@ -150,11 +150,14 @@ def test_oracle_bundle_adjust_matches_reference():
         adam_close(v.numpy(), g["dec1." + k])
 
 
-def adam_close(got, ref, lr=5e-3, tight=1e-6, frac=0.98):
-    """Parameters after a few Adam steps: Adam's step m / (sqrt(v) + eps) maps a
-    gradient of ~1e-9 to a step of ~lr/10, so ulp-level differences of
-    near-zero gradients (summation order) move a few elements by a fraction
-    of lr: >= 98 % of the elements within 1e-6, every element within 0.1 lr."""
+def adam_close(got, ref, lr=5e-3, tight=1e-6, frac=0.98, max_abs=None):
+    """Parameters after a few Adam steps.  Adam's step m / (sqrt(v) + eps) is
+    ±lr for any gradient well above eps = 1e-8 whatever its size, so an
+    element whose gradient is near zero (cancelling sums) moves by up to lr
+    in either direction depending on rounding: a different summation order
+    (float atomics on the GPU, torch-CPU here) flips a few of them.  The bar:
+    >= frac of the elements within `tight`, every element within max_abs
+    (default 0.1 lr: CPU-vs-CPU differences stay below a full step)."""
     d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
-    assert d.max() <= 0.1 * lr, d.max()
+    assert d.max() <= (0.1 * lr if max_abs is None else max_abs), d.max()
     assert (d <= tight).mean() >= frac, (d <= tight).mean()
