@@ -400,6 +400,31 @@ enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
 int64_t psvo_map_grad_floats(int64_t n_emb);                 /* width 128 */
 int64_t psvo_map_grad_floats_w(int64_t n_emb, int width);
 
+/* ---- keyframe pixel sampling (csrc/pixels.hip) ----------------------------
+ * Replaces sample_util.sample_rays (src/utils/sample_util.py:4-20) as called
+ * by frame.sample_rays (src/frame.py:83-85) for every keyframe in every
+ * bundle_adjust_frames iteration (render_helpers.py:620-640), plus the three
+ * boolean-mask gathers that follow it (:625-633).  Per frame f: the k pixels
+ * of [n_pix] with the largest score log(w/(Σw + 1e-7) + 1e-7) +
+ * g(u), g(u) = −log(−log(u + 1e-7) + 1e-7), all in f32 as the reference
+ * computes them; weights NULL = all ones (frame.py:84); Σw over the frame, or
+ * over all frames when joint_sum (sample_rays on a [B, H, W] mask); u f32
+ * [F, n_pix] when given (parity), else a counter-based 24-bit uniform from
+ * seed.  Ties at the k-th score are taken in pixel order.  Outputs, in pixel
+ * (= row-major mask) order: idx i64[F, k]; per frame the bool mask and the
+ * gathered rows of dirs / rgb / depth into out_* [F·k, 3] / [F·k, 3] / [F·k]
+ * (any NULL skips it).  workspace: psvo_sample_pixels_workspace_ints ints. */
+typedef struct psvo_pixel_frame {
+    const float *dirs;   /* [n_pix, 3] camera ray directions (frame.rays_d), or NULL */
+    const float *rgb;    /* [n_pix, 3], or NULL */
+    const float *depth;  /* [n_pix], or NULL */
+    uint8_t *mask;       /* [n_pix] bool out (frame.sample_mask), or NULL */
+} psvo_pixel_frame;
+int64_t psvo_sample_pixels_workspace_ints(int n_frames);
+int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights, int joint_sum,
+                       const float *u, uint64_t seed, const psvo_pixel_frame *frames, int *workspace, int64_t *idx,
+                       float *out_dirs, float *out_rgb, float *out_depth);
+
 /* ---- row-sparse gradient exchange (data parallel on large maps, §8e) ---- */
 /* Ints of workspace psvo_rows_compact needs for n_rows rows. */
 int64_t psvo_rows_workspace_ints(int64_t n_rows);

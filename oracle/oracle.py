@@ -498,3 +498,46 @@ def bundle_adjust(frames, picks, noises, map_states, decoder_params, poses0, sta
             o.step()
         losses.append(float(loss.detach()))
     return losses, emb.detach(), {k: v.detach() for k, v in params.items()}, torch.stack([p.detach() for p in poses])
+
+
+# ---------------------------------------------------------------- pixel sampling
+def pixel_uniforms(seed, n_frames, n_pix):
+    """The counter-based uniforms psvo_sample_pixels draws when no u is given
+    (csrc/pixels.hip px_uniform: a 64-bit finaliser of seed·φ + f·2^40 + i,
+    top 24 bits → [0, 1) like torch.rand).  numpy uint64 arithmetic wraps."""
+    with np.errstate(over="ignore"):
+        f = np.arange(n_frames, dtype=np.uint64)[:, None]
+        i = np.arange(n_pix, dtype=np.uint64)[None, :]
+        x = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + (f << np.uint64(40)) + i
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xFF51AFD7ED558CCD)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xC4CEB9FE1A85EC53)
+        x ^= x >> np.uint64(33)
+    top = ((x & np.uint64(0xFFFFFFFF)) >> np.uint64(8)).astype(np.float32)
+    return top * np.float32(1.0 / 16777216.0)
+
+
+def pixel_scores(mask, u):
+    """sample_util.py:12-17 + :5-8 in f32: log(mask / (mask.sum() + 1e-7) +
+    1e-7) + gumbel(u), one sum over the whole [B, H, W] mask."""
+    mask = torch.as_tensor(mask, dtype=torch.float32)
+    B = mask.shape[0]
+    probs = mask / (mask.sum() + 1e-7)
+    logp = torch.log(probs.reshape(B, -1) + 1e-7)
+    u = torch.as_tensor(u, dtype=torch.float32).reshape(B, -1)
+    return logp + (-torch.log(-torch.log(u + 1e-7) + 1e-7))
+
+
+def sample_rays(mask, n, u):
+    """sample_util.sample_rays (sample_util.py:12-20) with the uniforms
+    gumbel_like draws given: the n top scores per frame, as ascending pixel
+    indices [B, n] (the bool mask's pixels in row-major order).  Ties at the
+    n-th score: lowest pixel index first (torch.topk leaves it unspecified)."""
+    s = pixel_scores(mask, u).numpy()
+    B = s.shape[0]
+    out = np.empty((B, n), np.int64)
+    for b in range(B):
+        order = np.lexsort((np.arange(s.shape[1]), -s[b].astype(np.float64)))
+        out[b] = np.sort(order[:n])
+    return out

@@ -1,0 +1,350 @@
+// Keyframe pixel sampling of the mapping loop on the device.
+//
+// Reference: every bundle_adjust_frames iteration (render_helpers.py:620-640)
+// calls frame.sample_rays(N) per keyframe (frame.py:83-85), i.e.
+// sample_util.sample_rays (sample_util.py:4-20):
+//   p      = mask / (mask.sum() + 1e-7)                    (f32)
+//   score  = log(p + 1e-7) + g,  g = −log(−log(u + 1e-7) + 1e-7),  u ~ U[0, 1)
+//   picked = score.topk(N)  → a bool mask of the picked pixels
+// then gathers rays_d / rgb / depth of the mask's pixels in row-major order.
+// On the reference this is a full sort of H·W scores per keyframe per
+// iteration (torch.topk) plus three boolean-mask gathers; here it is one
+// radix select for all keyframes together, with the gathers fused into the
+// compaction that writes the picked pixels:
+//   k_px_hist<0>   scores → orderable u32 keys (recomputed each pass from the
+//                  counter-based u: no key array in HBM); 4096-bin histogram
+//                  of the top 12 key bits (LDS, then one atomic per non-empty
+//                  bin)
+//   k_px_hist<1,2> every block re-derives the previous pass's pick from the
+//                  global histogram (4096 bins, L2-resident), then histograms
+//                  the next 12 / 8 bits of the keys sharing the picked prefix
+//   k_px_count     the exact N-th largest key T: per block, keys > T and = T
+//   k_px_write     keys > T, plus the first (N − #{> T}) keys = T in pixel
+//                  order, written in pixel order (block offsets summed from
+//                  the ≤ 64 block counts of the frame); idx, mask and the
+//                  gathered rows
+// A frame's H·W keys are touched 5 times in registers only; the HBM traffic
+// is the mask (1 B / pixel, optional), the weights (4 B / pixel, optional)
+// and the N gathered rows.
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+constexpr int kPxThreads = 256;
+constexpr int kPxBlocks = 64;    // blocks per frame
+constexpr int kPxBins = 4096;    // 12-bit digits (the last pass: 8 bits)
+constexpr int kPxMaxFrames = 32;
+
+struct PxFrames {
+    psvo_pixel_frame f[kPxMaxFrames];
+};
+
+struct PxArgs {
+    int64_t n_pix, k, chunk;     // pixels per frame, picks per frame, pixels per block
+    const float *weights;        // [F, n_pix] or null (all ones)
+    const float *u;              // [F, n_pix] or null (counter-based from seed)
+    uint64_t seed;
+    int joint_sum;               // normalise by the sum over all frames (sample_rays on a [B, H, W] mask)
+    int n_frames;
+    int *hist;                   // [3][F][4096]
+    int *state;                  // [F][3][2]: (prefix, remaining) after passes 0, 1, 2
+    int *counts;                 // [F][kPxBlocks][2]: keys > T, keys = T
+    double *wsum;                // [F][kPxBlocks] partial weight sums
+};
+
+__device__ __forceinline__ uint32_t px_mix32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// torch.rand_like's 24-bit uniform in [0, 1)
+__device__ __forceinline__ float px_uniform(const PxArgs &a, int f, int64_t i) {
+    if (a.u) return a.u[(int64_t)f * a.n_pix + i];
+    const uint64_t key = a.seed * 0x9E3779B97F4A7C15ull + ((uint64_t)f << 40) + (uint64_t)i;
+    return (float)(px_mix32(key) >> 8) * (1.0f / 16777216.0f);
+}
+
+// the reference's score in f32 (sample_util.py:5-9, :14-17), as an orderable key
+__device__ __forceinline__ uint32_t px_key(const PxArgs &a, int f, int64_t i, float den) {
+    const float w = a.weights ? a.weights[(int64_t)f * a.n_pix + i] : 1.0f;
+    const float logp = logf(__fadd_rn(__fdiv_rn(w, den), 1e-7f));
+    const float uu = px_uniform(a, f, i);
+    const float g = -logf(__fadd_rn(-logf(__fadd_rn(uu, 1e-7f)), 1e-7f));
+    const float s = __fadd_rn(logp, g);
+    const uint32_t b = __float_as_uint(s);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// mask.sum() + 1e-7 of the frame (or of all frames): fixed-order sum of the
+// per-block partials (exact for 0/1 masks; weights null = all ones)
+__device__ __forceinline__ float px_den(const PxArgs &a, int f) {
+    double s;
+    if (!a.weights) {
+        s = (double)a.n_pix * (a.joint_sum ? a.n_frames : 1);
+    } else {
+        s = 0.0;
+        const int f0 = a.joint_sum ? 0 : f, f1 = a.joint_sum ? a.n_frames : f + 1;
+        for (int g = f0; g < f1; ++g)
+            for (int b = 0; b < kPxBlocks; ++b) s += a.wsum[g * kPxBlocks + b];
+    }
+    return __fadd_rn((float)s, 1e-7f);
+}
+
+__global__ __launch_bounds__(kPxThreads) void k_px_wsum(PxArgs a) {
+    __shared__ double part[kPxThreads / kWave];
+    const int f = blockIdx.y, b = blockIdx.x;
+    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
+    double s = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kPxThreads) s += (double)a.weights[(int64_t)f * a.n_pix + i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kPxThreads / kWave; ++w) t += part[w];
+        a.wsum[f * kPxBlocks + b] = t;
+    }
+}
+
+// Pick the bin holding the rem-th largest key of a 4096-bin histogram
+// (highest bin first): bin → *bin_out, keys still needed inside it → *rem_out.
+// Thread t owns bins [16t, 16t + 16).
+__device__ void px_select(const int *__restrict__ h, int rem, int *sh_suffix, int *bin_out, int *rem_out) {
+    const int t = threadIdx.x;
+    int v[16];
+    int s = 0;
+    for (int j = 0; j < 16; ++j) {
+        v[j] = h[t * 16 + j];
+        s += v[j];
+    }
+    sh_suffix[t] = s;
+    __syncthreads();
+    // inclusive suffix sum over threads (Hillis-Steele from the top)
+    for (int off = 1; off < kPxThreads; off <<= 1) {
+        const int x = t + off < kPxThreads ? sh_suffix[t + off] : 0;
+        __syncthreads();
+        sh_suffix[t] += x;
+        __syncthreads();
+    }
+    const int above = sh_suffix[t] - s;  // keys in the bins of threads t+1..
+    if (above < rem && rem <= above + s) {
+        int acc = above;
+        for (int j = 15; j >= 0; --j) {
+            if (acc + v[j] >= rem) {
+                *bin_out = t * 16 + j;
+                *rem_out = rem - acc;
+                break;
+            }
+            acc += v[j];
+        }
+    }
+    __syncthreads();
+}
+
+// the state after pass P − 1 (P ≥ 1): re-derived from the global histogram of
+// pass P − 1 and the state after pass P − 2 (written by the previous kernel)
+template <int P>
+__device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, uint32_t &prefix, int &rem) {
+    uint32_t pfx = 0;
+    int r = (int)a.k;
+    if (P >= 2) {
+        pfx = (uint32_t)a.state[(f * 3 + (P - 2)) * 2 + 0];
+        r = a.state[(f * 3 + (P - 2)) * 2 + 1];
+    }
+    px_select(a.hist + ((int64_t)(P - 1) * a.n_frames + f) * kPxBins, r, sh_suffix, &sh_res[0], &sh_res[1]);
+    const uint32_t bin = (uint32_t)sh_res[0];
+    // prefix bits so far: pass 0 → 12, pass 1 → 24, pass 2 → 32
+    prefix = P == 1 ? bin : (P == 2 ? (pfx << 12) | bin : (pfx << 8) | bin);
+    rem = sh_res[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.state[(f * 3 + (P - 1)) * 2 + 0] = (int)prefix;
+        a.state[(f * 3 + (P - 1)) * 2 + 1] = rem;
+    }
+}
+
+// pass P ∈ {0, 1, 2}: histogram of digit P of the keys whose higher digits
+// equal the prefix picked so far
+template <int P>
+__global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
+    __shared__ int h[kPxBins];
+    __shared__ int sh_suffix[kPxThreads];
+    __shared__ int sh_res[2];
+    const int f = blockIdx.y, b = blockIdx.x;
+    for (int j = threadIdx.x; j < kPxBins; j += kPxThreads) h[j] = 0;
+    uint32_t prefix = 0;
+    int rem = 0;
+    if constexpr (P >= 1) px_state<P>(a, f, sh_suffix, sh_res, prefix, rem);
+    __syncthreads();
+    const float den = px_den(a, f);
+    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kPxThreads) {
+        const uint32_t key = px_key(a, f, i, den);
+        if constexpr (P == 0) {
+            atomicAdd(&h[key >> 20], 1);
+        } else if constexpr (P == 1) {
+            if ((key >> 20) == prefix) atomicAdd(&h[(key >> 8) & 0xfffu], 1);
+        } else {
+            if ((key >> 8) == prefix) atomicAdd(&h[key & 0xffu], 1);
+        }
+    }
+    __syncthreads();
+    int *gh = a.hist + ((int64_t)P * a.n_frames + f) * kPxBins;
+    for (int j = threadIdx.x; j < kPxBins; j += kPxThreads)
+        if (h[j]) atomicAdd(&gh[j], h[j]);
+}
+
+// the exact N-th largest key T of the frame; per block: keys > T, keys = T
+__global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
+    __shared__ int sh_suffix[kPxThreads];
+    __shared__ int sh_res[2];
+    __shared__ int part[2][kPxThreads / kWave];
+    const int f = blockIdx.y, b = blockIdx.x;
+    uint32_t T;
+    int rem;
+    px_state<3>(a, f, sh_suffix, sh_res, T, rem);
+    const float den = px_den(a, f);
+    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
+    int gt = 0, eq = 0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kPxThreads) {
+        const uint32_t key = px_key(a, f, i, den);
+        gt += key > T;
+        eq += key == T;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        gt += __shfl_xor(gt, o, 64);
+        eq += __shfl_xor(eq, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = gt;
+        part[1][threadIdx.x >> 6] = eq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int g = 0, e = 0;
+        for (int w = 0; w < kPxThreads / kWave; ++w) {
+            g += part[0][w];
+            e += part[1][w];
+        }
+        a.counts[(f * kPxBlocks + b) * 2 + 0] = g;
+        a.counts[(f * kPxBlocks + b) * 2 + 1] = e;
+    }
+}
+
+// picked pixels in pixel order: index, mask and the gathered rows
+__global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, int64_t *__restrict__ idx,
+                                                         float *__restrict__ out_dirs, float *__restrict__ out_rgb,
+                                                         float *__restrict__ out_depth) {
+    __shared__ int wave_cnt[kPxThreads / kWave];
+    const int f = blockIdx.y, b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t T = (uint32_t)a.state[(f * 3 + 2) * 2 + 0];
+    const int ties = a.state[(f * 3 + 2) * 2 + 1];  // keys = T to take, in pixel order
+    int gt_before = 0, eq_before = 0;
+    for (int j = 0; j < b; ++j) {
+        gt_before += a.counts[(f * kPxBlocks + j) * 2 + 0];
+        eq_before += a.counts[(f * kPxBlocks + j) * 2 + 1];
+    }
+    int base = gt_before + min(eq_before, ties);  // output slot of this block's first pick
+    int eq_seen = eq_before;                      // keys = T before this round
+    const float den = px_den(a, f);
+    const psvo_pixel_frame F = fr.f[f];
+    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
+    for (int64_t r0 = i0; r0 < i1; r0 += kPxThreads) {
+        const int64_t i = r0 + threadIdx.x;
+        uint32_t key = 0;
+        if (i < i1) key = px_key(a, f, i, den);
+        const bool is_gt = i < i1 && key > T;
+        const bool is_eq = i < i1 && key == T;
+        // ties: rank among this round's keys = T (waves in order), then pick
+        const uint64_t beq = __ballot(is_eq);
+        if (lane == 0) wave_cnt[wave] = __popcll(beq);
+        __syncthreads();
+        int eq_rank = eq_seen + __popcll(beq & ((1ull << lane) - 1ull));
+        int eq_round = 0;
+        for (int w = 0; w < kPxThreads / kWave; ++w) {
+            if (w < wave) eq_rank += wave_cnt[w];
+            eq_round += wave_cnt[w];
+        }
+        __syncthreads();
+        const bool pick = is_gt || (is_eq && eq_rank < ties);
+        const uint64_t bp = __ballot(pick);
+        if (lane == 0) wave_cnt[wave] = __popcll(bp);
+        __syncthreads();
+        int o = base + __popcll(bp & ((1ull << lane) - 1ull));
+        int round_picks = 0;
+        for (int w = 0; w < kPxThreads / kWave; ++w) {
+            if (w < wave) o += wave_cnt[w];
+            round_picks += wave_cnt[w];
+        }
+        __syncthreads();
+        if (F.mask && i < i1) F.mask[i] = pick ? 1 : 0;
+        if (pick) {
+            const int64_t row = (int64_t)f * a.k + o;
+            if (idx) idx[row] = i;
+            if (out_dirs && F.dirs)
+                for (int c = 0; c < 3; ++c) out_dirs[row * 3 + c] = F.dirs[i * 3 + c];
+            if (out_rgb && F.rgb)
+                for (int c = 0; c < 3; ++c) out_rgb[row * 3 + c] = F.rgb[i * 3 + c];
+            if (out_depth && F.depth) out_depth[row] = F.depth[i];
+        }
+        base += round_picks;
+        eq_seen += eq_round;
+    }
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames) {
+    return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 + (int64_t)n_frames * kPxBlocks * 2 +
+           (int64_t)n_frames * kPxBlocks * 2 /* doubles */ + 2 /* alignment */;
+}
+
+extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights,
+                                  int joint_sum, const float *u, uint64_t seed, const psvo_pixel_frame *frames,
+                                  int *workspace, int64_t *idx, float *out_dirs, float *out_rgb, float *out_depth) {
+    PSVO_REQUIRE(n_frames >= 1 && n_frames <= kPxMaxFrames, "sample_pixels: %d frames (1..%d)", n_frames,
+                 kPxMaxFrames);
+    PSVO_REQUIRE(n_pix >= 1 && n_pix <= 0x7fffffff, "sample_pixels: bad pixel count %lld", (long long)n_pix);
+    PSVO_REQUIRE(k >= 1 && k <= n_pix, "sample_pixels: cannot take %lld of %lld pixels", (long long)k,
+                 (long long)n_pix);
+    PSVO_REQUIRE(workspace != nullptr, "sample_pixels: null workspace");
+    PxArgs a;
+    a.n_pix = n_pix;
+    a.k = k;
+    a.chunk = ((n_pix + kPxBlocks - 1) / kPxBlocks + kPxThreads - 1) / kPxThreads * kPxThreads;
+    a.weights = weights;
+    a.u = u;
+    a.seed = seed;
+    a.joint_sum = joint_sum ? 1 : 0;
+    a.n_frames = n_frames;
+    a.hist = workspace;
+    a.state = a.hist + (int64_t)3 * n_frames * kPxBins;
+    a.counts = a.state + (int64_t)n_frames * 6;
+    int *wp = a.counts + (int64_t)n_frames * kPxBlocks * 2;
+    wp += ((uintptr_t)wp & 7) ? 1 : 0;
+    a.wsum = reinterpret_cast<double *>(wp);
+    PxFrames fr = {};
+    if (frames)
+        for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];
+    hipStream_t st = as_stream(stream);
+    if (hipMemsetAsync(a.hist, 0, sizeof(int) * 3 * n_frames * kPxBins, st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
+    const dim3 grid(kPxBlocks, n_frames);
+    if (weights) hipLaunchKernelGGL(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
+    hipLaunchKernelGGL(k_px_hist<0>, grid, dim3(kPxThreads), 0, st, a);
+    hipLaunchKernelGGL(k_px_hist<1>, grid, dim3(kPxThreads), 0, st, a);
+    hipLaunchKernelGGL(k_px_hist<2>, grid, dim3(kPxThreads), 0, st, a);
+    hipLaunchKernelGGL(k_px_count, grid, dim3(kPxThreads), 0, st, a);
+    hipLaunchKernelGGL(k_px_write, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
+    return check_launch("sample_pixels");
+}

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import _lib as L
+from . import sample_util
 from .voxel_helpers import MAX_DEPTH, N_MAX_HITS, _intersect_sorted
 
 D_EMB = 16
@@ -454,9 +455,18 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         lr_pose = lr
         if tuple(kf.optim.param_groups[0]["betas"]) != tuple(embed_optim.param_groups[0]["betas"]):
             return False
+    # keyframes whose sample_rays is the reference's uniform gumbel top-k
+    # (frame.py:83-85) are sampled together in one native call with the
+    # gathers fused (psvo.sample_util.sample_frames); others through their own
+    # sample_rays and the boolean-mask gathers
+    batched = all(getattr(kf, "uniform_pixel_sampling", False) for kf in kfs)
     for it in range(num_iterations):
-        dirs, rgbs, depths = [], [], []
-        for kf in kfs:
+        if batched:
+            d_all, c_all, z_all = sample_util.sample_frames(kfs, N_rays)
+            dirs, rgbs, depths = [d_all], [c_all], [z_all]
+        else:
+            dirs, rgbs, depths = [], [], []
+        for kf in ([] if batched else kfs):
             kf.sample_rays(N_rays)
             idx = getattr(kf, "sample_idx", None)
             if idx is None:
@@ -475,8 +485,9 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         adam_step += 1
         cur = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
         dp = eng.grad_exchange is not None
-        eng.step_frames(torch.cat(dirs), N_rays, poses, pm, pv, cur, lr_pose or 0.0, torch.cat(rgbs),
-                        torch.cat(depths), seed, noise=nz, adam_step=adam_step, apply_adam=not dp)
+        cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs)  # noqa: E731
+        eng.step_frames(cat(dirs), N_rays, poses, pm, pv, cur, lr_pose or 0.0, cat(rgbs), cat(depths), seed,
+                        noise=nz, adam_step=adam_step, apply_adam=not dp)
         if dp:  # data parallel: sum the union-batch gradient over ranks, then the same Adam everywhere
             eng.grad_exchange()
             eng.adam()

@@ -241,18 +241,24 @@ class SyntheticFrame:
         self.rays_d = torch.from_numpy(d_cam).to(device)
         self.rgb = torch.from_numpy(col.reshape(H, W, 3).astype(np.float32)).to(device)
         self.depth = torch.from_numpy(t.reshape(H, W).astype(np.float32)).to(device)
-        self.gen = torch.Generator(device=device).manual_seed(seed)
+        self.gen = torch.Generator().manual_seed(seed)  # CPU: seeds for the device sampler, no sync
         self.sample_mask = None
 
+    # sample_rays below is the reference's frame.sample_rays (uniform gumbel
+    # top-k over all pixels): bundle_adjust_frames may sample these frames
+    # together (psvo.sample_util.sample_frames)
+    uniform_pixel_sampling = True
+
     def sample_rays(self, n):
-        """gumbel top-k over a uniform pixel distribution, on the frame's device"""
-        u = torch.rand(self.h * self.w, generator=self.gen, device=self.depth.device)
-        g = -torch.log(-torch.log(u + 1e-7) + 1e-7)
-        idx = torch.topk(g, n).indices.sort().values
-        mask = torch.zeros(self.h * self.w, dtype=torch.bool, device=self.depth.device)
-        mask[idx] = True
-        self.sample_mask = mask.view(self.h, self.w)
-        self.sample_idx = idx  # the mask's pixels in row-major order (no host sync to gather them)
+        """frame.py:83-85: sample_rays(ones_like(depth)[None], n)[0] on the
+        device (psvo.sample_util, gumbel top-k over a uniform distribution)."""
+        from . import sample_util
+        mask = torch.empty(self.h, self.w, dtype=torch.bool, device=self.depth.device)
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
+        idx = sample_util.sample_pixels(1, self.h * self.w, int(n), self.depth.device, seed=seed,
+                                        frames=[(None, None, None, mask)])
+        self.sample_mask = mask
+        self.sample_idx = idx[0]  # the mask's pixels in row-major order (no host sync to gather them)
 
 
 @dataclass

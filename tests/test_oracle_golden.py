@@ -156,8 +156,30 @@ def adam_close(got, ref, lr=5e-3, tight=1e-6, frac=0.98, max_abs=None):
     element whose gradient is near zero (cancelling sums) moves by up to lr
     in either direction depending on rounding: a different summation order
     (float atomics on the GPU, torch-CPU here) flips a few of them.  The bar:
-    >= frac of the elements within `tight`, every element within max_abs
+    >= frac of the elements (all but 2, for tiny tensors) within `tight`, every element within max_abs
     (default 0.1 lr: CPU-vs-CPU differences stay below a full step)."""
     d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
     assert d.max() <= (0.1 * lr if max_abs is None else max_abs), d.max()
-    assert (d <= tight).mean() >= frac, (d <= tight).mean()
+    # small tensors (biases, the rgb head): up to 2 flipped elements however few there are
+    n_out = int((d > tight).sum())
+    assert n_out <= max(2, (1.0 - frac) * d.size), ((d <= tight).mean(), n_out, d.size)
+
+
+def test_oracle_pixel_sampling_matches_reference():
+    """oracle.sample_rays against the reference's own sample_util.sample_rays
+    (tests/golden/P_pixels.npz, make_golden_pixels.py): with the uniforms its
+    torch.rand_like drew, the same picked pixels — uniform frame, a 0/1 mask
+    over two frames (one joint sum), fractional weights."""
+    from oracle import oracle as O
+    g = load_golden("P_pixels")
+    for c in range(int(g["n_cases"])):
+        idx = O.sample_rays(g[f"case{c}.mask"], int(g[f"case{c}.n"]), g[f"case{c}.u"])
+        assert np.array_equal(idx, g[f"case{c}.idx"]), c
+
+
+def test_oracle_pixel_uniforms_are_uniform():
+    from oracle import oracle as O
+    u = O.pixel_uniforms(12345, 2, 100000)
+    assert u.dtype == np.float32 and u.min() >= 0.0 and u.max() < 1.0
+    assert abs(float(u.mean()) - 0.5) < 0.005
+    assert not np.array_equal(u[0], u[1])
