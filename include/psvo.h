@@ -514,7 +514,7 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * uniform noise f32[200, K', max_steps] (voxel_helpers.py:323-328) or NULL
  * (drawn from seed).  No queued psvo_map_query may be pending.  Data parallel
  * (psvo_engine_set_exchange): each rank passes the keyframes of its part of
- * the union batch; pose gradients are summed over ranks (≤ 64 keyframes). */
+ * the union batch; pose gradients are summed over ranks.  At most 64 keyframes per call. */
 typedef struct psvo_map_frames {
     int n_frames;
     int64_t rays_per_frame;

@@ -315,13 +315,26 @@ extern "C" int64_t psvo_map_grad_floats_w(int64_t n_emb, int width) { return n_e
 // grads: [embeddings (n_emb x 16) | W1, b1, ..., W5, b5]
 // one launch for both optimisers (lr per tensor); the embedding gradient is
 // zeroed as it is consumed — the next iteration's atomics accumulate into it
-static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_t adam_step) {
-    float *p[11];
-    const float *g[11];
-    float *m[11], *v[11];
-    int64_t n[11];
-    double lr[11];
-    int zero[11];
+// the keyframe poses' Adam steps of a psvo_map_step_frames iteration, queued
+// with the map's (one launch) or alone (data parallel: the map waits for the
+// gradient all-reduce)
+struct PoseAdam {
+    int n = 0;
+    float *p[kXchMaxFrames], *m[kXchMaxFrames], *v[kXchMaxFrames];
+    const float *g[kXchMaxFrames];
+    int64_t step[kXchMaxFrames];
+    double lr = 0.0;
+};
+
+static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_t adam_step,
+                    const PoseAdam *pa = nullptr) {
+    constexpr int kMax = 11 + kXchMaxFrames;
+    float *p[kMax];
+    const float *g[kMax];
+    float *m[kMax], *v[kMax];
+    int64_t n[kMax], steps[kMax];
+    double lr[kMax];
+    int zero[kMax];
     p[0] = d->emb;
     g[0] = grads;
     m[0] = d->emb_m;
@@ -342,7 +355,19 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
         zero[1 + i] = 0;  // overwritten by the decoder backward
         off += kDecSizes[i];
     }
-    return adam_launch(st, 11, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero);
+    int cnt = 11;
+    for (int i = 0; i < cnt; ++i) steps[i] = adam_step;
+    for (int f = 0; pa && f < pa->n; ++f, ++cnt) {
+        p[cnt] = pa->p[f];
+        g[cnt] = pa->g[f];
+        m[cnt] = pa->m[f];
+        v[cnt] = pa->v[f];
+        n[cnt] = 6;
+        lr[cnt] = pa->lr;
+        zero[cnt] = 0;
+        steps[cnt] = pa->step[f];
+    }
+    return adam_launch(st, cnt, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero, steps);
 }
 
 extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
@@ -665,7 +690,7 @@ namespace {
 // the keyframe poses' part of an iteration (psvo_map_step_frames): per-frame
 // gradient from the rays' grad_o / grad_d, then each optimised pose's Adam
 int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const psvo_map_frames *fr,
-                  const Render &q, const float *grad_od, int64_t R) {
+                  const Render &q, const float *grad_od, int64_t R, PoseAdam *pa) {
     int rc = PSVO_OK;
     float *pg = fr->pose_grad;
     if (!pg) {
@@ -681,16 +706,16 @@ int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
         ENG_CALL(x.call(PSVO_XCH_SUM_F64, kXchF64Base, kXchF64Base, nw, st, "pose gradients"));
         ENG_CALL(pose_grads_from_f64(st, nw, pg, x.xf64 + kXchF64Base));
     }
+    pa->n = 0;
+    pa->lr = fr->lr_pose;
     for (int f = 0; f < fr->n_frames; ++f) {
         if (fr->pose_step[f] < 1) continue;  // stamp 0 / update_pose False: no optimiser (render_helpers.py:594-596)
-        float *p = fr->poses + f * 6;
-        float *m = fr->pose_m + f * 6;
-        float *v = fr->pose_v + f * 6;
-        const float *g = pg + f * 8;
-        int64_t n6 = 6;
-        int zero = 0;
-        double lr = fr->lr_pose;
-        ENG_CALL(adam_launch(st, 1, &p, &g, &m, &v, &n6, &lr, d->beta1, d->beta2, d->eps, 0.0, fr->pose_step[f], &zero));
+        const int k = pa->n++;
+        pa->p[k] = fr->poses + f * 6;
+        pa->m[k] = fr->pose_m + f * 6;
+        pa->v[k] = fr->pose_v + f * 6;
+        pa->g[k] = pg + f * 8;
+        pa->step[k] = fr->pose_step[f];
     }
     return PSVO_OK;
 }
@@ -822,11 +847,24 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
     ENG_CALL(guard.release());
-    if (fr) ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R));
-    // ---- optimiser steps (skipped when the caller all-reduces the gradients first)
+    PoseAdam pa;
+    if (fr) ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R, &pa));
+    // ---- optimiser steps, the poses' with the map's (the map's are skipped
+    // when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
-        ENG_CALL(map_adam(st, d, grads, adam_step));
+        ENG_CALL(map_adam(st, d, grads, adam_step, &pa));
         e->grads_clean = true;
+    } else if (pa.n > 0) {
+        int64_t n6[kXchMaxFrames];
+        double lr[kXchMaxFrames];
+        int zero[kXchMaxFrames];
+        for (int k = 0; k < pa.n; ++k) {
+            n6[k] = 6;
+            lr[k] = pa.lr;
+            zero[k] = 0;
+        }
+        ENG_CALL(adam_launch(st, pa.n, pa.p, pa.g, pa.m, pa.v, n6, lr, d->beta1, d->beta2, d->eps, 0.0, 1, zero,
+                             pa.step));
     }
     return PSVO_OK;
 }
@@ -843,7 +881,7 @@ extern "C" int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map
                                     int64_t adam_step, int flags, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && fr && fr->dirs_cam && fr->poses && fr->pose_step, "map_step_frames: null argument");
     PSVO_REQUIRE(fr->n_frames > 0 && fr->rays_per_frame > 0, "map_step_frames: bad sizes");
-    PSVO_REQUIRE(!e->x.on() || fr->n_frames <= kXchMaxFrames, "map_step_frames: at most %d keyframes per rank",
+    PSVO_REQUIRE(fr->n_frames <= kXchMaxFrames, "map_step_frames: at most %d keyframes per call (rank)",
                  kXchMaxFrames);
     PSVO_REQUIRE(e->q_count == 0, "map_step_frames: rays come from this step's poses (no queued query)");
     for (int f = 0; f < fr->n_frames; ++f)

@@ -34,13 +34,14 @@ struct AdamTable {
     float *v[kAdamMaxTensors];
     int64_t n[kAdamMaxTensors];
     float lr_bc1[kAdamMaxTensors];  // lr / (1 - β1^t) per tensor
+    float bc2_sqrt[kAdamMaxTensors];  // sqrt(1 - β2^t) per tensor (tensors may be at different steps t)
     int zero_grad[kAdamMaxTensors]; // write 0 into the gradient after use
     int block_begin[kAdamMaxTensors + 1];
     int count;
 };
 
-__global__ __launch_bounds__(256) void k_adam(AdamTable tab, float bc2_sqrt, float beta1, float beta2, float omb1,
-                                              float omb2, float eps, float wd) {
+__global__ __launch_bounds__(256) void k_adam(AdamTable tab, float beta1, float beta2, float omb1, float omb2,
+                                              float eps, float wd) {
     int ti = 0;
     while (ti + 1 < tab.count && (int)blockIdx.x >= tab.block_begin[ti + 1]) ++ti;
     const int64_t base = (int64_t)(blockIdx.x - tab.block_begin[ti]) * kAdamSlice;
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float bc2_sqrt, flo
     float *__restrict__ p = tab.p[ti];
     float *__restrict__ g = const_cast<float *>(tab.g[ti]);
     const float lr_bc1 = tab.lr_bc1[ti];
+    const float bc2_sqrt = tab.bc2_sqrt[ti];
     const bool zg = tab.zero_grad[ti] != 0;
     float *__restrict__ m = tab.m[ti];
     float *__restrict__ v = tab.v[ti];
@@ -71,17 +73,16 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float bc2_sqrt, flo
 using namespace psvo;
 
 // One launch over n_tensors tensors (chunks of kAdamMaxTensors); per-tensor
-// learning rate and optional gradient zeroing (the engine's accumulation
-// buffer is left zeroed for the next iteration's float atomics).
+// learning rate, optional per-tensor step number (`steps`, else `step` for
+// all: the engine steps the map and the keyframe poses, each pose at its own
+// Adam step, in one launch) and optional gradient zeroing (the engine's
+// accumulation buffer is left zeroed for the next iteration's float atomics).
 int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads,
                       float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, const double *lr,
                       double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                      const int *zero_grad) {
-    PSVO_REQUIRE(n_tensors >= 0 && step >= 1, "adam_step: bad arguments (n_tensors=%d step=%lld)", n_tensors,
-                 (long long)step);
-    const double bc1 = 1.0 - std::pow(beta1, (double)step);
-    const double bc2 = 1.0 - std::pow(beta2, (double)step);
-    const float bc2_sqrt = (float)std::sqrt(bc2);
+                      const int *zero_grad, const int64_t *steps) {
+    PSVO_REQUIRE(n_tensors >= 0 && (steps || step >= 1), "adam_step: bad arguments (n_tensors=%d step=%lld)",
+                 n_tensors, (long long)step);
     int t = 0;
     while (t < n_tensors) {
         AdamTable tab;
@@ -91,6 +92,10 @@ int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const
             if (numel[t] == 0) continue;
             PSVO_REQUIRE(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t], "adam_step: null pointer (tensor %d)",
                          t);
+            const int64_t tt = steps ? steps[t] : step;
+            PSVO_REQUIRE(tt >= 1, "adam_step: tensor %d at step %lld", t, (long long)tt);
+            const double bc1 = 1.0 - std::pow(beta1, (double)tt);
+            const double bc2 = 1.0 - std::pow(beta2, (double)tt);
             const int k = tab.count++;
             tab.p[k] = params[t];
             tab.g[k] = grads[t];
@@ -98,13 +103,14 @@ int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const
             tab.v[k] = exp_avg_sq[t];
             tab.n[k] = numel[t];
             tab.lr_bc1[k] = (float)(lr[t] / bc1);
+            tab.bc2_sqrt[k] = (float)std::sqrt(bc2);
             tab.zero_grad[k] = zero_grad ? zero_grad[t] : 0;
             tab.block_begin[k] = blocks;
             blocks += (int)div_up(numel[t], kAdamSlice);
         }
         tab.block_begin[tab.count] = blocks;
         if (blocks == 0) continue;
-        hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, st, tab, bc2_sqrt, (float)beta1, (float)beta2,
+        hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, st, tab, (float)beta1, (float)beta2,
                            (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
         const int rc = check_launch("adam_step");
         if (rc) return rc;

@@ -21,7 +21,7 @@
 //   k_px_count     the exact N-th largest key T: per block, keys > T and = T
 //   k_px_write     keys > T, plus the first (N − #{> T}) keys = T in pixel
 //                  order, written in pixel order (block offsets summed from
-//                  the ≤ 64 block counts of the frame); idx, mask and the
+//                  the ≤ 256 block counts of the frame); idx, mask and the
 //                  gathered rows
 // A frame's H·W keys are touched 5 times in registers only; the HBM traffic
 // is the mask (1 B / pixel, optional), the weights (4 B / pixel, optional)
@@ -34,7 +34,9 @@ namespace psvo {
 namespace {
 
 constexpr int kPxThreads = 256;
-constexpr int kPxBlocks = 64;    // blocks per frame
+constexpr int kPxPer = 4;                       // consecutive pixels per thread per round
+constexpr int kPxRound = kPxPer * kPxThreads;   // pixels per block per round
+constexpr int kPxMaxBlocks = 256;               // blocks per frame
 constexpr int kPxBins = 4096;    // 12-bit digits (the last pass: 8 bits)
 constexpr int kPxMaxFrames = 32;
 
@@ -43,7 +45,8 @@ struct PxFrames {
 };
 
 struct PxArgs {
-    int64_t n_pix, k, chunk;     // pixels per frame, picks per frame, pixels per block
+    int64_t n_pix, k, chunk;     // pixels per frame, picks per frame, pixels per block (whole rounds)
+    int nb;                      // blocks per frame
     const float *weights;        // [F, n_pix] or null (all ones)
     const float *u;              // [F, n_pix] or null (counter-based from seed)
     uint64_t seed;
@@ -51,8 +54,8 @@ struct PxArgs {
     int n_frames;
     int *hist;                   // [3][F][4096]
     int *state;                  // [F][3][2]: (prefix, remaining) after passes 0, 1, 2
-    int *counts;                 // [F][kPxBlocks][2]: keys > T, keys = T
-    double *wsum;                // [F][kPxBlocks] partial weight sums
+    int *counts;                 // [F][kPxMaxBlocks][2]: keys > T, keys = T
+    double *wsum;                // [F][kPxMaxBlocks] partial weight sums
 };
 
 __device__ __forceinline__ uint32_t px_mix32(uint64_t x) {
@@ -92,7 +95,7 @@ __device__ __forceinline__ float px_den(const PxArgs &a, int f) {
         s = 0.0;
         const int f0 = a.joint_sum ? 0 : f, f1 = a.joint_sum ? a.n_frames : f + 1;
         for (int g = f0; g < f1; ++g)
-            for (int b = 0; b < kPxBlocks; ++b) s += a.wsum[g * kPxBlocks + b];
+            for (int b = 0; b < a.nb; ++b) s += a.wsum[g * kPxMaxBlocks + b];
     }
     return __fadd_rn((float)s, 1e-7f);
 }
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_wsum(PxArgs a) {
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int w = 0; w < kPxThreads / kWave; ++w) t += part[w];
-        a.wsum[f * kPxBlocks + b] = t;
+        a.wsum[f * kPxMaxBlocks + b] = t;
     }
 }
 
@@ -184,20 +187,44 @@ __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
     __syncthreads();
     const float den = px_den(a, f);
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kPxThreads) {
-        const uint32_t key = px_key(a, f, i, den);
-        if constexpr (P == 0) {
-            atomicAdd(&h[key >> 20], 1);
-        } else if constexpr (P == 1) {
-            if ((key >> 20) == prefix) atomicAdd(&h[(key >> 8) & 0xfffu], 1);
-        } else {
-            if ((key >> 8) == prefix) atomicAdd(&h[key & 0xffu], 1);
+    for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q) {
+            const int64_t i = r0 + q;
+            if (i >= i1) break;
+            const uint32_t key = px_key(a, f, i, den);
+            if constexpr (P == 0) {
+                atomicAdd(&h[key >> 20], 1);
+            } else if constexpr (P == 1) {
+                if ((key >> 20) == prefix) atomicAdd(&h[(key >> 8) & 0xfffu], 1);
+            } else {
+                if ((key >> 8) == prefix) atomicAdd(&h[key & 0xffu], 1);
+            }
         }
     }
     __syncthreads();
     int *gh = a.hist + ((int64_t)P * a.n_frames + f) * kPxBins;
     for (int j = threadIdx.x; j < kPxBins; j += kPxThreads)
         if (h[j]) atomicAdd(&gh[j], h[j]);
+}
+
+// block sum of two counters (result valid in every thread)
+__device__ __forceinline__ void px_block_sum2(int &x, int &y, int (*part)[kPxThreads / kWave]) {
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = x;
+        part[1][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    x = y = 0;
+    for (int w = 0; w < kPxThreads / kWave; ++w) {
+        x += part[0][w];
+        y += part[1][w];
+    }
+    __syncthreads();
 }
 
 // the exact N-th largest key T of the frame; per block: keys > T, keys = T
@@ -212,90 +239,103 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
     const float den = px_den(a, f);
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     int gt = 0, eq = 0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kPxThreads) {
-        const uint32_t key = px_key(a, f, i, den);
-        gt += key > T;
-        eq += key == T;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        gt += __shfl_xor(gt, o, 64);
-        eq += __shfl_xor(eq, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        part[0][threadIdx.x >> 6] = gt;
-        part[1][threadIdx.x >> 6] = eq;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int g = 0, e = 0;
-        for (int w = 0; w < kPxThreads / kWave; ++w) {
-            g += part[0][w];
-            e += part[1][w];
+    for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q) {
+            const int64_t i = r0 + q;
+            if (i >= i1) break;
+            const uint32_t key = px_key(a, f, i, den);
+            gt += key > T;
+            eq += key == T;
         }
-        a.counts[(f * kPxBlocks + b) * 2 + 0] = g;
-        a.counts[(f * kPxBlocks + b) * 2 + 1] = e;
+    }
+    px_block_sum2(gt, eq, part);
+    if (threadIdx.x == 0) {
+        a.counts[(f * kPxMaxBlocks + b) * 2 + 0] = gt;
+        a.counts[(f * kPxMaxBlocks + b) * 2 + 1] = eq;
     }
 }
 
-// picked pixels in pixel order: index, mask and the gathered rows
+// picked pixels in pixel order: index, mask and the gathered rows.  Pixel p
+// is picked if key > T, or key = T and fewer than `ties` keys = T precede it;
+// its output row = #{keys > T before p} + min(#{keys = T before p}, ties).
+// Both counts come from one packed (eq << 16 | gt) block scan per round of
+// 1024 pixels (4 consecutive pixels per thread).
 __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, int64_t *__restrict__ idx,
                                                          float *__restrict__ out_dirs, float *__restrict__ out_rgb,
                                                          float *__restrict__ out_depth) {
-    __shared__ int wave_cnt[kPxThreads / kWave];
+    __shared__ int part[2][kPxThreads / kWave];
+    __shared__ int wave_tot[kPxThreads / kWave];
     const int f = blockIdx.y, b = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t T = (uint32_t)a.state[(f * 3 + 2) * 2 + 0];
     const int ties = a.state[(f * 3 + 2) * 2 + 1];  // keys = T to take, in pixel order
-    int gt_before = 0, eq_before = 0;
-    for (int j = 0; j < b; ++j) {
-        gt_before += a.counts[(f * kPxBlocks + j) * 2 + 0];
-        eq_before += a.counts[(f * kPxBlocks + j) * 2 + 1];
+    int gt_run = 0, eq_run = 0;                     // counts before this block, then before each round
+    for (int j = threadIdx.x; j < b; j += kPxThreads) {
+        gt_run += a.counts[(f * kPxMaxBlocks + j) * 2 + 0];
+        eq_run += a.counts[(f * kPxMaxBlocks + j) * 2 + 1];
     }
-    int base = gt_before + min(eq_before, ties);  // output slot of this block's first pick
-    int eq_seen = eq_before;                      // keys = T before this round
+    px_block_sum2(gt_run, eq_run, part);
     const float den = px_den(a, f);
     const psvo_pixel_frame F = fr.f[f];
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
-    for (int64_t r0 = i0; r0 < i1; r0 += kPxThreads) {
-        const int64_t i = r0 + threadIdx.x;
-        uint32_t key = 0;
-        if (i < i1) key = px_key(a, f, i, den);
-        const bool is_gt = i < i1 && key > T;
-        const bool is_eq = i < i1 && key == T;
-        // ties: rank among this round's keys = T (waves in order), then pick
-        const uint64_t beq = __ballot(is_eq);
-        if (lane == 0) wave_cnt[wave] = __popcll(beq);
+    for (int64_t rr = i0; rr < i1; rr += kPxRound) {
+        const int64_t r0 = rr + kPxPer * threadIdx.x;
+        uint32_t key[kPxPer];
+        int packed = 0;
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q) {
+            key[q] = 0;
+            if (r0 + q < i1) {
+                key[q] = px_key(a, f, r0 + q, den);
+                packed += (key[q] > T ? 1 : 0) + (key[q] == T ? (1 << 16) : 0);
+            }
+        }
+        // inclusive wave scan, then the waves before this one
+        int inc = packed;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wave_tot[wave] = inc;
         __syncthreads();
-        int eq_rank = eq_seen + __popcll(beq & ((1ull << lane) - 1ull));
-        int eq_round = 0;
+        int before = inc - packed, round_tot = 0;
         for (int w = 0; w < kPxThreads / kWave; ++w) {
-            if (w < wave) eq_rank += wave_cnt[w];
-            eq_round += wave_cnt[w];
+            if (w < wave) before += wave_tot[w];
+            round_tot += wave_tot[w];
         }
         __syncthreads();
-        const bool pick = is_gt || (is_eq && eq_rank < ties);
-        const uint64_t bp = __ballot(pick);
-        if (lane == 0) wave_cnt[wave] = __popcll(bp);
-        __syncthreads();
-        int o = base + __popcll(bp & ((1ull << lane) - 1ull));
-        int round_picks = 0;
-        for (int w = 0; w < kPxThreads / kWave; ++w) {
-            if (w < wave) o += wave_cnt[w];
-            round_picks += wave_cnt[w];
+        int gt_b = gt_run + (before & 0xffff), eq_b = eq_run + (before >> 16);
+        uint32_t mword = 0;
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q) {
+            const int64_t i = r0 + q;
+            if (i >= i1) break;
+            const bool is_gt = key[q] > T, is_eq = key[q] == T;
+            const bool pick = is_gt || (is_eq && eq_b < ties);
+            if (pick) {
+                const int64_t row = (int64_t)f * a.k + gt_b + min(eq_b, ties);
+                if (idx) idx[row] = i;
+                if (out_dirs && F.dirs)
+                    for (int c = 0; c < 3; ++c) out_dirs[row * 3 + c] = F.dirs[i * 3 + c];
+                if (out_rgb && F.rgb)
+                    for (int c = 0; c < 3; ++c) out_rgb[row * 3 + c] = F.rgb[i * 3 + c];
+                if (out_depth && F.depth) out_depth[row] = F.depth[i];
+            }
+            mword |= (pick ? 1u : 0u) << (8 * q);
+            gt_b += is_gt;
+            eq_b += is_eq;
         }
-        __syncthreads();
-        if (F.mask && i < i1) F.mask[i] = pick ? 1 : 0;
-        if (pick) {
-            const int64_t row = (int64_t)f * a.k + o;
-            if (idx) idx[row] = i;
-            if (out_dirs && F.dirs)
-                for (int c = 0; c < 3; ++c) out_dirs[row * 3 + c] = F.dirs[i * 3 + c];
-            if (out_rgb && F.rgb)
-                for (int c = 0; c < 3; ++c) out_rgb[row * 3 + c] = F.rgb[i * 3 + c];
-            if (out_depth && F.depth) out_depth[row] = F.depth[i];
+        if (F.mask && r0 < i1) {
+            uint8_t *m = F.mask + r0;
+            if (r0 + kPxPer <= i1 && ((uintptr_t)m & 3) == 0) {
+                *reinterpret_cast<uint32_t *>(m) = mword;
+            } else {
+                for (int q = 0; q < kPxPer && r0 + q < i1; ++q) m[q] = (uint8_t)(mword >> (8 * q));
+            }
         }
-        base += round_picks;
-        eq_seen += eq_round;
+        gt_run += round_tot & 0xffff;
+        eq_run += round_tot >> 16;
     }
 }
 
@@ -305,8 +345,8 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
 using namespace psvo;
 
 extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames) {
-    return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 + (int64_t)n_frames * kPxBlocks * 2 +
-           (int64_t)n_frames * kPxBlocks * 2 /* doubles */ + 2 /* alignment */;
+    return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 + (int64_t)n_frames * kPxMaxBlocks * 2 +
+           (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */;
 }
 
 extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights,
@@ -315,13 +355,16 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     PSVO_REQUIRE(n_frames >= 1 && n_frames <= kPxMaxFrames, "sample_pixels: %d frames (1..%d)", n_frames,
                  kPxMaxFrames);
     PSVO_REQUIRE(n_pix >= 1 && n_pix <= 0x7fffffff, "sample_pixels: bad pixel count %lld", (long long)n_pix);
-    PSVO_REQUIRE(k >= 1 && k <= n_pix, "sample_pixels: cannot take %lld of %lld pixels", (long long)k,
-                 (long long)n_pix);
+    PSVO_REQUIRE(k >= 1 && k <= n_pix && k < 65536 * 64, "sample_pixels: cannot take %lld of %lld pixels",
+                 (long long)k, (long long)n_pix);
     PSVO_REQUIRE(workspace != nullptr, "sample_pixels: null workspace");
     PxArgs a;
     a.n_pix = n_pix;
     a.k = k;
-    a.chunk = ((n_pix + kPxBlocks - 1) / kPxBlocks + kPxThreads - 1) / kPxThreads * kPxThreads;
+    // pixels per block: whole rounds of 1024, at most kPxMaxBlocks blocks per frame
+    const int64_t per = (n_pix + kPxMaxBlocks - 1) / kPxMaxBlocks;
+    a.chunk = ((per < kPxRound ? kPxRound : per) + kPxRound - 1) / kPxRound * kPxRound;
+    a.nb = (int)((n_pix + a.chunk - 1) / a.chunk);
     a.weights = weights;
     a.u = u;
     a.seed = seed;
@@ -330,7 +373,7 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     a.hist = workspace;
     a.state = a.hist + (int64_t)3 * n_frames * kPxBins;
     a.counts = a.state + (int64_t)n_frames * 6;
-    int *wp = a.counts + (int64_t)n_frames * kPxBlocks * 2;
+    int *wp = a.counts + (int64_t)n_frames * kPxMaxBlocks * 2;
     wp += ((uintptr_t)wp & 7) ? 1 : 0;
     a.wsum = reinterpret_cast<double *>(wp);
     PxFrames fr = {};
@@ -339,7 +382,7 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     hipStream_t st = as_stream(stream);
     if (hipMemsetAsync(a.hist, 0, sizeof(int) * 3 * n_frames * kPxBins, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
-    const dim3 grid(kPxBlocks, n_frames);
+    const dim3 grid(a.nb, n_frames);
     if (weights) hipLaunchKernelGGL(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
     hipLaunchKernelGGL(k_px_hist<0>, grid, dim3(kPxThreads), 0, st, a);
     hipLaunchKernelGGL(k_px_hist<1>, grid, dim3(kPxThreads), 0, st, a);

@@ -17,10 +17,11 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 // CUDA_CHECK_ERRORS calls exit(-1), cuda_utils.h:37-48): the binding raises.
 int check_launch(const char *what);
 
-// multi-tensor Adam launch (optim.hip): per-tensor lr, optional gradient zeroing
+// multi-tensor Adam launch (optim.hip): per-tensor lr, optional per-tensor
+// step numbers (steps: else `step` for all), optional gradient zeroing
 int adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads, float *const *exp_avg,
                 float *const *exp_avg_sq, const int64_t *numel, const double *lr, double beta1, double beta2,
-                double eps, double weight_decay, int64_t step, const int *zero_grad);
+                double eps, double weight_decay, int64_t step, const int *zero_grad, const int64_t *steps = nullptr);
 
 constexpr int kWave = 64;
 constexpr int kMaxHits = 50;        // voxel_helpers.py:561 (n_max hard-coded)
