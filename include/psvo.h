@@ -420,7 +420,7 @@ typedef struct psvo_pixel_frame {
     const float *depth;  /* [n_pix], or NULL */
     uint8_t *mask;       /* [n_pix] bool out (frame.sample_mask), or NULL */
 } psvo_pixel_frame;
-int64_t psvo_sample_pixels_workspace_ints(int n_frames);
+int64_t psvo_sample_pixels_workspace_ints(int n_frames, int64_t n_pix);
 int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights, int joint_sum,
                        const float *u, uint64_t seed, const psvo_pixel_frame *frames, int *workspace, int64_t *idx,
                        float *out_dirs, float *out_rgb, float *out_depth);

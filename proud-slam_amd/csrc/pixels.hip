@@ -11,10 +11,10 @@
 // iteration (torch.topk) plus three boolean-mask gathers; here it is one
 // radix select for all keyframes together, with the gathers fused into the
 // compaction that writes the picked pixels:
-//   k_px_hist<0>   scores → orderable u32 keys (recomputed each pass from the
-//                  counter-based u: no key array in HBM); 4096-bin histogram
-//                  of the top 12 key bits (LDS, then one atomic per non-empty
-//                  bin)
+//   k_px_hist<0>   scores → orderable u32 keys (stored: 4 B / pixel, read
+//                  back by the later passes — three f32 logs per pixel cost
+//                  more than the 4-B re-read); 4096-bin histogram of the top
+//                  12 key bits (LDS, then one atomic per non-empty bin)
 //   k_px_hist<1,2> every block re-derives the previous pass's pick from the
 //                  global histogram (4096 bins, L2-resident), then histograms
 //                  the next 12 / 8 bits of the keys sharing the picked prefix
@@ -23,9 +23,8 @@
 //                  order, written in pixel order (block offsets summed from
 //                  the ≤ 256 block counts of the frame); idx, mask and the
 //                  gathered rows
-// A frame's H·W keys are touched 5 times in registers only; the HBM traffic
-// is the mask (1 B / pixel, optional), the weights (4 B / pixel, optional)
-// and the N gathered rows.
+// HBM traffic per pixel: the key written once and read 4 times (20 B), the
+// mask (1 B, optional), the weights (4 B, optional); plus the N gathered rows.
 #include <hip/hip_runtime.h>
 
 #include "psvo_common.h"
@@ -56,6 +55,7 @@ struct PxArgs {
     int *state;                  // [F][3][2]: (prefix, remaining) after passes 0, 1, 2
     int *counts;                 // [F][kPxMaxBlocks][2]: keys > T, keys = T
     double *wsum;                // [F][kPxMaxBlocks] partial weight sums
+    uint32_t *keys;              // [F][n_pix] orderable score keys (written by pass 0)
 };
 
 __device__ __forceinline__ uint32_t px_mix32(uint64_t x) {
@@ -83,6 +83,19 @@ __device__ __forceinline__ uint32_t px_key(const PxArgs &a, int f, int64_t i, fl
     const float s = __fadd_rn(logp, g);
     const uint32_t b = __float_as_uint(s);
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// pass 0 computes the keys (three logs each) and stores them; later passes
+// stream them back (4 B / pixel) instead of recomputing
+template <bool kCompute>
+__device__ __forceinline__ uint32_t px_key_at(const PxArgs &a, int f, int64_t i, float den) {
+    if constexpr (kCompute) {
+        const uint32_t k = px_key(a, f, i, den);
+        a.keys[(int64_t)f * a.n_pix + i] = k;
+        return k;
+    } else {
+        return a.keys[(int64_t)f * a.n_pix + i];
+    }
 }
 
 // mask.sum() + 1e-7 of the frame (or of all frames): fixed-order sum of the
@@ -185,14 +198,14 @@ __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
     int rem = 0;
     if constexpr (P >= 1) px_state<P>(a, f, sh_suffix, sh_res, prefix, rem);
     __syncthreads();
-    const float den = px_den(a, f);
+    const float den = P == 0 ? px_den(a, f) : 0.0f;
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
 #pragma unroll
         for (int q = 0; q < kPxPer; ++q) {
             const int64_t i = r0 + q;
             if (i >= i1) break;
-            const uint32_t key = px_key(a, f, i, den);
+            const uint32_t key = px_key_at<P == 0>(a, f, i, den);
             if constexpr (P == 0) {
                 atomicAdd(&h[key >> 20], 1);
             } else if constexpr (P == 1) {
@@ -236,7 +249,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
     uint32_t T;
     int rem;
     px_state<3>(a, f, sh_suffix, sh_res, T, rem);
-    const float den = px_den(a, f);
+    const float den = 0.0f;
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     int gt = 0, eq = 0;
     for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
@@ -244,7 +257,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
         for (int q = 0; q < kPxPer; ++q) {
             const int64_t i = r0 + q;
             if (i >= i1) break;
-            const uint32_t key = px_key(a, f, i, den);
+            const uint32_t key = px_key_at<false>(a, f, i, den);
             gt += key > T;
             eq += key == T;
         }
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
         eq_run += a.counts[(f * kPxMaxBlocks + j) * 2 + 1];
     }
     px_block_sum2(gt_run, eq_run, part);
-    const float den = px_den(a, f);
+    const float den = 0.0f;
     const psvo_pixel_frame F = fr.f[f];
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     for (int64_t rr = i0; rr < i1; rr += kPxRound) {
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
         for (int q = 0; q < kPxPer; ++q) {
             key[q] = 0;
             if (r0 + q < i1) {
-                key[q] = px_key(a, f, r0 + q, den);
+                key[q] = px_key_at<false>(a, f, r0 + q, den);
                 packed += (key[q] > T ? 1 : 0) + (key[q] == T ? (1 << 16) : 0);
             }
         }
@@ -344,9 +357,9 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
 
 using namespace psvo;
 
-extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames) {
+extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames, int64_t n_pix) {
     return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 + (int64_t)n_frames * kPxMaxBlocks * 2 +
-           (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */;
+           (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */ + (int64_t)n_frames * n_pix;
 }
 
 extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights,
@@ -376,6 +389,7 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     int *wp = a.counts + (int64_t)n_frames * kPxMaxBlocks * 2;
     wp += ((uintptr_t)wp & 7) ? 1 : 0;
     a.wsum = reinterpret_cast<double *>(wp);
+    a.keys = reinterpret_cast<uint32_t *>(a.wsum + (int64_t)n_frames * kPxMaxBlocks);
     PxFrames fr = {};
     if (frames)
         for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];

@@ -45,7 +45,7 @@ _SIGNATURES = {
                                    _vp, _vp]),
     "psvo_criterion_reduce": (_i32, [_vp, _i64, _vp, _vp]),
     "psvo_rows_workspace_ints": (_i64, [_i64]),
-    "psvo_sample_pixels_workspace_ints": (_i64, [_i32]),
+    "psvo_sample_pixels_workspace_ints": (_i64, [_i32, _i64]),
     "psvo_sample_pixels": (_i32, [_vp, _i32, _i64, _i64, _vp, _i32, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_compact": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_scatter_add": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),

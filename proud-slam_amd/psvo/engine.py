@@ -63,6 +63,7 @@ class MappingEngine:
         self.step_no = 0
         self.loss_out = torch.empty(16, dtype=torch.float32, device=self.emb.device)
         self.stats = (ctypes.c_int * 16)()
+        self.stats_hook = None  # called with the step's statistics after each step_frames (bench accounting)
         d = MapDesc()
         d.n_nodes = self.centres.shape[0]
         d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
@@ -151,6 +152,8 @@ class MappingEngine:
                                          ctypes.addressof(self.stats))
         if rc != 0:
             raise self._error("psvo_map_step_frames", rc)
+        if self.stats_hook is not None:
+            self.stats_hook(self.stats)
         return self.loss_out[0]
 
     def _check_noise(self, nz, dirs, rpf, poses):

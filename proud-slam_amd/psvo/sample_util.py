@@ -39,8 +39,8 @@ def _seed(seed):
     return int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed) & (2 ** 64 - 1)
 
 
-def _workspace(n_frames, device):
-    n = L.lib().psvo_sample_pixels_workspace_ints(n_frames)
+def _workspace(n_frames, n_pix, device):
+    n = L.lib().psvo_sample_pixels_workspace_ints(n_frames, n_pix)
     return torch.empty(int(n), dtype=torch.int32, device=device)
 
 
@@ -74,7 +74,7 @@ def sample_pixels(n_frames, n_pix, k, device, weights=None, joint_sum=False, u=N
             arr[f].rgb = c.data_ptr() if c is not None else None
             arr[f].depth = z.data_ptr() if z is not None else None
             arr[f].mask = m.data_ptr() if m is not None else None
-    ws = _workspace(n_frames, device)
+    ws = _workspace(n_frames, n_pix, device)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     rc = L.lib().psvo_sample_pixels(L.stream_of(device), n_frames, n_pix, k, ptr(weights), 1 if joint_sum else 0,
                                     ptr(u), _seed(seed), ctypes.cast(arr, ctypes.c_void_p), ptr(ws), ptr(idx),

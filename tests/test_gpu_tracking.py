@@ -50,6 +50,21 @@ def _rays(pose, frame, mask):
     return ro, rd
 
 
+def _kernel_valued_rays(pose, frame, mask):
+    """The rays of _rays with the values k_pose_rays gives (the native
+    tracking step's own f32 rotation series, within 1e-5 of torch's:
+    test_pose_rays_and_grad_kernels), gradients still through torch — so a
+    ray that grazes a voxel face cannot take a different sample set in the
+    drop-in run than in the native one."""
+    from psvo import _lib as L
+    ro, rd = _rays(pose, frame, mask)
+    dirs = frame.rays_d[mask].contiguous()
+    ro_k, rd_k = torch.empty_like(dirs), torch.empty_like(dirs)
+    L.call("psvo_pose_rays", L.stream_of(dirs.device), dirs.shape[0], pose.data.detach().contiguous(), dirs, ro_k,
+           rd_k)
+    return ro + (ro_k.view_as(ro) - ro).detach(), rd + (rd_k.view_as(rd) - rd).detach()
+
+
 @pytest.mark.parametrize("depth_variance", [False, True])
 def test_pose_gradient_matches_oracle(depth_variance):
     from psvo.criterion import Criterion
@@ -171,7 +186,7 @@ def test_native_track_step_matches_autograd(depth_variance):
     # drop-in: render_rays + Criterion + autograd + torch Adam
     pose = _perturbed(T).to(DEV)
     opt = torch.optim.Adam(pose.parameters(), lr=1e-3)
-    ro, rd = _rays(pose, frame, mask)
+    ro, rd = _kernel_valued_rays(pose, frame, mask)
     out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, seed=11)
     out["ray_mask"] = out["ray_mask"].view(-1)
     loss, _ = crit(out, (rgb, depth), weight_depth_loss=depth_variance)
@@ -239,7 +254,7 @@ def test_native_track_frame_matches_dropin_trajectory():
     for it in range(iters):
         frame.sample_rays(1024)
         mask = frame.sample_mask
-        ro, rd = _rays(pose, frame, mask)
+        ro, rd = _kernel_valued_rays(pose, frame, mask)
         out = render_rays(ro, rd, ms, dec, None, 0.01, scene.voxel_size, 0.1, 10, 10.0, seed=base + it)
         out["ray_mask"] = out["ray_mask"].view(-1)
         loss, _ = crit(out, (frame.rgb[mask], frame.depth[mask]), weight_depth_loss=True)
