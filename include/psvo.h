@@ -514,7 +514,14 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * uniform noise f32[200, K', max_steps] (voxel_helpers.py:323-328) or NULL
  * (drawn from seed).  No queued psvo_map_query may be pending.  Data parallel
  * (psvo_engine_set_exchange): each rank passes the keyframes of its part of
- * the union batch; pose gradients are summed over ranks.  At most 64 keyframes per call. */
+ * the union batch; pose gradients are summed over ranks.  At most 64 keyframes per call.
+ * Look-ahead: with next_dirs_cam (the next iteration's camera directions,
+ * same layout; no injected noise) the call also queues the next iteration's
+ * query — its rays need this step's pose update, which runs on a side stream
+ * right after the embedding backward, so the next rays, intersection and
+ * sampling overlap this step's weight-gradient kernels.  The next call must
+ * pass dirs_cam == this next_dirs_cam and seed == next_seed; an unconsumed
+ * look-ahead is dropped by psvo_map_discard. */
 typedef struct psvo_map_frames {
     int n_frames;
     int64_t rays_per_frame;
@@ -523,6 +530,8 @@ typedef struct psvo_map_frames {
     const int64_t *pose_step;
     double lr_pose;
     float *pose_grad;
+    const float *next_dirs_cam;  /* NULL: no look-ahead */
+    uint64_t next_seed;
 } psvo_map_frames;
 int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *frames,
                          const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,

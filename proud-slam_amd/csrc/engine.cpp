@@ -50,6 +50,7 @@ struct QuerySet {
     bool pending = false;
     int64_t R = 0;
     const float *ro = nullptr, *rd = nullptr;
+    const float *dirs = nullptr;  // a psvo_map_step_frames look-ahead: the camera directions it was made from
     uint64_t seed = 0;
     int max_steps = 0;
 };
@@ -209,9 +210,12 @@ extern "C" int psvo_map_discard(psvo_engine *e) {
     PSVO_REQUIRE(e, "map_discard: null engine");
     while (e->q_count > 0) {
         QuerySet &q = e->qs[e->q_head];
-        if (e->side && hipEventRecord(q.freed, e->side) != hipSuccess)
+        // the stream the query was queued on: psvo_map_query's side stream,
+        // or aux for a psvo_map_step_frames look-ahead
+        hipStream_t qs = q.dirs ? e->aux : e->side;
+        if (qs && hipEventRecord(q.freed, qs) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_discard: event record failed");
-        q.freed_recorded = e->side != nullptr;
+        q.freed_recorded = qs != nullptr;
         q.pending = false;
         e->q_head ^= 1;
         e->q_count--;
@@ -456,6 +460,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     q.R = R;
     q.ro = rays_o;
     q.rd = rays_d;
+    q.dirs = nullptr;
     q.seed = seed;
     q.max_steps = max_steps;
     return PSVO_OK;
@@ -719,6 +724,42 @@ int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
     }
     return PSVO_OK;
 }
+
+// the poses' Adam steps on their own (one launch, each pose at its own step)
+int pose_adam(hipStream_t st, const psvo_map_desc *d, const PoseAdam &pa) {
+    if (pa.n == 0) return PSVO_OK;
+    int64_t n6[kXchMaxFrames];
+    double lr[kXchMaxFrames];
+    int zero[kXchMaxFrames];
+    for (int k = 0; k < pa.n; ++k) {
+        n6[k] = 6;
+        lr[k] = pa.lr;
+        zero[k] = 0;
+    }
+    return adam_launch(st, pa.n, pa.p, pa.g, pa.m, pa.v, n6, lr, d->beta1, d->beta2, d->eps, 0.0, 1, zero,
+                       const_cast<int64_t *>(pa.step));
+}
+
+// The next iteration's query, queued on `ps` after this step's pose update:
+// its rays (the updated poses applied to next_dirs_cam) into the engine's ray
+// buffers — this step's last reader of them, the embedding backward, ran
+// earlier on `ps` — then intersection + sampling into the free query set.
+int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const psvo_map_frames *fr,
+                     int64_t R) {
+    int rc = PSVO_OK;
+    PSVO_REQUIRE(e->q_count == 0, "map_step_frames: a query is already queued");
+    QuerySet &q = e->qs[e->q_head];
+    if (q.freed_recorded && hipStreamWaitEvent(st, q.freed, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step_frames: stream ordering failed");
+    ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
+    ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
+    ENG_CALL(psvo_pose_rays_frames(st, R, fr->rays_per_frame, fr->poses, fr->next_dirs_cam, rays_o, rays_d));
+    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)"));
+    q.dirs = fr->next_dirs_cam;
+    q.pending = true;
+    e->q_count++;
+    return PSVO_OK;
+}
 }  // namespace
 
 static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t n_rays, const float *rays_o,
@@ -848,23 +889,25 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     e->tm.pending = e->tm.on;
     ENG_CALL(guard.release());
     PoseAdam pa;
-    if (fr) ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R, &pa));
+    // look-ahead (psvo_map_frames.next_dirs_cam): the poses' gradient and
+    // Adam step right after the embedding backward on its stream, then the
+    // next iteration's rays + query there too — beside this step's weight
+    // gradients and the map's Adam
+    const bool ahead = fr && fr->next_dirs_cam;
+    hipStream_t ps = ahead ? eb : st;
+    if (fr) ENG_CALL(frames_update(e, ps, d, fr, q, grad_od, R, &pa));
+    if (ahead) {
+        ENG_CALL(pose_adam(ps, d, pa));
+        pa.n = 0;
+        ENG_CALL(frames_lookahead(e, ps, d, fr, R));
+    }
     // ---- optimiser steps, the poses' with the map's (the map's are skipped
     // when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step, &pa));
         e->grads_clean = true;
-    } else if (pa.n > 0) {
-        int64_t n6[kXchMaxFrames];
-        double lr[kXchMaxFrames];
-        int zero[kXchMaxFrames];
-        for (int k = 0; k < pa.n; ++k) {
-            n6[k] = 6;
-            lr[k] = pa.lr;
-            zero[k] = 0;
-        }
-        ENG_CALL(adam_launch(st, pa.n, pa.p, pa.g, pa.m, pa.v, n6, lr, d->beta1, d->beta2, d->eps, 0.0, 1, zero,
-                             pa.step));
+    } else {
+        ENG_CALL(pose_adam(st, d, pa));
     }
     return PSVO_OK;
 }
@@ -883,12 +926,19 @@ extern "C" int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map
     PSVO_REQUIRE(fr->n_frames > 0 && fr->rays_per_frame > 0, "map_step_frames: bad sizes");
     PSVO_REQUIRE(fr->n_frames <= kXchMaxFrames, "map_step_frames: at most %d keyframes per call (rank)",
                  kXchMaxFrames);
-    PSVO_REQUIRE(e->q_count == 0, "map_step_frames: rays come from this step's poses (no queued query)");
     for (int f = 0; f < fr->n_frames; ++f)
         PSVO_REQUIRE(fr->pose_step[f] < 1 || (fr->pose_m && fr->pose_v), "map_step_frames: pose Adam needs m / v");
+    PSVO_REQUIRE(!(fr->next_dirs_cam && noise), "map_step_frames: look-ahead needs drawn (not injected) noise");
     hipStream_t st = as_stream(stream);
     int rc = PSVO_OK;
     const int64_t R = (int64_t)fr->n_frames * fr->rays_per_frame;
+    if (e->q_count > 0) {  // the previous call's look-ahead: rays and query made from the updated poses
+        const QuerySet &q = e->qs[e->q_head];
+        PSVO_REQUIRE(q.dirs != nullptr && q.dirs == fr->dirs_cam && q.R == R && q.seed == seed && !noise,
+                     "map_step_frames: dirs_cam / seed differ from the previous call's next_dirs_cam / next_seed");
+        return map_step_impl(e, st, d, R, q.ro, q.rd, gt_rgb, gt_depth, nullptr, seed, adam_step, flags, loss_out,
+                             stats_out, fr);
+    }
     ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
     ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
     ENG_CALL(psvo_pose_rays_frames(st, R, fr->rays_per_frame, fr->poses, fr->dirs_cam, rays_o, rays_d));

@@ -33,7 +33,8 @@ class MapDesc(ctypes.Structure):
 class MapFrames(ctypes.Structure):
     """Mirror of psvo_map_frames (include/psvo.h)."""
     _fields_ = [("n_frames", _i32), ("rays_per_frame", _i64), ("dirs_cam", _vp), ("poses", _vp), ("pose_m", _vp),
-                ("pose_v", _vp), ("pose_step", _vp), ("lr_pose", _f64), ("pose_grad", _vp)]
+                ("pose_v", _vp), ("pose_step", _vp), ("lr_pose", _f64), ("pose_grad", _vp),
+                ("next_dirs_cam", _vp), ("next_seed", ctypes.c_uint64)]
 
 
 def _lib():
@@ -64,6 +65,7 @@ class MappingEngine:
         self.loss_out = torch.empty(16, dtype=torch.float32, device=self.emb.device)
         self.stats = (ctypes.c_int * 16)()
         self.stats_hook = None  # called with the step's statistics after each step_frames (bench accounting)
+        self._ahead = None  # the camera directions of a queued step_frames look-ahead
         d = MapDesc()
         d.n_nodes = self.centres.shape[0]
         d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
@@ -114,16 +116,27 @@ class MappingEngine:
             self.desc.lr_dec = float(lr_dec)
 
     def step_frames(self, dirs_cam, rays_per_frame, poses, pose_m, pose_v, pose_steps, lr_pose, rgb, depth, seed,
-                    noise=None, adam_step=None, apply_adam=True, pose_grad=None):
+                    noise=None, adam_step=None, apply_adam=True, pose_grad=None, next_dirs_cam=None, next_seed=0):
         """One bundle_adjust_frames iteration with keyframe pose updates
         (psvo_map_step_frames): rays from the current poses [F, 6] (frame f
         owns rows [f·rays_per_frame, (f+1)·rays_per_frame) of dirs_cam),
         render + loss + backward, Adam on embeddings / decoder and on every
         pose with pose_steps[f] ≥ 1 (its Adam step number; 0 = fixed pose).
-        poses / pose_m / pose_v are updated in place.  Returns the loss."""
+        poses / pose_m / pose_v are updated in place.  Returns the loss.
+        next_dirs_cam (contiguous f32 [F·rays_per_frame, 3]) / next_seed: the
+        next iteration's batch, whose query is queued beside this step's
+        weight gradients (the next call must pass exactly that tensor and seed)."""
         if self._queued:
             raise RuntimeError("MappingEngine.step_frames: a query() is queued (rays here come from the poses)")
-        dirs = dirs_cam.reshape(-1, 3).float().contiguous()
+        if self._ahead is not None and dirs_cam is self._ahead:
+            dirs = dirs_cam  # the look-ahead the previous call queued: the same storage
+        else:
+            dirs = dirs_cam.reshape(-1, 3).float().contiguous()
+        if next_dirs_cam is not None:
+            if not (next_dirs_cam.is_cuda and next_dirs_cam.dtype == torch.float32 and next_dirs_cam.is_contiguous()
+                    and tuple(next_dirs_cam.shape) == tuple(dirs.shape)) or noise is not None:
+                raise RuntimeError("MappingEngine.step_frames: next_dirs_cam must be a contiguous f32 [R, 3] "
+                                   "device tensor (and no injected noise)")
         n_f = poses.shape[0]
         for t in (poses, pose_m, pose_v):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == (n_f, 6)):
@@ -140,6 +153,8 @@ class MappingEngine:
         fr.pose_step = ctypes.cast(steps, ctypes.c_void_p)
         fr.lr_pose = float(lr_pose)
         fr.pose_grad = pose_grad.data_ptr() if pose_grad is not None else None
+        fr.next_dirs_cam = next_dirs_cam.data_ptr() if next_dirs_cam is not None else None
+        fr.next_seed = int(next_seed) & (2 ** 64 - 1)
         nz = None
         if noise is not None:
             nz = noise.to(device=dirs.device, dtype=torch.float32).contiguous()
@@ -151,7 +166,9 @@ class MappingEngine:
                                          0 if apply_adam else 1, self.loss_out.data_ptr(),
                                          ctypes.addressof(self.stats))
         if rc != 0:
+            self._ahead = None
             raise self._error("psvo_map_step_frames", rc)
+        self._ahead = next_dirs_cam  # kept alive until the next call consumes its query
         if self.stats_hook is not None:
             self.stats_hook(self.stats)
         return self.loss_out[0]
@@ -197,6 +214,7 @@ class MappingEngine:
         """Drop queries queued by query() that no step will consume."""
         L.call("psvo_map_discard", self.handle)
         self._queued.clear()
+        self._ahead = None
 
     def _sync_queue(self):
         """Drop the Python records of queries the engine consumed (a failed

@@ -418,7 +418,7 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
 
 
 def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays, num_iterations, update_pose,
-                          noise, seed_fn=None):
+                          noise, seed_fn=None, lookahead=True):
     emb = eng.emb
     params = eng.params
     st_e = _adam_state(embed_optim, emb)
@@ -460,38 +460,55 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     # gathers fused (psvo.sample_util.sample_frames); others through their own
     # sample_rays and the boolean-mask gathers
     batched = all(getattr(kf, "uniform_pixel_sampling", False) for kf in kfs)
-    for it in range(num_iterations):
+    cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs)  # noqa: E731
+
+    def draw(it):
+        """iteration it's pixels (dirs_cam, rgb, depth) and sampler seed, in
+        the order the reference draws them (pixels, then the sampler noise)"""
         if batched:
             d_all, c_all, z_all = sample_util.sample_frames(kfs, N_rays)
-            dirs, rgbs, depths = [d_all], [c_all], [z_all]
         else:
             dirs, rgbs, depths = [], [], []
-        for kf in ([] if batched else kfs):
-            kf.sample_rays(N_rays)
-            idx = getattr(kf, "sample_idx", None)
-            if idx is None:
-                idx = kf.sample_mask.reshape(-1).nonzero().squeeze(1)
-            idx = idx.to(dev)
-            if idx.numel() != N_rays:
-                raise RuntimeError("bundle_adjust_frames: sample_rays gave %d rays, expected %d" % (idx.numel(), N_rays))
-            dirs.append(kf.rays_d.reshape(-1, 3).to(dev)[idx])
-            rgbs.append(kf.rgb.reshape(-1, 3).to(dev)[idx])
-            depths.append(kf.depth.reshape(-1).to(dev)[idx])
+            for kf in kfs:
+                kf.sample_rays(N_rays)
+                idx = getattr(kf, "sample_idx", None)
+                if idx is None:
+                    idx = kf.sample_mask.reshape(-1).nonzero().squeeze(1)
+                idx = idx.to(dev)
+                if idx.numel() != N_rays:
+                    raise RuntimeError("bundle_adjust_frames: sample_rays gave %d rays, expected %d"
+                                       % (idx.numel(), N_rays))
+                dirs.append(kf.rays_d.reshape(-1, 3).to(dev)[idx])
+                rgbs.append(kf.rgb.reshape(-1, 3).to(dev)[idx])
+                depths.append(kf.depth.reshape(-1).to(dev)[idx])
+            d_all, c_all, z_all = cat(dirs), cat(rgbs), cat(depths)
+        d_all = d_all.reshape(-1, 3).to(torch.float32).contiguous()
         nz = noise(it) if callable(noise) else None
         if seed_fn is not None:
             seed = int(seed_fn(it))
         else:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if nz is None else 0
+        return d_all, c_all, z_all, nz, seed
+
+    # the next iteration's pixels are drawn before this one's step, so the
+    # engine queues its query beside this step's weight gradients
+    # (psvo_map_frames.next_dirs_cam); injected noise (tests) runs unpipelined
+    ahead = lookahead and not callable(noise)
+    cur = draw(0)
+    for it in range(num_iterations):
+        nxt = draw(it + 1) if ahead and it + 1 < num_iterations else None
+        d_all, c_all, z_all, nz, seed = cur
         adam_step += 1
-        cur = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
+        cur_steps = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
         dp = eng.grad_exchange is not None
-        cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs)  # noqa: E731
-        eng.step_frames(cat(dirs), N_rays, poses, pm, pv, cur, lr_pose or 0.0, cat(rgbs), cat(depths), seed,
-                        noise=nz, adam_step=adam_step, apply_adam=not dp)
+        eng.step_frames(d_all, N_rays, poses, pm, pv, cur_steps, lr_pose or 0.0, c_all, z_all, seed, noise=nz,
+                        adam_step=adam_step, apply_adam=not dp, next_dirs_cam=nxt[0] if nxt else None,
+                        next_seed=nxt[4] if nxt else 0)
         if dp:  # data parallel: sum the union-batch gradient over ranks, then the same Adam everywhere
             eng.grad_exchange()
             eng.adam()
-        pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur)]
+        pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur_steps)]
+        cur = nxt if nxt is not None else (draw(it + 1) if it + 1 < num_iterations else None)
     # write back: optimiser steps, pose parameters and their Adam state
     with torch.no_grad():
         for st in [st_e] + st_d:
@@ -510,7 +527,7 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
 def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, voxel_size, step_size,
                          N_rays=512, num_iterations=10, truncation=0.1, max_voxel_hit=10, max_distance=10,
                          learning_rate=[1e-2, 5e-3], embed_optim=None, model_optim=None, resnet_optim=None,
-                         update_pose=True, noise=None, use_engine=True, engine=None, seed_fn=None):
+                         update_pose=True, noise=None, use_engine=True, engine=None, seed_fn=None, lookahead=True):
     """render_helpers.py:559-676 — mapping's render-and-optimise loop.
 
     Runs on the native engine (one psvo_map_step_frames call per iteration)
@@ -521,14 +538,16 @@ def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_c
     (parity tests); `engine` — a prepared psvo.engine.MappingEngine to use
     (e.g. one with a data-parallel EngineExchange: every rank passes the
     keyframes of its share of the union batch); `seed_fn` — iteration →
-    sampler seed (must agree across ranks when data parallel)."""
+    sampler seed (must agree across ranks when data parallel); `lookahead` —
+    queue each next iteration's query beside the current step's weight
+    gradients (the default; same results, tests compare both)."""
     if use_engine:
         eng = engine
         if eng is None:
             eng = _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim,
                               model_optim, resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays)
         if eng is not None and _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
-                                                     num_iterations, update_pose, noise, seed_fn):
+                                                     num_iterations, update_pose, noise, seed_fn, lookahead):
             return
         if engine is not None:
             raise RuntimeError("bundle_adjust_frames: the given engine cannot run this call (optimiser state)")

@@ -95,3 +95,88 @@ def test_bundle_adjust_matches_reference(use_engine):
     assert all(int(mo.state[p]["step"]) == iters for p in dec.parameters())
     assert int(kfs[1].optim.state[kfs[1].pose.data]["step"]) == iters
     assert len(kfs[0].optim.state) == 0
+
+
+def _ba_scene(seed_frames):
+    from psvo import synthetic as syn
+    from psvo.decoder import Decoder
+    from psvo.octree import Octree, map_states
+    from psvo.pose import OptimizablePose
+    scene = syn.room0()
+    tree = Octree()
+    tree.init(scene.grid_dim, 16, scene.voxel_size, 8)
+    tree.insert(syn.surface_voxels(scene, seed=0))
+    emb = (torch.randn(max(20000, tree.count_nodes()), 16, generator=torch.Generator().manual_seed(1)) * 0.05)
+    emb = emb.to(DEV).requires_grad_(True)
+    ms = map_states(tree, emb, scene.voxel_size, device=DEV)
+    torch.manual_seed(0)
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    kfs = []
+    for f, T in enumerate(syn.camera_poses(scene, 3, seed=seed_frames)):
+        fr = syn.SyntheticFrame(scene, T, scale=0.25, seed=11 + f, device=DEV)
+        fr.stamp = f
+        fr.pose = OptimizablePose.from_matrix(T).to(DEV)
+        fr.optim = torch.optim.Adam(fr.pose.parameters(), lr=1e-3)
+        fr.get_pose = fr.pose.matrix
+        kfs.append(fr)
+    return scene, ms, emb, dec, kfs
+
+
+@pytest.mark.parametrize("batched", [True, False])
+def test_bundle_adjust_lookahead_matches_unpipelined(batched):
+    """The pipelined loop (each next iteration's rays + query queued beside
+    the current step's weight gradients, after its pose update) against one
+    query per step, from the same state and seeds: the look-ahead is really
+    queued and consumed, the poses agree to 1e-6 and the map to Adam's
+    ulp-amplification bar (the embedding gradient's float atomics make even
+    two runs of one mode differ in the last bits), with the native keyframe
+    sampler (batched) and through the frames' own sample_rays."""
+    import types
+    from psvo import _lib as L
+    from psvo import render_helpers as RH
+    from psvo.criterion import Criterion
+    from psvo.engine import MappingEngine
+    results, queued = [], []
+    orig = MappingEngine.step_frames
+
+    def spy(self, *a, **k):
+        out = orig(self, *a, **k)
+        queued.append(int(L.lib().psvo_engine_queued(self.handle)))
+        return out
+
+    MappingEngine.step_frames = spy
+    iters = 5
+    try:
+        for lookahead in (False, True):
+            torch.manual_seed(123)
+            scene, ms, emb, dec, kfs = _ba_scene(5)
+            if not batched:
+                for kf in kfs:
+                    kf.uniform_pixel_sampling = False
+            crit = Criterion(types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0,
+                                                             "sdf_weight": 5000.0, "fs_weight": 10.0,
+                                                             "sdf_truncation": 0.1}, data_specs={"max_depth": 10.0}))
+            eo = torch.optim.Adam([emb], lr=5e-3)
+            mo = torch.optim.Adam(dec.parameters(), lr=5e-3)
+            RH._ENGINES.clear()
+            RH.bundle_adjust_frames(kfs, ms, dec, None, crit, scene.voxel_size, 0.01, N_rays=512,
+                                    num_iterations=iters, embed_optim=eo, model_optim=mo, update_pose=True,
+                                    lookahead=lookahead)
+            torch.cuda.synchronize()
+            assert len(RH._ENGINES) == 1
+            results.append((emb.detach().cpu(), [p.detach().cpu() for p in dec.parameters()],
+                            [kf.pose.data.detach().cpu() for kf in kfs]))
+            RH._ENGINES.clear()
+    finally:
+        MappingEngine.step_frames = orig
+    # one query queued after every pipelined step but the last; none unpipelined
+    assert queued == [0] * iters + [1] * (iters - 1) + [0]
+    (e0, d0, p0), (e1, d1, p1) = results
+    bound = 2.0 * 5e-3 * iters
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-6)
+    assert not torch.equal(p1[1], _ba_scene(5)[4][1].pose.data.detach().cpu())  # the poses did move
+    changed = (e0 != _ba_scene(5)[2].detach().cpu()).any(-1)
+    adam_close(e1[changed].numpy(), e0[changed].numpy(), tight=1e-5, frac=0.97, max_abs=bound)
+    for a, b in zip(d1, d0):
+        adam_close(a.numpy(), b.numpy(), tight=1e-4, frac=0.99, max_abs=bound)
