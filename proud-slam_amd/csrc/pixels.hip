@@ -85,11 +85,20 @@ __device__ __forceinline__ uint32_t px_key(const PxArgs &a, int f, int64_t i, fl
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-// pass 0 computes the keys (three logs each) and stores them; later passes
-// stream them back (4 B / pixel) instead of recomputing
-template <bool kCompute>
+// Keys.  SCORE: the reference's f32 score (three logs) as a 32-bit key,
+// computed and stored by pass 0, streamed back by the later passes.  FAST
+// (uniform weights, generated uniforms — the keyframe sampler's case): the
+// 24-bit integer m behind u = m·2⁻²⁴ itself.  The score is a non-decreasing
+// function of u when every pixel has the same weight (log p is one constant,
+// g(u) and f32 rounding are monotone), so the n largest m are n largest
+// scores — a tie in score is a tie topk breaks arbitrarily too — with no
+// logs and no key array.
+template <bool FAST, bool kCompute>
 __device__ __forceinline__ uint32_t px_key_at(const PxArgs &a, int f, int64_t i, float den) {
-    if constexpr (kCompute) {
+    if constexpr (FAST) {
+        const uint64_t key = a.seed * 0x9E3779B97F4A7C15ull + ((uint64_t)f << 40) + (uint64_t)i;
+        return px_mix32(key) >> 8;
+    } else if constexpr (kCompute) {
         const uint32_t k = px_key(a, f, i, den);
         a.keys[(int64_t)f * a.n_pix + i] = k;
         return k;
@@ -97,6 +106,14 @@ __device__ __forceinline__ uint32_t px_key_at(const PxArgs &a, int f, int64_t i,
         return a.keys[(int64_t)f * a.n_pix + i];
     }
 }
+
+// radix digits, most significant first: SCORE 12 / 12 / 8 bits, FAST 12 / 12
+template <bool FAST>
+constexpr int px_passes() { return FAST ? 2 : 3; }
+template <bool FAST>
+constexpr int px_shift(int p) { return FAST ? (p == 0 ? 12 : 0) : (p == 0 ? 20 : (p == 1 ? 8 : 0)); }
+template <bool FAST>
+constexpr int px_width(int p) { return FAST ? 12 : (p == 2 ? 8 : 12); }
 
 // mask.sum() + 1e-7 of the frame (or of all frames): fixed-order sum of the
 // per-block partials (exact for 0/1 masks; weights null = all ones)
@@ -166,7 +183,7 @@ __device__ void px_select(const int *__restrict__ h, int rem, int *sh_suffix, in
 
 // the state after pass P − 1 (P ≥ 1): re-derived from the global histogram of
 // pass P − 1 and the state after pass P − 2 (written by the previous kernel)
-template <int P>
+template <bool FAST, int P>
 __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, uint32_t &prefix, int &rem) {
     uint32_t pfx = 0;
     int r = (int)a.k;
@@ -176,8 +193,8 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
     }
     px_select(a.hist + ((int64_t)(P - 1) * a.n_frames + f) * kPxBins, r, sh_suffix, &sh_res[0], &sh_res[1]);
     const uint32_t bin = (uint32_t)sh_res[0];
-    // prefix bits so far: pass 0 → 12, pass 1 → 24, pass 2 → 32
-    prefix = P == 1 ? bin : (P == 2 ? (pfx << 12) | bin : (pfx << 8) | bin);
+    // the key bits above px_shift(P − 1), fixed so far (after the last pass: the whole key)
+    prefix = P == 1 ? bin : (pfx << px_width<FAST>(P - 1)) | bin;
     rem = sh_res[1];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.state[(f * 3 + (P - 1)) * 2 + 0] = (int)prefix;
@@ -185,33 +202,33 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
     }
 }
 
-// pass P ∈ {0, 1, 2}: histogram of digit P of the keys whose higher digits
-// equal the prefix picked so far
-template <int P>
+// pass P: histogram of digit P of the keys whose higher digits equal the
+// prefix picked so far
+template <bool FAST, int P>
 __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
     __shared__ int h[kPxBins];
     __shared__ int sh_suffix[kPxThreads];
     __shared__ int sh_res[2];
+    constexpr int kShift = px_shift<FAST>(P);
+    constexpr uint32_t kMask = (1u << px_width<FAST>(P)) - 1u;
     const int f = blockIdx.y, b = blockIdx.x;
     for (int j = threadIdx.x; j < kPxBins; j += kPxThreads) h[j] = 0;
     uint32_t prefix = 0;
     int rem = 0;
-    if constexpr (P >= 1) px_state<P>(a, f, sh_suffix, sh_res, prefix, rem);
+    if constexpr (P >= 1) px_state<FAST, P>(a, f, sh_suffix, sh_res, prefix, rem);
     __syncthreads();
-    const float den = P == 0 ? px_den(a, f) : 0.0f;
+    const float den = (!FAST && P == 0) ? px_den(a, f) : 0.0f;
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
 #pragma unroll
         for (int q = 0; q < kPxPer; ++q) {
             const int64_t i = r0 + q;
             if (i >= i1) break;
-            const uint32_t key = px_key_at<P == 0>(a, f, i, den);
+            const uint32_t key = px_key_at<FAST, P == 0>(a, f, i, den);
             if constexpr (P == 0) {
-                atomicAdd(&h[key >> 20], 1);
-            } else if constexpr (P == 1) {
-                if ((key >> 20) == prefix) atomicAdd(&h[(key >> 8) & 0xfffu], 1);
+                atomicAdd(&h[(key >> kShift) & kMask], 1);
             } else {
-                if ((key >> 8) == prefix) atomicAdd(&h[key & 0xffu], 1);
+                if ((key >> px_shift<FAST>(P - 1)) == prefix) atomicAdd(&h[(key >> kShift) & kMask], 1);
             }
         }
     }
@@ -241,6 +258,7 @@ __device__ __forceinline__ void px_block_sum2(int &x, int &y, int (*part)[kPxThr
 }
 
 // the exact N-th largest key T of the frame; per block: keys > T, keys = T
+template <bool FAST>
 __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
     __shared__ int sh_suffix[kPxThreads];
     __shared__ int sh_res[2];
@@ -248,7 +266,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
     const int f = blockIdx.y, b = blockIdx.x;
     uint32_t T;
     int rem;
-    px_state<3>(a, f, sh_suffix, sh_res, T, rem);
+    px_state<FAST, px_passes<FAST>()>(a, f, sh_suffix, sh_res, T, rem);
     const float den = 0.0f;
     const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
     int gt = 0, eq = 0;
@@ -257,7 +275,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
         for (int q = 0; q < kPxPer; ++q) {
             const int64_t i = r0 + q;
             if (i >= i1) break;
-            const uint32_t key = px_key_at<false>(a, f, i, den);
+            const uint32_t key = px_key_at<FAST, false>(a, f, i, den);
             gt += key > T;
             eq += key == T;
         }
@@ -274,6 +292,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
 // its output row = #{keys > T before p} + min(#{keys = T before p}, ties).
 // Both counts come from one packed (eq << 16 | gt) block scan per round of
 // 1024 pixels (4 consecutive pixels per thread).
+template <bool FAST>
 __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, int64_t *__restrict__ idx,
                                                          float *__restrict__ out_dirs, float *__restrict__ out_rgb,
                                                          float *__restrict__ out_depth) {
@@ -281,8 +300,9 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
     __shared__ int wave_tot[kPxThreads / kWave];
     const int f = blockIdx.y, b = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t T = (uint32_t)a.state[(f * 3 + 2) * 2 + 0];
-    const int ties = a.state[(f * 3 + 2) * 2 + 1];  // keys = T to take, in pixel order
+    constexpr int kLast = px_passes<FAST>() - 1;
+    const uint32_t T = (uint32_t)a.state[(f * 3 + kLast) * 2 + 0];
+    const int ties = a.state[(f * 3 + kLast) * 2 + 1];  // keys = T to take, in pixel order
     int gt_run = 0, eq_run = 0;                     // counts before this block, then before each round
     for (int j = threadIdx.x; j < b; j += kPxThreads) {
         gt_run += a.counts[(f * kPxMaxBlocks + j) * 2 + 0];
@@ -300,7 +320,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
         for (int q = 0; q < kPxPer; ++q) {
             key[q] = 0;
             if (r0 + q < i1) {
-                key[q] = px_key_at<false>(a, f, r0 + q, den);
+                key[q] = px_key_at<FAST, false>(a, f, r0 + q, den);
                 packed += (key[q] > T ? 1 : 0) + (key[q] == T ? (1 << 16) : 0);
             }
         }
@@ -394,14 +414,22 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     if (frames)
         for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(a.hist, 0, sizeof(int) * 3 * n_frames * kPxBins, st) != hipSuccess)
+    if (hipMemsetAsync(a.hist, 0, sizeof(int) * (weights || u ? 3 : 2) * n_frames * kPxBins, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
     const dim3 grid(a.nb, n_frames);
     if (weights) hipLaunchKernelGGL(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
-    hipLaunchKernelGGL(k_px_hist<0>, grid, dim3(kPxThreads), 0, st, a);
-    hipLaunchKernelGGL(k_px_hist<1>, grid, dim3(kPxThreads), 0, st, a);
-    hipLaunchKernelGGL(k_px_hist<2>, grid, dim3(kPxThreads), 0, st, a);
-    hipLaunchKernelGGL(k_px_count, grid, dim3(kPxThreads), 0, st, a);
-    hipLaunchKernelGGL(k_px_write, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
+    if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys, two passes
+        hipLaunchKernelGGL((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
+    } else {
+        hipLaunchKernelGGL((k_px_hist<false, 0>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL((k_px_hist<false, 1>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL((k_px_hist<false, 2>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_px_count<false>, grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_px_write<false>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb,
+                           out_depth);
+    }
     return check_launch("sample_pixels");
 }
