@@ -36,6 +36,11 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: aggregate L2 (8 x 4 MiB) ≈34.5 T
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (v_mfma_f32_32x32x2_f32) dense peak
 
 
+def log(msg):
+    """Progress on stderr (setup of the large scenes takes minutes)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,10 +290,14 @@ def main():
     import types
     _lib.lib()
 
+    log(f"scene {args.scene}: octree, embeddings, decoder W={args.width}")
     scene, tree, ms, emb, dec = build_scene(args, device, rank)
+    log(f"{args.frames} keyframes ({tree.count_nodes()} octree nodes)")
     kfs = build_keyframes(args, scene, device, rank)
     batches = keyframe_batches(kfs, args.rays_per_frame, args.pool)
+    log("step-size calibration")
     step_size, spr = calibrate_step(ms, batches, args.samples_per_ray, scene.voxel_size, world)
+    log(f"step {step_size:.5f} m, {spr:.1f} samples / hit ray; timing the {args.path} path")
     crit_cfg, max_depth = SCENE_CRITERIA.get(args.scene, DEFAULT_CRITERIA)
     crit_args = types.SimpleNamespace(criteria=dict(crit_cfg), data_specs={"max_depth": max_depth})
     criterion = Criterion(crit_args)
@@ -588,7 +597,9 @@ def main():
         "kernels_ms": kt,
         "kernels_ms_overlapped": kt_overlap,
     }
+    log("done timing")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baseline")
         result["cpu_baseline"] = cpu_baseline(args, scene, tree, step_size, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

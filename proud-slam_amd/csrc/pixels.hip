@@ -88,7 +88,7 @@ __device__ __forceinline__ uint32_t px_key(const PxArgs &a, int f, int64_t i, fl
 // Keys.  SCORE: the reference's f32 score (three logs) as a 32-bit key,
 // computed and stored by pass 0, streamed back by the later passes.  FAST
 // (uniform weights, generated uniforms — the keyframe sampler's case): the
-// 24-bit integer m behind u = m·2⁻²⁴ itself.  The score is a non-decreasing
+// 24-bit integer m behind u = m·2⁻²⁴ itself, recomputed by every pass.  The score is a non-decreasing
 // function of u when every pixel has the same weight (log p is one constant,
 // g(u) and f32 rounding are monotone), so the n largest m are n largest
 // scores — a tie in score is a tie topk breaks arbitrarily too — with no
@@ -107,13 +107,15 @@ __device__ __forceinline__ uint32_t px_key_at(const PxArgs &a, int f, int64_t i,
     }
 }
 
-// radix digits, most significant first: SCORE 12 / 12 / 8 bits, FAST 12 / 12
+// radix digits, most significant first: SCORE 12 / 12 / 8 bits, FAST 8 / 8 / 8
+// (the 24-bit integer keys are uniform: with 8-bit digits a block flushes at
+// most 256 bins to the global histogram, not ~2,600 of 4,096)
 template <bool FAST>
-constexpr int px_passes() { return FAST ? 2 : 3; }
+constexpr int px_passes() { return 3; }
 template <bool FAST>
-constexpr int px_shift(int p) { return FAST ? (p == 0 ? 12 : 0) : (p == 0 ? 20 : (p == 1 ? 8 : 0)); }
+constexpr int px_shift(int p) { return FAST ? 16 - 8 * p : (p == 0 ? 20 : (p == 1 ? 8 : 0)); }
 template <bool FAST>
-constexpr int px_width(int p) { return FAST ? 12 : (p == 2 ? 8 : 12); }
+constexpr int px_width(int p) { return FAST ? 8 : (p == 2 ? 8 : 12); }
 
 // mask.sum() + 1e-7 of the frame (or of all frames): fixed-order sum of the
 // per-block partials (exact for 0/1 masks; weights null = all ones)
@@ -146,15 +148,16 @@ __global__ __launch_bounds__(kPxThreads) void k_px_wsum(PxArgs a) {
     }
 }
 
-// Pick the bin holding the rem-th largest key of a 4096-bin histogram
-// (highest bin first): bin → *bin_out, keys still needed inside it → *rem_out.
-// Thread t owns bins [16t, 16t + 16).
+// Pick the bin holding the rem-th largest key of a histogram of 256 · BPT
+// bins (highest bin first): bin → *bin_out, keys still needed inside it →
+// *rem_out.  Thread t owns bins [BPT·t, BPT·t + BPT).
+template <int BPT>
 __device__ void px_select(const int *__restrict__ h, int rem, int *sh_suffix, int *bin_out, int *rem_out) {
     const int t = threadIdx.x;
-    int v[16];
+    int v[BPT];
     int s = 0;
-    for (int j = 0; j < 16; ++j) {
-        v[j] = h[t * 16 + j];
+    for (int j = 0; j < BPT; ++j) {
+        v[j] = h[t * BPT + j];
         s += v[j];
     }
     sh_suffix[t] = s;
@@ -169,9 +172,9 @@ __device__ void px_select(const int *__restrict__ h, int rem, int *sh_suffix, in
     const int above = sh_suffix[t] - s;  // keys in the bins of threads t+1..
     if (above < rem && rem <= above + s) {
         int acc = above;
-        for (int j = 15; j >= 0; --j) {
+        for (int j = BPT - 1; j >= 0; --j) {
             if (acc + v[j] >= rem) {
-                *bin_out = t * 16 + j;
+                *bin_out = t * BPT + j;
                 *rem_out = rem - acc;
                 break;
             }
@@ -191,7 +194,8 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
         pfx = (uint32_t)a.state[(f * 3 + (P - 2)) * 2 + 0];
         r = a.state[(f * 3 + (P - 2)) * 2 + 1];
     }
-    px_select(a.hist + ((int64_t)(P - 1) * a.n_frames + f) * kPxBins, r, sh_suffix, &sh_res[0], &sh_res[1]);
+    px_select<(1 << px_width<FAST>(P - 1)) / kPxThreads>(a.hist + ((int64_t)(P - 1) * a.n_frames + f) * kPxBins, r,
+                                                         sh_suffix, &sh_res[0], &sh_res[1]);
     const uint32_t bin = (uint32_t)sh_res[0];
     // the key bits above px_shift(P − 1), fixed so far (after the last pass: the whole key)
     prefix = P == 1 ? bin : (pfx << px_width<FAST>(P - 1)) | bin;
@@ -211,8 +215,9 @@ __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
     __shared__ int sh_res[2];
     constexpr int kShift = px_shift<FAST>(P);
     constexpr uint32_t kMask = (1u << px_width<FAST>(P)) - 1u;
+    constexpr int kBins = 1 << px_width<FAST>(P);
     const int f = blockIdx.y, b = blockIdx.x;
-    for (int j = threadIdx.x; j < kPxBins; j += kPxThreads) h[j] = 0;
+    for (int j = threadIdx.x; j < kBins; j += kPxThreads) h[j] = 0;
     uint32_t prefix = 0;
     int rem = 0;
     if constexpr (P >= 1) px_state<FAST, P>(a, f, sh_suffix, sh_res, prefix, rem);
@@ -234,7 +239,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
     }
     __syncthreads();
     int *gh = a.hist + ((int64_t)P * a.n_frames + f) * kPxBins;
-    for (int j = threadIdx.x; j < kPxBins; j += kPxThreads)
+    for (int j = threadIdx.x; j < kBins; j += kPxThreads)
         if (h[j]) atomicAdd(&gh[j], h[j]);
 }
 
@@ -414,13 +419,14 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     if (frames)
         for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(a.hist, 0, sizeof(int) * (weights || u ? 3 : 2) * n_frames * kPxBins, st) != hipSuccess)
+    if (hipMemsetAsync(a.hist, 0, sizeof(int) * 3 * n_frames * kPxBins, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
     const dim3 grid(a.nb, n_frames);
     if (weights) hipLaunchKernelGGL(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
-    if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys, two passes
+    if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
         hipLaunchKernelGGL((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
         hipLaunchKernelGGL((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
+        hipLaunchKernelGGL((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
         hipLaunchKernelGGL(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
         hipLaunchKernelGGL(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
     } else {

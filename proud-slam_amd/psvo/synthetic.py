@@ -181,6 +181,31 @@ def _ray_boxes(o, d, boxes):
     return t_best, hit_box
 
 
+def _ray_boxes_torch(o, d, boxes, device):
+    """_ray_boxes in float64 torch on `device` (same IEEE operations, same
+    result; the numpy loop takes minutes for a full frame of config E's
+    1,125 boxes)."""
+    o = torch.as_tensor(np.ascontiguousarray(o), dtype=torch.float64, device=device)
+    d = torch.as_tensor(np.ascontiguousarray(d), dtype=torch.float64, device=device)
+    inv = 1.0 / d
+    t_best = torch.full((o.shape[0],), math.inf, dtype=torch.float64, device=device)
+    hit_box = torch.full((o.shape[0],), -1, dtype=torch.int64, device=device)
+    inf = torch.tensor(math.inf, dtype=torch.float64, device=device)
+    for bi, b in enumerate(boxes):
+        lo = torch.as_tensor(np.asarray(b.lo, np.float64), device=device)
+        hi = torch.as_tensor(np.asarray(b.hi, np.float64), device=device)
+        t0 = (lo - o) * inv
+        t1 = (hi - o) * inv
+        mn, mx = torch.minimum(t0, t1), torch.maximum(t0, t1)  # NaN propagates as in np.minimum / np.maximum
+        tmin = torch.fmax(torch.fmax(mn[:, 0], mn[:, 1]), mn[:, 2])  # np.nanmax: NaN ignored
+        tmax = torch.fmin(torch.fmin(mx[:, 0], mx[:, 1]), mx[:, 2])
+        t = tmax if b.inside else torch.where(tmin > 1e-6, tmin, inf)
+        ok = (tmax >= tmin) & (t > 1e-6) & (t < t_best)
+        t_best = torch.where(ok, t, t_best)
+        hit_box = torch.where(ok, torch.full_like(hit_box, bi), hit_box)
+    return t_best.cpu().numpy(), hit_box.cpu().numpy()
+
+
 def gumbel_topk_pixels(H, W, n, generator):
     """sample_util.py:4-20 on a uniform mask: n distinct pixel ids."""
     logp = torch.full((H * W,), math.log(1.0 / (H * W) + 1e-7))
@@ -233,7 +258,10 @@ class SyntheticFrame:
         Rm = np.asarray(T, np.float64)[:3, :3]
         d_world = d_cam.reshape(-1, 3).astype(np.float64) @ Rm.T
         o_world = np.broadcast_to(np.asarray(T, np.float64)[:3, 3], d_world.shape)
-        t, hb = _ray_boxes(o_world, d_world, scene.boxes)
+        if torch.device(device).type == "cuda":
+            t, hb = _ray_boxes_torch(o_world, d_world, scene.boxes, device)
+        else:
+            t, hb = _ray_boxes(o_world, d_world, scene.boxes)
         t = np.where(np.isfinite(t), t, 0.0)
         p = o_world + d_world * t[:, None]
         col = 0.5 + 0.5 * np.sin(np.stack([1.3 * p[:, 0] + 0.7 * hb, 1.7 * p[:, 1], 2.1 * p[:, 2] + 0.3 * hb], -1))
