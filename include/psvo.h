@@ -106,6 +106,21 @@ int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const float *rays_o,
                               float step_size, int *hit_idx, float *hit_t0, float *hit_t1, int *ray_nv,
                               float *ray_dsum, int *stats);
 
+/* The octree breadth-first with siblings contiguous, one 32-B record per
+ * node {f32 cx, cy, cz, side (int bits) | i32 reference id, first child
+ * record, child mask, 0} (csrc/tree_pack.hip), built on the device from the
+ * reference arrays: packed = n_nodes x 32 B (16-B aligned), workspace
+ * psvo_pack_tree_workspace_ints(n_nodes) ints.  Valid until the map changes. */
+int64_t psvo_pack_tree_workspace_ints(int64_t n_nodes);
+int psvo_pack_tree(void *stream, int64_t n_nodes, const float *centres, const int *structure, int *workspace,
+                   void *packed);
+/* psvo_ray_intersect_sorted reading the packed records (same results, the
+ * reference ids); centres / structure serve the serial-DFS fallback. */
+int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, const float *rays_o, const float *rays_d,
+                                     const void *packed, const float *centres, const int *structure, float voxel_size,
+                                     float max_distance, float step_size, int *hit_idx, float *hit_t0, float *hit_t1,
+                                     int *ray_nv, float *ray_dsum, int *stats);
+
 /* ray_rank[R] = rank among hit rays or -1; rank_ray[R_hit] = original ray. */
 int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray);
 
@@ -393,6 +408,9 @@ typedef struct psvo_map_desc {
     /* optional flat gradient buffer f32[psvo_map_grad_floats(n_emb)]:
      * [embeddings | W1, b1, ..., W5, b5]; NULL = engine-owned */
     float *grad_flat;
+    /* optional psvo_pack_tree records of this map: the query traverses them
+     * (same results); NULL = the reference arrays */
+    const void *packed;
 } psvo_map_desc;
 
 enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */

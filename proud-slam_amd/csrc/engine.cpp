@@ -421,7 +421,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     mark(e, st, PSVO_TIME_INTERSECT, 0);
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
-                                    ray_rank, rank_ray));
+                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed)));
     const EngineExchange &x = e->x;
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced

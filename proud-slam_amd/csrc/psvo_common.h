@@ -31,10 +31,16 @@ constexpr float kMaxDepthFill = 10.0f;  // voxel_helpers.py:24 MAX_DEPTH
 
 inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// one octree node as the packed traversal reads it (tree_pack.hip)
+struct PackRec {  // 32 B, 16-B aligned
+    float4 c;     // centre x, y, z; side (int bits)
+    int4 i;       // reference node id, first child record (-1: none), child mask, 0
+};
+
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray);
+                     int *rank_ray, const PackRec *packed = nullptr);
 
 // data-parallel query (svo_query.hip): rows of the exchanged slot-0 table for
 // a union batch of at most max_rays_global rays; pack this rank's 8 words;

@@ -247,10 +247,16 @@ __device__ uint64_t kth_key(const KeyLds &S, int n, int kth, int lane) {
     return found;
 }
 
+// PACKED: candidates are records of the breadth-first packed tree
+// (tree_pack.hip: centre + side and ref id / first child / child mask in one
+// 32-B record, siblings contiguous) instead of reference node ids into the
+// two AoS rows; the same floats, the same keys, the reference ids emitted.
+template <bool PACKED>
 __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
                                                           const float *__restrict__ rays_d,
                                                           const float *__restrict__ centres,
-                                                          const int *__restrict__ structure, float voxel_size,
+                                                          const int *__restrict__ structure,
+                                                          const PackRec *__restrict__ packed, float voxel_size,
                                                           float max_distance, float step_size,
                                                           int *__restrict__ hit_idx, float *__restrict__ hit_t0,
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
@@ -292,16 +298,26 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             const bool live = lane < n && !(bounded && key > kbound);
             const int n_eff = __popcll(__ballot(live));
             int row[8];
-            int side = 0;
+            int side = 0, first = 0, cmask = 0, ref = node;
             float a = 0.f, b = 0.f;
             bool hit = false;
             if (live) {
-                const int *rw = structure + (int64_t)node * 9;
+                if constexpr (PACKED) {
+                    const float4 pc = packed[node].c;
+                    const int4 pi = packed[node].i;
+                    side = __float_as_int(pc.w);
+                    ref = pi.x;
+                    first = pi.y;
+                    cmask = pi.z;
+                    hit = ray_aabb(o, inv, pc.x, pc.y, pc.z, half * (float)side, a, b);
+                } else {
+                    const int *rw = structure + (int64_t)node * 9;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) row[u] = rw[u];
-                side = rw[8];
-                const float *pc = centres + (int64_t)node * 3;
-                hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                    for (int u = 0; u < 8; ++u) row[u] = rw[u];
+                    side = rw[8];
+                    const float *pc = centres + (int64_t)node * 3;
+                    hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                }
             }
             const bool leaf = hit && side == 1;
             const bool inner = hit && side != 1;
@@ -311,8 +327,12 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             }
             int c = 0;
             if (inner) {
+                if constexpr (PACKED) {
+                    c = __popc(cmask);
+                } else {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) c += row[u] > -1;
+                    for (int u = 0; u < 8; ++u) c += row[u] > -1;
+                }
             }
             const int incl = wave_incl_scan(c, lane);
             // a prune drops everything below the popped chunk (all keys > kbound)
@@ -339,10 +359,11 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                 const int cd = dep + 1;
 #pragma unroll
                 for (int u = 7; u >= 0; --u) {
-                    if (row[u] > -1) {
+                    const bool present = PACKED ? ((cmask >> u) & 1) != 0 : row[u] > -1;
+                    if (present) {
                         const int pos = base + (T - 1 - g);
                         S.skey[pos] = key | key_digit(u, cd);
-                        S.snode[pos] = row[u];
+                        S.snode[pos] = PACKED ? first + __popc(cmask & ((1 << u) - 1)) : row[u];
                         S.sdep[pos] = (uint8_t)cd;
                         ++g;
                     }
@@ -352,7 +373,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             if (acc && leaf) {
                 const int pos = nl + __popcll(lb & below);
                 S.lkey[pos] = key;
-                S.lidx[pos] = node;
+                S.lidx[pos] = ref;
                 S.lt0[pos] = a;
                 S.lt1[pos] = b;
             }
@@ -1127,11 +1148,28 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st, n_rays,
-                       rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
-                       ray_nv, ray_dsum, stats);
+    hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+                       n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
+}
+
+extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, const float *rays_o, const float *rays_d,
+                                                const void *packed, const float *centres, const int *structure,
+                                                float voxel_size, float max_distance, float step_size, int *hit_idx,
+                                                float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum,
+                                                int *stats) {
+    PSVO_REQUIRE(n_rays >= 0, "ray_intersect_sorted_packed: n_rays < 0");
+    PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted_packed: step/voxel must be > 0");
+    PSVO_REQUIRE(packed && ((uintptr_t)packed & 15) == 0, "ray_intersect_sorted_packed: packed records (16-B aligned)");
+    if (n_rays == 0) return PSVO_OK;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+                       n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
+                       max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
+    return check_launch("ray_intersect_sorted_packed");
 }
 
 namespace psvo {
@@ -1140,13 +1178,18 @@ namespace psvo {
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray) {
+                     int *rank_ray, const PackRec *packed) {
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_intersect_sorted, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st, n_rays,
-                       rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1,
-                       ray_nv, ray_dsum, stats);
+    if (packed)
+        hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+                           n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+    else
+        hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+                           n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
     hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
                        ray_rank, rank_ray);
     return check_launch("intersect_ranked");

@@ -46,6 +46,9 @@ _SIGNATURES = {
     "psvo_criterion_reduce": (_i32, [_vp, _i64, _vp, _vp]),
     "psvo_rows_workspace_ints": (_i64, [_i64]),
     "psvo_sample_pixels_workspace_ints": (_i64, [_i32, _i64]),
+    "psvo_pack_tree_workspace_ints": (_i64, [_i64]),
+    "psvo_pack_tree": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "psvo_ray_intersect_sorted_packed": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _f32] + [_vp] * 6),
     "psvo_sample_pixels": (_i32, [_vp, _i32, _i64, _i64, _vp, _i32, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_compact": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_scatter_add": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),

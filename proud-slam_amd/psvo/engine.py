@@ -11,6 +11,7 @@ exp_avg / exp_avg_sq / step).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -27,7 +28,7 @@ class MapDesc(ctypes.Structure):
                 ("voxel_size", _f32), ("step_size", _f32), ("max_distance", _f32), ("truncation", _f32),
                 ("max_depth", _f32), ("w_rgb", _f32), ("w_depth", _f32), ("w_fs", _f32), ("w_sdf", _f32),
                 ("lr_emb", _f64), ("lr_dec", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
-                ("grad_flat", _vp)]
+                ("grad_flat", _vp), ("packed", _vp)]
 
 
 class MapFrames(ctypes.Structure):
@@ -87,6 +88,8 @@ class MappingEngine:
                                      dtype=torch.float32, device=self.emb.device)
         d.grad_flat = self.grad_flat.data_ptr()
         self.desc = d
+        self.packed = None
+        self.refresh_tree()
         self._queued = []   # (caller's rays_o, rays_d, seed, converted ro, rd) per queued query
         self.exchange = None
         self.grad_exchange = None
@@ -94,6 +97,23 @@ class MappingEngine:
         if not h:
             raise L.PsvoError("psvo_engine_new failed")
         self.handle = _vp(h)
+
+    def refresh_tree(self):
+        """(Re)build the breadth-first packed node records the query
+        traverses (psvo_pack_tree; same hits as the reference arrays) from the
+        current centres / structure — after the map changed in place.
+        PSVO_PACKED=0 keeps the reference-array traversal."""
+        if os.environ.get("PSVO_PACKED", "1") == "0":
+            self.packed = None
+            self.desc.packed = None
+            return
+        n = self.centres.shape[0]
+        dev = self.centres.device
+        if self.packed is None or self.packed.numel() != n * 32:
+            self.packed = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        ws = torch.empty(int(_lib().psvo_pack_tree_workspace_ints(n)), dtype=torch.int32, device=dev)
+        L.call("psvo_pack_tree", L.stream_of(dev), n, self.centres, self.structure, ws, self.packed)
+        self.desc.packed = self.packed.data_ptr()
 
     def bind_adam(self, emb_m, emb_v, dec_m, dec_v):
         """Use external Adam moments (e.g. the state tensors of the caller's

@@ -428,6 +428,7 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         return False  # parameters at different Adam steps: the engine steps them together
     eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
                   [st["exp_avg_sq"] for st in st_d])
+    eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
     eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
     adam_step = steps.pop()
     dev = emb.device
