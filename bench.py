@@ -516,6 +516,10 @@ def main():
     hs = head_stats if head_stats["n"] else stats
     h_n = max(hs["n"], 1)
     h_m, h_r, h_v = hs["m"] / h_n, hs["r_hit"] / h_n, hs["visits"] / h_n
+    if world > 1:  # per-GPU averages over the union of the ranks' batches (the calibration's population)
+        t = torch.tensor([h_m, h_r, h_v], dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        h_m, h_r, h_v = (float(x) / world for x in t.cpu())
     q_keys = ("intersect", "sample", "points", "interp_fwd", "interp_bwd")
     q_parts = {k: kt[k] for k in q_keys}
     q_ms = sum(q_parts.values())
