@@ -248,6 +248,20 @@ def _cpu_model():
     return None
 
 
+def _physical_cores():
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo: the host's physical cores."""
+    cores, phys = set(), None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+    except OSError:
+        return None
+    return len(cores) or None
+
+
 def cpu_baseline(args, scene, tree, step_size, seconds):
     """Oracle (reference algorithm restated: C kernels + torch-CPU render /
     loss / autograd) on the host cores, bounded sample of the same workload."""
@@ -271,10 +285,11 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
     dt = time.time() - t0
     rays = n_it * ro.shape[1]
     return {"value": rays / dt, "unit": "rays/s", "cores": int(torch.get_num_threads()), "kind": "port",
-            "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count(),
+            "cpu_model": _cpu_model(), "host_physical_cores": _physical_cores(), "host_logical_cpus": os.cpu_count(),
             "process_cpu_share": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
             "sample": f"{n_it} iterations x {ro.shape[1]} rays ({args.scene}, {args.frames}x{args.rays_per_frame}), "
-                      f"oracle C kernels single-thread + torch-CPU render/loss/backward, {dt:.1f}s"}
+                      f"oracle C kernels (OpenMP over rays) + torch-CPU render/loss/backward, "
+                      f"{torch.get_num_threads()} threads, {dt:.1f}s"}
 
 
 def main():

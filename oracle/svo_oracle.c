@@ -265,6 +265,9 @@ int64_t oracle_svo_intersect(int64_t n_rays, const float *ray_start, const float
 {
     const float half_voxel = voxelsize * 0.5f;
     int64_t visits = 0;
+    int overflow = 0;
+    /* rays are independent: OpenMP over rays (the CPU baseline's threads) */
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : visits) reduction(| : overflow)
     for (int64_t r = 0; r < n_rays; ++r) {
         int *oi = idx + r * n_max;
         float *omin = min_depth + r * n_max;
@@ -274,11 +277,14 @@ int64_t oracle_svo_intersect(int64_t n_rays, const float *ray_start, const float
             omin[l] = 0.0f;
             omax[l] = 0.0f;
         }
-        int stack[256];
+        int stack[256 + 8]; /* pushes of the last popped node may pass 256 before the check */
         int ptr = 0, cnt = 0;
         stack[0] = 0; /* root is node 0 (intersect_gpu.cu:232) */
         while (ptr > -1 && cnt < n_max) {
-            if (ptr >= 256) return -1; /* reference: assert(ptr < 256) */
+            if (ptr >= 256) { /* reference: assert(ptr < 256) */
+                overflow = 1;
+                break;
+            }
             const int k = stack[ptr--];
             ++visits;
             const int side = children9[(int64_t)k * 9 + 8];
@@ -298,7 +304,7 @@ int64_t oracle_svo_intersect(int64_t n_rays, const float *ray_start, const float
             }
         }
     }
-    return visits;
+    return overflow ? -1 : visits;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -322,6 +328,8 @@ void oracle_inverse_cdf(int b, int num_rays, int max_hits, int max_steps, float 
         int *out_idx = out_idx0 + (int64_t)bi * num_rays * max_steps;
         float *out_depth = out_depth0 + (int64_t)bi * num_rays * max_steps;
         float *out_dists = out_dists0 + (int64_t)bi * num_rays * max_steps;
+        /* rays write disjoint rows (the slot-0 / next-slot reads are reads) */
+#pragma omp parallel for schedule(dynamic, 64)
         for (int j = 0; j < num_rays; ++j) {
             const int H = j * max_hits, K = j * max_steps;
             int bin = 0, s = 0;
