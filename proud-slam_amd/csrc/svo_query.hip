@@ -230,22 +230,33 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     return v;
 }
 
-// 50th smallest key of the leaf list (keys unique): the threshold of the prune
+// kth smallest key of the leaf list (n <= 128, keys unique; the prune's
+// threshold is the 50th): a bitonic sort
+// of the 128 (padded) keys held two per lane — 28 compare-exchange stages of
+// register / cross-lane exchanges instead of an O(n²) rank count in LDS
 __device__ uint64_t kth_key(const KeyLds &S, int n, int kth, int lane) {
-    uint64_t found = ~0ull;
-    for (int i = lane; i < n; i += kWave) {
-        const uint64_t ki = S.lkey[i];
-        int rank = 0;
-        for (int j = 0; j < n; ++j) rank += S.lkey[j] < ki;
-        if (rank == kth) found = ki;
-    }
+    uint64_t v0 = lane < n ? S.lkey[lane] : ~0ull;
+    uint64_t v1 = lane + kWave < n ? S.lkey[lane + kWave] : ~0ull;
 #pragma unroll
-    for (int sh = 32; sh > 0; sh >>= 1) {
-        const uint64_t o = __shfl_xor(found, sh, kWave);
-        found = o < found ? o : found;
+    for (int k = 2; k <= 2 * kWave; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j == kWave) {  // partners lane / lane + 64: element lane ascends (k = 128)
+                const uint64_t lo = v0 < v1 ? v0 : v1, hi = v0 < v1 ? v1 : v0;
+                v0 = lo;
+                v1 = hi;
+            } else {
+                const bool lower = (lane & j) == 0;
+                const uint64_t p0 = __shfl_xor(v0, j, kWave), p1 = __shfl_xor(v1, j, kWave);
+                const bool up0 = (lane & k) == 0, up1 = ((lane + kWave) & k) == 0;
+                v0 = (lower == up0) ? (v0 < p0 ? v0 : p0) : (v0 < p0 ? p0 : v0);
+                v1 = (lower == up1) ? (v1 < p1 ? v1 : p1) : (v1 < p1 ? p1 : v1);
+            }
+        }
     }
-    return found;
+    return kth < kWave ? __shfl(v0, kth, kWave) : __shfl(v1, kth - kWave, kWave);
 }
+
 
 // PACKED: candidates are records of the breadth-first packed tree
 // (tree_pack.hip: centre + side and ref id / first child / child mask in one
