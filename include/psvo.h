@@ -466,11 +466,11 @@ void psvo_engine_free(psvo_engine *e);
  * operands were produced on (the collective must be ordered on it):
  *   PSVO_XCH_GATHER_I32: xi32[out + r·count + k] = rank r's xi32[in + k]
  *   PSVO_XCH_SUM_I32 / _F64: in-place sum of xi32 / xf64 [in, in + count)
- * PSVO_XCH_QUERY is or-ed into ops issued by psvo_map_query (they may run
- * concurrently with the previous step's: use a separate communicator).
+ * PSVO_XCH_QUERY is or-ed into ops issued by psvo_map_query or a
+ * psvo_map_step_frames look-ahead (they may run concurrently with the
+ * previous step's: use a separate communicator).
  * xi32: psvo_engine_exchange_words(world, max_rays_global) device int32;
- * xf64: 16 + 8 x 64 device doubles (count sums, loss sums, the keyframe pose
- * gradients of psvo_map_step_frames, summed over ranks).  Returns non-zero on failure.  Exchanged per step:
+ * xf64: 16 device doubles (count sums, loss sums).  Returns non-zero on failure.  Exchanged per step:
  * 8 + 1 words per rank (all-gathered), a [200, 50] int32 table of the
  * sampler's slot-0 voxel ids, 16 doubles; then the caller sums grad_flat
  * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam. */
@@ -531,8 +531,10 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * False); pose_grad: device f32[F][8] output or NULL.  noise: the sampler's
  * uniform noise f32[200, K', max_steps] (voxel_helpers.py:323-328) or NULL
  * (drawn from seed).  No queued psvo_map_query may be pending.  Data parallel
- * (psvo_engine_set_exchange): each rank passes the keyframes of its part of
- * the union batch; pose gradients are summed over ranks.  At most 64 keyframes per call.
+ * (psvo_engine_set_exchange): the keyframes are split over the ranks — each
+ * rank passes its own keyframes, whose rays form its part of the union batch
+ * (rank order) — so every pose gradient of the union-batch loss is local (no
+ * pose exchange); every rank steps the poses it owns.  At most 64 keyframes per call.
  * Look-ahead: with next_dirs_cam (the next iteration's camera directions,
  * same layout; no injected noise) the call also queues the next iteration's
  * query — its rays need this step's pose update, which runs on a side stream

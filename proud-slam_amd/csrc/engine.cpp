@@ -702,15 +702,11 @@ int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
         ENG_BUF(float, gbuf, kPoseGrad, (size_t)fr->n_frames * 8 * sizeof(float));
         pg = gbuf;
     }
+    // data parallel: a keyframe belongs to one rank (each rank passes its own
+    // keyframes), so its rays — and its whole pose gradient of the union-batch
+    // loss — are local: no exchange
     ENG_CALL(psvo_pose_grad_frames(st, fr->n_frames, fr->rays_per_frame, q.r_hit, q.rank_ray, fr->dirs_cam, grad_od,
                                    grad_od + R * 3, fr->poses, pg));
-    const EngineExchange &x = e->x;
-    if (x.on()) {  // a keyframe's rays may sit on several ranks: the pose gradient is their sum
-        const int64_t nw = (int64_t)fr->n_frames * 8;
-        ENG_CALL(pose_grads_to_f64(st, nw, pg, x.xf64 + kXchF64Base));
-        ENG_CALL(x.call(PSVO_XCH_SUM_F64, kXchF64Base, kXchF64Base, nw, st, "pose gradients"));
-        ENG_CALL(pose_grads_from_f64(st, nw, pg, x.xf64 + kXchF64Base));
-    }
     pa->n = 0;
     pa->lr = fr->lr_pose;
     for (int f = 0; f < fr->n_frames; ++f) {

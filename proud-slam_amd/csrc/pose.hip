@@ -233,22 +233,6 @@ extern "C" int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_pe
 }
 
 namespace psvo {
-// data-parallel keyframe poses: the [F][8] float gradients ↔ doubles of the
-// exchange buffer (summed over ranks as f64, then every rank steps alike)
-__global__ void k_f32_f64(int64_t n, const float *__restrict__ a, double *__restrict__ b, int dir) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (dir == 0) b[i] = (double)a[i];
-    else const_cast<float *>(a)[i] = (float)b[i];
-}
-int pose_grads_to_f64(hipStream_t st, int64_t n, const float *g, double *x) {
-    hipLaunchKernelGGL(k_f32_f64, dim3(div_up(n, 256)), dim3(256), 0, st, n, g, x, 0);
-    return check_launch("pose_grads_to_f64");
-}
-int pose_grads_from_f64(hipStream_t st, int64_t n, float *g, const double *x) {
-    hipLaunchKernelGGL(k_f32_f64, dim3(div_up(n, 256)), dim3(256), 0, st, n, g, const_cast<double *>(x), 1);
-    return check_launch("pose_grads_from_f64");
-}
 }  // namespace psvo
 
 extern "C" int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,

@@ -79,11 +79,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready);
 
-// pose.hip: [F][8] float pose gradients ↔ f64 exchange words
-int pose_grads_to_f64(hipStream_t st, int64_t n, const float *g, double *x);
-int pose_grads_from_f64(hipStream_t st, int64_t n, float *g, const double *x);
-constexpr int kXchF64Base = 16;   // f64 exchange words: [0, 8) counts, [8, 16) loss sums, then pose gradients
-constexpr int kXchMaxFrames = 64;
+constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
 // dfeat is written, before the weight-gradient kernels are queued

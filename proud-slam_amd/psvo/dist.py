@@ -268,7 +268,7 @@ class EngineExchange:
         self.query_group = query_group if query_group is not None else group
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.xi32 = None
-        self.xf64 = torch.zeros(16 + 8 * 64, dtype=torch.float64, device=self.device)  # include/psvo.h
+        self.xf64 = torch.zeros(16, dtype=torch.float64, device=self.device)  # include/psvo.h
         self.error = None
         self._cb = None
 

@@ -117,9 +117,9 @@ def _xch_worker(rank, world, port, q):
         x.apply(XCH_GATHER_I32 | XCH_QUERY, 0, 8, 8)
         xi[40:50] = rank + 1
         x.apply(XCH_SUM_I32 | XCH_QUERY, 40, 40, 10)
-        xf[:16] = torch.arange(16, dtype=torch.float64) * (rank + 1)
+        xf[:] = torch.arange(16, dtype=torch.float64) * (rank + 1)
         x.apply(XCH_SUM_F64, 8, 8, 8)
-        q.put((rank, xi.numpy().copy(), xf[:16].numpy().copy()))
+        q.put((rank, xi.numpy().copy(), xf.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
