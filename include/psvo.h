@@ -380,6 +380,13 @@ int psvo_mesh_vertex_rows(void *stream, int64_t n_vox, const float *voxels, int6
 /* One Adam step (torch.optim.Adam, amsgrad off) over n_tensors f32 tensors:
  * host arrays of device pointers and element counts; `step` is the step
  * number after increment (bias corrections 1 - beta^step). */
+/* Sparse-exact Adam support for the embedding table (16 floats per row):
+ * mark the vertex rows of M samples' leaves (leaf i32[M], vertex_idx
+ * i32[N,8]) in flags u8[n_emb]; flag the rows whose Adam moments are
+ * non-zero (a state carried over from an optimiser). */
+int psvo_adam_mark_rows(void *stream, int64_t m, const int *leaf, const int *vertex_idx, uint8_t *flags);
+int psvo_adam_flags_from_state(void *stream, int64_t n_rows, const float *exp_avg, const float *exp_avg_sq,
+                               uint8_t *flags);
 int psvo_adam_step(void *stream, int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, double lr, double beta1,
                    double beta2, double eps, double weight_decay, int64_t step);
@@ -411,6 +418,12 @@ typedef struct psvo_map_desc {
     /* optional psvo_pack_tree records of this map: the query traverses them
      * (same results); NULL = the reference arrays */
     const void *packed;
+    /* optional u8[n_emb] sticky flags of the embedding rows ever touched: a
+     * single-GPU step marks its samples' vertex rows and Adam steps only the
+     * flagged rows (an untouched row has g = m = v = 0: the dense step leaves
+     * it unchanged, so the result is the same).  Initialise from a bound
+     * optimiser state with psvo_adam_flags_from_state.  NULL = dense Adam. */
+    uint8_t *emb_row_flags;
 } psvo_map_desc;
 
 enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */

@@ -331,7 +331,7 @@ struct PoseAdam {
 };
 
 static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_t adam_step,
-                    const PoseAdam *pa = nullptr) {
+                    const PoseAdam *pa = nullptr, bool sparse_rows = false) {
     constexpr int kMax = 11 + kXchMaxFrames;
     float *p[kMax];
     const float *g[kMax];
@@ -339,6 +339,8 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
     int64_t n[kMax], steps[kMax];
     double lr[kMax];
     int zero[kMax];
+    const uint8_t *rows[kMax] = {};
+    if (sparse_rows) rows[0] = d->emb_row_flags;  // the embedding table: flagged rows only
     p[0] = d->emb;
     g[0] = grads;
     m[0] = d->emb_m;
@@ -371,7 +373,7 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
         zero[cnt] = 0;
         steps[cnt] = pa->step[f];
     }
-    return adam_launch(st, cnt, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero, steps);
+    return adam_launch(st, cnt, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero, steps, rows);
 }
 
 extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
@@ -803,6 +805,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
     ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
+    // sparse-exact Adam (single GPU): the rows this step can touch, beside the decoder
+    const bool sparse_rows = d->emb_row_flags && !dist && !(flags & PSVO_STEP_NO_ADAM);
+    if (sparse_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
     if (dist) {
         ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
                                   q.z_vals, crit_ws, sums_c));
@@ -900,7 +905,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // ---- optimiser steps, the poses' with the map's (the map's are skipped
     // when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
-        ENG_CALL(map_adam(st, d, grads, adam_step, &pa));
+        ENG_CALL(map_adam(st, d, grads, adam_step, &pa, sparse_rows));
         e->grads_clean = true;
     } else {
         ENG_CALL(pose_adam(st, d, pa));

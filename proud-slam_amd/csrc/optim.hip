@@ -36,6 +36,7 @@ struct AdamTable {
     float lr_bc1[kAdamMaxTensors];  // lr / (1 - β1^t) per tensor
     float bc2_sqrt[kAdamMaxTensors];  // sqrt(1 - β2^t) per tensor (tensors may be at different steps t)
     int zero_grad[kAdamMaxTensors]; // write 0 into the gradient after use
+    const uint8_t *rows[kAdamMaxTensors];  // per-16-element-row flags: only flagged rows are stepped (NULL: all)
     int block_begin[kAdamMaxTensors + 1];
     int count;
 };
@@ -53,7 +54,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float beta1, float 
     const bool zg = tab.zero_grad[ti] != 0;
     float *__restrict__ m = tab.m[ti];
     float *__restrict__ v = tab.v[ti];
+    const uint8_t *__restrict__ rf = tab.rows[ti];
     for (int64_t i = base + threadIdx.x; i < base + kAdamSlice && i < n; i += 256) {
+        if (rf && !rf[i >> 4]) continue;  // a row never touched: g = m = v = 0, the step leaves it as it is
         float gi = g[i];
         float pi = p[i];
         if (wd != 0.0f) gi = gi + wd * pi;
@@ -67,10 +70,61 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float beta1, float 
     }
 }
 
+// Rows touched by a step: every vertex row of the leaves its samples
+// interpolate (render_helpers.py:104-156: the rows that can receive an
+// embedding gradient).  Flags are sticky — once touched, a row's moments are
+// non-zero and Adam must step it every iteration (torch.optim.Adam steps all
+// elements); a row never touched has g = m = v = 0, which the dense step
+// leaves bit-for-bit unchanged, so skipping it is exact.
+__global__ __launch_bounds__(256) void k_adam_mark_rows(int64_t m, const int *__restrict__ leaf,
+                                                        const int *__restrict__ vertex_idx, uint8_t *__restrict__ rf) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m * 8) return;
+    const int64_t s = e >> 3;
+    const int v = vertex_idx[(int64_t)leaf[s] * 8 + (e & 7)];
+    if (v >= 0 && !rf[v]) rf[v] = 1;
+}
+
+// flags of rows whose moments are already non-zero (a bound optimiser state)
+__global__ __launch_bounds__(256) void k_adam_flags_from_state(int64_t n_rows, const float *__restrict__ m,
+                                                               const float *__restrict__ v, uint8_t *__restrict__ rf) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    bool nz = false;
+    for (int c = 0; c < 16; c += 4) {
+        const float4 a = *reinterpret_cast<const float4 *>(m + r * 16 + c);
+        const float4 b = *reinterpret_cast<const float4 *>(v + r * 16 + c);
+        nz |= a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f || b.x != 0.f || b.y != 0.f || b.z != 0.f ||
+              b.w != 0.f;
+    }
+    if (nz) rf[r] = 1;
+}
+
 }  // namespace
 }  // namespace psvo
 
 using namespace psvo;
+
+extern "C" int psvo_adam_mark_rows(void *stream, int64_t m, const int *leaf, const int *vertex_idx, uint8_t *flags) {
+    PSVO_REQUIRE(m >= 0, "adam_mark_rows: bad size");
+    if (m == 0) return PSVO_OK;
+    PSVO_REQUIRE(leaf && vertex_idx && flags, "adam_mark_rows: null pointer");
+    hipLaunchKernelGGL(psvo::k_adam_mark_rows, dim3(psvo::div_up(m * 8, 256)), dim3(256), 0, psvo::as_stream(stream),
+                       m, leaf, vertex_idx, flags);
+    return psvo::check_launch("adam_mark_rows");
+}
+
+extern "C" int psvo_adam_flags_from_state(void *stream, int64_t n_rows, const float *exp_avg,
+                                          const float *exp_avg_sq, uint8_t *flags) {
+    PSVO_REQUIRE(n_rows >= 0, "adam_flags_from_state: bad size");
+    if (n_rows == 0) return PSVO_OK;
+    PSVO_REQUIRE(exp_avg && exp_avg_sq && flags, "adam_flags_from_state: null pointer");
+    PSVO_REQUIRE(((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
+                 "adam_flags_from_state: moments must be 16-B aligned");
+    hipLaunchKernelGGL(psvo::k_adam_flags_from_state, dim3(psvo::div_up(n_rows, 256)), dim3(256), 0,
+                       psvo::as_stream(stream), n_rows, exp_avg, exp_avg_sq, flags);
+    return psvo::check_launch("adam_flags_from_state");
+}
 
 // One launch over n_tensors tensors (chunks of kAdamMaxTensors); per-tensor
 // learning rate, optional per-tensor step number (`steps`, else `step` for
@@ -80,7 +134,7 @@ using namespace psvo;
 int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads,
                       float *const *exp_avg, float *const *exp_avg_sq, const int64_t *numel, const double *lr,
                       double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                      const int *zero_grad, const int64_t *steps) {
+                      const int *zero_grad, const int64_t *steps, const uint8_t *const *row_flags) {
     PSVO_REQUIRE(n_tensors >= 0 && (steps || step >= 1), "adam_step: bad arguments (n_tensors=%d step=%lld)",
                  n_tensors, (long long)step);
     int t = 0;
@@ -105,6 +159,7 @@ int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const
             tab.lr_bc1[k] = (float)(lr[t] / bc1);
             tab.bc2_sqrt[k] = (float)std::sqrt(bc2);
             tab.zero_grad[k] = zero_grad ? zero_grad[t] : 0;
+            tab.rows[k] = row_flags ? row_flags[t] : nullptr;
             tab.block_begin[k] = blocks;
             blocks += (int)div_up(numel[t], kAdamSlice);
         }

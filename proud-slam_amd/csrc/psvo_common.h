@@ -21,7 +21,8 @@ int check_launch(const char *what);
 // step numbers (steps: else `step` for all), optional gradient zeroing
 int adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads, float *const *exp_avg,
                 float *const *exp_avg_sq, const int64_t *numel, const double *lr, double beta1, double beta2,
-                double eps, double weight_decay, int64_t step, const int *zero_grad, const int64_t *steps = nullptr);
+                double eps, double weight_decay, int64_t step, const int *zero_grad, const int64_t *steps = nullptr,
+                const uint8_t *const *row_flags = nullptr);
 
 constexpr int kWave = 64;
 constexpr int kMaxHits = 50;        // voxel_helpers.py:561 (n_max hard-coded)

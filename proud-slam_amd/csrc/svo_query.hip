@@ -1022,19 +1022,21 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
                                 const int *__restrict__ offsets, int *__restrict__ leaf, float *__restrict__ t,
                                 int *__restrict__ ray_of_sample, float *__restrict__ z_vals,
                                 uint8_t *__restrict__ mask) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= r_hit * s_max) return;
-    const int64_t r = e / s_max;
-    const int s = (int)(e - r * s_max);
-    const int v = s_idx[r * cap + s];
-    const float z = s_depth[r * cap + s];
-    z_vals[e] = z;
-    mask[e] = v != -1;
-    if (v != -1) {
-        const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
-        leaf[o] = v;
-        t[o] = z;
-        ray_of_sample[o] = (int)r;
+    // grid rows stride over the hit rays (no 64-bit division per element)
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= s_max) return;
+    for (int64_t r = blockIdx.y; r < r_hit; r += gridDim.y) {
+        const int64_t e = r * s_max + s;
+        const int v = s_idx[r * cap + s];
+        const float z = s_depth[r * cap + s];
+        z_vals[e] = z;
+        mask[e] = v != -1;
+        if (v != -1) {
+            const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
+            leaf[o] = v;
+            t[o] = z;
+            ray_of_sample[o] = (int)r;
+        }
     }
 }
 
@@ -1299,7 +1301,9 @@ extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int ma
     const int64_t total = r_hit * (int64_t)s_max;
     if (total == 0) return PSVO_OK;
     (void)ray_ns;
-    hipLaunchKernelGGL(k_sample_points, dim3(div_up(total, 256)), dim3(256), 0, as_stream(stream), r_hit, s_max,
-                       max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask);
+    const int bx = s_max <= 64 ? 64 : s_max <= 128 ? 128 : 256;
+    const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
+    hipLaunchKernelGGL(k_sample_points, dim3(div_up(s_max, bx), gy), dim3(bx), 0, as_stream(stream), r_hit,
+                       s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask);
     return check_launch("sample_points");
 }

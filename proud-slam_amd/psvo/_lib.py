@@ -47,6 +47,8 @@ _SIGNATURES = {
     "psvo_rows_workspace_ints": (_i64, [_i64]),
     "psvo_sample_pixels_workspace_ints": (_i64, [_i32, _i64]),
     "psvo_pack_tree_workspace_ints": (_i64, [_i64]),
+    "psvo_adam_mark_rows": (_i32, [_vp, _i64, _vp, _vp, _vp]),
+    "psvo_adam_flags_from_state": (_i32, [_vp, _i64, _vp, _vp, _vp]),
     "psvo_pack_tree": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "psvo_ray_intersect_sorted_packed": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _f32] + [_vp] * 6),
     "psvo_sample_pixels": (_i32, [_vp, _i32, _i64, _i64, _vp, _i32, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),

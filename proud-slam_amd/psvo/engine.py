@@ -28,7 +28,7 @@ class MapDesc(ctypes.Structure):
                 ("voxel_size", _f32), ("step_size", _f32), ("max_distance", _f32), ("truncation", _f32),
                 ("max_depth", _f32), ("w_rgb", _f32), ("w_depth", _f32), ("w_fs", _f32), ("w_sdf", _f32),
                 ("lr_emb", _f64), ("lr_dec", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
-                ("grad_flat", _vp), ("packed", _vp)]
+                ("grad_flat", _vp), ("packed", _vp), ("emb_row_flags", _vp)]
 
 
 class MapFrames(ctypes.Structure):
@@ -90,6 +90,12 @@ class MappingEngine:
         self.desc = d
         self.packed = None
         self.refresh_tree()
+        # sparse-exact Adam for the embedding table (include/psvo.h emb_row_flags;
+        # PSVO_SPARSE_ADAM=0: dense)
+        self.row_flags = None
+        if os.environ.get("PSVO_SPARSE_ADAM", "1") != "0":
+            self.row_flags = torch.zeros(self.emb.shape[0], dtype=torch.uint8, device=self.emb.device)
+            d.emb_row_flags = self.row_flags.data_ptr()
         self._queued = []   # (caller's rays_o, rays_d, seed, converted ro, rd) per queued query
         self.exchange = None
         self.grad_exchange = None
@@ -123,6 +129,9 @@ class MappingEngine:
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.shape == ref.shape):
                 raise RuntimeError("MappingEngine.bind_adam: moments must match the parameters (contiguous f32 CUDA)")
         self.emb_m, self.emb_v, self.dec_m, self.dec_v = emb_m, emb_v, list(dec_m), list(dec_v)
+        if self.row_flags is not None:  # rows whose carried-over moments are non-zero are live
+            L.call("psvo_adam_flags_from_state", L.stream_of(emb_m.device), emb_m.shape[0], emb_m, emb_v,
+                   self.row_flags)
         d = self.desc
         d.emb_m, d.emb_v = emb_m.data_ptr(), emb_v.data_ptr()
         for i in range(10):
