@@ -392,6 +392,7 @@ struct Render {
     int *rank_ray, *ray_ns, *offsets, *leaf, *ray_of;
     float *tt, *z_vals, *feat, *images, *sdf_s, *rgb_s, *act, *sdf, *weights, *color, *depth;
     uint64_t *masks;
+    bool z_recorded = false;  // e->z_ready marks the sample compaction on st (aux has not waited yet)
 };
 
 #define Q_BUF(T, name, slot, bytes)                                              \
@@ -560,6 +561,19 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     const float *s_depth = static_cast<const float *>(qset.a.p[kSDepth]);
     const int *ray_ns = static_cast<const int *>(qset.a.p[kRayNs]);
     const int *offsets = static_cast<const int *>(qset.a.p[kOffsets]);
+    float *const *W = d->dec;
+    const int width = d->width;
+    ENG_BUF(float, images, kImages, psvo_mlp_image_floats_w(width) * sizeof(float));
+    // the decoder's operand images depend only on the weights (the previous
+    // step's Adam is ordered before them on st): built on aux while the host
+    // waits for the query's read-back (psvo_map_step)
+    const bool early_images = fused_loss && engine_overlap(e);
+    if (early_images) {
+        ENG_CALL(fork_join(st, e->aux, e->prep_fork));
+        ENG_CALL(mlp_images(e->aux, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+        if (hipEventRecord(e->prep_done, e->aux) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+    }
     ENG_CALL(spin_wait(qset.done, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
@@ -580,16 +594,6 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     const size_t RS = (size_t)r_hit * s_max;
-    float *const *W = d->dec;
-    const int width = d->width;
-    ENG_BUF(float, images, kImages, psvo_mlp_image_floats_w(width) * sizeof(float));
-    // the decoder's operand images depend only on the weights: built on aux
-    // beside the sampler compaction and the interpolation (psvo_map_step)
-    const bool early_images = fused_loss && engine_overlap(e);
-    if (early_images) {
-        ENG_CALL(fork_join(st, e->aux, e->prep_fork));
-        ENG_CALL(mlp_images(e->aux, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
-    }
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
     ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
@@ -599,8 +603,13 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
                                 z_vals, smask));
     mark(e, st, PSVO_TIME_POINTS, 1);
-    // the loss normalisers can start now (psvo_map_step, on aux)
-    if (fused_loss && engine_overlap(e)) ENG_CALL(fork_join(st, e->aux, e->z_ready));
+    // the loss normalisers can start now (psvo_map_step, on aux; the host
+    // issues aux's wait after the decoder launch)
+    if (fused_loss && engine_overlap(e)) {
+        if (hipEventRecord(e->z_ready, st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+        o.z_recorded = true;
+    }
     // ---- forward: interpolation, decoder, compositing
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
     mark(e, st, PSVO_TIME_INTERP_FWD, 0);
@@ -617,7 +626,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
     mark(e, st, PSVO_TIME_MLP_FWD, 0);
     if (early_images) {
-        ENG_CALL(fork_join(e->aux, st, e->prep_done));
+        if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
         ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                                   images, sdf_s, rgb_s, act, masks));
     } else {
@@ -778,6 +788,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (overlap) ENG_CALL(ensure_aux(e));
     hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
+    if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     const int64_t M = q.m;
     const int64_t r_hit = q.r_hit;
     const int s_max = q.s_max;

@@ -5,8 +5,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in ${VALS:-0 1}; do
-  env $VAR=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$VAR=$v', round(d['ms_per_step'],4), [round(o['ms_per_step'],4) for o in d['other_path']], {k: round(v*1e3,1) for k, v in d['roofline']['parts_ms'].items()}, round(d['roofline']['frac'],3))"
+  t=${v//\//_}
+  env $VAR=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$t.json 2> gpurun_out/ab_$t.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/ab_$t.json'));print('$VAR=$v', round(d['ms_per_step'],4), [round(o['ms_per_step'],4) for o in d['other_path']], {k: round(v*1e3,1) for k, v in d['roofline']['parts_ms'].items()}, round(d['roofline']['frac'],3))"
 done
 if [ "${PROF:-0}" = "1" ]; then
   export $VAR=${PROF_VAL:-1}
