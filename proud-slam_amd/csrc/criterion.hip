@@ -102,28 +102,46 @@ __global__ __launch_bounds__(256) void k_crit_rays(int64_t r_hit, int s_max, int
     }
 }
 
-// fixed-order reduction of part[r_hit][8] → sums[8] (double)
-__global__ __launch_bounds__(256) void k_crit_reduce(int64_t r_hit, const float *__restrict__ part,
-                                                     double *__restrict__ sums) {
-    __shared__ double red[kNSums][256];
-    double acc[kNSums];
+// fixed-order reduction of part[r_hit][8] → sums[8] (double): 256 virtual
+// threads t each sum rows t, t+256, ..., then the pairwise tree
+// x[t] += x[t + w], w = 128 .. 1.  One wave plays all 256 (lane l holds
+// t = l + 64j, j = 0..3), so the two cross-wave levels are register adds and
+// the in-wave levels shuffles — the same pairs as an LDS tree, no LDS: the
+// engine runs this beside the persistent decoder kernels, whose LDS leaves
+// no room for a workgroup that needs any until they end.
+__global__ __launch_bounds__(64) void k_crit_reduce(int64_t r_hit, const float *__restrict__ part,
+                                                    double *__restrict__ sums) {
+    const int l = threadIdx.x;
+    double acc[4][kNSums];
 #pragma unroll
-    for (int k = 0; k < kNSums; ++k) acc[k] = 0.0;
-    for (int64_t r = threadIdx.x; r < r_hit; r += 256) {
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int k = 0; k < kNSums; ++k) acc[k] += (double)part[r * kNSums + k];
-    }
+        for (int k = 0; k < kNSums; ++k) acc[j][k] = 0.0;
+    static_assert(kNSums == 8, "two float4 per row");
+    for (int64_t r0 = 0; r0 < r_hit; r0 += 256) {
 #pragma unroll
-    for (int k = 0; k < kNSums; ++k) red[k][threadIdx.x] = acc[k];
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-#pragma unroll
-            for (int k = 0; k < kNSums; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        for (int j = 0; j < 4; ++j) {
+            const int64_t r = r0 + l + 64 * j;
+            if (r < r_hit) {
+                const float4 a = reinterpret_cast<const float4 *>(part)[r * 2];
+                const float4 b = reinterpret_cast<const float4 *>(part)[r * 2 + 1];
+                acc[j][0] += (double)a.x; acc[j][1] += (double)a.y; acc[j][2] += (double)a.z; acc[j][3] += (double)a.w;
+                acc[j][4] += (double)b.x; acc[j][5] += (double)b.y; acc[j][6] += (double)b.z; acc[j][7] += (double)b.w;
+            }
         }
-        __syncthreads();
     }
-    if (threadIdx.x < kNSums) sums[threadIdx.x] = red[threadIdx.x][0];
+#pragma unroll
+    for (int k = 0; k < kNSums; ++k) {
+        double v = acc[0][k] + acc[2][k];       // w = 128: t = l adds t + 128
+        const double v1 = acc[1][k] + acc[3][k];  //          t = l + 64 adds t + 128
+        v += v1;                                  // w = 64
+#pragma unroll
+        for (int w = 32; w > 0; w >>= 1) {  // lanes < w read lane + w (still holding its level value)
+            const double o = __shfl_down(v, w, 64);
+            if (l < w) v += o;
+        }
+        if (l == 0) sums[k] = v;
+    }
 }
 
 __global__ void k_crit_finalize(const double *__restrict__ sums, double n_hit, double n_cols, float rgb_w,
@@ -325,7 +343,8 @@ extern "C" int psvo_criterion_sums_ex(void *stream, int64_t r_hit, int s_max, in
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
                        max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, dtmp, dthr, workspace);
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_sums");
 }
 
@@ -346,7 +365,8 @@ extern "C" int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
                        rank_ray, gt_depth, z_vals, workspace);
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
                        fs_w, sdf_w, truncation, flags, coef);
     return check_launch("criterion_coef");
@@ -360,7 +380,8 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
     if (r_hit > 0)
         hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
                            max_depth, rank_ray, gt_depth, z_vals, workspace);
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, st, r_hit, workspace, sums);
+    PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");
 }
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
@@ -373,7 +394,8 @@ int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, 
 
 extern "C" int psvo_criterion_reduce(void *stream, int64_t r_hit, const float *workspace, double *sums) {
     PSVO_REQUIRE(r_hit > 0 && workspace && sums, "criterion_reduce: bad arguments");
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(256), 0, as_stream(stream), r_hit, workspace, sums);
+    PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
+    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, as_stream(stream), r_hit, workspace, sums);
     return check_launch("criterion_reduce");
 }
 

@@ -43,7 +43,10 @@ struct Arena {
 // updates), so the step that consumes it finds its sizes already on the host.
 struct QuerySet {
     Arena a;                      // slots kStats..kOffsets
-    int *host_stats = nullptr;    // pinned, PSVO_STAT_WORDS
+    int *host_stats = nullptr;    // coherent pinned, PSVO_STAT_WORDS + the landing flag
+    int seq = 0;                  // the flag value the current statistics carry
+    hipStream_t qstream = nullptr;  // the stream the query was queued on
+    const int *stats_zeroed = nullptr;  // the device statistics buffer a completed read-back left zeroed
     hipEvent_t done = nullptr;    // statistics landed (after the sampler)
     hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
     bool freed_recorded = false;
@@ -104,8 +107,12 @@ struct psvo_engine {
     // (and the loss normalisers beside the decoder forward, the loss value
     // beside the decoder backward)
     hipStream_t aux = nullptr;
+    // single GPU: the loss value (one-wave reduction, slow beside the
+    // persistent decoder kernels) on its own stream, so it delays neither the
+    // embedding backward on aux nor anything on the caller's stream
+    hipStream_t lossq = nullptr;
     hipEvent_t dfeat_ready = nullptr, emb_done = nullptr, z_ready = nullptr, coef_ready = nullptr,
-               grads_ready = nullptr, prep_fork = nullptr, prep_done = nullptr;
+               grads_ready = nullptr, prep_fork = nullptr, prep_done = nullptr, loss_done = nullptr;
     EngineTimer tm;
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
@@ -162,23 +169,35 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
     if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
 }
 
-// The host spins on an event (instead of a blocking sync) so it resumes
-// launching within ~1 µs of the read-back completing.
-int spin_wait(hipEvent_t ev, const char *who) {
-    hipError_t q;
-    while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
+// The host spins on the landing flag the device writes after the statistics
+// (k_stats_to_host: system-scope release) — it sees them as soon as they
+// land, without the event's completion-signal round trip; the event, recorded
+// after that kernel, is still queried now and then so a failed stream ends
+// the wait with its error.
+int spin_wait(const int *host_stats, int seq, hipEvent_t ev, const char *who) {
+    const int *flag = host_stats + PSVO_STAT_WORDS;
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
+        if ((it & 1023) == 0) {
+            const hipError_t q = hipEventQuery(ev);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
+            return set_error(PSVO_E_LAUNCH, "%s: stats read-back: event complete, flag %d != %d", who,
+                             __atomic_load_n(flag, __ATOMIC_ACQUIRE), seq);
+        }
     }
-    if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
-    return PSVO_OK;
 }
 
 int query_set_init(QuerySet &s) {
     if (s.host_stats) return PSVO_OK;
-    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_stats), PSVO_STAT_WORDS * sizeof(int), hipHostMallocDefault) !=
+    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_stats), (PSVO_STAT_WORDS + 1) * sizeof(int),
+                      hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
         hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s.freed, hipEventDisableTiming) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: query set allocation failed");
+    memset(s.host_stats, 0, (PSVO_STAT_WORDS + 1) * sizeof(int));  // flag 0: no statistics yet (seq starts at 1)
     return PSVO_OK;
 }
 
@@ -212,7 +231,7 @@ extern "C" int psvo_map_discard(psvo_engine *e) {
         QuerySet &q = e->qs[e->q_head];
         // the stream the query was queued on: psvo_map_query's side stream,
         // or aux for a psvo_map_step_frames look-ahead
-        hipStream_t qs = q.dirs ? e->aux : e->side;
+        hipStream_t qs = q.qstream;
         if (qs && hipEventRecord(q.freed, qs) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_discard: event record failed");
         q.freed_recorded = qs != nullptr;
@@ -285,6 +304,8 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     for (auto &q : e->qs) query_set_free(q);
     if (e->side) (void)hipStreamDestroy(e->side);
     if (e->aux) (void)hipStreamDestroy(e->aux);
+    if (e->lossq) (void)hipStreamDestroy(e->lossq);
+    if (e->loss_done) (void)hipEventDestroy(e->loss_done);
     if (e->dfeat_ready) (void)hipEventDestroy(e->dfeat_ready);
     if (e->emb_done) (void)hipEventDestroy(e->emb_done);
     if (e->z_ready) (void)hipEventDestroy(e->z_ready);
@@ -412,8 +433,9 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     int rc = PSVO_OK;
     void *stream = st;
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
-    if (hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
+    if (q.stats_zeroed != stats && hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
+    q.stats_zeroed = nullptr;  // until this query's read-back is queued
     Q_BUF(int, hit_idx, kHitIdx, R * kMaxHits * sizeof(int));
     Q_BUF(float, hit_t0, kHitT0, R * kMaxHits * sizeof(float));
     Q_BUF(float, hit_t1, kHitT1, R * kMaxHits * sizeof(float));
@@ -457,9 +479,12 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                                   noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
-    if (hipMemcpyAsync(q.host_stats, stats, PSVO_STAT_WORDS * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipEventRecord(q.done, st) != hipSuccess)
+    q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
+    ENG_CALL(psvo::stats_to_host(st, stats, q.host_stats, PSVO_STAT_WORDS, q.seq));
+    q.stats_zeroed = stats;
+    if (hipEventRecord(q.done, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: stats read-back failed", who);
+    q.qstream = st;
     q.R = R;
     q.ro = rays_o;
     q.rd = rays_d;
@@ -479,7 +504,7 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
         if (q.R != R || q.ro != rays_o || q.rd != rays_d || q.seed != seed)
             return set_error(PSVO_E_INVALID, "%s: rays / seed differ from the batch queued by psvo_map_query", who);
         // the step's kernels read the query's outputs: order the streams
-        if (hipStreamWaitEvent(st, q.done, 0) != hipSuccess)
+        if (q.qstream != st && hipStreamWaitEvent(st, q.done, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
         *out = &q;
         return PSVO_OK;
@@ -532,8 +557,9 @@ bool engine_overlap(psvo_engine *e) {
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done};
-    if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess)
+                         &e->prep_fork, &e->prep_done, &e->loss_done};
+    if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
     for (hipEvent_t *ev : evs)
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
@@ -574,7 +600,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         if (hipEventRecord(e->prep_done, e->aux) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
     }
-    ENG_CALL(spin_wait(qset.done, who));
+    ENG_CALL(spin_wait(qset.host_stats, qset.seq, qset.done, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
     // data-parallel: this rank's hit rays, padded to the union's S_max
@@ -819,7 +845,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     // sparse-exact Adam (single GPU): the rows this step can touch, beside the decoder
     const bool sparse_rows = d->emb_row_flags && !dist && !(flags & PSVO_STEP_NO_ADAM);
-    if (sparse_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
     if (dist) {
         ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
                                   q.z_vals, crit_ws, sums_c));
@@ -831,20 +856,28 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                                      d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
     }
     ENG_CALL(fork_join(ax, st, e->coef_ready));
+    // after the normalisers: the fused loss pass waits for them, Adam for the marks
+    if (sparse_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
     if (!empty)
         ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                      q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
                                      g_sdf_s, g_rgb_s));
-    // the loss value (not on the gradient path): aux, beside the decoder backward
-    ENG_CALL(fork_join(st, ax, e->grads_ready));
+    // the loss value (not on the gradient path), beside the decoder backward:
+    // data parallel on aux (its collective), single GPU on its own stream,
+    // joined into st before the optimiser step (loss_out / crit_ws ordered)
+    hipStream_t lq = (overlap && !dist) ? e->lossq : ax;
+    ENG_CALL(fork_join(st, lq, e->grads_ready));
     if (!empty) {
-        ENG_CALL(psvo_criterion_reduce(ax, r_hit, crit_ws, sums));
-    } else if (hipMemsetAsync(sums, 0, 8 * sizeof(double), ax) != hipSuccess) {
+        ENG_CALL(psvo_criterion_reduce(lq, r_hit, crit_ws, sums));
+    } else if (hipMemsetAsync(sums, 0, 8 * sizeof(double), lq) != hipSuccess) {
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     }
-    if (dist) ENG_CALL(x.call(PSVO_XCH_SUM_F64, 8, 8, 8, ax, "loss sums"));
-    ENG_CALL(psvo_criterion_finalize(ax, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
+    if (dist) ENG_CALL(x.call(PSVO_XCH_SUM_F64, 8, 8, 8, lq, "loss sums"));
+    ENG_CALL(psvo_criterion_finalize(lq, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
                                      d->truncation, crit_flags, loss_out));
+    if (lq != ax && hipEventRecord(e->loss_done, lq) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
+    const bool join_loss = lq != ax;
     const int n_split = 256;
     ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats_w(M, d->width, n_split) * sizeof(float));
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
@@ -898,6 +931,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                                      grad_od + R * 3, ib_ws));
     mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
+        return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
+    if (join_loss && hipStreamWaitEvent(st, e->loss_done, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
     ENG_CALL(guard.release());

@@ -38,6 +38,12 @@ struct PackRec {  // 32 B, 16-B aligned
     int4 i;       // reference node id, first child record (-1: none), child mask, 0
 };
 
+// the query's statistics words → coherent pinned host memory by one device
+// thread (zeroing them on the device), then host[words] = seq with a
+// system-scope release (the engine's host thread polls that word instead of
+// waiting for an event; svo_query.hip)
+int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq);
+
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,

@@ -495,6 +495,16 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     }
 }
 
+__global__ void k_stats_to_host(int *__restrict__ stats, int *host, int words, int seq) {
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < words; ++i) {
+        host[i] = stats[i];
+        stats[i] = 0;  // ready for the query set's next use (no memset launch)
+    }
+    __threadfence_system();
+    __hip_atomic_store(host + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // P (max valid hits), R_hit and max ceil(Σ/step) over the rays — one block.
 __device__ void ray_stats_body(int64_t n, const int *__restrict__ ray_nv, const float *__restrict__ ray_dsum,
                                float step_size, int *__restrict__ stats) {
@@ -1186,6 +1196,11 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
 }
 
 namespace psvo {
+int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq) {
+    hipLaunchKernelGGL(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
+    return check_launch("stats_to_host");
+}
+
 // psvo_ray_intersect_sorted + psvo_hit_rank with the two single-block
 // reductions fused into one launch (engine.cpp)
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,

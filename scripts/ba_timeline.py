@@ -1,0 +1,19 @@
+"""Kernel timeline of one bundle_adjust_frames iteration from a rocprofv3
+kernel trace: start / end / duration (us, relative to the iteration's
+k_pose_rays_frames) and queue of every kernel.  Usage: ba_timeline.py
+run_kernel_trace.csv [iteration index]"""
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+idx = [i for i, r in enumerate(rows) if "k_pose_rays_frames" in r["Kernel_Name"]]
+a, b = idx[k], idx[k + 1]
+t0 = int(rows[a]["Start_Timestamp"])
+for r in rows[a:b + 1]:
+    s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
+    m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
+    name = m.group(1) if m else r["Kernel_Name"][:40]
+    print(f"{s / 1e3:8.1f} {e / 1e3:8.1f} {(e - s) / 1e3:7.1f}  q{r['Queue_Id']}  {name}")
