@@ -779,7 +779,7 @@ int pose_adam(hipStream_t st, const psvo_map_desc *d, const PoseAdam &pa) {
 // buffers — this step's last reader of them, the embedding backward, ran
 // earlier on `ps` — then intersection + sampling into the free query set.
 int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const psvo_map_frames *fr,
-                     int64_t R) {
+                     int64_t R, const Render &cur, const float *grad_od) {
     int rc = PSVO_OK;
     PSVO_REQUIRE(e->q_count == 0, "map_step_frames: a query is already queued");
     QuerySet &q = e->qs[e->q_head];
@@ -787,7 +787,17 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
         return set_error(PSVO_E_LAUNCH, "map_step_frames: stream ordering failed");
     ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
     ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
-    ENG_CALL(psvo_pose_rays_frames(st, R, fr->rays_per_frame, fr->poses, fr->next_dirs_cam, rays_o, rays_d));
+    float *pg = fr->pose_grad;
+    if (!pg) {
+        ENG_BUF(float, gbuf, kPoseGrad, (size_t)fr->n_frames * 8 * sizeof(float));
+        pg = gbuf;
+    }
+    // this step's pose gradient, each optimised pose's Adam step and the next
+    // rays from the updated poses: one launch (frames_update + pose_adam +
+    // psvo_pose_rays_frames, the same arithmetic)
+    ENG_CALL(psvo::pose_step_frames(st, fr->n_frames, fr->rays_per_frame, cur.r_hit, cur.rank_ray, fr->dirs_cam,
+                                    grad_od, grad_od + R * 3, fr->poses, fr->pose_m, fr->pose_v, fr->pose_step,
+                                    fr->lr_pose, d->beta1, d->beta2, d->eps, pg, fr->next_dirs_cam, rays_o, rays_d));
     ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)"));
     q.dirs = fr->next_dirs_cam;
     q.pending = true;
@@ -942,12 +952,10 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // next iteration's rays + query there too — beside this step's weight
     // gradients and the map's Adam
     const bool ahead = fr && fr->next_dirs_cam;
-    hipStream_t ps = ahead ? eb : st;
-    if (fr) ENG_CALL(frames_update(e, ps, d, fr, q, grad_od, R, &pa));
     if (ahead) {
-        ENG_CALL(pose_adam(ps, d, pa));
-        pa.n = 0;
-        ENG_CALL(frames_lookahead(e, ps, d, fr, R));
+        ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od));
+    } else if (fr) {
+        ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R, &pa));
     }
     // ---- optimiser steps, the poses' with the map's (the map's are skipped
     // when the caller all-reduces the gradients first)

@@ -57,13 +57,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamTable tab, float beta1, float 
     const uint8_t *__restrict__ rf = tab.rows[ti];
     for (int64_t i = base + threadIdx.x; i < base + kAdamSlice && i < n; i += 256) {
         if (rf && !rf[i >> 4]) continue;  // a row never touched: g = m = v = 0, the step leaves it as it is
-        float gi = g[i];
-        float pi = p[i];
-        if (wd != 0.0f) gi = gi + wd * pi;
-        const float mi = beta1 * m[i] + omb1 * gi;
-        const float vi = beta2 * v[i] + omb2 * gi * gi;
-        const float denom = sqrtf(vi) / bc2_sqrt + eps;
-        p[i] = pi - lr_bc1 * mi / denom;
+        float pi = p[i], mi = m[i], vi = v[i];
+        adam_elem(pi, g[i], mi, vi, beta1, beta2, omb1, omb2, eps, wd, lr_bc1, bc2_sqrt);
+        p[i] = pi;
         m[i] = mi;
         v[i] = vi;
         if (zg) g[i] = 0.0f;

@@ -15,6 +15,8 @@
 // rotation() — one block, a fixed-order reduction.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "psvo_common.h"
 
 namespace psvo {
@@ -137,6 +139,75 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_grad_frames(int64_t r_hit
     pose_chain(poses + blockIdx.x * 6, tot, grads + blockIdx.x * 8);
 }
 
+struct PoseStepArgs {
+    int64_t step[kXchMaxFrames];
+    float lr_bc1[kXchMaxFrames], bc2_sqrt[kXchMaxFrames];
+};
+
+// k_pose_grad_frames + k_adam on the frame's pose + k_pose_rays_frames for
+// the frame's next rays, one block per frame (a frame's rays, gradient and
+// pose are its own: no grid-wide dependency)
+__global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
+    int64_t r_hit, const int *__restrict__ rank_ray, int64_t rpf, const float *__restrict__ dirs,
+    const float *__restrict__ g_o, const float *__restrict__ g_d, float *__restrict__ poses,
+    float *__restrict__ pose_m, float *__restrict__ pose_v, PoseStepArgs a, float beta1, float beta2, float omb1,
+    float omb2, float eps, float *__restrict__ grads, const float *__restrict__ next_dirs,
+    float *__restrict__ rays_o, float *__restrict__ rays_d) {
+    __shared__ float part[kGradThreads / 64][12];
+    __shared__ float pose_s[6];
+    const int f = blockIdx.x;
+    const int64_t lo = f * rpf, hi = lo + rpf;
+    float acc[12] = {};
+    for (int64_t r = threadIdx.x; r < r_hit; r += kGradThreads) {
+        const int64_t row = rank_ray[r];
+        if (row < lo || row >= hi) continue;
+        float dir[3], gd[3];
+        for (int j = 0; j < 3; ++j) {
+            acc[j] += g_o[row * 3 + j];
+            gd[j] = g_d[row * 3 + j];
+            dir[j] = dirs[row * 3 + j];
+        }
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) acc[3 + j * 3 + k] += gd[j] * dir[k];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = 0; i < 12; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+        if (lane == 0) part[wv][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot[12] = {};
+        for (int w = 0; w < kGradThreads / 64; ++w)
+            for (int i = 0; i < 12; ++i) tot[i] += part[w][i];
+        float *pose = poses + f * 6;
+        float *g = grads + f * 8;
+        pose_chain(pose, tot, g);
+        if (a.step[f] >= 1) {  // stamp 0 / update_pose False: fixed (render_helpers.py:594-596)
+            for (int i = 0; i < 6; ++i) {
+                float pi = pose[i], mi = pose_m[f * 6 + i], vi = pose_v[f * 6 + i];
+                adam_elem(pi, g[i], mi, vi, beta1, beta2, omb1, omb2, eps, 0.0f, a.lr_bc1[f], a.bc2_sqrt[f]);
+                pose[i] = pi;
+                pose_m[f * 6 + i] = mi;
+                pose_v[f * 6 + i] = vi;
+            }
+        }
+        for (int i = 0; i < 6; ++i) pose_s[i] = pose[i];
+    }
+    __syncthreads();
+    Rot q;
+    rotation(pose_s, q);
+    for (int64_t r = lo + threadIdx.x; r < hi; r += kGradThreads) {
+        const float d0 = next_dirs[r * 3 + 0], d1 = next_dirs[r * 3 + 1], d2 = next_dirs[r * 3 + 2];
+        for (int j = 0; j < 3; ++j) {
+            rays_d[r * 3 + j] = d0 * q.R[j][0] + d1 * q.R[j][1] + d2 * q.R[j][2];
+            rays_o[r * 3 + j] = pose_s[j];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kGradThreads) void k_pose_grad(int64_t r_hit, const int *__restrict__ rank_ray,
                                                             const float *__restrict__ dirs,
                                                             const float *__restrict__ g_o,
@@ -233,6 +304,29 @@ extern "C" int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_pe
 }
 
 namespace psvo {
+int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64_t r_hit, const int *rank_ray,
+                     const float *dirs, const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
+                     const int64_t *steps, double lr, double beta1, double beta2, double eps, float *grads,
+                     const float *next_dirs, float *rays_o, float *rays_d) {
+    PSVO_REQUIRE(n_frames > 0 && n_frames <= kXchMaxFrames && rays_per_frame > 0 && r_hit >= 0,
+                 "pose_step_frames: bad sizes");
+    PSVO_REQUIRE(rank_ray && dirs && g_o && g_d && poses && grads && next_dirs && rays_o && rays_d && steps,
+                 "pose_step_frames: null pointer");
+    PoseStepArgs a{};
+    for (int f = 0; f < n_frames; ++f) {
+        a.step[f] = steps[f];
+        if (steps[f] < 1) continue;
+        PSVO_REQUIRE(pose_m && pose_v, "pose_step_frames: pose Adam needs m / v");
+        const double bc1 = 1.0 - std::pow(beta1, (double)steps[f]);  // as adam_launch forms them
+        const double bc2 = 1.0 - std::pow(beta2, (double)steps[f]);
+        a.lr_bc1[f] = (float)(lr / bc1);
+        a.bc2_sqrt[f] = (float)std::sqrt(bc2);
+    }
+    hipLaunchKernelGGL(k_pose_step_frames, dim3(n_frames), dim3(kGradThreads), 0, st, r_hit, rank_ray, rays_per_frame,
+                       dirs, g_o, g_d, poses, pose_m, pose_v, a, (float)beta1, (float)beta2, (float)(1.0 - beta1),
+                       (float)(1.0 - beta2), (float)eps, grads, next_dirs, rays_o, rays_d);
+    return check_launch("pose_step_frames");
+}
 }  // namespace psvo
 
 extern "C" int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, const float *dirs, const float *g_o,

@@ -44,6 +44,29 @@ struct PackRec {  // 32 B, 16-B aligned
 // waiting for an event; svo_query.hip)
 int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq);
 
+// one element of the Adam step (k_adam; optim.hip's formulation), shared so
+// the fused pose step (pose.hip) computes the same bits
+__device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, float beta1, float beta2, float omb1,
+                                          float omb2, float eps, float wd, float lr_bc1, float bc2_sqrt) {
+    if (wd != 0.0f) g = g + wd * p;
+    const float mi = beta1 * m + omb1 * g;
+    const float vi = beta2 * v + omb2 * g * g;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p = p - lr_bc1 * mi / denom;
+    m = mi;
+    v = vi;
+}
+
+// the bundle-adjust look-ahead's pose work in one launch, one block per
+// keyframe (pose.hip): the frame's pose gradient (k_pose_grad_frames), its
+// Adam step when steps[f] >= 1 (k_adam's arithmetic, lr / bc1 and sqrt(bc2)
+// formed on the host as adam_launch does), then the frame's next rays
+// (k_pose_rays_frames) from the updated pose
+int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64_t r_hit, const int *rank_ray,
+                     const float *dirs, const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
+                     const int64_t *steps, double lr, double beta1, double beta2, double eps, float *grads,
+                     const float *next_dirs, float *rays_o, float *rays_d);
+
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
