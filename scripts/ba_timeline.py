@@ -1,6 +1,7 @@
 """Kernel timeline of one bundle_adjust_frames iteration from a rocprofv3
 kernel trace: start / end / duration (us, relative to the iteration's
-k_pose_rays_frames) and queue of every kernel.  Usage: ba_timeline.py
+look-ahead pose kernel: k_pose_step_frames, or k_pose_rays_frames before it
+existed) and queue of every kernel.  Usage: ba_timeline.py
 run_kernel_trace.csv [iteration index]"""
 import csv
 import re
@@ -9,7 +10,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-idx = [i for i, r in enumerate(rows) if "k_pose_rays_frames" in r["Kernel_Name"]]
+mark = "k_pose_step_frames" if any("k_pose_step_frames" in r["Kernel_Name"] for r in rows) else "k_pose_rays_frames"
+idx = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
 a, b = idx[k], idx[k + 1]
 t0 = int(rows[a]["Start_Timestamp"])
 for r in rows[a:b + 1]:
