@@ -114,6 +114,11 @@ struct psvo_engine {
     hipEvent_t dfeat_ready = nullptr, emb_done = nullptr, z_ready = nullptr, coef_ready = nullptr,
                grads_ready = nullptr, prep_fork = nullptr, prep_done = nullptr, loss_done = nullptr;
     EngineTimer tm;
+    // the decoder images a look-ahead step built on st after its Adam step,
+    // for the decoder whose W[0] it names; consumed by the next
+    // psvo_map_step_frames, dropped by every other call
+    bool images_next = false;
+    const float *images_w0 = nullptr;
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
 };
@@ -227,6 +232,7 @@ extern "C" int psvo_engine_queued(psvo_engine *e) { return e ? e->q_count : 0; }
 // stream work completed: the next query waits on the stream).
 extern "C" int psvo_map_discard(psvo_engine *e) {
     PSVO_REQUIRE(e, "map_discard: null engine");
+    e->images_next = false;
     while (e->q_count > 0) {
         QuerySet &q = e->qs[e->q_head];
         // the stream the query was queued on: psvo_map_query's side stream,
@@ -399,6 +405,7 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
 
 extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
     PSVO_REQUIRE(e && d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
+    e->images_next = false;  // the weights may change before the next step
     ENG_CALL(map_adam(as_stream(stream), d, d->grad_flat, adam_step));
     e->grads_clean = true;
     return PSVO_OK;
@@ -593,7 +600,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     // the decoder's operand images depend only on the weights (the previous
     // step's Adam is ordered before them on st): built on aux while the host
     // waits for the query's read-back (psvo_map_step)
-    const bool early_images = fused_loss && engine_overlap(e);
+    const bool prebuilt = fused_loss && e->images_next && e->images_w0 == W[0];
+    e->images_next = false;
+    const bool early_images = fused_loss && engine_overlap(e) && !prebuilt;
     if (early_images) {
         ENG_CALL(fork_join(st, e->aux, e->prep_fork));
         ENG_CALL(mlp_images(e->aux, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
@@ -651,8 +660,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     }
     ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
     mark(e, st, PSVO_TIME_MLP_FWD, 0);
-    if (early_images) {
-        if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+    if (early_images || prebuilt) {
+        if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
         ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                                   images, sdf_s, rgb_s, act, masks));
@@ -962,6 +971,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (!(flags & PSVO_STEP_NO_ADAM)) {
         ENG_CALL(map_adam(st, d, grads, adam_step, &pa, sparse_rows));
         e->grads_clean = true;
+        if (ahead) {  // the next iteration's decoder images, on st while it waits for the look-ahead query
+            ENG_BUF(float, images, kImages, psvo_mlp_image_floats_w(d->width) * sizeof(float));
+            ENG_CALL(mlp_images(st, d->width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+            e->images_next = true;
+            e->images_w0 = W[0];
+        }
     } else {
         ENG_CALL(pose_adam(st, d, pa));
     }
@@ -1005,6 +1020,7 @@ extern "C" int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map
 extern "C" int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
                               const float *rays_o, const float *rays_d, uint64_t seed) {
     PSVO_REQUIRE(e && d && rays_o && rays_d && n_rays > 0, "map_query: bad arguments");
+    e->images_next = false;  // the weights may change before the next step
     PSVO_REQUIRE(e->q_count < 2, "map_query: two queries already queued (run psvo_map_step)");
     hipStream_t st = as_stream(stream);
     if (!e->side) {
@@ -1030,6 +1046,7 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
                                float *pose_m, float *pose_v, double lr, uint64_t seed, int64_t adam_step, int flags,
                                float *pose_grad, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && dirs_cam && gt_rgb && gt_depth && pose && loss_out, "track_step: null argument");
+    e->images_next = false;  // the weights may change before the next step
     PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "track_step: bad sizes");
     PSVO_REQUIRE(d->width == 128 || d->width == 256, "track_step: decoder width %d unsupported (fused: 128, 256)",
                  d->width);
