@@ -97,7 +97,7 @@ def test_sharded_global_loss_and_grad_bucket_match_single_process():
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=300)  # gloo teardown can be slow on a loaded host
         assert p.exitcode == 0
     for rank, loss, n_hit, s_cols, grads in res:
         assert (n_hit, s_cols) == (R_HIT, S_MAX)
@@ -163,7 +163,7 @@ def test_sparse_row_sum_protocol(touched, expect):
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=300)  # gloo teardown can be slow on a loaded host
         assert p.exitcode == 0
     want = sum(_sparse_grad(r, n_rows, touched, 7) for r in range(world))
     got = [torch.from_numpy(r[2]) for r in res]
