@@ -104,8 +104,8 @@ struct psvo_engine {
     hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
     // the embedding backward runs on `aux` beside the decoder's weight
     // gradients (k_interp_bwd's 8-KB workgroups fit next to k_mlp_dw2's 152 KB)
-    // (and the loss normalisers beside the decoder forward, the loss value
-    // beside the decoder backward)
+    // (and the loss normalisers beside the decoder forward; data parallel,
+    // also the loss value beside the decoder backward)
     hipStream_t aux = nullptr;
     // single GPU: the loss value (one-wave reduction, slow beside the
     // persistent decoder kernels) on its own stream, so it delays neither the
