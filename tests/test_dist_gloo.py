@@ -74,7 +74,8 @@ def _worker(rank, world, port, q):
         loss, _ = O.criterion_from_sums(sums_g, n_hit, s_cols, O.REPLICA_CRITERIA)
         loss.backward()
         GradBucket(model.parameters(), op="sum").allreduce()
-        q.put((rank, float(loss), n_hit, s_cols, [p.grad.clone() for p in model.parameters()]))
+        # by value (numpy): tensors would travel as shared fds the exiting worker may close first
+        q.put((rank, float(loss.detach()), n_hit, s_cols, [p.grad.numpy().copy() for p in model.parameters()]))
     finally:
         dist.destroy_process_group()
 
@@ -103,10 +104,10 @@ def test_sharded_global_loss_and_grad_bucket_match_single_process():
         assert (n_hit, s_cols) == (R_HIT, S_MAX)
         assert abs(loss - float(loss1)) <= 1e-5 * abs(float(loss1))
         for a, b in zip(grads, grads1):
-            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * float(b.abs().max()))
+            torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-4, atol=1e-6 * float(b.abs().max()))
     # replicas stay identical
     for a, b in zip(res[0][4], res[1][4]):
-        assert torch.equal(a, b)
+        assert torch.equal(torch.from_numpy(a), torch.from_numpy(b))
 
 
 class _TorchRowOps:
