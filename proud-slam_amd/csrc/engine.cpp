@@ -438,7 +438,6 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                   const float *rays_o, const float *rays_d, uint64_t seed, const char *who,
                   const float *noise = nullptr) {
     int rc = PSVO_OK;
-    void *stream = st;
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (q.stats_zeroed != stats && hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
@@ -481,13 +480,14 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         ENG_CALL(dist_pack_smax(st, stats, x.xi32 + x.smax_in_off()));
         ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.smax_in_off(), x.smax_all_off(), 1, st, "S_max"));
         ENG_CALL(dist_smax(st, x.xi32 + x.smax_all_off(), x.world, stats));
-    } else {
-        ENG_CALL(psvo_sample_rays(stream, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size,
-                                  noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets));
     }
-    mark(e, st, PSVO_TIME_SAMPLE, 1);
     q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
-    ENG_CALL(psvo::stats_to_host(st, stats, q.host_stats, PSVO_STAT_WORDS, q.seq));
+    if (!x.on())  // the sampler's scan does the read-back
+        ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
+                                           d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
+                                           q.host_stats, q.seq));
+    mark(e, st, PSVO_TIME_SAMPLE, 1);
+    if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_stats, PSVO_STAT_WORDS, q.seq));
     q.stats_zeroed = stats;
     if (hipEventRecord(q.done, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: stats read-back failed", who);

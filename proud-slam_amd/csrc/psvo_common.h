@@ -43,6 +43,12 @@ struct PackRec {  // 32 B, 16-B aligned
 // system-scope release (the engine's host thread polls that word instead of
 // waiting for an event; svo_query.hip)
 int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq);
+// psvo_sample_rays (single GPU, whole batch) whose scan also does
+// stats_to_host's read-back (svo_query.hip)
+int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                        const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
+                        const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
+                        int *ray_ns, int *offsets, int *host, int seq);
 
 // one element of the Adam step (k_adam; optim.hip's formulation), shared so
 // the fused pose step (pose.hip) computes the same bits

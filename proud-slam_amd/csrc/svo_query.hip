@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
 // offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
-                                                       int *__restrict__ stats, int dist) {
+                                                       int *__restrict__ stats, int dist, int *host, int seq) {
     __shared__ int total;
     __shared__ int smax[16];
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
@@ -1022,6 +1022,14 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         offsets[n] = total;
         stats[PSVO_STAT_S_MAX] = mx;
         stats[PSVO_STAT_M] = total;
+        if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
+            for (int i = 0; i < PSVO_STAT_WORDS; ++i) {
+                host[i] = stats[i];
+                stats[i] = 0;
+            }
+            __threadfence_system();
+            __hip_atomic_store(host + PSVO_STAT_WORDS, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1196,6 +1204,21 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
 }
 
 namespace psvo {
+// the single-GPU sampler with the statistics read-back fused into its scan
+// (one launch less before the host can size the rest of the step)
+int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                        const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
+                        const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
+                        int *ray_ns, int *offsets, int *host, int seq) {
+    PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
+    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
+                       rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
+                       s_dist, ray_ns, nullptr, 0);
+    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0, host,
+                       seq);
+    return check_launch("sample_rays_to_host");
+}
+
 int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq) {
     hipLaunchKernelGGL(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
     return check_launch("stats_to_host");
@@ -1248,7 +1271,8 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch);
-    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1);
+    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
+                       nullptr, 0);
     return check_launch("dist_sample");
 }
 int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
@@ -1282,7 +1306,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0);
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
-                       stats, 0);
+                       stats, 0, nullptr, 0);
     return check_launch("sample_rays");
 }
 
