@@ -486,7 +486,10 @@ void psvo_engine_free(psvo_engine *e);
  * xf64: 16 device doubles (count sums, loss sums).  Returns non-zero on failure.  Exchanged per step:
  * 8 + 1 words per rank (all-gathered), a [200, 50] int32 table of the
  * sampler's slot-0 voxel ids, 16 doubles; then the caller sums grad_flat
- * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam. */
+ * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam.  A non-NULL fn turns
+ * the protocol on for any world, 1 included (the collectives are then
+ * identities: a one-rank communicator drives the whole callback path —
+ * tests/test_gpu_rccl.py); fn NULL turns it off. */
 enum { PSVO_XCH_GATHER_I32 = 1, PSVO_XCH_SUM_I32 = 2, PSVO_XCH_SUM_F64 = 3, PSVO_XCH_QUERY = 0x100 };
 typedef int (*psvo_exchange_fn)(void *user, int op, int64_t in_off, int64_t out_off, int64_t count, void *stream);
 int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global);

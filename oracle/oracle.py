@@ -252,7 +252,7 @@ def interp_features(xyz, leaf_idx, centres, vertex_idx, embeddings, voxel_size):
     c = centres[li]
     e = embeddings[vertex_idx[li].long()]            # [M,8,D]
     p = ((xyz - c) / voxel_size + 0.5).unsqueeze(1)  # [M,1,3]
-    q = _CORNERS.unsqueeze(0)
+    q = _CORNERS.to(p.dtype).unsqueeze(0)
     w = (p * q + (1 - p) * (1 - q)).prod(dim=-1, keepdim=True)
     return (w * e).sum(1)
 
@@ -291,12 +291,57 @@ def decoder_forward(params, x):
     return rgb, sdf[:, 0]
 
 
+def decoder_margins(params, x):
+    """For decoder inputs x [n,16], in fp64: (relu, sdf) relative margins per
+    sample.  relu: the smallest |a| / (Σ_j |W_ij h_j| + |b_i|) over the
+    units of the three ReLU layers (pts_linears 0 / 1, color_out 0); sdf: the
+    same ratio for the sdf output.  fp32 evaluates such a sum to within
+    ~n·2^-24 of its denominator in any summation order, so a margin below
+    ~1e-5 means two fp32 implementations can land on different sides of zero:
+    a ReLU unit switches (the derivative jumps by the unit's whole
+    contribution), or the sdf changes sign and the compositing's first sign
+    change — hence z_min, the truncation window and every weight of the ray
+    (render_helpers.py:531-545) — moves.  Discontinuities of the reference's
+    own fp32 function."""
+    F = torch.nn.functional
+    p = {k: v.detach().double() for k, v in params.items()}
+    x = x.detach().double()
+
+    def layer(h, w, b):
+        a = F.linear(h, w, b)
+        den = F.linear(h.abs(), w.abs(), b.abs())
+        return a, a.abs() / (den + 1e-300)
+
+    a1, m1 = layer(x, p["pts_linears.0.weight"], p["pts_linears.0.bias"])
+    a2, m2 = layer(a1.relu(), p["pts_linears.1.weight"], p["pts_linears.1.bias"])
+    o, mo = layer(a2.relu(), p["sdf_out.weight"], p["sdf_out.bias"])
+    _, m4 = layer(torch.cat([o[:, 1:], x], -1), p["color_out.0.weight"], p["color_out.0.bias"])
+    relu = torch.minimum(torch.minimum(m1.amin(-1), m2.amin(-1)), m4.amin(-1))
+    return relu, mo[:, 0]
+
+
+def relu_margins(params, x):
+    """decoder_margins' ReLU part."""
+    return decoder_margins(params, x)[0]
+
+
 # --------------------------------------------------------------------------
 # render_rays — render_helpers.py:351-556
 # --------------------------------------------------------------------------
 def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_size, truncation, max_distance,
-                noise=None, deterministic=False, generator=None, sum_order="torch"):
-    intersection, hits = ray_intersect_vox(rays_o, rays_d, map_states["voxel_center_xyz"],
+                noise=None, deterministic=False, generator=None, sum_order="torch", dtype=torch.float32,
+                capture=None):
+    """dtype: the arithmetic of everything after the sampler (interpolation,
+    decoder, compositing; the caller's criterion follows).  float32 is the
+    reference; float64 gives the same function evaluated without fp32
+    rounding at the same fp32 rays / depths / parameters (the intersection
+    and the sampler always run in fp32, as the reference's kernels) — the
+    yardstick for how far any fp32 summation order is from the exact value.
+    capture (dict, optional): receives the decoder inputs "feats" [M,16]
+    (ray-major sample order, gradients retained) and the per-ray sample
+    offsets "offsets" [R_hit+1]."""
+    intersection, hits = ray_intersect_vox(rays_o.detach().float(), rays_d.detach().float(),
+                                           map_states["voxel_center_xyz"].float(),
                                            map_states["voxel_structure"], voxel_size, max_distance)
     assert hits.sum() > 0
     ray_mask = hits.view(1, -1)
@@ -307,20 +352,30 @@ def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_siz
     depth = samples["sampled_point_depth"]
     sidx = samples["sampled_point_voxel_idx"].long()
     mask = sidx.ne(-1)
+    if dtype != torch.float32:
+        ro, rd, depth = ro.to(dtype), rd.to(dtype), depth.to(dtype)
+        decoder_params = {k: v.to(dtype) for k, v in decoder_params.items()}
     xyz = ro.unsqueeze(1) + rd.unsqueeze(1) * depth.unsqueeze(2)
-    feats = interp_features(xyz[mask], sidx[mask], map_states["voxel_center_xyz"], map_states["voxel_vertex_idx"],
-                            map_states["voxel_vertex_emb"], voxel_size)
+    feats = interp_features(xyz[mask], sidx[mask], map_states["voxel_center_xyz"].to(dtype),
+                            map_states["voxel_vertex_idx"], map_states["voxel_vertex_emb"].to(dtype), voxel_size)
+    if capture is not None:
+        if feats.requires_grad:
+            feats.retain_grad()
+        capture["feats"] = feats
+        capture["offsets"] = torch.cat([torch.zeros(1, dtype=torch.long), mask.sum(-1).cumsum(0)])
     rgb_s, sdf_s = decoder_forward(decoder_params, feats)
     R, S = mask.shape
-    sdf = torch.ones(R, S).masked_scatter(mask, sdf_s)
-    colour = torch.zeros(R, S, 3).masked_scatter(mask.unsqueeze(-1).expand(R, S, 3), rgb_s)
+    sdf = torch.ones(R, S, dtype=dtype).masked_scatter(mask, sdf_s)
+    colour = torch.zeros(R, S, 3, dtype=dtype).masked_scatter(mask.unsqueeze(-1).expand(R, S, 3), rgb_s)
     valid = mask.float()
     z = depth
     w = torch.sigmoid(sdf / truncation) * torch.sigmoid(-sdf / truncation)
     sign = sdf[:, 1:] * sdf[:, :-1]
     first = torch.argmax((sign < 0.0).float(), dim=1)[..., None]
     z_min = torch.gather(z, 1, first)
-    w = w * (z < z_min + truncation).float() * valid
+    # the comparison in fp32 as the reference makes it (exact for fp32 z; a dtype=float64 run keeps fp32's
+    # discrete decisions)
+    w = w * (z.float() < z_min.float() + truncation).to(w.dtype) * valid
     w = w / (w.sum(dim=-1, keepdim=True) + 1e-8)
     return {
         "weights": w,
@@ -337,6 +392,27 @@ def render_rays(rays_o, rays_d, map_states, decoder_params, step_size, voxel_siz
     }
 
 
+def ray_grads_from_dfeat(out, rays_o, rays_d, map_states, voxel_size, dfeat):
+    """The interpolation backward alone, in fp64: per hit ray, d_o = Σ_s
+    ∂feats_s/∂o · dfeat_s and d_d = Σ_s ∂feats_s/∂d · dfeat_s over the ray's
+    samples (render_helpers.py:104-156 differentiated through xyz = o + d·z),
+    for an arbitrary per-sample decoder-input gradient dfeat [M,16] in the
+    ray-major sample order of `out` (a render_rays result).  Returns
+    ([R_hit,3], [R_hit,3]) float64."""
+    hit = out["ray_mask"].view(-1)
+    ro = rays_o.reshape(-1, 3)[hit].detach().double().requires_grad_(True)
+    rd = rays_d.reshape(-1, 3)[hit].detach().double().requires_grad_(True)
+    sidx = out["samples"]["sampled_point_voxel_idx"].long()
+    mask = sidx.ne(-1)
+    z = out["z_vals"].detach().double()
+    xyz = ro.unsqueeze(1) + rd.unsqueeze(1) * z.unsqueeze(2)
+    feats = interp_features(xyz[mask], sidx[mask], map_states["voxel_center_xyz"].double(),
+                            map_states["voxel_vertex_idx"], map_states["voxel_vertex_emb"].detach().double(),
+                            voxel_size)
+    g_o, g_d = torch.autograd.grad(feats, [ro, rd], grad_outputs=dfeat.detach().double())
+    return g_o, g_d
+
+
 # --------------------------------------------------------------------------
 # Criterion — criterion.py:16-116 (weight_depth_loss=False path + median path)
 # --------------------------------------------------------------------------
@@ -347,7 +423,8 @@ def criterion(outputs, rgb_gt, depth_gt, weights_cfg, truncation, max_depth, wei
     z = outputs["z_vals"]
     sdf = outputs["sdf"]
     color_loss = (gt_color - outputs["color"]).abs().mean()
-    valid = (gt_depth > 0.01) & (gt_depth < max_depth)
+    # masks from the fp32 values (a float64 run keeps the reference's discrete decisions)
+    valid = (gt_depth.float() > 0.01) & (gt_depth.float() < max_depth)
     dl = (gt_depth - outputs["depth"]).abs()
     if weight_depth_loss:
         var = (outputs["weights"] * ((outputs["depth"].unsqueeze(-1) - z) ** 2)).sum(-1)
@@ -355,12 +432,13 @@ def criterion(outputs, rgb_gt, depth_gt, weights_cfg, truncation, max_depth, wei
         valid = (tmp < 10 * tmp.median()) & valid
     depth_loss = dl[valid].mean()
     d = gt_depth.unsqueeze(-1).expand(*z.shape)
-    front = (z < d - truncation).float()
-    back = (z > d + truncation).float()
-    dmask = ((d > 0.0) & (d < max_depth)).float()
+    z32, d32 = z.float(), d.float()
+    front = (z32 < d32 - truncation).to(z.dtype)
+    back = (z32 > d32 + truncation).to(z.dtype)
+    dmask = ((d32 > 0.0) & (d32 < max_depth)).to(z.dtype)
     sdf_mask = (1.0 - front) * (1.0 - back) * dmask
-    n_fs = torch.count_nonzero(front).float()
-    n_sdf = torch.count_nonzero(sdf_mask).float()
+    n_fs = torch.count_nonzero(front).to(z.dtype)
+    n_sdf = torch.count_nonzero(sdf_mask).to(z.dtype)
     fs_w = 1.0 - n_fs / (n_fs + n_sdf)
     sdf_w = 1.0 - n_sdf / (n_fs + n_sdf)
     fs_loss = torch.mean(torch.square(sdf * front - front)) * fs_w
@@ -416,10 +494,11 @@ SCANNET_CRITERIA = {"rgb_weight": 1.0, "depth_weight": 1.0, "sdf_weight": 5000.0
 def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_params, step_size, voxel_size,
                         truncation=0.1, max_distance=10.0, criteria=REPLICA_CRITERIA, noise=None,
                         deterministic=False, generator=None, rays_require_grad=True, sum_order="torch",
-                        max_depth=None):
+                        max_depth=None, dtype=torch.float32, capture=None):
     """One bundle-adjust iteration's differentiable part (render_helpers.py:648-671).
 
-    Returns outputs, loss and grads for embeddings, decoder params, rays_o, rays_d."""
+    Returns outputs, loss and grads for embeddings, decoder params, rays_o, rays_d
+    (dtype: see render_rays; the gradients come back in that dtype)."""
     emb = map_states["voxel_vertex_emb"].detach().clone().requires_grad_(True)
     params = {k: v.detach().clone().requires_grad_(True) for k, v in decoder_params.items()}
     ro = rays_o.detach().clone().requires_grad_(rays_require_grad)
@@ -427,8 +506,8 @@ def render_and_backward(rays_o, rays_d, rgb_gt, depth_gt, map_states, decoder_pa
     ms = dict(map_states)
     ms["voxel_vertex_emb"] = emb
     out = render_rays(ro, rd, ms, params, step_size, voxel_size, truncation, max_distance, noise, deterministic,
-                      generator, sum_order)
-    loss, parts = criterion(out, rgb_gt, depth_gt, criteria, truncation,
+                      generator, sum_order, dtype, capture)
+    loss, parts = criterion(out, rgb_gt.to(dtype), depth_gt.to(dtype), criteria, truncation,
                             max_distance if max_depth is None else max_depth)  # data_specs max_depth
     loss.backward()
     grads = {"embeddings": emb.grad, "rays_o": ro.grad, "rays_d": rd.grad}

@@ -80,7 +80,7 @@ struct EngineExchange {
     int nch = 1;               // launch chunks the slot-0 table covers
     int *xi32 = nullptr;       // psvo_engine_exchange_words(world, max_rays_global) int32
     double *xf64 = nullptr;    // 16 doubles: [0, 8) count sums, [8, 16) loss sums
-    bool on() const { return fn != nullptr && world > 1; }
+    bool on() const { return fn != nullptr; }  // world 1 included: the one-rank protocol (tests)
     // int32 word offsets
     int64_t in_off() const { return 0; }
     int64_t all_off() const { return psvo::kDistWordsPerRank; }
@@ -862,8 +862,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
     ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
-    // sparse-exact Adam (single GPU): the rows this step can touch, beside the decoder
-    const bool sparse_rows = d->emb_row_flags && !dist && !(flags & PSVO_STEP_NO_ADAM);
+    // sparse-exact Adam (single GPU): the rows this step can touch, beside the
+    // decoder — marked whenever the flags exist, also when the caller runs the
+    // Adam step itself (PSVO_STEP_NO_ADAM, then psvo_map_adam): a later fused
+    // step must still find these rows (their moments are non-zero from now on)
+    const bool mark_rows = d->emb_row_flags && !dist;
+    const bool sparse_rows = mark_rows && !(flags & PSVO_STEP_NO_ADAM);
     if (dist) {
         ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
                                   q.z_vals, crit_ws, sums_c));
@@ -876,7 +880,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     ENG_CALL(fork_join(ax, st, e->coef_ready));
     // after the normalisers: the fused loss pass waits for them, Adam for the marks
-    if (sparse_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
+    if (mark_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
     if (!empty)
         ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                      q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,

@@ -1068,7 +1068,7 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
 // exchanges 8 words (all-gather), then a [200 · nch, 50] slot-0 table
 // (all-reduce sum: each row is written by its owner, zeros elsewhere) — not
 // its hit lists.
-constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id of its first hit row
+constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id of its first hit row, flags
 
 __global__ void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
                             const int *__restrict__ hit_idx, int *__restrict__ out) {
@@ -1078,19 +1078,21 @@ __global__ void k_dist_pack(const int *__restrict__ stats, const int *__restrict
     out[1] = stats[PSVO_STAT_P];
     out[2] = stats[PSVO_STAT_MAX_CEIL];
     out[3] = r_hit > 0 ? hit_idx[(int64_t)rank_ray[0] * kMaxHits] : -1;
-    for (int k = 4; k < kDistWords; ++k) out[k] = 0;
+    out[4] = stats[PSVO_STAT_FLAGS];  // e.g. a DFS-stack overflow on one rank: every rank fails together
+    for (int k = 5; k < kDistWords; ++k) out[k] = 0;
 }
 
 // union-batch statistics from the gathered words (world x kDistWords)
 __global__ void k_dist_layout(const int *__restrict__ all, int world, int rank, int *__restrict__ stats) {
     if (threadIdx.x != 0) return;
-    int r_hit = 0, p = 0, mc = 0, begin = 0;
+    int r_hit = 0, p = 0, mc = 0, begin = 0, flags = 0;
     for (int r = 0; r < world; ++r) {
         const int *w = all + r * kDistWords;
         if (r < rank) begin += w[0];
         r_hit += w[0];
         p = max(p, w[1]);
         mc = max(mc, w[2]);
+        flags |= w[4];
     }
     // the logical row after this rank's last: the next rank holding hit rows,
     // or (past the union's last row) row 0, as the reference's row-0 padding
@@ -1105,6 +1107,7 @@ __global__ void k_dist_layout(const int *__restrict__ all, int world, int rank, 
     stats[PSVO_STAT_P] = p;
     stats[PSVO_STAT_R_HIT] = r_hit;
     stats[PSVO_STAT_MAX_CEIL] = mc;
+    stats[PSVO_STAT_FLAGS] |= flags;
 }
 
 // table row (b, c) = the voxel ids of logical row b·K' + c·800 (row 0 past the

@@ -193,8 +193,9 @@ class SparseRowSum:
     bit-identical.  Falls back to a dense all-reduce when the padded lists
     would move more bytes than the table.  Returns "sparse" or "dense"."""
 
-    def __init__(self, n_rows, width, device, group=None, ops=None):
+    def __init__(self, n_rows, width, device, group=None, ops=None, force=False):
         self.group = group
+        self.force = bool(force)  # run the protocol on one rank too (tests)
         self.ops = ops if ops is not None else DeviceRowOps()
         self.ids = torch.empty(n_rows, dtype=torch.int32, device=device)
         self.rows = torch.empty(n_rows, width, dtype=torch.float32, device=device)
@@ -203,8 +204,8 @@ class SparseRowSum:
 
     def __call__(self, grad2d):
         n_rows, width = grad2d.shape
-        ws = world()
-        if ws == 1:
+        ws = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+        if ws == 1 and not self.force:
             return "dense"
         self.ops.compact(grad2d, self.ids, self.rows, self.count, self.workspace)
         stage = torch.device("cpu") if _backend(self.group) == "gloo" else grad2d.device
@@ -213,7 +214,7 @@ class SparseRowSum:
         dist.all_gather(counts, cnt, group=self.group)
         counts = [int(c) for c in counts]
         n_max = max(counts)
-        if ws * n_max * (width + 1) >= n_rows * width:
+        if ws * n_max * (width + 1) >= n_rows * width and not (self.force and ws == 1):
             flat = grad2d if stage == grad2d.device else grad2d.to(stage)
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
             if flat is not grad2d:
@@ -257,12 +258,17 @@ class EngineExchange:
     stream; with gloo (CPU rehearsal / tests) operands are staged through the
     host.  `apply` is the whole protocol and works on CPU tensors too."""
 
-    def __init__(self, max_rays_global, device=None, group=None, query_group=None):
-        self.world = world()
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
+    def __init__(self, max_rays_global, device=None, group=None, query_group=None, force=False):
+        # force: run every collective even on one rank (identities) — the
+        # engine's data-parallel protocol end to end on a 1-rank communicator
+        # (tests/test_gpu_rccl.py drives the RCCL branch this way)
+        self.force = bool(force)
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
         self.max_rays_global = int(max_rays_global)
         self.group = group
-        self.nccl = self.world > 1 and _backend(group) == "nccl"
+        self.nccl = (self.world > 1 or self.force) and on and _backend(group) == "nccl"
         if query_group is None and self.nccl:
             query_group = dist.new_group(list(range(self.world)), backend="nccl")
         self.query_group = query_group if query_group is not None else group
@@ -286,7 +292,7 @@ class EngineExchange:
             dst = buf[out_off:out_off + count * self.world]
         else:
             src = dst = buf[in_off:in_off + count]
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             if op == XCH_GATHER_I32:
                 dst.copy_(src)
             return
@@ -349,19 +355,21 @@ class EngineGradExchange:
     row table, where a step touches a small fraction of the rows).  The
     result is averaged over ranks (op "mean", as GradBucket)."""
 
-    def __init__(self, engine, sparse_min_bytes=32 << 20, group=None, ops=None, op="mean"):
+    def __init__(self, engine, sparse_min_bytes=32 << 20, group=None, ops=None, op="mean", force=False):
         self.engine = engine
         self.group = group
+        self.force = bool(force)  # collectives on one rank too (tests)
         self.op = op  # "sum": the engine's union-batch loss (EngineExchange) — gradients add up
         self.n_emb = int(engine.emb.shape[0])
         self.sparse = None
         if self.n_emb * 16 * 4 >= sparse_min_bytes:
-            self.sparse = SparseRowSum(self.n_emb, 16, engine.grad_flat.device, group=group, ops=ops)
+            self.sparse = SparseRowSum(self.n_emb, 16, engine.grad_flat.device, group=group, ops=ops,
+                                       force=force)
         self.last_mode = "dense"
 
     def __call__(self):
-        ws = world()
-        if ws == 1:
+        ws = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+        if ws == 1 and not self.force:
             return
         flat = self.engine.grad_flat
         if self.sparse is None:

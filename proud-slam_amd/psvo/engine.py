@@ -188,6 +188,7 @@ class MappingEngine:
         if noise is not None:
             nz = noise.to(device=dirs.device, dtype=torch.float32).contiguous()
             self._check_noise(nz, dirs, int(rays_per_frame), poses)
+        prev_step = self.step_no
         self.step_no = self.step_no + 1 if adam_step is None else int(adam_step)
         rc = _lib().psvo_map_step_frames(self.handle, L.stream_of(dirs.device), ctypes.addressof(self.desc),
                                          ctypes.addressof(fr), gt_rgb.data_ptr(), gt_d.data_ptr(),
@@ -195,8 +196,15 @@ class MappingEngine:
                                          0 if apply_adam else 1, self.loss_out.data_ptr(),
                                          ctypes.addressof(self.stats))
         if rc != 0:
+            # as step(): the failed iteration did not happen — its Adam step number rolls back, and a
+            # look-ahead query it may have queued is dropped on the engine side too (the next call's
+            # fresh dirs_cam would otherwise be refused against it)
+            self.step_no = prev_step
+            err = self._error("psvo_map_step_frames", rc)
+            L.call("psvo_map_discard", self.handle)
+            self._queued.clear()
             self._ahead = None
-            raise self._error("psvo_map_step_frames", rc)
+            raise err
         self._ahead = next_dirs_cam  # kept alive until the next call consumes its query
         if self.stats_hook is not None:
             self.stats_hook(self.stats)
@@ -230,7 +238,9 @@ class MappingEngine:
                ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
         self.exchange = exchange
         from .dist import EngineGradExchange
-        self.grad_exchange = EngineGradExchange(self, op="sum")  # the union-batch loss: rank gradients add up
+        # the union-batch loss: rank gradients add up (on the exchange's group; forced one-rank runs too)
+        self.grad_exchange = EngineGradExchange(self, op="sum", group=exchange.group,
+                                                force=getattr(exchange, "force", False))
 
     def _error(self, name, rc):
         msg = _lib().psvo_last_error().decode()

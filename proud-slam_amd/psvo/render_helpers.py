@@ -380,7 +380,10 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
     below runs — the same kernels)."""
     from .engine import MappingEngine
     emb = map_states.get("voxel_vertex_emb")
-    if resnet is not None or resnet_optim is not None or model_optim is None or embed_optim is None:
+    # resnet / resnet_optim (Mapping.do_mapping passes both, mapping.py:195-213) are accepted: the render
+    # path never runs the point encoder (get_features_pcd is commented out, render_helpers.py:481), so its
+    # parameters never get a gradient; bundle_adjust_frames checks that resnet_optim's step is a no-op
+    if model_optim is None or embed_optim is None:
         return None
     if not (_is_adam(embed_optim) and _is_adam(model_optim)):
         return None
@@ -397,13 +400,22 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
     if not all(hasattr(loss_criteria, a) for a in ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight",
                                                    "truncation", "max_dpeth")):
         return None
+    # one truncation drives the engine's compositing and its loss: the render's (render_rays' argument)
+    # and the criterion's (criteria sdf_truncation) must agree — Mapping passes the same value
+    if float(truncation) != float(loss_criteria.truncation):
+        return None
+    if resnet_optim is not None:
+        mine = {id(emb)} | {id(p) for p in params}
+        if any(id(p) in mine for g in resnet_optim.param_groups for p in g["params"]):
+            return None
     for kf in keyframe_graph:
         if not (hasattr(kf, "sample_rays") and hasattr(kf, "rays_d") and getattr(kf, "pose", None) is not None):
             return None
     key = (emb.data_ptr(), emb.shape[0], id(sdf_network), map_states["voxel_center_xyz"].data_ptr(),
            map_states["voxel_center_xyz"].shape[0], map_states["voxel_structure"].data_ptr(),
            map_states["voxel_vertex_idx"].data_ptr(), float(voxel_size), float(step_size), float(truncation),
-           float(max_distance))
+           float(max_distance), float(loss_criteria.max_dpeth),
+           tuple(float(getattr(loss_criteria, a)) for a in ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight")))
     eng = _ENGINES.get(key)
     if eng is None:
         if len(_ENGINES) > 4:
@@ -533,7 +545,9 @@ def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_c
 
     Runs on the native engine (one psvo_map_step_frames call per iteration)
     whenever the optimisers are plain Adam over the map embeddings / fused
-    decoder and no point-feature network is attached; otherwise the autograd
+    decoder — including Mapping.do_mapping's call with the point encoder and
+    its optimiser (mapping.py:195-213), which the reference's render path never
+    runs (:481), so that optimiser's step is a no-op; otherwise the autograd
     loop below (same kernels).  Keywords beyond the reference signature:
     `noise` — a callable iteration → sampler noise [200, K', max_steps]
     (parity tests); `engine` — a prepared psvo.engine.MappingEngine to use
@@ -544,6 +558,16 @@ def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_c
     gradients (the default; same results, tests compare both)."""
     if use_engine:
         eng = engine
+        if resnet_optim is not None and num_iterations > 0:
+            # the reference zero_grads every optimiser each iteration (:667-669): set_to_none leaves the
+            # encoder's gradients None, backward never reaches them (:481), so its optim.step() (:674-676)
+            # is a no-op — torch optimisers skip parameters whose grad is None.  Anything else (grads kept
+            # as zero tensors: Adam would still move them by its momentum) takes the autograd loop.
+            resnet_optim.zero_grad()
+            if any(p.grad is not None for g in resnet_optim.param_groups for p in g["params"]):
+                eng = None
+                use_engine = False
+    if use_engine:
         if eng is None:
             eng = _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, embed_optim,
                               model_optim, resnet_optim, voxel_size, step_size, truncation, max_distance, N_rays)

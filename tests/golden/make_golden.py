@@ -15,13 +15,15 @@ tensorboardX) are replaced by empty stubs, torch.Tensor.cuda by identity
 a temp dir.  Noise drawn inside InverseCDFRaySampling is recorded so the
 build can inject the same noise.
 
-BA_room0.npz: the reference's bundle_adjust_frames (3 keyframes, 3
-iterations, pose Adam on the non-first keyframes) — see run_ba_case.
+BA_*.npz: the reference's bundle_adjust_frames (3 keyframes, 3 iterations,
+pose Adam on the non-first keyframes) — see run_ba_case / BA_CASES: room0
+at W = 128, the same with the points encoder + its optimiser passed as
+Mapping.do_mapping passes them, and ScanNet settings at W = 256.
 
 M_mesh_A.npz: the reference's get_scores / eval_points (mesh extraction's
 lattice scores and vertex colours) on the A octree's first 40 SURFACE voxels.
 
-Usage:  python tests/golden/make_golden.py     (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [case ...]   (writes tests/golden/<case>.npz; all by default)
 """
 from __future__ import annotations
 
@@ -249,23 +251,49 @@ def run_mesh_case(rh, nrgbd):
     return rec
 
 
-def run_ba_case(rh, nrgbd, crit_mod, noise_log):
+BA_CASES = {
+    # the round-2 golden: room0, W = 128, Replica criteria, no point encoder
+    "BA_room0": dict(scene="room0", width=128, crit="replica", max_depth=10.0, n_rays=160, resnet=False),
+    # the call Mapping.do_mapping makes (mapping.py:195-213): points_encoder
+    # (variations/resnet.py PointsResNet, replica.yaml:13-14 feature_n 16) and
+    # its Adam (mapping.py:93) passed as resnet / resnet_optim
+    "BA_room0_resnet": dict(scene="room0", width=128, crit="replica", max_depth=10.0, n_rays=160, resnet=True),
+    # ScanNet settings (scannet.yaml: W = 256, rgb_weight 1, max_depth 5 = max_distance, mapping.py:61)
+    "BA_scannet_w256": dict(scene="scannet0000", width=256, crit="scannet", max_depth=5.0, n_rays=128,
+                            resnet=True),
+}
+
+
+def _stub_torchvision():
+    """variations/resnet.py imports torchvision.models at module level (for
+    its commented-out ResNet-18 variant); the PointsResNet it defines is
+    plain Linear/ReLU.  torchvision is not installed here: an empty stub."""
+    if "torchvision" not in sys.modules:
+        tv = types.ModuleType("torchvision")
+        tv.models = types.ModuleType("torchvision.models")
+        sys.modules["torchvision"] = tv
+        sys.modules["torchvision.models"] = tv.models
+
+
+def run_ba_case(rh, nrgbd, crit_mod, noise_log, name="BA_room0"):
     """The reference bundle_adjust_frames (render_helpers.py:559-676): 3
     keyframes (stamps 0, 5, 9 — the first pose stays fixed, :594-596) of a
-    room0-shaped scene at a reduced resolution, 160 rays per frame, 3
-    iterations, Adam(embeddings) / Adam(decoder) lr 5e-3 and each keyframe's
-    pose Adam lr 1e-3 (frame.py:27).  Stub keyframes carry the reference's own
-    se3pose.OptimizablePose and replay recorded pixel samples; the sampler
-    noise of every iteration is recorded."""
+    synthetic scene at a reduced resolution, n_rays per frame, 3 iterations,
+    Adam(embeddings) / Adam(decoder) lr 5e-3 and each keyframe's pose Adam lr
+    1e-3 (frame.py:27); with `resnet` the reference's PointsResNet and its
+    Adam are passed as Mapping.do_mapping passes them.  Stub keyframes carry
+    the reference's own se3pose.OptimizablePose and replay recorded pixel
+    samples; the sampler noise of every iteration is recorded."""
     import importlib
+    spec = BA_CASES[name]
     se3 = importlib.import_module("se3pose")
-    scene = syn.room0()
+    scene = getattr(syn, spec["scene"])()
     vox = syn.surface_voxels(scene, seed=0)
     voxels, children, features = _octree(vox, 256)
     n_nodes = voxels.shape[0]
     Ts = syn.camera_poses(scene, 3, seed=17)
     frames = [syn.SyntheticFrame(scene, T, scale=0.06, seed=100 + i, device="cpu") for i, T in enumerate(Ts)]
-    n_rays, iters = 160, 3
+    n_rays, iters = spec["n_rays"], 3
     gen = torch.Generator().manual_seed(5)
     picks = [[torch.randperm(f.h * f.w, generator=gen)[:n_rays].sort().values for f in frames] for _ in range(iters)]
 
@@ -293,15 +321,23 @@ def run_ba_case(rh, nrgbd, crit_mod, noise_log):
     torch.manual_seed(77)
     emb0 = torch.randn(n_nodes, 16) * 0.3
     emb = emb0.clone().requires_grad_(True)
-    dec = nrgbd.Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none", multires=0)
+    dec = nrgbd.Decoder(depth=2, width=spec["width"], in_dim=16, skips=[], embedder="none", multires=0)
     dec0 = {k: v.detach().clone().numpy() for k, v in dec.state_dict().items()}
+    resnet, resnet_optim, res0 = None, None, {}
+    if spec["resnet"]:
+        _stub_torchvision()
+        resnet = importlib.import_module("variations.resnet").PointsResNet(16)  # replica.yaml:13-14
+        resnet.train()  # mapping.py:183
+        resnet_optim = torch.optim.Adam(resnet.parameters(), lr=5e-3)  # mapping.py:93
+        res0 = {k: v.detach().clone().numpy() for k, v in resnet.state_dict().items()}
     vt = torch.from_numpy(voxels)
     centres = (vt[:, :3] + vt[:, -1:] / 2) * 0.2
     structure = torch.cat([torch.from_numpy(children), vt[:, -1:]], -1).int()
     map_states = {"voxel_vertex_idx": torch.from_numpy(features), "voxel_center_xyz": centres.float(),
                   "voxel_structure": structure, "voxel_vertex_emb": emb}
-    args = types.SimpleNamespace(criteria={**O.REPLICA_CRITERIA, "sdf_truncation": 0.1},
-                                 data_specs={"max_depth": 10.0})
+    criteria = O.REPLICA_CRITERIA if spec["crit"] == "replica" else O.SCANNET_CRITERIA
+    args = types.SimpleNamespace(criteria={**criteria, "sdf_truncation": 0.1},
+                                 data_specs={"max_depth": spec["max_depth"]})
     crit = crit_mod.Criterion(args)
     losses = []
 
@@ -313,8 +349,10 @@ def run_ba_case(rh, nrgbd, crit_mod, noise_log):
     model_optim = torch.optim.Adam(dec.parameters(), lr=5e-3)
     noise_log.clear()
     torch.manual_seed(31)
-    rh.bundle_adjust_frames(kfs, map_states, dec, None, loss_rec, 0.2, 0.02, N_rays=n_rays, num_iterations=iters,
-                            embed_optim=embed_optim, model_optim=model_optim, update_pose=True)
+    # positional order of mapping.py:195-213 (max_distance = data_specs max_depth, mapping.py:61)
+    rh.bundle_adjust_frames(kfs, map_states, dec, resnet, loss_rec, 0.2, 0.02, n_rays, iters, 0.1, 10,
+                            spec["max_depth"], embed_optim=embed_optim, model_optim=model_optim,
+                            resnet_optim=resnet_optim, update_pose=True)
     assert len(noise_log) == iters, len(noise_log)
     emb1 = emb.detach()
     changed = torch.nonzero((emb1 != emb0).any(-1)).squeeze(1)
@@ -325,6 +363,18 @@ def run_ba_case(rh, nrgbd, crit_mod, noise_log):
                step_size=np.float32(0.02), n_rays=np.int64(n_rays), iters=np.int64(iters),
                losses=np.array(losses, np.float32), emb_changed_rows=changed.numpy().astype(np.int64),
                emb1_changed=emb1[changed].numpy())
+    if name != "BA_room0":  # the round-2 file keeps its keys
+        rec.update(width=np.int64(spec["width"]), max_depth=np.float32(spec["max_depth"]),
+                   crit=np.array([criteria[k] for k in ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight")],
+                                 np.float32))
+    if resnet is not None:
+        # the reference never runs the encoder on this path (render_helpers.py:481 commented out): its
+        # parameters never get a gradient and Adam never steps them (no state is created)
+        rec["resnet_optim_states"] = np.int64(len(resnet_optim.state))
+        for k, v in res0.items():
+            rec["res0." + k] = v
+        rec["res_unchanged"] = np.bool_(all(torch.equal(v, torch.from_numpy(res0[k]))
+                                            for k, v in resnet.state_dict().items()))
     for i, fr in enumerate(frames):
         rec[f"frame{i}.rays_d"] = fr.rays_d.numpy()
         rec[f"frame{i}.rgb"] = fr.rgb.numpy()
@@ -340,7 +390,9 @@ def run_ba_case(rh, nrgbd, crit_mod, noise_log):
     return rec
 
 
-def main():
+def main(only=()):
+    """only: case names to (re)generate (default: all)."""
+    want = (lambda n: not only or n in only)
     noise_log = []
     _install_stubs(noise_log)
     rh, nrgbd, crit_mod = _reference_modules()
@@ -349,6 +401,8 @@ def main():
         os.chdir(tmp)  # render_rays np.savetxt()s every call (render_helpers.py:403-404)
         try:
             for name in CASES:
+                if not want(name):
+                    continue
                 rec = run_case(name, rh, nrgbd, crit_mod, noise_log)
                 path = os.path.join(OUT_DIR, f"{name}.npz")
                 np.savez_compressed(path, **rec)
@@ -356,11 +410,16 @@ def main():
                       f"R_hit={int(rec['hits'].sum())} P={rec['hit_idx'].shape[-1]} S={rec['z_vals'].shape[-1]} "
                       f"loss={float(rec['loss']):.6f} -> {os.path.relpath(path, REPO)} "
                       f"({os.path.getsize(path) // 1024} KiB)")
-            rec = run_ba_case(rh, nrgbd, crit_mod, noise_log)
-            path = os.path.join(OUT_DIR, "BA_room0.npz")
-            np.savez_compressed(path, **rec)
-            print(f"BA_room0: nodes={int(rec['n_nodes'])} losses={rec['losses'].tolist()} "
-                  f"-> {os.path.relpath(path, REPO)} ({os.path.getsize(path) // 1024} KiB)")
+            for name in BA_CASES:
+                if not want(name):
+                    continue
+                rec = run_ba_case(rh, nrgbd, crit_mod, noise_log, name)
+                path = os.path.join(OUT_DIR, f"{name}.npz")
+                np.savez_compressed(path, **rec)
+                print(f"{name}: nodes={int(rec['n_nodes'])} losses={rec['losses'].tolist()} "
+                      f"-> {os.path.relpath(path, REPO)} ({os.path.getsize(path) // 1024} KiB)")
+            if not want("M_mesh_A"):
+                return
             rec = run_mesh_case(rh, nrgbd)
             path = os.path.join(OUT_DIR, "M_mesh_A.npz")
             np.savez_compressed(path, **rec)
@@ -371,4 +430,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -43,13 +43,43 @@ class _KF:
         self.sample_mask = m.view(self.h, self.w)
 
 
+class PointsEncoder(torch.nn.Module):
+    """Stand-in for the reference's points encoder (variations/resnet.py
+    PointsResNet(feature_n=16), replica.yaml:13-14): the same Linear / ReLU
+    stack and state_dict keys, so the golden's initial weights load."""
+
+    def __init__(self, feature_n=16):
+        super().__init__()
+        L, R = torch.nn.Linear, torch.nn.ReLU
+        self.resnet = torch.nn.Sequential(L(6, 64), R(), L(64, 128), R(), L(128, 256), R(), L(256, 512), R())
+        self.fc = L(512, feature_n)
+
+    def forward(self, x1, y):
+        x = torch.cat((x1, y), 2)
+        x = self.resnet(x.reshape(-1, x.shape[2])).view(x1.size(0), x1.size(1), -1)
+        return self.fc(x)
+
+
+BA_GOLDENS = ["BA_room0", "BA_room0_resnet", "BA_scannet_w256"]
+
+
+@pytest.mark.parametrize("name", BA_GOLDENS)
 @pytest.mark.parametrize("use_engine", [True, False])
-def test_bundle_adjust_matches_reference(use_engine):
+def test_bundle_adjust_matches_reference(use_engine, name):
+    """BA_room0: the round-2 call shape (no encoder); BA_room0_resnet: the
+    call Mapping.do_mapping makes — points encoder and its Adam passed
+    positionally as mapping.py:195-213 does (they must not keep the native
+    engine from running, and the encoder must come out untouched with no
+    Adam state, as in the reference); BA_scannet_w256: the same call at
+    ScanNet settings (W = 256 decoder, rgb weight 1, max_depth 5)."""
     import types
     from psvo import render_helpers as RH
     from psvo.criterion import Criterion
     from psvo.decoder import Decoder
-    g = load_golden("BA_room0")
+    from test_oracle_golden import ba_settings
+    g = load_golden(name)
+    crit_w, max_depth = ba_settings(g)
+    width = int(g["width"]) if "width" in g else 128
     n = int(g["n_nodes"])
     torch.manual_seed(int(g["emb_seed"]))
     emb0 = torch.randn(n, 16) * float(g["emb_std"])
@@ -57,23 +87,36 @@ def test_bundle_adjust_matches_reference(use_engine):
     ms = {"voxel_vertex_idx": torch.from_numpy(g["features"]).to(DEV),
           "voxel_center_xyz": torch.from_numpy(g["centres"]).to(DEV),
           "voxel_structure": torch.from_numpy(g["structure"]).to(DEV), "voxel_vertex_emb": emb}
-    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec = Decoder(depth=2, width=width, in_dim=16, skips=[], embedder="none").to(DEV)
     dec.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("dec0.")})
     iters = int(g["iters"])
     picks = [[g[f"pick{it}.{i}"] for i in range(3)] for it in range(iters)]
     noises = [torch.from_numpy(g[f"noise{it}"]) for it in range(iters)]
     kfs = [_KF(i, g, picks, st) for i, st in enumerate(g["stamps"])]
-    crit = Criterion(types.SimpleNamespace(criteria={"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0,
-                                                     "fs_weight": 10.0, "sdf_truncation": 0.1},
-                                           data_specs={"max_depth": 10.0}))
+    crit = Criterion(types.SimpleNamespace(criteria={**crit_w, "sdf_truncation": 0.1},
+                                           data_specs={"max_depth": max_depth}))
     eo = torch.optim.Adam([emb], lr=5e-3)
     mo = torch.optim.Adam(dec.parameters(), lr=5e-3)
+    resnet, ro = None, None
+    if "resnet_optim_states" in g:
+        resnet = PointsEncoder(16).to(DEV)
+        resnet.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("res0.")})
+        resnet.train()
+        ro = torch.optim.Adam(resnet.parameters(), lr=5e-3)
+        for p in resnet.parameters():  # a stale gradient from elsewhere: the reference's zero_grad drops it
+            p.grad = torch.ones_like(p)
     RH._ENGINES.clear()
-    RH.bundle_adjust_frames(kfs, ms, dec, None, crit, 0.2, float(g["step_size"]), N_rays=int(g["n_rays"]),
-                            num_iterations=iters, embed_optim=eo, model_optim=mo, update_pose=True,
+    # positional order of mapping.py:195-213
+    RH.bundle_adjust_frames(kfs, ms, dec, resnet, crit, 0.2, float(g["step_size"]), int(g["n_rays"]), iters, 0.1,
+                            10, max_depth, embed_optim=eo, model_optim=mo, resnet_optim=ro, update_pose=True,
                             noise=lambda it: noises[it], use_engine=use_engine)
     torch.cuda.synchronize()
     assert (len(RH._ENGINES) == 1) == use_engine  # the native path ran (or not)
+    if resnet is not None:
+        assert len(ro.state) == int(g["resnet_optim_states"]) == 0
+        assert all(p.grad is None for p in resnet.parameters())
+        for k, v in resnet.state_dict().items():
+            assert np.array_equal(v.cpu().numpy(), g["res0." + k]), k
     poses = np.stack([kf.pose.data.detach().cpu().numpy() for kf in kfs])
     np.testing.assert_allclose(poses, g["poses1"], rtol=0, atol=1e-5)
     assert np.array_equal(poses[0], g["pose0"][0])  # stamp 0: no pose optimiser

@@ -12,14 +12,16 @@ k_sample_fused on the same rays and noise:
     right on both sides (oracle.sequential_row_sums); that the sample COUNT
     does not depend on the order is checked separately: ⌈Σ/step⌉ agrees
     between torch's CPU order and the sequential one on every ray;
-  * the whole render + Criterion + backward chain at configs B (W=128) and
-    C (W=256): z_vals bit-exact, fp32 outputs rtol 1e-4 / atol 1e-5, loss
-    rtol 1e-4, gradients ≤ 2e-3 · max|ref| (float-atomic / GEMM order).
+  * the whole render + Criterion + backward chain at every config (B, D
+    W = 128; C, E W = 256): z_vals bit-exact, fp32 outputs rtol 1e-4 /
+    atol 1e-5, loss rtol 1e-4, gradients ≤ 2e-3 · max|ref| (float-atomic /
+    GEMM order), the per-ray pose gradients link by link against the fp64
+    oracle (test_render_loss_grads_full_size).
 
 Configs (BASELINE.json): B room0 4 x 1024 rays; C scannet0000 8 x 1024 rays
 (W = 256, max_depth 5); D office0 32 x 1024 rays (the whole global batch of
 the 8-GPU config on one GPU); E multiroom (>1M SURFACE leaves, depth-10 tree)
-4 x 1024 rays."""
+4 x 1024 rays, W = 256 as ARKit (configs/arkit/arkit.yaml:17)."""
 import math
 
 import numpy as np
@@ -35,7 +37,7 @@ CONFIGS = {
     "B": dict(scene="room0", frames=4, rays=1024, step=0.0078, width=128, max_depth=10.0),
     "C": dict(scene="scannet0000", frames=8, rays=1024, step=0.008, width=256, max_depth=5.0),
     "D": dict(scene="office0", frames=32, rays=1024, step=0.008, width=128, max_depth=10.0),
-    "E": dict(scene="multiroom", frames=4, rays=1024, step=0.008, width=128, max_depth=10.0),
+    "E": dict(scene="multiroom", frames=4, rays=1024, step=0.008, width=256, max_depth=10.0),
 }
 _CACHE = {}
 
@@ -119,8 +121,48 @@ def test_sampler_bit_exact_full_size(name):
         assert 60 < smp.m / smp.r_hit < 70  # the metric's ~64 samples per hit ray
 
 
-@pytest.mark.parametrize("name", ["B", "C"])
+def _capture_decoder(dec):
+    """Record the decoder's input features and their gradient (dfeat) on the
+    GPU path, in its ray-major sample order."""
+    cap = {}
+    fwd = dec.forward
+
+    def hooked(inputs):
+        x = inputs["emb"]
+        cap["x"] = x.detach()
+        if x.requires_grad:
+            x.register_hook(lambda g: cap.__setitem__("dfeat", g.detach()))
+        return fwd(inputs)
+
+    dec.forward = hooked
+    return cap
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
 def test_render_loss_grads_full_size(name):
+    """Render + Criterion + backward at full size against the oracle, with the
+    per-ray pose gradients (d rays_o, d rays_d) checked link by link:
+
+    1. values, loss, embedding / decoder gradients against the fp32 oracle
+       (the reference's arithmetic): rtol 1e-4 / ≤ 2e-3·max;
+    2. the interpolation backward: the GPU's d_o / d_d equal the exact (fp64)
+       chain applied to the GPU's OWN per-sample decoder-input gradient
+       dfeat, to 1e-4·max on every ray — so any per-ray difference from the
+       oracle comes from dfeat, not from the ray reduction;
+    3. the decoder: every sample's dfeat within 2e-4·max of the fp64 oracle
+       (the same function without fp32 rounding, oracle.render_rays
+       dtype=float64), in both fp32 implementations (GPU and oracle), except
+       near-ties (oracle.decoder_margins < 1e-5): a sample with a ReLU unit
+       whose pre-activation is within fp32 rounding of zero, or any sample of
+       a ray whose sdf is (the compositing's first sign change can move).
+       There fp32 rounding in ANY order can land on either side: a
+       discontinuity of the reference's own fp32 function
+       (scripts/debug_c256.py walks config C's worst rays: the fused path, the
+       torch-fp32 decoder and the fp32 oracle all flip the same unit at
+       |a| ~ 1e-7 and sit the same 9e-3·max from the exact d_o; config D has
+       a ray whose sdf is 2e-8 in fp32 and -6e-9 exactly);
+    4. d_o / d_d against the fp32 oracle: ≤ 2e-3·max on every ray except rays
+       holding such a near-tie (3), which stay ≤ 2e-2·max."""
     import types
     from psvo.criterion import Criterion
     from psvo.decoder import Decoder
@@ -138,11 +180,18 @@ def test_render_loss_grads_full_size(name):
     kp = (int(hit.sum()) + 199) // 200
     noise = torch.rand((200, kp, max_steps), generator=torch.Generator().manual_seed(13)).clamp(0.001, 0.999)
     rgb, depth = w.rgb.reshape(1, -1, 3), w.depth.reshape(1, -1)
-    o_res, o_loss, _, o_grads = O.render_and_backward(w.rays_o, w.rays_d, rgb, depth, ms_cpu, params, c["step"], vs,
+    orc = {}
+    for dt in (torch.float32, torch.float64):
+        cap = {}
+        res, loss_o, _, grads = O.render_and_backward(w.rays_o, w.rays_d, rgb, depth, ms_cpu, params, c["step"], vs,
                                                       0.1, 10.0, crit_w, noise=noise, sum_order="sequential",
-                                                      max_depth=c["max_depth"])
+                                                      max_depth=c["max_depth"], dtype=dt, capture=cap)
+        orc[dt] = (res, loss_o, grads, cap["feats"].grad.detach().double(), cap["feats"].detach())
+    o_res, o_loss, o_grads, dfeat32, _ = orc[torch.float32]
+    x_res64, _, o_grads64, dfeat64, x64 = orc[torch.float64]
     dec = Decoder(depth=2, width=c["width"], in_dim=16, skips=[], embedder="none").to(DEV)
     dec.load_state_dict(params)
+    gcap = _capture_decoder(dec)
     emb = ms["voxel_vertex_emb"].clone().requires_grad_(True)
     ms2 = dict(ms, voxel_vertex_emb=emb)
     ro = w.rays_o.to(DEV).requires_grad_(True)
@@ -152,6 +201,7 @@ def test_render_loss_grads_full_size(name):
                                            data_specs={"max_depth": c["max_depth"]}))
     loss, _ = crit(out, (rgb.to(DEV), depth.to(DEV)))
     loss.backward()
+    # 1. values and map / decoder gradients against the fp32 oracle
     assert torch.equal(out["ray_mask"].cpu(), o_res["ray_mask"])
     assert torch.equal(out["z_vals"].cpu(), o_res["z_vals"])
     tol = dict(rtol=1e-4, atol=1e-5)
@@ -159,23 +209,50 @@ def test_render_loss_grads_full_size(name):
     torch.testing.assert_close(out["color"].detach().cpu(), o_res["color"].detach(), **tol)
     torch.testing.assert_close(out["depth"].detach().cpu(), o_res["depth"].detach(), **tol)
     assert abs(float(loss) - float(o_loss)) <= 1e-4 * abs(float(o_loss))
-    pairs = [("embeddings", emb.grad, o_grads["embeddings"]), ("rays_o", ro.grad, o_grads["rays_o"]),
-             ("rays_d", rd.grad, o_grads["rays_d"])]
+    pairs = [("embeddings", emb.grad, o_grads["embeddings"])]
     for k, p in dec.named_parameters():
         pairs.append((k, p.grad, o_grads[k]))
     for k, a, b in pairs:
         scale = float(b.abs().max()) + 1e-12
-        d = (a.detach().cpu() - b).abs()
-        err = float(d.max())
-        if k in ("rays_o", "rays_d") and c["width"] == 256:
-            # per-ray d_o / d_d sum many cancelling per-sample terms (|Σ| ≪ Σ|·|).  At W = 256 the
-            # fused decoder (within 2e-4·max per sample, test_gpu_mlp.py) moves a few rays' sums more
-            # than the torch-fp32 decoder does (scripts/debug_c.py: 1 ray of 8,192 at 5e-3·max, the
-            # next at 1.8e-3; torch 10x closer) — an error concentrated in single rays, as a ReLU mask
-            # flipped by a different summation order at a near-zero pre-activation would give (not
-            # isolated further).  Bar: every ray within 1e-2·max, >= 99.9 % of rays within 2e-3·max
-            per_ray = d.reshape(-1, 3).amax(-1)
-            assert err <= 1e-2 * scale, (k, err, scale)
-            assert float((per_ray > 2e-3 * scale).float().mean()) <= 1e-3, (k, int((per_ray > 2e-3 * scale).sum()))
-            continue
+        err = float((a.detach().cpu() - b).abs().max())
         assert err <= 2e-3 * scale, (k, err, scale)
+    # 2. the interpolation backward, exact given the GPU's own dfeat
+    dfeat_gpu = gcap["dfeat"].cpu().double()
+    assert dfeat_gpu.shape == dfeat64.shape
+    c_o, c_d = O.ray_grads_from_dfeat(x_res64, w.rays_o, w.rays_d, ms_cpu, vs, dfeat_gpu)
+    g_o = ro.grad.detach().cpu()[0][hit].double()
+    g_d = rd.grad.detach().cpu()[0][hit].double()
+    for k, got, exp in (("rays_o", g_o, c_o), ("rays_d", g_d, c_d)):
+        err = float((got - exp).abs().max())
+        assert err <= 1e-4 * float(exp.abs().max()), (k, err, float(exp.abs().max()))
+    # 3. the decoder, per sample, against the exact value; near-ties excepted
+    dscale = float(dfeat64.abs().max())
+    dev_gpu = (dfeat_gpu - dfeat64).abs().amax(-1)
+    dev_o32 = (dfeat32 - dfeat64).abs().amax(-1)
+    off = torch.nonzero(torch.maximum(dev_gpu, dev_o32) > 2e-4 * dscale).squeeze(1)
+    offsets = torch.cat([torch.zeros(1, dtype=torch.long),
+                         x_res64["samples"]["sampled_point_voxel_idx"].ne(-1).sum(-1).cumsum(0)])
+    ray_of = lambda smp: torch.searchsorted(offsets, smp, right=True) - 1  # noqa: E731
+    tie_rays = torch.zeros(offsets.shape[0] - 1, dtype=torch.bool)
+    relu_tie = torch.zeros(off.shape[0], dtype=torch.bool)
+    if off.numel():
+        relu_m, _ = O.decoder_margins(params, x64[off])
+        relu_tie = relu_m < 1e-5
+        tie_rays[ray_of(off[relu_tie])] = True
+        # a ray whose sdf is a near-zero tie somewhere: the first sign change may move (every sample's weight)
+        for r in torch.unique(ray_of(off[~relu_tie])).tolist():
+            _, sdf_m = O.decoder_margins(params, x64[int(offsets[r]):int(offsets[r + 1])])
+            tie_rays[r] = bool((sdf_m < 1e-5).any())
+    explained = relu_tie | tie_rays[ray_of(off)]
+    assert bool(explained.all()), ("dfeat off the fp64 value with no near-tie", off[~explained][:5].tolist())
+    # ties are rare: measured on the fp32 oracle alone 78 of 32,768 rays at D (0.24 %)
+    assert int(tie_rays.sum()) <= max(4, 1e-2 * tie_rays.shape[0]), int(tie_rays.sum())
+    # 4. per-ray pose gradients against the fp32 oracle: rays without a near-tie at the 2e-3 bar
+    for k, got in (("rays_o", g_o), ("rays_d", g_d)):
+        ref = o_grads[k][0][hit].double()
+        scale = float(ref.abs().max())
+        per_ray = (got - ref).abs().amax(-1)
+        bad = per_ray > 2e-3 * scale
+        assert not bool((bad & ~tie_rays).any()), (k, torch.nonzero(bad & ~tie_rays).squeeze(1)[:5].tolist(),
+                                                   float(per_ray[bad & ~tie_rays].max() / scale))
+        assert float(per_ray.max()) <= 2e-2 * scale, (k, float(per_ray.max() / scale))

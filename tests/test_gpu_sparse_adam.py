@@ -17,13 +17,19 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def test_sparse_adam_equals_dense(monkeypatch):
+@pytest.mark.parametrize("mixed", [False, True])
+def test_sparse_adam_equals_dense(monkeypatch, mixed):
+    """mixed: the first iteration runs as step(apply_adam=False) + adam() (the
+    data-parallel pattern) on keyframe 0's rays only, the next two fused on
+    keyframes 1-3 — rows touched only by the first must keep being stepped
+    (their moments are non-zero) by the later sparse steps."""
     import test_gpu_fullsize_parity as F
     from psvo.decoder import Decoder
     from psvo.engine import MappingEngine
     c, w, ms, _ = F._setup("B")
     emb0 = ms["voxel_vertex_emb"].detach().clone()
     res = {}
+    n1 = w.rays_o.shape[1] // 4
     for flag in ("0", "1"):
         monkeypatch.setenv("PSVO_SPARSE_ADAM", flag)
         torch.manual_seed(0)
@@ -33,7 +39,14 @@ def test_sparse_adam_equals_dense(monkeypatch):
         assert (eng.row_flags is not None) == (flag == "1")
         dec1 = None
         for it in range(3):
-            eng.step(w.rays_o.to(DEV), w.rays_d.to(DEV), w.rgb.to(DEV), w.depth.to(DEV), seed=11 + it)
+            if mixed:
+                sl = slice(0, n1) if it == 0 else slice(n1, None)
+                ro, rd, rgb, dep = (t[:, sl].contiguous().to(DEV) for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
+                eng.step(ro, rd, rgb, dep, seed=11 + it, apply_adam=it > 0)
+                if it == 0:
+                    eng.adam()
+            else:
+                eng.step(w.rays_o.to(DEV), w.rays_d.to(DEV), w.rgb.to(DEV), w.depth.to(DEV), seed=11 + it)
             if it == 0:  # the first update does not depend on the float-atomic embedding gradient
                 dec1 = [p.detach().cpu().clone() for p in dec.parameters()]
         torch.cuda.synchronize()

@@ -1,5 +1,6 @@
 """Pin the CPU oracle to golden vectors produced by the reference's own Python
 path (tests/golden/make_golden.py).  CPU only."""
+import pytest
 import numpy as np
 import torch
 
@@ -114,8 +115,20 @@ def test_sampler_done_case_reads_next_slot():
     assert o_idx[0].tolist() == [[3, 3, 3, 3, 7], [7, 7, 7, 7, 11], [11, 11, 11, 11, 13], [13, 13, 13, 13, -1]]
 
 
-def _ba_inputs():
-    g = load_golden("BA_room0")
+BA_GOLDENS = ["BA_room0", "BA_room0_resnet", "BA_scannet_w256"]
+
+
+def ba_settings(g):
+    """(criteria dict, max_depth = max_distance) of a BA golden (mapping.py:61)."""
+    from oracle import oracle as O
+    if "crit" not in g:
+        return dict(O.REPLICA_CRITERIA), 10.0
+    names = ("rgb_weight", "depth_weight", "fs_weight", "sdf_weight")
+    return dict(zip(names, (float(x) for x in g["crit"]))), float(g["max_depth"])
+
+
+def _ba_inputs(name="BA_room0"):
+    g = load_golden(name)
     n = int(g["n_nodes"])
     torch.manual_seed(int(g["emb_seed"]))
     emb0 = torch.randn(n, 16) * float(g["emb_std"])
@@ -131,23 +144,40 @@ def _ba_inputs():
     return g, emb0, ms, frames, picks, noises, dec0
 
 
-def test_oracle_bundle_adjust_matches_reference():
+@pytest.mark.parametrize("name", BA_GOLDENS)
+def test_oracle_bundle_adjust_matches_reference(name):
     """The oracle's bundle_adjust_frames restatement (poses included) against
-    the reference's own run (BA_room0): losses of all 3 iterations, final
-    keyframe poses (the first, stamp 0, unchanged), embeddings, decoder."""
+    the reference's own runs (BA_*: room0 W = 128, the same with the points
+    encoder passed as Mapping.do_mapping passes it, ScanNet W = 256): losses
+    of all 3 iterations, final keyframe poses (the first, stamp 0,
+    unchanged), embeddings, decoder."""
     from oracle import oracle as O
-    g, emb0, ms, frames, picks, noises, dec0 = _ba_inputs()
+    g, emb0, ms, frames, picks, noises, dec0 = _ba_inputs(name)
+    crit, max_depth = ba_settings(g)
     losses, emb1, dec1, poses1 = O.bundle_adjust(frames, picks, noises, ms, dec0, g["pose0"], g["stamps"],
-                                                 float(g["step_size"]), 0.2, int(g["iters"]))
+                                                 float(g["step_size"]), 0.2, int(g["iters"]), criteria=crit,
+                                                 max_distance=max_depth)
+    if "resnet_optim_states" in g:  # the encoder never gets a gradient: Adam never creates state for it
+        assert int(g["resnet_optim_states"]) == 0 and bool(g["res_unchanged"])
     np.testing.assert_allclose(losses, g["losses"], rtol=1e-5)
-    np.testing.assert_allclose(poses1.numpy(), g["poses1"], rtol=0, atol=1e-6)
+    # W = 256: one pose element 5e-6 off (0.5 % of the pose lr) — summation order of the wider decoder's
+    # per-sample terms, amplified by Adam's normalised step
+    np.testing.assert_allclose(poses1.numpy(), g["poses1"], rtol=0, atol=1e-6 if name.startswith("BA_room0") else 1e-5)
     assert np.array_equal(poses1.numpy()[0], g["pose0"][0])
     rows = torch.from_numpy(g["emb_changed_rows"])
     changed = torch.nonzero((emb1 != emb0).any(-1)).squeeze(1)
     assert torch.equal(changed, rows)
-    adam_close(emb1[rows].numpy(), g["emb1_changed"])
-    for k, v in dec1.items():
-        adam_close(v.numpy(), g["dec1." + k])
+    if name.startswith("BA_room0"):
+        adam_close(emb1[rows].numpy(), g["emb1_changed"])
+        for k, v in dec1.items():
+            adam_close(v.numpy(), g["dec1." + k])
+    else:
+        # W = 256 (torch-CPU GEMMs of other shapes sum in another order than the reference's): measured
+        # 98.8 % of embedding elements within 1e-6 / 99.6 % within 1e-5, the worst 0.16 lr (a near-zero
+        # gradient's sign); decoder all but 2 elements within 1e-4
+        adam_close(emb1[rows].numpy(), g["emb1_changed"], tight=1e-5, frac=0.99, max_abs=2 * 5e-3)
+        for k, v in dec1.items():
+            adam_close(v.numpy(), g["dec1." + k], tight=1e-4, frac=0.999, max_abs=2 * 5e-3)
 
 
 def adam_close(got, ref, lr=5e-3, tight=1e-6, frac=0.98, max_abs=None):
