@@ -1,16 +1,21 @@
-"""Benchmark: rays/s for render + loss + backward (+ optimiser step) of the
-Proud-SLAM mapping render-and-optimise iteration (render_helpers.py:609-676)
-on synthetic Replica room0-shaped input (BASELINE.json configs[1]: 4096
-rays/iter = 4 keyframes x 1024 rays, 1x MI355X; ~64 samples/ray).
+"""Benchmark: rays/s for render + loss + backward (+ optimiser steps) of the
+Proud-SLAM mapping render-and-optimise iteration — bundle_adjust_frames
+(render_helpers.py:559-676) called exactly as Mapping.do_mapping calls it
+(mapping.py:195-213: points encoder + its Adam, torch Adam optimisers on the
+embeddings and decoder, keyframe pose optimisers) — on synthetic Replica
+room0-shaped input (BASELINE.json configs[1]: 4096 rays/iter = 4 keyframes x
+1024 rays, 1x MI355X; ~64 samples/ray).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--extras] [--no-traffic]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One process per GPU; every rank renders its own 4096 rays against the
-replicated octree (weak scaling) and the embedding + decoder gradients are
-summed over ranks with one RCCL all-reduce per step.  Rank 0 prints one JSON
-line.  Inputs (octree, embeddings, decoder, a pool of ray batches with GT)
-are resident in HBM before timing starts.
+One process per GPU; every rank renders its own keyframes' 4096 rays against
+the replicated octree (weak scaling); the loss is the union batch's and the
+embedding + decoder gradients are summed over ranks.  Rank 0
+prints one JSON line.  Inputs (octree, embeddings, decoder, full-resolution
+keyframes) are resident in HBM before timing starts.  The roofline carries
+kernel durations measured in the headline iterations and HBM bytes from two
+PMC passes over the same iterations (rocprofv3 children, before the JSON).
 """
 from __future__ import annotations
 
@@ -57,18 +62,18 @@ def parse():
     ap.add_argument("--pool", type=int, default=8, help="distinct ray batches cycled through")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--path", choices=("ba", "step", "autograd"), default="ba",
-                    help="headline: ba = the reference's bundle_adjust_frames API (keyframe poses optimised too; "
-                         "dispatches to the native engine), step = the engine's psvo_map_step on pre-built "
-                         "world-space ray batches, autograd = render_rays + Criterion + backward + Adam")
-    ap.add_argument("--autograd", action="store_true", help="same as --path autograd")
-    ap.add_argument("--exact-global-loss", action="store_true",
-                    help="(kept for compatibility: N>1 always computes the union-batch loss)")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--path", choices=("ba",), default="ba",
+                    help="headline: the reference's bundle_adjust_frames API as Mapping calls it (the other paths: "
+                         "--extras)")
+    ap.add_argument("--extras", action="store_true",
+                    help="also time the other paths (engine step on pre-built batches, drop-in autograd) and the "
+                         "serialised one-stream kernel breakdown (not part of the default run, so that a profile "
+                         "of the default command holds only headline-mode launches)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the PMC passes (rocprofv3 FETCH_SIZE / WRITE_SIZE children) that measure roofline.traffic")
+    ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # PMC child: headline iterations only
+    ap.add_argument("--step-size", type=float, default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
-    if a.autograd:
-        a.path = "autograd"
-    a.autograd = a.path == "autograd"
     big = a.scene in ("scannet0000", "multiroom")  # configs/scannet/scannet.yaml:17, configs/arkit/arkit.yaml:17
     if a.width is None:
         a.width = 256 if big else 128
@@ -207,37 +212,6 @@ def calibrate_step(ms, batches, target, voxel_size, world=1):
     return step, mean_samples(step)
 
 
-class KernelTimer:
-    """HIP events around chosen launches on the launching stream."""
-
-    def __init__(self):
-        self.events = {}
-        self.enabled = False
-
-    def __call__(self, name):
-        timer = self
-
-        class _Ctx:
-            def __enter__(self_):
-                if timer.enabled:
-                    s = torch.cuda.Event(enable_timing=True)
-                    s.record(torch.cuda.current_stream())
-                    self_.s = s
-
-            def __exit__(self_, *exc):
-                if timer.enabled:
-                    e = torch.cuda.Event(enable_timing=True)
-                    e.record(torch.cuda.current_stream())
-                    timer.events.setdefault(name, []).append((self_.s, e))
-        return _Ctx()
-
-    def mean_ms(self, name):
-        ev = self.events.get(name, [])
-        if not ev:
-            return float("nan")
-        return float(np.mean([s.elapsed_time(e) for s, e in ev]))
-
-
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -262,11 +236,30 @@ def _physical_cores():
     return len(cores) or None
 
 
+def _cpu_threads():
+    """Threads for the CPU baseline: the process's CPU share.  On the GPU box
+    that share is 16 host CPUs per GPU (the box sets OMP_NUM_THREADS=16 for
+    it), while the affinity mask shows the whole machine's CPUs; elsewhere the
+    affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return min(int(env), aff), f"OMP_NUM_THREADS={env}: the process's CPU share on this host " \
+                                   f"(affinity mask {aff} CPUs is the whole machine's)"
+    return aff, f"the process's affinity mask ({aff} CPUs)"
+
+
 def cpu_baseline(args, scene, tree, step_size, seconds):
     """Oracle (reference algorithm restated: C kernels + torch-CPU render /
     loss / autograd) on the host cores, bounded sample of the same workload."""
     from oracle import oracle as O
     from psvo import synthetic as syn
+    n_thr, why = _cpu_threads()
+    torch.set_num_threads(n_thr)  # torch-CPU render / loss / autograd; the C kernels use OpenMP (same count)
+    os.environ.setdefault("OMP_NUM_THREADS", str(n_thr))
     voxels, children, features = tree.export_arrays()
     g = torch.Generator().manual_seed(0)
     emb = torch.randn(voxels.shape[0], 16, generator=g) * 0.01
@@ -285,11 +278,75 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
     dt = time.time() - t0
     rays = n_it * ro.shape[1]
     return {"value": rays / dt, "unit": "rays/s", "cores": int(torch.get_num_threads()), "kind": "port",
+            "cores_reason": why,
             "cpu_model": _cpu_model(), "host_physical_cores": _physical_cores(), "host_logical_cpus": os.cpu_count(),
-            "process_cpu_share": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "process_affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
             "sample": f"{n_it} iterations x {ro.shape[1]} rays ({args.scene}, {args.frames}x{args.rays_per_frame}), "
                       f"oracle C kernels (OpenMP over rays) + torch-CPU render/loss/backward, "
                       f"{torch.get_num_threads()} threads, {dt:.1f}s"}
+
+
+CHAIN_KERNELS = ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples", "k_sample_points",
+                 "k_interp_fwd", "k_interp_bwd", "k_interp_bwd_rays")
+MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce", "k_dec256_prep",
+               "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
+
+
+def _short(name):
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0].split("<")[0].split("::")[-1].strip() or name[:40]
+
+
+def measure_traffic(args, step_size):
+    """roofline.traffic, measured for this workload by this run: two rocprofv3
+    PMC passes (FETCH_SIZE, then WRITE_SIZE: they cannot share a pass) over a
+    child `bench.py --probe` that runs only the headline bundle_adjust_frames
+    iterations with this run's step size.  Per kernel the median bytes per
+    launch (FETCH_SIZE doubled: gfx950 tallies a 128-B streaming request as
+    64 B, MI355X_MICROARCH.md §HBM; WRITE_SIZE as is; both count Infinity-
+    Cache traffic).  Returns (dict or None, note)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    from collections import defaultdict
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="psvo_pmc_") as tmp:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, c)
+            cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", c, "--output-format", "csv", "-d", d, "-o", "pmc",
+                   "--", sys.executable, os.path.abspath(__file__), "--probe", "--step-size", repr(step_size),
+                   "--scene", args.scene, "--frames", str(args.frames), "--rays-per-frame", str(args.rays_per_frame),
+                   "--width", str(args.width), "--steps", "8", "--warmup", "2", "--no-cpu-baseline"]
+            env = dict(os.environ, TMPDIR=tmp)
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True)
+            if r.returncode != 0:
+                return None, f"{c} pass failed (rc {r.returncode}): {r.stderr[-300:]}"
+            path = None
+            for root, _, files in os.walk(d):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        path = os.path.join(root, f)
+            if path is None:
+                return None, f"{c} pass wrote no counter_collection.csv"
+            vals = defaultdict(list)
+            for row in csv.DictReader(open(path)):
+                if row.get("Counter_Name") == c:
+                    vals[_short(row["Kernel_Name"])].append(float(row["Counter_Value"]) * 1024.0)  # KB units
+            out[c] = {k: sorted(v)[len(v) // 2] * (2.0 if c == "FETCH_SIZE" else 1.0) for k, v in vals.items()}
+    kern = {}
+    for k in set(out["FETCH_SIZE"]) | set(out["WRITE_SIZE"]):
+        f, w = out["FETCH_SIZE"].get(k, 0.0), out["WRITE_SIZE"].get(k, 0.0)
+        kern[k] = {"fetch": f, "write": w, "total": f + w}
+    res = {"kernels": kern,
+           "query_interp_bytes_per_step": sum(kern[k]["total"] for k in CHAIN_KERNELS if k in kern),
+           "interp_bwd_bytes_per_launch": kern.get("k_interp_bwd", {}).get("total"),
+           "mlp_bytes_per_step": sum(kern[k]["total"] for k in MLP_KERNELS if k in kern)}
+    return res, "measured by this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --probe " \
+                "(headline iterations), median bytes per launch, fetch = 2 x FETCH_SIZE (gfx950)"
 
 
 def main():
@@ -302,6 +359,7 @@ def main():
     from psvo import _lib
     from psvo import render_helpers as RH
     from psvo.criterion import Criterion
+    from psvo.point_feature import PointsResNet
     import types
     _lib.lib()
 
@@ -309,38 +367,37 @@ def main():
     scene, tree, ms, emb, dec = build_scene(args, device, rank)
     log(f"{args.frames} keyframes ({tree.count_nodes()} octree nodes)")
     kfs = build_keyframes(args, scene, device, rank)
-    batches = keyframe_batches(kfs, args.rays_per_frame, args.pool)
-    log("step-size calibration")
-    step_size, spr = calibrate_step(ms, batches, args.samples_per_ray, scene.voxel_size, world)
+    if args.step_size is not None:
+        step_size, spr = args.step_size, float("nan")
+        batches = None
+    else:
+        batches = keyframe_batches(kfs, args.rays_per_frame, args.pool)
+        log("step-size calibration")
+        step_size, spr = calibrate_step(ms, batches, args.samples_per_ray, scene.voxel_size, world)
     log(f"step {step_size:.5f} m, {spr:.1f} samples / hit ray; timing the {args.path} path")
     crit_cfg, max_depth = SCENE_CRITERIA.get(args.scene, DEFAULT_CRITERIA)
     crit_args = types.SimpleNamespace(criteria=dict(crit_cfg), data_specs={"max_depth": max_depth})
     criterion = Criterion(crit_args)
-    from psvo.optim import Adam  # torch.optim.Adam semantics, one HIP launch per step per optimiser
-    embed_optim = Adam([emb], lr=5e-3)
-    model_optim = Adam(dec.parameters(), lr=5e-3)
-    params = [emb] + list(dec.parameters())
-    timer = KernelTimer()
-    _lib.KERNEL_TIMER = timer
+    # Mapping's optimisers (mapping.py:81-82, 93) and its points encoder
+    # (mapping.py:36, variations/resnet.py; never run by the render path)
+    embed_optim = torch.optim.Adam([emb], lr=5e-3)
+    model_optim = torch.optim.Adam(dec.parameters(), lr=5e-3)
+    points_encoder = PointsResNet(16).to(device)
+    points_encoder.train()
+    resnet_optim = torch.optim.Adam(points_encoder.parameters(), lr=5e-3)
     stats = {"n": 0, "m": 0, "r_hit": 0, "visits": 0, "s_max": 0}  # the marked (breakdown) runs
     head_stats = dict(stats)  # the headline bundle_adjust_frames iterations
 
-    from psvo.dist import GlobalBatch, GlobalLossSums, GradBucket
     from psvo.engine import MappingEngine
-    # N > 1: both paths form the loss of the union of the ranks' rays (global
-    # sampler layout and normalisers) and sum the gradients with one flat
-    # all-reduce per step
-    bucket = GradBucket(params, op="sum")
-    reducer = GlobalLossSums() if world > 1 else None
-    gbatch = GlobalBatch() if world > 1 else None
-    engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=10.0,
-                           criteria=crit_args.criteria, max_depth=max_depth, lr_emb=5e-3, lr_dec=5e-3)
-    from psvo.dist import EngineExchange, EngineGradExchange
+    from psvo.dist import EngineExchange
+    # N > 1: the union batch's loss needs an engine with the
+    # ranks' exchange, handed to bundle_adjust_frames; N = 1: the reference's
+    # own call, dispatched to the native engine by bundle_adjust_frames itself
+    dp_engine = None
     if world > 1:
-        # the loss of the union of all ranks' rays: union-batch
-        # sampler layout and normalisers, gradients summed over ranks
-        engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
-    exchange = EngineGradExchange(engine, op="sum")
+        dp_engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=max_depth,
+                                  criteria=crit_args.criteria, max_depth=max_depth, lr_emb=5e-3, lr_dec=5e-3)
+        dp_engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
 
     def record_stats(m, r_hit, visits, s_max, into=None):
         sd = stats if into is None else into
@@ -350,90 +407,37 @@ def main():
         sd["visits"] += visits
         sd["s_max"] = max(sd["s_max"], s_max)
 
-    def step_autograd(i, record=False):
-        """The drop-in path: render_rays + Criterion + backward + Adam steps."""
-        ro, rd, rgb, depth = batches[i % len(batches)]
-        out = RH.render_rays(ro, rd, ms, dec, None, step_size, scene.voxel_size, 0.1, 10, 10.0, return_samples=True,
-                             seed=7919 * i + 1, batch=gbatch)
-        loss, _ = criterion(out, (rgb, depth), reduce_sums=reducer)
-        embed_optim.zero_grad()  # set_to_none, as optim.zero_grad() in render_helpers.py:668
-        model_optim.zero_grad()
-        loss.backward()
-        if world > 1:
-            bucket.allreduce()
-        embed_optim.step()
-        model_optim.step()
-        if record:
-            s = out["samples"]
-            record_stats(s.m, s.r_hit, s.visits, s.s_max)
-        return loss
-
-    eng_it = [0]  # engine iterations so far: the next batch is always the one already queued
-
-    def eng_batch(it):
-        # one seed for all ranks: the sampler noise is keyed by the union batch's logical row
-        return batches[it % len(batches)], 1000003 + it
-
-    def step_engine(i, record=False):
-        """The same iteration as one native call (psvo_map_step); the next
-        batch's ray query is queued first (psvo_map_query, side stream: it
-        reads only rays + octree, so it overlaps this step).  With N > 1 the
-        flat gradient bucket is all-reduced (RCCL) before the Adam steps."""
-        it = eng_it[0]
-        eng_it[0] += 1
-        (ro, rd, rgb, depth), seed = eng_batch(it)
-        if not engine._queued:
-            engine.query(ro, rd, seed)
-        (nro, nrd, _, _), nseed = eng_batch(it + 1)
-        engine.query(nro, nrd, nseed)
-        loss = engine.step(ro, rd, rgb, depth, seed=seed, apply_adam=(world == 1))
-        if world > 1:
-            exchange()  # flat RCCL all-reduce (row-sparse exchange for ≥ 32 MB tables), mean over ranks
-            engine.adam()
-        if record:
-            st = engine.last_stats
-            record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3])  # this rank's hit rays
-        return loss
-
-    def run(step_fn, steps, warmup, timed_hook=None):
-        for i in range(warmup):
-            step_fn(i)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        if timed_hook:
-            timed_hook(True)
-        t0 = time.perf_counter()
-        for i in range(steps):
-            step_fn(warmup + i, record=timed_hook is not None)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if timed_hook:
-            timed_hook(False)
-        if world > 1:
-            t = torch.tensor([el], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
-
-    # ---- bundle_adjust_frames (the reference's mapping API, render_helpers.py:
-    # 559-676): this rank's keyframes — full-resolution synthetic RGB-D frames
-    # with their own poses (optimised, lr 1e-3, frame.py:27) — each iteration
-    # samples rays_per_frame pixels per keyframe (gumbel top-k on the device),
-    # renders, back-propagates and steps every optimiser.  K steps = one call
-    # with num_iterations = K (how Mapping calls it).
+    # ---- bundle_adjust_frames as Mapping.do_mapping calls it (mapping.py:
+    # 195-213; render_helpers.py:559-676): this rank's keyframes — full-
+    # resolution synthetic RGB-D frames with their own poses (optimised, lr
+    # 1e-3, frame.py:27) — each iteration samples rays_per_frame pixels per
+    # keyframe (gumbel top-k on the device), renders, back-propagates and steps
+    # every optimiser.  K steps = one call with num_iterations = K.
     ba_calls = [0]
 
     def run_ba(steps):
-        engine.discard_queued()  # a look-ahead query of the engine-step runs
         call = ba_calls[0]
         ba_calls[0] += 1
-        RH.bundle_adjust_frames(kfs, ms, dec, None, criterion, scene.voxel_size, step_size,
-                                N_rays=args.rays_per_frame, num_iterations=steps, embed_optim=embed_optim,
-                                model_optim=model_optim, update_pose=True, engine=engine,
-                                seed_fn=lambda it: 1000003 * (call + 1) + it)  # same on every rank
+        if dp_engine is not None:
+            dp_engine.discard_queued()
+            RH.bundle_adjust_frames(kfs, ms, dec, points_encoder, criterion, scene.voxel_size, step_size,
+                                    args.rays_per_frame, steps, 0.1, 10, max_depth, learning_rate=[1e-2, 1e-3],
+                                    embed_optim=embed_optim, model_optim=model_optim, resnet_optim=resnet_optim,
+                                    update_pose=True, engine=dp_engine,
+                                    seed_fn=lambda it: 1000003 * (call + 1) + it)  # the same on every rank
+        else:
+            RH.bundle_adjust_frames(kfs, ms, dec, points_encoder, criterion, scene.voxel_size, step_size,
+                                    args.rays_per_frame, steps, 0.1, 10, max_depth, learning_rate=[1e-2, 1e-3],
+                                    embed_optim=embed_optim, model_optim=model_optim, resnet_optim=resnet_optim,
+                                    update_pose=True)
+
+    def head_engine():
+        if dp_engine is not None:
+            return dp_engine
+        engs = list(RH._ENGINES.values())
+        if len(engs) != 1:
+            raise RuntimeError("bench: bundle_adjust_frames did not run on the native engine")
+        return engs[0]
 
     def timed_ba(steps, warmup, record=False):
         if warmup:
@@ -441,69 +445,110 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        eng = head_engine() if warmup else None
+        if record and eng is not None:
+            eng.stats_hook = lambda st: record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3], head_stats)
         t0 = time.perf_counter()
-        if record:
-            engine.stats_hook = lambda st: record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3],
-                                                        head_stats)
         run_ba(steps)
-        engine.stats_hook = None
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if eng is not None:
+            eng.stats_hook = None
         if world > 1:
             t = torch.tensor([el], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el
 
-    # the headline steps run without HIP-event markers (each costs a few µs of
-    # GPU idle); the per-region breakdown comes from separate marked runs of
-    # the engine step (pre-built ray batches, the same kernels)
+    if args.probe:  # PMC child (measure_traffic): the headline iterations only
+        run_ba(args.warmup + args.steps)
+        torch.cuda.synchronize()
+        return
+    if args.path != "ba":
+        raise SystemExit("bench.py: the headline is --path ba (the other paths run with --extras)")
+    elapsed = timed_ba(args.steps, max(1, args.warmup), record=True)
+    path_desc = ("bundle_adjust_frames as Mapping.do_mapping calls it (points encoder + its Adam, torch Adam "
+                 "optimisers; per-iteration gumbel pixel sampling on the device, keyframe poses optimised) — "
+                 "dispatched by bundle_adjust_frames to psvo_map_step_frames")
+    eng = head_engine()
+    # the kernels' durations as the headline runs them: HIP events on the
+    # launching streams inside the same bundle_adjust_frames iterations
     n_mark = max(5, min(args.steps, 20))
-    kt_overlap = None
+    eng.set_timing("overlap")
+    timed_ba(n_mark, 0)
+    kt_overlap = eng.timing()
+    eng.set_timing(False)
+    kt_serial = None
     others = []
-    if args.path == "ba":
-        elapsed = timed_ba(args.steps, args.warmup, record=True)
-        path_desc = ("bundle_adjust_frames (drop-in API: per-iteration gumbel pixel sampling on the device, "
-                     "keyframe poses optimised; dispatched to psvo_map_step_frames)")
-    elif args.path == "autograd":
-        elapsed = run(step_autograd, args.steps, args.warmup)
-        path_desc = "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)"
-    else:
-        elapsed = run(step_engine, args.steps, args.warmup)
-        path_desc = "native engine (psvo_map_step on pre-built world-space ray batches, next query one step ahead)"
-    if args.path == "autograd":
-        timer.enabled = True
-        run(step_autograd, n_mark, 0, lambda on: None)
-        timer.enabled = False
-        kt = {k: timer.mean_ms(k) for k in MappingEngine.REGIONS}
-    else:
-        engine.set_timing(True)      # regions serialised on one stream
-        run(step_engine, n_mark, 2, lambda on: None)
-        kt = engine.timing()
-        engine.set_timing("overlap")  # the same regions as the headline steps run them
-        run(step_engine, n_mark, 0)
-        kt_overlap = engine.timing()
-        engine.set_timing(False)
-    # the other paths, for reference (not the headline number)
-    other_steps = max(5, min(args.steps, 20))
     rays_step = args.frames * args.rays_per_frame
-    if world == 1:
-        if args.path != "step":
-            el2 = run(step_engine, other_steps, 2)
-            others.append({"path": "native engine step (psvo_map_step, fixed poses, pre-built rays)",
-                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
-        if args.path != "autograd":
-            el2 = run(step_autograd, other_steps, 2)
-            others.append({"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)",
-                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
-        if args.path != "ba":
-            el2 = timed_ba(other_steps, 2)
-            others.append({"path": "bundle_adjust_frames (native engine, poses optimised)",
-                           "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
-    other = others if others else {"path": "not run at N > 1 (the headline path only)"}
-    rays_per_step = args.frames * args.rays_per_frame
+    if args.extras and world == 1:
+        # the serialised one-stream breakdown and the other paths, on a separate
+        # engine over pre-built world-space batches (fixed poses)
+        if batches is None:
+            batches = keyframe_batches(kfs, args.rays_per_frame, args.pool)
+        from psvo.optim import Adam
+        x_emb = emb.detach().clone().requires_grad_(True)
+        x_ms = dict(ms, voxel_vertex_emb=x_emb)
+        x_eo = Adam([x_emb], lr=5e-3)
+        x_mo = Adam(dec.parameters(), lr=5e-3)
+        engine = MappingEngine(x_ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=max_depth,
+                               criteria=crit_args.criteria, max_depth=max_depth, lr_emb=5e-3, lr_dec=5e-3)
+        eng_it = [0]
+
+        def step_engine(i, record=False):
+            it = eng_it[0]
+            eng_it[0] += 1
+            ro, rd, rgb, depth = batches[it % len(batches)]
+            seed = 1000003 + it
+            if not engine._queued:
+                engine.query(ro, rd, seed)
+            nro, nrd, _, _ = batches[(it + 1) % len(batches)]
+            engine.query(nro, nrd, seed + 1)
+            loss = engine.step(ro, rd, rgb, depth, seed=seed)
+            if record:
+                st = engine.last_stats
+                record_stats(st[4], st[1], st[5], st[3])
+            return loss
+
+        def step_autograd(i, record=False):
+            ro, rd, rgb, depth = batches[i % len(batches)]
+            out = RH.render_rays(ro, rd, x_ms, dec, None, step_size, scene.voxel_size, 0.1, 10, max_depth,
+                                 return_samples=True, seed=7919 * i + 1)
+            loss, _ = criterion(out, (rgb, depth))
+            x_eo.zero_grad()
+            x_mo.zero_grad()
+            loss.backward()
+            x_eo.step()
+            x_mo.step()
+            return loss
+
+        def run(step_fn, steps, warmup, record=False):
+            for i in range(warmup):
+                step_fn(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                step_fn(warmup + i, record)
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+
+        engine.set_timing(True)      # regions serialised on one stream
+        run(step_engine, n_mark, 2, record=True)
+        kt_serial = engine.timing()
+        engine.set_timing(False)
+        engine.discard_queued()
+        other_steps = max(5, min(args.steps, 20))
+        el2 = run(step_engine, other_steps, 2)
+        others.append({"path": "native engine step (psvo_map_step, fixed poses, pre-built rays)",
+                       "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
+        engine.discard_queued()
+        el2 = run(step_autograd, other_steps, 2)
+        others.append({"path": "drop-in autograd (render_rays + Criterion + backward + psvo.optim.Adam)",
+                       "value": rays_step * other_steps / el2, "ms_per_step": 1000.0 * el2 / other_steps})
+        engine.close()
+    rays_per_step = rays_step
     total_rays = rays_per_step * args.steps * world
     value = total_rays / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -511,79 +556,65 @@ def main():
     # Rooflines.  Primary — the north star's "octree query+interp
     # kernel": algorithmic bytes per step = per ray 24 B + 48 B per AABB-tested
     # node (V counted by the kernel) + per valid sample 12 B (sampler output)
-    # + 628 B (interp fwd) + 1,664 B (interp bwd), over the summed HIP-event
-    # time of its launches (intersect + stats + hit rank, sampler + scan,
-    # sample compaction, interp fwd, interp bwd).  Three fractions: the
-    # algorithmic bytes against HBM (the contract's `frac`; > 1 would mean the
-    # gathers are served from L2, and the bound is then reported as L2), the
-    # same against the L2's ≈34.5 TB/s, and the PMC-counted HBM bytes
-    # (FETCH_SIZE x 2 + WRITE_SIZE, profiles/traffic.json) against HBM.  Times
-    # from the serialised marked run (`time_ms`) and as the headline steps
-    # overlap them (`time_ms_overlapped`).  Secondary — the decoder (dominant
-    # by time): fwd, δ chain and weight gradients are each W-dependent MACs per
-    # sample (3 x 2 x MACs FLOP/sample), MFMA-bound.
-    n_rec = max(stats["n"], 1)
-    m_avg = stats["m"] / n_rec
-    r_avg = stats["r_hit"] / n_rec
-    v_avg = stats["visits"] / n_rec
-    # the headline workload: the timed bundle_adjust_frames iterations' own
-    # statistics (else the marked runs', which replay the headline's batches)
-    hs = head_stats if head_stats["n"] else stats
+    # + 628 B (interp fwd) + 1,664 B (interp bwd), over the summed durations of
+    # its launches AS THE HEADLINE RUNS THEM (HIP events on their streams
+    # inside bundle_adjust_frames iterations: intersect + stats + hit rank,
+    # sampler + scan, sample compaction, interp fwd, interp bwd).  In the
+    # headline these kernels share the chip with the decoder (the look-ahead
+    # query beside the weight gradients, the embedding backward beside
+    # k_mlp_dw2), so their durations are longer than alone; the one-stream
+    # serialised durations are reported beside it with --extras.  Traffic:
+    # PMC-counted HBM bytes of the same iterations (measure_traffic).
+    # Secondary — the decoder (dominant by time), MFMA-bound.
+    hs = head_stats
     h_n = max(hs["n"], 1)
     h_m, h_r, h_v = hs["m"] / h_n, hs["r_hit"] / h_n, hs["visits"] / h_n
-    if world > 1:  # per-GPU averages over the union of the ranks' batches (the calibration's population)
+    if world > 1:  # per-GPU averages over the union of the ranks' batches
         t = torch.tensor([h_m, h_r, h_v], dtype=torch.float64, device=device)
         dist.all_reduce(t)
         h_m, h_r, h_v = (float(x) / world for x in t.cpu())
     q_keys = ("intersect", "sample", "points", "interp_fwd", "interp_bwd")
-    q_parts = {k: kt[k] for k in q_keys}
+    q_parts = {k: kt_overlap[k] for k in q_keys}
     q_ms = sum(q_parts.values())
-    q_ms_ov = sum(kt_overlap[k] for k in q_keys) if kt_overlap else None
-    bytes_query = rays_step * 24.0 + v_avg * 48.0 + m_avg * 12.0
-    bytes_qi = bytes_query + m_avg * (628.0 + 1664.0)
-    traffic = {}
-    if os.path.exists(args.traffic_json):
+    bytes_qi = rays_step * 24.0 + h_v * 48.0 + h_m * 12.0 + h_m * (628.0 + 1664.0)
+    traffic, traffic_note = None, "not measured (N > 1 or --no-traffic)"
+    if world == 1 and not args.no_traffic:
+        log("PMC passes (roofline.traffic)")
         try:
-            traffic = json.load(open(args.traffic_json))
-        except Exception:
-            traffic = {}
-        if traffic.get("scene", "room0") != args.scene:  # PMC passes of another scene: not this workload's bytes
-            traffic = {}
+            traffic, traffic_note = measure_traffic(args, step_size)
+        except Exception as exc:  # noqa: BLE001 — the headline stands without it
+            traffic, traffic_note = None, f"PMC passes failed: {type(exc).__name__}: {exc}"
+    tr = traffic or {}
 
-    def bw_roof(kernel, alg_bytes, ms, ms_ov, counter_bytes, extra=None):
+    def bw_roof(kernel, alg_bytes, ms, counter_bytes, ms_serial=None, extra=None):
         gbs = alg_bytes / (ms * 1e-3) / 1e9 if ms and ms > 0 else None
-        frac_hbm = gbs / HBM_PEAK_GBS if gbs else None
-        bound, peak = ("hbm", HBM_PEAK_GBS) if (frac_hbm is None or frac_hbm <= 1.0) else ("l2", L2_PEAK_GBS)
-        r = {"kernel": kernel, "bound": bound, "achieved": gbs, "peak": peak, "unit": "GB/s",
-             "frac": gbs / peak if gbs else None, "traffic": counter_bytes,
-             "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": ms, "time_ms_overlapped": ms_ov,
-             "frac_hbm_algorithmic": frac_hbm,
-             "frac_l2_algorithmic": gbs / L2_PEAK_GBS if gbs else None,
+        r = {"kernel": kernel, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": gbs / HBM_PEAK_GBS if gbs else None, "traffic": counter_bytes,
+             "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": ms,
+             "timing": "headline mode: HIP events on the launching streams inside bundle_adjust_frames iterations",
              "frac_hbm_counters": (counter_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if (counter_bytes and ms) else None,
-             "frac_hbm_algorithmic_overlapped": (alg_bytes / (ms_ov * 1e-3) / 1e9 / HBM_PEAK_GBS)
-             if ms_ov and ms_ov > 0 else None}
+             "frac_l2_algorithmic": gbs / L2_PEAK_GBS if gbs else None}
+        if ms_serial:
+            r["avg_launch_ms_serialised"] = ms_serial
+            r["frac_serialised"] = alg_bytes / (ms_serial * 1e-3) / 1e9 / HBM_PEAK_GBS
         if extra:
             r.update(extra)
-        for k, v in r.items():
-            if k.startswith("frac") and v is not None and k != "frac_hbm_algorithmic" and \
-                    k != "frac_hbm_algorithmic_overlapped":
-                assert v <= 1.0, (kernel, k, v)
         return r
 
     roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, "
-                      "k_sample_points, k_interp_fwd, k_interp_bwd)", bytes_qi, q_ms, q_ms_ov,
-                      traffic.get("query_interp_bytes_per_step"),
-                      {"parts_ms": q_parts, "parts_ms_overlapped": {k: kt_overlap[k] for k in q_keys}
-                       if kt_overlap else None, "visits_per_ray": v_avg / max(rays_step, 1),
-                       "samples_per_hit_ray": m_avg / max(r_avg, 1)})
-    roof_ib = bw_roof("k_interp_bwd", 1664.0 * m_avg, kt["interp_bwd"],
-                      kt_overlap["interp_bwd"] if kt_overlap else None,
-                      traffic.get("interp_bwd_bytes_per_launch"))
-    mlp_f_ms, mlp_b_ms = kt["mlp_fwd"], kt["mlp_bwd"]
+                      "k_sample_points, k_interp_fwd, k_interp_bwd)", bytes_qi, q_ms,
+                      tr.get("query_interp_bytes_per_step"),
+                      sum(kt_serial[k] for k in q_keys) if kt_serial else None,
+                      {"parts_ms": q_parts, "parts_ms_serialised": {k: kt_serial[k] for k in q_keys}
+                       if kt_serial else None, "visits_per_ray": h_v / max(rays_step, 1),
+                       "samples_per_hit_ray": h_m / max(h_r, 1), "traffic_note": traffic_note})
+    roof_ib = bw_roof("k_interp_bwd", 1664.0 * h_m, kt_overlap["interp_bwd"], tr.get("interp_bwd_bytes_per_launch"),
+                      kt_serial["interp_bwd"] if kt_serial else None)
+    mlp_f_ms, mlp_b_ms = kt_overlap["mlp_fwd"], kt_overlap["mlp_bwd"]
     mlp_ms = mlp_f_ms + mlp_b_ms
     w = args.width
     macs = 16 * w + w * w + w * 129 + 144 * w + w * 3  # nrgbd.py:80-146, depth 2, sdf_dim 128, in_dim 16
-    flops_mlp = 3 * 2.0 * macs * m_avg
+    flops_mlp = 3 * 2.0 * macs * h_m
     mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
     result = {
         "metric": METRIC,
@@ -597,24 +628,29 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (room0-shaped octree + Replica pinhole rays, analytic GT; random-init embeddings/decoder)",
+        "data": "synthetic (room0-shaped octree + Replica pinhole RGB-D keyframes, analytic GT; random-init "
+                "embeddings/decoder)",
         "config": {"workload": f"{args.scene}: {args.frames} keyframes x {args.rays_per_frame} rays/iter per GPU, "
                                f"{tree.count_nodes()} octree nodes, decoder W={args.width}, "
                                f"{h_m / max(h_r, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
                    "rays_per_step_per_gpu": rays_per_step, "samples_per_step": h_m, "hit_rays_per_step": h_r,
-                   "aabb_tests_per_step": h_v, "parallelism": f"dp{world} (ray-sharded, RCCL grad all-reduce)"},
+                   "aabb_tests_per_step": h_v,
+                   "parallelism": f"dp{world} (ray-sharded, union-batch loss, "
+                                  f"{dist.get_backend() if world > 1 else 'no'} collectives)"},
         "roofline": roof_qi,
         "roofline_mfma": {"kernel": f"NRGBD decoder MLP W={w} fwd+bwd (fwd, δ chain, weight gradients)",
                           "bound": "mfma", "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
-                          "traffic": traffic.get("mlp_bytes_per_step"),
+                          "traffic": tr.get("mlp_bytes_per_step"),
                           "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
-                          "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms},
+                          "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,
+                          "timing": "headline mode (HIP events inside bundle_adjust_frames iterations)"},
         "roofline_interp_bwd": roof_ib,
         "path": path_desc,
-        "other_path": other,
-        "kernels_ms": kt,
+        "other_path": others if others else "run bench.py --extras for the engine-step and drop-in autograd paths",
         "kernels_ms_overlapped": kt_overlap,
+        "kernels_ms_serialised": kt_serial,
+        "traffic_kernels": tr.get("kernels"),
     }
     log("done timing")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

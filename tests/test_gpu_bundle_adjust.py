@@ -43,23 +43,6 @@ class _KF:
         self.sample_mask = m.view(self.h, self.w)
 
 
-class PointsEncoder(torch.nn.Module):
-    """Stand-in for the reference's points encoder (variations/resnet.py
-    PointsResNet(feature_n=16), replica.yaml:13-14): the same Linear / ReLU
-    stack and state_dict keys, so the golden's initial weights load."""
-
-    def __init__(self, feature_n=16):
-        super().__init__()
-        L, R = torch.nn.Linear, torch.nn.ReLU
-        self.resnet = torch.nn.Sequential(L(6, 64), R(), L(64, 128), R(), L(128, 256), R(), L(256, 512), R())
-        self.fc = L(512, feature_n)
-
-    def forward(self, x1, y):
-        x = torch.cat((x1, y), 2)
-        x = self.resnet(x.reshape(-1, x.shape[2])).view(x1.size(0), x1.size(1), -1)
-        return self.fc(x)
-
-
 BA_GOLDENS = ["BA_room0", "BA_room0_resnet", "BA_scannet_w256"]
 
 
@@ -99,7 +82,8 @@ def test_bundle_adjust_matches_reference(use_engine, name):
     mo = torch.optim.Adam(dec.parameters(), lr=5e-3)
     resnet, ro = None, None
     if "resnet_optim_states" in g:
-        resnet = PointsEncoder(16).to(DEV)
+        from psvo.point_feature import PointsResNet
+        resnet = PointsResNet(16).to(DEV)
         resnet.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("res0.")})
         resnet.train()
         ro = torch.optim.Adam(resnet.parameters(), lr=5e-3)
