@@ -318,7 +318,13 @@ constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF
               kImgB4 = kImgF4 + 18432, kImgB3 = kImgB4 + 20480, kImgB2 = kImgB3 + 16384, kImgB1 = kImgB2 + 16384,
               kImgVec = kImgB1 + 4096,    // the small vectors in their LDS layout (kOffB1..kOffW), padded
               kVecPad = 1280,             // to whole 1-KB glds pieces
-              kImgTotal = kImgVec + kVecPad;  // 111,872 floats
+              // k_mlp_bwd3's chain (v_mfma_f32_16x16x4_f32, 16-sample units): Wᵀ as 16 × 16
+              // blocks (ob, kb), lane (m, q) holding Wᵀ[16ob + m][16kb + 4q .. 4q + 3]
+              kImgC4 = kImgVec + kVecPad,   // W4ᵀ: 9 × 8 blocks (144 rows: f and x)
+              kImgC3 = kImgC4 + 9 * 8 * 256,  // W3[1:]ᵀ
+              kImgC2 = kImgC3 + 8 * 8 * 256,  // W2ᵀ
+              kImgC1 = kImgC2 + 8 * 8 * 256,  // W1ᵀ: 1 × 8 blocks
+              kImgTotal = kImgC1 + 8 * 256;   // 165,120 floats
 
 __device__ __forceinline__ void inv_perm_acc(int pos, int nkb, int &i, int &k) {
     const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
@@ -357,6 +363,15 @@ __global__ __launch_bounds__(256) void k_mlp_prep(MlpParams p, float *__restrict
     if (e >= kImgTotal) return;
     int i, k;
     float v = 0.0f;
+    if (e >= kImgC4) {  // chain16 images: [ob][kb][lane (m, q)][4]
+        const int sec = e < kImgC3 ? 4 : e < kImgC2 ? 3 : e < kImgC1 ? 2 : 1;
+        const int pos = e - (sec == 4 ? kImgC4 : sec == 3 ? kImgC3 : sec == 2 ? kImgC2 : kImgC1);
+        const int j = pos & 3, ln = (pos >> 2) & 63, blk = pos >> 8;
+        const int o = 16 * (blk >> 3) + (ln & 15), in = 16 * (blk & 7) + 4 * (ln >> 4) + j;  // Wᵀ[o][in]
+        img[e] = sec == 4 ? w4[in * 144 + o] : sec == 3 ? w3[(1 + in) * 128 + o] : sec == 2 ? w2[in * 128 + o]
+                                                                                             : p.w1[in * 16 + o];
+        return;
+    }
     if (e >= kImgVec) {
         img[e] = vec_elem(p, e - kImgVec);
         return;
@@ -1499,6 +1514,528 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
     wait_vm(0);
 }
 
+// ---------------------------------------------------------------------------
+// Fused backward: the δ chain AND the weight gradients in one persistent
+// kernel, the δ's handed from the chain to the weight-gradient MFMAs through
+// LDS instead of HBM (k_mlp_bwd2 + k_mlp_dw2 move 2 KB/sample of δ's out and
+// back: ≈ 1.1 GB per step at config B).
+//
+// The chain needs features on the MFMA reduction axis (accumulator = next B
+// operand, lane = sample); a weight gradient Σ_s δ[o][s] a[i][s] needs the
+// samples there (lane = feature).  So every δ crosses lanes once: the chain
+// wave writes its δ tile into LDS and the gradient MFMAs read it back
+// transposed.  The chain runs v_mfma_f32_16x16x4_f32 on 16-sample units
+// (an activation is 8 blocks × 4 registers, a quarter of the 32-sample f32x16
+// form's 64 × ... — the register file has to hold the weight-gradient
+// accumulators too), lane (n, q) holding features 16·ob + 4q + j of sample n
+// (j = register); its weights stream from L2 as MFMA A operands (Wᵀ images
+// kImgC4..kImgC1, every CU reads the same 213 KB).
+//
+// One 8-wave workgroup per CU loops over rounds of four 16-sample units.
+// Waves 0-3 (one per SIMD) run the chain of one unit each and own the
+// gradients whose other operand is x or c1: W1 and the x columns of W4 (row
+// block = wave), W5 (column block = wave); waves 4-7 (one per SIMD) own
+// column block d = wave − 4 of W2, W3 and W4 (4 row blocks each, 192
+// accumulator registers) and the biases of row block d.  A round is four
+// phases separated by one barrier; a phase's exports are read in the next:
+//   phase  chain wave c (unit u0 + 4r + c)                       gradient waves (the round's 4 units)
+//   P0     δ5, δc1, x → LDS; δ[f; x] = W4ᵀ δc1; dW1 += δh1(r−1) ⊗ x
+//   P1     δf, δsdf → LDS; δh2 = (W3ᵀ [δsdf; δf]) ⊙ m2;          dW4 += δc1 ⊗ f
+//          dW4x += δc1 ⊗ x; dW5 += δ5 ⊗ c1
+//   P2     δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1                          dW3 += [δsdf; δf] ⊗ h2
+//   P3     δh1 → LDS; dfeat = W1ᵀ δh1 + δx_c                      dW2 += δh2 ⊗ h1
+// plus a last P0 for the final round's dW1.  Per accumulator the MFMA
+// order is fixed (rounds, units, k-steps in order): deterministic.  Each
+// workgroup writes one slab of every layer; k_mlp_dw_reduce sums them.
+//
+// LDS image of a unit's δ (and of its x): 128 (16) rows × 16 slots, sample
+// n at slot 8(n&1) + n/2 (k-step t of the 32x32x2 gradient MFMA takes
+// samples 2t, 2t+1 — the CF tile's order), the four 16-B chunks of row r
+// XOR-permuted by (r >> 2) & 3: the chain's ds_write_b32 (4 rows × 16
+// slots) are at most 2-way, the gradient waves' ds_read_b128 (32 rows ×
+// one chunk) conflict-free.
+constexpr int kU = 16;                                  // samples per chain unit
+constexpr int kUImg = 128 * kU;                         // a unit's δ image (8 KB)
+constexpr int kB3Slot = kVecPad;                        // δ images [set 2][unit 4]
+constexpr int kB3Small = kB3Slot + 2 * 4 * kUImg;       // per-sample rows [set 2][unit 4][4][16]: δ5 / δsdf
+constexpr int kB3X = kB3Small + 2 * 4 * 4 * kU;         // x images [round parity 2][unit 4][16 × 16]
+constexpr int kLdsBwd3 = (kB3X + 2 * 4 * 16 * kU) * 4;  // 80,896 B
+static_assert(kLdsBwd3 <= 160 * 1024, "bwd3 LDS budget");
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// 16-B buffer load: descriptor in SGPRs, one 32-bit lane offset + a
+// wave-uniform byte offset (no 64-bit per-lane address arithmetic)
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float *p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
+}
+
+// acc[ob] += Wᵀ blocks (ob, kb) of the image at float offset `img_off` · in[kb]
+// (16 × 16 × 4 MFMAs; the A operands stream from L2 through a ring D k-blocks deep)
+template <int NKB, int NOB, int D>
+__device__ __forceinline__ void gemm16(__amdgpu_buffer_rsrc_t rs, int img_off, const f32x4v (&in)[NKB],
+                                       f32x4v (&acc)[NOB], int lane) {
+    auto ld = [&](int kb, int ob) { return bload4(rs, lane * 16, (img_off + (ob * NKB + kb) * 256) * 4); };
+    float4 ring[D + 1][NOB];
+#pragma unroll
+    for (int s = 0; s < D; ++s)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) ring[s][ob] = ld(s, ob);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        const int cs = kb % (D + 1);
+        if (kb + D < NKB) {
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) ring[(kb + D) % (D + 1)][ob] = ld(kb + D, ob);
+        }
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[ob] = mfma16(ring[cs][ob].x, in[kb][0], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[ob] = mfma16(ring[cs][ob].y, in[kb][1], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[ob] = mfma16(ring[cs][ob].z, in[kb][2], acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[ob] = mfma16(ring[cs][ob].w, in[kb][3], acc[ob]);
+        if (kb + D < NKB) __builtin_amdgcn_sched_group_barrier(0x020, NOB, 0);  // the prefetch
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NOB, 0);                // this block's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void zero4(f32x4v (&v)[N]) {
+#pragma unroll
+    for (int b = 0; b < N; ++b) v[b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+}
+
+// ReLU mask of a 128-feature activation: feature 16·ob + 4q + j is bit
+// 8·ob + j of w (the forward's mask word of lane-half q & 1, shifted by 4·(q >> 1))
+__device__ __forceinline__ void mask16(f32x4v (&v)[8], uint64_t w) {
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t keep = 0u - (uint32_t)((w >> (8 * ob + j)) & 1u);
+            v[ob][j] = __uint_as_float(__float_as_uint(v[ob][j]) & keep);
+        }
+}
+
+// a chain wave's activation → its unit image (rows 16·ob + 4q + j; `wb` = the
+// lane's base: 64q + ((chunk ^ q) << 2) + word)
+template <int NOB>
+__device__ __forceinline__ void lds_u_store(float *img, int wb, const f32x4v (&v)[NOB]) {
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) img[wb + 256 * ob + 16 * j] = v[ob][j];
+}
+
+struct BwdIn16 {
+    uint64_t mk[3];  // the forward's mask words of lane-half q & 1
+    float y[3], g[3], gs;
+    float4 x;        // x features 4q .. 4q + 3
+};
+
+__device__ __forceinline__ void load_bwd_in16(const float *__restrict__ rgb_in, const uint64_t *__restrict__ masks,
+                                              const float *__restrict__ g_sdf, const float *__restrict__ g_rgb,
+                                              const float *__restrict__ feat, int64_t s, bool valid, int q,
+                                              BwdIn16 &in) {
+    const int64_t sv = valid ? s : 0;
+    const uint64_t *mk = masks + (sv * 2 + (q & 1)) * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        in.mk[i] = mk[i];
+        in.y[i] = rgb_in[sv * 3 + i];
+        in.g[i] = g_rgb[sv * 3 + i];
+    }
+    in.gs = g_sdf[sv];
+    in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
+}
+
+// chain wave: acc += δ rows [32c, 32c + 32) of the round's unit images ⊗ the
+// units' x images (16 valid columns: lanes ≥ 16 feed zeros); bsum: Σ of the rows
+__device__ __forceinline__ void xgrad16(const float *dset, const float *xset, int c, int64_t ubase, int64_t u1,
+                                        int lane, f32x16 &acc, float *bsum) {
+    const int i = lane & 31, h = lane >> 5;
+    const bool xv = i < 16;
+    int ra[2], rx[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        ra[g] = i * kU + (((2 * h + g) ^ ((i >> 2) & 3)) << 2);
+        rx[g] = (i & 15) * kU + (((2 * h + g) ^ (((i & 15) >> 2) & 3)) << 2);
+    }
+#pragma unroll
+    for (int up = 0; up < 4; ++up) {
+        if (ubase + up >= u1) break;  // wave-uniform
+        const float *dl = dset + up * kUImg + 32 * c * kU;
+        const float *xl = xset + up * 16 * kU;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const float4 a = *reinterpret_cast<const float4 *>(dl + ra[g]);
+            float4 b = *reinterpret_cast<const float4 *>(xl + rx[g]);
+            if (!xv) b = make_float4(0.f, 0.f, 0.f, 0.f);
+            acc = mfma(a.x, b.x, acc);
+            acc = mfma(a.y, b.y, acc);
+            acc = mfma(a.z, b.z, acc);
+            acc = mfma(a.w, b.w, acc);
+            if (bsum) *bsum += (a.x + a.y) + (a.z + a.w);
+        }
+    }
+}
+
+// byte offset within a CF tile of lane (i, h)'s operand: row 32·blk + i,
+// 16-B group h·4 + 2·hf + g (hf: the unit's half of the 32-sample tile).
+// Computed, not selected from a table: a runtime index into a register
+// array sends the array to scratch.
+__device__ __forceinline__ int cf_voff(int blk, int lane, int hf, int g) {
+    const int row = 32 * blk + (lane & 31);
+    return (row * kTileS + ((((lane >> 5) * 4 + 2 * hf + g) ^ ((row >> 1) & 7)) << 2)) * 4;
+}
+
+// chain wave c: dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials
+__device__ __forceinline__ void w5grad16(const float *sset, __amdgpu_buffer_rsrc_t c1m, int c, int64_t ubase,
+                                         int64_t u1, int lane, float (&w5)[3], float (&b5)[3]) {
+    const int h = lane >> 5;
+    float4 cl[4][2];
+#pragma unroll
+    for (int up = 0; up < 4; ++up) {
+        int64_t u = ubase + up;
+        if (u >= u1) u = u1 - 1;  // in range (data unused)
+        const int hf = (int)(u & 1);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) cl[up][g] = bload4(c1m, cf_voff(c, lane, hf, g), (int)((u >> 1) * (kCfTile * 4)));
+    }
+#pragma unroll
+    for (int up = 0; up < 4; ++up) {
+        if (ubase + up >= u1) break;
+        const float *sl = sset + up * 4 * kU + 8 * h;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float4 w = *reinterpret_cast<const float4 *>(sl + ch * kU + 4 * g);
+                const float4 a = cl[up][g];
+                w5[ch] += (a.x * w.x + a.y * w.y) + (a.z * w.z + a.w * w.w);
+                b5[ch] += (w.x + w.y) + (w.z + w.w);
+            }
+    }
+}
+
+// gradient wave, one phase: acc[ob] += δ (the round's unit images, all 4 row
+// blocks) ⊗ the activation's column block d (global CF tiles, two k-groups
+// ahead); bsum += Σ of row block d.  EX = 2 (W3 phase): row0 += δsdf ⊗ h2
+// column block d, b30 += Σ δsdf.
+template <int EX>
+__device__ __forceinline__ void dw_phase16(const float *dset, const float *sset, __amdgpu_buffer_rsrc_t act,
+                                           int64_t ubase, int64_t u1, int d, int lane, f32x16 (&acc)[kNB],
+                                           float &bsum, float &row0, float &b30) {
+    const int i = lane & 31, h = lane >> 5;
+    int ra[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) ra[g] = i * kU + (((2 * h + g) ^ ((i >> 2) & 3)) << 2);
+    auto bsrc = [&](int q) {  // step q = (unit q >> 1, k-group q & 1)
+        int64_t u = ubase + (q >> 1);
+        if (u >= u1) u = u1 - 1;
+        return bload4(act, cf_voff(d, lane, (int)(u & 1), q & 1), (int)((u >> 1) * (kCfTile * 4)));
+    };
+    float4 ring[3];
+    ring[0] = bsrc(0);
+    ring[1] = bsrc(1);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int up = q >> 1, g = q & 1;
+        const float4 b = ring[q % 3];
+        if (q + 2 < 8) ring[(q + 2) % 3] = bsrc(q + 2);
+        if (ubase + up < u1) {  // wave-uniform
+            const float *dl = dset + up * kUImg;
+            float4 a[kNB];
+#pragma unroll
+            for (int ob = 0; ob < kNB; ++ob) a[ob] = *reinterpret_cast<const float4 *>(dl + 32 * ob * kU + ra[g]);
+#pragma unroll
+            for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].x, b.x, acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].y, b.y, acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].z, b.z, acc[ob]);
+#pragma unroll
+            for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].w, b.w, acc[ob]);
+            {  // row block d's sum: its own read (a[d] with a runtime d would put a[] in scratch)
+                const float4 ad = *reinterpret_cast<const float4 *>(dl + 32 * d * kU + ra[g]);
+                bsum += (ad.x + ad.y) + (ad.z + ad.w);
+            }
+            if (EX == 2) {
+                const float4 w = *reinterpret_cast<const float4 *>(sset + up * 4 * kU + 8 * h + 4 * g);
+                row0 += (b.x * w.x + b.y * w.y) + (b.z * w.z + b.w * w.w);
+                b30 += (w.x + w.y) + (w.z + w.w);
+            }
+        }
+    }
+}
+
+struct Bwd3Src {
+    const float *rgb, *g_sdf, *g_rgb, *feat;
+    const uint64_t *masks;
+    const float *act;  // CF [h1 | h2 | f | c1]
+    float *dfeat;
+};
+
+// W = false (frozen decoder: dfeat only, e.g. tracking): all 8 waves run the
+// chain (8 units per round), no exports, no gradients — the same chain
+// arithmetic, so dfeat is bit-identical to the training call's.
+template <bool W>
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const float *__restrict__ img, Bwd3Src src,
+                                                            DwGrid g, float *__restrict__ slabs) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples)
+    const int64_t tstride = n_tiles * kCfTile;
+    const int64_t tb = tstride * 4;
+    const int64_t n_units = (m + kU - 1) / kU;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    constexpr int kPer = W ? 4 : 8;  // units per round
+    const int n_rounds = (int)((u1 - u0 + kPer - 1) / kPer);
+    float *const slot = lds + kB3Slot, *const small = lds + kB3Small, *const xim = lds + kB3X;
+    auto dset = [&](int s) { return slot + s * 4 * kUImg; };
+    auto sset = [&](int s) { return small + s * 4 * 4 * kU; };
+    auto xset = [&](int par) { return xim + par * 4 * 16 * kU; };
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    const int b = blockIdx.x;
+    const int i = lane & 31, h = lane >> 5;
+    const __amdgpu_buffer_rsrc_t c1m = rsrc_of(src.act + 3 * tstride, tb);
+    if (!W || wave < 4) {
+        // ================= chain wave c
+        const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
+        const int c = wave;
+        const int n = lane & 15, q = lane >> 4;
+        const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot
+        const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
+        f32x16 acc1, acc4x;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc1[r] = acc4x[r] = 0.f;
+        float b1p = 0.f, w5[3] = {0.f, 0.f, 0.f}, b5[3] = {0.f, 0.f, 0.f};
+        BwdIn16 nin;
+        {
+            const int64_t u = u0 + c;
+            const int64_t s = u * kU + n;
+            load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, s, u < u1 && s < m, q, nin);
+        }
+        [[maybe_unused]] constexpr int kStampK = 1;
+        PSVO_STAMP_DECL;
+        for (int r = 0; r <= n_rounds; ++r) {
+            PSVO_STAMP(0);
+            const int64_t ubase = u0 + kPer * (int64_t)r;
+            const int64_t u = ubase + c;
+            const bool active = r < n_rounds && u < u1;  // wave-uniform
+            const int64_t s = u * kU + n;
+            const bool valid = active && s < m;
+            // ---- P0: δ5 / δc1 / x → LDS; δ[f; x] = W4ᵀ δc1; dW1 of the previous round
+            f32x4v fa[8], fb[8], dxc[1];
+            float dsdf = 0.f;
+            uint64_t m1 = 0, m2 = 0;
+            if (r < n_rounds) {
+                const BwdIn16 in = nin;
+                float d5[3];
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch)  // roundings spelled out: both instantiations give the same bits
+                    d5[ch] = valid ? __fmul_rn(in.g[ch], __fmul_rn(in.y[ch], __fsub_rn(1.0f, in.y[ch]))) : 0.0f;
+                dsdf = valid ? in.gs : 0.0f;
+                const int sh = 4 * (q >> 1);
+                m1 = valid ? in.mk[0] >> sh : 0;
+                m2 = valid ? in.mk[1] >> sh : 0;
+                const uint64_t m4 = valid ? in.mk[2] >> sh : 0;
+                if (W) {
+                    float *xl = xset(r & 1) + c * 16 * kU;
+                    xl[wb + 0] = valid ? in.x.x : 0.f;
+                    xl[wb + 16] = valid ? in.x.y : 0.f;
+                    xl[wb + 32] = valid ? in.x.z : 0.f;
+                    xl[wb + 48] = valid ? in.x.w : 0.f;
+                }
+                if (W && q == 0) {
+                    float *sl = sset(0) + c * 4 * kU;
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) sl[ch * kU + sn] = d5[ch];
+                }
+                if (active) {
+#pragma unroll
+                    for (int ob = 0; ob < 8; ++ob) {  // δc1 = W5ᵀ δ5 ⊙ mask
+                        const int k = 16 * ob + 4 * q;
+                        const float4 w0 = *reinterpret_cast<const float4 *>(lds + kOffW5 + k);
+                        const float4 w1 = *reinterpret_cast<const float4 *>(lds + kOffW5 + 128 + k);
+                        const float4 w2 = *reinterpret_cast<const float4 *>(lds + kOffW5 + 256 + k);
+                        auto dot3 = [&](float a0, float a1, float a2) {
+                            return fmaf(a2, d5[2], fmaf(a1, d5[1], __fmul_rn(a0, d5[0])));
+                        };
+                        fb[ob] = f32x4v{dot3(w0.x, w1.x, w2.x), dot3(w0.y, w1.y, w2.y), dot3(w0.z, w1.z, w2.z),
+                                        dot3(w0.w, w1.w, w2.w)};
+                    }
+                    mask16(fb, m4);
+                    if (W) lds_u_store<8>(dset(0) + c * kUImg, wb, fb);
+                    zero4(fa);
+                    zero4(dxc);
+                    gemm16<8, 4, 2>(wrs, kImgC4, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);  // δf
+                    gemm16<8, 4, 2>(wrs, kImgC4 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
+                    gemm16<8, 1, 4>(wrs, kImgC4 + 8 * 8 * 256, fb, dxc, lane);  // δx_c
+                }
+            }
+            if (W && r > 0) xgrad16(dset(1), xset((r - 1) & 1), c, ubase - 4, u1, lane, acc1, &b1p);
+            PSVO_STAMP(1);
+            raw_barrier();
+            PSVO_STAMP(2);
+            if (r == n_rounds) break;
+            // ---- P1: δf / δsdf → LDS; δh2 = W3ᵀ [δsdf; δf] ⊙ m2; dW4x, dW5
+            if (W && q == 0) sset(1)[c * 4 * kU + sn] = dsdf;
+            if (active) {
+                if (W) lds_u_store<8>(dset(1) + c * kUImg, wb, fa);
+#pragma unroll
+                for (int ob = 0; ob < 8; ++ob) {
+                    const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
+                    fb[ob] = f32x4v{__fmul_rn(w.x, dsdf), __fmul_rn(w.y, dsdf), __fmul_rn(w.z, dsdf), __fmul_rn(w.w, dsdf)};
+                }
+                gemm16<8, 4, 2>(wrs, kImgC3, fa, *reinterpret_cast<f32x4v(*)[4]>(&fb[0]), lane);
+                gemm16<8, 4, 2>(wrs, kImgC3 + 4 * 8 * 256, fa, *reinterpret_cast<f32x4v(*)[4]>(&fb[4]), lane);
+                mask16(fb, m2);  // δh2
+            }
+            if (W) {
+                xgrad16(dset(0), xset(r & 1), c, ubase, u1, lane, acc4x, nullptr);
+                w5grad16(sset(0), c1m, c, ubase, u1, lane, w5, b5);
+            }
+            PSVO_STAMP(3);
+            raw_barrier();
+            PSVO_STAMP(4);
+            // ---- P2: δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1
+            if (active) {
+                if (W) lds_u_store<8>(dset(0) + c * kUImg, wb, fb);
+                zero4(fa);
+                gemm16<8, 4, 2>(wrs, kImgC2, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);
+                gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
+                mask16(fa, m1);  // δh1
+            }
+            PSVO_STAMP(5);
+            raw_barrier();
+            PSVO_STAMP(6);
+            // ---- P3: δh1 → LDS; dfeat = W1ᵀ δh1 + δx_c; the next unit's inputs
+            if (W && active) lds_u_store<8>(dset(1) + c * kUImg, wb, fa);
+            if (r + 1 < n_rounds) {
+                const int64_t un = u + kPer;
+                const int64_t snx = un * kU + n;
+                load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, snx, un < u1 && snx < m, q, nin);
+            }
+            if (active) {
+                f32x4v t1[1];
+                zero4(t1);
+                gemm16<8, 1, 4>(wrs, kImgC1, fa, t1, lane);
+                if (valid)
+                    *reinterpret_cast<float4 *>(src.dfeat + s * kIn + 4 * q) =
+                        make_float4(__fadd_rn(t1[0][0], dxc[0][0]), __fadd_rn(t1[0][1], dxc[0][1]),
+                                    __fadd_rn(t1[0][2], dxc[0][2]), __fadd_rn(t1[0][3], dxc[0][3]));
+            }
+            PSVO_STAMP(7);
+            raw_barrier();
+            PSVO_STAMP(8);
+            PSVO_STAMP_FLUSH(1);
+        }
+        if (!W) return;
+        // ---- slabs: W1 row block c + b1; W4's x columns of row block c; W5 column block c (+ b5)
+        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
+        float *s4 = slabs + g.slab_off[3] + (int64_t)b * g.slab_len[3];
+        float *s5 = slabs + g.slab_off[4] + (int64_t)b * g.slab_len[4];
+        if (i < 16) {
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int row = 32 * c + phi(rr, h);
+                s1[row * 16 + i] = acc1[rr];
+                s4[row * 144 + 128 + i] = acc4x[rr];
+            }
+        }
+        const float bv = b1p + __shfl_xor(b1p, 32, 64);
+        float v5[3], t5[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            v5[ch] = w5[ch] + __shfl_xor(w5[ch], 32, 64);
+            t5[ch] = b5[ch] + __shfl_xor(b5[ch], 32, 64);  // every lane of a half holds its half's Σ δ5
+        }
+        if (h == 0) {
+            s1[128 * 16 + 32 * c + i] = bv;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) s5[ch * 128 + 32 * c + i] = v5[ch];
+        }
+        if (c == 0 && lane == 0) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) s5[3 * 128 + ch] = t5[ch];
+        }
+    } else {
+        // ================= gradient wave: column block d of W2 / W3 / W4, biases of row block d
+        const int d = wave - 4;
+        f32x16 acc2[kNB], acc3[kNB], acc4[kNB];
+        zero(acc2);
+        zero(acc3);
+        zero(acc4);
+        float b2p = 0.f, b3p = 0.f, b4p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f;
+        const __amdgpu_buffer_rsrc_t h1m = rsrc_of(src.act, tb), h2m = rsrc_of(src.act + tstride, tb),
+                                     fm = rsrc_of(src.act + 2 * tstride, tb);
+        [[maybe_unused]] constexpr int kStampK = 1;
+        PSVO_STAMP_DECL;
+        for (int r = 0; r < n_rounds; ++r) {
+            const int64_t ubase = u0 + 4 * (int64_t)r;
+            PSVO_STAMP(0);
+            PSVO_STAMP(1);
+            raw_barrier();  // P0 done: δc1 in set 0
+            PSVO_STAMP(2);
+            dw_phase16<0>(dset(0), nullptr, fm, ubase, u1, d, lane, acc4, b4p, unused0, unused1);
+            PSVO_STAMP(3);
+            raw_barrier();  // P1 done: δf / δsdf in set 1
+            PSVO_STAMP(4);
+            dw_phase16<2>(dset(1), sset(1), h2m, ubase, u1, d, lane, acc3, b3p, r0, b30);
+            PSVO_STAMP(5);
+            raw_barrier();  // P2 done: δh2 in set 0
+            PSVO_STAMP(6);
+            dw_phase16<0>(dset(0), nullptr, h1m, ubase, u1, d, lane, acc2, b2p, unused0, unused1);
+            PSVO_STAMP(7);
+            raw_barrier();  // P3 done
+            PSVO_STAMP(8);
+            PSVO_STAMP_FLUSH(1);
+        }
+        raw_barrier();  // the chain's last P0
+        const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
+        float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
+        float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
+        float *s4 = slabs + g.slab_off[3] + (int64_t)b * g.slab_len[3];
+        {
+            f32x16 t[kNB][1];
+#pragma unroll
+            for (int k = 0; k < kNB; ++k) t[k][0] = acc2[k];
+            dw_store<kNB, 1>(s2, 128, 0, 128, rb, cb, t, lane);
+#pragma unroll
+            for (int k = 0; k < kNB; ++k) t[k][0] = acc3[k];
+            dw_store<kNB, 1>(s3, 128, 1, 128, rb, cb, t, lane);
+#pragma unroll
+            for (int k = 0; k < kNB; ++k) t[k][0] = acc4[k];
+            dw_store<kNB, 1>(s4, 144, 0, 144, rb, cb, t, lane);
+        }
+        const float v2 = b2p + __shfl_xor(b2p, 32, 64), v3 = b3p + __shfl_xor(b3p, 32, 64),
+                    v4 = b4p + __shfl_xor(b4p, 32, 64), vr0 = r0 + __shfl_xor(r0, 32, 64),
+                    v30 = b30 + __shfl_xor(b30, 32, 64);
+        if (h == 0) {
+            s2[128 * 128 + 32 * d + i] = v2;
+            s3[129 * 128 + 1 + 32 * d + i] = v3;
+            s4[128 * 144 + 32 * d + i] = v4;
+            s3[32 * d + i] = vr0;  // W3 row 0 (sdf)
+        }
+        if (d == 0 && lane == 0) s3[129 * 128] = v30;
+    }
+}
+
 static int device_cus() {
     static int cus = 0;
     if (cus == 0) {
@@ -1666,11 +2203,44 @@ static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
     *slab_floats = off;
 }
 
+// PSVO_MLP_BWD=2: the two-kernel backward (k_mlp_bwd2 δ's through HBM, then
+// k_mlp_dw2) instead of the fused k_mlp_bwd3 (A/B, profiling)
+static bool use_bwd3() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PSVO_MLP_BWD");
+        v = (e && e[0] == '2') ? 0 : 1;
+    }
+    return v == 1 && use_fwd2();
+}
+
+// k_mlp_bwd3: one workgroup per CU (at most one per round of 4 units), each
+// writing a slab of every layer
+static int bwd3_grid(int64_t m) {
+    const int64_t rounds = (m + 4 * kU - 1) / (4 * kU);
+    return (int)(rounds < device_cus() ? (rounds > 0 ? rounds : 1) : device_cus());
+}
+static void dw_grid_uniform(int n, DwGrid *g, int *slab_floats) {
+    int off = 0;
+    for (int l = 0; l < 5; ++l) {
+        g->wg_begin[l] = 0;  // (k_mlp_dw2 only)
+        g->n_split[l] = n;
+        g->slab_off[l] = off;
+        g->slab_len[l] = kDwRows[l] * kDwCols[l] + kDwRows[l];
+        off += n * g->slab_len[l];
+    }
+    *slab_floats = off;
+}
+
 extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split);
 
 extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
+    if (use_bwd3()) {  // per-sample δ5 of the dfeat-only path + the fused kernel's slabs
+        dw_grid_uniform(bwd3_grid(m), &g, &slab);
+        return m * 3 + slab;
+    }
     dw_grid(m, n_split, &g, &slab);
     const int64_t mp = (m + kCh - 1) / kCh * kCh;
     return mp * 4 * 128 + m * 3 + slab;
@@ -1707,6 +2277,59 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     hipStream_t st = as_stream(stream);
     DwGrid g;
     int slab_floats;
+    float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
+    auto reduce = [&](float *slabs) {
+        DwDst d;
+        int e = 0;
+        for (int l = 0; l < 5; ++l) {
+            d.w[l] = gw[l];
+            d.b[l] = gb[l];
+            d.rows[l] = kDwRows[l];
+            d.cols[l] = kDwCols[l];
+            d.elem_begin[l] = e;
+            e += kDwRows[l] * kDwCols[l] + kDwRows[l];
+        }
+        d.elem_begin[5] = e;
+        hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, st, g, slabs, d, accumulate);
+        return check_launch("mlp_dw_reduce");
+    };
+    if (use_bwd3()) {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
+        static bool attr3 = false;
+        if (!attr3) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd3<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd3);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd3<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd3);
+            attr3 = true;
+        }
+        Bwd3Src src{rgb, g_sdf, g_rgb, feat, masks, act, dfeat};
+        if (!want_w) {
+            if (m > 0) {
+                const int64_t rounds = div_up(div_up(m, kU), 8);
+                const int grid = (int)(rounds < device_cus() ? rounds : device_cus());
+                hipLaunchKernelGGL(k_mlp_bwd3<false>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g,
+                                   nullptr);
+                const int rc = check_launch("mlp_bwd3");
+                if (rc) return rc;
+            }
+            if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
+            return PSVO_OK;
+        }
+        const int grid = bwd3_grid(m);
+        dw_grid_uniform(grid, &g, &slab_floats);
+        float *slabs = workspace + m * 3;
+        if (m > 0) {
+            hipLaunchKernelGGL(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs);
+            const int rc = check_launch("mlp_bwd3");
+            if (rc) return rc;
+        } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
+            return set_error(PSVO_E_LAUNCH, "mlp_bwd: memset failed");
+        }
+        if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
+        return reduce(slabs);
+    }
     dw_grid(m, n_split, &g, &slab_floats);
     float *ws = workspace;
     const int64_t mp = (m + kCh - 1) / kCh * kCh;  // CF matrices hold whole 64-sample chunks
@@ -1772,20 +2395,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
-    DwDst d;
-    float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
-    int e = 0;
-    for (int l = 0; l < 5; ++l) {
-        d.w[l] = gw[l];
-        d.b[l] = gb[l];
-        d.rows[l] = kDwRows[l];
-        d.cols[l] = kDwCols[l];
-        d.elem_begin[l] = e;
-        e += kDwRows[l] * kDwCols[l] + kDwRows[l];
-    }
-    d.elem_begin[5] = e;
-    hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, st, g, slabs, d, accumulate);
-    return check_launch("mlp_dw_reduce");
+    return reduce(slabs);
 }
 }  // namespace psvo
 

@@ -1,4 +1,4 @@
-"""Diagnostic: where k_mlp_fwd2 / k_mlp_bwd2 spend a tile (s_memtime stamps of
+"""Diagnostic: where k_mlp_fwd2 / k_mlp_bwd3 spend a tile / round (s_memtime stamps of
 the lib/diag/libpsvo_stamps.so build, `make -C proud-slam_amd/csrc stamps`).
 Read the SHARES of the segments, not the absolute time (the stamps fence the
 code).  Prints per-segment mean cycles over (workgroup, wave, tile)."""
@@ -17,7 +17,7 @@ _lib.LIB_PATH = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_sta
 from psvo.decoder import Decoder  # noqa: E402
 
 FWD = ["L1", "bar1", "L2", "bar2", "L3(+sdf)", "bar3(+stage,x)", "L4", "epilogue"]
-BWD = ["bar1", "W4T", "bar2", "W3T", "bar3", "W2T", "bar4", "W1T+dfeat"]
+B3 = ["P0", "bar0", "P1", "bar1", "P2", "bar2", "P3", "bar3"]
 
 
 def main():
@@ -35,12 +35,10 @@ def main():
     rc = L.psvo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(buf.nbytes))
     assert rc == 0, rc
     n_wg_tiles = (m + 255) // 256
-    for k, names in ((0, FWD), (1, BWD)):
+    for k, names in ((0, FWD),):
         st = buf[k].astype(np.int64)
         npts = len(names) + 1
-        p0 = 0 if k == 0 else 1  # bwd2 has no point 0 (diagnostic-build compiler issue)
-        st = st[..., p0:]
-        rows, spans = [], []
+        rows = []
         for wg in range(256):
             n_it = len(range(wg, n_wg_tiles, 256))
             for w in range(8):
@@ -49,21 +47,34 @@ def main():
                     if v[0] == 0 or v[-1] == 0:
                         continue
                     rows.append(np.diff(v))
-                    spans.append(v[-1] - v[0])
-            # per-WG: first tile start .. last tile end
         d = np.array(rows, dtype=np.float64)
         tot = d.sum(1).mean()
-        print(f"{'fwd2' if k == 0 else 'bwd2'}: {len(rows)} wave-tiles, mean tile {tot:.0f} cycles")
+        print(f"fwd2: {len(rows)} wave-tiles, mean tile {tot:.0f} cycles")
         for i, nm in enumerate(names):
             print(f"   {nm:16s} {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot:5.1f}%)  p90 {np.percentile(d[:, i], 90):9.0f}")
-        # workgroup-level: iterations per WG and the tail
-        first = st[:, :, 0, 0]
-        its = np.array([len(range(wg, n_wg_tiles, 256)) for wg in range(256)])
-        last_end = np.array([st[wg, :, min(its[wg], 8) - 1, npts - 1].max() for wg in range(256)])
-        t0 = first[first > 0].min()
-        print(f"   kernel span (stamps) {(last_end.max() - t0):.0f} cycles; WG end spread "
-              f"{np.percentile(last_end - t0, [0, 50, 90, 100]).round()}; tiles/WG {np.bincount(its)}")
-    dw_report(buf)
+    b3_report(buf, m)
+
+
+def b3_report(buf, m):
+    """k_mlp_bwd3: per round, chain waves (0-3) and gradient waves (4-7) separately."""
+    st = buf[1].astype(np.int64)
+    n_units = (m + 15) // 16
+    for role, waves in (("chain", range(4)), ("grad", range(4, 8))):
+        rows = []
+        for wg in range(256):
+            u0, u1 = n_units * wg // 256, n_units * (wg + 1) // 256
+            n_rounds = (u1 - u0 + 3) // 4
+            for w in waves:
+                for it in range(min(n_rounds, 8)):
+                    v = st[wg, w, it, :9]
+                    if v[0] == 0 or v[8] == 0:
+                        continue
+                    rows.append(np.diff(v))
+        d = np.array(rows, dtype=np.float64)
+        tot = d.sum(1).mean()
+        print(f"bwd3 {role}: {len(rows)} wave-rounds, mean round {tot:.0f} cycles")
+        for i, nm in enumerate(B3):
+            print(f"   {nm:8s} {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot:5.1f}%)  p90 {np.percentile(d[:, i], 90):9.0f}")
 
 
 def dw_report(buf):
