@@ -933,25 +933,43 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         if (!(flags & PSVO_STEP_NO_ADAM)) ENG_CALL(map_adam(st, d, grads, adam_step));
         return PSVO_OK;
     }
+    // width 128: the interpolation backward runs inside the fused decoder
+    // backward (embedding scatter into grad_emb, dL/dx per sample), then only
+    // the per-ray d_o / d_d sums remain; otherwise k_interp_bwd after dfeat
+    const bool fuse_ib = psvo::mlp_bwd_fuses_interp(d->width);
+    const bool emb_dirty = !(e->grads_clean && e->clean_buf == grad_emb);
+    if (fuse_ib && emb_dirty && hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    float *gx = nullptr;
+    if (fuse_ib) {
+        ENG_BUF(float, gxb, kIbWs, (size_t)M * 3 * sizeof(float));
+        gx = gxb;
+    }
+    const psvo::InterpFuse ipf{q.leaf, q.ray_of, q.rank_ray, d->vertex_idx, q.tt, rays_o, rays_d, d->centres, d->emb,
+                               d->voxel_size, grad_emb, gx};
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
     ENG_CALL(mlp_bwd(st, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
-                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr));
+                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
-    // embedding backward: after dfeat (k_mlp_bwd2), beside k_mlp_dw2 / reduce
+    // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
     hipStream_t eb = ax;
     if (overlap && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
-    if (!(e->grads_clean && e->clean_buf == grad_emb) &&
+    if (!fuse_ib && emb_dirty &&
         hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), eb) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     e->grads_clean = false;
     e->clean_buf = grad_emb;
-    ENG_BUF(float, ib_ws, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
     mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
-    ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf, q.tt,
-                                     rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb, grad_od,
-                                     grad_od + R * 3, ib_ws));
+    if (fuse_ib) {
+        ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, q.offsets, q.rank_ray, q.tt, gx, grad_od, grad_od + R * 3));
+    } else {
+        ENG_BUF(float, ib_ws, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
+        ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf,
+                                         q.tt, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb,
+                                         grad_od, grad_od + R * 3, ib_ws));
+    }
     mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");

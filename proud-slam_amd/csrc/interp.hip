@@ -299,7 +299,53 @@ __global__ __launch_bounds__(256) void k_interp_bwd_rays(int64_t r_hit, int c_ma
     else grad_d[row * 3 + k - 3] = v;
 }
 
+// d_o / d_d of each ray from its samples' dL/dx (the fused decoder backward's
+// InterpFuse::gx): one wave per ray, lane l sums samples l, l + 64, ... in
+// order, then a fixed shuffle tree — deterministic
+__global__ __launch_bounds__(256) void k_interp_rays_gx(int64_t r_hit, const int *__restrict__ offsets,
+                                                        const int *__restrict__ ray_index, const float *__restrict__ t,
+                                                        const float *__restrict__ gx, float *__restrict__ grad_o,
+                                                        float *__restrict__ grad_d) {
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int lane = threadIdx.x & 63;
+    const int beg = offsets[r], end = offsets[r + 1];
+    float go[3] = {0.f, 0.f, 0.f}, gd[3] = {0.f, 0.f, 0.f};
+    for (int s = beg + lane; s < end; s += 64) {
+        const float ts = t[s];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = gx[(int64_t)s * 3 + a];
+            go[a] += v;
+            gd[a] += v * ts;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            go[a] += __shfl_xor(go[a], sh, 64);
+            gd[a] += __shfl_xor(gd[a], sh, 64);
+        }
+    if (lane == 0) {
+        const int64_t row = ray_index ? ray_index[r] : r;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            grad_o[row * 3 + a] = go[a];
+            grad_d[row * 3 + a] = gd[a];
+        }
+    }
+}
+
 }  // namespace
+
+int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int *ray_index, const float *t,
+                   const float *gx, float *grad_o, float *grad_d) {
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_interp_rays_gx, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, offsets, ray_index, t, gx,
+                       grad_o, grad_d);
+    return check_launch("interp_rays_gx");
+}
 }  // namespace psvo
 
 using namespace psvo;

@@ -1556,10 +1556,12 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
 // one chunk) conflict-free.
 constexpr int kU = 16;                                  // samples per chain unit
 constexpr int kUImg = 128 * kU;                         // a unit's δ image (8 KB)
-constexpr int kB3Slot = kVecPad;                        // δ images [set 2][unit 4]
-constexpr int kB3Small = kB3Slot + 2 * 4 * kUImg;       // per-sample rows [set 2][unit 4][4][16]: δ5 / δsdf
+constexpr int kB3Slot = kVecPad;                        // δ images [set 3][unit 4]
+constexpr int kB3Small = kB3Slot + 3 * 4 * kUImg;       // per-sample rows [set 2][unit 4][4][16]: δ5 / δsdf
 constexpr int kB3X = kB3Small + 2 * 4 * 4 * kU;         // x images [round parity 2][unit 4][16 × 16]
-constexpr int kLdsBwd3 = (kB3X + 2 * 4 * 16 * kU) * 4;  // 80,896 B
+constexpr int kB3I = kB3X + 2 * 4 * 16 * kU;            // interpolation backward scatter staging [chain wave 4][512]
+constexpr int kB3A = kB3I + 4 * 512;                    // chain accumulators dW1 / dW4x [chain wave 4][2][4][lane 64][4]
+constexpr int kLdsBwd3 = (kB3A + 4 * 2 * 1024) * 4;     // 154,624 B
 static_assert(kLdsBwd3 <= 160 * 1024, "bwd3 LDS budget");
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -1661,10 +1663,23 @@ __device__ __forceinline__ void load_bwd_in16(const float *__restrict__ rgb_in, 
 }
 
 // chain wave: acc += δ rows [32c, 32c + 32) of the round's unit images ⊗ the
-// units' x images (16 valid columns: lanes ≥ 16 feed zeros); bsum: Σ of the rows
+// units' x images (16 valid columns: lanes ≥ 16 feed zeros); bsum: Σ of the
+// rows.  The accumulator lives in LDS between phases (`page`: [4][lane][4]
+// floats, this wave's own): read, accumulated, written back — the same bits
+// as a register-resident accumulator, 16 registers free in the other phases.
 __device__ __forceinline__ void xgrad16(const float *dset, const float *xset, int c, int64_t ubase, int64_t u1,
-                                        int lane, f32x16 &acc, float *bsum) {
+                                        int lane, float *page, float *bsum) {
     const int i = lane & 31, h = lane >> 5;
+    if (ubase >= u1) return;
+    f32x16 acc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4 *>(page + (k * 64 + lane) * 4);
+        acc[4 * k] = v.x;
+        acc[4 * k + 1] = v.y;
+        acc[4 * k + 2] = v.z;
+        acc[4 * k + 3] = v.w;
+    }
     const bool xv = i < 16;
     int ra[2], rx[2];
 #pragma unroll
@@ -1689,6 +1704,10 @@ __device__ __forceinline__ void xgrad16(const float *dset, const float *xset, in
             if (bsum) *bsum += (a.x + a.y) + (a.z + a.w);
         }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<float4 *>(page + (k * 64 + lane) * 4) =
+            make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
 }
 
 // byte offset within a CF tile of lane (i, h)'s operand: row 32·blk + i,
@@ -1700,61 +1719,70 @@ __device__ __forceinline__ int cf_voff(int blk, int lane, int hf, int g) {
     return (row * kTileS + ((((lane >> 5) * 4 + 2 * hf + g) ^ ((row >> 1) & 7)) << 2)) * 4;
 }
 
-// chain wave c: dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials
-__device__ __forceinline__ void w5grad16(const float *sset, __amdgpu_buffer_rsrc_t c1m, int c, int64_t ubase,
-                                         int64_t u1, int lane, float (&w5)[3], float (&b5)[3]) {
+// chain wave c: dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials; the c1
+// operands of two units in flight at a time
+__device__ __forceinline__ void w5_grad(const float *sset, __amdgpu_buffer_rsrc_t c1m, int c, int64_t ubase,
+                                        int64_t u1, int lane, float (&w5)[3], float (&b5)[3]) {
     const int h = lane >> 5;
-    float4 cl[4][2];
 #pragma unroll
-    for (int up = 0; up < 4; ++up) {
-        int64_t u = ubase + up;
-        if (u >= u1) u = u1 - 1;  // in range (data unused)
-        const int hf = (int)(u & 1);
+    for (int pr = 0; pr < 2; ++pr) {
+        float4 cl[2][2];
 #pragma unroll
-        for (int g = 0; g < 2; ++g) cl[up][g] = bload4(c1m, cf_voff(c, lane, hf, g), (int)((u >> 1) * (kCfTile * 4)));
-    }
+        for (int k = 0; k < 2; ++k) {
+            int64_t u = ubase + 2 * pr + k;
+            if (u >= u1) u = u1 - 1;  // in range (data unused)
 #pragma unroll
-    for (int up = 0; up < 4; ++up) {
-        if (ubase + up >= u1) break;
-        const float *sl = sset + up * 4 * kU + 8 * h;
+            for (int g = 0; g < 2; ++g)
+                cl[k][g] = bload4(c1m, cf_voff(c, lane, (int)(u & 1), g), (int)((u >> 1) * (kCfTile * 4)));
+        }
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
+        for (int k = 0; k < 2; ++k) {
+            const int up = 2 * pr + k;
+            if (ubase + up >= u1) break;
+            const float *sl = sset + up * 4 * kU + 8 * h;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const float4 w = *reinterpret_cast<const float4 *>(sl + ch * kU + 4 * g);
-                const float4 a = cl[up][g];
-                w5[ch] += (a.x * w.x + a.y * w.y) + (a.z * w.z + a.w * w.w);
-                b5[ch] += (w.x + w.y) + (w.z + w.w);
-            }
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float4 w = *reinterpret_cast<const float4 *>(sl + ch * kU + 4 * g);
+                    const float4 a = cl[k][g];
+                    w5[ch] += (a.x * w.x + a.y * w.y) + (a.z * w.z + a.w * w.w);
+                    b5[ch] += (w.x + w.y) + (w.z + w.w);
+                }
+        }
     }
 }
 
-// gradient wave, one phase: acc[ob] += δ (the round's unit images, all 4 row
-// blocks) ⊗ the activation's column block d (global CF tiles, two k-groups
-// ahead); bsum += Σ of row block d.  EX = 2 (W3 phase): row0 += δsdf ⊗ h2
-// column block d, b30 += Σ δsdf.
-template <int EX>
-__device__ __forceinline__ void dw_phase16(const float *dset, const float *sset, __amdgpu_buffer_rsrc_t act,
-                                           int64_t ubase, int64_t u1, int d, int lane, f32x16 (&acc)[kNB],
-                                           float &bsum, float &row0, float &b30) {
+// gradient wave B operand: step q (unit q >> 1, k-group q & 1) of column block d
+__device__ __forceinline__ float4 dw_bsrc(__amdgpu_buffer_rsrc_t act, int64_t ubase, int64_t u1, int d, int lane, int q) {
+    int64_t u = ubase + (q >> 1);
+    if (u >= u1) u = u1 - 1;  // in range (data unused)
+    if (u < 0) u = 0;
+    return bload4(act, cf_voff(d, lane, (int)(u & 1), q & 1), (int)((u >> 1) * (kCfTile * 4)));
+}
+
+// gradient wave, one job (a phase's layer): acc[ob] += δ (the round's unit
+// images, all 4 row blocks) ⊗ the activation's column block d; bsum += Σ of
+// row block d; EX = 2 (W3): row0 += δsdf ⊗ h2, b30 += Σ δsdf.  The B
+// operands run through a 3-slot ring two steps ahead that continues into
+// the next job (its first two loads are issued here, before the barrier):
+// step q of a job with ring offset RO uses slot (RO + q) % 3.
+template <int EX, int RO>
+__device__ __forceinline__ void dw_job(float4 (&ring)[3], const float *dset, const float *sset,
+                                       __amdgpu_buffer_rsrc_t act, int64_t ubase, bool on,
+                                       __amdgpu_buffer_rsrc_t act_n, int64_t ubase_n, bool has_n, int64_t u1, int d,
+                                       int lane, f32x16 (&acc)[kNB], float &bsum, float &row0, float &b30) {
     const int i = lane & 31, h = lane >> 5;
     int ra[2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) ra[g] = i * kU + (((2 * h + g) ^ ((i >> 2) & 3)) << 2);
-    auto bsrc = [&](int q) {  // step q = (unit q >> 1, k-group q & 1)
-        int64_t u = ubase + (q >> 1);
-        if (u >= u1) u = u1 - 1;
-        return bload4(act, cf_voff(d, lane, (int)(u & 1), q & 1), (int)((u >> 1) * (kCfTile * 4)));
-    };
-    float4 ring[3];
-    ring[0] = bsrc(0);
-    ring[1] = bsrc(1);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int up = q >> 1, g = q & 1;
-        const float4 b = ring[q % 3];
-        if (q + 2 < 8) ring[(q + 2) % 3] = bsrc(q + 2);
-        if (ubase + up < u1) {  // wave-uniform
+        const float4 b = ring[(RO + q) % 3];
+        if (q + 2 < 8) ring[(RO + q + 2) % 3] = dw_bsrc(act, ubase, u1, d, lane, q + 2);
+        else if (has_n) ring[(RO + q + 2) % 3] = dw_bsrc(act_n, ubase_n, u1, d, lane, q - 6);
+        if (on && ubase + up < u1) {  // wave-uniform
             const float *dl = dset + up * kUImg;
             float4 a[kNB];
 #pragma unroll
@@ -1780,6 +1808,117 @@ __device__ __forceinline__ void dw_phase16(const float *dset, const float *sset,
     }
 }
 
+// The interpolation backward of one 16-sample unit on its chain wave (see
+// k_mlp_bwd3): lane (n, q) holds sample n's dfeat dims 4q..4q+3 — k_interp_bwd's
+// 4-lanes-per-sample layout, the same arithmetic (roundings spelled out as in
+// interp.hip's contract(off)).  dL/dx goes to ip.gx; the embedding scatter's
+// operands (w [8][16], g [16][16], vid [16][8]) are staged in `stg` for
+// scatter_unit (the same wave, right after).
+__device__ __forceinline__ void interp_bwd_unit(const InterpFuse &ip, float *stg, int64_t m, int64_t s, bool valid,
+                                                int n, int q, float ts, const float (&o)[3], const float (&d)[3],
+                                                const float (&cen)[3], int4 vid0, int4 vid1, const float4 (&ev)[8],
+                                                float4 g) {
+    float p[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float x = __fadd_rn(o[a], __fmul_rn(d[a], ts));
+        p[a] = __fadd_rn(__fdiv_rn(__fsub_rn(x, cen[a]), ip.voxel_size), 0.5f);
+    }
+    const float ax[2] = {__fsub_rn(1.0f, p[0]), p[0]};
+    const float ay[2] = {__fsub_rn(1.0f, p[1]), p[1]};
+    const float az[2] = {__fsub_rn(1.0f, p[2]), p[2]};
+    if (!valid) g = make_float4(0.f, 0.f, 0.f, 0.f);
+    // dL/dx: eg_k = E[vid_k] · g over the sample's 4 lanes (n + 16q)
+    float eg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float4 e = ev[k];
+        float a = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(e.x, g.x), __fmul_rn(e.y, g.y)), __fmul_rn(e.z, g.z)),
+                            __fmul_rn(e.w, g.w));
+        a = __fadd_rn(a, __shfl_xor(a, 16, 64));
+        a = __fadd_rn(a, __shfl_xor(a, 32, 64));
+        eg[k] = a;
+    }
+    if (valid && q == 0) {
+        float dp[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ix = (k >> 2) & 1, iy = (k >> 1) & 1, iz = k & 1;
+            const float sx = ix ? 1.f : -1.f, sy = iy ? 1.f : -1.f, sz = iz ? 1.f : -1.f;
+            dp[0] = __fadd_rn(dp[0], __fmul_rn(__fmul_rn(__fmul_rn(sx, ay[iy]), az[iz]), eg[k]));
+            dp[1] = __fadd_rn(dp[1], __fmul_rn(__fmul_rn(__fmul_rn(sy, ax[ix]), az[iz]), eg[k]));
+            dp[2] = __fadd_rn(dp[2], __fmul_rn(__fmul_rn(__fmul_rn(sz, ax[ix]), ay[iy]), eg[k]));
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) ip.gx[s * 3 + a] = __fdiv_rn(dp[a], ip.voxel_size);
+    }
+    if (ip.grad_emb == nullptr) return;
+    // the scatter's operands: this lane's weights w[2q], w[2q + 1] and vertex rows
+    float *Bw = stg, *Bg = stg + 128;
+    int *Bv = reinterpret_cast<int *>(stg + 384);
+    const int k0 = 2 * q, k1 = 2 * q + 1;
+    const float w0 = __fmul_rn(__fmul_rn(ax[(k0 >> 2) & 1], ay[(k0 >> 1) & 1]), az[k0 & 1]);
+    const float w1 = __fmul_rn(__fmul_rn(ax[(k1 >> 2) & 1], ay[(k1 >> 1) & 1]), az[k1 & 1]);
+    Bg[(4 * q + 0) * 16 + n] = g.x;
+    Bg[(4 * q + 1) * 16 + n] = g.y;
+    Bg[(4 * q + 2) * 16 + n] = g.z;
+    Bg[(4 * q + 3) * 16 + n] = g.w;
+    Bw[k0 * 16 + n] = w0;
+    Bw[k1 * 16 + n] = w1;
+    Bv[n * 8 + k0] = q == 0 ? vid0.x : q == 1 ? vid0.z : q == 2 ? vid1.x : vid1.z;
+    Bv[n * 8 + k1] = q == 0 ? vid0.y : q == 1 ? vid0.w : q == 2 ? vid1.y : vid1.w;
+}
+
+// The embedding scatter of one staged unit (interp_bwd_unit), summed per
+// leaf run first (k_interp_bwd's scheme): lane j owns corners j >> 4 and
+// (j >> 4) + 4 of dim j & 15, so a flush is two atomic instructions each
+// covering four whole 64-B rows.
+// `lf`: this lane's sample leaf (lane n holds sample n's: read with readlane,
+// no memory access on the run loop's critical path)
+__device__ __forceinline__ void scatter_unit(const InterpFuse &ip, const float *stg, int64_t u, int64_t m, int lane,
+                                             int lf_lane) {
+    const float *Bw = stg, *Bg = stg + 128;
+    const int *Bv = reinterpret_cast<const int *>(stg + 384);
+    const int64_t left = m - u * kU;
+    const int n_slots = (int)(left < kU ? left : kU);
+    const int ek0 = lane >> 4, ed = lane & 15;
+    int cur = -1, cv0 = 0, cv1 = 0;
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {  // four slots per LDS read (few live registers)
+        if (4 * c4 >= n_slots) break;
+        const float4 a4 = *reinterpret_cast<const float4 *>(Bw + ek0 * 16 + 4 * c4);
+        const float4 b4 = *reinterpret_cast<const float4 *>(Bw + (ek0 + 4) * 16 + 4 * c4);
+        const float4 g4 = *reinterpret_cast<const float4 *>(Bg + ed * 16 + 4 * c4);
+        const float wa[4] = {a4.x, a4.y, a4.z, a4.w}, wb[4] = {b4.x, b4.y, b4.z, b4.w},
+                    gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int sl = 4 * c4 + j;
+            if (sl < n_slots) {
+                const int lf = __builtin_amdgcn_readlane(lf_lane, sl);
+                if (lf != cur) {
+                    if (cur >= 0) {
+                        atomicAdd(ip.grad_emb + (int64_t)cv0 * 16 + ed, acc0);
+                        atomicAdd(ip.grad_emb + (int64_t)cv1 * 16 + ed, acc1);
+                    }
+                    cur = lf;
+                    cv0 = Bv[sl * 8 + ek0];
+                    cv1 = Bv[sl * 8 + ek0 + 4];
+                    acc0 = 0.f;
+                    acc1 = 0.f;
+                }
+                acc0 = __fadd_rn(acc0, __fmul_rn(wa[j], gv[j]));
+                acc1 = __fadd_rn(acc1, __fmul_rn(wb[j], gv[j]));
+            }
+        }
+    }
+    if (cur >= 0) {
+        atomicAdd(ip.grad_emb + (int64_t)cv0 * 16 + ed, acc0);
+        atomicAdd(ip.grad_emb + (int64_t)cv1 * 16 + ed, acc1);
+    }
+}
+
 struct Bwd3Src {
     const float *rgb, *g_sdf, *g_rgb, *feat;
     const uint64_t *masks;
@@ -1790,9 +1929,17 @@ struct Bwd3Src {
 // W = false (frozen decoder: dfeat only, e.g. tracking): all 8 waves run the
 // chain (8 units per round), no exports, no gradients — the same chain
 // arithmetic, so dfeat is bit-identical to the training call's.
+//
+// With ip.gx set (W only; the mapping engine) the chain wave also runs the
+// interpolation backward of its unit in P3, right after dfeat (which is then
+// not stored): the samples' leaf / ray / vertex rows load during P2, the 8
+// embedding rows at the start of P3 (beside the W1ᵀ GEMM), then dL/dx per
+// sample (ip.gx, summed per ray by k_interp_rays_gx) and the embedding
+// scatter, summed over each leaf run of the unit first (k_interp_bwd's
+// scheme: lanes own (corner, dim), whole 64-B rows per atomic instruction).
 template <bool W>
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const float *__restrict__ img, Bwd3Src src,
-                                                            DwGrid g, float *__restrict__ slabs) {
+                                                            DwGrid g, float *__restrict__ slabs, InterpFuse ip) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1805,6 +1952,9 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
     const int n_rounds = (int)((u1 - u0 + kPer - 1) / kPer);
     float *const slot = lds + kB3Slot, *const small = lds + kB3Small, *const xim = lds + kB3X;
     auto dset = [&](int s) { return slot + s * 4 * kUImg; };
+    // the chain's 4 exports per round rotate over 3 sets: export e = 4r + phase → set e mod 3,
+    // so an export stays readable for two phases (dW2 runs in the next round's P0)
+    auto eset = [&](int e) { return dset(((e % 3) + 3) % 3); };
     auto sset = [&](int s) { return small + s * 4 * 4 * kU; };
     auto xset = [&](int par) { return xim + par * 4 * 16 * kU; };
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
@@ -1820,9 +1970,12 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         const int n = lane & 15, q = lane >> 4;
         const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot
         const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
-        f32x16 acc1, acc4x;
+        float *const page1 = lds + kB3A + c * 2048, *const page4x = page1 + 1024;  // dW1, dW4x accumulators
+        if (W) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[r] = acc4x[r] = 0.f;
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         float b1p = 0.f, w5[3] = {0.f, 0.f, 0.f}, b5[3] = {0.f, 0.f, 0.f};
         BwdIn16 nin;
         {
@@ -1880,7 +2033,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                                         dot3(w0.w, w1.w, w2.w)};
                     }
                     mask16(fb, m4);
-                    if (W) lds_u_store<8>(dset(0) + c * kUImg, wb, fb);
+                    if (W) lds_u_store<8>(eset(4 * r) + c * kUImg, wb, fb);
                     zero4(fa);
                     zero4(dxc);
                     gemm16<8, 4, 2>(wrs, kImgC4, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);  // δf
@@ -1888,7 +2041,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                     gemm16<8, 1, 4>(wrs, kImgC4 + 8 * 8 * 256, fb, dxc, lane);  // δx_c
                 }
             }
-            if (W && r > 0) xgrad16(dset(1), xset((r - 1) & 1), c, ubase - 4, u1, lane, acc1, &b1p);
+            if (W && r > 0) xgrad16(eset(4 * r - 1), xset((r - 1) & 1), c, ubase - 4, u1, lane, page1, &b1p);
             PSVO_STAMP(1);
             raw_barrier();
             PSVO_STAMP(2);
@@ -1896,7 +2049,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             // ---- P1: δf / δsdf → LDS; δh2 = W3ᵀ [δsdf; δf] ⊙ m2; dW4x, dW5
             if (W && q == 0) sset(1)[c * 4 * kU + sn] = dsdf;
             if (active) {
-                if (W) lds_u_store<8>(dset(1) + c * kUImg, wb, fa);
+                if (W) lds_u_store<8>(eset(4 * r + 1) + c * kUImg, wb, fa);
 #pragma unroll
                 for (int ob = 0; ob < 8; ++ob) {
                     const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
@@ -1907,25 +2060,58 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                 mask16(fb, m2);  // δh2
             }
             if (W) {
-                xgrad16(dset(0), xset(r & 1), c, ubase, u1, lane, acc4x, nullptr);
-                w5grad16(sset(0), c1m, c, ubase, u1, lane, w5, b5);
+                xgrad16(eset(4 * r), xset(r & 1), c, ubase, u1, lane, page4x, nullptr);
+                w5_grad(sset(0), c1m, c, ubase, u1, lane, w5, b5);
+            }
+            // the interpolation backward's sample data, one dependent level per phase
+            const bool fuse = W && ip.gx != nullptr;  // uniform
+            int lf = 0, ro = 0;
+            float ts = 0.f;
+            if (fuse && valid) {
+                lf = ip.leaf[s];
+                ro = ip.ray_of[s];
+                ts = ip.t[s];
             }
             PSVO_STAMP(3);
             raw_barrier();
             PSVO_STAMP(4);
-            // ---- P2: δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1
+            // ---- P2: δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1 (+ the interpolation backward's sample data)
+            int4 vid0 = make_int4(0, 0, 0, 0), vid1 = make_int4(0, 0, 0, 0);
+            float cen[3] = {0.f, 0.f, 0.f};
+            int row = 0;
+            if (fuse && valid) {
+                vid0 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8);
+                vid1 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8 + 4);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
+                row = ip.rank_ray[ro];
+            }
             if (active) {
-                if (W) lds_u_store<8>(dset(0) + c * kUImg, wb, fb);
+                if (W) lds_u_store<8>(eset(4 * r + 2) + c * kUImg, wb, fb);
                 zero4(fa);
                 gemm16<8, 4, 2>(wrs, kImgC2, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);
                 gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
                 mask16(fa, m1);  // δh1
             }
+            float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
+            float4 ev[8];
+            if (fuse) {  // the 8 embedding rows (used in P3)
+                const int vid[8] = {vid0.x, vid0.y, vid0.z, vid0.w, vid1.x, vid1.y, vid1.z, vid1.w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) ev[k] = reinterpret_cast<const float4 *>(ip.emb)[(int64_t)vid[k] * 4 + q];
+                if (valid) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        ro3[a] = ip.rays_o[(int64_t)row * 3 + a];
+                        rd3[a] = ip.rays_d[(int64_t)row * 3 + a];
+                    }
+                }
+            }
             PSVO_STAMP(5);
             raw_barrier();
             PSVO_STAMP(6);
             // ---- P3: δh1 → LDS; dfeat = W1ᵀ δh1 + δx_c; the next unit's inputs
-            if (W && active) lds_u_store<8>(dset(1) + c * kUImg, wb, fa);
+            if (W && active) lds_u_store<8>(eset(4 * r + 3) + c * kUImg, wb, fa);
             if (r + 1 < n_rounds) {
                 const int64_t un = u + kPer;
                 const int64_t snx = un * kU + n;
@@ -1935,10 +2121,20 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                 f32x4v t1[1];
                 zero4(t1);
                 gemm16<8, 1, 4>(wrs, kImgC1, fa, t1, lane);
-                if (valid)
-                    *reinterpret_cast<float4 *>(src.dfeat + s * kIn + 4 * q) =
-                        make_float4(__fadd_rn(t1[0][0], dxc[0][0]), __fadd_rn(t1[0][1], dxc[0][1]),
-                                    __fadd_rn(t1[0][2], dxc[0][2]), __fadd_rn(t1[0][3], dxc[0][3]));
+                const float4 gf = make_float4(__fadd_rn(t1[0][0], dxc[0][0]), __fadd_rn(t1[0][1], dxc[0][1]),
+                                              __fadd_rn(t1[0][2], dxc[0][2]), __fadd_rn(t1[0][3], dxc[0][3]));
+                if (!fuse) {
+                    if (valid) *reinterpret_cast<float4 *>(src.dfeat + s * kIn + 4 * q) = gf;
+                } else {
+                    interp_bwd_unit(ip, lds + kB3I + c * 512, m, s, valid, n, q, ts, ro3, rd3, cen, vid0, vid1, ev,
+                                    gf);
+                    if (ip.grad_emb != nullptr) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging is this wave's own
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        scatter_unit(ip, lds + kB3I + c * 512, u, m, lane, lf);
+                    }
+                }
             }
             PSVO_STAMP(7);
             raw_barrier();
@@ -1954,8 +2150,9 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
 #pragma unroll
             for (int rr = 0; rr < 16; ++rr) {
                 const int row = 32 * c + phi(rr, h);
-                s1[row * 16 + i] = acc1[rr];
-                s4[row * 144 + 128 + i] = acc4x[rr];
+                const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
+                s1[row * 16 + i] = page1[pos];
+                s4[row * 144 + 128 + i] = page4x[pos];
             }
         }
         const float bv = b1p + __shfl_xor(b1p, 32, 64);
@@ -1986,27 +2183,38 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                                      fm = rsrc_of(src.act + 2 * tstride, tb);
         [[maybe_unused]] constexpr int kStampK = 1;
         PSVO_STAMP_DECL;
-        for (int r = 0; r < n_rounds; ++r) {
+        float4 ring[3];  // B operands, continuous across the jobs (see dw_job)
+        ring[0] = dw_bsrc(h1m, u0 - 4, u1, d, lane, 0);
+        ring[1] = dw_bsrc(h1m, u0 - 4, u1, d, lane, 1);
+        for (int r = 0; r <= n_rounds; ++r) {
             const int64_t ubase = u0 + 4 * (int64_t)r;
             PSVO_STAMP(0);
+            // P0: dW2 of the previous round (δh2: its export 2), beside the chain's W4ᵀ
+            dw_job<0, 0>(ring, eset(4 * r - 2), nullptr, h1m, ubase - 4, r > 0, fm, ubase, r < n_rounds, u1, d,
+                         lane, acc2, b2p, unused0, unused1);
+
             PSVO_STAMP(1);
-            raw_barrier();  // P0 done: δc1 in set 0
+            raw_barrier();
             PSVO_STAMP(2);
-            dw_phase16<0>(dset(0), nullptr, fm, ubase, u1, d, lane, acc4, b4p, unused0, unused1);
+            if (r == n_rounds) break;
+            // P1: dW4 (δc1: export 0)
+            dw_job<0, 2>(ring, eset(4 * r), nullptr, fm, ubase, true, h2m, ubase, true, u1, d, lane, acc4, b4p,
+                         unused0, unused1);
             PSVO_STAMP(3);
-            raw_barrier();  // P1 done: δf / δsdf in set 1
+            raw_barrier();
             PSVO_STAMP(4);
-            dw_phase16<2>(dset(1), sset(1), h2m, ubase, u1, d, lane, acc3, b3p, r0, b30);
+            // P2: dW3 (δf, δsdf: export 1)
+            dw_job<2, 1>(ring, eset(4 * r + 1), sset(1), h2m, ubase, true, h1m, ubase, true, u1, d, lane, acc3, b3p,
+                         r0, b30);
             PSVO_STAMP(5);
-            raw_barrier();  // P2 done: δh2 in set 0
+            raw_barrier();
             PSVO_STAMP(6);
-            dw_phase16<0>(dset(0), nullptr, h1m, ubase, u1, d, lane, acc2, b2p, unused0, unused1);
+            // P3: (the chain's W1ᵀ)
             PSVO_STAMP(7);
-            raw_barrier();  // P3 done
+            raw_barrier();
             PSVO_STAMP(8);
             PSVO_STAMP_FLUSH(1);
         }
-        raw_barrier();  // the chain's last P0
         const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
         float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
         float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
@@ -2260,7 +2468,9 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
-            float *workspace, hipEvent_t dfeat_ready) {
+            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip) {
+    PSVO_REQUIRE(ip == nullptr || (width == kW && use_bwd3() && gw1 != nullptr),
+                 "mlp_bwd: the fused interpolation backward needs the width-128 fused weight-gradient path");
     if (width == 256) {
         PSVO_REQUIRE(m >= 0, "mlp_bwd: bad sizes");
         PSVO_REQUIRE(images != nullptr && masks != nullptr, "mlp_bwd: images / masks of the training forward required");
@@ -2308,7 +2518,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
                 const int64_t rounds = div_up(div_up(m, kU), 8);
                 const int grid = (int)(rounds < device_cus() ? rounds : device_cus());
                 hipLaunchKernelGGL(k_mlp_bwd3<false>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g,
-                                   nullptr);
+                                   nullptr, InterpFuse{});
                 const int rc = check_launch("mlp_bwd3");
                 if (rc) return rc;
             }
@@ -2320,7 +2530,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         dw_grid_uniform(grid, &g, &slab_floats);
         float *slabs = workspace + m * 3;
         if (m > 0) {
-            hipLaunchKernelGGL(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs);
+            hipLaunchKernelGGL(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs,
+                               ip ? *ip : InterpFuse{});
             const int rc = check_launch("mlp_bwd3");
             if (rc) return rc;
         } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
@@ -2397,6 +2608,10 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     if (rc) return rc;
     return reduce(slabs);
 }
+}  // namespace psvo
+
+namespace psvo {
+bool mlp_bwd_fuses_interp(int width) { return width == kW && use_bwd3(); }
 }  // namespace psvo
 
 extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,

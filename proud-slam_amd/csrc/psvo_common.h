@@ -117,14 +117,35 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
+// The interpolation backward (interp.hip's k_interp_bwd: embedding scatter
+// and dL/dx) folded into the width-128 fused decoder backward, per 16-sample
+// unit right after its dfeat: grad_emb (zeroed by the caller) += the
+// trilinear scatter, gx[M][3] = dL/dx of every sample (psvo_interp_rays_gx
+// sums them per ray into d_o / d_d).  Engine only (mlp_bwd `ip`).
+struct InterpFuse {
+    const int *leaf, *ray_of, *rank_ray, *vertex_idx;
+    const float *t, *rays_o, *rays_d, *centres, *emb;
+    float voxel_size;
+    float *grad_emb;
+    float *gx;
+};
+
+// d_o / d_d of every hit ray from the samples' dL/dx (InterpFuse::gx)
+int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int *ray_index, const float *t,
+                   const float *gx, float *grad_o, float *grad_d);
+
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
-// dfeat is written, before the weight-gradient kernels are queued
+// dfeat is written, before the weight-gradient kernels are queued; with `ip`
+// (width 128, fused backward) it also runs the interpolation backward and
+// dfeat is not stored
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
             const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
-            float *workspace, hipEvent_t dfeat_ready);
+            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr);
+// whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
+bool mlp_bwd_fuses_interp(int width);
 
 // the decoder's LDS operand images (k_mlp_prep) on their own, and
 // psvo_mlp_fwd without rebuilding them (the engine prepares them on its aux
