@@ -287,9 +287,9 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
 
 
 CHAIN_KERNELS = ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples", "k_sample_points",
-                 "k_interp_fwd", "k_interp_bwd", "k_interp_bwd_rays")
-MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce", "k_dec256_prep",
-               "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
+                 "k_interp_fwd")
+MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd3", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce",
+               "k_dec256_prep", "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
 
 
 def _short(name):
@@ -343,7 +343,7 @@ def measure_traffic(args, step_size):
         kern[k] = {"fetch": f, "write": w, "total": f + w}
     res = {"kernels": kern,
            "query_interp_bytes_per_step": sum(kern[k]["total"] for k in CHAIN_KERNELS if k in kern),
-           "interp_bwd_bytes_per_launch": kern.get("k_interp_bwd", {}).get("total"),
+           "bwd_fused_bytes_per_launch": (kern.get("k_mlp_bwd3") or kern.get("k_interp_bwd") or {}).get("total"),
            "mlp_bytes_per_step": sum(kern[k]["total"] for k in MLP_KERNELS if k in kern)}
     return res, "measured by this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --probe " \
                 "(headline iterations), median bytes per launch, fetch = 2 x FETCH_SIZE (gfx950)"
@@ -554,16 +554,16 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     # Rooflines.  Primary — the north star's "octree query+interp
-    # kernel": algorithmic bytes per step = per ray 24 B + 48 B per AABB-tested
-    # node (V counted by the kernel) + per valid sample 12 B (sampler output)
-    # + 628 B (interp fwd) + 1,664 B (interp bwd), over the summed durations of
-    # its launches AS THE HEADLINE RUNS THEM (HIP events on their streams
-    # inside bundle_adjust_frames iterations: intersect + stats + hit rank,
-    # sampler + scan, sample compaction, interp fwd, interp bwd).  In the
-    # headline these kernels share the chip with the decoder (the look-ahead
-    # query beside the weight gradients, the embedding backward beside
-    # k_mlp_dw2), so their durations are longer than alone; the one-stream
-    # serialised durations are reported beside it with --extras.  Traffic:
+    # kernel", as the kernels launched for it: algorithmic bytes per step =
+    # per ray 24 B + 48 B per AABB-tested node (V counted by the kernel) + per
+    # valid sample 12 B (sampler output) + 628 B (interp fwd), over the summed
+    # durations of those launches AS THE HEADLINE RUNS THEM (HIP events on
+    # their streams inside bundle_adjust_frames iterations: intersect + stats
+    # + hit rank, sampler + scan, sample compaction, interp fwd).  The
+    # interpolation BACKWARD (1,664 B / sample) runs inside the fused decoder
+    # backward k_mlp_bwd3 (width 128), beside its MFMAs: it has no duration of
+    # its own and is reported with that kernel (roofline_bwd_fused).  The
+    # one-stream serialised durations are reported with --extras.  Traffic:
     # PMC-counted HBM bytes of the same iterations (measure_traffic).
     # Secondary — the decoder (dominant by time), MFMA-bound.
     hs = head_stats
@@ -573,10 +573,11 @@ def main():
         t = torch.tensor([h_m, h_r, h_v], dtype=torch.float64, device=device)
         dist.all_reduce(t)
         h_m, h_r, h_v = (float(x) / world for x in t.cpu())
-    q_keys = ("intersect", "sample", "points", "interp_fwd", "interp_bwd")
+    fused_ib = args.width == 128 and os.environ.get("PSVO_MLP_BWD", "") != "2"  # interp bwd inside k_mlp_bwd3
+    q_keys = ("intersect", "sample", "points", "interp_fwd") + (() if fused_ib else ("interp_bwd",))
     q_parts = {k: kt_overlap[k] for k in q_keys}
     q_ms = sum(q_parts.values())
-    bytes_qi = rays_step * 24.0 + h_v * 48.0 + h_m * 12.0 + h_m * (628.0 + 1664.0)
+    bytes_qi = rays_step * 24.0 + h_v * 48.0 + h_m * 12.0 + h_m * (628.0 + (0.0 if fused_ib else 1664.0))
     traffic, traffic_note = None, "not measured (N > 1 or --no-traffic)"
     if world == 1 and not args.no_traffic:
         log("PMC passes (roofline.traffic)")
@@ -602,20 +603,33 @@ def main():
         return r
 
     roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, "
-                      "k_sample_points, k_interp_fwd, k_interp_bwd)", bytes_qi, q_ms,
+                      "k_sample_points, k_interp_fwd" + (")" if fused_ib else ", k_interp_bwd)"), bytes_qi, q_ms,
                       tr.get("query_interp_bytes_per_step"),
                       sum(kt_serial[k] for k in q_keys) if kt_serial else None,
                       {"parts_ms": q_parts, "parts_ms_serialised": {k: kt_serial[k] for k in q_keys}
                        if kt_serial else None, "visits_per_ray": h_v / max(rays_step, 1),
                        "samples_per_hit_ray": h_m / max(h_r, 1), "traffic_note": traffic_note})
-    roof_ib = bw_roof("k_interp_bwd", 1664.0 * h_m, kt_overlap["interp_bwd"], tr.get("interp_bwd_bytes_per_launch"),
-                      kt_serial["interp_bwd"] if kt_serial else None)
     mlp_f_ms, mlp_b_ms = kt_overlap["mlp_fwd"], kt_overlap["mlp_bwd"]
     mlp_ms = mlp_f_ms + mlp_b_ms
     w = args.width
     macs = 16 * w + w * w + w * 129 + 144 * w + w * 3  # nrgbd.py:80-146, depth 2, sdf_dim 128, in_dim 16
     flops_mlp = 3 * 2.0 * macs * h_m
     mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
+    if fused_ib:  # k_mlp_bwd3: δ chain + weight gradients (2 x 107.5 kFLOP / sample) + the interpolation backward
+        b_tf = 2 * 2.0 * macs * h_m / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
+        ib_gbs = 1664.0 * h_m / (mlp_b_ms * 1e-3) / 1e9 if mlp_b_ms > 0 else None
+        roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
+                             "interpolation backward: embedding scatter + dL/dx)",
+                   "bound": "mfma", "achieved": b_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                   "frac": b_tf / MFMA_F32_PEAK_TFS if b_tf else None,
+                   "traffic": tr.get("bwd_fused_bytes_per_launch"), "avg_launch_ms": mlp_b_ms,
+                   "algorithmic_flops_per_launch": 2 * 2.0 * macs * h_m,
+                   "interp_bwd_algorithmic_bytes": 1664.0 * h_m,
+                   "interp_bwd_bytes_over_kernel_time_frac_hbm": ib_gbs / HBM_PEAK_GBS if ib_gbs else None,
+                   "timing": "headline mode (HIP events inside bundle_adjust_frames iterations)"}
+    else:
+        roof_ib = bw_roof("k_interp_bwd", 1664.0 * h_m, kt_overlap["interp_bwd"],
+                          tr.get("bwd_fused_bytes_per_launch"), kt_serial["interp_bwd"] if kt_serial else None)
     result = {
         "metric": METRIC,
         "value": value,
@@ -645,7 +659,7 @@ def main():
                           "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,
                           "timing": "headline mode (HIP events inside bundle_adjust_frames iterations)"},
-        "roofline_interp_bwd": roof_ib,
+        "roofline_bwd_fused" if fused_ib else "roofline_interp_bwd": roof_ib,
         "path": path_desc,
         "other_path": others if others else "run bench.py --extras for the engine-step and drop-in autograd paths",
         "kernels_ms_overlapped": kt_overlap,
