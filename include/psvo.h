@@ -422,8 +422,17 @@ typedef struct psvo_map_desc {
      * single-GPU step marks its samples' vertex rows and Adam steps only the
      * flagged rows (an untouched row has g = m = v = 0: the dense step leaves
      * it unchanged, so the result is the same).  Initialise from a bound
-     * optimiser state with psvo_adam_flags_from_state.  NULL = dense Adam. */
+     * optimiser state with psvo_adam_flags_from_state.  NULL = dense Adam.
+     * Data parallel: the step does not mark them (every rank must hold the
+     * union of all ranks' rows); the gradient exchange marks the rows it
+     * exchanged (psvo_rows_mark / psvo_rows_flags_from_grad) and
+     * psvo_map_adam steps the flagged rows. */
     uint8_t *emb_row_flags;
+    /* optional u8[n_emb], data parallel only: the rows THIS rank's step
+     * touched (marked by the step, cleared by the exchange,
+     * psvo_rows_compact_flagged / psvo_rows_clear): the row-sparse exchange
+     * finds them without a pass over the gradient table. */
+    uint8_t *emb_row_local;
 } psvo_map_desc;
 
 enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
@@ -469,6 +478,16 @@ int psvo_rows_compact(void *stream, int64_t n_rows, int width, const float *grad
  * are padding and skipped).  Applying every rank's list in rank order gives
  * every rank the same sums, bit for bit. */
 int psvo_rows_scatter_add(void *stream, int64_t n_list, int width, const int *ids, const float *rows, float *grad);
+/* psvo_rows_compact over the rows with flags[r] != 0 (n_rows bytes read, not
+ * the table; a flagged all-zero row is listed too). */
+int psvo_rows_compact_flagged(void *stream, int64_t n_rows, int width, const float *grad, const uint8_t *flags,
+                              int *workspace, int *ids, float *rows, int *count);
+/* grad[ids[i]] = 0 and, if flags, flags[ids[i]] = 0 for i < n_list (ids < 0 skipped). */
+int psvo_rows_clear(void *stream, int64_t n_list, int width, const int *ids, float *grad, uint8_t *flags);
+/* flags[ids[i]] = 1 for i < n_list (ids < 0 skipped). */
+int psvo_rows_mark(void *stream, int64_t n_list, const int *ids, uint8_t *flags);
+/* flags[r] = 1 for every row of grad f32[n_rows, width] with a non-zero element. */
+int psvo_rows_flags_from_grad(void *stream, int64_t n_rows, int width, const float *grad, uint8_t *flags);
 
 psvo_engine *psvo_engine_new(void);
 void psvo_engine_free(psvo_engine *e);

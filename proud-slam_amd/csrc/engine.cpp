@@ -406,7 +406,10 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
 extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
     PSVO_REQUIRE(e && d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
     e->images_next = false;  // the weights may change before the next step
-    ENG_CALL(map_adam(as_stream(stream), d, d->grad_flat, adam_step));
+    // sparse-exact when the row flags exist: a single-GPU step marked its rows
+    // (also under PSVO_STEP_NO_ADAM); data parallel, the gradient exchange
+    // marked the union of all ranks' rows
+    ENG_CALL(map_adam(as_stream(stream), d, d->grad_flat, adam_step, nullptr, d->emb_row_flags != nullptr));
     e->grads_clean = true;
     return PSVO_OK;
 }
@@ -868,6 +871,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // step must still find these rows (their moments are non-zero from now on)
     const bool mark_rows = d->emb_row_flags && !dist;
     const bool sparse_rows = mark_rows && !(flags & PSVO_STEP_NO_ADAM);
+    // data parallel: this rank's rows into emb_row_local (the row-sparse
+    // exchange lists them; the union flags come from what it exchanged)
+    uint8_t *const mark_into = mark_rows ? d->emb_row_flags : (dist ? d->emb_row_local : nullptr);
     if (dist) {
         ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
                                   q.z_vals, crit_ws, sums_c));
@@ -880,7 +886,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     ENG_CALL(fork_join(ax, st, e->coef_ready));
     // after the normalisers: the fused loss pass waits for them, Adam for the marks
-    if (mark_rows) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, d->emb_row_flags));
+    if (mark_into && !empty) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, mark_into));
     if (!empty)
         ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                      q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,

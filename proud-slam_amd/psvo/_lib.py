@@ -54,6 +54,10 @@ _SIGNATURES = {
     "psvo_sample_pixels": (_i32, [_vp, _i32, _i64, _i64, _vp, _i32, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_compact": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "psvo_rows_scatter_add": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "psvo_rows_compact_flagged": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "psvo_rows_clear": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "psvo_rows_mark": (_i32, [_vp, _i64, _vp, _vp]),
+    "psvo_rows_flags_from_grad": (_i32, [_vp, _i64, _i32, _vp, _vp]),
     "psvo_mlp_image_floats": (_i64, []),
     "psvo_mlp_image_floats_w": (_i64, [_i32]),
     "psvo_mlp_act_floats": (_i64, [_i64, _i32]),

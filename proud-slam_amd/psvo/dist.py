@@ -175,6 +175,21 @@ class DeviceRowOps:
         self.L.call("psvo_rows_scatter_add", self.L.stream_of(grad2d.device), ids.shape[0], grad2d.shape[1], ids,
                     rows, grad2d)
 
+    def compact_flagged(self, grad2d, flags, ids, rows, count, workspace):
+        self.L.call("psvo_rows_compact_flagged", self.L.stream_of(grad2d.device), grad2d.shape[0], grad2d.shape[1],
+                    grad2d, flags, workspace, ids, rows, count)
+
+    def clear(self, ids, grad2d, flags):
+        self.L.call("psvo_rows_clear", self.L.stream_of(grad2d.device), ids.shape[0], grad2d.shape[1], ids, grad2d,
+                    flags)
+
+    def mark(self, ids, flags):
+        self.L.call("psvo_rows_mark", self.L.stream_of(flags.device), ids.shape[0], ids, flags)
+
+    def flags_from_grad(self, grad2d, flags):
+        self.L.call("psvo_rows_flags_from_grad", self.L.stream_of(grad2d.device), grad2d.shape[0], grad2d.shape[1],
+                    grad2d, flags)
+
     def workspace_ints(self, n_rows):
         return int(self.L.lib().psvo_rows_workspace_ints(n_rows))
 
@@ -191,7 +206,15 @@ class SparseRowSum:
     (id, row) lists, zero grad2d and scatter-add the lists in rank order — the
     same additions in the same order on every rank, so replicas stay
     bit-identical.  Falls back to a dense all-reduce when the padded lists
-    would move more bytes than the table.  Returns "sparse" or "dense"."""
+    would move more bytes than the table.  Returns "sparse" or "dense".
+
+    With the engine's row flags (sparse-exact Adam under data parallelism):
+    `local` u8[n_rows] = the rows this rank's step touched (its gradient is
+    zero elsewhere) — the rows are found from those flags and the rank's own
+    rows are zeroed before the lists are added back, so no pass touches the
+    dense table; `union` u8[n_rows] (sticky, identical on every rank) gets
+    every exchanged row marked, the set Adam then steps.  `local` is
+    cleared for the next step."""
 
     def __init__(self, n_rows, width, device, group=None, ops=None, force=False):
         self.group = group
@@ -202,28 +225,38 @@ class SparseRowSum:
         self.count = torch.zeros(1, dtype=torch.int32, device=device)
         self.workspace = torch.empty(max(1, self.ops.workspace_ints(n_rows)), dtype=torch.int32, device=device)
 
-    def __call__(self, grad2d):
+    def __call__(self, grad2d, local=None, union=None):
         n_rows, width = grad2d.shape
         ws = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
         if ws == 1 and not self.force:
             return "dense"
-        self.ops.compact(grad2d, self.ids, self.rows, self.count, self.workspace)
+        if local is not None:
+            self.ops.compact_flagged(grad2d, local, self.ids, self.rows, self.count, self.workspace)
+        else:
+            self.ops.compact(grad2d, self.ids, self.rows, self.count, self.workspace)
         stage = torch.device("cpu") if _backend(self.group) == "gloo" else grad2d.device
         cnt = self.count.to(stage, torch.int64)
         counts = [torch.empty_like(cnt) for _ in range(ws)]
         dist.all_gather(counts, cnt, group=self.group)
         counts = [int(c) for c in counts]
         n_max = max(counts)
+        mine = int(counts[dist.get_rank(self.group) if self.group is not None else dist.get_rank()])
         if ws * n_max * (width + 1) >= n_rows * width and not (self.force and ws == 1):
             flat = grad2d if stage == grad2d.device else grad2d.to(stage)
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
             if flat is not grad2d:
                 grad2d.copy_(flat)
+            if union is not None:
+                self.ops.flags_from_grad(grad2d, union)
+            if local is not None:
+                local.zero_()
             return "dense"
         if n_max == 0:  # no rank touched a row: the sum is zero (and gloo rejects empty gathers)
-            grad2d.zero_()
+            if local is not None:
+                self.ops.clear(self.ids[:mine], grad2d, local)
+            else:
+                grad2d.zero_()
             return "sparse"
-        mine = int(counts[dist.get_rank(self.group) if self.group is not None else dist.get_rank()])
         ids = torch.full((n_max,), -1, dtype=torch.int32, device=stage)
         rows = torch.zeros((n_max, width), dtype=torch.float32, device=stage)
         ids[:mine].copy_(self.ids[:mine])
@@ -232,11 +265,17 @@ class SparseRowSum:
         all_rows = [torch.empty_like(rows) for _ in range(ws)]
         dist.all_gather(all_ids, ids, group=self.group)
         dist.all_gather(all_rows, rows, group=self.group)
-        grad2d.zero_()
+        if local is not None:  # the gradient is zero outside this rank's listed rows
+            self.ops.clear(self.ids[:mine], grad2d, local)
+        else:
+            grad2d.zero_()
         for r in range(ws):
             k = counts[r]
             if k:
-                self.ops.scatter_add(all_ids[r][:k].to(grad2d.device), all_rows[r][:k].to(grad2d.device), grad2d)
+                rid = all_ids[r][:k].to(grad2d.device)
+                self.ops.scatter_add(rid, all_rows[r][:k].to(grad2d.device), grad2d)
+                if union is not None:
+                    self.ops.mark(rid, union)
         return "sparse"
 
 
@@ -361,6 +400,7 @@ class EngineGradExchange:
         self.force = bool(force)  # collectives on one rank too (tests)
         self.op = op  # "sum": the engine's union-batch loss (EngineExchange) — gradients add up
         self.n_emb = int(engine.emb.shape[0])
+        self.ops = ops if ops is not None else DeviceRowOps()
         self.sparse = None
         if self.n_emb * 16 * 4 >= sparse_min_bytes:
             self.sparse = SparseRowSum(self.n_emb, 16, engine.grad_flat.device, group=group, ops=ops,
@@ -372,12 +412,17 @@ class EngineGradExchange:
         if ws == 1 and not self.force:
             return
         flat = self.engine.grad_flat
+        n = self.n_emb * 16
+        union, local = self.engine.row_flags, self.engine.row_local  # sparse-exact Adam (engine.set_exchange)
         if self.sparse is None:
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
             self.last_mode = "dense"
+            if union is not None:  # the summed gradient's non-zero rows (a small table: one cheap pass)
+                self.ops.flags_from_grad(flat[:n].view(self.n_emb, 16), union)
+            if local is not None:
+                local.zero_()
         else:
-            n = self.n_emb * 16
-            self.last_mode = self.sparse(flat[:n].view(self.n_emb, 16))
+            self.last_mode = self.sparse(flat[:n].view(self.n_emb, 16), local=local, union=union)
             dist.all_reduce(flat[n:], op=dist.ReduceOp.SUM, group=self.group)
         if self.op == "mean":
             flat.div_(ws)

@@ -28,7 +28,7 @@ class MapDesc(ctypes.Structure):
                 ("voxel_size", _f32), ("step_size", _f32), ("max_distance", _f32), ("truncation", _f32),
                 ("max_depth", _f32), ("w_rgb", _f32), ("w_depth", _f32), ("w_fs", _f32), ("w_sdf", _f32),
                 ("lr_emb", _f64), ("lr_dec", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
-                ("grad_flat", _vp), ("packed", _vp), ("emb_row_flags", _vp)]
+                ("grad_flat", _vp), ("packed", _vp), ("emb_row_flags", _vp), ("emb_row_local", _vp)]
 
 
 class MapFrames(ctypes.Structure):
@@ -93,6 +93,7 @@ class MappingEngine:
         # sparse-exact Adam for the embedding table (include/psvo.h emb_row_flags;
         # PSVO_SPARSE_ADAM=0: dense)
         self.row_flags = None
+        self.row_local = None  # data parallel: this rank's touched rows (set_exchange)
         if os.environ.get("PSVO_SPARSE_ADAM", "1") != "0":
             self.row_flags = torch.zeros(self.emb.shape[0], dtype=torch.uint8, device=self.emb.device)
             d.emb_row_flags = self.row_flags.data_ptr()
@@ -237,6 +238,12 @@ class MappingEngine:
         L.call("psvo_engine_set_exchange", self.handle, exchange.rank, exchange.world, exchange.max_rays_global,
                ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
         self.exchange = exchange
+        if self.row_flags is not None and self.row_local is None:
+            # sparse-exact Adam under data parallelism: the step marks this
+            # rank's rows here, the gradient exchange marks the union into
+            # row_flags (include/psvo.h emb_row_local)
+            self.row_local = torch.zeros_like(self.row_flags)
+            self.desc.emb_row_local = self.row_local.data_ptr()
         from .dist import EngineGradExchange
         # the union-batch loss: rank gradients add up (on the exchange's group; forced one-rank runs too)
         self.grad_exchange = EngineGradExchange(self, op="sum", group=exchange.group,

@@ -53,7 +53,7 @@ class PickFrame(syn.SyntheticFrame):
         self.sample_idx = idx
 
 
-def run(scene, tree, emb0, frames_ids, dev, exchange=None):
+def run(scene, tree, emb0, frames_ids, dev, exchange=None, sparse=False):
     torch.manual_seed(0)
     dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(dev)
     emb = emb0.clone().to(dev).requires_grad_(True)
@@ -67,7 +67,8 @@ def run(scene, tree, emb0, frames_ids, dev, exchange=None):
                         max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
     if exchange is not None:
         eng.set_exchange(exchange)
-        eng.grad_exchange = EngineGradExchange(eng, op="sum")
+        # sparse: the row-sparse embedding exchange (config E's) forced on this small table
+        eng.grad_exchange = EngineGradExchange(eng, op="sum", sparse_min_bytes=0 if sparse else 32 << 20)
     losses = []
     orig = eng.step_frames
 
@@ -82,13 +83,16 @@ def run(scene, tree, emb0, frames_ids, dev, exchange=None):
                             seed_fn=lambda it: 7777 + it)
     torch.cuda.synchronize()
     res = {"loss": losses, "emb": emb.detach().cpu(), "dec": [p.detach().cpu() for p in dec.parameters()],
-           "poses": {f: kf.pose.data.detach().cpu() for f, kf in zip(frames_ids, kfs)}}
+           "poses": {f: kf.pose.data.detach().cpu() for f, kf in zip(frames_ids, kfs)},
+           "modes": [] if eng.grad_exchange is None else [eng.grad_exchange.last_mode],
+           "flags": None if eng.row_flags is None else eng.row_flags.cpu()}
     eng.close()
     return res
 
 
 def main():
     out_dir = sys.argv[1]
+    sparse = len(sys.argv) > 2 and sys.argv[2] == "sparse"
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
@@ -100,10 +104,12 @@ def main():
     emb0 = torch.randn(max(20000, tree.count_nodes()), 16, generator=torch.Generator().manual_seed(5)) * 0.1
     per = N_FRAMES // world
     mine = list(range(rank * per, (rank + 1) * per))
-    res = run(scene, tree, emb0, mine, dev, EngineExchange(N_FRAMES * N_RAYS, device=dev))
+    res = run(scene, tree, emb0, mine, dev, EngineExchange(N_FRAMES * N_RAYS, device=dev), sparse=sparse)
     torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     if rank == 0:
+        if sparse:
+            os.environ["PSVO_SPARSE_ADAM"] = "0"  # the reference: one process, dense Adam on every row
         torch.save(run(scene, tree, emb0, list(range(N_FRAMES)), dev), os.path.join(out_dir, "single.pt"))
     dist.barrier()
     dist.destroy_process_group()

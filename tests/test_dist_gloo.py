@@ -6,6 +6,7 @@ gradients sum to the single-process gradients."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -128,6 +129,24 @@ class _TorchRowOps:
         keep = ids >= 0
         grad2d[ids[keep].long()] += rows[keep]
 
+    def compact_flagged(self, grad2d, flags, ids, rows, count, workspace):
+        nz = (flags != 0).nonzero().flatten()
+        ids[: nz.numel()] = nz.to(torch.int32)
+        rows[: nz.numel()] = grad2d[nz]
+        count[0] = nz.numel()
+
+    def clear(self, ids, grad2d, flags):
+        keep = ids[ids >= 0].long()
+        grad2d[keep] = 0
+        if flags is not None:
+            flags[keep] = 0
+
+    def mark(self, ids, flags):
+        flags[ids[ids >= 0].long()] = 1
+
+    def flags_from_grad(self, grad2d, flags):
+        flags[(grad2d != 0).any(1)] = 1
+
 
 def _sparse_grad(rank, n_rows, touched, seed):
     g = torch.Generator().manual_seed(seed + rank)
@@ -172,3 +191,58 @@ def test_sparse_row_sum_protocol(touched, expect):
         assert mode == expect
         torch.testing.assert_close(grad, want, rtol=1e-6, atol=1e-6)
     assert torch.equal(got[0], got[1]) and torch.equal(got[0], got[2])
+
+
+def _flags_worker(rank, world, port, q, n_rows, touched):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from psvo.dist import SparseRowSum
+        grad = _sparse_grad(rank, n_rows, touched, 11)
+        local = (grad != 0).any(1).to(torch.uint8)
+        local[rank] = 1  # a flagged row whose gradient is zero: listed, harmless
+        union = torch.zeros(n_rows, dtype=torch.uint8)
+        union[500] = 1   # sticky from earlier steps (identical on every rank)
+        mode = SparseRowSum(n_rows, 16, "cpu", ops=_TorchRowOps())(grad, local=local, union=union)
+        q.put((rank, mode, grad.numpy().copy(), local.numpy().copy(), union.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("touched,expect", [(40, "sparse"), (900, "dense")])
+def test_sparse_row_sum_with_row_flags(touched, expect):
+    """Sparse-exact Adam under data parallelism: with the engine's row flags
+    the exchange finds a rank's rows from its `local` flags (no table scan),
+    every rank ends with the summed gradient, the union flags mark every
+    exchanged row (plus the sticky ones) identically on every rank — the set
+    Adam steps — and `local` is cleared for the next step."""
+    n_rows, world = 1000, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flags_worker, args=(r, world, port, q, n_rows, touched)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    grads = [_sparse_grad(r, n_rows, touched, 11) for r in range(world)]
+    want = sum(grads)
+    touched_any = torch.zeros(n_rows, dtype=torch.bool)
+    for g in grads:
+        touched_any |= (g != 0).any(1)
+    for rank, mode, grad, local, union in res:
+        assert mode == expect
+        torch.testing.assert_close(torch.from_numpy(grad), want, rtol=1e-6, atol=1e-6)
+        assert not local.any()
+        u = torch.from_numpy(union).bool()
+        assert bool(u[500]) and bool((u | ~touched_any).all())  # every touched row flagged
+        # nothing beyond the exchanged rows: touched, sticky, or (sparse) a listed zero row
+        extra = u & ~touched_any
+        extra[500] = False
+        if expect == "sparse":
+            extra[:world] = False
+        assert not extra.any()
+    assert all(np.array_equal(res[0][4], r[4]) for r in res) and all(np.array_equal(res[0][2], r[2]) for r in res)

@@ -36,6 +36,40 @@ def test_rows_compact_matches_torch(n_rows, touched):
     assert torch.equal(rows, grad[want])
 
 
+@pytest.mark.parametrize("n_rows,touched", [(1, 1), (1023, 100), (250001, 30000), (70000, 0)])
+def test_rows_flag_kernels_match_torch(n_rows, touched):
+    """The data-parallel sparse-Adam half: compaction from a flag array
+    (listing a flagged all-zero row too), clearing a list's rows and flags,
+    marking a list, flags from a gradient's non-zero rows."""
+    from psvo import _lib as L
+    g = torch.Generator().manual_seed(n_rows + 2 * touched)
+    grad = torch.zeros(n_rows, 16)
+    flags = torch.zeros(n_rows, dtype=torch.uint8)
+    if touched:
+        idx = torch.randperm(n_rows, generator=g)[:touched]
+        grad[idx] = torch.randn(touched, 16, generator=g)
+        flags[idx] = 1
+    flags[0] = 1  # flagged, possibly all-zero
+    grad, flags = grad.to(DEV), flags.to(DEV)
+    ids = torch.full((n_rows,), -7, dtype=torch.int32, device=DEV)
+    rows = torch.empty(n_rows, 16, device=DEV)
+    count = torch.empty(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(max(1, int(L.lib().psvo_rows_workspace_ints(n_rows))), dtype=torch.int32, device=DEV)
+    L.call("psvo_rows_compact_flagged", L.stream_of(DEV), n_rows, 16, grad, flags, ws, ids, rows, count)
+    k = int(count)
+    want = flags.nonzero().flatten()
+    assert torch.equal(ids[:k].long(), want) and torch.equal(rows[:k], grad[want])
+    nzf = torch.zeros(n_rows, dtype=torch.uint8, device=DEV)
+    L.call("psvo_rows_flags_from_grad", L.stream_of(DEV), n_rows, 16, grad, nzf)
+    assert torch.equal(nzf.bool(), (grad != 0).any(1))
+    marks = torch.zeros(n_rows, dtype=torch.uint8, device=DEV)
+    pad = torch.cat([ids[:k], torch.full((3,), -1, dtype=torch.int32, device=DEV)])
+    L.call("psvo_rows_mark", L.stream_of(DEV), pad.shape[0], pad, marks)
+    assert torch.equal(marks, flags)
+    L.call("psvo_rows_clear", L.stream_of(DEV), pad.shape[0], 16, pad, grad, flags)
+    assert not grad.any() and not flags.any()
+
+
 def test_rows_scatter_add_in_rank_order():
     from psvo import _lib as L
     g = torch.Generator().manual_seed(3)
