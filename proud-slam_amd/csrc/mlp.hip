@@ -1525,8 +1525,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
 // samples there (lane = feature).  So every δ crosses lanes once: the chain
 // wave writes its δ tile into LDS and the gradient MFMAs read it back
 // transposed.  The chain runs v_mfma_f32_16x16x4_f32 on 16-sample units
-// (an activation is 8 blocks × 4 registers, a quarter of the 32-sample f32x16
-// form's 64 × ... — the register file has to hold the weight-gradient
+// (an activation is 8 blocks × 4 = 32 registers, half of the 32-sample
+// 32x32x2 form's 64 — the register file has to hold the weight-gradient
 // accumulators too), lane (n, q) holding features 16·ob + 4q + j of sample n
 // (j = register); its weights stream from L2 as MFMA A operands (Wᵀ images
 // kImgC4..kImgC1, every CU reads the same 213 KB).
@@ -1541,9 +1541,9 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
 //   phase  chain wave c (unit u0 + 4r + c)                       gradient waves (the round's 4 units)
 //   P0     δ5, δc1, x → LDS; δ[f; x] = W4ᵀ δc1; dW1 += δh1(r−1) ⊗ x
 //   P1     δf, δsdf → LDS; δh2 = (W3ᵀ [δsdf; δf]) ⊙ m2;          dW4 += δc1 ⊗ f
-//          dW4x += δc1 ⊗ x; dW5 += δ5 ⊗ c1
-//   P2     δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1                          dW3 += [δsdf; δf] ⊗ h2
-//   P3     δh1 → LDS; dfeat = W1ᵀ δh1 + δx_c                      dW2 += δh2 ⊗ h1
+//          dW4x += δc1 ⊗ x
+//   P2     δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ m1; dW5 += δ5 ⊗ c1         dW3 += [δsdf; δf] ⊗ h2
+//   P3     δh1 → LDS; dfeat = W1ᵀ δh1 + δx_c (+ interp bwd)       dW2 += δh2 ⊗ h1
 // plus a last P0 for the final round's dW1.  Per accumulator the MFMA
 // order is fixed (rounds, units, k-steps in order): deterministic.  Each
 // workgroup writes one slab of every layer; k_mlp_dw_reduce sums them.
@@ -1556,12 +1556,12 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const flo
 // one chunk) conflict-free.
 constexpr int kU = 16;                                  // samples per chain unit
 constexpr int kUImg = 128 * kU;                         // a unit's δ image (8 KB)
-constexpr int kB3Slot = kVecPad;                        // δ images [set 3][unit 4]
-constexpr int kB3Small = kB3Slot + 3 * 4 * kUImg;       // per-sample rows [set 2][unit 4][4][16]: δ5 / δsdf
+constexpr int kB3Slot = kVecPad;                        // δ images [set 2][unit 4]
+constexpr int kB3Small = kB3Slot + 2 * 4 * kUImg;       // per-sample rows [set 2][unit 4][4][16]: δ5 / δsdf
 constexpr int kB3X = kB3Small + 2 * 4 * 4 * kU;         // x images [round parity 2][unit 4][16 × 16]
 constexpr int kB3I = kB3X + 2 * 4 * 16 * kU;            // interpolation backward scatter staging [chain wave 4][512]
 constexpr int kB3A = kB3I + 4 * 512;                    // chain accumulators dW1 / dW4x [chain wave 4][2][4][lane 64][4]
-constexpr int kLdsBwd3 = (kB3A + 4 * 2 * 1024) * 4;     // 154,624 B
+constexpr int kLdsBwd3 = (kB3A + 4 * 2 * 1024) * 4;     // 121,856 B
 static_assert(kLdsBwd3 <= 160 * 1024, "bwd3 LDS budget");
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -1719,8 +1719,9 @@ __device__ __forceinline__ int cf_voff(int blk, int lane, int hf, int g) {
     return (row * kTileS + ((((lane >> 5) * 4 + 2 * hf + g) ^ ((row >> 1) & 7)) << 2)) * 4;
 }
 
-// chain wave c: dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials; the c1
-// operands of two units in flight at a time
+// chain wave c (P2): dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials; the
+// c1 operands of two units in flight at a time (loaded in the phase: staging
+// them through LDS one phase ahead measured slower, the copies land in P1)
 __device__ __forceinline__ void w5_grad(const float *sset, __amdgpu_buffer_rsrc_t c1m, int c, int64_t ubase,
                                         int64_t u1, int lane, float (&w5)[3], float (&b5)[3]) {
     const int h = lane >> 5;
@@ -1952,9 +1953,9 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
     const int n_rounds = (int)((u1 - u0 + kPer - 1) / kPer);
     float *const slot = lds + kB3Slot, *const small = lds + kB3Small, *const xim = lds + kB3X;
     auto dset = [&](int s) { return slot + s * 4 * kUImg; };
-    // the chain's 4 exports per round rotate over 3 sets: export e = 4r + phase → set e mod 3,
-    // so an export stays readable for two phases (dW2 runs in the next round's P0)
-    auto eset = [&](int e) { return dset(((e % 3) + 3) % 3); };
+    // the chain's 4 exports per round alternate over 2 sets (export e = 4r + phase → set e mod 2):
+    // each is read in the phase after its write, the next write to its set is a phase later
+    auto eset = [&](int e) { return dset(((e % 2) + 2) % 2); };
     auto sset = [&](int s) { return small + s * 4 * 4 * kU; };
     auto xset = [&](int par) { return xim + par * 4 * 16 * kU; };
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
@@ -1962,7 +1963,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
     raw_barrier();
     const int b = blockIdx.x;
     const int i = lane & 31, h = lane >> 5;
-    const __amdgpu_buffer_rsrc_t c1m = rsrc_of(src.act + 3 * tstride, tb);
     if (!W || wave < 4) {
         // ================= chain wave c
         const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
@@ -2061,7 +2061,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             }
             if (W) {
                 xgrad16(eset(4 * r), xset(r & 1), c, ubase, u1, lane, page4x, nullptr);
-                w5_grad(sset(0), c1m, c, ubase, u1, lane, w5, b5);
             }
             // the interpolation backward's sample data, one dependent level per phase
             const bool fuse = W && ip.gx != nullptr;  // uniform
@@ -2093,6 +2092,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                 gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
                 mask16(fa, m1);  // δh1
             }
+            if (W) w5_grad(sset(0), rsrc_of(src.act + 3 * tstride, tb), c, ubase, u1, lane, w5, b5);
             float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
             float4 ev[8];
             if (fuse) {  // the 8 embedding rows (used in P3)
@@ -2184,32 +2184,31 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         [[maybe_unused]] constexpr int kStampK = 1;
         PSVO_STAMP_DECL;
         float4 ring[3];  // B operands, continuous across the jobs (see dw_job)
-        ring[0] = dw_bsrc(h1m, u0 - 4, u1, d, lane, 0);
-        ring[1] = dw_bsrc(h1m, u0 - 4, u1, d, lane, 1);
+        ring[0] = dw_bsrc(fm, u0, u1, d, lane, 0);
+        ring[1] = dw_bsrc(fm, u0, u1, d, lane, 1);
         for (int r = 0; r <= n_rounds; ++r) {
             const int64_t ubase = u0 + 4 * (int64_t)r;
             PSVO_STAMP(0);
-            // P0: dW2 of the previous round (δh2: its export 2), beside the chain's W4ᵀ
-            dw_job<0, 0>(ring, eset(4 * r - 2), nullptr, h1m, ubase - 4, r > 0, fm, ubase, r < n_rounds, u1, d,
-                         lane, acc2, b2p, unused0, unused1);
-
+            // P0: (the chain's W4ᵀ and dW1)
             PSVO_STAMP(1);
             raw_barrier();
             PSVO_STAMP(2);
             if (r == n_rounds) break;
             // P1: dW4 (δc1: export 0)
-            dw_job<0, 2>(ring, eset(4 * r), nullptr, fm, ubase, true, h2m, ubase, true, u1, d, lane, acc4, b4p,
+            dw_job<0, 0>(ring, eset(4 * r), nullptr, fm, ubase, true, h2m, ubase, true, u1, d, lane, acc4, b4p,
                          unused0, unused1);
             PSVO_STAMP(3);
             raw_barrier();
             PSVO_STAMP(4);
             // P2: dW3 (δf, δsdf: export 1)
-            dw_job<2, 1>(ring, eset(4 * r + 1), sset(1), h2m, ubase, true, h1m, ubase, true, u1, d, lane, acc3, b3p,
+            dw_job<2, 2>(ring, eset(4 * r + 1), sset(1), h2m, ubase, true, h1m, ubase, true, u1, d, lane, acc3, b3p,
                          r0, b30);
             PSVO_STAMP(5);
             raw_barrier();
             PSVO_STAMP(6);
-            // P3: (the chain's W1ᵀ)
+            // P3: dW2 (δh2: export 2), beside the chain's W1ᵀ and interpolation backward
+            dw_job<0, 1>(ring, eset(4 * r + 2), nullptr, h1m, ubase, true, fm, ubase + 4, r + 1 < n_rounds, u1, d,
+                         lane, acc2, b2p, unused0, unused1);
             PSVO_STAMP(7);
             raw_barrier();
             PSVO_STAMP(8);
