@@ -1561,7 +1561,8 @@ constexpr int kB3Small = kB3Slot + 2 * 4 * kUImg;       // per-sample rows [set 
 constexpr int kB3X = kB3Small + 2 * 4 * 4 * kU;         // x images [round parity 2][unit 4][16 × 16]
 constexpr int kB3I = kB3X + 2 * 4 * 16 * kU;            // interpolation backward scatter staging [chain wave 4][512]
 constexpr int kB3A = kB3I + 4 * 512;                    // chain accumulators dW1 / dW4x [chain wave 4][2][4][lane 64][4]
-constexpr int kLdsBwd3 = (kB3A + 4 * 2 * 1024) * 4;     // 121,856 B
+constexpr int kB3W5 = kB3A + 4 * 2 * 1024;              // gradient waves' dW5 / b5 partials [wave 4][lane 64][8]
+constexpr int kLdsBwd3 = (kB3W5 + 4 * 64 * 8) * 4;      // 130,048 B
 static_assert(kLdsBwd3 <= 160 * 1024, "bwd3 LDS budget");
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -1719,26 +1720,27 @@ __device__ __forceinline__ int cf_voff(int blk, int lane, int hf, int g) {
     return (row * kTileS + ((((lane >> 5) * 4 + 2 * hf + g) ^ ((row >> 1) & 7)) << 2)) * 4;
 }
 
-// chain wave c (P2): dW5 column block c += δ5 ⊗ c1 (VALU), b5 partials; the
-// c1 operands of two units in flight at a time (loaded in the phase: staging
-// them through LDS one phase ahead measured slower, the copies land in P1)
+// gradient wave c (P0, the previous round's units): dW5 column block c +=
+// δ5 ⊗ c1 (VALU), b5 partials — in the phase where the gradient waves have
+// no GEMM (on the chain, in P2, it lengthened the chain's longest phase); the
+// c1 operands of two units in flight at a time
 __device__ __forceinline__ void w5_grad(const float *sset, __amdgpu_buffer_rsrc_t c1m, int c, int64_t ubase,
                                         int64_t u1, int lane, float (&w5)[3], float (&b5)[3]) {
     const int h = lane >> 5;
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-        float4 cl[2][2];
+    for (int pr = 0; pr < 4; ++pr) {
+        float4 cl[1][2];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            int64_t u = ubase + 2 * pr + k;
+        for (int k = 0; k < 1; ++k) {
+            int64_t u = ubase + pr + k;
             if (u >= u1) u = u1 - 1;  // in range (data unused)
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 cl[k][g] = bload4(c1m, cf_voff(c, lane, (int)(u & 1), g), (int)((u >> 1) * (kCfTile * 4)));
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int up = 2 * pr + k;
+        for (int k = 0; k < 1; ++k) {
+            const int up = pr + k;
             if (ubase + up >= u1) break;
             const float *sl = sset + up * 4 * kU + 8 * h;
 #pragma unroll
@@ -1976,7 +1978,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             for (int k = 0; k < 8; ++k)
                 *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        float b1p = 0.f, w5[3] = {0.f, 0.f, 0.f}, b5[3] = {0.f, 0.f, 0.f};
+        float b1p = 0.f;
         BwdIn16 nin;
         {
             const int64_t u = u0 + c;
@@ -2014,8 +2016,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                     xl[wb + 32] = valid ? in.x.z : 0.f;
                     xl[wb + 48] = valid ? in.x.w : 0.f;
                 }
-                if (W && q == 0) {
-                    float *sl = sset(0) + c * 4 * kU;
+                if (W && q == 0) {  // δ5: rows 0..2 of the round's small set (read by dW5 a round later)
+                    float *sl = sset(r & 1) + c * 4 * kU;
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) sl[ch * kU + sn] = d5[ch];
                 }
@@ -2047,7 +2049,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             PSVO_STAMP(2);
             if (r == n_rounds) break;
             // ---- P1: δf / δsdf → LDS; δh2 = W3ᵀ [δsdf; δf] ⊙ m2; dW4x, dW5
-            if (W && q == 0) sset(1)[c * 4 * kU + sn] = dsdf;
+            if (W && q == 0) sset(r & 1)[c * 4 * kU + 3 * kU + sn] = dsdf;  // row 3
             if (active) {
                 if (W) lds_u_store<8>(eset(4 * r + 1) + c * kUImg, wb, fa);
 #pragma unroll
@@ -2092,7 +2094,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
                 gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
                 mask16(fa, m1);  // δh1
             }
-            if (W) w5_grad(sset(0), rsrc_of(src.act + 3 * tstride, tb), c, ubase, u1, lane, w5, b5);
             float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
             float4 ev[8];
             if (fuse) {  // the 8 embedding rows (used in P3)
@@ -2145,7 +2146,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         // ---- slabs: W1 row block c + b1; W4's x columns of row block c; W5 column block c (+ b5)
         float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
         float *s4 = slabs + g.slab_off[3] + (int64_t)b * g.slab_len[3];
-        float *s5 = slabs + g.slab_off[4] + (int64_t)b * g.slab_len[4];
         if (i < 16) {
 #pragma unroll
             for (int rr = 0; rr < 16; ++rr) {
@@ -2156,21 +2156,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             }
         }
         const float bv = b1p + __shfl_xor(b1p, 32, 64);
-        float v5[3], t5[3];
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            v5[ch] = w5[ch] + __shfl_xor(w5[ch], 32, 64);
-            t5[ch] = b5[ch] + __shfl_xor(b5[ch], 32, 64);  // every lane of a half holds its half's Σ δ5
-        }
-        if (h == 0) {
-            s1[128 * 16 + 32 * c + i] = bv;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) s5[ch * 128 + 32 * c + i] = v5[ch];
-        }
-        if (c == 0 && lane == 0) {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) s5[3 * 128 + ch] = t5[ch];
-        }
+        if (h == 0) s1[128 * 16 + 32 * c + i] = bv;
     } else {
         // ================= gradient wave: column block d of W2 / W3 / W4, biases of row block d
         const int d = wave - 4;
@@ -2179,6 +2165,11 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         zero(acc3);
         zero(acc4);
         float b2p = 0.f, b3p = 0.f, b4p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f;
+        // dW5 / b5 partials live in LDS between rounds (registers are full with dW2..4)
+        float *const page5 = lds + kB3W5 + d * 512 + lane * 8;
+        *reinterpret_cast<float4 *>(page5) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4 *>(page5 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        const __amdgpu_buffer_rsrc_t c1m = rsrc_of(src.act + 3 * tstride, tb);
         const __amdgpu_buffer_rsrc_t h1m = rsrc_of(src.act, tb), h2m = rsrc_of(src.act + tstride, tb),
                                      fm = rsrc_of(src.act + 2 * tstride, tb);
         [[maybe_unused]] constexpr int kStampK = 1;
@@ -2189,7 +2180,16 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         for (int r = 0; r <= n_rounds; ++r) {
             const int64_t ubase = u0 + 4 * (int64_t)r;
             PSVO_STAMP(0);
-            // P0: (the chain's W4ᵀ and dW1)
+            // P0: dW5 of the previous round (δ5 in its small set), beside the chain's W4ᵀ and dW1
+            if (r > 0) {
+                float w5[3] = {0.f, 0.f, 0.f}, b5[3] = {0.f, 0.f, 0.f};
+                w5_grad(sset((r - 1) & 1), c1m, d, ubase - 4, u1, lane, w5, b5);
+                float4 p0 = *reinterpret_cast<float4 *>(page5), p1 = *reinterpret_cast<float4 *>(page5 + 4);
+                p0.x += w5[0]; p0.y += w5[1]; p0.z += w5[2];
+                p1.x += b5[0]; p1.y += b5[1]; p1.z += b5[2];
+                *reinterpret_cast<float4 *>(page5) = p0;
+                *reinterpret_cast<float4 *>(page5 + 4) = p1;
+            }
             PSVO_STAMP(1);
             raw_barrier();
             PSVO_STAMP(2);
@@ -2201,7 +2201,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             raw_barrier();
             PSVO_STAMP(4);
             // P2: dW3 (δf, δsdf: export 1)
-            dw_job<2, 2>(ring, eset(4 * r + 1), sset(1), h2m, ubase, true, h1m, ubase, true, u1, d, lane, acc3, b3p,
+            dw_job<2, 2>(ring, eset(4 * r + 1), sset(r & 1) + 3 * kU, h2m, ubase, true, h1m, ubase, true, u1, d, lane, acc3, b3p,
                          r0, b30);
             PSVO_STAMP(5);
             raw_barrier();
@@ -2240,6 +2240,24 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             s3[32 * d + i] = vr0;  // W3 row 0 (sdf)
         }
         if (d == 0 && lane == 0) s3[129 * 128] = v30;
+        // W5 column block d (+ b5)
+        float *s5 = slabs + g.slab_off[4] + (int64_t)b * g.slab_len[4];
+        const float4 p0 = *reinterpret_cast<const float4 *>(page5), p1 = *reinterpret_cast<const float4 *>(page5 + 4);
+        const float w5[3] = {p0.x, p0.y, p0.z}, b5[3] = {p1.x, p1.y, p1.z};
+        float v5[3], t5[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            v5[ch] = w5[ch] + __shfl_xor(w5[ch], 32, 64);
+            t5[ch] = b5[ch] + __shfl_xor(b5[ch], 32, 64);  // every lane of a half holds its half's Σ δ5
+        }
+        if (h == 0) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) s5[ch * 128 + 32 * d + i] = v5[ch];
+        }
+        if (d == 0 && lane == 0) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) s5[3 * 128 + ch] = t5[ch];
+        }
     }
 }
 
