@@ -113,6 +113,12 @@ struct psvo_engine {
     hipStream_t lossq = nullptr;
     hipEvent_t dfeat_ready = nullptr, emb_done = nullptr, z_ready = nullptr, coef_ready = nullptr,
                grads_ready = nullptr, prep_fork = nullptr, prep_done = nullptr, loss_done = nullptr;
+    // a look-ahead step's tail split (map_step_impl): the weight-gradient sum,
+    // the optimiser step and the next decoder images on aux, while st runs the
+    // pose step and the next query; every later reader of the weights on st
+    // waits for adam_done first (render, before the interpolation)
+    hipEvent_t adam_done = nullptr;
+    bool adam_pending = false;
     EngineTimer tm;
     // the decoder images a look-ahead step built on st after its Adam step,
     // for the decoder whose W[0] it names; consumed by the next
@@ -174,6 +180,15 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
     if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
 }
 
+// st waits for a split tail's optimiser step (map_step_impl) if one is pending
+int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
+    if (!e->adam_pending) return PSVO_OK;
+    if (hipStreamWaitEvent(st, e->adam_done, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+    e->adam_pending = false;
+    return PSVO_OK;
+}
+
 // The host spins on the landing flag the device writes after the statistics
 // (k_stats_to_host: system-scope release) — it sees them as soon as they
 // land, without the event's completion-signal round trip; the event, recorded
@@ -233,6 +248,12 @@ extern "C" int psvo_engine_queued(psvo_engine *e) { return e ? e->q_count : 0; }
 extern "C" int psvo_map_discard(psvo_engine *e) {
     PSVO_REQUIRE(e, "map_discard: null engine");
     e->images_next = false;
+    // no caller stream to order: the optimiser step of a split tail completes here
+    if (e->adam_pending) {
+        if (hipEventSynchronize(e->adam_done) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_discard: optimiser step failed");
+        e->adam_pending = false;
+    }
     while (e->q_count > 0) {
         QuerySet &q = e->qs[e->q_head];
         // the stream the query was queued on: psvo_map_query's side stream,
@@ -309,7 +330,10 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
     for (auto &q : e->qs) query_set_free(q);
     if (e->side) (void)hipStreamDestroy(e->side);
-    if (e->aux) (void)hipStreamDestroy(e->aux);
+    if (e->aux) {
+        (void)hipStreamSynchronize(e->aux);  // a pending tail split's optimiser step
+        (void)hipStreamDestroy(e->aux);
+    }
     if (e->lossq) (void)hipStreamDestroy(e->lossq);
     if (e->loss_done) (void)hipEventDestroy(e->loss_done);
     if (e->dfeat_ready) (void)hipEventDestroy(e->dfeat_ready);
@@ -319,6 +343,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->grads_ready) (void)hipEventDestroy(e->grads_ready);
     if (e->prep_fork) (void)hipEventDestroy(e->prep_fork);
     if (e->prep_done) (void)hipEventDestroy(e->prep_done);
+    if (e->adam_done) (void)hipEventDestroy(e->adam_done);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
@@ -406,6 +431,7 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
 extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
     PSVO_REQUIRE(e && d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
     e->images_next = false;  // the weights may change before the next step
+    ENG_CALL(join_adam(e, as_stream(stream), "map_adam"));
     // sparse-exact when the row flags exist: a single-GPU step marked its rows
     // (also under PSVO_STEP_NO_ADAM); data parallel, the gradient exchange
     // marked the union of all ranks' rows
@@ -567,12 +593,14 @@ bool engine_overlap(psvo_engine *e) {
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done, &e->loss_done};
+                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
+    // stream-ordering events on one device: no system-scope fence (its L2
+    // write-back, ≈ dirty bytes ÷ 6 TB/s, would sit between the kernels)
     for (hipEvent_t *ev : evs)
-        if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
+        if (hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "engine: event creation failed");
     return PSVO_OK;
 }
@@ -648,7 +676,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
         o.z_recorded = true;
     }
-    // ---- forward: interpolation, decoder, compositing
+    // ---- forward: interpolation, decoder, compositing (after the previous
+    // step's optimiser step when its tail ran on aux)
+    ENG_CALL(join_adam(e, st, who));
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
     mark(e, st, PSVO_TIME_INTERP_FWD, 0);
     ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
@@ -943,6 +973,13 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // backward (embedding scatter into grad_emb, dL/dx per sample), then only
     // the per-ray d_o / d_d sums remain; otherwise k_interp_bwd after dfeat
     const bool fuse_ib = psvo::mlp_bwd_fuses_interp(d->width);
+    // look-ahead with the fused backward (single GPU or the caller's Adam
+    // skipped): the tail splits — st runs the per-ray d_o / d_d sums, the pose
+    // step and the next query right after the decoder backward; aux sums the
+    // weight-gradient slabs, steps the optimiser and builds the next decoder
+    // images beside them (the next step's render waits for adam_done)
+    const bool ahead = fr && fr->next_dirs_cam;
+    const bool split = fuse_ib && overlap && ahead && !(flags & PSVO_STEP_NO_ADAM);
     const bool emb_dirty = !(e->grads_clean && e->clean_buf == grad_emb);
     if (fuse_ib && emb_dirty && hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
@@ -956,11 +993,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
     ENG_CALL(mlp_bwd(st, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
-                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr));
+                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr,
+                     split ? ax : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
-    hipStream_t eb = ax;
-    if (overlap && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
+    hipStream_t eb = split ? st : ax;
+    if (overlap && !split && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     if (!fuse_ib && emb_dirty &&
         hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), eb) != hipSuccess)
@@ -977,9 +1015,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                                          grad_od, grad_od + R * 3, ib_ws));
     }
     mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
-    if (overlap && (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
+    if (overlap && !split &&
+        (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
-    if (join_loss && hipStreamWaitEvent(st, e->loss_done, 0) != hipSuccess)
+    // the loss value's reads of crit_ws before the next step's writes: through
+    // st, or (split) through aux's optimiser step, which the next render waits for
+    if (join_loss && hipStreamWaitEvent(split ? ax : st, e->loss_done, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
     ENG_CALL(guard.release());
@@ -988,7 +1029,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // Adam step right after the embedding backward on its stream, then the
     // next iteration's rays + query there too — beside this step's weight
     // gradients and the map's Adam
-    const bool ahead = fr && fr->next_dirs_cam;
     if (ahead) {
         ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od));
     } else if (fr) {
@@ -997,13 +1037,19 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // ---- optimiser steps, the poses' with the map's (the map's are skipped
     // when the caller all-reduces the gradients first)
     if (!(flags & PSVO_STEP_NO_ADAM)) {
-        ENG_CALL(map_adam(st, d, grads, adam_step, &pa, sparse_rows));
+        hipStream_t os = split ? ax : st;
+        ENG_CALL(map_adam(os, d, grads, adam_step, &pa, sparse_rows));
         e->grads_clean = true;
-        if (ahead) {  // the next iteration's decoder images, on st while it waits for the look-ahead query
+        if (ahead) {  // the next iteration's decoder images, while the look-ahead query runs
             ENG_BUF(float, images, kImages, psvo_mlp_image_floats_w(d->width) * sizeof(float));
-            ENG_CALL(mlp_images(st, d->width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+            ENG_CALL(mlp_images(os, d->width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
             e->images_next = true;
             e->images_w0 = W[0];
+        }
+        if (split) {
+            if (hipEventRecord(e->adam_done, ax) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
+            e->adam_pending = true;
         }
     } else {
         ENG_CALL(pose_adam(st, d, pa));

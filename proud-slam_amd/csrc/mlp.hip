@@ -681,8 +681,14 @@ __device__ __forceinline__ void glds4(const float *g, float *l) {
                  : "memory");
 }
 
+// streaming (nt) store of one float at base[i]: the slabs are read once, by
+// the reduce kernel (a kernel boundary also pays ≈ dirty bytes ÷ 6 TB/s for
+// what stays dirty in L2; measured: nt slab stores 0.99 -> 0.985 ms per BA
+// iteration, write-through (sc1) ones no gain)
+__device__ __forceinline__ void store_nt(float *base, int i, float v) { __builtin_nontemporal_store(v, base + i); }
+
 // write C blocks to the slab (rows offset `row_off` in the layer's matrix)
-template <int NR, int NC>
+template <int NR, int NC, bool NT = false>
 __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int max_col, const int (&rb)[NR],
                                          const int (&cb)[NC], const f32x16 (&acc)[NR][NC], int lane) {
     const int x = lane & 31, h = lane >> 5;
@@ -693,7 +699,13 @@ __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int
             const int col = 32 * cb[j] + x;
             if (col >= max_col) continue;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) slab[(row_off + 32 * rb[i] + phi(r, h)) * cols + col] = acc[i][j][r];
+            for (int r = 0; r < 16; ++r) {
+                if (NT) {
+                    store_nt(slab, (row_off + 32 * rb[i] + phi(r, h)) * cols + col, acc[i][j][r]);
+                } else {
+                    slab[(row_off + 32 * rb[i] + phi(r, h)) * cols + col] = acc[i][j][r];
+                }
+            }
         }
 }
 
@@ -2151,12 +2163,12 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             for (int rr = 0; rr < 16; ++rr) {
                 const int row = 32 * c + phi(rr, h);
                 const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
-                s1[row * 16 + i] = page1[pos];
-                s4[row * 144 + 128 + i] = page4x[pos];
+                store_nt(s1, row * 16 + i, page1[pos]);
+                store_nt(s4, row * 144 + 128 + i, page4x[pos]);
             }
         }
         const float bv = b1p + __shfl_xor(b1p, 32, 64);
-        if (h == 0) s1[128 * 16 + 32 * c + i] = bv;
+        if (h == 0) store_nt(s1, 128 * 16 + 32 * c + i, bv);
     } else {
         // ================= gradient wave: column block d of W2 / W3 / W4, biases of row block d
         const int d = wave - 4;
@@ -2222,24 +2234,24 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             f32x16 t[kNB][1];
 #pragma unroll
             for (int k = 0; k < kNB; ++k) t[k][0] = acc2[k];
-            dw_store<kNB, 1>(s2, 128, 0, 128, rb, cb, t, lane);
+            dw_store<kNB, 1, true>(s2, 128, 0, 128, rb, cb, t, lane);
 #pragma unroll
             for (int k = 0; k < kNB; ++k) t[k][0] = acc3[k];
-            dw_store<kNB, 1>(s3, 128, 1, 128, rb, cb, t, lane);
+            dw_store<kNB, 1, true>(s3, 128, 1, 128, rb, cb, t, lane);
 #pragma unroll
             for (int k = 0; k < kNB; ++k) t[k][0] = acc4[k];
-            dw_store<kNB, 1>(s4, 144, 0, 144, rb, cb, t, lane);
+            dw_store<kNB, 1, true>(s4, 144, 0, 144, rb, cb, t, lane);
         }
         const float v2 = b2p + __shfl_xor(b2p, 32, 64), v3 = b3p + __shfl_xor(b3p, 32, 64),
                     v4 = b4p + __shfl_xor(b4p, 32, 64), vr0 = r0 + __shfl_xor(r0, 32, 64),
                     v30 = b30 + __shfl_xor(b30, 32, 64);
         if (h == 0) {
-            s2[128 * 128 + 32 * d + i] = v2;
-            s3[129 * 128 + 1 + 32 * d + i] = v3;
-            s4[128 * 144 + 32 * d + i] = v4;
-            s3[32 * d + i] = vr0;  // W3 row 0 (sdf)
+            store_nt(s2, 128 * 128 + 32 * d + i, v2);
+            store_nt(s3, 129 * 128 + 1 + 32 * d + i, v3);
+            store_nt(s4, 128 * 144 + 32 * d + i, v4);
+            store_nt(s3, 32 * d + i, vr0);  // W3 row 0 (sdf)
         }
-        if (d == 0 && lane == 0) s3[129 * 128] = v30;
+        if (d == 0 && lane == 0) store_nt(s3, 129 * 128, v30);
         // W5 column block d (+ b5)
         float *s5 = slabs + g.slab_off[4] + (int64_t)b * g.slab_len[4];
         const float4 p0 = *reinterpret_cast<const float4 *>(page5), p1 = *reinterpret_cast<const float4 *>(page5 + 4);
@@ -2252,11 +2264,11 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         }
         if (h == 0) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) s5[ch * 128 + 32 * d + i] = v5[ch];
+            for (int ch = 0; ch < 3; ++ch) store_nt(s5, ch * 128 + 32 * d + i, v5[ch]);
         }
         if (d == 0 && lane == 0) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) s5[3 * 128 + ch] = t5[ch];
+            for (int ch = 0; ch < 3; ++ch) store_nt(s5, 3 * 128 + ch, t5[ch]);
         }
     }
 }
@@ -2485,7 +2497,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
-            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip) {
+            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream) {
     PSVO_REQUIRE(ip == nullptr || (width == kW && use_bwd3() && gw1 != nullptr),
                  "mlp_bwd: the fused interpolation backward needs the width-128 fused weight-gradient path");
     if (width == 256) {
@@ -2505,7 +2517,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     DwGrid g;
     int slab_floats;
     float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
-    auto reduce = [&](float *slabs) {
+    auto reduce = [&](float *slabs, hipStream_t rs) {
         DwDst d;
         int e = 0;
         for (int l = 0; l < 5; ++l) {
@@ -2517,7 +2529,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             e += kDwRows[l] * kDwCols[l] + kDwRows[l];
         }
         d.elem_begin[5] = e;
-        hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, st, g, slabs, d, accumulate);
+        hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate);
         return check_launch("mlp_dw_reduce");
     };
     if (use_bwd3()) {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
@@ -2556,7 +2568,13 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         }
         if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
-        return reduce(slabs);
+        if (reduce_stream && reduce_stream != st) {  // the slab sum beside the caller's next work on st
+            PSVO_REQUIRE(dfeat_ready != nullptr, "mlp_bwd: a separate reduce stream needs the dfeat_ready event");
+            if (hipStreamWaitEvent(reduce_stream, dfeat_ready, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "mlp_bwd: stream wait failed");
+            return reduce(slabs, reduce_stream);
+        }
+        return reduce(slabs, st);
     }
     dw_grid(m, n_split, &g, &slab_floats);
     float *ws = workspace;
@@ -2623,7 +2641,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;
-    return reduce(slabs);
+    return reduce(slabs, st);
 }
 }  // namespace psvo
 

@@ -143,7 +143,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
-            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr);
+            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr,
+            hipStream_t reduce_stream = nullptr);
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
 

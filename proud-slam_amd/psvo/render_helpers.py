@@ -504,12 +504,35 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         return d_all, c_all, z_all, nz, seed
 
     # the next iteration's pixels are drawn before this one's step, so the
-    # engine queues its query beside this step's weight gradients
-    # (psvo_map_frames.next_dirs_cam); injected noise (tests) runs unpipelined
+    # engine queues its query right after this step's backward
+    # (psvo_map_frames.next_dirs_cam); injected noise (tests) runs unpipelined.
+    # Pipelined, the draws run on a stream of their own: they depend on nothing
+    # the steps write, and on the step's stream they would sit between the
+    # look-ahead query and the next render
     ahead = lookahead and not callable(noise)
-    cur = draw(0)
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev) if ahead and num_iterations > 1 else None
+    if side is not None:
+        side.wait_stream(main)  # the keyframes as the caller left them
+
+    def draw_ahead(it):
+        if side is None:
+            return draw(it), None
+        with torch.cuda.stream(side):
+            out = draw(it)
+        for t in out[:3]:
+            t.record_stream(main)  # freed blocks are reused only after the steps that read them
+        ev = torch.cuda.Event()
+        ev.record(side)
+        return out, ev
+
+    cur, cur_ready = draw_ahead(0)
+    if cur_ready is not None:
+        main.wait_event(cur_ready)
     for it in range(num_iterations):
-        nxt = draw(it + 1) if ahead and it + 1 < num_iterations else None
+        nxt, nxt_ready = draw_ahead(it + 1) if ahead and it + 1 < num_iterations else (None, None)
+        if nxt_ready is not None:
+            main.wait_event(nxt_ready)  # the look-ahead's pose step reads its dirs; the next step its colours
         d_all, c_all, z_all, nz, seed = cur
         adam_step += 1
         cur_steps = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
@@ -522,6 +545,8 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             eng.adam()
         pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur_steps)]
         cur = nxt if nxt is not None else (draw(it + 1) if it + 1 < num_iterations else None)
+    if side is not None:
+        main.wait_stream(side)  # frames' sample_mask / sample_idx of the last draw
     # write back: optimiser steps, pose parameters and their Adam state
     with torch.no_grad():
         for st in [st_e] + st_d:

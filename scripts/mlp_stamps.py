@@ -75,6 +75,20 @@ def b3_report(buf, m):
         print(f"bwd3 {role}: {len(rows)} wave-rounds, mean round {tot:.0f} cycles")
         for i, nm in enumerate(B3):
             print(f"   {nm:8s} {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot:5.1f}%)  p90 {np.percentile(d[:, i], 90):9.0f}")
+        if role == "chain":  # sub-phase stamps 9..14 (0 where the code did not run)
+            subs = []
+            for wg in range(256):
+                u0, u1 = n_units * wg // 256, n_units * (wg + 1) // 256
+                for w in waves:
+                    for it in range(min((u1 - u0 + 3) // 4, 8)):
+                        subs.append(st[wg, w, it, :15])
+            sv = np.array(subs, dtype=np.int64)
+            for nm, a, b in (("P0 prep", 0, 9), ("P0 W4T", 9, 10), ("P0 dW1", 10, 1), ("P1 W3T", 2, 11),
+                             ("P1 dW4x", 11, 3), ("P2 W2T", 4, 12), ("P2 loads", 12, 5), ("P3 W1T", 6, 13),
+                             ("P3 interp", 13, 14), ("P3 scatter", 14, 7)):
+                ok = (sv[:, a] > 0) & (sv[:, b] > 0)
+                if ok.any():
+                    print(f"     {nm:10s} {np.mean(sv[ok, b] - sv[ok, a]):9.0f}")
 
 
 def dw_report(buf):
