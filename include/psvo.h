@@ -572,11 +572,14 @@ int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t 
  * pose exchange); every rank steps the poses it owns.  At most 64 keyframes per call.
  * Look-ahead: with next_dirs_cam (the next iteration's camera directions,
  * same layout; no injected noise) the call also queues the next iteration's
- * query — its rays need this step's pose update, which runs on a side stream
- * right after the embedding backward, so the next rays, intersection and
- * sampling overlap this step's weight-gradient kernels.  The next call must
- * pass dirs_cam == this next_dirs_cam and seed == next_seed; an unconsumed
- * look-ahead is dropped by psvo_map_discard. */
+ * query — its rays need this step's pose update, which runs right after the
+ * decoder backward, so the next rays, intersection and sampling overlap this
+ * step's weight-gradient sum and optimiser step.  The next call must pass
+ * dirs_cam == this next_dirs_cam and seed == next_seed; an unconsumed
+ * look-ahead is dropped by psvo_map_discard.  next_stream (or NULL: the
+ * call's stream): the stream next_dirs_cam (and the next call's gt_rgb /
+ * gt_depth) is being produced on; the step orders only its look-ahead pose
+ * step after the work queued there so far, not the whole iteration. */
 typedef struct psvo_map_frames {
     int n_frames;
     int64_t rays_per_frame;
@@ -587,6 +590,7 @@ typedef struct psvo_map_frames {
     float *pose_grad;
     const float *next_dirs_cam;  /* NULL: no look-ahead */
     uint64_t next_seed;
+    void *next_stream;           /* hipStream_t producing next_dirs_cam, or NULL */
 } psvo_map_frames;
 int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *frames,
                          const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,

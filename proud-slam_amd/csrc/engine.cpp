@@ -23,7 +23,7 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kQSlots };
+             kOffsets, kStatsKeep, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -48,6 +48,7 @@ struct QuerySet {
     hipStream_t qstream = nullptr;  // the stream the query was queued on
     const int *stats_zeroed = nullptr;  // the device statistics buffer a completed read-back left zeroed
     hipEvent_t done = nullptr;    // statistics landed (after the sampler)
+    bool done_recorded = false;   // a query consumed on its own stream skips it (one packet less there)
     hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
     bool freed_recorded = false;
     bool pending = false;
@@ -119,6 +120,10 @@ struct psvo_engine {
     // waits for adam_done first (render, before the interpolation)
     hipEvent_t adam_done = nullptr;
     bool adam_pending = false;
+    hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
+    // capacities of the device-sized forward (render): samples, samples per ray
+    int64_t m_cap = 0;
+    int s_cap = 0;
     EngineTimer tm;
     // the decoder images a look-ahead step built on st after its Adam step,
     // for the decoder whose W[0] it names; consumed by the next
@@ -191,18 +196,21 @@ int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
 
 // The host spins on the landing flag the device writes after the statistics
 // (k_stats_to_host: system-scope release) — it sees them as soon as they
-// land, without the event's completion-signal round trip; the event, recorded
-// after that kernel, is still queried now and then so a failed stream ends
-// the wait with its error.
-int spin_wait(const int *host_stats, int seq, hipEvent_t ev, const char *who) {
+// land, without the event's completion-signal round trip; the event recorded
+// after that kernel (or, without one, the query's stream) is still queried
+// now and then so a failed stream ends the wait with its error.
+int spin_wait(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who) {
     const int *flag = host_stats + PSVO_STAT_WORDS;
     for (unsigned it = 1;; ++it) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
         if ((it & 1023) == 0) {
-            const hipError_t q = hipEventQuery(ev);
+            const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(qs);
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
-            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
+            // the event (no system-scope fence) may complete just before the
+            // kernel's own system-scope flag store is visible: poll a while more
+            for (unsigned k = 0; k < (1u << 22); ++k)
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
             return set_error(PSVO_E_LAUNCH, "%s: stats read-back: event complete, flag %d != %d", who,
                              __atomic_load_n(flag, __ATOMIC_ACQUIRE), seq);
         }
@@ -214,8 +222,10 @@ int query_set_init(QuerySet &s) {
     if (hipHostMalloc(reinterpret_cast<void **>(&s.host_stats), (PSVO_STAT_WORDS + 1) * sizeof(int),
                       hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
-        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s.freed, hipEventDisableTiming) != hipSuccess)
+        // device-side ordering only: the statistics reach the host through the
+        // scan kernel's own system-scope release (k_scan_samples / k_stats_to_host)
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&s.freed, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: query set allocation failed");
     memset(s.host_stats, 0, (PSVO_STAT_WORDS + 1) * sizeof(int));  // flag 0: no statistics yet (seq starts at 1)
     return PSVO_OK;
@@ -344,6 +354,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->prep_fork) (void)hipEventDestroy(e->prep_fork);
     if (e->prep_done) (void)hipEventDestroy(e->prep_done);
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
+    if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
 }
@@ -465,7 +476,7 @@ struct Render {
 // max_steps; an overflow is flagged and reported by the consumer).
 int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_desc *d, int64_t R,
                   const float *rays_o, const float *rays_d, uint64_t seed, const char *who,
-                  const float *noise = nullptr) {
+                  const float *noise = nullptr, bool record_done = true) {
     int rc = PSVO_OK;
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (q.stats_zeroed != stats && hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
@@ -501,6 +512,8 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     Q_BUF(float, s_dist, kSDist, (size_t)R * max_steps * sizeof(float));
     Q_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
     Q_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
+    // the statistics as the device-sized forward reads them (the read-back zeroes `stats`)
+    Q_BUF(int, stats_keep, kStatsKeep, PSVO_STAT_WORDS * sizeof(int));
     mark(e, st, PSVO_TIME_SAMPLE, 0);
     if (x.on()) {
         ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
@@ -514,11 +527,12 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     if (!x.on())  // the sampler's scan does the read-back
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
-                                           q.host_stats, q.seq));
+                                           q.host_stats, q.seq, stats_keep));
     mark(e, st, PSVO_TIME_SAMPLE, 1);
     if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_stats, PSVO_STAT_WORDS, q.seq));
     q.stats_zeroed = stats;
-    if (hipEventRecord(q.done, st) != hipSuccess)
+    q.done_recorded = record_done;
+    if (record_done && hipEventRecord(q.done, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: stats read-back failed", who);
     q.qstream = st;
     q.R = R;
@@ -540,8 +554,14 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
         if (q.R != R || q.ro != rays_o || q.rd != rays_d || q.seed != seed)
             return set_error(PSVO_E_INVALID, "%s: rays / seed differ from the batch queued by psvo_map_query", who);
         // the step's kernels read the query's outputs: order the streams
-        if (q.qstream != st && hipStreamWaitEvent(st, q.done, 0) != hipSuccess)
-            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        if (q.qstream != st) {
+            // a look-ahead queued without the event: its stream's position now (at or after the query)
+            if (!q.done_recorded && hipEventRecord(q.done, q.qstream) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            q.done_recorded = true;
+            if (hipStreamWaitEvent(st, q.done, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        }
         *out = &q;
         return PSVO_OK;
     }
@@ -593,7 +613,7 @@ bool engine_overlap(psvo_engine *e) {
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done};
+                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
@@ -640,11 +660,70 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         if (hipEventRecord(e->prep_done, e->aux) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
     }
-    ENG_CALL(spin_wait(qset.host_stats, qset.seq, qset.done, who));
+    const bool dist = e->x.on();
+    // Device-sized forward (PSVO_DEV_SIZED=1; mapping step, width 128, one
+    // GPU, once a step has sized the buffers): sample compaction,
+    // interpolation and the decoder forward are queued before the query's
+    // statistics reach the host — their kernels read R_hit / S_max / M on the
+    // device (DevBatch) — so the host's read-back no longer gates them.  A
+    // batch beyond the capacities writes nothing and is re-run host-sized
+    // below.  Measured (config B, same box): 0.3–2 % SLOWER than
+    // host-sized — the GPU still idles ≈ 17 µs after the sampler's scan and
+    // ≈ 11 µs at the stream joins before the interpolation, now without the
+    // host's read-back to hide behind — so host-sized stays the default.
+    const char *dz = getenv("PSVO_DEV_SIZED");
+    const bool host_sized = !(dz && *dz == '1');
+    const bool dev_sized = fused_loss && want_act && width == 128 && !dist && e->m_cap > 0 && !host_sized;
+    const int64_t Rq = qset.R;
+    bool dev_done = false;
+    float *feat = nullptr, *sdf_s = nullptr, *rgb_s = nullptr, *act = nullptr, *z_vals = nullptr, *tt = nullptr;
+    int *leaf = nullptr, *ray_of = nullptr;
+    uint64_t *masks = nullptr;
+    if (dev_sized) {
+        const psvo::DevBatch db{static_cast<const int *>(qset.a.p[kStatsKeep]), Rq, e->m_cap,
+                                e->s_cap < max_steps ? e->s_cap : max_steps};
+        const size_t RSc = (size_t)Rq * db.s_cap;
+        ENG_BUF(int, leaf_b, kLeaf, db.m_cap * sizeof(int));
+        ENG_BUF(float, tt_b, kT, db.m_cap * sizeof(float));
+        ENG_BUF(int, ray_of_b, kRayOf, db.m_cap * sizeof(int));
+        ENG_BUF(float, z_b, kZ, RSc * sizeof(float));
+        ENG_BUF(uint8_t, smask, kMask, RSc);
+        ENG_BUF(float, feat_b, kFeat, db.m_cap * 16 * sizeof(float));
+        ENG_BUF(float, sdf_b, kSdfS, db.m_cap * sizeof(float));
+        ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
+        ENG_BUF(float, act_b, kAct, (size_t)psvo_mlp_act_floats(db.m_cap, width) * sizeof(float));
+        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(db.m_cap, width) * sizeof(uint64_t));
+        mark(e, st, PSVO_TIME_POINTS, 0);
+        ENG_CALL(psvo::sample_points_dev(st, db, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, z_b,
+                                         smask));
+        mark(e, st, PSVO_TIME_POINTS, 1);
+        if (engine_overlap(e)) {
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
+        ENG_CALL(join_adam(e, st, who));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+        ENG_CALL(psvo::interp_fwd_dev(st, db, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
+                                      d->centres, d->vertex_idx, d->emb, feat_b));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        if (early_images) {
+            if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        } else if (!prebuilt) {
+            ENG_CALL(mlp_images(st, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+        }
+        mark(e, st, PSVO_TIME_MLP_FWD, 0);
+        ENG_CALL(psvo::mlp_fwd_dev(st, db, feat_b, images, sdf_b, rgb_b, act_b, masks_b));
+        mark(e, st, PSVO_TIME_MLP_FWD, 1);
+        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, z_vals = z_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
+        act = act_b, masks = masks_b;
+        dev_done = true;  // unless the batch turns out not to fit
+    }
+    ENG_CALL(spin_wait(qset.host_stats, qset.seq, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
     // data-parallel: this rank's hit rays, padded to the union's S_max
-    const bool dist = e->x.on();
     const int r_hit = dist ? hs[PSVO_STAT_R_HIT_LOCAL] : hs[PSVO_STAT_R_HIT];
     if (hs[PSVO_STAT_FLAGS] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
     if (hs[PSVO_STAT_FLAGS] & 4) return set_error(PSVO_E_OVERFLOW, "%s: union batch exceeds max_rays_global", who);
@@ -659,50 +738,65 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.s_max = s_max;
     if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
-    const size_t RS = (size_t)r_hit * s_max;
-    ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
-    ENG_BUF(float, tt, kT, M * sizeof(float));
-    ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
-    ENG_BUF(float, z_vals, kZ, RS * sizeof(float));
-    ENG_BUF(uint8_t, smask, kMask, RS);
-    mark(e, st, PSVO_TIME_POINTS, 0);
-    ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt, ray_of,
-                                z_vals, smask));
-    mark(e, st, PSVO_TIME_POINTS, 1);
-    // the loss normalisers can start now (psvo_map_step, on aux; the host
-    // issues aux's wait after the decoder launch)
-    if (fused_loss && engine_overlap(e)) {
-        if (hipEventRecord(e->z_ready, st) != hipSuccess)
-            return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
-        o.z_recorded = true;
+    if (dev_done && (M > e->m_cap || s_max > e->s_cap || s_max > max_steps || r_hit > Rq)) dev_done = false;
+    // the next steps' capacities: this batch with headroom (never shrinking)
+    if (fused_loss && want_act && width == 128 && !dist) {
+        const int64_t mc = M + M / 4 + 256;
+        const int sc = s_max + s_max / 4 + 8;
+        if (mc > e->m_cap) e->m_cap = mc;
+        if (sc > e->s_cap) e->s_cap = sc;
     }
-    // ---- forward: interpolation, decoder, compositing (after the previous
-    // step's optimiser step when its tail ran on aux)
-    ENG_CALL(join_adam(e, st, who));
-    ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
-    mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-    ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
-                             d->vertex_idx, d->emb, feat));
-    mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-    ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
-    ENG_BUF(float, rgb_s, kRgbS, M * 3 * sizeof(float));
-    float *act = nullptr;
-    if (want_act) {
-        ENG_BUF(float, abuf, kAct, (size_t)psvo_mlp_act_floats(M, width) * sizeof(float));
-        act = abuf;
+    if (!dev_done) {
+        const size_t RS = (size_t)r_hit * s_max;
+        ENG_BUF(int, leaf_b, kLeaf, M * sizeof(int));
+        ENG_BUF(float, tt_b, kT, M * sizeof(float));
+        ENG_BUF(int, ray_of_b, kRayOf, M * sizeof(int));
+        ENG_BUF(float, z_b, kZ, RS * sizeof(float));
+        ENG_BUF(uint8_t, smask, kMask, RS);
+        mark(e, st, PSVO_TIME_POINTS, 0);
+        ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf_b, tt_b,
+                                    ray_of_b, z_b, smask));
+        mark(e, st, PSVO_TIME_POINTS, 1);
+        // the loss normalisers can start now (psvo_map_step, on aux; the host
+        // issues aux's wait after the decoder launch)
+        if (fused_loss && engine_overlap(e)) {
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
+        // ---- forward: interpolation, decoder, compositing (after the previous
+        // step's optimiser step when its tail ran on aux)
+        ENG_CALL(join_adam(e, st, who));
+        ENG_BUF(float, feat_b, kFeat, M * 16 * sizeof(float));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+        ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
+                                 d->centres, d->vertex_idx, d->emb, feat_b));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        ENG_BUF(float, sdf_b, kSdfS, M * sizeof(float));
+        ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
+        float *act_p = nullptr;
+        if (want_act) {
+            ENG_BUF(float, abuf, kAct, (size_t)psvo_mlp_act_floats(M, width) * sizeof(float));
+            act_p = abuf;
+        }
+        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
+        mark(e, st, PSVO_TIME_MLP_FWD, 0);
+        if (dev_sized) {  // the images were prepared (or waited for) above
+            ENG_CALL(mlp_fwd_prepared(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
+                                      W[9], images, sdf_b, rgb_b, act_p, masks_b));
+        } else if (early_images || prebuilt) {
+            if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+            ENG_CALL(mlp_fwd_prepared(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
+                                      W[9], images, sdf_b, rgb_b, act_p, masks_b));
+        } else {
+            ENG_CALL(psvo_mlp_fwd(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
+                                  W[9], images, sdf_b, rgb_b, act_p, masks_b));
+        }
+        mark(e, st, PSVO_TIME_MLP_FWD, 1);
+        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, z_vals = z_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
+        act = act_p, masks = masks_b;
     }
-    ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
-    mark(e, st, PSVO_TIME_MLP_FWD, 0);
-    if (early_images || prebuilt) {
-        if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
-            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
-        ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                                  images, sdf_s, rgb_s, act, masks));
-    } else {
-        ENG_CALL(psvo_mlp_fwd(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                              images, sdf_s, rgb_s, act, masks));
-    }
-    mark(e, st, PSVO_TIME_MLP_FWD, 1);
     o.r_hit = r_hit;
     o.m = M;
     o.s_max = s_max;
@@ -720,6 +814,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.act = act;
     o.masks = masks;
     if (fused_loss) return PSVO_OK;  // compositing is part of psvo_composite_loss
+    const size_t RS = (size_t)r_hit * s_max;
     ENG_BUF(float, sdf, kSdf, RS * sizeof(float));
     ENG_BUF(float, weights, kWeights, RS * sizeof(float));
     ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
@@ -821,7 +916,7 @@ int pose_adam(hipStream_t st, const psvo_map_desc *d, const PoseAdam &pa) {
 // buffers — this step's last reader of them, the embedding backward, ran
 // earlier on `ps` — then intersection + sampling into the free query set.
 int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const psvo_map_frames *fr,
-                     int64_t R, const Render &cur, const float *grad_od) {
+                     int64_t R, const Render &cur, const float *grad_od, bool record_done) {
     int rc = PSVO_OK;
     PSVO_REQUIRE(e->q_count == 0, "map_step_frames: a query is already queued");
     QuerySet &q = e->qs[e->q_head];
@@ -840,7 +935,8 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
     ENG_CALL(psvo::pose_step_frames(st, fr->n_frames, fr->rays_per_frame, cur.r_hit, cur.rank_ray, fr->dirs_cam,
                                     grad_od, grad_od + R * 3, fr->poses, fr->pose_m, fr->pose_v, fr->pose_step,
                                     fr->lr_pose, d->beta1, d->beta2, d->eps, pg, fr->next_dirs_cam, rays_o, rays_d));
-    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)"));
+    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)", nullptr,
+                           record_done));
     q.dirs = fr->next_dirs_cam;
     q.pending = true;
     e->q_count++;
@@ -865,6 +961,14 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
     hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward
+    // the look-ahead's inputs made on another stream: its position now, waited
+    // for by the look-ahead's pose step only (psvo_map_frames.next_stream)
+    const bool wait_next = fr && fr->next_dirs_cam && fr->next_stream && as_stream(fr->next_stream) != st;
+    if (wait_next) {
+        ENG_CALL(ensure_aux(e));
+        if (hipEventRecord(e->next_ready, as_stream(fr->next_stream)) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
+    }
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
@@ -1030,7 +1134,10 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // next iteration's rays + query there too — beside this step's weight
     // gradients and the map's Adam
     if (ahead) {
-        ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od));
+        if (wait_next && hipStreamWaitEvent(eb, e->next_ready, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
+        // queued on the step's own stream (split tail): consumed there, no event
+        ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od, eb != st));
     } else if (fr) {
         ENG_CALL(frames_update(e, st, d, fr, q, grad_od, R, &pa));
     }

@@ -45,7 +45,9 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
                                                     const float *__restrict__ rays_d,
                                                     const float *__restrict__ centres,
                                                     const int *__restrict__ vertex_idx,
-                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat) {
+                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat,
+                                                    DevBatch dev) {
+    if (dev.stats) m = dev_batch_m(dev);  // device-sized launch (DevBatch)
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = g >> 2;
     const int q = (int)(g & 3);
@@ -359,9 +361,21 @@ extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size,
     hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
                        t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb),
-                       reinterpret_cast<float4 *>(feat));
+                       reinterpret_cast<float4 *>(feat), DevBatch{});
     return check_launch("interp_fwd");
 }
+
+namespace psvo {
+int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
+                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
+                   const float *centres, const int *vertex_idx, const float *emb, float *feat) {
+    PSVO_REQUIRE(b.stats && b.m_cap > 0 && voxel_size > 0.f, "interp_fwd_dev: bad sizes");
+    hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(b.m_cap * 4, 256)), dim3(256), 0, st, b.m_cap, voxel_size, leaf, t,
+                       ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
+                       reinterpret_cast<const float4 *>(emb), reinterpret_cast<float4 *>(feat), b);
+    return check_launch("interp_fwd_dev");
+}
+}  // namespace psvo
 
 extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets,
                                const int *ray_index, const int *leaf, const float *t, const float *rays_o, const float *rays_d,

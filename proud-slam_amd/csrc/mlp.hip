@@ -1191,8 +1191,10 @@ __device__ __forceinline__ void stage8(float *dst, const float *img, int n_float
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const float *__restrict__ feat,
                                                             const float *__restrict__ img,
                                                             float *__restrict__ sdf_out, float *__restrict__ rgb_out,
-                                                            float *__restrict__ act, uint64_t *__restrict__ masks) {
+                                                            float *__restrict__ act, uint64_t *__restrict__ masks,
+                                                            DevBatch dev) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (dev.stats) m = dev_batch_m(dev);  // device-sized launch (DevBatch)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
@@ -2375,7 +2377,7 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
         hipLaunchKernelGGL(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
-                           masks);
+                           masks, DevBatch{});
     } else {
         hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf,
                            rgb, act, masks);
@@ -2384,6 +2386,25 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
 }
 
 namespace psvo {
+int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const float *images, float *sdf, float *rgb,
+                float *act, uint64_t *masks) {
+    PSVO_REQUIRE(b.stats && b.m_cap > 0 && b.m_cap <= kMaxSamples && images && sdf && rgb,
+                 "mlp_fwd_dev: bad arguments");
+    PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd_dev: act needs masks");
+    PSVO_REQUIRE(use_fwd2(), "mlp_fwd_dev: the persistent forward (k_mlp_fwd2) is required");
+    static bool attr2 = false;
+    if (!attr2) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
+        attr2 = true;
+    }
+    // one workgroup per CU whatever the batch (the balanced split gives small
+    // batches empty workgroups, which only stage and leave)
+    hipLaunchKernelGGL(k_mlp_fwd2, dim3(device_cus()), dim3(kF2Threads), kLdsFwd2, st, b.m_cap, feat, images, sdf, rgb,
+                       act, masks, b);
+    return check_launch("mlp_fwd_dev");
+}
+
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images) {

@@ -48,7 +48,7 @@ int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq);
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, int *host, int seq);
+                        int *ray_ns, int *offsets, int *host, int seq, int *keep = nullptr);
 
 // one element of the Adam step (k_adam; optim.hip's formulation), shared so
 // the fused pose step (pose.hip) computes the same bits
@@ -116,6 +116,33 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
+
+// A device-sized launch of the render's forward (engine: no host read-back
+// before it): the batch's R_hit / S_max / M come from the query's statistics
+// on the device, the buffers hold r_cap × s_cap and m_cap; a batch beyond
+// them (or a failed query) makes every such kernel do nothing, and the host,
+// which reads the statistics while the decoder runs, re-runs host-sized.
+struct DevBatch {
+    const int *stats;
+    int64_t r_cap, m_cap;
+    int s_cap;
+};
+__device__ __forceinline__ bool dev_batch_fits(const DevBatch &b) {
+    return b.stats[PSVO_STAT_R_HIT] <= b.r_cap && b.stats[PSVO_STAT_S_MAX] <= b.s_cap &&
+           b.stats[PSVO_STAT_M] <= b.m_cap && !(b.stats[PSVO_STAT_FLAGS] & 3);
+}
+// M of the batch, or 0 when it does not fit
+__device__ __forceinline__ int64_t dev_batch_m(const DevBatch &b) {
+    return dev_batch_fits(b) ? (int64_t)b.stats[PSVO_STAT_M] : 0;
+}
+int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, const int *s_idx, const float *s_depth,
+                      const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals, uint8_t *mask);
+int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
+                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
+                   const float *centres, const int *vertex_idx, const float *emb, float *feat);
+// the width-128 training forward (k_mlp_fwd2) on the device-sized batch; images prepared
+int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const float *images, float *sdf, float *rgb,
+                float *act, uint64_t *masks);
 
 // The interpolation backward (interp.hip's k_interp_bwd: embedding scatter
 // and dL/dx) folded into the width-128 fused decoder backward, per 16-sample

@@ -1002,10 +1002,13 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     if (lane == 0) ray_ns[il] = count;
 }
 
-// offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.
+// offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.  With
+// `host` the statistics go to the host and `stats` is zeroed for the next
+// query (`keep`, if set, holds a device copy).
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
-                                                       int *__restrict__ stats, int dist, int *host, int seq) {
+                                                       int *__restrict__ stats, int dist, int *host, int seq,
+                                                       int *__restrict__ keep) {
     __shared__ int total;
     __shared__ int smax[16];
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
@@ -1025,6 +1028,7 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
             for (int i = 0; i < PSVO_STAT_WORDS; ++i) {
                 host[i] = stats[i];
+                if (keep) keep[i] = stats[i];  // the device-sized forward's copy (DevBatch)
                 stats[i] = 0;
             }
             __threadfence_system();
@@ -1035,11 +1039,18 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
 
 // ---------------------------------------------------------------------------
 // z_vals / mask [R_hit, S_max] and ray-major compacted samples.
+// dev.stats (device-sized launch, psvo::sample_points_dev, DevBatch): R_hit
+// and S_max come from the query's statistics on the device.
 __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__restrict__ s_idx,
                                 const float *__restrict__ s_depth, const int *__restrict__ ray_ns,
                                 const int *__restrict__ offsets, int *__restrict__ leaf, float *__restrict__ t,
                                 int *__restrict__ ray_of_sample, float *__restrict__ z_vals,
-                                uint8_t *__restrict__ mask) {
+                                uint8_t *__restrict__ mask, DevBatch dev) {
+    if (dev.stats) {
+        const bool fits = dev_batch_fits(dev);
+        r_hit = fits ? dev.stats[PSVO_STAT_R_HIT] : 0;
+        s_max = dev.stats[PSVO_STAT_S_MAX];
+    }
     // grid rows stride over the hit rays (no 64-bit division per element)
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= s_max) return;
@@ -1212,13 +1223,13 @@ namespace psvo {
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, int *host, int seq) {
+                        int *ray_ns, int *offsets, int *host, int seq, int *keep) {
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, nullptr, 0);
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0, host,
-                       seq);
+                       seq, keep);
     return check_launch("sample_rays_to_host");
 }
 
@@ -1275,7 +1286,7 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch);
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
-                       nullptr, 0);
+                       nullptr, 0, nullptr);
     return check_launch("dist_sample");
 }
 int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
@@ -1309,7 +1320,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0);
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
-                       stats, 0, nullptr, 0);
+                       stats, 0, nullptr, 0, nullptr);
     return check_launch("sample_rays");
 }
 
@@ -1346,6 +1357,20 @@ extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int ma
     const int bx = s_max <= 64 ? 64 : s_max <= 128 ? 128 : 256;
     const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
     hipLaunchKernelGGL(k_sample_points, dim3(div_up(s_max, bx), gy), dim3(bx), 0, as_stream(stream), r_hit,
-                       s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask);
+                       s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask,
+                       DevBatch{});
     return check_launch("sample_points");
 }
+
+namespace psvo {
+int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, const int *s_idx, const float *s_depth,
+                      const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals, uint8_t *mask) {
+    PSVO_REQUIRE(b.stats && b.r_cap > 0 && b.s_cap > 0 && b.s_cap <= max_steps_cap && b.m_cap > 0,
+                 "sample_points_dev: bad sizes");
+    const int bx = b.s_cap <= 64 ? 64 : b.s_cap <= 128 ? 128 : 256;
+    const unsigned gy = (unsigned)(b.r_cap < 65535 ? b.r_cap : 65535);
+    hipLaunchKernelGGL(k_sample_points, dim3(div_up(b.s_cap, bx), gy), dim3(bx), 0, st, b.r_cap, b.s_cap,
+                       max_steps_cap, s_idx, s_depth, nullptr, offsets, leaf, t, ray_of_sample, z_vals, mask, b);
+    return check_launch("sample_points_dev");
+}
+}  // namespace psvo

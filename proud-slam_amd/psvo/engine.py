@@ -35,7 +35,7 @@ class MapFrames(ctypes.Structure):
     """Mirror of psvo_map_frames (include/psvo.h)."""
     _fields_ = [("n_frames", _i32), ("rays_per_frame", _i64), ("dirs_cam", _vp), ("poses", _vp), ("pose_m", _vp),
                 ("pose_v", _vp), ("pose_step", _vp), ("lr_pose", _f64), ("pose_grad", _vp),
-                ("next_dirs_cam", _vp), ("next_seed", ctypes.c_uint64)]
+                ("next_dirs_cam", _vp), ("next_seed", ctypes.c_uint64), ("next_stream", _vp)]
 
 
 def _lib():
@@ -146,7 +146,8 @@ class MappingEngine:
             self.desc.lr_dec = float(lr_dec)
 
     def step_frames(self, dirs_cam, rays_per_frame, poses, pose_m, pose_v, pose_steps, lr_pose, rgb, depth, seed,
-                    noise=None, adam_step=None, apply_adam=True, pose_grad=None, next_dirs_cam=None, next_seed=0):
+                    noise=None, adam_step=None, apply_adam=True, pose_grad=None, next_dirs_cam=None, next_seed=0,
+                    next_stream=None):
         """One bundle_adjust_frames iteration with keyframe pose updates
         (psvo_map_step_frames): rays from the current poses [F, 6] (frame f
         owns rows [f·rays_per_frame, (f+1)·rays_per_frame) of dirs_cam),
@@ -155,7 +156,10 @@ class MappingEngine:
         poses / pose_m / pose_v are updated in place.  Returns the loss.
         next_dirs_cam (contiguous f32 [F·rays_per_frame, 3]) / next_seed: the
         next iteration's batch, whose query is queued beside this step's
-        weight gradients (the next call must pass exactly that tensor and seed)."""
+        weight gradients (the next call must pass exactly that tensor and seed).
+        next_stream: the torch stream next_dirs_cam (and the next call's rgb /
+        depth) is produced on, if not the current one — only the look-ahead's
+        pose step waits for it."""
         if self._queued:
             raise RuntimeError("MappingEngine.step_frames: a query() is queued (rays here come from the poses)")
         if self._ahead is not None and dirs_cam is self._ahead:
@@ -185,6 +189,7 @@ class MappingEngine:
         fr.pose_grad = pose_grad.data_ptr() if pose_grad is not None else None
         fr.next_dirs_cam = next_dirs_cam.data_ptr() if next_dirs_cam is not None else None
         fr.next_seed = int(next_seed) & (2 ** 64 - 1)
+        fr.next_stream = next_stream.cuda_stream if next_stream is not None else None
         nz = None
         if noise is not None:
             nz = noise.to(device=dirs.device, dtype=torch.float32).contiguous()

@@ -530,16 +530,16 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     if cur_ready is not None:
         main.wait_event(cur_ready)
     for it in range(num_iterations):
-        nxt, nxt_ready = draw_ahead(it + 1) if ahead and it + 1 < num_iterations else (None, None)
-        if nxt_ready is not None:
-            main.wait_event(nxt_ready)  # the look-ahead's pose step reads its dirs; the next step its colours
+        # the engine orders the look-ahead's pose step (reads nxt's dirs) after
+        # the draw queued on `side` (next_stream), and with it the next step
+        nxt, _ = draw_ahead(it + 1) if ahead and it + 1 < num_iterations else (None, None)
         d_all, c_all, z_all, nz, seed = cur
         adam_step += 1
         cur_steps = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
         dp = eng.grad_exchange is not None
         eng.step_frames(d_all, N_rays, poses, pm, pv, cur_steps, lr_pose or 0.0, c_all, z_all, seed, noise=nz,
                         adam_step=adam_step, apply_adam=not dp, next_dirs_cam=nxt[0] if nxt else None,
-                        next_seed=nxt[4] if nxt else 0)
+                        next_seed=nxt[4] if nxt else 0, next_stream=side if nxt else None)
         if dp:  # data parallel: sum the union-batch gradient over ranks, then the same Adam everywhere
             eng.grad_exchange()
             eng.adam()

@@ -163,3 +163,44 @@ def test_failed_step_does_not_wedge_the_engine():
     loss2 = float(eng.step(ro, rd, rgb, depth, seed=4))  # nothing queued: fresh query
     assert np.isfinite(loss2)
     eng.close()
+
+
+def test_device_sized_forward_matches_host_sized(monkeypatch):
+    """The render's forward queued before the query's statistics reach the
+    host (PSVO_DEV_SIZED=1: sample compaction, interpolation, decoder forward
+    sized on the device — engine.cpp render, DevBatch) against every launch
+    host-sized (the default), over batches that grow past the capacities (the
+    re-run path) and shrink again: same losses and statistics, bit-identical
+    decoder; embeddings up to the order of the interpolation backward's float
+    atomics."""
+    from copy import deepcopy
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ro, rd, rgb, dep = (t.reshape(-1, t.shape[-1]) if t.dim() == 3 else t.reshape(-1)
+                        for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
+    R = ro.shape[0]
+    sizes = [R // 4, R, R // 4, R, R // 2]  # the first full batch outgrows the capacities of the quarter one
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    runs = []
+    for dev_sized in ("0", "1"):
+        monkeypatch.setenv("PSVO_DEV_SIZED", dev_sized)
+        d = deepcopy(dec)
+        e = emb0.clone().to(DEV)
+        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), d, 0.2, 0.01, truncation=0.1, max_distance=10.0,
+                            criteria=crit, max_depth=10.0)
+        losses, stats = [], []
+        for it, n in enumerate(sizes):
+            b = [t[:n].to(DEV).contiguous() for t in (ro, rd, rgb, dep)]
+            losses.append(float(eng.step(*b, seed=70 + it)))
+            stats.append(list(eng.last_stats))
+        torch.cuda.synchronize()
+        runs.append((losses, stats, [p.detach().clone() for p in d.fused_params()], e.clone()))
+        eng.close()
+    (la, sa, da, ea), (lb, sb, db, eb) = runs
+    assert sa == sb
+    assert la[0] == lb[0]  # both host-sized (no capacities yet)
+    np.testing.assert_allclose(lb, la, rtol=1e-4)
+    for p, q in zip(da, db):
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=1e-6)
