@@ -1094,32 +1094,70 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     const psvo::InterpFuse ipf{q.leaf, q.ray_of, q.rank_ray, d->vertex_idx, q.tt, rays_o, rays_d, d->centres, d->emb,
                                d->voxel_size, grad_emb, gx};
+    // width 256 without the fused interpolation backward: k_interp_bwd runs
+    // beside the weight-gradient kernels on aux, or (PSVO_IB256_SERIAL=1)
+    // between the δ chain and them on st, with the whole chip to itself
+    const char *ibs = getenv("PSVO_IB256_SERIAL");
+    const bool ib_serial = !fuse_ib && ibs && *ibs == '1';
+    float *ib_ws = nullptr;
+    if (ib_serial) {
+        ENG_BUF(float, ibw, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
+        ib_ws = ibw;
+    }
+    struct IbCtx {
+        psvo_engine *e;
+        const Render *q;
+        const psvo_map_desc *d;
+        const float *rays_o, *rays_d, *dfeat;
+        float *grad_emb, *grad_od, *ws;
+        int64_t R;
+        bool dirty;
+    };
+    float *dfeat_p = dfeat;
+    IbCtx ibc{e, &q, d, rays_o, rays_d, dfeat_p, grad_emb, grad_od, ib_ws, R, emb_dirty};
+    const psvo::BwdHook ib_hook{[](void *c, hipStream_t s) -> int {
+                                    const IbCtx &x = *static_cast<const IbCtx *>(c);
+                                    if (x.dirty && hipMemsetAsync(x.grad_emb, 0, (size_t)x.d->n_emb * 16 * sizeof(float),
+                                                                  s) != hipSuccess)
+                                        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+                                    mark(x.e, s, PSVO_TIME_INTERP_BWD, 0);
+                                    const int rc = psvo_interp_bwd_chunked(
+                                        s, x.q->r_hit, x.q->s_max, 16, x.d->voxel_size, x.q->offsets, x.q->rank_ray,
+                                        x.q->leaf, x.q->tt, x.rays_o, x.rays_d, x.d->centres, x.d->vertex_idx,
+                                        x.d->emb, x.dfeat, x.grad_emb, x.grad_od, x.grad_od + x.R * 3, x.ws);
+                                    mark(x.e, s, PSVO_TIME_INTERP_BWD, 1);
+                                    return rc;
+                                },
+                                &ibc};
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
     ENG_CALL(mlp_bwd(st, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr,
-                     split ? ax : nullptr));
+                     split ? ax : nullptr, ib_serial ? &ib_hook : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
-    hipStream_t eb = split ? st : ax;
-    if (overlap && !split && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
+    // (ib_serial: it ran inside mlp_bwd, on st)
+    hipStream_t eb = (split || ib_serial) ? st : ax;
+    if (overlap && eb != st && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
-    if (!fuse_ib && emb_dirty &&
+    if (!fuse_ib && !ib_serial && emb_dirty &&
         hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), eb) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     e->grads_clean = false;
     e->clean_buf = grad_emb;
-    mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
     if (fuse_ib) {
+        mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
         ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, q.offsets, q.rank_ray, q.tt, gx, grad_od, grad_od + R * 3));
-    } else {
-        ENG_BUF(float, ib_ws, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
+        mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
+    } else if (!ib_serial) {
+        mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
+        ENG_BUF(float, ib_ws2, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
         ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf,
                                          q.tt, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb,
-                                         grad_od, grad_od + R * 3, ib_ws));
+                                         grad_od, grad_od + R * 3, ib_ws2));
+        mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     }
-    mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
-    if (overlap && !split &&
+    if (overlap && eb != st &&
         (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     // the loss value's reads of crit_ws before the next step's writes: through

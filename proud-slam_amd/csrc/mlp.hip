@@ -2518,7 +2518,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
-            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream) {
+            float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream,
+            const BwdHook *before_dw) {
     PSVO_REQUIRE(ip == nullptr || (width == kW && use_bwd3() && gw1 != nullptr),
                  "mlp_bwd: the fused interpolation backward needs the width-128 fused weight-gradient path");
     if (width == 256) {
@@ -2527,7 +2528,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         PSVO_REQUIRE(gw1 == nullptr || act != nullptr, "mlp_bwd: weight gradients need the forward's activations");
         float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
         return dec256_bwd(as_stream(stream), m, feat, images, rgb, act, masks, g_sdf, g_rgb, dfeat, gw, gb, accumulate,
-                          workspace, dfeat_ready);
+                          workspace, dfeat_ready, before_dw);
     }
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");

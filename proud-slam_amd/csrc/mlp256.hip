@@ -861,7 +861,8 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
 
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
-               float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready) {
+               float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
+               const BwdHook *before_dw) {
     (void)feat;
     const int64_t n_tiles = (m + kChainTile - 1) / kChainTile;
     const int64_t n16 = dec256_tiles16(m);
@@ -899,6 +900,10 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
     if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "dec256_bwd: event record failed");
     if (!want_w) return PSVO_OK;
+    if (before_dw) {
+        const int rc = before_dw->fn(before_dw->ctx, st);
+        if (rc) return rc;
+    }
     DwPlan pl;
     int64_t slab_floats;
     dw_plan(m, &pl, &slab_floats);

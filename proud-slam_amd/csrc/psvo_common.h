@@ -111,9 +111,17 @@ int dec256_images(hipStream_t st, const float *w1, const float *b1, const float 
                   const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
 int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images, float *sdf, float *rgb, float *act,
                uint64_t *masks);
+// work a caller puts between the width-256 δ chain (dfeat written) and its
+// weight-gradient kernels, on the same stream (the engine's interpolation
+// backward, serialised: PSVO_IB256_SERIAL=1)
+struct BwdHook {
+    int (*fn)(void *ctx, hipStream_t st);
+    void *ctx;
+};
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
-               float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready);
+               float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
+               const BwdHook *before_dw = nullptr);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
@@ -171,7 +179,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr,
-            hipStream_t reduce_stream = nullptr);
+            hipStream_t reduce_stream = nullptr, const BwdHook *before_dw = nullptr);
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
 
