@@ -93,6 +93,7 @@ enum {
     PSVO_STAT_R_HIT_LOCAL = 9,   /* this rank's hit rays */
     PSVO_STAT_NEXT_COL0 = 10,    /* first voxel id of the global row after this rank's last */
     PSVO_STAT_S_MAX_LOCAL = 11,  /* this rank's max valid samples per ray */
+    PSVO_STAT_ROUNDS = 12,       /* traversal rounds of the wave-per-ray intersect, summed over rays (diagnostic) */
     PSVO_STAT_WORDS = 16
 };
 

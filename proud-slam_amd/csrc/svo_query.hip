@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     const int64_t r = (int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave;
     const float half = voxel_size * 0.5f;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int visits = 0;
+    int visits = 0, rounds = 0;
     bool overflow_stack = false, spill = false;
     if (r < n_rays) {
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
@@ -296,6 +296,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         }
         wave_lds_sync();
         while (sp > 0) {  // wave-uniform trip count
+            ++rounds;
             const int n = min(sp, kWave);
             uint64_t key = 0;
             int node = 0, dep = 0;
@@ -473,23 +474,26 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     // visits / overflow: one atomic per block (per-ray P, R_hit and max ceil
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
     // at the memory side)
-    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves];
+    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves], blk_rd[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
         blk_vis[threadIdx.x / kWave] = wvis;
         blk_ov[threadIdx.x / kWave] = wov;
         blk_sp[threadIdx.x / kWave] = spill ? 1 : 0;
+        blk_rd[threadIdx.x / kWave] = rounds;  // wave-uniform
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int v = 0, ov = 0, sps = 0;
+        int v = 0, ov = 0, sps = 0, rd = 0;
         for (int w = 0; w < kIsWaves; ++w) {
             v += blk_vis[w];
             ov |= blk_ov[w];
             sps += blk_sp[w];
+            rd += blk_rd[w];
         }
         atomicAdd(stats + PSVO_STAT_VISITS, v);
+        atomicAdd(stats + PSVO_STAT_ROUNDS, rd);
         if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
