@@ -1020,7 +1020,11 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     ENG_CALL(fork_join(ax, st, e->coef_ready));
     // after the normalisers: the fused loss pass waits for them, Adam for the marks
-    if (mark_into && !empty) ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, mark_into));
+    // (width 128: the fused backward's embedding scatter flags the rows it touches instead — the mark
+    // kernel beside the decoder forward slowed it by ≈ 17 µs)
+    const bool marks_in_bwd = psvo::mlp_bwd_fuses_interp(d->width);
+    if (mark_into && !empty && !marks_in_bwd)
+        ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, mark_into));
     if (!empty)
         ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                      q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
@@ -1092,8 +1096,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_BUF(float, gxb, kIbWs, (size_t)M * 3 * sizeof(float));
         gx = gxb;
     }
-    const psvo::InterpFuse ipf{q.leaf, q.ray_of, q.rank_ray, d->vertex_idx, q.tt, rays_o, rays_d, d->centres, d->emb,
-                               d->voxel_size, grad_emb, gx};
+    const psvo::InterpFuse ipf{q.leaf,   q.ray_of,     q.rank_ray, d->vertex_idx, q.tt, rays_o, rays_d, d->centres,
+                               d->emb,   d->voxel_size, grad_emb,   gx,            mark_into};
     // width 256 without the fused interpolation backward: k_interp_bwd runs
     // beside the weight-gradient kernels on aux, or (PSVO_IB256_SERIAL=1)
     // between the δ chain and them on st, with the whole chip to itself

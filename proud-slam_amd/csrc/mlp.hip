@@ -1922,6 +1922,10 @@ __device__ __forceinline__ void scatter_unit(const InterpFuse &ip, const float *
                     cur = lf;
                     cv0 = Bv[sl * 8 + ek0];
                     cv1 = Bv[sl * 8 + ek0 + 4];
+                    if (ip.row_flags != nullptr && ed == 0) {  // the rows this step touches (psvo_adam_mark_rows' set)
+                        ip.row_flags[cv0] = 1;
+                        ip.row_flags[cv1] = 1;
+                    }
                     acc0 = 0.f;
                     acc1 = 0.f;
                 }

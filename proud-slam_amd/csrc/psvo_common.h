@@ -163,6 +163,7 @@ struct InterpFuse {
     float voxel_size;
     float *grad_emb;
     float *gx;
+    uint8_t *row_flags;  // or null: every embedding row the scatter touches is flagged (sparse-exact Adam)
 };
 
 // d_o / d_d of every hit ray from the samples' dL/dx (InterpFuse::gx)
