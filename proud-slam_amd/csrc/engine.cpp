@@ -9,8 +9,10 @@
 // idle behind every read-back.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <cmath>
 
@@ -199,11 +201,39 @@ int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
 // land, without the event's completion-signal round trip; the event recorded
 // after that kernel (or, without one, the query's stream) is still queried
 // now and then so a failed stream ends the wait with its error.
+// PSVO_HOST_WAIT_STATS=1: the host's time in these waits, printed when the
+// engine is freed (is the iteration host-bound? a host that never waits is)
+struct HostWait {
+    double ns = 0;
+    long calls = 0, spun = 0;
+};
+HostWait g_host_wait;
+inline double now_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e9 + t.tv_nsec;
+}
+int spin_wait_impl(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who);
 int spin_wait(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who) {
+    static const bool on = getenv("PSVO_HOST_WAIT_STATS") && *getenv("PSVO_HOST_WAIT_STATS") == '1';
+    if (!on) return spin_wait_impl(host_stats, seq, ev, qs, who);
+    const bool ready = __atomic_load_n(host_stats + PSVO_STAT_WORDS, __ATOMIC_ACQUIRE) == seq;
+    const double t0 = now_ns();
+    const int rc = spin_wait_impl(host_stats, seq, ev, qs, who);
+    g_host_wait.ns += now_ns() - t0;
+    g_host_wait.calls += 1;
+    g_host_wait.spun += ready ? 0 : 1;
+    return rc;
+}
+int spin_wait_impl(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who) {
     const int *flag = host_stats + PSVO_STAT_WORDS;
+    // the runtime query (error detection only) costs microseconds: at most one
+    // per 0.5 ms of waiting, so the flag is seen as soon as it lands
+    double next_query = now_ns() + 5e5;
     for (unsigned it = 1;; ++it) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
-        if ((it & 1023) == 0) {
+        if ((it & 255) == 0 && now_ns() >= next_query) {
+            next_query = now_ns() + 5e5;
             const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(qs);
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
@@ -332,6 +362,9 @@ extern "C" int psvo_engine_timing(psvo_engine *e, double *mean_ms) {
 
 extern "C" void psvo_engine_free(psvo_engine *e) {
     if (!e) return;
+    if (g_host_wait.calls > 0)
+        fprintf(stderr, "psvo: host waited for the query statistics %ld times (%ld not yet landed), %.1f us each\n",
+                g_host_wait.calls, g_host_wait.spun, g_host_wait.ns / 1e3 / g_host_wait.calls);
     (void)hipDeviceSynchronize();
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r)
         for (int k = 0; k < 2; ++k)
@@ -758,7 +791,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
                                     ray_of_b, z_b, smask));
         mark(e, st, PSVO_TIME_POINTS, 1);
         // the loss normalisers can start now (psvo_map_step, on aux; the host
-        // issues aux's wait after the decoder launch)
+        // issues aux's wait after the decoder launch: queued before it, their
+        // three launches delay the forward's — measured 1.2 % slower)
         if (fused_loss && engine_overlap(e)) {
             if (hipEventRecord(e->z_ready, st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
@@ -969,6 +1003,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         if (hipEventRecord(e->next_ready, as_stream(fr->next_stream)) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     }
+    const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
@@ -998,7 +1033,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
     ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
-    const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     // sparse-exact Adam (single GPU): the rows this step can touch, beside the
     // decoder — marked whenever the flags exist, also when the caller runs the
     // Adam step itself (PSVO_STEP_NO_ADAM, then psvo_map_adam): a later fused
