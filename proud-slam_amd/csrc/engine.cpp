@@ -25,7 +25,7 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kStatsKeep, kQSlots };
+             kOffsets, kStatsKeep, kBlkOut, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -523,9 +523,10 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     Q_BUF(int, ray_rank, kRayRank, R * sizeof(int));
     Q_BUF(int, rank_ray, kRankRay, R * sizeof(int));
     mark(e, st, PSVO_TIME_INTERSECT, 0);
+    Q_BUF(int, blk_out, kBlkOut, (size_t)(R + 3) / 4 * 2 * sizeof(int));  // per intersect block: tests, rounds
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
-                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed)));
+                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out));
     const EngineExchange &x = e->x;
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced

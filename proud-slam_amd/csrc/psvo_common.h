@@ -76,7 +76,7 @@ int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray, const PackRec *packed = nullptr);
+                     int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr);
 
 // data-parallel query (svo_query.hip): rows of the exchanged slot-0 table for
 // a union batch of at most max_rays_global rays; pack this rank's 8 words;

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           float max_distance, float step_size,
                                                           int *__restrict__ hit_idx, float *__restrict__ hit_t0,
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
-                                                          float *__restrict__ ray_dsum, int *__restrict__ stats) {
+                                                          float *__restrict__ ray_dsum, int *__restrict__ stats,
+                                                          int *__restrict__ blk_out) {
     __shared__ KeyLds lds_all[kIsWaves];
     KeyLds &S = lds_all[threadIdx.x / kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -492,8 +493,13 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             sps += blk_sp[w];
             rd += blk_rd[w];
         }
-        atomicAdd(stats + PSVO_STAT_VISITS, v);
-        atomicAdd(stats + PSVO_STAT_ROUNDS, rd);
+        if (blk_out) {  // summed by k_ray_stats_rank: no same-address atomics (they serialise at the memory side)
+            blk_out[2 * blockIdx.x] = v;
+            blk_out[2 * blockIdx.x + 1] = rd;
+        } else {
+            atomicAdd(stats + PSVO_STAT_VISITS, v);
+            atomicAdd(stats + PSVO_STAT_ROUNDS, rd);
+        }
         if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
@@ -615,7 +621,21 @@ __global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restr
 __global__ __launch_bounds__(1024) void k_ray_stats_rank(int64_t n, const int *__restrict__ ray_nv,
                                                          const float *__restrict__ ray_dsum, float step_size,
                                                          int *__restrict__ stats, int *__restrict__ ray_rank,
-                                                         int *__restrict__ rank_ray) {
+                                                         int *__restrict__ rank_ray, const int *__restrict__ blk_out,
+                                                         int n_blk) {
+    if (blk_out) {  // the intersect blocks' AABB tests / traversal rounds
+        int v = 0, rd = 0;
+        for (int i = threadIdx.x; i < n_blk; i += blockDim.x) {
+            v += blk_out[2 * i];
+            rd += blk_out[2 * i + 1];
+        }
+        v = wave_sum(v);
+        rd = wave_sum(rd);
+        if ((threadIdx.x & (kWave - 1)) == 0) {
+            atomicAdd(stats + PSVO_STAT_VISITS, v);  // 16 waves: 16 atomics
+            atomicAdd(stats + PSVO_STAT_ROUNDS, rd);
+        }
+    }
     ray_stats_body(n, ray_nv, ray_dsum, step_size, stats);
     __syncthreads();
     hit_rank_body(n, ray_nv, ray_rank, rank_ray);
@@ -1199,7 +1219,7 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
@@ -1216,7 +1236,7 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
-                       max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+                       max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
@@ -1247,20 +1267,20 @@ int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq) {
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray, const PackRec *packed) {
+                     int *rank_ray, const PackRec *packed, int *blk_out) {
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
     if (packed)
         hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out);
     else
         hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats);
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out);
     hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
-                       ray_rank, rank_ray);
+                       ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
     return check_launch("intersect_ranked");
 }
 }  // namespace psvo
