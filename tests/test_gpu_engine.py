@@ -170,9 +170,9 @@ def test_device_sized_forward_matches_host_sized(monkeypatch):
     host (PSVO_DEV_SIZED=1: sample compaction, interpolation, decoder forward
     sized on the device — engine.cpp render, DevBatch) against every launch
     host-sized (the default), over batches that grow past the capacities (the
-    re-run path) and shrink again: same losses and statistics, bit-identical
-    decoder; embeddings up to the order of the interpolation backward's float
-    atomics."""
+    re-run path) and shrink again: same losses (rtol 1e-4) and statistics;
+    decoder and embeddings up to the order of the interpolation backward's
+    float atomics."""
     from copy import deepcopy
     from psvo.engine import MappingEngine
     from psvo.octree import map_states
@@ -201,6 +201,9 @@ def test_device_sized_forward_matches_host_sized(monkeypatch):
     assert sa == sb
     assert la[0] == lb[0]  # both host-sized (no capacities yet)
     np.testing.assert_allclose(lb, la, rtol=1e-4)
+    # after the first step the embeddings differ by the order of the scatter's float atomics
+    # (either mode, run to run), and Adam's m / sqrt(v) can turn that noise on a near-zero
+    # gradient into a visible fraction of a step (lr 5e-3): bars at 1 % of one step
     for p, q in zip(da, db):
-        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
+    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
