@@ -56,6 +56,34 @@ __device__ __forceinline__ bool ray_aabb(const float o[3], const float inv[3], f
     return true;
 }
 
+// ray_aabb without the early exits: the same comparisons on the same values
+// in the same order (NaNs included), the verdict accumulated instead of
+// returned.  The traversal's node record is then consumed in one basic block,
+// so the compiler cannot sink the y / z loads behind the x test (a second
+// dependent memory round trip per round); t_lo / t_hi are set only on a hit.
+__device__ __forceinline__ bool ray_aabb_nb(const float o[3], const float inv[3], float cx, float cy, float cz,
+                                            float half, float &t_lo, float &t_hi) {
+    float lo_all = 0.0f, hi_all = 100000.0f;
+    bool miss = false;
+    const float c[3] = {cx, cy, cz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float lo = (c[a] - half - o[a]) * inv[a];
+        float hi = (c[a] + half - o[a]) * inv[a];
+        const bool sw = hi < lo;
+        const float l2 = sw ? hi : lo, h2 = sw ? lo : hi;
+        miss = miss | (h2 < lo_all) | (l2 > hi_all);
+        lo_all = (l2 > lo_all) ? l2 : lo_all;
+        hi_all = (h2 < hi_all) ? h2 : hi_all;
+        miss = miss | (lo_all > hi_all);
+    }
+    if (!miss) {
+        t_lo = lo_all;
+        t_hi = hi_all;
+    }
+    return !miss;
+}
+
 __device__ __forceinline__ int child_mask(const int *__restrict__ children, int node) {
     const int *row = children + (int64_t)node * 9;
     int m = 0;
@@ -221,40 +249,29 @@ __device__ __forceinline__ uint64_t key_digit(int u, int depth) {
     return (uint64_t)(7 - u) << (3 * (kLevels - depth));
 }
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+// inclusive prefix sum over the wave of v in [0, 16) (a node's child count):
+// one ballot + lane-mask count per bit instead of six dependent cross-lane
+// shuffles
+__device__ __forceinline__ int wave_incl_scan16(int v) {
+    int s = v;
 #pragma unroll
-    for (int s = 1; s < kWave; s <<= 1) {
-        const int t = __shfl_up(v, s, kWave);
-        if (lane >= s) v += t;
+    for (int b = 0; b < 4; ++b) {
+        const uint64_t m = __ballot((v >> b) & 1);
+        s += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
     }
-    return v;
+    return s;
 }
 
-// kth smallest key of the leaf list (n <= 128, keys unique; the prune's
-// threshold is the 50th): a bitonic sort
-// of the 128 (padded) keys held two per lane — 28 compare-exchange stages of
-// register / cross-lane exchanges instead of an O(n²) rank count in LDS
-__device__ uint64_t kth_key(const KeyLds &S, int n, int kth, int lane) {
-    uint64_t v0 = lane < n ? S.lkey[lane] : ~0ull;
-    uint64_t v1 = lane + kWave < n ? S.lkey[lane + kWave] : ~0ull;
+// number of keys below k in the ascending list a[0, n), n <= 64: a
+// branch-free binary search of 7 uniform steps (the leaf list is kept sorted
+// by merging each round's leaves into it, so the prune's threshold — the 50th
+// smallest key — is simply its last entry; no per-round selection)
+__device__ __forceinline__ int count_below(const uint64_t *a, int n, uint64_t k) {
+    int lo = 0;
 #pragma unroll
-    for (int k = 2; k <= 2 * kWave; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j == kWave) {  // partners lane / lane + 64: element lane ascends (k = 128)
-                const uint64_t lo = v0 < v1 ? v0 : v1, hi = v0 < v1 ? v1 : v0;
-                v0 = lo;
-                v1 = hi;
-            } else {
-                const bool lower = (lane & j) == 0;
-                const uint64_t p0 = __shfl_xor(v0, j, kWave), p1 = __shfl_xor(v1, j, kWave);
-                const bool up0 = (lane & k) == 0, up1 = ((lane + kWave) & k) == 0;
-                v0 = (lower == up0) ? (v0 < p0 ? v0 : p0) : (v0 < p0 ? p0 : v0);
-                v1 = (lower == up1) ? (v1 < p1 ? v1 : p1) : (v1 < p1 ? p1 : v1);
-            }
-        }
-    }
-    return kth < kWave ? __shfl(v0, kth, kWave) : __shfl(v1, kth - kWave, kWave);
+    for (int step = kWave; step > 0; step >>= 1)
+        if (lo + step <= n && a[lo + step - 1] < k) lo += step;
+    return lo;
 }
 
 
@@ -322,14 +339,14 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     ref = pi.x;
                     first = pi.y;
                     cmask = pi.z;
-                    hit = ray_aabb(o, inv, pc.x, pc.y, pc.z, half * (float)side, a, b);
+                    hit = ray_aabb_nb(o, inv, pc.x, pc.y, pc.z, half * (float)side, a, b);
                 } else {
                     const int *rw = structure + (int64_t)node * 9;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) row[u] = rw[u];
                     side = rw[8];
                     const float *pc = centres + (int64_t)node * 3;
-                    hit = ray_aabb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                    hit = ray_aabb_nb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
                 }
             }
             const bool leaf = hit && side == 1;
@@ -347,7 +364,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     for (int u = 0; u < 8; ++u) c += row[u] > -1;
                 }
             }
-            const int incl = wave_incl_scan(c, lane);
+            const int incl = wave_incl_scan16(c);
             // a prune drops everything below the popped chunk (all keys > kbound)
             const int floor_ = (n_eff < n) ? 0 : sp - n;
             const bool ok = !live || floor_ + (n_eff - 1 - lane) + incl <= kStk;
@@ -357,7 +374,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                 spill = true;
                 break;
             }
-            const int T = J > 0 ? __shfl(incl, J - 1, kWave) : 0;
+            const int T = J > 0 ? __builtin_amdgcn_readlane(incl, J - 1) : 0;
             const bool acc = lane < J;
             wave_lds_sync();  // every lane has read its candidate before the stack is rewritten
             if (live && !acc) {  // re-queued tail keeps its order on top of the floor
@@ -382,47 +399,48 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     }
                 }
             }
-            const uint64_t lb = __ballot(acc && leaf);
-            if (acc && leaf) {
-                const int pos = nl + __popcll(lb & below);
-                S.lkey[pos] = key;
-                S.lidx[pos] = ref;
-                S.lt0[pos] = a;
-                S.lt1[pos] = b;
-            }
             visits += acc ? 1 : 0;
-            nl += __popcll(lb);
             sp = base + T;
-            wave_lds_sync();
-            if (nl >= kMaxHits) {  // keep the 50 smallest keys; later candidates beyond them are dropped
-                kbound = kth_key(S, nl, kMaxHits - 1, lane);
-                bounded = true;
-                wave_lds_sync();
-                int w = 0;
-                for (int i0 = 0; i0 < nl; i0 += kWave) {
-                    const int i = i0 + lane;
-                    uint64_t kk = 0;
-                    int ix = 0;
-                    float ta = 0.f, tb = 0.f;
-                    const bool keep = i < nl && (kk = S.lkey[i]) <= kbound;
-                    if (i < nl) {
-                        ix = S.lidx[i];
-                        ta = S.lt0[i];
-                        tb = S.lt1[i];
-                    }
-                    const uint64_t kb = __ballot(keep);
-                    wave_lds_sync();
-                    if (keep) {
-                        const int pos = w + __popcll(kb & below);
-                        S.lkey[pos] = kk;
-                        S.lidx[pos] = ix;
-                        S.lt0[pos] = ta;
-                        S.lt1[pos] = tb;
-                    }
-                    w += __popcll(kb);
-                    wave_lds_sync();
+            const bool fresh = acc && leaf;
+            const uint64_t lb = __ballot(fresh);
+            if (lb) {  // merge this round's leaves (keys ascend with the lane) into the key-sorted list
+                const int m = __popcll(lb), q = __popcll(lb & below);
+                if (fresh) S.lkey[kWave + q] = key;  // scratch past the list (nl <= 50)
+                const bool hold = lane < nl;
+                uint64_t hk = 0;
+                int hi = 0;
+                float h0 = 0.f, h1 = 0.f;
+                if (hold) {
+                    hk = S.lkey[lane];
+                    hi = S.lidx[lane];
+                    h0 = S.lt0[lane];
+                    h1 = S.lt1[lane];
                 }
-                nl = w;
+                wave_lds_sync();
+                // final positions: own rank + the other list's keys below (keys are unique)
+                const int pn = q + count_below(S.lkey, nl, key);
+                const int po = lane + count_below(S.lkey + kWave, m, hk);
+                wave_lds_sync();
+                if (fresh && pn < kMaxHits) {
+                    S.lkey[pn] = key;
+                    S.lidx[pn] = ref;
+                    S.lt0[pn] = a;
+                    S.lt1[pn] = b;
+                }
+                if (hold && po < kMaxHits) {
+                    S.lkey[po] = hk;
+                    S.lidx[po] = hi;
+                    S.lt0[po] = h0;
+                    S.lt1[po] = h1;
+                }
+                nl = min(nl + m, kMaxHits);
+                wave_lds_sync();
+                if (nl == kMaxHits) {  // the 50 smallest keys kept; later candidates beyond them are dropped
+                    kbound = S.lkey[kMaxHits - 1];
+                    bounded = true;
+                }
+            } else {
+                wave_lds_sync();
             }
         }
         if (spill) {  // serial DFS on lane 0 (reference order by construction; key = emission index)
@@ -438,22 +456,23 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             nl = cnt;
             wave_lds_sync();
         }
-        // stable sort by t_in (ties: DFS order = key), trim at max_distance
+        // stable sort by t_in (ties: DFS order = key = list order, both paths
+        // leave the list key-sorted), trim at max_distance; nl <= 50: one
+        // entry per lane, the others' t_in read lane to lane
         int nv = 0;
-        for (int i = lane; i < nl; i += kWave) {
-            const float ti = S.lt0[i];
-            const uint64_t ki = S.lkey[i];
-            int rank = 0;
-            for (int j = 0; j < nl; ++j) {
-                const float tj = S.lt0[j];
-                rank += (tj < ti) || (tj == ti && S.lkey[j] < ki);
-            }
+        const float ti = lane < nl ? S.lt0[lane] : 0.f;
+        int rank = 0;
+        for (int j = 0; j < nl; ++j) {
+            const float tj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ti), j));
+            rank += (tj < ti) || (tj == ti && j < lane);
+        }
+        if (lane < nl) {
             const bool in = !(ti > max_distance);
             nv += in;
-            const float bi = S.lt1[i];
+            const float bi = S.lt1[lane];
             S.hd[rank] = bi - ti;
             if (in) {
-                hit_idx[r * kMaxHits + rank] = S.lidx[i];
+                hit_idx[r * kMaxHits + rank] = S.lidx[lane];
                 hit_t0[r * kMaxHits + rank] = ti;
                 hit_t1[r * kMaxHits + rank] = bi;
             }
@@ -617,12 +636,109 @@ __global__ __launch_bounds__(1024) void k_hit_rank(int64_t n, const int *__restr
     hit_rank_body(n, ray_nv, ray_rank, rank_ray);
 }
 
-// k_ray_stats + k_hit_rank in one launch (the engine's path)
+// k_ray_stats + k_hit_rank in one launch (the engine's path).  Up to
+// kRankPasses·1024 rays every input is read once, in one round of
+// independent loads, and held in registers: ray i = k·1024 + t is thread t's
+// pass k, its rank among the hit rays = the hit rays of the earlier passes +
+// of the earlier waves of this pass (ballot counts in LDS, one scan) + the
+// lower lanes (mbcnt).  The serial version (more rays) read ray_nv three
+// times behind three barriers — dependent memory round trips on the
+// critical path between the traversal and the sampler.
+constexpr int kRankPasses = 8;
+
 __global__ __launch_bounds__(1024) void k_ray_stats_rank(int64_t n, const int *__restrict__ ray_nv,
                                                          const float *__restrict__ ray_dsum, float step_size,
                                                          int *__restrict__ stats, int *__restrict__ ray_rank,
                                                          int *__restrict__ rank_ray, const int *__restrict__ blk_out,
                                                          int n_blk) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    if (n <= (int64_t)kRankPasses * 1024 && n_blk <= 2048) {
+        __shared__ int s_cnt[kRankPasses * 16];
+        __shared__ int s_red[5][16];
+        int nv[kRankPasses];
+        float ds[kRankPasses];
+        int v_blk = 0, r_blk = 0;
+        if (blk_out) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int b = j * 1024 + tid;
+                if (b < n_blk) {
+                    v_blk += blk_out[2 * b];
+                    r_blk += blk_out[2 * b + 1];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRankPasses; ++k) {
+            const int64_t i = (int64_t)k * 1024 + tid;
+            nv[k] = i < n ? ray_nv[i] : 0;
+            ds[k] = i < n ? ray_dsum[i] : 0.f;
+        }
+        int p = 0, mc = 0;
+#pragma unroll
+        for (int k = 0; k < kRankPasses; ++k) {
+            p = max(p, nv[k]);
+            if (nv[k] > 0) mc = max(mc, (int)ceilf(__fdiv_rn(ds[k], step_size)));
+            const uint64_t m = __ballot(nv[k] > 0);
+            if (lane == 0) s_cnt[k * 16 + w] = __popcll(m);
+        }
+        p = wave_max(p);
+        mc = wave_max(mc);
+        const int vs = wave_sum(v_blk), rs = wave_sum(r_blk);
+        if (lane == 0) {
+            s_red[0][w] = p;
+            s_red[1][w] = mc;
+            s_red[2][w] = vs;
+            s_red[3][w] = rs;
+        }
+        __syncthreads();
+        const int nw = blockDim.x / kWave;
+        if (w == 0) {  // exclusive scan of the (pass, wave) hit counts, two per lane
+            const int a0 = (lane * 2) / 16 < kRankPasses && (lane * 2) % 16 < nw ? s_cnt[lane * 2] : 0;
+            const int a1 = (lane * 2 + 1) / 16 < kRankPasses && (lane * 2 + 1) % 16 < nw ? s_cnt[lane * 2 + 1] : 0;
+            int incl = a0 + a1;
+#pragma unroll
+            for (int sh = 1; sh < kWave; sh <<= 1) {
+                const int t = __shfl_up(incl, sh, kWave);
+                if (lane >= sh) incl += t;
+            }
+            if (lane * 2 < kRankPasses * 16) {
+                s_cnt[lane * 2] = incl - a0 - a1;
+                s_cnt[lane * 2 + 1] = incl - a1;
+            }
+            if (lane == kWave - 1) s_red[4][0] = incl;  // hit rays
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int pp = 0, mm = 0, vv = 0, rr = 0;
+            for (int k = 0; k < nw; ++k) {
+                pp = max(pp, s_red[0][k]);
+                mm = max(mm, s_red[1][k]);
+                vv += s_red[2][k];
+                rr += s_red[3][k];
+            }
+            stats[PSVO_STAT_P] = pp;
+            stats[PSVO_STAT_R_HIT] = s_red[4][0];
+            stats[PSVO_STAT_MAX_CEIL] = mm;
+            if (blk_out) {
+                atomicAdd(stats + PSVO_STAT_VISITS, vv);
+                atomicAdd(stats + PSVO_STAT_ROUNDS, rr);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRankPasses; ++k) {
+            const int64_t i = (int64_t)k * 1024 + tid;
+            const uint64_t m = __ballot(nv[k] > 0);
+            if (i < n) {
+                const int rk = s_cnt[k * 16 + w] +
+                               (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                ray_rank[i] = nv[k] > 0 ? rk : -1;
+                if (nv[k] > 0) rank_ray[rk] = (int)i;
+            }
+        }
+        return;
+    }
     if (blk_out) {  // the intersect blocks' AABB tests / traversal rounds
         int v = 0, rd = 0;
         for (int i = threadIdx.x; i < n_blk; i += blockDim.x) {
