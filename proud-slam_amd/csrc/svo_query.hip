@@ -524,14 +524,15 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     }
 }
 
+// one wave, one word per lane (words <= 64)
 __global__ void k_stats_to_host(int *__restrict__ stats, int *host, int words, int seq) {
-    if (threadIdx.x != 0) return;
-    for (int i = 0; i < words; ++i) {
+    const int i = threadIdx.x;
+    if (i < words) {
         host[i] = stats[i];
         stats[i] = 0;  // ready for the query set's next use (no memset launch)
     }
     __threadfence_system();
-    __hip_atomic_store(host + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i == 0) __hip_atomic_store(host + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // P (max valid hits), R_hit and max ceil(Σ/step) over the rays — one block.
@@ -576,8 +577,14 @@ __global__ __launch_bounds__(1024) void k_ray_stats(int64_t n, const int *__rest
 // ---------------------------------------------------------------------------
 // Single-workgroup exclusive scan (n ≲ 10^6): each thread owns a contiguous
 // run; run totals scanned in LDS.
+// Runs of up to kRegRun elements (n ≤ 8·1024 with 1024 threads) are read
+// once, in one round of independent loads, and kept in registers (the
+// general loop re-reads them after the barriers); `lmax`, if set, receives
+// the thread's largest value.
+constexpr int kRegRun = 8;
+
 template <typename F>
-__device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *total) {
+__device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *total, int *lmax = nullptr) {
     // thread t scans the run [t·per, (t+1)·per); the run totals are scanned
     // with wave shuffles and one LDS pass over the ≤ 16 wave totals
     // (2 barriers instead of a 2·log2(1024)-barrier Hillis–Steele pass)
@@ -588,8 +595,25 @@ __device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *
     const int64_t per = (n + nt - 1) / nt;
     const int64_t beg = tid * per;
     const int64_t end = beg + per < n ? beg + per : n;
-    int local = 0;
-    for (int64_t i = beg; i < end; ++i) local += value(i);
+    const bool in_regs = per <= kRegRun;  // block-uniform
+    int vals[kRegRun];
+    int local = 0, mx = 0;
+    if (in_regs) {
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k) vals[k] = beg + k < end ? value(beg + k) : 0;
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k) {
+            local += vals[k];
+            mx = max(mx, vals[k]);
+        }
+    } else {
+        for (int64_t i = beg; i < end; ++i) {
+            const int v = value(i);
+            local += v;
+            mx = max(mx, v);
+        }
+    }
+    if (lmax) *lmax = mx;
     int incl = local;
 #pragma unroll
     for (int sh = 1; sh < kWave; sh <<= 1) {
@@ -609,9 +633,18 @@ __device__ void block_scan_runs(int64_t n, F value, int *__restrict__ out, int *
     }
     __syncthreads();
     int run = (w > 0 ? s_wave[w - 1] : 0) + incl - local;
-    for (int64_t i = beg; i < end; ++i) {
-        out[i] = run;
-        run += value(i);
+    if (in_regs) {
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k)
+            if (beg + k < end) {
+                out[beg + k] = run;
+                run += vals[k];
+            }
+    } else {
+        for (int64_t i = beg; i < end; ++i) {
+            out[i] = run;
+            run += value(i);
+        }
     }
     if (tid == nt - 1) *total = s_wave[nw - 1];
 }
@@ -1154,25 +1187,29 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
                                : n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
     const int64_t n = max((int64_t)0, min(n_own, r_hit_cap));
-    block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total);
     int mx = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mx = max(mx, ray_ns[i]);
+    block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total, &mx);
     mx = wave_max(mx);
     if ((threadIdx.x & (kWave - 1)) == 0) smax[threadIdx.x / kWave] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kWave) {  // wave 0; with `host` one statistics word per lane (no serial copy loop)
+        const int lane = threadIdx.x;
         for (int k = 1; k < (int)(blockDim.x / kWave); ++k) mx = max(mx, smax[k]);
-        offsets[n] = total;
-        stats[PSVO_STAT_S_MAX] = mx;
-        stats[PSVO_STAT_M] = total;
+        const int tot = total;
+        if (lane == 0) offsets[n] = tot;
         if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
-            for (int i = 0; i < PSVO_STAT_WORDS; ++i) {
-                host[i] = stats[i];
-                if (keep) keep[i] = stats[i];  // the device-sized forward's copy (DevBatch)
-                stats[i] = 0;
+            if (lane < PSVO_STAT_WORDS) {
+                const int v = lane == PSVO_STAT_S_MAX ? mx : lane == PSVO_STAT_M ? tot : stats[lane];
+                host[lane] = v;
+                if (keep) keep[lane] = v;  // the device-sized forward's copy (DevBatch)
+                stats[lane] = 0;
             }
             __threadfence_system();
-            __hip_atomic_store(host + PSVO_STAT_WORDS, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0)
+                __hip_atomic_store(host + PSVO_STAT_WORDS, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (lane == 0) {
+            stats[PSVO_STAT_S_MAX] = mx;
+            stats[PSVO_STAT_M] = tot;
         }
     }
 }
