@@ -32,10 +32,16 @@ constexpr float kMaxDepthFill = 10.0f;  // voxel_helpers.py:24 MAX_DEPTH
 
 inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// records the packed traversal's top start tests per ray (two per lane;
+// svo_query.hip top_start, tree_pack.hip k_pt_top): more would cost more
+// AABB work than the rounds they save (room0's first 512 records: five times
+// the tests of a whole walk)
+constexpr int kPackTopMax = 128;
+
 // one octree node as the packed traversal reads it (tree_pack.hip)
 struct PackRec {  // 32 B, 16-B aligned
     float4 c;     // centre x, y, z; side (int bits)
-    int4 i;       // reference node id, first child record (-1: none), child mask, 0
+    int4 i;       // reference node id, first child record (-1: none), child mask, spare (tree_pack.hip)
 };
 
 // the query's statistics words → coherent pinned host memory by one device

@@ -234,6 +234,30 @@ constexpr int kStk = 512;    // candidate stack entries per ray
 constexpr int kBfsL = 128;   // leaf list capacity (≤ 49 + 64 between compactions)
 constexpr int kIsWaves = 4;  // waves (rays) per block
 
+// Diagnostic build only (-DPSVO_IS_STAMPS, `make is_stamps`: lib/diag/): per
+// ray, k_intersect_sorted's cycles by segment (s_memtime; scalar reads of the
+// clock only), read through psvo_debug_is_stamps (scripts/intersect_stamps.py).
+// Segments: [0] whole ray, [1] pop + node load + AABB test, [2] scan +
+// re-queue + child push, [3] leaf merge, [4] final sort + output, [5] rounds,
+// [6] rounds that found leaves, [7] AABB tests.  The product build has none.
+#ifdef PSVO_IS_STAMPS
+constexpr int kIsStampRays = 16384;
+__device__ unsigned long long psvo_g_is_stamps[kIsStampRays][8];
+#define IS_T(v)                                                                   \
+    do {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+    } while (0)
+#define IS_DECL unsigned long long is_t0 = 0, is_ta = 0, is_tb = 0, is_acc[5] = {0, 0, 0, 0, 0}, is_lr = 0
+#define IS_MARK(var) IS_T(var)
+#define IS_ADD(k, from, to) is_acc[k] += (to) - (from)
+#else
+#define IS_DECL
+#define IS_MARK(var)
+#define IS_ADD(k, from, to)
+#endif
+
 struct KeyLds {
     uint64_t skey[kStk];
     int snode[kStk];
@@ -275,6 +299,109 @@ __device__ __forceinline__ int count_below(const uint64_t *a, int n, uint64_t k)
 }
 
 
+// The packed traversal's start below the root.  Every ray descends the same
+// few top levels one round each (room0: 9 rounds per ray, one per level), so
+// the records above the start level m (records [0, n_top), breadth-first,
+// n_top <= 128; tree_pack.hip stores n_top and m in the root's spare word and
+// the parent record in the others') are tested all at once — one round of
+// independent loads — and "hit with every ancestor" is resolved by pointer
+// jumping over the parent links (cross-lane, no LDS passes).  A node is
+// tested by the reference's walk iff its parent passed (PSVO_STAT_VISITS
+// counts exactly those).  The children of the passing level-(m−1) records
+// are the level-m candidates, pushed in record order (within a level,
+// breadth-first order is descending key order), the smallest key on top —
+// the state the rounds would have reached, minus their latency.  The top
+// levels hold no leaves (tree_pack.hip checks), so no prune can have applied.
+// Returns the stack depth, or −1 (more than kStk candidates: the caller
+// starts at the root).
+__device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const float o[3], const float inv[3],
+                         float half, int n_top, int m, int lane, int &visits) {
+    constexpr int kB = kPackTopMax / kWave;  // n_top <= kPackTopMax
+    static_assert(kB == 2, "the pointer jumping below gathers from two batches");
+    bool pa[kB];           // hit, then: hit and every ancestor hit
+    int anc[kB], par[kB], first[kB], cmask[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        const int j = b * kWave + lane;
+        pa[b] = false;
+        anc[b] = par[b] = -1;
+        first[b] = -1;
+        cmask[b] = 0;
+        if (j < n_top) {
+            const float4 pc = packed[j].c;
+            const int4 pi = packed[j].i;
+            float a = 0.f, t = 0.f;
+            pa[b] = ray_aabb_nb(o, inv, pc.x, pc.y, pc.z, half * (float)__float_as_int(pc.w), a, t);
+            par[b] = anc[b] = j == 0 ? -1 : pi.w;
+            first[b] = pi.y;
+            cmask[b] = pi.z;
+        }
+    }
+    // pointer jumping: pa[j] = AND of the hits from j up to (excluding) anc[j]
+    for (;;) {
+        const bool more = anc[0] >= 0 || anc[1] >= 0;
+        if (!__ballot(more)) break;
+        int wd[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) wd[b] = (anc[b] & 0xFF) | (pa[b] ? 0x100 : 0);  // anc -1 → 0xFF
+        bool npa[kB];
+        int nanc[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int a = anc[b];
+            const int w0 = __shfl(wd[0], a & (kWave - 1), kWave), w1 = __shfl(wd[1], a & (kWave - 1), kWave);
+            const int w = (a >> 6) ? w1 : w0;
+            npa[b] = a >= 0 ? (pa[b] && (w & 0x100)) : pa[b];
+            nanc[b] = a >= 0 ? ((w & 0xFF) == 0xFF ? -1 : (w & 0xFF)) : -1;
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            pa[b] = npa[b];
+            anc[b] = nanc[b];
+        }
+    }
+    // tested by the reference's walk: the root, and every node whose parent passed
+    int tested = 0;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        const int p = par[b];
+        const int f0 = __shfl((int)pa[0], p & (kWave - 1), kWave), f1 = __shfl((int)pa[1], p & (kWave - 1), kWave);
+        const bool parent_ok = (p >> 6) ? f1 : f0;
+        tested += (b * kWave + lane < n_top) && (b * kWave + lane == 0 || (p >= 0 && parent_ok)) ? 1 : 0;
+    }
+    // the level-m candidates: children of the passing level-(m-1) records
+    // (those whose children lie past the top records), in record order.
+    // Their keys: the candidate's rank in descending record order (= key
+    // order within a level) in the level-m digit positions — the same order
+    // as the path keys for every key this ray ever compares.
+    int cnt[kB];
+    int total = 0;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        cnt[b] = (pa[b] && first[b] >= n_top) ? __popc(cmask[b]) : 0;
+        total += cnt[b];
+    }
+    total = wave_sum(total);
+    if (total > kStk) return -1;
+    const int shift = 3 * (kLevels - m);
+    int run = 0;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        const int incl = wave_incl_scan16(cnt[b]);
+        if (cnt[b]) {
+            int g = run + incl - cnt[b];
+            for (int k = 0; k < cnt[b]; ++k, ++g) {
+                S.skey[g] = (uint64_t)(total - 1 - g) << shift;
+                S.snode[g] = first[b] + k;
+                S.sdep[g] = (uint8_t)m;
+            }
+        }
+        run += __builtin_amdgcn_readlane(incl, kWave - 1);
+    }
+    visits += tested;
+    return total;
+}
+
 // PACKED: candidates are records of the breadth-first packed tree
 // (tree_pack.hip: centre + side and ref id / first child / child mask in one
 // 32-B record, siblings contiguous) instead of reference node ids into the
@@ -299,22 +426,32 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     int visits = 0, rounds = 0;
     bool overflow_stack = false, spill = false;
     if (r < n_rays) {
+        IS_DECL;
+        IS_MARK(is_t0);
         const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
         const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
         float inv[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, d[a]);
-        int nl = 0, sp = 1;
+        int nl = 0, sp = -1;
         bool bounded = false;
         uint64_t kbound = ~0ull;
-        if (lane == 0) {  // the root is the first candidate
-            S.skey[0] = 0;
-            S.snode[0] = 0;
-            S.sdep[0] = 0;
+        if constexpr (PACKED) {
+            const int tw = packed[0].i.w;  // records above the start level | start level << 16 (0: none)
+            if (tw > 0) sp = top_start(S, packed, o, inv, half, tw & 0xFFFF, tw >> 16, lane, visits);
+        }
+        if (sp < 0) {
+            if (lane == 0) {  // the root is the first candidate
+                S.skey[0] = 0;
+                S.snode[0] = 0;
+                S.sdep[0] = 0;
+            }
+            sp = 1;
         }
         wave_lds_sync();
         while (sp > 0) {  // wave-uniform trip count
             ++rounds;
+            IS_MARK(is_ta);
             const int n = min(sp, kWave);
             uint64_t key = 0;
             int node = 0, dep = 0;
@@ -349,6 +486,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     hit = ray_aabb_nb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
                 }
             }
+            IS_MARK(is_tb);
+            IS_ADD(1, is_ta, is_tb);
             const bool leaf = hit && side == 1;
             const bool inner = hit && side != 1;
             if (__ballot(inner && dep >= kLevels)) {  // deeper than the reference's stack
@@ -399,6 +538,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     }
                 }
             }
+            IS_MARK(is_ta);
+            IS_ADD(2, is_tb, is_ta);
             visits += acc ? 1 : 0;
             sp = base + T;
             const bool fresh = acc && leaf;
@@ -439,9 +580,14 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                     kbound = S.lkey[kMaxHits - 1];
                     bounded = true;
                 }
+#ifdef PSVO_IS_STAMPS
+                ++is_lr;
+#endif
             } else {
                 wave_lds_sync();
             }
+            IS_MARK(is_tb);
+            IS_ADD(3, is_ta, is_tb);
         }
         if (spill) {  // serial DFS on lane 0 (reference order by construction; key = emission index)
             int cnt = 0;
@@ -456,6 +602,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             nl = cnt;
             wave_lds_sync();
         }
+        IS_MARK(is_ta);
         // stable sort by t_in (ties: DFS order = key = list order, both paths
         // leave the list key-sorted), trim at max_distance; nl <= 50: one
         // entry per lane, the others' t_in read lane to lane
@@ -490,6 +637,18 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             ray_nv[r] = nv;
             ray_dsum[r] = dsum;
         }
+#ifdef PSVO_IS_STAMPS
+        IS_MARK(is_tb);
+        IS_ADD(4, is_ta, is_tb);
+        const int is_vis = wave_sum(visits);
+        if (lane == 0 && r < kIsStampRays) {
+            psvo_g_is_stamps[r][0] = is_tb - is_t0;
+            for (int k = 1; k < 5; ++k) psvo_g_is_stamps[r][k] = is_acc[k];
+            psvo_g_is_stamps[r][5] = (unsigned long long)rounds;
+            psvo_g_is_stamps[r][6] = is_lr;
+            psvo_g_is_stamps[r][7] = (unsigned long long)is_vis;
+        }
+#endif
     }
     // visits / overflow: one atomic per block (per-ray P, R_hit and max ceil
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
@@ -1551,3 +1710,10 @@ int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, cons
     return check_launch("sample_points_dev");
 }
 }  // namespace psvo
+
+#ifdef PSVO_IS_STAMPS
+extern "C" int psvo_debug_is_stamps(void *dst, int64_t bytes) {
+    if (bytes < (int64_t)sizeof(psvo::psvo_g_is_stamps)) return -1;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(psvo::psvo_g_is_stamps), sizeof(psvo::psvo_g_is_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif

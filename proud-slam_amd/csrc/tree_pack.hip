@@ -11,7 +11,10 @@
 // own lines.  The packed layout:
 //
 //   rec[i] = { float4 (cx, cy, cz, side as int bits),
-//              int4   (reference node id, first child record, child mask, 0) }
+//              int4   (reference node id, first child record, child mask, spare) }
+//
+// (spare: the traversal's start level for the root and the parent record for
+// the next 127 records, k_pt_top; 0 elsewhere)
 //
 // in breadth-first order with a node's existing children at consecutive
 // records first + rank(u) (rank = popcount(mask & ((1 << u) − 1))), so a
@@ -147,6 +150,37 @@ __global__ __launch_bounds__(kPtThreads) void k_pt_emit(int level, const float *
     }
 }
 
+// The traversal's start level (svo_query.hip, top_start): the deepest level
+// m >= 2 such that the records above it — [0, meta[m].first), breadth-first —
+// number at most kTopMax and hold no leaf (side 1).  The root's spare word
+// gets that count | m << 16 (0: start at the root); each other record among
+// the first kTopMax gets its parent record.
+constexpr int kTopMax = kPackTopMax;
+
+__global__ __launch_bounds__(512) void k_pt_top(PtWork w, PackRec *__restrict__ rec) {
+    __shared__ int leaf_at;
+    const int total = w.meta[(kPtMaxDepth - 1) * 2 + 0] + w.meta[(kPtMaxDepth - 1) * 2 + 1];
+    if (threadIdx.x == 0) leaf_at = kTopMax;
+    __syncthreads();
+    const int j = threadIdx.x;
+    if (j < total && j < kTopMax) {
+        if (__float_as_int(rec[j].c.w) == 1) atomicMin(&leaf_at, j);
+        const int4 ri = rec[j].i;  // the parent link of each child among the first kTopMax records
+        if (ri.y >= 0)
+            for (int k = 0; k < __popc(ri.z) && ri.y + k < kTopMax; ++k) rec[ri.y + k].i.w = j;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int word = 0;
+        for (int m = 2; m < kPtMaxDepth; ++m) {
+            const int n = w.meta[m * 2 + 0];  // records of the levels above m
+            if (n > kTopMax || n > leaf_at || w.meta[(m - 1) * 2 + 1] == 0) break;
+            word = n | m << 16;
+        }
+        rec[0].i.w = word;
+    }
+}
+
 __global__ void k_pt_init(PtWork w) {
     w.lists[0][0] = 0;  // the root is node 0 (the traversal's first candidate)
     w.meta[0] = 0;
@@ -186,5 +220,6 @@ extern "C" int psvo_pack_tree(void *stream, int64_t n_nodes, const float *centre
         hipLaunchKernelGGL(k_pt_scan, dim3(1), dim3(1024), 0, st, level, w);
         hipLaunchKernelGGL(k_pt_emit, dim3(nb), dim3(kPtThreads), 0, st, level, centres, structure, w, rec);
     }
+    hipLaunchKernelGGL(k_pt_top, dim3(1), dim3(512), 0, st, w, rec);
     return check_launch("pack_tree");
 }

@@ -125,7 +125,10 @@ def test_engine_query_ahead_matches_inline():
     np.testing.assert_allclose(lb, la, rtol=1e-4)
     for p, q in zip(decs[0].fused_params(), decs[1].fused_params()):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(embs[0], embs[1], rtol=1e-4, atol=1e-6)
+    # the embedding gradient is a float-atomic scatter whose order depends on
+    # what runs beside it (the ahead engine's next query does): after step 1
+    # the two differ by that order, amplified where Adam's second moment is tiny
+    torch.testing.assert_close(embs[0], embs[1], rtol=1e-4, atol=5e-5)
     # a step whose batch is not the queued one is refused
     ahead.query(halves[0][0], halves[0][1], 7)
     with pytest.raises(RuntimeError):

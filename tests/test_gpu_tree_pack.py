@@ -60,6 +60,7 @@ def test_packed_records_and_traversal(name):
         k = S[lvl, :8]
         lvl = k[k > -1]
         reach.append(lvl)
+    starts = np.cumsum([0] + [r.size for r in reach])  # first record of each level
     reach = np.concatenate(reach)
     m = reach.size
     assert np.unique(reach).size == m
@@ -83,6 +84,21 @@ def test_packed_records_and_traversal(name):
     pos = np.repeat(first[has] - (np.cumsum(ch) - ch), ch) + np.arange(ch.sum())
     child_ref = ref_id[pos]
     assert np.array_equal(child_ref, kids[has][present[has]])
+    # spare word (the traversal's top start): the parent record for records
+    # 1..127, 0 beyond; the root's = n_top | m << 16 with m the deepest level
+    # >= 2 with <= 128 records above it, none a leaf (0: start at the root)
+    parent = np.zeros(m, dtype=np.int64)
+    parent[pos] = np.repeat(np.nonzero(has)[0], ch)
+    top = min(m, 128)
+    assert np.array_equal(rec[1:top, 7], parent[1:top])
+    assert np.all(rec[top:, 7] == 0)
+    word = 0
+    for lv in range(2, len(starts)):
+        n = starts[lv]
+        if n > 128 or np.any(rec[:n, 3] == 1) or starts[lv] == starts[lv - 1]:
+            break
+        word = n | lv << 16
+    assert rec[0, 7] == word and word > 0
     # traversal: bit-exact to the reference-layout kernel
     ro = w.rays_o.reshape(-1, 3).to(DEV).contiguous()
     rd = w.rays_d.reshape(-1, 3).to(DEV).contiguous()
@@ -90,7 +106,13 @@ def test_packed_records_and_traversal(name):
     b = _intersect(ms, ro, rd, w.scene.voxel_size, c["step"], packed)
     for k in ("idx", "t0", "t1", "nv", "ds"):
         assert torch.equal(a[k], b[k]), k
-    assert torch.equal(a["st"][:8], b["st"][:8])  # P, R_hit, max ceil, visits, spills, flags
+    # P, R_hit, max ceil, spills, flags; the AABB-test count (a diagnostic)
+    # may differ: the packed walk tests the top levels in full before any
+    # prune can apply, the reference-layout one in key-ordered rounds
+    keep = [0, 1, 2, 3, 4, 6, 7]
+    assert torch.equal(a["st"][keep], b["st"][keep])
+    va, vb = int(a["st"][5]), int(b["st"][5])
+    assert abs(va - vb) <= 0.02 * va, (va, vb)
     assert int(a["st"][6]) == 0  # no serial-DFS fallback on either side
 
 
