@@ -36,7 +36,10 @@ inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // svo_query.hip top_start, tree_pack.hip k_pt_top): more would cost more
 // AABB work than the rounds they save (room0's first 512 records: five times
 // the tests of a whole walk)
-constexpr int kPackTopMax = 128;
+#ifndef PSVO_PACK_TOP_MAX
+#define PSVO_PACK_TOP_MAX 128
+#endif
+constexpr int kPackTopMax = PSVO_PACK_TOP_MAX;  // a multiple of 64, <= 512
 
 // one octree node as the packed traversal reads it (tree_pack.hip)
 struct PackRec {  // 32 B, 16-B aligned

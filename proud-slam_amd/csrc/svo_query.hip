@@ -317,7 +317,6 @@ __device__ __forceinline__ int count_below(const uint64_t *a, int n, uint64_t k)
 __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const float o[3], const float inv[3],
                          float half, int n_top, int m, int lane, int &visits) {
     constexpr int kB = kPackTopMax / kWave;  // n_top <= kPackTopMax
-    static_assert(kB == 2, "the pointer jumping below gathers from two batches");
     bool pa[kB];           // hit, then: hit and every ancestor hit
     int anc[kB], par[kB], first[kB], cmask[kB];
 #pragma unroll
@@ -339,20 +338,26 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
     }
     // pointer jumping: pa[j] = AND of the hits from j up to (excluding) anc[j]
     for (;;) {
-        const bool more = anc[0] >= 0 || anc[1] >= 0;
+        bool more = false;
+#pragma unroll
+        for (int b = 0; b < kB; ++b) more = more || anc[b] >= 0;
         if (!__ballot(more)) break;
         int wd[kB];
 #pragma unroll
-        for (int b = 0; b < kB; ++b) wd[b] = (anc[b] & 0xFF) | (pa[b] ? 0x100 : 0);  // anc -1 → 0xFF
+        for (int b = 0; b < kB; ++b) wd[b] = (anc[b] & 0x3FF) | (pa[b] ? 0x400 : 0);  // anc -1 → 0x3FF
         bool npa[kB];
         int nanc[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
             const int a = anc[b];
-            const int w0 = __shfl(wd[0], a & (kWave - 1), kWave), w1 = __shfl(wd[1], a & (kWave - 1), kWave);
-            const int w = (a >> 6) ? w1 : w0;
-            npa[b] = a >= 0 ? (pa[b] && (w & 0x100)) : pa[b];
-            nanc[b] = a >= 0 ? ((w & 0xFF) == 0xFF ? -1 : (w & 0xFF)) : -1;
+            int w = 0;
+#pragma unroll
+            for (int sb = 0; sb < kB; ++sb) {
+                const int v = __shfl(wd[sb], a & (kWave - 1), kWave);
+                if ((a >> 6) == sb) w = v;
+            }
+            npa[b] = a >= 0 ? (pa[b] && (w & 0x400)) : pa[b];
+            nanc[b] = a >= 0 ? ((w & 0x3FF) == 0x3FF ? -1 : (w & 0x3FF)) : -1;
         }
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
@@ -365,8 +370,12 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
         const int p = par[b];
-        const int f0 = __shfl((int)pa[0], p & (kWave - 1), kWave), f1 = __shfl((int)pa[1], p & (kWave - 1), kWave);
-        const bool parent_ok = (p >> 6) ? f1 : f0;
+        bool parent_ok = false;
+#pragma unroll
+        for (int sb = 0; sb < kB; ++sb) {
+            const int v = __shfl((int)pa[sb], p & (kWave - 1), kWave);
+            if ((p >> 6) == sb) parent_ok = v != 0;
+        }
         tested += (b * kWave + lane < n_top) && (b * kWave + lane == 0 || (p >= 0 && parent_ok)) ? 1 : 0;
     }
     // the level-m candidates: children of the passing level-(m-1) records
