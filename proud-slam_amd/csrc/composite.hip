@@ -45,12 +45,15 @@ __device__ __forceinline__ float comp_gw(float gdp, float z, float gwx, const fl
                                                                                    0.f, gr, gg, gb);
 }
 // dL/dsdf_s through the weights (kept samples) plus the direct term g
-__device__ __forceinline__ float comp_gsdf(float gw, float dot, float tot, bool keep, float sdf, float tr, float g) {
-    const float a = sdf / tr;
-    const float sp = sigm(a), sn = sigm(-a);
+__device__ __forceinline__ float comp_gsdf_sig(float gw, float dot, float tot, bool keep, float sp, float sn, float tr,
+                                               float g) {
     const float gu = keep ? (gw - dot) / tot : 0.f;
     const float du = sp * sn * (sn - sp) / tr;
     return fmaf(gu, du, g);
+}
+__device__ __forceinline__ float comp_gsdf(float gw, float dot, float tot, bool keep, float sdf, float tr, float g) {
+    const float a = sdf / tr;
+    return comp_gsdf_sig(gw, dot, tot, keep, sigm(a), sigm(-a), tr, g);
 }
 
 __global__ __launch_bounds__(256) void k_composite_fwd(int64_t r_hit, int s_max, float tr,
@@ -227,7 +230,13 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
+    // the ray's ground truth and the coefficients depend on nothing computed
+    // here: their loads go out first, beside the sample loads
+    const int64_t orig = rank_ray[r];
     const int off = offsets[r], ns = ray_ns[r];
+    const float d = gt_depth[orig];
+    const float gt0 = gt_rgb[orig * 3 + 0], gt1 = gt_rgb[orig * 3 + 1], gt2 = gt_rgb[orig * 3 + 2];
+    const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
     const float *z = z_vals + r * s_max;
     auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
     constexpr int JR = J > 0 ? J : 1;
@@ -257,26 +266,59 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     };
 #define PSVO_FOR_S(lim) for (int j = 0, s = lane; (J == 0 || j < J) && s < (lim); ++j, s += 64)
     // ---- forward (k_composite_fwd)
+    // sdf of sample s + 1 (J > 0: the next lane's, or lane 0's of the next
+    // slot — exchanged with every lane active, before the per-lane loops)
+    float pn[JR];
+    if constexpr (J > 0) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const float dn = __shfl_down(pr[j], 1, 64);
+            const float nx = __shfl(pr[j + 1 < J ? j + 1 : j], 0, 64);
+            pn[j] = lane < 63 ? dn : nx;
+        }
+    }
     int first = s_max;
     PSVO_FOR_S(s_max) {
         const float v = P(j, s);
-        if (s + 1 < s_max && sdf_at(s + 1) * v < 0.0f) first = min(first, s);
+        float v1;
+        if constexpr (J > 0) v1 = pn[j];
+        else v1 = s + 1 < s_max ? sdf_at(s + 1) : 0.f;
+        if (s + 1 < s_max && v1 * v < 0.0f) first = min(first, s);
     }
     first = wmin(first);
     const float zmin = z[first == s_max ? 0 : first];
+    // σ(a), σ(−a) per sample (registers when J > 0: computed once, the same
+    // bits as recomputing them in each pass)
+    float spr[JR], snr[JR], wr[JR];
+#pragma unroll
+    for (int j = 0; j < JR; ++j) spr[j] = snr[j] = wr[j] = 0.f;
     float tot = 0.f;
     PSVO_FOR_S(s_max) {
         const float a = P(j, s) / tr;
-        float w = sigm(a) * sigm(-a);
+        const float sp = sigm(a), sn = sigm(-a);
+        float w = sp * sn;
         const bool keep = (Z(j, s) < zmin + tr) && (s < ns);
         tot += keep ? w : 0.0f;
+        if constexpr (J > 0) {
+            spr[j] = sp;
+            snr[j] = sn;
+            wr[j] = keep ? w : 0.0f;
+        }
     }
     tot = wsum(tot) + 1e-8f;
+    if constexpr (J > 0) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) wr[j] = wr[j] / tot;
+    }
     auto weight_at = [&](int j, int s) {  // normalised weight W_s (0 outside the kept set)
-        const float a = P(j, s) / tr;
-        const float w = sigm(a) * sigm(-a);
-        const bool keep = (Z(j, s) < zmin + tr) && (s < ns);
-        return (keep ? w : 0.0f) / tot;
+        if constexpr (J > 0) {
+            return wr[j];
+        } else {
+            const float a = P(j, s) / tr;
+            const float w = sigm(a) * sigm(-a);
+            const bool keep = (Z(j, s) < zmin + tr) && (s < ns);
+            return (keep ? w : 0.0f) / tot;
+        }
     };
     float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f;
     PSVO_FOR_S(s_max) {
@@ -293,9 +335,6 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     cb = wsum(cb);
     dd = wsum(dd);
     // ---- loss partials (k_crit_rays) and d loss / d {colour, depth} (k_crit_bwd)
-    const int64_t orig = rank_ray[r];
-    const float d = gt_depth[orig];
-    const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
     float qfs = 0.f, qsdf = 0.f;
     PSVO_FOR_S(s_max) {
         const CritTerms t = crit_terms(Z(j, s), P(j, s), d, tr, max_depth);
@@ -305,10 +344,11 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     qfs = wsum(qfs);
     qsdf = wsum(qsdf);
     const float rgb[3] = {cr, cg, cb};
+    const float gt[3] = {gt0, gt1, gt2};
     float gcol[3], ac = 0.f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float e = gt_rgb[orig * 3 + c] - rgb[c];
+        const float e = gt[c] - rgb[c];
         ac += fabsf(e);
         gcol[c] = -ccol * (e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f));
     }
@@ -342,7 +382,10 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         const float gw = comp_gw3(gdp, zs, 0.f, true, C(j, s, 0), C(j, s, 1), C(j, s, 2), gcol[0], gcol[1], gcol[2]);
         const float p = P(j, s);
         const float gsdf = crit_grad(cfs, csdf, crit_terms(zs, p, d, tr, max_depth));  // k_crit_bwd's term
-        g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, zs < zmin + tr, p, tr, gsdf);
+        if constexpr (J > 0)
+            g_sdf_s[off + s] = comp_gsdf_sig(gw, dot, tot, zs < zmin + tr, spr[j], snr[j], tr, gsdf);
+        else
+            g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, zs < zmin + tr, p, tr, gsdf);
         float *gc = g_rgb_s + (int64_t)(off + s) * 3;
         gc[0] = W * gcol[0];
         gc[1] = W * gcol[1];
