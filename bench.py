@@ -287,7 +287,7 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
 
 
 CHAIN_KERNELS = ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples", "k_sample_points",
-                 "k_interp_fwd")
+                 "k_interp_fwd", "k_points_interp")
 MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd3", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce",
                "k_dec256_prep", "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
 
@@ -602,8 +602,9 @@ def main():
             r.update(extra)
         return r
 
-    roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, "
-                      "k_sample_points, k_interp_fwd" + (")" if fused_ib else ", k_interp_bwd)"), bytes_qi, q_ms,
+    roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, " +
+                      ("k_points_interp = compaction + interp fwd" if os.environ.get("PSVO_FUSED_POINTS") == "1"
+                       else "k_sample_points, k_interp_fwd") + (")" if fused_ib else ", k_interp_bwd)"), bytes_qi, q_ms,
                       tr.get("query_interp_bytes_per_step"),
                       sum(kt_serial[k] for k in q_keys) if kt_serial else None,
                       {"parts_ms": q_parts, "parts_ms_serialised": {k: kt_serial[k] for k in q_keys}

@@ -787,10 +787,30 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(int, ray_of_b, kRayOf, M * sizeof(int));
         ENG_BUF(float, z_b, kZ, RS * sizeof(float));
         ENG_BUF(uint8_t, smask, kMask, RS);
+        ENG_BUF(float, feat_b, kFeat, M * 16 * sizeof(float));
+        // PSVO_FUSED_POINTS=1: compaction + interpolation as one launch
+        // (k_points_interp; it reads the embeddings, so the previous step's
+        // optimiser join moves in front of it).  Measured (config B, same
+        // box): 24.5 µs for the one kernel against 6.7 + 13.8 for
+        // the two (half its lanes hold slots past their ray's samples) and
+        // 0.96-0.99 vs 0.94-0.96 ms per iteration, so the split stays default.
+        const char *sp = getenv("PSVO_FUSED_POINTS");
+        const bool fuse_pi = sp && *sp == '1';
+        if (fuse_pi) ENG_CALL(join_adam(e, st, who));
         mark(e, st, PSVO_TIME_POINTS, 0);
-        ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf_b, tt_b,
-                                    ray_of_b, z_b, smask));
+        if (fuse_pi) {
+            ENG_CALL(psvo::points_interp(st, r_hit, s_max, max_steps, d->voxel_size, s_idx, s_depth, offsets, leaf_b,
+                                         tt_b, ray_of_b, z_b, smask, rank_ray, rays_o, rays_d, d->centres,
+                                         d->vertex_idx, d->emb, feat_b));
+        } else {
+            ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf_b,
+                                        tt_b, ray_of_b, z_b, smask));
+        }
         mark(e, st, PSVO_TIME_POINTS, 1);
+        if (fuse_pi) {  // the interpolation ran inside the points region
+            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        }
         // the loss normalisers can start now (psvo_map_step, on aux; the host
         // issues aux's wait after the decoder launch: queued before it, their
         // three launches delay the forward's — measured 1.2 % slower)
@@ -801,12 +821,13 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         }
         // ---- forward: interpolation, decoder, compositing (after the previous
         // step's optimiser step when its tail ran on aux)
-        ENG_CALL(join_adam(e, st, who));
-        ENG_BUF(float, feat_b, kFeat, M * 16 * sizeof(float));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-        ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
-                                 d->centres, d->vertex_idx, d->emb, feat_b));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        if (!fuse_pi) {
+            ENG_CALL(join_adam(e, st, who));
+            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+            ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
+                                     d->centres, d->vertex_idx, d->emb, feat_b));
+            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        }
         ENG_BUF(float, sdf_b, kSdfS, M * sizeof(float));
         ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
         float *act_p = nullptr;

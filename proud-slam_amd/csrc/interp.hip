@@ -78,6 +78,69 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
     feat[s * 4 + q] = acc;
 }
 
+// k_sample_points and k_interp_fwd in one pass over the sampler's [R_hit, cap]
+// rows (engine, host-sized forward): four lanes per (hit ray, step) slot; a
+// valid slot (a prefix of its row) interpolates straight from the sampler's
+// voxel id and depth, and its q = 0 lane writes the compacted leaf / t /
+// ray_of_sample and the [R_hit, S_max] z_vals / mask entries of the slot.
+// Same arithmetic as the two kernels (same bits); the compacted arrays are
+// not read back, and one launch and the stream gap between the two go.
+__global__ __launch_bounds__(256) void k_points_interp(int64_t r_hit, int s_max, int cap, float voxel_size,
+                                                       const int *__restrict__ s_idx,
+                                                       const float *__restrict__ s_depth,
+                                                       const int *__restrict__ offsets, int *__restrict__ leaf,
+                                                       float *__restrict__ t, int *__restrict__ ray_of_sample,
+                                                       float *__restrict__ z_vals, uint8_t *__restrict__ mask,
+                                                       const int *__restrict__ ray_index,
+                                                       const float *__restrict__ rays_o,
+                                                       const float *__restrict__ rays_d,
+                                                       const float *__restrict__ centres,
+                                                       const int *__restrict__ vertex_idx,
+                                                       const float4 *__restrict__ emb, float4 *__restrict__ feat) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = g >> 2;
+    const int q = g & 3;
+    if (s >= s_max) return;
+    for (int64_t r = blockIdx.y; r < r_hit; r += gridDim.y) {
+        const int v = s_idx[r * cap + s];
+        const float z = s_depth[r * cap + s];
+        const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
+        if (q == 0) {
+            const int64_t e = r * s_max + s;
+            z_vals[e] = z;
+            mask[e] = v != -1;
+            if (v != -1) {
+                leaf[o] = v;
+                t[o] = z;
+                ray_of_sample[o] = (int)r;
+            }
+        }
+        if (v == -1) continue;
+        const int ray = ray_index ? ray_index[r] : (int)r;
+        float p[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float x = rays_o[(int64_t)ray * 3 + a] + rays_d[(int64_t)ray * 3 + a] * z;
+            p[a] = __fdiv_rn(x - centres[(int64_t)v * 3 + a], voxel_size) + 0.5f;
+        }
+        float w[8];
+        corner_weights(p[0], p[1], p[2], w);
+        const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)v * 8);
+        const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)v * 8 + 4);
+        const int vid[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float4 e4 = emb[(int64_t)vid[k] * 4 + q];
+            acc.x = acc.x + w[k] * e4.x;
+            acc.y = acc.y + w[k] * e4.y;
+            acc.z = acc.z + w[k] * e4.z;
+            acc.w = acc.w + w[k] * e4.w;
+        }
+        feat[o * 4 + q] = acc;
+    }
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -374,6 +437,22 @@ int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const in
                        ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb), reinterpret_cast<float4 *>(feat), b);
     return check_launch("interp_fwd_dev");
+}
+
+int points_interp(hipStream_t st, int64_t r_hit, int s_max, int max_steps_cap, float voxel_size, const int *s_idx,
+                  const float *s_depth, const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals,
+                  uint8_t *mask, const int *ray_index, const float *rays_o, const float *rays_d,
+                  const float *centres, const int *vertex_idx, const float *emb, float *feat) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max >= 0 && s_max <= max_steps_cap && voxel_size > 0.f,
+                 "points_interp: bad sizes");
+    if (r_hit == 0 || s_max == 0) return PSVO_OK;
+    const int bx = s_max <= 16 ? 64 : s_max <= 32 ? 128 : 256;  // 4 lanes per slot
+    const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
+    hipLaunchKernelGGL(k_points_interp, dim3(div_up((int64_t)s_max * 4, bx), gy), dim3(bx), 0, st, r_hit, s_max,
+                       max_steps_cap, voxel_size, s_idx, s_depth, offsets, leaf, t, ray_of_sample, z_vals, mask,
+                       ray_index, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
+                       reinterpret_cast<float4 *>(feat));
+    return check_launch("points_interp");
 }
 }  // namespace psvo
 

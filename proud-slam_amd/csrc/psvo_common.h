@@ -157,6 +157,12 @@ int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, cons
 int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
                    const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
                    const float *centres, const int *vertex_idx, const float *emb, float *feat);
+// sample compaction + interpolation forward in one launch (k_points_interp:
+// the outputs of psvo_sample_points and psvo_interp_fwd, same bits)
+int points_interp(hipStream_t st, int64_t r_hit, int s_max, int max_steps_cap, float voxel_size, const int *s_idx,
+                  const float *s_depth, const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals,
+                  uint8_t *mask, const int *ray_index, const float *rays_o, const float *rays_d,
+                  const float *centres, const int *vertex_idx, const float *emb, float *feat);
 // the width-128 training forward (k_mlp_fwd2) on the device-sized batch; images prepared
 int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const float *images, float *sdf, float *rgb,
                 float *act, uint64_t *masks);

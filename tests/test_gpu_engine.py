@@ -210,3 +210,43 @@ def test_device_sized_forward_matches_host_sized(monkeypatch):
     for p, q in zip(da, db):
         torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
     torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
+
+
+def test_fused_points_interp_matches_split(monkeypatch):
+    """Sample compaction + interpolation forward as one launch
+    (k_points_interp, PSVO_FUSED_POINTS=1) against the two kernels (the
+    default: k_sample_points, then k_interp_fwd): the same
+    arithmetic, so every step's forward — loss and statistics — is bit-equal
+    from equal state; parameters after several steps within the order of
+    the interpolation backward's float atomics (as the device-sized test)."""
+    from copy import deepcopy
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ro, rd, rgb, dep = (t.reshape(-1, t.shape[-1]) if t.dim() == 3 else t.reshape(-1)
+                        for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
+    R = ro.shape[0]
+    sizes = [R, R // 2, R]
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("PSVO_FUSED_POINTS", fused)
+        d = deepcopy(dec)
+        e = emb0.clone().to(DEV)
+        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), d, 0.2, 0.01, truncation=0.1, max_distance=10.0,
+                            criteria=crit, max_depth=10.0)
+        losses, stats = [], []
+        for it, n in enumerate(sizes):
+            b = [t[:n].to(DEV).contiguous() for t in (ro, rd, rgb, dep)]
+            losses.append(float(eng.step(*b, seed=90 + it)))
+            stats.append(list(eng.last_stats))
+        torch.cuda.synchronize()
+        runs.append((losses, stats, [p.detach().clone() for p in d.fused_params()], e.clone()))
+        eng.close()
+    (la, sa, da, ea), (lb, sb, db, eb) = runs
+    assert sa == sb
+    assert la[0] == lb[0]  # same state, same forward bits
+    np.testing.assert_allclose(lb, la, rtol=1e-4)
+    for p, q in zip(da, db):
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
+    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
