@@ -543,7 +543,9 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                           kMaxHits + 1;
     Q_BUF(int, s_idx, kSIdx, (size_t)R * max_steps * sizeof(int));
     Q_BUF(float, s_depth, kSDepth, (size_t)R * max_steps * sizeof(float));
-    Q_BUF(float, s_dist, kSDist, (size_t)R * max_steps * sizeof(float));
+    // the sampler's distance rows (render_helpers' sampled_dists) are not read
+    // on this path: the sampler skips them (nullptr)
+    float *const s_dist = nullptr;
     Q_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
     Q_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
     // the statistics as the device-sized forward reads them (the read-back zeroes `stats`)

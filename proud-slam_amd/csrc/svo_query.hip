@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
     int *oi = s_idx + (int64_t)il * max_steps_cap;
     float *od = s_depth + (int64_t)il * max_steps_cap;
-    float *os = s_dist + (int64_t)il * max_steps_cap;
+    float *os = s_dist ? s_dist + (int64_t)il * max_steps_cap : nullptr;  // the engine reads no distances
     const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
     const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
     int count = 0;
@@ -1329,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
             // voxel_helpers.py:654-656: clamp dists, MAX_DEPTH / 0 where idx == -1
             oi[s] = v;
             od[s] = v == -1 ? kMaxDepthFill : dep;
-            os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
+            if (os) os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
             count += (v != -1);
         },
         lane, W);
@@ -1337,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     for (int s = s_written + lane; s < cap; s += kWave) {  // up to max_steps: readers stop at S_max <= max_steps
         oi[s] = -1;
         od[s] = kMaxDepthFill;
-        os[s] = 0.0f;
+        if (os) os[s] = 0.0f;
     }
     count = wave_sum(count);
     if (lane == 0) ray_ns[il] = count;
