@@ -436,7 +436,11 @@ typedef struct psvo_map_desc {
     uint8_t *emb_row_local;
 } psvo_map_desc;
 
-enum { PSVO_STEP_NO_ADAM = 1 }; /* psvo_map_step flags */
+/* psvo_map_step / psvo_map_step_frames flags: NO_ADAM stops after the
+ * gradients (then psvo_map_adam); NO_LOSS skips the loss value (loss_out is
+ * not written — the gradients do not need it; data parallel, every rank must
+ * pass the same flags: the loss sums' collective is skipped too) */
+enum { PSVO_STEP_NO_ADAM = 1, PSVO_STEP_NO_LOSS = 4 };
 
 int64_t psvo_map_grad_floats(int64_t n_emb);                 /* width 128 */
 int64_t psvo_map_grad_floats_w(int64_t n_emb, int width);
@@ -592,6 +596,11 @@ typedef struct psvo_map_frames {
     const float *next_dirs_cam;  /* NULL: no look-ahead */
     uint64_t next_seed;
     void *next_stream;           /* hipStream_t producing next_dirs_cam, or NULL */
+    /* optional: the next call's gt_depth (same storage).  On one GPU with
+     * PSVO_STEP_NO_LOSS the look-ahead's sampler then also counts the
+     * Criterion's normalisers (criterion.py:70-101), so the next step needs no
+     * separate count pass; NULL: the next step counts them itself. */
+    const float *next_gt_depth;
 } psvo_map_frames;
 int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *frames,
                          const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,
@@ -603,8 +612,26 @@ int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_
                     uint64_t seed, int64_t adam_step, int flags, float *pose_grad, float *loss_out, int *stats_out);
 
 /* Both Adam steps of the iteration from desc->grad_flat (one launch; the
- * embedding gradient is zeroed as it is consumed). */
+ * embedding gradient is zeroed as it is consumed).  With emb_row_flags the
+ * embedding step is row-sparse when the flags are known to hold every row
+ * with a gradient: always on one GPU (the step marked them); in data-parallel
+ * mode (psvo_engine_set_exchange) only with PSVO_ADAM_ROWS_EXCHANGED — the
+ * caller's gradient exchange marked the union of all ranks' rows
+ * (psvo_rows_mark / psvo_rows_flags_from_grad).  Otherwise the step is dense
+ * and the flags are refreshed from the moments (psvo_adam_flags_from_state)
+ * and emb_row_local cleared.  psvo_map_adam = psvo_map_adam_ex(…, 0). */
+enum { PSVO_ADAM_ROWS_EXCHANGED = 1 };
 int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step);
+int psvo_map_adam_ex(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step, int flags);
+/* `stream` waits for the optimiser step a look-ahead psvo_map_step_frames
+ * left running on the engine's side stream (its weights are pending until
+ * then; every engine call joins it itself). */
+int psvo_map_join(psvo_engine *e, void *stream);
+/* The last mapping step's per-ray loss gradients d rays_o / d rays_d (the
+ * interpolation backward's ray sums, what the keyframe pose gradient is
+ * formed from) into grad_o / grad_d f32[n_rays, 3], original ray order; rows
+ * of rays that hit nothing are undefined.  n_rays must be that step's. */
+int psvo_engine_grad_rays(psvo_engine *e, void *stream, int64_t n_rays, float *grad_o, float *grad_d);
 
 /* ---- octree builder on the device (csrc/octree_gpu.hip) ----------------
  * The same tree as psvo_octree_* (Octree::insert, octree.cpp:104-294: ids in

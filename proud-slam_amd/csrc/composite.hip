@@ -218,7 +218,7 @@ template <int J>
 __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max, float tr, float max_depth,
                                                         const int *__restrict__ offsets,
                                                         const int *__restrict__ ray_ns,
-                                                        const float *__restrict__ z_vals,
+                                                        const float *__restrict__ z_vals, int z_stride,
                                                         const int *__restrict__ rank_ray,
                                                         const float *__restrict__ gt_rgb,
                                                         const float *__restrict__ gt_depth,
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const float d = gt_depth[orig];
     const float gt0 = gt_rgb[orig * 3 + 0], gt1 = gt_rgb[orig * 3 + 1], gt2 = gt_rgb[orig * 3 + 2];
     const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
-    const float *z = z_vals + r * s_max;
+    const float *z = z_vals + r * z_stride;  // the sampler row ([R, cap]) or the padded [R_hit, S_max] row
     auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
     constexpr int JR = J > 0 ? J : 1;
     float zr[JR], pr[JR], c0r[JR], c1r[JR], c2r[JR];
@@ -422,12 +422,32 @@ extern "C" int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float 
     return check_launch("composite_bwd");
 }
 
+namespace psvo {
+// psvo_composite_loss reading z from rows of stride z_stride >= s_max (the
+// sampler's [R, cap] depth rows: the engine skips the padded [R_hit, S_max]
+// copy; entries s_max..z_stride are never read)
+int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
+                     const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
+                     const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
+                     float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
+}  // namespace psvo
+
 extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
                                    const int *offsets, const int *ray_ns, const float *z_vals, const int *rank_ray,
                                    const float *gt_rgb, const float *gt_depth, const float *sdf_s,
                                    const float *rgb_s, const float *coef, float *workspace, float *color,
                                    float *depth, float *grad_sdf_s, float *grad_rgb_s) {
-    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_loss: bad sizes");
+    return psvo::composite_loss_z(stream, r_hit, s_max, truncation, max_depth, offsets, ray_ns, z_vals, s_max,
+                                  rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace, color, depth, grad_sdf_s,
+                                  grad_rgb_s);
+}
+
+int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                           const int *offsets, const int *ray_ns, const float *z_vals, int z_stride,
+                           const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *sdf_s,
+                           const float *rgb_s, const float *coef, float *workspace, float *color, float *depth,
+                           float *grad_sdf_s, float *grad_rgb_s) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max, "composite_loss: bad sizes");
     PSVO_REQUIRE(offsets && ray_ns && z_vals && rank_ray && gt_rgb && gt_depth && sdf_s && rgb_s && coef &&
                      workspace && color && depth && grad_sdf_s && grad_rgb_s,
                  "composite_loss: null pointer");
@@ -438,7 +458,7 @@ extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float
                 : s_max <= 512 ? k_composite_loss<8>
                                : k_composite_loss<0>;
     hipLaunchKernelGGL(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
-                       max_depth, offsets, ray_ns, z_vals, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace,
-                       color, depth, grad_sdf_s, grad_rgb_s);
+                       max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
+                       workspace, color, depth, grad_sdf_s, grad_rgb_s);
     return check_launch("composite_loss");
 }

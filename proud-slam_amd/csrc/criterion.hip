@@ -222,12 +222,13 @@ __global__ __launch_bounds__(256) void k_crit_bwd(int64_t r_hit, int s_max, floa
 __global__ __launch_bounds__(256) void k_crit_counts(int64_t r_hit, int s_max, float tr, float max_depth,
                                                      const int *__restrict__ rank_ray,
                                                      const float *__restrict__ gt_depth,
-                                                     const float *__restrict__ z_vals, float *__restrict__ part) {
+                                                     const float *__restrict__ z_vals, int z_stride,
+                                                     float *__restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const float d = gt_depth[rank_ray[r]];
-    const float *z = z_vals + r * s_max;
+    const float *z = z_vals + r * z_stride;
     float nf = 0.f, ns = 0.f;
     for (int s = lane; s < s_max; s += 64) {
         const SampleTerms t = sample_terms(z[s], 1.0f, d, tr, max_depth);
@@ -249,16 +250,10 @@ __global__ __launch_bounds__(256) void k_crit_counts(int64_t r_hit, int s_max, f
 __global__ void k_crit_coef(const double *__restrict__ sums, double n_hit, double n_cols, float rgb_w, float depth_w,
                             float fs_w, float sdf_w, float tr, int flags, float *__restrict__ coef) {
     if (threadIdx.x != 0) return;
-    const double n_el = n_hit * n_cols;
-    const float n_valid = (float)sums[kNValid];
-    const float n_f = (float)sums[kNFront], n_s = (float)sums[kNSdf];
-    const float n_tot = n_s + n_f;
-    const float fs_weight = 1.0f - n_f / n_tot;
-    const float sdf_weight = 1.0f - n_s / n_tot;
-    coef[0] = (flags & kFlagColor) ? (float)(rgb_w / (3.0 * n_hit)) : 0.0f;
-    coef[1] = (flags & kFlagDepth) ? depth_w / n_valid : 0.0f;
-    coef[2] = (flags & kFlagSdf) ? (float)(2.0 * (double)(fs_w * fs_weight) / n_el) : 0.0f;
-    coef[3] = (flags & kFlagSdf) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
+    static_assert(kFlagColor == PSVO_CRIT_USE_COLOR && kFlagDepth == PSVO_CRIT_USE_DEPTH &&
+                  kFlagSdf == PSVO_CRIT_USE_SDF, "flag bits");
+    crit_coef_from_counts(sums[kNValid], sums[kNFront], sums[kNSdf], n_hit, n_cols, rgb_w, depth_w, fs_w, sdf_w, tr,
+                          flags, coef);
 }
 
 // tracking's depth filter (criterion.py:45-50): per hit ray
@@ -362,9 +357,18 @@ extern "C" int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float
                                    float *coef) {
     PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_coef: bad sizes");
     PSVO_REQUIRE(rank_ray && gt_depth && z_vals && workspace && sums && coef, "criterion_coef: null pointer");
+    return psvo::criterion_coef_z(stream, r_hit, s_max, truncation, max_depth, rank_ray, gt_depth, z_vals, s_max,
+                                  rgb_w, depth_w, fs_w, sdf_w, flags, workspace, sums, coef);
+}
+
+int psvo::criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
+                           const int *rank_ray, const float *gt_depth, const float *z_vals, int z_stride, float rgb_w,
+                           float depth_w, float fs_w, float sdf_w, int flags, float *workspace, double *sums,
+                           float *coef) {
+    PSVO_REQUIRE(z_stride >= s_max, "criterion_coef: z stride %d < S_max %d", z_stride, s_max);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
-                       rank_ray, gt_depth, z_vals, workspace);
+                       rank_ray, gt_depth, z_vals, z_stride, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
@@ -379,7 +383,7 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
                      const float *gt_depth, const float *z_vals, float *workspace, double *sums) {
     if (r_hit > 0)
         hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
-                           max_depth, rank_ray, gt_depth, z_vals, workspace);
+                           max_depth, rank_ray, gt_depth, z_vals, s_max, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");

@@ -25,7 +25,7 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kStatsKeep, kBlkOut, kQSlots };
+             kOffsets, kStatsKeep, kBlkOut, kRayCnt, kCoefQ, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -45,7 +45,8 @@ struct Arena {
 // updates), so the step that consumes it finds its sizes already on the host.
 struct QuerySet {
     Arena a;                      // slots kStats..kOffsets
-    int *host_stats = nullptr;    // coherent pinned, PSVO_STAT_WORDS + the landing flag
+    unsigned long long *host_raw = nullptr;  // coherent pinned, PSVO_STAT_WORDS {seq, value} granules
+    int host_stats[PSVO_STAT_WORDS] = {};     // the values of the last statistics that landed
     int seq = 0;                  // the flag value the current statistics carry
     hipStream_t qstream = nullptr;  // the stream the query was queued on
     const int *stats_zeroed = nullptr;  // the device statistics buffer a completed read-back left zeroed
@@ -57,6 +58,9 @@ struct QuerySet {
     int64_t R = 0;
     const float *ro = nullptr, *rd = nullptr;
     const float *dirs = nullptr;  // a psvo_map_step_frames look-ahead: the camera directions it was made from
+    // the GT depths the sampler counted the Criterion's normalisers with
+    // (coefficients in slot kCoefQ), or null: the step computes them itself
+    const float *counts_gt = nullptr;
     uint64_t seed = 0;
     int max_steps = 0;
 };
@@ -196,11 +200,12 @@ int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
     return PSVO_OK;
 }
 
-// The host spins on the landing flag the device writes after the statistics
-// (k_stats_to_host: system-scope release) — it sees them as soon as they
-// land, without the event's completion-signal round trip; the event recorded
-// after that kernel (or, without one, the query's stream) is still queried
-// now and then so a failed stream ends the wait with its error.
+// The host spins on the statistics granules the device writes (each word
+// tagged with the query's seq, relaxed system-scope stores: stat_to_host) —
+// it sees them as soon as they land, without the event's completion-signal
+// round trip and without a system-scope release on the device; the event
+// recorded after that kernel (or, without one, the query's stream) is still
+// queried now and then so a failed stream ends the wait with its error.
 // PSVO_HOST_WAIT_STATS=1: the host's time in these waits, printed when the
 // engine is freed (is the iteration host-bound? a host that never waits is)
 struct HostWait {
@@ -213,43 +218,54 @@ inline double now_ns() {
     clock_gettime(CLOCK_MONOTONIC, &t);
     return t.tv_sec * 1e9 + t.tv_nsec;
 }
-int spin_wait_impl(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who);
-int spin_wait(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who) {
+// every granule tagged `seq`: decode the values into out
+bool stats_landed(const unsigned long long *raw, int seq, int *out) {
+    int v[PSVO_STAT_WORDS];
+    for (int k = 0; k < PSVO_STAT_WORDS; ++k) {
+        const unsigned long long g = __atomic_load_n(raw + k, __ATOMIC_ACQUIRE);
+        if ((int)(g >> 32) != seq) return false;
+        v[k] = (int)(unsigned)g;
+    }
+    memcpy(out, v, sizeof(v));
+    return true;
+}
+int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who);
+int spin_wait(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) {
     static const bool on = getenv("PSVO_HOST_WAIT_STATS") && *getenv("PSVO_HOST_WAIT_STATS") == '1';
-    if (!on) return spin_wait_impl(host_stats, seq, ev, qs, who);
-    const bool ready = __atomic_load_n(host_stats + PSVO_STAT_WORDS, __ATOMIC_ACQUIRE) == seq;
+    if (!on) return spin_wait_impl(q, ev, qs, who);
+    int tmp[PSVO_STAT_WORDS];
+    const bool ready = stats_landed(q.host_raw, q.seq, tmp);
     const double t0 = now_ns();
-    const int rc = spin_wait_impl(host_stats, seq, ev, qs, who);
+    const int rc = spin_wait_impl(q, ev, qs, who);
     g_host_wait.ns += now_ns() - t0;
     g_host_wait.calls += 1;
     g_host_wait.spun += ready ? 0 : 1;
     return rc;
 }
-int spin_wait_impl(const int *host_stats, int seq, hipEvent_t ev, hipStream_t qs, const char *who) {
-    const int *flag = host_stats + PSVO_STAT_WORDS;
+int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) {
     // the runtime query (error detection only) costs microseconds: at most one
-    // per 0.5 ms of waiting, so the flag is seen as soon as it lands
+    // per 0.5 ms of waiting, so the statistics are seen as soon as they land
     double next_query = now_ns() + 5e5;
     for (unsigned it = 1;; ++it) {
-        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
+        if (stats_landed(q.host_raw, q.seq, q.host_stats)) return PSVO_OK;
         if ((it & 255) == 0 && now_ns() >= next_query) {
             next_query = now_ns() + 5e5;
-            const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(qs);
-            if (q == hipErrorNotReady) continue;
-            if (q != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(q));
+            const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(qs);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: stats read-back: %s", who, hipGetErrorString(e));
             // the event (no system-scope fence) may complete just before the
-            // kernel's own system-scope flag store is visible: poll a while more
+            // kernel's system-scope granule stores are visible: poll a while more
             for (unsigned k = 0; k < (1u << 22); ++k)
-                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return PSVO_OK;
-            return set_error(PSVO_E_LAUNCH, "%s: stats read-back: event complete, flag %d != %d", who,
-                             __atomic_load_n(flag, __ATOMIC_ACQUIRE), seq);
+                if (stats_landed(q.host_raw, q.seq, q.host_stats)) return PSVO_OK;
+            return set_error(PSVO_E_LAUNCH, "%s: stats read-back: event complete, granules not tagged %d", who,
+                             q.seq);
         }
     }
 }
 
 int query_set_init(QuerySet &s) {
-    if (s.host_stats) return PSVO_OK;
-    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_stats), (PSVO_STAT_WORDS + 1) * sizeof(int),
+    if (s.host_raw) return PSVO_OK;
+    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_raw), PSVO_STAT_WORDS * sizeof(unsigned long long),
                       hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
         // device-side ordering only: the statistics reach the host through the
@@ -257,14 +273,14 @@ int query_set_init(QuerySet &s) {
         hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
         hipEventCreateWithFlags(&s.freed, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: query set allocation failed");
-    memset(s.host_stats, 0, (PSVO_STAT_WORDS + 1) * sizeof(int));  // flag 0: no statistics yet (seq starts at 1)
+    memset(s.host_raw, 0, PSVO_STAT_WORDS * sizeof(unsigned long long));  // tag 0: no statistics yet (seq from 1)
     return PSVO_OK;
 }
 
 void query_set_free(QuerySet &s) {
     for (int k = 0; k < kQSlots; ++k)
         if (s.a.p[k]) (void)hipFree(s.a.p[k]);
-    if (s.host_stats) (void)hipHostFree(s.host_stats);
+    if (s.host_raw) (void)hipHostFree(s.host_raw);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.freed) (void)hipEventDestroy(s.freed);
 }
@@ -472,16 +488,34 @@ static int map_adam(hipStream_t st, const psvo_map_desc *d, float *grads, int64_
     return adam_launch(st, cnt, p, g, m, v, n, lr, d->beta1, d->beta2, d->eps, 0.0, adam_step, zero, steps, rows);
 }
 
-extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
+extern "C" int psvo_map_adam_ex(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step,
+                                int flags) {
     PSVO_REQUIRE(e && d && d->grad_flat && adam_step >= 1, "map_adam: needs desc->grad_flat and adam_step >= 1");
     e->images_next = false;  // the weights may change before the next step
-    ENG_CALL(join_adam(e, as_stream(stream), "map_adam"));
-    // sparse-exact when the row flags exist: a single-GPU step marked its rows
-    // (also under PSVO_STEP_NO_ADAM); data parallel, the gradient exchange
-    // marked the union of all ranks' rows
-    ENG_CALL(map_adam(as_stream(stream), d, d->grad_flat, adam_step, nullptr, d->emb_row_flags != nullptr));
+    hipStream_t st = as_stream(stream);
+    ENG_CALL(join_adam(e, st, "map_adam"));
+    // sparse-exact when the row flags hold every row with a gradient: a
+    // single-GPU step marked its rows itself (also under PSVO_STEP_NO_ADAM);
+    // data parallel, only the gradient exchange knows the union of all ranks'
+    // rows, so the caller says it marked them (PSVO_ADAM_ROWS_EXCHANGED)
+    const bool flags_complete = !e->x.on() || (flags & PSVO_ADAM_ROWS_EXCHANGED);
+    const bool sparse = d->emb_row_flags != nullptr && flags_complete;
+    ENG_CALL(map_adam(st, d, d->grad_flat, adam_step, nullptr, sparse));
+    if (d->emb_row_flags && !sparse) {
+        // dense step under the exchange without a union mark (one unforced
+        // rank, a caller's own all-reduce): keep the flags sticky-complete —
+        // every row whose moments are now non-zero — so a later sparse step
+        // still steps them; this rank's marks are spent
+        ENG_CALL(psvo_adam_flags_from_state(st, d->n_emb, d->emb_m, d->emb_v, d->emb_row_flags));
+        if (d->emb_row_local && hipMemsetAsync(d->emb_row_local, 0, (size_t)d->n_emb, st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_adam: memset failed");
+    }
     e->grads_clean = true;
     return PSVO_OK;
+}
+
+extern "C" int psvo_map_adam(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t adam_step) {
+    return psvo_map_adam_ex(e, stream, d, adam_step, 0);
 }
 
 namespace {
@@ -494,6 +528,7 @@ struct Render {
     float *tt, *z_vals, *feat, *images, *sdf_s, *rgb_s, *act, *sdf, *weights, *color, *depth;
     uint64_t *masks;
     bool z_recorded = false;  // e->z_ready marks the sample compaction on st (aux has not waited yet)
+    int z_stride = 0;         // row stride of z_vals: s_max (padded copy) or the sampler's row capacity
 };
 
 #define Q_BUF(T, name, slot, bytes)                                              \
@@ -509,7 +544,7 @@ struct Render {
 // max_steps; an overflow is flagged and reported by the consumer).
 int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_desc *d, int64_t R,
                   const float *rays_o, const float *rays_d, uint64_t seed, const char *who,
-                  const float *noise = nullptr, bool record_done = true) {
+                  const float *noise = nullptr, bool record_done = true, const float *counts_gt = nullptr) {
     int rc = PSVO_OK;
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (q.stats_zeroed != stats && hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
@@ -560,12 +595,24 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         ENG_CALL(dist_smax(st, x.xi32 + x.smax_all_off(), x.world, stats));
     }
     q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
-    if (!x.on())  // the sampler's scan does the read-back
+    q.counts_gt = nullptr;
+    if (!x.on()) {  // the sampler's scan does the read-back (and, given the GT depths, the loss normalisers)
+        psvo::SampleCounts sc{};
+        const bool counts = counts_gt && psvo::sampler_counts(R);
+        if (counts) {
+            Q_BUF(int, ray_cnt, kRayCnt, (size_t)R * sizeof(int));
+            Q_BUF(float, coefq, kCoefQ, 4 * sizeof(float));
+            sc = psvo::SampleCounts{counts_gt, ray_cnt, coefq, d->truncation, d->max_depth, d->w_rgb, d->w_depth,
+                                    d->w_fs, d->w_sdf,
+                                    PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF};
+            q.counts_gt = counts_gt;
+        }
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
-                                           q.host_stats, q.seq, stats_keep));
+                                           q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr));
+    }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
-    if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_stats, PSVO_STAT_WORDS, q.seq));
+    if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_raw, PSVO_STAT_WORDS, q.seq));
     q.stats_zeroed = stats;
     q.done_recorded = record_done;
     if (record_done && hipEventRecord(q.done, st) != hipSuccess)
@@ -584,7 +631,8 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
 // psvo_map_query prepared for exactly this batch, or a fresh query enqueued
 // on `st` itself.
 int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R, const float *rays_o,
-               const float *rays_d, uint64_t seed, const char *who, QuerySet **out, const float *noise = nullptr) {
+               const float *rays_d, uint64_t seed, const char *who, QuerySet **out, const float *noise = nullptr,
+               const float *counts_gt = nullptr) {
     if (e->q_count > 0) {
         QuerySet &q = e->qs[e->q_head];
         if (q.R != R || q.ro != rays_o || q.rd != rays_d || q.seed != seed)
@@ -602,7 +650,7 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
         return PSVO_OK;
     }
     QuerySet &q = e->qs[e->q_head];
-    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, seed, who, noise));
+    ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, seed, who, noise, true, counts_gt));
     *out = &q;
     return PSVO_OK;
 }
@@ -756,7 +804,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         act = act_b, masks = masks_b;
         dev_done = true;  // unless the batch turns out not to fit
     }
-    ENG_CALL(spin_wait(qset.host_stats, qset.seq, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
+    ENG_CALL(spin_wait(qset, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
     // data-parallel: this rank's hit rays, padded to the union's S_max
@@ -798,9 +846,31 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         // 0.96-0.99 vs 0.94-0.96 ms per iteration, so the split stays default.
         const char *sp = getenv("PSVO_FUSED_POINTS");
         const bool fuse_pi = sp && *sp == '1';
-        if (fuse_pi) ENG_CALL(join_adam(e, st, who));
-        mark(e, st, PSVO_TIME_POINTS, 0);
-        if (fuse_pi) {
+        // the mapping step on one GPU: no padded [R_hit, S_max] copy at all —
+        // the loss kernels read z from the sampler's depth rows, and the
+        // compaction happens inside the interpolation (k_interp_fwd_rays, one
+        // wave per hit ray); PSVO_SPLIT_QUERY=1 keeps the separate kernels
+        const char *sq = getenv("PSVO_SPLIT_QUERY");
+        const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(sq && *sq == '1');
+        if (rays_path) {
+            // the loss normalisers need only z: aux may start them now
+            if (engine_overlap(e)) {
+                if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                    return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+                o.z_recorded = true;
+            }
+            ENG_CALL(join_adam(e, st, who));
+            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+            ENG_CALL(psvo::interp_fwd_rays(st, r_hit, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray,
+                                           rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b,
+                                           ray_of_b, feat_b, psvo::DevBatch{}));
+            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+            z_b = const_cast<float *>(s_depth);
+            o.z_stride = max_steps;
+        }
+        if (!rays_path) mark(e, st, PSVO_TIME_POINTS, 0);
+        if (rays_path) {
+        } else if (fuse_pi) {
             ENG_CALL(psvo::points_interp(st, r_hit, s_max, max_steps, d->voxel_size, s_idx, s_depth, offsets, leaf_b,
                                          tt_b, ray_of_b, z_b, smask, rank_ray, rays_o, rays_d, d->centres,
                                          d->vertex_idx, d->emb, feat_b));
@@ -808,7 +878,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf_b,
                                         tt_b, ray_of_b, z_b, smask));
         }
-        mark(e, st, PSVO_TIME_POINTS, 1);
+        if (!rays_path) mark(e, st, PSVO_TIME_POINTS, 1);
         if (fuse_pi) {  // the interpolation ran inside the points region
             mark(e, st, PSVO_TIME_INTERP_FWD, 0);
             mark(e, st, PSVO_TIME_INTERP_FWD, 1);
@@ -816,14 +886,14 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         // the loss normalisers can start now (psvo_map_step, on aux; the host
         // issues aux's wait after the decoder launch: queued before it, their
         // three launches delay the forward's — measured 1.2 % slower)
-        if (fused_loss && engine_overlap(e)) {
+        if (fused_loss && engine_overlap(e) && !rays_path) {
             if (hipEventRecord(e->z_ready, st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
             o.z_recorded = true;
         }
         // ---- forward: interpolation, decoder, compositing (after the previous
         // step's optimiser step when its tail ran on aux)
-        if (!fuse_pi) {
+        if (!fuse_pi && !rays_path) {
             ENG_CALL(join_adam(e, st, who));
             mark(e, st, PSVO_TIME_INTERP_FWD, 0);
             ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
@@ -865,6 +935,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.ray_of = ray_of;
     o.tt = tt;
     o.z_vals = z_vals;
+    if (o.z_stride == 0) o.z_stride = s_max;
     o.feat = feat;
     o.images = images;
     o.sdf_s = sdf_s;
@@ -994,7 +1065,7 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
                                     grad_od, grad_od + R * 3, fr->poses, fr->pose_m, fr->pose_v, fr->pose_step,
                                     fr->lr_pose, d->beta1, d->beta2, d->eps, pg, fr->next_dirs_cam, rays_o, rays_d));
     ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)", nullptr,
-                           record_done));
+                           record_done, fr->next_gt_depth));
     q.dirs = fr->next_dirs_cam;
     q.pending = true;
     e->q_count++;
@@ -1014,7 +1085,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const int64_t R = n_rays;
     Render q;
     QuerySet *qset = nullptr;
-    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise));
+    // the normalisers from the sampler's tail: single GPU, and only when the
+    // loss value is not wanted (its reduction reads the counts k_crit_counts
+    // writes into the loss partials)
+    const bool want_loss = !(flags & PSVO_STEP_NO_LOSS);
+    const float *counts_gt = (!e->x.on() && !want_loss) ? gt_depth : nullptr;
+    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise, counts_gt));
     QueryGuard guard{e, st, qset};
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
@@ -1027,6 +1103,19 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         if (hipEventRecord(e->next_ready, as_stream(fr->next_stream)) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     }
+    // Cross-stream waits cost the critical stream a few microseconds each
+    // wherever they sit between two of its kernels.  The ones this step needs
+    // on st anyway — the previous step's optimiser (before the interpolation
+    // reads the embeddings) and, split, the draw of the next pixels (before
+    // the look-ahead's pose step) — are queued here, in front of the render:
+    // st reaches them right after the queued query's sampler, while the host
+    // is still reading that query's statistics back, so they cost nothing.
+    const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_fuses_interp(d->width) &&
+                            !(flags & PSVO_STEP_NO_ADAM);
+    const bool early_next = wait_next && split_tail;
+    if (early_next && hipStreamWaitEvent(st, e->next_ready, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
+    ENG_CALL(join_adam(e, st, "map_step"));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
@@ -1052,7 +1141,13 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         sums_c = sc;
         sums = sl;
     }
-    ENG_BUF(float, coef, kCoef, 4 * sizeof(float));
+    // the sampler counted the normalisers for exactly this GT (its tail wrote the coefficients)
+    const bool coef_q = counts_gt && qset->counts_gt == counts_gt;
+    float *coef = coef_q ? static_cast<float *>(qset->a.p[kCoefQ]) : nullptr;
+    if (!coef_q) {
+        ENG_BUF(float, cbuf, kCoef, 4 * sizeof(float));
+        coef = cbuf;
+    }
     ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
     ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
     ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
@@ -1072,11 +1167,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_CALL(x.call(PSVO_XCH_SUM_F64, 0, 0, 8, ax, "loss normalisers"));
         ENG_CALL(criterion_coef_from_sums(ax, sums_c, n_hit, s_max, d->truncation, d->w_rgb, d->w_depth, d->w_fs,
                                           d->w_sdf, crit_flags, coef));
-    } else {
-        ENG_CALL(psvo_criterion_coef(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth, q.z_vals,
-                                     d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
+    } else if (!coef_q) {
+        ENG_CALL(psvo::criterion_coef_z(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
+                                        q.z_vals, q.z_stride, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags,
+                                        crit_ws, sums_c, coef));
     }
-    ENG_CALL(fork_join(ax, st, e->coef_ready));
+    if (!coef_q) ENG_CALL(fork_join(ax, st, e->coef_ready));
     // after the normalisers: the fused loss pass waits for them, Adam for the marks
     // (width 128: the fused backward's embedding scatter flags the rows it touches instead — the mark
     // kernel beside the decoder forward slowed it by ≈ 17 µs)
@@ -1084,25 +1180,30 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (mark_into && !empty && !marks_in_bwd)
         ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, mark_into));
     if (!empty)
-        ENG_CALL(psvo_composite_loss(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
-                                     q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef, crit_ws, color, depth,
-                                     g_sdf_s, g_rgb_s));
+        ENG_CALL(psvo::composite_loss_z(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns,
+                                        q.z_vals, q.z_stride, q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef,
+                                        crit_ws, color, depth, g_sdf_s, g_rgb_s));
     // the loss value (not on the gradient path), beside the decoder backward:
     // data parallel on aux (its collective), single GPU on its own stream,
     // joined into st before the optimiser step (loss_out / crit_ws ordered)
+    // PSVO_STEP_NO_LOSS: the caller does not read the value (bundle_adjust_frames
+    // discards it, render_helpers.py:662-676): no reduction, no collective (every
+    // rank passes the same flags)
     hipStream_t lq = (overlap && !dist) ? e->lossq : ax;
-    ENG_CALL(fork_join(st, lq, e->grads_ready));
-    if (!empty) {
-        ENG_CALL(psvo_criterion_reduce(lq, r_hit, crit_ws, sums));
-    } else if (hipMemsetAsync(sums, 0, 8 * sizeof(double), lq) != hipSuccess) {
-        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+    if (want_loss) {
+        ENG_CALL(fork_join(st, lq, e->grads_ready));
+        if (!empty) {
+            ENG_CALL(psvo_criterion_reduce(lq, r_hit, crit_ws, sums));
+        } else if (hipMemsetAsync(sums, 0, 8 * sizeof(double), lq) != hipSuccess) {
+            return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+        }
+        if (dist) ENG_CALL(x.call(PSVO_XCH_SUM_F64, 8, 8, 8, lq, "loss sums"));
+        ENG_CALL(psvo_criterion_finalize(lq, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
+                                         d->truncation, crit_flags, loss_out));
+        if (lq != ax && hipEventRecord(e->loss_done, lq) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     }
-    if (dist) ENG_CALL(x.call(PSVO_XCH_SUM_F64, 8, 8, 8, lq, "loss sums"));
-    ENG_CALL(psvo_criterion_finalize(lq, sums, n_hit, s_max, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf,
-                                     d->truncation, crit_flags, loss_out));
-    if (lq != ax && hipEventRecord(e->loss_done, lq) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
-    const bool join_loss = lq != ax;
+    const bool join_loss = want_loss && lq != ax;
     const int n_split = 256;
     ENG_BUF(float, mlp_ws, kMlpWs, psvo_mlp_workspace_floats_w(M, d->width, n_split) * sizeof(float));
     ENG_BUF(float, dfeat, kDfeat, M * 16 * sizeof(float));
@@ -1223,7 +1324,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         (hipEventRecord(e->emb_done, eb) != hipSuccess || hipStreamWaitEvent(st, e->emb_done, 0) != hipSuccess))
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     // the loss value's reads of crit_ws before the next step's writes: through
-    // st, or (split) through aux's optimiser step, which the next render waits for
+    // st, or (split) through aux's optimiser step, which the next render waits
+    // for; split, st joins it too once the look-ahead is queued (below)
     if (join_loss && hipStreamWaitEvent(split ? ax : st, e->loss_done, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     e->tm.pending = e->tm.on;
@@ -1234,7 +1336,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // next iteration's rays + query there too — beside this step's weight
     // gradients and the map's Adam
     if (ahead) {
-        if (wait_next && hipStreamWaitEvent(eb, e->next_ready, 0) != hipSuccess)
+        if (wait_next && !early_next && hipStreamWaitEvent(eb, e->next_ready, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
         // queued on the step's own stream (split tail): consumed there, no event
         ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od, eb != st));
@@ -1261,7 +1363,31 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     } else {
         ENG_CALL(pose_adam(st, d, pa));
     }
+    // split tail: loss_out is written on the loss stream; the caller reads it
+    // on st (the loss pass ends long before the look-ahead's pose step, so
+    // this wait, queued behind the look-ahead, costs nothing).  The weights
+    // stay pending on aux until the next engine call or psvo_map_join.
+    if (split && join_loss && hipStreamWaitEvent(st, e->loss_done, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: stream join failed");
     return PSVO_OK;
+}
+
+extern "C" int psvo_engine_grad_rays(psvo_engine *e, void *stream, int64_t n_rays, float *grad_o, float *grad_d) {
+    PSVO_REQUIRE(e && grad_o && grad_d && n_rays > 0, "engine_grad_rays: bad arguments");
+    const size_t bytes = (size_t)n_rays * 3 * sizeof(float);
+    PSVO_REQUIRE(e->a.p[kGradOD] && e->a.cap[kGradOD] >= 2 * bytes, "engine_grad_rays: no step of %lld rays ran",
+                 (long long)n_rays);
+    const float *g = static_cast<const float *>(e->a.p[kGradOD]);
+    hipStream_t st = as_stream(stream);
+    if (hipMemcpyAsync(grad_o, g, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(grad_d, g + n_rays * 3, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine_grad_rays: copy failed");
+    return PSVO_OK;
+}
+
+extern "C" int psvo_map_join(psvo_engine *e, void *stream) {
+    PSVO_REQUIRE(e, "map_join: null engine");
+    return join_adam(e, as_stream(stream), "map_join");
 }
 
 extern "C" int psvo_map_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,

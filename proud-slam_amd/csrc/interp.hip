@@ -78,6 +78,71 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
     feat[s * 4 + q] = acc;
 }
 
+// Sample compaction + interpolation forward for the engine's mapping path,
+// one wave per hit ray: the ray's valid samples — the prefix s < ns of its
+// sampler row s_idx / s_depth [R, cap] — go to the compact, ray-major
+// positions offsets[r] + s as leaf / t / ray_of_sample (what the backward
+// reads) and as features; the ray's origin / direction and offsets are loaded
+// once per wave, not per sample.  Four lanes per sample, 16 samples per pass;
+// a pass's lanes idle only past the ray's last sample (the slot-grid
+// k_points_interp below left half its lanes on empty slots).  Same arithmetic
+// as k_interp_fwd, so the same bits.
+__global__ __launch_bounds__(256) void k_interp_fwd_rays(int64_t r_hit, int cap, float voxel_size,
+                                                         const int *__restrict__ s_idx,
+                                                         const float *__restrict__ s_depth,
+                                                         const int *__restrict__ offsets,
+                                                         const int *__restrict__ ray_index,
+                                                         const float *__restrict__ rays_o,
+                                                         const float *__restrict__ rays_d,
+                                                         const float *__restrict__ centres,
+                                                         const int *__restrict__ vertex_idx,
+                                                         const float4 *__restrict__ emb, int *__restrict__ leaf,
+                                                         float *__restrict__ t, int *__restrict__ ray_of_sample,
+                                                         float4 *__restrict__ feat, DevBatch dev) {
+    if (dev.stats) r_hit = dev_batch_fits(dev) ? dev.stats[PSVO_STAT_R_HIT] : 0;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int lane = threadIdx.x & 63;
+    const int q = lane & 3;
+    const int beg = offsets[r], ns = offsets[r + 1] - beg;
+    const int64_t ray = ray_index ? ray_index[r] : r;
+    const float o[3] = {rays_o[ray * 3 + 0], rays_o[ray * 3 + 1], rays_o[ray * 3 + 2]};
+    const float d[3] = {rays_d[ray * 3 + 0], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]};
+    const int *row_i = s_idx + r * cap;
+    const float *row_z = s_depth + r * cap;
+    for (int s = lane >> 2; s < ns; s += kWave / 4) {
+        const int lf = row_i[s];
+        const float ts = row_z[s];
+        const int64_t m = beg + s;
+        if (q == 0) {
+            leaf[m] = lf;
+            t[m] = ts;
+            ray_of_sample[m] = (int)r;
+        }
+        float p[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float x = o[a] + d[a] * ts;
+            p[a] = __fdiv_rn(x - centres[(int64_t)lf * 3 + a], voxel_size) + 0.5f;
+        }
+        float w[8];
+        corner_weights(p[0], p[1], p[2], w);
+        const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8);
+        const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8 + 4);
+        const int vid[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float4 e = emb[(int64_t)vid[k] * 4 + q];
+            acc.x = acc.x + w[k] * e.x;
+            acc.y = acc.y + w[k] * e.y;
+            acc.z = acc.z + w[k] * e.z;
+            acc.w = acc.w + w[k] * e.w;
+        }
+        feat[m * 4 + q] = acc;
+    }
+}
+
 // k_sample_points and k_interp_fwd in one pass over the sampler's [R_hit, cap]
 // rows (engine, host-sized forward): four lanes per (hit ray, step) slot; a
 // valid slot (a prefix of its row) interpolates straight from the sampler's
@@ -429,6 +494,19 @@ extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size,
 }
 
 namespace psvo {
+int interp_fwd_rays(hipStream_t st, int64_t r_hit, int cap, float voxel_size, const int *s_idx, const float *s_depth,
+                    const int *offsets, const int *ray_index, const float *rays_o, const float *rays_d,
+                    const float *centres, const int *vertex_idx, const float *emb, int *leaf, float *t,
+                    int *ray_of_sample, float *feat, const DevBatch &dev) {
+    PSVO_REQUIRE(r_hit >= 0 && cap > 0 && voxel_size > 0.f, "interp_fwd_rays: bad sizes");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_interp_fwd_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, voxel_size, s_idx,
+                       s_depth, offsets, ray_index, rays_o, rays_d, centres, vertex_idx,
+                       reinterpret_cast<const float4 *>(emb), leaf, t, ray_of_sample, reinterpret_cast<float4 *>(feat),
+                       dev);
+    return check_launch("interp_fwd_rays");
+}
+
 int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
                    const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
                    const float *centres, const int *vertex_idx, const float *emb, float *feat) {

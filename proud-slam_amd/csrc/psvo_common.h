@@ -47,17 +47,33 @@ struct PackRec {  // 32 B, 16-B aligned
     int4 i;       // reference node id, first child record (-1: none), child mask, spare (tree_pack.hip)
 };
 
-// the query's statistics words → coherent pinned host memory by one device
-// thread (zeroing them on the device), then host[words] = seq with a
-// system-scope release (the engine's host thread polls that word instead of
-// waiting for an event; svo_query.hip)
-int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq);
+// the query's statistics words → coherent pinned host memory as {seq, value}
+// granules (stat_to_host; zeroing them on the device): the engine's host
+// thread polls the tags instead of waiting for an event (svo_query.hip)
+int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq);
+// The Criterion's normalisers (criterion.py:70-101: the valid-depth rays and
+// the front / sdf samples over the padded [R_hit, S_max] layout) depend only
+// on the samples' depths and the rays' GT depth, so the sampler counts them
+// per ray as it emits samples (ray_cnt i32[R]) and its last workgroup turns
+// the sums into the backward coefficients coef f32[4] (crit_coef_from_counts:
+// k_crit_coef's bits).  gt_depth null: not counted.
+struct SampleCounts {
+    const float *gt_depth;
+    int *ray_cnt;
+    float *coef;
+    float tr, max_depth, w_rgb, w_depth, w_fs, w_sdf;
+    int crit_flags;
+};
 // psvo_sample_rays (single GPU, whole batch) whose scan also does
-// stats_to_host's read-back (svo_query.hip)
+// stats_to_host's read-back (svo_query.hip); with counts (and at most
+// 256 · kTailPasses rays, the in-launch tail) also the normalisers
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, int *host, int seq, int *keep = nullptr);
+                        int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep = nullptr,
+                        const SampleCounts *counts = nullptr);
+// whether sample_rays_to_host computes the counts for a batch of r rays (its in-launch tail)
+bool sampler_counts(int64_t r);
 
 // one element of the Adam step (k_adam; optim.hip's formulation), shared so
 // the fused pose step (pose.hip) computes the same bits
@@ -109,6 +125,27 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef);
 
+struct DevBatch;
+// psvo_criterion_coef / psvo_composite_loss reading z from rows of stride
+// z_stride >= s_max (the sampler's [R, cap] depth rows, the engine's mapping
+// path: no padded [R_hit, S_max] copy)
+int criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
+                     const float *gt_depth, const float *z_vals, int z_stride, float rgb_w, float depth_w, float fs_w,
+                     float sdf_w, int flags, float *workspace, double *sums, float *coef);
+int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
+                     const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
+                     const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
+                     float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
+// sample compaction + interpolation forward, one wave per hit ray (the
+// engine's mapping path, interp.hip k_interp_fwd_rays): the valid prefix of
+// each sampler row s_idx / s_depth [R, cap] goes to compact positions
+// offsets[r] + s — leaf / t / ray_of_sample and the features (k_interp_fwd's
+// arithmetic, the same bits); dev.stats: R_hit from the device statistics
+int interp_fwd_rays(hipStream_t st, int64_t r_hit, int cap, float voxel_size, const int *s_idx, const float *s_depth,
+                    const int *offsets, const int *ray_index, const float *rays_o, const float *rays_d,
+                    const float *centres, const int *vertex_idx, const float *emb, int *leaf, float *t,
+                    int *ray_of_sample, float *feat, const DevBatch &dev);
+
 // width-256 decoder (mlp256.hip): sizes, operand images, forward (act /
 // masks NULL: inference), backward (gw[0] NULL: δ chain to dfeat only)
 int64_t dec256_tiles16(int64_t m);
@@ -133,6 +170,73 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
                const BwdHook *before_dw = nullptr);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
+
+// ---- in-launch hand-off to the last-arriving workgroup ---------------------
+// (cdna_hip_programming.md §5 "in-launch split-K reduction", sc1 form; the
+// per-XCD L2s are not coherent).  Every word another workgroup reads in the
+// same launch is stored write-through (sc1: a relaxed agent-scope atomic store
+// on a global pointer) and read back with sc1 loads, so no release / acquire
+// fence (an L2 write-back / invalidate) is needed; each storing wave drains
+// its stores before the workgroup takes its ticket.
+typedef __attribute__((address_space(1))) int g_i32;
+typedef __attribute__((address_space(1))) float g_f32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ void st_wt(int *p, int v) {
+    __hip_atomic_store((g_i32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(float *p, float v) {
+    __hip_atomic_store((g_f32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_wt(const int *p) {
+    return __hip_atomic_load((g_i32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float *p) {
+    return __hip_atomic_load((g_f32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// true in the last workgroup of the launch to arrive (block-uniform); that
+// workgroup re-zeroes the counter for the next launch (zero before the first)
+__device__ __forceinline__ bool last_block(int *counter, int *lds_word) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int n = (int)(gridDim.x * gridDim.y * gridDim.z);
+        const int t = __hip_atomic_fetch_add((g_i32 *)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_word = t == n - 1;
+        if (t == n - 1) __hip_atomic_store((g_i32 *)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const bool last = *lds_word != 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
+    return last;
+}
+// query statistics to the host: PSVO_STAT_WORDS 8-byte granules {seq, value}
+// written by relaxed system-scope stores into coherent pinned memory — each
+// word carries its own tag, so no system-scope release (an L2 write-back on
+// the critical stream) orders them; the host polls until every tag is seq
+__device__ __forceinline__ void stat_to_host(unsigned long long *host, int word, int v, int seq) {
+    __hip_atomic_store((g_u64 *)(host + word), ((unsigned long long)(unsigned)seq << 32) | (unsigned)v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// the Criterion's backward coefficients from the batch's count sums
+// (criterion.py:70-101; k_crit_coef and the sampler's tail share this, so
+// both give the same bits): coef = {colour, depth, fs, sdf}; flags PSVO_CRIT_USE_*
+__device__ __forceinline__ void crit_coef_from_counts(double n_valid_d, double n_f_d, double n_s_d, double n_hit,
+                                                      double n_cols, float rgb_w, float depth_w, float fs_w,
+                                                      float sdf_w, float tr, int flags, float *coef) {
+    const double n_el = n_hit * n_cols;
+    const float n_valid = (float)n_valid_d;
+    const float n_f = (float)n_f_d, n_s = (float)n_s_d;
+    const float n_tot = n_s + n_f;
+    const float fs_weight = 1.0f - n_f / n_tot;
+    const float sdf_weight = 1.0f - n_s / n_tot;
+    coef[0] = (flags & PSVO_CRIT_USE_COLOR) ? (float)(rgb_w / (3.0 * n_hit)) : 0.0f;
+    coef[1] = (flags & PSVO_CRIT_USE_DEPTH) ? depth_w / n_valid : 0.0f;
+    coef[2] = (flags & PSVO_CRIT_USE_SDF) ? (float)(2.0 * (double)(fs_w * fs_weight) / n_el) : 0.0f;
+    coef[3] = (flags & PSVO_CRIT_USE_SDF) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
+}
+// stats word indices of the two tail counters (zeroed with the statistics)
+constexpr int kStatIsTail = 13, kStatSmpTail = 14;
+constexpr int kTailPasses = 32;  // rays per thread of a 256-thread tail: up to 8192 rays per query
 
 // A device-sized launch of the render's forward (engine: no host read-back
 // before it): the batch's R_hit / S_max / M come from the query's statistics

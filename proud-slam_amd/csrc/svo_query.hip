@@ -411,6 +411,94 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
     return total;
 }
 
+// k_ray_stats_rank for one 256-thread workgroup, the last of the traversal
+// launch to arrive (the traversal's per-ray outputs are sc1-stored; read here
+// with sc1 loads): P, R_hit, max ⌈Σ/step⌉, the AABB tests / rounds, and each
+// hit ray's rank.  Ray i = k·256 + t is thread t's pass k; a pass's hit
+// ballot per wave goes to LDS, one scan of the (pass, wave) counts, then the
+// ranks from the ballots (mbcnt) — nothing held in registers across the
+// passes (this runs inside the traversal kernel: its VGPR budget is the
+// traversal's).  n <= 256 · kTailPasses.
+__device__ __noinline__ void stats_rank_tail(int64_t n, const int *__restrict__ ray_nv,
+                                             const float *__restrict__ ray_dsum, float step_size,
+                                             int *__restrict__ stats, int *__restrict__ ray_rank,
+                                             int *__restrict__ rank_ray, const int *__restrict__ blk_out, int n_blk) {
+    constexpr int kW = 4;  // waves
+    __shared__ uint64_t s_hit[kTailPasses * kW];
+    __shared__ int s_cnt[kTailPasses * kW];
+    __shared__ int s_red[4][kW];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    int v_blk = 0, r_blk = 0;
+    for (int b = tid; b < n_blk; b += 256) {
+        v_blk += ld_wt(blk_out + 2 * b);
+        r_blk += ld_wt(blk_out + 2 * b + 1);
+    }
+    int p = 0, mc = 0;
+    const int passes = (int)((n + 255) / 256);
+    for (int k = 0; k < passes; ++k) {
+        const int64_t i = (int64_t)k * 256 + tid;
+        const int nv = i < n ? ld_wt(ray_nv + i) : 0;
+        const float ds = i < n ? ld_wt(ray_dsum + i) : 0.f;
+        p = max(p, nv);
+        if (nv > 0) mc = max(mc, (int)ceilf(__fdiv_rn(ds, step_size)));
+        const uint64_t m = __ballot(nv > 0);
+        if (lane == 0) {
+            s_hit[k * kW + w] = m;
+            s_cnt[k * kW + w] = __popcll(m);
+        }
+    }
+    p = wave_max(p);
+    mc = wave_max(mc);
+    const int vs = wave_sum(v_blk), rs = wave_sum(r_blk);
+    if (lane == 0) {
+        s_red[0][w] = p;
+        s_red[1][w] = mc;
+        s_red[2][w] = vs;
+        s_red[3][w] = rs;
+    }
+    __syncthreads();
+    static_assert(kTailPasses * kW == 2 * kWave, "one scan pass: two counts per lane");
+    if (w == 0) {  // exclusive scan of the (pass, wave) counts, pass-major (= ray order), two per lane
+        const int a0 = lane * 2 < passes * kW ? s_cnt[lane * 2] : 0;
+        const int a1 = lane * 2 + 1 < passes * kW ? s_cnt[lane * 2 + 1] : 0;
+        int incl = a0 + a1;
+#pragma unroll
+        for (int sh = 1; sh < kWave; sh <<= 1) {
+            const int t = __shfl_up(incl, sh, kWave);
+            if (lane >= sh) incl += t;
+        }
+        s_cnt[lane * 2] = incl - a0 - a1;
+        s_cnt[lane * 2 + 1] = incl - a1;
+        if (lane == kWave - 1) {
+            int pp = 0, mm = 0, vv = 0, rr = 0;
+            for (int k = 0; k < kW; ++k) {
+                pp = max(pp, s_red[0][k]);
+                mm = max(mm, s_red[1][k]);
+                vv += s_red[2][k];
+                rr += s_red[3][k];
+            }
+            stats[PSVO_STAT_P] = pp;
+            stats[PSVO_STAT_R_HIT] = incl;
+            stats[PSVO_STAT_MAX_CEIL] = mm;
+            stats[PSVO_STAT_VISITS] += vv;
+            stats[PSVO_STAT_ROUNDS] += rr;
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < passes; ++k) {
+        const int64_t i = (int64_t)k * 256 + tid;
+        const uint64_t m = s_hit[k * kW + w];
+        if (i < n) {
+            const bool h = (m >> lane) & 1ull;
+            const int rk =
+                s_cnt[k * kW + w] +
+                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            ray_rank[i] = h ? rk : -1;
+            if (h) rank_ray[rk] = (int)i;
+        }
+    }
+}
+
 // PACKED: candidates are records of the breadth-first packed tree
 // (tree_pack.hip: centre + side and ref id / first child / child mask in one
 // 32-B record, siblings contiguous) instead of reference node ids into the
@@ -425,7 +513,11 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           int *__restrict__ hit_idx, float *__restrict__ hit_t0,
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
                                                           float *__restrict__ ray_dsum, int *__restrict__ stats,
-                                                          int *__restrict__ blk_out) {
+                                                          int *__restrict__ blk_out, int *__restrict__ ray_rank,
+                                                          int *__restrict__ rank_ray) {
+    // rank_ray != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
+    // runs in the launch's last-arriving workgroup (stats_rank_tail)
+    const bool tail = rank_ray != nullptr;
     __shared__ KeyLds lds_all[kIsWaves];
     KeyLds &S = lds_all[threadIdx.x / kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -643,8 +735,13 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         if (lane == 0) {
             float dsum = 0.0f;
             for (int l = 0; l < nv; ++l) dsum = dsum + S.hd[l];
-            ray_nv[r] = nv;
-            ray_dsum[r] = dsum;
+            if (tail) {  // read by the last workgroup of this launch
+                st_wt(ray_nv + r, nv);
+                st_wt(ray_dsum + r, dsum);
+            } else {
+                ray_nv[r] = nv;
+                ray_dsum[r] = dsum;
+            }
         }
 #ifdef PSVO_IS_STAMPS
         IS_MARK(is_tb);
@@ -680,7 +777,10 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             sps += blk_sp[w];
             rd += blk_rd[w];
         }
-        if (blk_out) {  // summed by k_ray_stats_rank: no same-address atomics (they serialise at the memory side)
+        if (tail) {
+            st_wt(blk_out + 2 * blockIdx.x, v);
+            st_wt(blk_out + 2 * blockIdx.x + 1, rd);
+        } else if (blk_out) {  // summed by k_ray_stats_rank: no same-address atomics (they serialise at the memory side)
             blk_out[2 * blockIdx.x] = v;
             blk_out[2 * blockIdx.x + 1] = rd;
         } else {
@@ -690,17 +790,20 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
+    if (!tail) return;
+    __shared__ int is_last;
+    if (!last_block(stats + kStatIsTail, &is_last)) return;
+    stats_rank_tail(n_rays, ray_nv, ray_dsum, step_size, stats, ray_rank, rank_ray, blk_out, (int)gridDim.x);
 }
 
 // one wave, one word per lane (words <= 64)
-__global__ void k_stats_to_host(int *__restrict__ stats, int *host, int words, int seq) {
+__global__ void k_stats_to_host(int *__restrict__ stats, unsigned long long *host, int words, int seq) {
     const int i = threadIdx.x;
     if (i < words) {
-        host[i] = stats[i];
+        const int v = stats[i];
         stats[i] = 0;  // ready for the query set's next use (no memset launch)
+        stat_to_host(host, i, v, seq);
     }
-    __threadfence_system();
-    if (i == 0) __hip_atomic_store(host + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // P (max valid hits), R_hit and max ceil(Σ/step) over the rays — one block.
@@ -1261,6 +1364,37 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
 // parallel rank samples its own rays inside the GLOBAL [200, K', P] layout
 // this way: rank_ray / hit_* / dsum / stats then describe
 // the all-gathered batch, and the noise key is the global logical index.
+// the scan of the ray sample counts and the statistics read-back in the
+// sampler launch's last-arriving workgroup (single GPU; offsets == nullptr:
+// k_scan_samples runs after the launch instead)
+struct SampleTail {
+    int *offsets;              // [R_hit + 1] exclusive scan of ray_ns
+    unsigned long long *host;  // PSVO_STAT_WORDS granules (stat_to_host)
+    int seq;
+    int *keep;                 // device copy of the statistics (DevBatch), or null
+    SampleCounts c;            // the Criterion's normalisers (c.gt_depth null: not counted)
+};
+// ray_cnt word: valid front / sdf samples (12 bits each), then whether a
+// padded sample (z = MAX_DEPTH) is front / sdf, whether the ray's depth is valid
+__device__ __forceinline__ int pack_counts(int nf, int nsm, bool pf, bool psm, bool valid) {
+    return nf | (nsm << 12) | ((int)pf << 24) | ((int)psm << 25) | ((int)valid << 26);
+}
+
+__device__ void scan_samples_tail(int64_t n, const int *__restrict__ ray_ns, int *__restrict__ stats,
+                                  const SampleTail &tl);
+
+// one ray of k_sample_fused; returns its valid-sample count, or -1 when the
+// wave has no ray (the launch covers r_hit_cap rows)
+__device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                int max_steps_cap, const int *__restrict__ rank_ray,
+                                                const int *__restrict__ hit_idx, const float *__restrict__ hit_t0,
+                                                const float *__restrict__ hit_t1, const float *__restrict__ ray_dsum,
+                                                float step_size, const float *__restrict__ noise, uint64_t seed,
+                                                int *__restrict__ stats, int *__restrict__ s_idx,
+                                                float *__restrict__ s_depth, float *__restrict__ s_dist,
+                                                const int *__restrict__ slot0, int slot0_nch, int &il_out,
+                                                WaveBins &W, const SampleTail &tl, int &cnt_word);
+
 __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
                                                       const int *__restrict__ rank_ray,
@@ -1272,7 +1406,35 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
                                                       int *__restrict__ stats, int *__restrict__ s_idx,
                                                       float *__restrict__ s_depth, float *__restrict__ s_dist,
                                                       int *__restrict__ ray_ns, const int *__restrict__ slot0,
-                                                      int slot0_nch) {
+                                                      int slot0_nch, SampleTail tl) {
+    __shared__ WaveBins bins_all[4];
+    int il = 0, cnt_word = 0;
+    const int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
+                                       ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
+                                       slot0_nch, il, bins_all[threadIdx.x / kWave], tl, cnt_word);
+    if (!tl.offsets) {
+        if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) ray_ns[il] = count;
+        return;
+    }
+    if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) {
+        st_wt(ray_ns + il, count);
+        if (tl.c.gt_depth) st_wt(tl.c.ray_cnt + il, cnt_word);
+    }
+    __shared__ int is_last;
+    if (!last_block(stats + kStatSmpTail, &is_last)) return;
+    const int64_t r_hit = ld_wt(stats + PSVO_STAT_R_HIT);
+    scan_samples_tail(min(r_hit, r_hit_cap), ray_ns, stats, tl);
+}
+
+__device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                int max_steps_cap, const int *__restrict__ rank_ray,
+                                                const int *__restrict__ hit_idx, const float *__restrict__ hit_t0,
+                                                const float *__restrict__ hit_t1, const float *__restrict__ ray_dsum,
+                                                float step_size, const float *__restrict__ noise, uint64_t seed,
+                                                int *__restrict__ stats, int *__restrict__ s_idx,
+                                                float *__restrict__ s_depth, float *__restrict__ s_dist,
+                                                const int *__restrict__ slot0, int slot0_nch, int &il_out,
+                                                WaveBins &W, const SampleTail &tl, int &cnt_word) {
     const int P = stats[PSVO_STAT_P];
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
@@ -1283,10 +1445,9 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     const int lane = threadIdx.x & (kWave - 1);
     const int il = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
     const int i = (int)row_begin + il;                                        // logical row
-    __shared__ WaveBins bins_all[4];
-    WaveBins &W = bins_all[threadIdx.x / kWave];
+    il_out = il;
     const int64_t n_own = n_rows < 0 ? (int64_t)r_hit - row_begin : n_rows;
-    if (i >= r_hit || il >= n_own || il >= r_hit_cap || P <= 0) return;
+    if (i >= r_hit || il >= n_own || il >= r_hit_cap || P <= 0) return -1;
     if (max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + PSVO_STAT_FLAGS, 2);
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
     const int b = i / kp;
@@ -1301,7 +1462,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     if (slot0) {
         if (c >= slot0_nch) {  // the exchanged table covers slot0_nch launch chunks
             if (lane == 0) atomicOr(stats + PSVO_STAT_FLAGS, 4);
-            return;
+            return -1;
         }
         rows.slot0 = slot0;
         rows.slot0_row = b * slot0_nch + c;
@@ -1317,6 +1478,12 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     const float *nz = noise ? noise + ((int64_t)b * kp + j) * max_steps : nullptr;
     const uint64_t key = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)(b * kp + j) << 20);
     int count = 0;
+    // the normalisers' per-sample terms (criterion.hip sample_terms) on the stored depths
+    const bool counting = tl.c.gt_depth != nullptr;
+    const float gd = counting ? tl.c.gt_depth[orig] : 0.f;
+    const float lo_t = gd - tl.c.tr, hi_t = gd + tl.c.tr;
+    const bool dm = gd > 0.0f && gd < tl.c.max_depth;
+    int nf = 0, nsm = 0;
     const int s_end = sample_wave(
         rows, steps_j, P, nr, jj * P,
         [&](int cs) {
@@ -1331,6 +1498,11 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
             od[s] = v == -1 ? kMaxDepthFill : dep;
             if (os) os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
             count += (v != -1);
+            if (counting && v != -1) {
+                const bool f = dep < lo_t;
+                nf += f;
+                nsm += !f && !(dep > hi_t) && dm;
+            }
         },
         lane, W);
     const int s_written = s_end < cap ? s_end : cap;
@@ -1339,8 +1511,98 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
         od[s] = kMaxDepthFill;
         if (os) os[s] = 0.0f;
     }
-    count = wave_sum(count);
-    if (lane == 0) ray_ns[il] = count;
+    if (counting) {
+        const bool pf = kMaxDepthFill < lo_t;  // a padded sample: z = MAX_DEPTH
+        const bool psm = !pf && !(kMaxDepthFill > hi_t) && dm;
+        cnt_word = pack_counts(wave_sum(nf), wave_sum(nsm), pf, psm, gd > 0.01f && gd < tl.c.max_depth);
+    }
+    return wave_sum(count);
+}
+
+// k_scan_samples' work in the sampler's last workgroup (256 threads): thread
+// t owns the run [t·per, (t+1)·per) of ray_ns (per <= kTailPasses, read with
+// sc1 loads into registers), the run totals are scanned across waves, then
+// offsets, S_max / M and the statistics read-back (granules, no
+// system-scope release); the device statistics are zeroed for the next query
+__device__ void scan_samples_tail(int64_t n, const int *__restrict__ ray_ns, int *__restrict__ stats,
+                                  const SampleTail &tl) {
+    __shared__ int s_wave[4], s_max4[4];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int per = (int)((n + 255) / 256);
+    const int64_t beg = (int64_t)tid * per;
+    int vals[kTailPasses];
+    int local = 0, mx = 0;
+    // normaliser counts, exact integers (k_crit_counts' float sums of 0 / 1 are exact too)
+    long long c_nf = 0, c_nsm = 0, c_pf = 0, c_psm = 0, c_valid = 0, c_nspf = 0, c_nspsm = 0;
+#pragma unroll
+    for (int k = 0; k < kTailPasses; ++k) {
+        const bool in = k < per && beg + k < n;
+        vals[k] = in ? ld_wt(ray_ns + beg + k) : 0;
+        local += vals[k];
+        mx = max(mx, vals[k]);
+        if (tl.c.gt_depth && in) {
+            const int cw = ld_wt(tl.c.ray_cnt + beg + k);
+            const int pf = (cw >> 24) & 1, psm = (cw >> 25) & 1;
+            c_nf += cw & 0xFFF;
+            c_nsm += (cw >> 12) & 0xFFF;
+            c_pf += pf;
+            c_psm += psm;
+            c_valid += (cw >> 26) & 1;
+            c_nspf += pf ? vals[k] : 0;
+            c_nspsm += psm ? vals[k] : 0;
+        }
+    }
+    int incl = local;
+#pragma unroll
+    for (int sh = 1; sh < kWave; sh <<= 1) {
+        const int t = __shfl_up(incl, sh, kWave);
+        if (lane >= sh) incl += t;
+    }
+    mx = wave_max(mx);
+    if (lane == kWave - 1) s_wave[w] = incl;
+    if (lane == 0) s_max4[w] = mx;
+    __syncthreads();
+    int before = 0, tot = 0, smax = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        before += k < w ? s_wave[k] : 0;
+        tot += s_wave[k];
+        smax = max(smax, s_max4[k]);
+    }
+    int run = before + incl - local;
+#pragma unroll
+    for (int k = 0; k < kTailPasses; ++k)
+        if (k < per && beg + k < n) {
+            tl.offsets[beg + k] = run;
+            run += vals[k];
+        }
+    if (tid == 0) tl.offsets[n] = tot;
+    if (tl.c.gt_depth) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
+        __shared__ long long s_c[7][4];
+        long long c[7] = {c_nf, c_nsm, c_pf, c_psm, c_valid, c_nspf, c_nspsm};
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            long long v = c[k];
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, kWave);
+            if (lane == 0) s_c[k][w] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            long long t[7];
+            for (int k = 0; k < 7; ++k) t[k] = s_c[k][0] + s_c[k][1] + s_c[k][2] + s_c[k][3];
+            const long long n_f = t[0] + (long long)smax * t[2] - t[5];
+            const long long n_s = t[1] + (long long)smax * t[3] - t[6];
+            crit_coef_from_counts((double)t[4], (double)n_f, (double)n_s, (double)n, (double)smax, tl.c.w_rgb,
+                                  tl.c.w_depth, tl.c.w_fs, tl.c.w_sdf, tl.c.tr, tl.c.crit_flags, tl.c.coef);
+        }
+    }
+    if (w == 0 && lane < PSVO_STAT_WORDS) {
+        const int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : ld_wt(stats + lane);
+        if (tl.keep) tl.keep[lane] = v;
+        stats[lane] = 0;  // ready for the query set's next use (no memset launch)
+        stat_to_host(tl.host, lane, v, tl.seq);
+    }
 }
 
 // offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.  With
@@ -1348,8 +1610,8 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
 // query (`keep`, if set, holds a device copy).
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
-                                                       int *__restrict__ stats, int dist, int *host, int seq,
-                                                       int *__restrict__ keep) {
+                                                       int *__restrict__ stats, int dist, unsigned long long *host,
+                                                       int seq, int *__restrict__ keep) {
     __shared__ int total;
     __shared__ int smax[16];
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
@@ -1368,13 +1630,10 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
             if (lane < PSVO_STAT_WORDS) {
                 const int v = lane == PSVO_STAT_S_MAX ? mx : lane == PSVO_STAT_M ? tot : stats[lane];
-                host[lane] = v;
                 if (keep) keep[lane] = v;  // the device-sized forward's copy (DevBatch)
                 stats[lane] = 0;
+                stat_to_host(host, lane, v, seq);
             }
-            __threadfence_system();
-            if (lane == 0)
-                __hip_atomic_store(host + PSVO_STAT_WORDS, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         } else if (lane == 0) {
             stats[PSVO_STAT_S_MAX] = mx;
             stats[PSVO_STAT_M] = tot;
@@ -1540,7 +1799,7 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr);
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
@@ -1557,28 +1816,49 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
-                       max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr);
+                       max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
+                       nullptr);
     hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
 
 namespace psvo {
+// PSVO_SPLIT_QUERY=1: the statistics / rank pass and the sample scan as
+// kernels of their own (A/B, tests), not the launches' last workgroups
+static bool split_query() {
+    const char *v = getenv("PSVO_SPLIT_QUERY");
+    return v && *v == '1';
+}
+bool sampler_counts(int64_t r) { return !split_query() && r <= (int64_t)256 * kTailPasses; }
 // the single-GPU sampler with the statistics read-back fused into its scan
 // (one launch less before the host can size the rest of the step)
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, int *host, int seq, int *keep) {
+                        int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep,
+                        const SampleCounts *counts) {
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
+    // up to 256 · kTailPasses hit rays the scan and the read-back run in the
+    // sampler launch's last workgroup (counter word zeroed with the statistics)
+    const bool tail = sampler_counts(r_hit_cap);
+    SampleTail tl{};
+    if (tail) {
+        tl.offsets = offsets;
+        if (counts) tl.c = *counts;
+    }
+    tl.host = host;
+    tl.seq = seq;
+    tl.keep = keep;
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
-                       s_dist, ray_ns, nullptr, 0);
-    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0, host,
-                       seq, keep);
+                       s_dist, ray_ns, nullptr, 0, tl);
+    if (!tail)
+        hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
+                           host, seq, keep);
     return check_launch("sample_rays_to_host");
 }
 
-int stats_to_host(hipStream_t st, int *stats, int *host, int words, int seq) {
+int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq) {
     hipLaunchKernelGGL(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
     return check_launch("stats_to_host");
 }
@@ -1592,16 +1872,22 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
+    // up to 256 · kTailPasses rays the statistics / rank pass runs in the
+    // traversal launch's last workgroup (no second launch, no kernel boundary
+    // between them); the counter word is zero (memset / the last read-back)
+    const bool tail = !split_query() && blk_out && n_rays <= (int64_t)256 * kTailPasses;
+    int *rr = tail ? ray_rank : nullptr, *rk = tail ? rank_ray : nullptr;
     if (packed)
         hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out);
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
     else
         hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out);
-    hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
-                       ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
+    if (!tail)
+        hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
+                           ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
     return check_launch("intersect_ranked");
 }
 }  // namespace psvo
@@ -1629,7 +1915,7 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
     if (r_hit_cap == 0) return PSVO_OK;
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
-                       s_dist, ray_ns, table, nch);
+                       s_dist, ray_ns, table, nch, SampleTail{});
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
                        nullptr, 0, nullptr);
     return check_launch("dist_sample");
@@ -1663,7 +1949,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
-                       s_idx, s_depth, s_dist, ray_ns, nullptr, 0);
+                       s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{});
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
                        stats, 0, nullptr, 0, nullptr);
     return check_launch("sample_rays");

@@ -82,6 +82,9 @@ _SIGNATURES = {
     "psvo_engine_timing": (_i32, [_vp, _vp]),
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
+    "psvo_map_adam_ex": (_i32, [_vp, _vp, _vp, _i64, _i32]),
+    "psvo_map_join": (_i32, [_vp, _vp]),
+    "psvo_engine_grad_rays": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "psvo_map_query": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _u64]),
     "psvo_map_step_frames": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_pose_rays_frames": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
@@ -171,6 +174,8 @@ def lib():
                             f"__graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
+            if os.environ.get("PSVO_LIB_PATH") and not hasattr(L, name):
+                continue  # an older diagnostic build (A/B runs) may predate an entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

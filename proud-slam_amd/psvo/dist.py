@@ -303,6 +303,8 @@ class EngineExchange:
         # (tests/test_gpu_rccl.py drives the RCCL branch this way)
         self.force = bool(force)
         on = dist.is_available() and dist.is_initialized()
+        if self.force and not on:
+            raise RuntimeError("EngineExchange(force=True) needs an initialised torch.distributed process group")
         self.world = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
         self.max_rays_global = int(max_rays_global)
@@ -406,11 +408,19 @@ class EngineGradExchange:
             self.sparse = SparseRowSum(self.n_emb, 16, engine.grad_flat.device, group=group, ops=ops,
                                        force=force)
         self.last_mode = "dense"
+        self._rows_marked = False  # this step's exchange marked the union rows (MappingEngine.adam)
+
+    def take_rows_marked(self):
+        """True once after an exchange that marked every exchanged row into
+        the engine's union flags: the next Adam step may be row-sparse."""
+        m, self._rows_marked = self._rows_marked, False
+        return m
 
     def __call__(self):
+        self._rows_marked = False
         ws = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
         if ws == 1 and not self.force:
-            return
+            return  # no exchange ran: the engine's Adam steps the table densely
         flat = self.engine.grad_flat
         n = self.n_emb * 16
         union, local = self.engine.row_flags, self.engine.row_local  # sparse-exact Adam (engine.set_exchange)
@@ -424,5 +434,6 @@ class EngineGradExchange:
         else:
             self.last_mode = self.sparse(flat[:n].view(self.n_emb, 16), local=local, union=union)
             dist.all_reduce(flat[n:], op=dist.ReduceOp.SUM, group=self.group)
+        self._rows_marked = union is not None
         if self.op == "mean":
             flat.div_(ws)

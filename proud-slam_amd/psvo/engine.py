@@ -35,7 +35,8 @@ class MapFrames(ctypes.Structure):
     """Mirror of psvo_map_frames (include/psvo.h)."""
     _fields_ = [("n_frames", _i32), ("rays_per_frame", _i64), ("dirs_cam", _vp), ("poses", _vp), ("pose_m", _vp),
                 ("pose_v", _vp), ("pose_step", _vp), ("lr_pose", _f64), ("pose_grad", _vp),
-                ("next_dirs_cam", _vp), ("next_seed", ctypes.c_uint64), ("next_stream", _vp)]
+                ("next_dirs_cam", _vp), ("next_seed", ctypes.c_uint64), ("next_stream", _vp),
+                ("next_gt_depth", _vp)]
 
 
 def _lib():
@@ -66,6 +67,9 @@ class MappingEngine:
         self.loss_out = torch.empty(16, dtype=torch.float32, device=self.emb.device)
         self.stats = (ctypes.c_int * 16)()
         self.stats_hook = None  # called with the step's statistics after each step_frames (bench accounting)
+        # bundle_adjust_frames discards the loss (render_helpers.py:662-676), so its steps skip the value
+        # (PSVO_STEP_NO_LOSS); set True to have step_frames return it there too (tests that record it)
+        self.ba_loss = os.environ.get("PSVO_BA_LOSS", "0") == "1"
         self._ahead = None  # the camera directions of a queued step_frames look-ahead
         d = MapDesc()
         d.n_nodes = self.centres.shape[0]
@@ -147,13 +151,14 @@ class MappingEngine:
 
     def step_frames(self, dirs_cam, rays_per_frame, poses, pose_m, pose_v, pose_steps, lr_pose, rgb, depth, seed,
                     noise=None, adam_step=None, apply_adam=True, pose_grad=None, next_dirs_cam=None, next_seed=0,
-                    next_stream=None):
+                    next_stream=None, want_loss=True, next_depth=None):
         """One bundle_adjust_frames iteration with keyframe pose updates
         (psvo_map_step_frames): rays from the current poses [F, 6] (frame f
         owns rows [f·rays_per_frame, (f+1)·rays_per_frame) of dirs_cam),
         render + loss + backward, Adam on embeddings / decoder and on every
         pose with pose_steps[f] ≥ 1 (its Adam step number; 0 = fixed pose).
-        poses / pose_m / pose_v are updated in place.  Returns the loss.
+        poses / pose_m / pose_v are updated in place.  Returns the loss
+        (want_loss=False: None — the value is not computed, PSVO_STEP_NO_LOSS).
         next_dirs_cam (contiguous f32 [F·rays_per_frame, 3]) / next_seed: the
         next iteration's batch, whose query is queued beside this step's
         weight gradients (the next call must pass exactly that tensor and seed).
@@ -190,6 +195,14 @@ class MappingEngine:
         fr.next_dirs_cam = next_dirs_cam.data_ptr() if next_dirs_cam is not None else None
         fr.next_seed = int(next_seed) & (2 ** 64 - 1)
         fr.next_stream = next_stream.cuda_stream if next_stream is not None else None
+        # the next call's GT depths (it must pass this very tensor): the look-ahead's sampler counts the
+        # loss normalisers with them (PSVO_STEP_NO_LOSS steps)
+        nd = None
+        if next_depth is not None and next_dirs_cam is not None:
+            nd = next_depth.reshape(-1)
+            if not (nd.is_cuda and nd.dtype == torch.float32 and nd.is_contiguous()):
+                nd = None
+        fr.next_gt_depth = nd.data_ptr() if nd is not None else None
         nz = None
         if noise is not None:
             nz = noise.to(device=dirs.device, dtype=torch.float32).contiguous()
@@ -199,22 +212,27 @@ class MappingEngine:
         rc = _lib().psvo_map_step_frames(self.handle, L.stream_of(dirs.device), ctypes.addressof(self.desc),
                                          ctypes.addressof(fr), gt_rgb.data_ptr(), gt_d.data_ptr(),
                                          nz.data_ptr() if nz is not None else None, int(seed), self.step_no,
-                                         0 if apply_adam else 1, self.loss_out.data_ptr(),
-                                         ctypes.addressof(self.stats))
+                                         (0 if apply_adam else 1) | (0 if want_loss else 4),
+                                         self.loss_out.data_ptr(), ctypes.addressof(self.stats))
         if rc != 0:
             # as step(): the failed iteration did not happen — its Adam step number rolls back, and a
             # look-ahead query it may have queued is dropped on the engine side too (the next call's
             # fresh dirs_cam would otherwise be refused against it)
             self.step_no = prev_step
             err = self._error("psvo_map_step_frames", rc)
-            L.call("psvo_map_discard", self.handle)
-            self._queued.clear()
-            self._ahead = None
+            try:
+                L.call("psvo_map_discard", self.handle)
+            except L.PsvoError:
+                pass  # a faulted stream: the step's own error is the one to report
+            finally:
+                self._queued.clear()
+                self._ahead = None
             raise err
         self._ahead = next_dirs_cam  # kept alive until the next call consumes its query
+        self._ahead_depth = nd
         if self.stats_hook is not None:
             self.stats_hook(self.stats)
-        return self.loss_out[0]
+        return self.loss_out[0] if want_loss else None
 
     def _check_noise(self, nz, dirs, rpf, poses):
         """Injected sampler noise must have the layout this batch's sampler
@@ -317,8 +335,14 @@ class MappingEngine:
         return self.loss_out[0]
 
     def adam(self):
-        """Both Adam steps from self.grad_flat (after a step(apply_adam=False))."""
-        L.call("psvo_map_adam", self.handle, L.stream_of(self.emb.device), ctypes.addressof(self.desc), self.step_no)
+        """Both Adam steps from self.grad_flat (after a step(apply_adam=False)).
+        Data parallel, the embedding step is row-sparse only when this step's
+        gradient exchange marked the union of all ranks' rows; otherwise the
+        engine steps the table densely (psvo_map_adam_ex, include/psvo.h)."""
+        ge = self.grad_exchange
+        marked = ge is not None and ge.take_rows_marked()
+        L.call("psvo_map_adam_ex", self.handle, L.stream_of(self.emb.device), ctypes.addressof(self.desc),
+               self.step_no, 1 if marked else 0)
 
     def set_timing(self, on):
         """HIP events around the decoder fwd / bwd and interp fwd / bwd launches.

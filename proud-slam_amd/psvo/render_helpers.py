@@ -539,7 +539,8 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         dp = eng.grad_exchange is not None
         eng.step_frames(d_all, N_rays, poses, pm, pv, cur_steps, lr_pose or 0.0, c_all, z_all, seed, noise=nz,
                         adam_step=adam_step, apply_adam=not dp, next_dirs_cam=nxt[0] if nxt else None,
-                        next_seed=nxt[4] if nxt else 0, next_stream=side if nxt else None)
+                        next_seed=nxt[4] if nxt else 0, next_stream=side if nxt else None,
+                        want_loss=eng.ba_loss, next_depth=nxt[2] if nxt else None)
         if dp:  # data parallel: sum the union-batch gradient over ranks, then the same Adam everywhere
             eng.grad_exchange()
             eng.adam()

@@ -70,6 +70,7 @@ def run(scene, tree, emb0, frames_ids, dev, exchange=None, sparse=False):
         # sparse: the row-sparse embedding exchange (config E's) forced on this small table
         eng.grad_exchange = EngineGradExchange(eng, op="sum", sparse_min_bytes=0 if sparse else 32 << 20)
     losses = []
+    eng.ba_loss = True  # bundle_adjust_frames' steps return their loss (recorded below)
     orig = eng.step_frames
 
     def spy(*a, **k):

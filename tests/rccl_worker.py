@@ -87,6 +87,7 @@ def ba_loop(tree, emb0, scene, dev, exchange=None):
     if exchange is not None:
         eng.set_exchange(exchange)
     losses = []
+    eng.ba_loss = True  # bundle_adjust_frames' steps return their loss (recorded below)
     eng.stats_hook = None
     orig = eng.step_frames
 

@@ -141,3 +141,14 @@ def test_engine_exchange_apply_gloo():
         np.testing.assert_array_equal(xi[40:50], np.full(10, 3))
         np.testing.assert_array_equal(xf[:8], np.arange(8) * (rank + 1))  # untouched half
         np.testing.assert_array_equal(xf[8:], np.arange(8, 16) * 3.0)
+
+
+def test_forced_exchange_needs_process_group():
+    """force=True runs every collective even on one rank: without an
+    initialised process group that must fail here, not inside a step's
+    ctypes callback."""
+    from psvo.dist import EngineExchange
+    assert not (dist.is_available() and dist.is_initialized())
+    with pytest.raises(RuntimeError, match="process group"):
+        EngineExchange(max_rays_global=64, force=True)
+    assert EngineExchange(max_rays_global=64).world == 1

@@ -250,3 +250,61 @@ def test_fused_points_interp_matches_split(monkeypatch):
     for p, q in zip(da, db):
         torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
     torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
+
+
+def _frames_of(w, n):
+    """Keyframe poses [F, 6] and camera-frame directions of a workload's rays
+    (world directions rotated back by each pose)."""
+    from oracle import oracle as O
+    from psvo.pose import OptimizablePose
+    poses, dirs = [], []
+    rd = w.rays_d[0].double()
+    for f, T in enumerate(w.poses):
+        p = OptimizablePose.from_matrix(np.asarray(T)).data.detach().double()
+        poses.append(p.float())
+        dirs.append((rd[f * n:(f + 1) * n] @ O.se3_rotation(p)).float())
+    return torch.stack(poses).contiguous().to(DEV), torch.cat(dirs).contiguous().to(DEV)
+
+
+def test_query_tails_and_sampler_counts_match_split_kernels(monkeypatch):
+    """The round-4 query chain — the statistics / rank pass in the traversal
+    launch's last workgroup, the sample scan and read-back in the sampler's,
+    the compaction inside the interpolation (k_interp_fwd_rays), and (with
+    PSVO_STEP_NO_LOSS) the loss normalisers counted by the sampler — against
+    the separate kernels (PSVO_SPLIT_QUERY=1: k_ray_stats_rank, k_scan_samples,
+    k_sample_points, k_crit_counts → reduce → coef), two psvo_map_step_frames
+    iterations stopped before Adam from the same state and seeds: the same
+    statistics, the decoder gradient bit for bit (it depends on the forward,
+    the coefficients and the deterministic decoder backward only), the
+    embedding gradient up to the scatter's float-atomic order, the pose
+    gradient to 1e-5 of its max."""
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    n = 512
+    poses, dirs = _frames_of(w, n)
+    rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    runs = {}
+    for mode in ("split", "tails_loss", "tails_counts"):
+        monkeypatch.setenv("PSVO_SPLIT_QUERY", "1" if mode == "split" else "0")
+        e = emb0.clone().to(DEV)
+        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
+                            max_distance=10.0, criteria=crit, max_depth=10.0)
+        out = []
+        for it in range(2):
+            pg = torch.zeros(poses.shape[0], 8, device=DEV)
+            eng.step_frames(dirs, n, poses.clone(), torch.zeros_like(poses), torch.zeros_like(poses), [0, 1], 1e-3,
+                            rgb, depth, seed=500 + it, apply_adam=False, pose_grad=pg,
+                            want_loss=mode != "tails_counts")
+            torch.cuda.synchronize()
+            out.append((list(eng.last_stats), eng.grad_flat.cpu().clone(), pg.cpu()))
+        runs[mode] = out
+        eng.close()
+    n_emb = emb0.shape[0] * 16
+    for mode in ("tails_loss", "tails_counts"):
+        for (sa, ga, pa), (sb, gb, pb) in zip(runs["split"], runs[mode]):
+            assert sa[:13] == sb[:13], (mode, sa, sb)  # statistics (words past 12: the tails' counters, zero)
+            assert torch.equal(ga[n_emb:], gb[n_emb:]), mode  # decoder gradient: bit for bit
+            torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-5, atol=1e-6 * float(ga[:n_emb].abs().max()))
+            torch.testing.assert_close(pb, pa, rtol=0, atol=1e-5 * float(pa.abs().max()))

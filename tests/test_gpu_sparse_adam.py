@@ -85,3 +85,44 @@ def test_flags_from_carried_state():
     want[live] = 1
     want[7] = 1
     assert torch.equal(flags.cpu(), want)
+
+
+def test_one_rank_unforced_exchange_steps_every_row():
+    """An exchange set on ONE rank without force (torchrun with one process,
+    or a caller's own all-reduce): the step marks only its local flags and the
+    gradient exchange returns early without marking the union, so Adam must
+    not be row-sparse on the stale union flags (psvo_map_adam_ex: dense, then
+    the flags refreshed from the moments).  Three iterations against the
+    plain single-GPU engine: the same rows move, to Adam's ulp bar, and the
+    union flags cover every row with moments."""
+    import test_gpu_fullsize_parity as F
+    from psvo.decoder import Decoder
+    from psvo.dist import EngineExchange
+    from psvo.engine import MappingEngine
+    c, w, ms, _ = F._setup("B")
+    emb0 = ms["voxel_vertex_emb"].detach().clone()
+    res = {}
+    for mode in ("plain", "exchange"):
+        torch.manual_seed(0)
+        dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+        emb = emb0.clone()
+        eng = MappingEngine(dict(ms, voxel_vertex_emb=emb), dec, w.scene.voxel_size, c["step"])
+        if mode == "exchange":
+            eng.set_exchange(EngineExchange(w.rays_o.shape[1], device=DEV))  # no process group: world 1
+        args = (w.rays_o.to(DEV), w.rays_d.to(DEV), w.rgb.to(DEV), w.depth.to(DEV))
+        for it in range(3):
+            if mode == "exchange":
+                eng.step(*args, seed=11 + it, apply_adam=False)
+                eng.grad_exchange()
+                eng.adam()
+            else:
+                eng.step(*args, seed=11 + it)
+        torch.cuda.synchronize()
+        res[mode] = (emb.cpu(), eng.row_flags.cpu(), eng.emb_m.cpu())
+        eng.close()
+    (e_p, f_p, m_p), (e_x, f_x, m_x) = res["plain"], res["exchange"]
+    e0 = emb0.cpu()
+    moved_p, moved_x = (e_p != e0).any(-1), (e_x != e0).any(-1)
+    assert int(moved_p.sum()) > 100 and torch.equal(moved_p, moved_x)
+    assert bool(f_x[(m_x != 0).any(-1)].all())  # every row with moments is flagged for later sparse steps
+    adam_close(e_x[moved_p].numpy(), e_p[moved_p].numpy(), tight=1e-5, frac=0.97, max_abs=2.0 * 5e-3 * 3)
