@@ -287,7 +287,15 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
 
 
 CHAIN_KERNELS = ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples", "k_sample_points",
-                 "k_interp_fwd", "k_points_interp")
+                 "k_interp_fwd", "k_points_interp", "k_interp_fwd_rays")
+# the kernels each timed region of the query + interp chain launches (for the
+# per-region PMC traffic): intersect (+ its statistics / rank tail or pass),
+# sampler (+ scan), compaction, interpolation (the headline's k_interp_fwd_rays
+# does the compaction too)
+REGION_KERNELS = {"intersect": ("k_intersect_sorted", "k_ray_stats_rank"),
+                  "sample": ("k_sample_fused", "k_scan_samples"),
+                  "points": ("k_sample_points",),
+                  "interp_fwd": ("k_interp_fwd", "k_interp_fwd_rays", "k_points_interp")}
 MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd3", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce",
                "k_dec256_prep", "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
 
@@ -414,6 +422,7 @@ def main():
     # keyframe (gumbel top-k on the device), renders, back-propagates and steps
     # every optimiser.  K steps = one call with num_iterations = K.
     ba_calls = [0]
+    pace = {}  # the headline run's GPU-side period and the host's waits (timed_ba)
 
     def run_ba(steps):
         call = ba_calls[0]
@@ -446,14 +455,28 @@ def main():
         if world > 1:
             dist.barrier()
         eng = head_engine() if warmup else None
+        clocked = False
         if record and eng is not None:
             eng.stats_hook = lambda st: record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3], head_stats)
+            try:  # an event at each step's entry on its stream: the GPU-side period
+                eng.set_clock(steps)
+                eng.host_wait_stats(reset=True)
+                clocked = True
+            except AttributeError:  # an older library (A/B runs) without the clock
+                pass
         t0 = time.perf_counter()
         run_ba(steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if clocked:
+            period, n_clk = eng.clock()
+            eng.set_clock(0)
+            w_us, w_calls, w_waited = eng.host_wait_stats(reset=True)
+            pace.update(gpu_ms_per_step=period, clock_steps=n_clk,
+                        host_wait_us_per_step=w_us / max(w_calls, 1), host_waits=w_calls,
+                        host_waits_before_landing=w_waited)
         if eng is not None:
             eng.stats_hook = None
         if world > 1:
@@ -477,9 +500,20 @@ def main():
     # launching streams inside the same bundle_adjust_frames iterations
     n_mark = max(5, min(args.steps, 20))
     eng.set_timing("overlap")
+    if world > 1:  # the exchanges' own durations, in the same marked iterations
+        from psvo import dist as D
+        D.TIMER = D.CollectiveTimer()
     timed_ba(n_mark, 0)
     kt_overlap = eng.timing()
     eng.set_timing(False)
+    collectives = None
+    if world > 1:
+        coll_ms = D.TIMER.total_ms()
+        collectives = {"collective_ms_per_step": coll_ms / n_mark, "collectives_per_step": D.TIMER.count / n_mark,
+                       "backend": dist.get_backend(),
+                       "timing": "HIP events around each RCCL call on its stream (gloo: host time of the "
+                                 "host-staged call), marked iterations"}
+        D.TIMER = None
     kt_serial = None
     others = []
     rays_step = args.frames * args.rays_per_frame
@@ -575,9 +609,15 @@ def main():
         h_m, h_r, h_v = (float(x) / world for x in t.cpu())
     fused_ib = args.width == 128 and os.environ.get("PSVO_MLP_BWD", "") != "2"  # interp bwd inside k_mlp_bwd3
     q_keys = ("intersect", "sample", "points", "interp_fwd") + (() if fused_ib else ("interp_bwd",))
-    q_parts = {k: kt_overlap[k] for k in q_keys}
+    # a region the step did not mark (the headline has no separate compaction) counts 0
+    q_parts = {k: max(kt_overlap[k], 0.0) for k in q_keys}
     q_ms = sum(q_parts.values())
     bytes_qi = rays_step * 24.0 + h_v * 48.0 + h_m * 12.0 + h_m * (628.0 + (0.0 if fused_ib else 1664.0))
+    # the same byte model per region: traversal 24 B / ray + 48 B / AABB-tested node,
+    # sampler output 12 B / sample, interpolation 628 B / sample (8 × 64-B vertex rows + 64-B feature
+    # + the 12-B compacted sample), interp bwd 1,664 B / sample where it has a launch of its own
+    region_bytes = {"intersect": rays_step * 24.0 + h_v * 48.0, "sample": h_m * 12.0, "points": 0.0,
+                    "interp_fwd": h_m * 628.0, "interp_bwd": h_m * 1664.0}
     traffic, traffic_note = None, "not measured (N > 1 or --no-traffic)"
     if world == 1 and not args.no_traffic:
         log("PMC passes (roofline.traffic)")
@@ -602,13 +642,34 @@ def main():
             r.update(extra)
         return r
 
-    roof_qi = bw_roof("octree query+interp (k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, " +
-                      ("k_points_interp = compaction + interp fwd" if os.environ.get("PSVO_FUSED_POINTS") == "1"
-                       else "k_sample_points, k_interp_fwd") + (")" if fused_ib else ", k_interp_bwd)"), bytes_qi, q_ms,
-                      tr.get("query_interp_bytes_per_step"),
+    split_q = os.environ.get("PSVO_SPLIT_QUERY") == "1"
+    chain_desc = ("k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, " +
+                  ("k_points_interp = compaction + interp fwd" if os.environ.get("PSVO_FUSED_POINTS") == "1"
+                   else "k_sample_points, k_interp_fwd")) if split_q or world > 1 else \
+        ("k_intersect_sorted with the statistics / hit-rank pass in its last workgroup, k_sample_fused with the "
+         "sample scan, the loss normalisers and the read-back in its last workgroup, k_interp_fwd_rays = "
+         "compaction + interp fwd")
+    kern_tr = tr.get("kernels") or {}
+    per_region = {}
+    for k in q_keys:
+        ms_k = q_parts[k]
+        if ms_k <= 0:
+            continue
+        frac_k = region_bytes[k] / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS
+        counted = sum(kern_tr[n]["total"] for n in REGION_KERNELS.get(k, ()) if n in kern_tr) if kern_tr else None
+        cfrac = counted / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS if counted else None
+        per_region[k] = {"ms": ms_k, "algorithmic_bytes": region_bytes[k], "frac": frac_k,
+                         "hbm_bytes_counted": counted, "frac_hbm_counters": cfrac,
+                         # an algorithmic rate above the HBM peak cannot come from HBM: the table / tree
+                         # reads hit the XCD L2s or the 256-MB MALL
+                         "served_from": ("L2/MALL (algorithmic bytes exceed what HBM could deliver)" if frac_k > 1.0
+                                         else "mostly L2/MALL (counted HBM bytes < 1/2 of algorithmic)"
+                                         if counted is not None and counted < 0.5 * region_bytes[k] else "HBM")}
+    roof_qi = bw_roof("octree query+interp (" + chain_desc + (")" if fused_ib else ", k_interp_bwd)"), bytes_qi,
+                      q_ms, tr.get("query_interp_bytes_per_step"),
                       sum(kt_serial[k] for k in q_keys) if kt_serial else None,
                       {"parts_ms": q_parts, "parts_ms_serialised": {k: kt_serial[k] for k in q_keys}
-                       if kt_serial else None, "visits_per_ray": h_v / max(rays_step, 1),
+                       if kt_serial else None, "per_region": per_region, "visits_per_ray": h_v / max(rays_step, 1),
                        "samples_per_hit_ray": h_m / max(h_r, 1), "traffic_note": traffic_note})
     mlp_f_ms, mlp_b_ms = kt_overlap["mlp_fwd"], kt_overlap["mlp_bwd"]
     mlp_ms = mlp_f_ms + mlp_b_ms
@@ -639,6 +700,12 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        # the steady-state iteration period as the GPU ran it (events at each step's entry on its
+        # stream) and how often the host had to wait for a query's statistics — a host that never
+        # waits set the pace; one that waits on nearly every step was paced by the GPU
+        "gpu_ms_per_step": pace.get("gpu_ms_per_step"),
+        "pace": dict(pace, note="gpu_ms_per_step excludes each bundle_adjust_frames call's setup / write-back "
+                                "and its first, un-pipelined iteration; ms_per_step is the wall clock of the call"),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -667,6 +734,9 @@ def main():
         "kernels_ms_serialised": kt_serial,
         "traffic_kernels": tr.get("kernels"),
     }
+    if collectives:
+        result["collectives"] = collectives
+        result["collective_ms_per_step"] = collectives["collective_ms_per_step"]
     log("done timing")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline")

@@ -532,6 +532,17 @@ enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, P
 int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators; on = 1: regions serialised
                                                            on one stream, 2: as run (side streams overlap) */
 int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
+/* The iteration period as the GPU runs it: with max_steps > 0 every mapping
+ * step records an event on the caller's stream at its entry (up to max_steps;
+ * resets the count; 0 turns it off); psvo_engine_clock gives the mean time
+ * between the first and the last recorded event per step (-1 if fewer than
+ * two) — synchronises on the last event. */
+int psvo_engine_set_clock(psvo_engine *e, int max_steps);
+int psvo_engine_clock(psvo_engine *e, double *period_ms, int *n_steps);
+/* The host's waits for query statistics (all engines of the process): total
+ * microseconds, calls, and calls that found them not yet landed (the GPU set
+ * the pace); reset != 0 zeroes the counters. */
+int psvo_host_wait_stats(double *wait_us, long long *calls, long long *waited, int reset);
 
 /* One iteration on n_rays rays (rays_o/rays_d f32[R,3], gt_rgb f32[R,3],
  * gt_depth f32[R]): sampler noise from `seed`; Adam bias corrections for

@@ -102,8 +102,19 @@ struct EngineExchange {
     }
 };
 
+// psvo_engine_set_clock: an event on the caller's stream at the entry of
+// every mapping step — the GPU reaches it when the previous step's work on
+// that stream (through the look-ahead query) is done, so consecutive events
+// are the iteration period as the GPU runs it
+struct EngineClock {
+    std::vector<hipEvent_t> ev;
+    int n = 0;
+    bool on = false;
+};
+
 struct psvo_engine {
     EngineExchange x;
+    EngineClock clk;
     psvo::Arena a;
     psvo::QuerySet qs[2];           // FIFO of queries: head = the next step's
     int q_head = 0, q_count = 0;
@@ -231,8 +242,6 @@ bool stats_landed(const unsigned long long *raw, int seq, int *out) {
 }
 int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who);
 int spin_wait(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) {
-    static const bool on = getenv("PSVO_HOST_WAIT_STATS") && *getenv("PSVO_HOST_WAIT_STATS") == '1';
-    if (!on) return spin_wait_impl(q, ev, qs, who);
     int tmp[PSVO_STAT_WORDS];
     const bool ready = stats_landed(q.host_raw, q.seq, tmp);
     const double t0 = now_ns();
@@ -376,9 +385,46 @@ extern "C" int psvo_engine_timing(psvo_engine *e, double *mean_ms) {
     return PSVO_OK;
 }
 
+extern "C" int psvo_engine_set_clock(psvo_engine *e, int max_steps) {
+    PSVO_REQUIRE(e && max_steps >= 0, "engine_set_clock: bad arguments");
+    while ((int)e->clk.ev.size() < max_steps) {
+        hipEvent_t ev;
+        if (hipEventCreate(&ev) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine_set_clock: event failed");
+        e->clk.ev.push_back(ev);
+    }
+    e->clk.n = 0;
+    e->clk.on = max_steps > 0;
+    return PSVO_OK;
+}
+
+extern "C" int psvo_engine_clock(psvo_engine *e, double *period_ms, int *n_steps) {
+    PSVO_REQUIRE(e && period_ms && n_steps, "engine_clock: null argument");
+    *period_ms = -1.0;
+    *n_steps = e->clk.n;
+    if (e->clk.n >= 2) {
+        float ms = 0.f;
+        hipEvent_t a = e->clk.ev[0], b = e->clk.ev[e->clk.n - 1];
+        if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "engine_clock: event read failed");
+        *period_ms = ms / (double)(e->clk.n - 1);
+    }
+    return PSVO_OK;
+}
+
+extern "C" int psvo_host_wait_stats(double *wait_us, long long *calls, long long *waited, int reset) {
+    PSVO_REQUIRE(wait_us && calls && waited, "host_wait_stats: null argument");
+    *wait_us = g_host_wait.ns / 1e3;
+    *calls = g_host_wait.calls;
+    *waited = g_host_wait.spun;
+    if (reset) g_host_wait = HostWait();
+    return PSVO_OK;
+}
+
 extern "C" void psvo_engine_free(psvo_engine *e) {
     if (!e) return;
-    if (g_host_wait.calls > 0)
+    for (hipEvent_t ev : e->clk.ev) (void)hipEventDestroy(ev);
+    static const bool report = getenv("PSVO_HOST_WAIT_STATS") && *getenv("PSVO_HOST_WAIT_STATS") == '1';
+    if (report && g_host_wait.calls > 0)
         fprintf(stderr, "psvo: host waited for the query statistics %ld times (%ld not yet landed), %.1f us each\n",
                 g_host_wait.calls, g_host_wait.spun, g_host_wait.ns / 1e3 / g_host_wait.calls);
     (void)hipDeviceSynchronize();
@@ -763,7 +809,52 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     float *feat = nullptr, *sdf_s = nullptr, *rgb_s = nullptr, *act = nullptr, *z_vals = nullptr, *tt = nullptr;
     int *leaf = nullptr, *ray_of = nullptr;
     uint64_t *masks = nullptr;
-    if (dev_sized) {
+    const char *sq = getenv("PSVO_SPLIT_QUERY");
+    const char *sp = getenv("PSVO_FUSED_POINTS");
+    const bool fuse_pi = sp && *sp == '1';
+    // the mapping step on one GPU: no padded [R_hit, S_max] copy at all —
+    // the loss kernels read z from the sampler's depth rows, and the
+    // compaction happens inside the interpolation (k_interp_fwd_rays, one
+    // wave per hit ray); PSVO_SPLIT_QUERY=1 keeps the separate kernels
+    const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(sq && *sq == '1');
+    if (dev_sized && rays_path) {
+        // device-sized, round-4 chain: the interpolation (with the compaction)
+        // over every ray slot, R_hit read on the device, and the decoder
+        // forward over the device's M — both queued before the statistics land
+        const psvo::DevBatch db{static_cast<const int *>(qset.a.p[kStatsKeep]), Rq, e->m_cap, max_steps};
+        ENG_BUF(int, leaf_b, kLeaf, db.m_cap * sizeof(int));
+        ENG_BUF(float, tt_b, kT, db.m_cap * sizeof(float));
+        ENG_BUF(int, ray_of_b, kRayOf, db.m_cap * sizeof(int));
+        ENG_BUF(float, feat_b, kFeat, db.m_cap * 16 * sizeof(float));
+        ENG_BUF(float, sdf_b, kSdfS, db.m_cap * sizeof(float));
+        ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
+        ENG_BUF(float, act_b, kAct, (size_t)psvo_mlp_act_floats(db.m_cap, width) * sizeof(float));
+        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(db.m_cap, width) * sizeof(uint64_t));
+        if (engine_overlap(e)) {  // the loss normalisers need only z (aux)
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
+        ENG_CALL(join_adam(e, st, who));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+        ENG_CALL(psvo::interp_fwd_rays(st, Rq, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray, rays_o,
+                                       rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b, ray_of_b, feat_b, db));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        if (early_images) {
+            if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        } else if (!prebuilt) {
+            ENG_CALL(mlp_images(st, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
+        }
+        mark(e, st, PSVO_TIME_MLP_FWD, 0);
+        ENG_CALL(psvo::mlp_fwd_dev(st, db, feat_b, images, sdf_b, rgb_b, act_b, masks_b));
+        mark(e, st, PSVO_TIME_MLP_FWD, 1);
+        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
+        z_vals = const_cast<float *>(s_depth);
+        o.z_stride = max_steps;
+        act = act_b, masks = masks_b;
+        dev_done = true;  // unless the batch turns out not to fit
+    } else if (dev_sized) {
         const psvo::DevBatch db{static_cast<const int *>(qset.a.p[kStatsKeep]), Rq, e->m_cap,
                                 e->s_cap < max_steps ? e->s_cap : max_steps};
         const size_t RSc = (size_t)Rq * db.s_cap;
@@ -822,7 +913,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.s_max = s_max;
     if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
-    if (dev_done && (M > e->m_cap || s_max > e->s_cap || s_max > max_steps || r_hit > Rq)) dev_done = false;
+    if (dev_done && (M > e->m_cap || (!rays_path && s_max > e->s_cap) || s_max > max_steps || r_hit > Rq))
+        dev_done = false;
     // the next steps' capacities: this batch with headroom (never shrinking)
     if (fused_loss && want_act && width == 128 && !dist) {
         const int64_t mc = M + M / 4 + 256;
@@ -844,14 +936,8 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         // box): 24.5 µs for the one kernel against 6.7 + 13.8 for
         // the two (half its lanes hold slots past their ray's samples) and
         // 0.96-0.99 vs 0.94-0.96 ms per iteration, so the split stays default.
-        const char *sp = getenv("PSVO_FUSED_POINTS");
-        const bool fuse_pi = sp && *sp == '1';
-        // the mapping step on one GPU: no padded [R_hit, S_max] copy at all —
-        // the loss kernels read z from the sampler's depth rows, and the
-        // compaction happens inside the interpolation (k_interp_fwd_rays, one
-        // wave per hit ray); PSVO_SPLIT_QUERY=1 keeps the separate kernels
-        const char *sq = getenv("PSVO_SPLIT_QUERY");
-        const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(sq && *sq == '1');
+        o.z_stride = 0;  // a device-sized attempt that did not fit: host-sized below
+        o.z_recorded = false;
         if (rays_path) {
             // the loss normalisers need only z: aux may start them now
             if (engine_overlap(e)) {
@@ -1092,6 +1178,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const float *counts_gt = (!e->x.on() && !want_loss) ? gt_depth : nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise, counts_gt));
     QueryGuard guard{e, st, qset};
+    if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
     hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward

@@ -80,6 +80,9 @@ _SIGNATURES = {
     "psvo_engine_exchange_words": (_i64, [_i32, _i64]),
     "psvo_engine_set_exchange": (_i32, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
     "psvo_engine_timing": (_i32, [_vp, _vp]),
+    "psvo_engine_set_clock": (_i32, [_vp, _i32]),
+    "psvo_engine_clock": (_i32, [_vp, _vp, _vp]),
+    "psvo_host_wait_stats": (_i32, [_vp, _vp, _vp, _i32]),
     "psvo_map_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
     "psvo_map_adam_ex": (_i32, [_vp, _vp, _vp, _i64, _i32]),

@@ -30,6 +30,45 @@ def world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+class CollectiveTimer:
+    """Durations of the data-parallel engine's collectives (bench.py's
+    collective_ms_per_step): RCCL ones by HIP events on the stream each runs
+    on, gloo ones (host-staged, blocking) by the host clock."""
+
+    def __init__(self):
+        self.pairs = []     # (start, end) torch.cuda.Event
+        self.host_s = 0.0   # gloo: seconds of host time
+        self.count = 0
+
+    def cuda(self, stream=None):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        self.pairs.append((a, b))
+        self.count += 1
+        return a, b
+
+    def total_ms(self):
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.pairs) + 1e3 * self.host_s
+
+
+TIMER = None  # a CollectiveTimer while the bench measures the exchanges
+
+
+class _HostSpan:
+    def __enter__(self):
+        import time
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        import time
+        if TIMER is not None:
+            TIMER.host_s += time.perf_counter() - self.t0
+            TIMER.count += 1
+        return False
+
+
 class GradBucket:
     """Flat all-reduce of the gradients of `params` (one collective).
 
@@ -340,11 +379,20 @@ class EngineExchange:
         if self.nccl:
             ctx = torch.cuda.stream(torch.cuda.ExternalStream(stream)) if stream else _nullctx()
             with ctx:
+                ev = TIMER.cuda() if TIMER is not None else None
+                if ev:
+                    ev[0].record()
                 if op == XCH_GATHER_I32:
                     dist.all_gather_into_tensor(dst, src, group=grp)
                 else:
                     dist.all_reduce(dst, op=dist.ReduceOp.SUM, group=grp)
+                if ev:
+                    ev[1].record()
             return
+        with _HostSpan():
+            self._apply_gloo(op, src, dst, grp, stream)
+
+    def _apply_gloo(self, op, src, dst, grp, stream):
         # gloo: stage through the host, ordered on the engine's stream
         if stream and src.is_cuda:
             torch.cuda.ExternalStream(stream).synchronize()
@@ -421,6 +469,18 @@ class EngineGradExchange:
         ws = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
         if ws == 1 and not self.force:
             return  # no exchange ran: the engine's Adam steps the table densely
+        if TIMER is None:
+            return self._exchange(ws)
+        if _backend(self.group) == "nccl":
+            a, b = TIMER.cuda()
+            a.record()
+            self._exchange(ws)
+            b.record()
+        else:
+            with _HostSpan():
+                self._exchange(ws)
+
+    def _exchange(self, ws):
         flat = self.engine.grad_flat
         n = self.n_emb * 16
         union, local = self.engine.row_flags, self.engine.row_local  # sparse-exact Adam (engine.set_exchange)

@@ -350,6 +350,25 @@ class MappingEngine:
         untimed step runs them (side streams overlapping the main stream)."""
         L.call("psvo_engine_set_timing", self.handle, 2 if on == "overlap" else int(bool(on)))
 
+    def set_clock(self, max_steps):
+        """Record an event on the launching stream at each mapping step's entry
+        (up to max_steps; 0: off) — see clock()."""
+        L.call("psvo_engine_set_clock", self.handle, int(max_steps))
+
+    def clock(self):
+        """(mean GPU-side period per step in ms or None, steps recorded)."""
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        L.call("psvo_engine_clock", self.handle, ctypes.byref(ms), ctypes.byref(n))
+        return (ms.value if ms.value >= 0 else None), n.value
+
+    @staticmethod
+    def host_wait_stats(reset=False):
+        """(µs the host spent waiting for query statistics, waits, waits that
+        found them not yet landed) since the last reset, process-wide."""
+        us, calls, waited = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_longlong()
+        L.call("psvo_host_wait_stats", ctypes.byref(us), ctypes.byref(calls), ctypes.byref(waited), int(reset))
+        return us.value, calls.value, waited.value
+
     REGIONS = ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd", "intersect", "sample", "points")
 
     def timing(self):
