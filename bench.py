@@ -287,14 +287,14 @@ def cpu_baseline(args, scene, tree, step_size, seconds):
 
 
 CHAIN_KERNELS = ("k_intersect_sorted", "k_ray_stats_rank", "k_sample_fused", "k_scan_samples", "k_sample_points",
-                 "k_interp_fwd", "k_points_interp", "k_interp_fwd_rays")
+                 "k_interp_fwd", "k_points_interp", "k_interp_fwd_rays", "k_compact_rays")
 # the kernels each timed region of the query + interp chain launches (for the
 # per-region PMC traffic): intersect (+ its statistics / rank tail or pass),
 # sampler (+ scan), compaction, interpolation (the headline's k_interp_fwd_rays
 # does the compaction too)
 REGION_KERNELS = {"intersect": ("k_intersect_sorted", "k_ray_stats_rank"),
                   "sample": ("k_sample_fused", "k_scan_samples"),
-                  "points": ("k_sample_points",),
+                  "points": ("k_sample_points", "k_compact_rays"),
                   "interp_fwd": ("k_interp_fwd", "k_interp_fwd_rays", "k_points_interp")}
 MLP_KERNELS = ("k_mlp_prep", "k_mlp_fwd2", "k_mlp_bwd3", "k_mlp_bwd2", "k_mlp_dw2", "k_mlp_dw_reduce",
                "k_dec256_prep", "k_dec256_fwd", "k_dec256_bwd", "k_dec256_dw", "k_dec256_dw_reduce")
@@ -642,13 +642,21 @@ def main():
             r.update(extra)
         return r
 
-    split_q = os.environ.get("PSVO_SPLIT_QUERY") == "1"
-    chain_desc = ("k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples, " +
-                  ("k_points_interp = compaction + interp fwd" if os.environ.get("PSVO_FUSED_POINTS") == "1"
-                   else "k_sample_points, k_interp_fwd")) if split_q or world > 1 else \
-        ("k_intersect_sorted with the statistics / hit-rank pass in its last workgroup, k_sample_fused with the "
-         "sample scan, the loss normalisers and the read-back in its last workgroup, k_interp_fwd_rays = "
-         "compaction + interp fwd")
+    env = os.environ.get
+    if env("PSVO_QUERY_TAILS") == "1" and world == 1:
+        q_desc = ("k_intersect_sorted with the statistics / hit-rank pass in its last workgroup, k_sample_fused "
+                  "with the sample scan and read-back in its last workgroup")
+    else:
+        q_desc = "k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples"
+    if env("PSVO_FUSED_POINTS") == "1":
+        i_desc = "k_points_interp = compaction + interp fwd"
+    elif world > 1 or env("PSVO_PADDED_Z") == "1":
+        i_desc = "k_sample_points, k_interp_fwd"
+    elif env("PSVO_INTERP_RAYS") == "1":
+        i_desc = "k_interp_fwd_rays = compaction + interp fwd"
+    else:
+        i_desc = "k_compact_rays, k_interp_fwd"
+    chain_desc = q_desc + ", " + i_desc
     kern_tr = tr.get("kernels") or {}
     per_region = {}
     for k in q_keys:

@@ -54,6 +54,7 @@ struct QuerySet {
     bool done_recorded = false;   // a query consumed on its own stream skips it (one packet less there)
     hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
     bool freed_recorded = false;
+    hipStream_t freed_on = nullptr;  // the stream `freed` was recorded on (a wait on that stream is implied)
     bool pending = false;
     int64_t R = 0;
     const float *ro = nullptr, *rd = nullptr;
@@ -73,6 +74,7 @@ struct EngineTimer {
     bool on = false;
     bool overlap = false;  // mode 2: events on the streams the regions run on, side streams kept
     bool pending = false;  // events of the last step not yet read
+    unsigned used = 0;     // regions the last step marked (a step may skip one: no compaction kernel)
     hipEvent_t ev[PSVO_TIME_REGIONS][2] = {};
     double ms[PSVO_TIME_REGIONS] = {};
     int64_t n[PSVO_TIME_REGIONS] = {};
@@ -189,17 +191,23 @@ void timer_collect(psvo_engine *e) {
     EngineTimer &t = e->tm;
     if (!t.pending) return;
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
+        if (!(t.used & (1u << r))) continue;  // never recorded: reading it would leave a sticky HIP error
         float ms = 0.f;
         if (hipEventSynchronize(t.ev[r][1]) == hipSuccess && hipEventElapsedTime(&ms, t.ev[r][0], t.ev[r][1]) == hipSuccess) {
             t.ms[r] += ms;
             t.n[r] += 1;
+        } else {
+            (void)hipGetLastError();  // not the next launch's error
         }
     }
+    t.used = 0;
     t.pending = false;
 }
 
 inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
-    if (e->tm.on) (void)hipEventRecord(e->tm.ev[region][end], st);
+    if (!e->tm.on) return;
+    (void)hipEventRecord(e->tm.ev[region][end], st);
+    if (end) e->tm.used |= 1u << region;
 }
 
 // st waits for a split tail's optimiser step (map_step_impl) if one is pending
@@ -327,6 +335,7 @@ extern "C" int psvo_map_discard(psvo_engine *e) {
         if (qs && hipEventRecord(q.freed, qs) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_discard: event record failed");
         q.freed_recorded = qs != nullptr;
+        q.freed_on = qs;
         q.pending = false;
         e->q_head ^= 1;
         e->q_count--;
@@ -724,6 +733,7 @@ struct QueryGuard {
 int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
     if (hipEventRecord(q->freed, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
     q->freed_recorded = true;
+    q->freed_on = st;
     if (e->q_count > 0 && q == &e->qs[e->q_head]) {
         q->pending = false;
         e->q_head ^= 1;
@@ -766,7 +776,7 @@ int fork_join(hipStream_t from, hipStream_t st, hipEvent_t ev) {
 // (mapping); tracking keeps only the masks.
 int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qset, const float *rays_o,
            const float *rays_d, bool want_act, int *stats_out, const char *who, Render &o,
-           bool fused_loss = false) {
+           bool fused_loss = false, bool need_z_event = true) {
     int rc = PSVO_OK;
     void *stream = st;
     const int max_steps = qset.max_steps;
@@ -809,14 +819,19 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     float *feat = nullptr, *sdf_s = nullptr, *rgb_s = nullptr, *act = nullptr, *z_vals = nullptr, *tt = nullptr;
     int *leaf = nullptr, *ray_of = nullptr;
     uint64_t *masks = nullptr;
-    const char *sq = getenv("PSVO_SPLIT_QUERY");
     const char *sp = getenv("PSVO_FUSED_POINTS");
     const bool fuse_pi = sp && *sp == '1';
     // the mapping step on one GPU: no padded [R_hit, S_max] copy at all —
-    // the loss kernels read z from the sampler's depth rows, and the
-    // compaction happens inside the interpolation (k_interp_fwd_rays, one
-    // wave per hit ray); PSVO_SPLIT_QUERY=1 keeps the separate kernels
-    const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(sq && *sq == '1');
+    // the loss kernels read z from the sampler's depth rows (stride
+    // max_steps) and the compaction is ray-major (k_compact_rays: a wave per
+    // hit ray over its ≈ 64 valid entries, not the S_max-wide row), then
+    // k_interp_fwd; PSVO_INTERP_RAYS=1: compaction inside a ray-major
+    // interpolation (k_interp_fwd_rays, one launch); PSVO_PADDED_Z=1 (or
+    // PSVO_FUSED_POINTS=1): the padded copy as the autograd path makes it
+    const char *ir = getenv("PSVO_INTERP_RAYS");
+    const char *pz = getenv("PSVO_PADDED_Z");
+    const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(pz && *pz == '1');
+    const bool interp_rays = rays_path && ir && *ir == '1';
     if (dev_sized && rays_path) {
         // device-sized, round-4 chain: the interpolation (with the compaction)
         // over every ray slot, R_hit read on the device, and the decoder
@@ -830,15 +845,25 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
         ENG_BUF(float, act_b, kAct, (size_t)psvo_mlp_act_floats(db.m_cap, width) * sizeof(float));
         ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(db.m_cap, width) * sizeof(uint64_t));
-        if (engine_overlap(e)) {  // the loss normalisers need only z (aux)
+        if (engine_overlap(e) && need_z_event) {  // the loss normalisers need only z (aux)
             if (hipEventRecord(e->z_ready, st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
             o.z_recorded = true;
         }
+        if (!interp_rays) {
+            mark(e, st, PSVO_TIME_POINTS, 0);
+            ENG_CALL(psvo::compact_rays(st, Rq, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, db));
+            mark(e, st, PSVO_TIME_POINTS, 1);
+        }
         ENG_CALL(join_adam(e, st, who));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-        ENG_CALL(psvo::interp_fwd_rays(st, Rq, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray, rays_o,
-                                       rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b, ray_of_b, feat_b, db));
+        if (interp_rays)
+            ENG_CALL(psvo::interp_fwd_rays(st, Rq, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray,
+                                           rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b, ray_of_b,
+                                           feat_b, db));
+        else
+            ENG_CALL(psvo::interp_fwd_dev(st, db, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
+                                          d->centres, d->vertex_idx, d->emb, feat_b));
         mark(e, st, PSVO_TIME_INTERP_FWD, 1);
         if (early_images) {
             if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
@@ -939,17 +964,28 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         o.z_stride = 0;  // a device-sized attempt that did not fit: host-sized below
         o.z_recorded = false;
         if (rays_path) {
-            // the loss normalisers need only z: aux may start them now
-            if (engine_overlap(e)) {
+            // the loss normalisers need only z: aux may start them now (a
+            // marker packet on st: none when aux has nothing to wait for)
+            if (engine_overlap(e) && need_z_event) {
                 if (hipEventRecord(e->z_ready, st) != hipSuccess)
                     return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
                 o.z_recorded = true;
             }
+            if (!interp_rays) {
+                mark(e, st, PSVO_TIME_POINTS, 0);
+                ENG_CALL(psvo::compact_rays(st, r_hit, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b,
+                                            psvo::DevBatch{}));
+                mark(e, st, PSVO_TIME_POINTS, 1);
+            }
             ENG_CALL(join_adam(e, st, who));
             mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-            ENG_CALL(psvo::interp_fwd_rays(st, r_hit, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray,
-                                           rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b,
-                                           ray_of_b, feat_b, psvo::DevBatch{}));
+            if (interp_rays)
+                ENG_CALL(psvo::interp_fwd_rays(st, r_hit, max_steps, d->voxel_size, s_idx, s_depth, offsets,
+                                               rank_ray, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b,
+                                               tt_b, ray_of_b, feat_b, psvo::DevBatch{}));
+            else
+                ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o,
+                                         rays_d, d->centres, d->vertex_idx, d->emb, feat_b));
             mark(e, st, PSVO_TIME_INTERP_FWD, 1);
             z_b = const_cast<float *>(s_depth);
             o.z_stride = max_steps;
@@ -1135,7 +1171,9 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
     int rc = PSVO_OK;
     PSVO_REQUIRE(e->q_count == 0, "map_step_frames: a query is already queued");
     QuerySet &q = e->qs[e->q_head];
-    if (q.freed_recorded && hipStreamWaitEvent(st, q.freed, 0) != hipSuccess)
+    // the set's last consumer ran on st itself: stream order suffices (no wait
+    // packet between the backward and the pose step)
+    if (q.freed_recorded && q.freed_on != st && hipStreamWaitEvent(st, q.freed, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step_frames: stream ordering failed");
     ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
     ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
@@ -1205,7 +1243,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     ENG_CALL(join_adam(e, st, "map_step"));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
-    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true));
+    // aux waits for z only to count the normalisers itself, or to mark the
+    // rows the width-256 backward's scatter will touch
+    const bool coef_known = counts_gt && qset->counts_gt == counts_gt;
+    const bool need_z = !coef_known || e->x.on() ||
+                        (d->emb_row_flags && !psvo::mlp_bwd_fuses_interp(d->width));
+    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     const int64_t M = q.m;

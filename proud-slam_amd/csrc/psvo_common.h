@@ -136,6 +136,10 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
                      const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
                      const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
                      float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
+// sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
+// the valid prefix of each sampler row → leaf / t / ray_of_sample at offsets[r] + s
+int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const float *s_depth, const int *offsets,
+                 int *leaf, float *t, int *ray_of_sample, const DevBatch &dev);
 // sample compaction + interpolation forward, one wave per hit ray (the
 // engine's mapping path, interp.hip k_interp_fwd_rays): the valid prefix of
 // each sampler row s_idx / s_depth [R, cap] goes to compact positions

@@ -1412,8 +1412,11 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     const int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
                                        ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
                                        slot0_nch, il, bins_all[threadIdx.x / kWave], tl, cnt_word);
-    if (!tl.offsets) {
-        if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) ray_ns[il] = count;
+    if (!tl.offsets) {  // k_scan_samples reads them after the launch
+        if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) {
+            ray_ns[il] = count;
+            if (tl.c.gt_depth) tl.c.ray_cnt[il] = cnt_word;
+        }
         return;
     }
     if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) {
@@ -1611,9 +1614,10 @@ __device__ void scan_samples_tail(int64_t n, const int *__restrict__ ray_ns, int
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
                                                        int *__restrict__ stats, int dist, unsigned long long *host,
-                                                       int seq, int *__restrict__ keep) {
+                                                       int seq, int *__restrict__ keep, SampleCounts cnt) {
     __shared__ int total;
     __shared__ int smax[16];
+    __shared__ long long s_c[7][16];
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
                                : n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
     const int64_t n = max((int64_t)0, min(n_own, r_hit_cap));
@@ -1621,12 +1625,52 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
     block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total, &mx);
     mx = wave_max(mx);
     if ((threadIdx.x & (kWave - 1)) == 0) smax[threadIdx.x / kWave] = mx;
+    if (cnt.gt_depth) {  // the loss normalisers' per-ray counts (k_sample_fused), exact integer sums
+        long long c[7] = {};
+        for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)blockDim.x * 8) {
+            int cw[8], ns[8];  // one round of independent loads, then the sums
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t i = i0 + (int64_t)k * blockDim.x;
+                cw[k] = i < n ? cnt.ray_cnt[i] : 0;
+                ns[k] = i < n ? ray_ns[i] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int pf = (cw[k] >> 24) & 1, psm = (cw[k] >> 25) & 1;
+                c[0] += cw[k] & 0xFFF;
+                c[1] += (cw[k] >> 12) & 0xFFF;
+                c[2] += pf;
+                c[3] += psm;
+                c[4] += (cw[k] >> 26) & 1;
+                c[5] += pf ? ns[k] : 0;
+                c[6] += psm ? ns[k] : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) c[k] += __shfl_xor(c[k], sh, kWave);
+            if ((threadIdx.x & (kWave - 1)) == 0) s_c[k][threadIdx.x / kWave] = c[k];
+        }
+    }
     __syncthreads();
     if (threadIdx.x < kWave) {  // wave 0; with `host` one statistics word per lane (no serial copy loop)
         const int lane = threadIdx.x;
         for (int k = 1; k < (int)(blockDim.x / kWave); ++k) mx = max(mx, smax[k]);
         const int tot = total;
         if (lane == 0) offsets[n] = tot;
+        if (cnt.gt_depth && lane == 0) {  // the count sums over the padded [R_hit, S_max] layout → coefficients
+            long long t[7];
+            for (int k = 0; k < 7; ++k) {
+                t[k] = 0;
+                for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t[k] += s_c[k][w];
+            }
+            const long long n_f = t[0] + (long long)mx * t[2] - t[5];
+            const long long n_s = t[1] + (long long)mx * t[3] - t[6];
+            crit_coef_from_counts((double)t[4], (double)n_f, (double)n_s, (double)n, (double)mx, cnt.w_rgb,
+                                  cnt.w_depth, cnt.w_fs, cnt.w_sdf, cnt.tr, cnt.crit_flags, cnt.coef);
+        }
         if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
             if (lane < PSVO_STAT_WORDS) {
                 const int v = lane == PSVO_STAT_S_MAX ? mx : lane == PSVO_STAT_M ? tot : stats[lane];
@@ -1670,6 +1714,28 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
             t[o] = z;
             ray_of_sample[o] = (int)r;
         }
+    }
+}
+
+// Ray-major sample compaction only (the engine's mapping path: the loss
+// kernels read z from the sampler's rows, so no padded [R_hit, S_max] copy):
+// one wave per hit ray copies the valid prefix of its sampler row to the
+// compact arrays — ns ≈ 64 entries, not the S_max-wide row k_sample_points
+// walks.  dev.stats: R_hit from the device statistics.
+__global__ __launch_bounds__(256) void k_compact_rays(int64_t r_hit, int cap, const int *__restrict__ s_idx,
+                                                      const float *__restrict__ s_depth,
+                                                      const int *__restrict__ offsets, int *__restrict__ leaf,
+                                                      float *__restrict__ t, int *__restrict__ ray_of_sample,
+                                                      DevBatch dev) {
+    if (dev.stats) r_hit = dev_batch_fits(dev) ? dev.stats[PSVO_STAT_R_HIT] : 0;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= r_hit) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int beg = offsets[r], ns = offsets[r + 1] - beg;
+    for (int s = lane; s < ns; s += kWave) {
+        leaf[beg + s] = s_idx[r * cap + s];
+        t[beg + s] = s_depth[r * cap + s];
+        ray_of_sample[beg + s] = (int)r;
     }
 }
 
@@ -1823,13 +1889,17 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
 }
 
 namespace psvo {
-// PSVO_SPLIT_QUERY=1: the statistics / rank pass and the sample scan as
-// kernels of their own (A/B, tests), not the launches' last workgroups
+// The statistics / rank pass and the sample scan run as kernels of their own
+// by default.  PSVO_QUERY_TAILS=1 runs them in the traversal's and the
+// sampler's last-arriving workgroups instead (no kernel boundary): measured
+// slower on room0 — 42 vs 33 µs and 35 vs 24 µs per region (four interleaved
+// A/B runs): one workgroup's dependent sc1 round trips cost more
+// than the ≈2 µs boundary they save.
 static bool split_query() {
-    const char *v = getenv("PSVO_SPLIT_QUERY");
-    return v && *v == '1';
+    const char *v = getenv("PSVO_QUERY_TAILS");
+    return !(v && *v == '1');
 }
-bool sampler_counts(int64_t r) { return !split_query() && r <= (int64_t)256 * kTailPasses; }
+bool sampler_counts(int64_t r) { return split_query() || r <= (int64_t)256 * kTailPasses; }
 // the single-GPU sampler with the statistics read-back fused into its scan
 // (one launch less before the host can size the rest of the step)
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
@@ -1840,12 +1910,10 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
     // up to 256 · kTailPasses hit rays the scan and the read-back run in the
     // sampler launch's last workgroup (counter word zeroed with the statistics)
-    const bool tail = sampler_counts(r_hit_cap);
+    const bool tail = !split_query() && r_hit_cap <= (int64_t)256 * kTailPasses;
     SampleTail tl{};
-    if (tail) {
-        tl.offsets = offsets;
-        if (counts) tl.c = *counts;
-    }
+    if (tail) tl.offsets = offsets;
+    if (counts) tl.c = *counts;
     tl.host = host;
     tl.seq = seq;
     tl.keep = keep;
@@ -1854,7 +1922,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                        s_dist, ray_ns, nullptr, 0, tl);
     if (!tail)
         hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
-                           host, seq, keep);
+                           host, seq, keep, tl.c);
     return check_launch("sample_rays_to_host");
 }
 
@@ -1917,7 +1985,7 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch, SampleTail{});
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
-                       nullptr, 0, nullptr);
+                       nullptr, 0, nullptr, SampleCounts{});
     return check_launch("dist_sample");
 }
 int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
@@ -1951,7 +2019,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{});
     hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
-                       stats, 0, nullptr, 0, nullptr);
+                       stats, 0, nullptr, 0, nullptr, SampleCounts{});
     return check_launch("sample_rays");
 }
 
@@ -1994,6 +2062,15 @@ extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int ma
 }
 
 namespace psvo {
+int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const float *s_depth, const int *offsets,
+                 int *leaf, float *t, int *ray_of_sample, const DevBatch &dev) {
+    PSVO_REQUIRE(r_hit >= 0 && cap > 0, "compact_rays: bad sizes");
+    if (r_hit == 0) return PSVO_OK;
+    hipLaunchKernelGGL(k_compact_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, s_idx, s_depth, offsets,
+                       leaf, t, ray_of_sample, dev);
+    return check_launch("compact_rays");
+}
+
 int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, const int *s_idx, const float *s_depth,
                       const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals, uint8_t *mask) {
     PSVO_REQUIRE(b.stats && b.r_cap > 0 && b.s_cap > 0 && b.s_cap <= max_steps_cap && b.m_cap > 0,

@@ -93,6 +93,8 @@ class MappingEngine:
         d.grad_flat = self.grad_flat.data_ptr()
         self.desc = d
         self.packed = None
+        self._tree_key = None   # the map arrays (pointer, shape, version) the packed tree was built from
+        self._bound_key = None  # the embedding moments (pointer, version) the row flags were seeded from
         self.refresh_tree()
         # sparse-exact Adam for the embedding table (include/psvo.h emb_row_flags;
         # PSVO_SPARSE_ADAM=0: dense)
@@ -109,11 +111,31 @@ class MappingEngine:
             raise L.PsvoError("psvo_engine_new failed")
         self.handle = _vp(h)
 
-    def refresh_tree(self):
+    def _map_key(self):
+        ms = self.ms
+        return tuple((t.data_ptr(), tuple(t.shape), t._version)
+                     for t in (ms["voxel_center_xyz"], ms["voxel_structure"], ms["voxel_vertex_idx"]))
+
+    def refresh_tree(self, force=False):
         """(Re)build the breadth-first packed node records the query
         traverses (psvo_pack_tree; same hits as the reference arrays) from the
-        current centres / structure — after the map changed in place.
+        current centres / structure — when the map's arrays changed since the
+        last build (another tensor, or an in-place write: torch's version
+        counter), or with force.  A changed map's arrays are taken again first
+        (the engine holds int32 / f32 copies where the caller's dtype differs).
         PSVO_PACKED=0 keeps the reference-array traversal."""
+        key = self._map_key()
+        if not force and key == self._tree_key:
+            return  # unchanged: no 17-level repack on every bundle_adjust_frames call
+        if self._tree_key is not None:
+            self.centres = self.ms["voxel_center_xyz"].float().contiguous()
+            self.structure = self.ms["voxel_structure"].int().contiguous()
+            self.vertex_idx = self.ms["voxel_vertex_idx"].int().contiguous()
+            d = self.desc
+            d.n_nodes = self.centres.shape[0]
+            d.centres, d.structure, d.vertex_idx = (t.data_ptr() for t in (self.centres, self.structure,
+                                                                            self.vertex_idx))
+        self._tree_key = key
         if os.environ.get("PSVO_PACKED", "1") == "0":
             self.packed = None
             self.desc.packed = None
@@ -134,9 +156,13 @@ class MappingEngine:
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.shape == ref.shape):
                 raise RuntimeError("MappingEngine.bind_adam: moments must match the parameters (contiguous f32 CUDA)")
         self.emb_m, self.emb_v, self.dec_m, self.dec_v = emb_m, emb_v, list(dec_m), list(dec_v)
-        if self.row_flags is not None:  # rows whose carried-over moments are non-zero are live
+        # rows whose carried-over moments are non-zero are live — unless these are the very moments of the
+        # last bind, unwritten by torch since (the engine writes them in place and keeps the flags itself)
+        key = (emb_m.data_ptr(), emb_m._version, emb_v.data_ptr(), emb_v._version)
+        if self.row_flags is not None and key != self._bound_key:
             L.call("psvo_adam_flags_from_state", L.stream_of(emb_m.device), emb_m.shape[0], emb_m, emb_v,
                    self.row_flags)
+        self._bound_key = key
         d = self.desc
         d.emb_m, d.emb_v = emb_m.data_ptr(), emb_v.data_ptr()
         for i in range(10):

@@ -20,6 +20,7 @@ octree 256× per intersection; this path syncs twice and copies nothing.
 """
 from __future__ import annotations
 
+import os
 from copy import deepcopy
 
 import torch
@@ -429,8 +430,31 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
     return eng
 
 
+class _CallClock:
+    """PSVO_BA_PROFILE=1: host timestamps of one bundle_adjust_frames call's
+    phases (setup, each step's submission, write-back) to stderr — where a
+    call's fixed cost goes (bench.py's per-call overhead)."""
+
+    def __init__(self):
+        import time
+        self.on = os.environ.get("PSVO_BA_PROFILE") == "1"
+        self.t0 = time.perf_counter()
+        self.marks = []
+
+    def __call__(self, what):
+        if self.on:
+            import time
+            self.marks.append((what, time.perf_counter() - self.t0))
+
+    def report(self):
+        if self.on and self.marks:
+            import sys
+            sys.stderr.write("ba-call " + " ".join(f"{w}={t * 1e3:.3f}" for w, t in self.marks) + "\n")
+
+
 def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays, num_iterations, update_pose,
                           noise, seed_fn=None, lookahead=True):
+    clk = _CallClock()
     emb = eng.emb
     params = eng.params
     st_e = _adam_state(embed_optim, emb)
@@ -438,9 +462,12 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     steps = {int(st_e["step"].item())} | {int(st["step"].item()) for st in st_d}
     if len(steps) != 1:
         return False  # parameters at different Adam steps: the engine steps them together
+    clk("state")
     eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
                   [st["exp_avg_sq"] for st in st_d])
+    clk("bind")
     eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
+    clk("tree")
     eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
     adam_step = steps.pop()
     dev = emb.device
@@ -448,19 +475,23 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     kfs = list(keyframe_graph)
     upd = [bool(kf.stamp != 0 and update_pose and getattr(kf, "optim", None) is not None) for kf in kfs]
     pose_params = [kf.pose.data for kf in kfs]
-    poses = torch.stack([p.detach().to(dev, torch.float32) for p in pose_params]).contiguous()
-    pm = torch.zeros_like(poses)
-    pv = torch.zeros_like(poses)
+    poses = torch.stack([p.detach().to(dev, torch.float32).reshape(6) for p in pose_params]).contiguous()
     pstep = [0] * len(kfs)
     lr_pose = None
+    zero6 = None
+    m_rows, v_rows = [], []
     for f, kf in enumerate(kfs):
         if not upd[f]:
+            if zero6 is None:
+                zero6 = torch.zeros(6, dtype=torch.float32, device=dev)
+            m_rows.append(zero6)
+            v_rows.append(zero6)
             continue
         if not _is_adam(kf.optim):
             return False
         st = _adam_state(kf.optim, pose_params[f])
-        pm[f].copy_(st["exp_avg"].reshape(6))
-        pv[f].copy_(st["exp_avg_sq"].reshape(6))
+        m_rows.append(st["exp_avg"].to(dev, torch.float32).reshape(6))
+        v_rows.append(st["exp_avg_sq"].to(dev, torch.float32).reshape(6))
         pstep[f] = int(st["step"].item())
         lr = kf.optim.param_groups[0]["lr"]
         if lr_pose is not None and lr != lr_pose:
@@ -468,6 +499,8 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         lr_pose = lr
         if tuple(kf.optim.param_groups[0]["betas"]) != tuple(embed_optim.param_groups[0]["betas"]):
             return False
+    pm = torch.stack(m_rows).contiguous()  # the poses' Adam moments [F, 6], one gather each
+    pv = torch.stack(v_rows).contiguous()
     # keyframes whose sample_rays is the reference's uniform gumbel top-k
     # (frame.py:83-85) are sampled together in one native call with the
     # gathers fused (psvo.sample_util.sample_frames); others through their own
@@ -526,9 +559,11 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         ev.record(side)
         return out, ev
 
+    clk("poses")
     cur, cur_ready = draw_ahead(0)
     if cur_ready is not None:
         main.wait_event(cur_ready)
+    clk("draw0")
     for it in range(num_iterations):
         # the engine orders the look-ahead's pose step (reads nxt's dirs) after
         # the draw queued on `side` (next_stream), and with it the next step
@@ -546,6 +581,8 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             eng.adam()
         pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur_steps)]
         cur = nxt if nxt is not None else (draw(it + 1) if it + 1 < num_iterations else None)
+        if it < 2 or it == num_iterations - 1:
+            clk(f"step{it}")
     if side is not None:
         main.wait_stream(side)  # frames' sample_mask / sample_idx of the last draw
     # write back: optimiser steps, pose parameters and their Adam state
@@ -560,6 +597,8 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             st["exp_avg"].copy_(pm[f].to(st["exp_avg"].device).reshape(st["exp_avg"].shape))
             st["exp_avg_sq"].copy_(pv[f].to(st["exp_avg_sq"].device).reshape(st["exp_avg_sq"].shape))
             st["step"].fill_(float(pstep[f]))
+    clk("writeback")
+    clk.report()
     return True
 
 

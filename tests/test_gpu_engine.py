@@ -266,17 +266,23 @@ def _frames_of(w, n):
     return torch.stack(poses).contiguous().to(DEV), torch.cat(dirs).contiguous().to(DEV)
 
 
-def test_query_tails_and_sampler_counts_match_split_kernels(monkeypatch):
-    """The round-4 query chain — the statistics / rank pass in the traversal
-    launch's last workgroup, the sample scan and read-back in the sampler's,
-    the compaction inside the interpolation (k_interp_fwd_rays), and (with
-    PSVO_STEP_NO_LOSS) the loss normalisers counted by the sampler — against
-    the separate kernels (PSVO_SPLIT_QUERY=1: k_ray_stats_rank, k_scan_samples,
-    k_sample_points, k_crit_counts → reduce → coef), two psvo_map_step_frames
-    iterations stopped before Adam from the same state and seeds: the same
-    statistics, the decoder gradient bit for bit (it depends on the forward,
-    the coefficients and the deterministic decoder backward only), the
-    embedding gradient up to the scatter's float-atomic order, the pose
+def test_query_chain_variants_match_padded_path(monkeypatch):
+    """The mapping step's round-4 query / forward chain against the padded
+    path the autograd route takes (PSVO_PADDED_Z=1: k_sample_points writes
+    the [R_hit, S_max] z / mask copy, the loss normalisers by k_crit_counts →
+    reduce → coef on the aux stream), two psvo_map_step_frames iterations
+    stopped before Adam from the same state and seeds, every variant:
+      default_loss  z read from the sampler's rows (stride max_steps), the
+                    ray-major compaction (k_compact_rays), the count chain;
+      counts        + PSVO_STEP_NO_LOSS: the normalisers counted by the
+                    sampler and turned into coefficients by k_scan_samples;
+      tails         + PSVO_QUERY_TAILS=1: the statistics / rank pass and the
+                    scan (with the counts) in the launches' last workgroups;
+      interp_rays   + PSVO_INTERP_RAYS=1: compaction inside a ray-major
+                    interpolation (k_interp_fwd_rays).
+    The same statistics, the decoder gradient bit for bit (it depends on the
+    forward, the coefficients and the deterministic decoder backward only),
+    the embedding gradient up to the scatter's float-atomic order, the pose
     gradient to 1e-5 of its max."""
     from psvo.engine import MappingEngine
     from psvo.octree import map_states
@@ -285,9 +291,12 @@ def test_query_tails_and_sampler_counts_match_split_kernels(monkeypatch):
     poses, dirs = _frames_of(w, n)
     rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
     crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    modes = {"padded": ({"PSVO_PADDED_Z": "1"}, True), "default_loss": ({}, True), "counts": ({}, False),
+             "tails": ({"PSVO_QUERY_TAILS": "1"}, False), "interp_rays": ({"PSVO_INTERP_RAYS": "1"}, False)}
     runs = {}
-    for mode in ("split", "tails_loss", "tails_counts"):
-        monkeypatch.setenv("PSVO_SPLIT_QUERY", "1" if mode == "split" else "0")
+    for mode, (env, want_loss) in modes.items():
+        for k in ("PSVO_PADDED_Z", "PSVO_QUERY_TAILS", "PSVO_INTERP_RAYS"):
+            monkeypatch.setenv(k, env.get(k, "0"))
         e = emb0.clone().to(DEV)
         eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
                             max_distance=10.0, criteria=crit, max_depth=10.0)
@@ -295,15 +304,16 @@ def test_query_tails_and_sampler_counts_match_split_kernels(monkeypatch):
         for it in range(2):
             pg = torch.zeros(poses.shape[0], 8, device=DEV)
             eng.step_frames(dirs, n, poses.clone(), torch.zeros_like(poses), torch.zeros_like(poses), [0, 1], 1e-3,
-                            rgb, depth, seed=500 + it, apply_adam=False, pose_grad=pg,
-                            want_loss=mode != "tails_counts")
+                            rgb, depth, seed=500 + it, apply_adam=False, pose_grad=pg, want_loss=want_loss)
             torch.cuda.synchronize()
             out.append((list(eng.last_stats), eng.grad_flat.cpu().clone(), pg.cpu()))
         runs[mode] = out
         eng.close()
     n_emb = emb0.shape[0] * 16
-    for mode in ("tails_loss", "tails_counts"):
-        for (sa, ga, pa), (sb, gb, pb) in zip(runs["split"], runs[mode]):
+    for mode in modes:
+        if mode == "padded":
+            continue
+        for (sa, ga, pa), (sb, gb, pb) in zip(runs["padded"], runs[mode]):
             assert sa[:13] == sb[:13], (mode, sa, sb)  # statistics (words past 12: the tails' counters, zero)
             assert torch.equal(ga[n_emb:], gb[n_emb:]), mode  # decoder gradient: bit for bit
             torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-5, atol=1e-6 * float(ga[:n_emb].abs().max()))
