@@ -39,6 +39,10 @@ METRIC = "rays/sec render+backward, Replica room0, 64 samples/ray, 1/2/4/8 MI355
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: aggregate L2 (8 x 4 MiB) ≈34.5 TB/s
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (v_mfma_f32_32x32x2_f32) dense peak
+TIMING_NOTE = ("headline mode, inside bundle_adjust_frames iterations: every kernel of a region timed by a HIP "
+               "event pair bound to its own dispatch (hipExtLaunchKernel start / stop: the span rocprofv3 "
+               "--kernel-trace reports, on the stream it runs on); a region = the sum of its kernels' spans "
+               "(PSVO_TIMING_MARKERS=1: marker events around the region instead)")
 
 
 def log(msg):
@@ -458,6 +462,7 @@ def main():
         clocked = False
         if record and eng is not None:
             eng.stats_hook = lambda st: record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3], head_stats)
+        if record and eng is not None and os.environ.get("PSVO_BENCH_NO_CLOCK") != "1":
             try:  # an event at each step's entry on its stream: the GPU-side period
                 eng.set_clock(steps)
                 eng.host_wait_stats(reset=True)
@@ -632,7 +637,7 @@ def main():
         r = {"kernel": kernel, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": gbs / HBM_PEAK_GBS if gbs else None, "traffic": counter_bytes,
              "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": ms,
-             "timing": "headline mode: HIP events on the launching streams inside bundle_adjust_frames iterations",
+             "timing": TIMING_NOTE,
              "frac_hbm_counters": (counter_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if (counter_bytes and ms) else None,
              "frac_l2_algorithmic": gbs / L2_PEAK_GBS if gbs else None}
         if ms_serial:
@@ -696,7 +701,7 @@ def main():
                    "algorithmic_flops_per_launch": 2 * 2.0 * macs * h_m,
                    "interp_bwd_algorithmic_bytes": 1664.0 * h_m,
                    "interp_bwd_bytes_over_kernel_time_frac_hbm": ib_gbs / HBM_PEAK_GBS if ib_gbs else None,
-                   "timing": "headline mode (HIP events inside bundle_adjust_frames iterations)"}
+                   "timing": TIMING_NOTE}
     else:
         roof_ib = bw_roof("k_interp_bwd", 1664.0 * h_m, kt_overlap["interp_bwd"],
                           tr.get("bwd_fused_bytes_per_launch"), kt_serial["interp_bwd"] if kt_serial else None)
@@ -734,7 +739,7 @@ def main():
                           "traffic": tr.get("mlp_bytes_per_step"),
                           "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,
-                          "timing": "headline mode (HIP events inside bundle_adjust_frames iterations)"},
+                          "timing": TIMING_NOTE},
         "roofline_bwd_fused" if fused_ib else "roofline_interp_bwd": roof_ib,
         "path": path_desc,
         "other_path": others if others else "run bench.py --extras for the engine-step and drop-in autograd paths",

@@ -404,7 +404,7 @@ extern "C" int psvo_composite_fwd(void *stream, int64_t r_hit, int s_max, float 
                                   float *sdf, float *weights, float *color, float *depth, float *z_min) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_fwd: bad sizes");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_composite_fwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+    psvo::launch(k_composite_fwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
                        truncation, offsets, ray_ns, z_vals, sdf_s, rgb_s, sdf, weights, color, depth, z_min);
     return check_launch("composite_fwd");
 }
@@ -416,7 +416,7 @@ extern "C" int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float 
                                   float *grad_rgb_s) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f, "composite_bwd: bad sizes");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_composite_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
+    psvo::launch(k_composite_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max,
                        truncation, offsets, ray_ns, z_vals, sdf, weights, rgb_s, grad_color, grad_depth,
                        grad_weights, grad_sdf, grad_sdf_s, grad_rgb_s);
     return check_launch("composite_bwd");
@@ -457,7 +457,7 @@ int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncat
                 : s_max <= 256 ? k_composite_loss<4>
                 : s_max <= 512 ? k_composite_loss<8>
                                : k_composite_loss<0>;
-    hipLaunchKernelGGL(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
+    psvo::launch(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
                        max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
                        workspace, color, depth, grad_sdf_s, grad_rgb_s);
     return check_launch("composite_loss");

@@ -319,11 +319,11 @@ extern "C" int psvo_criterion_depth_filter(void *stream, int64_t r_hit, int s_ma
     PSVO_REQUIRE(r_hit <= kMedianMax, "criterion_depth_filter: %lld hit rays > %d (single-block median)",
                  (long long)r_hit, kMedianMax);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_crit_depth_tmp, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, rank_ray, gt_depth,
+    psvo::launch(k_crit_depth_tmp, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, rank_ray, gt_depth,
                        depth, weights, z_vals, dtmp);
     int n2 = 1;
     while (n2 < r_hit) n2 <<= 1;
-    hipLaunchKernelGGL(k_crit_depth_thr, dim3(1), dim3(1024), n2 * sizeof(float), st, r_hit, dtmp, dthr);
+    psvo::launch(k_crit_depth_thr, dim3(1), dim3(1024), n2 * sizeof(float), st, r_hit, dtmp, dthr);
     return check_launch("criterion_depth_filter");
 }
 
@@ -336,10 +336,10 @@ extern "C" int psvo_criterion_sums_ex(void *stream, int64_t r_hit, int s_max, in
                  "criterion_sums: null pointer");
     PSVO_REQUIRE((dtmp == nullptr) == (dthr == nullptr), "criterion_sums: depth filter needs tmp and threshold");
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
+    psvo::launch(k_crit_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, pad_extra, truncation,
                        max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, dtmp, dthr, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
+    psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_sums");
 }
 
@@ -367,11 +367,11 @@ int psvo::criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncat
                            float *coef) {
     PSVO_REQUIRE(z_stride >= s_max, "criterion_coef: z stride %d < S_max %d", z_stride, s_max);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
+    psvo::launch(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
                        rank_ray, gt_depth, z_vals, z_stride, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
-    hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
+    psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
+    psvo::launch(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
                        fs_w, sdf_w, truncation, flags, coef);
     return check_launch("criterion_coef");
 }
@@ -382,15 +382,15 @@ namespace psvo {
 int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
                      const float *gt_depth, const float *z_vals, float *workspace, double *sums) {
     if (r_hit > 0)
-        hipLaunchKernelGGL(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
+        psvo::launch(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
                            max_depth, rank_ray, gt_depth, z_vals, s_max, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
+    psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");
 }
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef) {
-    hipLaunchKernelGGL(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)n_hit, (double)n_cols, rgb_w, depth_w,
+    psvo::launch(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)n_hit, (double)n_cols, rgb_w, depth_w,
                        fs_w, sdf_w, truncation, flags, coef);
     return check_launch("criterion_coef");
 }
@@ -399,7 +399,7 @@ int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, 
 extern "C" int psvo_criterion_reduce(void *stream, int64_t r_hit, const float *workspace, double *sums) {
     PSVO_REQUIRE(r_hit > 0 && workspace && sums, "criterion_reduce: bad arguments");
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
-    hipLaunchKernelGGL(k_crit_reduce, dim3(1), dim3(64), 0, as_stream(stream), r_hit, workspace, sums);
+    psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, as_stream(stream), r_hit, workspace, sums);
     return check_launch("criterion_reduce");
 }
 
@@ -407,7 +407,7 @@ extern "C" int psvo_criterion_finalize(void *stream, const double *sums, int64_t
                                        float depth_w, float fs_w, float sdf_w, float truncation, int flags,
                                        float *out) {
     PSVO_REQUIRE(n_hit > 0 && s_max > 0, "criterion_finalize: bad sizes");
-    hipLaunchKernelGGL(k_crit_finalize, dim3(1), dim3(64), 0, as_stream(stream), sums, (double)n_hit, (double)s_max,
+    psvo::launch(k_crit_finalize, dim3(1), dim3(64), 0, as_stream(stream), sums, (double)n_hit, (double)s_max,
                        rgb_w, depth_w, fs_w, sdf_w, truncation, flags, out);
     return check_launch("criterion_finalize");
 }
@@ -419,7 +419,7 @@ extern "C" int psvo_criterion_bwd_ex(void *stream, int64_t r_hit, int s_max, flo
                                      float *g_color, float *g_depth, float *g_sdf) {
     PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_bwd: bad sizes");
     PSVO_REQUIRE((dtmp == nullptr) == (dthr == nullptr), "criterion_bwd: depth filter needs tmp and threshold");
-    hipLaunchKernelGGL(k_crit_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
+    psvo::launch(k_crit_bwd, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
                        max_depth, rank_ray, gt_rgb, gt_depth, color, depth, sdf, z_vals, out, g_loss, dtmp, dthr,
                        g_color, g_depth, g_sdf);
     return check_launch("criterion_bwd");

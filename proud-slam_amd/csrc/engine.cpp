@@ -16,6 +16,7 @@
 
 #include <cmath>
 
+#include <utility>
 #include <vector>
 
 #include "psvo_common.h"
@@ -74,10 +75,15 @@ struct EngineTimer {
     bool on = false;
     bool overlap = false;  // mode 2: events on the streams the regions run on, side streams kept
     bool pending = false;  // events of the last step not yet read
+    bool markers = false;  // PSVO_TIMING_MARKERS=1: marker events around each region (the old timing)
     unsigned used = 0;     // regions the last step marked (a step may skip one: no compaction kernel)
     hipEvent_t ev[PSVO_TIME_REGIONS][2] = {};
     double ms[PSVO_TIME_REGIONS] = {};
     int64_t n[PSVO_TIME_REGIONS] = {};
+    // kernel-bound timing (the default): the regions' kernels' own spans
+    psvo::KernelClock kc;
+    double kms[PSVO_TIME_REGIONS] = {};     // Σ kernel spans collected
+    int64_t starts[PSVO_TIME_REGIONS] = {};  // region instances queued (a region's time = kms / starts)
 };
 
 // Data-parallel exchange (psvo_engine_set_exchange): the caller's collective
@@ -161,6 +167,10 @@ using namespace psvo;
         if (_rc != PSVO_OK) return _rc; \
     } while (0)
 
+namespace psvo {
+KernelClock *g_kclock = nullptr;
+}
+
 namespace {
 
 // device buffer of at least `bytes` for `slot`; growing synchronises the
@@ -187,8 +197,35 @@ void *slot_buf(psvo_engine *e, hipStream_t st, int slot, size_t bytes, int *rc) 
     return arena_buf(e->a, st, slot, bytes, rc);
 }
 
-void timer_collect(psvo_engine *e) {
+// block = false: only the pairs whose kernels have finished (a timed step's
+// host must not wait for kernels it queued ahead); the rest move to the front
+void timer_collect(psvo_engine *e, bool block = false) {
     EngineTimer &t = e->tm;
+    if (!t.markers) {  // kernel-bound
+        psvo::KernelClock &c = t.kc;
+        int w = 0;
+        for (int i = 0; i < c.n; ++i) {
+            const hipError_t q = block ? hipEventSynchronize(c.ev[i][1]) : hipEventQuery(c.ev[i][1]);
+            if (q == hipErrorNotReady) {
+                if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // not an error
+                if (w != i) {
+                    std::swap(c.ev[w][0], c.ev[i][0]);
+                    std::swap(c.ev[w][1], c.ev[i][1]);
+                    c.region[w] = c.region[i];
+                }
+                ++w;
+                continue;
+            }
+            float ms = 0.f;
+            if (q == hipSuccess && hipEventElapsedTime(&ms, c.ev[i][0], c.ev[i][1]) == hipSuccess)
+                t.kms[c.region[i]] += ms;
+            else
+                (void)hipGetLastError();  // not the next launch's error
+        }
+        c.n = w;
+        t.pending = false;
+        return;
+    }
     if (!t.pending) return;
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
         if (!(t.used & (1u << r))) continue;  // never recorded: reading it would leave a sticky HIP error
@@ -205,9 +242,22 @@ void timer_collect(psvo_engine *e) {
 }
 
 inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
-    if (!e->tm.on) return;
-    (void)hipEventRecord(e->tm.ev[region][end], st);
-    if (end) e->tm.used |= 1u << region;
+    EngineTimer &t = e->tm;
+    if (!t.on) return;
+    if (t.markers) {
+        (void)hipEventRecord(t.ev[region][end], st);
+        if (end) t.used |= 1u << region;
+        return;
+    }
+    psvo::KernelClock &c = t.kc;
+    if (!end) {
+        if (c.n + 32 > psvo::KernelClock::kMax) timer_collect(e, true);  // room for the region's kernels
+        if (c.depth < 8) c.stack[c.depth++] = region;
+        t.starts[region] += 1;
+        psvo::g_kclock = &c;
+    } else if (c.depth > 0) {
+        c.depth--;
+    }
 }
 
 // st waits for a split tail's optimiser step (map_step_impl) if one is pending
@@ -372,25 +422,47 @@ extern "C" int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int
 
 extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
     PSVO_REQUIRE(e, "engine_set_timing: null engine");
-    if (on && !e->tm.ev[0][0])
+    EngineTimer &t = e->tm;
+    const char *mk = getenv("PSVO_TIMING_MARKERS");
+    if (on && !t.ev[0][0])
         for (int r = 0; r < PSVO_TIME_REGIONS; ++r)
             for (int k = 0; k < 2; ++k)
-                if (hipEventCreate(&e->tm.ev[r][k]) != hipSuccess)
+                // a device-scope release: a marker with the default system-scope one
+                // writes the L2 back between the kernels it brackets (measured in the time)
+                if (hipEventCreateWithFlags(&t.ev[r][k], hipEventReleaseToDevice) != hipSuccess)
                     return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
-    timer_collect(e);
-    e->tm.on = on != 0;
-    e->tm.overlap = on == 2;
+    if (on && !t.kc.ev[0][0])
+        for (int i = 0; i < psvo::KernelClock::kMax; ++i)
+            for (int k = 0; k < 2; ++k)
+                if (hipEventCreate(&t.kc.ev[i][k]) != hipSuccess)
+                    return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
+    timer_collect(e, true);
+    if (psvo::g_kclock == &t.kc) psvo::g_kclock = nullptr;
+    t.kc.depth = 0;
+    t.kc.overflow = false;
+    t.on = on != 0;
+    t.overlap = on == 2;
+    t.markers = mk && *mk == '1';
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
-        e->tm.ms[r] = 0.0;
-        e->tm.n[r] = 0;
+        t.ms[r] = 0.0;
+        t.n[r] = 0;
+        t.kms[r] = 0.0;
+        t.starts[r] = 0;
     }
     return PSVO_OK;
 }
 
 extern "C" int psvo_engine_timing(psvo_engine *e, double *mean_ms) {
     PSVO_REQUIRE(e && mean_ms, "engine_timing: null argument");
-    timer_collect(e);
-    for (int r = 0; r < PSVO_TIME_REGIONS; ++r) mean_ms[r] = e->tm.n[r] ? e->tm.ms[r] / (double)e->tm.n[r] : -1.0;
+    EngineTimer &t = e->tm;
+    timer_collect(e, true);
+    for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
+        if (t.markers)
+            mean_ms[r] = t.n[r] ? t.ms[r] / (double)t.n[r] : -1.0;
+        else  // a region whose instances launched no kernel reads 0 (e.g. no separate compaction)
+            mean_ms[r] = t.starts[r] ? t.kms[r] / (double)t.starts[r] : -1.0;
+    }
+    PSVO_REQUIRE(t.markers || !t.kc.overflow, "engine_timing: more kernels per step than timing slots");
     return PSVO_OK;
 }
 
@@ -398,7 +470,11 @@ extern "C" int psvo_engine_set_clock(psvo_engine *e, int max_steps) {
     PSVO_REQUIRE(e && max_steps >= 0, "engine_set_clock: bad arguments");
     while ((int)e->clk.ev.size() < max_steps) {
         hipEvent_t ev;
-        if (hipEventCreate(&ev) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine_set_clock: event failed");
+        // device-scope release: the clock's marker sits between the query's scan
+        // and the compaction on the critical stream (a system-scope one costs
+        // an L2 write-back there)
+        if (hipEventCreateWithFlags(&ev, hipEventReleaseToDevice) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "engine_set_clock: event failed");
         e->clk.ev.push_back(ev);
     }
     e->clk.n = 0;
@@ -440,6 +516,10 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r)
         for (int k = 0; k < 2; ++k)
             if (e->tm.ev[r][k]) (void)hipEventDestroy(e->tm.ev[r][k]);
+    if (psvo::g_kclock == &e->tm.kc) psvo::g_kclock = nullptr;
+    for (int i = 0; i < psvo::KernelClock::kMax; ++i)
+        for (int k = 0; k < 2; ++k)
+            if (e->tm.kc.ev[i][k]) (void)hipEventDestroy(e->tm.kc.ev[i][k]);
     for (int s = 0; s < kSlots; ++s)
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
     for (auto &q : e->qs) query_set_free(q);
@@ -1238,10 +1318,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // is still reading that query's statistics back, so they cost nothing.
     const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_fuses_interp(d->width) &&
                             !(flags & PSVO_STEP_NO_ADAM);
-    const bool early_next = wait_next && split_tail;
+    // PSVO_LATE_WAITS=1 (A/B): both waits where their consumers are instead
+    static const bool late_waits = getenv("PSVO_LATE_WAITS") && *getenv("PSVO_LATE_WAITS") == '1';
+    const bool early_next = wait_next && split_tail && !late_waits;
     if (early_next && hipStreamWaitEvent(st, e->next_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
-    ENG_CALL(join_adam(e, st, "map_step"));
+    if (!late_waits) ENG_CALL(join_adam(e, st, "map_step"));
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     // aux waits for z only to count the normalisers itself, or to mark the
     // rows the width-256 backward's scatter will touch

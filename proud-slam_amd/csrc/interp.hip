@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void k_interp_rays_gx(int64_t r_hit, const int
 int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int *ray_index, const float *t,
                    const float *gx, float *grad_o, float *grad_d) {
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_interp_rays_gx, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, offsets, ray_index, t, gx,
+    psvo::launch(k_interp_rays_gx, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, offsets, ray_index, t, gx,
                        grad_o, grad_d);
     return check_launch("interp_rays_gx");
 }
@@ -486,7 +486,7 @@ extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size,
     PSVO_REQUIRE(d == 16, "interp_fwd: embedding dim %d unsupported (16 only)", d);
     PSVO_REQUIRE(m >= 0 && voxel_size > 0.f, "interp_fwd: bad sizes");
     if (m == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
+    psvo::launch(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
                        t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<float4 *>(feat), DevBatch{});
@@ -500,7 +500,7 @@ int interp_fwd_rays(hipStream_t st, int64_t r_hit, int cap, float voxel_size, co
                     int *ray_of_sample, float *feat, const DevBatch &dev) {
     PSVO_REQUIRE(r_hit >= 0 && cap > 0 && voxel_size > 0.f, "interp_fwd_rays: bad sizes");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_interp_fwd_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, voxel_size, s_idx,
+    psvo::launch(k_interp_fwd_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, voxel_size, s_idx,
                        s_depth, offsets, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb), leaf, t, ray_of_sample, reinterpret_cast<float4 *>(feat),
                        dev);
@@ -511,7 +511,7 @@ int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const in
                    const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
                    const float *centres, const int *vertex_idx, const float *emb, float *feat) {
     PSVO_REQUIRE(b.stats && b.m_cap > 0 && voxel_size > 0.f, "interp_fwd_dev: bad sizes");
-    hipLaunchKernelGGL(k_interp_fwd, dim3(div_up(b.m_cap * 4, 256)), dim3(256), 0, st, b.m_cap, voxel_size, leaf, t,
+    psvo::launch(k_interp_fwd, dim3(div_up(b.m_cap * 4, 256)), dim3(256), 0, st, b.m_cap, voxel_size, leaf, t,
                        ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb), reinterpret_cast<float4 *>(feat), b);
     return check_launch("interp_fwd_dev");
@@ -526,7 +526,7 @@ int points_interp(hipStream_t st, int64_t r_hit, int s_max, int max_steps_cap, f
     if (r_hit == 0 || s_max == 0) return PSVO_OK;
     const int bx = s_max <= 16 ? 64 : s_max <= 32 ? 128 : 256;  // 4 lanes per slot
     const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
-    hipLaunchKernelGGL(k_points_interp, dim3(div_up((int64_t)s_max * 4, bx), gy), dim3(bx), 0, st, r_hit, s_max,
+    psvo::launch(k_points_interp, dim3(div_up((int64_t)s_max * 4, bx), gy), dim3(bx), 0, st, r_hit, s_max,
                        max_steps_cap, voxel_size, s_idx, s_depth, offsets, leaf, t, ray_of_sample, z_vals, mask,
                        ray_index, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<float4 *>(feat));
@@ -543,12 +543,12 @@ extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_s
     PSVO_REQUIRE(grad_o != nullptr && grad_d != nullptr, "interp_bwd: grad_o / grad_d required");
     if (r_hit == 0) return PSVO_OK;
     if (grad_emb)
-        hipLaunchKernelGGL(k_interp_bwd<true>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+        psvo::launch(k_interp_bwd<true>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            grad_emb, grad_o, grad_d, 0, 1, nullptr);
     else
-        hipLaunchKernelGGL(k_interp_bwd<false>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+        psvo::launch(k_interp_bwd<false>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            nullptr, grad_o, grad_d, 0, 1, nullptr);
@@ -573,16 +573,16 @@ extern "C" int psvo_interp_bwd_chunked(void *stream, int64_t r_hit, int s_max, i
     const int64_t units = r_hit * c_max;
     hipStream_t st = as_stream(stream);
     if (grad_emb)
-        hipLaunchKernelGGL(k_interp_bwd<true>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+        psvo::launch(k_interp_bwd<true>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
                            ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            grad_emb, grad_o, grad_d, kInterpChunk, c_max, workspace);
     else
-        hipLaunchKernelGGL(k_interp_bwd<false>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+        psvo::launch(k_interp_bwd<false>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
                            ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            nullptr, grad_o, grad_d, kInterpChunk, c_max, workspace);
-    hipLaunchKernelGGL(k_interp_bwd_rays, dim3(div_up(r_hit * 6, 256)), dim3(256), 0, st, r_hit, c_max, ray_index,
+    psvo::launch(k_interp_bwd_rays, dim3(div_up(r_hit * 6, 256)), dim3(256), 0, st, r_hit, c_max, ray_index,
                        workspace, grad_o, grad_d);
     return check_launch("interp_bwd_chunked");
 }

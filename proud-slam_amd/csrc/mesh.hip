@@ -532,7 +532,7 @@ extern "C" int psvo_mesh_grid_feat(void *stream, int64_t n_vox, int res, float v
     Lin lin{};
     (void)psvo_mesh_linspace(res, lin.v);
     const int64_t n = n_vox * res * res * res;
-    hipLaunchKernelGGL(k_grid_feat, dim3(div_up(n * 4, 256)), dim3(256), 0, as_stream(stream), n, res, voxel_size,
+    psvo::launch(k_grid_feat, dim3(div_up(n * 4, 256)), dim3(256), 0, as_stream(stream), n, res, voxel_size,
                        lin, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<float4 *>(feat));
     return check_launch("mesh_grid_feat");
@@ -542,7 +542,7 @@ extern "C" int psvo_mesh_point_feat(void *stream, int64_t n, float voxel_size, c
                                     const float *centres, const int *vertex_idx, const float *emb, float *feat) {
     PSVO_REQUIRE(n >= 0 && voxel_size > 0.f, "mesh_point_feat: bad sizes");
     if (n == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_point_feat, dim3(div_up(n * 4, 256)), dim3(256), 0, as_stream(stream), n, voxel_size, xyz,
+    psvo::launch(k_point_feat, dim3(div_up(n * 4, 256)), dim3(256), 0, as_stream(stream), n, voxel_size, xyz,
                        row, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
                        reinterpret_cast<float4 *>(feat));
     return check_launch("mesh_point_feat");
@@ -553,8 +553,8 @@ extern "C" int psvo_mesh_mc_count(void *stream, int64_t n_vox, int res, const fl
     PSVO_REQUIRE(n_vox > 0 && res >= 2 && res <= kMcMaxRes, "mesh_mc_count: bad sizes");
     PSVO_REQUIRE(sdf && nv && nt && vbase && tbase && totals, "mesh_mc_count: null pointer");
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_mc_count, dim3((unsigned)n_vox), dim3(kMcThreads), 0, st, n_vox, res, sdf, nv, nt);
-    hipLaunchKernelGGL(k_mc_offsets, dim3(1), dim3(kMcThreads), 0, st, n_vox, nv, nt, vbase, tbase, totals);
+    psvo::launch(k_mc_count, dim3((unsigned)n_vox), dim3(kMcThreads), 0, st, n_vox, res, sdf, nv, nt);
+    psvo::launch(k_mc_offsets, dim3(1), dim3(kMcThreads), 0, st, n_vox, nv, nt, vbase, tbase, totals);
     return check_launch("mesh_mc_count");
 }
 
@@ -563,7 +563,7 @@ extern "C" int psvo_mesh_mc_emit(void *stream, int64_t n_vox, int res, float vox
                                  float *verts, int *faces) {
     PSVO_REQUIRE(n_vox > 0 && res >= 2 && res <= kMcMaxRes && voxel_size > 0.f, "mesh_mc_emit: bad sizes");
     PSVO_REQUIRE(sdf && centres && nv && vbase && tbase, "mesh_mc_emit: null pointer");
-    hipLaunchKernelGGL(k_mc_emit, dim3((unsigned)n_vox), dim3(kMcThreads), 0, as_stream(stream), n_vox, res,
+    psvo::launch(k_mc_emit, dim3((unsigned)n_vox), dim3(kMcThreads), 0, as_stream(stream), n_vox, res,
                        voxel_size, sdf, centres, nv, vbase, tbase, verts, faces);
     return check_launch("mesh_mc_emit");
 }
@@ -584,9 +584,9 @@ extern "C" int psvo_mesh_vertex_rows(void *stream, int64_t n_vox, const float *v
     if (hipMemsetAsync(table, 0xFF, (size_t)cap * 16, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "mesh_vertex_rows: memset failed");
     if (n_vox > 0)
-        hipLaunchKernelGGL(k_vox_map_insert, dim3(div_up(n_vox, 256)), dim3(256), 0, st, n_vox, voxels,
+        psvo::launch(k_vox_map_insert, dim3(div_up(n_vox, 256)), dim3(256), 0, st, n_vox, voxels,
                            (int)(cap - 1), reinterpret_cast<int4 *>(table));
-    hipLaunchKernelGGL(k_vertex_rows, dim3(div_up(n_verts, 256)), dim3(256), 0, st, n_verts, voxel_size, verts,
+    psvo::launch(k_vertex_rows, dim3(div_up(n_verts, 256)), dim3(256), 0, st, n_verts, voxel_size, verts,
                        (int)(cap - 1), reinterpret_cast<const int4 *>(table), row);
     return check_launch("mesh_vertex_rows");
 }

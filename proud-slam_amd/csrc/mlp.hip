@@ -2357,7 +2357,7 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
     }
     hipStream_t st = as_stream(stream);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    if (!images_ready) hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
+    if (!images_ready) psvo::launch(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
     if (rgb == nullptr) {  // sdf only (inference)
         PSVO_REQUIRE(act == nullptr && masks == nullptr, "mlp_fwd: the sdf-only forward is inference only");
         static bool attr_s = false;
@@ -2368,7 +2368,7 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         }
         const int64_t tiles = div_up(m, kF2Tile);
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-        hipLaunchKernelGGL(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf);
+        psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf);
         return check_launch("mlp_fwd");
     }
     if (use_fwd2()) {
@@ -2380,10 +2380,10 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         }
         const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-        hipLaunchKernelGGL(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
+        psvo::launch(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
                            masks, DevBatch{});
     } else {
-        hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf,
+        psvo::launch(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf,
                            rgb, act, masks);
     }
     return check_launch("mlp_fwd");
@@ -2404,7 +2404,7 @@ int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const floa
     }
     // one workgroup per CU whatever the batch (the balanced split gives small
     // batches empty workgroups, which only stage and leave)
-    hipLaunchKernelGGL(k_mlp_fwd2, dim3(device_cus()), dim3(kF2Threads), kLdsFwd2, st, b.m_cap, feat, images, sdf, rgb,
+    psvo::launch(k_mlp_fwd2, dim3(device_cus()), dim3(kF2Threads), kLdsFwd2, st, b.m_cap, feat, images, sdf, rgb,
                        act, masks, b);
     return check_launch("mlp_fwd_dev");
 }
@@ -2414,7 +2414,7 @@ int mlp_images(void *stream, int width, const float *w1, const float *b1, const 
                float *images) {
     if (width == 256) return dec256_images(as_stream(stream), w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, as_stream(stream), p, images);
+    psvo::launch(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, as_stream(stream), p, images);
     return check_launch("mlp_images");
 }
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
@@ -2555,7 +2555,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             e += kDwRows[l] * kDwCols[l] + kDwRows[l];
         }
         d.elem_begin[5] = e;
-        hipLaunchKernelGGL(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate);
+        psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate);
         return check_launch("mlp_dw_reduce");
     };
     if (use_bwd3()) {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
@@ -2572,7 +2572,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             if (m > 0) {
                 const int64_t rounds = div_up(div_up(m, kU), 8);
                 const int grid = (int)(rounds < device_cus() ? rounds : device_cus());
-                hipLaunchKernelGGL(k_mlp_bwd3<false>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g,
+                psvo::launch(k_mlp_bwd3<false>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g,
                                    nullptr, InterpFuse{});
                 const int rc = check_launch("mlp_bwd3");
                 if (rc) return rc;
@@ -2585,7 +2585,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         dw_grid_uniform(grid, &g, &slab_floats);
         float *slabs = workspace + m * 3;
         if (m > 0) {
-            hipLaunchKernelGGL(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs,
+            psvo::launch(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs,
                                ip ? *ip : InterpFuse{});
             const int rc = check_launch("mlp_bwd3");
             if (rc) return rc;
@@ -2631,10 +2631,10 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             }
             const int64_t tiles = div_up(m, kF2Tile);
             const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-            hipLaunchKernelGGL(k_mlp_bwd2, dim3(grid), dim3(kF2Threads), kLdsBwd2, st, m, images, rgb, masks, g_sdf,
+            psvo::launch(k_mlp_bwd2, dim3(grid), dim3(kF2Threads), kLdsBwd2, st, m, images, rgb, masks, g_sdf,
                                g_rgb, o);
         } else {
-            hipLaunchKernelGGL(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p,
+            psvo::launch(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p,
                                images, rgb, masks, g_sdf, g_rgb, o);
         }
         int rc = check_launch("mlp_bwd_data");
@@ -2663,7 +2663,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     for (int l = 0; l < n_launch; ++l) {
         const int wg0 = n_launch == 1 ? 0 : g.wg_begin[l];
         const int nwg = n_launch == 1 ? g.wg_begin[4] : g.wg_begin[l + 1] - g.wg_begin[l];
-        hipLaunchKernelGGL(k_mlp_dw2, dim3(nwg), dim3(64 * kDw2Waves), kDw2Lds * 4, st, m, src, zblk, g, slabs, wg0);
+        psvo::launch(k_mlp_dw2, dim3(nwg), dim3(64 * kDw2Waves), kDw2Lds * 4, st, m, src, zblk, g, slabs, wg0);
     }
     int rc = check_launch("mlp_dw");
     if (rc) return rc;

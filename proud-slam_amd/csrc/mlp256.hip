@@ -32,6 +32,8 @@
 // TF32-like rounding), the numerics class of the reference's torch.float32.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "psvo_common.h"
 
@@ -192,13 +194,20 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// The chain kernels: 4 waves (one per SIMD, 512 registers each), a wave owns
-// NC = 2 groups of 16 samples; every A operand (one ds_read_b128 = 4 k-steps
-// of one output block) feeds 4 x NC MFMAs.
+// The chain kernels: 8 waves (two per SIMD, ≤ 256 registers each), a wave
+// owns NC = 1 group of 16 samples; every A operand (one ds_read_b128 = 4
+// k-steps of one output block) feeds 4 x NC MFMAs.  Two waves per SIMD keep
+// the MFMA pipe busy across one wave's barrier waits, ReLU passes and stores
+// (4 waves x 2 groups, 512 registers each: fwd 1,309 -> 1,264 us, bwd 1,263
+// -> 1,198 us at config C's 466 k samples; -DPSVO_DEC256_WAVES=4
+// -DPSVO_DEC256_NC=2 builds that layout for A/B).
 #ifndef PSVO_DEC256_NC
-#define PSVO_DEC256_NC 2
+#define PSVO_DEC256_NC 1
 #endif
-constexpr int kCWaves = 4, kCThreads = 64 * kCWaves, kNC = PSVO_DEC256_NC;
+#ifndef PSVO_DEC256_WAVES
+#define PSVO_DEC256_WAVES 8
+#endif
+constexpr int kCWaves = PSVO_DEC256_WAVES, kCThreads = 64 * kCWaves, kNC = PSVO_DEC256_NC;
 constexpr int kChainTile = kCWaves * kNC * kTileW;  // samples per chain-kernel workgroup iteration
 static_assert(kTileWG % kChainTile == 0, "chain tile");
 
@@ -209,8 +218,9 @@ static_assert(kTileWG % kChainTile == 0, "chain tile");
 // accumulators, so no two consecutive MFMAs share one.
 template <int NOB, int NIN, int IB0, int NIB>
 __device__ __forceinline__ void gemm_chunk(f32x4 (&acc)[kNC][NOB], const f32x4 (&in)[kNC][NIN], const float *buf,
-                                           int lane) {
+                                           int lane, bool on = true) {
     static_assert(IB0 + NIB <= NIN, "chunk input blocks");
+    if (!on) return;  // wave-uniform: a wave without samples in the last round
     constexpr int NG = (NOB + 3) / 4;
     constexpr int NSTEP = NIB * NG;
     f32x4 a[2][4];
@@ -254,30 +264,46 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[kNC][NOB]) {
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob) acc[c][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
-// ReLU in place; mask bit 4 ob + i = (value > 0), one word per sample group
+// ReLU in place; mask bit 4 ob + i = (value > 0), one word per sample group.
+// No compares (mlp.hip's relu): y = max(v, 0) and (−u) & ~u (u = bits of y)
+// has its sign bit set exactly for positive non-zero y — per-element compare
+// results held as SGPR-pair lane masks spilled ~730 SGPRs to VGPR lanes here
+// (v_writelane / v_readlane in the tile loop).
 template <int NOB>
 __device__ __forceinline__ void relu_mask(f32x4 (&acc)[kNC][NOB], uint64_t (&m)[kNC]) {
 #pragma unroll
     for (int c = 0; c < kNC; ++c) {
-        m[c] = 0;
+        uint32_t half[2] = {0u, 0u};
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const bool pos = acc[c][ob][i] > 0.0f;
-                m[c] |= (uint64_t)pos << (4 * ob + i);
-                acc[c][ob][i] = pos ? acc[c][ob][i] : 0.0f;
+                float y = acc[c][ob][i];
+                asm volatile("" : "+v"(y));  // in program order: not all hoisted and kept live at once
+                y = fmaxf(y, 0.0f);
+                acc[c][ob][i] = y;
+                const uint32_t u = __float_as_uint(y);
+                const int bit = 4 * ob + i;
+                half[bit >> 5] |= (((0u - u) & ~u) >> 31) << (bit & 31);
+                asm volatile("" : "+v"(half[bit >> 5]));
             }
+        m[c] = (uint64_t)half[0] | ((uint64_t)half[1] << 32);
     }
 }
 template <int NOB>
 __device__ __forceinline__ void apply_mask(f32x4 (&acc)[kNC][NOB], const uint64_t (&m)[kNC]) {
 #pragma unroll
-    for (int c = 0; c < kNC; ++c)
+    for (int c = 0; c < kNC; ++c) {
+        const uint32_t half[2] = {(uint32_t)m[c], (uint32_t)(m[c] >> 32)};
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[c][ob][i] = ((m[c] >> (4 * ob + i)) & 1) ? acc[c][ob][i] : 0.0f;
+            for (int i = 0; i < 4; ++i) {
+                const int bit = 4 * ob + i;
+                const uint32_t keep = 0u - ((half[bit >> 5] >> (bit & 31)) & 1u);
+                acc[c][ob][i] = __uint_as_float(__float_as_uint(acc[c][ob][i]) & keep);
+            }
+    }
 }
 
 // tile-feature-major store: feature f of sample n at f·16 + swz(f, n) in a
@@ -343,6 +369,28 @@ struct Ring {
     }
 };
 
+// The chain kernels' work plan: rounds over the grid's wave slots, a wave's
+// unit = kNC consecutive 16-sample tiles.  Every round but the last fills all
+// slots (round r, workgroup b, wave w → tiles of 128-sample block r·G + b);
+// the last round's units are spread over the workgroups first (unit
+// w·G + b), so a partial round costs each workgroup one or two busy waves
+// instead of whole tiles on a few workgroups (3,643 blocks on 256 workgroups:
+// 15 → 14.5 tile times at config C).  A wave without a unit (t16 ≥ n16) skips
+// the MFMAs and stores but still streams its share of the weight chunks.
+struct ChainPlan {
+    int64_t n16, full, rounds;
+    __device__ ChainPlan(int64_t m) {
+        n16 = (m + kTileW - 1) / kTileW;
+        const int64_t slots = (int64_t)gridDim.x * kCWaves * kNC;
+        full = n16 / slots;
+        rounds = full + (n16 % slots ? 1 : 0);
+    }
+    __device__ int64_t t16(int64_t r, int wave) const {
+        return r < full ? (((int64_t)r * gridDim.x + blockIdx.x) * kCWaves + wave) * kNC
+                        : full * (int64_t)gridDim.x * kCWaves * kNC + ((int64_t)wave * gridDim.x + blockIdx.x) * kNC;
+    }
+};
+
 // ---- forward ---------------------------------------------------------------
 __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t n_tiles, const float *__restrict__ feat,
                                                              const float *__restrict__ img, float *__restrict__ sdf,
@@ -351,19 +399,21 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
     float *vec = lds;  // kVecN
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int e = threadIdx.x; e < kVecN; e += kCThreads) vec[e] = img[kImgMats + e];
-    int64_t tile = blockIdx.x;
-    if (tile >= n_tiles) return;
+    (void)n_tiles;
+    const ChainPlan P(m);
+    if (P.rounds == 0) return;
     Ring R{lds + ((kVecN + 63) / 64) * 64, img, 0, wave, lane, false};
     stream_chunk<kCWaves>(img + fwd_chunk(0).img_off, R.ring, chunk_floats(fwd_chunk(0)), wave, lane);
     stream_chunk<kCWaves>(img + fwd_chunk(1).img_off, R.ring + kChunkFloats, chunk_floats(fwd_chunk(1)), wave, lane);
     const int n = lane & 15, g = lane >> 4;
     auto plan = [](int c) { return fwd_chunk(c); };
     const bool train = act.h1 != nullptr;  // inference (no act): per-sample outputs only
-    for (; tile < n_tiles; tile += gridDim.x) {
-        R.more = tile + gridDim.x < n_tiles;
+    for (int64_t rd = 0; rd < P.rounds; ++rd) {
+        R.more = rd + 1 < P.rounds;
         R.img = img;
         asm volatile("" : "+s"(R.img));  // chunk addresses are rebuilt per tile, not kept live across it
-        const int64_t t16 = (tile * kCWaves + wave) * kNC;  // this wave's first 16-sample tile
+        const int64_t t16 = P.t16(rd, wave);  // this wave's first 16-sample tile
+        const bool on = t16 < P.n16;          // wave-uniform
         f32x4 x[kNC][1];
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
@@ -374,21 +424,21 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
         // L1, L2
         f32x4 h1[kNC][16], h2[kNC][16];
         init_bias(h1, vec + kVB1, lane);
-        gemm_chunk<16, 1, 0, 1>(h1, x, R.next<kFwdChunks>(0, plan), lane);
+        gemm_chunk<16, 1, 0, 1>(h1, x, R.next<kFwdChunks>(0, plan), lane, on);
         relu_mask(h1, m1);
         init_bias(h2, vec + kVB2, lane);
-#define F2(K) gemm_chunk<16, 16, 2 * (K - 1), 2>(h2, h1, R.next<kFwdChunks>(K, plan), lane);
+#define F2(K) gemm_chunk<16, 16, 2 * (K - 1), 2>(h2, h1, R.next<kFwdChunks>(K, plan), lane, on);
         F2(1) F2(2) F2(3) F2(4) F2(5) F2(6) F2(7) F2(8)
 #undef F2
-        if (train) store_tiles(act.h1, t16, 256, h1, lane);
+        if (train && on) store_tiles(act.h1, t16, 256, h1, lane);
         relu_mask(h2, m2);
         // L3: rows [f (blocks 0..7) | sdf (block 8, row 0)]
         f32x4 o3[kNC][9];
         init_bias(o3, vec + kVB3, lane);
-#define F3(K) gemm_chunk<9, 16, 2 * (K - 9), 2>(o3, h2, R.next<kFwdChunks>(K, plan), lane);
+#define F3(K) gemm_chunk<9, 16, 2 * (K - 9), 2>(o3, h2, R.next<kFwdChunks>(K, plan), lane, on);
         F3(9) F3(10) F3(11) F3(12) F3(13) F3(14) F3(15) F3(16)
 #undef F3
-        if (train) store_tiles(act.h2, t16, 256, h2, lane);
+        if (train && on) store_tiles(act.h2, t16, 256, h2, lane);
         float sdf_v[kNC];
         f32x4 fx[kNC][9];
 #pragma unroll
@@ -401,28 +451,28 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
         // L4
         f32x4 c1[kNC][16];
         init_bias(c1, vec + kVB4, lane);
-        gemm_chunk<16, 9, 0, 2>(c1, fx, R.next<kFwdChunks>(17, plan), lane);
-        gemm_chunk<16, 9, 2, 2>(c1, fx, R.next<kFwdChunks>(18, plan), lane);
-        gemm_chunk<16, 9, 4, 2>(c1, fx, R.next<kFwdChunks>(19, plan), lane);
-        gemm_chunk<16, 9, 6, 2>(c1, fx, R.next<kFwdChunks>(20, plan), lane);
-        gemm_chunk<16, 9, 8, 1>(c1, fx, R.next<kFwdChunks>(21, plan), lane);
-        if (train) store_tiles(act.fx, t16, 144, fx, lane);
+        gemm_chunk<16, 9, 0, 2>(c1, fx, R.next<kFwdChunks>(17, plan), lane, on);
+        gemm_chunk<16, 9, 2, 2>(c1, fx, R.next<kFwdChunks>(18, plan), lane, on);
+        gemm_chunk<16, 9, 4, 2>(c1, fx, R.next<kFwdChunks>(19, plan), lane, on);
+        gemm_chunk<16, 9, 6, 2>(c1, fx, R.next<kFwdChunks>(20, plan), lane, on);
+        gemm_chunk<16, 9, 8, 1>(c1, fx, R.next<kFwdChunks>(21, plan), lane, on);
+        if (train && on) store_tiles(act.fx, t16, 144, fx, lane);
         relu_mask(c1, m4);
         // L5
         f32x4 o5[kNC][1];
         init_bias(o5, vec + kVB5, lane);
-        gemm_chunk<1, 16, 0, 16>(o5, c1, R.next<kFwdChunks>(22, plan), lane);
-        if (train) store_tiles(act.c1, t16, 256, c1, lane);
+        gemm_chunk<1, 16, 0, 16>(o5, c1, R.next<kFwdChunks>(22, plan), lane, on);
+        if (train && on) store_tiles(act.c1, t16, 256, c1, lane);
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
-            if (act.masks) {
+            if (act.masks && on) {
                 uint64_t *mk = act.masks + (t16 + c) * 3 * 64;
                 mk[lane] = m1[c];
                 mk[64 + lane] = m2[c];
                 mk[128 + lane] = m4[c];
             }
             const int64_t s = (t16 + c) * kTileW + n;
-            if (s < m && g == 0) {
+            if (on && s < m && g == 0) {
                 sdf[s] = sdf_v[c];
                 if (rgb) {
                     rgb[s * 3 + 0] = sigmoidf(o5[c][0][0]);
@@ -442,29 +492,31 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
                                                              float *__restrict__ dfeat) {
     extern __shared__ __align__(16) float lds[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int64_t tile = blockIdx.x;
-    if (tile >= n_tiles) return;
+    (void)n_tiles;
+    const ChainPlan P(m);
+    if (P.rounds == 0) return;
     Ring R{lds, img, 0, wave, lane, false};
     stream_chunk<kCWaves>(img + bwd_chunk(0).img_off, R.ring, chunk_floats(bwd_chunk(0)), wave, lane);
     stream_chunk<kCWaves>(img + bwd_chunk(1).img_off, R.ring + kChunkFloats, chunk_floats(bwd_chunk(1)), wave, lane);
     const int n = lane & 15, g = lane >> 4;
     const bool want_w = dl.d1 != nullptr;
     auto plan = [](int c) { return bwd_chunk(c); };
-    for (; tile < n_tiles; tile += gridDim.x) {
-        R.more = tile + gridDim.x < n_tiles;
+    for (int64_t rd = 0; rd < P.rounds; ++rd) {
+        R.more = rd + 1 < P.rounds;
         R.img = img;
         asm volatile("" : "+s"(R.img));
-        const int64_t t16 = (tile * kCWaves + wave) * kNC;
+        const int64_t t16 = P.t16(rd, wave);
+        const bool on = t16 < P.n16;  // wave-uniform
         uint64_t m1[kNC], m2[kNC], m4[kNC];
         // δ of the rgb logits: g_rgb · σ' (rows 0..2 of a 16-row block, lanes g == 0)
         f32x4 d5[kNC][1];
         float gs[kNC];
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
-            const uint64_t *mk = act.masks + (t16 + c) * 3 * 64;
-            m1[c] = mk[lane];
-            m2[c] = mk[64 + lane];
-            m4[c] = mk[128 + lane];
+            const uint64_t *mk = act.masks + (on ? t16 + c : 0) * 3 * 64;
+            m1[c] = on ? mk[lane] : 0;
+            m2[c] = on ? mk[64 + lane] : 0;
+            m4[c] = on ? mk[128 + lane] : 0;
             const int64_t s = (t16 + c) * kTileW + n;
             d5[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
             gs[c] = 0.0f;
@@ -482,15 +534,15 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         // δc1 = (W5ᵀ δ5) ⊙ m_c1
         f32x4 dc1[kNC][16];
         zero(dc1);
-        gemm_chunk<16, 1, 0, 1>(dc1, d5, R.next<kBwdChunks>(0, plan), lane);
+        gemm_chunk<16, 1, 0, 1>(dc1, d5, R.next<kBwdChunks>(0, plan), lane, on);
         apply_mask(dc1, m4);
         // δ[f; x] = W4ᵀ δc1
         f32x4 dfx[kNC][9];
         zero(dfx);
-#define B4(K) gemm_chunk<9, 16, 2 * (K - 1), 2>(dfx, dc1, R.next<kBwdChunks>(K, plan), lane);
+#define B4(K) gemm_chunk<9, 16, 2 * (K - 1), 2>(dfx, dc1, R.next<kBwdChunks>(K, plan), lane, on);
         B4(1) B4(2) B4(3) B4(4) B4(5) B4(6) B4(7) B4(8)
 #undef B4
-        if (want_w) {
+        if (want_w && on) {
             store_tiles(dl.d4, t16, 256, dc1, lane);
             store_tiles(dl.d5, t16, 16, d5, lane);
         }
@@ -503,28 +555,28 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         }
         f32x4 dh2[kNC][16];
         zero(dh2);
-        gemm_chunk<16, 9, 0, 2>(dh2, dfx, R.next<kBwdChunks>(9, plan), lane);
-        gemm_chunk<16, 9, 2, 2>(dh2, dfx, R.next<kBwdChunks>(10, plan), lane);
-        gemm_chunk<16, 9, 4, 2>(dh2, dfx, R.next<kBwdChunks>(11, plan), lane);
-        gemm_chunk<16, 9, 6, 2>(dh2, dfx, R.next<kBwdChunks>(12, plan), lane);
-        gemm_chunk<16, 9, 8, 1>(dh2, dfx, R.next<kBwdChunks>(13, plan), lane);
-        if (want_w) store_tiles(dl.d3, t16, 144, dfx, lane);
+        gemm_chunk<16, 9, 0, 2>(dh2, dfx, R.next<kBwdChunks>(9, plan), lane, on);
+        gemm_chunk<16, 9, 2, 2>(dh2, dfx, R.next<kBwdChunks>(10, plan), lane, on);
+        gemm_chunk<16, 9, 4, 2>(dh2, dfx, R.next<kBwdChunks>(11, plan), lane, on);
+        gemm_chunk<16, 9, 6, 2>(dh2, dfx, R.next<kBwdChunks>(12, plan), lane, on);
+        gemm_chunk<16, 9, 8, 1>(dh2, dfx, R.next<kBwdChunks>(13, plan), lane, on);
+        if (want_w && on) store_tiles(dl.d3, t16, 144, dfx, lane);
         apply_mask(dh2, m2);
         // δh1 = (W2ᵀ δh2) ⊙ m_h1
         f32x4 dh1[kNC][16];
         zero(dh1);
-#define B2(K) gemm_chunk<16, 16, 2 * (K - 14), 2>(dh1, dh2, R.next<kBwdChunks>(K, plan), lane);
+#define B2(K) gemm_chunk<16, 16, 2 * (K - 14), 2>(dh1, dh2, R.next<kBwdChunks>(K, plan), lane, on);
         B2(14) B2(15) B2(16) B2(17) B2(18) B2(19) B2(20) B2(21)
 #undef B2
-        if (want_w) store_tiles(dl.d2, t16, 256, dh2, lane);
+        if (want_w && on) store_tiles(dl.d2, t16, 256, dh2, lane);
         apply_mask(dh1, m1);
         // δx = W1ᵀ δh1 + the x rows of δ[f; x]
-        gemm_chunk<1, 16, 0, 16>(dx, dh1, R.next<kBwdChunks>(22, plan), lane);
-        if (want_w) store_tiles(dl.d1, t16, 256, dh1, lane);
+        gemm_chunk<1, 16, 0, 16>(dx, dh1, R.next<kBwdChunks>(22, plan), lane, on);
+        if (want_w && on) store_tiles(dl.d1, t16, 256, dh1, lane);
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
             const int64_t s = (t16 + c) * kTileW + n;
-            if (s < m) *reinterpret_cast<f32x4 *>(dfeat + s * 16 + 4 * g) = dx[c][0];
+            if (on && s < m) *reinterpret_cast<f32x4 *>(dfeat + s * 16 + 4 * g) = dx[c][0];
         }
     }
 }
@@ -793,10 +845,17 @@ static void dw_plan(int64_t m, DwPlan *pl, int64_t *slab_floats) {
     // 1,600 B, L1 + L5: 16.4 kFLOP | 2,112 B (memory-bound: by FLOPs alone it
     // got 14 workgroups and set the kernel's time)
     const int cus = device_cus256();
-    const int w[4] = {213, 120, 120, 107};
+    int w[4] = {213, 120, 120, 107};
+    static const char *wenv = getenv("PSVO_DW256_W");  // A/B: "w0,w1,w2,w3"
+    if (wenv) {
+        int v[4];
+        if (sscanf(wenv, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0)
+            for (int t = 0; t < 4; ++t) w[t] = v[t];
+    }
+    const double wsum = (double)(w[0] + w[1] + w[2] + w[3]);
     int n[4], tot = 0;
     for (int t = 0; t < 4; ++t) {
-        n[t] = (int)((double)cus * w[t] / 560.0 + 0.5);
+        n[t] = (int)((double)cus * w[t] / wsum + 0.5);
         if (n[t] < 1) n[t] = 1;
         if (n[t] > n16) n[t] = (int)(n16 > 0 ? n16 : 1);
         tot += n[t];
@@ -825,7 +884,7 @@ int64_t dec256_workspace_floats(int64_t m) {
 int dec256_images(hipStream_t st, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
                   const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images) {
     Params p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    hipLaunchKernelGGL(k_dec256_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
+    psvo::launch(k_dec256_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
     return check_launch("dec256_images");
 }
 
@@ -854,7 +913,7 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_dec256_fwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, feat, images, sdf,
+    psvo::launch(k_dec256_fwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, feat, images, sdf,
                        rgb, a);
     return check_launch("dec256_fwd");
 }
@@ -892,7 +951,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             attr = true;
         }
-        hipLaunchKernelGGL(k_dec256_bwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, images, rgb,
+        psvo::launch(k_dec256_bwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, images, rgb,
                            g_sdf, g_rgb, a, d, dfeat);
         const int rc = check_launch("dec256_bwd");
         if (rc) return rc;
@@ -922,7 +981,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
         dattr = true;
     }
     if (m > 0) {
-        hipLaunchKernelGGL(k_dec256_dw, dim3(pl.wg_begin[4]), dim3(kThreads), kDwLds, st, op, pl, slabs);
+        psvo::launch(k_dec256_dw, dim3(pl.wg_begin[4]), dim3(kThreads), kDwLds, st, op, pl, slabs);
         const int rc = check_launch("dec256_dw");
         if (rc) return rc;
     } else if (hipMemsetAsync(slabs, 0, slab_floats * sizeof(float), st) != hipSuccess) {
@@ -934,7 +993,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
         o.gb[l] = gb[l];
     }
     const int total = (256 * 256 + 256) + (129 * 256 + 129) + (256 * 144 + 256) + (256 * 16 + 256) + (3 * 256 + 3);
-    hipLaunchKernelGGL(k_dec256_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, st, pl, slabs, o, accumulate);
+    psvo::launch(k_dec256_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, st, pl, slabs, o, accumulate);
     return check_launch("dec256_dw_reduce");
 }
 

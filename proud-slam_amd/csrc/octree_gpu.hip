@@ -382,7 +382,7 @@ int dt_alloc_nodes(psvo_dtree *tr, int64_t cap, hipStream_t st) {
         (void)hipMemcpyAsync(n.type, tr->nd.type, tr->count * sizeof(int8_t), hipMemcpyDeviceToDevice, st);
         (void)hipMemcpyAsync(n.child, tr->nd.child, tr->count * 8 * sizeof(int), hipMemcpyDeviceToDevice, st);
     }
-    hipLaunchKernelGGL(k_dt_fill_child, dim3(div_up((cap - tr->count) * 8, 256)), dim3(256), 0, st, n.child,
+    psvo::launch(k_dt_fill_child, dim3(div_up((cap - tr->count) * 8, 256)), dim3(256), 0, st, n.child,
                        tr->count * 8, cap * 8);
     if (tr->cap > 0) {
         (void)hipStreamSynchronize(st);
@@ -405,9 +405,9 @@ int dt_alloc_table(psvo_dtree *tr, hipStream_t st, uint64_t min_slots) {
         hipMalloc(&t.flags, slots * sizeof(unsigned)) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "dtree: out of device memory (hash table)");
     t.mask = slots - 1;
-    hipLaunchKernelGGL(k_dt_fill, dim3(div_up((int64_t)slots, 256)), dim3(256), 0, st, t, slots);
+    psvo::launch(k_dt_fill, dim3(div_up((int64_t)slots, 256)), dim3(256), 0, st, t, slots);
     if (tr->count > 0)
-        hipLaunchKernelGGL(k_dt_rehash, dim3(div_up(tr->count, 256)), dim3(256), 0, st, t, tr->nd, tr->count, tr->D);
+        psvo::launch(k_dt_rehash, dim3(div_up(tr->count, 256)), dim3(256), 0, st, t, tr->nd, tr->count, tr->D);
     if (tr->t.key) {
         (void)hipStreamSynchronize(st);
         (void)hipFree(tr->t.key);
@@ -446,7 +446,7 @@ extern "C" void *psvo_dtree_new(void *stream, int grid_dim, int64_t capacity) {
     (void)hipMemcpyAsync(tr->nd.side, &side, sizeof(side), hipMemcpyHostToDevice, st);
     (void)hipMemcpyAsync(tr->nd.type, &nl, sizeof(nl), hipMemcpyHostToDevice, st);
     tr->count = 1;
-    hipLaunchKernelGGL(k_dt_rehash, dim3(1), dim3(64), 0, st, tr->t, tr->nd, (int64_t)1, tr->D);
+    psvo::launch(k_dt_rehash, dim3(1), dim3(64), 0, st, tr->t, tr->nd, (int64_t)1, tr->D);
     if (hipStreamSynchronize(st) != hipSuccess) {
         set_error(PSVO_E_LAUNCH, "dtree_new: device init failed");
         delete tr;
@@ -501,7 +501,7 @@ extern "C" int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64
         }
         int ov = 0;
         (void)hipMemsetAsync(overflow, 0, sizeof(int), st);
-        hipLaunchKernelGGL(k_dt_walk, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, overflow);
+        psvo::launch(k_dt_walk, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, overflow);
         if (hipMemcpyAsync(&ov, overflow, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "dtree_insert: walk failed (%s)", hipGetErrorString(hipGetLastError()));
@@ -511,10 +511,10 @@ extern "C" int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64
         int rc = dt_alloc_table(tr, st, want);
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_dt_flag, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, flag);
-    hipLaunchKernelGGL(k_dt_scan_local, dim3(nb), dim3(1024), 0, st, flag, ne, rank, totals);
-    hipLaunchKernelGGL(k_dt_scan_totals, dim3(1), dim3(1024), 0, st, totals, nb, sum);
-    hipLaunchKernelGGL(k_dt_scan_add, dim3(nb), dim3(1024), 0, st, rank, ne, totals);
+    psvo::launch(k_dt_flag, g, b, 0, st, tr->t, vox, n_walks, tr->D, tr->w_next, flag);
+    psvo::launch(k_dt_scan_local, dim3(nb), dim3(1024), 0, st, flag, ne, rank, totals);
+    psvo::launch(k_dt_scan_totals, dim3(1), dim3(1024), 0, st, totals, nb, sum);
+    psvo::launch(k_dt_scan_add, dim3(nb), dim3(1024), 0, st, rank, ne, totals);
     int created = 0;
     if (hipMemcpyAsync(&created, sum, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -525,9 +525,9 @@ extern "C" int psvo_dtree_insert(void *tree, void *stream, const int *vox, int64
         int rc = dt_alloc_nodes(tr, cap, st);
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_dt_create, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->shift, tr->size, flag, rank,
+    psvo::launch(k_dt_create, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->shift, tr->size, flag, rank,
                        tr->count);
-    hipLaunchKernelGGL(k_dt_link, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->size, flag);
+    psvo::launch(k_dt_link, g, b, 0, st, tr->t, tr->nd, vox, n_walks, tr->D, tr->size, flag);
     tr->count += created;
     tr->w_next += (unsigned)n_walks;
     return check_launch("dtree_insert");
@@ -549,7 +549,7 @@ extern "C" int64_t psvo_dtree_count_leaves(void *tree, void *stream) {
         out = tr->scratch;
     }
     (void)hipMemsetAsync(out, 0, sizeof(int), st);
-    hipLaunchKernelGGL(k_dt_count_type, dim3(div_up(tr->count, 256)), dim3(256), 0, st, tr->nd.type, tr->count,
+    psvo::launch(k_dt_count_type, dim3(div_up(tr->count, 256)), dim3(256), 0, st, tr->nd.type, tr->count,
                        kDtSurface, out);
     int v = 0;
     (void)hipMemcpyAsync(&v, out, sizeof(int), hipMemcpyDeviceToHost, st);
@@ -561,7 +561,7 @@ extern "C" int psvo_dtree_export(void *tree, void *stream, float voxel_size, flo
                                  int *features, float *centres, int *structure) {
     psvo_dtree *tr = static_cast<psvo_dtree *>(tree);
     PSVO_REQUIRE(tr != nullptr, "dtree_export: null tree");
-    hipLaunchKernelGGL(k_dt_export, dim3(div_up(tr->count, 256)), dim3(256), 0, as_stream(stream), tr->t, tr->nd,
+    psvo::launch(k_dt_export, dim3(div_up(tr->count, 256)), dim3(256), 0, as_stream(stream), tr->t, tr->nd,
                        tr->count, tr->D, voxel_size, voxels, children, features, centres, structure);
     return check_launch("dtree_export");
 }
@@ -570,7 +570,7 @@ extern "C" int psvo_dtree_probe(void *tree, void *stream, const int *vox, int64_
     psvo_dtree *tr = static_cast<psvo_dtree *>(tree);
     PSVO_REQUIRE(tr != nullptr && n >= 0 && (corners == 1 || corners == 8), "dtree_probe: bad arguments");
     if (n == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_dt_probe, dim3(div_up(n * corners, 256)), dim3(256), 0, as_stream(stream), tr->t, vox, n,
+    psvo::launch(k_dt_probe, dim3(div_up(n * corners, 256)), dim3(256), 0, as_stream(stream), tr->t, vox, n,
                        tr->D, corners, hit);
     return check_launch("dtree_probe");
 }

@@ -105,7 +105,7 @@ extern "C" int psvo_adam_mark_rows(void *stream, int64_t m, const int *leaf, con
     PSVO_REQUIRE(m >= 0, "adam_mark_rows: bad size");
     if (m == 0) return PSVO_OK;
     PSVO_REQUIRE(leaf && vertex_idx && flags, "adam_mark_rows: null pointer");
-    hipLaunchKernelGGL(psvo::k_adam_mark_rows, dim3(psvo::div_up(m * 8, 256)), dim3(256), 0, psvo::as_stream(stream),
+    psvo::launch(psvo::k_adam_mark_rows, dim3(psvo::div_up(m * 8, 256)), dim3(256), 0, psvo::as_stream(stream),
                        m, leaf, vertex_idx, flags);
     return psvo::check_launch("adam_mark_rows");
 }
@@ -117,7 +117,7 @@ extern "C" int psvo_adam_flags_from_state(void *stream, int64_t n_rows, const fl
     PSVO_REQUIRE(exp_avg && exp_avg_sq && flags, "adam_flags_from_state: null pointer");
     PSVO_REQUIRE(((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
                  "adam_flags_from_state: moments must be 16-B aligned");
-    hipLaunchKernelGGL(psvo::k_adam_flags_from_state, dim3(psvo::div_up(n_rows, 256)), dim3(256), 0,
+    psvo::launch(psvo::k_adam_flags_from_state, dim3(psvo::div_up(n_rows, 256)), dim3(256), 0,
                        psvo::as_stream(stream), n_rows, exp_avg, exp_avg_sq, flags);
     return psvo::check_launch("adam_flags_from_state");
 }
@@ -161,7 +161,7 @@ int psvo::adam_launch(hipStream_t st, int n_tensors, float *const *params, const
         }
         tab.block_begin[tab.count] = blocks;
         if (blocks == 0) continue;
-        hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, st, tab, (float)beta1, (float)beta2,
+        psvo::launch(k_adam, dim3(blocks), dim3(256), 0, st, tab, (float)beta1, (float)beta2,
                            (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
         const int rc = check_launch("adam_step");
         if (rc) return rc;

@@ -422,19 +422,19 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     if (hipMemsetAsync(a.hist, 0, sizeof(int) * 3 * n_frames * kPxBins, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
     const dim3 grid(a.nb, n_frames);
-    if (weights) hipLaunchKernelGGL(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
+    if (weights) psvo::launch(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
     if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
-        hipLaunchKernelGGL((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
+        psvo::launch((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
     } else {
-        hipLaunchKernelGGL((k_px_hist<false, 0>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL((k_px_hist<false, 1>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL((k_px_hist<false, 2>), grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_px_count<false>, grid, dim3(kPxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_px_write<false>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb,
+        psvo::launch((k_px_hist<false, 0>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<false, 1>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<false, 2>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_count<false>, grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_write<false>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb,
                            out_depth);
     }
     return check_launch("sample_pixels");

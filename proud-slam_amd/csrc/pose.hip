@@ -279,7 +279,7 @@ extern "C" int psvo_pose_rays(void *stream, int64_t n, const float *pose, const 
                               float *rays_d) {
     PSVO_REQUIRE(n > 0, "pose_rays: bad size");
     PSVO_REQUIRE(pose && dirs && rays_o && rays_d, "pose_rays: null pointer");
-    hipLaunchKernelGGL(k_pose_rays, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, pose, dirs, rays_o,
+    psvo::launch(k_pose_rays, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, pose, dirs, rays_o,
                        rays_d);
     return check_launch("pose_rays");
 }
@@ -288,7 +288,7 @@ extern "C" int psvo_pose_rays_frames(void *stream, int64_t n, int64_t rays_per_f
                                      const float *dirs, float *rays_o, float *rays_d) {
     PSVO_REQUIRE(n > 0 && rays_per_frame > 0 && n % rays_per_frame == 0, "pose_rays_frames: bad sizes");
     PSVO_REQUIRE(poses && dirs && rays_o && rays_d, "pose_rays_frames: null pointer");
-    hipLaunchKernelGGL(k_pose_rays_frames, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, rays_per_frame,
+    psvo::launch(k_pose_rays_frames, dim3(div_up(n, 256)), dim3(256), 0, as_stream(stream), n, rays_per_frame,
                        poses, dirs, rays_o, rays_d);
     return check_launch("pose_rays_frames");
 }
@@ -298,7 +298,7 @@ extern "C" int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_pe
                                      const float *poses, float *grads) {
     PSVO_REQUIRE(n_frames > 0 && rays_per_frame > 0 && r_hit >= 0, "pose_grad_frames: bad sizes");
     PSVO_REQUIRE(rank_ray && dirs && g_o && g_d && poses && grads, "pose_grad_frames: null pointer");
-    hipLaunchKernelGGL(k_pose_grad_frames, dim3(n_frames), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray,
+    psvo::launch(k_pose_grad_frames, dim3(n_frames), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray,
                        rays_per_frame, dirs, g_o, g_d, poses, grads);
     return check_launch("pose_grad_frames");
 }
@@ -322,7 +322,7 @@ int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64
         a.lr_bc1[f] = (float)(lr / bc1);
         a.bc2_sqrt[f] = (float)std::sqrt(bc2);
     }
-    hipLaunchKernelGGL(k_pose_step_frames, dim3(n_frames), dim3(kGradThreads), 0, st, r_hit, rank_ray, rays_per_frame,
+    psvo::launch(k_pose_step_frames, dim3(n_frames), dim3(kGradThreads), 0, st, r_hit, rank_ray, rays_per_frame,
                        dirs, g_o, g_d, poses, pose_m, pose_v, a, (float)beta1, (float)beta2, (float)(1.0 - beta1),
                        (float)(1.0 - beta2), (float)eps, grads, next_dirs, rays_o, rays_d);
     return check_launch("pose_step_frames");
@@ -333,7 +333,7 @@ extern "C" int psvo_pose_grad(void *stream, int64_t r_hit, const int *rank_ray, 
                               const float *g_d, const float *pose, float *grad) {
     PSVO_REQUIRE(r_hit >= 0, "pose_grad: bad size");
     PSVO_REQUIRE(dirs && g_o && g_d && pose && grad, "pose_grad: null pointer");
-    hipLaunchKernelGGL(k_pose_grad, dim3(1), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray, dirs, g_o,
+    psvo::launch(k_pose_grad, dim3(1), dim3(kGradThreads), 0, as_stream(stream), r_hit, rank_ray, dirs, g_o,
                        g_d, pose, grad);
     return check_launch("pose_grad");
 }

@@ -1,12 +1,49 @@
 // Internal helpers shared by the psvo HIP translation units (gfx950 only).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/psvo.h"
 
 namespace psvo {
+
+// Kernel-bound timing (the engine's timed regions, psvo_engine_set_timing):
+// while a region is armed every kernel launched through psvo::launch takes a
+// (start, stop) event pair bound to its own dispatch (hipExtLaunchKernel), so
+// a region's time is the sum of its kernels' execution spans — what a
+// rocprofv3 kernel trace reports — with no marker packets between the
+// kernels.  One host thread queues a timed step; regions may nest (the
+// innermost armed region owns a launch).
+struct KernelClock {
+    static constexpr int kMax = 192;
+    hipEvent_t ev[kMax][2] = {};
+    int region[kMax] = {};
+    int n = 0;                   // pairs taken since the last collection
+    int stack[8] = {};           // armed regions, innermost last
+    int depth = 0;
+    bool overflow = false;       // more launches than pairs: the surplus ran untimed
+};
+extern KernelClock *g_kclock;  // engine.cpp: set while an engine with timing on queues a step
+
+template <typename... KArgs, typename... A>
+inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A &&...a) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    KernelClock *c = g_kclock;
+    if (c && c->depth > 0) {
+        if (c->n < KernelClock::kMax) {
+            const int i = c->n++;
+            c->region[i] = c->stack[c->depth - 1];
+            e0 = c->ev[i][0];
+            e1 = c->ev[i][1];
+        } else {
+            c->overflow = true;
+        }
+    }
+    hipExtLaunchKernelGGL(k, grid, block, lds, st, e0, e1, 0u, static_cast<KArgs>(a)...);
+}
+
 
 // Set the thread-local error message; returns `code` for tail calls.
 int set_error(int code, const char *fmt, ...);

@@ -165,9 +165,9 @@ static int rows_compact(void *stream, int64_t n_rows, int width, const float *gr
             return set_error(PSVO_E_LAUNCH, "rows_compact: memset failed");
         return PSVO_OK;
     }
-    hipLaunchKernelGGL(k_rows_count, dim3(n_blocks), dim3(256), 0, st, n_rows, width, grad, flags, workspace);
-    hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(1024), 0, st, n_blocks, workspace, count);
-    hipLaunchKernelGGL(k_rows_write, dim3(n_blocks), dim3(256), 0, st, n_rows, width, grad, flags, workspace, ids,
+    psvo::launch(k_rows_count, dim3(n_blocks), dim3(256), 0, st, n_rows, width, grad, flags, workspace);
+    psvo::launch(k_rows_scan, dim3(1), dim3(1024), 0, st, n_blocks, workspace, count);
+    psvo::launch(k_rows_write, dim3(n_blocks), dim3(256), 0, st, n_rows, width, grad, flags, workspace, ids,
                        rows);
     return check_launch("rows_compact");
 }
@@ -187,7 +187,7 @@ extern "C" int psvo_rows_clear(void *stream, int64_t n_list, int width, const in
     PSVO_REQUIRE(n_list >= 0 && width > 0, "rows_clear: bad sizes");
     PSVO_REQUIRE(n_list == 0 || (ids && grad), "rows_clear: null pointer");
     if (n_list == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_rows_clear, dim3(div_up(n_list * width, 256)), dim3(256), 0, as_stream(stream), n_list,
+    psvo::launch(k_rows_clear, dim3(div_up(n_list * width, 256)), dim3(256), 0, as_stream(stream), n_list,
                        width, ids, grad, flags);
     return check_launch("rows_clear");
 }
@@ -196,7 +196,7 @@ extern "C" int psvo_rows_mark(void *stream, int64_t n_list, const int *ids, uint
     PSVO_REQUIRE(n_list >= 0, "rows_mark: bad size");
     PSVO_REQUIRE(n_list == 0 || (ids && flags), "rows_mark: null pointer");
     if (n_list == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_rows_mark, dim3(div_up(n_list, 256)), dim3(256), 0, as_stream(stream), n_list, ids, flags);
+    psvo::launch(k_rows_mark, dim3(div_up(n_list, 256)), dim3(256), 0, as_stream(stream), n_list, ids, flags);
     return check_launch("rows_mark");
 }
 
@@ -204,7 +204,7 @@ extern "C" int psvo_rows_flags_from_grad(void *stream, int64_t n_rows, int width
     PSVO_REQUIRE(n_rows >= 0 && width > 0, "rows_flags_from_grad: bad sizes");
     PSVO_REQUIRE(n_rows == 0 || (grad && flags), "rows_flags_from_grad: null pointer");
     if (n_rows == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_rows_flags_from_grad, dim3(div_up(n_rows, 256)), dim3(256), 0, as_stream(stream), n_rows,
+    psvo::launch(k_rows_flags_from_grad, dim3(div_up(n_rows, 256)), dim3(256), 0, as_stream(stream), n_rows,
                        width, grad, flags);
     return check_launch("rows_flags_from_grad");
 }
@@ -214,7 +214,7 @@ extern "C" int psvo_rows_scatter_add(void *stream, int64_t n_list, int width, co
     PSVO_REQUIRE(n_list >= 0 && width > 0, "rows_scatter_add: bad sizes");
     PSVO_REQUIRE(n_list == 0 || (ids && rows && grad), "rows_scatter_add: null pointer");
     if (n_list == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_rows_scatter_add, dim3(div_up(n_list * width, 256)), dim3(256), 0, as_stream(stream),
+    psvo::launch(k_rows_scatter_add, dim3(div_up(n_list * width, 256)), dim3(256), 0, as_stream(stream),
                        n_list, width, ids, rows, grad);
     return check_launch("rows_scatter_add");
 }

@@ -1621,13 +1621,112 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
     const int64_t n_own = dist ? (int64_t)stats[PSVO_STAT_R_HIT_LOCAL]
                                : n_rows < 0 ? (int64_t)stats[PSVO_STAT_R_HIT] - row_begin : n_rows;
     const int64_t n = max((int64_t)0, min(n_own, r_hit_cap));
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave, nw = blockDim.x / kWave;
+    if ((n + blockDim.x - 1) / blockDim.x <= kRegRun) {
+        // ≤ 8 rays per thread (R_hit ≤ 8,192): one round of independent loads —
+        // the ray's sample count and its normaliser count word side by side —,
+        // run sums / maxima / count sums in registers (32-bit: ≤ 8,192 rays of
+        // ≤ 4,095 counts), one barrier, then the wave totals combined in
+        // registers (every thread reads the ≤ 16 wave words it needs)
+        __shared__ int s_wave[16], s_red[8][16];
+        const int per = (int)((n + blockDim.x - 1) / blockDim.x);
+        const int64_t beg = (int64_t)tid * per;
+        int vals[kRegRun], cw[kRegRun];
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k) {
+            const bool in = k < per && beg + k < n;
+            vals[k] = in ? ray_ns[beg + k] : 0;
+            cw[k] = in && cnt.gt_depth ? cnt.ray_cnt[beg + k] : 0;
+        }
+        int local = 0, mx = 0, c[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k) {
+            local += vals[k];
+            mx = max(mx, vals[k]);
+            const int pf = (cw[k] >> 24) & 1, psm = (cw[k] >> 25) & 1;
+            c[0] += cw[k] & 0xFFF;
+            c[1] += (cw[k] >> 12) & 0xFFF;
+            c[2] += pf;
+            c[3] += psm;
+            c[4] += (cw[k] >> 26) & 1;
+            c[5] += pf ? vals[k] : 0;
+            c[6] += psm ? vals[k] : 0;
+        }
+        int incl = local;
+#pragma unroll
+        for (int sh = 1; sh < kWave; sh <<= 1) {
+            const int t = __shfl_up(incl, sh, kWave);
+            if (lane >= sh) incl += t;
+        }
+        mx = wave_max(mx);
+        if (cnt.gt_depth) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) c[k] = wave_sum(c[k]);
+        }
+        if (lane == kWave - 1) s_wave[w] = incl;
+        if (lane == 0) {
+            s_red[7][w] = mx;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) s_red[k][w] = c[k];
+        }
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int k = 0; k < nw; ++k) {
+            const int v = s_wave[k];
+            before += k < w ? v : 0;
+            tot += v;
+        }
+        int run = before + incl - local;
+#pragma unroll
+        for (int k = 0; k < kRegRun; ++k)
+            if (k < per && beg + k < n) {
+                offsets[beg + k] = run;
+                run += vals[k];
+            }
+        if (w != 0) return;
+        // wave 0: the block's maximum and count sums over the ≤ 16 wave words
+        const bool wl = lane < nw;
+        int bm = wl ? s_red[7][lane] : 0;
+#pragma unroll
+        for (int sh = 8; sh > 0; sh >>= 1) bm = max(bm, __shfl_xor(bm, sh, kWave));
+        bm = __shfl(bm, 0, kWave);
+        if (lane == 0) offsets[n] = tot;
+        if (cnt.gt_depth) {
+            int t[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                int v = wl ? s_red[k][lane] : 0;
+#pragma unroll
+                for (int sh = 8; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, kWave);
+                t[k] = v;
+            }
+            if (lane == 0) {  // the count sums over the padded [R_hit, S_max] layout → coefficients
+                const long long n_f = (long long)t[0] + (long long)bm * t[2] - t[5];
+                const long long n_s = (long long)t[1] + (long long)bm * t[3] - t[6];
+                crit_coef_from_counts((double)t[4], (double)n_f, (double)n_s, (double)n, (double)bm, cnt.w_rgb,
+                                      cnt.w_depth, cnt.w_fs, cnt.w_sdf, cnt.tr, cnt.crit_flags, cnt.coef);
+            }
+        }
+        if (host) {  // the engine's read-back (every reader of stats is past the barrier)
+            if (lane < PSVO_STAT_WORDS) {
+                const int v = lane == PSVO_STAT_S_MAX ? bm : lane == PSVO_STAT_M ? tot : stats[lane];
+                if (keep) keep[lane] = v;  // the device-sized forward's copy (DevBatch)
+                stats[lane] = 0;
+                stat_to_host(host, lane, v, seq);
+            }
+        } else if (lane == 0) {
+            stats[PSVO_STAT_S_MAX] = bm;
+            stats[PSVO_STAT_M] = tot;
+        }
+        return;
+    }
     int mx = 0;
     block_scan_runs(n, [&](int64_t i) { return ray_ns[i]; }, offsets, &total, &mx);
     mx = wave_max(mx);
-    if ((threadIdx.x & (kWave - 1)) == 0) smax[threadIdx.x / kWave] = mx;
+    if (lane == 0) smax[w] = mx;
     if (cnt.gt_depth) {  // the loss normalisers' per-ray counts (k_sample_fused), exact integer sums
         long long c[7] = {};
-        for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)blockDim.x * 8) {
+        for (int64_t i0 = tid; i0 < n; i0 += (int64_t)blockDim.x * 8) {
             int cw[8], ns[8];  // one round of independent loads, then the sums
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -1651,20 +1750,19 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         for (int k = 0; k < 7; ++k) {
 #pragma unroll
             for (int sh = 32; sh > 0; sh >>= 1) c[k] += __shfl_xor(c[k], sh, kWave);
-            if ((threadIdx.x & (kWave - 1)) == 0) s_c[k][threadIdx.x / kWave] = c[k];
+            if (lane == 0) s_c[k][w] = c[k];
         }
     }
     __syncthreads();
-    if (threadIdx.x < kWave) {  // wave 0; with `host` one statistics word per lane (no serial copy loop)
-        const int lane = threadIdx.x;
-        for (int k = 1; k < (int)(blockDim.x / kWave); ++k) mx = max(mx, smax[k]);
+    if (tid < kWave) {  // wave 0; with `host` one statistics word per lane (no serial copy loop)
+        for (int k = 1; k < nw; ++k) mx = max(mx, smax[k]);
         const int tot = total;
         if (lane == 0) offsets[n] = tot;
         if (cnt.gt_depth && lane == 0) {  // the count sums over the padded [R_hit, S_max] layout → coefficients
             long long t[7];
             for (int k = 0; k < 7; ++k) {
                 t[k] = 0;
-                for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t[k] += s_c[k][w];
+                for (int q = 0; q < nw; ++q) t[k] += s_c[k][q];
             }
             const long long n_f = t[0] + (long long)mx * t[2] - t[5];
             const long long n_s = t[1] + (long long)mx * t[3] - t[6];
@@ -1834,7 +1932,7 @@ extern "C" int psvo_svo_intersect(void *stream, int b, int n, int m, float voxel
     PSVO_REQUIRE(n_max <= kMaxHits, "svo_intersect: n_max=%d exceeds %d", n_max, kMaxHits);
     const int64_t total = (int64_t)b * m;
     if (total == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_svo_intersect_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, n, m,
+    psvo::launch(k_svo_intersect_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, n, m,
                        voxelsize, n_max, ray_start, ray_dir, points, children, idx, min_depth, max_depth);
     return check_launch("svo_intersect");
 }
@@ -1849,7 +1947,7 @@ extern "C" int psvo_inverse_cdf_sampling(void *stream, int b, int num_rays, int 
                  max_steps);
     const int64_t total = (int64_t)b * num_rays;
     if (total == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_sample_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, num_rays,
+    psvo::launch(k_sample_raw, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, num_rays,
                        max_hits, max_steps, fixed_step_size, pts_idx, min_depth, max_depth, uniform_noise, probs,
                        steps, sampled_idx, sampled_depth, sampled_dists);
     return check_launch("inverse_cdf_sampling");
@@ -1863,10 +1961,10 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "ray_intersect_sorted: step/voxel must be > 0");
     if (n_rays == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+    psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
                        hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr);
-    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
+    psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
 
@@ -1880,11 +1978,11 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     PSVO_REQUIRE(packed && ((uintptr_t)packed & 15) == 0, "ray_intersect_sorted_packed: packed records (16-B aligned)");
     if (n_rays == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+    psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
                        max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
                        nullptr);
-    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
+    psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
 
@@ -1917,17 +2015,17 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     tl.host = host;
     tl.seq = seq;
     tl.keep = keep;
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, nullptr, 0, tl);
     if (!tail)
-        hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
+        psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
                            host, seq, keep, tl.c);
     return check_launch("sample_rays_to_host");
 }
 
 int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq) {
-    hipLaunchKernelGGL(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
+    psvo::launch(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
     return check_launch("stats_to_host");
 }
 
@@ -1946,15 +2044,15 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
     const bool tail = !split_query() && blk_out && n_rays <= (int64_t)256 * kTailPasses;
     int *rr = tail ? ray_rank : nullptr, *rk = tail ? rank_ray : nullptr;
     if (packed)
-        hipLaunchKernelGGL(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+        psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
     else
-        hipLaunchKernelGGL(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+        psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
     if (!tail)
-        hipLaunchKernelGGL(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
+        psvo::launch(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
                            ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
     return check_launch("intersect_ranked");
 }
@@ -1966,13 +2064,13 @@ int dist_slot0_rows(int64_t max_rays_global) {
     return kSamplerG * (int)((kp + kSamplerChunk - 1) / kSamplerChunk);
 }
 int dist_pack(hipStream_t st, const int *stats, const int *rank_ray, const int *hit_idx, int *out) {
-    hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(64), 0, st, stats, rank_ray, hit_idx, out);
+    psvo::launch(k_dist_pack, dim3(1), dim3(64), 0, st, stats, rank_ray, hit_idx, out);
     return check_launch("dist_pack");
 }
 int dist_layout(hipStream_t st, const int *all, int world, int rank, int *stats, const int *rank_ray,
                 const int *hit_idx, int nch, int *table) {
-    hipLaunchKernelGGL(k_dist_layout, dim3(1), dim3(64), 0, st, all, world, rank, stats);
-    hipLaunchKernelGGL(k_dist_slot0, dim3(kSamplerG * nch), dim3(64), 0, st, stats, rank_ray, hit_idx, nch, table);
+    psvo::launch(k_dist_layout, dim3(1), dim3(64), 0, st, all, world, rank, stats);
+    psvo::launch(k_dist_slot0, dim3(kSamplerG * nch), dim3(64), 0, st, stats, rank_ray, hit_idx, nch, table);
     return check_launch("dist_layout");
 }
 // the fused sampler + scan over this rank's rows (stats from dist_layout)
@@ -1981,19 +2079,19 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
                 int *offsets) {
     if (r_hit_cap == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch, SampleTail{});
-    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
+    psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
                        nullptr, 0, nullptr, SampleCounts{});
     return check_launch("dist_sample");
 }
 int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
-    hipLaunchKernelGGL(k_dist_pack_smax, dim3(1), dim3(64), 0, st, stats, out);
+    psvo::launch(k_dist_pack_smax, dim3(1), dim3(64), 0, st, stats, out);
     return check_launch("dist_pack_smax");
 }
 int dist_smax(hipStream_t st, const int *all, int world, int *stats) {
-    hipLaunchKernelGGL(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats);
+    psvo::launch(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats);
     return check_launch("dist_smax");
 }
 }  // namespace psvo
@@ -2001,7 +2099,7 @@ int dist_smax(hipStream_t st, const int *all, int world, int *stats) {
 extern "C" int psvo_hit_rank(void *stream, int64_t n_rays, const int *ray_nv, int *ray_rank, int *rank_ray) {
     PSVO_REQUIRE(n_rays >= 0, "hit_rank: n_rays < 0");
     if (n_rays == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_hit_rank, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_rank, rank_ray);
+    psvo::launch(k_hit_rank, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_rank, rank_ray);
     return check_launch("hit_rank");
 }
 
@@ -2015,10 +2113,10 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
     PSVO_REQUIRE(offsets != nullptr && ray_ns != nullptr, "sample_rays: ray_ns / offsets required");
     if (r_hit_cap == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{});
-    hipLaunchKernelGGL(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
+    psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
                        stats, 0, nullptr, 0, nullptr, SampleCounts{});
     return check_launch("sample_rays");
 }
@@ -2035,14 +2133,14 @@ extern "C" int psvo_ray_stats(void *stream, int64_t n_rays, const int *ray_nv, c
                               float step_size, int *stats) {
     PSVO_REQUIRE(n_rays >= 0 && step_size > 0.0f, "ray_stats: bad arguments");
     if (n_rays == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_ray_stats, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_dsum, step_size,
+    psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, as_stream(stream), n_rays, ray_nv, ray_dsum, step_size,
                        stats);
     return check_launch("ray_stats");
 }
 
 extern "C" int psvo_scan_counts(void *stream, int64_t n, const int *counts, int *offsets) {
     PSVO_REQUIRE(n >= 0, "scan_counts: n < 0");
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, as_stream(stream), n, counts, offsets);
+    psvo::launch(k_scan_counts, dim3(1), dim3(1024), 0, as_stream(stream), n, counts, offsets);
     return check_launch("scan_counts");
 }
 
@@ -2055,7 +2153,7 @@ extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int ma
     (void)ray_ns;
     const int bx = s_max <= 64 ? 64 : s_max <= 128 ? 128 : 256;
     const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
-    hipLaunchKernelGGL(k_sample_points, dim3(div_up(s_max, bx), gy), dim3(bx), 0, as_stream(stream), r_hit,
+    psvo::launch(k_sample_points, dim3(div_up(s_max, bx), gy), dim3(bx), 0, as_stream(stream), r_hit,
                        s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask,
                        DevBatch{});
     return check_launch("sample_points");
@@ -2066,7 +2164,7 @@ int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const
                  int *leaf, float *t, int *ray_of_sample, const DevBatch &dev) {
     PSVO_REQUIRE(r_hit >= 0 && cap > 0, "compact_rays: bad sizes");
     if (r_hit == 0) return PSVO_OK;
-    hipLaunchKernelGGL(k_compact_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, s_idx, s_depth, offsets,
+    psvo::launch(k_compact_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, s_idx, s_depth, offsets,
                        leaf, t, ray_of_sample, dev);
     return check_launch("compact_rays");
 }
@@ -2077,7 +2175,7 @@ int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, cons
                  "sample_points_dev: bad sizes");
     const int bx = b.s_cap <= 64 ? 64 : b.s_cap <= 128 ? 128 : 256;
     const unsigned gy = (unsigned)(b.r_cap < 65535 ? b.r_cap : 65535);
-    hipLaunchKernelGGL(k_sample_points, dim3(div_up(b.s_cap, bx), gy), dim3(bx), 0, st, b.r_cap, b.s_cap,
+    psvo::launch(k_sample_points, dim3(div_up(b.s_cap, bx), gy), dim3(bx), 0, st, b.r_cap, b.s_cap,
                        max_steps_cap, s_idx, s_depth, nullptr, offsets, leaf, t, ray_of_sample, z_vals, mask, b);
     return check_launch("sample_points_dev");
 }

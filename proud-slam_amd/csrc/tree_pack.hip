@@ -213,13 +213,13 @@ extern "C" int psvo_pack_tree(void *stream, int64_t n_nodes, const float *centre
     PackRec *rec = static_cast<PackRec *>(packed);
     if (hipMemsetAsync(w.meta, 0, sizeof(int) * 2 * kPtMaxDepth, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "pack_tree: memset failed");
-    hipLaunchKernelGGL(k_pt_init, dim3(1), dim3(1), 0, st, w);
+    psvo::launch(k_pt_init, dim3(1), dim3(1), 0, st, w);
     const int nb = (int)((n_nodes + kPtBlock - 1) / kPtBlock);
     for (int level = 0; level < kPtMaxDepth; ++level) {
-        hipLaunchKernelGGL(k_pt_count, dim3(nb), dim3(kPtThreads), 0, st, level, structure, w);
-        hipLaunchKernelGGL(k_pt_scan, dim3(1), dim3(1024), 0, st, level, w);
-        hipLaunchKernelGGL(k_pt_emit, dim3(nb), dim3(kPtThreads), 0, st, level, centres, structure, w, rec);
+        psvo::launch(k_pt_count, dim3(nb), dim3(kPtThreads), 0, st, level, structure, w);
+        psvo::launch(k_pt_scan, dim3(1), dim3(1024), 0, st, level, w);
+        psvo::launch(k_pt_emit, dim3(nb), dim3(kPtThreads), 0, st, level, centres, structure, w, rec);
     }
-    hipLaunchKernelGGL(k_pt_top, dim3(1), dim3(512), 0, st, w, rec);
+    psvo::launch(k_pt_top, dim3(1), dim3(512), 0, st, w, rec);
     return check_launch("pack_tree");
 }

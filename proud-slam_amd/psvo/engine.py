@@ -371,9 +371,12 @@ class MappingEngine:
                self.step_no, 1 if marked else 0)
 
     def set_timing(self, on):
-        """HIP events around the decoder fwd / bwd and interp fwd / bwd launches.
-        on=True: regions serialised on one stream; on="overlap": as the
-        untimed step runs them (side streams overlapping the main stream)."""
+        """Per-region kernel time (query: intersect / sample / points, interp fwd
+        / bwd, decoder fwd / bwd): each kernel a region launches is timed by a
+        HIP event pair bound to its own dispatch, a region is the sum of its
+        kernels' spans (PSVO_TIMING_MARKERS=1: marker events around the
+        region).  on=True: regions serialised on one stream; on="overlap": as
+        the untimed step runs them (side streams overlapping the main stream)."""
         L.call("psvo_engine_set_timing", self.handle, 2 if on == "overlap" else int(bool(on)))
 
     def set_clock(self, max_steps):

@@ -462,45 +462,28 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     steps = {int(st_e["step"].item())} | {int(st["step"].item()) for st in st_d}
     if len(steps) != 1:
         return False  # parameters at different Adam steps: the engine steps them together
-    clk("state")
-    eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
-                  [st["exp_avg_sq"] for st in st_d])
-    clk("bind")
-    eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
-    clk("tree")
-    eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
     adam_step = steps.pop()
     dev = emb.device
-    # keyframe poses [F, 6] and their Adam state on the device
+    # the keyframes' pose optimisers: checked (host only) before anything is
+    # queued, so a call that falls back to the autograd loop has drawn nothing
     kfs = list(keyframe_graph)
     upd = [bool(kf.stamp != 0 and update_pose and getattr(kf, "optim", None) is not None) for kf in kfs]
     pose_params = [kf.pose.data for kf in kfs]
-    poses = torch.stack([p.detach().to(dev, torch.float32).reshape(6) for p in pose_params]).contiguous()
-    pstep = [0] * len(kfs)
+    pose_st = [None] * len(kfs)
     lr_pose = None
-    zero6 = None
-    m_rows, v_rows = [], []
     for f, kf in enumerate(kfs):
         if not upd[f]:
-            if zero6 is None:
-                zero6 = torch.zeros(6, dtype=torch.float32, device=dev)
-            m_rows.append(zero6)
-            v_rows.append(zero6)
             continue
         if not _is_adam(kf.optim):
             return False
-        st = _adam_state(kf.optim, pose_params[f])
-        m_rows.append(st["exp_avg"].to(dev, torch.float32).reshape(6))
-        v_rows.append(st["exp_avg_sq"].to(dev, torch.float32).reshape(6))
-        pstep[f] = int(st["step"].item())
         lr = kf.optim.param_groups[0]["lr"]
         if lr_pose is not None and lr != lr_pose:
             return False
         lr_pose = lr
         if tuple(kf.optim.param_groups[0]["betas"]) != tuple(embed_optim.param_groups[0]["betas"]):
             return False
-    pm = torch.stack(m_rows).contiguous()  # the poses' Adam moments [F, 6], one gather each
-    pv = torch.stack(v_rows).contiguous()
+        pose_st[f] = _adam_state(kf.optim, pose_params[f])
+    clk("state")
     # keyframes whose sample_rays is the reference's uniform gumbel top-k
     # (frame.py:83-85) are sampled together in one native call with the
     # gathers fused (psvo.sample_util.sample_frames); others through their own
@@ -559,11 +542,35 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         ev.record(side)
         return out, ev
 
-    clk("poses")
+    # the first pixels are queued first: the GPU draws them while the host
+    # binds the optimiser state and packs the poses (the call's fixed cost)
     cur, cur_ready = draw_ahead(0)
+    clk("draw0")
+    eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
+                  [st["exp_avg_sq"] for st in st_d])
+    eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
+    eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
+    # keyframe poses [F, 6] and their Adam state on the device
+    poses = torch.stack([p.detach().to(dev, torch.float32).reshape(6) for p in pose_params]).contiguous()
+    pstep = [0] * len(kfs)
+    zero6 = None
+    m_rows, v_rows = [], []
+    for f in range(len(kfs)):
+        st = pose_st[f]
+        if st is None:
+            if zero6 is None:
+                zero6 = torch.zeros(6, dtype=torch.float32, device=dev)
+            m_rows.append(zero6)
+            v_rows.append(zero6)
+            continue
+        m_rows.append(st["exp_avg"].to(dev, torch.float32).reshape(6))
+        v_rows.append(st["exp_avg_sq"].to(dev, torch.float32).reshape(6))
+        pstep[f] = int(st["step"].item())
+    pm = torch.stack(m_rows).contiguous()  # the poses' Adam moments [F, 6], one gather each
+    pv = torch.stack(v_rows).contiguous()
     if cur_ready is not None:
         main.wait_event(cur_ready)
-    clk("draw0")
+    clk("poses")
     for it in range(num_iterations):
         # the engine orders the look-ahead's pose step (reads nxt's dirs) after
         # the draw queued on `side` (next_stream), and with it the next step
