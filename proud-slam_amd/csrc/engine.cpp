@@ -144,6 +144,8 @@ struct psvo_engine {
     // pose step and the next query; every later reader of the weights on st
     // waits for adam_done first (render, before the interpolation)
     hipEvent_t adam_done = nullptr;
+    hipEvent_t pf_fork = nullptr;  // the L2 warm-up for the look-ahead query forks from the backward here
+    float *pf_sink = nullptr;
     bool adam_pending = false;
     hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
     // capacities of the device-sized forward (render): samples, samples per ray
@@ -538,6 +540,8 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->prep_fork) (void)hipEventDestroy(e->prep_fork);
     if (e->prep_done) (void)hipEventDestroy(e->prep_done);
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
+    if (e->pf_fork) (void)hipEventDestroy(e->pf_fork);
+    if (e->pf_sink) (void)hipFree(e->pf_sink);
     if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
@@ -833,7 +837,7 @@ bool engine_overlap(psvo_engine *e) {
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready};
+                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready, &e->pf_fork};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
@@ -1511,6 +1515,24 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr,
                      split ? ax : nullptr, ib_serial ? &ib_hook : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
+    // PSVO_PREFETCH=1 (A/B, off by default): warm the XCD L2s with the
+    // query's / the interpolation's read-only arrays (maps whose arrays fit)
+    // while the per-ray sums and the pose step run.  Measured (config B, one
+    // box, three interleaved pairs): the intersect region 26.2-28.1 ->
+    // 24.4-26.7 us, but the iteration 0.922-0.938 -> 0.946-0.948 ms — the
+    // sweep competes with the step's tail on the other queues
+    static const bool prefetch = getenv("PSVO_PREFETCH") && *getenv("PSVO_PREFETCH") == '1';
+    if (prefetch && split && !dist && e->lossq) {
+        const int64_t nn = d->n_nodes;
+        const void *pp[4] = {d->packed, d->vertex_idx, d->centres, d->emb};
+        const int64_t pb[4] = {d->packed ? nn * 32 : 0, nn * 8 * 4, nn * 3 * 4 / 16 * 16, d->n_emb * 16 * 4};
+        if (pb[0] + pb[1] + pb[2] + pb[3] <= (int64_t)3 << 20) {
+            if (!e->pf_sink && hipMalloc(reinterpret_cast<void **>(&e->pf_sink), 64) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "map_step: hipMalloc failed");
+            ENG_CALL(fork_join(st, e->lossq, e->pf_fork));
+            ENG_CALL(psvo::l2_prefetch(e->lossq, 4, pp, pb, e->pf_sink));
+        }
+    }
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
     // (ib_serial: it ran inside mlp_bwd, on st)
     hipStream_t eb = (split || ib_serial) ? st : ax;

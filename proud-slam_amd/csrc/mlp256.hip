@@ -45,8 +45,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWaves = 8, kThreads = 64 * kWaves;
 constexpr int kTileW = 16;                 // samples per wave
 constexpr int kTileWG = kWaves * kTileW;   // samples per workgroup iteration
-constexpr int kChunkFloats = 8192;         // 32 KB ring buffer
-constexpr int kRing = 3;
+// The weight images stream through LDS in chunks of kIbPer input blocks
+// (all of a layer's output blocks): 4 input blocks = 64 KB chunks in a ring
+// of 2 (13 chunks, i.e. 13 workgroup barriers per tile); PSVO_DEC256_IBPER=2:
+// 32 KB chunks in a ring of 3 (23 chunks), the earlier layout, for A/B.
+#ifndef PSVO_DEC256_IBPER
+#define PSVO_DEC256_IBPER 4
+#endif
+constexpr int kIbPer = PSVO_DEC256_IBPER;
+static_assert(kIbPer == 2 || kIbPer == 4, "chunk width");
+constexpr int kChunkFloats = kIbPer * 16 * 256;  // a chunk of the widest layer (16 output blocks)
+constexpr int kRing = kIbPer == 4 ? 2 : 3;
 
 // ---- weight images (floats) ----------------------------------------------
 // forward: L1 [1][16], L2 [16][16], L3 [16][9], L4 [9][16], L5 [16][1]  ([ib][ob] blocks of 256 floats)
@@ -77,24 +86,35 @@ struct Chunk {
 __host__ __device__ constexpr Chunk chunk_of(Img im, int ib0, int nib) { return {im.off + ib0 * im.nob * kBlk, im.nob, ib0, nib}; }
 __host__ __device__ constexpr int chunk_floats(Chunk c) { return c.nib * c.nob * kBlk; }
 
-// forward: 1 + 8 + 8 + 5 + 1 = 23 chunks
-constexpr int kFwdChunks = 23;
+// chunks per layer: ceil(input blocks / kIbPer); L1 and L5 (one output /
+// input block row) are one chunk each
+constexpr int chunks_of(int nib) { return (nib + kIbPer - 1) / kIbPer; }
+constexpr int kN16 = chunks_of(16), kN9 = chunks_of(9);
+// forward: L1 | L2 (kN16) | L3 (kN16) | L4 (kN9) | L5
+constexpr int kFwdL2 = 1, kFwdL3 = kFwdL2 + kN16, kFwdL4 = kFwdL3 + kN16, kFwdL5 = kFwdL4 + kN9,
+              kFwdChunks = kFwdL5 + 1;
+__host__ __device__ constexpr Chunk layer_chunk(Img im, int j) {
+    return chunk_of(im, kIbPer * j, im.nib - kIbPer * j < kIbPer ? im.nib - kIbPer * j : kIbPer);
+}
 __host__ __device__ constexpr Chunk fwd_chunk(int c) {
-    return c == 0    ? chunk_of(kF1, 0, 1)
-           : c <= 8  ? chunk_of(kF2, 2 * (c - 1), 2)
-           : c <= 16 ? chunk_of(kF3, 2 * (c - 9), 2)
-           : c <= 21 ? chunk_of(kF4, 2 * (c - 17), c == 21 ? 1 : 2)
-                     : chunk_of(kF5, 0, 16);
+    return c == 0         ? chunk_of(kF1, 0, 1)
+           : c < kFwdL3   ? layer_chunk(kF2, c - kFwdL2)
+           : c < kFwdL4   ? layer_chunk(kF3, c - kFwdL3)
+           : c < kFwdL5   ? layer_chunk(kF4, c - kFwdL4)
+                          : chunk_of(kF5, 0, 16);
 }
-// backward (data): 1 + 8 + 5 + 8 + 1 = 23 chunks
-constexpr int kBwdChunks = 23;
+// backward (data): W5ᵀ | W4ᵀ (kN16) | W3ᵀ (kN9) | W2ᵀ (kN16) | W1ᵀ
+constexpr int kBwdL4 = 1, kBwdL3 = kBwdL4 + kN16, kBwdL2 = kBwdL3 + kN9, kBwdL1 = kBwdL2 + kN16,
+              kBwdChunks = kBwdL1 + 1;
 __host__ __device__ constexpr Chunk bwd_chunk(int c) {
-    return c == 0    ? chunk_of(kB5, 0, 1)
-           : c <= 8  ? chunk_of(kB4, 2 * (c - 1), 2)
-           : c <= 13 ? chunk_of(kB3, 2 * (c - 9), c == 13 ? 1 : 2)
-           : c <= 21 ? chunk_of(kB2, 2 * (c - 14), 2)
-                     : chunk_of(kB1, 0, 16);
+    return c == 0         ? chunk_of(kB5, 0, 1)
+           : c < kBwdL3   ? layer_chunk(kB4, c - kBwdL4)
+           : c < kBwdL2   ? layer_chunk(kB3, c - kBwdL3)
+           : c < kBwdL1   ? layer_chunk(kB2, c - kBwdL2)
+                          : chunk_of(kB1, 0, 16);
 }
+static_assert(chunk_floats(chunk_of(kF5, 0, 16)) <= kChunkFloats && chunk_floats(chunk_of(kB1, 0, 16)) <= kChunkFloats,
+              "one-chunk layers fit a ring buffer");
 
 // effective (out x in) matrices of the images, from the torch parameters
 struct Params {
@@ -343,10 +363,12 @@ struct Dlt {
     float *d1, *d2, *d3, *d4, *d5;  // δh1 [256], δh2 [256], [δf; g_sdf] [144], δc1 [256], δ5 [16] tiles
 };
 
-// The program's chunks run in order per tile; at chunk k the ring holds
-// chunks k, k+1 and chunk k+2 is issued (the next tile's first chunks at the
-// end of a tile).  Waves of a tile past M still take part (zero inputs, no
-// per-sample output stores).
+// The program's chunks run in order per tile.  Ring of 3: at chunk k the
+// ring holds chunks k, k+1 and chunk k+2 is issued; ring of 2: chunk k+1 is
+// issued into the buffer chunk k−1 held.  Either way the barrier first waits
+// for every outstanding copy (vmcnt(0)), so a chunk lands while the one
+// before it is computed; the next tile's first chunks are issued at the end
+// of a tile.
 struct Ring {
     float *ring;
     const float *img;
@@ -355,19 +377,39 @@ struct Ring {
     template <int NCH, typename Plan>
     __device__ __forceinline__ const float *next(int k, Plan plan) {
         chunk_barrier();
-        const int k2 = k + 2;
+        constexpr int kAhead = kRing - 1;
+        const int k2 = k + kAhead;
         if (k2 < NCH || more) {
             const Chunk c = plan(k2 < NCH ? k2 : k2 - NCH);
             const float *src = img;
             asm volatile("" : "+s"(src));  // the chunk address is formed here, not hoisted (SGPR spills)
-            stream_chunk<kCWaves>(src + c.img_off, ring + ((slot + 2) % kRing) * kChunkFloats, chunk_floats(c), wave,
-                                  lane);
+            stream_chunk<kCWaves>(src + c.img_off, ring + ((slot + kAhead) % kRing) * kChunkFloats, chunk_floats(c),
+                                  wave, lane);
         }
         const float *b = ring + slot * kChunkFloats;
         slot = (slot + 1) % kRing;
         return b;
     }
+    // the first kRing − 1 chunks of a program, before its first tile
+    template <typename Plan>
+    __device__ __forceinline__ void prime(Plan plan) {
+#pragma unroll
+        for (int c = 0; c < kRing - 1; ++c)
+            stream_chunk<kCWaves>(img + plan(c).img_off, ring + c * kChunkFloats, chunk_floats(plan(c)), wave, lane);
+    }
 };
+
+// chunks [C0, C0 + N) of one layer: input blocks [kIbPer·j, …) of `in` into `acc`
+template <int NCH, int C0, int J, int N, int NOB, int NIN, typename Plan>
+__device__ __forceinline__ void layer_chunks(Ring &R, f32x4 (&acc)[kNC][NOB], const f32x4 (&in)[kNC][NIN], Plan plan,
+                                             int lane, bool on) {
+    if constexpr (J < N) {
+        constexpr int IB0 = J * kIbPer;
+        constexpr int NIB = NIN - IB0 < kIbPer ? NIN - IB0 : kIbPer;
+        gemm_chunk<NOB, NIN, IB0, NIB>(acc, in, R.next<NCH>(C0 + J, plan), lane, on);
+        layer_chunks<NCH, C0, J + 1, N, NOB, NIN>(R, acc, in, plan, lane, on);
+    }
+}
 
 // The chain kernels' work plan: rounds over the grid's wave slots, a wave's
 // unit = kNC consecutive 16-sample tiles.  Every round but the last fills all
@@ -403,10 +445,9 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
     const ChainPlan P(m);
     if (P.rounds == 0) return;
     Ring R{lds + ((kVecN + 63) / 64) * 64, img, 0, wave, lane, false};
-    stream_chunk<kCWaves>(img + fwd_chunk(0).img_off, R.ring, chunk_floats(fwd_chunk(0)), wave, lane);
-    stream_chunk<kCWaves>(img + fwd_chunk(1).img_off, R.ring + kChunkFloats, chunk_floats(fwd_chunk(1)), wave, lane);
     const int n = lane & 15, g = lane >> 4;
     auto plan = [](int c) { return fwd_chunk(c); };
+    R.prime(plan);
     const bool train = act.h1 != nullptr;  // inference (no act): per-sample outputs only
     for (int64_t rd = 0; rd < P.rounds; ++rd) {
         R.more = rd + 1 < P.rounds;
@@ -427,17 +468,13 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
         gemm_chunk<16, 1, 0, 1>(h1, x, R.next<kFwdChunks>(0, plan), lane, on);
         relu_mask(h1, m1);
         init_bias(h2, vec + kVB2, lane);
-#define F2(K) gemm_chunk<16, 16, 2 * (K - 1), 2>(h2, h1, R.next<kFwdChunks>(K, plan), lane, on);
-        F2(1) F2(2) F2(3) F2(4) F2(5) F2(6) F2(7) F2(8)
-#undef F2
+        layer_chunks<kFwdChunks, kFwdL2, 0, kN16>(R, h2, h1, plan, lane, on);
         if (train && on) store_tiles(act.h1, t16, 256, h1, lane);
         relu_mask(h2, m2);
         // L3: rows [f (blocks 0..7) | sdf (block 8, row 0)]
         f32x4 o3[kNC][9];
         init_bias(o3, vec + kVB3, lane);
-#define F3(K) gemm_chunk<9, 16, 2 * (K - 9), 2>(o3, h2, R.next<kFwdChunks>(K, plan), lane, on);
-        F3(9) F3(10) F3(11) F3(12) F3(13) F3(14) F3(15) F3(16)
-#undef F3
+        layer_chunks<kFwdChunks, kFwdL3, 0, kN16>(R, o3, h2, plan, lane, on);
         if (train && on) store_tiles(act.h2, t16, 256, h2, lane);
         float sdf_v[kNC];
         f32x4 fx[kNC][9];
@@ -451,17 +488,13 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
         // L4
         f32x4 c1[kNC][16];
         init_bias(c1, vec + kVB4, lane);
-        gemm_chunk<16, 9, 0, 2>(c1, fx, R.next<kFwdChunks>(17, plan), lane, on);
-        gemm_chunk<16, 9, 2, 2>(c1, fx, R.next<kFwdChunks>(18, plan), lane, on);
-        gemm_chunk<16, 9, 4, 2>(c1, fx, R.next<kFwdChunks>(19, plan), lane, on);
-        gemm_chunk<16, 9, 6, 2>(c1, fx, R.next<kFwdChunks>(20, plan), lane, on);
-        gemm_chunk<16, 9, 8, 1>(c1, fx, R.next<kFwdChunks>(21, plan), lane, on);
+        layer_chunks<kFwdChunks, kFwdL4, 0, kN9>(R, c1, fx, plan, lane, on);
         if (train && on) store_tiles(act.fx, t16, 144, fx, lane);
         relu_mask(c1, m4);
         // L5
         f32x4 o5[kNC][1];
         init_bias(o5, vec + kVB5, lane);
-        gemm_chunk<1, 16, 0, 16>(o5, c1, R.next<kFwdChunks>(22, plan), lane, on);
+        gemm_chunk<1, 16, 0, 16>(o5, c1, R.next<kFwdChunks>(kFwdL5, plan), lane, on);
         if (train && on) store_tiles(act.c1, t16, 256, c1, lane);
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
@@ -496,11 +529,10 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
     const ChainPlan P(m);
     if (P.rounds == 0) return;
     Ring R{lds, img, 0, wave, lane, false};
-    stream_chunk<kCWaves>(img + bwd_chunk(0).img_off, R.ring, chunk_floats(bwd_chunk(0)), wave, lane);
-    stream_chunk<kCWaves>(img + bwd_chunk(1).img_off, R.ring + kChunkFloats, chunk_floats(bwd_chunk(1)), wave, lane);
     const int n = lane & 15, g = lane >> 4;
     const bool want_w = dl.d1 != nullptr;
     auto plan = [](int c) { return bwd_chunk(c); };
+    R.prime(plan);
     for (int64_t rd = 0; rd < P.rounds; ++rd) {
         R.more = rd + 1 < P.rounds;
         R.img = img;
@@ -539,9 +571,7 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         // δ[f; x] = W4ᵀ δc1
         f32x4 dfx[kNC][9];
         zero(dfx);
-#define B4(K) gemm_chunk<9, 16, 2 * (K - 1), 2>(dfx, dc1, R.next<kBwdChunks>(K, plan), lane, on);
-        B4(1) B4(2) B4(3) B4(4) B4(5) B4(6) B4(7) B4(8)
-#undef B4
+        layer_chunks<kBwdChunks, kBwdL4, 0, kN16>(R, dfx, dc1, plan, lane, on);
         if (want_w && on) {
             store_tiles(dl.d4, t16, 256, dc1, lane);
             store_tiles(dl.d5, t16, 16, d5, lane);
@@ -555,23 +585,17 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         }
         f32x4 dh2[kNC][16];
         zero(dh2);
-        gemm_chunk<16, 9, 0, 2>(dh2, dfx, R.next<kBwdChunks>(9, plan), lane, on);
-        gemm_chunk<16, 9, 2, 2>(dh2, dfx, R.next<kBwdChunks>(10, plan), lane, on);
-        gemm_chunk<16, 9, 4, 2>(dh2, dfx, R.next<kBwdChunks>(11, plan), lane, on);
-        gemm_chunk<16, 9, 6, 2>(dh2, dfx, R.next<kBwdChunks>(12, plan), lane, on);
-        gemm_chunk<16, 9, 8, 1>(dh2, dfx, R.next<kBwdChunks>(13, plan), lane, on);
+        layer_chunks<kBwdChunks, kBwdL3, 0, kN9>(R, dh2, dfx, plan, lane, on);
         if (want_w && on) store_tiles(dl.d3, t16, 144, dfx, lane);
         apply_mask(dh2, m2);
         // δh1 = (W2ᵀ δh2) ⊙ m_h1
         f32x4 dh1[kNC][16];
         zero(dh1);
-#define B2(K) gemm_chunk<16, 16, 2 * (K - 14), 2>(dh1, dh2, R.next<kBwdChunks>(K, plan), lane, on);
-        B2(14) B2(15) B2(16) B2(17) B2(18) B2(19) B2(20) B2(21)
-#undef B2
+        layer_chunks<kBwdChunks, kBwdL2, 0, kN16>(R, dh1, dh2, plan, lane, on);
         if (want_w && on) store_tiles(dl.d2, t16, 256, dh2, lane);
         apply_mask(dh1, m1);
         // δx = W1ᵀ δh1 + the x rows of δ[f; x]
-        gemm_chunk<1, 16, 0, 16>(dx, dh1, R.next<kBwdChunks>(22, plan), lane, on);
+        gemm_chunk<1, 16, 0, 16>(dx, dh1, R.next<kBwdChunks>(kBwdL1, plan), lane, on);
         if (want_w && on) store_tiles(dl.d1, t16, 256, dh1, lane);
 #pragma unroll
         for (int c = 0; c < kNC; ++c) {
@@ -599,7 +623,16 @@ struct DwPlan {
     int slab_off[5];  // floats: slab of type t starts at slab_off[t] + (wg - wg_begin[t]) * slab_size[t]
     int slab_size[4];
 };
-constexpr int kDwLds = 3 * 8704 * 4;                    // 3 stages of ≤ 8,704 floats (L15: 4,096+256+256+4,096)
+// L3 / L4 workgroups (18 output blocks a wave) take kDwTpb 16-sample tiles
+// per stage: one barrier per kDwTpb tiles (their per-tile MFMA work is about
+// half of L2's 32 blocks); 3 stages of ≤ 12,800 floats
+#ifndef PSVO_DW256_TPB
+#define PSVO_DW256_TPB 2
+#endif
+constexpr int kDwTpb = PSVO_DW256_TPB;
+constexpr int kDwSt = 6400 * kDwTpb > 8704 ? 6400 * kDwTpb : 8704;  // floats per stage
+constexpr int kDwLds = 3 * kDwSt * 4;
+static_assert(kDwLds <= 160 * 1024, "dw LDS budget");
 
 // block ownership: wave w, layer type t → list of (mb, nb) with mb < MB_t, nb < NB_t
 // L2 (16x16): mb 4(w>>1)..+3, nb 8(w&1)..+7    -> 32 blocks
@@ -696,47 +729,62 @@ __device__ void dw_run(const DwOps &op, const DwPlan &pl, float *slabs, float *l
                   NP3 = T == 3 ? 16 : 0;
     constexpr int NPT = NP0 + NP1 + NP2 + NP3;
     constexpr int PER = (NPT + kWaves - 1) / kWaves;
-    auto fill = [&](int64_t t, float *st) {
-        const float *base[4];
-        if (T == 3) {
-            base[0] = op.a[3] + t * 256 * 16;               // δh1
-            base[1] = op.b[3] + t * 144 * 16 + 128 * 16;    // x rows of [f; x]
-            base[2] = op.a5 + t * 16 * 16;                  // δ5
-            base[3] = op.b5 + t * 256 * 16;                 // c1
-        } else {
-            base[0] = op.a[T] + t * FA * 16;
-            base[1] = op.b[T] + t * FB * 16;
-            base[2] = base[3] = base[0];
-        }
-        uint32_t voff = (uint32_t)lane * 16u;
-        asm volatile("" : "+v"(voff));
+    constexpr int TPB = (T == 1 || T == 2) ? kDwTpb : 1;  // tiles per stage
+    // stage s holds tiles t0 + TPB·s + j; past t1 the last tile is copied again
+    // (same copy count per wave) and not computed
+    auto fill = [&](int64_t sg, float *st) {
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            int p = wave + k * kWaves;
-            p = p < NPT ? p : NPT - 1;
-            const int r = p < NP0 ? 0 : p < NP0 + NP1 ? 1 : p < NP0 + NP1 + NP2 ? 2 : 3;
-            const int q = p - (r == 0 ? 0 : r == 1 ? NP0 : r == 2 ? NP0 + NP1 : NP0 + NP1 + NP2);
-            glds16s(base[r] + q * 256, voff, st + p * 256);
+        for (int j = 0; j < TPB; ++j) {
+            int64_t t = t0 + TPB * sg + j;
+            t = t < t1 ? t : t1 - 1;
+            const float *base[4];
+            if (T == 3) {
+                base[0] = op.a[3] + t * 256 * 16;               // δh1
+                base[1] = op.b[3] + t * 144 * 16 + 128 * 16;    // x rows of [f; x]
+                base[2] = op.a5 + t * 16 * 16;                  // δ5
+                base[3] = op.b5 + t * 256 * 16;                 // c1
+            } else {
+                base[0] = op.a[T] + t * FA * 16;
+                base[1] = op.b[T] + t * FB * 16;
+                base[2] = base[3] = base[0];
+            }
+            uint32_t voff = (uint32_t)lane * 16u;
+            asm volatile("" : "+v"(voff));
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                int p = wave + k * kWaves;
+                p = p < NPT ? p : NPT - 1;
+                const int r = p < NP0 ? 0 : p < NP0 + NP1 ? 1 : p < NP0 + NP1 + NP2 ? 2 : 3;
+                const int q = p - (r == 0 ? 0 : r == 1 ? NP0 : r == 2 ? NP0 + NP1 : NP0 + NP1 + NP2);
+                glds16s(base[r] + q * 256, voff, st + j * kStageF + p * 256);
+            }
         }
     };
-    constexpr int kSt = 8704;
-    static_assert(kStageF <= kSt && NPT * 256 == kStageF, "dw stage");
-    if (t0 < t1) fill(t0, lds);
-    if (t0 + 1 < t1) fill(t0 + 1, lds + kSt);
+    static_assert(TPB * kStageF <= kDwSt && NPT * 256 == kStageF, "dw stage");
+    const int64_t n_sg = t0 < t1 ? (t1 - t0 + TPB - 1) / TPB : 0;
+    if (n_sg > 0) fill(0, lds);
+    if (n_sg > 1) fill(1, lds + kDwSt);
     int slot = 0;
-    for (int64_t t = t0; t < t1; ++t) {
-        // this wave's copies of tile t landed (tile t + 1's may be in flight), then all waves'
-        if (t + 1 < t1) wait_vm_lds<PER>(); else wait_vm_lds<0>();
+    for (int64_t sg = 0; sg < n_sg; ++sg) {
+        // this wave's copies of stage sg landed (stage sg + 1's may be in flight), then all waves'
+        if (sg + 1 < n_sg) wait_vm_lds<PER * TPB>(); else wait_vm_lds<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + 2 < t1) fill(t + 2, lds + ((slot + 2) % 3) * kSt);
-        const float *st = lds + slot * kSt;
-        if (T == 3) {
-            // x rows sit at stage row offset 256 (rows 128..143 of fx): block index 0 of a 16-row tile
-            dw_tile<MB, NB>(acc, bsum, true, st, st + 4096 - 0, mb, nb, lane);
-            dw_tile<1, 2>(acc5, bsum5, wave == 0, st + 4352, st + 4608, mb5, nb5, lane);
-        } else {
-            dw_tile<MB, NB>(acc, bsum, bias_main, st, st + FA * 16, mb, nb, lane);
+        if (sg + 2 < n_sg) fill(sg + 2, lds + ((slot + 2) % 3) * kDwSt);
+        auto tile = [&](int j) {
+            const float *st = lds + slot * kDwSt + j * kStageF;
+            if (T == 3) {
+                // x rows sit at stage row offset 256 (rows 128..143 of fx): block index 0 of a 16-row tile
+                dw_tile<MB, NB>(acc, bsum, true, st, st + 4096 - 0, mb, nb, lane);
+                dw_tile<1, 2>(acc5, bsum5, wave == 0, st + 4352, st + 4608, mb5, nb5, lane);
+            } else {
+                dw_tile<MB, NB>(acc, bsum, bias_main, st, st + FA * 16, mb, nb, lane);
+            }
+        };
+        tile(0);
+        if constexpr (TPB == 2) {
+            __builtin_amdgcn_sched_barrier(0);  // the second tile's operand loads not hoisted into the first's MFMAs
+            if (t0 + 2 * sg + 1 < t1) tile(1);  // uniform: the last stage's missing tile
         }
         slot = (slot + 1) % 3;
     }
@@ -845,7 +893,10 @@ static void dw_plan(int64_t m, DwPlan *pl, int64_t *slab_floats) {
     // 1,600 B, L1 + L5: 16.4 kFLOP | 2,112 B (memory-bound: by FLOPs alone it
     // got 14 workgroups and set the kernel's time)
     const int cus = device_cus256();
-    int w[4] = {213, 120, 120, 107};
+    // per-type weights measured at config C (466 k samples, one box, decoder
+    // alone): {213,120,120,107} 1,310 us -> {213,130,130,60} 1,195-1,200 us —
+    // the W1 / W5 type's byte-bound tiles finish early with fewer workgroups
+    int w[4] = {213, 130, 130, 60};
     static const char *wenv = getenv("PSVO_DW256_W");  // A/B: "w0,w1,w2,w3"
     if (wenv) {
         int v[4];
@@ -853,14 +904,28 @@ static void dw_plan(int64_t m, DwPlan *pl, int64_t *slab_floats) {
             for (int t = 0; t < 4; ++t) w[t] = v[t];
     }
     const double wsum = (double)(w[0] + w[1] + w[2] + w[3]);
+    // exactly `cus` workgroups (largest remainders): one more than the CUs
+    // would run two of them back to back on one CU (104 KB of LDS each)
     int n[4], tot = 0;
+    double rem[4];
     for (int t = 0; t < 4; ++t) {
-        n[t] = (int)((double)cus * w[t] / wsum + 0.5);
-        if (n[t] < 1) n[t] = 1;
-        if (n[t] > n16) n[t] = (int)(n16 > 0 ? n16 : 1);
+        const double q = (double)cus * w[t] / wsum;
+        n[t] = (int)q;
+        rem[t] = q - n[t];
         tot += n[t];
     }
-    (void)tot;
+    while (tot < cus) {
+        int b = 0;
+        for (int t = 1; t < 4; ++t)
+            if (rem[t] > rem[b]) b = t;
+        n[b] += 1;
+        rem[b] = -1.0;
+        tot += 1;
+    }
+    for (int t = 0; t < 4; ++t) {
+        if (n[t] < 1) n[t] = 1;
+        if (n[t] > n16) n[t] = (int)(n16 > 0 ? n16 : 1);
+    }
     pl->wg_begin[0] = 0;
     for (int t = 0; t < 4; ++t) pl->wg_begin[t + 1] = pl->wg_begin[t] + n[t];
     const int sz[4] = {256 * 256 + 256, 144 * 256 + 144, 256 * 144 + 256, 256 * 16 + 256 + 16 * 256 + 16};

@@ -175,6 +175,10 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
                      float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
 // the valid prefix of each sampler row → leaf / t / ray_of_sample at offsets[r] + s
+// Warm every XCD's L2 with up to 4 small read-only arrays (bytes multiple of
+// 16) right before the kernels that read them (svo_query.hip); `sink` gets a
+// write only in the impossible case that keeps the loads alive.
+int l2_prefetch(hipStream_t st, int n, const void *const *ptr, const int64_t *bytes, float *sink);
 int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const float *s_depth, const int *offsets,
                  int *leaf, float *t, int *ray_of_sample, const DevBatch &dev);
 // sample compaction + interpolation forward, one wave per hit ray (the

@@ -452,6 +452,21 @@ class _CallClock:
             sys.stderr.write("ba-call " + " ".join(f"{w}={t * 1e3:.3f}" for w, t in self.marks) + "\n")
 
 
+def _pose_pack_key(kfs, pose_params, pose_st, upd, dev):
+    """Identity + version of every tensor the packed poses / moments / steps
+    are made from (an in-place write anywhere bumps a version)."""
+    key = [str(dev), tuple(upd)]
+    for f in range(len(kfs)):
+        p = pose_params[f]
+        key.append((id(p), p._version, p.data_ptr()))
+        st = pose_st[f]
+        if st is not None:
+            for n in ("exp_avg", "exp_avg_sq", "step"):
+                t = st[n]
+                key.append((id(t), t._version, t.data_ptr()))
+    return tuple(key)
+
+
 def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays, num_iterations, update_pose,
                           noise, seed_fn=None, lookahead=True):
     clk = _CallClock()
@@ -550,24 +565,34 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
                   [st["exp_avg_sq"] for st in st_d])
     eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
     eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
-    # keyframe poses [F, 6] and their Adam state on the device
-    poses = torch.stack([p.detach().to(dev, torch.float32).reshape(6) for p in pose_params]).contiguous()
-    pstep = [0] * len(kfs)
-    zero6 = None
-    m_rows, v_rows = [], []
-    for f in range(len(kfs)):
-        st = pose_st[f]
-        if st is None:
-            if zero6 is None:
-                zero6 = torch.zeros(6, dtype=torch.float32, device=dev)
-            m_rows.append(zero6)
-            v_rows.append(zero6)
-            continue
-        m_rows.append(st["exp_avg"].to(dev, torch.float32).reshape(6))
-        v_rows.append(st["exp_avg_sq"].to(dev, torch.float32).reshape(6))
-        pstep[f] = int(st["step"].item())
-    pm = torch.stack(m_rows).contiguous()  # the poses' Adam moments [F, 6], one gather each
-    pv = torch.stack(v_rows).contiguous()
+    # keyframe poses [F, 6] and their Adam state on the device — packed again
+    # only when a tensor changed since this engine's last call wrote them back
+    # (torch's version counters; the packed copies then still hold exactly the
+    # written-back values): the repack's ~15 small torch ops were most of a
+    # call's host setup
+    pack_key = _pose_pack_key(kfs, pose_params, pose_st, upd, dev)
+    cached = getattr(eng, "_pose_pack", None)
+    if cached is not None and cached[0] == pack_key:
+        poses, pm, pv, pstep = cached[1], cached[2], cached[3], list(cached[4])
+    else:
+        poses = torch.stack([p.detach().to(dev, torch.float32).reshape(6) for p in pose_params]).contiguous()
+        pstep = [0] * len(kfs)
+        zero6 = None
+        m_rows, v_rows = [], []
+        for f in range(len(kfs)):
+            st = pose_st[f]
+            if st is None:
+                if zero6 is None:
+                    zero6 = torch.zeros(6, dtype=torch.float32, device=dev)
+                m_rows.append(zero6)
+                v_rows.append(zero6)
+                continue
+            m_rows.append(st["exp_avg"].to(dev, torch.float32).reshape(6))
+            v_rows.append(st["exp_avg_sq"].to(dev, torch.float32).reshape(6))
+            pstep[f] = int(st["step"].item())
+        pm = torch.stack(m_rows).contiguous()  # the poses' Adam moments [F, 6], one gather each
+        pv = torch.stack(v_rows).contiguous()
+    eng._pose_pack = None  # the packed copies change under the steps below
     if cur_ready is not None:
         main.wait_event(cur_ready)
     clk("poses")
@@ -604,6 +629,9 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             st["exp_avg"].copy_(pm[f].to(st["exp_avg"].device).reshape(st["exp_avg"].shape))
             st["exp_avg_sq"].copy_(pv[f].to(st["exp_avg_sq"].device).reshape(st["exp_avg_sq"].shape))
             st["step"].fill_(float(pstep[f]))
+    # the caller's tensors now equal the packed copies: the next call reuses
+    # them unless something writes the poses / their Adam state in between
+    eng._pose_pack = (_pose_pack_key(kfs, pose_params, pose_st, upd, dev), poses, pm, pv, tuple(pstep))
     clk("writeback")
     clk.report()
     return True

@@ -318,3 +318,39 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
             assert torch.equal(ga[n_emb:], gb[n_emb:]), mode  # decoder gradient: bit for bit
             torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-5, atol=1e-6 * float(ga[:n_emb].abs().max()))
             torch.testing.assert_close(pb, pa, rtol=0, atol=1e-5 * float(pa.abs().max()))
+
+
+def test_kernel_bound_region_timing():
+    """psvo_engine_set_timing: every region's time is the sum of its kernels'
+    own dispatch spans (hipExtLaunchKernel start / stop pairs) — positive for
+    the regions the step runs, 0 for one that launched nothing, the query
+    regions far below the decoder's, and the same results as an untimed run."""
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ro, rd = w.rays_o.to(DEV), w.rays_d.to(DEV)
+    rgb, depth = w.rgb.to(DEV), w.depth.to(DEV)
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    losses = []
+    for timed in (False, "overlap", True):
+        from copy import deepcopy
+        emb = emb0.clone().to(DEV)
+        ms = map_states(tree, emb, 0.2, device=DEV)
+        eng = MappingEngine(ms, deepcopy(dec), 0.2, 0.01, truncation=0.1, max_distance=10.0, criteria=crit,
+                            max_depth=10.0, lr_emb=5e-3, lr_dec=5e-3)
+        if timed:
+            eng.set_timing(timed)
+        out = [float(eng.step(ro, rd, rgb, depth, seed=300 + it)) for it in range(3)]
+        torch.cuda.synchronize()
+        losses.append(out)
+        if timed:
+            t = eng.timing()
+            for k in ("intersect", "sample", "interp_fwd", "mlp_fwd", "mlp_bwd"):
+                assert t[k] > 0.0 and np.isfinite(t[k]), (k, t)
+            assert t["intersect"] < t["mlp_fwd"] and t["sample"] < t["mlp_fwd"], t
+            assert t["mlp_fwd"] < 1e3 and t["mlp_bwd"] < 1e3, t  # ms per step: a sane span, not an event mix-up
+            eng.set_timing(False)
+        eng.close()
+    for other in losses[1:]:  # the first loss exactly; later ones up to the embedding scatter's atomic order
+        assert other[0] == losses[0][0]
+        np.testing.assert_allclose(other, losses[0], rtol=1e-4)
