@@ -638,6 +638,12 @@ int psvo_map_adam_ex(psvo_engine *e, void *stream, const psvo_map_desc *d, int64
  * left running on the engine's side stream (its weights are pending until
  * then; every engine call joins it itself). */
 int psvo_map_join(psvo_engine *e, void *stream);
+/* `stream` waits for the end of the last mapping step's decoder backward
+ * (its δ chain; a no-op before the first step).  The pipelined
+ * bundle_adjust_frames loop queues its next keyframe pixel draw behind it,
+ * so the draw runs beside the latency-bound look-ahead query instead of
+ * beside the persistent decoder kernels. */
+int psvo_map_side_wait(psvo_engine *e, void *stream);
 /* The last mapping step's per-ray loss gradients d rays_o / d rays_d (the
  * interpolation backward's ray sums, what the keyframe pose gradient is
  * formed from) into grad_o / grad_d f32[n_rays, 3], original ray order; rows

@@ -145,6 +145,7 @@ struct psvo_engine {
     // waits for adam_done first (render, before the interpolation)
     hipEvent_t adam_done = nullptr;
     hipEvent_t pf_fork = nullptr;  // the L2 warm-up for the look-ahead query forks from the backward here
+    bool bwd_recorded = false;     // dfeat_ready holds a step's decoder backward end (psvo_map_side_wait)
     float *pf_sink = nullptr;
     bool adam_pending = false;
     hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
@@ -1320,7 +1321,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // the look-ahead's pose step) — are queued here, in front of the render:
     // st reaches them right after the queued query's sampler, while the host
     // is still reading that query's statistics back, so they cost nothing.
-    const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_fuses_interp(d->width) &&
+    const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_split_tail(d->width) &&
                             !(flags & PSVO_STEP_NO_ADAM);
     // PSVO_LATE_WAITS=1 (A/B): both waits where their consumers are instead
     static const bool late_waits = getenv("PSVO_LATE_WAITS") && *getenv("PSVO_LATE_WAITS") == '1';
@@ -1463,7 +1464,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // weight-gradient slabs, steps the optimiser and builds the next decoder
     // images beside them (the next step's render waits for adam_done)
     const bool ahead = fr && fr->next_dirs_cam;
-    const bool split = fuse_ib && overlap && ahead && !(flags & PSVO_STEP_NO_ADAM);
+    const bool split = psvo::mlp_bwd_split_tail(d->width) && overlap && ahead && !(flags & PSVO_STEP_NO_ADAM);
     const bool emb_dirty = !(e->grads_clean && e->clean_buf == grad_emb);
     if (fuse_ib && emb_dirty && hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
@@ -1515,6 +1516,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                      G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr,
                      split ? ax : nullptr, ib_serial ? &ib_hook : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
+    if (overlap) e->bwd_recorded = true;  // mlp_bwd recorded dfeat_ready on st
     // PSVO_PREFETCH=1 (A/B, off by default): warm the XCD L2s with the
     // query's / the interpolation's read-only arrays (maps whose arrays fit)
     // while the per-ray sums and the pose step run.  Measured (config B, one
@@ -1617,6 +1619,14 @@ extern "C" int psvo_engine_grad_rays(psvo_engine *e, void *stream, int64_t n_ray
     if (hipMemcpyAsync(grad_o, g, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(grad_d, g + n_rays * 3, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine_grad_rays: copy failed");
+    return PSVO_OK;
+}
+
+extern "C" int psvo_map_side_wait(psvo_engine *e, void *stream) {
+    PSVO_REQUIRE(e, "map_side_wait: null engine");
+    if (!e->dfeat_ready || !e->bwd_recorded) return PSVO_OK;
+    if (hipStreamWaitEvent(as_stream(stream), e->dfeat_ready, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_side_wait: stream wait failed");
     return PSVO_OK;
 }
 

@@ -35,6 +35,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "interp_fuse.h"
 #include "psvo_common.h"
 
 namespace psvo {
@@ -518,11 +519,42 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
 }
 
 // ---- backward (data) --------------------------------------------------------
+// The fused interpolation backward of a wave's 16 samples (k_dec256_bwd's
+// tile tail): the embedding rows and the ray are gathered here, then dL/dx and
+// the scatter (interp_fuse.h).  Not inlined: inside the chain's loop the
+// compiler ran out of registers (the activations' 190 plus the gathers), and
+// at the tail of a tile nothing of the chain is live across the call.
+__device__ __attribute__((noinline)) void interp_tail(const InterpFuse ip, float *stg, int64_t m, int64_t s,
+                                                      bool valid, int n, int g, int lane, int64_t u, int lf, int row,
+                                                      float ts, float c0, float c1, float c2, int4 vid0, int4 vid1,
+                                                      float4 gf) {
+    const float cen[3] = {c0, c1, c2};
+    float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
+    float4 ev[8];
+    const int vid[8] = {vid0.x, vid0.y, vid0.z, vid0.w, vid1.x, vid1.y, vid1.z, vid1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ev[k] = reinterpret_cast<const float4 *>(ip.emb)[(int64_t)vid[k] * 4 + g];
+    if (valid) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            ro3[a] = ip.rays_o[(int64_t)row * 3 + a];
+            rd3[a] = ip.rays_d[(int64_t)row * 3 + a];
+        }
+    }
+    ifuse::interp_bwd_unit(ip, stg, m, s, valid, n, g, ts, ro3, rd3, cen, vid0, vid1, ev, gf);
+    if (ip.grad_emb != nullptr) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging is this wave's own
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ifuse::scatter_unit(ip, stg, u, m, lane, lf);
+    }
+}
+
 __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t n_tiles, const float *__restrict__ img,
                                                              const float *__restrict__ rgb,
                                                              const float *__restrict__ g_sdf,
                                                              const float *__restrict__ g_rgb, Act act, Dlt dl,
-                                                             float *__restrict__ dfeat) {
+                                                             float *__restrict__ dfeat, InterpFuse ip) {
     extern __shared__ __align__(16) float lds[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     (void)n_tiles;
@@ -531,6 +563,14 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
     Ring R{lds, img, 0, wave, lane, false};
     const int n = lane & 15, g = lane >> 4;
     const bool want_w = dl.d1 != nullptr;
+    // ip.gx set (the mapping engine, kNC = 1): the interpolation backward of
+    // the wave's 16 samples right after their dfeat (k_mlp_bwd3's scheme,
+    // interp_fuse.h) instead of a dfeat store and a k_interp_bwd launch
+    // beside the weight-gradient kernel; its sample data loads one
+    // dependent level per layer (leaf / ray / t, then the leaf's vertex rows
+    // and centre, then the embedding rows and the ray) under the chain's MFMAs
+    const bool fuse = kNC == 1 && ip.gx != nullptr;  // uniform
+    float *const stg = lds + kRing * kChunkFloats + wave * 512;
     auto plan = [](int c) { return bwd_chunk(c); };
     R.prime(plan);
     for (int64_t rd = 0; rd < P.rounds; ++rd) {
@@ -563,6 +603,15 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
                 }
             }
         }
+        const int64_t s0 = t16 * kTileW + n;  // this lane's sample (kNC = 1)
+        const bool fvalid = fuse && on && s0 < m;
+        int lf = 0, ro = 0;
+        float ts = 0.f;
+        if (fvalid) {
+            lf = ip.leaf[s0];
+            ro = ip.ray_of[s0];
+            ts = ip.t[s0];
+        }
         // δc1 = (W5ᵀ δ5) ⊙ m_c1
         f32x4 dc1[kNC][16];
         zero(dc1);
@@ -572,6 +621,16 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         f32x4 dfx[kNC][9];
         zero(dfx);
         layer_chunks<kBwdChunks, kBwdL4, 0, kN16>(R, dfx, dc1, plan, lane, on);
+        int4 vid0 = make_int4(0, 0, 0, 0), vid1 = make_int4(0, 0, 0, 0);
+        float cen[3] = {0.f, 0.f, 0.f};
+        int row = 0;
+        if (fvalid) {
+            vid0 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8);
+            vid1 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8 + 4);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
+            row = ip.rank_ray[ro];
+        }
         if (want_w && on) {
             store_tiles(dl.d4, t16, 256, dc1, lane);
             store_tiles(dl.d5, t16, 16, d5, lane);
@@ -597,10 +656,17 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
         // δx = W1ᵀ δh1 + the x rows of δ[f; x]
         gemm_chunk<1, 16, 0, 16>(dx, dh1, R.next<kBwdChunks>(kBwdL1, plan), lane, on);
         if (want_w && on) store_tiles(dl.d1, t16, 256, dh1, lane);
+        if (fuse) {
+            if (on) {  // dL/dx per sample (summed per ray by k_interp_rays_gx) and the embedding scatter
+                const float4 gf = make_float4(dx[0][0][0], dx[0][0][1], dx[0][0][2], dx[0][0][3]);
+                interp_tail(ip, stg, m, s0, fvalid, n, g, lane, t16, lf, row, ts, cen[0], cen[1], cen[2], vid0, vid1, gf);
+            }
+        } else {
 #pragma unroll
-        for (int c = 0; c < kNC; ++c) {
-            const int64_t s = (t16 + c) * kTileW + n;
-            if (on && s < m) *reinterpret_cast<f32x4 *>(dfeat + s * 16 + 4 * g) = dx[c][0];
+            for (int c = 0; c < kNC; ++c) {
+                const int64_t s = (t16 + c) * kTileW + n;
+                if (on && s < m) *reinterpret_cast<f32x4 *>(dfeat + s * 16 + 4 * g) = dx[c][0];
+            }
         }
     }
 }
@@ -986,7 +1052,9 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const BwdHook *before_dw) {
+               const BwdHook *before_dw, const InterpFuse *ip) {
+    PSVO_REQUIRE(ip == nullptr || (kNC == 1 && gw[0] != nullptr),
+                 "dec256_bwd: the fused interpolation backward needs the weight-gradient path (1 group per wave)");
     (void)feat;
     const int64_t n_tiles = (m + kChainTile - 1) / kChainTile;
     const int64_t n16 = dec256_tiles16(m);
@@ -1009,7 +1077,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
         ws += n16 * 16 * (256 + 256 + 144 + 256 + 16);
     }
     if (m > 0) {
-        const int lds = kRing * kChunkFloats * 4;
+        const int lds = (kRing * kChunkFloats + kCWaves * 512) * 4;  // ring + per-wave scatter staging
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dec256_bwd),
@@ -1017,7 +1085,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
             attr = true;
         }
         psvo::launch(k_dec256_bwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, images, rgb,
-                           g_sdf, g_rgb, a, d, dfeat);
+                           g_sdf, g_rgb, a, d, dfeat, ip ? *ip : InterpFuse{});
         const int rc = check_launch("dec256_bwd");
         if (rc) return rc;
     }

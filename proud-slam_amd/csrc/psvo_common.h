@@ -209,10 +209,13 @@ struct BwdHook {
     int (*fn)(void *ctx, hipStream_t st);
     void *ctx;
 };
+struct InterpFuse;
+// ip (the mapping engine's width-256 step): the interpolation backward runs
+// inside the δ-chain kernel (dfeat is then not stored), as at width 128
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const BwdHook *before_dw = nullptr);
+               const BwdHook *before_dw = nullptr, const InterpFuse *ip = nullptr);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
@@ -347,6 +350,10 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             hipStream_t reduce_stream = nullptr, const BwdHook *before_dw = nullptr);
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
+// the look-ahead's split tail (psvo_map_step_frames): the weight-gradient
+// slab sum and the optimiser on the side stream beside the next query — width
+// 128 only (the width-256 weight-gradient kernel holds every CU)
+bool mlp_bwd_split_tail(int width);
 
 // the decoder's LDS operand images (k_mlp_prep) on their own, and
 // psvo_mlp_fwd without rebuilding them (the engine prepares them on its aux

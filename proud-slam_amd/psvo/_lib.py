@@ -87,6 +87,7 @@ _SIGNATURES = {
     "psvo_map_adam": (_i32, [_vp, _vp, _vp, _i64]),
     "psvo_map_adam_ex": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "psvo_map_join": (_i32, [_vp, _vp]),
+    "psvo_map_side_wait": (_i32, [_vp, _vp]),
     "psvo_engine_grad_rays": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "psvo_map_query": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _u64]),
     "psvo_map_step_frames": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),

@@ -175,6 +175,11 @@ class MappingEngine:
         if lr_dec is not None:
             self.desc.lr_dec = float(lr_dec)
 
+    def side_wait(self, stream):
+        """`stream` (a torch stream) waits for the end of the last step's
+        decoder backward (psvo_map_side_wait; a no-op before the first)."""
+        L.call("psvo_map_side_wait", self.handle, ctypes.c_void_p(stream.cuda_stream))
+
     def step_frames(self, dirs_cam, rays_per_frame, poses, pose_m, pose_v, pose_steps, lr_pose, rgb, depth, seed,
                     noise=None, adam_step=None, apply_adam=True, pose_grad=None, next_dirs_cam=None, next_seed=0,
                     next_stream=None, want_loss=True, next_depth=None):

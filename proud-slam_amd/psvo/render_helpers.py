@@ -546,9 +546,17 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     if side is not None:
         side.wait_stream(main)  # the keyframes as the caller left them
 
+    # each next draw waits for the previous step's decoder backward on the
+    # engine's stream: it then runs beside the latency-bound look-ahead query
+    # rather than beside the persistent decoder kernels it slowed
+    # (PSVO_DRAW_AFTER_BWD=0: as soon as queued, A/B)
+    draw_after_bwd = os.environ.get("PSVO_DRAW_AFTER_BWD", "1") != "0"
+
     def draw_ahead(it):
         if side is None:
             return draw(it), None
+        if draw_after_bwd and it > 0:
+            eng.side_wait(side)
         with torch.cuda.stream(side):
             out = draw(it)
         for t in out[:3]:
