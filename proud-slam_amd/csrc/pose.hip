@@ -103,6 +103,43 @@ __device__ void pose_chain(const float *__restrict__ pose, const float (&tot)[12
 
 // Σ over the hit rays of ray range [ray_lo, ray_hi) (hit ranks keep ray order,
 // so they are one contiguous run of rank_ray) → pose gradient; block = frame
+// Σ over the frame's hit rays [lo, hi) (rank order, thread t: ranks t,
+// t + kGradThreads, …) of d rays_o and of d rays_d ⊗ dir: the rank → ray
+// reads of up to kPoseBatch ranks issued together, then their gradient rows,
+// then the sums in rank order — the same additions as one rank at a time,
+// without a dependent pair of memory round trips per rank
+constexpr int kPoseBatch = 8;
+__device__ __forceinline__ void frame_ray_sums(int64_t r_hit, const int *__restrict__ rank_ray, int64_t lo, int64_t hi,
+                                               const float *__restrict__ dirs, const float *__restrict__ g_o,
+                                               const float *__restrict__ g_d, float (&acc)[12]) {
+    for (int64_t r0 = threadIdx.x; r0 < r_hit; r0 += (int64_t)kGradThreads * kPoseBatch) {
+        int64_t row[kPoseBatch];
+#pragma unroll
+        for (int k = 0; k < kPoseBatch; ++k) {
+            const int64_t r = r0 + (int64_t)k * kGradThreads;
+            row[k] = r < r_hit ? rank_ray[r] : -1;
+        }
+        float go[kPoseBatch][3], gd[kPoseBatch][3], dir[kPoseBatch][3];
+#pragma unroll
+        for (int k = 0; k < kPoseBatch; ++k) {
+            const bool in = row[k] >= lo && row[k] < hi;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                go[k][j] = in ? g_o[row[k] * 3 + j] : 0.f;
+                gd[k][j] = in ? g_d[row[k] * 3 + j] : 0.f;
+                dir[k][j] = in ? dirs[row[k] * 3 + j] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPoseBatch; ++k) {
+            if (!(row[k] >= lo && row[k] < hi)) continue;
+            for (int j = 0; j < 3; ++j) acc[j] += go[k][j];
+            for (int j = 0; j < 3; ++j)
+                for (int i = 0; i < 3; ++i) acc[3 + j * 3 + i] += gd[k][j] * dir[k][i];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kGradThreads) void k_pose_grad_frames(int64_t r_hit, const int *__restrict__ rank_ray,
                                                                    int64_t rpf, const float *__restrict__ dirs,
                                                                    const float *__restrict__ g_o,
@@ -112,18 +149,7 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_grad_frames(int64_t r_hit
     __shared__ float part[kGradThreads / 64][12];
     const int64_t lo = blockIdx.x * rpf, hi = lo + rpf;
     float acc[12] = {};
-    for (int64_t r = threadIdx.x; r < r_hit; r += kGradThreads) {
-        const int64_t row = rank_ray[r];
-        if (row < lo || row >= hi) continue;
-        float dir[3], gd[3];
-        for (int j = 0; j < 3; ++j) {
-            acc[j] += g_o[row * 3 + j];
-            gd[j] = g_d[row * 3 + j];
-            dir[j] = dirs[row * 3 + j];
-        }
-        for (int j = 0; j < 3; ++j)
-            for (int k = 0; k < 3; ++k) acc[3 + j * 3 + k] += gd[j] * dir[k];
-    }
+    frame_ray_sums(r_hit, rank_ray, lo, hi, dirs, g_o, g_d, acc);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int i = 0; i < 12; ++i) {
         float v = acc[i];
@@ -158,18 +184,7 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     const int f = blockIdx.x;
     const int64_t lo = f * rpf, hi = lo + rpf;
     float acc[12] = {};
-    for (int64_t r = threadIdx.x; r < r_hit; r += kGradThreads) {
-        const int64_t row = rank_ray[r];
-        if (row < lo || row >= hi) continue;
-        float dir[3], gd[3];
-        for (int j = 0; j < 3; ++j) {
-            acc[j] += g_o[row * 3 + j];
-            gd[j] = g_d[row * 3 + j];
-            dir[j] = dirs[row * 3 + j];
-        }
-        for (int j = 0; j < 3; ++j)
-            for (int k = 0; k < 3; ++k) acc[3 + j * 3 + k] += gd[j] * dir[k];
-    }
+    frame_ray_sums(r_hit, rank_ray, lo, hi, dirs, g_o, g_d, acc);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int i = 0; i < 12; ++i) {
         float v = acc[i];
