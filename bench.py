@@ -42,7 +42,8 @@ MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (v_mfma_f32_32x
 TIMING_NOTE = ("headline mode, inside bundle_adjust_frames iterations: every kernel of a region timed by a HIP "
                "event pair bound to its own dispatch (hipExtLaunchKernel start / stop: the span rocprofv3 "
                "--kernel-trace reports, on the stream it runs on); a region = the sum of its kernels' spans "
-               "(PSVO_TIMING_MARKERS=1: marker events around the region instead)")
+               "(PSVO_TIMING_SPAN=1: first kernel's start to last kernel's end; PSVO_TIMING_MARKERS=1: marker "
+               "events around the region)")
 
 
 def log(msg):

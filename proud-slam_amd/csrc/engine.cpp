@@ -206,26 +206,56 @@ void timer_collect(psvo_engine *e, bool block = false) {
     EngineTimer &t = e->tm;
     if (!t.markers) {  // kernel-bound
         psvo::KernelClock &c = t.kc;
-        int w = 0;
-        for (int i = 0; i < c.n; ++i) {
-            const hipError_t q = block ? hipEventSynchronize(c.ev[i][1]) : hipEventQuery(c.ev[i][1]);
-            if (q == hipErrorNotReady) {
-                if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // not an error
-                if (w != i) {
-                    std::swap(c.ev[w][0], c.ev[i][0]);
-                    std::swap(c.ev[w][1], c.ev[i][1]);
-                    c.region[w] = c.region[i];
+        auto ready = [&](hipEvent_t ev) {
+            const hipError_t q = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
+            if (q == hipErrorNotReady && hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // not an error
+            return q;
+        };
+        if (c.sum) {
+            int w = 0;
+            for (int i = 0; i < c.n; ++i) {
+                const hipError_t q = ready(c.ev[i][1]);
+                if (q == hipErrorNotReady) {
+                    if (w != i) {
+                        std::swap(c.ev[w][0], c.ev[i][0]);
+                        std::swap(c.ev[w][1], c.ev[i][1]);
+                        c.region[w] = c.region[i];
+                    }
+                    ++w;
+                    continue;
                 }
-                ++w;
-                continue;
+                float ms = 0.f;
+                if (q == hipSuccess && hipEventElapsedTime(&ms, c.ev[i][0], c.ev[i][1]) == hipSuccess)
+                    t.kms[c.region[i]] += ms;
+                else
+                    (void)hipGetLastError();  // not the next launch's error
             }
-            float ms = 0.f;
-            if (q == hipSuccess && hipEventElapsedTime(&ms, c.ev[i][0], c.ev[i][1]) == hipSuccess)
-                t.kms[c.region[i]] += ms;
-            else
-                (void)hipGetLastError();  // not the next launch's error
+            c.n = w;
+        } else {
+            // closed instances in queue order; an unfinished one ends this pass
+            // (its pairs and the later ones' stay until a later collection)
+            int done = 0;
+            for (; done < c.n_inst; ++done) {
+                const psvo::KernelClock::Inst &I = c.inst[done];
+                bool open = false;
+                for (int d = 0; d < c.depth; ++d) open |= c.stack[d] == done;
+                if (open) break;
+                if (I.first < 0) continue;  // no kernel: the region's instance counts 0
+                const hipError_t q = ready(c.ev[I.last][1]);
+                if (q == hipErrorNotReady) break;
+                float ms = 0.f;
+                if (q == hipSuccess && hipEventElapsedTime(&ms, c.ev[I.first][0], c.ev[I.last][1]) == hipSuccess)
+                    t.kms[I.region] += ms;
+                else
+                    (void)hipGetLastError();
+            }
+            if (done > 0) {  // drop the collected instances (the open ones keep their stack slots)
+                for (int k = done; k < c.n_inst; ++k) c.inst[k - done] = c.inst[k];
+                c.n_inst -= done;
+                for (int d = 0; d < c.depth; ++d) c.stack[d] -= done;
+            }
+            if (c.n_inst == 0) c.n = 0;  // every pair read: the slots start over
         }
-        c.n = w;
         t.pending = false;
         return;
     }
@@ -254,10 +284,22 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
     }
     psvo::KernelClock &c = t.kc;
     if (!end) {
-        if (c.n + 32 > psvo::KernelClock::kMax) timer_collect(e, true);  // room for the region's kernels
-        if (c.depth < 8) c.stack[c.depth++] = region;
+        if (c.n + 32 > psvo::KernelClock::kMax || c.n_inst + 2 > psvo::KernelClock::kMaxInst)
+            timer_collect(e, true);  // room for the region's kernels
         t.starts[region] += 1;
         psvo::g_kclock = &c;
+        if (c.depth >= 8) {
+            c.overflow = true;
+            return;
+        }
+        if (c.sum) {
+            c.stack[c.depth++] = region;
+        } else if (c.n_inst < psvo::KernelClock::kMaxInst) {
+            c.inst[c.n_inst] = psvo::KernelClock::Inst{region, -1, -1};
+            c.stack[c.depth++] = c.n_inst++;
+        } else {
+            c.overflow = true;
+        }
     } else if (c.depth > 0) {
         c.depth--;
     }
@@ -446,6 +488,10 @@ extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
     t.on = on != 0;
     t.overlap = on == 2;
     t.markers = mk && *mk == '1';
+    const char *ks = getenv("PSVO_TIMING_SPAN");
+    t.kc.sum = !(ks && *ks == '1');
+    t.kc.n = 0;
+    t.kc.n_inst = 0;
     for (int r = 0; r < PSVO_TIME_REGIONS; ++r) {
         t.ms[r] = 0.0;
         t.n[r] = 0;

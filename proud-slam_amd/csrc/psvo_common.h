@@ -10,20 +10,28 @@
 namespace psvo {
 
 // Kernel-bound timing (the engine's timed regions, psvo_engine_set_timing):
-// while a region is armed every kernel launched through psvo::launch takes a
-// (start, stop) event pair bound to its own dispatch (hipExtLaunchKernel), so
-// a region's time is the sum of its kernels' execution spans — what a
-// rocprofv3 kernel trace reports — with no marker packets between the
-// kernels.  One host thread queues a timed step; regions may nest (the
-// innermost armed region owns a launch).
+// while a region is armed every kernel launched through psvo::launch gets
+// events bound to its own dispatch (hipExtLaunchKernel) — no marker packets
+// between the kernels.  Default: every kernel gets a (start, stop) pair and
+// a region is the sum of its kernels' spans (what rocprofv3's kernel trace
+// reports for them); PSVO_TIMING_SPAN=1: an instance of a region is timed
+// from its first kernel's start to its last kernel's end (only the first
+// kernel carries a start event; the gaps between the kernels count).  One
+// host thread queues a timed step; regions nest (the innermost open instance
+// owns a launch).
 struct KernelClock {
-    static constexpr int kMax = 192;
+    static constexpr int kMax = 192, kMaxInst = 64;
     hipEvent_t ev[kMax][2] = {};
-    int region[kMax] = {};
-    int n = 0;                   // pairs taken since the last collection
-    int stack[8] = {};           // armed regions, innermost last
+    int region[kMax] = {};        // sum mode: the pair's region
+    int n = 0;                    // pairs taken since the last full collection
+    struct Inst {
+        int region, first, last;  // pair indices (−1: no kernel yet)
+    } inst[kMaxInst] = {};
+    int n_inst = 0;
+    int stack[8] = {};            // open instances (span mode) / regions (sum mode), innermost last
     int depth = 0;
-    bool overflow = false;       // more launches than pairs: the surplus ran untimed
+    bool sum = false;
+    bool overflow = false;        // more launches / instances than slots: the surplus ran untimed
 };
 extern KernelClock *g_kclock;  // engine.cpp: set while an engine with timing on queues a step
 
@@ -34,16 +42,24 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hip
     if (c && c->depth > 0) {
         if (c->n < KernelClock::kMax) {
             const int i = c->n++;
-            c->region[i] = c->stack[c->depth - 1];
-            e0 = c->ev[i][0];
             e1 = c->ev[i][1];
+            if (c->sum) {
+                c->region[i] = c->stack[c->depth - 1];
+                e0 = c->ev[i][0];
+            } else {
+                KernelClock::Inst &I = c->inst[c->stack[c->depth - 1]];
+                if (I.first < 0) {
+                    I.first = i;
+                    e0 = c->ev[i][0];
+                }
+                I.last = i;
+            }
         } else {
             c->overflow = true;
         }
     }
     hipExtLaunchKernelGGL(k, grid, block, lds, st, e0, e1, 0u, static_cast<KArgs>(a)...);
 }
-
 
 // Set the thread-local error message; returns `code` for tail calls.
 int set_error(int code, const char *fmt, ...);

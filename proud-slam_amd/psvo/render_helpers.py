@@ -546,11 +546,13 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     if side is not None:
         side.wait_stream(main)  # the keyframes as the caller left them
 
-    # each next draw waits for the previous step's decoder backward on the
-    # engine's stream: it then runs beside the latency-bound look-ahead query
-    # rather than beside the persistent decoder kernels it slowed
-    # (PSVO_DRAW_AFTER_BWD=0: as soon as queued, A/B)
-    draw_after_bwd = os.environ.get("PSVO_DRAW_AFTER_BWD", "1") != "0"
+    # PSVO_DRAW_AFTER_BWD=1 (A/B, off): each next draw waits for the previous
+    # step's decoder backward (psvo_map_side_wait), so it runs beside the
+    # look-ahead query instead of beside the persistent decoder kernels.
+    # Measured (config B, three interleaved pairs, one box): 1.000-1.059 vs
+    # 0.985-1.000 ms per iteration as soon as queued (C: 3.711 vs 3.693 ms) —
+    # the decoder kernels gain less than the latency-bound query loses
+    draw_after_bwd = os.environ.get("PSVO_DRAW_AFTER_BWD", "0") == "1"
 
     def draw_ahead(it):
         if side is None:
