@@ -649,12 +649,16 @@ def main():
         return r
 
     env = os.environ.get
-    if env("PSVO_QUERY_TAILS") == "1" and world == 1:
-        q_desc = ("k_intersect_sorted with the statistics / hit-rank pass in its last workgroup, k_sample_fused "
-                  "with the sample scan and read-back in its last workgroup")
-    else:
-        q_desc = "k_intersect_sorted+k_ray_stats_rank, k_sample_fused+k_scan_samples"
-    if env("PSVO_FUSED_POINTS") == "1":
+    lb = env("PSVO_QUERY_SPLIT") != "1" and rays_step <= 16384  # the look-back query (svo_query.hip / lookback.h)
+    lb_smp = lb and world == 1 and env("PSVO_LB_SAMPLER") != "0"
+    lb_compact = lb_smp and env("PSVO_LB_COMPACT") != "0"
+    q_desc = ("k_intersect_sorted (hit ranks / statistics by in-launch look-back)" if lb
+              else "k_intersect_sorted+k_ray_stats_rank")
+    q_desc += (", k_sample_fused (sample scan, read-back" + (" and compaction" if lb_compact else "") +
+               " by in-launch look-back)" if lb_smp else ", k_sample_fused+k_scan_samples")
+    if lb_compact and env("PSVO_FUSED_POINTS") != "1" and env("PSVO_PADDED_Z") != "1" and env("PSVO_DEV_SIZED") != "1":
+        i_desc = "k_interp_fwd"
+    elif env("PSVO_FUSED_POINTS") == "1":
         i_desc = "k_points_interp = compaction + interp fwd"
     elif world > 1 or env("PSVO_PADDED_Z") == "1":
         i_desc = "k_sample_points, k_interp_fwd"

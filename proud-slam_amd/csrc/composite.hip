@@ -237,7 +237,11 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const float d = gt_depth[orig];
     const float gt0 = gt_rgb[orig * 3 + 0], gt1 = gt_rgb[orig * 3 + 1], gt2 = gt_rgb[orig * 3 + 2];
     const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
-    const float *z = z_vals + r * z_stride;  // the sampler row ([R, cap]) or the padded [R_hit, S_max] row
+    // the sampler row ([R, cap]: past its ns valid samples the padding
+    // MAX_DEPTH is implied, the look-back sampler does not write it) or the
+    // padded [R_hit, S_max] row
+    const float *z = z_vals + r * z_stride;
+    auto z_at = [&](int s) { return s < ns ? z[s] : kMaxDepthFill; };
     auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
     constexpr int JR = J > 0 ? J : 1;
     float zr[JR], pr[JR], c0r[JR], c1r[JR], c2r[JR];
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const int s = lane + 64 * j;
-            zr[j] = s < s_max ? z[s] : 0.f;
+            zr[j] = s < s_max ? z_at(s) : 0.f;
             pr[j] = sdf_at(s);
             const bool v = s < ns;
             const float *c = rgb_s + (int64_t)(off + (v ? s : 0)) * 3;
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         }
     }
     auto Z = [&](int j, int s) {
-        if constexpr (J > 0) return zr[j]; else return z[s];
+        if constexpr (J > 0) return zr[j]; else return z_at(s);
     };
     auto P = [&](int j, int s) {
         if constexpr (J > 0) return pr[j]; else return sdf_at(s);
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         if (s + 1 < s_max && v1 * v < 0.0f) first = min(first, s);
     }
     first = wmin(first);
-    const float zmin = z[first == s_max ? 0 : first];
+    const float zmin = z_at(first == s_max ? 0 : first);
     // σ(a), σ(−a) per sample (registers when J > 0: computed once, the same
     // bits as recomputing them in each pass)
     float spr[JR], snr[JR], wr[JR];

@@ -223,15 +223,18 @@ __global__ __launch_bounds__(256) void k_crit_counts(int64_t r_hit, int s_max, f
                                                      const int *__restrict__ rank_ray,
                                                      const float *__restrict__ gt_depth,
                                                      const float *__restrict__ z_vals, int z_stride,
-                                                     float *__restrict__ part) {
+                                                     const int *__restrict__ ray_ns, float *__restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const float d = gt_depth[rank_ray[r]];
     const float *z = z_vals + r * z_stride;
+    // ray_ns (sampler rows): past the ray's valid samples the padding
+    // MAX_DEPTH is implied (the look-back sampler does not write it)
+    const int n_in = ray_ns ? ray_ns[r] : s_max;
     float nf = 0.f, ns = 0.f;
     for (int s = lane; s < s_max; s += 64) {
-        const SampleTerms t = sample_terms(z[s], 1.0f, d, tr, max_depth);
+        const SampleTerms t = sample_terms(s < n_in ? z[s] : kMaxDepthFill, 1.0f, d, tr, max_depth);
         nf += t.f;
         ns += t.sm;
     }
@@ -358,17 +361,17 @@ extern "C" int psvo_criterion_coef(void *stream, int64_t r_hit, int s_max, float
     PSVO_REQUIRE(r_hit > 0 && s_max > 0, "criterion_coef: bad sizes");
     PSVO_REQUIRE(rank_ray && gt_depth && z_vals && workspace && sums && coef, "criterion_coef: null pointer");
     return psvo::criterion_coef_z(stream, r_hit, s_max, truncation, max_depth, rank_ray, gt_depth, z_vals, s_max,
-                                  rgb_w, depth_w, fs_w, sdf_w, flags, workspace, sums, coef);
+                                  nullptr, rgb_w, depth_w, fs_w, sdf_w, flags, workspace, sums, coef);
 }
 
 int psvo::criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
-                           const int *rank_ray, const float *gt_depth, const float *z_vals, int z_stride, float rgb_w,
-                           float depth_w, float fs_w, float sdf_w, int flags, float *workspace, double *sums,
-                           float *coef) {
+                           const int *rank_ray, const float *gt_depth, const float *z_vals, int z_stride,
+                           const int *ray_ns, float rgb_w, float depth_w, float fs_w, float sdf_w, int flags,
+                           float *workspace, double *sums, float *coef) {
     PSVO_REQUIRE(z_stride >= s_max, "criterion_coef: z stride %d < S_max %d", z_stride, s_max);
     hipStream_t st = as_stream(stream);
     psvo::launch(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation, max_depth,
-                       rank_ray, gt_depth, z_vals, z_stride, workspace);
+                       rank_ray, gt_depth, z_vals, z_stride, ray_ns, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     psvo::launch(k_crit_coef, dim3(1), dim3(64), 0, st, sums, (double)r_hit, (double)s_max, rgb_w, depth_w,
@@ -383,7 +386,7 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
                      const float *gt_depth, const float *z_vals, float *workspace, double *sums) {
     if (r_hit > 0)
         psvo::launch(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
-                           max_depth, rank_ray, gt_depth, z_vals, s_max, workspace);
+                           max_depth, rank_ray, gt_depth, z_vals, s_max, nullptr, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");

@@ -26,7 +26,7 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kStatsKeep, kBlkOut, kRayCnt, kCoefQ, kQSlots };
+             kOffsets, kStatsKeep, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -51,6 +51,8 @@ struct QuerySet {
     int seq = 0;                  // the flag value the current statistics carry
     hipStream_t qstream = nullptr;  // the stream the query was queued on
     const int *stats_zeroed = nullptr;  // the device statistics buffer a completed read-back left zeroed
+    const void *lb_zeroed = nullptr;    // the look-back descriptor buffer, zeroed once at allocation (tags ≠ 0)
+    bool compacted = false;             // the sampler compacted the samples (slots kLeafQ / kTQ / kRayOfQ)
     hipEvent_t done = nullptr;    // statistics landed (after the sampler)
     bool done_recorded = false;   // a query consumed on its own stream skips it (one packet less there)
     hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
@@ -126,6 +128,7 @@ struct psvo_engine {
     psvo::Arena a;
     psvo::QuerySet qs[2];           // FIFO of queries: head = the next step's
     int q_head = 0, q_count = 0;
+    uint32_t lb_tag = 0;            // the last look-back descriptor tag handed out (lookback.h)
     hipStream_t side = nullptr;     // psvo_map_query's stream
     hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
     // the embedding backward runs on `aux` beside the decoder's weight
@@ -745,10 +748,26 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     Q_BUF(int, rank_ray, kRankRay, R * sizeof(int));
     mark(e, st, PSVO_TIME_INTERSECT, 0);
     Q_BUF(int, blk_out, kBlkOut, (size_t)(R + 3) / 4 * 2 * sizeof(int));  // per intersect block: tests, rounds
+    const EngineExchange &x = e->x;
+    // the statistics / rank pass and the sample scan inside the traversal and
+    // sampler launches (decoupled look-back; the sampler's only on one GPU)
+    unsigned long long *lb = nullptr;
+    uint32_t tag = 0;
+    if (psvo::query_lookback(R)) {
+        const size_t lb_bytes = (size_t)psvo::lookback_granules(R) * sizeof(unsigned long long);
+        lb = reinterpret_cast<unsigned long long *>(arena_buf(q.a, st, kLbDesc, lb_bytes, &rc));
+        if (!lb) return rc;
+        if (q.lb_zeroed != lb) {  // fresh memory: no stale granule may carry a future tag
+            if (hipMemsetAsync(lb, 0, q.a.cap[kLbDesc], st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
+            q.lb_zeroed = lb;
+        }
+        e->lb_tag = e->lb_tag == 0xffffffffu ? 1u : e->lb_tag + 1u;
+        tag = e->lb_tag;
+    }
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
-                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out));
-    const EngineExchange &x = e->x;
+                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out, lb, tag));
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced
         ENG_CALL(dist_pack(st, stats, rank_ray, hit_idx, x.xi32 + x.in_off()));
@@ -782,9 +801,10 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     }
     q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
     q.counts_gt = nullptr;
+    q.compacted = false;
     if (!x.on()) {  // the sampler's scan does the read-back (and, given the GT depths, the loss normalisers)
         psvo::SampleCounts sc{};
-        const bool counts = counts_gt && psvo::sampler_counts(R);
+        const bool counts = counts_gt != nullptr;
         if (counts) {
             Q_BUF(int, ray_cnt, kRayCnt, (size_t)R * sizeof(int));
             Q_BUF(float, coefq, kCoefQ, 4 * sizeof(float));
@@ -793,9 +813,23 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                                     PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF};
             q.counts_gt = counts_gt;
         }
+        // look-back sampler: the ray-major compaction in the same launch
+        // (capacity R · max_steps: every row fits; PSVO_LB_COMPACT=0: k_compact_rays after the read-back)
+        unsigned long long *lbs = psvo::sampler_lookback() ? lb : nullptr;
+        int *leaf_q = nullptr, *ray_of_q = nullptr;
+        float *t_q = nullptr;
+        if (lbs && psvo::sampler_compacts()) {
+            const size_t cap = (size_t)R * max_steps;
+            Q_BUF(int, lq_, kLeafQ, cap * sizeof(int));
+            Q_BUF(float, tq_, kTQ, cap * sizeof(float));
+            Q_BUF(int, rq_, kRayOfQ, cap * sizeof(int));
+            leaf_q = lq_, t_q = tq_, ray_of_q = rq_;
+        }
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
-                                           q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr));
+                                           q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr, lbs, tag, leaf_q,
+                                           t_q, ray_of_q));
+        q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
     if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_raw, PSVO_STAT_WORDS, q.seq));
@@ -1056,6 +1090,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     const int *hs = qset.host_stats;
     // data-parallel: this rank's hit rays, padded to the union's S_max
     const int r_hit = dist ? hs[PSVO_STAT_R_HIT_LOCAL] : hs[PSVO_STAT_R_HIT];
+    if (hs[PSVO_STAT_FLAGS] & 8) return set_error(PSVO_E_LAUNCH, "%s: query look-back wait abandoned", who);
     if (hs[PSVO_STAT_FLAGS] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
     if (hs[PSVO_STAT_FLAGS] & 4) return set_error(PSVO_E_OVERFLOW, "%s: union batch exceeds max_rays_global", who);
     if (hs[PSVO_STAT_R_HIT] == 0)
@@ -1094,6 +1129,11 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         // 0.96-0.99 vs 0.94-0.96 ms per iteration, so the split stays default.
         o.z_stride = 0;  // a device-sized attempt that did not fit: host-sized below
         o.z_recorded = false;
+        if (rays_path && qset.compacted) {  // the sampler compacted in its launch (look-back offsets)
+            leaf_b = static_cast<int *>(qset.a.p[kLeafQ]);
+            tt_b = static_cast<float *>(qset.a.p[kTQ]);
+            ray_of_b = static_cast<int *>(qset.a.p[kRayOfQ]);
+        }
         if (rays_path) {
             // the loss normalisers need only z: aux may start them now (a
             // marker packet on st: none when aux has nothing to wait for)
@@ -1102,7 +1142,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
                     return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
                 o.z_recorded = true;
             }
-            if (!interp_rays) {
+            if (!interp_rays && !qset.compacted) {
                 mark(e, st, PSVO_TIME_POINTS, 0);
                 ENG_CALL(psvo::compact_rays(st, r_hit, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b,
                                             psvo::DevBatch{}));
@@ -1433,8 +1473,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                                           d->w_sdf, crit_flags, coef));
     } else if (!coef_q) {
         ENG_CALL(psvo::criterion_coef_z(ax, r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
-                                        q.z_vals, q.z_stride, d->w_rgb, d->w_depth, d->w_fs, d->w_sdf, crit_flags,
-                                        crit_ws, sums_c, coef));
+                                        q.z_vals, q.z_stride, q.ray_ns, d->w_rgb,
+                                        d->w_depth, d->w_fs, d->w_sdf, crit_flags, crit_ws, sums_c, coef));
     }
     if (!coef_q) ENG_CALL(fork_join(ax, st, e->coef_ready));
     // after the normalisers: the fused loss pass waits for them, Adam for the marks

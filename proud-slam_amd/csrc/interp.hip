@@ -167,9 +167,12 @@ __global__ __launch_bounds__(256) void k_points_interp(int64_t r_hit, int s_max,
     const int q = g & 3;
     if (s >= s_max) return;
     for (int64_t r = blockIdx.y; r < r_hit; r += gridDim.y) {
-        const int v = s_idx[r * cap + s];
-        const float z = s_depth[r * cap + s];
-        const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
+        // valid samples form a prefix of each row; past it the padding
+        // (-1, MAX_DEPTH) is implied — the look-back sampler does not write it
+        const bool in = s < offsets[r + 1] - offsets[r];
+        const int v = in ? s_idx[r * cap + s] : -1;
+        const float z = in ? s_depth[r * cap + s] : kMaxDepthFill;
+        const int64_t o = offsets[r] + s;
         if (q == 0) {
             const int64_t e = r * s_max + s;
             z_vals[e] = z;

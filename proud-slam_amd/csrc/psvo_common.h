@@ -118,15 +118,27 @@ struct SampleCounts {
     int crit_flags;
 };
 // psvo_sample_rays (single GPU, whole batch) whose scan also does
-// stats_to_host's read-back (svo_query.hip); with counts (and at most
-// 256 · kTailPasses rays, the in-launch tail) also the normalisers
+// stats_to_host's read-back (svo_query.hip); with counts also the
+// normalisers.  lb_desc (query_lookback): the scan runs inside the sampler
+// launch by look-back (lookback.h) over the descriptors after the
+// traversal's (lookback_granules(r_hit_cap) granules, tag ≠ 0 fresh per
+// query), the rows hold only their valid prefix, and with leaf / t / ray_of
+// (capacity r_hit_cap · max_steps_cap) the launch also does k_compact_rays'
+// compaction
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                         int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep = nullptr,
-                        const SampleCounts *counts = nullptr);
-// whether sample_rays_to_host computes the counts for a batch of r rays (its in-launch tail)
-bool sampler_counts(int64_t r);
+                        const SampleCounts *counts = nullptr, unsigned long long *lb_desc = nullptr,
+                        uint32_t lb_tag = 0, int *leaf = nullptr, float *t = nullptr, int *ray_of = nullptr);
+// whether a query of r rays runs its statistics / rank pass and its sample
+// scan by look-back (PSVO_QUERY_SPLIT=1: never), and its descriptor granules
+constexpr int64_t kLbMaxRays = 16384;  // 4 rays per workgroup, <= 64 · 64 workgroups (lookback.h)
+constexpr int kLbIsGranules = 5, kLbSmpGranules = 8;
+bool query_lookback(int64_t r);
+bool sampler_lookback();  // PSVO_LB_SAMPLER=0: the traversal's look-back only
+bool sampler_compacts();  // PSVO_LB_COMPACT=0: the look-back sampler without the compaction
+int64_t lookback_granules(int64_t r);
 
 // one element of the Adam step (k_adam; optim.hip's formulation), shared so
 // the fused pose step (pose.hip) computes the same bits
@@ -154,7 +166,8 @@ int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr);
+                     int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr,
+                     unsigned long long *lb_desc = nullptr, uint32_t lb_tag = 0);
 
 // data-parallel query (svo_query.hip): rows of the exchanged slot-0 table for
 // a union batch of at most max_rays_global rays; pack this rank's 8 words;
@@ -181,10 +194,11 @@ int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, 
 struct DevBatch;
 // psvo_criterion_coef / psvo_composite_loss reading z from rows of stride
 // z_stride >= s_max (the sampler's [R, cap] depth rows, the engine's mapping
-// path: no padded [R_hit, S_max] copy)
+// path: no padded [R_hit, S_max] copy; ray_ns: the rows' valid samples, past
+// which MAX_DEPTH is implied — the look-back sampler writes no padding)
 int criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
-                     const float *gt_depth, const float *z_vals, int z_stride, float rgb_w, float depth_w, float fs_w,
-                     float sdf_w, int flags, float *workspace, double *sums, float *coef);
+                     const float *gt_depth, const float *z_vals, int z_stride, const int *ray_ns, float rgb_w,
+                     float depth_w, float fs_w, float sdf_w, int flags, float *workspace, double *sums, float *coef);
 int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
                      const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
                      const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
@@ -235,13 +249,12 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
-// ---- in-launch hand-off to the last-arriving workgroup ---------------------
-// (cdna_hip_programming.md §5 "in-launch split-K reduction", sc1 form; the
-// per-XCD L2s are not coherent).  Every word another workgroup reads in the
-// same launch is stored write-through (sc1: a relaxed agent-scope atomic store
-// on a global pointer) and read back with sc1 loads, so no release / acquire
-// fence (an L2 write-back / invalidate) is needed; each storing wave drains
-// its stores before the workgroup takes its ticket.
+// ---- in-launch hand-offs between workgroups --------------------------------
+// (cdna_hip_programming.md §6 G16, sc1 form; the per-XCD L2s are not
+// coherent).  Every word another workgroup reads in the same launch is stored
+// write-through (sc1: a relaxed agent-scope atomic store on a global pointer)
+// and read back with sc1 loads, so no release / acquire fence (an L2
+// write-back / invalidate) is needed (lookback.h's descriptors).
 typedef __attribute__((address_space(1))) int g_i32;
 typedef __attribute__((address_space(1))) float g_f32;
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
@@ -256,22 +269,6 @@ __device__ __forceinline__ int ld_wt(const int *p) {
 }
 __device__ __forceinline__ float ld_wt(const float *p) {
     return __hip_atomic_load((g_f32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// true in the last workgroup of the launch to arrive (block-uniform); that
-// workgroup re-zeroes the counter for the next launch (zero before the first)
-__device__ __forceinline__ bool last_block(int *counter, int *lds_word) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int n = (int)(gridDim.x * gridDim.y * gridDim.z);
-        const int t = __hip_atomic_fetch_add((g_i32 *)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *lds_word = t == n - 1;
-        if (t == n - 1) __hip_atomic_store((g_i32 *)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const bool last = *lds_word != 0;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
-    return last;
 }
 // query statistics to the host: PSVO_STAT_WORDS 8-byte granules {seq, value}
 // written by relaxed system-scope stores into coherent pinned memory — each
@@ -298,9 +295,6 @@ __device__ __forceinline__ void crit_coef_from_counts(double n_valid_d, double n
     coef[2] = (flags & PSVO_CRIT_USE_SDF) ? (float)(2.0 * (double)(fs_w * fs_weight) / n_el) : 0.0f;
     coef[3] = (flags & PSVO_CRIT_USE_SDF) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
 }
-// stats word indices of the two tail counters (zeroed with the statistics)
-constexpr int kStatIsTail = 13, kStatSmpTail = 14;
-constexpr int kTailPasses = 32;  // rays per thread of a 256-thread tail: up to 8192 rays per query
 
 // A device-sized launch of the render's forward (engine: no host read-back
 // before it): the batch's R_hit / S_max / M come from the query's statistics

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include "psvo_common.h"
+#include "lookback.h"
 
 namespace psvo {
 namespace {
@@ -411,94 +412,6 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
     return total;
 }
 
-// k_ray_stats_rank for one 256-thread workgroup, the last of the traversal
-// launch to arrive (the traversal's per-ray outputs are sc1-stored; read here
-// with sc1 loads): P, R_hit, max ⌈Σ/step⌉, the AABB tests / rounds, and each
-// hit ray's rank.  Ray i = k·256 + t is thread t's pass k; a pass's hit
-// ballot per wave goes to LDS, one scan of the (pass, wave) counts, then the
-// ranks from the ballots (mbcnt) — nothing held in registers across the
-// passes (this runs inside the traversal kernel: its VGPR budget is the
-// traversal's).  n <= 256 · kTailPasses.
-__device__ __noinline__ void stats_rank_tail(int64_t n, const int *__restrict__ ray_nv,
-                                             const float *__restrict__ ray_dsum, float step_size,
-                                             int *__restrict__ stats, int *__restrict__ ray_rank,
-                                             int *__restrict__ rank_ray, const int *__restrict__ blk_out, int n_blk) {
-    constexpr int kW = 4;  // waves
-    __shared__ uint64_t s_hit[kTailPasses * kW];
-    __shared__ int s_cnt[kTailPasses * kW];
-    __shared__ int s_red[4][kW];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    int v_blk = 0, r_blk = 0;
-    for (int b = tid; b < n_blk; b += 256) {
-        v_blk += ld_wt(blk_out + 2 * b);
-        r_blk += ld_wt(blk_out + 2 * b + 1);
-    }
-    int p = 0, mc = 0;
-    const int passes = (int)((n + 255) / 256);
-    for (int k = 0; k < passes; ++k) {
-        const int64_t i = (int64_t)k * 256 + tid;
-        const int nv = i < n ? ld_wt(ray_nv + i) : 0;
-        const float ds = i < n ? ld_wt(ray_dsum + i) : 0.f;
-        p = max(p, nv);
-        if (nv > 0) mc = max(mc, (int)ceilf(__fdiv_rn(ds, step_size)));
-        const uint64_t m = __ballot(nv > 0);
-        if (lane == 0) {
-            s_hit[k * kW + w] = m;
-            s_cnt[k * kW + w] = __popcll(m);
-        }
-    }
-    p = wave_max(p);
-    mc = wave_max(mc);
-    const int vs = wave_sum(v_blk), rs = wave_sum(r_blk);
-    if (lane == 0) {
-        s_red[0][w] = p;
-        s_red[1][w] = mc;
-        s_red[2][w] = vs;
-        s_red[3][w] = rs;
-    }
-    __syncthreads();
-    static_assert(kTailPasses * kW == 2 * kWave, "one scan pass: two counts per lane");
-    if (w == 0) {  // exclusive scan of the (pass, wave) counts, pass-major (= ray order), two per lane
-        const int a0 = lane * 2 < passes * kW ? s_cnt[lane * 2] : 0;
-        const int a1 = lane * 2 + 1 < passes * kW ? s_cnt[lane * 2 + 1] : 0;
-        int incl = a0 + a1;
-#pragma unroll
-        for (int sh = 1; sh < kWave; sh <<= 1) {
-            const int t = __shfl_up(incl, sh, kWave);
-            if (lane >= sh) incl += t;
-        }
-        s_cnt[lane * 2] = incl - a0 - a1;
-        s_cnt[lane * 2 + 1] = incl - a1;
-        if (lane == kWave - 1) {
-            int pp = 0, mm = 0, vv = 0, rr = 0;
-            for (int k = 0; k < kW; ++k) {
-                pp = max(pp, s_red[0][k]);
-                mm = max(mm, s_red[1][k]);
-                vv += s_red[2][k];
-                rr += s_red[3][k];
-            }
-            stats[PSVO_STAT_P] = pp;
-            stats[PSVO_STAT_R_HIT] = incl;
-            stats[PSVO_STAT_MAX_CEIL] = mm;
-            stats[PSVO_STAT_VISITS] += vv;
-            stats[PSVO_STAT_ROUNDS] += rr;
-        }
-    }
-    __syncthreads();
-    for (int k = 0; k < passes; ++k) {
-        const int64_t i = (int64_t)k * 256 + tid;
-        const uint64_t m = s_hit[k * kW + w];
-        if (i < n) {
-            const bool h = (m >> lane) & 1ull;
-            const int rk =
-                s_cnt[k * kW + w] +
-                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            ray_rank[i] = h ? rk : -1;
-            if (h) rank_ray[rk] = (int)i;
-        }
-    }
-}
-
 // PACKED: candidates are records of the breadth-first packed tree
 // (tree_pack.hip: centre + side and ref id / first child / child mask in one
 // 32-B record, siblings contiguous) instead of reference node ids into the
@@ -514,10 +427,11 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           float *__restrict__ hit_t1, int *__restrict__ ray_nv,
                                                           float *__restrict__ ray_dsum, int *__restrict__ stats,
                                                           int *__restrict__ blk_out, int *__restrict__ ray_rank,
-                                                          int *__restrict__ rank_ray) {
-    // rank_ray != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
-    // runs in the launch's last-arriving workgroup (stats_rank_tail)
-    const bool tail = rank_ray != nullptr;
+                                                          int *__restrict__ rank_ray, unsigned long long *lb_desc,
+                                                          uint32_t lb_tag) {
+    // lb_desc != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
+    // runs in this launch by decoupled look-back (lookback.h): each workgroup
+    // ranks its own hit rays, the last one writes P / R_hit / max ⌈Σ/step⌉
     __shared__ KeyLds lds_all[kIsWaves];
     KeyLds &S = lds_all[threadIdx.x / kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -525,6 +439,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     const float half = voxel_size * 0.5f;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int visits = 0, rounds = 0;
+    int w_nv = 0, w_mc = 0;  // this wave's ray: valid hits, ⌈Σ/step⌉ (lane 0)
     bool overflow_stack = false, spill = false;
     if (r < n_rays) {
         IS_DECL;
@@ -735,13 +650,10 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         if (lane == 0) {
             float dsum = 0.0f;
             for (int l = 0; l < nv; ++l) dsum = dsum + S.hd[l];
-            if (tail) {  // read by the last workgroup of this launch
-                st_wt(ray_nv + r, nv);
-                st_wt(ray_dsum + r, dsum);
-            } else {
-                ray_nv[r] = nv;
-                ray_dsum[r] = dsum;
-            }
+            ray_nv[r] = nv;
+            ray_dsum[r] = dsum;
+            w_nv = nv;
+            w_mc = nv > 0 ? (int)ceilf(__fdiv_rn(dsum, step_size)) : 0;  // k_ray_stats' arithmetic
         }
 #ifdef PSVO_IS_STAMPS
         IS_MARK(is_tb);
@@ -760,6 +672,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
     // at the memory side)
     __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves], blk_rd[kIsWaves];
+    __shared__ int blk_nv[kIsWaves], blk_mc[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
@@ -767,6 +680,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         blk_ov[threadIdx.x / kWave] = wov;
         blk_sp[threadIdx.x / kWave] = spill ? 1 : 0;
         blk_rd[threadIdx.x / kWave] = rounds;  // wave-uniform
+        blk_nv[threadIdx.x / kWave] = w_nv;
+        blk_mc[threadIdx.x / kWave] = w_mc;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -777,9 +692,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             sps += blk_sp[w];
             rd += blk_rd[w];
         }
-        if (tail) {
-            st_wt(blk_out + 2 * blockIdx.x, v);
-            st_wt(blk_out + 2 * blockIdx.x + 1, rd);
+        if (lb_desc) {
+            // summed by the look-back below
         } else if (blk_out) {  // summed by k_ray_stats_rank: no same-address atomics (they serialise at the memory side)
             blk_out[2 * blockIdx.x] = v;
             blk_out[2 * blockIdx.x + 1] = rd;
@@ -790,10 +704,35 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
-    if (!tail) return;
-    __shared__ int is_last;
-    if (!last_block(stats + kStatIsTail, &is_last)) return;
-    stats_rank_tail(n_rays, ray_nv, ray_dsum, step_size, stats, ray_rank, rank_ray, blk_out, (int)gridDim.x);
+    if (!lb_desc || threadIdx.x >= kWave) return;
+    // wave 0: the workgroup's aggregate {hit rays, P, max ⌈Σ/step⌉, AABB
+    // tests, rounds} → its exclusive prefix → the hit ranks of its rays
+    const int nv_l = lane < kIsWaves ? blk_nv[lane] : 0;
+    const uint64_t hm = __ballot(nv_l > 0);
+    uint32_t agg[5] = {(uint32_t)__popcll(hm), 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int w = 0; w < kIsWaves; ++w) {
+        agg[1] = max(agg[1], (uint32_t)blk_nv[w]);
+        agg[2] = max(agg[2], (uint32_t)blk_mc[w]);
+        agg[3] += (uint32_t)blk_vis[w];
+        agg[4] += (uint32_t)blk_rd[w];
+    }
+    uint32_t ex[5];
+    const bool ok = lb_scan<5, 0b00110u>(lb_desc, (int)blockIdx.x, (int)gridDim.x, lb_tag, lane, agg, ex);
+    const int64_t rr = (int64_t)blockIdx.x * kIsWaves + lane;
+    if (lane < kIsWaves && rr < n_rays) {
+        const int rk = (int)ex[0] + __popcll(hm & below);
+        ray_rank[rr] = nv_l > 0 ? rk : -1;
+        if (nv_l > 0) rank_ray[rk] = (int)rr;
+    }
+    if (lane == 0 && blockIdx.x == gridDim.x - 1) {  // the stats words were zeroed by the last read-back
+        stats[PSVO_STAT_P] = (int)max(ex[1], agg[1]);
+        stats[PSVO_STAT_R_HIT] = (int)(ex[0] + agg[0]);
+        stats[PSVO_STAT_MAX_CEIL] = (int)max(ex[2], agg[2]);
+        atomicAdd(stats + PSVO_STAT_VISITS, (int)(ex[3] + agg[3]));
+        atomicAdd(stats + PSVO_STAT_ROUNDS, (int)(ex[4] + agg[4]));
+    }
+    if (!ok && lane == 0) atomicOr(stats + PSVO_STAT_FLAGS, kLbFlagTimeout);
 }
 
 // one wave, one word per lane (words <= 64)
@@ -1364,24 +1303,35 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
 // parallel rank samples its own rays inside the GLOBAL [200, K', P] layout
 // this way: rank_ray / hit_* / dsum / stats then describe
 // the all-gathered batch, and the noise key is the global logical index.
-// the scan of the ray sample counts and the statistics read-back in the
-// sampler launch's last-arriving workgroup (single GPU; offsets == nullptr:
-// k_scan_samples runs after the launch instead)
+// the scan of the ray sample counts, the normaliser sums and the statistics
+// read-back inside the sampler launch by decoupled look-back (single GPU;
+// desc == nullptr: k_scan_samples runs after the launch instead)
 struct SampleTail {
     int *offsets;              // [R_hit + 1] exclusive scan of ray_ns
     unsigned long long *host;  // PSVO_STAT_WORDS granules (stat_to_host)
     int seq;
     int *keep;                 // device copy of the statistics (DevBatch), or null
     SampleCounts c;            // the Criterion's normalisers (c.gt_depth null: not counted)
+    unsigned long long *desc;  // look-back descriptors (lookback.h), or null
+    uint32_t tag;              // this launch's descriptor tag
+    // with desc: the ray-major compacted samples (k_compact_rays' output:
+    // leaf / t / ray_of_sample at offsets[r] + s, capacity R · max_steps_cap),
+    // or null.  With desc the rows hold only their valid prefix (no padding:
+    // every reader implies (-1, MAX_DEPTH) past the ray's count)
+    int *leaf;
+    float *t;
+    int *ray_of;
 };
+constexpr int kSmpStage = 256;  // a row's first samples staged in LDS for the in-launch compaction
 // ray_cnt word: valid front / sdf samples (12 bits each), then whether a
 // padded sample (z = MAX_DEPTH) is front / sdf, whether the ray's depth is valid
 __device__ __forceinline__ int pack_counts(int nf, int nsm, bool pf, bool psm, bool valid) {
     return nf | (nsm << 12) | ((int)pf << 24) | ((int)psm << 25) | ((int)valid << 26);
 }
 
-__device__ void scan_samples_tail(int64_t n, const int *__restrict__ ray_ns, int *__restrict__ stats,
-                                  const SampleTail &tl);
+template <int NG>
+__device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__restrict__ stats, const SampleTail &tl,
+                                int *s_off, int st_word, int max_steps_cap);
 
 // one ray of k_sample_fused; returns its valid-sample count, or -1 when the
 // wave has no ray (the launch covers r_hit_cap rows)
@@ -1393,7 +1343,8 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 int *__restrict__ stats, int *__restrict__ s_idx,
                                                 float *__restrict__ s_depth, float *__restrict__ s_dist,
                                                 const int *__restrict__ slot0, int slot0_nch, int &il_out,
-                                                WaveBins &W, const SampleTail &tl, int &cnt_word);
+                                                WaveBins &W, const SampleTail &tl, int &cnt_word, int *stage_i,
+                                                float *stage_z);
 
 __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
@@ -1408,25 +1359,61 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
                                                       int *__restrict__ ray_ns, const int *__restrict__ slot0,
                                                       int slot0_nch, SampleTail tl) {
     __shared__ WaveBins bins_all[4];
+    // look-back mode (the engine's single-GPU query: row_begin 0, all rows):
+    // the rows of this batch, read before any workgroup can re-zero `stats`
+    // (the last one does, after every workgroup in front of it published)
+    const int n_lb = tl.desc && stats[PSVO_STAT_P] > 0 ? (int)min((int64_t)stats[PSVO_STAT_R_HIT], r_hit_cap) : 0;
+    const int last_lb = n_lb > 0 ? (n_lb - 1) / 4 : 0;  // the workgroup holding the last row
+    if (tl.desc && (int)blockIdx.x > last_lb) return;
+    __shared__ int stage_i[4][kSmpStage];
+    __shared__ float stage_z[4][kSmpStage];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const bool compact = tl.desc && tl.leaf;
+    // the statistics words for the read-back, loaded now (the traversal's
+    // are final; the one flag this launch adds is derived, not re-read):
+    // no dependent round trip after the look-back in the last workgroup
+    const int st_word = tl.desc && w == 0 && lane < PSVO_STAT_WORDS ? stats[lane] : 0;
     int il = 0, cnt_word = 0;
     const int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
                                        ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
-                                       slot0_nch, il, bins_all[threadIdx.x / kWave], tl, cnt_word);
-    if (!tl.offsets) {  // k_scan_samples reads them after the launch
-        if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) {
+                                       slot0_nch, il, bins_all[w], tl, cnt_word, compact ? stage_i[w] : nullptr,
+                                       compact ? stage_z[w] : nullptr);
+    if (!tl.desc) {  // k_scan_samples reads them after the launch
+        if (count >= 0 && lane == 0) {
             ray_ns[il] = count;
             if (tl.c.gt_depth) tl.c.ray_cnt[il] = cnt_word;
         }
         return;
     }
-    if (count >= 0 && (threadIdx.x & (kWave - 1)) == 0) {
-        st_wt(ray_ns + il, count);
-        if (tl.c.gt_depth) st_wt(tl.c.ray_cnt + il, cnt_word);
+    __shared__ int s_ns[4], s_cw[4], s_off[4];
+    if (lane == 0) {
+        if (count >= 0) ray_ns[il] = count;
+        s_ns[w] = count;  // -1: no row
+        s_cw[w] = cnt_word;
     }
-    __shared__ int is_last;
-    if (!last_block(stats + kStatSmpTail, &is_last)) return;
-    const int64_t r_hit = ld_wt(stats + PSVO_STAT_R_HIT);
-    scan_samples_tail(min(r_hit, r_hit_cap), ray_ns, stats, tl);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have landed (read back below)
+    __syncthreads();
+    if (w == 0) {
+        if (tl.c.gt_depth)
+            scan_samples_lb<8>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
+        else
+            scan_samples_lb<2>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
+    }
+    if (!compact) return;
+    __syncthreads();
+    // k_compact_rays' work: the row's valid prefix to its compacted place —
+    // the first kSmpStage samples from LDS, the rest (rows longer than that)
+    // read back from the row with sc1 loads (this wave's own stores, past L1)
+    if (count <= 0) return;
+    const int off = s_off[w];
+    const int *oi = s_idx + (int64_t)il * max_steps_cap;
+    const float *od = s_depth + (int64_t)il * max_steps_cap;
+    for (int s = lane; s < count; s += kWave) {
+        const bool st = s < kSmpStage;
+        tl.leaf[off + s] = st ? stage_i[w][s] : ld_wt(oi + s);
+        tl.t[off + s] = st ? stage_z[w][s] : ld_wt(od + s);
+        tl.ray_of[off + s] = il;
+    }
 }
 
 __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
@@ -1437,7 +1424,8 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 int *__restrict__ stats, int *__restrict__ s_idx,
                                                 float *__restrict__ s_depth, float *__restrict__ s_dist,
                                                 const int *__restrict__ slot0, int slot0_nch, int &il_out,
-                                                WaveBins &W, const SampleTail &tl, int &cnt_word) {
+                                                WaveBins &W, const SampleTail &tl, int &cnt_word, int *stage_i,
+                                                float *stage_z) {
     const int P = stats[PSVO_STAT_P];
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
@@ -1475,6 +1463,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     }
     const float steps_j = __fdiv_rn(dsum, step_size);
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
+    const bool nopad = tl.desc != nullptr;  // look-back mode: rows end at their valid prefix
     int *oi = s_idx + (int64_t)il * max_steps_cap;
     float *od = s_depth + (int64_t)il * max_steps_cap;
     float *os = s_dist ? s_dist + (int64_t)il * max_steps_cap : nullptr;  // the engine reads no distances
@@ -1496,10 +1485,15 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
         },
         [&](int s, int v, float dep, float dis) {
             if (s >= cap) return;
+            if (nopad && v == -1) return;  // the implied padding
             // voxel_helpers.py:654-656: clamp dists, MAX_DEPTH / 0 where idx == -1
             oi[s] = v;
             od[s] = v == -1 ? kMaxDepthFill : dep;
             if (os) os[s] = v == -1 ? 0.0f : fmaxf(dis, 0.0f);
+            if (stage_i && s < kSmpStage) {  // v != -1 here (nopad)
+                stage_i[s] = v;
+                stage_z[s] = dep;
+            }
             count += (v != -1);
             if (counting && v != -1) {
                 const bool f = dep < lo_t;
@@ -1508,7 +1502,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
             }
         },
         lane, W);
-    const int s_written = s_end < cap ? s_end : cap;
+    const int s_written = nopad ? cap : s_end < cap ? s_end : cap;
     for (int s = s_written + lane; s < cap; s += kWave) {  // up to max_steps: readers stop at S_max <= max_steps
         oi[s] = -1;
         od[s] = kMaxDepthFill;
@@ -1522,86 +1516,67 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     return wave_sum(count);
 }
 
-// k_scan_samples' work in the sampler's last workgroup (256 threads): thread
-// t owns the run [t·per, (t+1)·per) of ray_ns (per <= kTailPasses, read with
-// sc1 loads into registers), the run totals are scanned across waves, then
-// offsets, S_max / M and the statistics read-back (granules, no
-// system-scope release); the device statistics are zeroed for the next query
-__device__ void scan_samples_tail(int64_t n, const int *__restrict__ ray_ns, int *__restrict__ stats,
-                                  const SampleTail &tl) {
-    __shared__ int s_wave[4], s_max4[4];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    const int per = (int)((n + 255) / 256);
-    const int64_t beg = (int64_t)tid * per;
-    int vals[kTailPasses];
-    int local = 0, mx = 0;
-    // normaliser counts, exact integers (k_crit_counts' float sums of 0 / 1 are exact too)
-    long long c_nf = 0, c_nsm = 0, c_pf = 0, c_psm = 0, c_valid = 0, c_nspf = 0, c_nspsm = 0;
+// k_scan_samples' work for one sampler workgroup (its 4 rows), wave 0 only:
+// the workgroup's aggregate {M, S_max, and with the normalisers nf, nsm,
+// Σ_pf ns, Σ_psm ns, pf | psm << 16, valid} → its exclusive prefix by look-
+// back → its rows' offsets; the workgroup holding row n − 1 (block 0 when
+// there is no row) writes offsets[n], the loss coefficients and the
+// statistics read-back (granules, no system-scope release), and zeroes the
+// device statistics for the next query.  Integer sums: exact, the same
+// totals as k_scan_samples.
+template <int NG>
+__device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__restrict__ stats, const SampleTail &tl,
+                                int *s_off, int st_word, int max_steps_cap) {
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t agg[NG];
 #pragma unroll
-    for (int k = 0; k < kTailPasses; ++k) {
-        const bool in = k < per && beg + k < n;
-        vals[k] = in ? ld_wt(ray_ns + beg + k) : 0;
-        local += vals[k];
-        mx = max(mx, vals[k]);
-        if (tl.c.gt_depth && in) {
-            const int cw = ld_wt(tl.c.ray_cnt + beg + k);
-            const int pf = (cw >> 24) & 1, psm = (cw >> 25) & 1;
-            c_nf += cw & 0xFFF;
-            c_nsm += (cw >> 12) & 0xFFF;
-            c_pf += pf;
-            c_psm += psm;
-            c_valid += (cw >> 26) & 1;
-            c_nspf += pf ? vals[k] : 0;
-            c_nspsm += psm ? vals[k] : 0;
-        }
-    }
-    int incl = local;
-#pragma unroll
-    for (int sh = 1; sh < kWave; sh <<= 1) {
-        const int t = __shfl_up(incl, sh, kWave);
-        if (lane >= sh) incl += t;
-    }
-    mx = wave_max(mx);
-    if (lane == kWave - 1) s_wave[w] = incl;
-    if (lane == 0) s_max4[w] = mx;
-    __syncthreads();
-    int before = 0, tot = 0, smax = 0;
+    for (int g = 0; g < NG; ++g) agg[g] = 0;
+    int before = 0;  // samples of this workgroup's rows in front of lane's row
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        before += k < w ? s_wave[k] : 0;
-        tot += s_wave[k];
-        smax = max(smax, s_max4[k]);
+        const int c = max(s_ns[k], 0);
+        before += k < lane ? c : 0;
+        agg[0] += (uint32_t)c;
+        agg[1] = max(agg[1], (uint32_t)c);
+        if constexpr (NG == 8) {
+            const int cw = s_ns[k] >= 0 ? s_cw[k] : 0;
+            const int pf = (cw >> 24) & 1, psm = (cw >> 25) & 1;
+            agg[2] += (uint32_t)(cw & 0xFFF);
+            agg[3] += (uint32_t)((cw >> 12) & 0xFFF);
+            agg[4] += pf ? (uint32_t)c : 0u;
+            agg[5] += psm ? (uint32_t)c : 0u;
+            agg[6] += (uint32_t)(pf | (psm << 16));
+            agg[7] += (uint32_t)((cw >> 26) & 1);
+        }
     }
-    int run = before + incl - local;
-#pragma unroll
-    for (int k = 0; k < kTailPasses; ++k)
-        if (k < per && beg + k < n) {
-            tl.offsets[beg + k] = run;
-            run += vals[k];
-        }
-    if (tid == 0) tl.offsets[n] = tot;
-    if (tl.c.gt_depth) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
-        __shared__ long long s_c[7][4];
-        long long c[7] = {c_nf, c_nsm, c_pf, c_psm, c_valid, c_nspf, c_nspsm};
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            long long v = c[k];
-#pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, kWave);
-            if (lane == 0) s_c[k][w] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            long long t[7];
-            for (int k = 0; k < 7; ++k) t[k] = s_c[k][0] + s_c[k][1] + s_c[k][2] + s_c[k][3];
-            const long long n_f = t[0] + (long long)smax * t[2] - t[5];
-            const long long n_s = t[1] + (long long)smax * t[3] - t[6];
-            crit_coef_from_counts((double)t[4], (double)n_f, (double)n_s, (double)n, (double)smax, tl.c.w_rgb,
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's flag atomics land before its descriptors
+    uint32_t ex[NG];
+    const int last = n > 0 ? (n - 1) / 4 : 0;  // the workgroups past it returned without a descriptor
+    const bool ok = lb_scan<NG, 0b10u>(tl.desc, (int)blockIdx.x, last + 1, tl.tag, lane, agg, ex);
+    const int il = (int)blockIdx.x * 4 + lane;
+    if (lane < 4) s_off[lane] = (int)ex[0] + before;  // the in-launch compaction's
+    if (lane < 4 && il < n) tl.offsets[il] = (int)ex[0] + before;
+    if ((int)blockIdx.x != last) return;
+    const int tot = (int)(ex[0] + agg[0]);
+    const int smax = (int)max(ex[1], agg[1]);
+    if (lane == 0) tl.offsets[n] = tot;
+    if constexpr (NG == 8) {
+        if (lane == 0) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
+            const uint32_t pp = ex[6] + agg[6];
+            const long long t_nf = ex[2] + agg[2], t_nsm = ex[3] + agg[3], t_nspf = ex[4] + agg[4],
+                            t_nspsm = ex[5] + agg[5], t_pf = pp & 0xFFFF, t_psm = pp >> 16, t_valid = ex[7] + agg[7];
+            const long long n_f = t_nf + (long long)smax * t_pf - t_nspf;
+            const long long n_s = t_nsm + (long long)smax * t_psm - t_nspsm;
+            crit_coef_from_counts((double)t_valid, (double)n_f, (double)n_s, (double)n, (double)smax, tl.c.w_rgb,
                                   tl.c.w_depth, tl.c.w_fs, tl.c.w_sdf, tl.c.tr, tl.c.crit_flags, tl.c.coef);
         }
     }
-    if (w == 0 && lane < PSVO_STAT_WORDS) {
-        const int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : ld_wt(stats + lane);
+    // the sampler's own flag (sample_fused_ray: max_steps beyond the rows' capacity)
+    const int max_steps = __shfl(st_word, PSVO_STAT_MAX_CEIL, kWave) + __shfl(st_word, PSVO_STAT_P, kWave);
+    if (lane < PSVO_STAT_WORDS) {
+        int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : st_word;
+        if (lane == PSVO_STAT_FLAGS && n > 0 && max_steps > max_steps_cap) v |= 2;
+        if (lane == PSVO_STAT_FLAGS && !ok) v |= kLbFlagTimeout;
         if (tl.keep) tl.keep[lane] = v;
         stats[lane] = 0;  // ready for the query set's next use (no memset launch)
         stat_to_host(tl.host, lane, v, tl.seq);
@@ -1802,12 +1777,15 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
     if (s >= s_max) return;
     for (int64_t r = blockIdx.y; r < r_hit; r += gridDim.y) {
         const int64_t e = r * s_max + s;
-        const int v = s_idx[r * cap + s];
-        const float z = s_depth[r * cap + s];
+        // valid samples form a prefix of each row; past it the padding
+        // (-1, MAX_DEPTH) is implied — the look-back sampler does not write it
+        const bool in = s < offsets[r + 1] - offsets[r];
+        const int v = in ? s_idx[r * cap + s] : -1;
+        const float z = in ? s_depth[r * cap + s] : kMaxDepthFill;
         z_vals[e] = z;
         mask[e] = v != -1;
         if (v != -1) {
-            const int64_t o = offsets[r] + s;  // valid samples form a prefix of each row
+            const int64_t o = offsets[r] + s;
             leaf[o] = v;
             t[o] = z;
             ray_of_sample[o] = (int)r;
@@ -1963,7 +1941,7 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     hipStream_t st = as_stream(stream);
     psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr);
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr, nullptr, 0u);
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
@@ -1981,44 +1959,64 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
                        max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
-                       nullptr);
+                       nullptr, nullptr, 0u);
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
 
 namespace psvo {
-// The statistics / rank pass and the sample scan run as kernels of their own
-// by default.  PSVO_QUERY_TAILS=1 runs them in the traversal's and the
-// sampler's last-arriving workgroups instead (no kernel boundary): measured
-// slower on room0 — 42 vs 33 µs and 35 vs 24 µs per region (four interleaved
-// A/B runs): one workgroup's dependent sc1 round trips cost more
-// than the ≈2 µs boundary they save.
-static bool split_query() {
-    const char *v = getenv("PSVO_QUERY_TAILS");
-    return !(v && *v == '1');
+// The statistics / rank pass and the sample scan: by default inside the
+// traversal and sampler launches by decoupled look-back (lookback.h; up to
+// kLbMaxRays rays: the packed pf / psm count granule); PSVO_QUERY_SPLIT=1
+// runs them as kernels of their own (k_ray_stats_rank, k_scan_samples).  The
+// round-3 in-launch variant — the launch's last-arriving workgroup re-reading
+// every ray — measured slower than the split kernels (one workgroup's
+// dependent sc1 round trips) and is gone.
+bool query_lookback(int64_t r) {
+    const char *v = getenv("PSVO_QUERY_SPLIT");  // read per query: tests switch it between steps
+    const bool split = v && *v == '1';
+    return !split && r > 0 && r <= kLbMaxRays;
 }
-bool sampler_counts(int64_t r) { return split_query() || r <= (int64_t)256 * kTailPasses; }
+bool sampler_lookback() {
+    const char *v = getenv("PSVO_LB_SAMPLER");  // 0: the sampler's scan as k_scan_samples (A/B)
+    return !(v && *v == '0');
+}
+bool sampler_compacts() {
+    const char *v = getenv("PSVO_LB_COMPACT");  // 0: k_compact_rays after the read-back (A/B)
+    return !(v && *v == '0');
+}
+int64_t lookback_granules(int64_t r) {
+    return lb_granules<kLbIsGranules>(div_up(r, 4)) + lb_granules<kLbSmpGranules>(div_up(r, 4));
+}
 // the single-GPU sampler with the statistics read-back fused into its scan
 // (one launch less before the host can size the rest of the step)
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                         int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep,
-                        const SampleCounts *counts) {
+                        const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
+                        float *t, int *ray_of) {
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
-    // up to 256 · kTailPasses hit rays the scan and the read-back run in the
-    // sampler launch's last workgroup (counter word zeroed with the statistics)
-    const bool tail = !split_query() && r_hit_cap <= (int64_t)256 * kTailPasses;
+    PSVO_REQUIRE(!lb_desc || (r_hit_cap <= kLbMaxRays && lb_tag != 0), "sample_rays_to_host: look-back arguments");
     SampleTail tl{};
-    if (tail) tl.offsets = offsets;
     if (counts) tl.c = *counts;
     tl.host = host;
     tl.seq = seq;
     tl.keep = keep;
+    if (lb_desc) {  // after the traversal's descriptors (lookback_granules)
+        tl.offsets = offsets;
+        tl.desc = lb_desc + lb_granules<kLbIsGranules>(div_up(r_hit_cap, 4));
+        tl.tag = lb_tag;
+        if (leaf && t && ray_of) {
+            tl.leaf = leaf;
+            tl.t = t;
+            tl.ray_of = ray_of;
+        }
+    }
     psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, nullptr, 0, tl);
-    if (!tail)
+    if (!lb_desc)
         psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
                            host, seq, keep, tl.c);
     return check_launch("sample_rays_to_host");
@@ -2034,24 +2032,25 @@ int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int word
 int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const float *rays_d, const float *centres,
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
-                     int *rank_ray, const PackRec *packed, int *blk_out) {
+                     int *rank_ray, const PackRec *packed, int *blk_out, unsigned long long *lb_desc,
+                     uint32_t lb_tag) {
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
+    PSVO_REQUIRE(!lb_desc || (n_rays <= kLbMaxRays && lb_tag != 0), "intersect_ranked: look-back arguments");
     if (n_rays == 0) return PSVO_OK;
-    // up to 256 · kTailPasses rays the statistics / rank pass runs in the
-    // traversal launch's last workgroup (no second launch, no kernel boundary
-    // between them); the counter word is zero (memset / the last read-back)
-    const bool tail = !split_query() && blk_out && n_rays <= (int64_t)256 * kTailPasses;
-    int *rr = tail ? ray_rank : nullptr, *rk = tail ? rank_ray : nullptr;
+    // lb_desc: the statistics / rank pass inside the traversal launch (look-
+    // back; the stats words are zero: memset / the last read-back)
     if (packed)
         psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
+                           lb_tag);
     else
         psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, rr, rk);
-    if (!tail)
+                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
+                           lb_tag);
+    if (!lb_desc)
         psvo::launch(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
                            ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
     return check_launch("intersect_ranked");

@@ -275,9 +275,9 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
       default_loss  z read from the sampler's rows (stride max_steps), the
                     ray-major compaction (k_compact_rays), the count chain;
       counts        + PSVO_STEP_NO_LOSS: the normalisers counted by the
-                    sampler and turned into coefficients by k_scan_samples;
-      tails         + PSVO_QUERY_TAILS=1: the statistics / rank pass and the
-                    scan (with the counts) in the launches' last workgroups;
+                    sampler and turned into coefficients by its look-back scan;
+      split         + PSVO_QUERY_SPLIT=1: the statistics / rank pass and the
+                    scan (with the counts) as kernels of their own;
       interp_rays   + PSVO_INTERP_RAYS=1: compaction inside a ray-major
                     interpolation (k_interp_fwd_rays).
     The same statistics, the decoder gradient bit for bit (it depends on the
@@ -292,10 +292,10 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
     rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
     crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
     modes = {"padded": ({"PSVO_PADDED_Z": "1"}, True), "default_loss": ({}, True), "counts": ({}, False),
-             "tails": ({"PSVO_QUERY_TAILS": "1"}, False), "interp_rays": ({"PSVO_INTERP_RAYS": "1"}, False)}
+             "split": ({"PSVO_QUERY_SPLIT": "1"}, False), "interp_rays": ({"PSVO_INTERP_RAYS": "1"}, False)}
     runs = {}
     for mode, (env, want_loss) in modes.items():
-        for k in ("PSVO_PADDED_Z", "PSVO_QUERY_TAILS", "PSVO_INTERP_RAYS"):
+        for k in ("PSVO_PADDED_Z", "PSVO_QUERY_SPLIT", "PSVO_INTERP_RAYS"):
             monkeypatch.setenv(k, env.get(k, "0"))
         e = emb0.clone().to(DEV)
         eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
@@ -314,10 +314,56 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
         if mode == "padded":
             continue
         for (sa, ga, pa), (sb, gb, pb) in zip(runs["padded"], runs[mode]):
-            assert sa[:13] == sb[:13], (mode, sa, sb)  # statistics (words past 12: the tails' counters, zero)
+            assert sa[:13] == sb[:13], (mode, sa, sb)  # statistics (words past 12: zero)
             assert torch.equal(ga[n_emb:], gb[n_emb:]), mode  # decoder gradient: bit for bit
             torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-5, atol=1e-6 * float(ga[:n_emb].abs().max()))
             torch.testing.assert_close(pb, pa, rtol=0, atol=1e-5 * float(pa.abs().max()))
+
+
+def test_lookback_query_matches_split_kernels(monkeypatch):
+    """The query's statistics / rank pass and sample scan by decoupled look-
+    back inside the traversal and sampler launches (the default) against the
+    split kernels (PSVO_QUERY_SPLIT=1: k_ray_stats_rank, k_scan_samples) on
+    ragged batches — 1, 3, 5, 257 and 1,001 rays (a partial last workgroup,
+    one to 251 workgroups: one to four tiles of 64, a partial last tile), a batch whose
+first 600 rays miss the octree (leading workgroups with no hit ray) and
+    4,096 rays (16 tiles): the same statistics words, the same loss (bit for bit) and the
+    same decoder gradient; the embedding gradient up to the scatter's order."""
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    ro, rd = w.rays_o.reshape(-1, 3).to(DEV), w.rays_d.reshape(-1, 3).to(DEV)
+    rgb, dep = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randint(0, ro.shape[0], (4096,), generator=g).to(DEV)
+    ro4, rd4, rgb4, dep4 = ro[idx].contiguous(), rd[idx].contiguous(), rgb[idx].contiguous(), dep[idx].contiguous()
+    miss = ro4.clone()
+    miss[:600] = -50.0
+    rdm = rd4.clone()
+    rdm[:600] = torch.tensor([-1.0, 0.0, 0.0], device=DEV)
+    batches = [(ro4[:k], rd4[:k], rgb4[:k], dep4[:k]) for k in (1, 3, 5, 257, 1001)]
+    batches += [(miss, rdm, rgb4, dep4), (ro4, rd4, rgb4, dep4)]
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    runs = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("PSVO_QUERY_SPLIT", split)
+        eng = MappingEngine(map_states(tree, emb0.clone().to(DEV), 0.2, device=DEV), dec, 0.2, 0.01,
+                            truncation=0.1, max_distance=10.0, criteria=crit, max_depth=10.0)
+        out = []
+        for i, (o, d, c, z) in enumerate(batches):
+            loss = float(eng.step(o.contiguous(), d.contiguous(), c.contiguous(), z.contiguous(), seed=900 + i,
+                                  apply_adam=False))
+            torch.cuda.synchronize()
+            out.append((list(eng.last_stats), loss, eng.grad_flat.cpu().clone()))
+        runs[split] = out
+        eng.close()
+    n_emb = emb0.shape[0] * 16
+    for i, ((sa, la, ga), (sb, lb, gb)) in enumerate(zip(runs["1"], runs["0"])):
+        assert sa[:13] == sb[:13], (i, sa, sb)
+        assert sb[1] > 0, i
+        assert la == lb, (i, la, lb)
+        assert torch.equal(ga[n_emb:], gb[n_emb:]), i
+        torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-5, atol=1e-6 * float(ga[:n_emb].abs().max()))
 
 
 def test_kernel_bound_region_timing():
