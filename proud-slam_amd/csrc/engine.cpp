@@ -148,6 +148,7 @@ struct psvo_engine {
     // waits for adam_done first (render, before the interpolation)
     hipEvent_t adam_done = nullptr;
     hipEvent_t pf_fork = nullptr;  // the L2 warm-up for the look-ahead query forks from the backward here
+    hipEvent_t stats_fork = nullptr;  // PSVO_STATS_SIDE: the read-back kernel forks from the sampler here
     bool bwd_recorded = false;     // dfeat_ready holds a step's decoder backward end (psvo_map_side_wait)
     float *pf_sink = nullptr;
     bool adam_pending = false;
@@ -311,6 +312,15 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
 // st waits for a split tail's optimiser step (map_step_impl) if one is pending
 int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
     if (!e->adam_pending) return PSVO_OK;
+    // already done (the usual case: the optimiser step ran beside the query):
+    // no barrier packet in front of the interpolation — the command processor
+    // resolves even a satisfied cross-queue wait with a few µs of latency
+    const hipError_t q = hipEventQuery(e->adam_done);
+    if (q == hipSuccess) {
+        e->adam_pending = false;
+        return PSVO_OK;
+    }
+    if (q == hipErrorNotReady && hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // not an error
     if (hipStreamWaitEvent(st, e->adam_done, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
     e->adam_pending = false;
@@ -479,10 +489,16 @@ extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
                 // writes the L2 back between the kernels it brackets (measured in the time)
                 if (hipEventCreateWithFlags(&t.ev[r][k], hipEventReleaseToDevice) != hipSuccess)
                     return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
+    // the kernel-bound pairs: device-scope release too (PSVO_TIMING_SYSFENCE=1:
+    // the default system-scope one, A/B) — the stop event is the kernel's own
+    // completion signal, and a system-scope release there adds an L2
+    // write-back to the span that the untimed kernel does not pay
+    const char *sf = getenv("PSVO_TIMING_SYSFENCE");
+    const unsigned kc_flags = (sf && *sf == '1') ? hipEventDefault : hipEventReleaseToDevice;
     if (on && !t.kc.ev[0][0])
         for (int i = 0; i < psvo::KernelClock::kMax; ++i)
             for (int k = 0; k < 2; ++k)
-                if (hipEventCreate(&t.kc.ev[i][k]) != hipSuccess)
+                if (hipEventCreateWithFlags(&t.kc.ev[i][k], kc_flags) != hipSuccess)
                     return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
     timer_collect(e, true);
     if (psvo::g_kclock == &t.kc) psvo::g_kclock = nullptr;
@@ -591,6 +607,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->prep_done) (void)hipEventDestroy(e->prep_done);
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
     if (e->pf_fork) (void)hipEventDestroy(e->pf_fork);
+    if (e->stats_fork) (void)hipEventDestroy(e->stats_fork);
     if (e->pf_sink) (void)hipFree(e->pf_sink);
     if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
@@ -825,10 +842,19 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
             Q_BUF(int, rq_, kRayOfQ, cap * sizeof(int));
             leaf_q = lq_, t_q = tq_, ray_of_q = rq_;
         }
+        // PSVO_STATS_SIDE=1 (A/B): the sampler writes no host memory; the
+        // read-back is a kernel of its own on lossq, forked after the sampler
+        const char *ss = getenv("PSVO_STATS_SIDE");
+        const bool side = lbs && ss && *ss == '1' && e->lossq;
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
-                                           q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr, lbs, tag, leaf_q,
-                                           t_q, ray_of_q));
+                                           side ? nullptr : q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr,
+                                           lbs, tag, leaf_q, t_q, ray_of_q));
+        if (side) {
+            if (hipEventRecord(e->stats_fork, st) != hipSuccess || hipStreamWaitEvent(e->lossq, e->stats_fork, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: stream ordering failed", who);
+            ENG_CALL(psvo::keep_to_host(e->lossq, stats_keep, q.host_raw, PSVO_STAT_WORDS, q.seq));
+        }
         q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
@@ -918,7 +944,8 @@ bool engine_overlap(psvo_engine *e) {
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready, &e->pf_fork};
+                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready, &e->pf_fork,
+                         &e->stats_fork};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
@@ -1005,6 +1032,11 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(int, leaf_b, kLeaf, db.m_cap * sizeof(int));
         ENG_BUF(float, tt_b, kT, db.m_cap * sizeof(float));
         ENG_BUF(int, ray_of_b, kRayOf, db.m_cap * sizeof(int));
+        if (qset.compacted) {  // the sampler compacted in its launch (capacity R · max_steps)
+            leaf_b = static_cast<int *>(qset.a.p[kLeafQ]);
+            tt_b = static_cast<float *>(qset.a.p[kTQ]);
+            ray_of_b = static_cast<int *>(qset.a.p[kRayOfQ]);
+        }
         ENG_BUF(float, feat_b, kFeat, db.m_cap * 16 * sizeof(float));
         ENG_BUF(float, sdf_b, kSdfS, db.m_cap * sizeof(float));
         ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
@@ -1015,7 +1047,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
             o.z_recorded = true;
         }
-        if (!interp_rays) {
+        if (!interp_rays && !qset.compacted) {
             mark(e, st, PSVO_TIME_POINTS, 0);
             ENG_CALL(psvo::compact_rays(st, Rq, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, db));
             mark(e, st, PSVO_TIME_POINTS, 1);
@@ -1400,17 +1432,19 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         if (hipEventRecord(e->next_ready, as_stream(fr->next_stream)) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     }
-    // Cross-stream waits cost the critical stream a few microseconds each
-    // wherever they sit between two of its kernels.  The ones this step needs
-    // on st anyway — the previous step's optimiser (before the interpolation
-    // reads the embeddings) and, split, the draw of the next pixels (before
-    // the look-ahead's pose step) — are queued here, in front of the render:
-    // st reaches them right after the queued query's sampler, while the host
-    // is still reading that query's statistics back, so they cost nothing.
+    // The two cross-stream waits this step needs on st — the previous step's
+    // optimiser (before the interpolation reads the embeddings) and, split,
+    // the draw of the next pixels (before the look-ahead's pose step) — sit
+    // where their consumers are.  PSVO_LATE_WAITS=0 (A/B) queues both here,
+    // in front of the render (st reaches them right after the queued query's
+    // sampler, while the host reads that query's statistics back): round 3's
+    // default, measured slower in round 4 (config B, one box, three
+    // interleaved pairs: 0.941-0.942 vs 0.928-0.932 ms per iteration) — the
+    // next draw co-runs with the persistent decoder kernels and ends late, so
+    // the render then waits for it.
     const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_split_tail(d->width) &&
                             !(flags & PSVO_STEP_NO_ADAM);
-    // PSVO_LATE_WAITS=1 (A/B): both waits where their consumers are instead
-    static const bool late_waits = getenv("PSVO_LATE_WAITS") && *getenv("PSVO_LATE_WAITS") == '1';
+    static const bool late_waits = !(getenv("PSVO_LATE_WAITS") && *getenv("PSVO_LATE_WAITS") == '0');
     const bool early_next = wait_next && split_tail && !late_waits;
     if (early_next && hipStreamWaitEvent(st, e->next_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");

@@ -104,6 +104,8 @@ struct PackRec {  // 32 B, 16-B aligned
 // granules (stat_to_host; zeroing them on the device): the engine's host
 // thread polls the tags instead of waiting for an event (svo_query.hip)
 int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq);
+// the same granules from the statistics' device copy, which stays as it is
+int keep_to_host(hipStream_t st, const int *keep, unsigned long long *host, int words, int seq);
 // The Criterion's normalisers (criterion.py:70-101: the valid-depth rays and
 // the front / sdf samples over the padded [R_hit, S_max] layout) depend only
 // on the samples' depths and the rays' GT depth, so the sampler counts them

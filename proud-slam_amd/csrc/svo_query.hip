@@ -735,6 +735,14 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     if (!ok && lane == 0) atomicOr(stats + PSVO_STAT_FLAGS, kLbFlagTimeout);
 }
 
+// the statistics read-back from the device copy (`keep`, which the device-
+// sized kernels read: not zeroed), on a stream of its own (engine: the
+// sampler then writes no host memory)
+__global__ void k_keep_to_host(const int *__restrict__ keep, unsigned long long *host, int words, int seq) {
+    const int i = threadIdx.x;
+    if (i < words) stat_to_host(host, i, keep[i], seq);
+}
+
 // one wave, one word per lane (words <= 64)
 __global__ void k_stats_to_host(int *__restrict__ stats, unsigned long long *host, int words, int seq) {
     const int i = threadIdx.x;
@@ -1579,7 +1587,7 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
         if (lane == PSVO_STAT_FLAGS && !ok) v |= kLbFlagTimeout;
         if (tl.keep) tl.keep[lane] = v;
         stats[lane] = 0;  // ready for the query set's next use (no memset launch)
-        stat_to_host(tl.host, lane, v, tl.seq);
+        if (tl.host) stat_to_host(tl.host, lane, v, tl.seq);  // else k_keep_to_host on another stream
     }
 }
 
@@ -1996,7 +2004,8 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep,
                         const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
                         float *t, int *ray_of) {
-    PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host, "sample_rays_to_host: bad arguments");
+    PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && (host || (lb_desc && keep)),
+                 "sample_rays_to_host: bad arguments");
     PSVO_REQUIRE(!lb_desc || (r_hit_cap <= kLbMaxRays && lb_tag != 0), "sample_rays_to_host: look-back arguments");
     SampleTail tl{};
     if (counts) tl.c = *counts;
@@ -2022,6 +2031,10 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     return check_launch("sample_rays_to_host");
 }
 
+int keep_to_host(hipStream_t st, const int *keep, unsigned long long *host, int words, int seq) {
+    psvo::launch(k_keep_to_host, dim3(1), dim3(64), 0, st, keep, host, words, seq);
+    return check_launch("keep_to_host");
+}
 int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq) {
     psvo::launch(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
     return check_launch("stats_to_host");
