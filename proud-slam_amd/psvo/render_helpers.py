@@ -430,6 +430,20 @@ def _engine_for(keyframe_graph, map_states, sdf_network, resnet, loss_criteria, 
     return eng
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    """The pixel draws' stream, one per device for the process: creating a
+    stream costs the host ≈ 0.35 ms, a third of a call's fixed cost
+    (PSVO_BA_PROFILE=1, config B)."""
+    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return s
+
+
 class _CallClock:
     """PSVO_BA_PROFILE=1: host timestamps of one bundle_adjust_frames call's
     phases (setup, each step's submission, write-back) to stderr — where a
@@ -542,9 +556,10 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     # look-ahead query and the next render
     ahead = lookahead and not callable(noise)
     main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(device=dev) if ahead and num_iterations > 1 else None
+    side = _side_stream(dev) if ahead and num_iterations > 1 else None
     if side is not None:
         side.wait_stream(main)  # the keyframes as the caller left them
+    clk("side")
 
     # PSVO_DRAW_AFTER_BWD=1 (A/B, off): each next draw waits for the previous
     # step's decoder backward (psvo_map_side_wait), so it runs beside the
@@ -561,8 +576,12 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             eng.side_wait(side)
         with torch.cuda.stream(side):
             out = draw(it)
+        if it == 0:
+            clk("draw")
         for t in out[:3]:
             t.record_stream(main)  # freed blocks are reused only after the steps that read them
+        if it > 0:  # later draws are ordered by the engine (next_stream), no event needed
+            return out, None
         ev = torch.cuda.Event()
         ev.record(side)
         return out, ev
@@ -573,7 +592,9 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     clk("draw0")
     eng.bind_adam(st_e["exp_avg"], st_e["exp_avg_sq"], [st["exp_avg"] for st in st_d],
                   [st["exp_avg_sq"] for st in st_d])
+    clk("bind")
     eng.refresh_tree()  # the map may have grown / changed in place since the engine was made
+    clk("tree")
     eng.set_lr(embed_optim.param_groups[0]["lr"], model_optim.param_groups[0]["lr"])
     # keyframe poses [F, 6] and their Adam state on the device — packed again
     # only when a tensor changed since this engine's last call wrote them back
