@@ -108,7 +108,7 @@ __device__ void pose_chain(const float *__restrict__ pose, const float (&tot)[12
 // reads of up to kPoseBatch ranks issued together, then their gradient rows,
 // then the sums in rank order — the same additions as one rank at a time,
 // without a dependent pair of memory round trips per rank
-constexpr int kPoseBatch = 8;
+constexpr int kPoseBatch = 4;  // 8 spilled 14 VGPRs to scratch at 1,024 threads (128 VGPRs per lane)
 __device__ __forceinline__ void frame_ray_sums(int64_t r_hit, const int *__restrict__ rank_ray, int64_t lo, int64_t hi,
                                                const float *__restrict__ dirs, const float *__restrict__ g_o,
                                                const float *__restrict__ g_d, float (&acc)[12]) {
@@ -183,6 +183,12 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     __shared__ float pose_s[6];
     const int f = blockIdx.x;
     const int64_t lo = f * rpf, hi = lo + rpf;
+    // the next rays' camera directions depend on nothing here: loaded first
+    // (one thread per ray when rpf <= kGradThreads), beside the gradient rows
+    const int64_t r1 = lo + threadIdx.x;
+    float nd[3] = {0.f, 0.f, 0.f};
+    if (rpf <= kGradThreads && r1 < hi)
+        for (int j = 0; j < 3; ++j) nd[j] = next_dirs[r1 * 3 + j];
     float acc[12] = {};
     frame_ray_sums(r_hit, rank_ray, lo, hi, dirs, g_o, g_d, acc);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -214,6 +220,14 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     __syncthreads();
     Rot q;
     rotation(pose_s, q);
+    if (rpf <= kGradThreads) {
+        if (r1 < hi)
+            for (int j = 0; j < 3; ++j) {
+                rays_d[r1 * 3 + j] = nd[0] * q.R[j][0] + nd[1] * q.R[j][1] + nd[2] * q.R[j][2];
+                rays_o[r1 * 3 + j] = pose_s[j];
+            }
+        return;
+    }
     for (int64_t r = lo + threadIdx.x; r < hi; r += kGradThreads) {
         const float d0 = next_dirs[r * 3 + 0], d1 = next_dirs[r * 3 + 1], d2 = next_dirs[r * 3 + 2];
         for (int j = 0; j < 3; ++j) {
