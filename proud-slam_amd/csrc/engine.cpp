@@ -310,12 +310,28 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
 }
 
 // st waits for a split tail's optimiser step (map_step_impl) if one is pending
-int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
+inline double now_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e9 + t.tv_nsec;
+}
+// host_spin (the device-sized forward, queued before the query's statistics
+// land): the host polls the optimiser step's event for up to 2 ms instead of
+// queueing a cross-queue barrier — a barrier-AND packet is taken up as soon
+// as the kernel in front of it is dispatched, and one still pending then
+// wakes ≈ 20 µs after its signal (profiles/r04yt_ba_timeline.txt: the
+// interpolation 25 µs after the sampler with nothing else in between)
+int join_adam(psvo_engine *e, hipStream_t st, const char *who, bool host_spin = false) {
     if (!e->adam_pending) return PSVO_OK;
     // already done (the usual case: the optimiser step ran beside the query):
     // no barrier packet in front of the interpolation — the command processor
     // resolves even a satisfied cross-queue wait with a few µs of latency
-    const hipError_t q = hipEventQuery(e->adam_done);
+    const double t_end = host_spin ? now_ns() + 2e6 : 0.0;
+    hipError_t q;
+    for (;;) {
+        q = hipEventQuery(e->adam_done);
+        if (q != hipErrorNotReady || !host_spin || now_ns() > t_end) break;
+    }
     if (q == hipSuccess) {
         e->adam_pending = false;
         return PSVO_OK;
@@ -340,11 +356,6 @@ struct HostWait {
     long calls = 0, spun = 0;
 };
 HostWait g_host_wait;
-inline double now_ns() {
-    timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return t.tv_sec * 1e9 + t.tv_nsec;
-}
 // every granule tagged `seq`: decode the values into out
 bool stats_landed(const unsigned long long *raw, int seq, int *out) {
     int v[PSVO_STAT_WORDS];
@@ -1052,7 +1063,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             ENG_CALL(psvo::compact_rays(st, Rq, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, db));
             mark(e, st, PSVO_TIME_POINTS, 1);
         }
-        ENG_CALL(join_adam(e, st, who));
+        ENG_CALL(join_adam(e, st, who, true));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
         if (interp_rays)
             ENG_CALL(psvo::interp_fwd_rays(st, Rq, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray,
