@@ -208,9 +208,17 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
 
 // pass P: histogram of digit P of the keys whose higher digits equal the
 // prefix picked so far
-template <bool FAST, int P>
+// LB: the LDS histogram's bins.  kPxBins (16 KB) by default: the draw then
+// cannot co-reside with k_mlp_fwd2 (it leaves 3 KB of a CU's LDS) and waits
+// for CUs it frees.  PSVO_PX_SMALL_LDS=1 (A/B): the FAST digit's 256 bins
+// (1 KB), so the draw runs beside the decoder forward — measured slower
+// (config B, three interleaved pairs, one box: 0.921–0.926 vs 0.912–0.930
+// ms, GPU period 0.900–0.903 vs 0.893–0.901: the decoder kernels lose more
+// than the draw gains; profiles/r04px_ab_draw_lds.txt)
+template <bool FAST, int P, int LB = kPxBins>
 __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
-    __shared__ int h[kPxBins];
+    static_assert(LB >= (1 << px_width<FAST>(P)), "LDS histogram too small for the digit");
+    __shared__ int h[LB];
     __shared__ int sh_suffix[kPxThreads];
     __shared__ int sh_res[2];
     constexpr int kShift = px_shift<FAST>(P);
@@ -423,7 +431,14 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
     const dim3 grid(a.nb, n_frames);
     if (weights) psvo::launch(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
-    if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
+    static const bool small = getenv("PSVO_PX_SMALL_LDS") && *getenv("PSVO_PX_SMALL_LDS") == '1';
+    if (!weights && !u && small) {  // A/B: 1-KB LDS histograms (beside the decoder forward)
+        psvo::launch((k_px_hist<true, 0, 256>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<true, 1, 256>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch((k_px_hist<true, 2, 256>), grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
+        psvo::launch(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
+    } else if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
         psvo::launch((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
         psvo::launch((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
         psvo::launch((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
