@@ -226,7 +226,8 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
                                                         const float *__restrict__ rgb_s,
                                                         const float *__restrict__ coef, float *__restrict__ part,
                                                         float *__restrict__ color, float *__restrict__ depth,
-                                                        float *__restrict__ g_sdf_s, float *__restrict__ g_rgb_s) {
+                                                        float *__restrict__ g_sdf_s, float *__restrict__ g_rgb_s,
+                                                        int partials) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
@@ -234,6 +235,11 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     // here: their loads go out first, beside the sample loads
     const int64_t orig = rank_ray[r];
     const int off = offsets[r], ns = ray_ns[r];
+    // past the ray's ns valid samples every pass adds nothing (weights 0, no
+    // sign change between padding sdfs of 1, colours masked): those passes
+    // stop at ns — the same bits — and only the loss partials, which count
+    // the padded samples (criterion.py:70-101), run to s_max
+    const int lim = ns < s_max ? ns : s_max;
     const float d = gt_depth[orig];
     const float gt0 = gt_rgb[orig * 3 + 0], gt1 = gt_rgb[orig * 3 + 1], gt2 = gt_rgb[orig * 3 + 2];
     const float ccol = coef[0], cdep = coef[1], cfs = coef[2], csdf = coef[3];
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         }
     }
     int first = s_max;
-    PSVO_FOR_S(s_max) {
+    PSVO_FOR_S(lim) {
         const float v = P(j, s);
         float v1;
         if constexpr (J > 0) v1 = pn[j];
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
 #pragma unroll
     for (int j = 0; j < JR; ++j) spr[j] = snr[j] = wr[j] = 0.f;
     float tot = 0.f;
-    PSVO_FOR_S(s_max) {
+    PSVO_FOR_S(lim) {
         const float a = P(j, s) / tr;
         const float sp = sigm(a), sn = sigm(-a);
         float w = sp * sn;
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         }
     };
     float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f;
-    PSVO_FOR_S(s_max) {
+    PSVO_FOR_S(lim) {
         const float w = weight_at(j, s);
         if (s < ns) {
             cr += w * C(j, s, 0);
@@ -340,13 +346,15 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     dd = wsum(dd);
     // ---- loss partials (k_crit_rays) and d loss / d {colour, depth} (k_crit_bwd)
     float qfs = 0.f, qsdf = 0.f;
-    PSVO_FOR_S(s_max) {
-        const CritTerms t = crit_terms(Z(j, s), P(j, s), d, tr, max_depth);
-        qfs = crit_sq_add(qfs, t.xfs);
-        qsdf = crit_sq_add(qsdf, t.ysdf);
+    if (partials) {  // the loss value's (not on the gradient path)
+        PSVO_FOR_S(s_max) {
+            const CritTerms t = crit_terms(Z(j, s), P(j, s), d, tr, max_depth);
+            qfs = crit_sq_add(qfs, t.xfs);
+            qsdf = crit_sq_add(qsdf, t.ysdf);
+        }
+        qfs = wsum(qfs);
+        qsdf = wsum(qsdf);
     }
-    qfs = wsum(qfs);
-    qsdf = wsum(qsdf);
     const float rgb[3] = {cr, cg, cb};
     const float gt[3] = {gt0, gt1, gt2};
     float gcol[3], ac = 0.f;
@@ -364,16 +372,18 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         color[r * 3 + 1] = cg;
         color[r * 3 + 2] = cb;
         depth[r] = dd;
-        float *o = part + r * kPartN;
-        o[kPartColor] = ac;
-        o[kPartDepth] = valid ? fabsf(ed) : 0.0f;
-        o[kPartQFs] = qfs;
-        o[kPartQSdf] = qsdf;
-        o[7] = 0.0f;
+        if (partials) {
+            float *o = part + r * kPartN;
+            o[kPartColor] = ac;
+            o[kPartDepth] = valid ? fabsf(ed) : 0.0f;
+            o[kPartQFs] = qfs;
+            o[kPartQSdf] = qsdf;
+            o[7] = 0.0f;
+        }
     }
     // ---- compositing backward (k_composite_bwd, g_weights = 0)
     float dot = 0.f;
-    PSVO_FOR_S(s_max) {
+    PSVO_FOR_S(lim) {
         const bool v = s < ns;
         const float gw = comp_gw3(gdp, Z(j, s), 0.f, v, v ? C(j, s, 0) : 0.f, v ? C(j, s, 1) : 0.f,
                                   v ? C(j, s, 2) : 0.f, gcol[0], gcol[1], gcol[2]);
@@ -443,14 +453,14 @@ extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float
                                    float *depth, float *grad_sdf_s, float *grad_rgb_s) {
     return psvo::composite_loss_z(stream, r_hit, s_max, truncation, max_depth, offsets, ray_ns, z_vals, s_max,
                                   rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace, color, depth, grad_sdf_s,
-                                  grad_rgb_s);
+                                  grad_rgb_s, true);
 }
 
 int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
                            const int *offsets, const int *ray_ns, const float *z_vals, int z_stride,
                            const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *sdf_s,
                            const float *rgb_s, const float *coef, float *workspace, float *color, float *depth,
-                           float *grad_sdf_s, float *grad_rgb_s) {
+                           float *grad_sdf_s, float *grad_rgb_s, bool partials) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max, "composite_loss: bad sizes");
     PSVO_REQUIRE(offsets && ray_ns && z_vals && rank_ray && gt_rgb && gt_depth && sdf_s && rgb_s && coef &&
                      workspace && color && depth && grad_sdf_s && grad_rgb_s,
@@ -463,6 +473,6 @@ int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncat
                                : k_composite_loss<0>;
     psvo::launch(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
                        max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
-                       workspace, color, depth, grad_sdf_s, grad_rgb_s);
+                       workspace, color, depth, grad_sdf_s, grad_rgb_s, partials ? 1 : 0);
     return check_launch("composite_loss");
 }

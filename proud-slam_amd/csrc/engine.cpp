@@ -1531,7 +1531,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (!empty)
         ENG_CALL(psvo::composite_loss_z(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns,
                                         q.z_vals, q.z_stride, q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef,
-                                        crit_ws, color, depth, g_sdf_s, g_rgb_s));
+                                        crit_ws, color, depth, g_sdf_s, g_rgb_s, want_loss || dist));
     // the loss value (not on the gradient path), beside the decoder backward:
     // data parallel on aux (its collective), single GPU on its own stream,
     // joined into st before the optimiser step (loss_out / crit_ws ordered)

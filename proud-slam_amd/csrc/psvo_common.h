@@ -204,7 +204,8 @@ int criterion_coef_z(void *stream, int64_t r_hit, int s_max, float truncation, f
 int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
                      const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
                      const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
-                     float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
+                     float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s,
+                     bool partials = true);  // false: no loss partials (the loss value is not wanted)
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
 // the valid prefix of each sampler row → leaf / t / ray_of_sample at offsets[r] + s
 // Warm every XCD's L2 with up to 4 small read-only arrays (bytes multiple of
