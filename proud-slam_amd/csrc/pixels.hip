@@ -161,6 +161,9 @@ __global__ __launch_bounds__(kPxThreads) void k_px_wsum(PxArgs a) {
 // more than kPxCandCap) candidates is left to the radix passes, which run
 // after them and return at once for the frames the candidates settled: one
 // full pass over the pixels instead of five beside the decoder forward.
+// Opt-in (PSVO_PX_CAND=1): measured slower in the bundle-adjust loop — the
+// per-frame sort workgroups hold four CUs the persistent decoder backward
+// then waits for.
 constexpr int kPxCandCap = 4096;       // candidates per frame (LDS sort of 4,096 u64)
 constexpr int kPxCandBlk = 256;        // candidates per k_px_cand workgroup
 constexpr int kPxCandMaxPick = 1024;   // n <= this
