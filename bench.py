@@ -613,7 +613,7 @@ def main():
         t = torch.tensor([h_m, h_r, h_v], dtype=torch.float64, device=device)
         dist.all_reduce(t)
         h_m, h_r, h_v = (float(x) / world for x in t.cpu())
-    fused_ib = args.width == 128 and os.environ.get("PSVO_MLP_BWD", "") != "2"  # interp bwd inside k_mlp_bwd3
+    fused_ib = args.width == 128  # interp bwd inside k_mlp_bwd3
     q_keys = ("intersect", "sample", "points", "interp_fwd") + (() if fused_ib else ("interp_bwd",))
     # a region the step did not mark (the headline has no separate compaction) counts 0
     q_parts = {k: max(kt_overlap[k], 0.0) for k in q_keys}
@@ -648,22 +648,16 @@ def main():
             r.update(extra)
         return r
 
-    env = os.environ.get
-    lb = env("PSVO_QUERY_SPLIT") != "1" and rays_step <= 16384  # the look-back query (svo_query.hip / lookback.h)
-    lb_smp = lb and world == 1 and env("PSVO_LB_SAMPLER") != "0"
-    lb_compact = lb_smp and env("PSVO_LB_COMPACT") != "0"
+    lb = rays_step <= 16384  # the look-back query (svo_query.hip / lookback.h)
+    lb_smp = lb and world == 1
     q_desc = ("k_intersect_sorted (hit ranks / statistics by in-launch look-back)" if lb
               else "k_intersect_sorted+k_ray_stats_rank")
-    q_desc += (", k_sample_fused (sample scan, read-back" + (" and compaction" if lb_compact else "") +
-               " by in-launch look-back)" if lb_smp else ", k_sample_fused+k_scan_samples")
-    if lb_compact and env("PSVO_FUSED_POINTS") != "1" and env("PSVO_PADDED_Z") != "1" and env("PSVO_DEV_SIZED") != "1":
+    q_desc += (", k_sample_fused (sample scan, read-back and compaction by in-launch look-back)" if lb_smp
+               else ", k_sample_fused+k_scan_samples")
+    if lb_smp:
         i_desc = "k_interp_fwd"
-    elif env("PSVO_FUSED_POINTS") == "1":
-        i_desc = "k_points_interp = compaction + interp fwd"
-    elif world > 1 or env("PSVO_PADDED_Z") == "1":
+    elif world > 1:
         i_desc = "k_sample_points, k_interp_fwd"
-    elif env("PSVO_INTERP_RAYS") == "1":
-        i_desc = "k_interp_fwd_rays = compaction + interp fwd"
     else:
         i_desc = "k_compact_rays, k_interp_fwd"
     chain_desc = q_desc + ", " + i_desc

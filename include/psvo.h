@@ -526,9 +526,31 @@ int psvo_engine_queued(psvo_engine *e);
 /* Drop the queued queries (e.g. the look-ahead query of a loop that ended). */
 int psvo_map_discard(psvo_engine *e);
 
+/* Which production kernels a mapping step runs, for cross-checks (each form
+ * also runs by default elsewhere): PSVO_PATH_QUERY_SPLIT — the query's
+ * statistics / rank pass and its sample scan as kernels of their own
+ * (k_ray_stats_rank, k_scan_samples: queries above 16,384 rays and the
+ * data-parallel sampler) instead of inside the traversal and sampler launches;
+ * PSVO_PATH_PADDED — the padded [R_hit, S_max] z copy and the loss
+ * normalisers counted in the step (the data-parallel / tracking forward);
+ * PSVO_PATH_DENSE_DECODER — the width-128 decoder forward and backward on
+ * every sample (the tracking / autograd form) instead of the sparse decoder
+ * (the sdf trunk on every sample, the full decoder on the samples whose
+ * gradients can be non-zero: composited or inside a loss mask). */
+enum { PSVO_PATH_QUERY_SPLIT = 1, PSVO_PATH_PADDED = 2, PSVO_PATH_DENSE_DECODER = 4 };
+int psvo_engine_set_paths(psvo_engine *e, int paths);   /* with no query queued */
+
+/* The sparse decoder's sample selection (synchronises `stream`, which must
+ * order the engine's steps): out[0] / out[1] kept / composited samples of the
+ * last step, out[2] / out[3] their sums since the last reset, out[4] the steps
+ * summed; reset != 0 zeroes the sums.  An abandoned look-back wait of any
+ * step is reported as an error. */
+int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *out, int reset);
+
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
-       PSVO_TIME_INTERSECT = 4, PSVO_TIME_SAMPLE = 5, PSVO_TIME_POINTS = 6, PSVO_TIME_REGIONS = 7 };
+       PSVO_TIME_INTERSECT = 4, PSVO_TIME_SAMPLE = 5, PSVO_TIME_POINTS = 6, PSVO_TIME_SELECT = 7,
+       PSVO_TIME_REGIONS = 8 };
 int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumulators; on = 1: regions serialised
                                                            on one stream, 2: as run (side streams overlap) */
 int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
@@ -610,17 +632,28 @@ typedef struct psvo_map_frames {
     /* optional: the next call's gt_depth (same storage).  On one GPU with
      * PSVO_STEP_NO_LOSS the look-ahead's sampler then also counts the
      * Criterion's normalisers (criterion.py:70-101), so the next step needs no
-     * separate count pass; NULL: the next step counts them itself. */
+     * separate count pass; NULL: the next step counts them itself.  The
+     * values are read when the look-ahead runs: they must not change until
+     * the consuming call (its counts would no longer match; the engine
+     * matches only the pointer).  Rows that may exceed 4095 samples are
+     * counted in the next step instead. */
     const float *next_gt_depth;
 } psvo_map_frames;
 int psvo_map_step_frames(psvo_engine *e, void *stream, const psvo_map_desc *d, const psvo_map_frames *frames,
                          const float *gt_rgb, const float *gt_depth, const float *noise, uint64_t seed,
                          int64_t adam_step, int flags, float *loss_out, int *stats_out);
 
+/* One tracking iteration (track_frame's loop body, render_helpers.py:708-722)
+ * on camera-frame directions: world rays from pose [t | w], render, Criterion
+ * (PSVO_TRACK_DEPTH_FILTER: weight_depth_loss, the median depth filter),
+ * backward to the pose only and its Adam step.  noise: the sampler's uniform
+ * noise [200, K', max_steps] as the reference draws it (tests), or NULL:
+ * drawn on the device from `seed`. */
 enum { PSVO_TRACK_DEPTH_FILTER = 2 };
 int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays, const float *dirs_cam,
                     const float *gt_rgb, const float *gt_depth, float *pose, float *pose_m, float *pose_v, double lr,
-                    uint64_t seed, int64_t adam_step, int flags, float *pose_grad, float *loss_out, int *stats_out);
+                    const float *noise, uint64_t seed, int64_t adam_step, int flags, float *pose_grad,
+                    float *loss_out, int *stats_out);
 
 /* Both Adam steps of the iteration from desc->grad_flat (one launch; the
  * embedding gradient is zeroed as it is consumed).  With emb_row_flags the

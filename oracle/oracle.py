@@ -579,6 +579,38 @@ def bundle_adjust(frames, picks, noises, map_states, decoder_params, poses0, sta
     return losses, emb.detach(), {k: v.detach() for k, v in params.items()}, torch.stack([p.detach() for p in poses])
 
 
+
+def track_frame(rays_d_cam, rgb, depth, picks, noises, map_states, decoder_params, pose0, step_size, voxel_size,
+                n_iters, lr=1e-3, criteria=REPLICA_CRITERIA, truncation=0.1, max_distance=10.0, max_depth=10.0,
+                weight_depth_loss=True):
+    """track_frame (render_helpers.py:679-761): pose-only Adam (torch, CPU)
+    on one frame against the frozen map, rays = pose applied to the picked
+    camera directions (:708-716), Criterion with weight_depth_loss (the
+    depth-variance median filter, criterion.py:45-50).  picks[it]: sorted
+    pixel ids; noises[it]: the sampler noise of iteration it.  Returns
+    (losses, pose, the last iteration's hit mask)."""
+    pose = torch.tensor(pose0, dtype=torch.float32).requires_grad_(True)
+    opt = torch.optim.Adam([pose], lr=lr)
+    params = {k: v.detach() for k, v in decoder_params.items()}
+    ms = dict(map_states)
+    ms["voxel_vertex_emb"] = map_states["voxel_vertex_emb"].detach()
+    losses, hit = [], None
+    for it in range(n_iters):
+        idx = torch.as_tensor(picks[it]).long()
+        d = rays_d_cam.reshape(-1, 3)[idx] @ se3_rotation(pose).transpose(-1, -2)
+        ro = pose[:3].reshape(1, -1).expand_as(d)
+        out = render_rays(ro[None], d[None], ms, params, step_size, voxel_size, truncation, max_distance,
+                          noise=torch.as_tensor(noises[it]))
+        loss, _ = criterion(out, rgb.reshape(-1, 3)[idx][None], depth.reshape(-1)[idx][None], criteria, truncation,
+                            max_depth, weight_depth_loss=weight_depth_loss)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+        hit = out["ray_mask"].reshape(-1).clone()
+    return losses, pose.detach(), hit
+
+
 # ---------------------------------------------------------------- pixel sampling
 def pixel_uniforms(seed, n_frames, n_pix):
     """The counter-based uniforms psvo_sample_pixels draws when no u is given

@@ -14,6 +14,7 @@
 // lanes in strides; reductions are wave shuffles, so no LDS and no atomics.
 #include <hip/hip_runtime.h>
 
+#include "lookback.h"
 #include "psvo_common.h"
 
 namespace psvo {
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
                                                         const float *__restrict__ coef, float *__restrict__ part,
                                                         float *__restrict__ color, float *__restrict__ depth,
                                                         float *__restrict__ g_sdf_s, float *__restrict__ g_rgb_s,
-                                                        int partials) {
+                                                        int partials, const int *__restrict__ cidx) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
@@ -249,6 +250,11 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     const float *z = z_vals + r * z_stride;
     auto z_at = [&](int s) { return s < ns ? z[s] : kMaxDepthFill; };
     auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };  // padded row (pad 1)
+    // cidx (the sparse decoder, k_select_samples): the decoder ran on the
+    // samples the backward needs only — sample s's colour and its gradients
+    // live at cidx[off + s], and -1 marks a sample whose weight and loss
+    // terms are zero (no colour read, no gradient written: both are 0)
+    auto ci_at = [&](int s) { return s < ns ? (cidx ? cidx[off + s] : off + s) : -1; };
     constexpr int JR = J > 0 ? J : 1;
     float zr[JR], pr[JR], c0r[JR], c1r[JR], c2r[JR];
     if constexpr (J > 0) {
@@ -257,8 +263,9 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
             const int s = lane + 64 * j;
             zr[j] = s < s_max ? z_at(s) : 0.f;
             pr[j] = sdf_at(s);
-            const bool v = s < ns;
-            const float *c = rgb_s + (int64_t)(off + (v ? s : 0)) * 3;
+            const int ci = ci_at(s);
+            const bool v = ci >= 0;
+            const float *c = rgb_s + (int64_t)(v ? ci : 0) * 3;
             c0r[j] = v ? c[0] : 0.f;
             c1r[j] = v ? c[1] : 0.f;
             c2r[j] = v ? c[2] : 0.f;
@@ -272,7 +279,10 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
     };
     auto C = [&](int j, int s, int k) {
         if constexpr (J > 0) return k == 0 ? c0r[j] : (k == 1 ? c1r[j] : c2r[j]);
-        else return rgb_s[(int64_t)(off + s) * 3 + k];
+        else {
+            const int ci = ci_at(s);
+            return ci >= 0 ? rgb_s[(int64_t)ci * 3 + k] : 0.f;
+        }
     };
 #define PSVO_FOR_S(lim) for (int j = 0, s = lane; (J == 0 || j < J) && s < (lim); ++j, s += 64)
     // ---- forward (k_composite_fwd)
@@ -396,16 +406,191 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
         const float gw = comp_gw3(gdp, zs, 0.f, true, C(j, s, 0), C(j, s, 1), C(j, s, 2), gcol[0], gcol[1], gcol[2]);
         const float p = P(j, s);
         const float gsdf = crit_grad(cfs, csdf, crit_terms(zs, p, d, tr, max_depth));  // k_crit_bwd's term
+        const int gi = ci_at(s);
+        if (gi < 0) continue;  // a dropped sample: both gradients are exactly 0
         if constexpr (J > 0)
-            g_sdf_s[off + s] = comp_gsdf_sig(gw, dot, tot, zs < zmin + tr, spr[j], snr[j], tr, gsdf);
+            g_sdf_s[gi] = comp_gsdf_sig(gw, dot, tot, zs < zmin + tr, spr[j], snr[j], tr, gsdf);
         else
-            g_sdf_s[off + s] = comp_gsdf(gw, dot, tot, zs < zmin + tr, p, tr, gsdf);
-        float *gc = g_rgb_s + (int64_t)(off + s) * 3;
+            g_sdf_s[gi] = comp_gsdf(gw, dot, tot, zs < zmin + tr, p, tr, gsdf);
+        float *gc = g_rgb_s + (int64_t)gi * 3;
         gc[0] = W * gcol[0];
         gc[1] = W * gcol[1];
         gc[2] = W * gcol[2];
     }
 #undef PSVO_FOR_S
+}
+
+
+// ---------------------------------------------------------------------------
+// The sparse decoder's sample selection (engine, width 128): which samples
+// the decoder backward needs.  A sample's gradients are exactly zero unless
+//   - it is composited: z < z_min + tr (render_helpers.py:532-539; the only
+//     samples with a weight, so the only ones whose colour reaches the loss,
+//     :544, and whose sdf reaches it through the weights), or
+//   - it lies in a loss mask: front (z < d − tr) or the sdf band
+//     (criterion.py:78-116);
+// the rest (≈ 36 % at config B) get no loss term and no weight.  Every
+// kept sample goes to a compact, ray-major index (cidx; -1: dropped) and the
+// decoder forward (colours, activations) and backward run on the kept
+// samples only — the same per-sample arithmetic, so the same colours, sdf
+// and per-sample gradients; only the weight gradients' summation order
+// changes.  z_min, the masks and `first` are computed exactly as
+// k_composite_loss computes them (same expressions, same padding).
+//
+// One wave per ray (rpw rays per wave when R_hit > 16,384: the look-back's
+// 4,096 workgroups), 4 waves per workgroup; the compact ray offsets by
+// decoupled look-back over {kept, composited} (lookback.h): one launch.
+constexpr int kSelWaves = 4, kSelMaxRpw = 16;
+struct SelectArgs {
+    const float4 *feat;      // [M][16] the interpolated features (4 float4 per sample)
+    const int *leaf, *ray_of;
+    const float *t;
+    int *cidx;               // [M]
+    int *offb;               // [R_hit + 1]
+    float4 *feat_b;          // [M_b][16]
+    int *leaf_b, *ray_of_b;  // [M_b]
+    float *t_b;
+    int *counts;             // [0] kept M_b, [1] composited, [2] flags (look-back abandoned: bit 3), [3] pad,
+                             // then u64 running sums of kept / composited samples and of launches
+    unsigned long long *desc;
+    uint32_t tag;
+};
+
+// the ray's z_min (k_composite_loss's first sign change of the padded sdf row)
+__device__ __forceinline__ float sel_zmin(int lane, int s_max, int ns, int off, const float *z,
+                                          const float *__restrict__ sdf_s) {
+    const int lim = ns < s_max ? ns : s_max;
+    auto sdf_at = [&](int s) { return s < ns ? sdf_s[off + s] : 1.0f; };
+    int first = s_max;
+    for (int s = lane; s < lim; s += 64) {
+        const float v = sdf_at(s);
+        const float v1 = s + 1 < s_max ? sdf_at(s + 1) : 0.f;
+        if (s + 1 < s_max && v1 * v < 0.0f) first = min(first, s);
+    }
+    first = wmin(first);
+    const int f0 = first == s_max ? 0 : first;
+    return f0 < ns ? z[f0] : kMaxDepthFill;
+}
+
+struct SelFlags {
+    bool keep, comp;
+};
+__device__ __forceinline__ SelFlags sel_flags(float zs, float zmin, float d, float tr, float max_depth) {
+#pragma clang fp contract(off)
+    SelFlags o;
+    o.comp = zs < zmin + tr;
+    const bool f = zs < (d - tr);
+    const bool b = zs > (d + tr);
+    const bool dm = d > 0.0f && d < max_depth;
+    o.keep = o.comp || f || (!b && dm);
+    return o;
+}
+
+__global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, int s_max, float tr, float max_depth,
+                                                        const int *__restrict__ offsets,
+                                                        const int *__restrict__ ray_ns,
+                                                        const float *__restrict__ z_vals, int z_stride,
+                                                        const int *__restrict__ rank_ray,
+                                                        const float *__restrict__ gt_depth,
+                                                        const float *__restrict__ sdf_s, SelectArgs a) {
+    __shared__ int s_nb[kSelWaves * kSelMaxRpw], s_off[kSelWaves * kSelMaxRpw];
+    __shared__ float s_zmin[kSelWaves * kSelMaxRpw];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t r0 = ((int64_t)blockIdx.x * kSelWaves + w) * rpw;
+    const uint64_t below = (1ull << lane) - 1ull;
+    // ---- count: kept / composited samples per ray
+    int nc_w = 0;
+    for (int k = 0; k < rpw; ++k) {
+        const int64_t r = r0 + k;
+        int nb = 0, nc = 0;
+        float zmin = 0.f;
+        if (r < r_hit) {
+            const int off = offsets[r], ns = ray_ns[r];
+            const float *z = z_vals + r * z_stride;
+            const float d = gt_depth[rank_ray[r]];
+            zmin = sel_zmin(lane, s_max, ns, off, z, sdf_s);
+            for (int s0 = 0; s0 < ns; s0 += 64) {
+                const int s = s0 + lane;
+                SelFlags f{false, false};
+                if (s < ns) f = sel_flags(z[s], zmin, d, tr, max_depth);
+                nb += __popcll(__ballot(f.keep));
+                nc += __popcll(__ballot(f.comp && s < ns));
+            }
+        }
+        if (lane == 0) {
+            s_nb[w * rpw + k] = nb;
+            s_zmin[w * rpw + k] = zmin;
+        }
+        nc_w += nc;
+    }
+    if (lane == 0) s_off[w] = nc_w;  // (scratch: the wave's composited count)
+    __syncthreads();
+    if (w == 0) {
+        const int n_r = kSelWaves * rpw;
+        int v = 0;
+        for (int i = lane; i < n_r; i += 64) v += s_nb[i];
+        int c = lane < kSelWaves ? s_off[lane] : 0;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            v += __shfl_xor(v, sh, 64);
+            c += __shfl_xor(c, sh, 64);
+        }
+        const uint32_t agg[2] = {(uint32_t)v, (uint32_t)c};
+        uint32_t ex[2];
+        const bool ok = lb_scan<2, 0u>(a.desc, (int)blockIdx.x, (int)gridDim.x, a.tag, lane, agg, ex);
+        if (lane == 0) {
+            s_base = ok ? (int)ex[0] : -1;
+            if ((int)blockIdx.x == (int)gridDim.x - 1) {
+                a.offb[r_hit] = (int)(ex[0] + agg[0]);
+                a.counts[0] = ok ? (int)(ex[0] + agg[0]) : 0;  // an abandoned wait: an empty compact batch
+                a.counts[1] = (int)(ex[1] + agg[1]);
+                unsigned long long *sums = reinterpret_cast<unsigned long long *>(a.counts + 4);
+                sums[0] += ex[0] + agg[0];  // one writer per launch, launches stream-ordered
+                sums[1] += ex[1] + agg[1];
+                sums[2] += 1;
+            }
+            if (!ok) atomicOr(a.counts + 2, kLbFlagTimeout);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive ray offsets of the workgroup's rays
+        int run = s_base;
+        for (int i = 0; i < kSelWaves * rpw; ++i) {
+            s_off[i] = run;
+            run += s_nb[i];
+        }
+    }
+    __syncthreads();
+    if (s_base < 0) return;  // the prefix is undefined: no stores
+    // ---- write: compact index of every sample, the kept samples' rows
+    for (int k = 0; k < rpw; ++k) {
+        const int64_t r = r0 + k;
+        if (r >= r_hit) break;
+        const int off = offsets[r], ns = ray_ns[r];
+        const float *z = z_vals + r * z_stride;
+        const float d = gt_depth[rank_ray[r]];
+        const float zmin = s_zmin[w * rpw + k];
+        int base = s_off[w * rpw + k];
+        if (lane == 0) a.offb[r] = base;
+        for (int s0 = 0; s0 < ns; s0 += 64) {
+            const int s = s0 + lane;
+            bool keep = false;
+            if (s < ns) keep = sel_flags(z[s], zmin, d, tr, max_depth).keep;
+            const uint64_t bal = __ballot(keep);
+            const int j = base + __popcll(bal & below);
+            if (s < ns) a.cidx[off + s] = keep ? j : -1;
+            if (keep) {
+                const int64_t src = off + s;
+                a.leaf_b[j] = a.leaf[src];
+                a.t_b[j] = a.t[src];
+                a.ray_of_b[j] = (int)r;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a.feat_b[(int64_t)j * 4 + q] = a.feat[src * 4 + q];
+            }
+            base += __popcll(bal);
+        }
+    }
 }
 
 }  // namespace
@@ -436,15 +621,6 @@ extern "C" int psvo_composite_bwd(void *stream, int64_t r_hit, int s_max, float 
     return check_launch("composite_bwd");
 }
 
-namespace psvo {
-// psvo_composite_loss reading z from rows of stride z_stride >= s_max (the
-// sampler's [R, cap] depth rows: the engine skips the padded [R_hit, S_max]
-// copy; entries s_max..z_stride are never read)
-int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
-                     const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
-                     const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
-                     float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s);
-}  // namespace psvo
 
 extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
                                    const int *offsets, const int *ray_ns, const float *z_vals, const int *rank_ray,
@@ -453,14 +629,14 @@ extern "C" int psvo_composite_loss(void *stream, int64_t r_hit, int s_max, float
                                    float *depth, float *grad_sdf_s, float *grad_rgb_s) {
     return psvo::composite_loss_z(stream, r_hit, s_max, truncation, max_depth, offsets, ray_ns, z_vals, s_max,
                                   rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef, workspace, color, depth, grad_sdf_s,
-                                  grad_rgb_s, true);
+                                  grad_rgb_s, true, nullptr);
 }
 
 int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, float max_depth,
                            const int *offsets, const int *ray_ns, const float *z_vals, int z_stride,
                            const int *rank_ray, const float *gt_rgb, const float *gt_depth, const float *sdf_s,
                            const float *rgb_s, const float *coef, float *workspace, float *color, float *depth,
-                           float *grad_sdf_s, float *grad_rgb_s, bool partials) {
+                           float *grad_sdf_s, float *grad_rgb_s, bool partials, const int *cidx) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max, "composite_loss: bad sizes");
     PSVO_REQUIRE(offsets && ray_ns && z_vals && rank_ray && gt_rgb && gt_depth && sdf_s && rgb_s && coef &&
                      workspace && color && depth && grad_sdf_s && grad_rgb_s,
@@ -473,6 +649,33 @@ int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncat
                                : k_composite_loss<0>;
     psvo::launch(kern, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit, s_max, truncation,
                        max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_rgb, gt_depth, sdf_s, rgb_s, coef,
-                       workspace, color, depth, grad_sdf_s, grad_rgb_s, partials ? 1 : 0);
+                       workspace, color, depth, grad_sdf_s, grad_rgb_s, partials ? 1 : 0, cidx);
     return check_launch("composite_loss");
+}
+
+int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth,
+                         const int *offsets, const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray,
+                         const float *gt_depth, const float *sdf_s, const float *feat, const int *leaf, const float *t,
+                         const int *ray_of, int *cidx, int *offb, float *feat_b, int *leaf_b, float *t_b,
+                         int *ray_of_b, int *counts, unsigned long long *desc, uint32_t tag) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0,
+                 "select_samples: bad sizes");
+    const int rpw = select_rays_per_wave(r_hit);
+    PSVO_REQUIRE(rpw <= kSelMaxRpw, "select_samples: %lld hit rays exceed the selection's %d",
+                 (long long)r_hit, kSelWaves * kSelMaxRpw * kLbMaxBlocks);
+    if (r_hit == 0) return PSVO_OK;
+    SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offb,
+                 reinterpret_cast<float4 *>(feat_b), leaf_b, ray_of_b, t_b, counts, desc, tag};
+    psvo::launch(k_select_samples, dim3(div_up(r_hit, (int64_t)kSelWaves * rpw)), dim3(64 * kSelWaves), 0, st, r_hit,
+                 rpw, s_max, truncation, max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_depth, sdf_s, a);
+    return check_launch("select_samples");
+}
+
+int psvo::select_rays_per_wave(int64_t r_hit) {
+    const int64_t per = (int64_t)kSelWaves * kLbMaxBlocks;  // rays at one per wave
+    return r_hit <= per ? 1 : (int)((r_hit + per - 1) / per);
+}
+
+int64_t psvo::select_granules(int64_t r_hit) {
+    return lb_granules<2>(div_up(r_hit, (int64_t)kSelWaves * select_rays_per_wave(r_hit)));
 }

@@ -26,12 +26,14 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kStatsKeep, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kQSlots };
+             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
-    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kIbWs, kSlots
+    kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kIbWs,
+    // the sparse decoder (select_samples): compact index, ray offsets, the kept samples' rows, counts, look-back
+    kCidx, kOffB, kFeatB, kLeafB, kTB, kRayOfB, kSdfB, kSelCnt, kSelDesc, kSlots
 };
 
 struct Arena {
@@ -147,21 +149,18 @@ struct psvo_engine {
     // pose step and the next query; every later reader of the weights on st
     // waits for adam_done first (render, before the interpolation)
     hipEvent_t adam_done = nullptr;
-    hipEvent_t pf_fork = nullptr;  // the L2 warm-up for the look-ahead query forks from the backward here
-    hipEvent_t stats_fork = nullptr;  // PSVO_STATS_SIDE: the read-back kernel forks from the sampler here
     bool bwd_recorded = false;     // dfeat_ready holds a step's decoder backward end (psvo_map_side_wait)
-    float *pf_sink = nullptr;
     bool adam_pending = false;
     hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
-    // capacities of the device-sized forward (render): samples, samples per ray
-    int64_t m_cap = 0;
-    int s_cap = 0;
     EngineTimer tm;
     // the decoder images a look-ahead step built on st after its Adam step,
     // for the decoder whose W[0] it names; consumed by the next
     // psvo_map_step_frames, dropped by every other call
     bool images_next = false;
     const float *images_w0 = nullptr;
+    int paths = 0;                  // PSVO_PATH_* (psvo_engine_set_paths)
+    uint32_t sel_tag = 0;           // the sample selection's look-back descriptor tag
+    const void *sel_zeroed = nullptr;  // its descriptor buffer, zeroed once at allocation
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
 };
@@ -175,7 +174,7 @@ using namespace psvo;
     } while (0)
 
 namespace psvo {
-KernelClock *g_kclock = nullptr;
+thread_local KernelClock *g_kclock = nullptr;
 }
 
 namespace {
@@ -292,6 +291,10 @@ inline void mark(psvo_engine *e, hipStream_t st, int region, int end) {
             timer_collect(e, true);  // room for the region's kernels
         t.starts[region] += 1;
         psvo::g_kclock = &c;
+        c.streams[0] = st;  // the region's stream and the engine's side streams
+        c.streams[1] = e->aux;
+        c.streams[2] = e->lossq;
+        c.streams[3] = e->side;
         if (c.depth >= 8) {
             c.overflow = true;
             return;
@@ -315,23 +318,12 @@ inline double now_ns() {
     clock_gettime(CLOCK_MONOTONIC, &t);
     return t.tv_sec * 1e9 + t.tv_nsec;
 }
-// host_spin (the device-sized forward, queued before the query's statistics
-// land): the host polls the optimiser step's event for up to 2 ms instead of
-// queueing a cross-queue barrier — a barrier-AND packet is taken up as soon
-// as the kernel in front of it is dispatched, and one still pending then
-// wakes ≈ 20 µs after its signal (profiles/r04yt_ba_timeline.txt: the
-// interpolation 25 µs after the sampler with nothing else in between)
-int join_adam(psvo_engine *e, hipStream_t st, const char *who, bool host_spin = false) {
+int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
     if (!e->adam_pending) return PSVO_OK;
     // already done (the usual case: the optimiser step ran beside the query):
     // no barrier packet in front of the interpolation — the command processor
     // resolves even a satisfied cross-queue wait with a few µs of latency
-    const double t_end = host_spin ? now_ns() + 2e6 : 0.0;
-    hipError_t q;
-    for (;;) {
-        q = hipEventQuery(e->adam_done);
-        if (q != hipErrorNotReady || !host_spin || now_ns() > t_end) break;
-    }
+    const hipError_t q = hipEventQuery(e->adam_done);
     if (q == hipSuccess) {
         e->adam_pending = false;
         return PSVO_OK;
@@ -489,6 +481,35 @@ extern "C" int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int
     return PSVO_OK;
 }
 
+extern "C" int psvo_engine_set_paths(psvo_engine *e, int paths) {
+    PSVO_REQUIRE(e && (paths & ~(PSVO_PATH_QUERY_SPLIT | PSVO_PATH_PADDED | PSVO_PATH_DENSE_DECODER)) == 0, "engine_set_paths: bad arguments");
+    PSVO_REQUIRE(e->q_count == 0, "engine_set_paths: queries are queued");
+    e->paths = paths;
+    return PSVO_OK;
+}
+
+extern "C" int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *out, int reset) {
+    PSVO_REQUIRE(e && out, "engine_select_stats: null argument");
+    for (int i = 0; i < 5; ++i) out[i] = 0;
+    if (!e->a.p[kSelCnt]) return PSVO_OK;  // no sparse step yet
+    hipStream_t st = as_stream(stream);
+    int c[psvo::kSelCountInts];
+    if (hipMemcpyAsync(c, e->a.p[kSelCnt], sizeof(c), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine_select_stats: copy failed");
+    unsigned long long u[3];
+    memcpy(u, c + 4, sizeof(u));
+    out[0] = c[0];
+    out[1] = c[1];
+    out[2] = (int64_t)u[0];
+    out[3] = (int64_t)u[1];
+    out[4] = (int64_t)u[2];
+    PSVO_REQUIRE(!(c[2] & 8), "engine_select_stats: a sample selection's look-back wait was abandoned");
+    if (reset && hipMemsetAsync(static_cast<int *>(e->a.p[kSelCnt]) + 4, 0, 6 * sizeof(int), st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine_select_stats: memset failed");
+    return PSVO_OK;
+}
+
 extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
     PSVO_REQUIRE(e, "engine_set_timing: null engine");
     EngineTimer &t = e->tm;
@@ -500,12 +521,10 @@ extern "C" int psvo_engine_set_timing(psvo_engine *e, int on) {
                 // writes the L2 back between the kernels it brackets (measured in the time)
                 if (hipEventCreateWithFlags(&t.ev[r][k], hipEventReleaseToDevice) != hipSuccess)
                     return set_error(PSVO_E_LAUNCH, "engine_set_timing: hipEventCreate failed");
-    // the kernel-bound pairs: device-scope release too (PSVO_TIMING_SYSFENCE=1:
-    // the default system-scope one, A/B) — the stop event is the kernel's own
-    // completion signal, and a system-scope release there adds an L2
-    // write-back to the span that the untimed kernel does not pay
-    const char *sf = getenv("PSVO_TIMING_SYSFENCE");
-    const unsigned kc_flags = (sf && *sf == '1') ? hipEventDefault : hipEventReleaseToDevice;
+    // the kernel-bound pairs: device-scope release too — the stop event is
+    // the kernel's own completion signal, and a system-scope release there
+    // adds an L2 write-back to the span that the untimed kernel does not pay
+    const unsigned kc_flags = hipEventReleaseToDevice;
     if (on && !t.kc.ev[0][0])
         for (int i = 0; i < psvo::KernelClock::kMax; ++i)
             for (int k = 0; k < 2; ++k)
@@ -617,9 +636,6 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->prep_fork) (void)hipEventDestroy(e->prep_fork);
     if (e->prep_done) (void)hipEventDestroy(e->prep_done);
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
-    if (e->pf_fork) (void)hipEventDestroy(e->pf_fork);
-    if (e->stats_fork) (void)hipEventDestroy(e->stats_fork);
-    if (e->pf_sink) (void)hipFree(e->pf_sink);
     if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
     delete e;
@@ -746,6 +762,7 @@ struct Render {
     uint64_t *masks;
     bool z_recorded = false;  // e->z_ready marks the sample compaction on st (aux has not waited yet)
     int z_stride = 0;         // row stride of z_vals: s_max (padded copy) or the sampler's row capacity
+    bool sparse = false;      // the decoder ran the sdf trunk only (sdf_s): the rest after select_samples
 };
 
 #define Q_BUF(T, name, slot, bytes)                                              \
@@ -781,7 +798,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     // sampler launches (decoupled look-back; the sampler's only on one GPU)
     unsigned long long *lb = nullptr;
     uint32_t tag = 0;
-    if (psvo::query_lookback(R)) {
+    if (psvo::query_lookback(R) && !(e->paths & PSVO_PATH_QUERY_SPLIT)) {
         const size_t lb_bytes = (size_t)psvo::lookback_granules(R) * sizeof(unsigned long long);
         lb = reinterpret_cast<unsigned long long *>(arena_buf(q.a, st, kLbDesc, lb_bytes, &rc));
         if (!lb) return rc;
@@ -816,8 +833,6 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     float *const s_dist = nullptr;
     Q_BUF(int, ray_ns, kRayNs, (size_t)R * sizeof(int));
     Q_BUF(int, offsets, kOffsets, (size_t)(R + 1) * sizeof(int));
-    // the statistics as the device-sized forward reads them (the read-back zeroes `stats`)
-    Q_BUF(int, stats_keep, kStatsKeep, PSVO_STAT_WORDS * sizeof(int));
     mark(e, st, PSVO_TIME_SAMPLE, 0);
     if (x.on()) {
         ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
@@ -832,7 +847,9 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     q.compacted = false;
     if (!x.on()) {  // the sampler's scan does the read-back (and, given the GT depths, the loss normalisers)
         psvo::SampleCounts sc{};
-        const bool counts = counts_gt != nullptr;
+        // the per-ray counts pack into 12-bit fields (svo_query.hip pack_counts):
+        // rows that may hold more than 4095 samples count in the step instead (k_crit_counts)
+        const bool counts = counts_gt != nullptr && max_steps <= 4095;
         if (counts) {
             Q_BUF(int, ray_cnt, kRayCnt, (size_t)R * sizeof(int));
             Q_BUF(float, coefq, kCoefQ, 4 * sizeof(float));
@@ -842,30 +859,20 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
             q.counts_gt = counts_gt;
         }
         // look-back sampler: the ray-major compaction in the same launch
-        // (capacity R · max_steps: every row fits; PSVO_LB_COMPACT=0: k_compact_rays after the read-back)
-        unsigned long long *lbs = psvo::sampler_lookback() ? lb : nullptr;
+        // (capacity R · max_steps: every row fits); otherwise k_compact_rays after the read-back
         int *leaf_q = nullptr, *ray_of_q = nullptr;
         float *t_q = nullptr;
-        if (lbs && psvo::sampler_compacts()) {
+        if (lb) {
             const size_t cap = (size_t)R * max_steps;
             Q_BUF(int, lq_, kLeafQ, cap * sizeof(int));
             Q_BUF(float, tq_, kTQ, cap * sizeof(float));
             Q_BUF(int, rq_, kRayOfQ, cap * sizeof(int));
             leaf_q = lq_, t_q = tq_, ray_of_q = rq_;
         }
-        // PSVO_STATS_SIDE=1 (A/B): the sampler writes no host memory; the
-        // read-back is a kernel of its own on lossq, forked after the sampler
-        const char *ss = getenv("PSVO_STATS_SIDE");
-        const bool side = lbs && ss && *ss == '1' && e->lossq;
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
-                                           side ? nullptr : q.host_raw, q.seq, stats_keep, counts ? &sc : nullptr,
-                                           lbs, tag, leaf_q, t_q, ray_of_q));
-        if (side) {
-            if (hipEventRecord(e->stats_fork, st) != hipSuccess || hipStreamWaitEvent(e->lossq, e->stats_fork, 0) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: stream ordering failed", who);
-            ENG_CALL(psvo::keep_to_host(e->lossq, stats_keep, q.host_raw, PSVO_STAT_WORDS, q.seq));
-        }
+                                           q.host_raw, q.seq, counts ? &sc : nullptr, lb, tag, leaf_q, t_q,
+                                           ray_of_q));
         q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
@@ -944,19 +951,13 @@ int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
     return PSVO_OK;
 }
 
-// render_rays (render_helpers.py:363-556) on the device, after the query:
-// sample compaction (sized by the query's read-back), interpolation, decoder,
-// Work beside the main stream on `aux` (PSVO_SERIAL_BWD=1 or timed runs:
-// everything on the caller's stream, in dependency order).
-bool engine_overlap(psvo_engine *e) {
-    static const bool serial = getenv("PSVO_SERIAL_BWD") && *getenv("PSVO_SERIAL_BWD") == '1';
-    return !serial && (!e->tm.on || e->tm.overlap);
-}
+// Work beside the main stream on `aux` (timed runs in mode 1: everything on
+// the caller's stream, in dependency order).
+bool engine_overlap(psvo_engine *e) { return !e->tm.on || e->tm.overlap; }
 int ensure_aux(psvo_engine *e) {
     if (e->aux) return PSVO_OK;
     hipEvent_t *evs[] = {&e->dfeat_ready, &e->emb_done, &e->z_ready, &e->coef_ready, &e->grads_ready,
-                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready, &e->pf_fork,
-                         &e->stats_fork};
+                         &e->prep_fork, &e->prep_done, &e->loss_done, &e->adam_done, &e->next_ready};
     if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->lossq, hipStreamNonBlocking) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
@@ -975,11 +976,13 @@ int fork_join(hipStream_t from, hipStream_t st, hipEvent_t ev) {
     return PSVO_OK;
 }
 
+// render_rays (render_helpers.py:363-556) on the device, after the query:
+// sample compaction (sized by the query's read-back), interpolation, decoder,
 // compositing.  want_act: keep the decoder activations for weight gradients
 // (mapping); tracking keeps only the masks.
 int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qset, const float *rays_o,
            const float *rays_d, bool want_act, int *stats_out, const char *who, Render &o,
-           bool fused_loss = false, bool need_z_event = true) {
+           bool fused_loss = false, bool need_z_event = true, bool sparse = false) {
     int rc = PSVO_OK;
     void *stream = st;
     const int max_steps = qset.max_steps;
@@ -1004,130 +1007,13 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
     }
     const bool dist = e->x.on();
-    // Device-sized forward (PSVO_DEV_SIZED=1; mapping step, width 128, one
-    // GPU, once a step has sized the buffers): sample compaction,
-    // interpolation and the decoder forward are queued before the query's
-    // statistics reach the host — their kernels read R_hit / S_max / M on the
-    // device (DevBatch) — so the host's read-back no longer gates them.  A
-    // batch beyond the capacities writes nothing and is re-run host-sized
-    // below.  Measured (config B, same box): 0.3–2 % SLOWER than
-    // host-sized — the GPU still idles ≈ 17 µs after the sampler's scan and
-    // ≈ 11 µs at the stream joins before the interpolation, now without the
-    // host's read-back to hide behind — so host-sized stays the default.
-    const char *dz = getenv("PSVO_DEV_SIZED");
-    const bool host_sized = !(dz && *dz == '1');
-    const bool dev_sized = fused_loss && want_act && width == 128 && !dist && e->m_cap > 0 && !host_sized;
-    const int64_t Rq = qset.R;
-    bool dev_done = false;
-    float *feat = nullptr, *sdf_s = nullptr, *rgb_s = nullptr, *act = nullptr, *z_vals = nullptr, *tt = nullptr;
-    int *leaf = nullptr, *ray_of = nullptr;
-    uint64_t *masks = nullptr;
-    const char *sp = getenv("PSVO_FUSED_POINTS");
-    const bool fuse_pi = sp && *sp == '1';
-    // the mapping step on one GPU: no padded [R_hit, S_max] copy at all —
-    // the loss kernels read z from the sampler's depth rows (stride
-    // max_steps) and the compaction is ray-major (k_compact_rays: a wave per
-    // hit ray over its ≈ 64 valid entries, not the S_max-wide row), then
-    // k_interp_fwd; PSVO_INTERP_RAYS=1: compaction inside a ray-major
-    // interpolation (k_interp_fwd_rays, one launch); PSVO_PADDED_Z=1 (or
-    // PSVO_FUSED_POINTS=1): the padded copy as the autograd path makes it
-    const char *ir = getenv("PSVO_INTERP_RAYS");
-    const char *pz = getenv("PSVO_PADDED_Z");
-    const bool rays_path = fused_loss && want_act && !dist && !fuse_pi && !(pz && *pz == '1');
-    const bool interp_rays = rays_path && ir && *ir == '1';
-    if (dev_sized && rays_path) {
-        // device-sized, round-4 chain: the interpolation (with the compaction)
-        // over every ray slot, R_hit read on the device, and the decoder
-        // forward over the device's M — both queued before the statistics land
-        const psvo::DevBatch db{static_cast<const int *>(qset.a.p[kStatsKeep]), Rq, e->m_cap, max_steps};
-        ENG_BUF(int, leaf_b, kLeaf, db.m_cap * sizeof(int));
-        ENG_BUF(float, tt_b, kT, db.m_cap * sizeof(float));
-        ENG_BUF(int, ray_of_b, kRayOf, db.m_cap * sizeof(int));
-        if (qset.compacted) {  // the sampler compacted in its launch (capacity R · max_steps)
-            leaf_b = static_cast<int *>(qset.a.p[kLeafQ]);
-            tt_b = static_cast<float *>(qset.a.p[kTQ]);
-            ray_of_b = static_cast<int *>(qset.a.p[kRayOfQ]);
-        }
-        ENG_BUF(float, feat_b, kFeat, db.m_cap * 16 * sizeof(float));
-        ENG_BUF(float, sdf_b, kSdfS, db.m_cap * sizeof(float));
-        ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
-        ENG_BUF(float, act_b, kAct, (size_t)psvo_mlp_act_floats(db.m_cap, width) * sizeof(float));
-        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(db.m_cap, width) * sizeof(uint64_t));
-        if (engine_overlap(e) && need_z_event) {  // the loss normalisers need only z (aux)
-            if (hipEventRecord(e->z_ready, st) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
-            o.z_recorded = true;
-        }
-        if (!interp_rays && !qset.compacted) {
-            mark(e, st, PSVO_TIME_POINTS, 0);
-            ENG_CALL(psvo::compact_rays(st, Rq, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, db));
-            mark(e, st, PSVO_TIME_POINTS, 1);
-        }
-        ENG_CALL(join_adam(e, st, who, true));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-        if (interp_rays)
-            ENG_CALL(psvo::interp_fwd_rays(st, Rq, max_steps, d->voxel_size, s_idx, s_depth, offsets, rank_ray,
-                                           rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b, tt_b, ray_of_b,
-                                           feat_b, db));
-        else
-            ENG_CALL(psvo::interp_fwd_dev(st, db, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
-                                          d->centres, d->vertex_idx, d->emb, feat_b));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-        if (early_images) {
-            if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
-        } else if (!prebuilt) {
-            ENG_CALL(mlp_images(st, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
-        }
-        mark(e, st, PSVO_TIME_MLP_FWD, 0);
-        ENG_CALL(psvo::mlp_fwd_dev(st, db, feat_b, images, sdf_b, rgb_b, act_b, masks_b));
-        mark(e, st, PSVO_TIME_MLP_FWD, 1);
-        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
-        z_vals = const_cast<float *>(s_depth);
-        o.z_stride = max_steps;
-        act = act_b, masks = masks_b;
-        dev_done = true;  // unless the batch turns out not to fit
-    } else if (dev_sized) {
-        const psvo::DevBatch db{static_cast<const int *>(qset.a.p[kStatsKeep]), Rq, e->m_cap,
-                                e->s_cap < max_steps ? e->s_cap : max_steps};
-        const size_t RSc = (size_t)Rq * db.s_cap;
-        ENG_BUF(int, leaf_b, kLeaf, db.m_cap * sizeof(int));
-        ENG_BUF(float, tt_b, kT, db.m_cap * sizeof(float));
-        ENG_BUF(int, ray_of_b, kRayOf, db.m_cap * sizeof(int));
-        ENG_BUF(float, z_b, kZ, RSc * sizeof(float));
-        ENG_BUF(uint8_t, smask, kMask, RSc);
-        ENG_BUF(float, feat_b, kFeat, db.m_cap * 16 * sizeof(float));
-        ENG_BUF(float, sdf_b, kSdfS, db.m_cap * sizeof(float));
-        ENG_BUF(float, rgb_b, kRgbS, db.m_cap * 3 * sizeof(float));
-        ENG_BUF(float, act_b, kAct, (size_t)psvo_mlp_act_floats(db.m_cap, width) * sizeof(float));
-        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(db.m_cap, width) * sizeof(uint64_t));
-        mark(e, st, PSVO_TIME_POINTS, 0);
-        ENG_CALL(psvo::sample_points_dev(st, db, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b, z_b,
-                                         smask));
-        mark(e, st, PSVO_TIME_POINTS, 1);
-        if (engine_overlap(e)) {
-            if (hipEventRecord(e->z_ready, st) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
-            o.z_recorded = true;
-        }
-        ENG_CALL(join_adam(e, st, who));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-        ENG_CALL(psvo::interp_fwd_dev(st, db, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
-                                      d->centres, d->vertex_idx, d->emb, feat_b));
-        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-        if (early_images) {
-            if (hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
-        } else if (!prebuilt) {
-            ENG_CALL(mlp_images(st, width, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], images));
-        }
-        mark(e, st, PSVO_TIME_MLP_FWD, 0);
-        ENG_CALL(psvo::mlp_fwd_dev(st, db, feat_b, images, sdf_b, rgb_b, act_b, masks_b));
-        mark(e, st, PSVO_TIME_MLP_FWD, 1);
-        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, z_vals = z_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
-        act = act_b, masks = masks_b;
-        dev_done = true;  // unless the batch turns out not to fit
-    }
+    // the mapping step on one GPU: no padded [R_hit, S_max] copy — the loss
+    // kernels read z from the sampler's depth rows (stride max_steps) and the
+    // samples are compacted ray-major (by the look-back sampler in its own
+    // launch, else k_compact_rays: a wave per hit ray over its ≈ 64 valid
+    // entries); data parallel and tracking: the padded copy the autograd path
+    // makes (k_sample_points)
+    const bool rays_path = fused_loss && want_act && !dist && !(e->paths & PSVO_PATH_PADDED);
     ENG_CALL(spin_wait(qset, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
@@ -1147,123 +1033,84 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.s_max = s_max;
     if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
-    if (dev_done && (M > e->m_cap || (!rays_path && s_max > e->s_cap) || s_max > max_steps || r_hit > Rq))
-        dev_done = false;
-    // the next steps' capacities: this batch with headroom (never shrinking)
-    if (fused_loss && want_act && width == 128 && !dist) {
-        const int64_t mc = M + M / 4 + 256;
-        const int sc = s_max + s_max / 4 + 8;
-        if (mc > e->m_cap) e->m_cap = mc;
-        if (sc > e->s_cap) e->s_cap = sc;
-    }
-    if (!dev_done) {
-        const size_t RS = (size_t)r_hit * s_max;
-        ENG_BUF(int, leaf_b, kLeaf, M * sizeof(int));
-        ENG_BUF(float, tt_b, kT, M * sizeof(float));
-        ENG_BUF(int, ray_of_b, kRayOf, M * sizeof(int));
-        ENG_BUF(float, z_b, kZ, RS * sizeof(float));
-        ENG_BUF(uint8_t, smask, kMask, RS);
-        ENG_BUF(float, feat_b, kFeat, M * 16 * sizeof(float));
-        // PSVO_FUSED_POINTS=1: compaction + interpolation as one launch
-        // (k_points_interp; it reads the embeddings, so the previous step's
-        // optimiser join moves in front of it).  Measured (config B, same
-        // box): 24.5 µs for the one kernel against 6.7 + 13.8 for
-        // the two (half its lanes hold slots past their ray's samples) and
-        // 0.96-0.99 vs 0.94-0.96 ms per iteration, so the split stays default.
-        o.z_stride = 0;  // a device-sized attempt that did not fit: host-sized below
-        o.z_recorded = false;
-        if (rays_path && qset.compacted) {  // the sampler compacted in its launch (look-back offsets)
-            leaf_b = static_cast<int *>(qset.a.p[kLeafQ]);
-            tt_b = static_cast<float *>(qset.a.p[kTQ]);
-            ray_of_b = static_cast<int *>(qset.a.p[kRayOfQ]);
+    ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
+    ENG_BUF(float, tt, kT, M * sizeof(float));
+    ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
+    ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
+    float *z_vals = nullptr;
+    o.z_recorded = false;
+    if (rays_path) {
+        if (qset.compacted) {  // the sampler compacted in its launch (look-back offsets)
+            leaf = static_cast<int *>(qset.a.p[kLeafQ]);
+            tt = static_cast<float *>(qset.a.p[kTQ]);
+            ray_of = static_cast<int *>(qset.a.p[kRayOfQ]);
         }
-        if (rays_path) {
-            // the loss normalisers need only z: aux may start them now (a
-            // marker packet on st: none when aux has nothing to wait for)
-            if (engine_overlap(e) && need_z_event) {
-                if (hipEventRecord(e->z_ready, st) != hipSuccess)
-                    return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
-                o.z_recorded = true;
-            }
-            if (!interp_rays && !qset.compacted) {
-                mark(e, st, PSVO_TIME_POINTS, 0);
-                ENG_CALL(psvo::compact_rays(st, r_hit, max_steps, s_idx, s_depth, offsets, leaf_b, tt_b, ray_of_b,
-                                            psvo::DevBatch{}));
-                mark(e, st, PSVO_TIME_POINTS, 1);
-            }
-            ENG_CALL(join_adam(e, st, who));
-            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-            if (interp_rays)
-                ENG_CALL(psvo::interp_fwd_rays(st, r_hit, max_steps, d->voxel_size, s_idx, s_depth, offsets,
-                                               rank_ray, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, leaf_b,
-                                               tt_b, ray_of_b, feat_b, psvo::DevBatch{}));
-            else
-                ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o,
-                                         rays_d, d->centres, d->vertex_idx, d->emb, feat_b));
-            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-            z_b = const_cast<float *>(s_depth);
-            o.z_stride = max_steps;
-        }
-        if (!rays_path) mark(e, st, PSVO_TIME_POINTS, 0);
-        if (rays_path) {
-        } else if (fuse_pi) {
-            ENG_CALL(psvo::points_interp(st, r_hit, s_max, max_steps, d->voxel_size, s_idx, s_depth, offsets, leaf_b,
-                                         tt_b, ray_of_b, z_b, smask, rank_ray, rays_o, rays_d, d->centres,
-                                         d->vertex_idx, d->emb, feat_b));
-        } else {
-            ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf_b,
-                                        tt_b, ray_of_b, z_b, smask));
-        }
-        if (!rays_path) mark(e, st, PSVO_TIME_POINTS, 1);
-        if (fuse_pi) {  // the interpolation ran inside the points region
-            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
-        }
-        // the loss normalisers can start now (psvo_map_step, on aux; the host
-        // issues aux's wait after the decoder launch: queued before it, their
-        // three launches delay the forward's — measured 1.2 % slower)
-        if (fused_loss && engine_overlap(e) && !rays_path) {
+        // the loss normalisers need only z: aux may start them now (a
+        // marker packet on st: none when aux has nothing to wait for)
+        if (engine_overlap(e) && need_z_event) {
             if (hipEventRecord(e->z_ready, st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
             o.z_recorded = true;
         }
-        // ---- forward: interpolation, decoder, compositing (after the previous
-        // step's optimiser step when its tail ran on aux)
-        if (!fuse_pi && !rays_path) {
-            ENG_CALL(join_adam(e, st, who));
-            mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-            ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf_b, tt_b, ray_of_b, rank_ray, rays_o, rays_d,
-                                     d->centres, d->vertex_idx, d->emb, feat_b));
-            mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        if (!qset.compacted) {
+            mark(e, st, PSVO_TIME_POINTS, 0);
+            ENG_CALL(psvo::compact_rays(st, r_hit, max_steps, s_idx, s_depth, offsets, leaf, tt, ray_of));
+            mark(e, st, PSVO_TIME_POINTS, 1);
         }
-        ENG_BUF(float, sdf_b, kSdfS, M * sizeof(float));
+        z_vals = const_cast<float *>(s_depth);
+        o.z_stride = max_steps;
+    } else {
+        const size_t RS = (size_t)r_hit * s_max;
+        ENG_BUF(float, z_b, kZ, RS * sizeof(float));
+        ENG_BUF(uint8_t, smask, kMask, RS);
+        mark(e, st, PSVO_TIME_POINTS, 0);
+        ENG_CALL(psvo_sample_points(stream, r_hit, s_max, max_steps, s_idx, s_depth, ray_ns, offsets, leaf, tt,
+                                    ray_of, z_b, smask));
+        mark(e, st, PSVO_TIME_POINTS, 1);
+        // the loss normalisers can start now (psvo_map_step, on aux)
+        if (fused_loss && engine_overlap(e)) {
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
+        z_vals = z_b;
+        o.z_stride = s_max;
+    }
+    // ---- forward: interpolation, decoder (after the previous step's
+    // optimiser step when its tail ran on aux)
+    ENG_CALL(join_adam(e, st, who));
+    mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+    ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
+                             d->vertex_idx, d->emb, feat));
+    mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+    ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
+    float *rgb_s = nullptr, *act = nullptr;
+    uint64_t *masks = nullptr;
+    // sparse: the sdf trunk (h1, h2, the sdf row: 18.6 of 53.8 k MACs per
+    // sample) on every sample — the compositing weights need every sdf — and
+    // the full decoder later, on the samples select_samples keeps
+    o.sparse = sparse;
+    if (!sparse) {
         ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
-        float *act_p = nullptr;
+        rgb_s = rgb_b;
         if (want_act) {
             ENG_BUF(float, abuf, kAct, (size_t)psvo_mlp_act_floats(M, width) * sizeof(float));
-            act_p = abuf;
+            act = abuf;
         }
-        ENG_BUF(uint64_t, masks_b, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
-        mark(e, st, PSVO_TIME_MLP_FWD, 0);
-        if (dev_sized) {  // the images were prepared (or waited for) above
-            ENG_CALL(mlp_fwd_prepared(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
-                                      W[9], images, sdf_b, rgb_b, act_p, masks_b));
-        } else if (early_images || prebuilt) {
-            if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
-            ENG_CALL(mlp_fwd_prepared(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
-                                      W[9], images, sdf_b, rgb_b, act_p, masks_b));
-        } else {
-            ENG_CALL(psvo_mlp_fwd(stream, M, width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8],
-                                  W[9], images, sdf_b, rgb_b, act_p, masks_b));
-        }
-        mark(e, st, PSVO_TIME_MLP_FWD, 1);
-        leaf = leaf_b, tt = tt_b, ray_of = ray_of_b, z_vals = z_b, feat = feat_b, sdf_s = sdf_b, rgb_s = rgb_b;
-        act = act_p, masks = masks_b;
+        ENG_BUF(uint64_t, mbuf, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
+        masks = mbuf;
     }
-    o.r_hit = r_hit;
-    o.m = M;
-    o.s_max = s_max;
+    mark(e, st, PSVO_TIME_MLP_FWD, 0);
+    if (early_images || prebuilt) {
+        if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                                  images, sdf_s, rgb_s, act, masks));
+    } else {
+        ENG_CALL(psvo_mlp_fwd(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                              images, sdf_s, rgb_s, act, masks));
+    }
+    mark(e, st, PSVO_TIME_MLP_FWD, 1);
     o.rank_ray = const_cast<int *>(rank_ray);
     o.ray_ns = const_cast<int *>(ray_ns);
     o.offsets = const_cast<int *>(offsets);
@@ -1271,7 +1118,6 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.ray_of = ray_of;
     o.tt = tt;
     o.z_vals = z_vals;
-    if (o.z_stride == 0) o.z_stride = s_max;
     o.feat = feat;
     o.images = images;
     o.sdf_s = sdf_s;
@@ -1444,29 +1290,21 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     }
     // The two cross-stream waits this step needs on st — the previous step's
-    // optimiser (before the interpolation reads the embeddings) and, split,
+    // optimiser (before the interpolation reads the embeddings: render) and
     // the draw of the next pixels (before the look-ahead's pose step) — sit
-    // where their consumers are.  PSVO_LATE_WAITS=0 (A/B) queues both here,
-    // in front of the render (st reaches them right after the queued query's
-    // sampler, while the host reads that query's statistics back): round 3's
-    // default, measured slower in round 4 (config B, one box, three
-    // interleaved pairs: 0.941-0.942 vs 0.928-0.932 ms per iteration) — the
-    // next draw co-runs with the persistent decoder kernels and ends late, so
-    // the render then waits for it.
-    const bool split_tail = fr && fr->next_dirs_cam && overlap && psvo::mlp_bwd_split_tail(d->width) &&
-                            !(flags & PSVO_STEP_NO_ADAM);
-    static const bool late_waits = !(getenv("PSVO_LATE_WAITS") && *getenv("PSVO_LATE_WAITS") == '0');
-    const bool early_next = wait_next && split_tail && !late_waits;
-    if (early_next && hipStreamWaitEvent(st, e->next_ready, 0) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
-    if (!late_waits) ENG_CALL(join_adam(e, st, "map_step"));
+    // where their consumers are.  Queued here, in front of the render, both
+    // measured slower (round 4, config B: 0.941 vs 0.928-0.932 ms per
+    // iteration): the next draw co-runs with the persistent decoder kernels
+    // and ends late, so the render then waits for it.
     const int crit_flags = PSVO_CRIT_USE_COLOR | PSVO_CRIT_USE_DEPTH | PSVO_CRIT_USE_SDF;
     // aux waits for z only to count the normalisers itself, or to mark the
     // rows the width-256 backward's scatter will touch
     const bool coef_known = counts_gt && qset->counts_gt == counts_gt;
     const bool need_z = !coef_known || e->x.on() ||
                         (d->emb_row_flags && !psvo::mlp_bwd_fuses_interp(d->width));
-    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z));
+    // the sparse decoder (width 128): render runs the sdf trunk only
+    const bool sparse_dec = d->width == 128 && !(e->paths & PSVO_PATH_DENSE_DECODER);
+    ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z, sparse_dec));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     const int64_t M = q.m;
@@ -1480,6 +1318,54 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const bool dist = x.on();
     const bool empty = dist && (r_hit == 0 || M == 0);
     const int64_t n_hit = dist ? qset->host_stats[PSVO_STAT_R_HIT] : r_hit;
+    // ---- the sparse decoder: the samples whose gradients can be non-zero
+    // (composited, or inside a loss mask: composite.hip k_select_samples) get
+    // compact indices, then the full decoder forward runs on them — sized on
+    // the device (the kept count never reaches the host)
+    float *const *W = d->dec;
+    Render qb = q;  // what the loss pass and the backward read per sample: the kept samples when sparse
+    int *cidx = nullptr, *sel_cnt = nullptr;
+    if (q.sparse && !empty) {
+        ENG_BUF(int, cx, kCidx, M * sizeof(int));
+        ENG_BUF(int, offb, kOffB, (size_t)(r_hit + 1) * sizeof(int));
+        ENG_BUF(float, feat_b, kFeatB, M * 16 * sizeof(float));
+        ENG_BUF(int, leaf_b, kLeafB, M * sizeof(int));
+        ENG_BUF(float, t_b, kTB, M * sizeof(float));
+        ENG_BUF(int, ray_of_b, kRayOfB, M * sizeof(int));
+        ENG_BUF(int, cnt, kSelCnt, psvo::kSelCountInts * sizeof(int));
+        ENG_BUF(unsigned long long, desc, kSelDesc,
+                (size_t)psvo::select_granules(r_hit) * sizeof(unsigned long long));
+        if (e->sel_zeroed != desc) {  // fresh memory: no stale granule may carry a future tag
+            if (hipMemsetAsync(desc, 0, e->a.cap[kSelDesc], st) != hipSuccess ||
+                hipMemsetAsync(cnt, 0, psvo::kSelCountInts * sizeof(int), st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
+            e->sel_zeroed = desc;
+        }
+        e->sel_tag = e->sel_tag == 0xffffffffu ? 1u : e->sel_tag + 1u;
+        mark(e, st, PSVO_TIME_SELECT, 0);
+        ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
+                                      q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, cx,
+                                      offb, feat_b, leaf_b, t_b, ray_of_b, cnt, desc, e->sel_tag));
+        mark(e, st, PSVO_TIME_SELECT, 1);
+        ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
+        ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
+        ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
+        ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
+        mark(e, st, PSVO_TIME_MLP_FWD, 0);
+        ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                                  q.images, sdf_b, rgb_b, act, masks, cnt));
+        mark(e, st, PSVO_TIME_MLP_FWD, 1);
+        qb.offsets = offb;
+        qb.leaf = leaf_b;
+        qb.tt = t_b;
+        qb.ray_of = ray_of_b;
+        qb.feat = feat_b;
+        qb.rgb_s = rgb_b;
+        qb.act = act;
+        qb.masks = masks;
+        cidx = cx;
+        sel_cnt = cnt;
+    }
     // ---- loss and backward (d loss = 1): normalisers on aux (after the
     // sampler, beside the decoder forward), then one fused per-ray pass
     ENG_BUF(float, crit_ws, kCritWs, psvo_criterion_workspace_floats(r_hit) * sizeof(float));
@@ -1530,8 +1416,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_CALL(psvo_adam_mark_rows(ax, M, q.leaf, d->vertex_idx, mark_into));
     if (!empty)
         ENG_CALL(psvo::composite_loss_z(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns,
-                                        q.z_vals, q.z_stride, q.rank_ray, gt_rgb, gt_depth, q.sdf_s, q.rgb_s, coef,
-                                        crit_ws, color, depth, g_sdf_s, g_rgb_s, want_loss || dist));
+                                        q.z_vals, q.z_stride, q.rank_ray, gt_rgb, gt_depth, q.sdf_s, qb.rgb_s, coef,
+                                        crit_ws, color, depth, g_sdf_s, g_rgb_s, want_loss || dist, cidx));
     // the loss value (not on the gradient path), beside the decoder backward:
     // data parallel on aux (its collective), single GPU on its own stream,
     // joined into st before the optimiser step (loss_out / crit_ws ordered)
@@ -1573,7 +1459,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             off += kDecSizes[i];
         }
     }
-    float *const *W = d->dec;
     ENG_BUF(float, grad_od, kGradOD, (size_t)R * 6 * sizeof(float));
     if (empty) {  // no samples on this rank: its part of the gradient is zero
         ENG_CALL(fork_join(ax, st, e->emb_done));
@@ -1604,83 +1489,29 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_BUF(float, gxb, kIbWs, (size_t)M * 3 * sizeof(float));
         gx = gxb;
     }
-    const psvo::InterpFuse ipf{q.leaf,   q.ray_of,     q.rank_ray, d->vertex_idx, q.tt, rays_o, rays_d, d->centres,
+    const psvo::InterpFuse ipf{qb.leaf,  qb.ray_of,    q.rank_ray, d->vertex_idx, qb.tt, rays_o, rays_d, d->centres,
                                d->emb,   d->voxel_size, grad_emb,   gx,            mark_into};
-    // width 256 without the fused interpolation backward: k_interp_bwd runs
-    // beside the weight-gradient kernels on aux, or (PSVO_IB256_SERIAL=1)
-    // between the δ chain and them on st, with the whole chip to itself
-    const char *ibs = getenv("PSVO_IB256_SERIAL");
-    const bool ib_serial = !fuse_ib && ibs && *ibs == '1';
-    float *ib_ws = nullptr;
-    if (ib_serial) {
-        ENG_BUF(float, ibw, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
-        ib_ws = ibw;
-    }
-    struct IbCtx {
-        psvo_engine *e;
-        const Render *q;
-        const psvo_map_desc *d;
-        const float *rays_o, *rays_d, *dfeat;
-        float *grad_emb, *grad_od, *ws;
-        int64_t R;
-        bool dirty;
-    };
-    float *dfeat_p = dfeat;
-    IbCtx ibc{e, &q, d, rays_o, rays_d, dfeat_p, grad_emb, grad_od, ib_ws, R, emb_dirty};
-    const psvo::BwdHook ib_hook{[](void *c, hipStream_t s) -> int {
-                                    const IbCtx &x = *static_cast<const IbCtx *>(c);
-                                    if (x.dirty && hipMemsetAsync(x.grad_emb, 0, (size_t)x.d->n_emb * 16 * sizeof(float),
-                                                                  s) != hipSuccess)
-                                        return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
-                                    mark(x.e, s, PSVO_TIME_INTERP_BWD, 0);
-                                    const int rc = psvo_interp_bwd_chunked(
-                                        s, x.q->r_hit, x.q->s_max, 16, x.d->voxel_size, x.q->offsets, x.q->rank_ray,
-                                        x.q->leaf, x.q->tt, x.rays_o, x.rays_d, x.d->centres, x.d->vertex_idx,
-                                        x.d->emb, x.dfeat, x.grad_emb, x.grad_od, x.grad_od + x.R * 3, x.ws);
-                                    mark(x.e, s, PSVO_TIME_INTERP_BWD, 1);
-                                    return rc;
-                                },
-                                &ibc};
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
-    ENG_CALL(mlp_bwd(st, M, d->width, q.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
-                     q.rgb_s, q.act, q.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6], G[7],
-                     G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr, fuse_ib ? &ipf : nullptr,
-                     split ? ax : nullptr, ib_serial ? &ib_hook : nullptr));
+    ENG_CALL(mlp_bwd(st, M, d->width, qb.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
+                     qb.rgb_s, qb.act, qb.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6],
+                     G[7], G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr,
+                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     if (overlap) e->bwd_recorded = true;  // mlp_bwd recorded dfeat_ready on st
-    // PSVO_PREFETCH=1 (A/B, off by default): warm the XCD L2s with the
-    // query's / the interpolation's read-only arrays (maps whose arrays fit)
-    // while the per-ray sums and the pose step run.  Measured (config B, one
-    // box, three interleaved pairs): the intersect region 26.2-28.1 ->
-    // 24.4-26.7 us, but the iteration 0.922-0.938 -> 0.946-0.948 ms — the
-    // sweep competes with the step's tail on the other queues
-    static const bool prefetch = getenv("PSVO_PREFETCH") && *getenv("PSVO_PREFETCH") == '1';
-    if (prefetch && split && !dist && e->lossq) {
-        const int64_t nn = d->n_nodes;
-        const void *pp[4] = {d->packed, d->vertex_idx, d->centres, d->emb};
-        const int64_t pb[4] = {d->packed ? nn * 32 : 0, nn * 8 * 4, nn * 3 * 4 / 16 * 16, d->n_emb * 16 * 4};
-        if (pb[0] + pb[1] + pb[2] + pb[3] <= (int64_t)3 << 20) {
-            if (!e->pf_sink && hipMalloc(reinterpret_cast<void **>(&e->pf_sink), 64) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "map_step: hipMalloc failed");
-            ENG_CALL(fork_join(st, e->lossq, e->pf_fork));
-            ENG_CALL(psvo::l2_prefetch(e->lossq, 4, pp, pb, e->pf_sink));
-        }
-    }
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
-    // (ib_serial: it ran inside mlp_bwd, on st)
-    hipStream_t eb = (split || ib_serial) ? st : ax;
+    hipStream_t eb = split ? st : ax;
     if (overlap && eb != st && hipStreamWaitEvent(eb, e->dfeat_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
-    if (!fuse_ib && !ib_serial && emb_dirty &&
+    if (!fuse_ib && emb_dirty &&
         hipMemsetAsync(grad_emb, 0, (size_t)d->n_emb * 16 * sizeof(float), eb) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     e->grads_clean = false;
     e->clean_buf = grad_emb;
     if (fuse_ib) {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
-        ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, q.offsets, q.rank_ray, q.tt, gx, grad_od, grad_od + R * 3));
+        ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, qb.offsets, q.rank_ray, qb.tt, gx, grad_od, grad_od + R * 3));
         mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
-    } else if (!ib_serial) {
+    } else {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
         ENG_BUF(float, ib_ws2, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
         ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf,
@@ -1704,7 +1535,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // next iteration's rays + query there too — beside this step's weight
     // gradients and the map's Adam
     if (ahead) {
-        if (wait_next && !early_next && hipStreamWaitEvent(eb, e->next_ready, 0) != hipSuccess)
+        if (wait_next && hipStreamWaitEvent(eb, e->next_ready, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
         // queued on the step's own stream (split tail): consumed there, no event
         ENG_CALL(frames_lookahead(e, eb, d, fr, R, q, grad_od, eb != st));
@@ -1826,8 +1657,8 @@ extern "C" int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc 
 
 extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc *d, int64_t n_rays,
                                const float *dirs_cam, const float *gt_rgb, const float *gt_depth, float *pose,
-                               float *pose_m, float *pose_v, double lr, uint64_t seed, int64_t adam_step, int flags,
-                               float *pose_grad, float *loss_out, int *stats_out) {
+                               float *pose_m, float *pose_v, double lr, const float *noise, uint64_t seed,
+                               int64_t adam_step, int flags, float *pose_grad, float *loss_out, int *stats_out) {
     PSVO_REQUIRE(e && d && dirs_cam && gt_rgb && gt_depth && pose && loss_out, "track_step: null argument");
     e->images_next = false;  // the weights may change before the next step
     PSVO_REQUIRE(n_rays > 0 && adam_step >= 1, "track_step: bad sizes");
@@ -1845,7 +1676,7 @@ extern "C" int psvo_track_step(psvo_engine *e, void *stream, const psvo_map_desc
     PSVO_REQUIRE(e->q_count == 0, "track_step: the engine has queued mapping queries");
     PSVO_REQUIRE(!e->x.on(), "track_step: tracking runs on one GPU (SURVEY §8e: its median filter is global)");
     QuerySet *qset = nullptr;
-    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "track_step", &qset));
+    ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "track_step", &qset, noise));
     QueryGuard guard{e, st, qset};
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, false, stats_out, "track_step", q));
     // ---- loss (optionally with the median depth filter) and backward

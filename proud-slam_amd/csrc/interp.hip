@@ -45,9 +45,7 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
                                                     const float *__restrict__ rays_d,
                                                     const float *__restrict__ centres,
                                                     const int *__restrict__ vertex_idx,
-                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat,
-                                                    DevBatch dev) {
-    if (dev.stats) m = dev_batch_m(dev);  // device-sized launch (DevBatch)
+                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = g >> 2;
     const int q = (int)(g & 3);
@@ -76,137 +74,6 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
         acc.w = acc.w + w[k] * e.w;
     }
     feat[s * 4 + q] = acc;
-}
-
-// Sample compaction + interpolation forward for the engine's mapping path,
-// one wave per hit ray: the ray's valid samples — the prefix s < ns of its
-// sampler row s_idx / s_depth [R, cap] — go to the compact, ray-major
-// positions offsets[r] + s as leaf / t / ray_of_sample (what the backward
-// reads) and as features; the ray's origin / direction and offsets are loaded
-// once per wave, not per sample.  Four lanes per sample, 16 samples per pass;
-// a pass's lanes idle only past the ray's last sample (the slot-grid
-// k_points_interp below left half its lanes on empty slots).  Same arithmetic
-// as k_interp_fwd, so the same bits.
-__global__ __launch_bounds__(256) void k_interp_fwd_rays(int64_t r_hit, int cap, float voxel_size,
-                                                         const int *__restrict__ s_idx,
-                                                         const float *__restrict__ s_depth,
-                                                         const int *__restrict__ offsets,
-                                                         const int *__restrict__ ray_index,
-                                                         const float *__restrict__ rays_o,
-                                                         const float *__restrict__ rays_d,
-                                                         const float *__restrict__ centres,
-                                                         const int *__restrict__ vertex_idx,
-                                                         const float4 *__restrict__ emb, int *__restrict__ leaf,
-                                                         float *__restrict__ t, int *__restrict__ ray_of_sample,
-                                                         float4 *__restrict__ feat, DevBatch dev) {
-    if (dev.stats) r_hit = dev_batch_fits(dev) ? dev.stats[PSVO_STAT_R_HIT] : 0;
-    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (r >= r_hit) return;
-    const int lane = threadIdx.x & 63;
-    const int q = lane & 3;
-    const int beg = offsets[r], ns = offsets[r + 1] - beg;
-    const int64_t ray = ray_index ? ray_index[r] : r;
-    const float o[3] = {rays_o[ray * 3 + 0], rays_o[ray * 3 + 1], rays_o[ray * 3 + 2]};
-    const float d[3] = {rays_d[ray * 3 + 0], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]};
-    const int *row_i = s_idx + r * cap;
-    const float *row_z = s_depth + r * cap;
-    for (int s = lane >> 2; s < ns; s += kWave / 4) {
-        const int lf = row_i[s];
-        const float ts = row_z[s];
-        const int64_t m = beg + s;
-        if (q == 0) {
-            leaf[m] = lf;
-            t[m] = ts;
-            ray_of_sample[m] = (int)r;
-        }
-        float p[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float x = o[a] + d[a] * ts;
-            p[a] = __fdiv_rn(x - centres[(int64_t)lf * 3 + a], voxel_size) + 0.5f;
-        }
-        float w[8];
-        corner_weights(p[0], p[1], p[2], w);
-        const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8);
-        const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)lf * 8 + 4);
-        const int vid[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float4 e = emb[(int64_t)vid[k] * 4 + q];
-            acc.x = acc.x + w[k] * e.x;
-            acc.y = acc.y + w[k] * e.y;
-            acc.z = acc.z + w[k] * e.z;
-            acc.w = acc.w + w[k] * e.w;
-        }
-        feat[m * 4 + q] = acc;
-    }
-}
-
-// k_sample_points and k_interp_fwd in one pass over the sampler's [R_hit, cap]
-// rows (engine, host-sized forward): four lanes per (hit ray, step) slot; a
-// valid slot (a prefix of its row) interpolates straight from the sampler's
-// voxel id and depth, and its q = 0 lane writes the compacted leaf / t /
-// ray_of_sample and the [R_hit, S_max] z_vals / mask entries of the slot.
-// Same arithmetic as the two kernels (same bits); the compacted arrays are
-// not read back, and one launch and the stream gap between the two go.
-__global__ __launch_bounds__(256) void k_points_interp(int64_t r_hit, int s_max, int cap, float voxel_size,
-                                                       const int *__restrict__ s_idx,
-                                                       const float *__restrict__ s_depth,
-                                                       const int *__restrict__ offsets, int *__restrict__ leaf,
-                                                       float *__restrict__ t, int *__restrict__ ray_of_sample,
-                                                       float *__restrict__ z_vals, uint8_t *__restrict__ mask,
-                                                       const int *__restrict__ ray_index,
-                                                       const float *__restrict__ rays_o,
-                                                       const float *__restrict__ rays_d,
-                                                       const float *__restrict__ centres,
-                                                       const int *__restrict__ vertex_idx,
-                                                       const float4 *__restrict__ emb, float4 *__restrict__ feat) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int s = g >> 2;
-    const int q = g & 3;
-    if (s >= s_max) return;
-    for (int64_t r = blockIdx.y; r < r_hit; r += gridDim.y) {
-        // valid samples form a prefix of each row; past it the padding
-        // (-1, MAX_DEPTH) is implied — the look-back sampler does not write it
-        const bool in = s < offsets[r + 1] - offsets[r];
-        const int v = in ? s_idx[r * cap + s] : -1;
-        const float z = in ? s_depth[r * cap + s] : kMaxDepthFill;
-        const int64_t o = offsets[r] + s;
-        if (q == 0) {
-            const int64_t e = r * s_max + s;
-            z_vals[e] = z;
-            mask[e] = v != -1;
-            if (v != -1) {
-                leaf[o] = v;
-                t[o] = z;
-                ray_of_sample[o] = (int)r;
-            }
-        }
-        if (v == -1) continue;
-        const int ray = ray_index ? ray_index[r] : (int)r;
-        float p[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float x = rays_o[(int64_t)ray * 3 + a] + rays_d[(int64_t)ray * 3 + a] * z;
-            p[a] = __fdiv_rn(x - centres[(int64_t)v * 3 + a], voxel_size) + 0.5f;
-        }
-        float w[8];
-        corner_weights(p[0], p[1], p[2], w);
-        const int4 v0 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)v * 8);
-        const int4 v1 = *reinterpret_cast<const int4 *>(vertex_idx + (int64_t)v * 8 + 4);
-        const int vid[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float4 e4 = emb[(int64_t)vid[k] * 4 + q];
-            acc.x = acc.x + w[k] * e4.x;
-            acc.y = acc.y + w[k] * e4.y;
-            acc.z = acc.z + w[k] * e4.z;
-            acc.w = acc.w + w[k] * e4.w;
-        }
-        feat[o * 4 + q] = acc;
-    }
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -492,50 +359,10 @@ extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size,
     psvo::launch(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
                        t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb),
-                       reinterpret_cast<float4 *>(feat), DevBatch{});
+                       reinterpret_cast<float4 *>(feat));
     return check_launch("interp_fwd");
 }
 
-namespace psvo {
-int interp_fwd_rays(hipStream_t st, int64_t r_hit, int cap, float voxel_size, const int *s_idx, const float *s_depth,
-                    const int *offsets, const int *ray_index, const float *rays_o, const float *rays_d,
-                    const float *centres, const int *vertex_idx, const float *emb, int *leaf, float *t,
-                    int *ray_of_sample, float *feat, const DevBatch &dev) {
-    PSVO_REQUIRE(r_hit >= 0 && cap > 0 && voxel_size > 0.f, "interp_fwd_rays: bad sizes");
-    if (r_hit == 0) return PSVO_OK;
-    psvo::launch(k_interp_fwd_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, voxel_size, s_idx,
-                       s_depth, offsets, ray_index, rays_o, rays_d, centres, vertex_idx,
-                       reinterpret_cast<const float4 *>(emb), leaf, t, ray_of_sample, reinterpret_cast<float4 *>(feat),
-                       dev);
-    return check_launch("interp_fwd_rays");
-}
-
-int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
-                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
-                   const float *centres, const int *vertex_idx, const float *emb, float *feat) {
-    PSVO_REQUIRE(b.stats && b.m_cap > 0 && voxel_size > 0.f, "interp_fwd_dev: bad sizes");
-    psvo::launch(k_interp_fwd, dim3(div_up(b.m_cap * 4, 256)), dim3(256), 0, st, b.m_cap, voxel_size, leaf, t,
-                       ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
-                       reinterpret_cast<const float4 *>(emb), reinterpret_cast<float4 *>(feat), b);
-    return check_launch("interp_fwd_dev");
-}
-
-int points_interp(hipStream_t st, int64_t r_hit, int s_max, int max_steps_cap, float voxel_size, const int *s_idx,
-                  const float *s_depth, const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals,
-                  uint8_t *mask, const int *ray_index, const float *rays_o, const float *rays_d,
-                  const float *centres, const int *vertex_idx, const float *emb, float *feat) {
-    PSVO_REQUIRE(r_hit >= 0 && s_max >= 0 && s_max <= max_steps_cap && voxel_size > 0.f,
-                 "points_interp: bad sizes");
-    if (r_hit == 0 || s_max == 0) return PSVO_OK;
-    const int bx = s_max <= 16 ? 64 : s_max <= 32 ? 128 : 256;  // 4 lanes per slot
-    const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
-    psvo::launch(k_points_interp, dim3(div_up((int64_t)s_max * 4, bx), gy), dim3(bx), 0, st, r_hit, s_max,
-                       max_steps_cap, voxel_size, s_idx, s_depth, offsets, leaf, t, ray_of_sample, z_vals, mask,
-                       ray_index, rays_o, rays_d, centres, vertex_idx, reinterpret_cast<const float4 *>(emb),
-                       reinterpret_cast<float4 *>(feat));
-    return check_launch("points_interp");
-}
-}  // namespace psvo
 
 extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets,
                                const int *ray_index, const int *leaf, const float *t, const float *rays_o, const float *rays_d,

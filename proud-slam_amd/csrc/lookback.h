@@ -20,11 +20,17 @@
 // combine by sum, or by max where bit g of MAXMASK is set (all values ≥ 0,
 // 0 is the identity of both).
 //
-// Progress: a workgroup waits only for lower-numbered workgroups; workgroups
-// are dispatched in index order, so the lowest unfinished one is resident.
-// A wait that never ends (a bug) is abandoned after kLbSpinMax re-reads
-// (≳ 65 ms): lb_scan returns false, the caller raises PSVO_STAT_FLAGS bit 3
-// and the engine reports the batch as failed — the grid still drains.
+// Progress: a workgroup waits only for lower-numbered workgroups.  On a
+// multi-XCD part the workgroups are dealt round-robin to the XCDs and each
+// XCD dispatches its share in index order, so on every XCD the lowest
+// unfinished workgroup is resident once it holds a slot; a waiter can still
+// spin while a lower workgroup of another XCD is queued behind a co-running
+// kernel (e.g. the width-256 dW kernel at one workgroup per CU) — the wait
+// then lasts as long as that kernel holds the CUs.  A wait that never ends
+// (a bug) is abandoned after kLbSpinMax re-reads (≳ 65 ms): lb_scan returns
+// false, the caller raises PSVO_STAT_FLAGS bit 3, stores no rank / offset /
+// compacted sample from the undefined prefix, and the engine reports the
+// batch as failed — the grid still drains.
 #pragma once
 #include "psvo_common.h"
 

@@ -38,8 +38,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kW = 128;     // decoder width
 constexpr int kIn = 16;     // embedding dim
 constexpr int kNB = kW / 32;
-constexpr int kTile = 128;  // samples per workgroup
-constexpr int kThreads = 256;
 
 // LDS carve (floats): small vectors first, then the staged weight image.
 constexpr int kOffB1 = 0, kOffB2 = kOffB1 + 128, kOffB3 = kOffB2 + 128, kOffB4 = kOffB3 + 132,
@@ -47,9 +45,6 @@ constexpr int kOffB1 = 0, kOffB2 = kOffB1 + 128, kOffB3 = kOffB2 + 128, kOffB4 =
 constexpr int kOffW3r0 = kOffB5 + 4, kOffW5 = kOffW3r0 + 128;  // W3 row 0 (sdf), W5 [3][128]
 constexpr int kOffW = kOffW5 + 3 * 128;               // = 1032 floats (16-B aligned)
 constexpr int kImgFwd = 128 * 144;                    // largest forward image (W4)
-constexpr int kImgBwd = 160 * 128;                    // largest backward image (W4ᵀ, 5 x 4 blocks)
-constexpr int kLdsFwd = (kOffW + kImgFwd) * 4;        // 77,856 B → 2 workgroups / CU
-constexpr int kLdsBwd = (kOffW + kImgBwd) * 4;        // 86,048 B
 
 __device__ __forceinline__ int phi(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -314,10 +309,9 @@ struct CfQueue {
 // kernels read it, built once per weight update by k_mlp_prep (a gather,
 // coalesced writes) so that staging is a straight 16-B copy.
 //   fwd: W1 (perm_x), W2, W3 rows 1..128 (perm_acc), W4 ([f | x])
-//   bwd: W4ᵀ (5 product blocks), W3ᵀ rows 1..128, W2ᵀ, W1ᵀ (1 block)
+//   bwd (k_mlp_bwd3's chain): W4ᵀ, W3[1:]ᵀ, W2ᵀ, W1ᵀ as 16 × 16 blocks
 constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF4 = kImgF3 + 16384,
-              kImgB4 = kImgF4 + 18432, kImgB3 = kImgB4 + 20480, kImgB2 = kImgB3 + 16384, kImgB1 = kImgB2 + 16384,
-              kImgVec = kImgB1 + 4096,    // the small vectors in their LDS layout (kOffB1..kOffW), padded
+              kImgVec = kImgF4 + 18432,   // the small vectors in their LDS layout (kOffB1..kOffW), padded
               kVecPad = 1280,             // to whole 1-KB glds pieces
               // k_mlp_bwd3's chain (v_mfma_f32_16x16x4_f32, 16-sample units): Wᵀ as 16 × 16
               // blocks (ob, kb), lane (m, q) holding Wᵀ[16ob + m][16kb + 4q .. 4q + 3]
@@ -325,7 +319,7 @@ constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF
               kImgC3 = kImgC4 + 9 * 8 * 256,  // W3[1:]ᵀ
               kImgC2 = kImgC3 + 8 * 8 * 256,  // W2ᵀ
               kImgC1 = kImgC2 + 8 * 8 * 256,  // W1ᵀ: 1 × 8 blocks
-              kImgTotal = kImgC1 + 8 * 256;   // 165,120 floats
+              kImgTotal = kImgC1 + 8 * 256;   // 107,776 floats
 
 __device__ __forceinline__ void inv_perm_acc(int pos, int nkb, int &i, int &k) {
     const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
@@ -386,7 +380,7 @@ __global__ __launch_bounds__(256) void k_mlp_prep(MlpParams p, float *__restrict
     } else if (e < kImgF4) {
         inv_perm_acc(e - kImgF3, 4, i, k);
         v = w3[(i + 1) * 128 + k];
-    } else if (e < kImgB4) {
+    } else {
         const int pos = e - kImgF4;
         if (pos < 16384) {
             inv_perm_acc(pos, 4, i, k);
@@ -395,18 +389,6 @@ __global__ __launch_bounds__(256) void k_mlp_prep(MlpParams p, float *__restrict
             inv_perm_x(pos - 16384, i, k);
             v = w4[i * 144 + 128 + k];
         }
-    } else if (e < kImgB3) {  // W4ᵀ: product row i = column of W4 (< 144), reduction k = row of W4
-        inv_perm_acc(e - kImgB4, 4, i, k);
-        v = i < 144 ? w4[k * 144 + i] : 0.0f;
-    } else if (e < kImgB2) {
-        inv_perm_acc(e - kImgB3, 4, i, k);
-        v = w3[(k + 1) * 128 + i];
-    } else if (e < kImgB1) {
-        inv_perm_acc(e - kImgB2, 4, i, k);
-        v = w2[k * 128 + i];
-    } else {
-        inv_perm_acc(e - kImgB1, 4, i, k);
-        v = i < 16 ? w1[k * 16 + i] : 0.0f;
     }
     img[e] = v;
 }
@@ -421,38 +403,6 @@ __device__ __forceinline__ void raw_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// n floats (n % (4 NT) == 0 up to a tail) of a prepared image → LDS: batches
-// of 8 16-B loads in flight per thread before their LDS writes
-template <int NT>
-__device__ __forceinline__ void copy_img(float *wl, const float *__restrict__ img, int n) {
-    const float4 *src = reinterpret_cast<const float4 *>(img);
-    float4 *dst = reinterpret_cast<float4 *>(wl);
-    const int n4 = n >> 2;
-    int e = threadIdx.x;
-    for (; e + 7 * NT < n4; e += 8 * NT) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[e + u * NT];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dst[e + u * NT] = v[u];
-    }
-    for (; e < n4; e += NT) dst[e] = src[e];
-}
-
-__device__ __forceinline__ void stage_vectors(float *lds, const MlpParams &p) {
-    for (int e = threadIdx.x; e < 128; e += kThreads) {
-        lds[kOffB1 + e] = p.b1[e];
-        lds[kOffB2 + e] = p.b2[e];
-        lds[kOffB4 + e] = p.b4[e];
-        lds[kOffW3r0 + e] = p.w3[e];  // W3 row 0 (sdf)
-        lds[kOffW5 + e] = p.w5[e];
-        lds[kOffW5 + 128 + e] = p.w5[128 + e];
-        lds[kOffW5 + 256 + e] = p.w5[256 + e];
-    }
-    for (int e = threadIdx.x; e < 129; e += kThreads) lds[kOffB3 + e] = p.b3[e];
-    if (threadIdx.x < 3) lds[kOffB5 + threadIdx.x] = p.b5[threadIdx.x];
-}
-
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 __device__ __forceinline__ void load_x(const float *__restrict__ feat, int64_t s, bool valid, int h, float (&x)[8]) {
@@ -460,204 +410,6 @@ __device__ __forceinline__ void load_x(const float *__restrict__ feat, int64_t s
 #pragma unroll
     for (int t = 0; t < 8; ++t) x[t] = valid ? fr[2 * t + h] : 0.0f;
 }
-
-// ---------------------------------------------------------------------------
-// forward: feat[M,16] → sdf[M], rgb[M,3].  Training mode (act != null) also
-// stores the row-major activations the weight gradients need
-// (act = [h1 | h2 | f | c1], each [M][128]) and the ReLU masks of h1, h2, c1
-// (masks [M][2][3] u64: lane-half h of sample s holds bits of its 64
-// features), so the backward never re-runs the forward.
-__global__ __launch_bounds__(kThreads, 2) void k_mlp_fwd(int64_t m, const float *__restrict__ feat, MlpParams p,
-                                                         const float *__restrict__ img,
-                                                         float *__restrict__ sdf_out, float *__restrict__ rgb_out,
-                                                         float *__restrict__ act, uint64_t *__restrict__ masks) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *wl = lds + kOffW;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int h = lane >> 5;
-    const int64_t s = (int64_t)blockIdx.x * kTile + wave * 32 + (lane & 31);
-    const bool valid = s < m;
-    const bool save = act != nullptr;
-    float x[8];
-    load_x(feat, s, valid, h, x);
-    stage_vectors(lds, p);
-    copy_img<kThreads>(wl, img + kImgF1, 2048);
-    raw_barrier();
-    f32x16 a[kNB], bacc[kNB];
-    init_bias(a, lds + kOffB1, h);
-    gemm_x(wl, x, a, lane);
-    const uint64_t m1 = relu(a);  // h1
-    const int64_t tile = (int64_t)blockIdx.x * (kTile / 32) + wave;
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;   // CF matrices hold whole 64-sample chunks
-    const int64_t tstride = n_tiles * 32 * 128;        // floats per CF matrix
-    const int64_t tbytes = tstride * 4;                // < 2^31 (psvo_mlp_fwd checks m)
-    const CfStore cfs(tile, lane, n_tiles);
-    if (save) cfs.store(act, tbytes, a);
-    raw_barrier();
-    copy_img<kThreads>(wl, img + kImgF2, 16384);
-    raw_barrier();
-    init_bias(bacc, lds + kOffB2, h);
-    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    const uint64_t m2 = relu(bacc);  // h2
-    if (save) cfs.store(act + tstride, tbytes, bacc);
-    raw_barrier();
-    copy_img<kThreads>(wl, img + kImgF3, 16384);  // W3 rows 1..128 → f
-    raw_barrier();
-    const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
-    init_bias(a, lds + kOffB3 + 1, h);
-    gemm_acc<kNB, kNB>(wl, bacc, a, lane);  // f
-    if (save) cfs.store(act + 2 * tstride, tbytes, a);
-    raw_barrier();
-    copy_img<kThreads>(wl, img + kImgF4, 18432);  // W4: [f | x]
-    raw_barrier();
-    init_bias(bacc, lds + kOffB4, h);
-    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    gemm_x(wl + kNB * kNB * 16 * 64, x, bacc, lane);
-    const uint64_t m4 = relu(bacc);  // c1
-    if (save) cfs.store(act + 3 * tstride, tbytes, bacc);
-    if (masks != nullptr && valid) {
-        uint64_t *mk = masks + (s * 2 + h) * 3;
-        mk[0] = m1;
-        mk[1] = m2;
-        mk[2] = m4;
-    }
-    float rgb[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf(lds[kOffB5 + c] + row_dot(lds + kOffW5 + 128 * c, bacc, h));
-    if (valid && h == 0) {
-        sdf_out[s] = sdf;
-        rgb_out[s * 3 + 0] = rgb[0];
-        rgb_out[s * 3 + 1] = rgb[1];
-        rgb_out[s * 3 + 2] = rgb[2];
-    }
-}
-
-// ---------------------------------------------------------------------------
-// backward (data): chain the δ's from (g_sdf, g_rgb) down to dx using the
-// forward's rgb and ReLU masks.  Writes the row-major δ operands of the
-// weight gradients: D1 = δh1, D2 = δh2, D3 = δf, D4 = δc1 [M][128] (post
-// mask), D5 = δ(rgb logits) [M][3], and dfeat [M][16].
-struct BwdOut {
-    float *d1, *d2, *d3, *d4, *d5, *dfeat;
-};
-
-constexpr int kThreadsBwd = 512;
-constexpr int kTileBwd = 256;
-
-__global__ __launch_bounds__(kThreadsBwd, 1) void k_mlp_bwd_data(int64_t m, MlpParams p,
-                                                                 const float *__restrict__ img,
-                                                                 const float *__restrict__ rgb_in,
-                                                                 const uint64_t *__restrict__ masks,
-                                                                 const float *__restrict__ g_sdf,
-                                                                 const float *__restrict__ g_rgb, BwdOut o) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *wl = lds + kOffW;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int h = lane >> 5;
-    const int64_t s = (int64_t)blockIdx.x * kTileBwd + wave * 32 + (lane & 31);
-    const bool valid = s < m;
-    const int64_t tile = (int64_t)blockIdx.x * (kTileBwd / 32) + wave;
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
-    const int64_t tbytes = n_tiles * 32 * 128 * 4;
-    const CfStore cfs(tile, lane, n_tiles);
-    uint64_t m1 = 0, m2 = 0, m4 = 0;
-    float d5[3] = {0.f, 0.f, 0.f};
-    float dsdf = 0.0f;
-    if (valid) {
-        const uint64_t *mk = masks + (s * 2 + h) * 3;
-        m1 = mk[0];
-        m2 = mk[1];
-        m4 = mk[2];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float y = rgb_in[s * 3 + c];
-            d5[c] = g_rgb[s * 3 + c] * (y * (1.0f - y));  // sigmoid backward
-        }
-        dsdf = g_sdf[s];
-    }
-    if (valid && h == 0) {
-        o.d5[s * 3 + 0] = d5[0];
-        o.d5[s * 3 + 1] = d5[1];
-        o.d5[s * 3 + 2] = d5[2];
-    }
-    stage_vectors(lds, p);
-    // ---- δc1 = W5ᵀ δ5 ⊙ mask (VALU); overlap with the W4ᵀ staging
-    copy_img<kThreadsBwd>(wl, img + kImgB4, 20480);
-    raw_barrier();
-    f32x16 a[kNB], bacc[kNB];
-#pragma unroll
-    for (int b = 0; b < kNB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int k = 32 * b + phi(r, h);
-            const float v = lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
-            bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
-        }
-    cfs.store(o.d4, tbytes, bacc);
-    // ---- [δf ; δx_c] = W4ᵀ δc1   (5 row blocks: f rows 0..127, x rows 128..143)
-    f32x16 t5[5];
-    zero(t5);
-    gemm_acc<kNB, 5>(wl, bacc, t5, lane);
-    float dxc[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
-#pragma unroll
-    for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-    cfs.store(o.d3, tbytes, a);
-    // ---- δh2 = (W3[1:]ᵀ δf + W3[0]ᵀ δsdf) ⊙ mask
-    raw_barrier();
-    copy_img<kThreadsBwd>(wl, img + kImgB3, 16384);
-    raw_barrier();
-#pragma unroll
-    for (int b = 0; b < kNB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
-    gemm_acc<kNB, kNB>(wl, a, bacc, lane);
-    apply_mask(bacc, m2);
-    cfs.store(o.d2, tbytes, bacc);
-    // ---- δh1 = W2ᵀ δh2 ⊙ mask
-    raw_barrier();
-    copy_img<kThreadsBwd>(wl, img + kImgB2, 16384);
-    raw_barrier();
-    zero(a);
-    gemm_acc<kNB, kNB>(wl, bacc, a, lane);
-    apply_mask(a, m1);
-    cfs.store(o.d1, tbytes, a);
-    // ---- dx = W1ᵀ δh1 + δx_c   (one row block, rows 0..15 valid)
-    raw_barrier();
-    copy_img<kThreadsBwd>(wl, img + kImgB1, 4096);
-    raw_barrier();
-    f32x16 t1[1];
-    zero(t1);
-    gemm_acc<kNB, 1>(wl, a, t1, lane);
-    if (valid) {
-        float *dst = o.dfeat + s * kIn;
-#pragma unroll
-        for (int rg = 0; rg < 2; ++rg)
-            *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
-                make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
-                            t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// backward (weights) operands (k_mlp_dw2 below):
-//   L0: W1 128x16   D = δh1 | A = x (16 rows from feat, 16 zero rows); W5 3x128 = δ5 ⊗ c1
-//   L1: W2 128x128  D = δh2 | A = h1
-//   L2: W3 rows 1..128 D = δf | A = h2 (+ the sdf row g_sdf ⊗ h2, db3)
-//   L3: W4 128x144  D = δc1 | A = [f | x]
-struct DwSrc {
-    const float *D[4];  // CF: δh1, δh2, δf, δc1
-    const float *A[4];  // CF: (unused), h1, h2, f
-    const float *c1;    // CF
-    const float *d5;    // [M][3]
-    const float *feat;  // [M][16]
-    const float *g_sdf; // [M]
-};
-
-constexpr int kDwA = 160;  // A image rows (W4: 128 f + 16 x + 16 zero)
 
 // global → LDS copies (global_load_lds_*): LDS destination = wave-uniform
 // base (M0) + lane × size.  Issued through inline asm so that the compiler's
@@ -670,13 +422,6 @@ __device__ __forceinline__ uint32_t lds_addr(const float *l) {
 __device__ __forceinline__ void glds16(const float *g, float *l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(l)))
-                 : "memory");
-}
-__device__ __forceinline__ void glds4(const float *g, float *l) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(l)))
                  : "memory");
@@ -710,9 +455,7 @@ __device__ __forceinline__ void dw_store(float *slab, int cols, int row_off, int
         }
 }
 
-// Double-buffered stage: D [128][64], A [160][64] CF images, raw x rows
-// [64][16] and raw per-sample scalars (g_sdf or δ5 [64][3]), all filled by
-// global_load_lds; the raw pieces are re-laid out LDS→LDS after landing.
+// s_waitcnt vmcnt(n) for this wave's global_load_lds copies (the kernels count them)
 __device__ __forceinline__ void wait_vm(int n) {
     // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima); n <= 63
     asm volatile("" ::: "memory");
@@ -738,315 +481,6 @@ struct DwGrid {
     int slab_off[5];  // float offset of matrix l's first slab
     int slab_len[5];  // rows*cols + rows
 };
-
-// ---------------------------------------------------------------------------
-// weight gradients: dW_L = Σ_s δ_L[:, s] ⊗ a_{L-1}[:, s] (+ biases, the W3 sdf
-// row, W5), split-K over 32-sample CF tiles: workgroup (layer L, split) sums
-// a contiguous range of tiles into its slab; k_mlp_dw_reduce adds the slabs.
-// Tiles stream through a ring of 4 LDS stages with three in flight while one
-// is consumed (straight 1-KB global_load_lds copies: the CF tile IS the
-// operand image; the x rows and per-sample weights come by 4-B gathers whose
-// out-of-range samples read a zero block), so the copy engine, not a layout
-// pass, sits between HBM and the MFMAs.  8 waves (2 per SIMD): L1..L3 wave w
-// owns rows {2(w>>2), 2(w>>2)+1} × column w&3 (32 × 32 blocks), the x
-// columns of W4 on waves 0, 1, 6, 7 (one per SIMD); L0 (W1, 4 row blocks) runs its MFMAs
-// on waves 0..3 and W5 = δ5 ⊗ c1 on waves 4..7.  Bias sums and the W3 sdf row
-// ride on the MFMA operands already in registers.  One barrier per tile;
-// per-wave copy counts are uniform, so the wait is a compile-time vmcnt.
-constexpr int kDw2Waves = 8;
-constexpr int kS2D = 0, kS2A = 128 * kTileS, kS2S = kS2A + kDwA * kTileS, kStage2 = kS2S + 64 * kDw2Waves;
-constexpr int kDw2Stages = 3;
-constexpr int kDw2Lds = kDw2Stages * kStage2;  // 116,736 B: room beside it for 2 k_interp_bwd workgroups
-static_assert(kDw2Lds * 4 <= 160 * 1024, "dw2 LDS budget");
-
-template <int N>
-__device__ __forceinline__ void wait_vm_c() {
-    static_assert(N >= 0 && N <= 63, "vmcnt range");
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
-    asm volatile("" ::: "memory");
-}
-
-// rows [r0, r0+8) of a CF tile → stage rows [dr0, dr0+8): one 1-KB copy
-// (dr0 ≡ r0 mod 16, so the row swizzle carries over)
-__device__ __forceinline__ void s2_rows(float *stage, const float *tile, int r0, int dr0, int lane) {
-    glds16(tile + r0 * kTileS + lane * 4, stage + dr0 * kTileS);
-}
-
-// tile-local sample of logical group g (= h·4 + t4), element e
-__device__ __forceinline__ int s2_sample(int g, int e) { return 2 * (4 * (g & 3) + e) + (g >> 2); }
-
-// x features k0, k0+1 → A rows arow0, arow0+1 (2 rows × 32 floats per wave instruction)
-__device__ __forceinline__ void s2_x(float *stage, const float *feat, const float *zblk, int64_t s0, int64_t m, int k0,
-                                     int arow0, int lane) {
-    const int dr = arow0 + (lane >> 5), q = lane & 31, k = k0 + (lane >> 5);
-    const int g = (q >> 2) ^ ((dr >> 1) & 7), e = q & 3;
-    const int64_t sg = s0 + s2_sample(g, e);
-    glds4(sg < m ? feat + sg * 16 + k : zblk, stage + kS2A + arow0 * kTileS);
-}
-
-template <int L>
-__device__ __forceinline__ void dw2_issue(const DwSrc &src, const float *zblk, int64_t t, int64_t m, float *stage,
-                                          int wave, int lane) {
-    const float *dt = src.D[L] + t * kCfTile;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) s2_rows(stage + kS2D, dt, (8 * i + wave) * 8, (8 * i + wave) * 8, lane);
-    if (L == 1 || L == 2 || L == 3) {
-        const float *at = src.A[L] + t * kCfTile;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) s2_rows(stage + kS2A, at, (8 * i + wave) * 8, (8 * i + wave) * 8, lane);
-    }
-    if (L == 0) {  // c1 → A rows 32..159
-        const float *at = src.c1 + t * kCfTile;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) s2_rows(stage + kS2A, at, (8 * i + wave) * 8, 32 + (8 * i + wave) * 8, lane);
-    }
-    const int64_t s0 = t * kTileS;
-    if (L == 0 || L == 3) {  // x: 16 rows, one 2-row instruction per wave
-        const int rbase = (L == 0) ? 0 : 128;
-        s2_x(stage, src.feat, zblk, s0, m, 2 * wave, rbase + 2 * wave, lane);
-    }
-    if (L == 0 || L == 2) {  // per-sample weights [ch][h][16] (δ5 for L0, g_sdf for L2)
-        const int idx = wave * 64 + lane;
-        const int nch = (L == 0) ? 3 : 1;
-        const float *srcp = zblk;
-        if (idx < 32 * nch) {
-            const int ch = idx >> 5, q = idx & 31;
-            const int64_t sg = s0 + 2 * (q & 15) + (q >> 4);
-            if (sg < m) srcp = (L == 0) ? src.d5 + sg * 3 + ch : src.g_sdf + sg;
-        }
-        glds4(srcp, stage + kS2S + wave * 64);
-    }
-}
-
-template <int L>
-constexpr int dw2_count() { return 2 + ((L == 0) ? 2 + 1 + 1 : (L == 3) ? 2 + 1 : (L == 2) ? 2 + 1 : 2); }
-
-template <int L>
-__device__ __forceinline__ void dw2_layer(int64_t m, const DwSrc &src, const float *zblk, int split, int n_split,
-                                          float *slab, float *slab5, float *lds) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = lane & 31, h = lane >> 5;
-    const int64_t n_units = (m + kTileS - 1) / kTileS;
-    const int64_t u_beg = n_units * split / n_split, u_end = n_units * (split + 1) / n_split;
-    constexpr int NR = (L == 0) ? 1 : 2;
-    constexpr int NC = 1;
-    constexpr bool XBLK = (L == 3);
-    constexpr int NOP = NR + NC + (XBLK ? 1 : 0);
-    constexpr int NI = dw2_count<L>();
-    int rb[NR], cb[NC];
-    if (L == 0) {
-        rb[0] = wave & 3;
-        cb[0] = 0;
-    } else {
-        rb[0] = 2 * (wave >> 2);
-        rb[NR - 1] = 2 * (wave >> 2) + 1;
-        cb[0] = wave & 3;
-    }
-    const bool mfma_wave = (L != 0) || wave < 4;
-    // the 4 x row blocks on waves 0, 1, 6, 7: one per SIMD (waves w and w+4 share SIMD w&3)
-    const bool xwave = XBLK && ((wave >> 2) == 0 ? (wave & 3) < 2 : (wave & 3) >= 2);
-    const int xsel = wave & 1;
-    const bool own_bias = (L == 0) ? wave < 4 : ((wave & 3) == 0);  // D rows summed once
-    const bool own_sdf = (L == 2) && ((wave >> 2) == 0);             // A columns dotted once
-    f32x16 acc[NR][NC];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) zero(acc[i]);
-    f32x16 accx[1];
-    zero(accx);
-    float bsum[NR], sdfp[NC];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) bsum[i] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) sdfp[j] = 0.f;
-    float w5[3] = {0.f, 0.f, 0.f}, vb = 0.f;  // L0: W5 partials; db5 (L0) / db3[0] (L2) partials
-    // rows no copy writes: W1 rows 16..31, W4 rows 144..159
-    if (L == 0 || L == 3) {
-        const int r0 = (L == 0) ? 16 : 144;
-        for (int e = threadIdx.x; e < 16 * kTileS; e += 64 * kDw2Waves)
-#pragma unroll
-            for (int st = 0; st < kDw2Stages; ++st) lds[st * kStage2 + kS2A + r0 * kTileS + e] = 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kDw2Stages - 1; ++k)
-        if (u_beg + k < u_end) dw2_issue<L>(src, zblk, u_beg + k, m, lds + k * kStage2, wave, lane);
-#ifdef PSVO_STAMPS
-    unsigned long long dws_[8] = {};  // start, end, wait, barrier, issue, mfma, units
-    auto dw_now = []() {
-        unsigned long long t_;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return t_;
-    };
-    dws_[0] = dw_now();
-    unsigned long long t_a_ = dws_[0];
-#define PSVO_DW_SEG(k)                     \
-    do {                                   \
-        const unsigned long long t_b_ = dw_now(); \
-        dws_[k] += t_b_ - t_a_;            \
-        t_a_ = t_b_;                       \
-    } while (0)
-#else
-#define PSVO_DW_SEG(k)
-#endif
-    for (int64_t u = u_beg; u < u_end; ++u) {
-        float *st = lds + ((int)((u - u_beg) % kDw2Stages)) * kStage2;
-        // tile u landed for this wave: only the newer in-flight tiles may still be outstanding
-        const int64_t ahead = (u_end - 1 - u) < (kDw2Stages - 2) ? (u_end - 1 - u) : (kDw2Stages - 2);
-        if (ahead >= 2) wait_vm_c<2 * NI>();
-        else if (ahead == 1) wait_vm_c<NI>();
-        else wait_vm_c<0>();
-        PSVO_DW_SEG(2);
-        raw_barrier();  // ... for every wave; and every wave is done with tile u-1's stage
-        PSVO_DW_SEG(3);
-        if (u + kDw2Stages - 1 < u_end)
-            dw2_issue<L>(src, zblk, u + kDw2Stages - 1, m,
-                         lds + ((int)((u + kDw2Stages - 1 - u_beg) % kDw2Stages)) * kStage2, wave, lane);
-        PSVO_DW_SEG(4);
-        const float *Dl = st + kS2D, *Al = st + kS2A, *Sl = st + kS2S;
-        if (L == 0 && wave >= 4) {  // W5 = δ5 ⊗ c1 (A rows 32..159): thread = (c1 row, k-half); db5
-            const int tw = threadIdx.x - 256;
-            const int row = 32 + (tw & 127), hh = tw >> 7;
-#pragma unroll
-            for (int t4 = 0; t4 < 4; ++t4) {
-                const float4 a = *reinterpret_cast<const float4 *>(Al + cf_row_slot(row, hh * 4 + t4));
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    const float4 w = *reinterpret_cast<const float4 *>(Sl + ch * 32 + hh * 16 + 4 * t4);
-                    w5[ch] += (a.x * w.x + a.y * w.y) + (a.z * w.z + a.w * w.w);
-                }
-            }
-            if (wave < 7 && lane < 32) vb += Sl[(wave - 4) * 32 + lane];
-        }
-        if (L == 2 && wave == 0 && lane < 32) vb += Sl[lane];  // db3[0] = Σ g_sdf
-        if (mfma_wave) {
-            // MFMAs; the operands of k-group t4+1 are read before the MFMAs of t4
-            auto load = [&](int t4, float4 (&o)[NOP]) {
-#pragma unroll
-                for (int i = 0; i < NR; ++i)
-                    o[i] = *reinterpret_cast<const float4 *>(Dl + cf_row_slot(32 * rb[i] + x, h * 4 + t4));
-#pragma unroll
-                for (int j = 0; j < NC; ++j)
-                    o[NR + j] = *reinterpret_cast<const float4 *>(Al + cf_row_slot(32 * cb[j] + x, h * 4 + t4));
-                if (XBLK) o[NOP - 1] = *reinterpret_cast<const float4 *>(Al + cf_row_slot(128 + x, h * 4 + t4));
-            };
-            float4 cur[NOP];
-            load(0, cur);
-#pragma unroll
-            for (int t4 = 0; t4 < 4; ++t4) {
-                float4 nxt[NOP];
-                if (t4 + 1 < 4) load(t4 + 1, nxt);
-                const float4 dx = (XBLK && NR > 1 && xsel) ? cur[NR - 1] : cur[0];
-#define PSVO_DW2_K(c)                                                                                         \
-                _Pragma("unroll") for (int i = 0; i < NR; ++i)                                                \
-                    _Pragma("unroll") for (int j = 0; j < NC; ++j) acc[i][j] = mfma(cur[i].c, cur[NR + j].c, acc[i][j]); \
-                if (xwave) accx[0] = mfma(dx.c, cur[NOP - 1].c, accx[0]);
-                PSVO_DW2_K(x)
-                PSVO_DW2_K(y)
-                PSVO_DW2_K(z)
-                PSVO_DW2_K(w)
-#undef PSVO_DW2_K
-                if (own_bias) {
-#pragma unroll
-                    for (int i = 0; i < NR; ++i) bsum[i] += (cur[i].x + cur[i].y) + (cur[i].z + cur[i].w);
-                }
-                if (L == 2 && own_sdf) {
-                    const float4 w = *reinterpret_cast<const float4 *>(Sl + h * 16 + 4 * t4);
-#pragma unroll
-                    for (int j = 0; j < NC; ++j)
-                        sdfp[j] += (cur[NR + j].x * w.x + cur[NR + j].y * w.y) +
-                                   (cur[NR + j].z * w.z + cur[NR + j].w * w.w);
-                }
-                if (t4 + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, NOP, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 4 * NR * NC, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (t4 + 1 < 4) {
-#pragma unroll
-                    for (int i = 0; i < NOP; ++i) cur[i] = nxt[i];
-                }
-            }
-        }
-        PSVO_DW_SEG(5);
-    }
-    wait_vm_c<0>();
-#ifdef PSVO_STAMPS
-    dws_[1] = dw_now();
-    dws_[6] = (unsigned long long)(u_end - u_beg);
-    dws_[7] = (unsigned long long)L;
-    {
-        const int wg_ = blockIdx.x + 0;
-        if (lane == 0 && wg_ < 256)
-            for (int i_ = 0; i_ < 8; ++i_) psvo_g_stamps[2][wg_][wave][0][i_] = dws_[i_];
-    }
-#endif
-#undef PSVO_DW_SEG
-    // ---- the slab: [rows][cols] weights, then [rows] bias
-    constexpr int ROWS = (L == 2) ? 129 : 128;
-    constexpr int COLS = (L == 0) ? 16 : (L == 3 ? 144 : 128);
-    constexpr int ROW_OFF = (L == 2) ? 1 : 0;
-    if (mfma_wave) dw_store<NR, NC>(slab, COLS, ROW_OFF, COLS, rb, cb, acc, lane);
-    if (xwave) {
-        const int rbx[1] = {rb[xsel]}, cbx[1] = {4};
-        const f32x16 tmp[1][1] = {{accx[0]}};
-        dw_store<1, 1>(slab, COLS, 0, COLS, rbx, cbx, tmp, lane);
-    }
-    float *bias = slab + ROWS * COLS;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
-        if (own_bias && h == 0) bias[ROW_OFF + 32 * rb[i] + x] = v;
-    }
-    if (L == 2) {
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const float v = sdfp[j] + __shfl_xor(sdfp[j], 32, 64);
-            if (own_sdf && h == 0) slab[32 * cb[j] + x] = v;  // sdf row = row 0
-        }
-        float b = vb;  // lanes 0..31 of wave 0: partial Σ g_sdf
-#pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
-        if (wave == 0 && lane == 0) bias[0] = b;
-    }
-    if (L == 0) {
-        __syncthreads();  // the stages are free: combine the two k-halves of W5 through LDS
-        float *red = lds;
-        const int tw = threadIdx.x - 256;
-        if (tw >= 128) {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) red[ch * 128 + (tw - 128)] = w5[ch];
-        }
-        __syncthreads();
-        if (tw >= 0 && tw < 128) {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) slab5[ch * 128 + tw] = w5[ch] + red[ch * 128 + tw];
-        }
-        float b = vb;
-#pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) b += __shfl_xor(b, sh, 64);
-        if (wave >= 4 && wave < 7 && lane == 0) slab5[3 * 128 + (wave - 4)] = b;
-    }
-}
-
-__global__ __launch_bounds__(64 * kDw2Waves, 1) void k_mlp_dw2(int64_t m, DwSrc src, const float *__restrict__ zblk,
-                                                               DwGrid g, float *__restrict__ slabs, int wg_offset) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int wg = blockIdx.x + wg_offset;
-    int L = 0;
-#pragma unroll
-    for (int l = 1; l < 4; ++l) L += (wg >= g.wg_begin[l]);
-    const int split = wg - g.wg_begin[L];
-    const int n_split = g.wg_begin[L + 1] - g.wg_begin[L];
-    float *slab = slabs + g.slab_off[L] + (int64_t)split * g.slab_len[L];
-    float *slab5 = slabs + g.slab_off[4] + (int64_t)split * g.slab_len[4];
-    switch (L) {
-        case 0: dw2_layer<0>(m, src, zblk, split, n_split, slab, slab5, lds); break;
-        case 1: dw2_layer<1>(m, src, zblk, split, n_split, slab, slab5, lds); break;
-        case 2: dw2_layer<2>(m, src, zblk, split, n_split, slab, slab5, lds); break;
-        default: dw2_layer<3>(m, src, zblk, split, n_split, slab, slab5, lds); break;
-    }
-}
 
 struct DwDst {
     float *w[5], *b[5];
@@ -1193,9 +627,9 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
                                                             const float *__restrict__ img,
                                                             float *__restrict__ sdf_out, float *__restrict__ rgb_out,
                                                             float *__restrict__ act, uint64_t *__restrict__ masks,
-                                                            DevBatch dev) {
+                                                            const int *__restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    if (dev.stats) m = dev_batch_m(dev);  // device-sized launch (DevBatch)
+    if (m_dev) m = __builtin_amdgcn_readfirstlane(*m_dev);  // the sparse decoder's kept samples (<= m)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
@@ -1369,162 +803,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m, const flo
         (void)relu(bacc);
         const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
         if (valid && h == 0) sdf_out[s] = sdf;
-    }
-    wait_vm(0);
-}
-
-// ---------------------------------------------------------------------------
-// backward (data), persistent + double-buffered like k_mlp_fwd2: 8 waves ×
-// 32 samples per tile; W4ᵀ / W2ᵀ stream through an 80-KB buffer and W3ᵀ /
-// W1ᵀ through a 64-KB one, each image issued (global_load_lds) one layer
-// ahead; each δ is stored from inside the GEMM that consumes it; the next
-// tile's per-sample inputs load during the W1ᵀ layer.
-constexpr int kB2BufA = kVecPad, kB2BufB = kB2BufA + 20480;
-constexpr int kLdsBwd2 = (kB2BufB + 16384) * 4;  // 152,576 B
-static_assert(kLdsBwd2 <= 160 * 1024, "bwd2 LDS budget");
-
-struct BwdIn {
-    uint64_t mk[3];
-    float y[3], g[3], gs;
-};
-
-__device__ __forceinline__ void load_bwd_in(const float *__restrict__ rgb_in, const uint64_t *__restrict__ masks,
-                                            const float *__restrict__ g_sdf, const float *__restrict__ g_rgb,
-                                            int64_t s, bool valid, int h, BwdIn &in) {
-    const int64_t q = valid ? s : 0;
-    const uint64_t *mk = masks + (q * 2 + h) * 3;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        in.mk[i] = mk[i];
-        in.y[i] = rgb_in[q * 3 + i];
-        in.g[i] = g_rgb[q * 3 + i];
-    }
-    in.gs = g_sdf[q];
-}
-
-__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd2(int64_t m, const float *__restrict__ img,
-                                                            const float *__restrict__ rgb_in,
-                                                            const uint64_t *__restrict__ masks,
-                                                            const float *__restrict__ g_sdf,
-                                                            const float *__restrict__ g_rgb, BwdOut o) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *bufA = lds + kB2BufA, *bufB = lds + kB2BufB;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5;
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;
-    const int64_t tbytes = n_tiles * 32 * 128 * 4;
-    // balanced split of the 32-sample units, as k_mlp_fwd2
-    const int64_t n_units = (m + kTileS - 1) / kTileS;
-    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
-    const int n_it = (int)((u1 - u0 + kF2Waves - 1) / kF2Waves);
-    [[maybe_unused]] constexpr int kStampK = 1;
-    BwdIn nin;
-    {
-        const int64_t u = u0 + wave;
-        const int64_t s = u * kTileS + (lane & 31);
-        load_bwd_in(rgb_in, masks, g_sdf, g_rgb, s, u < u1 && s < m, h, nin);
-    }
-    stage8(lds, img + kImgVec, kVecPad, wave, lane);
-    stage8(bufA, img + kImgB4, 20480, wave, lane);
-    wait_vm(0);
-    raw_barrier();
-    PSVO_STAMP_DECL;
-    for (int it = 0; it < n_it; ++it) {
-        const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
-        const bool active = u < u1;  // wave-uniform
-        const int64_t s = u * kTileS + (lane & 31);
-        const bool valid = active && s < m;
-        const bool more = it + 1 < n_it;
-        const CfStore cfs(u, lane, n_tiles);
-        const BwdIn in = nin;
-        float d5[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) d5[c] = valid ? in.g[c] * (in.y[c] * (1.0f - in.y[c])) : 0.0f;  // sigmoid bwd
-        const float dsdf = valid ? in.gs : 0.0f;
-        const uint64_t m1 = valid ? in.mk[0] : 0, m2 = valid ? in.mk[1] : 0, m4 = valid ? in.mk[2] : 0;
-        if (valid && h == 0) {
-            o.d5[s * 3 + 0] = d5[0];
-            o.d5[s * 3 + 1] = d5[1];
-            o.d5[s * 3 + 2] = d5[2];
-        }
-        // ---- W4ᵀ layer (bufA); W3ᵀ → bufB
-        PSVO_STAMP(1);
-        wait_vm(0);
-        raw_barrier();
-        PSVO_STAMP(2);
-        stage8(bufB, img + kImgB3, 16384, wave, lane);
-        f32x16 a[kNB], bacc[kNB];
-        float dxc[8];
-        if (active) {
-#pragma unroll
-            for (int b = 0; b < kNB; ++b)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {  // δc1 = W5ᵀ δ5 ⊙ mask
-                    const int k = 32 * b + phi(r, h);
-                    const float v =
-                        lds[kOffW5 + k] * d5[0] + lds[kOffW5 + 128 + k] * d5[1] + lds[kOffW5 + 256 + k] * d5[2];
-                    bacc[b][r] = __uint_as_float(__float_as_uint(v) & (0u - (uint32_t)((m4 >> (16 * b + r)) & 1)));
-                }
-            f32x16 t5[5];
-            zero(t5);
-            gemm_acc<kNB, 5>(bufA, bacc, t5, lane, CfQueue(cfs, o.d4, tbytes, o.d4 != nullptr, bacc));  // + δc1
-#pragma unroll
-            for (int r = 0; r < 8; ++r) dxc[r] = t5[4][r];
-#pragma unroll
-            for (int b = 0; b < kNB; ++b) a[b] = t5[b];  // δf
-        }
-        // ---- W3ᵀ layer (bufB); W2ᵀ → bufA
-        PSVO_STAMP(3);
-        wait_vm(0);
-        raw_barrier();
-        PSVO_STAMP(4);
-        stage8(bufA, img + kImgB2, 16384, wave, lane);
-        if (active) {
-#pragma unroll
-            for (int b = 0; b < kNB; ++b)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) bacc[b][r] = lds[kOffW3r0 + 32 * b + phi(r, h)] * dsdf;
-            gemm_acc<kNB, kNB>(bufB, a, bacc, lane, CfQueue(cfs, o.d3, tbytes, o.d3 != nullptr, a));  // + δf stores
-            apply_mask(bacc, m2);
-        }
-        // ---- W2ᵀ layer (bufA); W1ᵀ → bufB
-        PSVO_STAMP(5);
-        wait_vm(0);
-        raw_barrier();
-        PSVO_STAMP(6);
-        stage8(bufB, img + kImgB1, 4096, wave, lane);
-        if (active) {
-            zero(a);
-            gemm_acc<kNB, kNB>(bufA, bacc, a, lane, CfQueue(cfs, o.d2, tbytes, o.d2 != nullptr, bacc));  // + δh2
-            apply_mask(a, m1);
-        }
-        // ---- W1ᵀ layer (bufB); next iteration's W4ᵀ → bufA and its inputs
-        PSVO_STAMP(7);
-        wait_vm(0);
-        raw_barrier();
-        PSVO_STAMP(8);
-        if (more) {
-            stage8(bufA, img + kImgB4, 20480, wave, lane);
-            const int64_t un = u + kF2Waves;
-            const int64_t sn = un * kTileS + (lane & 31);
-            load_bwd_in(rgb_in, masks, g_sdf, g_rgb, sn, un < u1 && sn < m, h, nin);
-        }
-        if (active) {
-            f32x16 t1[1];
-            zero(t1);
-            gemm_acc<kNB, 1>(bufB, a, t1, lane, CfQueue(cfs, o.d1, tbytes, o.d1 != nullptr, a));  // + δh1 stores
-            if (valid) {
-                float *dst = o.dfeat + s * kIn;
-#pragma unroll
-                for (int rg = 0; rg < 2; ++rg)
-                    *reinterpret_cast<float4 *>(dst + 8 * rg + 4 * h) =
-                        make_float4(t1[0][4 * rg] + dxc[4 * rg], t1[0][4 * rg + 1] + dxc[4 * rg + 1],
-                                    t1[0][4 * rg + 2] + dxc[4 * rg + 2], t1[0][4 * rg + 3] + dxc[4 * rg + 3]);
-            }
-        }
-        PSVO_STAMP(9);
-        PSVO_STAMP_FLUSH(1);
     }
     wait_vm(0);
 }
@@ -1849,8 +1127,10 @@ struct Bwd3Src {
 // scheme: lanes own (corner, dim), whole 64-B rows per atomic instruction).
 template <bool W>
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const float *__restrict__ img, Bwd3Src src,
-                                                            DwGrid g, float *__restrict__ slabs, InterpFuse ip) {
+                                                            DwGrid g, float *__restrict__ slabs, InterpFuse ip,
+                                                            const int *__restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (m_dev) m = __builtin_amdgcn_readfirstlane(*m_dev);  // the sparse decoder's kept samples (<= m)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples)
@@ -2179,15 +1459,6 @@ static int device_cus() {
     return cus;
 }
 
-static bool use_fwd2() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PSVO_MLP_FWD");
-        v = (e && e[0] == '1') ? 0 : 1;  // PSVO_MLP_FWD=1: the per-tile fwd / bwd_data kernels (A/B)
-    }
-    return v == 1;
-}
-
 }  // namespace
 }  // namespace psvo
 
@@ -2218,12 +1489,13 @@ extern "C" int64_t psvo_mlp_mask_words(int64_t m, int width) {
 static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                             const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                            float *act, uint64_t *masks, bool images_ready) {
+                            float *act, uint64_t *masks, bool images_ready, const int *m_dev = nullptr) {
     if (width == 256) {
         PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
         PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats_w floats)");
         PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd: act needs masks");
         PSVO_REQUIRE(m <= ((int64_t)1 << 31) / 256, "mlp_fwd: m = %lld too large", (long long)m);
+        PSVO_REQUIRE(m_dev == nullptr, "mlp_fwd: a device sample count is width 128 only");
         hipStream_t st = as_stream(stream);
         if (!images_ready) {
             const int rc = dec256_images(st, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images);
@@ -2238,12 +1510,6 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
     PSVO_REQUIRE(m <= kMaxSamples, "mlp_fwd: m = %lld > %lld (32-bit CF offsets)", (long long)m,
                  (long long)kMaxSamples);
     if (m == 0) return PSVO_OK;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd);
-        attr = true;
-    }
     hipStream_t st = as_stream(stream);
     MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
     if (!images_ready) psvo::launch(k_mlp_prep, dim3(div_up(kImgTotal, 256)), dim3(256), 0, st, p, images);
@@ -2260,44 +1526,20 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf);
         return check_launch("mlp_fwd");
     }
-    if (use_fwd2()) {
-        static bool attr2 = false;
-        if (!attr2) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
-            attr2 = true;
-        }
-        const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
-        const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-        psvo::launch(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act,
-                           masks, DevBatch{});
-    } else {
-        psvo::launch(k_mlp_fwd, dim3(div_up(m, kTile)), dim3(kThreads), kLdsFwd, st, m, feat, p, images, sdf,
-                           rgb, act, masks);
-    }
-    return check_launch("mlp_fwd");
-}
-
-namespace psvo {
-int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const float *images, float *sdf, float *rgb,
-                float *act, uint64_t *masks) {
-    PSVO_REQUIRE(b.stats && b.m_cap > 0 && b.m_cap <= kMaxSamples && images && sdf && rgb,
-                 "mlp_fwd_dev: bad arguments");
-    PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd_dev: act needs masks");
-    PSVO_REQUIRE(use_fwd2(), "mlp_fwd_dev: the persistent forward (k_mlp_fwd2) is required");
     static bool attr2 = false;
     if (!attr2) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
         attr2 = true;
     }
-    // one workgroup per CU whatever the batch (the balanced split gives small
-    // batches empty workgroups, which only stage and leave)
-    psvo::launch(k_mlp_fwd2, dim3(device_cus()), dim3(kF2Threads), kLdsFwd2, st, b.m_cap, feat, images, sdf, rgb,
-                       act, masks, b);
-    return check_launch("mlp_fwd_dev");
+    const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
+    const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
+    psvo::launch(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act, masks,
+                 m_dev);
+    return check_launch("mlp_fwd");
 }
 
+namespace psvo {
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images) {
@@ -2309,9 +1551,9 @@ int mlp_images(void *stream, int width, const float *w1, const float *b1, const 
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                     float *act, uint64_t *masks) {
+                     float *act, uint64_t *masks, const int *m_dev) {
     return mlp_fwd_impl(stream, m, width, feat, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images, sdf, rgb, act, masks,
-                        true);
+                        true, m_dev);
 }
 }  // namespace psvo
 
@@ -2325,46 +1567,6 @@ extern "C" int psvo_mlp_fwd(void *stream, int64_t m, int width, const float *fea
 
 static const int kDwRows[5] = {128, 128, 129, 128, 3};
 static const int kDwCols[5] = {16, 128, 128, 144, 128};
-// relative per-tile time of the workgroup types (W1+W5, W2, W3, W4): s_memtime stamps
-// (scripts/mlp_stamps.py) at the bench size, 3010 / 5713 / 5929 / 7258 cycles per wave
-static const int kDw2Weight[4] = {28, 53, 55, 67};
-
-static void dw_grid(int64_t m, int n_split, DwGrid *g, int *slab_floats) {
-    const int64_t chunks = (m + kTileS - 1) / kTileS;  // split units: CF tiles
-    const int *kDwWeightSel = kDw2Weight;
-    int wsum = 0;
-    for (int l = 0; l < 4; ++l) wsum += kDwWeightSel[l];
-    int wg = 0;
-    for (int l = 0; l < 4; ++l) {
-        int sp = (int)((int64_t)n_split * kDwWeightSel[l] / wsum);
-        if (sp < 1) sp = 1;
-        if (sp > chunks) sp = (int)(chunks > 0 ? chunks : 1);
-        g->wg_begin[l] = wg;
-        g->n_split[l] = sp;
-        wg += sp;
-    }
-    g->wg_begin[4] = wg;
-    g->n_split[4] = g->n_split[0];  // W5 slabs come from the W1 workgroups
-    int off = 0;
-    for (int l = 0; l < 5; ++l) {
-        g->slab_off[l] = off;
-        g->slab_len[l] = kDwRows[l] * kDwCols[l] + kDwRows[l];
-        off += g->n_split[l] * g->slab_len[l];
-    }
-    *slab_floats = off;
-}
-
-// PSVO_MLP_BWD=2: the two-kernel backward (k_mlp_bwd2 δ's through HBM, then
-// k_mlp_dw2) instead of the fused k_mlp_bwd3 (A/B, profiling)
-static bool use_bwd3() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PSVO_MLP_BWD");
-        v = (e && e[0] == '2') ? 0 : 1;
-    }
-    return v == 1 && use_fwd2();
-}
-
 // k_mlp_bwd3: one workgroup per CU (at most one per round of 4 units), each
 // writing a slab of every layer
 static int bwd3_grid(int64_t m) {
@@ -2374,7 +1576,6 @@ static int bwd3_grid(int64_t m) {
 static void dw_grid_uniform(int n, DwGrid *g, int *slab_floats) {
     int off = 0;
     for (int l = 0; l < 5; ++l) {
-        g->wg_begin[l] = 0;  // (k_mlp_dw2 only)
         g->n_split[l] = n;
         g->slab_off[l] = off;
         g->slab_len[l] = kDwRows[l] * kDwCols[l] + kDwRows[l];
@@ -2386,15 +1587,11 @@ static void dw_grid_uniform(int n, DwGrid *g, int *slab_floats) {
 extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split);
 
 extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
+    (void)n_split;  // k_mlp_bwd3 writes one slab per workgroup
     DwGrid g;
     int slab;
-    if (use_bwd3()) {  // per-sample δ5 of the dfeat-only path + the fused kernel's slabs
-        dw_grid_uniform(bwd3_grid(m), &g, &slab);
-        return m * 3 + slab;
-    }
-    dw_grid(m, n_split, &g, &slab);
-    const int64_t mp = (m + kCh - 1) / kCh * kCh;
-    return mp * 4 * 128 + m * 3 + slab;
+    dw_grid_uniform(bwd3_grid(m), &g, &slab);
+    return m * 3 + slab;
 }
 
 extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split) {
@@ -2412,16 +1609,17 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream,
-            const BwdHook *before_dw) {
-    PSVO_REQUIRE(ip == nullptr || ((width == 256 || (width == kW && use_bwd3())) && gw1 != nullptr),
+            const int *m_dev) {
+    PSVO_REQUIRE(ip == nullptr || ((width == 256 || width == kW) && gw1 != nullptr),
                  "mlp_bwd: the fused interpolation backward needs a fused weight-gradient path");
     if (width == 256) {
         PSVO_REQUIRE(m >= 0, "mlp_bwd: bad sizes");
         PSVO_REQUIRE(images != nullptr && masks != nullptr, "mlp_bwd: images / masks of the training forward required");
         PSVO_REQUIRE(gw1 == nullptr || act != nullptr, "mlp_bwd: weight gradients need the forward's activations");
         float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
+        PSVO_REQUIRE(m_dev == nullptr, "mlp_bwd: a device sample count is width 128 only");
         return dec256_bwd(as_stream(stream), m, feat, images, rgb, act, masks, g_sdf, g_rgb, dfeat, gw, gb, accumulate,
-                          workspace, dfeat_ready, before_dw, ip);
+                          workspace, dfeat_ready, ip);
     }
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");
@@ -2447,7 +1645,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate);
         return check_launch("mlp_dw_reduce");
     };
-    if (use_bwd3()) {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
+    {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
         static bool attr3 = false;
         if (!attr3) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd3<true>),
@@ -2462,7 +1660,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
                 const int64_t rounds = div_up(div_up(m, kU), 8);
                 const int grid = (int)(rounds < device_cus() ? rounds : device_cus());
                 psvo::launch(k_mlp_bwd3<false>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g,
-                                   nullptr, InterpFuse{});
+                             nullptr, InterpFuse{}, m_dev);
                 const int rc = check_launch("mlp_bwd3");
                 if (rc) return rc;
             }
@@ -2475,7 +1673,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         float *slabs = workspace + m * 3;
         if (m > 0) {
             psvo::launch(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs,
-                               ip ? *ip : InterpFuse{});
+                         ip ? *ip : InterpFuse{}, m_dev);
             const int rc = check_launch("mlp_bwd3");
             if (rc) return rc;
         } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
@@ -2491,90 +1689,15 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         }
         return reduce(slabs, st);
     }
-    dw_grid(m, n_split, &g, &slab_floats);
-    float *ws = workspace;
-    const int64_t mp = (m + kCh - 1) / kCh * kCh;  // CF matrices hold whole 64-sample chunks
-    BwdOut o;
-    o.d1 = ws; ws += mp * 128;
-    o.d2 = ws; ws += mp * 128;
-    o.d3 = ws; ws += mp * 128;
-    o.d4 = ws; ws += mp * 128;
-    o.d5 = ws; ws += m * 3;
-    float *slabs = ws;
-    o.dfeat = dfeat;
-    if (!want_w) o.d1 = o.d2 = o.d3 = o.d4 = nullptr;  // δ feeds only the weight gradients
-    MlpParams p{w1, b1, w2, b2, w3, b3, w4, b4, w5, b5};
-    if (m > 0) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd_data),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd);
-            attr = true;
-        }
-        if (use_fwd2()) {
-            static bool attr2 = false;
-            if (!attr2) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd2),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd2);
-                attr2 = true;
-            }
-            const int64_t tiles = div_up(m, kF2Tile);
-            const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-            psvo::launch(k_mlp_bwd2, dim3(grid), dim3(kF2Threads), kLdsBwd2, st, m, images, rgb, masks, g_sdf,
-                               g_rgb, o);
-        } else {
-            psvo::launch(k_mlp_bwd_data, dim3(div_up(m, kTileBwd)), dim3(kThreadsBwd), kLdsBwd, st, m, p,
-                               images, rgb, masks, g_sdf, g_rgb, o);
-        }
-        int rc = check_launch("mlp_bwd_data");
-        if (rc) return rc;
-    }
-    if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
-    if (!want_w) return PSVO_OK;
-    DwSrc src;
-    src.D[0] = o.d1; src.D[1] = o.d2; src.D[2] = o.d3; src.D[3] = o.d4;
-    src.A[0] = nullptr; src.A[1] = act; src.A[2] = act + mp * 128; src.A[3] = act + 2 * mp * 128;
-    src.c1 = act + 3 * mp * 128;
-    src.d5 = o.d5;
-    src.feat = feat;
-    src.g_sdf = g_sdf;
-    static bool dw_attr = false;
-    if (!dw_attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_dw2),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDw2Lds * 4);
-        dw_attr = true;
-    }
-    const float *zblk = images + kImgVec + kOffW;  // zero floats of the vector image (k_mlp_prep)
-    // PSVO_DW_LAYER=1 (profiling aid): launch each layer's workgroups as their own dispatch
-    static const char *only = getenv("PSVO_DW_LAYER");
-    const int n_launch = (only && *only) ? 4 : 1;
-    for (int l = 0; l < n_launch; ++l) {
-        const int wg0 = n_launch == 1 ? 0 : g.wg_begin[l];
-        const int nwg = n_launch == 1 ? g.wg_begin[4] : g.wg_begin[l + 1] - g.wg_begin[l];
-        psvo::launch(k_mlp_dw2, dim3(nwg), dim3(64 * kDw2Waves), kDw2Lds * 4, st, m, src, zblk, g, slabs, wg0);
-    }
-    int rc = check_launch("mlp_dw");
-    if (rc) return rc;
-    return reduce(slabs, st);
 }
 }  // namespace psvo
 
 namespace psvo {
-// width 256: PSVO_IB256_FUSED=1 runs the interpolation backward inside
-// k_dec256_bwd (A/B, off by default).  Measured (configs C / E, one box, two
-// interleaved pairs each): 3.705 / 2.221 ms fused vs 3.671-3.691 /
-// 2.208-2.270 ms with k_interp_bwd beside the weight-gradient kernel — there
-// the scatter's atomics overlap the dW MFMAs for free, fused they lengthen
-// the δ chain (+65-100 us)
-bool mlp_bwd_fuses_interp(int width) {
-    if (width == 256) {
-        static const bool fused = getenv("PSVO_IB256_FUSED") && *getenv("PSVO_IB256_FUSED") == '1';
-        return fused;
-    }
-    return width == kW && use_bwd3();
-}
-bool mlp_bwd_split_tail(int width) { return width == kW && use_bwd3(); }
+// width 128: the interpolation backward runs inside k_mlp_bwd3; width 256:
+// k_interp_bwd beside the weight-gradient kernel (measured faster than inside
+// k_dec256_bwd: there the scatter's atomics overlap the dW MFMAs)
+bool mlp_bwd_fuses_interp(int width) { return width == kW; }
+bool mlp_bwd_split_tail(int width) { return width == kW; }
 }  // namespace psvo
 
 extern "C" int psvo_mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,

@@ -962,13 +962,7 @@ static void dw_plan(int64_t m, DwPlan *pl, int64_t *slab_floats) {
     // per-type weights measured at config C (466 k samples, one box, decoder
     // alone): {213,120,120,107} 1,310 us -> {213,130,130,60} 1,195-1,200 us —
     // the W1 / W5 type's byte-bound tiles finish early with fewer workgroups
-    int w[4] = {213, 130, 130, 60};
-    static const char *wenv = getenv("PSVO_DW256_W");  // A/B: "w0,w1,w2,w3"
-    if (wenv) {
-        int v[4];
-        if (sscanf(wenv, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0)
-            for (int t = 0; t < 4; ++t) w[t] = v[t];
-    }
+    const int w[4] = {213, 130, 130, 60};
     const double wsum = (double)(w[0] + w[1] + w[2] + w[3]);
     // exactly `cus` workgroups (largest remainders): one more than the CUs
     // would run two of them back to back on one CU (104 KB of LDS each)
@@ -1052,7 +1046,7 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const BwdHook *before_dw, const InterpFuse *ip) {
+               const InterpFuse *ip) {
     PSVO_REQUIRE(ip == nullptr || (kNC == 1 && gw[0] != nullptr),
                  "dec256_bwd: the fused interpolation backward needs the weight-gradient path (1 group per wave)");
     (void)feat;
@@ -1092,10 +1086,6 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
     if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "dec256_bwd: event record failed");
     if (!want_w) return PSVO_OK;
-    if (before_dw) {
-        const int rc = before_dw->fn(before_dw->ctx, st);
-        if (rc) return rc;
-    }
     DwPlan pl;
     int64_t slab_floats;
     dw_plan(m, &pl, &slab_floats);

@@ -56,9 +56,6 @@ struct PxArgs {
     int *counts;                 // [F][kPxMaxBlocks][2]: keys > T, keys = T
     double *wsum;                // [F][kPxMaxBlocks] partial weight sums
     uint32_t *keys;              // [F][n_pix] orderable score keys (written by pass 0)
-    // the FAST draw's candidate path (k_px_cand / k_px_pick), or nulls
-    int *fast;                   // [0, 32) candidates per frame, [32, 64) frame done (1) / overflow (−1)
-    uint32_t cand_t0;            // 24-bit keys >= cand_t0 are candidates (≈ 2k expected per frame)
 };
 
 __device__ __forceinline__ uint32_t px_mix32(uint64_t x) {
@@ -151,144 +148,6 @@ __global__ __launch_bounds__(kPxThreads) void k_px_wsum(PxArgs a) {
     }
 }
 
-// The FAST draw's first try: the picks are the n largest 24-bit keys m (ties
-// in pixel order), and the keys are uniform, so the ≈ 2n pixels with m >=
-// t0 (t0 set for 2n expected, ± √2n) hold them whenever there are >= n of
-// them.  k_px_cand collects those candidates (and writes every mask byte 0)
-// in one pass over the pixels; k_px_pick sorts a frame's candidates by (m
-// desc, pixel asc) in LDS, takes the first n — exactly the radix path's
-// picks — and writes them in pixel order.  A frame with fewer than n (or
-// more than kPxCandCap) candidates is left to the radix passes, which run
-// after them and return at once for the frames the candidates settled: one
-// full pass over the pixels instead of five beside the decoder forward.
-// Opt-in (PSVO_PX_CAND=1): measured slower in the bundle-adjust loop — the
-// per-frame sort workgroups hold four CUs the persistent decoder backward
-// then waits for.
-constexpr int kPxCandCap = 4096;       // candidates per frame (LDS sort of 4,096 u64)
-constexpr int kPxCandBlk = 256;        // candidates per k_px_cand workgroup
-constexpr int kPxCandMaxPick = 1024;   // n <= this
-constexpr int kPxPickThreads = 1024;
-
-__device__ __forceinline__ bool px_settled(const PxArgs &a, int f) { return a.fast && a.fast[32 + f] == 1; }
-
-__global__ __launch_bounds__(kPxThreads) void k_px_cand(PxArgs a, PxFrames fr) {
-    __shared__ uint32_t s_h[kPxCandBlk], s_i[kPxCandBlk];
-    __shared__ int s_n, s_base;
-    const int f = blockIdx.y, b = blockIdx.x;
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    uint8_t *mask = fr.f[f].mask;
-    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
-    for (int64_t r0 = i0 + kPxPer * threadIdx.x; r0 < i1; r0 += kPxRound) {
-#pragma unroll
-        for (int q = 0; q < kPxPer; ++q) {
-            const int64_t i = r0 + q;
-            if (i >= i1) break;
-            const uint32_t m = px_key_at<true, false>(a, f, i, 0.0f);
-            if (m >= a.cand_t0) {
-                const int at = atomicAdd(&s_n, 1);
-                if (at < kPxCandBlk) {
-                    s_h[at] = m;
-                    s_i[at] = (uint32_t)i;
-                }
-            }
-        }
-        if (mask) {  // every mask byte 0 here; k_px_pick sets the picks
-            uint8_t *mp = mask + r0;
-            if (r0 + kPxPer <= i1 && ((uintptr_t)mp & 3) == 0) {
-                *reinterpret_cast<uint32_t *>(mp) = 0u;
-            } else {
-                for (int q = 0; q < kPxPer && r0 + q < i1; ++q) mp[q] = 0;
-            }
-        }
-    }
-    __syncthreads();
-    const int n = s_n;
-    if (threadIdx.x == 0) {
-        if (n > kPxCandBlk) {
-            atomicExch(a.fast + 32 + f, -1);  // this block alone overflows: the radix passes
-            s_base = kPxCandCap;
-        } else {
-            s_base = n > 0 ? atomicAdd(a.fast + f, n) : 0;  // one per workgroup (no per-pixel atomics)
-        }
-    }
-    __syncthreads();
-    const int base = s_base;
-    uint32_t *ch = a.keys + (int64_t)f * a.n_pix, *ci = ch + kPxCandCap;
-    for (int j = threadIdx.x; j < n && j < kPxCandBlk; j += kPxThreads)
-        if (base + j < kPxCandCap) {
-            ch[base + j] = s_h[j];
-            ci[base + j] = s_i[j];
-        }
-}
-
-// one workgroup per frame: bitonic sort (descending) of the frame's
-// candidates as (m << 32 | ~pixel) — m desc, then pixel asc —, the first n
-// pixels sorted ascending, then index / mask / gathered rows in pixel order
-__global__ __launch_bounds__(kPxPickThreads) void k_px_pick(PxArgs a, PxFrames fr, int64_t *__restrict__ idx,
-                                                            float *__restrict__ out_dirs, float *__restrict__ out_rgb,
-                                                            float *__restrict__ out_depth) {
-    __shared__ uint64_t s_k[kPxCandCap];
-    __shared__ uint32_t s_p[kPxCandMaxPick];
-    const int f = blockIdx.x, t = threadIdx.x;
-    const int c = a.fast[f];
-    const int n = (int)a.k;
-    if (a.fast[32 + f] != 0 || c < n || c > kPxCandCap) return;  // overflow / too few: the radix passes
-    int N = 1;
-    while (N < c) N <<= 1;
-    const uint32_t *ch = a.keys + (int64_t)f * a.n_pix, *ci = ch + kPxCandCap;
-    for (int j = t; j < N; j += kPxPickThreads)
-        s_k[j] = j < c ? (((uint64_t)ch[j] << 32) | (uint64_t)(~ci[j])) : 0ull;  // pads sort last
-    __syncthreads();
-    for (int size = 2; size <= N; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int j = t; j < N; j += kPxPickThreads) {
-                const int l = j ^ stride;
-                if (l > j) {
-                    const uint64_t x = s_k[j], y = s_k[l];
-                    const bool desc = (j & size) == 0;  // descending runs first: the whole array descends
-                    if (desc ? x < y : x > y) {
-                        s_k[j] = y;
-                        s_k[l] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    int P = 1;
-    while (P < n) P <<= 1;
-    for (int j = t; j < P; j += kPxPickThreads) s_p[j] = j < n ? ~(uint32_t)s_k[j] : 0xffffffffu;
-    __syncthreads();
-    for (int size = 2; size <= P; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int j = t; j < P; j += kPxPickThreads) {
-                const int l = j ^ stride;
-                if (l > j) {
-                    const uint32_t x = s_p[j], y = s_p[l];
-                    const bool asc = (j & size) == 0;
-                    if (asc ? x > y : x < y) {
-                        s_p[j] = y;
-                        s_p[l] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    const psvo_pixel_frame F = fr.f[f];
-    for (int r = t; r < n; r += kPxPickThreads) {
-        const int64_t i = s_p[r];
-        const int64_t row = (int64_t)f * n + r;
-        if (idx) idx[row] = i;
-        if (out_dirs && F.dirs)
-            for (int q = 0; q < 3; ++q) out_dirs[row * 3 + q] = F.dirs[i * 3 + q];
-        if (out_rgb && F.rgb)
-            for (int q = 0; q < 3; ++q) out_rgb[row * 3 + q] = F.rgb[i * 3 + q];
-        if (out_depth && F.depth) out_depth[row] = F.depth[i];
-        if (F.mask) F.mask[i] = 1;
-    }
-    if (t == 0) a.fast[32 + f] = 1;
-}
-
 // Pick the bin holding the rem-th largest key of a histogram of 256 · BPT
 // bins (highest bin first): bin → *bin_out, keys still needed inside it →
 // *rem_out.  Thread t owns bins [BPT·t, BPT·t + BPT).
@@ -349,20 +208,14 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
 
 // pass P: histogram of digit P of the keys whose higher digits equal the
 // prefix picked so far
-// LB: the LDS histogram's bins.  kPxBins (16 KB) by default: the draw then
-// cannot co-reside with k_mlp_fwd2 (it leaves 3 KB of a CU's LDS) and waits
-// for CUs it frees.  PSVO_PX_SMALL_LDS=1 (A/B): the FAST digit's 256 bins
-// (1 KB), so the draw runs beside the decoder forward — measured slower
-// (config B, three interleaved pairs, one box: 0.921–0.926 vs 0.912–0.930
-// ms, GPU period 0.900–0.903 vs 0.893–0.901: the decoder kernels lose more
-// than the draw gains; profiles/r04px_ab_draw_lds.txt)
-template <bool FAST, int P, int LB = kPxBins>
+// (a 16-KB LDS histogram whatever the digit: 1-KB histograms for the FAST
+// digits, co-resident with the decoder forward, measured slower — the
+// decoder loses more than the draw gains, profiles/r04px_ab_draw_lds.txt)
+template <bool FAST, int P>
 __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
-    static_assert(LB >= (1 << px_width<FAST>(P)), "LDS histogram too small for the digit");
-    __shared__ int h[LB];
+    __shared__ int h[kPxBins];
     __shared__ int sh_suffix[kPxThreads];
     __shared__ int sh_res[2];
-    if (px_settled(a, blockIdx.y)) return;  // the candidate path picked this frame
     constexpr int kShift = px_shift<FAST>(P);
     constexpr uint32_t kMask = (1u << px_width<FAST>(P)) - 1u;
     constexpr int kBins = 1 << px_width<FAST>(P);
@@ -419,7 +272,6 @@ __global__ __launch_bounds__(kPxThreads) void k_px_count(PxArgs a) {
     __shared__ int sh_res[2];
     __shared__ int part[2][kPxThreads / kWave];
     const int f = blockIdx.y, b = blockIdx.x;
-    if (px_settled(a, f)) return;
     uint32_t T;
     int rem;
     px_state<FAST, px_passes<FAST>()>(a, f, sh_suffix, sh_res, T, rem);
@@ -455,7 +307,6 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
     __shared__ int part[2][kPxThreads / kWave];
     __shared__ int wave_tot[kPxThreads / kWave];
     const int f = blockIdx.y, b = blockIdx.x;
-    if (px_settled(a, f)) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kLast = px_passes<FAST>() - 1;
     const uint32_t T = (uint32_t)a.state[(f * 3 + kLast) * 2 + 0];
@@ -535,7 +386,7 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
 using namespace psvo;
 
 extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames, int64_t n_pix) {
-    return 64 /* candidate counters / flags */ + (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 +
+    return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 +
            (int64_t)n_frames * kPxMaxBlocks * 2 +
            (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */ + (int64_t)n_frames * n_pix;
 }
@@ -561,9 +412,7 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     a.seed = seed;
     a.joint_sum = joint_sum ? 1 : 0;
     a.n_frames = n_frames;
-    a.fast = nullptr;
-    a.cand_t0 = 0;
-    a.hist = workspace + 64;
+    a.hist = workspace;
     a.state = a.hist + (int64_t)3 * n_frames * kPxBins;
     a.counts = a.state + (int64_t)n_frames * 6;
     int *wp = a.counts + (int64_t)n_frames * kPxMaxBlocks * 2;
@@ -574,29 +423,11 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     if (frames)
         for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(workspace, 0, sizeof(int) * (64 + 3 * n_frames * kPxBins), st) != hipSuccess)
+    if (hipMemsetAsync(workspace, 0, sizeof(int) * (3 * n_frames * kPxBins), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
     const dim3 grid(a.nb, n_frames);
     if (weights) psvo::launch(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
-    static const bool small = getenv("PSVO_PX_SMALL_LDS") && *getenv("PSVO_PX_SMALL_LDS") == '1';
-    if (!weights && !u && small) {  // A/B: 1-KB LDS histograms (beside the decoder forward)
-        psvo::launch((k_px_hist<true, 0, 256>), grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch((k_px_hist<true, 1, 256>), grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch((k_px_hist<true, 2, 256>), grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
-    } else if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
-        // the candidate path first (PSVO_PX_CAND=1; unset / 0: the radix passes alone)
-        const char *cv = getenv("PSVO_PX_CAND");  // read per call: tests switch it
-        const bool cand_off = !(cv && *cv == '1');
-        if (!cand_off && k <= kPxCandMaxPick && n_pix >= 32 * k && n_pix >= 2 * kPxCandCap) {
-            a.fast = workspace;
-            const double want = 2.0 * (double)k * 16777216.0 / (double)n_pix;  // 2k expected candidates
-            a.cand_t0 = (uint32_t)(16777216.0 - ceil(want));
-            psvo::launch(k_px_cand, grid, dim3(kPxThreads), 0, st, a, fr);
-            psvo::launch(k_px_pick, dim3(n_frames), dim3(kPxPickThreads), 0, st, a, fr, idx, out_dirs, out_rgb,
-                         out_depth);
-        }
+    if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
         psvo::launch((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
         psvo::launch((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
         psvo::launch((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);

@@ -32,14 +32,23 @@ struct KernelClock {
     int depth = 0;
     bool sum = false;
     bool overflow = false;        // more launches / instances than slots: the surplus ran untimed
+    hipStream_t streams[4] = {};  // the arming engine's streams: launches on any other stream are not its own
+    bool owns(hipStream_t st) const {
+        for (hipStream_t s : streams)
+            if (s == st) return true;
+        return false;
+    }
 };
-extern KernelClock *g_kclock;  // engine.cpp: set while an engine with timing on queues a step
+// engine.cpp: set while an engine with timing on queues a step, on the thread
+// that queues it (another thread's launches, e.g. a tracking engine's, are
+// never attributed to it)
+extern thread_local KernelClock *g_kclock;
 
 template <typename... KArgs, typename... A>
 inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A &&...a) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     KernelClock *c = g_kclock;
-    if (c && c->depth > 0) {
+    if (c && c->depth > 0 && c->owns(st)) {
         if (c->n < KernelClock::kMax) {
             const int i = c->n++;
             e1 = c->ev[i][1];
@@ -105,7 +114,6 @@ struct PackRec {  // 32 B, 16-B aligned
 // thread polls the tags instead of waiting for an event (svo_query.hip)
 int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq);
 // the same granules from the statistics' device copy, which stays as it is
-int keep_to_host(hipStream_t st, const int *keep, unsigned long long *host, int words, int seq);
 // The Criterion's normalisers (criterion.py:70-101: the valid-depth rays and
 // the front / sdf samples over the padded [R_hit, S_max] layout) depend only
 // on the samples' depths and the rays' GT depth, so the sampler counts them
@@ -130,16 +138,14 @@ struct SampleCounts {
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep = nullptr,
+                        int *ray_ns, int *offsets, unsigned long long *host, int seq,
                         const SampleCounts *counts = nullptr, unsigned long long *lb_desc = nullptr,
                         uint32_t lb_tag = 0, int *leaf = nullptr, float *t = nullptr, int *ray_of = nullptr);
 // whether a query of r rays runs its statistics / rank pass and its sample
-// scan by look-back (PSVO_QUERY_SPLIT=1: never), and its descriptor granules
+// scan by look-back (up to kLbMaxRays rays), and its descriptor granules
 constexpr int64_t kLbMaxRays = 16384;  // 4 rays per workgroup, <= 64 · 64 workgroups (lookback.h)
 constexpr int kLbIsGranules = 5, kLbSmpGranules = 8;
 bool query_lookback(int64_t r);
-bool sampler_lookback();  // PSVO_LB_SAMPLER=0: the traversal's look-back only
-bool sampler_compacts();  // PSVO_LB_COMPACT=0: the look-back sampler without the compaction
 int64_t lookback_granules(int64_t r);
 
 // one element of the Adam step (k_adam; optim.hip's formulation), shared so
@@ -193,7 +199,6 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef);
 
-struct DevBatch;
 // psvo_criterion_coef / psvo_composite_loss reading z from rows of stride
 // z_stride >= s_max (the sampler's [R, cap] depth rows, the engine's mapping
 // path: no padded [R_hit, S_max] copy; ray_ns: the rows' valid samples, past
@@ -205,24 +210,30 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
                      const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_rgb,
                      const float *gt_depth, const float *sdf_s, const float *rgb_s, const float *coef,
                      float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s,
-                     bool partials = true);  // false: no loss partials (the loss value is not wanted)
+                     bool partials = true,  // false: no loss partials (the loss value is not wanted)
+                     const int *cidx = nullptr);  // the sparse decoder's compact sample index (select_samples)
+// The sparse decoder's sample selection (composite.hip k_select_samples): the
+// samples whose gradients can be non-zero (composited or inside a loss mask)
+// get compact, ray-major indices cidx[s] (-1: dropped), compact ray offsets
+// offb [R_hit + 1] and compact copies of their features / leaf / t / ray;
+// counts[0] = kept samples (the compact decoder launches read it on the
+// device), counts[1] = composited samples, counts[2] |= 8 if the look-back
+// wait was abandoned (then counts[0] = 0); counts + 4: u64 running sums of
+// kept / composited samples and of launches (kSelCountInts ints, zeroed
+// once).  desc: select_granules(r_hit) granules, zeroed once; tag fresh per
+// launch (≠ 0).
+constexpr int kSelCountInts = 10;
+int select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
+                   const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_depth,
+                   const float *sdf_s, const float *feat, const int *leaf, const float *t, const int *ray_of,
+                   int *cidx, int *offb, float *feat_b, int *leaf_b, float *t_b, int *ray_of_b, int *counts,
+                   unsigned long long *desc, uint32_t tag);
+int select_rays_per_wave(int64_t r_hit);
+int64_t select_granules(int64_t r_hit);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
 // the valid prefix of each sampler row → leaf / t / ray_of_sample at offsets[r] + s
-// Warm every XCD's L2 with up to 4 small read-only arrays (bytes multiple of
-// 16) right before the kernels that read them (svo_query.hip); `sink` gets a
-// write only in the impossible case that keeps the loads alive.
-int l2_prefetch(hipStream_t st, int n, const void *const *ptr, const int64_t *bytes, float *sink);
 int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const float *s_depth, const int *offsets,
-                 int *leaf, float *t, int *ray_of_sample, const DevBatch &dev);
-// sample compaction + interpolation forward, one wave per hit ray (the
-// engine's mapping path, interp.hip k_interp_fwd_rays): the valid prefix of
-// each sampler row s_idx / s_depth [R, cap] goes to compact positions
-// offsets[r] + s — leaf / t / ray_of_sample and the features (k_interp_fwd's
-// arithmetic, the same bits); dev.stats: R_hit from the device statistics
-int interp_fwd_rays(hipStream_t st, int64_t r_hit, int cap, float voxel_size, const int *s_idx, const float *s_depth,
-                    const int *offsets, const int *ray_index, const float *rays_o, const float *rays_d,
-                    const float *centres, const int *vertex_idx, const float *emb, int *leaf, float *t,
-                    int *ray_of_sample, float *feat, const DevBatch &dev);
+                 int *leaf, float *t, int *ray_of_sample);
 
 // width-256 decoder (mlp256.hip): sizes, operand images, forward (act /
 // masks NULL: inference), backward (gw[0] NULL: δ chain to dfeat only)
@@ -235,20 +246,13 @@ int dec256_images(hipStream_t st, const float *w1, const float *b1, const float 
                   const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
 int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images, float *sdf, float *rgb, float *act,
                uint64_t *masks);
-// work a caller puts between the width-256 δ chain (dfeat written) and its
-// weight-gradient kernels, on the same stream (the engine's interpolation
-// backward, serialised: PSVO_IB256_SERIAL=1)
-struct BwdHook {
-    int (*fn)(void *ctx, hipStream_t st);
-    void *ctx;
-};
 struct InterpFuse;
 // ip (the mapping engine's width-256 step): the interpolation backward runs
 // inside the δ-chain kernel (dfeat is then not stored), as at width 128
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const BwdHook *before_dw = nullptr, const InterpFuse *ip = nullptr);
+               const InterpFuse *ip = nullptr);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 
@@ -299,39 +303,6 @@ __device__ __forceinline__ void crit_coef_from_counts(double n_valid_d, double n
     coef[3] = (flags & PSVO_CRIT_USE_SDF) ? (float)(2.0 * (double)(sdf_w * sdf_weight) / n_el) * tr : 0.0f;
 }
 
-// A device-sized launch of the render's forward (engine: no host read-back
-// before it): the batch's R_hit / S_max / M come from the query's statistics
-// on the device, the buffers hold r_cap × s_cap and m_cap; a batch beyond
-// them (or a failed query) makes every such kernel do nothing, and the host,
-// which reads the statistics while the decoder runs, re-runs host-sized.
-struct DevBatch {
-    const int *stats;
-    int64_t r_cap, m_cap;
-    int s_cap;
-};
-__device__ __forceinline__ bool dev_batch_fits(const DevBatch &b) {
-    return b.stats[PSVO_STAT_R_HIT] <= b.r_cap && b.stats[PSVO_STAT_S_MAX] <= b.s_cap &&
-           b.stats[PSVO_STAT_M] <= b.m_cap && !(b.stats[PSVO_STAT_FLAGS] & 3);
-}
-// M of the batch, or 0 when it does not fit
-__device__ __forceinline__ int64_t dev_batch_m(const DevBatch &b) {
-    return dev_batch_fits(b) ? (int64_t)b.stats[PSVO_STAT_M] : 0;
-}
-int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, const int *s_idx, const float *s_depth,
-                      const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals, uint8_t *mask);
-int interp_fwd_dev(hipStream_t st, const DevBatch &b, float voxel_size, const int *leaf, const float *t,
-                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
-                   const float *centres, const int *vertex_idx, const float *emb, float *feat);
-// sample compaction + interpolation forward in one launch (k_points_interp:
-// the outputs of psvo_sample_points and psvo_interp_fwd, same bits)
-int points_interp(hipStream_t st, int64_t r_hit, int s_max, int max_steps_cap, float voxel_size, const int *s_idx,
-                  const float *s_depth, const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals,
-                  uint8_t *mask, const int *ray_index, const float *rays_o, const float *rays_d,
-                  const float *centres, const int *vertex_idx, const float *emb, float *feat);
-// the width-128 training forward (k_mlp_fwd2) on the device-sized batch; images prepared
-int mlp_fwd_dev(hipStream_t st, const DevBatch &b, const float *feat, const float *images, float *sdf, float *rgb,
-                float *act, uint64_t *masks);
-
 // The interpolation backward (interp.hip's k_interp_bwd: embedding scatter
 // and dL/dx) folded into the width-128 fused decoder backward, per 16-sample
 // unit right after its dfeat: grad_emb (zeroed by the caller) += the
@@ -353,14 +324,16 @@ int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int 
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
 // dfeat is written, before the weight-gradient kernels are queued; with `ip`
 // (width 128, fused backward) it also runs the interpolation backward and
-// dfeat is not stored
+// dfeat is not stored.  m_dev (width 128; the sparse decoder): the sample
+// count is read on the device (select_samples' counts[0] <= m; the buffers
+// are sized for m).
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
             const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr,
-            hipStream_t reduce_stream = nullptr, const BwdHook *before_dw = nullptr);
+            hipStream_t reduce_stream = nullptr, const int *m_dev = nullptr);
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
 // the look-ahead's split tail (psvo_map_step_frames): the weight-gradient
@@ -377,7 +350,7 @@ int mlp_images(void *stream, int width, const float *w1, const float *b1, const 
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                     float *act, uint64_t *masks);
+                     float *act, uint64_t *masks, const int *m_dev = nullptr);  // m_dev: as mlp_bwd (width 128)
 
 }  // namespace psvo
 

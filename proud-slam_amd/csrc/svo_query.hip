@@ -720,10 +720,10 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     uint32_t ex[5];
     const bool ok = lb_scan<5, 0b00110u>(lb_desc, (int)blockIdx.x, (int)gridDim.x, lb_tag, lane, agg, ex);
     const int64_t rr = (int64_t)blockIdx.x * kIsWaves + lane;
-    if (lane < kIsWaves && rr < n_rays) {
+    if (lane < kIsWaves && rr < n_rays) {  // an abandoned wait (!ok) leaves `ex` undefined: no rank stores
         const int rk = (int)ex[0] + __popcll(hm & below);
-        ray_rank[rr] = nv_l > 0 ? rk : -1;
-        if (nv_l > 0) rank_ray[rk] = (int)rr;
+        ray_rank[rr] = (nv_l > 0 && ok) ? rk : -1;
+        if (nv_l > 0 && ok) rank_ray[rk] = (int)rr;
     }
     if (lane == 0 && blockIdx.x == gridDim.x - 1) {  // the stats words were zeroed by the last read-back
         stats[PSVO_STAT_P] = (int)max(ex[1], agg[1]);
@@ -733,14 +733,6 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         atomicAdd(stats + PSVO_STAT_ROUNDS, (int)(ex[4] + agg[4]));
     }
     if (!ok && lane == 0) atomicOr(stats + PSVO_STAT_FLAGS, kLbFlagTimeout);
-}
-
-// the statistics read-back from the device copy (`keep`, which the device-
-// sized kernels read: not zeroed), on a stream of its own (engine: the
-// sampler then writes no host memory)
-__global__ void k_keep_to_host(const int *__restrict__ keep, unsigned long long *host, int words, int seq) {
-    const int i = threadIdx.x;
-    if (i < words) stat_to_host(host, i, keep[i], seq);
 }
 
 // one wave, one word per lane (words <= 64)
@@ -1318,7 +1310,6 @@ struct SampleTail {
     int *offsets;              // [R_hit + 1] exclusive scan of ray_ns
     unsigned long long *host;  // PSVO_STAT_WORDS granules (stat_to_host)
     int seq;
-    int *keep;                 // device copy of the statistics (DevBatch), or null
     SampleCounts c;            // the Criterion's normalisers (c.gt_depth null: not counted)
     unsigned long long *desc;  // look-back descriptors (lookback.h), or null
     uint32_t tag;              // this launch's descriptor tag
@@ -1412,8 +1403,8 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     // k_compact_rays' work: the row's valid prefix to its compacted place —
     // the first kSmpStage samples from LDS, the rest (rows longer than that)
     // read back from the row with sc1 loads (this wave's own stores, past L1)
-    if (count <= 0) return;
     const int off = s_off[w];
+    if (count <= 0 || off < 0) return;
     const int *oi = s_idx + (int64_t)il * max_steps_cap;
     const float *od = s_depth + (int64_t)il * max_steps_cap;
     for (int s = lane; s < count; s += kWave) {
@@ -1562,8 +1553,9 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
     const int last = n > 0 ? (n - 1) / 4 : 0;  // the workgroups past it returned without a descriptor
     const bool ok = lb_scan<NG, 0b10u>(tl.desc, (int)blockIdx.x, last + 1, tl.tag, lane, agg, ex);
     const int il = (int)blockIdx.x * 4 + lane;
-    if (lane < 4) s_off[lane] = (int)ex[0] + before;  // the in-launch compaction's
-    if (lane < 4 && il < n) tl.offsets[il] = (int)ex[0] + before;
+    // an abandoned wait (!ok: `ex` undefined) stores no offset, and the compaction skips its rows
+    if (lane < 4) s_off[lane] = ok ? (int)ex[0] + before : -1;  // the in-launch compaction's
+    if (lane < 4 && il < n && ok) tl.offsets[il] = (int)ex[0] + before;
     if ((int)blockIdx.x != last) return;
     const int tot = (int)(ex[0] + agg[0]);
     const int smax = (int)max(ex[1], agg[1]);
@@ -1585,19 +1577,18 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
         int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : st_word;
         if (lane == PSVO_STAT_FLAGS && n > 0 && max_steps > max_steps_cap) v |= 2;
         if (lane == PSVO_STAT_FLAGS && !ok) v |= kLbFlagTimeout;
-        if (tl.keep) tl.keep[lane] = v;
         stats[lane] = 0;  // ready for the query set's next use (no memset launch)
-        if (tl.host) stat_to_host(tl.host, lane, v, tl.seq);  // else k_keep_to_host on another stream
+        if (tl.host) stat_to_host(tl.host, lane, v, tl.seq);
     }
 }
 
 // offsets[0..R_hit] = exclusive scan of ray_ns; S_max and M into stats.  With
 // `host` the statistics go to the host and `stats` is zeroed for the next
-// query (`keep`, if set, holds a device copy).
+// query.
 __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                        const int *__restrict__ ray_ns, int *__restrict__ offsets,
                                                        int *__restrict__ stats, int dist, unsigned long long *host,
-                                                       int seq, int *__restrict__ keep, SampleCounts cnt) {
+                                                       int seq, SampleCounts cnt) {
     __shared__ int total;
     __shared__ int smax[16];
     __shared__ long long s_c[7][16];
@@ -1693,7 +1684,6 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         if (host) {  // the engine's read-back (every reader of stats is past the barrier)
             if (lane < PSVO_STAT_WORDS) {
                 const int v = lane == PSVO_STAT_S_MAX ? bm : lane == PSVO_STAT_M ? tot : stats[lane];
-                if (keep) keep[lane] = v;  // the device-sized forward's copy (DevBatch)
                 stats[lane] = 0;
                 stat_to_host(host, lane, v, seq);
             }
@@ -1755,7 +1745,6 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
         if (host) {  // the engine's read-back, as k_stats_to_host (every reader of stats is past the barrier)
             if (lane < PSVO_STAT_WORDS) {
                 const int v = lane == PSVO_STAT_S_MAX ? mx : lane == PSVO_STAT_M ? tot : stats[lane];
-                if (keep) keep[lane] = v;  // the device-sized forward's copy (DevBatch)
                 stats[lane] = 0;
                 stat_to_host(host, lane, v, seq);
             }
@@ -1768,18 +1757,11 @@ __global__ __launch_bounds__(1024) void k_scan_samples(int64_t row_begin, int64_
 
 // ---------------------------------------------------------------------------
 // z_vals / mask [R_hit, S_max] and ray-major compacted samples.
-// dev.stats (device-sized launch, psvo::sample_points_dev, DevBatch): R_hit
-// and S_max come from the query's statistics on the device.
 __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__restrict__ s_idx,
                                 const float *__restrict__ s_depth, const int *__restrict__ ray_ns,
                                 const int *__restrict__ offsets, int *__restrict__ leaf, float *__restrict__ t,
                                 int *__restrict__ ray_of_sample, float *__restrict__ z_vals,
-                                uint8_t *__restrict__ mask, DevBatch dev) {
-    if (dev.stats) {
-        const bool fits = dev_batch_fits(dev);
-        r_hit = fits ? dev.stats[PSVO_STAT_R_HIT] : 0;
-        s_max = dev.stats[PSVO_STAT_S_MAX];
-    }
+                                uint8_t *__restrict__ mask) {
     // grid rows stride over the hit rays (no 64-bit division per element)
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= s_max) return;
@@ -1805,13 +1787,11 @@ __global__ void k_sample_points(int64_t r_hit, int s_max, int cap, const int *__
 // kernels read z from the sampler's rows, so no padded [R_hit, S_max] copy):
 // one wave per hit ray copies the valid prefix of its sampler row to the
 // compact arrays — ns ≈ 64 entries, not the S_max-wide row k_sample_points
-// walks.  dev.stats: R_hit from the device statistics.
+// walks.
 __global__ __launch_bounds__(256) void k_compact_rays(int64_t r_hit, int cap, const int *__restrict__ s_idx,
                                                       const float *__restrict__ s_depth,
                                                       const int *__restrict__ offsets, int *__restrict__ leaf,
-                                                      float *__restrict__ t, int *__restrict__ ray_of_sample,
-                                                      DevBatch dev) {
-    if (dev.stats) r_hit = dev_batch_fits(dev) ? dev.stats[PSVO_STAT_R_HIT] : 0;
+                                                      float *__restrict__ t, int *__restrict__ ray_of_sample) {
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const int lane = threadIdx.x & (kWave - 1);
@@ -1975,24 +1955,13 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
 namespace psvo {
 // The statistics / rank pass and the sample scan: by default inside the
 // traversal and sampler launches by decoupled look-back (lookback.h; up to
-// kLbMaxRays rays: the packed pf / psm count granule); PSVO_QUERY_SPLIT=1
-// runs them as kernels of their own (k_ray_stats_rank, k_scan_samples).  The
+// kLbMaxRays rays: the packed pf / psm count granule); beyond that, and on
+// the data-parallel sampler, as kernels of their own (k_ray_stats_rank,
+// k_scan_samples).  The
 // round-3 in-launch variant — the launch's last-arriving workgroup re-reading
 // every ray — measured slower than the split kernels (one workgroup's
 // dependent sc1 round trips) and is gone.
-bool query_lookback(int64_t r) {
-    const char *v = getenv("PSVO_QUERY_SPLIT");  // read per query: tests switch it between steps
-    const bool split = v && *v == '1';
-    return !split && r > 0 && r <= kLbMaxRays;
-}
-bool sampler_lookback() {
-    const char *v = getenv("PSVO_LB_SAMPLER");  // 0: the sampler's scan as k_scan_samples (A/B)
-    return !(v && *v == '0');
-}
-bool sampler_compacts() {
-    const char *v = getenv("PSVO_LB_COMPACT");  // 0: k_compact_rays after the read-back (A/B)
-    return !(v && *v == '0');
-}
+bool query_lookback(int64_t r) { return r > 0 && r <= kLbMaxRays; }
 int64_t lookback_granules(int64_t r) {
     return lb_granules<kLbIsGranules>(div_up(r, 4)) + lb_granules<kLbSmpGranules>(div_up(r, 4));
 }
@@ -2001,17 +1970,15 @@ int64_t lookback_granules(int64_t r) {
 int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
-                        int *ray_ns, int *offsets, unsigned long long *host, int seq, int *keep,
-                        const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
+                        int *ray_ns, int *offsets, unsigned long long *host, int seq, const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
                         float *t, int *ray_of) {
-    PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && (host || (lb_desc && keep)),
+    PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host,
                  "sample_rays_to_host: bad arguments");
     PSVO_REQUIRE(!lb_desc || (r_hit_cap <= kLbMaxRays && lb_tag != 0), "sample_rays_to_host: look-back arguments");
     SampleTail tl{};
     if (counts) tl.c = *counts;
     tl.host = host;
     tl.seq = seq;
-    tl.keep = keep;
     if (lb_desc) {  // after the traversal's descriptors (lookback_granules)
         tl.offsets = offsets;
         tl.desc = lb_desc + lb_granules<kLbIsGranules>(div_up(r_hit_cap, 4));
@@ -2027,14 +1994,10 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                        s_dist, ray_ns, nullptr, 0, tl);
     if (!lb_desc)
         psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
-                           host, seq, keep, tl.c);
+                           host, seq, tl.c);
     return check_launch("sample_rays_to_host");
 }
 
-int keep_to_host(hipStream_t st, const int *keep, unsigned long long *host, int words, int seq) {
-    psvo::launch(k_keep_to_host, dim3(1), dim3(64), 0, st, keep, host, words, seq);
-    return check_launch("keep_to_host");
-}
 int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq) {
     psvo::launch(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
     return check_launch("stats_to_host");
@@ -2095,7 +2058,7 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch, SampleTail{});
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
-                       nullptr, 0, nullptr, SampleCounts{});
+                       nullptr, 0, SampleCounts{});
     return check_launch("dist_sample");
 }
 int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
@@ -2129,7 +2092,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{});
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
-                       stats, 0, nullptr, 0, nullptr, SampleCounts{});
+                       stats, 0, nullptr, 0, SampleCounts{});
     return check_launch("sample_rays");
 }
 
@@ -2166,70 +2129,20 @@ extern "C" int psvo_sample_points(void *stream, int64_t r_hit, int s_max, int ma
     const int bx = s_max <= 64 ? 64 : s_max <= 128 ? 128 : 256;
     const unsigned gy = (unsigned)(r_hit < 65535 ? r_hit : 65535);
     psvo::launch(k_sample_points, dim3(div_up(s_max, bx), gy), dim3(bx), 0, as_stream(stream), r_hit,
-                       s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask,
-                       DevBatch{});
+                       s_max, max_steps_cap, s_idx, s_depth, ray_ns, offsets, leaf, t, ray_of_sample, z_vals, mask);
     return check_launch("sample_points");
 }
 
 namespace psvo {
-namespace {
-// The query's and the interpolation's read-only arrays (packed octree
-// records, leaf vertex rows / centres, the embedding table) are cold in the
-// XCD L2s at each iteration's query: the decoder's activations streamed
-// through them since.  Workgroup b runs on XCD b mod 8 (round-robin
-// dispatch); the kPerXcd workgroups of each XCD sweep every array once, so
-// the query's dependent record loads hit L2 instead of the MALL / HBM.
-constexpr int kPerXcd = 16;
-struct PrefetchList {
-    const float4 *p[4];
-    int64_t n16[4];
-    int n;
-};
-__global__ __launch_bounds__(256) void k_l2_prefetch(PrefetchList L, float *__restrict__ sink) {
-    const int k = blockIdx.x >> 3;  // this workgroup's share of its XCD's sweep
-    float acc = 0.f;
-    for (int a = 0; a < L.n; ++a)
-        for (int64_t i = (int64_t)k * 256 + threadIdx.x; i < L.n16[a]; i += (int64_t)kPerXcd * 256) {
-            const float4 v = L.p[a][i];
-            acc += v.x;
-        }
-    if (acc == 1.2345678e-37f) sink[0] = acc;  // keeps the loads; practically never taken
-}
-}  // namespace
-
-int l2_prefetch(hipStream_t st, int n, const void *const *ptr, const int64_t *bytes, float *sink) {
-    PSVO_REQUIRE(n >= 0 && n <= 4 && sink, "l2_prefetch: bad arguments");
-    PrefetchList L{};
-    for (int a = 0; a < n; ++a) {
-        if (!ptr[a] || bytes[a] <= 0) continue;
-        L.p[L.n] = static_cast<const float4 *>(ptr[a]);
-        L.n16[L.n] = bytes[a] / 16;
-        L.n++;
-    }
-    if (L.n == 0) return PSVO_OK;
-    psvo::launch(k_l2_prefetch, dim3(8 * kPerXcd), dim3(256), 0, st, L, sink);
-    return check_launch("l2_prefetch");
-}
-
 int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const float *s_depth, const int *offsets,
-                 int *leaf, float *t, int *ray_of_sample, const DevBatch &dev) {
+                 int *leaf, float *t, int *ray_of_sample) {
     PSVO_REQUIRE(r_hit >= 0 && cap > 0, "compact_rays: bad sizes");
     if (r_hit == 0) return PSVO_OK;
     psvo::launch(k_compact_rays, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, cap, s_idx, s_depth, offsets,
-                       leaf, t, ray_of_sample, dev);
+                       leaf, t, ray_of_sample);
     return check_launch("compact_rays");
 }
 
-int sample_points_dev(hipStream_t st, const DevBatch &b, int max_steps_cap, const int *s_idx, const float *s_depth,
-                      const int *offsets, int *leaf, float *t, int *ray_of_sample, float *z_vals, uint8_t *mask) {
-    PSVO_REQUIRE(b.stats && b.r_cap > 0 && b.s_cap > 0 && b.s_cap <= max_steps_cap && b.m_cap > 0,
-                 "sample_points_dev: bad sizes");
-    const int bx = b.s_cap <= 64 ? 64 : b.s_cap <= 128 ? 128 : 256;
-    const unsigned gy = (unsigned)(b.r_cap < 65535 ? b.r_cap : 65535);
-    psvo::launch(k_sample_points, dim3(div_up(b.s_cap, bx), gy), dim3(bx), 0, st, b.r_cap, b.s_cap,
-                       max_steps_cap, s_idx, s_depth, nullptr, offsets, leaf, t, ray_of_sample, z_vals, mask, b);
-    return check_launch("sample_points_dev");
-}
 }  // namespace psvo
 
 #ifdef PSVO_IS_STAMPS

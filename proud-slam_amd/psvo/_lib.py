@@ -75,6 +75,8 @@ _SIGNATURES = {
     "psvo_engine_new": (_vp, []),
     "psvo_engine_free": (None, [_vp]),
     "psvo_engine_set_timing": (_i32, [_vp, _i32]),
+    "psvo_engine_set_paths": (_i32, [_vp, _i32]),
+    "psvo_engine_select_stats": (_i32, [_vp, _vp, _vp, _i32]),
     "psvo_engine_queued": (_i32, [_vp]),
     "psvo_map_discard": (_i32, [_vp]),
     "psvo_engine_exchange_words": (_i64, [_i32, _i64]),
@@ -93,8 +95,8 @@ _SIGNATURES = {
     "psvo_map_step_frames": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _i64, _i32, _vp, _vp]),
     "psvo_pose_rays_frames": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "psvo_pose_grad_frames": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _u64, _i64, _i32, _vp, _vp,
-                               _vp]),
+    "psvo_track_step": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _u64, _i64, _i32, _vp,
+                               _vp, _vp]),
     "psvo_pose_rays": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "psvo_mesh_linspace": (_i32, [_i32, _vp]),
     "psvo_mesh_case_table": (_i32, [_vp, _vp]),

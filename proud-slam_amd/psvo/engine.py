@@ -375,6 +375,26 @@ class MappingEngine:
         L.call("psvo_map_adam_ex", self.handle, L.stream_of(self.emb.device), ctypes.addressof(self.desc),
                self.step_no, 1 if marked else 0)
 
+    PATH_QUERY_SPLIT, PATH_PADDED, PATH_DENSE_DECODER = 1, 2, 4
+
+    def set_paths(self, paths):
+        """Run the alternative production kernels on this single-GPU engine
+        (cross-checks): PATH_QUERY_SPLIT — the query's statistics / rank pass
+        and sample scan as kernels of their own; PATH_PADDED — the padded z
+        copy and in-step loss normalisers; PATH_DENSE_DECODER — the width-128
+        decoder on every sample instead of the sparse decoder
+        (psvo_engine_set_paths)."""
+        L.call("psvo_engine_set_paths", self.handle, int(paths))
+
+    def select_stats(self, reset=False):
+        """The sparse decoder's sample selection (synchronises): {"kept",
+        "composited"} of the last step and their sums over "steps" steps since
+        the last reset (psvo_engine_select_stats)."""
+        out = (ctypes.c_int64 * 5)()
+        L.call("psvo_engine_select_stats", self.handle, L.stream_of(self.emb.device), ctypes.cast(out, ctypes.c_void_p),
+               int(bool(reset)))
+        return {"kept": out[0], "composited": out[1], "kept_sum": out[2], "composited_sum": out[3], "steps": out[4]}
+
     def set_timing(self, on):
         """Per-region kernel time (query: intersect / sample / points, interp fwd
         / bwd, decoder fwd / bwd): each kernel a region launches is timed by a
@@ -403,7 +423,7 @@ class MappingEngine:
         L.call("psvo_host_wait_stats", ctypes.byref(us), ctypes.byref(calls), ctypes.byref(waited), int(reset))
         return us.value, calls.value, waited.value
 
-    REGIONS = ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd", "intersect", "sample", "points")
+    REGIONS = ("mlp_fwd", "mlp_bwd", "interp_fwd", "interp_bwd", "intersect", "sample", "points", "select")
 
     def timing(self):
         """Mean ms per step of each PSVO_TIME_* region since set_timing(True)."""
@@ -482,28 +502,36 @@ class TrackingEngine:
         self.pose_v.zero_()
         self.step_no = 0
 
-    def step(self, dirs_cam, rgb, depth, seed, lr=1e-3, depth_variance=False, apply_adam=True):
+    def step(self, dirs_cam, rgb, depth, seed, lr=1e-3, depth_variance=False, apply_adam=True, noise=None):
         """One iteration on camera-frame directions [R,3] with their gt rgb
-        [R,3] / depth [R]; returns the loss (0-dim device tensor, reused)."""
+        [R,3] / depth [R]; returns the loss (0-dim device tensor, reused).
+        noise: the sampler's noise [200, K', max_steps] (as the reference
+        draws it; tests), else drawn on the device from `seed`."""
         dirs = dirs_cam.reshape(-1, 3).float().contiguous()
         gt_rgb = rgb.reshape(-1, 3).float().contiguous()
         gt_d = depth.reshape(-1).float().contiguous()
+        nz = None
+        if noise is not None:
+            nz = torch.as_tensor(noise).to(device=self.dev, dtype=torch.float32).contiguous()
+            if nz.dim() != 3 or nz.shape[0] != 200 or nz.shape[1] != -(-dirs.shape[0] // 200):
+                raise ValueError(f"TrackingEngine.step: noise must be [200, K', max_steps], got {tuple(nz.shape)}")
         self.step_no += 1
         flags = (0 if apply_adam else 1) | (2 if depth_variance else 0)
         rc = _lib().psvo_track_step(self.handle, L.stream_of(self.dev), ctypes.addressof(self.desc), dirs.shape[0],
                                     dirs.data_ptr(), gt_rgb.data_ptr(), gt_d.data_ptr(), self.pose.data_ptr(),
-                                    self.pose_m.data_ptr(), self.pose_v.data_ptr(), float(lr), int(seed),
-                                    self.step_no, flags, self.pose_grad.data_ptr(), self.loss_out.data_ptr(),
-                                    ctypes.addressof(self.stats))
+                                    self.pose_m.data_ptr(), self.pose_v.data_ptr(), float(lr),
+                                    nz.data_ptr() if nz is not None else None, int(seed), self.step_no, flags,
+                                    self.pose_grad.data_ptr(), self.loss_out.data_ptr(), ctypes.addressof(self.stats))
         if rc != 0:
             raise L.PsvoError(f"psvo_track_step failed (code {rc}): {_lib().psvo_last_error().decode()}")
         return self.loss_out[0]
 
     def track_frame(self, frame_pose, curr_frame, N_rays=512, num_iterations=10, learning_rate=1e-3,
-                    depth_variance=False, seed=None):
+                    depth_variance=False, seed=None, noise=None):
         """track_frame (render_helpers.py:679-761) on the native step: samples
         N_rays pixels per iteration from curr_frame (sample_rays → sample_idx)
-        and returns an OptimizablePose holding the optimised parameters."""
+        and returns an OptimizablePose holding the optimised parameters.
+        noise: a callable iteration → the sampler noise (tests)."""
         from .pose import OptimizablePose
         self.reset(frame_pose.data.detach())
         dirs_all = curr_frame.rays_d.reshape(-1, 3)
@@ -514,7 +542,7 @@ class TrackingEngine:
             curr_frame.sample_rays(N_rays)
             idx = curr_frame.sample_idx
             self.step(dirs_all.index_select(0, idx), rgb_all.index_select(0, idx), depth_all.index_select(0, idx),
-                      base + it, learning_rate, depth_variance)
+                      base + it, learning_rate, depth_variance, noise=noise(it) if callable(noise) else None)
         return OptimizablePose(self.pose.detach().clone())
 
     @property

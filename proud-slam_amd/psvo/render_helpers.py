@@ -561,19 +561,12 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         side.wait_stream(main)  # the keyframes as the caller left them
     clk("side")
 
-    # PSVO_DRAW_AFTER_BWD=1 (A/B, off): each next draw waits for the previous
-    # step's decoder backward (psvo_map_side_wait), so it runs beside the
-    # look-ahead query instead of beside the persistent decoder kernels.
-    # Measured (config B, three interleaved pairs, one box): 1.000-1.059 vs
-    # 0.985-1.000 ms per iteration as soon as queued (C: 3.711 vs 3.693 ms) —
-    # the decoder kernels gain less than the latency-bound query loses
-    draw_after_bwd = os.environ.get("PSVO_DRAW_AFTER_BWD", "0") == "1"
-
+    # each next draw is queued as soon as its step is (beside the persistent
+    # decoder kernels); ordered after the previous step's decoder backward it
+    # measured slower (round 4, config B: 1.000-1.059 vs 0.985-1.000 ms)
     def draw_ahead(it):
         if side is None:
             return draw(it), None
-        if draw_after_bwd and it > 0:
-            eng.side_wait(side)
         with torch.cuda.stream(side):
             out = draw(it)
         if it == 0:
@@ -746,8 +739,10 @@ def bundle_adjust_frames(keyframe_graph, map_states, sdf_network, resnet, loss_c
 
 def track_frame(frame_pose, curr_frame, map_states, sdf_network, resnet, loss_criteria, voxel_size, N_rays=512,
                 step_size=0.05, num_iterations=10, truncation=0.1, learning_rate=1e-3, max_voxel_hit=10,
-                max_distance=10, profiler=None, depth_variance=False):
-    """render_helpers.py:679-761 — pose-only optimisation of one frame."""
+                max_distance=10, profiler=None, depth_variance=False, noise=None):
+    """render_helpers.py:679-761 — pose-only optimisation of one frame.
+    noise: a callable iteration → the sampler noise (tests; the reference
+    draws it inside InverseCDFRaySampling)."""
     init_pose = deepcopy(frame_pose).cuda()
     init_pose.requires_grad_(True)
     optim = torch.optim.Adam(init_pose.parameters(), lr=learning_rate)
@@ -762,7 +757,8 @@ def track_frame(frame_pose, curr_frame, map_states, sdf_network, resnet, loss_cr
         ray_start_iter = init_pose.translation().reshape(1, 1, -1).expand_as(ray_dirs_iter).cuda().contiguous()
         final_outputs = render_rays(ray_start_iter, ray_dirs_iter, map_states, sdf_network, resnet, step_size,
                                     voxel_size, truncation, max_voxel_hit, max_distance,
-                                    profiler=profiler if it == 0 else None)
+                                    profiler=profiler if it == 0 else None,
+                                    noise=noise(it) if callable(noise) else None)
         hit_mask = final_outputs["ray_mask"].view(N_rays)
         final_outputs["ray_mask"] = hit_mask
         loss, _ = loss_criteria(final_outputs, (rgb, depth), weight_depth_loss=depth_variance)

@@ -20,6 +20,10 @@ pose Adam on the non-first keyframes) — see run_ba_case / BA_CASES: room0
 at W = 128, the same with the points encoder + its optimiser passed as
 Mapping.do_mapping passes them, and ScanNet settings at W = 256.
 
+T_track.npz: the reference's track_frame with depth_variance=True (the call
+Tracking.do_tracking makes): per-iteration losses, noise and picks, the
+median depth filter's dropped rays, the final pose and hit mask.
+
 M_mesh_A.npz: the reference's get_scores / eval_points (mesh extraction's
 lattice scores and vertex colours) on the A octree's first 40 SURFACE voxels.
 
@@ -390,6 +394,101 @@ def run_ba_case(rh, nrgbd, crit_mod, noise_log, name="BA_room0"):
     return rec
 
 
+def track_setup():
+    """The T_track case's inputs (also rebuilt by the tests): room0, one frame
+    at 0.1 of the Replica resolution, a start pose perturbed from the frame's
+    pose, N_rays pixels per iteration replayed from seeded permutations."""
+    scene = syn.room0()
+    vox = syn.surface_voxels(scene, seed=0)
+    T = syn.camera_poses(scene, 1, seed=23)[0]
+    from scipy.spatial.transform import Rotation as Rr
+    dT = np.eye(4)
+    dT[:3, :3] = Rr.from_rotvec([0.012, -0.02, 0.016]).as_matrix()
+    dT[:3, 3] = [0.03, -0.015, 0.025]
+    return scene, vox, T, T @ dT
+
+
+def run_track_case(rh, nrgbd, crit_mod, noise_log):
+    """The reference track_frame (render_helpers.py:679-761) with
+    depth_variance=True — the call Tracking.do_tracking makes
+    (tracking.py:130-147): Criterion(weight_depth_loss=True), the depth
+    variance median filter (criterion.py:45-50) — 3 iterations of pose-only
+    Adam (lr 1e-3) from a perturbed pose.  Per iteration: the loss, the
+    sampler noise, the replayed pixel picks and how many hit rays the median
+    filter dropped; then the final pose and the last hit mask."""
+    import importlib
+    se3 = importlib.import_module("se3pose")
+    scene, vox, T, T0 = track_setup()
+    voxels, children, features = _octree(vox, 256)
+    n_nodes = voxels.shape[0]
+    fr = syn.SyntheticFrame(scene, T, scale=0.1, seed=41, device="cpu")
+    n_rays, iters = 256, 3
+    gen = torch.Generator().manual_seed(9)
+    picks = [torch.randperm(fr.h * fr.w, generator=gen)[:n_rays].sort().values for _ in range(iters)]
+
+    class Frame:
+        def __init__(self):
+            self.rays_d, self.rgb, self.depth = fr.rays_d, fr.rgb, fr.depth
+            self.calls = 0
+
+        def sample_rays(self, n):
+            idx = picks[self.calls]
+            self.calls += 1
+            m = torch.zeros(fr.h * fr.w, dtype=torch.bool)
+            m[idx] = True
+            self.sample_mask = m.view(fr.h, fr.w)
+
+    torch.manual_seed(55)
+    emb = torch.randn(n_nodes, 16) * 0.3
+    dec = nrgbd.Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none", multires=0)
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    vt = torch.from_numpy(voxels)
+    centres = (vt[:, :3] + vt[:, -1:] / 2) * 0.2
+    structure = torch.cat([torch.from_numpy(children), vt[:, -1:]], -1).int()
+    map_states = {"voxel_vertex_idx": torch.from_numpy(features), "voxel_center_xyz": centres.float(),
+                  "voxel_structure": structure, "voxel_vertex_emb": emb}
+    args = types.SimpleNamespace(criteria={**O.REPLICA_CRITERIA, "sdf_truncation": 0.1},
+                                 data_specs={"max_depth": 10.0})
+    crit = crit_mod.Criterion(args)
+    losses, dropped = [], []
+
+    def loss_rec(outputs, obs, **kw):
+        loss, parts = crit(outputs, obs, **kw)
+        losses.append(float(loss))
+        with torch.no_grad():  # the hit rays criterion.py:45-50 drops from the depth loss
+            gd = obs[1][outputs["ray_mask"]]
+            valid = (gd > 0.01) & (gd < 10.0)
+            dl = (gd - outputs["depth"]).abs()
+            var = torch.sum(outputs["weights"] * ((outputs["depth"].unsqueeze(-1) - outputs["z_vals"]) ** 2), -1)
+            tmp = dl / torch.sqrt(var + 1e-10)
+            dropped.append(int((valid & ~(tmp < 10 * tmp.median())).sum()))
+        return loss, parts
+    pose0 = se3.OptimizablePose.from_matrix(torch.tensor(T0, dtype=torch.float32))
+    p0 = pose0.data.detach().numpy().copy()
+    noise_log.clear()
+    torch.manual_seed(61)
+    pose1, _, hit = rh.track_frame(pose0, Frame(), map_states, dec, None, loss_rec, 0.2, N_rays=n_rays,
+                                   step_size=0.02, num_iterations=iters, truncation=0.1, learning_rate=1e-3,
+                                   max_voxel_hit=10, max_distance=10, depth_variance=True)
+    assert len(noise_log) == iters, len(noise_log)
+    rec = dict(voxels=voxels, children=children, features=features, centres=centres.numpy(),
+               structure=structure.numpy(), embeddings=emb.numpy(), rays_d=fr.rays_d.numpy(), rgb=fr.rgb.numpy(),
+               depth=fr.depth.numpy(), pose0=p0, pose1=pose1.data.detach().numpy(), hit_mask=hit.numpy(),
+               losses=np.array(losses, np.float32), depth_filter_dropped=np.array(dropped, np.int64),
+               step_size=np.float32(0.02), voxel_size=np.float32(0.2), truncation=np.float32(0.1),
+               max_distance=np.float32(10.0), max_depth=np.float32(10.0), lr=np.float32(1e-3),
+               n_rays=np.int64(n_rays), iters=np.int64(iters),
+               crit=np.array([O.REPLICA_CRITERIA[k] for k in ("rgb_weight", "depth_weight", "fs_weight",
+                                                              "sdf_weight")], np.float32))
+    for it in range(iters):
+        rec[f"noise{it}"] = noise_log[it].numpy()
+        rec[f"pick{it}"] = picks[it].numpy()
+    for k, v in dec.state_dict().items():
+        rec["dec." + k] = v.numpy()
+    return rec
+
+
 def main(only=()):
     """only: case names to (re)generate (default: all)."""
     want = (lambda n: not only or n in only)
@@ -418,6 +517,13 @@ def main(only=()):
                 np.savez_compressed(path, **rec)
                 print(f"{name}: nodes={int(rec['n_nodes'])} losses={rec['losses'].tolist()} "
                       f"-> {os.path.relpath(path, REPO)} ({os.path.getsize(path) // 1024} KiB)")
+            if want("T_track"):
+                rec = run_track_case(rh, nrgbd, crit_mod, noise_log)
+                path = os.path.join(OUT_DIR, "T_track.npz")
+                np.savez_compressed(path, **rec)
+                print(f"T_track: losses={rec['losses'].tolist()} dropped={rec['depth_filter_dropped'].tolist()} "
+                      f"hits={int(rec['hit_mask'].sum())} -> {os.path.relpath(path, REPO)} "
+                      f"({os.path.getsize(path) // 1024} KiB)")
             if not want("M_mesh_A"):
                 return
             rec = run_mesh_case(rh, nrgbd)

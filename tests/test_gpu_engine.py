@@ -1,9 +1,12 @@
 """The native mapping iteration (psvo.engine.MappingEngine → psvo_map_step)
 against the autograd path (render_rays + Criterion + loss.backward() +
-psvo.optim.Adam) on the same rays, seeds and initial state: the loss of the
-first iteration and the decoder update are bit-identical (same kernels, same
-order; the decoder gradients are deterministic); embeddings agree up to the
-order of the float atomics in the interpolation backward."""
+psvo.optim.Adam) on the same rays, seeds and initial state: with the dense
+decoder the loss of the first iteration and the decoder update are
+bit-identical (same kernels, same order; the decoder gradients are
+deterministic); embeddings agree up to the order of the float atomics in the
+interpolation backward.  The sparse decoder (the default) against the dense
+one: the same forward bits, gradients up to the weight gradients' summation
+order."""
 import types
 
 import numpy as np
@@ -67,6 +70,7 @@ def test_engine_matches_autograd_path():
     ms_e = map_states(tree, emb_e, 0.2, device=DEV)
     eng = MappingEngine(ms_e, dec_e, 0.2, step, truncation=0.1, max_distance=10.0, criteria=crit, max_depth=10.0,
                         lr_emb=5e-3, lr_dec=5e-3)
+    eng.set_paths(MappingEngine.PATH_DENSE_DECODER)  # every sample through the decoder, as autograd runs it
     losses_e = []
     for it in range(2):
         losses_e.append(float(eng.step(ro, rd, rgb, depth, seed=100 + it)))
@@ -81,6 +85,57 @@ def test_engine_matches_autograd_path():
     st = eng.last_stats
     assert st[1] > 0 and st[4] > 0  # R_hit, M
     eng.close()
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_sparse_decoder_matches_dense(padded):
+    """The sparse decoder (the sdf trunk on every sample, the full decoder
+    forward and backward on the kept samples only: composited or inside a
+    loss mask, composite.hip k_select_samples) against the dense decoder on
+    every sample, two psvo_map_step_frames iterations stopped before Adam
+    from the same state and seeds, on the single-GPU chain and on the padded
+    one (the data-parallel forward): the loss bit for bit (the forward's sdf
+    and colours are the same bits), the statistics equal, the embedding /
+    decoder gradients and the pose gradient up to the summation order of the
+    weight gradients / the scatter.  A dropped sample's gradient is exactly
+    zero, so a substantial fraction of samples must be dropped and the
+    composited ones kept."""
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    n = 512
+    poses, dirs = _frames_of(w, n)
+    rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    base = MappingEngine.PATH_PADDED if padded else 0
+    runs = {}
+    for mode in ("dense", "sparse"):
+        e = emb0.clone().to(DEV)
+        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
+                            max_distance=10.0, criteria=crit, max_depth=10.0)
+        eng.set_paths(base | (MappingEngine.PATH_DENSE_DECODER if mode == "dense" else 0))
+        out = []
+        for it in range(2):
+            pg = torch.zeros(poses.shape[0], 8, device=DEV)
+            loss = eng.step_frames(dirs, n, poses.clone(), torch.zeros_like(poses), torch.zeros_like(poses), [0, 1],
+                                   1e-3, rgb, depth, seed=700 + it, apply_adam=False, pose_grad=pg, want_loss=True)
+            torch.cuda.synchronize()
+            out.append((float(loss), list(eng.last_stats), eng.grad_flat.cpu().clone(), pg.cpu()))
+        if mode == "sparse":
+            sel = eng.select_stats()
+            m = out[-1][1][4]
+            assert sel["steps"] == 2 and 0 < sel["composited"] <= sel["kept"] < m, (sel, m)
+            assert sel["kept"] < 0.9 * m, (sel, m)  # the selection drops samples
+        runs[mode] = out
+        eng.close()
+    n_emb = emb0.shape[0] * 16
+    for (la, sa, ga, pa), (lb, sb, gb, pb) in zip(runs["dense"], runs["sparse"]):
+        assert sa[:13] == sb[:13]
+        assert la == lb, (la, lb)
+        gd, gs = ga[n_emb:], gb[n_emb:]
+        torch.testing.assert_close(gs, gd, rtol=1e-4, atol=1e-5 * float(gd.abs().max()))
+        torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-4, atol=1e-5 * float(ga[:n_emb].abs().max()))
+        torch.testing.assert_close(pb, pa, rtol=0, atol=1e-4 * float(pa.abs().max()))
 
 
 def test_engine_query_ahead_matches_inline():
@@ -168,90 +223,6 @@ def test_failed_step_does_not_wedge_the_engine():
     eng.close()
 
 
-def test_device_sized_forward_matches_host_sized(monkeypatch):
-    """The render's forward queued before the query's statistics reach the
-    host (PSVO_DEV_SIZED=1: sample compaction, interpolation, decoder forward
-    sized on the device — engine.cpp render, DevBatch) against every launch
-    host-sized (the default), over batches that grow past the capacities (the
-    re-run path) and shrink again: same losses (rtol 1e-4) and statistics;
-    decoder and embeddings up to the order of the interpolation backward's
-    float atomics."""
-    from copy import deepcopy
-    from psvo.engine import MappingEngine
-    from psvo.octree import map_states
-    w, tree, emb0, dec = _setup()
-    ro, rd, rgb, dep = (t.reshape(-1, t.shape[-1]) if t.dim() == 3 else t.reshape(-1)
-                        for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
-    R = ro.shape[0]
-    sizes = [R // 4, R, R // 4, R, R // 2]  # the first full batch outgrows the capacities of the quarter one
-    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
-    runs = []
-    for dev_sized in ("0", "1"):
-        monkeypatch.setenv("PSVO_DEV_SIZED", dev_sized)
-        d = deepcopy(dec)
-        e = emb0.clone().to(DEV)
-        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), d, 0.2, 0.01, truncation=0.1, max_distance=10.0,
-                            criteria=crit, max_depth=10.0)
-        losses, stats = [], []
-        for it, n in enumerate(sizes):
-            b = [t[:n].to(DEV).contiguous() for t in (ro, rd, rgb, dep)]
-            losses.append(float(eng.step(*b, seed=70 + it)))
-            stats.append(list(eng.last_stats))
-        torch.cuda.synchronize()
-        runs.append((losses, stats, [p.detach().clone() for p in d.fused_params()], e.clone()))
-        eng.close()
-    (la, sa, da, ea), (lb, sb, db, eb) = runs
-    assert sa == sb
-    assert la[0] == lb[0]  # both host-sized (no capacities yet)
-    np.testing.assert_allclose(lb, la, rtol=1e-4)
-    # after the first step the embeddings differ by the order of the scatter's float atomics
-    # (either mode, run to run), and Adam's m / sqrt(v) can turn that noise on a near-zero
-    # gradient into a visible fraction of a step (lr 5e-3): bars at 1 % of one step
-    for p, q in zip(da, db):
-        torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
-    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
-
-
-def test_fused_points_interp_matches_split(monkeypatch):
-    """Sample compaction + interpolation forward as one launch
-    (k_points_interp, PSVO_FUSED_POINTS=1) against the two kernels (the
-    default: k_sample_points, then k_interp_fwd): the same
-    arithmetic, so every step's forward — loss and statistics — is bit-equal
-    from equal state; parameters after several steps within the order of
-    the interpolation backward's float atomics (as the device-sized test)."""
-    from copy import deepcopy
-    from psvo.engine import MappingEngine
-    from psvo.octree import map_states
-    w, tree, emb0, dec = _setup()
-    ro, rd, rgb, dep = (t.reshape(-1, t.shape[-1]) if t.dim() == 3 else t.reshape(-1)
-                        for t in (w.rays_o, w.rays_d, w.rgb, w.depth))
-    R = ro.shape[0]
-    sizes = [R, R // 2, R]
-    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
-    runs = []
-    for fused in ("0", "1"):
-        monkeypatch.setenv("PSVO_FUSED_POINTS", fused)
-        d = deepcopy(dec)
-        e = emb0.clone().to(DEV)
-        eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), d, 0.2, 0.01, truncation=0.1, max_distance=10.0,
-                            criteria=crit, max_depth=10.0)
-        losses, stats = [], []
-        for it, n in enumerate(sizes):
-            b = [t[:n].to(DEV).contiguous() for t in (ro, rd, rgb, dep)]
-            losses.append(float(eng.step(*b, seed=90 + it)))
-            stats.append(list(eng.last_stats))
-        torch.cuda.synchronize()
-        runs.append((losses, stats, [p.detach().clone() for p in d.fused_params()], e.clone()))
-        eng.close()
-    (la, sa, da, ea), (lb, sb, db, eb) = runs
-    assert sa == sb
-    assert la[0] == lb[0]  # same state, same forward bits
-    np.testing.assert_allclose(lb, la, rtol=1e-4)
-    for p, q in zip(da, db):
-        torch.testing.assert_close(p, q, rtol=1e-4, atol=5e-5)
-    torch.testing.assert_close(ea, eb, rtol=1e-4, atol=5e-5)
-
-
 def _frames_of(w, n):
     """Keyframe poses [F, 6] and camera-frame directions of a workload's rays
     (world directions rotated back by each pose)."""
@@ -266,20 +237,20 @@ def _frames_of(w, n):
     return torch.stack(poses).contiguous().to(DEV), torch.cat(dirs).contiguous().to(DEV)
 
 
-def test_query_chain_variants_match_padded_path(monkeypatch):
-    """The mapping step's round-4 query / forward chain against the padded
-    path the autograd route takes (PSVO_PADDED_Z=1: k_sample_points writes
-    the [R_hit, S_max] z / mask copy, the loss normalisers by k_crit_counts →
-    reduce → coef on the aux stream), two psvo_map_step_frames iterations
-    stopped before Adam from the same state and seeds, every variant:
+def test_query_chain_variants_match_padded_path():
+    """The mapping step's query / forward chain against the padded path the
+    autograd route and the data-parallel step take (PATH_PADDED: k_sample_points
+    writes the [R_hit, S_max] z / mask copy, the loss normalisers by
+    k_crit_counts → reduce → coef on the aux stream), two
+    psvo_map_step_frames iterations stopped before Adam from the same state
+    and seeds, every variant:
       default_loss  z read from the sampler's rows (stride max_steps), the
-                    ray-major compaction (k_compact_rays), the count chain;
+                    ray-major compaction in the sampler's launch, the count chain;
       counts        + PSVO_STEP_NO_LOSS: the normalisers counted by the
                     sampler and turned into coefficients by its look-back scan;
-      split         + PSVO_QUERY_SPLIT=1: the statistics / rank pass and the
-                    scan (with the counts) as kernels of their own;
-      interp_rays   + PSVO_INTERP_RAYS=1: compaction inside a ray-major
-                    interpolation (k_interp_fwd_rays).
+      split         + PATH_QUERY_SPLIT: the statistics / rank pass and the
+                    scan (with the counts) as kernels of their own, then
+                    k_compact_rays.
     The same statistics, the decoder gradient bit for bit (it depends on the
     forward, the coefficients and the deterministic decoder backward only),
     the embedding gradient up to the scatter's float-atomic order, the pose
@@ -291,15 +262,14 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
     poses, dirs = _frames_of(w, n)
     rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
     crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
-    modes = {"padded": ({"PSVO_PADDED_Z": "1"}, True), "default_loss": ({}, True), "counts": ({}, False),
-             "split": ({"PSVO_QUERY_SPLIT": "1"}, False), "interp_rays": ({"PSVO_INTERP_RAYS": "1"}, False)}
+    modes = {"padded": (MappingEngine.PATH_PADDED, True), "default_loss": (0, True), "counts": (0, False),
+             "split": (MappingEngine.PATH_QUERY_SPLIT, False)}
     runs = {}
-    for mode, (env, want_loss) in modes.items():
-        for k in ("PSVO_PADDED_Z", "PSVO_QUERY_SPLIT", "PSVO_INTERP_RAYS"):
-            monkeypatch.setenv(k, env.get(k, "0"))
+    for mode, (paths, want_loss) in modes.items():
         e = emb0.clone().to(DEV)
         eng = MappingEngine(map_states(tree, e, 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
                             max_distance=10.0, criteria=crit, max_depth=10.0)
+        eng.set_paths(paths)
         out = []
         for it in range(2):
             pg = torch.zeros(poses.shape[0], 8, device=DEV)
@@ -320,10 +290,10 @@ def test_query_chain_variants_match_padded_path(monkeypatch):
             torch.testing.assert_close(pb, pa, rtol=0, atol=1e-5 * float(pa.abs().max()))
 
 
-def test_lookback_query_matches_split_kernels(monkeypatch):
+def test_lookback_query_matches_split_kernels():
     """The query's statistics / rank pass and sample scan by decoupled look-
     back inside the traversal and sampler launches (the default) against the
-    split kernels (PSVO_QUERY_SPLIT=1: k_ray_stats_rank, k_scan_samples) on
+    split kernels (PATH_QUERY_SPLIT: k_ray_stats_rank, k_scan_samples) on
     ragged batches — 1, 3, 5, 257 and 1,001 rays (a partial last workgroup,
     one to 251 workgroups: one to four tiles of 64, a partial last tile), a batch whose
 first 600 rays miss the octree (leading workgroups with no hit ray) and
@@ -346,9 +316,9 @@ first 600 rays miss the octree (leading workgroups with no hit ray) and
     crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
     runs = {}
     for split in ("0", "1"):
-        monkeypatch.setenv("PSVO_QUERY_SPLIT", split)
         eng = MappingEngine(map_states(tree, emb0.clone().to(DEV), 0.2, device=DEV), dec, 0.2, 0.01,
                             truncation=0.1, max_distance=10.0, criteria=crit, max_depth=10.0)
+        eng.set_paths(MappingEngine.PATH_QUERY_SPLIT if split == "1" else 0)
         out = []
         for i, (o, d, c, z) in enumerate(batches):
             loss = float(eng.step(o.contiguous(), d.contiguous(), c.contiguous(), z.contiguous(), seed=900 + i,

@@ -63,6 +63,44 @@ def test_grid_svo_intersect_matches_oracle(golden):
     np.testing.assert_array_equal(hi.cpu().numpy()[0], np.where(g["raw_idx"] >= 0, g["raw_t1"], 0))
 
 
+
+def test_grid_svo_intersect_reference_layout(golden):
+    """grid.svo_intersect called exactly as an unchanged voxel_helpers.py
+    calls it (SparseVoxelOctreeRayIntersect.forward, voxel_helpers.py:112-154):
+    G = min(256, 2e9 / (points + children numel)) blocks, the rays padded by
+    repeating the first H − N, reshaped to [G, K, 3], the octree expanded G
+    times with .contiguous(); every batch b's rows against the C oracle,
+    then the reference's reshape / trim back to [1, N, n_max]."""
+    import grid
+    _, g = golden
+    ro = torch.from_numpy(g["rays_o"]).to(DEV)
+    rd = torch.from_numpy(g["rays_d"]).to(DEV)
+    points = torch.from_numpy(g["centres"]).to(DEV)
+    children = torch.from_numpy(g["structure"]).to(DEV)
+    G = min(256, int(2 * 10 ** 9 / (points.numel() + children.numel())))
+    S, N = ro.shape[:2]
+    K = int(np.ceil(N / G))
+    H = K * G
+    assert G > 1  # several blocks (padded rows where N is not a multiple of G)
+    if H > N:
+        ro = torch.cat([ro, ro[:, :H - N]], 1)
+        rd = torch.cat([rd, rd[:, :H - N]], 1)
+    ro, rd = ro.reshape(S * G, K, 3), rd.reshape(S * G, K, 3)
+    pts = points.expand(S * G, *points.size()).contiguous()
+    ch = children.expand(S * G, *children.size()).contiguous()
+    idx, lo, hi = grid.svo_intersect(ro.float(), rd.float(), pts.float(), ch.int(), 0.2, 50)
+    assert tuple(idx.shape) == (G, K, 50)
+    pad = np.concatenate([np.arange(N), np.arange(H - N)])  # the ray each padded row repeats
+    want_idx = g["raw_idx"][pad].reshape(G, K, 50)
+    want_lo = np.where(g["raw_idx"] >= 0, g["raw_t0"], 0)[pad].reshape(G, K, 50)
+    want_hi = np.where(g["raw_idx"] >= 0, g["raw_t1"], 0)[pad].reshape(G, K, 50)
+    for b in range(G):  # batch by batch: each block reads its own copy of the tree
+        np.testing.assert_array_equal(idx[b].cpu().numpy(), want_idx[b], err_msg=f"batch {b}")
+        np.testing.assert_array_equal(lo[b].cpu().numpy(), want_lo[b], err_msg=f"batch {b}")
+        np.testing.assert_array_equal(hi[b].cpu().numpy(), want_hi[b], err_msg=f"batch {b}")
+    out = idx.reshape(S, H, -1)[:, :N]  # voxel_helpers.py:148-154
+    np.testing.assert_array_equal(out.cpu().numpy()[0], g["raw_idx"])
+
 def test_ray_intersect_vox_matches_golden(golden):
     from psvo.voxel_helpers import ray_intersect_vox
     _, g = golden

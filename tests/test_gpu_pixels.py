@@ -87,29 +87,6 @@ def test_sample_frames_matches_oracle(H, W, F, n):
         assert torch.equal(depth[sl], fr.depth[m])
 
 
-@pytest.mark.parametrize("n", [1024, 700, 1])
-def test_candidate_draw_matches_radix_passes(monkeypatch, n):
-    """The FAST draw's candidate path (k_px_cand + k_px_pick: the ≈ 2n pixels
-    whose 24-bit keys clear a threshold, sorted in LDS) against the radix
-    passes alone (PSVO_PX_CAND=0) on full-size keyframes: the same picks,
-    masks and gathered rows, bit for bit."""
-    from psvo import sample_util
-    H, W, F = 680, 1200, 4
-    frames = [_Frame(H, W, 200 + f) for f in range(F)]
-    outs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("PSVO_PX_CAND", mode)
-        dirs, rgb, depth = sample_util.sample_frames(frames, n, seed=4242 + n)
-        torch.cuda.synchronize()
-        outs[mode] = (dirs.clone(), rgb.clone(), depth.clone(), [fr.sample_idx.clone() for fr in frames],
-                      [fr.sample_mask.clone() for fr in frames])
-    a, b = outs["1"], outs["0"]
-    for x, y in zip(a[:3], b[:3]):
-        assert torch.equal(x, y)
-    for x, y in zip(a[3] + a[4], b[3] + b[4]):
-        assert torch.equal(x, y)
-
-
 def test_sample_pixels_edges():
     from psvo import sample_util
     H, W = 33, 41

@@ -268,3 +268,93 @@ def test_native_track_frame_matches_dropin_trajectory():
     torch.testing.assert_close(out_pose.data, pose.data.detach(), rtol=0, atol=1e-5)
     assert float((out_pose.data.cpu() - _perturbed(T).data).abs().max()) > 1e-4
     eng.close()
+
+
+def _golden_track():
+    """T_track (tests/golden/make_golden.py run_track_case): the reference's
+    own track_frame with depth_variance=True — map, decoder, frame, start
+    pose, replayed picks and the sampler noise of every iteration."""
+    from conftest import load_golden
+    from psvo.decoder import Decoder
+    g = load_golden("T_track")
+    ms = {"voxel_center_xyz": torch.from_numpy(g["centres"]).to(DEV),
+          "voxel_structure": torch.from_numpy(g["structure"]).to(DEV),
+          "voxel_vertex_idx": torch.from_numpy(g["features"]).to(DEV),
+          "voxel_vertex_emb": torch.from_numpy(g["embeddings"]).to(DEV)}
+    dec = Decoder(depth=2, width=128, in_dim=16, skips=[], embedder="none").to(DEV)
+    dec.load_state_dict({k[len("dec."):]: torch.from_numpy(v) for k, v in g.items() if k.startswith("dec.")})
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    iters = int(g["iters"])
+    picks = [torch.from_numpy(g[f"pick{i}"]).to(DEV) for i in range(iters)]
+    noises = [torch.from_numpy(g[f"noise{i}"]) for i in range(iters)]
+    H, W = g["depth"].shape
+
+    class Frame:  # replays the reference run's pixel picks (frame.sample_rays → sample_mask / sample_idx)
+        def __init__(self):
+            self.rays_d = torch.from_numpy(g["rays_d"]).to(DEV)
+            self.rgb = torch.from_numpy(g["rgb"]).to(DEV)
+            self.depth = torch.from_numpy(g["depth"]).to(DEV)
+            self.calls = 0
+
+        def sample_rays(self, n):
+            idx = picks[self.calls]
+            self.calls += 1
+            m = torch.zeros(H * W, dtype=torch.bool, device=DEV)
+            m[idx] = True
+            self.sample_mask, self.sample_idx = m.view(H, W), idx
+
+    return g, ms, dec, Frame, noises
+
+
+def test_track_frame_matches_reference_golden():
+    """The drop-in track_frame (autograd over the HIP kernels) and the native
+    TrackingEngine.track_frame (psvo_track_step) against the reference's own
+    track_frame with depth_variance=True on the same map, frame, picks and
+    sampler noise (tests/golden/T_track.npz): per-iteration losses (rtol
+    1e-4), the final pose (1e-5: 1 % of one Adam step), the hit mask
+    exactly; the median depth filter drops rays on every iteration."""
+    from psvo.criterion import Criterion
+    from psvo.engine import TrackingEngine
+    from psvo.pose import OptimizablePose
+    from psvo.render_helpers import track_frame
+    g, ms, dec, Frame, noises = _golden_track()
+    assert (g["depth_filter_dropped"] > 0).all()
+    iters, n = int(g["iters"]), int(g["n_rays"])
+    crit_cfg = dict(zip(("rgb_weight", "depth_weight", "fs_weight", "sdf_weight"), g["crit"].tolist()))
+    crit = Criterion(types.SimpleNamespace(criteria=dict(crit_cfg, sdf_truncation=float(g["truncation"])),
+                                           data_specs={"max_depth": float(g["max_depth"])}))
+    losses = []
+
+    def loss_rec(outputs, obs, **kw):
+        loss, parts = crit(outputs, obs, **kw)
+        losses.append(float(loss))
+        return loss, parts
+    pose0 = OptimizablePose(torch.from_numpy(g["pose0"]))
+    pose, _, hit = track_frame(pose0, Frame(), ms, dec, None, loss_rec, float(g["voxel_size"]), N_rays=n,
+                               step_size=float(g["step_size"]), num_iterations=iters,
+                               truncation=float(g["truncation"]), learning_rate=float(g["lr"]),
+                               max_distance=float(g["max_distance"]), depth_variance=True,
+                               noise=lambda it: noises[it])
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-4)
+    np.testing.assert_allclose(pose.data.detach().cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(hit.cpu().numpy(), g["hit_mask"])
+    # native: one psvo_track_step per iteration
+    eng = TrackingEngine(ms, dec, float(g["voxel_size"]), float(g["step_size"]), float(g["truncation"]),
+                         float(g["max_distance"]), crit_cfg, float(g["max_depth"]))
+    eng.reset(torch.from_numpy(g["pose0"]))
+    fr = Frame()
+    dirs_all, rgb_all, depth_all = fr.rays_d.reshape(-1, 3), fr.rgb.reshape(-1, 3), fr.depth.reshape(-1)
+    native = []
+    for it in range(iters):
+        fr.sample_rays(n)
+        idx = fr.sample_idx
+        native.append(float(eng.step(dirs_all[idx], rgb_all[idx], depth_all[idx], seed=0, lr=float(g["lr"]),
+                                     depth_variance=True, noise=noises[it])))
+        assert eng.last_stats[0] > 0
+    np.testing.assert_allclose(native, g["losses"], rtol=1e-4)
+    np.testing.assert_allclose(eng.pose.cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
+    out = eng.track_frame(OptimizablePose(torch.from_numpy(g["pose0"])), Frame(), N_rays=n, num_iterations=iters,
+                          learning_rate=float(g["lr"]), depth_variance=True, noise=lambda it: noises[it])
+    np.testing.assert_allclose(out.data.cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
+    eng.close()

@@ -213,3 +213,25 @@ def test_oracle_pixel_uniforms_are_uniform():
     assert u.dtype == np.float32 and u.min() >= 0.0 and u.max() < 1.0
     assert abs(float(u.mean()) - 0.5) < 0.005
     assert not np.array_equal(u[0], u[1])
+
+
+def test_track_frame_matches_reference_golden():
+    """The oracle's tracking loop (render + Criterion with the median depth
+    filter + pose Adam) against the reference's own track_frame with
+    depth_variance=True (tests/golden/T_track.npz, tracking.py:130-147): the
+    per-iteration losses, the final pose and the hit mask."""
+    g = load_golden("T_track")
+    ms = O.map_states_from_export(g["voxels"], g["children"], g["features"], float(g["voxel_size"]),
+                                  torch.from_numpy(g["embeddings"]))
+    iters = int(g["iters"])
+    assert (g["depth_filter_dropped"] > 0).all()  # the median filter is exercised on every iteration
+    losses, pose, hit = O.track_frame(torch.from_numpy(g["rays_d"]), torch.from_numpy(g["rgb"]),
+                                      torch.from_numpy(g["depth"]), [g[f"pick{i}"] for i in range(iters)],
+                                      [g[f"noise{i}"] for i in range(iters)], ms, _decoder_params(g), g["pose0"],
+                                      float(g["step_size"]), float(g["voxel_size"]), iters, lr=float(g["lr"]),
+                                      truncation=float(g["truncation"]), max_distance=float(g["max_distance"]),
+                                      max_depth=float(g["max_depth"]), weight_depth_loss=True)
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-5)
+    # 1 % of one Adam step (lr 1e-3): the pose gradient's summation order (a few ulps at |t| ≈ 11)
+    np.testing.assert_allclose(pose.numpy(), g["pose1"], rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(hit.numpy(), g["hit_mask"])
