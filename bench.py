@@ -453,6 +453,8 @@ def main():
             raise RuntimeError("bench: bundle_adjust_frames did not run on the native engine")
         return engs[0]
 
+    sel_stats = {}
+
     def timed_ba(steps, warmup, record=False):
         if warmup:
             run_ba(warmup)
@@ -463,6 +465,7 @@ def main():
         clocked = False
         if record and eng is not None:
             eng.stats_hook = lambda st: record_stats(st[4], st[9] if world > 1 else st[1], st[5], st[3], head_stats)
+            eng.select_stats(reset=True)  # the sparse decoder's kept / composited samples of the timed steps
         if record and eng is not None and os.environ.get("PSVO_BENCH_NO_CLOCK") != "1":
             try:  # an event at each step's entry on its stream: the GPU-side period
                 eng.set_clock(steps)
@@ -485,6 +488,8 @@ def main():
                         host_waits_before_landing=w_waited)
         if eng is not None:
             eng.stats_hook = None
+        if record and eng is not None:
+            sel_stats.update(eng.select_stats())
         if world > 1:
             t = torch.tensor([el], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -687,22 +692,34 @@ def main():
     mlp_ms = mlp_f_ms + mlp_b_ms
     w = args.width
     macs = 16 * w + w * w + w * 129 + 144 * w + w * 3  # nrgbd.py:80-146, depth 2, sdf_dim 128, in_dim 16
-    flops_mlp = 3 * 2.0 * macs * h_m
-    mlp_tf = flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
+    trunk = 16 * w + w * w + w  # h1, h2 and the sdf row: what the sparse decoder runs on every sample
+    flops_mlp = 3 * 2.0 * macs * h_m  # algorithmic: the reference's forward + δ chain + weight gradients, every sample
+    steps_sel = sel_stats.get("steps", 0)
+    kept = sel_stats["kept_sum"] / steps_sel if steps_sel else None  # per step (this rank)
+    comp = sel_stats["composited_sum"] / steps_sel if steps_sel else None
+    if world > 1 and kept is not None:
+        t = torch.tensor([kept, comp], dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        kept, comp = (float(x) / world for x in t.cpu())
+    # executed: the sdf trunk on every sample, the whole decoder forward and backward on the kept ones
+    flops_exec = (2.0 * trunk * h_m + 3 * 2.0 * macs * kept) if kept is not None else flops_mlp
+    mlp_tf = flops_exec / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
+    m_bwd = kept if kept is not None else h_m  # the samples the backward runs on
     if fused_ib:  # k_mlp_bwd3: δ chain + weight gradients (2 x 107.5 kFLOP / sample) + the interpolation backward
-        b_tf = 2 * 2.0 * macs * h_m / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
-        ib_gbs = 1664.0 * h_m / (mlp_b_ms * 1e-3) / 1e9 if mlp_b_ms > 0 else None
+        b_tf = 2 * 2.0 * macs * m_bwd / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
+        ib_gbs = 1664.0 * m_bwd / (mlp_b_ms * 1e-3) / 1e9 if mlp_b_ms > 0 else None
         roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
                              "interpolation backward: embedding scatter + dL/dx)",
                    "bound": "mfma", "achieved": b_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                    "frac": b_tf / MFMA_F32_PEAK_TFS if b_tf else None,
                    "traffic": tr.get("bwd_fused_bytes_per_launch"), "avg_launch_ms": mlp_b_ms,
-                   "algorithmic_flops_per_launch": 2 * 2.0 * macs * h_m,
-                   "interp_bwd_algorithmic_bytes": 1664.0 * h_m,
+                   "flops_per_launch_executed": 2 * 2.0 * macs * m_bwd,
+                   "samples_per_launch": m_bwd,
+                   "interp_bwd_bytes": 1664.0 * m_bwd,
                    "interp_bwd_bytes_over_kernel_time_frac_hbm": ib_gbs / HBM_PEAK_GBS if ib_gbs else None,
                    "timing": TIMING_NOTE}
     else:
-        roof_ib = bw_roof("k_interp_bwd", 1664.0 * h_m, kt_overlap["interp_bwd"],
+        roof_ib = bw_roof("k_interp_bwd", 1664.0 * m_bwd, kt_overlap["interp_bwd"],
                           tr.get("bwd_fused_bytes_per_launch"), kt_serial["interp_bwd"] if kt_serial else None)
     result = {
         "metric": METRIC,
@@ -729,6 +746,10 @@ def main():
                                f"{h_m / max(h_r, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
                    "rays_per_step_per_gpu": rays_per_step, "samples_per_step": h_m, "hit_rays_per_step": h_r,
                    "aabb_tests_per_step": h_v,
+                   # the sparse decoder: samples whose gradients can be non-zero (the full decoder runs on
+                   # these) and the composited ones (a compositing weight: z < z_min + truncation)
+                   "decoder_kept_fraction": kept / h_m if kept is not None and h_m else None,
+                   "composited_fraction": comp / h_m if comp is not None and h_m else None,
                    "parallelism": f"dp{world} (ray-sharded, union-batch loss, "
                                   f"{dist.get_backend() if world > 1 else 'no'} collectives)"},
         "roofline": roof_qi,
@@ -736,7 +757,12 @@ def main():
                           "bound": "mfma", "achieved": mlp_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": (mlp_tf / MFMA_F32_PEAK_TFS) if mlp_tf else None,
                           "traffic": tr.get("mlp_bytes_per_step"),
-                          "algorithmic_flops_per_launch": flops_mlp, "avg_launch_ms": mlp_ms,
+                          "flops_executed_per_step": flops_exec,
+                          "flops_algorithmic_per_step": flops_mlp,
+                          "achieved_basis": "executed FLOPs (sdf trunk on every sample, the whole decoder forward + "
+                                            "backward on the kept samples) / time",
+                          "effective_algorithmic_tflops": flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None,
+                          "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,
                           "timing": TIMING_NOTE},
         "roofline_bwd_fused" if fused_ib else "roofline_interp_bwd": roof_ib,

@@ -1110,7 +1110,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_CALL(psvo_mlp_fwd(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                               images, sdf_s, rgb_s, act, masks));
     }
-    mark(e, st, PSVO_TIME_MLP_FWD, 1);
+    // sparse: the region stays open over the selection (its own, nested
+    // region) and the compact forward (map_step_impl closes it)
+    if (!sparse) mark(e, st, PSVO_TIME_MLP_FWD, 1);
     o.rank_ray = const_cast<int *>(rank_ray);
     o.ray_ns = const_cast<int *>(ray_ns);
     o.offsets = const_cast<int *>(offsets);
@@ -1302,8 +1304,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const bool coef_known = counts_gt && qset->counts_gt == counts_gt;
     const bool need_z = !coef_known || e->x.on() ||
                         (d->emb_row_flags && !psvo::mlp_bwd_fuses_interp(d->width));
-    // the sparse decoder (width 128): render runs the sdf trunk only
-    const bool sparse_dec = d->width == 128 && !(e->paths & PSVO_PATH_DENSE_DECODER);
+    // the sparse decoder: render runs the sdf trunk only
+    const bool sparse_dec = !(e->paths & PSVO_PATH_DENSE_DECODER);
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z, sparse_dec));
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
@@ -1351,7 +1353,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
         ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
-        mark(e, st, PSVO_TIME_MLP_FWD, 0);
         ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                                   q.images, sdf_b, rgb_b, act, masks, cnt));
         mark(e, st, PSVO_TIME_MLP_FWD, 1);
@@ -1514,8 +1515,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     } else {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
         ENG_BUF(float, ib_ws2, kIbWs, psvo_interp_bwd_workspace_floats(q.r_hit, q.s_max) * sizeof(float));
-        ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, q.offsets, q.rank_ray, q.leaf,
-                                         q.tt, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb,
+        ENG_CALL(psvo_interp_bwd_chunked(eb, q.r_hit, q.s_max, 16, d->voxel_size, qb.offsets, q.rank_ray, qb.leaf,
+                                         qb.tt, rays_o, rays_d, d->centres, d->vertex_idx, d->emb, dfeat, grad_emb,
                                          grad_od, grad_od + R * 3, ib_ws2));
         mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     }

@@ -1495,13 +1495,12 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats_w floats)");
         PSVO_REQUIRE(act == nullptr || masks != nullptr, "mlp_fwd: act needs masks");
         PSVO_REQUIRE(m <= ((int64_t)1 << 31) / 256, "mlp_fwd: m = %lld too large", (long long)m);
-        PSVO_REQUIRE(m_dev == nullptr, "mlp_fwd: a device sample count is width 128 only");
         hipStream_t st = as_stream(stream);
         if (!images_ready) {
             const int rc = dec256_images(st, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images);
             if (rc) return rc;
         }
-        return dec256_fwd(st, m, feat, images, sdf, rgb, act, masks);
+        return dec256_fwd(st, m, feat, images, sdf, rgb, act, masks, m_dev);
     }
     PSVO_REQUIRE(width == kW, "mlp_fwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
@@ -1617,9 +1616,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         PSVO_REQUIRE(images != nullptr && masks != nullptr, "mlp_bwd: images / masks of the training forward required");
         PSVO_REQUIRE(gw1 == nullptr || act != nullptr, "mlp_bwd: weight gradients need the forward's activations");
         float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
-        PSVO_REQUIRE(m_dev == nullptr, "mlp_bwd: a device sample count is width 128 only");
         return dec256_bwd(as_stream(stream), m, feat, images, rgb, act, masks, g_sdf, g_rgb, dfeat, gw, gb, accumulate,
-                          workspace, dfeat_ready, ip);
+                          workspace, dfeat_ready, ip, m_dev);
     }
     PSVO_REQUIRE(width == kW, "mlp_bwd: width %d unsupported (fused paths: 128, 256)", width);
     PSVO_REQUIRE(m >= 0 && n_split > 0, "mlp_bwd: bad sizes");

@@ -75,7 +75,10 @@ constexpr Img kB4{16, 9, kB5.off + 1 * 16 * kBlk};
 constexpr Img kB3{9, 16, kB4.off + 16 * 9 * kBlk};
 constexpr Img kB2{16, 16, kB3.off + 9 * 16 * kBlk};
 constexpr Img kB1{16, 1, kB2.off + 16 * 16 * kBlk};
-constexpr int kImgMats = kB1.off + 16 * 1 * kBlk;
+// the sdf row alone (W3 row 0 as one output block: the same values as row 128
+// of kF3's block 8), for the sdf trunk (k_dec256_trunk)
+constexpr Img kS3{16, 1, kB1.off + 16 * 1 * kBlk};
+constexpr int kImgMats = kS3.off + 16 * 1 * kBlk;
 // bias vectors (forward order of the chain: b3 as [f rows | sdf | 0 pad], b5 padded to 16)
 constexpr int kVB1 = 0, kVB2 = 256, kVB3 = 512, kVB4 = 512 + 144, kVB5 = kVB4 + 256, kVecN = kVB5 + 16;
 constexpr int kImgTotal = kImgMats + kVecN;
@@ -107,6 +110,11 @@ __host__ __device__ constexpr Chunk fwd_chunk(int c) {
 // backward (data): W5ᵀ | W4ᵀ (kN16) | W3ᵀ (kN9) | W2ᵀ (kN16) | W1ᵀ
 constexpr int kBwdL4 = 1, kBwdL3 = kBwdL4 + kN16, kBwdL2 = kBwdL3 + kN9, kBwdL1 = kBwdL2 + kN16,
               kBwdChunks = kBwdL1 + 1;
+// the sdf trunk: L1 | L2 (kN16) | the sdf row
+constexpr int kTrkL2 = 1, kTrkS3 = kTrkL2 + kN16, kTrkChunks = kTrkS3 + 1;
+__host__ __device__ constexpr Chunk trunk_chunk(int c) {
+    return c == 0 ? chunk_of(kF1, 0, 1) : c < kTrkS3 ? layer_chunk(kF2, c - kTrkL2) : chunk_of(kS3, 0, 16);
+}
 __host__ __device__ constexpr Chunk bwd_chunk(int c) {
     return c == 0         ? chunk_of(kB5, 0, 1)
            : c < kBwdL3   ? layer_chunk(kB4, c - kBwdL4)
@@ -132,7 +140,8 @@ __device__ float mat_at(const Params &p, int which, int o, int j) {
         case 6: return p.w4[j * 144 + o];                                              // W4ᵀ  [144][256]
         case 7: return j < 128 ? p.w3[(j + 1) * 256 + o] : j == 128 ? p.w3[o] : 0.0f;  // W3ᵀ  [256][144]
         case 8: return p.w2[j * 256 + o];                                              // W2ᵀ
-        default: return p.w1[j * 16 + o];                                              // W1ᵀ  [16][256]
+        case 9: return p.w1[j * 16 + o];                                               // W1ᵀ  [16][256]
+        default: return o == 0 ? p.w3[j] : 0.0f;                                       // the sdf row [1 (16)][256]
     }
 }
 
@@ -153,16 +162,16 @@ __global__ __launch_bounds__(256) void k_dec256_prep(Params p, float *__restrict
         img[e] = x;
         return;
     }
-    const Img ims[10] = {kF1, kF2, kF3, kF4, kF5, kB5, kB4, kB3, kB2, kB1};
+    const Img ims[11] = {kF1, kF2, kF3, kF4, kF5, kB5, kB4, kB3, kB2, kB1, kS3};
     int which = 0;
-    for (int k = 1; k < 10; ++k)
+    for (int k = 1; k < 11; ++k)
         if (e >= ims[k].off) which = k;
     const Img im = ims[which];
     const int r = e - im.off;
     const int i = r & 3, lane = (r >> 2) & 63, blk = r >> 8;
     const int ob = blk % im.nob, ib = blk / im.nob;
     const int o = 16 * ob + (lane & 15), j = 16 * ib + 4 * (lane >> 4) + i;
-    img[e] = mat_at(p, which, o, j);  // fwd images 0..4, bwd 5..9
+    img[e] = mat_at(p, which, o, j);  // fwd images 0..4, bwd 5..9, the sdf row 10
 }
 
 // ---- device helpers ------------------------------------------------------
@@ -437,8 +446,10 @@ struct ChainPlan {
 // ---- forward ---------------------------------------------------------------
 __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t n_tiles, const float *__restrict__ feat,
                                                              const float *__restrict__ img, float *__restrict__ sdf,
-                                                             float *__restrict__ rgb, Act act) {
+                                                             float *__restrict__ rgb, Act act,
+                                                             const int *__restrict__ m_dev) {
     extern __shared__ __align__(16) float lds[];
+    if (m_dev) m = __builtin_amdgcn_readfirstlane(*m_dev);  // the sparse decoder's kept samples (<= m)
     float *vec = lds;  // kVecN
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int e = threadIdx.x; e < kVecN; e += kCThreads) vec[e] = img[kImgMats + e];
@@ -518,6 +529,55 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
     }
 }
 
+// ---- the sdf trunk: h1, h2 and the sdf row only (sparse decoder; sdf-only
+// inference): 73.3 of 140.3 k MACs per sample.  The same chunks, MFMAs and
+// order as k_dec256_fwd's L1 / L2, and the sdf row from kS3 — W3 row 0 as
+// one output block — accumulated over the same k-steps in the same order as
+// block 8 of k_dec256_fwd's L3: the same sdf bits.
+__global__ __launch_bounds__(kCThreads, 1) void k_dec256_trunk(int64_t m, const float *__restrict__ feat,
+                                                               const float *__restrict__ img,
+                                                               float *__restrict__ sdf) {
+    extern __shared__ __align__(16) float lds[];
+    float *vec = lds;  // kVecN
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int e = threadIdx.x; e < kVecN; e += kCThreads) vec[e] = img[kImgMats + e];
+    const ChainPlan P(m);
+    if (P.rounds == 0) return;
+    Ring R{lds + ((kVecN + 63) / 64) * 64, img, 0, wave, lane, false};
+    const int n = lane & 15, g = lane >> 4;
+    auto plan = [](int c) { return trunk_chunk(c); };
+    R.prime(plan);
+    for (int64_t rd = 0; rd < P.rounds; ++rd) {
+        R.more = rd + 1 < P.rounds;
+        R.img = img;
+        asm volatile("" : "+s"(R.img));
+        const int64_t t16 = P.t16(rd, wave);
+        const bool on = t16 < P.n16;  // wave-uniform
+        f32x4 x[kNC][1];
+#pragma unroll
+        for (int c = 0; c < kNC; ++c) {
+            const int64_t s = (t16 + c) * kTileW + n;
+            x[c][0] = s < m ? *reinterpret_cast<const f32x4 *>(feat + s * 16 + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        uint64_t m1[kNC], m2[kNC];
+        f32x4 h1[kNC][16], h2[kNC][16];
+        init_bias(h1, vec + kVB1, lane);
+        gemm_chunk<16, 1, 0, 1>(h1, x, R.next<kTrkChunks>(0, plan), lane, on);
+        relu_mask(h1, m1);
+        init_bias(h2, vec + kVB2, lane);
+        layer_chunks<kTrkChunks, kTrkL2, 0, kN16>(R, h2, h1, plan, lane, on);
+        relu_mask(h2, m2);
+        f32x4 o3[kNC][1];
+        init_bias(o3, vec + kVB3 + 128, lane);  // block 8's biases: row 128 = the sdf's
+        gemm_chunk<1, 16, 0, 16>(o3, h2, R.next<kTrkChunks>(kTrkS3, plan), lane, on);
+#pragma unroll
+        for (int c = 0; c < kNC; ++c) {
+            const int64_t s = (t16 + c) * kTileW + n;
+            if (on && s < m && g == 0) sdf[s] = o3[c][0][0];
+        }
+    }
+}
+
 // ---- backward (data) --------------------------------------------------------
 // The fused interpolation backward of a wave's 16 samples (k_dec256_bwd's
 // tile tail): the embedding rows and the ray are gathered here, then dL/dx and
@@ -554,8 +614,10 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_bwd(int64_t m, int64_t 
                                                              const float *__restrict__ rgb,
                                                              const float *__restrict__ g_sdf,
                                                              const float *__restrict__ g_rgb, Act act, Dlt dl,
-                                                             float *__restrict__ dfeat, InterpFuse ip) {
+                                                             float *__restrict__ dfeat, InterpFuse ip,
+                                                             const int *__restrict__ m_dev) {
     extern __shared__ __align__(16) float lds[];
+    if (m_dev) m = __builtin_amdgcn_readfirstlane(*m_dev);  // the sparse decoder's kept samples (<= m)
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     (void)n_tiles;
     const ChainPlan P(m);
@@ -866,15 +928,19 @@ __device__ void dw_run(const DwOps &op, const DwPlan &pl, float *slabs, float *l
     }
 }
 
-__global__ __launch_bounds__(kThreads, 1) void k_dec256_dw(DwOps op, DwPlan pl, float *__restrict__ slabs) {
+__global__ __launch_bounds__(kThreads, 1) void k_dec256_dw(DwOps op, DwPlan pl, float *__restrict__ slabs,
+                                                            const int *__restrict__ m_dev) {
     extern __shared__ __align__(16) float lds[];
     const int wg = blockIdx.x;
     int t = 0;
     while (t < 3 && wg >= pl.wg_begin[t + 1]) ++t;
     const int nwg = pl.wg_begin[t + 1] - pl.wg_begin[t];
     const int k = wg - pl.wg_begin[t];
-    const int64_t per = (pl.n16 + nwg - 1) / nwg;
-    const int64_t t0 = k * per, t1 = t0 + per < pl.n16 ? t0 + per : pl.n16;
+    // the sparse decoder: the kept samples' tiles (the plan's workgroups were sized for the upper bound)
+    const int64_t n16 = m_dev ? (int64_t)((__builtin_amdgcn_readfirstlane(*m_dev) + kTileW - 1) / kTileW) : pl.n16;
+    const int64_t per = (n16 + nwg - 1) / nwg;
+    int64_t t0 = k * per, t1 = t0 + per < n16 ? t0 + per : n16;
+    if (t0 > t1) t0 = t1;  // a workgroup past the kept tiles: an empty range, zero slabs
     switch (t) {
         case 0: dw_run<0>(op, pl, slabs, lds, wg, t0, t1); break;
         case 1: dw_run<1>(op, pl, slabs, lds, wg, t0, t1); break;
@@ -1019,9 +1085,21 @@ static int grid_for(int64_t n_tiles) {
 }
 
 int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images, float *sdf, float *rgb, float *act,
-               uint64_t *masks) {
+               uint64_t *masks, const int *m_dev) {
     if (m == 0) return PSVO_OK;
     const int64_t n_tiles = (m + kChainTile - 1) / kChainTile;
+    if (!rgb && !act && !masks) {  // sdf only: the trunk
+        PSVO_REQUIRE(m_dev == nullptr, "dec256_fwd: the sdf trunk runs host-sized");
+        const int lds = (((kVecN + 63) / 64) * 64 + kRing * kChunkFloats) * 4;
+        static bool tattr = false;
+        if (!tattr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dec256_trunk),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            tattr = true;
+        }
+        psvo::launch(k_dec256_trunk, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, feat, images, sdf);
+        return check_launch("dec256_trunk");
+    }
     const int64_t n16 = dec256_tiles16(m);
     Act a{};
     if (act) {
@@ -1039,14 +1117,14 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
         attr = true;
     }
     psvo::launch(k_dec256_fwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, feat, images, sdf,
-                       rgb, a);
+                 rgb, a, m_dev);
     return check_launch("dec256_fwd");
 }
 
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const InterpFuse *ip) {
+               const InterpFuse *ip, const int *m_dev) {
     PSVO_REQUIRE(ip == nullptr || (kNC == 1 && gw[0] != nullptr),
                  "dec256_bwd: the fused interpolation backward needs the weight-gradient path (1 group per wave)");
     (void)feat;
@@ -1079,7 +1157,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
             attr = true;
         }
         psvo::launch(k_dec256_bwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, images, rgb,
-                           g_sdf, g_rgb, a, d, dfeat, ip ? *ip : InterpFuse{});
+                     g_sdf, g_rgb, a, d, dfeat, ip ? *ip : InterpFuse{}, m_dev);
         const int rc = check_launch("dec256_bwd");
         if (rc) return rc;
     }
@@ -1104,7 +1182,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
         dattr = true;
     }
     if (m > 0) {
-        psvo::launch(k_dec256_dw, dim3(pl.wg_begin[4]), dim3(kThreads), kDwLds, st, op, pl, slabs);
+        psvo::launch(k_dec256_dw, dim3(pl.wg_begin[4]), dim3(kThreads), kDwLds, st, op, pl, slabs, m_dev);
         const int rc = check_launch("dec256_dw");
         if (rc) return rc;
     } else if (hipMemsetAsync(slabs, 0, slab_floats * sizeof(float), st) != hipSuccess) {

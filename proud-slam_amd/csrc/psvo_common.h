@@ -244,15 +244,17 @@ int64_t dec256_mask_words(int64_t m);
 int64_t dec256_workspace_floats(int64_t m);
 int dec256_images(hipStream_t st, const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
                   const float *b3, const float *w4, const float *b4, const float *w5, const float *b5, float *images);
+// rgb, act and masks all null: the sdf trunk only (k_dec256_trunk, the same sdf
+// bits).  m_dev: the sample count read on the device (<= m; buffers sized for m)
 int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images, float *sdf, float *rgb, float *act,
-               uint64_t *masks);
+               uint64_t *masks, const int *m_dev = nullptr);
 struct InterpFuse;
 // ip (the mapping engine's width-256 step): the interpolation backward runs
 // inside the δ-chain kernel (dfeat is then not stored), as at width 128
 int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images, const float *rgb, const float *act,
                const uint64_t *masks, const float *g_sdf, const float *g_rgb, float *dfeat, float *const gw[5],
                float *const gb[5], int accumulate, float *workspace, hipEvent_t dfeat_ready,
-               const InterpFuse *ip = nullptr);
+               const InterpFuse *ip = nullptr, const int *m_dev = nullptr);
 
 constexpr int kXchMaxFrames = 64;  // keyframes per psvo_map_step_frames call
 

@@ -91,3 +91,48 @@ def test_grid_module_rejects_host_tensors():
         grid.svo_intersect(x.transpose(1, 2), x, x, x, 0.2, 50)
     with pytest.raises(NotImplementedError):
         grid.ball_intersect(x, x, x, 0.1, 4)
+
+
+def test_torchscript_octree_class_matches_python_octree():
+    """torch.classes.svo.Octree (lib/libsvo_torch.so, the reference's
+    TorchScript class: bindings.cpp:4-35) loaded the way mapping.py:18-19,
+    86-87 loads it: insert, the counts, has_voxel / try_insert, the export
+    and a pickle round trip (def_pickle replays the inserts) equal the Python
+    psvo.octree.Octree on the same voxels."""
+    import io
+    import pickle
+    from psvo import synthetic as syn
+    torch.classes.load_library(os.path.join(REPO, "proud-slam_amd", "lib", "libsvo_torch.so"))
+    vox = syn.surface_voxels(syn.room0(), seed=0)
+    half = vox.shape[0] // 2
+    t = torch.classes.svo.Octree()
+    t.init(256, 16, 0.2, 8)
+    ref = Octree()
+    ref.init(256, 16, 0.2, 8)
+    for part in (vox[:half], vox[half:]):
+        pts = torch.from_numpy(part).int()
+        t.insert(pts, pts, pts.float())  # mapping.py:292: (voxels, colors, points)
+        ref.insert(part)
+    assert t.count_nodes() == ref.count_nodes() and t.count_leaf_nodes() == ref.count_leaf_nodes()
+    got = t.get_centres_and_children()
+    want = ref.get_centres_and_children()
+    assert len(got) == 5
+    for a, b in zip(got[:3], want[:3]):
+        assert torch.equal(a, b)
+    assert tuple(got[3].shape) == (ref.count_nodes(), 8, 4) and tuple(got[4].shape) == (ref.count_nodes(), 8, 3)
+    assert t.has_voxel(torch.from_numpy(vox[0]).int()) == ref.has_voxel(vox[0])
+    probe = torch.from_numpy(vox[:64] + 1).int()
+    assert t.try_insert(probe) == ref.try_insert(vox[:64] + 1)
+    assert torch.equal(t.get_leaf_voxels(), ref.get_leaf_voxels())
+    # pickling: the construction inputs, replayed into a fresh tree
+    buf = io.BytesIO()
+    torch.save(t, buf)  # the TorchScript pickler (def_pickle)
+    buf.seek(0)
+    t2 = torch.load(buf, weights_only=False)  # our own file, written above
+    assert t2.count_nodes() == t.count_nodes()
+    for a, b in zip(t2.get_centres_and_children()[:3], got[:3]):
+        assert torch.equal(a, b)
+    t3 = pickle.loads(pickle.dumps(t))
+    assert torch.equal(t3.get_centres_and_children()[0], got[0])
+    with pytest.raises(RuntimeError, match="not initialized"):
+        torch.classes.svo.Octree().count_nodes()

@@ -87,8 +87,8 @@ def test_engine_matches_autograd_path():
     eng.close()
 
 
-@pytest.mark.parametrize("padded", [False, True])
-def test_sparse_decoder_matches_dense(padded):
+@pytest.mark.parametrize("padded,sdf_shift", [(False, 0.0), (True, 0.0), (False, 0.5), (True, 0.5)])
+def test_sparse_decoder_matches_dense(padded, sdf_shift):
     """The sparse decoder (the sdf trunk on every sample, the full decoder
     forward and backward on the kept samples only: composited or inside a
     loss mask, composite.hip k_select_samples) against the dense decoder on
@@ -98,11 +98,17 @@ def test_sparse_decoder_matches_dense(padded):
     and colours are the same bits), the statistics equal, the embedding /
     decoder gradients and the pose gradient up to the summation order of the
     weight gradients / the scatter.  A dropped sample's gradient is exactly
-    zero, so a substantial fraction of samples must be dropped and the
-    composited ones kept."""
+    zero.  The random decoder's sdf is negative nearly everywhere: the first
+    sign change is at the padding (pad 1) and every sample is composited;
+    shifted positive (sdf_shift) there is no sign change, z_min is the first
+    sample and most samples are dropped."""
+    from copy import deepcopy
     from psvo.engine import MappingEngine
     from psvo.octree import map_states
     w, tree, emb0, dec = _setup()
+    dec = deepcopy(dec)
+    with torch.no_grad():
+        dec.sdf_out.bias[0] += sdf_shift
     n = 512
     poses, dirs = _frames_of(w, n)
     rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
@@ -124,8 +130,9 @@ def test_sparse_decoder_matches_dense(padded):
         if mode == "sparse":
             sel = eng.select_stats()
             m = out[-1][1][4]
-            assert sel["steps"] == 2 and 0 < sel["composited"] <= sel["kept"] < m, (sel, m)
-            assert sel["kept"] < 0.9 * m, (sel, m)  # the selection drops samples
+            assert sel["steps"] == 2 and 0 < sel["composited"] <= sel["kept"] <= m, (sel, m)
+            if sdf_shift > 0:
+                assert sel["kept"] < 0.8 * m, (sel, m)  # the selection drops samples
         runs[mode] = out
         eng.close()
     n_emb = emb0.shape[0] * 16

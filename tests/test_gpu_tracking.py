@@ -356,5 +356,5 @@ def test_track_frame_matches_reference_golden():
     np.testing.assert_allclose(eng.pose.cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
     out = eng.track_frame(OptimizablePose(torch.from_numpy(g["pose0"])), Frame(), N_rays=n, num_iterations=iters,
                           learning_rate=float(g["lr"]), depth_variance=True, noise=lambda it: noises[it])
-    np.testing.assert_allclose(out.data.cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(out.data.detach().cpu().numpy(), g["pose1"], rtol=0, atol=1e-5)
     eng.close()
