@@ -410,7 +410,8 @@ def main():
     if world > 1:
         dp_engine = MappingEngine(ms, dec, scene.voxel_size, step_size, truncation=0.1, max_distance=max_depth,
                                   criteria=crit_args.criteria, max_depth=max_depth, lr_emb=5e-3, lr_dec=5e-3)
-        dp_engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device))
+        dp_engine.set_exchange(EngineExchange(args.frames * args.rays_per_frame * world, device=device,
+                                              max_rays_rank=args.frames * args.rays_per_frame))
 
     def record_stats(m, r_hit, visits, s_max, into=None):
         sd = stats if into is None else into
@@ -701,19 +702,26 @@ def main():
         t = torch.tensor([kept, comp], dtype=torch.float64, device=device)
         dist.all_reduce(t)
         kept, comp = (float(x) / world for x in t.cpu())
-    # executed: the sdf trunk on every sample, the whole decoder forward and backward on the kept ones
-    flops_exec = (2.0 * trunk * h_m + 3 * 2.0 * macs * kept) if kept is not None else flops_mlp
+    # executed: the sdf trunk on every sample; the whole decoder forward and backward on the kept
+    # ones — width 128 on the composited ones only, the trunk forward + backward (δ chain, dW1, dW2,
+    # the sdf row of W3) on the kept samples that only the direct sdf loss reaches (class B)
+    two_class = w == 128 and kept is not None
+    n_b = max(kept - comp, 0.0) if two_class else 0.0
+    n_full = comp if two_class else kept
+    flops_exec = (2.0 * trunk * h_m + 3 * 2.0 * macs * n_full + 3 * 2.0 * trunk * n_b) if kept is not None \
+        else flops_mlp
+    flops_bwd = (2 * 2.0 * macs * n_full + 2 * 2.0 * trunk * n_b) if kept is not None else 2 * 2.0 * macs * h_m
     mlp_tf = flops_exec / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
     m_bwd = kept if kept is not None else h_m  # the samples the backward runs on
-    if fused_ib:  # k_mlp_bwd3: δ chain + weight gradients (2 x 107.5 kFLOP / sample) + the interpolation backward
-        b_tf = 2 * 2.0 * macs * m_bwd / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
+    if fused_ib:  # k_mlp_bwd3 (+ k_mlp_bwd3t): δ chain + weight gradients + the interpolation backward
+        b_tf = flops_bwd / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
         ib_gbs = 1664.0 * m_bwd / (mlp_b_ms * 1e-3) / 1e9 if mlp_b_ms > 0 else None
-        roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
+        roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_bwd3t + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
                              "interpolation backward: embedding scatter + dL/dx)",
                    "bound": "mfma", "achieved": b_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                    "frac": b_tf / MFMA_F32_PEAK_TFS if b_tf else None,
                    "traffic": tr.get("bwd_fused_bytes_per_launch"), "avg_launch_ms": mlp_b_ms,
-                   "flops_per_launch_executed": 2 * 2.0 * macs * m_bwd,
+                   "flops_per_launch_executed": flops_bwd,
                    "samples_per_launch": m_bwd,
                    "interp_bwd_bytes": 1664.0 * m_bwd,
                    "interp_bwd_bytes_over_kernel_time_frac_hbm": ib_gbs / HBM_PEAK_GBS if ib_gbs else None,
@@ -760,7 +768,8 @@ def main():
                           "flops_executed_per_step": flops_exec,
                           "flops_algorithmic_per_step": flops_mlp,
                           "achieved_basis": "executed FLOPs (sdf trunk on every sample, the whole decoder forward + "
-                                            "backward on the kept samples) / time",
+                                            "backward on the composited samples (W=256: on every kept sample), the "
+                                            "trunk forward + backward on the other kept samples) / time",
                           "effective_algorithmic_tflops": flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None,
                           "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,

@@ -506,19 +506,27 @@ void psvo_engine_free(psvo_engine *e);
  * PSVO_XCH_QUERY is or-ed into ops issued by psvo_map_query or a
  * psvo_map_step_frames look-ahead (they may run concurrently with the
  * previous step's: use a separate communicator).
- * xi32: psvo_engine_exchange_words(world, max_rays_global) device int32;
- * xf64: 16 device doubles (count sums, loss sums).  Returns non-zero on failure.  Exchanged per step:
- * 8 + 1 words per rank (all-gathered), a [200, 50] int32 table of the
- * sampler's slot-0 voxel ids, 16 doubles; then the caller sums grad_flat
- * over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam.  A non-NULL fn turns
+ * xi32: psvo_engine_exchange_words(world, max_rays_global, max_rays_rank)
+ * device int32 (max_rays_global: rays of the union batch; max_rays_rank:
+ * of one rank's shard, 0 = max_rays_global; a larger shard fails the query);
+ * xf64: 16 device doubles (count sums, loss sums).  Returns non-zero on
+ * failure.  Exchanged per step, query phase: ONE all-gather of 8 words + a
+ * hit-count byte per hit ray of the rank (ceil(max_rays_rank / 4) words) —
+ * the union layout and the sampler's slot-0 table follow on every rank —
+ * then ONE all-gather of 8 words after the sampler (S_max and, when the
+ * step's GT depth was known at query time and the loss value is not wanted,
+ * the loss normalisers' counts); step phase: the normaliser counts (8
+ * doubles summed) only when the query could not count them, the loss sums
+ * (8 doubles) only when the loss value is wanted; then the caller sums
+ * grad_flat over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam.  A non-NULL fn turns
  * the protocol on for any world, 1 included (the collectives are then
  * identities: a one-rank communicator drives the whole callback path —
  * tests/test_gpu_rccl.py); fn NULL turns it off. */
 enum { PSVO_XCH_GATHER_I32 = 1, PSVO_XCH_SUM_I32 = 2, PSVO_XCH_SUM_F64 = 3, PSVO_XCH_QUERY = 0x100 };
 typedef int (*psvo_exchange_fn)(void *user, int op, int64_t in_off, int64_t out_off, int64_t count, void *stream);
-int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global);
-int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_rays_global, psvo_exchange_fn fn,
-                             void *user, int *xi32, double *xf64);
+int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global, int64_t max_rays_rank);
+int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_rays_global, int64_t max_rays_rank,
+                             psvo_exchange_fn fn, void *user, int *xi32, double *xf64);
 
 /* Queries psvo_map_query queued and no step has consumed yet (0..2).  A step
  * that fails after picking up its queued query still consumes it. */

@@ -422,36 +422,44 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
 
 
 // ---------------------------------------------------------------------------
-// The sparse decoder's sample selection (engine, width 128): which samples
-// the decoder backward needs.  A sample's gradients are exactly zero unless
+// The sparse decoder's sample selection (engine): which samples the decoder
+// backward needs, and how much of it.  A sample's gradients are exactly zero
+// unless
 //   - it is composited: z < z_min + tr (render_helpers.py:532-539; the only
 //     samples with a weight, so the only ones whose colour reaches the loss,
 //     :544, and whose sdf reaches it through the weights), or
 //   - it lies in a loss mask: front (z < d − tr) or the sdf band
-//     (criterion.py:78-116);
-// the rest (≈ 36 % at config B) get no loss term and no weight.  Every
-// kept sample goes to a compact, ray-major index (cidx; -1: dropped) and the
-// decoder forward (colours, activations) and backward run on the kept
-// samples only — the same per-sample arithmetic, so the same colours, sdf
-// and per-sample gradients; only the weight gradients' summation order
-// changes.  z_min, the masks and `first` are computed exactly as
-// k_composite_loss computes them (same expressions, same padding).
+//     (criterion.py:78-116) — then only its sdf has a gradient (the direct
+//     loss term), so its colour head (sdf_out's feature columns, W4, W5) has
+//     no gradient and no use: the decoder TRUNK (h1, h2, the sdf row) is all
+//     its backward needs.
+// The rest (≈ 32 % at config B) get no loss term and no weight.  Class A
+// (composited) goes to compact, ray-major indices [0, M_A) — the whole
+// decoder runs on them —, class B (kept, not composited) to [cap, cap + M_B)
+// — the trunk only (split = 0: every kept sample is class A, e.g. the width-256
+// decoder).  cidx[s] is the sample's compact index (-1: dropped); the same
+// per-sample arithmetic runs on either class, so the same colours, sdf and
+// per-sample gradients: only the weight gradients' summation order changes.
+// z_min, the masks and `first` are computed exactly as k_composite_loss
+// computes them (same expressions, same padding).
 //
 // One wave per ray (rpw rays per wave when R_hit > 16,384: the look-back's
-// 4,096 workgroups), 4 waves per workgroup; the compact ray offsets by
-// decoupled look-back over {kept, composited} (lookback.h): one launch.
+// 4,096 workgroups), 4 waves per workgroup; the compact ray offsets of both
+// classes by decoupled look-back over {A, B, composited} (lookback.h): one launch.
 constexpr int kSelWaves = 4, kSelMaxRpw = 16;
 struct SelectArgs {
     const float4 *feat;      // [M][16] the interpolated features (4 float4 per sample)
     const int *leaf, *ray_of;
     const float *t;
     int *cidx;               // [M]
-    int *offb;               // [R_hit + 1]
-    float4 *feat_b;          // [M_b][16]
-    int *leaf_b, *ray_of_b;  // [M_b]
-    float *t_b;
-    int *counts;             // [0] kept M_b, [1] composited, [2] flags (look-back abandoned: bit 3), [3] pad,
-                             // then u64 running sums of kept / composited samples and of launches
+    int *offa, *offb;        // [R_hit + 1] each: the classes' compact ray offsets (offb: split only)
+    float4 *feat_c;          // [2 cap][16]: class A rows at [0, M_A), class B at [cap, cap + M_B)
+    int *leaf_c, *ray_of_c;  // [2 cap]
+    float *t_c;
+    int64_t cap;             // class B's base index (the step's sample count M)
+    int split;
+    int *counts;             // [0] M_A, [1] M_B, [2] flags (look-back abandoned: bit 3), [3] pad, then u64
+                             // running sums of kept / composited samples and of launches
     unsigned long long *desc;
     uint32_t tag;
 };
@@ -493,17 +501,19 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
                                                         const int *__restrict__ rank_ray,
                                                         const float *__restrict__ gt_depth,
                                                         const float *__restrict__ sdf_s, SelectArgs a) {
-    __shared__ int s_nb[kSelWaves * kSelMaxRpw], s_off[kSelWaves * kSelMaxRpw];
+    __shared__ int s_na[kSelWaves * kSelMaxRpw], s_nb[kSelWaves * kSelMaxRpw];
+    __shared__ int s_oa[kSelWaves * kSelMaxRpw], s_ob[kSelWaves * kSelMaxRpw];
     __shared__ float s_zmin[kSelWaves * kSelMaxRpw];
-    __shared__ int s_base;
+    __shared__ int s_nc[kSelWaves], s_base[2];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t r0 = ((int64_t)blockIdx.x * kSelWaves + w) * rpw;
     const uint64_t below = (1ull << lane) - 1ull;
-    // ---- count: kept / composited samples per ray
+    const bool split = a.split != 0;
+    // ---- count the classes per ray
     int nc_w = 0;
     for (int k = 0; k < rpw; ++k) {
         const int64_t r = r0 + k;
-        int nb = 0, nc = 0;
+        int na = 0, nb = 0;
         float zmin = 0.f;
         if (r < r_hit) {
             const int off = offsets[r], ns = ray_ns[r];
@@ -514,55 +524,67 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
                 const int s = s0 + lane;
                 SelFlags f{false, false};
                 if (s < ns) f = sel_flags(z[s], zmin, d, tr, max_depth);
-                nb += __popcll(__ballot(f.keep));
-                nc += __popcll(__ballot(f.comp && s < ns));
+                const int nk = __popcll(__ballot(f.keep)), nc = __popcll(__ballot(f.comp && s < ns));
+                na += split ? nc : nk;
+                nb += split ? nk - nc : 0;
+                nc_w += nc;
             }
         }
         if (lane == 0) {
+            s_na[w * rpw + k] = na;
             s_nb[w * rpw + k] = nb;
             s_zmin[w * rpw + k] = zmin;
         }
-        nc_w += nc;
     }
-    if (lane == 0) s_off[w] = nc_w;  // (scratch: the wave's composited count)
+    if (lane == 0) s_nc[w] = nc_w;
     __syncthreads();
     if (w == 0) {
         const int n_r = kSelWaves * rpw;
-        int v = 0;
-        for (int i = lane; i < n_r; i += 64) v += s_nb[i];
-        int c = lane < kSelWaves ? s_off[lane] : 0;
+        int va = 0, vb = 0;
+        for (int i = lane; i < n_r; i += 64) {
+            va += s_na[i];
+            vb += s_nb[i];
+        }
+        int c = lane < kSelWaves ? s_nc[lane] : 0;
 #pragma unroll
         for (int sh = 32; sh > 0; sh >>= 1) {
-            v += __shfl_xor(v, sh, 64);
+            va += __shfl_xor(va, sh, 64);
+            vb += __shfl_xor(vb, sh, 64);
             c += __shfl_xor(c, sh, 64);
         }
-        const uint32_t agg[2] = {(uint32_t)v, (uint32_t)c};
-        uint32_t ex[2];
-        const bool ok = lb_scan<2, 0u>(a.desc, (int)blockIdx.x, (int)gridDim.x, a.tag, lane, agg, ex);
+        const uint32_t agg[3] = {(uint32_t)va, (uint32_t)vb, (uint32_t)c};
+        uint32_t ex[3];
+        const bool ok = lb_scan<3, 0u>(a.desc, (int)blockIdx.x, (int)gridDim.x, a.tag, lane, agg, ex);
         if (lane == 0) {
-            s_base = ok ? (int)ex[0] : -1;
+            s_base[0] = ok ? (int)ex[0] : -1;
+            s_base[1] = (int)ex[1];
             if ((int)blockIdx.x == (int)gridDim.x - 1) {
-                a.offb[r_hit] = (int)(ex[0] + agg[0]);
-                a.counts[0] = ok ? (int)(ex[0] + agg[0]) : 0;  // an abandoned wait: an empty compact batch
-                a.counts[1] = (int)(ex[1] + agg[1]);
+                const uint32_t ta = ex[0] + agg[0], tb = ex[1] + agg[1], tc = ex[2] + agg[2];
+                a.offa[r_hit] = (int)ta;
+                if (split) a.offb[r_hit] = (int)tb;
+                a.counts[0] = ok ? (int)ta : 0;  // an abandoned wait: empty compact batches
+                a.counts[1] = ok ? (int)tb : 0;
+                a.counts[3] = ok ? (int)tc : 0;  // composited (the statistics; split: = counts[0])
                 unsigned long long *sums = reinterpret_cast<unsigned long long *>(a.counts + 4);
-                sums[0] += ex[0] + agg[0];  // one writer per launch, launches stream-ordered
-                sums[1] += ex[1] + agg[1];
+                sums[0] += ta + tb;  // one writer per launch, launches stream-ordered
+                sums[1] += tc;
                 sums[2] += 1;
             }
             if (!ok) atomicOr(a.counts + 2, kLbFlagTimeout);
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive ray offsets of the workgroup's rays
-        int run = s_base;
+    if (threadIdx.x == 0) {  // exclusive ray offsets of the workgroup's rays, per class
+        int ra = s_base[0], rb = s_base[1];
         for (int i = 0; i < kSelWaves * rpw; ++i) {
-            s_off[i] = run;
-            run += s_nb[i];
+            s_oa[i] = ra;
+            s_ob[i] = rb;
+            ra += s_na[i];
+            rb += s_nb[i];
         }
     }
     __syncthreads();
-    if (s_base < 0) return;  // the prefix is undefined: no stores
+    if (s_base[0] < 0) return;  // the prefix is undefined: no stores
     // ---- write: compact index of every sample, the kept samples' rows
     for (int k = 0; k < rpw; ++k) {
         const int64_t r = r0 + k;
@@ -571,24 +593,31 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
         const float *z = z_vals + r * z_stride;
         const float d = gt_depth[rank_ray[r]];
         const float zmin = s_zmin[w * rpw + k];
-        int base = s_off[w * rpw + k];
-        if (lane == 0) a.offb[r] = base;
+        int ba = s_oa[w * rpw + k], bb = s_ob[w * rpw + k];
+        if (lane == 0) {
+            a.offa[r] = ba;
+            if (split) a.offb[r] = bb;
+        }
         for (int s0 = 0; s0 < ns; s0 += 64) {
             const int s = s0 + lane;
-            bool keep = false;
-            if (s < ns) keep = sel_flags(z[s], zmin, d, tr, max_depth).keep;
-            const uint64_t bal = __ballot(keep);
-            const int j = base + __popcll(bal & below);
-            if (s < ns) a.cidx[off + s] = keep ? j : -1;
-            if (keep) {
+            SelFlags f{false, false};
+            if (s < ns) f = sel_flags(z[s], zmin, d, tr, max_depth);
+            const bool in_a = split ? (f.comp && s < ns) : f.keep;
+            const bool in_b = split && f.keep && !f.comp;
+            const uint64_t bal_a = __ballot(in_a), bal_b = __ballot(in_b);
+            const int64_t j = in_a ? (int64_t)(ba + __popcll(bal_a & below))
+                                   : a.cap + bb + __popcll(bal_b & below);
+            if (s < ns) a.cidx[off + s] = (in_a || in_b) ? (int)j : -1;
+            if (in_a || in_b) {
                 const int64_t src = off + s;
-                a.leaf_b[j] = a.leaf[src];
-                a.t_b[j] = a.t[src];
-                a.ray_of_b[j] = (int)r;
+                a.leaf_c[j] = a.leaf[src];
+                a.t_c[j] = a.t[src];
+                a.ray_of_c[j] = (int)r;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) a.feat_b[(int64_t)j * 4 + q] = a.feat[src * 4 + q];
+                for (int q = 0; q < 4; ++q) a.feat_c[j * 4 + q] = a.feat[src * 4 + q];
             }
-            base += __popcll(bal);
+            ba += __popcll(bal_a);
+            bb += __popcll(bal_b);
         }
     }
 }
@@ -656,16 +685,17 @@ int psvo::composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncat
 int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth,
                          const int *offsets, const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray,
                          const float *gt_depth, const float *sdf_s, const float *feat, const int *leaf, const float *t,
-                         const int *ray_of, int *cidx, int *offb, float *feat_b, int *leaf_b, float *t_b,
-                         int *ray_of_b, int *counts, unsigned long long *desc, uint32_t tag) {
-    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0,
+                         const int *ray_of, int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c,
+                         int *leaf_c, float *t_c, int *ray_of_c, int *counts, unsigned long long *desc, uint32_t tag) {
+    PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0 && cap > 0,
                  "select_samples: bad sizes");
+    PSVO_REQUIRE(!split || offb != nullptr, "select_samples: the split needs class B's offsets");
     const int rpw = select_rays_per_wave(r_hit);
     PSVO_REQUIRE(rpw <= kSelMaxRpw, "select_samples: %lld hit rays exceed the selection's %d",
                  (long long)r_hit, kSelWaves * kSelMaxRpw * kLbMaxBlocks);
     if (r_hit == 0) return PSVO_OK;
-    SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offb,
-                 reinterpret_cast<float4 *>(feat_b), leaf_b, ray_of_b, t_b, counts, desc, tag};
+    SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offa, offb,
+                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, cap, split ? 1 : 0, counts, desc, tag};
     psvo::launch(k_select_samples, dim3(div_up(r_hit, (int64_t)kSelWaves * rpw)), dim3(64 * kSelWaves), 0, st, r_hit,
                  rpw, s_max, truncation, max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_depth, sdf_s, a);
     return check_launch("select_samples");
@@ -677,5 +707,5 @@ int psvo::select_rays_per_wave(int64_t r_hit) {
 }
 
 int64_t psvo::select_granules(int64_t r_hit) {
-    return lb_granules<2>(div_up(r_hit, (int64_t)kSelWaves * select_rays_per_wave(r_hit)));
+    return lb_granules<3>(div_up(r_hit, (int64_t)kSelWaves * select_rays_per_wave(r_hit)));
 }

@@ -29,6 +29,7 @@ namespace {
 
 enum { kSumColor = 0, kSumDepth, kNValid, kNFront, kNSdf, kSqFs, kSqSdf, kNSums = 8 };
 enum { kFlagColor = 1, kFlagDepth = 2, kFlagSdf = 4 };
+static_assert(kNValid == 2 && kNFront == 3 && kNSdf == 4, "svo_query.hip k_dist_smax writes these slots");
 // out[] layout (PSVO_CRIT_* in psvo.h)
 enum { kOutLoss = 0, kOutColor, kOutDepth, kOutFs, kOutSdf, kOutFsW, kOutSdfW, kOutCColor, kOutCDepth, kOutCFs,
        kOutCSdf };
@@ -248,6 +249,50 @@ __global__ __launch_bounds__(256) void k_crit_counts(int64_t r_hit, int s_max, f
     }
 }
 
+// data parallel: this rank's count words for the query's second all-gather
+// (psvo_common.h dist_counts) — one wave per local hit row (sampler rows,
+// valid prefix ray_ns), integer atomics (exact, order-free); the padding's
+// terms stay per ray so the union S_max can be applied after the gather
+__global__ __launch_bounds__(256) void k_dist_counts(const int *__restrict__ stats, const int *__restrict__ rank_ray,
+                                                     const float *__restrict__ gt_depth,
+                                                     const float *__restrict__ z_rows, int z_stride,
+                                                     const int *__restrict__ ray_ns, float tr, float max_depth,
+                                                     int *__restrict__ in) {
+    __shared__ int red[7];
+    if (blockIdx.x == 0 && threadIdx.x == 0) in[0] = stats[PSVO_STAT_S_MAX];
+    if (!gt_depth) return;
+    if (threadIdx.x < 7) red[threadIdx.x] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r < stats[PSVO_STAT_R_HIT_LOCAL]) {
+        const float d = gt_depth[rank_ray[r]];
+        const float *z = z_rows + r * z_stride;
+        const int n_in = ray_ns[r];
+        float nf = 0.f, nsm = 0.f;
+        for (int s = lane; s < n_in; s += 64) {
+            const SampleTerms t = sample_terms(z[s], 1.0f, d, tr, max_depth);
+            nf += t.f;
+            nsm += t.sm;
+        }
+        nf = wsum(nf);
+        nsm = wsum(nsm);
+        if (lane == 0) {
+            const SampleTerms pad = sample_terms(kMaxDepthFill, 1.0f, d, tr, max_depth);
+            const int pf = pad.f != 0.0f, ps = pad.sm != 0.0f;
+            atomicAdd(red + 0, (d > 0.01f && d < max_depth) ? 1 : 0);
+            atomicAdd(red + 1, (int)nf);
+            atomicAdd(red + 2, (int)nsm);
+            atomicAdd(red + 3, pf);
+            atomicAdd(red + 4, pf * n_in);
+            atomicAdd(red + 5, ps);
+            atomicAdd(red + 6, ps * n_in);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 7 && red[threadIdx.x] != 0) atomicAdd(in + 1 + threadIdx.x, red[threadIdx.x]);
+}
+
 // the backward coefficients of k_crit_finalize from the count sums alone
 // (same arithmetic, so the two agree bit for bit)
 __global__ void k_crit_coef(const double *__restrict__ sums, double n_hit, double n_cols, float rgb_w, float depth_w,
@@ -390,6 +435,13 @@ int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation,
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");
+}
+int dist_counts(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const float *gt_depth,
+                const float *z_rows, int z_stride, const int *ray_ns, float truncation, float max_depth, int *in) {
+    const int64_t blocks = gt_depth ? (R + 3) / 4 : 1;
+    psvo::launch(k_dist_counts, dim3((int)(blocks > 0 ? blocks : 1)), dim3(256), 0, st, stats, rank_ray, gt_depth,
+                 z_rows, z_stride, ray_ns, truncation, max_depth, in);
+    return check_launch("dist_counts");
 }
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef) {

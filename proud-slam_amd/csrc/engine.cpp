@@ -26,14 +26,16 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kQSlots };
+             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kDistSums, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
     kDepth, kZmin, kCritWs, kSums, kGLoss, kGColor, kGDepth, kGSdf, kGSdfS, kGRgbS, kMlpWs, kDfeat, kDecGrad,
     kGradEmb, kGradOD, kRaysO, kRaysD, kDTmp, kPoseGrad, kSumsC, kCoef, kIbWs,
     // the sparse decoder (select_samples): compact index, ray offsets, the kept samples' rows, counts, look-back
-    kCidx, kOffB, kFeatB, kLeafB, kTB, kRayOfB, kSdfB, kSelCnt, kSelDesc, kSlots
+    kCidx, kOffB, kFeatB, kLeafB, kTB, kRayOfB, kSdfB, kSelCnt, kSelDesc,
+    // its class B (the trunk only): ray offsets, activations and masks
+    kOffB2, kActB, kMasksB, kSlots
 };
 
 struct Arena {
@@ -97,16 +99,18 @@ struct EngineExchange {
     void *user = nullptr;
     int rank = 0, world = 1;
     int nch = 1;               // launch chunks the slot-0 table covers
-    int *xi32 = nullptr;       // psvo_engine_exchange_words(world, max_rays_global) int32
+    int cw = 8;                // words per rank of the query's first gather (dist_count_words(max_rays_rank))
+    int64_t max_rays_rank = 0;
+    int *xi32 = nullptr;       // psvo_engine_exchange_words(world, max_rays_global, max_rays_rank) int32
     double *xf64 = nullptr;    // 16 doubles: [0, 8) count sums, [8, 16) loss sums
     bool on() const { return fn != nullptr; }  // world 1 included: the one-rank protocol (tests)
-    // int32 word offsets
+    // int32 word offsets: [first gather: in | all ranks] [second gather: in | all ranks] [slot-0 count table]
     int64_t in_off() const { return 0; }
-    int64_t all_off() const { return psvo::kDistWordsPerRank; }
-    int64_t smax_in_off() const { return all_off() + (int64_t)world * psvo::kDistWordsPerRank; }
-    int64_t smax_all_off() const { return smax_in_off() + 8; }
-    int64_t table_off() const { return (smax_all_off() + world + 63) / 64 * 64; }
-    int64_t table_words() const { return (int64_t)psvo::kSamplerG * nch * psvo::kMaxHits; }
+    int64_t all_off() const { return cw; }
+    int64_t q2_in_off() const { return all_off() + (int64_t)world * cw; }
+    int64_t q2_all_off() const { return q2_in_off() + psvo::kDistWordsPerRank; }
+    int64_t table_off() const { return (q2_all_off() + (int64_t)world * psvo::kDistWordsPerRank + 63) / 64 * 64; }
+    int64_t table_words() const { return (int64_t)psvo::kSamplerG * nch; }
     int call(int op, int64_t in, int64_t out, int64_t count, hipStream_t st, const char *what) const {
         const int rc = fn(user, op, in, out, count, st);
         if (rc != 0) return psvo::set_error(PSVO_E_LAUNCH, "exchange (%s) failed with %d", what, rc);
@@ -454,28 +458,35 @@ extern "C" int psvo_map_discard(psvo_engine *e) {
     return PSVO_OK;
 }
 
-extern "C" int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global) {
-    if (world < 1 || max_rays_global < 1) return -1;
+static EngineExchange exchange_layout(int world, int64_t max_rays_global, int64_t max_rays_rank) {
     EngineExchange x;
     x.world = world;
     x.nch = dist_slot0_rows(max_rays_global) / kSamplerG;
+    x.max_rays_rank = max_rays_rank > 0 ? max_rays_rank : max_rays_global;
+    x.cw = dist_count_words((int)x.max_rays_rank);
+    return x;
+}
+
+extern "C" int64_t psvo_engine_exchange_words(int world, int64_t max_rays_global, int64_t max_rays_rank) {
+    if (world < 1 || max_rays_global < 1 || max_rays_rank < 0 || max_rays_rank > max_rays_global) return -1;
+    const EngineExchange x = exchange_layout(world, max_rays_global, max_rays_rank);
     return x.table_off() + x.table_words();
 }
 
 extern "C" int psvo_engine_set_exchange(psvo_engine *e, int rank, int world, int64_t max_rays_global,
-                                        psvo_exchange_fn fn, void *user, int *xi32, double *xf64) {
+                                        int64_t max_rays_rank, psvo_exchange_fn fn, void *user, int *xi32,
+                                        double *xf64) {
     PSVO_REQUIRE(e, "engine_set_exchange: null engine");
-    PSVO_REQUIRE(world >= 1 && rank >= 0 && rank < world && max_rays_global >= 1,
-                 "engine_set_exchange: bad rank %d / world %d / max_rays_global %lld", rank, world,
-                 (long long)max_rays_global);
+    PSVO_REQUIRE(world >= 1 && rank >= 0 && rank < world && max_rays_global >= 1 && max_rays_rank >= 0 &&
+                     max_rays_rank <= max_rays_global,
+                 "engine_set_exchange: bad rank %d / world %d / max_rays_global %lld / max_rays_rank %lld", rank,
+                 world, (long long)max_rays_global, (long long)max_rays_rank);
     PSVO_REQUIRE(e->q_count == 0, "engine_set_exchange: queries are queued");
     PSVO_REQUIRE(!fn || (xi32 && xf64), "engine_set_exchange: exchange buffers required");
-    e->x = EngineExchange();
+    e->x = exchange_layout(world, max_rays_global, max_rays_rank);
     e->x.fn = fn;
     e->x.user = user;
     e->x.rank = rank;
-    e->x.world = world;
-    e->x.nch = dist_slot0_rows(max_rays_global) / kSamplerG;
     e->x.xi32 = xi32;
     e->x.xf64 = xf64;
     return PSVO_OK;
@@ -499,8 +510,8 @@ extern "C" int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *o
         return set_error(PSVO_E_LAUNCH, "engine_select_stats: copy failed");
     unsigned long long u[3];
     memcpy(u, c + 4, sizeof(u));
-    out[0] = c[0];
-    out[1] = c[1];
+    out[0] = (int64_t)c[0] + c[1];  // kept: class A + class B
+    out[1] = c[3];                  // composited
     out[2] = (int64_t)u[0];
     out[3] = (int64_t)u[1];
     out[4] = (int64_t)u[2];
@@ -814,14 +825,13 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
                                     ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out, lb, tag));
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
-    if (x.on()) {  // union-batch layout: 8 words all-gathered, then the slot-0 table all-reduced
-        ENG_CALL(dist_pack(st, stats, rank_ray, hit_idx, x.xi32 + x.in_off()));
-        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), kDistWordsPerRank, st,
-                        "query stats"));
-        ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, stats, rank_ray, hit_idx, x.nch,
-                             x.xi32 + x.table_off()));
-        ENG_CALL(x.call(PSVO_XCH_SUM_I32 | PSVO_XCH_QUERY, x.table_off(), x.table_off(), x.table_words(), st,
-                        "slot-0 table"));
+    if (x.on()) {  // union-batch layout: ONE all-gather (8 words + the hit rows' counts), then local
+        if (R > x.max_rays_rank)
+            return set_error(PSVO_E_INVALID, "%s: %lld rays exceed the exchange's max_rays_rank %lld", who,
+                             (long long)R, (long long)x.max_rays_rank);
+        ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off()));
+        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), x.cw, st, "query layout"));
+        ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, x.cw, x.nch, stats, x.xi32 + x.table_off()));
     }
     mark(e, st, PSVO_TIME_INTERSECT, 1);
     const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
@@ -837,13 +847,21 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     if (x.on()) {
         ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
                              x.xi32 + x.table_off(), x.nch, s_idx, s_depth, s_dist, ray_ns, offsets));
-        // S_max of the union: every rank pads its [R_hit, S_max] blocks to it
-        ENG_CALL(dist_pack_smax(st, stats, x.xi32 + x.smax_in_off()));
-        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.smax_in_off(), x.smax_all_off(), 1, st, "S_max"));
-        ENG_CALL(dist_smax(st, x.xi32 + x.smax_all_off(), x.world, stats));
+        // S_max of the union (every rank pads its [R_hit, S_max] blocks to it) and, given the
+        // step's GT depths, the loss normalisers' counts: ONE all-gather of 8 words
+        double *qsums = nullptr;
+        if (counts_gt) {
+            Q_BUF(double, qs_, kDistSums, 8 * sizeof(double));
+            qsums = qs_;
+        }
+        ENG_CALL(dist_counts(st, R, stats, rank_ray, counts_gt, s_depth, max_steps, ray_ns, d->truncation,
+                             d->max_depth, x.xi32 + x.q2_in_off()));
+        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.q2_in_off(), x.q2_all_off(), kDistWordsPerRank, st,
+                        "S_max + counts"));
+        ENG_CALL(dist_smax(st, x.xi32 + x.q2_all_off(), x.world, stats, x.xi32 + x.q2_in_off(), qsums));
     }
     q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
-    q.counts_gt = nullptr;
+    q.counts_gt = x.on() ? counts_gt : nullptr;  // data parallel: the union's count sums in kDistSums
     q.compacted = false;
     if (!x.on()) {  // the sampler's scan does the read-back (and, given the GT depths, the loss normalisers)
         psvo::SampleCounts sc{};
@@ -1271,11 +1289,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const int64_t R = n_rays;
     Render q;
     QuerySet *qset = nullptr;
-    // the normalisers from the sampler's tail: single GPU, and only when the
-    // loss value is not wanted (its reduction reads the counts k_crit_counts
-    // writes into the loss partials)
+    // the normalisers from the query — single GPU the sampler's tail, data
+    // parallel the query's second gather — only when the loss value is not
+    // wanted (its reduction reads the counts k_crit_counts writes into the
+    // loss partials)
     const bool want_loss = !(flags & PSVO_STEP_NO_LOSS);
-    const float *counts_gt = (!e->x.on() && !want_loss) ? gt_depth : nullptr;
+    const float *counts_gt = !want_loss ? gt_depth : nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise, counts_gt));
     QueryGuard guard{e, st, qset};
     if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
@@ -1321,19 +1340,26 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const bool empty = dist && (r_hit == 0 || M == 0);
     const int64_t n_hit = dist ? qset->host_stats[PSVO_STAT_R_HIT] : r_hit;
     // ---- the sparse decoder: the samples whose gradients can be non-zero
-    // (composited, or inside a loss mask: composite.hip k_select_samples) get
-    // compact indices, then the full decoder forward runs on them — sized on
-    // the device (the kept count never reaches the host)
+    // get compact indices (composite.hip k_select_samples) — class A
+    // (composited) at [0, M_A): the whole decoder forward; width 128, class B
+    // (only the direct sdf loss term) at [M, M + M_B): the trunk's
+    // activations (k_mlp_trunk2) — sized on the device (the counts never
+    // reach the host)
     float *const *W = d->dec;
     Render qb = q;  // what the loss pass and the backward read per sample: the kept samples when sparse
     int *cidx = nullptr, *sel_cnt = nullptr;
+    const bool two_class = q.sparse && d->width == 128;
+    int *offb = nullptr;
+    float *act_b = nullptr;
+    uint64_t *masks_b = nullptr;
     if (q.sparse && !empty) {
+        const int64_t M2 = 2 * M;  // the compact rows: class A at [0, M), class B at [M, 2 M)
         ENG_BUF(int, cx, kCidx, M * sizeof(int));
-        ENG_BUF(int, offb, kOffB, (size_t)(r_hit + 1) * sizeof(int));
-        ENG_BUF(float, feat_b, kFeatB, M * 16 * sizeof(float));
-        ENG_BUF(int, leaf_b, kLeafB, M * sizeof(int));
-        ENG_BUF(float, t_b, kTB, M * sizeof(float));
-        ENG_BUF(int, ray_of_b, kRayOfB, M * sizeof(int));
+        ENG_BUF(int, offa, kOffB, (size_t)(r_hit + 1) * sizeof(int));
+        ENG_BUF(float, feat_c, kFeatB, M2 * 16 * sizeof(float));
+        ENG_BUF(int, leaf_c, kLeafB, M2 * sizeof(int));
+        ENG_BUF(float, t_c, kTB, M2 * sizeof(float));
+        ENG_BUF(int, ray_of_c, kRayOfB, M2 * sizeof(int));
         ENG_BUF(int, cnt, kSelCnt, psvo::kSelCountInts * sizeof(int));
         ENG_BUF(unsigned long long, desc, kSelDesc,
                 (size_t)psvo::select_granules(r_hit) * sizeof(unsigned long long));
@@ -1343,25 +1369,36 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
                 return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
             e->sel_zeroed = desc;
         }
+        if (two_class) {
+            ENG_BUF(int, ob, kOffB2, (size_t)(r_hit + 1) * sizeof(int));
+            offb = ob;
+        }
         e->sel_tag = e->sel_tag == 0xffffffffu ? 1u : e->sel_tag + 1u;
         mark(e, st, PSVO_TIME_SELECT, 0);
         ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
-                                      q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, cx,
-                                      offb, feat_b, leaf_b, t_b, ray_of_b, cnt, desc, e->sel_tag));
+                                      q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, M,
+                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, cnt, desc, e->sel_tag));
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
-        ENG_BUF(float, rgb_b, kRgbS, M * 3 * sizeof(float));
+        ENG_BUF(float, rgb_c, kRgbS, M2 * 3 * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
         ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
-        ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_b, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                                  q.images, sdf_b, rgb_b, act, masks, cnt));
+        ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_c, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
+                                  q.images, sdf_b, rgb_c, act, masks, cnt));
+        if (two_class) {
+            ENG_BUF(float, ab, kActB, (size_t)psvo_mlp_act_floats(M, d->width) / 2 * sizeof(float));  // h1, h2
+            ENG_BUF(uint64_t, mb, kMasksB, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
+            ENG_CALL(psvo::mlp_fwd_trunk(st, M, cnt + 1, feat_c + M * 16, q.images, ab, mb, rgb_c + M * 3));
+            act_b = ab;
+            masks_b = mb;
+        }
         mark(e, st, PSVO_TIME_MLP_FWD, 1);
-        qb.offsets = offb;
-        qb.leaf = leaf_b;
-        qb.tt = t_b;
-        qb.ray_of = ray_of_b;
-        qb.feat = feat_b;
-        qb.rgb_s = rgb_b;
+        qb.offsets = offa;
+        qb.leaf = leaf_c;
+        qb.tt = t_c;
+        qb.ray_of = ray_of_c;
+        qb.feat = feat_c;
+        qb.rgb_s = rgb_c;
         qb.act = act;
         qb.masks = masks;
         cidx = cx;
@@ -1378,7 +1415,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         sums = sl;
     }
     // the sampler counted the normalisers for exactly this GT (its tail wrote the coefficients)
-    const bool coef_q = counts_gt && qset->counts_gt == counts_gt;
+    const bool coef_q = !dist && counts_gt && qset->counts_gt == counts_gt;
+    // data parallel: the query gathered the union's counts for exactly this GT
+    const bool sums_q = dist && counts_gt && qset->counts_gt == counts_gt;
     float *coef = coef_q ? static_cast<float *>(qset->a.p[kCoefQ]) : nullptr;
     if (!coef_q) {
         ENG_BUF(float, cbuf, kCoef, 4 * sizeof(float));
@@ -1386,8 +1425,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     ENG_BUF(float, color, kColor, (size_t)r_hit * 3 * sizeof(float));
     ENG_BUF(float, depth, kDepth, (size_t)r_hit * sizeof(float));
-    ENG_BUF(float, g_sdf_s, kGSdfS, M * sizeof(float));
-    ENG_BUF(float, g_rgb_s, kGRgbS, M * 3 * sizeof(float));
+    const int64_t m_rows = q.sparse ? 2 * M : M;  // per-sample gradient rows (the sparse decoder: at cidx)
+    ENG_BUF(float, g_sdf_s, kGSdfS, m_rows * sizeof(float));
+    ENG_BUF(float, g_rgb_s, kGRgbS, m_rows * 3 * sizeof(float));
     // sparse-exact Adam (single GPU): the rows this step can touch, beside the
     // decoder — marked whenever the flags exist, also when the caller runs the
     // Adam step itself (PSVO_STEP_NO_ADAM, then psvo_map_adam): a later fused
@@ -1398,9 +1438,13 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // exchange lists them; the union flags come from what it exchanged)
     uint8_t *const mark_into = mark_rows ? d->emb_row_flags : (dist ? d->emb_row_local : nullptr);
     if (dist) {
-        ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray, gt_depth,
-                                  q.z_vals, crit_ws, sums_c));
-        ENG_CALL(x.call(PSVO_XCH_SUM_F64, 0, 0, 8, ax, "loss normalisers"));
+        if (sums_q) {
+            sums_c = static_cast<double *>(qset->a.p[kDistSums]);
+        } else {
+            ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray,
+                                      gt_depth, q.z_vals, crit_ws, sums_c));
+            ENG_CALL(x.call(PSVO_XCH_SUM_F64, 0, 0, 8, ax, "loss normalisers"));
+        }
         ENG_CALL(criterion_coef_from_sums(ax, sums_c, n_hit, s_max, d->truncation, d->w_rgb, d->w_depth, d->w_fs,
                                           d->w_sdf, crit_flags, coef));
     } else if (!coef_q) {
@@ -1487,16 +1531,21 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
     float *gx = nullptr;
     if (fuse_ib) {
-        ENG_BUF(float, gxb, kIbWs, (size_t)M * 3 * sizeof(float));
+        ENG_BUF(float, gxb, kIbWs, (size_t)m_rows * 3 * sizeof(float));
         gx = gxb;
     }
     const psvo::InterpFuse ipf{qb.leaf,  qb.ray_of,    q.rank_ray, d->vertex_idx, qb.tt, rays_o, rays_d, d->centres,
                                d->emb,   d->voxel_size, grad_emb,   gx,            mark_into};
     mark(e, st, PSVO_TIME_MLP_BWD, 0);
+    // the sparse decoder's class B: its rows at [M, 2 M) of the compact arrays
+    const psvo::InterpFuse ipf_b{qb.leaf + M, qb.ray_of + M, q.rank_ray, d->vertex_idx, qb.tt + M, rays_o, rays_d,
+                                 d->centres, d->emb, d->voxel_size, grad_emb, gx ? gx + 3 * M : nullptr, mark_into};
+    const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, masks_b, g_sdf_s + M, qb.feat + M * 16, act_b,
+                             fuse_ib ? &ipf_b : nullptr};
     ENG_CALL(mlp_bwd(st, M, d->width, qb.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      qb.rgb_s, qb.act, qb.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6],
                      G[7], G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr,
-                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt));
+                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt, act_b ? &tbw : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     if (overlap) e->bwd_recorded = true;  // mlp_bwd recorded dfeat_ready on st
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
@@ -1510,7 +1559,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     e->clean_buf = grad_emb;
     if (fuse_ib) {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
-        ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, qb.offsets, q.rank_ray, qb.tt, gx, grad_od, grad_od + R * 3));
+        ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, qb.offsets, q.rank_ray, qb.tt, gx, grad_od, grad_od + R * 3,
+                                      act_b ? offb : nullptr, act_b ? qb.tt + M : nullptr,
+                                      act_b ? gx + 3 * M : nullptr));
         mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     } else {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);

@@ -305,19 +305,24 @@ __global__ __launch_bounds__(256) void k_interp_bwd_rays(int64_t r_hit, int c_ma
 __global__ __launch_bounds__(256) void k_interp_rays_gx(int64_t r_hit, const int *__restrict__ offsets,
                                                         const int *__restrict__ ray_index, const float *__restrict__ t,
                                                         const float *__restrict__ gx, float *__restrict__ grad_o,
-                                                        float *__restrict__ grad_d) {
+                                                        float *__restrict__ grad_d, const int *__restrict__ offsets2,
+                                                        const float *__restrict__ t2, const float *__restrict__ gx2) {
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= r_hit) return;
     const int lane = threadIdx.x & 63;
-    const int beg = offsets[r], end = offsets[r + 1];
     float go[3] = {0.f, 0.f, 0.f}, gd[3] = {0.f, 0.f, 0.f};
-    for (int s = beg + lane; s < end; s += 64) {
-        const float ts = t[s];
+    for (int seg = 0; seg < (offsets2 ? 2 : 1); ++seg) {
+        const int *of = seg ? offsets2 : offsets;
+        const float *ts_ = seg ? t2 : t, *gx_ = seg ? gx2 : gx;
+        const int beg = of[r], end = of[r + 1];
+        for (int s = beg + lane; s < end; s += 64) {
+            const float ts = ts_[s];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = gx[(int64_t)s * 3 + a];
-            go[a] += v;
-            gd[a] += v * ts;
+            for (int a = 0; a < 3; ++a) {
+                const float v = gx_[(int64_t)s * 3 + a];
+                go[a] += v;
+                gd[a] += v * ts;
+            }
         }
     }
 #pragma unroll
@@ -340,10 +345,11 @@ __global__ __launch_bounds__(256) void k_interp_rays_gx(int64_t r_hit, const int
 }  // namespace
 
 int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int *ray_index, const float *t,
-                   const float *gx, float *grad_o, float *grad_d) {
+                   const float *gx, float *grad_o, float *grad_d, const int *offsets2, const float *t2,
+                   const float *gx2) {
     if (r_hit == 0) return PSVO_OK;
     psvo::launch(k_interp_rays_gx, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, offsets, ray_index, t, gx,
-                       grad_o, grad_d);
+                 grad_o, grad_d, offsets2, t2, gx2);
     return check_launch("interp_rays_gx");
 }
 }  // namespace psvo

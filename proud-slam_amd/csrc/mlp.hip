@@ -488,7 +488,10 @@ struct DwDst {
     int elem_begin[6];
 };
 
-__global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst dst, int accumulate) {
+// slabs_b (or null): k_mlp_bwd3t's slabs (the same layout), whose W1, W2, W3
+// row 0 and b3[0] elements are added (the rest of its slabs is not written)
+__global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst dst, int accumulate,
+                                const float *__restrict__ slabs_b) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= dst.elem_begin[5]) return;
     int L = 0;
@@ -508,6 +511,10 @@ __global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst
         for (int u = 0; u < 8; ++u) v += q[u];
     }
     for (; sp < n_split; ++sp) v += p[sp * stride];
+    if (slabs_b && (L < 2 || (L == 2 && (rel < 128 || rel == 129 * 128)))) {
+        const float *pb = slabs_b + g.slab_off[L] + rel;
+        for (int k = 0; k < n_split; ++k) v += pb[k * stride];
+    }
     const int nw = dst.rows[L] * dst.cols[L];
     float *out = rel < nw ? dst.w[L] + rel : dst.b[L] + (rel - nw);
     *out = accumulate ? *out + v : v;
@@ -803,6 +810,74 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m, const flo
         (void)relu(bacc);
         const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
         if (valid && h == 0) sdf_out[s] = sdf;
+    }
+    wait_vm(0);
+}
+
+// The sparse decoder's class B (samples with only a loss term on their sdf,
+// composite.hip k_select_samples): the trunk's activations for the trunk
+// backward (k_mlp_bwd3t) — h1 and h2 as CF tiles (matrices 0 and 1 of `act`,
+// the layout k_mlp_fwd2 writes; h1 stored from inside the W2 GEMM), the ReLU
+// masks (m1, m2; the c1 word 0) — and zero colours (the compositing pass
+// reads a colour for every kept sample; these carry weight 0).  The same
+// instruction sequence as k_mlp_sdf2 / k_mlp_fwd2's first two layers: the
+// same h1 / h2 bits.  m: the class's count on the device.
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk2(const int *__restrict__ m_dev,
+                                                              const float *__restrict__ feat,
+                                                              const float *__restrict__ img, float *__restrict__ act,
+                                                              uint64_t *__restrict__ masks, float *__restrict__ rgb) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int64_t m = __builtin_amdgcn_readfirstlane(*m_dev);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples): the layout k_mlp_bwd3t reads
+    const int64_t tstride = n_tiles * 32 * 128;
+    const int64_t tbytes = tstride * 4;
+    float *w2 = lds + kF2Buf0;
+    int64_t t = blockIdx.x;
+    float xn[8];
+    {
+        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+        load_x(feat, s, s < m, h, xn);
+    }
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
+    stage8(w2, img + kImgF2, 16384, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    for (; t < n_wg_tiles; t += gridDim.x) {
+        const int64_t u = t * kF2Waves + wave;  // this wave's 32-sample CF tile
+        const int64_t s = u * kTileS + (lane & 31);
+        const bool valid = s < m;
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = xn[i];
+        if (t + gridDim.x < n_wg_tiles) {
+            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+            load_x(feat, sn, sn < m, h, xn);
+        }
+        const CfStore cfs(u, lane, n_tiles);
+        f32x16 a[kNB], bacc[kNB];
+        init_bias(a, lds + kOffB1, h);
+        gemm_x(lds + kF2W1, x, a, lane);
+        const uint64_t m1 = relu(a);
+        init_bias(bacc, lds + kOffB2, h);
+        gemm_acc<kNB, kNB>(w2, a, bacc, lane, CfQueue(cfs, act, tbytes, true, a));  // + h1 stores
+        const uint64_t m2 = relu(bacc);
+        cfs.store(act + tstride, tbytes, bacc);  // h2
+        if (valid) {
+            uint64_t *mk = masks + (s * 2 + h) * 3;
+            mk[0] = m1;
+            mk[1] = m2;
+            mk[2] = 0;
+            if (h == 0) {
+                rgb[s * 3 + 0] = 0.f;
+                rgb[s * 3 + 1] = 0.f;
+                rgb[s * 3 + 2] = 0.f;
+            }
+        }
     }
     wait_vm(0);
 }
@@ -1448,6 +1523,253 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
     }
 }
 
+// ---------------------------------------------------------------------------
+// The trunk backward (the sparse decoder's class B: samples whose only loss
+// term is the direct one on their sdf — composite.hip k_select_samples): the
+// colour head's δ's are exactly zero there (g_rgb = 0, so δ5 = δc1 = δf = 0),
+// so the chain is
+//   δh2 = W3[0]ᵀ dsdf ⊙ m2 (VALU),  δh1 = W2ᵀ δh2 ⊙ m1,  dfeat = W1ᵀ δh1
+// and the weight gradients dW2 += δh2 ⊗ h1, dW1 += δh1 ⊗ x, W3 row 0 +=
+// dsdf ⊗ h2 (+ the biases): 37.1 of k_mlp_bwd3's 107.5 k MACs per sample.
+// The same unit images, operand layouts and chain arithmetic as k_mlp_bwd3
+// (the same per-sample dfeat bits), in two phases per round of four
+// 16-sample units:
+//   phase  chain wave c (unit u0 + 4r + c)                         gradient wave d
+//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2;    dW2 col block d += δh2(r−1) ⊗ h1(r−1)
+//          dW1 row block c += δh1(r−1) ⊗ x(r−1)
+//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          W3 row 0 (cols of block d) += dsdf(r) · h2(r)
+//          backward (dL/dx, the embedding scatter)
+// plus a last phase A for the final round's dW2 / dW1.  Writes one slab per
+// workgroup of W1 (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the
+// DwGrid layout; k_mlp_dw_reduce adds these elements only).  m: the class's
+// sample count on the device.
+constexpr int kT3H2 = kVecPad;                // δh2 images [set 2][unit 4]
+constexpr int kT3H1 = kT3H2 + 2 * 4 * kUImg;  // δh1 images [unit 4]
+constexpr int kT3S = kT3H1 + 4 * kUImg;       // dsdf rows [unit 4][16]
+constexpr int kT3X = kT3S + 4 * kU;           // x images [round parity 2][unit 4][16 × 16]
+constexpr int kT3I = kT3X + 2 * 4 * 16 * kU;  // interpolation backward staging [chain wave 4][512]
+constexpr int kT3A = kT3I + 4 * 512;          // dW1 accumulators [chain wave 4][4][lane 64][4]
+constexpr int kLdsBwd3t = (kT3A + 4 * 1024) * 4;  // 136,448 B
+static_assert(kLdsBwd3t <= 160 * 1024, "bwd3t LDS budget");
+
+struct TrunkIn {
+    uint64_t m1, m2;
+    float gs;
+    float4 x;
+};
+__device__ __forceinline__ void load_trunk_in(const uint64_t *__restrict__ masks, const float *__restrict__ g_sdf,
+                                              const float *__restrict__ feat, int64_t s, bool valid, int q,
+                                              TrunkIn &in) {
+    const int64_t sv = valid ? s : 0;
+    const uint64_t *mk = masks + (sv * 2 + (q & 1)) * 3;
+    in.m1 = mk[0];
+    in.m2 = mk[1];
+    in.gs = g_sdf[sv];
+    in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
+}
+
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restrict__ m_dev,
+                                                             const float *__restrict__ img,
+                                                             const uint64_t *__restrict__ masks,
+                                                             const float *__restrict__ g_sdf,
+                                                             const float *__restrict__ feat,
+                                                             const float *__restrict__ act, DwGrid g,
+                                                             float *__restrict__ slabs, InterpFuse ip) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int64_t m = __builtin_amdgcn_readfirstlane(*m_dev);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples): k_mlp_trunk2's layout
+    const int64_t tstride = n_tiles * kCfTile;
+    const int64_t tb = tstride * 4;
+    const int64_t n_units = (m + kU - 1) / kU;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int n_rounds = (int)((u1 - u0 + 3) / 4);
+    auto h2set = [&](int par) { return lds + kT3H2 + (par & 1) * 4 * kUImg; };
+    float *const h1set = lds + kT3H1, *const sset = lds + kT3S;
+    auto xset = [&](int par) { return lds + kT3X + (par & 1) * 4 * 16 * kU; };
+    stage8(lds, img + kImgVec, kVecPad, wave, lane);
+    wait_vm(0);
+    raw_barrier();
+    const int b = blockIdx.x;
+    const int i = lane & 31, h = lane >> 5;
+    const bool fuse = ip.gx != nullptr;  // uniform
+    if (wave < 4) {
+        // ================= chain wave c
+        const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
+        const int c = wave;
+        const int n = lane & 15, q = lane >> 4;
+        const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot
+        const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
+        float *const page1 = lds + kT3A + c * 1024;  // dW1 accumulators
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        float b1p = 0.f;
+        TrunkIn nin;
+        {
+            const int64_t u = u0 + c;
+            const int64_t s = u * kU + n;
+            load_trunk_in(masks, g_sdf, feat, s, u < u1 && s < m, q, nin);
+        }
+        for (int r = 0; r <= n_rounds; ++r) {
+            const int64_t ubase = u0 + 4 * (int64_t)r;
+            const int64_t u = ubase + c;
+            const bool active = r < n_rounds && u < u1;  // wave-uniform
+            const int64_t s = u * kU + n;
+            const bool valid = active && s < m;
+            // ---- A: δh2, dsdf, x → LDS; δh1 = W2ᵀ δh2 ⊙ m1; dW1 of the previous round
+            f32x4v fa[8];
+            uint64_t m1 = 0;
+            if (r < n_rounds) {
+                const TrunkIn in = nin;
+                const float dsdf = valid ? in.gs : 0.0f;
+                const int sh = 4 * (q >> 1);
+                m1 = valid ? in.m1 >> sh : 0;
+                const uint64_t m2 = valid ? in.m2 >> sh : 0;
+                float *xl = xset(r) + c * 16 * kU;
+                xl[wb + 0] = valid ? in.x.x : 0.f;
+                xl[wb + 16] = valid ? in.x.y : 0.f;
+                xl[wb + 32] = valid ? in.x.z : 0.f;
+                xl[wb + 48] = valid ? in.x.w : 0.f;
+                if (q == 0) sset[c * kU + sn] = dsdf;
+                if (active) {
+                    f32x4v fb[8];
+#pragma unroll
+                    for (int ob = 0; ob < 8; ++ob) {  // δh2 = W3[0]ᵀ dsdf ⊙ m2 (k_mlp_bwd3's δf = 0 case)
+                        const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
+                        fb[ob] = f32x4v{__fmul_rn(w.x, dsdf), __fmul_rn(w.y, dsdf), __fmul_rn(w.z, dsdf),
+                                        __fmul_rn(w.w, dsdf)};
+                    }
+                    mask16(fb, m2);
+                    lds_u_store<8>(h2set(r) + c * kUImg, wb, fb);
+                    zero4(fa);
+                    gemm16<8, 4, 2>(wrs, kImgC2, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);
+                    gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
+                    mask16(fa, m1);  // δh1
+                }
+            }
+            if (r > 0) xgrad16(h1set, xset(r - 1), c, ubase - 4, u1, lane, page1, &b1p);
+            // the interpolation backward's sample data, one dependent level per phase
+            int lf = 0, ro = 0;
+            float ts = 0.f;
+            if (fuse && valid) {
+                lf = ip.leaf[s];
+                ro = ip.ray_of[s];
+                ts = ip.t[s];
+            }
+            raw_barrier();
+            if (r == n_rounds) break;
+            // ---- B: δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation backward; the next unit's inputs
+            if (active) lds_u_store<8>(h1set + c * kUImg, wb, fa);
+            int4 vid0 = make_int4(0, 0, 0, 0), vid1 = make_int4(0, 0, 0, 0);
+            float cen[3] = {0.f, 0.f, 0.f};
+            int row = 0;
+            if (fuse && valid) {
+                vid0 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8);
+                vid1 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8 + 4);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
+                row = ip.rank_ray[ro];
+            }
+            if (r + 1 < n_rounds) {
+                const int64_t un = u + 4;
+                const int64_t snx = un * kU + n;
+                load_trunk_in(masks, g_sdf, feat, snx, un < u1 && snx < m, q, nin);
+            }
+            if (active) {
+                f32x4v t1[1];
+                zero4(t1);
+                gemm16<8, 1, 4>(wrs, kImgC1, fa, t1, lane);
+                const float4 gf = make_float4(t1[0][0], t1[0][1], t1[0][2], t1[0][3]);
+                if (fuse) {
+                    float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
+                    float4 ev[8];
+                    const int vid[8] = {vid0.x, vid0.y, vid0.z, vid0.w, vid1.x, vid1.y, vid1.z, vid1.w};
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) ev[k] = reinterpret_cast<const float4 *>(ip.emb)[(int64_t)vid[k] * 4 + q];
+                    if (valid) {
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+                            ro3[a] = ip.rays_o[(int64_t)row * 3 + a];
+                            rd3[a] = ip.rays_d[(int64_t)row * 3 + a];
+                        }
+                    }
+                    interp_bwd_unit(ip, lds + kT3I + c * 512, m, s, valid, n, q, ts, ro3, rd3, cen, vid0, vid1, ev,
+                                    gf);
+                    if (ip.grad_emb != nullptr) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging is this wave's own
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        scatter_unit(ip, lds + kT3I + c * 512, u, m, lane, lf);
+                    }
+                }
+            }
+            raw_barrier();
+        }
+        // ---- slab: W1 row block c + b1
+        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
+        if (i < 16) {
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int row = 32 * c + phi(rr, h);
+                const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
+                store_nt(s1, row * 16 + i, page1[pos]);
+            }
+        }
+        const float bv = b1p + __shfl_xor(b1p, 32, 64);
+        if (h == 0) store_nt(s1, 128 * 16 + 32 * c + i, bv);
+    } else {
+        // ================= gradient wave: column block d of W2, row 0 of W3 (cols of block d), biases
+        const int d = wave - 4;
+        f32x16 acc2[kNB];
+        zero(acc2);
+        float b2p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f;
+        const __amdgpu_buffer_rsrc_t h1m = rsrc_of(act, tb), h2m = rsrc_of(act + tstride, tb);
+        float4 ring[3];
+        for (int r = 0; r <= n_rounds; ++r) {
+            const int64_t ubase = u0 + 4 * (int64_t)r;
+            // A: dW2 of the previous round (its δh2 set, h1 tiles)
+            if (r > 0) {
+                ring[0] = dw_bsrc(h1m, ubase - 4, u1, d, lane, 0);
+                ring[1] = dw_bsrc(h1m, ubase - 4, u1, d, lane, 1);
+                dw_job<0, 0>(ring, h2set(r - 1), nullptr, h1m, ubase - 4, true, h1m, ubase, false, u1, d, lane, acc2,
+                             b2p, unused0, unused1);
+            }
+            raw_barrier();
+            if (r == n_rounds) break;
+            // B: W3 row 0 += dsdf ⊙ h2 (this round's dsdf rows, h2 tiles)
+#pragma unroll
+            for (int qq = 0; qq < 8; ++qq) {
+                const int up = qq >> 1, gg = qq & 1;
+                if (ubase + up < u1) {  // wave-uniform
+                    const float4 bb = dw_bsrc(h2m, ubase, u1, d, lane, qq);
+                    const float4 w = *reinterpret_cast<const float4 *>(sset + up * kU + 8 * h + 4 * gg);
+                    r0 += (bb.x * w.x + bb.y * w.y) + (bb.z * w.z + bb.w * w.w);
+                    b30 += (w.x + w.y) + (w.z + w.w);
+                }
+            }
+            raw_barrier();
+        }
+        const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
+        float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
+        float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
+        {
+            f32x16 t[kNB][1];
+#pragma unroll
+            for (int k = 0; k < kNB; ++k) t[k][0] = acc2[k];
+            dw_store<kNB, 1, true>(s2, 128, 0, 128, rb, cb, t, lane);
+        }
+        const float v2 = b2p + __shfl_xor(b2p, 32, 64), vr0 = r0 + __shfl_xor(r0, 32, 64),
+                    v30 = b30 + __shfl_xor(b30, 32, 64);
+        if (h == 0) {
+            store_nt(s2, 128 * 128 + 32 * d + i, v2);
+            store_nt(s3, 32 * d + i, vr0);  // W3 row 0 (sdf)
+        }
+        if (d == 0 && lane == 0) store_nt(s3, 129 * 128, v30);
+    }
+}
+
 static int device_cus() {
     static int cus = 0;
     if (cus == 0) {
@@ -1539,6 +1861,23 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
 }
 
 namespace psvo {
+int mlp_fwd_trunk(hipStream_t st, int64_t m_cap, const int *m_dev, const float *feat, const float *images, float *act,
+                  uint64_t *masks, float *rgb) {
+    PSVO_REQUIRE(m_cap >= 0 && m_cap <= kMaxSamples && m_dev && images && act && masks && rgb,
+                 "mlp_fwd_trunk: bad arguments");
+    if (m_cap == 0) return PSVO_OK;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk2),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSdf2);
+        attr = true;
+    }
+    const int64_t tiles = div_up(m_cap, kF2Tile);
+    const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
+    psvo::launch(k_mlp_trunk2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m_dev, feat, images, act, masks, rgb);
+    return check_launch("mlp_fwd_trunk");
+}
+
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images) {
@@ -1590,7 +1929,7 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
     dw_grid_uniform(bwd3_grid(m), &g, &slab);
-    return m * 3 + slab;
+    return m * 3 + 2 * (int64_t)slab;  // k_mlp_bwd3's slabs, then k_mlp_bwd3t's (the sparse decoder's class B)
 }
 
 extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split) {
@@ -1608,7 +1947,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream,
-            const int *m_dev) {
+            const int *m_dev, const TrunkBwd *tb) {
     PSVO_REQUIRE(ip == nullptr || ((width == 256 || width == kW) && gw1 != nullptr),
                  "mlp_bwd: the fused interpolation backward needs a fused weight-gradient path");
     if (width == 256) {
@@ -1628,6 +1967,9 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     DwGrid g;
     int slab_floats;
     float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
+    PSVO_REQUIRE(tb == nullptr || (gw1 != nullptr && tb->m_dev && tb->masks && tb->g_sdf && tb->feat && tb->act),
+                 "mlp_bwd: the trunk backward needs the weight-gradient path and its inputs");
+    float *slabs_b = nullptr;
     auto reduce = [&](float *slabs, hipStream_t rs) {
         DwDst d;
         int e = 0;
@@ -1640,7 +1982,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             e += kDwRows[l] * kDwCols[l] + kDwRows[l];
         }
         d.elem_begin[5] = e;
-        psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate);
+        psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate,
+                     static_cast<const float *>(slabs_b));
         return check_launch("mlp_dw_reduce");
     };
     {  // fused δ chain + weight gradients (or the chain alone: frozen decoder)
@@ -1676,6 +2019,19 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             if (rc) return rc;
         } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
             return set_error(PSVO_E_LAUNCH, "mlp_bwd: memset failed");
+        }
+        if (tb && m > 0) {  // the trunk backward of the sparse decoder's class B, its own slabs
+            static bool attr_t = false;
+            if (!attr_t) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd3t),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd3t);
+                attr_t = true;
+            }
+            slabs_b = slabs + slab_floats;
+            psvo::launch(k_mlp_bwd3t, dim3(grid), dim3(kF2Threads), kLdsBwd3t, st, tb->m_dev, images, tb->masks,
+                         tb->g_sdf, tb->feat, tb->act, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{});
+            const int rc = check_launch("mlp_bwd3t");
+            if (rc) return rc;
         }
         if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");

@@ -177,21 +177,30 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr,
                      unsigned long long *lb_desc = nullptr, uint32_t lb_tag = 0);
 
-// data-parallel query (svo_query.hip): rows of the exchanged slot-0 table for
-// a union batch of at most max_rays_global rays; pack this rank's 8 words;
-// union statistics + slot-0 table from the gathered words; the sampler over
-// the rank's rows; S_max of the union
+// data-parallel query (svo_query.hip): rows of the slot-0 count table for a
+// union batch of at most max_rays_global rays; the words one rank
+// contributes to the query's first all-gather (8 words + a hit-count byte per
+// hit row, for at most max_rays_rank rays); pack them; union statistics +
+// slot-0 count table from the gathered words; the sampler over the rank's
+// rows; after the second all-gather ([S_max, 7 count words] per rank) the
+// union S_max and normaliser sums
 constexpr int kDistWordsPerRank = 8;
 int dist_slot0_rows(int64_t max_rays_global);
-int dist_pack(hipStream_t st, const int *stats, const int *rank_ray, const int *hit_idx, int *out);
-int dist_layout(hipStream_t st, const int *all, int world, int rank, int *stats, const int *rank_ray,
-                const int *hit_idx, int nch, int *table);
+int dist_count_words(int max_rays_rank);
+int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
+              const int *ray_nv, int *out);
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table);
 int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                 const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
                 int *offsets);
-int dist_pack_smax(hipStream_t st, const int *stats, int *out);
-int dist_smax(hipStream_t st, const int *all, int world, int *stats);
+int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, double *sums);
+// this rank's words of the second gather: in[0] = S_max of its rows; given
+// the GT depths, in[1..7] += n_valid, Σ front / Σ sdf-band over the valid
+// samples, and per padding class (front, band: sample_terms of the MAX_DEPTH
+// fill) the rays and their Σ ns — in[1..7] zero on entry (criterion.hip)
+int dist_counts(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const float *gt_depth,
+                const float *z_rows, int z_stride, const int *ray_ns, float truncation, float max_depth, int *in);
 
 // psvo_criterion_coef split at the count sums (criterion.hip)
 int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
@@ -212,22 +221,24 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
                      float *workspace, float *color, float *depth, float *grad_sdf_s, float *grad_rgb_s,
                      bool partials = true,  // false: no loss partials (the loss value is not wanted)
                      const int *cidx = nullptr);  // the sparse decoder's compact sample index (select_samples)
-// The sparse decoder's sample selection (composite.hip k_select_samples): the
-// samples whose gradients can be non-zero (composited or inside a loss mask)
-// get compact, ray-major indices cidx[s] (-1: dropped), compact ray offsets
-// offb [R_hit + 1] and compact copies of their features / leaf / t / ray;
-// counts[0] = kept samples (the compact decoder launches read it on the
-// device), counts[1] = composited samples, counts[2] |= 8 if the look-back
-// wait was abandoned (then counts[0] = 0); counts + 4: u64 running sums of
-// kept / composited samples and of launches (kSelCountInts ints, zeroed
-// once).  desc: select_granules(r_hit) granules, zeroed once; tag fresh per
-// launch (≠ 0).
+// The sparse decoder's sample selection (composite.hip k_select_samples):
+// the samples whose gradients can be non-zero get compact, ray-major indices
+// cidx[s] (-1: dropped) — class A (composited: the whole decoder) at
+// [0, M_A), class B (only a loss term: the decoder trunk) at [cap, cap + M_B)
+// (split = false: every kept sample in class A) —, the classes' compact ray
+// offsets offa / offb [R_hit + 1] and compact copies of their features /
+// leaf / t / ray ([2 cap] arrays).  counts[0] = M_A, counts[1] = M_B (the
+// compact decoder launches read them on the device), counts[2] |= 8 if the
+// look-back wait was abandoned (then both are 0); counts + 4: u64 running
+// sums of kept / composited samples and of launches (kSelCountInts ints,
+// zeroed once).  desc: select_granules(r_hit) granules, zeroed once; tag
+// fresh per launch (≠ 0).
 constexpr int kSelCountInts = 10;
 int select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *offsets,
                    const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_depth,
                    const float *sdf_s, const float *feat, const int *leaf, const float *t, const int *ray_of,
-                   int *cidx, int *offb, float *feat_b, int *leaf_b, float *t_b, int *ray_of_b, int *counts,
-                   unsigned long long *desc, uint32_t tag);
+                   int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c, int *leaf_c, float *t_c,
+                   int *ray_of_c, int *counts, unsigned long long *desc, uint32_t tag);
 int select_rays_per_wave(int64_t r_hit);
 int64_t select_granules(int64_t r_hit);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
@@ -319,9 +330,12 @@ struct InterpFuse {
     uint8_t *row_flags;  // or null: every embedding row the scatter touches is flagged (sparse-exact Adam)
 };
 
-// d_o / d_d of every hit ray from the samples' dL/dx (InterpFuse::gx)
+// d_o / d_d of every hit ray from the samples' dL/dx (InterpFuse::gx);
+// offsets2 / t2 / gx2 (or null): a second segment of each ray (the sparse
+// decoder's class B), summed after the first
 int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int *ray_index, const float *t,
-                   const float *gx, float *grad_o, float *grad_d);
+                   const float *gx, float *grad_o, float *grad_d, const int *offsets2 = nullptr,
+                   const float *t2 = nullptr, const float *gx2 = nullptr);
 
 // psvo_mlp_bwd that records `dfeat_ready` (if not null) on the stream once
 // dfeat is written, before the weight-gradient kernels are queued; with `ip`
@@ -329,13 +343,22 @@ int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int 
 // dfeat is not stored.  m_dev (width 128; the sparse decoder): the sample
 // count is read on the device (select_samples' counts[0] <= m; the buffers
 // are sized for m).
+// the sparse decoder's class B (k_mlp_bwd3t after k_mlp_bwd3, width 128):
+// its count on the device, the forward's masks / activations (h1, h2:
+// mlp_fwd_trunk), dL/dsdf, the features and the fused interpolation backward
+struct TrunkBwd {
+    const int *m_dev;
+    const uint64_t *masks;
+    const float *g_sdf, *feat, *act;
+    const InterpFuse *ip;
+};
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
             const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
             const float *b5, const float *images, const float *rgb, const float *act, const uint64_t *masks,
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr,
-            hipStream_t reduce_stream = nullptr, const int *m_dev = nullptr);
+            hipStream_t reduce_stream = nullptr, const int *m_dev = nullptr, const TrunkBwd *tb = nullptr);
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
 // the look-ahead's split tail (psvo_map_step_frames): the weight-gradient
@@ -349,6 +372,11 @@ bool mlp_bwd_split_tail(int width);
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images);
+// the sparse decoder's class B forward (k_mlp_trunk2, width 128): h1 / h2 CF
+// tiles into act (buffers for m_cap samples), the masks, zero colours; the
+// class count read on the device
+int mlp_fwd_trunk(hipStream_t st, int64_t m_cap, const int *m_dev, const float *feat, const float *images, float *act,
+                  uint64_t *masks, float *rgb);
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,

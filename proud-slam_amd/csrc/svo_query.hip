@@ -1052,7 +1052,8 @@ struct FusedRows {
         return hit_idx[at(e)];
     }
     __device__ int idx_slot0(int col) const {
-        if (slot0) return slot0[(int64_t)slot0_row * kMaxHits + col];
+        // the slot-0 row's valid hits are its prefix [0, nv): only "== -1" is asked
+        if (slot0) return col < slot0[slot0_row] ? 0 : -1;
         return hit_idx[(int64_t)rank_ray[real(base_row)] * kMaxHits + col];
     }
     __device__ float lo_at(int e) const { return hit_t0[at(e)]; }
@@ -1075,9 +1076,10 @@ struct FusedRows {
     }
     // data-parallel engine: this rank holds only the logical rows
     // [row_begin, row_end) (rank_ray / hit_* are local); the sampler reads
-    // other rows only as slot 0's voxel ids (the exchanged slot-0 table) and
-    // as the first voxel id of the row after its own (next_col0)
-    const int *slot0 = nullptr;  // [200 · nch][kMaxHits]
+    // other rows only as slot 0's hit counts (the slot-0 table, built from
+    // the exchanged counts) and as the first voxel id of the row after its
+    // own (next_col0)
+    const int *slot0 = nullptr;  // [200 · nch] valid hits of each launch chunk's slot-0 row
     int slot0_row = 0;           // table row of (block, chunk)
     int row_begin = 0, row_end = 0, next_col0 = -1;
 };
@@ -1807,81 +1809,106 @@ __global__ __launch_bounds__(256) void k_compact_rays(int64_t r_hit, int cap, co
 // Data-parallel query (engine.cpp): each rank samples
 // its own hit rays inside the [200, K', P] layout of the union batch (ranks
 // in order).  Besides P / R_hit / max ceil(steps) of the union, the sampler
-// reads other ranks' rows in two places only (sample_gpu.cu:224-237): the
-// voxel ids of each launch block's slot-0 row (idx_slot0) and the first voxel
-// id of the row after a ray's own (a ray with exactly P bins).  So a rank
-// exchanges 8 words (all-gather), then a [200 · nch, 50] slot-0 table
-// (all-reduce sum: each row is written by its owner, zeros elsewhere) — not
-// its hit lists.
+// reads other ranks' rows in two places only (sample_gpu.cu:224-237): whether
+// column k of each launch chunk's slot-0 row is a hit (idx_slot0(k) == -1 —
+// a row's hits are its prefix, so that is k < the row's hit count) and the
+// first voxel id of the row after a ray's own (a ray with exactly P bins).
+// So ONE all-gather carries everything: per rank 8 words and the hit count
+// of each of its hit rows (a byte each, rank order) — every rank then builds
+// the union layout and the [200 · nch] slot-0 count table itself.
 constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id of its first hit row, flags
 
-__global__ void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
-                            const int *__restrict__ hit_idx, int *__restrict__ out) {
-    if (threadIdx.x != 0) return;
+// this rank's words: thread t packs the hit counts of its hit rows 4t..4t+3
+__global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
+                                                   const int *__restrict__ hit_idx, const int *__restrict__ ray_nv,
+                                                   int *__restrict__ out) {
     const int r_hit = stats[PSVO_STAT_R_HIT];
-    out[0] = r_hit;
-    out[1] = stats[PSVO_STAT_P];
-    out[2] = stats[PSVO_STAT_MAX_CEIL];
-    out[3] = r_hit > 0 ? hit_idx[(int64_t)rank_ray[0] * kMaxHits] : -1;
-    out[4] = stats[PSVO_STAT_FLAGS];  // e.g. a DFS-stack overflow on one rank: every rank fails together
-    for (int k = 5; k < kDistWords; ++k) out[k] = 0;
-}
-
-// union-batch statistics from the gathered words (world x kDistWords)
-__global__ void k_dist_layout(const int *__restrict__ all, int world, int rank, int *__restrict__ stats) {
-    if (threadIdx.x != 0) return;
-    int r_hit = 0, p = 0, mc = 0, begin = 0, flags = 0;
-    for (int r = 0; r < world; ++r) {
-        const int *w = all + r * kDistWords;
-        if (r < rank) begin += w[0];
-        r_hit += w[0];
-        p = max(p, w[1]);
-        mc = max(mc, w[2]);
-        flags |= w[4];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        out[0] = r_hit;
+        out[1] = stats[PSVO_STAT_P];
+        out[2] = stats[PSVO_STAT_MAX_CEIL];
+        out[3] = r_hit > 0 ? hit_idx[(int64_t)rank_ray[0] * kMaxHits] : -1;
+        out[4] = stats[PSVO_STAT_FLAGS];  // e.g. a DFS-stack overflow on one rank: every rank fails together
+        for (int k = 5; k < kDistWords; ++k) out[k] = 0;
     }
-    // the logical row after this rank's last: the next rank holding hit rows,
-    // or (past the union's last row) row 0, as the reference's row-0 padding
-    int next = -1;
-    for (int r = rank + 1; r < world && next < 0; ++r)
-        if (all[r * kDistWords] > 0) next = r;
-    for (int r = 0; r < world && next < 0; ++r)
-        if (all[r * kDistWords] > 0) next = r;
-    stats[PSVO_STAT_R_HIT_LOCAL] = all[rank * kDistWords];
-    stats[PSVO_STAT_ROW_BEGIN] = begin;
-    stats[PSVO_STAT_NEXT_COL0] = next >= 0 ? all[next * kDistWords + 3] : -1;
-    stats[PSVO_STAT_P] = p;
-    stats[PSVO_STAT_R_HIT] = r_hit;
-    stats[PSVO_STAT_MAX_CEIL] = mc;
-    stats[PSVO_STAT_FLAGS] |= flags;
+    const int j0 = 4 * t;
+    if (j0 >= r_hit) return;
+    uint32_t w = 0;
+    for (int k = 0; k < 4 && j0 + k < r_hit; ++k) w |= (uint32_t)ray_nv[rank_ray[j0 + k]] << (8 * k);  // nv <= 50
+    out[kDistWords + t] = (int)w;
 }
 
-// table row (b, c) = the voxel ids of logical row b·K' + c·800 (row 0 past the
-// union's end) if this rank holds it, else zeros
-__global__ void k_dist_slot0(const int *__restrict__ stats, const int *__restrict__ rank_ray,
-                             const int *__restrict__ hit_idx, int nch, int *__restrict__ table) {
-    const int r_hit = stats[PSVO_STAT_R_HIT];
-    const int begin = stats[PSVO_STAT_ROW_BEGIN];
-    const int n_loc = stats[PSVO_STAT_R_HIT_LOCAL];
+// union-batch statistics and the slot-0 count table from the gathered words
+// (world x stride): table[b · nch + c] = hit count of logical row b·K' + c·800
+// (row 0 past the union's end)
+__global__ __launch_bounds__(256) void k_dist_layout(const int *__restrict__ all, int world, int rank, int stride,
+                                                     int nch, int *__restrict__ stats, int *__restrict__ table) {
+    int r_hit = 0;
+    for (int r = 0; r < world; ++r) r_hit += all[r * stride];
+    if (threadIdx.x == 0) {
+        int p = 0, mc = 0, begin = 0, flags = 0;
+        for (int r = 0; r < world; ++r) {
+            const int *w = all + r * stride;
+            if (r < rank) begin += w[0];
+            p = max(p, w[1]);
+            mc = max(mc, w[2]);
+            flags |= w[4];
+        }
+        // the logical row after this rank's last: the next rank holding hit rows,
+        // or (past the union's last row) row 0, as the reference's row-0 padding
+        int next = -1;
+        for (int r = rank + 1; r < world && next < 0; ++r)
+            if (all[r * stride] > 0) next = r;
+        for (int r = 0; r < world && next < 0; ++r)
+            if (all[r * stride] > 0) next = r;
+        stats[PSVO_STAT_R_HIT_LOCAL] = all[rank * stride];
+        stats[PSVO_STAT_ROW_BEGIN] = begin;
+        stats[PSVO_STAT_NEXT_COL0] = next >= 0 ? all[next * stride + 3] : -1;
+        stats[PSVO_STAT_P] = p;
+        stats[PSVO_STAT_R_HIT] = r_hit;
+        stats[PSVO_STAT_MAX_CEIL] = mc;
+        stats[PSVO_STAT_FLAGS] |= flags;
+    }
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
-    const int row = blockIdx.x;  // b * nch + c
-    const int b = row / nch, c = row - b * nch;
-    int lrow = b * kp + c * kSamplerChunk;
-    if (lrow >= r_hit) lrow = 0;
-    const bool mine = lrow >= begin && lrow < begin + n_loc;
-    for (int col = threadIdx.x; col < kMaxHits; col += blockDim.x)
-        table[(int64_t)row * kMaxHits + col] = mine ? hit_idx[(int64_t)rank_ray[lrow - begin] * kMaxHits + col] : 0;
+    for (int row = threadIdx.x; row < kSamplerG * nch; row += blockDim.x) {
+        const int b = row / nch, c = row - b * nch;
+        int lrow = b * kp + c * kSamplerChunk;
+        if (lrow >= r_hit) lrow = 0;
+        int nv = 0;
+        if (r_hit > 0) {
+            int o = 0, beg = 0;
+            while (lrow >= beg + all[o * stride]) beg += all[o++ * stride];  // the owner: lrow < r_hit
+            const int j = lrow - beg;
+            nv = (int)(((uint32_t)all[o * stride + kDistWords + (j >> 2)] >> (8 * (j & 3))) & 0xffu);
+        }
+        table[row] = nv;
+    }
 }
 
-__global__ void k_dist_pack_smax(const int *__restrict__ stats, int *__restrict__ out) {
-    if (threadIdx.x == 0) out[0] = stats[PSVO_STAT_S_MAX];
-}
-
-__global__ void k_dist_smax(const int *__restrict__ all, int world, int *__restrict__ stats) {
+// after the gather of [S_max, count words] (world x 8): the union S_max and,
+// given the rank's counts (dist_counts), the union's normaliser sums —
+// integers, so any summation order gives the single-GPU doubles; zeroes the
+// rank's count words for the next query's atomics
+__global__ void k_dist_smax(const int *__restrict__ all, int world, int *__restrict__ stats, int *__restrict__ in,
+                            double *__restrict__ sums) {
     if (threadIdx.x != 0) return;
     int mx = 0;
-    for (int r = 0; r < world; ++r) mx = max(mx, all[r]);
+    for (int r = 0; r < world; ++r) mx = max(mx, all[r * kDistWords]);
     stats[PSVO_STAT_S_MAX_LOCAL] = stats[PSVO_STAT_S_MAX];
     stats[PSVO_STAT_S_MAX] = mx;
+    if (sums) {
+        long long c[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (int r = 0; r < world; ++r)
+            for (int k = 0; k < 7; ++k) c[k] += all[r * kDistWords + 1 + k];
+        // words: n_valid, Σ front, Σ sdf band (valid samples), rays whose padding is front,
+        // Σ their ns, rays whose padding is in the band, Σ their ns (dist_counts)
+        for (int k = 0; k < 8; ++k) sums[k] = 0.0;
+        sums[2] = (double)c[0];                       // kNValid
+        sums[3] = (double)(c[1] + mx * c[3] - c[4]);  // kNFront: + (S_max − ns) per padded-front ray
+        sums[4] = (double)(c[2] + mx * c[5] - c[6]);  // kNSdf
+    }
+    for (int k = 1; k < kDistWords; ++k) in[k] = 0;
 }
 
 }  // namespace
@@ -2038,14 +2065,15 @@ int dist_slot0_rows(int64_t max_rays_global) {
     const int64_t kp = (max_rays_global + kSamplerG - 1) / kSamplerG;
     return kSamplerG * (int)((kp + kSamplerChunk - 1) / kSamplerChunk);
 }
-int dist_pack(hipStream_t st, const int *stats, const int *rank_ray, const int *hit_idx, int *out) {
-    psvo::launch(k_dist_pack, dim3(1), dim3(64), 0, st, stats, rank_ray, hit_idx, out);
+int dist_count_words(int max_rays_rank) { return kDistWords + (max_rays_rank + 3) / 4; }
+int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
+              const int *ray_nv, int *out) {
+    psvo::launch(k_dist_pack, dim3((int)div_up(div_up(R, 4), 256) + (R == 0)), dim3(256), 0, st, stats, rank_ray,
+                 hit_idx, ray_nv, out);
     return check_launch("dist_pack");
 }
-int dist_layout(hipStream_t st, const int *all, int world, int rank, int *stats, const int *rank_ray,
-                const int *hit_idx, int nch, int *table) {
-    psvo::launch(k_dist_layout, dim3(1), dim3(64), 0, st, all, world, rank, stats);
-    psvo::launch(k_dist_slot0, dim3(kSamplerG * nch), dim3(64), 0, st, stats, rank_ray, hit_idx, nch, table);
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table) {
+    psvo::launch(k_dist_layout, dim3(1), dim3(256), 0, st, all, world, rank, stride, nch, stats, table);
     return check_launch("dist_layout");
 }
 // the fused sampler + scan over this rank's rows (stats from dist_layout)
@@ -2061,12 +2089,8 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                        nullptr, 0, SampleCounts{});
     return check_launch("dist_sample");
 }
-int dist_pack_smax(hipStream_t st, const int *stats, int *out) {
-    psvo::launch(k_dist_pack_smax, dim3(1), dim3(64), 0, st, stats, out);
-    return check_launch("dist_pack_smax");
-}
-int dist_smax(hipStream_t st, const int *all, int world, int *stats) {
-    psvo::launch(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats);
+int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, double *sums) {
+    psvo::launch(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats, in, sums);
     return check_launch("dist_smax");
 }
 }  // namespace psvo

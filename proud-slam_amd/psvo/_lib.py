@@ -79,8 +79,8 @@ _SIGNATURES = {
     "psvo_engine_select_stats": (_i32, [_vp, _vp, _vp, _i32]),
     "psvo_engine_queued": (_i32, [_vp]),
     "psvo_map_discard": (_i32, [_vp]),
-    "psvo_engine_exchange_words": (_i64, [_i32, _i64]),
-    "psvo_engine_set_exchange": (_i32, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
+    "psvo_engine_exchange_words": (_i64, [_i32, _i64, _i64]),
+    "psvo_engine_set_exchange": (_i32, [_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp, _vp]),
     "psvo_engine_timing": (_i32, [_vp, _vp]),
     "psvo_engine_set_clock": (_i32, [_vp, _i32]),
     "psvo_engine_clock": (_i32, [_vp, _vp, _vp]),

@@ -325,10 +325,13 @@ class EngineExchange:
     """The collectives of the data-parallel native engine (psvo_engine_set_exchange,
     include/psvo.h): the engine computes the loss of the UNION of all ranks'
     rays — bit-identical sample layout and normalisers to one GPU rendering the
-    concatenated batch — and calls back here for four small collectives per
-    step (8 + 1 words all-gathered and a 40-KB slot-0 table summed in the
-    query phase, 16 doubles summed in the step), each on the HIP stream the
-    engine produced the operand on.
+    concatenated batch — and calls back here for its collectives, each on the
+    HIP stream the engine produced the operand on: two all-gathers in the
+    query phase (8 words + a hit-count byte per ray of the shard; S_max + the
+    loss normalisers' counts), plus 8 doubles summed in the step when the
+    query could not count the normalisers or the loss value is wanted.
+    max_rays_rank: the largest shard a rank passes (default: the union's
+    max_rays_global) — it sizes the first all-gather.
 
     With RCCL ("nccl") the query-phase collectives run on their own
     communicator (they are issued one step ahead, concurrently with the
@@ -336,7 +339,7 @@ class EngineExchange:
     stream; with gloo (CPU rehearsal / tests) operands are staged through the
     host.  `apply` is the whole protocol and works on CPU tensors too."""
 
-    def __init__(self, max_rays_global, device=None, group=None, query_group=None, force=False):
+    def __init__(self, max_rays_global, device=None, group=None, query_group=None, force=False, max_rays_rank=None):
         # force: run every collective even on one rank (identities) — the
         # engine's data-parallel protocol end to end on a 1-rank communicator
         # (tests/test_gpu_rccl.py drives the RCCL branch this way)
@@ -347,6 +350,7 @@ class EngineExchange:
         self.world = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
         self.max_rays_global = int(max_rays_global)
+        self.max_rays_rank = int(max_rays_rank) if max_rays_rank is not None else self.max_rays_global
         self.group = group
         self.nccl = (self.world > 1 or self.force) and on and _backend(group) == "nccl"
         if query_group is None and self.nccl:

@@ -285,12 +285,15 @@ class MappingEngine:
         """Data-parallel mode (psvo.dist.EngineExchange): every step computes
         the loss of the union of all ranks' rays; sum grad_flat over ranks
         (psvo.dist.EngineGradExchange(op="sum")) before adam()."""
-        n = int(_lib().psvo_engine_exchange_words(exchange.world, exchange.max_rays_global))
+        n = int(_lib().psvo_engine_exchange_words(exchange.world, exchange.max_rays_global, exchange.max_rays_rank))
+        if n < 0:
+            raise ValueError(f"EngineExchange: bad sizes (max_rays_global {exchange.max_rays_global}, "
+                             f"max_rays_rank {exchange.max_rays_rank})")
         xi32, xf64 = exchange.buffers(n)
         if xi32.device != self.emb.device:
             raise RuntimeError("EngineExchange buffers must live on the engine's device")
         L.call("psvo_engine_set_exchange", self.handle, exchange.rank, exchange.world, exchange.max_rays_global,
-               ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
+               exchange.max_rays_rank, ctypes.cast(exchange.callback(), _vp), None, xi32, xf64)
         self.exchange = exchange
         if self.row_flags is not None and self.row_local is None:
             # sparse-exact Adam under data parallelism: the step marks this

@@ -27,4 +27,19 @@ if [ "${PROFILE:-0}" = "1" ]; then
   for it in 8 12; do python3 scripts/ba_timeline.py gpurun_out/${R}_prof/run_kernel_trace.csv $it > gpurun_out/${R}_ba_timeline_$it.txt 2>&1 || true; done
   rm -f gpurun_out/${R}_prof/run_kernel_trace.csv.bak
 fi
+if [ "${CONFIGS:-0}" = "1" ]; then  # C: ScanNet W=256 8x1024; E: multiroom W=256
+  timeout -k 10 400 python bench.py --scene scannet0000 --steps 20 --warmup 5 --no-cpu-baseline --no-traffic \
+      > gpurun_out/${R}_bench_C.json 2> gpurun_out/${R}_bench_C.err
+  rc=$?; echo "C rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  timeout -k 10 500 python bench.py --scene multiroom --steps 20 --warmup 5 --no-cpu-baseline --no-traffic \
+      > gpurun_out/${R}_bench_E.json 2> gpurun_out/${R}_bench_E.err
+  rc=$?; echo "E rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  python3 - gpurun_out/${R}_bench_C.json gpurun_out/${R}_bench_E.json <<'PY'
+import json, sys
+for f in sys.argv[1:]:
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f, round(d["value"]), d["ms_per_step"], d["gpu_ms_per_step"], d["config"].get("decoder_kept_fraction"),
+          d["roofline_mfma"]["fwd_ms"], d["roofline_mfma"]["bwd_ms"])
+PY
+fi
 echo done

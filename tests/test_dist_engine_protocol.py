@@ -2,11 +2,12 @@
 psvo_engine_set_exchange; csrc/svo_query.hip k_dist_*).
 
 1. Sufficiency: a rank samples its rows of the union batch's [200, K', P]
-   layout from its own hit lists plus (a) the slot-0 rows' voxel ids and (b)
-   the first voxel id of the row after its last — nothing else of other
+   layout from its own hit lists plus (a) the slot-0 rows' hit COUNTS (their
+   voxel ids are read only as "== -1", and a row's hits are its prefix) and
+   (b) the first voxel id of the row after its last — nothing else of other
    ranks' rows.  Checked with the oracle sampler (sample_gpu.cu:133-239
-   restated): poisoning every other row except (a) and (b) leaves the
-   shard's samples bit-identical.
+   restated): poisoning every other row — slot-0 rows down to junk ids over
+   their hit prefix — except (b) leaves the shard's samples bit-identical.
 2. psvo.dist.EngineExchange.apply over gloo, world size 2: all-gather and
    in-place sums on the exchange buffers, as the engine calls them."""
 import os
@@ -77,19 +78,24 @@ def test_slot0_table_and_next_col0_suffice(n, cuts, step):
     want = _sample(idx, lo, hi, step, noise)
     slot0_rows = {b * kp for b in range(G)}  # chunk 0 only: kp < 800
     for a, b in zip(cuts[:-1], cuts[1:]):
-        # this rank's view: its rows, the slot-0 voxel ids (k_dist_slot0),
-        # the next row's first voxel id (k_dist_layout's next_col0); all else junk
+        # this rank's view: its rows, the slot-0 rows' hit counts (k_dist_layout's
+        # table), the next row's first voxel id (next_col0); all else junk
         pi, pl, ph = idx.copy(), lo.copy(), hi.copy()
         other = np.ones(H, bool)
         other[a:b] = False
         junk = np.where(rng.random((H, p)) < 0.5, -1, rng.integers(0, 5000, size=(H, p))).astype(np.int32)
         jl = rng.uniform(0, 3, size=(H, p)).astype(np.float32)
         keep_idx = np.zeros((H, p), bool)
-        for r in slot0_rows:
-            keep_idx[r] = True
         keep_idx[b if b < H else 0, 0] = True
         sel = other[:, None] & ~keep_idx
         pi[sel] = junk[sel]
+        for r in slot0_rows:  # only the count survives: other junk ids over the hit prefix, -1 after
+            if other[r]:
+                nv = int((idx[r] != -1).sum())
+                pi[r] = -1
+                pi[r, :nv] = rng.integers(0, 5000, size=nv) + 7
+                if keep_idx[r, 0]:  # also the row after the shard: its first id (next_col0)
+                    pi[r, 0] = idx[r, 0]
         pl[other] = jl[other]
         ph[other] = jl[other] + 0.05
         got = _sample(pi, pl, ph, step, noise)

@@ -5,17 +5,21 @@ protocol the engine runs (include/psvo.h psvo_engine_set_exchange,
 csrc/engine.cpp query_enqueue / map_step_impl) through
 psvo.dist.EngineExchange.apply on the engine's exchange-buffer layout:
 
-  1. the 8 statistics words all-gathered (k_dist_pack, restated below);
-  2. the union layout (k_dist_layout: P, R_hit, max ⌈Σ/step⌉, the rank's first
-     row, the first voxel id of the row after its last) and the [200·nch, 50]
-     slot-0 table summed (k_dist_slot0);
+  1. ONE all-gather of the 8 statistics words + a hit-count byte per hit row
+     (k_dist_pack, restated below);
+  2. on every rank, the union layout (k_dist_layout: P, R_hit, max ⌈Σ/step⌉,
+     the rank's first row, the first voxel id of the row after its last) and
+     the [200·nch] slot-0 count table from the gathered bytes;
   3. each rank samples only its own rows of the union's [200, K', P] sampler
      layout (the oracle sampler, sample_gpu.cu:133-239), every other row of
-     its view poisoned except what the table and next_col0 give it;
-  4. S_max all-gathered (k_dist_pack_smax / k_dist_smax);
-  5. the Criterion's count and loss sums all-reduced (f64, criterion.py:70-101:
-     normalisers over the union's padded [R_hit, S_max] layout), and the
-     decoder-stand-in's gradients summed over ranks.
+     its view poisoned — slot-0 rows keep only their hit count — and
+     next_col0;
+  4. ONE all-gather of [S_max, 7 count words] (k_dist_counts / k_dist_smax):
+     the union S_max and the Criterion's normaliser counts over the union's
+     padded [R_hit, S_max] layout (criterion.py:70-101), the padding applied
+     after the gather;
+  5. the loss sums all-reduced (f64), and the decoder-stand-in's gradients
+     summed over ranks.
 
 Against one process on the concatenated batch: the same P, R_hit, S_max, M,
 every rank's sample ids / depths bit-identical to its rows of the single
@@ -123,16 +127,25 @@ def _render_loss(model, s_idx, s_dep, gt_rgb, gt_d, s_cols):
                             torch.from_numpy(gt_d).double(), TR, MAX_D, pad_extra=s_cols - s_loc)
 
 
-def _layout(world, n_rays):
+def _layout(world, n_rays, n_rank=None):
     """EngineExchange's int32 word offsets (csrc/engine.cpp struct EngineExchange)."""
-    w8 = 8
-    smax_in = w8 + world * w8
-    smax_all = smax_in + 8
-    table_off = (smax_all + world + 63) // 64 * 64
+    cw = 8 + ((n_rank if n_rank else n_rays) + 3) // 4  # 8 words + a hit-count byte per ray of the shard
+    q2_in = cw + world * cw
+    q2_all = q2_in + 8
+    table_off = (q2_all + world * 8 + 63) // 64 * 64
     kp = (n_rays + G - 1) // G
     nch = (kp + 799) // 800
-    return dict(all=w8, smax_in=smax_in, smax_all=smax_all, table=table_off, nch=nch,
-                words=table_off + G * nch * 50)
+    return dict(cw=cw, all=cw, q2_in=q2_in, q2_all=q2_all, table=table_off, nch=nch, words=table_off + G * nch)
+
+
+def _pad_terms(d):
+    """Per ray: does the MAX_DEPTH padding (z = 10) count as front / as in the
+    sdf band (criterion.py:78-88 on the padded columns)."""
+    zp = 10.0
+    fp = zp < d - TR
+    bp = zp > d + TR
+    smp = ~fp & ~bp & (d > 0.0) & (d < MAX_D)
+    return fp, smp
 
 
 def _single():
@@ -155,22 +168,32 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from psvo.dist import XCH_GATHER_I32, XCH_QUERY, XCH_SUM_F64, XCH_SUM_I32, EngineExchange, GradBucket
+        from psvo.dist import XCH_GATHER_I32, XCH_QUERY, XCH_SUM_F64, EngineExchange, GradBucket
         idx, lo, hi, noise, gt_rgb, gt_d = _batch()
         a, b = CUTS[rank], CUTS[rank + 1]
         n_loc = b - a
         lay = _layout(world, N_RAYS)
         x = EngineExchange(max_rays_global=N_RAYS)
         xi, xf = x.buffers(lay["words"])
-        # 1. this rank's 8 words (k_dist_pack): R_hit, P, max ceil, first voxel id of its first row, flags
+        assert x.max_rays_rank == N_RAYS
+        # 1. this rank's words (k_dist_pack): R_hit, P, max ceil, first voxel id of its first row, flags,
+        #    then a byte per hit row: its hit count — ONE all-gather
         d_loc = np.where(idx[a:b] >= 0, hi[a:b] - lo[a:b], 0).astype(np.float32)
-        p_loc = int((idx[a:b] != -1).sum(1).max()) if n_loc else 0
+        nv_loc = (idx[a:b] != -1).sum(1).astype(np.uint32)
+        p_loc = int(nv_loc.max()) if n_loc else 0
         mc_loc = int(np.ceil(_row_sums(d_loc) / np.float32(STEP)).max()) if n_loc else 0
+        cw = lay["cw"]
         xi[0:8] = torch.tensor([n_loc, p_loc, mc_loc, int(idx[a, 0]) if n_loc else -1, 0, 0, 0, 0],
                                dtype=torch.int32)
-        x.apply(XCH_GATHER_I32 | XCH_QUERY, 0, lay["all"], 8)
-        words = xi[lay["all"]:lay["all"] + 8 * world].view(world, 8).numpy()
-        # 2. union layout (k_dist_layout)
+        packed = np.zeros(4 * (cw - 8), np.uint32)
+        packed[:n_loc] = nv_loc
+        packed = packed.reshape(-1, 4)
+        words_nv = packed[:, 0] | (packed[:, 1] << 8) | (packed[:, 2] << 16) | (packed[:, 3] << 24)
+        xi[8:cw] = torch.from_numpy(words_nv.view(np.int32))
+        x.apply(XCH_GATHER_I32 | XCH_QUERY, 0, lay["all"], cw)
+        gathered = xi[lay["all"]:lay["all"] + cw * world].view(world, cw).numpy()
+        words = gathered[:, :8]
+        # 2. union layout (k_dist_layout), on every rank from the gathered words alone
         r_hit = int(words[:, 0].sum())
         p_all = int(words[:, 1].max())
         mc_all = int(words[:, 2].max())
@@ -178,18 +201,20 @@ def _worker(rank, world, port, q):
         order = [r for r in range(rank + 1, world) if words[r, 0] > 0] + [r for r in range(world) if words[r, 0] > 0]
         next_col0 = int(words[order[0], 3]) if order else -1
         assert begin == a
-        #    the slot-0 table (k_dist_slot0): row (blk, c) = ids of logical row blk·K' + c·800 if this rank holds it
+        #    the slot-0 count table: row (blk, c) = hit count of logical row blk·K' + c·800 (its owner's byte)
         kp = (r_hit + G - 1) // G
         nch = lay["nch"]
-        table = xi[lay["table"]:lay["words"]].view(G * nch, 50)
-        table.zero_()
+        begins = np.concatenate([[0], np.cumsum(words[:, 0])])
+        nv_bytes = gathered[:, 8:].view(np.uint32)
+        table = np.zeros(G * nch, np.int64)
         for blk in range(G):
             for c in range(nch):
                 lrow = blk * kp + c * 800
                 lrow = lrow if lrow < r_hit else 0
-                if a <= lrow < b:
-                    table[blk * nch + c, :P] = torch.from_numpy(idx[lrow])
-        x.apply(XCH_SUM_I32 | XCH_QUERY, lay["table"], lay["table"], G * nch * 50)
+                o = int(np.searchsorted(begins, lrow, side="right") - 1)
+                j = lrow - int(begins[o])
+                table[blk * nch + c] = (int(nv_bytes[o, j >> 2]) >> (8 * (j & 3))) & 0xFF
+                assert table[blk * nch + c] == int((idx[lrow] != -1).sum())
         # 3. sample this rank's rows from its own hits + the table + next_col0; everything else poisoned
         rng = np.random.default_rng(77 + rank)
         v_idx = rng.integers(0, 5000, size=idx.shape).astype(np.int32)
@@ -200,8 +225,10 @@ def _worker(rank, world, port, q):
         for blk in range(G):
             for c in range(nch):
                 lrow = blk * kp + c * 800
-                if lrow < r_hit and not (a <= lrow < b):
-                    v_idx[lrow] = table[blk * nch + c, :P].numpy()
+                if lrow < r_hit and not (a <= lrow < b):  # only the hit count survives: junk ids, then -1
+                    nv = int(table[blk * nch + c])
+                    v_idx[lrow] = -1
+                    v_idx[lrow, :nv] = rng.integers(0, 5000, size=nv)
         if n_loc and b < r_hit:
             v_idx[b, 0] = next_col0
         elif n_loc:  # past the union's last row: the reference pads with copies of row 0
@@ -210,18 +237,29 @@ def _worker(rank, world, port, q):
         s_idx, s_dep = s_idx[a:b], s_dep[a:b]
         ns = (s_idx != -1).sum(1)
         s_loc = int(ns.max()) if n_loc else 0
-        # 4. S_max of the union (k_dist_pack_smax / k_dist_smax)
-        xi[lay["smax_in"]] = s_loc
-        x.apply(XCH_GATHER_I32 | XCH_QUERY, lay["smax_in"], lay["smax_all"], 1)
-        s_max = int(xi[lay["smax_all"]:lay["smax_all"] + world].max())
-        # 5. counts and loss sums all-reduced (f64), the loss of the union; gradients summed over ranks
+        # 4. [S_max, counts] — ONE all-gather (k_dist_counts / k_dist_smax): the valid samples' counts and,
+        #    per padding class, the rays and their Σ ns; the union S_max applied to the padding afterwards
+        d = gt_d[a:b].astype(np.float64)
+        valid_s = s_idx != -1
+        z = s_dep.astype(np.float64)
+        front = valid_s & (z < (d - TR)[:, None])
+        back = valid_s & (z > (d + TR)[:, None])
+        band = valid_s & ~front & ~back & ((d > 0.0) & (d < MAX_D))[:, None]
+        fp, smp = _pad_terms(d)
+        xi[lay["q2_in"]:lay["q2_in"] + 8] = torch.tensor(
+            [s_loc, int(((d > 0.01) & (d < MAX_D)).sum()), int(front.sum()), int(band.sum()), int(fp.sum()),
+             int(ns[fp].sum()), int(smp.sum()), int(ns[smp].sum())], dtype=torch.int32)
+        x.apply(XCH_GATHER_I32 | XCH_QUERY, lay["q2_in"], lay["q2_all"], 8)
+        g2 = xi[lay["q2_all"]:lay["q2_all"] + 8 * world].view(world, 8).numpy().astype(np.int64)
+        s_max = int(g2[:, 0].max())
+        c = g2[:, 1:].sum(0)
+        counts = (float(c[0]), float(c[1] + s_max * c[3] - c[4]), float(c[2] + s_max * c[5] - c[6]))
+        # 5. loss sums all-reduced (f64), the loss of the union; gradients summed over ranks
         model = _model()
         sums = _render_loss(model, s_idx[:, :s_loc], s_dep[:, :s_loc], gt_rgb[a:b], gt_d[a:b], s_max)
-        xf[0:8] = sums.detach()  # the engine's count half (k_crit_counts' sums) at offset 0 ...
-        x.apply(XCH_SUM_F64, 0, 0, 8)
-        xf[8:16] = sums.detach()  # ... and the loss half at offset 8
+        xf[8:16] = sums.detach()  # the engine's loss half at offset 8
         x.apply(XCH_SUM_F64, 8, 8, 8)
-        assert torch.equal(xf[0:8], xf[8:16])
+        assert counts == tuple(float(v) for v in xf[10:13]), (counts, xf[10:13])  # n_valid, n_front, n_sdf
         sums_g = sums + (xf[8:16] - sums).detach()  # global values, local gradient paths
         loss, _ = O.criterion_from_sums(sums_g, r_hit, s_max, O.REPLICA_CRITERIA)
         loss.backward()
@@ -242,8 +280,10 @@ def _free_port():
 
 def test_layout_matches_engine_exchange_words():
     from psvo import _lib as L
-    for world, n in ((1, 4096), (2, 8192), (8, N_RAYS), (8, 32768), (8, 200 * 800 + 1)):
-        assert int(L.lib().psvo_engine_exchange_words(world, n)) == _layout(world, n)["words"]
+    for world, n, nr in ((1, 4096, 0), (2, 8192, 4096), (8, N_RAYS, 0), (8, 32768, 4096), (8, 200 * 800 + 1, 0),
+                         (3, 1400, 789)):
+        assert int(L.lib().psvo_engine_exchange_words(world, n, nr)) == _layout(world, n, nr)["words"]
+    assert int(L.lib().psvo_engine_exchange_words(2, 100, 101)) == -1  # a shard larger than the union
 
 
 def test_union_protocol_world8_equals_one_process():
