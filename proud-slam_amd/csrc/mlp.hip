@@ -489,32 +489,49 @@ struct DwDst {
 };
 
 // slabs_b (or null): k_mlp_bwd3t's slabs (the same layout), whose W1, W2, W3
-// row 0 and b3[0] elements are added (the rest of its slabs is not written)
-__global__ void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst dst, int accumulate,
-                                const float *__restrict__ slabs_b) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= dst.elem_begin[5]) return;
-    int L = 0;
-#pragma unroll
-    for (int l = 1; l < 5; ++l) L += (e >= dst.elem_begin[l]);
-    const int rel = e - dst.elem_begin[L];
-    const int n_split = g.n_split[L];
-    const float *p = slabs + g.slab_off[L] + rel;
-    const int64_t stride = g.slab_len[L];
+// row 0 and b3[0] elements are added (the rest of its slabs is not written).
+// A workgroup sums 64 elements: wave k over the k-th quarter of the slabs
+// (batches of 8 independent loads, lane = element: 256-B rows), then the
+// quarters in order — a fixed order, so deterministic.  (One thread per
+// element over all 2 × 256 slabs left ≈ 150 workgroups on 256 CUs, each
+// thread with up to 512 loads in flight one batch at a time: 132 µs.)
+constexpr int kDwRedEl = 64;
+__device__ __forceinline__ float dw_sum_range(const float *__restrict__ p, int64_t stride, int b, int e) {
     float v = 0.0f;
-    int sp = 0;
-    for (; sp + 8 <= n_split; sp += 8) {
+    int sp = b;
+    for (; sp + 8 <= e; sp += 8) {
         float q[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) q[u] = p[(sp + u) * stride];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v += q[u];
     }
-    for (; sp < n_split; ++sp) v += p[sp * stride];
-    if (slabs_b && (L < 2 || (L == 2 && (rel < 128 || rel == 129 * 128)))) {
-        const float *pb = slabs_b + g.slab_off[L] + rel;
-        for (int k = 0; k < n_split; ++k) v += pb[k * stride];
+    for (; sp < e; ++sp) v += p[sp * stride];
+    return v;
+}
+__global__ __launch_bounds__(256) void k_mlp_dw_reduce(DwGrid g, const float *__restrict__ slabs, DwDst dst,
+                                                       int accumulate, const float *__restrict__ slabs_b) {
+    __shared__ float part[4][kDwRedEl];
+    const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+    const int e = blockIdx.x * kDwRedEl + lane;
+    const bool in = e < dst.elem_begin[5];
+    int L = 0;
+#pragma unroll
+    for (int l = 1; l < 5; ++l) L += (e >= dst.elem_begin[l]);
+    const int rel = in ? e - dst.elem_begin[L] : 0;
+    const int n_split = g.n_split[L];
+    const int64_t stride = g.slab_len[L];
+    const int b = n_split * k / 4, en = n_split * (k + 1) / 4;
+    float v = 0.0f;
+    if (in) {
+        v = dw_sum_range(slabs + g.slab_off[L] + rel, stride, b, en);
+        if (slabs_b && (L < 2 || (L == 2 && (rel < 128 || rel == 129 * 128))))
+            v += dw_sum_range(slabs_b + g.slab_off[L] + rel, stride, b, en);
     }
+    part[k][lane] = v;
+    __syncthreads();
+    if (k != 0 || !in) return;
+    v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
     const int nw = dst.rows[L] * dst.cols[L];
     float *out = rel < nw ? dst.w[L] + rel : dst.b[L] + (rel - nw);
     *out = accumulate ? *out + v : v;
@@ -1982,7 +1999,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             e += kDwRows[l] * kDwCols[l] + kDwRows[l];
         }
         d.elem_begin[5] = e;
-        psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, 256)), dim3(256), 0, rs, g, slabs, d, accumulate,
+        psvo::launch(k_mlp_dw_reduce, dim3(div_up(e, kDwRedEl)), dim3(256), 0, rs, g, slabs, d, accumulate,
                      static_cast<const float *>(slabs_b));
         return check_launch("mlp_dw_reduce");
     };

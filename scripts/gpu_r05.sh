@@ -20,12 +20,13 @@ if [ "${BENCH:-1}" = "1" ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 if [ "${PROFILE:-0}" = "1" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${R}_prof -o run -- \
+  API=""; [ "${PROFILE_API:-0}" = "1" ] && API="--hip-runtime-trace"
+  timeout -k 10 400 rocprofv3 --kernel-trace ${API} --stats --output-format csv -d gpurun_out/${R}_prof -o run -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic ${BENCH_ARGS:-} \
       > gpurun_out/${R}_prof_bench.json 2> gpurun_out/${R}_prof.err
   rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
   for it in 8 12; do python3 scripts/ba_timeline.py gpurun_out/${R}_prof/run_kernel_trace.csv $it > gpurun_out/${R}_ba_timeline_$it.txt 2>&1 || true; done
-  rm -f gpurun_out/${R}_prof/run_kernel_trace.csv.bak
+  rm -f gpurun_out/${R}_prof/run_kernel_trace.csv.bak gpurun_out/${R}_prof/run_hip_api_trace.csv.bak
 fi
 if [ "${CONFIGS:-0}" = "1" ]; then  # C: ScanNet W=256 8x1024; E: multiroom W=256
   timeout -k 10 400 python bench.py --scene scannet0000 --steps 20 --warmup 5 --no-cpu-baseline --no-traffic \
