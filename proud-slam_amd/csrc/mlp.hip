@@ -1552,11 +1552,15 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
 // (the same per-sample dfeat bits), in two phases per round of four
 // 16-sample units:
 //   phase  chain wave c (unit u0 + 4r + c)                         gradient wave d
-//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2;    dW2 col block d += δh2(r−1) ⊗ h1(r−1)
+//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2;    (loads only: h1 / h2 tiles of round r)
 //          dW1 row block c += δh1(r−1) ⊗ x(r−1)
-//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          W3 row 0 (cols of block d) += dsdf(r) · h2(r)
-//          backward (dL/dx, the embedding scatter)
-// plus a last phase A for the final round's dW2 / dW1.  Writes one slab per
+//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          dW2 col block d += δh2(r) ⊗ h1(r);
+//          backward (dL/dx, the embedding scatter)                 W3 row 0 (cols of block d) += dsdf(r) · h2(r)
+// plus a last phase A for the final round's dW1.  A chain wave and a
+// gradient wave share each SIMD's matrix unit, so the two GEMMs of 128 × 128
+// (W2ᵀ, dW2) sit in different phases: the chain's (latency-bound)
+// interpolation backward overlaps the gradient MFMAs (measured with both in
+// phase A: 31 k cycles per round, the phase at 2 × 8 k MFMA cycles).  Writes one slab per
 // workgroup of W1 (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the
 // DwGrid layout; k_mlp_dw_reduce adds these elements only).  m: the class's
 // sample count on the device.
@@ -1611,6 +1615,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
     const int b = blockIdx.x;
     const int i = lane & 31, h = lane >> 5;
     const bool fuse = ip.gx != nullptr;  // uniform
+    [[maybe_unused]] constexpr int kStampK = 2;
+    PSVO_STAMP_DECL;
     if (wave < 4) {
         // ================= chain wave c
         const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
@@ -1624,17 +1630,40 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
             *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
         float b1p = 0.f;
         TrunkIn nin;
+        // the interpolation backward's sample data one round ahead (leaf, ray,
+        // t), its vertex ids / centre / rank row at the top of phase A: phase B
+        // then waits for one dependent level (the vertex rows, the ray) only
+        int lf_n = 0, ro_n = 0;
+        float ts_n = 0.f;
         {
             const int64_t u = u0 + c;
             const int64_t s = u * kU + n;
             load_trunk_in(masks, g_sdf, feat, s, u < u1 && s < m, q, nin);
+            if (fuse && u < u1 && s < m) {
+                lf_n = ip.leaf[s];
+                ro_n = ip.ray_of[s];
+                ts_n = ip.t[s];
+            }
         }
         for (int r = 0; r <= n_rounds; ++r) {
+            PSVO_STAMP(0);
             const int64_t ubase = u0 + 4 * (int64_t)r;
             const int64_t u = ubase + c;
             const bool active = r < n_rounds && u < u1;  // wave-uniform
             const int64_t s = u * kU + n;
             const bool valid = active && s < m;
+            const int lf = lf_n, ro = ro_n;
+            const float ts = ts_n;
+            int4 vid0 = make_int4(0, 0, 0, 0), vid1 = make_int4(0, 0, 0, 0);
+            float cen[3] = {0.f, 0.f, 0.f};
+            int row = 0;
+            if (fuse && valid) {
+                vid0 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8);
+                vid1 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8 + 4);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
+                row = ip.rank_ray[ro];
+            }
             // ---- A: δh2, dsdf, x → LDS; δh1 = W2ᵀ δh2 ⊙ m1; dW1 of the previous round
             f32x4v fa[8];
             uint64_t m1 = 0;
@@ -1661,43 +1690,37 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                     mask16(fb, m2);
                     lds_u_store<8>(h2set(r) + c * kUImg, wb, fb);
                     zero4(fa);
-                    gemm16<8, 4, 2>(wrs, kImgC2, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[0]), lane);
-                    gemm16<8, 4, 2>(wrs, kImgC2 + 4 * 8 * 256, fb, *reinterpret_cast<f32x4v(*)[4]>(&fa[4]), lane);
+                    gemm16<8, 8, 2>(wrs, kImgC2, fb, fa, lane);  // one ring over all 8 output blocks
                     mask16(fa, m1);  // δh1
                 }
             }
+            PSVO_STAMP(1);
             if (r > 0) xgrad16(h1set, xset(r - 1), c, ubase - 4, u1, lane, page1, &b1p);
-            // the interpolation backward's sample data, one dependent level per phase
-            int lf = 0, ro = 0;
-            float ts = 0.f;
-            if (fuse && valid) {
-                lf = ip.leaf[s];
-                ro = ip.ray_of[s];
-                ts = ip.t[s];
-            }
+            PSVO_STAMP(2);
             raw_barrier();
-            if (r == n_rounds) break;
+            PSVO_STAMP(3);
+            if (r == n_rounds) {
+                PSVO_STAMP_FLUSH(0);
+                break;
+            }
             // ---- B: δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation backward; the next unit's inputs
             if (active) lds_u_store<8>(h1set + c * kUImg, wb, fa);
-            int4 vid0 = make_int4(0, 0, 0, 0), vid1 = make_int4(0, 0, 0, 0);
-            float cen[3] = {0.f, 0.f, 0.f};
-            int row = 0;
-            if (fuse && valid) {
-                vid0 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8);
-                vid1 = *reinterpret_cast<const int4 *>(ip.vertex_idx + (int64_t)lf * 8 + 4);
-#pragma unroll
-                for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
-                row = ip.rank_ray[ro];
-            }
             if (r + 1 < n_rounds) {
                 const int64_t un = u + 4;
                 const int64_t snx = un * kU + n;
-                load_trunk_in(masks, g_sdf, feat, snx, un < u1 && snx < m, q, nin);
+                const bool vn = un < u1 && snx < m;
+                load_trunk_in(masks, g_sdf, feat, snx, vn, q, nin);
+                if (fuse && vn) {
+                    lf_n = ip.leaf[snx];
+                    ro_n = ip.ray_of[snx];
+                    ts_n = ip.t[snx];
+                }
             }
             if (active) {
                 f32x4v t1[1];
                 zero4(t1);
                 gemm16<8, 1, 4>(wrs, kImgC1, fa, t1, lane);
+                PSVO_STAMP(4);
                 const float4 gf = make_float4(t1[0][0], t1[0][1], t1[0][2], t1[0][3]);
                 if (fuse) {
                     float ro3[3] = {0.f, 0.f, 0.f}, rd3[3] = {0.f, 0.f, 0.f};
@@ -1714,6 +1737,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                     }
                     interp_bwd_unit(ip, lds + kT3I + c * 512, m, s, valid, n, q, ts, ro3, rd3, cen, vid0, vid1, ev,
                                     gf);
+                    PSVO_STAMP(5);
                     if (ip.grad_emb != nullptr) {
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging is this wave's own
                         __builtin_amdgcn_wave_barrier();
@@ -1722,7 +1746,10 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                     }
                 }
             }
+            PSVO_STAMP(6);
             raw_barrier();
+            PSVO_STAMP(7);
+            PSVO_STAMP_FLUSH(0);
         }
         // ---- slab: W1 row block c + b1
         float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
@@ -1743,30 +1770,43 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
         zero(acc2);
         float b2p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f;
         const __amdgpu_buffer_rsrc_t h1m = rsrc_of(act, tb), h2m = rsrc_of(act + tstride, tb);
-        float4 ring[3];
+        float4 ring[3], h2t[8];
         for (int r = 0; r <= n_rounds; ++r) {
+            PSVO_STAMP(0);
             const int64_t ubase = u0 + 4 * (int64_t)r;
-            // A: dW2 of the previous round (its δh2 set, h1 tiles)
-            if (r > 0) {
-                ring[0] = dw_bsrc(h1m, ubase - 4, u1, d, lane, 0);
-                ring[1] = dw_bsrc(h1m, ubase - 4, u1, d, lane, 1);
-                dw_job<0, 0>(ring, h2set(r - 1), nullptr, h1m, ubase - 4, true, h1m, ubase, false, u1, d, lane, acc2,
-                             b2p, unused0, unused1);
+            // A (the chain's GEMM phase): no MFMAs here — the SIMD's matrix
+            // unit is the chain wave's; this round's h1 / h2 tiles start loading
+            if (r < n_rounds) {
+#pragma unroll
+                for (int qq = 0; qq < 8; ++qq) h2t[qq] = dw_bsrc(h2m, ubase, u1, d, lane, qq);
+                ring[0] = dw_bsrc(h1m, ubase, u1, d, lane, 0);
+                ring[1] = dw_bsrc(h1m, ubase, u1, d, lane, 1);
             }
+            PSVO_STAMP(1);
             raw_barrier();
-            if (r == n_rounds) break;
-            // B: W3 row 0 += dsdf ⊙ h2 (this round's dsdf rows, h2 tiles)
+            PSVO_STAMP(3);
+            if (r == n_rounds) {
+                PSVO_STAMP_FLUSH(0);
+                break;
+            }
+            // B (beside the chain's interpolation backward): dW2 += δh2 ⊗ h1 of
+            // this round (its δh2 set from phase A), W3 row 0 += dsdf ⊙ h2
+            dw_job<0, 0>(ring, h2set(r), nullptr, h1m, ubase, true, h1m, ubase, false, u1, d, lane, acc2, b2p,
+                         unused0, unused1);
 #pragma unroll
             for (int qq = 0; qq < 8; ++qq) {
                 const int up = qq >> 1, gg = qq & 1;
                 if (ubase + up < u1) {  // wave-uniform
-                    const float4 bb = dw_bsrc(h2m, ubase, u1, d, lane, qq);
+                    const float4 bb = h2t[qq];
                     const float4 w = *reinterpret_cast<const float4 *>(sset + up * kU + 8 * h + 4 * gg);
                     r0 += (bb.x * w.x + bb.y * w.y) + (bb.z * w.z + bb.w * w.w);
                     b30 += (w.x + w.y) + (w.z + w.w);
                 }
             }
+            PSVO_STAMP(6);
             raw_barrier();
+            PSVO_STAMP(7);
+            PSVO_STAMP_FLUSH(0);
         }
         const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
         float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
