@@ -26,7 +26,7 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kDistSums, kQSlots };
+             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kDistSums, kMDev, kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -163,6 +163,7 @@ struct psvo_engine {
     bool images_next = false;
     const float *images_w0 = nullptr;
     int paths = 0;                  // PSVO_PATH_* (psvo_engine_set_paths)
+    int64_t m_early = 0;            // the device-sized forward's capacity (render): 1.25 × the largest M seen
     uint32_t sel_tag = 0;           // the sample selection's look-back descriptor tag
     const void *sel_zeroed = nullptr;  // its descriptor buffer, zeroed once at allocation
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
@@ -768,7 +769,7 @@ namespace {
 struct Render {
     int64_t r_hit = 0, m = 0;
     int s_max = 0;
-    int *rank_ray, *ray_ns, *offsets, *leaf, *ray_of;
+    int *rank_ray, *ray_rank, *ray_ns, *offsets, *leaf, *ray_of;
     float *tt, *z_vals, *feat, *images, *sdf_s, *rgb_s, *act, *sdf, *weights, *color, *depth;
     uint64_t *masks;
     bool z_recorded = false;  // e->z_ready marks the sample compaction on st (aux has not waited yet)
@@ -878,19 +879,20 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         }
         // look-back sampler: the ray-major compaction in the same launch
         // (capacity R · max_steps: every row fits); otherwise k_compact_rays after the read-back
-        int *leaf_q = nullptr, *ray_of_q = nullptr;
+        int *leaf_q = nullptr, *ray_of_q = nullptr, *m_dev = nullptr;
         float *t_q = nullptr;
         if (lb) {
             const size_t cap = (size_t)R * max_steps;
             Q_BUF(int, lq_, kLeafQ, cap * sizeof(int));
             Q_BUF(float, tq_, kTQ, cap * sizeof(float));
             Q_BUF(int, rq_, kRayOfQ, cap * sizeof(int));
-            leaf_q = lq_, t_q = tq_, ray_of_q = rq_;
+            Q_BUF(int, md_, kMDev, sizeof(int));
+            leaf_q = lq_, t_q = tq_, ray_of_q = rq_, m_dev = md_;
         }
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
                                            q.host_raw, q.seq, counts ? &sc : nullptr, lb, tag, leaf_q, t_q,
-                                           ray_of_q));
+                                           ray_of_q, m_dev));
         q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
@@ -1032,6 +1034,41 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     // entries); data parallel and tracking: the padded copy the autograd path
     // makes (k_sample_points)
     const bool rays_path = fused_loss && want_act && !dist && !(e->paths & PSVO_PATH_PADDED);
+    // The device-sized forward: the interpolation and the sdf trunk queued
+    // BEFORE the host waits for the query's statistics, sized on the device
+    // (the sampler's M, kMDev) within a capacity grown from earlier batches —
+    // the GPU runs them straight after the sampler instead of after the
+    // host's read-back and launch (≈ 19 µs of idle GPU per step at config B).
+    // A batch beyond the capacity makes them write nothing; the host then
+    // runs them sized by the read-back, as without this path.
+    const int64_t m_early = std::min<int64_t>(e->m_early, (int64_t)qset.R * max_steps);
+    const bool early = rays_path && sparse && width == 128 && qset.compacted && qset.a.p[kMDev] && m_early > 0 &&
+                       (early_images || prebuilt) && !(e->paths & PSVO_PATH_QUERY_SPLIT);
+    float *feat_e = nullptr, *sdf_e = nullptr;
+    if (early) {
+        const int *m_dev = static_cast<const int *>(qset.a.p[kMDev]);
+        ENG_BUF(float, fe, kFeat, m_early * 16 * sizeof(float));
+        ENG_BUF(float, se, kSdfS, m_early * sizeof(float));
+        feat_e = fe;
+        sdf_e = se;
+        if (engine_overlap(e) && need_z_event) {  // the loss normalisers need only z (the sampler's rows)
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
+        ENG_CALL(join_adam(e, st, who));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+        ENG_CALL(psvo::interp_fwd_dev(st, m_early, m_dev, d->voxel_size, static_cast<const int *>(qset.a.p[kLeafQ]),
+                                      static_cast<const float *>(qset.a.p[kTQ]),
+                                      static_cast<const int *>(qset.a.p[kRayOfQ]), rank_ray, rays_o, rays_d,
+                                      d->centres, d->vertex_idx, d->emb, feat_e));
+        mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+        mark(e, st, PSVO_TIME_MLP_FWD, 0);
+        if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        ENG_CALL(mlp_fwd_prepared(stream, m_early, width, feat_e, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7],
+                                  W[8], W[9], images, sdf_e, nullptr, nullptr, nullptr, m_dev));
+    }
     ENG_CALL(spin_wait(qset, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
     timer_collect(e);  // the previous step's events completed before this read-back
     const int *hs = qset.host_stats;
@@ -1051,12 +1088,16 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.s_max = s_max;
     if (dist && (r_hit == 0 || M == 0)) return PSVO_OK;  // an empty shard still joins the collectives
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
+    // the device-sized forward covered this batch (else: it wrote nothing, run it host-sized below)
+    const bool early_done = early && M <= m_early;
+    if (rays_path && sparse && width == 128) e->m_early = std::max<int64_t>(e->m_early, M + M / 4);
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
     ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));
     ENG_BUF(float, feat, kFeat, M * 16 * sizeof(float));
+    if (early_done && feat != feat_e) return set_error(PSVO_E_LAUNCH, "%s: feature buffer moved", who);
     float *z_vals = nullptr;
-    o.z_recorded = false;
+    if (!early) o.z_recorded = false;
     if (rays_path) {
         if (qset.compacted) {  // the sampler compacted in its launch (look-back offsets)
             leaf = static_cast<int *>(qset.a.p[kLeafQ]);
@@ -1065,7 +1106,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         }
         // the loss normalisers need only z: aux may start them now (a
         // marker packet on st: none when aux has nothing to wait for)
-        if (engine_overlap(e) && need_z_event) {
+        if (engine_overlap(e) && need_z_event && !o.z_recorded) {
             if (hipEventRecord(e->z_ready, st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
             o.z_recorded = true;
@@ -1097,11 +1138,14 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     // ---- forward: interpolation, decoder (after the previous step's
     // optimiser step when its tail ran on aux)
     ENG_CALL(join_adam(e, st, who));
-    mark(e, st, PSVO_TIME_INTERP_FWD, 0);
-    ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
-                             d->vertex_idx, d->emb, feat));
-    mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+    if (!early_done) {  // (a batch beyond the device-sized forward's capacity: its region is already marked)
+        if (!early) mark(e, st, PSVO_TIME_INTERP_FWD, 0);
+        ENG_CALL(psvo_interp_fwd(stream, M, 16, d->voxel_size, leaf, tt, ray_of, rank_ray, rays_o, rays_d, d->centres,
+                                 d->vertex_idx, d->emb, feat));
+        if (!early) mark(e, st, PSVO_TIME_INTERP_FWD, 1);
+    }
     ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
+    if (early_done && sdf_s != sdf_e) return set_error(PSVO_E_LAUNCH, "%s: sdf buffer moved", who);
     float *rgb_s = nullptr, *act = nullptr;
     uint64_t *masks = nullptr;
     // sparse: the sdf trunk (h1, h2, the sdf row: 18.6 of 53.8 k MACs per
@@ -1118,8 +1162,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(uint64_t, mbuf, kMasks, (size_t)psvo_mlp_mask_words(M, width) * sizeof(uint64_t));
         masks = mbuf;
     }
-    mark(e, st, PSVO_TIME_MLP_FWD, 0);
-    if (early_images || prebuilt) {
+    if (!early) mark(e, st, PSVO_TIME_MLP_FWD, 0);  // (the device-sized forward opened it)
+    if (early_done) {
+    } else if (early_images || prebuilt) {
         if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
         ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
@@ -1132,6 +1177,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     // region) and the compact forward (map_step_impl closes it)
     if (!sparse) mark(e, st, PSVO_TIME_MLP_FWD, 1);
     o.rank_ray = const_cast<int *>(rank_ray);
+    o.ray_rank = static_cast<int *>(qset.a.p[kRayRank]);
     o.ray_ns = const_cast<int *>(ray_ns);
     o.offsets = const_cast<int *>(offsets);
     o.leaf = leaf;
@@ -1211,8 +1257,8 @@ int frames_update(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, const 
     // data parallel: a keyframe belongs to one rank (each rank passes its own
     // keyframes), so its rays — and its whole pose gradient of the union-batch
     // loss — are local: no exchange
-    ENG_CALL(psvo_pose_grad_frames(st, fr->n_frames, fr->rays_per_frame, q.r_hit, q.rank_ray, fr->dirs_cam, grad_od,
-                                   grad_od + R * 3, fr->poses, pg));
+    ENG_CALL(psvo::pose_grad_frames_rays(st, fr->n_frames, fr->rays_per_frame, q.ray_rank, fr->dirs_cam, grad_od,
+                                         grad_od + R * 3, fr->poses, pg));
     pa->n = 0;
     pa->lr = fr->lr_pose;
     for (int f = 0; f < fr->n_frames; ++f) {
@@ -1265,7 +1311,7 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
     // this step's pose gradient, each optimised pose's Adam step and the next
     // rays from the updated poses: one launch (frames_update + pose_adam +
     // psvo_pose_rays_frames, the same arithmetic)
-    ENG_CALL(psvo::pose_step_frames(st, fr->n_frames, fr->rays_per_frame, cur.r_hit, cur.rank_ray, fr->dirs_cam,
+    ENG_CALL(psvo::pose_step_frames(st, fr->n_frames, fr->rays_per_frame, cur.ray_rank, fr->dirs_cam,
                                     grad_od, grad_od + R * 3, fr->poses, fr->pose_m, fr->pose_v, fr->pose_step,
                                     fr->lr_pose, d->beta1, d->beta2, d->eps, pg, fr->next_dirs_cam, rays_o, rays_d));
     ENG_CALL(query_enqueue(e, st, q, d, R, rays_o, rays_d, fr->next_seed, "map_step_frames (look-ahead)", nullptr,

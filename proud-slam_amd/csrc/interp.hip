@@ -37,19 +37,12 @@ __device__ __forceinline__ void corner_weights(float px, float py, float pz, flo
     for (int k = 0; k < 8; ++k) w[k] = (ax[(k >> 2) & 1] * ay[(k >> 1) & 1]) * az[k & 1];
 }
 
-__global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size, const int *__restrict__ leaf,
-                                                    const float *__restrict__ t,
-                                                    const int *__restrict__ ray_of_sample,
-                                                    const int *__restrict__ ray_index,
-                                                    const float *__restrict__ rays_o,
-                                                    const float *__restrict__ rays_d,
-                                                    const float *__restrict__ centres,
-                                                    const int *__restrict__ vertex_idx,
-                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t s = g >> 2;
-    const int q = (int)(g & 3);
-    if (s >= m) return;
+__device__ __forceinline__ void interp_one(int64_t s, int q, float voxel_size, const int *__restrict__ leaf,
+                                           const float *__restrict__ t, const int *__restrict__ ray_of_sample,
+                                           const int *__restrict__ ray_index, const float *__restrict__ rays_o,
+                                           const float *__restrict__ rays_d, const float *__restrict__ centres,
+                                           const int *__restrict__ vertex_idx, const float4 *__restrict__ emb,
+                                           float4 *__restrict__ feat) {
     const int lf = leaf[s];
     const int r = ray_index ? ray_index[ray_of_sample[s]] : ray_of_sample[s];
     const float ts = t[s];
@@ -74,6 +67,27 @@ __global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size,
         acc.w = acc.w + w[k] * e.w;
     }
     feat[s * 4 + q] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_interp_fwd(int64_t m, float voxel_size, const int *__restrict__ leaf,
+                                                    const float *__restrict__ t,
+                                                    const int *__restrict__ ray_of_sample,
+                                                    const int *__restrict__ ray_index,
+                                                    const float *__restrict__ rays_o,
+                                                    const float *__restrict__ rays_d,
+                                                    const float *__restrict__ centres,
+                                                    const int *__restrict__ vertex_idx,
+                                                    const float4 *__restrict__ emb, float4 *__restrict__ feat,
+                                                    const int *__restrict__ m_dev) {
+    // m_dev: the sample count on the device (a launch queued before the host
+    // knows it; m is then the buffers' capacity — a larger batch is left to
+    // the host-sized launch after the read-back), the grid striding over it
+    int64_t mm = m_dev ? (int64_t)*m_dev : m;
+    if (mm > m) mm = 0;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < mm * 4;
+         g += (int64_t)gridDim.x * blockDim.x)
+        interp_one(g >> 2, (int)(g & 3), voxel_size, leaf, t, ray_of_sample, ray_index, rays_o, rays_d, centres,
+                   vertex_idx, emb, feat);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -365,9 +379,25 @@ extern "C" int psvo_interp_fwd(void *stream, int64_t m, int d, float voxel_size,
     psvo::launch(k_interp_fwd, dim3(div_up(m * 4, 256)), dim3(256), 0, as_stream(stream), m, voxel_size, leaf,
                        t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
                        reinterpret_cast<const float4 *>(emb),
-                       reinterpret_cast<float4 *>(feat));
+                       reinterpret_cast<float4 *>(feat), static_cast<const int *>(nullptr));
     return check_launch("interp_fwd");
 }
+
+namespace psvo {
+// the interpolation over m_dev ≤ m_cap samples (the count on the device):
+// one pass over at most 4,096 workgroups, striding
+int interp_fwd_dev(hipStream_t st, int64_t m_cap, const int *m_dev, float voxel_size, const int *leaf, const float *t,
+                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
+                   const float *centres, const int *vertex_idx, const float *emb, float *feat) {
+    PSVO_REQUIRE(m_cap >= 0 && m_dev && voxel_size > 0.f, "interp_fwd_dev: bad arguments");
+    if (m_cap == 0) return PSVO_OK;
+    const int64_t blocks = div_up(m_cap * 4, 256);
+    psvo::launch(k_interp_fwd, dim3((int)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, st, m_cap, voxel_size, leaf,
+                 t, ray_of_sample, ray_index, rays_o, rays_d, centres, vertex_idx,
+                 reinterpret_cast<const float4 *>(emb), reinterpret_cast<float4 *>(feat), m_dev);
+    return check_launch("interp_fwd_dev");
+}
+}  // namespace psvo
 
 
 extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_size, const int *offsets,

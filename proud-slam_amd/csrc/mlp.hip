@@ -788,10 +788,14 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
 // k_mlp_fwd2's first two layers, so the sdf is bit-identical to its output.
 constexpr int kLdsSdf2 = (kF2Buf0 + 16384) * 4;
 
-__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m, const float *__restrict__ feat,
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, const float *__restrict__ feat,
                                                             const float *__restrict__ img,
-                                                            float *__restrict__ sdf_out) {
+                                                            float *__restrict__ sdf_out, const int *__restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    // m_dev: the count on the device, m_host the buffers' capacity (a larger
+    // batch: nothing here, the host-sized launch after the read-back)
+    int64_t m = m_dev ? (int64_t)__builtin_amdgcn_readfirstlane(*m_dev) : m_host;
+    if (m > m_host) m = 0;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
@@ -1552,8 +1556,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
 // (the same per-sample dfeat bits), in two phases per round of four
 // 16-sample units:
 //   phase  chain wave c (unit u0 + 4r + c)                         gradient wave d
-//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2;    (loads only: h1 / h2 tiles of round r)
-//          dW1 row block c += δh1(r−1) ⊗ x(r−1)
+//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2    dW1 row block d += δh1(r−1) ⊗ x(r−1);
+//                                                                  h1 / h2 tiles of round r start loading
 //   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          dW2 col block d += δh2(r) ⊗ h1(r);
 //          backward (dL/dx, the embedding scatter)                 W3 row 0 (cols of block d) += dsdf(r) · h2(r)
 // plus a last phase A for the final round's dW1.  A chain wave and a
@@ -1624,11 +1628,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
         const int n = lane & 15, q = lane >> 4;
         const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot
         const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
-        float *const page1 = lds + kT3A + c * 1024;  // dW1 accumulators
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-        float b1p = 0.f;
         TrunkIn nin;
         // the interpolation backward's sample data one round ahead (leaf, ray,
         // t), its vertex ids / centre / rank row at the top of phase A: phase B
@@ -1695,7 +1694,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                 }
             }
             PSVO_STAMP(1);
-            if (r > 0) xgrad16(h1set, xset(r - 1), c, ubase - 4, u1, lane, page1, &b1p);
             PSVO_STAMP(2);
             raw_barrier();
             PSVO_STAMP(3);
@@ -1751,31 +1749,24 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
             PSVO_STAMP(7);
             PSVO_STAMP_FLUSH(0);
         }
-        // ---- slab: W1 row block c + b1
-        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
-        if (i < 16) {
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
-                const int row = 32 * c + phi(rr, h);
-                const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
-                store_nt(s1, row * 16 + i, page1[pos]);
-            }
-        }
-        const float bv = b1p + __shfl_xor(b1p, 32, 64);
-        if (h == 0) store_nt(s1, 128 * 16 + 32 * c + i, bv);
     } else {
         // ================= gradient wave: column block d of W2, row 0 of W3 (cols of block d), biases
         const int d = wave - 4;
         f32x16 acc2[kNB];
         zero(acc2);
-        float b2p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f;
+        float b2p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f, b1p = 0.f;
+        float *const page1 = lds + kT3A + d * 1024;  // dW1 row block d accumulators
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
         const __amdgpu_buffer_rsrc_t h1m = rsrc_of(act, tb), h2m = rsrc_of(act + tstride, tb);
         float4 ring[3], h2t[8];
         for (int r = 0; r <= n_rounds; ++r) {
             PSVO_STAMP(0);
             const int64_t ubase = u0 + 4 * (int64_t)r;
-            // A (the chain's GEMM phase): no MFMAs here — the SIMD's matrix
-            // unit is the chain wave's; this round's h1 / h2 tiles start loading
+            // A (the chain's W2ᵀ GEMM): dW1 row block d += δh1(r−1) ⊗ x(r−1)
+            // (32 MFMAs beside the chain's 256); this round's h1 / h2 tiles start loading
+            if (r > 0) xgrad16(h1set, xset(r - 1), d, ubase - 4, u1, lane, page1, &b1p);
             if (r < n_rounds) {
 #pragma unroll
                 for (int qq = 0; qq < 8; ++qq) h2t[qq] = dw_bsrc(h2m, ubase, u1, d, lane, qq);
@@ -1808,6 +1799,18 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
             PSVO_STAMP(7);
             PSVO_STAMP_FLUSH(0);
         }
+        // ---- slabs: W1 row block d + b1, W2 column block d + b2, W3 row 0 + b3[0]
+        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
+        if (i < 16) {
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int row = 32 * d + phi(rr, h);
+                const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
+                store_nt(s1, row * 16 + i, page1[pos]);
+            }
+        }
+        const float bv = b1p + __shfl_xor(b1p, 32, 64);
+        if (h == 0) store_nt(s1, 128 * 16 + 32 * d + i, bv);
         const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
         float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
         float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
@@ -1901,7 +1904,7 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         }
         const int64_t tiles = div_up(m, kF2Tile);
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-        psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf);
+        psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf, m_dev);
         return check_launch("mlp_fwd");
     }
     static bool attr2 = false;

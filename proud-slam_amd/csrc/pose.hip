@@ -165,22 +165,84 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_grad_frames(int64_t r_hit
     pose_chain(poses + blockIdx.x * 6, tot, grads + blockIdx.x * 8);
 }
 
+// The engine's per-frame sums (bundle_adjust_frames' look-ahead and its
+// unpipelined step): thread t takes the frame's rays lo + t, lo + t + T, …
+// directly — a hit ray is one with ray_rank >= 0, its gradient rows are read
+// beside the rank (one memory round trip, not rank → ray → rows) — then the
+// wave butterflies and the 16 wave partials summed by 12 threads in wave
+// order: a fixed order, so every run gives the same bits.
+__device__ __forceinline__ void frame_sums_direct(const int *__restrict__ ray_rank, int64_t lo, int64_t hi,
+                                                  const float *__restrict__ dirs, const float *__restrict__ g_o,
+                                                  const float *__restrict__ g_d, float (&part)[kGradThreads / 64][12],
+                                                  float (&tot)[12]) {
+    float acc[12] = {};
+    for (int64_t r = lo + threadIdx.x; r < hi; r += kGradThreads) {
+        const bool in = ray_rank[r] >= 0;  // the rows of a ray without hits are not written
+        float go[3], gd[3], dir[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            go[j] = g_o[r * 3 + j];
+            gd[j] = g_d[r * 3 + j];
+            dir[j] = dirs[r * 3 + j];
+        }
+        if (!in) continue;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] += go[j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) acc[3 + j * 3 + i] += gd[j] * dir[i];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+        if (lane == 0) part[wv][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        float t = 0.f;
+        for (int w = 0; w < kGradThreads / 64; ++w) t += part[w][threadIdx.x];
+        tot[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kGradThreads) void k_pose_grad_rays(const int *__restrict__ ray_rank, int64_t rpf,
+                                                                 const float *__restrict__ dirs,
+                                                                 const float *__restrict__ g_o,
+                                                                 const float *__restrict__ g_d,
+                                                                 const float *__restrict__ poses,
+                                                                 float *__restrict__ grads) {
+    __shared__ float part[kGradThreads / 64][12];
+    __shared__ float tot[12];
+    const int64_t lo = blockIdx.x * rpf;
+    frame_sums_direct(ray_rank, lo, lo + rpf, dirs, g_o, g_d, part, tot);
+    if (threadIdx.x != 0) return;
+    float t[12];
+    for (int i = 0; i < 12; ++i) t[i] = tot[i];
+    pose_chain(poses + blockIdx.x * 6, t, grads + blockIdx.x * 8);
+}
+
 struct PoseStepArgs {
     int64_t step[kXchMaxFrames];
     float lr_bc1[kXchMaxFrames], bc2_sqrt[kXchMaxFrames];
 };
 
-// k_pose_grad_frames + k_adam on the frame's pose + k_pose_rays_frames for
-// the frame's next rays, one block per frame (a frame's rays, gradient and
-// pose are its own: no grid-wide dependency)
+// k_pose_grad_rays + k_adam on the frame's pose + k_pose_rays_frames for the
+// frame's next rays, one block per frame (a frame's rays, gradient and pose
+// are its own: no grid-wide dependency); the updated rotation is formed once
+// (thread 0) and shared through LDS
 __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
-    int64_t r_hit, const int *__restrict__ rank_ray, int64_t rpf, const float *__restrict__ dirs,
-    const float *__restrict__ g_o, const float *__restrict__ g_d, float *__restrict__ poses,
-    float *__restrict__ pose_m, float *__restrict__ pose_v, PoseStepArgs a, float beta1, float beta2, float omb1,
-    float omb2, float eps, float *__restrict__ grads, const float *__restrict__ next_dirs,
-    float *__restrict__ rays_o, float *__restrict__ rays_d) {
+    const int *__restrict__ ray_rank, int64_t rpf, const float *__restrict__ dirs, const float *__restrict__ g_o,
+    const float *__restrict__ g_d, float *__restrict__ poses, float *__restrict__ pose_m, float *__restrict__ pose_v,
+    PoseStepArgs a, float beta1, float beta2, float omb1, float omb2, float eps, float *__restrict__ grads,
+    const float *__restrict__ next_dirs, float *__restrict__ rays_o, float *__restrict__ rays_d) {
     __shared__ float part[kGradThreads / 64][12];
-    __shared__ float pose_s[6];
+    __shared__ float tot[12];
+    __shared__ float rot_s[12];  // R row-major, then t
     const int f = blockIdx.x;
     const int64_t lo = f * rpf, hi = lo + rpf;
     // the next rays' camera directions depend on nothing here: loaded first
@@ -189,50 +251,48 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     float nd[3] = {0.f, 0.f, 0.f};
     if (rpf <= kGradThreads && r1 < hi)
         for (int j = 0; j < 3; ++j) nd[j] = next_dirs[r1 * 3 + j];
-    float acc[12] = {};
-    frame_ray_sums(r_hit, rank_ray, lo, hi, dirs, g_o, g_d, acc);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int i = 0; i < 12; ++i) {
-        float v = acc[i];
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
-        if (lane == 0) part[wv][i] = v;
-    }
-    __syncthreads();
+    frame_sums_direct(ray_rank, lo, hi, dirs, g_o, g_d, part, tot);
     if (threadIdx.x == 0) {
-        float tot[12] = {};
-        for (int w = 0; w < kGradThreads / 64; ++w)
-            for (int i = 0; i < 12; ++i) tot[i] += part[w][i];
+        float t[12];
+        for (int i = 0; i < 12; ++i) t[i] = tot[i];
         float *pose = poses + f * 6;
         float *g = grads + f * 8;
-        pose_chain(pose, tot, g);
+        pose_chain(pose, t, g);
+        float p6[6];
+        for (int i = 0; i < 6; ++i) p6[i] = pose[i];
         if (a.step[f] >= 1) {  // stamp 0 / update_pose False: fixed (render_helpers.py:594-596)
             for (int i = 0; i < 6; ++i) {
-                float pi = pose[i], mi = pose_m[f * 6 + i], vi = pose_v[f * 6 + i];
-                adam_elem(pi, g[i], mi, vi, beta1, beta2, omb1, omb2, eps, 0.0f, a.lr_bc1[f], a.bc2_sqrt[f]);
-                pose[i] = pi;
+                float mi = pose_m[f * 6 + i], vi = pose_v[f * 6 + i];
+                adam_elem(p6[i], g[i], mi, vi, beta1, beta2, omb1, omb2, eps, 0.0f, a.lr_bc1[f], a.bc2_sqrt[f]);
+                pose[i] = p6[i];
                 pose_m[f * 6 + i] = mi;
                 pose_v[f * 6 + i] = vi;
             }
         }
-        for (int i = 0; i < 6; ++i) pose_s[i] = pose[i];
+        Rot q;
+        rotation(p6, q);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) rot_s[i * 3 + j] = q.R[i][j];
+        for (int j = 0; j < 3; ++j) rot_s[9 + j] = p6[j];
     }
     __syncthreads();
-    Rot q;
-    rotation(pose_s, q);
+    float R[3][3], t0[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[i][j] = rot_s[i * 3 + j];
+    for (int j = 0; j < 3; ++j) t0[j] = rot_s[9 + j];
     if (rpf <= kGradThreads) {
         if (r1 < hi)
             for (int j = 0; j < 3; ++j) {
-                rays_d[r1 * 3 + j] = nd[0] * q.R[j][0] + nd[1] * q.R[j][1] + nd[2] * q.R[j][2];
-                rays_o[r1 * 3 + j] = pose_s[j];
+                rays_d[r1 * 3 + j] = nd[0] * R[j][0] + nd[1] * R[j][1] + nd[2] * R[j][2];
+                rays_o[r1 * 3 + j] = t0[j];
             }
         return;
     }
     for (int64_t r = lo + threadIdx.x; r < hi; r += kGradThreads) {
         const float d0 = next_dirs[r * 3 + 0], d1 = next_dirs[r * 3 + 1], d2 = next_dirs[r * 3 + 2];
         for (int j = 0; j < 3; ++j) {
-            rays_d[r * 3 + j] = d0 * q.R[j][0] + d1 * q.R[j][1] + d2 * q.R[j][2];
-            rays_o[r * 3 + j] = pose_s[j];
+            rays_d[r * 3 + j] = d0 * R[j][0] + d1 * R[j][1] + d2 * R[j][2];
+            rays_o[r * 3 + j] = t0[j];
         }
     }
 }
@@ -333,13 +393,20 @@ extern "C" int psvo_pose_grad_frames(void *stream, int n_frames, int64_t rays_pe
 }
 
 namespace psvo {
-int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64_t r_hit, const int *rank_ray,
-                     const float *dirs, const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
+int pose_grad_frames_rays(hipStream_t st, int n_frames, int64_t rays_per_frame, const int *ray_rank,
+                          const float *dirs, const float *g_o, const float *g_d, const float *poses, float *grads) {
+    PSVO_REQUIRE(n_frames > 0 && rays_per_frame > 0, "pose_grad_frames: bad sizes");
+    PSVO_REQUIRE(ray_rank && dirs && g_o && g_d && poses && grads, "pose_grad_frames: null pointer");
+    psvo::launch(k_pose_grad_rays, dim3(n_frames), dim3(kGradThreads), 0, st, ray_rank, rays_per_frame, dirs, g_o,
+                 g_d, poses, grads);
+    return check_launch("pose_grad_frames");
+}
+int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, const int *ray_rank, const float *dirs,
+                     const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
                      const int64_t *steps, double lr, double beta1, double beta2, double eps, float *grads,
                      const float *next_dirs, float *rays_o, float *rays_d) {
-    PSVO_REQUIRE(n_frames > 0 && n_frames <= kXchMaxFrames && rays_per_frame > 0 && r_hit >= 0,
-                 "pose_step_frames: bad sizes");
-    PSVO_REQUIRE(rank_ray && dirs && g_o && g_d && poses && grads && next_dirs && rays_o && rays_d && steps,
+    PSVO_REQUIRE(n_frames > 0 && n_frames <= kXchMaxFrames && rays_per_frame > 0, "pose_step_frames: bad sizes");
+    PSVO_REQUIRE(ray_rank && dirs && g_o && g_d && poses && grads && next_dirs && rays_o && rays_d && steps,
                  "pose_step_frames: null pointer");
     PoseStepArgs a{};
     for (int f = 0; f < n_frames; ++f) {
@@ -351,9 +418,9 @@ int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64
         a.lr_bc1[f] = (float)(lr / bc1);
         a.bc2_sqrt[f] = (float)std::sqrt(bc2);
     }
-    psvo::launch(k_pose_step_frames, dim3(n_frames), dim3(kGradThreads), 0, st, r_hit, rank_ray, rays_per_frame,
-                       dirs, g_o, g_d, poses, pose_m, pose_v, a, (float)beta1, (float)beta2, (float)(1.0 - beta1),
-                       (float)(1.0 - beta2), (float)eps, grads, next_dirs, rays_o, rays_d);
+    psvo::launch(k_pose_step_frames, dim3(n_frames), dim3(kGradThreads), 0, st, ray_rank, rays_per_frame, dirs, g_o,
+                 g_d, poses, pose_m, pose_v, a, (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
+                 (float)eps, grads, next_dirs, rays_o, rays_d);
     return check_launch("pose_step_frames");
 }
 }  // namespace psvo

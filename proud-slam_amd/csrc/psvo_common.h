@@ -140,7 +140,8 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                         int *ray_ns, int *offsets, unsigned long long *host, int seq,
                         const SampleCounts *counts = nullptr, unsigned long long *lb_desc = nullptr,
-                        uint32_t lb_tag = 0, int *leaf = nullptr, float *t = nullptr, int *ray_of = nullptr);
+                        uint32_t lb_tag = 0, int *leaf = nullptr, float *t = nullptr, int *ray_of = nullptr,
+                        int *m_out = nullptr);  // with the compaction: M on the device
 // whether a query of r rays runs its statistics / rank pass and its sample
 // scan by look-back (up to kLbMaxRays rays), and its descriptor granules
 constexpr int64_t kLbMaxRays = 16384;  // 4 rays per workgroup, <= 64 · 64 workgroups (lookback.h)
@@ -161,13 +162,22 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
     v = vi;
 }
 
-// the bundle-adjust look-ahead's pose work in one launch, one block per
-// keyframe (pose.hip): the frame's pose gradient (k_pose_grad_frames), its
-// Adam step when steps[f] >= 1 (k_adam's arithmetic, lr / bc1 and sqrt(bc2)
-// formed on the host as adam_launch does), then the frame's next rays
-// (k_pose_rays_frames) from the updated pose
-int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, int64_t r_hit, const int *rank_ray,
-                     const float *dirs, const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
+// the bundle-adjust pose work (pose.hip), over each frame's rays directly
+// (ray_rank[r] >= 0: a hit ray; the engine's sums — one fixed order for both
+// calls): the frames' pose gradients (k_pose_grad_rays), and the
+// look-ahead's whole pose step in one launch, one block per keyframe — the
+// gradient, its Adam step when steps[f] >= 1 (k_adam's arithmetic, lr / bc1
+// and sqrt(bc2) formed on the host as adam_launch does), then the frame's
+// next rays (k_pose_rays_frames) from the updated pose
+// the interpolation forward over the device's sample count m_dev <= m_cap
+// (interp.hip; psvo_interp_fwd's arithmetic)
+int interp_fwd_dev(hipStream_t st, int64_t m_cap, const int *m_dev, float voxel_size, const int *leaf, const float *t,
+                   const int *ray_of_sample, const int *ray_index, const float *rays_o, const float *rays_d,
+                   const float *centres, const int *vertex_idx, const float *emb, float *feat);
+int pose_grad_frames_rays(hipStream_t st, int n_frames, int64_t rays_per_frame, const int *ray_rank,
+                          const float *dirs, const float *g_o, const float *g_d, const float *poses, float *grads);
+int pose_step_frames(hipStream_t st, int n_frames, int64_t rays_per_frame, const int *ray_rank, const float *dirs,
+                     const float *g_o, const float *g_d, float *poses, float *pose_m, float *pose_v,
                      const int64_t *steps, double lr, double beta1, double beta2, double eps, float *grads,
                      const float *next_dirs, float *rays_o, float *rays_d);
 

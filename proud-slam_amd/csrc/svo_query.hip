@@ -1322,6 +1322,7 @@ struct SampleTail {
     int *leaf;
     float *t;
     int *ray_of;
+    int *m_out;  // or null: the batch's sample count M, on the device (the step's device-sized forward)
 };
 constexpr int kSmpStage = 256;  // a row's first samples staged in LDS for the in-launch compaction
 // ray_cnt word: valid front / sdf samples (12 bits each), then whether a
@@ -1561,7 +1562,10 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
     if ((int)blockIdx.x != last) return;
     const int tot = (int)(ex[0] + agg[0]);
     const int smax = (int)max(ex[1], agg[1]);
-    if (lane == 0) tl.offsets[n] = tot;
+    if (lane == 0) {
+        tl.offsets[n] = tot;
+        if (tl.m_out) *tl.m_out = ok ? tot : 0;  // an abandoned wait: no samples (the flag reports it)
+    }
     if constexpr (NG == 8) {
         if (lane == 0) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
             const uint32_t pp = ex[6] + agg[6];
@@ -1998,7 +2002,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                         int *ray_ns, int *offsets, unsigned long long *host, int seq, const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
-                        float *t, int *ray_of) {
+                        float *t, int *ray_of, int *m_out) {
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host,
                  "sample_rays_to_host: bad arguments");
     PSVO_REQUIRE(!lb_desc || (r_hit_cap <= kLbMaxRays && lb_tag != 0), "sample_rays_to_host: look-back arguments");
@@ -2014,6 +2018,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
             tl.leaf = leaf;
             tl.t = t;
             tl.ray_of = ray_of;
+            tl.m_out = m_out;
         }
     }
     psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,

@@ -145,6 +145,44 @@ def test_sparse_decoder_matches_dense(padded, sdf_shift):
         torch.testing.assert_close(pb, pa, rtol=0, atol=1e-4 * float(pa.abs().max()))
 
 
+def test_device_sized_forward_capacity_fallback():
+    """The device-sized forward (engine.cpp render: interpolation and sdf
+    trunk queued before the host reads the query's statistics, sized by the
+    sampler's device-side M within a capacity of 1.25 × the largest M seen):
+    a batch 4 × larger than the last exceeds the capacity, the queued kernels
+    write nothing and the host-sized launch runs instead; the next batch of
+    that size fits.  Each step's loss bit for bit against the dense decoder
+    (no device-sized forward), gradients as in test_sparse_decoder_matches_dense."""
+    from psvo.engine import MappingEngine
+    from psvo.octree import map_states
+    w, tree, emb0, dec = _setup()
+    rgb, depth = w.rgb.reshape(-1, 3).to(DEV), w.depth.reshape(-1).to(DEV)
+    crit = {"rgb_weight": 0.5, "depth_weight": 1.0, "sdf_weight": 5000.0, "fs_weight": 10.0}
+    sizes = [128, 512, 512, 128]
+    runs = {}
+    for mode in ("dense", "sparse"):
+        eng = MappingEngine(map_states(tree, emb0.clone().to(DEV), 0.2, device=DEV), dec, 0.2, 0.01, truncation=0.1,
+                            max_distance=10.0, criteria=crit, max_depth=10.0)
+        eng.set_paths(MappingEngine.PATH_DENSE_DECODER if mode == "dense" else 0)
+        out = []
+        for it, n in enumerate(sizes):
+            poses, dirs = _frames_of(w, n)
+            pg = torch.zeros(poses.shape[0], 8, device=DEV)
+            loss = eng.step_frames(dirs, n, poses.clone(), torch.zeros_like(poses), torch.zeros_like(poses), [0, 1],
+                                   1e-3, rgb, depth, seed=900 + it, apply_adam=False, pose_grad=pg, want_loss=True)
+            torch.cuda.synchronize()
+            out.append((float(loss), list(eng.last_stats), eng.grad_flat.cpu().clone()))
+        runs[mode] = out
+        eng.close()
+    n_emb = emb0.shape[0] * 16
+    for (la, sa, ga), (lb, sb, gb) in zip(runs["dense"], runs["sparse"]):
+        assert sa[:13] == sb[:13]
+        assert la == lb, (la, lb)
+        torch.testing.assert_close(gb[n_emb:], ga[n_emb:], rtol=1e-4, atol=1e-5 * float(ga[n_emb:].abs().max()))
+        torch.testing.assert_close(gb[:n_emb], ga[:n_emb], rtol=1e-4, atol=1e-5 * float(ga[:n_emb].abs().max()))
+    assert runs["sparse"][1][1][4] > 1.25 * runs["sparse"][0][1][4]  # the second batch is beyond the capacity
+
+
 def test_engine_query_ahead_matches_inline():
     """psvo_map_query (next batch's intersection + sampling on the side stream,
     one step ahead) gives the same iterations as queries inline in the step."""
