@@ -1051,11 +1051,6 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(float, se, kSdfS, m_early * sizeof(float));
         feat_e = fe;
         sdf_e = se;
-        if (engine_overlap(e) && need_z_event) {  // the loss normalisers need only z (the sampler's rows)
-            if (hipEventRecord(e->z_ready, st) != hipSuccess)
-                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
-            o.z_recorded = true;
-        }
         ENG_CALL(join_adam(e, st, who));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
         ENG_CALL(psvo::interp_fwd_dev(st, m_early, m_dev, d->voxel_size, static_cast<const int *>(qset.a.p[kLeafQ]),
@@ -1068,6 +1063,13 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
         ENG_CALL(mlp_fwd_prepared(stream, m_early, width, feat_e, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7],
                                   W[8], W[9], images, sdf_e, nullptr, nullptr, nullptr, m_dev));
+        // the loss normalisers need only z (the sampler's rows): aux may start
+        // them after these (a marker in front of them delays the interpolation)
+        if (engine_overlap(e) && need_z_event) {
+            if (hipEventRecord(e->z_ready, st) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+            o.z_recorded = true;
+        }
     }
     ENG_CALL(spin_wait(qset, qset.done_recorded ? qset.done : nullptr, qset.qstream, who));
     timer_collect(e);  // the previous step's events completed before this read-back
@@ -1343,8 +1345,6 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const float *counts_gt = !want_loss ? gt_depth : nullptr;
     ENG_CALL(take_query(e, st, d, R, rays_o, rays_d, seed, "map_step", &qset, noise, counts_gt));
     QueryGuard guard{e, st, qset};
-    if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     const bool overlap = engine_overlap(e);
     if (overlap) ENG_CALL(ensure_aux(e));
     hipStream_t ax = overlap ? e->aux : st;  // side work: loss normalisers / value, embedding backward
@@ -1372,6 +1372,10 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // the sparse decoder: render runs the sdf trunk only
     const bool sparse_dec = !(e->paths & PSVO_PATH_DENSE_DECODER);
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z, sparse_dec));
+    // the step clock's marker: behind the forward's first kernels on st (a
+    // marker between the query and the interpolation delays the latter)
+    if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     const int64_t M = q.m;

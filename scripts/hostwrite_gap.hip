@@ -30,6 +30,12 @@ __global__ void k_b(unsigned long long *stamp) {
 
 __global__ void k_c() {}
 
+// spins ~us microseconds (s_memrealtime, 100 MHz)
+__global__ void k_spin(int us) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)us * 100ull) __builtin_amdgcn_s_sleep(2);
+}
+
 int main() {
     float *rows;
     unsigned long long *dev, *host, *stamp;
@@ -64,6 +70,24 @@ int main() {
         }
         printf("%s stats%s%s%s: gap A.last-store -> B.start %.2f us\n", (mode & 1) ? "host" : "device",
                (mode & 2) ? " + satisfied wait" : "", mode >= 4 ? " + marker" : "", mode >= 6 ? " + timed marker" : "",
+               sum / reps);
+    }
+    // a cross-stream wait on an event NOT complete when the host queues it:
+    // s2 spins `us` then records; s runs A (then waits, then B)
+    for (int us : {2, 10, 30, 60}) {
+        double sum = 0.0, a_dur = 0.0;
+        const int reps = 20;
+        for (int r = 0; r < reps + 3; ++r) {
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s2, us);
+            hipEventRecord(ev, s2);
+            hipLaunchKernelGGL(k_a, dim3(1024), dim3(256), 0, s, rows, dev, stamp, 64);
+            hipStreamWaitEvent(s, ev, 0);
+            hipLaunchKernelGGL(k_b, dim3(1), dim3(64), 0, s, stamp);
+            hipStreamSynchronize(s);
+            hipStreamSynchronize(s2);
+            if (r >= 3) sum += (double)(stamp[1] - stamp[0]) / 100.0;
+        }
+        printf("pending cross-stream wait (other stream spins %d us): gap A.last-store -> B.start %.2f us\n", us,
                sum / reps);
     }
     return 0;
