@@ -428,10 +428,12 @@ namespace psvo {
 // psvo_criterion_coef in two halves, so that a data-parallel engine can
 // all-reduce the count sums (union-batch normalisers) between them
 int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
-                     const float *gt_depth, const float *z_vals, float *workspace, double *sums) {
+                     const float *gt_depth, const float *z_vals, int z_stride, const int *ray_ns, float *workspace,
+                     double *sums) {
+    PSVO_REQUIRE(z_stride >= s_max, "criterion_counts: z stride %d < S_max %d", z_stride, s_max);
     if (r_hit > 0)
         psvo::launch(k_crit_counts, dim3(div_up(r_hit, 4)), dim3(256), 0, st, r_hit, s_max, truncation,
-                           max_depth, rank_ray, gt_depth, z_vals, s_max, nullptr, workspace);
+                           max_depth, rank_ray, gt_depth, z_vals, z_stride, ray_ns, workspace);
     PSVO_REQUIRE(((uintptr_t)workspace & 15) == 0, "criterion: workspace must be 16-B aligned");
     psvo::launch(k_crit_reduce, dim3(1), dim3(64), 0, st, r_hit, workspace, sums);
     return check_launch("criterion_counts");

@@ -1027,13 +1027,14 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
             return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
     }
     const bool dist = e->x.on();
-    // the mapping step on one GPU: no padded [R_hit, S_max] copy — the loss
-    // kernels read z from the sampler's depth rows (stride max_steps) and the
-    // samples are compacted ray-major (by the look-back sampler in its own
-    // launch, else k_compact_rays: a wave per hit ray over its ≈ 64 valid
-    // entries); data parallel and tracking: the padded copy the autograd path
-    // makes (k_sample_points)
-    const bool rays_path = fused_loss && want_act && !dist && !(e->paths & PSVO_PATH_PADDED);
+    // the mapping step: no padded [R_hit, S_max] copy — the loss kernels read
+    // z from the sampler's depth rows (stride max_steps; the union S_max of a
+    // data-parallel step is at most every rank's max_steps) and the samples
+    // are compacted ray-major (by the look-back sampler in its own launch,
+    // else k_compact_rays: a wave per hit ray over its ≈ 64 valid entries);
+    // tracking and PSVO_PATH_PADDED: the padded copy the autograd path makes
+    // (k_sample_points)
+    const bool rays_path = fused_loss && want_act && !(e->paths & PSVO_PATH_PADDED);
     // The device-sized forward: the interpolation and the sdf trunk queued
     // BEFORE the host waits for the query's statistics, sized on the device
     // (the sampler's M, kMDev) within a capacity grown from earlier batches —
@@ -1492,7 +1493,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             sums_c = static_cast<double *>(qset->a.p[kDistSums]);
         } else {
             ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray,
-                                      gt_depth, q.z_vals, crit_ws, sums_c));
+                                      gt_depth, q.z_vals, q.z_stride, q.z_stride == s_max ? nullptr : q.ray_ns,
+                                      crit_ws, sums_c));
             ENG_CALL(x.call(PSVO_XCH_SUM_F64, 0, 0, 8, ax, "loss normalisers"));
         }
         ENG_CALL(criterion_coef_from_sums(ax, sums_c, n_hit, s_max, d->truncation, d->w_rgb, d->w_depth, d->w_fs,

@@ -214,7 +214,8 @@ int dist_counts(hipStream_t st, int64_t R, const int *stats, const int *rank_ray
 
 // psvo_criterion_coef split at the count sums (criterion.hip)
 int criterion_counts(hipStream_t st, int64_t r_hit, int s_max, float truncation, float max_depth, const int *rank_ray,
-                     const float *gt_depth, const float *z_vals, float *workspace, double *sums);
+                     const float *gt_depth, const float *z_vals, int z_stride, const int *ray_ns, float *workspace,
+                     double *sums);
 int criterion_coef_from_sums(hipStream_t st, const double *sums, int64_t n_hit, int n_cols, float truncation,
                              float rgb_w, float depth_w, float fs_w, float sdf_w, int flags, float *coef);
 
