@@ -26,7 +26,8 @@ namespace {
 
 // buffers of one query (intersection + sampling of a ray batch): a query set
 enum QSlot { kStats, kHitIdx, kHitT0, kHitT1, kRayNv, kRayDsum, kRayRank, kRankRay, kSIdx, kSDepth, kSDist, kRayNs,
-             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kDistSums, kMDev, kQSlots };
+             kOffsets, kBlkOut, kRayCnt, kCoefQ, kLbDesc, kLeafQ, kTQ, kRayOfQ, kDistSums, kMDev, kNvRank, kCol0Rank,
+             kQSlots };
 // buffers of the rest of a step
 enum Slot {
     kLeaf, kT, kRayOf, kZ, kMask, kFeat, kImages, kSdfS, kRgbS, kAct, kMasks, kSdf, kWeights, kColor,
@@ -822,15 +823,24 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         e->lb_tag = e->lb_tag == 0xffffffffu ? 1u : e->lb_tag + 1u;
         tag = e->lb_tag;
     }
+    // with the look-back: each rank's hit count and first voxel id by rank
+    // (the sampler's only reads of other rows, one load each)
+    int *nv_rank = nullptr, *col0_rank = nullptr;
+    if (lb) {
+        Q_BUF(int, nr_, kNvRank, R * sizeof(int));
+        Q_BUF(int, c0_, kCol0Rank, R * sizeof(int));
+        nv_rank = nr_, col0_rank = c0_;
+    }
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
-                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out, lb, tag));
+                                    ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out, lb, tag,
+                                    nv_rank, col0_rank));
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: ONE all-gather (8 words + the hit rows' counts), then local
         if (R > x.max_rays_rank)
             return set_error(PSVO_E_INVALID, "%s: %lld rays exceed the exchange's max_rays_rank %lld", who,
                              (long long)R, (long long)x.max_rays_rank);
-        ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off()));
+        ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off(), nv_rank));
         ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), x.cw, st, "query layout"));
         ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, x.cw, x.nch, stats, x.xi32 + x.table_off()));
     }
@@ -847,7 +857,8 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     mark(e, st, PSVO_TIME_SAMPLE, 0);
     if (x.on()) {
         ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
-                             x.xi32 + x.table_off(), x.nch, s_idx, s_depth, s_dist, ray_ns, offsets));
+                             x.xi32 + x.table_off(), x.nch, s_idx, s_depth, s_dist, ray_ns, offsets, nv_rank,
+                             col0_rank));
         // S_max of the union (every rank pads its [R_hit, S_max] blocks to it) and, given the
         // step's GT depths, the loss normalisers' counts: ONE all-gather of 8 words
         double *qsums = nullptr;
@@ -892,7 +903,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         ENG_CALL(psvo::sample_rays_to_host(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
                                            d->step_size, noise, seed, stats, s_idx, s_depth, s_dist, ray_ns, offsets,
                                            q.host_raw, q.seq, counts ? &sc : nullptr, lb, tag, leaf_q, t_q,
-                                           ray_of_q, m_dev));
+                                           ray_of_q, m_dev, nv_rank, col0_rank));
         q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);

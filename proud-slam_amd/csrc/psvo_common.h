@@ -141,7 +141,8 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         int *ray_ns, int *offsets, unsigned long long *host, int seq,
                         const SampleCounts *counts = nullptr, unsigned long long *lb_desc = nullptr,
                         uint32_t lb_tag = 0, int *leaf = nullptr, float *t = nullptr, int *ray_of = nullptr,
-                        int *m_out = nullptr);  // with the compaction: M on the device
+                        int *m_out = nullptr,  // with the compaction: M on the device
+                        const int *nv_rank = nullptr, const int *col0_rank = nullptr);  // intersect_ranked's copies
 // whether a query of r rays runs its statistics / rank pass and its sample
 // scan by look-back (up to kLbMaxRays rays), and its descriptor granules
 constexpr int64_t kLbMaxRays = 16384;  // 4 rays per workgroup, <= 64 · 64 workgroups (lookback.h)
@@ -185,7 +186,8 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr,
-                     unsigned long long *lb_desc = nullptr, uint32_t lb_tag = 0);
+                     unsigned long long *lb_desc = nullptr, uint32_t lb_tag = 0,
+                     int *nv_rank = nullptr, int *col0_rank = nullptr);  // look-back: by-rank hit count, first id
 
 // data-parallel query (svo_query.hip): rows of the slot-0 count table for a
 // union batch of at most max_rays_global rays; the words one rank
@@ -198,12 +200,12 @@ constexpr int kDistWordsPerRank = 8;
 int dist_slot0_rows(int64_t max_rays_global);
 int dist_count_words(int max_rays_rank);
 int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
-              const int *ray_nv, int *out);
+              const int *ray_nv, int *out, const int *nv_rank = nullptr);
 int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table);
 int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                 const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
-                int *offsets);
+                int *offsets, const int *nv_rank = nullptr, const int *col0_rank = nullptr);
 int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, double *sums);
 // this rank's words of the second gather: in[0] = S_max of its rows; given
 // the GT depths, in[1..7] += n_valid, Σ front / Σ sdf-band over the valid

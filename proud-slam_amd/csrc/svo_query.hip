@@ -253,10 +253,30 @@ __device__ unsigned long long psvo_g_is_stamps[kIsStampRays][8];
 #define IS_DECL unsigned long long is_t0 = 0, is_ta = 0, is_tb = 0, is_acc[5] = {0, 0, 0, 0, 0}, is_lr = 0
 #define IS_MARK(var) IS_T(var)
 #define IS_ADD(k, from, to) is_acc[k] += (to) - (from)
+// k_sample_fused per workgroup (s_memrealtime, 100 MHz — one clock for all
+// CUs): [0] entry, [1] its rays sampled (wave 0), [2] the row stores drained
+// + barrier, [3] the look-back's prefix known (wave 0), [4] compaction done
+__device__ unsigned long long psvo_g_smp_stamps[4096][8];
+#define SMP_T(k)                                                                          \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                   \
+        if ((threadIdx.x & 63) == 0 && w == 0) psvo_g_smp_stamps[blockIdx.x & 4095][k] = t_; \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+    } while (0)
+#define SMP_T0(k)                                                                         \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                   \
+        if (threadIdx.x == 0) psvo_g_smp_stamps[blockIdx.x & 4095][k] = t_;               \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+    } while (0)
 #else
 #define IS_DECL
 #define IS_MARK(var)
 #define IS_ADD(k, from, to)
+#define SMP_T(k)
+#define SMP_T0(k)
 #endif
 
 struct KeyLds {
@@ -428,7 +448,8 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
                                                           float *__restrict__ ray_dsum, int *__restrict__ stats,
                                                           int *__restrict__ blk_out, int *__restrict__ ray_rank,
                                                           int *__restrict__ rank_ray, unsigned long long *lb_desc,
-                                                          uint32_t lb_tag) {
+                                                          uint32_t lb_tag, int *__restrict__ nv_rank,
+                                                          int *__restrict__ col0_rank) {
     // lb_desc != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
     // runs in this launch by decoupled look-back (lookback.h): each workgroup
     // ranks its own hit rays, the last one writes P / R_hit / max ⌈Σ/step⌉
@@ -439,7 +460,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     const float half = voxel_size * 0.5f;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int visits = 0, rounds = 0;
-    int w_nv = 0, w_mc = 0;  // this wave's ray: valid hits, ⌈Σ/step⌉ (lane 0)
+    int w_nv = 0, w_mc = 0, w_c0 = -1;  // this wave's ray: valid hits, ⌈Σ/step⌉ (lane 0), first hit's id
     bool overflow_stack = false, spill = false;
     if (r < n_rays) {
         IS_DECL;
@@ -641,6 +662,11 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
             }
         }
         nv = wave_sum(nv);
+        {  // the first (nearest) hit's voxel id, for the sampler's by-rank copy
+            const uint64_t m0 = __ballot(lane < nl && rank == 0 && !(ti > max_distance));
+            const int c0 = __builtin_amdgcn_readlane(lane < nl ? S.lidx[lane] : -1, m0 ? __ffsll((unsigned long long)m0) - 1 : 0);
+            w_c0 = m0 ? c0 : -1;
+        }
         for (int l = nv + lane; l < kMaxHits; l += kWave) {
             hit_idx[r * kMaxHits + l] = -1;
             hit_t0[r * kMaxHits + l] = max_distance;
@@ -672,7 +698,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
     // at the memory side)
     __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves], blk_rd[kIsWaves];
-    __shared__ int blk_nv[kIsWaves], blk_mc[kIsWaves];
+    __shared__ int blk_nv[kIsWaves], blk_mc[kIsWaves], blk_c0[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
@@ -682,6 +708,7 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
         blk_rd[threadIdx.x / kWave] = rounds;  // wave-uniform
         blk_nv[threadIdx.x / kWave] = w_nv;
         blk_mc[threadIdx.x / kWave] = w_mc;
+        blk_c0[threadIdx.x / kWave] = w_c0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -723,7 +750,13 @@ __global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const 
     if (lane < kIsWaves && rr < n_rays) {  // an abandoned wait (!ok) leaves `ex` undefined: no rank stores
         const int rk = (int)ex[0] + __popcll(hm & below);
         ray_rank[rr] = (nv_l > 0 && ok) ? rk : -1;
-        if (nv_l > 0 && ok) rank_ray[rk] = (int)rr;
+        if (nv_l > 0 && ok) {
+            rank_ray[rk] = (int)rr;
+            if (nv_rank) {  // by rank: the sampler's reads of other rows, one load each
+                nv_rank[rk] = nv_l;
+                col0_rank[rk] = blk_c0[lane];
+            }
+        }
     }
     if (lane == 0 && blockIdx.x == gridDim.x - 1) {  // the stats words were zeroed by the last read-back
         stats[PSVO_STAT_P] = (int)max(ex[1], agg[1]);
@@ -1045,6 +1078,7 @@ struct FusedRows {
         return (int64_t)rank_ray[real(lrow) - row_begin] * kMaxHits + col;
     }
     __device__ int idx_at(int e) const {
+        if (fast) return e < P ? hit_idx[own_base + e] : next_c0;  // beyond the own row only (row + 1, col 0) is read
         if (slot0) {
             const int lrow = base_row + (jj * P + e) / P;
             if (lrow < row_begin || lrow >= row_end) return next_col0;  // only (own row + 1, col 0) is read
@@ -1053,6 +1087,7 @@ struct FusedRows {
     }
     __device__ int idx_slot0(int col) const {
         // the slot-0 row's valid hits are its prefix [0, nv): only "== -1" is asked
+        if (fast) return col < slot0_nv ? 0 : -1;
         if (slot0) return col < slot0[slot0_row] ? 0 : -1;
         return hit_idx[(int64_t)rank_ray[real(base_row)] * kMaxHits + col];
     }
@@ -1082,6 +1117,11 @@ struct FusedRows {
     const int *slot0 = nullptr;  // [200 · nch] valid hits of each launch chunk's slot-0 row
     int slot0_row = 0;           // table row of (block, chunk)
     int row_begin = 0, row_end = 0, next_col0 = -1;
+    // the engine's launches (the by-rank copies of the traversal: hit count
+    // and first id per rank): the two reads of other rows preloaded with the
+    // ray's own row — no rank → ray → row chain
+    bool fast = false;
+    int slot0_nv = 0, next_c0 = -1;
 };
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
@@ -1202,6 +1242,7 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
     const uint64_t inval = __ballot(own && lane >= 1 && idx_b == -1);
     const int nb = inval ? min(__ffsll((unsigned long long)inval) - 1, max_hits) : max_hits;
     // hcdf_b: the serial running sum, same order of float additions
+    SMP_T0(5);
     float acc = 0.0f, hcdf_b = 0.0f;
     for (int k = 0; k < nb; ++k) {
         const float pk = __shfl(prob_b, k, kWave);
@@ -1227,6 +1268,7 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
     W.idx[lane] = idx_b;
     W.c[lane] = c_b;
     wave_lds_sync();
+    SMP_T0(6);
     const int cs_end = W.c[nb - 1];  // first cs past the last valid bin
     const bool done = cs_end < total_steps;
     const int cs_lim = done ? cs_end : total_steps;
@@ -1264,6 +1306,7 @@ __device__ int sample_wave(const Rows &rows, float steps_j, int max_hits, int nu
             emit(cs + b, W.idx[b], (z + z_low) * 0.5f, z - z_low);
         }
     }
+    SMP_T0(7);
     // ends of the bins the main loop passed
     const int b_last = total_steps > 0 && !done ? bin_of(total_steps - 1) : 0;
     const int n_ends = done ? nb : b_last;
@@ -1344,9 +1387,10 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 float step_size, const float *__restrict__ noise, uint64_t seed,
                                                 int *__restrict__ stats, int *__restrict__ s_idx,
                                                 float *__restrict__ s_depth, float *__restrict__ s_dist,
-                                                const int *__restrict__ slot0, int slot0_nch, int &il_out,
-                                                WaveBins &W, const SampleTail &tl, int &cnt_word, int *stage_i,
-                                                float *stage_z);
+                                                const int *__restrict__ slot0, int slot0_nch,
+                                                const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
+                                                int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
+                                                int *stage_i, float *stage_z);
 
 __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
@@ -1359,7 +1403,8 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
                                                       int *__restrict__ stats, int *__restrict__ s_idx,
                                                       float *__restrict__ s_depth, float *__restrict__ s_dist,
                                                       int *__restrict__ ray_ns, const int *__restrict__ slot0,
-                                                      int slot0_nch, SampleTail tl) {
+                                                      int slot0_nch, SampleTail tl, const int *__restrict__ nv_rank,
+                                                      const int *__restrict__ col0_rank) {
     __shared__ WaveBins bins_all[4];
     // look-back mode (the engine's single-GPU query: row_begin 0, all rows):
     // the rows of this batch, read before any workgroup can re-zero `stats`
@@ -1370,6 +1415,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     __shared__ int stage_i[4][kSmpStage];
     __shared__ float stage_z[4][kSmpStage];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    SMP_T(0);
     const bool compact = tl.desc && tl.leaf;
     // the statistics words for the read-back, loaded now (the traversal's
     // are final; the one flag this launch adds is derived, not re-read):
@@ -1378,8 +1424,9 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
     int il = 0, cnt_word = 0;
     const int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
                                        ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
-                                       slot0_nch, il, bins_all[w], tl, cnt_word, compact ? stage_i[w] : nullptr,
-                                       compact ? stage_z[w] : nullptr);
+                                       slot0_nch, nv_rank, col0_rank, il, bins_all[w], tl, cnt_word,
+                                       compact ? stage_i[w] : nullptr, compact ? stage_z[w] : nullptr);
+    SMP_T(1);
     if (!tl.desc) {  // k_scan_samples reads them after the launch
         if (count >= 0 && lane == 0) {
             ray_ns[il] = count;
@@ -1393,15 +1440,21 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
         s_ns[w] = count;  // -1: no row
         s_cw[w] = cnt_word;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have landed (read back below)
+    // the counts publish before the rows' stores drain: a workgroup's
+    // successors wait for its aggregate, not for its stores (measured: the
+    // drain in front of the look-back cost up to 7 µs at the launch's tail)
     __syncthreads();
+    SMP_T(2);
     if (w == 0) {
         if (tl.c.gt_depth)
             scan_samples_lb<8>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
         else
             scan_samples_lb<2>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
     }
+    SMP_T(3);
     if (!compact) return;
+    // a row longer than the LDS stage is re-read below: this wave's own stores first
+    if (count > kSmpStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // k_compact_rays' work: the row's valid prefix to its compacted place —
     // the first kSmpStage samples from LDS, the rest (rows longer than that)
@@ -1416,6 +1469,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
         tl.t[off + s] = st ? stage_z[w][s] : ld_wt(od + s);
         tl.ray_of[off + s] = il;
     }
+    SMP_T(4);
 }
 
 __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
@@ -1425,12 +1479,17 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 float step_size, const float *__restrict__ noise, uint64_t seed,
                                                 int *__restrict__ stats, int *__restrict__ s_idx,
                                                 float *__restrict__ s_depth, float *__restrict__ s_dist,
-                                                const int *__restrict__ slot0, int slot0_nch, int &il_out,
-                                                WaveBins &W, const SampleTail &tl, int &cnt_word, int *stage_i,
-                                                float *stage_z) {
+                                                const int *__restrict__ slot0, int slot0_nch,
+                                                const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
+                                                int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
+                                                int *stage_i, float *stage_z) {
     const int P = stats[PSVO_STAT_P];
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
+    // the engine's launches (row_begin 0, or a data-parallel rank's own rows
+    // indexed locally): the ray's rank → ray read beside the statistics words
+    const int il_s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int orig_s = (nv_rank && il_s < r_hit_cap) ? rank_ray[il_s] : 0;
     if (slot0) {  // data-parallel engine: the rank's rows, local rank_ray / hit arrays
         row_begin = stats[PSVO_STAT_ROW_BEGIN];
         n_rows = stats[PSVO_STAT_R_HIT_LOCAL];
@@ -1448,7 +1507,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     const int c = j / kSamplerChunk;
     const int jj = j - c * kSamplerChunk;
     const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
-    const int orig = slot0 ? rank_ray[il] : rank_ray[i];
+    const int orig = nv_rank ? orig_s : slot0 ? rank_ray[il] : rank_ray[i];
     const float dsum = ray_dsum[orig];
     FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj,
                    (int64_t)orig * kMaxHits, dsum};
@@ -1462,6 +1521,16 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
         rows.row_begin = (int)row_begin;
         rows.row_end = (int)(row_begin + n_rows);
         rows.next_col0 = stats[PSVO_STAT_NEXT_COL0];
+    }
+    if (nv_rank) {  // the two reads of other rows, beside the own row's loads
+        rows.fast = true;
+        if (slot0) {
+            rows.slot0_nv = slot0[rows.slot0_row];
+            rows.next_c0 = il + 1 < n_rows ? col0_rank[il + 1] : rows.next_col0;
+        } else {
+            rows.slot0_nv = nv_rank[rows.base_row];  // base_row <= i < R_hit
+            rows.next_c0 = col0_rank[i + 1 < r_hit ? i + 1 : 0];
+        }
     }
     const float steps_j = __fdiv_rn(dsum, step_size);
     const int cap = max_steps < max_steps_cap ? max_steps : max_steps_cap;
@@ -1825,7 +1894,7 @@ constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id o
 // this rank's words: thread t packs the hit counts of its hit rows 4t..4t+3
 __global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
                                                    const int *__restrict__ hit_idx, const int *__restrict__ ray_nv,
-                                                   int *__restrict__ out) {
+                                                   int *__restrict__ out, const int *__restrict__ nv_rank) {
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
@@ -1839,7 +1908,8 @@ __global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats
     const int j0 = 4 * t;
     if (j0 >= r_hit) return;
     uint32_t w = 0;
-    for (int k = 0; k < 4 && j0 + k < r_hit; ++k) w |= (uint32_t)ray_nv[rank_ray[j0 + k]] << (8 * k);  // nv <= 50
+    for (int k = 0; k < 4 && j0 + k < r_hit; ++k)  // nv <= 50
+        w |= (uint32_t)(nv_rank ? nv_rank[j0 + k] : ray_nv[rank_ray[j0 + k]]) << (8 * k);
     out[kDistWords + t] = (int)w;
 }
 
@@ -1960,7 +2030,8 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     hipStream_t st = as_stream(stream);
     psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
-                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr, nullptr, 0u);
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr, nullptr, 0u,
+                       nullptr, nullptr);
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
@@ -1978,7 +2049,7 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
                        max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
-                       nullptr, nullptr, 0u);
+                       nullptr, nullptr, 0u, nullptr, nullptr);
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
@@ -2002,7 +2073,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size,
                         const float *noise, uint64_t seed, int *stats, int *s_idx, float *s_depth, float *s_dist,
                         int *ray_ns, int *offsets, unsigned long long *host, int seq, const SampleCounts *counts, unsigned long long *lb_desc, uint32_t lb_tag, int *leaf,
-                        float *t, int *ray_of, int *m_out) {
+                        float *t, int *ray_of, int *m_out, const int *nv_rank, const int *col0_rank) {
     PSVO_REQUIRE(r_hit_cap > 0 && max_steps_cap > 0 && offsets && ray_ns && host,
                  "sample_rays_to_host: bad arguments");
     PSVO_REQUIRE(!lb_desc || (r_hit_cap <= kLbMaxRays && lb_tag != 0), "sample_rays_to_host: look-back arguments");
@@ -2023,7 +2094,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     }
     psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
-                       s_dist, ray_ns, nullptr, 0, tl);
+                       s_dist, ray_ns, nullptr, 0, tl, nv_rank, col0_rank);
     if (!lb_desc)
         psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, -1, r_hit_cap, ray_ns, offsets, stats, 0,
                            host, seq, tl.c);
@@ -2041,8 +2112,10 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray, const PackRec *packed, int *blk_out, unsigned long long *lb_desc,
-                     uint32_t lb_tag) {
+                     uint32_t lb_tag, int *nv_rank, int *col0_rank) {
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
+    PSVO_REQUIRE((nv_rank == nullptr) == (col0_rank == nullptr) && (!nv_rank || lb_desc),
+                 "intersect_ranked: the by-rank copies come with the look-back pass");
     PSVO_REQUIRE(step_size > 0.0f && voxel_size > 0.0f, "intersect_ranked: step/voxel must be > 0");
     PSVO_REQUIRE(!lb_desc || (n_rays <= kLbMaxRays && lb_tag != 0), "intersect_ranked: look-back arguments");
     if (n_rays == 0) return PSVO_OK;
@@ -2052,12 +2125,12 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
         psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
-                           lb_tag);
+                           lb_tag, nv_rank, col0_rank);
     else
         psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
-                           lb_tag);
+                           lb_tag, nv_rank, col0_rank);
     if (!lb_desc)
         psvo::launch(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
                            ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
@@ -2072,9 +2145,9 @@ int dist_slot0_rows(int64_t max_rays_global) {
 }
 int dist_count_words(int max_rays_rank) { return kDistWords + (max_rays_rank + 3) / 4; }
 int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
-              const int *ray_nv, int *out) {
+              const int *ray_nv, int *out, const int *nv_rank) {
     psvo::launch(k_dist_pack, dim3((int)div_up(div_up(R, 4), 256) + (R == 0)), dim3(256), 0, st, stats, rank_ray,
-                 hit_idx, ray_nv, out);
+                 hit_idx, ray_nv, out, nv_rank);
     return check_launch("dist_pack");
 }
 int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table) {
@@ -2085,11 +2158,11 @@ int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride,
 int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                 const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
-                int *offsets) {
+                int *offsets, const int *nv_rank, const int *col0_rank) {
     if (r_hit_cap == 0) return PSVO_OK;
     psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
-                       s_dist, ray_ns, table, nch, SampleTail{});
+                       s_dist, ray_ns, table, nch, SampleTail{}, nv_rank, col0_rank);
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
                        nullptr, 0, SampleCounts{});
     return check_launch("dist_sample");
@@ -2119,7 +2192,8 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
     hipStream_t st = as_stream(stream);
     psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
-                       s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{});
+                       s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{}, static_cast<const int *>(nullptr),
+                       static_cast<const int *>(nullptr));
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, row_begin, n_rows, r_hit_cap, ray_ns, offsets,
                        stats, 0, nullptr, 0, SampleCounts{});
     return check_launch("sample_rays");
@@ -2175,6 +2249,13 @@ int compact_rays(hipStream_t st, int64_t r_hit, int cap, const int *s_idx, const
 }  // namespace psvo
 
 #ifdef PSVO_IS_STAMPS
+extern "C" int psvo_debug_smp_stamps(void *dst, int64_t bytes) {
+    if (bytes < (int64_t)sizeof(psvo::psvo_g_smp_stamps)) return -1;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(psvo::psvo_g_smp_stamps), sizeof(psvo::psvo_g_smp_stamps)) ==
+                   hipSuccess
+               ? 0
+               : -2;
+}
 extern "C" int psvo_debug_is_stamps(void *dst, int64_t bytes) {
     if (bytes < (int64_t)sizeof(psvo::psvo_g_is_stamps)) return -1;
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(psvo::psvo_g_is_stamps), sizeof(psvo::psvo_g_is_stamps)) == hipSuccess ? 0 : -2;
