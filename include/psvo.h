@@ -563,8 +563,9 @@ int psvo_engine_set_timing(psvo_engine *e, int on);        /* resets the accumul
                                                            on one stream, 2: as run (side streams overlap) */
 int psvo_engine_timing(psvo_engine *e, double *mean_ms);   /* mean ms per region, -1 if none */
 /* The iteration period as the GPU runs it: with max_steps > 0 every mapping
- * step records an event on the caller's stream once its forward's first
- * kernels are queued (the same point of every step; up to max_steps;
+ * step records an event after its optimiser step, on the stream that runs it
+ * (the caller's, or the engine's aux stream for a look-ahead step's split
+ * tail: the same point of every step; up to max_steps;
  * resets the count; 0 turns it off); psvo_engine_clock gives the mean time
  * between the first and the last recorded event per step (-1 if fewer than
  * two) — synchronises on the last event. */

@@ -324,12 +324,21 @@ inline double now_ns() {
     clock_gettime(CLOCK_MONOTONIC, &t);
     return t.tv_sec * 1e9 + t.tv_nsec;
 }
-int join_adam(psvo_engine *e, hipStream_t st, const char *who) {
+// host_wait_us > 0: first poll the event from the host for up to that long
+// (the device-sized forward is queued while the query still runs: a host
+// that waits for the optimiser here keeps the cross-queue barrier — ≈ 20 µs
+// of idle GPU between the sampler and the interpolation, measured — out of
+// the stream)
+int join_adam(psvo_engine *e, hipStream_t st, const char *who, double host_wait_us = 0.0) {
     if (!e->adam_pending) return PSVO_OK;
     // already done (the usual case: the optimiser step ran beside the query):
     // no barrier packet in front of the interpolation — the command processor
     // resolves even a satisfied cross-queue wait with a few µs of latency
-    const hipError_t q = hipEventQuery(e->adam_done);
+    hipError_t q = hipEventQuery(e->adam_done);
+    if (q == hipErrorNotReady && host_wait_us > 0.0) {
+        const double t_end = now_ns() + host_wait_us * 1e3;
+        while (q == hipErrorNotReady && now_ns() < t_end) q = hipEventQuery(e->adam_done);
+    }
     if (q == hipSuccess) {
         e->adam_pending = false;
         return PSVO_OK;
@@ -1063,7 +1072,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         ENG_BUF(float, se, kSdfS, m_early * sizeof(float));
         feat_e = fe;
         sdf_e = se;
-        ENG_CALL(join_adam(e, st, who));
+        ENG_CALL(join_adam(e, st, who, 2000.0));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
         ENG_CALL(psvo::interp_fwd_dev(st, m_early, m_dev, d->voxel_size, static_cast<const int *>(qset.a.p[kLeafQ]),
                                       static_cast<const float *>(qset.a.p[kTQ]),
@@ -1384,10 +1393,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // the sparse decoder: render runs the sdf trunk only
     const bool sparse_dec = !(e->paths & PSVO_PATH_DENSE_DECODER);
     ENG_CALL(render(e, st, d, *qset, rays_o, rays_d, true, stats_out, "map_step", q, true, need_z, sparse_dec));
-    // the step clock's marker: behind the forward's first kernels on st (a
-    // marker between the query and the interpolation delays the latter)
-    if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
+    // (the step clock's marker is recorded after the optimiser step, below:
+    // on st between two dependent kernels a marker costs ≈ 5 µs, measured)
     if (q.z_recorded && hipStreamWaitEvent(ax, e->z_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
     const int64_t M = q.m;
@@ -1576,6 +1583,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         e->grads_clean = false;
         ENG_CALL(guard.release());
         if (!(flags & PSVO_STEP_NO_ADAM)) ENG_CALL(map_adam(st, d, grads, adam_step));
+        if (e->clk.on && e->clk.n < (int)e->clk.ev.size() && hipEventRecord(e->clk.ev[e->clk.n++], st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
         return PSVO_OK;
     }
     // width 128: the interpolation backward runs inside the fused decoder
@@ -1677,6 +1686,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     } else {
         ENG_CALL(pose_adam(st, d, pa));
     }
+    // the step clock: after the optimiser step, on the stream that ran it (a
+    // look-ahead step's: aux, where nothing waits behind the marker) — the
+    // same point of every step
+    if (e->clk.on && e->clk.n < (int)e->clk.ev.size() &&
+        hipEventRecord(e->clk.ev[e->clk.n++], (split && !(flags & PSVO_STEP_NO_ADAM)) ? ax : st) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "map_step: event record failed");
     // split tail: loss_out is written on the loss stream; the caller reads it
     // on st (the loss pass ends long before the look-ahead's pose step, so
     // this wait, queued behind the look-ahead, costs nothing).  The weights
