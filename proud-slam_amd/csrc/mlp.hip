@@ -799,27 +799,29 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, cons
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
     float *w2 = lds + kF2Buf0;
-    int64_t t = blockIdx.x;
+    // the balanced split of k_mlp_fwd2 / k_mlp_trunk2: workgroup b owns the
+    // 32-sample tiles [u0, u1), wave w the tiles u0 + w, u0 + w + 8, …
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
     float xn[8];
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_x(feat, s, s < m, h, xn);
+        const int64_t s = (u0 + wave) * kTileS + (lane & 31);
+        load_x(feat, s, u0 + wave < u1 && s < m, h, xn);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
     stage8(w2, img + kImgF2, 16384, wave, lane);
     wait_vm(0);
     raw_barrier();
-    for (; t < n_wg_tiles; t += gridDim.x) {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
+    for (int64_t u = u0 + wave; u < u1; u += kF2Waves) {  // no barriers below
+        const int64_t s = u * kTileS + (lane & 31);
         const bool valid = s < m;
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = xn[i];
-        if (t + gridDim.x < n_wg_tiles) {
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+        if (u + kF2Waves < u1) {
+            const int64_t sn = (u + kF2Waves) * kTileS + (lane & 31);
             load_x(feat, sn, sn < m, h, xn);
         }
         f32x16 a[kNB], bacc[kNB];
@@ -852,31 +854,35 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk2(const int *__restr
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
-    const int64_t n_wg_tiles = (m + kF2Tile - 1) / kF2Tile;
     const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples): the layout k_mlp_bwd3t reads
     const int64_t tstride = n_tiles * 32 * 128;
     const int64_t tbytes = tstride * 4;
     float *w2 = lds + kF2Buf0;
-    int64_t t = blockIdx.x;
+    // k_mlp_fwd2's balanced split: workgroup b owns the 32-sample tiles
+    // [u0, u1), wave w the tiles u0 + w, u0 + w + 8, … — the waves sharing a
+    // SIMD (w, w + 4) then hold floor / ceil of the average, where a split by
+    // whole 256-sample workgroup tiles left a third of the SIMDs with twice
+    // the work at this kernel's sizes (≈ 1.4 tiles per workgroup)
+    const int64_t n_units = (m + kTileS - 1) / kTileS;
+    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
     float xn[8];
     {
-        const int64_t s = t * kF2Tile + wave * 32 + (lane & 31);
-        load_x(feat, s, s < m, h, xn);
+        const int64_t s = (u0 + wave) * kTileS + (lane & 31);
+        load_x(feat, s, u0 + wave < u1 && s < m, h, xn);
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
     stage8(w2, img + kImgF2, 16384, wave, lane);
     wait_vm(0);
     raw_barrier();
-    for (; t < n_wg_tiles; t += gridDim.x) {
-        const int64_t u = t * kF2Waves + wave;  // this wave's 32-sample CF tile
+    for (int64_t u = u0 + wave; u < u1; u += kF2Waves) {  // this wave's 32-sample CF tiles (no barriers below)
         const int64_t s = u * kTileS + (lane & 31);
         const bool valid = s < m;
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = xn[i];
-        if (t + gridDim.x < n_wg_tiles) {
-            const int64_t sn = (t + gridDim.x) * kF2Tile + wave * 32 + (lane & 31);
+        if (u + kF2Waves < u1) {
+            const int64_t sn = (u + kF2Waves) * kTileS + (lane & 31);
             load_x(feat, sn, sn < m, h, xn);
         }
         const CfStore cfs(u, lane, n_tiles);
