@@ -456,6 +456,8 @@ struct SelectArgs {
     float4 *feat_c;          // [2 cap][16]: class A rows at [0, M_A), class B at [cap, cap + M_B)
     int *leaf_c, *ray_of_c;  // [2 cap]
     float *t_c;
+    float *rgb_c;            // [2 cap][3] (split): class B's colours, written 0 (their weights are 0;
+                             // the fused trunk kernel computes no colour head)
     int64_t cap;             // class B's base index (the step's sample count M)
     int split;
     int *counts;             // [0] M_A, [1] M_B, [2] flags (look-back abandoned: bit 3), [3] pad, then u64
@@ -615,6 +617,10 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
                 a.ray_of_c[j] = (int)r;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) a.feat_c[j * 4 + q] = a.feat[src * 4 + q];
+                if (in_b) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) a.rgb_c[j * 3 + k] = 0.f;
+                }
             }
             ba += __popcll(bal_a);
             bb += __popcll(bal_b);
@@ -686,16 +692,18 @@ int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncat
                          const int *offsets, const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray,
                          const float *gt_depth, const float *sdf_s, const float *feat, const int *leaf, const float *t,
                          const int *ray_of, int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c,
-                         int *leaf_c, float *t_c, int *ray_of_c, int *counts, unsigned long long *desc, uint32_t tag) {
+                         int *leaf_c, float *t_c, int *ray_of_c, float *rgb_c, int *counts, unsigned long long *desc,
+                         uint32_t tag) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0 && cap > 0,
                  "select_samples: bad sizes");
-    PSVO_REQUIRE(!split || offb != nullptr, "select_samples: the split needs class B's offsets");
+    PSVO_REQUIRE(!split || (offb != nullptr && rgb_c != nullptr),
+                 "select_samples: the split needs class B's offsets and colour rows");
     const int rpw = select_rays_per_wave(r_hit);
     PSVO_REQUIRE(rpw <= kSelMaxRpw, "select_samples: %lld hit rays exceed the selection's %d",
                  (long long)r_hit, kSelWaves * kSelMaxRpw * kLbMaxBlocks);
     if (r_hit == 0) return PSVO_OK;
     SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offa, offb,
-                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, cap, split ? 1 : 0, counts, desc, tag};
+                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, rgb_c, cap, split ? 1 : 0, counts, desc, tag};
     psvo::launch(k_select_samples, dim3(div_up(r_hit, (int64_t)kSelWaves * rpw)), dim3(64 * kSelWaves), 0, st, r_hit,
                  rpw, s_max, truncation, max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_depth, sdf_s, a);
     return check_launch("select_samples");

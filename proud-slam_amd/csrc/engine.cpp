@@ -36,7 +36,7 @@ enum Slot {
     // the sparse decoder (select_samples): compact index, ray offsets, the kept samples' rows, counts, look-back
     kCidx, kOffB, kFeatB, kLeafB, kTB, kRayOfB, kSdfB, kSelCnt, kSelDesc,
     // its class B (the trunk only): ray offsets, activations and masks
-    kOffB2, kActB, kMasksB, kSlots
+    kOffB2, kSlots
 };
 
 struct Arena {
@@ -1412,15 +1412,13 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // get compact indices (composite.hip k_select_samples) — class A
     // (composited) at [0, M_A): the whole decoder forward; width 128, class B
     // (only the direct sdf loss term) at [M, M + M_B): the trunk's
-    // activations (k_mlp_trunk2) — sized on the device (the counts never
+    // forward + backward in one kernel (k_mlp_trunk_fb) — sized on the device (the counts never
     // reach the host)
     float *const *W = d->dec;
     Render qb = q;  // what the loss pass and the backward read per sample: the kept samples when sparse
     int *cidx = nullptr, *sel_cnt = nullptr;
     const bool two_class = q.sparse && d->width == 128;
     int *offb = nullptr;
-    float *act_b = nullptr;
-    uint64_t *masks_b = nullptr;
     if (q.sparse && !empty) {
         const int64_t M2 = 2 * M;  // the compact rows: class A at [0, M), class B at [M, 2 M)
         ENG_BUF(int, cx, kCidx, M * sizeof(int));
@@ -1442,25 +1440,19 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             ENG_BUF(int, ob, kOffB2, (size_t)(r_hit + 1) * sizeof(int));
             offb = ob;
         }
+        ENG_BUF(float, rgb_c, kRgbS, M2 * 3 * sizeof(float));
         e->sel_tag = e->sel_tag == 0xffffffffu ? 1u : e->sel_tag + 1u;
         mark(e, st, PSVO_TIME_SELECT, 0);
         ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                       q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, M,
-                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, cnt, desc, e->sel_tag));
+                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, rgb_c, cnt, desc,
+                                      e->sel_tag));
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
-        ENG_BUF(float, rgb_c, kRgbS, M2 * 3 * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
         ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
         ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_c, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                                   q.images, sdf_b, rgb_c, act, masks, cnt));
-        if (two_class) {
-            ENG_BUF(float, ab, kActB, (size_t)psvo_mlp_act_floats(M, d->width) / 2 * sizeof(float));  // h1, h2
-            ENG_BUF(uint64_t, mb, kMasksB, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
-            ENG_CALL(psvo::mlp_fwd_trunk(st, M, cnt + 1, feat_c + M * 16, q.images, ab, mb, rgb_c + M * 3));
-            act_b = ab;
-            masks_b = mb;
-        }
         mark(e, st, PSVO_TIME_MLP_FWD, 1);
         qb.offsets = offa;
         qb.leaf = leaf_c;
@@ -1612,12 +1604,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // the sparse decoder's class B: its rows at [M, 2 M) of the compact arrays
     const psvo::InterpFuse ipf_b{qb.leaf + M, qb.ray_of + M, q.rank_ray, d->vertex_idx, qb.tt + M, rays_o, rays_d,
                                  d->centres, d->emb, d->voxel_size, grad_emb, gx ? gx + 3 * M : nullptr, mark_into};
-    const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, masks_b, g_sdf_s + M, qb.feat + M * 16, act_b,
+    const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, g_sdf_s + M, qb.feat + M * 16,
                              fuse_ib ? &ipf_b : nullptr};
     ENG_CALL(mlp_bwd(st, M, d->width, qb.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      qb.rgb_s, qb.act, qb.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6],
                      G[7], G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr,
-                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt, act_b ? &tbw : nullptr));
+                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt, two_class ? &tbw : nullptr));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     if (overlap) e->bwd_recorded = true;  // mlp_bwd recorded dfeat_ready on st
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce
@@ -1632,8 +1624,8 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (fuse_ib) {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);
         ENG_CALL(psvo::interp_rays_gx(eb, q.r_hit, qb.offsets, q.rank_ray, qb.tt, gx, grad_od, grad_od + R * 3,
-                                      act_b ? offb : nullptr, act_b ? qb.tt + M : nullptr,
-                                      act_b ? gx + 3 * M : nullptr));
+                                      two_class ? offb : nullptr, two_class ? qb.tt + M : nullptr,
+                                      two_class ? gx + 3 * M : nullptr));
         mark(e, eb, PSVO_TIME_INTERP_BWD, 1);
     } else {
         mark(e, eb, PSVO_TIME_INTERP_BWD, 0);

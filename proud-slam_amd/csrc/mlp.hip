@@ -319,7 +319,11 @@ constexpr int kImgF1 = 0, kImgF2 = kImgF1 + 2048, kImgF3 = kImgF2 + 16384, kImgF
               kImgC3 = kImgC4 + 9 * 8 * 256,  // W3[1:]ᵀ
               kImgC2 = kImgC3 + 8 * 8 * 256,  // W2ᵀ
               kImgC1 = kImgC2 + 8 * 8 * 256,  // W1ᵀ: 1 × 8 blocks
-              kImgTotal = kImgC1 + 8 * 256;   // 107,776 floats
+              // the trunk kernel's forward in the same chain layout (W, not Wᵀ):
+              // lane (m, q) holding W[16ob + m][16kb + 4q .. 4q + 3]
+              kImgT1 = kImgC1 + 8 * 256,    // W1: 8 × 1 blocks
+              kImgT2 = kImgT1 + 8 * 256,    // W2: 8 × 8 blocks
+              kImgTotal = kImgT2 + 8 * 8 * 256;  // 126,208 floats
 
 __device__ __forceinline__ void inv_perm_acc(int pos, int nkb, int &i, int &k) {
     const int c = pos & 3, lane = (pos >> 2) & 63, rest = pos >> 8;
@@ -358,6 +362,15 @@ __global__ __launch_bounds__(256) void k_mlp_prep(MlpParams p, float *__restrict
     if (e >= kImgTotal) return;
     int i, k;
     float v = 0.0f;
+    if (e >= kImgT1) {  // the trunk kernel's forward images: W[o][in], [ob][kb][lane (m, q)][4]
+        const bool t1 = e < kImgT2;
+        const int pos = e - (t1 ? kImgT1 : kImgT2);
+        const int j = pos & 3, ln = (pos >> 2) & 63, blk = pos >> 8;
+        const int nkb = t1 ? 1 : 8;
+        const int o = 16 * (blk / nkb) + (ln & 15), in = 16 * (blk % nkb) + 4 * (ln >> 4) + j;
+        img[e] = t1 ? p.w1[o * 16 + in] : w2[o * 128 + in];
+        return;
+    }
     if (e >= kImgC4) {  // chain16 images: [ob][kb][lane (m, q)][4]
         const int sec = e < kImgC3 ? 4 : e < kImgC2 ? 3 : e < kImgC1 ? 2 : 1;
         const int pos = e - (sec == 4 ? kImgC4 : sec == 3 ? kImgC3 : sec == 2 ? kImgC2 : kImgC1);
@@ -488,7 +501,7 @@ struct DwDst {
     int elem_begin[6];
 };
 
-// slabs_b (or null): k_mlp_bwd3t's slabs (the same layout), whose W1, W2, W3
+// slabs_b (or null): k_mlp_trunk_fb's slabs (the same layout), whose W1, W2, W3
 // row 0 and b3[0] elements are added (the rest of its slabs is not written).
 // A workgroup sums 64 elements: wave k over the k-th quarter of the slabs
 // (batches of 8 independent loads, lane = element: 256-B rows), then the
@@ -800,7 +813,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, cons
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
     float *w2 = lds + kF2Buf0;
-    // the balanced split of k_mlp_fwd2 / k_mlp_trunk2: workgroup b owns the
+    // the balanced split of k_mlp_fwd2: workgroup b owns the
     // 32-sample tiles [u0, u1), wave w the tiles u0 + w, u0 + w + 8, …
     const int64_t n_units = (m + kTileS - 1) / kTileS;
     const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
@@ -833,78 +846,6 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, cons
         (void)relu(bacc);
         const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
         if (valid && h == 0) sdf_out[s] = sdf;
-    }
-    wait_vm(0);
-}
-
-// The sparse decoder's class B (samples with only a loss term on their sdf,
-// composite.hip k_select_samples): the trunk's activations for the trunk
-// backward (k_mlp_bwd3t) — h1 and h2 as CF tiles (matrices 0 and 1 of `act`,
-// the layout k_mlp_fwd2 writes; h1 stored from inside the W2 GEMM), the ReLU
-// masks (m1, m2; the c1 word 0) — and zero colours (the compositing pass
-// reads a colour for every kept sample; these carry weight 0).  The same
-// instruction sequence as k_mlp_sdf2 / k_mlp_fwd2's first two layers: the
-// same h1 / h2 bits.  m: the class's count on the device.
-__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk2(const int *__restrict__ m_dev,
-                                                              const float *__restrict__ feat,
-                                                              const float *__restrict__ img, float *__restrict__ act,
-                                                              uint64_t *__restrict__ masks, float *__restrict__ rgb) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int64_t m = __builtin_amdgcn_readfirstlane(*m_dev);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5;
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples): the layout k_mlp_bwd3t reads
-    const int64_t tstride = n_tiles * 32 * 128;
-    const int64_t tbytes = tstride * 4;
-    float *w2 = lds + kF2Buf0;
-    // k_mlp_fwd2's balanced split: workgroup b owns the 32-sample tiles
-    // [u0, u1), wave w the tiles u0 + w, u0 + w + 8, … — the waves sharing a
-    // SIMD (w, w + 4) then hold floor / ceil of the average, where a split by
-    // whole 256-sample workgroup tiles left a third of the SIMDs with twice
-    // the work at this kernel's sizes (≈ 1.4 tiles per workgroup)
-    const int64_t n_units = (m + kTileS - 1) / kTileS;
-    const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
-    float xn[8];
-    {
-        const int64_t s = (u0 + wave) * kTileS + (lane & 31);
-        load_x(feat, s, u0 + wave < u1 && s < m, h, xn);
-    }
-    stage8(lds, img + kImgVec, kVecPad, wave, lane);
-    stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
-    stage8(w2, img + kImgF2, 16384, wave, lane);
-    wait_vm(0);
-    raw_barrier();
-    for (int64_t u = u0 + wave; u < u1; u += kF2Waves) {  // this wave's 32-sample CF tiles (no barriers below)
-        const int64_t s = u * kTileS + (lane & 31);
-        const bool valid = s < m;
-        float x[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = xn[i];
-        if (u + kF2Waves < u1) {
-            const int64_t sn = (u + kF2Waves) * kTileS + (lane & 31);
-            load_x(feat, sn, sn < m, h, xn);
-        }
-        const CfStore cfs(u, lane, n_tiles);
-        f32x16 a[kNB], bacc[kNB];
-        init_bias(a, lds + kOffB1, h);
-        gemm_x(lds + kF2W1, x, a, lane);
-        const uint64_t m1 = relu(a);
-        init_bias(bacc, lds + kOffB2, h);
-        gemm_acc<kNB, kNB>(w2, a, bacc, lane, CfQueue(cfs, act, tbytes, true, a));  // + h1 stores
-        const uint64_t m2 = relu(bacc);
-        cfs.store(act + tstride, tbytes, bacc);  // h2
-        if (valid) {
-            uint64_t *mk = masks + (s * 2 + h) * 3;
-            mk[0] = m1;
-            mk[1] = m2;
-            mk[2] = 0;
-            if (h == 0) {
-                rgb[s * 3 + 0] = 0.f;
-                rgb[s * 3 + 1] = 0.f;
-                rgb[s * 3 + 2] = 0.f;
-            }
-        }
     }
     wait_vm(0);
 }
@@ -1551,74 +1492,124 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
 }
 
 // ---------------------------------------------------------------------------
-// The trunk backward (the sparse decoder's class B: samples whose only loss
-// term is the direct one on their sdf — composite.hip k_select_samples): the
-// colour head's δ's are exactly zero there (g_rgb = 0, so δ5 = δc1 = δf = 0),
-// so the chain is
-//   δh2 = W3[0]ᵀ dsdf ⊙ m2 (VALU),  δh1 = W2ᵀ δh2 ⊙ m1,  dfeat = W1ᵀ δh1
-// and the weight gradients dW2 += δh2 ⊗ h1, dW1 += δh1 ⊗ x, W3 row 0 +=
-// dsdf ⊗ h2 (+ the biases): 37.1 of k_mlp_bwd3's 107.5 k MACs per sample.
-// The same unit images, operand layouts and chain arithmetic as k_mlp_bwd3
-// (the same per-sample dfeat bits), in two phases per round of four
-// 16-sample units:
+// The sparse decoder's class B (samples whose only loss term is the direct
+// one on their sdf — composite.hip k_select_samples): their colour head's δ's
+// are exactly zero (g_rgb = 0, so δ5 = δc1 = δf = 0), so forward and backward
+// need the trunk only:
+//   h1 = relu(W1 x + b1),  h2 = relu(W2 h1 + b2)                       (forward)
+//   δh2 = W3[0]ᵀ dsdf ⊙ [h2 > 0],  δh1 = W2ᵀ δh2 ⊙ [h1 > 0],  dfeat = W1ᵀ δh1
+//   dW1 += δh1 ⊗ x,  dW2 += δh2 ⊗ h1,  W3 row 0 += dsdf · h2  (+ b1, b2, b3[0])
+// 54 k MACs per sample, in ONE kernel that keeps the activations on chip (no
+// activation round trip through HBM, no separate forward launch: the two
+// measured 57 + 110 µs at config B).  The forward is recomputed here with the
+// chain's 16 × 16 × 4 MFMAs (the sdf came from k_mlp_sdf2: the same values up
+// to the accumulation order, which only the ReLU masks' ties could see).
+// Rounds of four 16-sample units, two phases each:
 //   phase  chain wave c (unit u0 + 4r + c)                         gradient wave d
-//   A      δh2 → LDS (set r & 1), dsdf, x → LDS; δh1 = W2ᵀ δh2    dW1 row block d += δh1(r−1) ⊗ x(r−1);
-//                                                                  h1 / h2 tiles of round r start loading
-//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          dW2 col block d += δh2(r) ⊗ h1(r);
-//          backward (dL/dx, the embedding scatter)                 W3 row 0 (cols of block d) += dsdf(r) · h2(r)
+//   A      x → LDS; h1 (W1) → LDS (CF image); h2 (W2); W3 row 0    dW1 row block d += δh1(r−1) ⊗ x(r−1)
+//          partial (registers); δh2 → LDS; δh1 = W2ᵀ δh2
+//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          dW2 col block d += δh2(r) ⊗ h1(r)
+//          backward (dL/dx, the embedding scatter)                 (both operands from LDS)
 // plus a last phase A for the final round's dW1.  A chain wave and a
-// gradient wave share each SIMD's matrix unit, so the two GEMMs of 128 × 128
-// (W2ᵀ, dW2) sit in different phases: the chain's (latency-bound)
-// interpolation backward overlaps the gradient MFMAs (measured with both in
-// phase A: 31 k cycles per round, the phase at 2 × 8 k MFMA cycles).  Writes one slab per
-// workgroup of W1 (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the
-// DwGrid layout; k_mlp_dw_reduce adds these elements only).  m: the class's
-// sample count on the device.
-constexpr int kT3H2 = kVecPad;                // δh2 images [set 2][unit 4]
-constexpr int kT3H1 = kT3H2 + 2 * 4 * kUImg;  // δh1 images [unit 4]
-constexpr int kT3S = kT3H1 + 4 * kUImg;       // dsdf rows [unit 4][16]
-constexpr int kT3X = kT3S + 4 * kU;           // x images [round parity 2][unit 4][16 × 16]
-constexpr int kT3I = kT3X + 2 * 4 * 16 * kU;  // interpolation backward staging [chain wave 4][512]
-constexpr int kT3A = kT3I + 4 * 512;          // dW1 accumulators [chain wave 4][4][lane 64][4]
-constexpr int kLdsBwd3t = (kT3A + 4 * 1024) * 4;  // 136,448 B
-static_assert(kLdsBwd3t <= 160 * 1024, "bwd3t LDS budget");
+// gradient wave share each SIMD's matrix unit: the chain's forward + W2ᵀ
+// fill phase A, the gradient waves' dW2 overlaps the chain's latency-bound
+// interpolation backward in phase B.  Writes one slab per workgroup of W1
+// (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the DwGrid layout;
+// k_mlp_dw_reduce adds these elements only).  m: the class's count on the device.
+constexpr int kT4H2 = kVecPad;                 // δh2 unit images [unit 4]
+constexpr int kT4H1 = kT4H2 + 4 * kUImg;       // δh1 unit images [unit 4]
+constexpr int kT4CF = kT4H1 + 4 * kUImg;       // h1 as CF tiles [2] (the round's units: slot up → tile up / 2, half up % 2)
+constexpr int kT4X = kT4CF + 2 * kCfTile;      // x images [round parity 2][unit 4][16 × 16]
+constexpr int kT4I = kT4X + 2 * 4 * 16 * kU;   // interpolation backward staging [chain wave 4][512]
+constexpr int kT4A = kT4I + 4 * 512;           // dW1 accumulators [gradient wave 4][4][lane 64][4]
+constexpr int kT4R = kT4A + 4 * 1024;          // W3 row 0 / b3[0] partials [chain wave 4][132]
+constexpr int kLdsTrunk = (kT4R + 4 * 132) * 4;  // 138,304 B
+static_assert(kLdsTrunk <= 160 * 1024, "trunk kernel LDS budget");
+
+// the chain's ReLU: v = max(v, 0) and the mask word mask16 reads (feature
+// 16·ob + 4q + j of the lane's sample ↔ bit 8·ob + j)
+// Σ of v over the 16 lanes of the lane's DPP row (the chain's samples n of one
+// q group), in every lane of the row: quad xor 1, xor 2, half-row mirror, row mirror
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_mov<0x141>(v);  // row_half_mirror
+    v += dpp_mov<0x140>(v);  // row_mirror
+    return v;
+}
+
+__device__ __forceinline__ uint64_t relu16(f32x4v (&v)[8]) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool on = v[ob][j] > 0.0f;
+            w |= (uint64_t)on << (8 * ob + j);
+            v[ob][j] = on ? v[ob][j] : 0.0f;
+        }
+    return w;
+}
+
+// gradient wave, dW2 += δh2 (the round's unit images) ⊗ h1 (the round's CF
+// image in LDS), column block d — dw_job's arithmetic with both operands on chip
+__device__ __forceinline__ void dw_job_lds(const float *dset, const float *cf, int64_t ubase, int64_t u1, int d,
+                                           int lane, f32x16 (&acc)[kNB], float &bsum) {
+    const int i = lane & 31, h = lane >> 5;
+    int ra[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) ra[g] = i * kU + (((2 * h + g) ^ ((i >> 2) & 3)) << 2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int up = q >> 1, g = q & 1;
+        if (ubase + up >= u1) break;  // wave-uniform
+        const float4 b = *reinterpret_cast<const float4 *>(cf + (up >> 1) * kCfTile + cf_voff(d, lane, up & 1, g) / 4);
+        const float *dl = dset + up * kUImg;
+        float4 a[kNB];
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) a[ob] = *reinterpret_cast<const float4 *>(dl + 32 * ob * kU + ra[g]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].x, b.x, acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].y, b.y, acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].z, b.z, acc[ob]);
+#pragma unroll
+        for (int ob = 0; ob < kNB; ++ob) acc[ob] = mfma(a[ob].w, b.w, acc[ob]);
+        const float4 ad = *reinterpret_cast<const float4 *>(dl + 32 * d * kU + ra[g]);
+        bsum += (ad.x + ad.y) + (ad.z + ad.w);
+    }
+}
 
 struct TrunkIn {
-    uint64_t m1, m2;
     float gs;
     float4 x;
 };
-__device__ __forceinline__ void load_trunk_in(const uint64_t *__restrict__ masks, const float *__restrict__ g_sdf,
-                                              const float *__restrict__ feat, int64_t s, bool valid, int q,
-                                              TrunkIn &in) {
+__device__ __forceinline__ void load_trunk_in(const float *__restrict__ g_sdf, const float *__restrict__ feat,
+                                              int64_t s, bool valid, int q, TrunkIn &in) {
     const int64_t sv = valid ? s : 0;
-    const uint64_t *mk = masks + (sv * 2 + (q & 1)) * 3;
-    in.m1 = mk[0];
-    in.m2 = mk[1];
     in.gs = g_sdf[sv];
     in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
 }
 
-__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restrict__ m_dev,
-                                                             const float *__restrict__ img,
-                                                             const uint64_t *__restrict__ masks,
-                                                             const float *__restrict__ g_sdf,
-                                                             const float *__restrict__ feat,
-                                                             const float *__restrict__ act, DwGrid g,
-                                                             float *__restrict__ slabs, InterpFuse ip) {
+__global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__restrict__ m_dev,
+                                                                const float *__restrict__ img,
+                                                                const float *__restrict__ g_sdf,
+                                                                const float *__restrict__ feat, DwGrid g,
+                                                                float *__restrict__ slabs, InterpFuse ip) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int64_t m = __builtin_amdgcn_readfirstlane(*m_dev);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t n_tiles = (m + kCh - 1) / kCh * 2;  // CF tiles (32 samples): k_mlp_trunk2's layout
-    const int64_t tstride = n_tiles * kCfTile;
-    const int64_t tb = tstride * 4;
     const int64_t n_units = (m + kU - 1) / kU;
     const int64_t u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
     const int n_rounds = (int)((u1 - u0 + 3) / 4);
-    auto h2set = [&](int par) { return lds + kT3H2 + (par & 1) * 4 * kUImg; };
-    float *const h1set = lds + kT3H1, *const sset = lds + kT3S;
-    auto xset = [&](int par) { return lds + kT3X + (par & 1) * 4 * 16 * kU; };
+    float *const h2set = lds + kT4H2, *const h1set = lds + kT4H1, *const cf = lds + kT4CF;
+    auto xset = [&](int par) { return lds + kT4X + (par & 1) * 4 * 16 * kU; };
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     wait_vm(0);
     raw_barrier();
@@ -1632,18 +1623,21 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
         const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
         const int c = wave;
         const int n = lane & 15, q = lane >> 4;
-        const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot
+        const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot in a unit image
         const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
+        // the sample's column in the round's CF image (k_mlp_fwd2's layout, as dw_bsrc reads it)
+        const int cf_grp = 4 * (n & 1) + 2 * (c & 1) + (n >> 3), cf_el = (n >> 1) & 3;
+        float *const cf_tile = cf + (c >> 1) * kCfTile;
+        float *const page3 = lds + kT4R + c * 132;  // W3 row 0 (+ b3[0]) partials of this wave's units
+        if (lane < 33) *reinterpret_cast<float4 *>(page3 + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+        float b30p = 0.f;
         TrunkIn nin;
-        // the interpolation backward's sample data one round ahead (leaf, ray,
-        // t), its vertex ids / centre / rank row at the top of phase A: phase B
-        // then waits for one dependent level (the vertex rows, the ray) only
         int lf_n = 0, ro_n = 0;
         float ts_n = 0.f;
         {
             const int64_t u = u0 + c;
             const int64_t s = u * kU + n;
-            load_trunk_in(masks, g_sdf, feat, s, u < u1 && s < m, q, nin);
+            load_trunk_in(g_sdf, feat, s, u < u1 && s < m, q, nin);
             if (fuse && u < u1 && s < m) {
                 lf_n = ip.leaf[s];
                 ro_n = ip.ray_of[s];
@@ -1669,38 +1663,77 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                 for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
                 row = ip.rank_ray[ro];
             }
-            // ---- A: δh2, dsdf, x → LDS; δh1 = W2ᵀ δh2 ⊙ m1; dW1 of the previous round
+            // ---- A: x → LDS; forward h1 → LDS, h2; δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ [h1 > 0]
             f32x4v fa[8];
             uint64_t m1 = 0;
             if (r < n_rounds) {
                 const TrunkIn in = nin;
                 const float dsdf = valid ? in.gs : 0.0f;
-                const int sh = 4 * (q >> 1);
-                m1 = valid ? in.m1 >> sh : 0;
-                const uint64_t m2 = valid ? in.m2 >> sh : 0;
+                const float4 xv = valid ? in.x : make_float4(0.f, 0.f, 0.f, 0.f);
                 float *xl = xset(r) + c * 16 * kU;
-                xl[wb + 0] = valid ? in.x.x : 0.f;
-                xl[wb + 16] = valid ? in.x.y : 0.f;
-                xl[wb + 32] = valid ? in.x.z : 0.f;
-                xl[wb + 48] = valid ? in.x.w : 0.f;
-                if (q == 0) sset[c * kU + sn] = dsdf;
+                xl[wb + 0] = xv.x;
+                xl[wb + 16] = xv.y;
+                xl[wb + 32] = xv.z;
+                xl[wb + 48] = xv.w;
                 if (active) {
+                    f32x4v xin[1] = {f32x4v{xv.x, xv.y, xv.z, xv.w}};
+                    f32x4v hb[8];
+#pragma unroll
+                    for (int ob = 0; ob < 8; ++ob) {
+                        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB1 + 16 * ob + 4 * q);
+                        hb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+                    }
+                    gemm16<1, 8, 1>(wrs, kImgT1, xin, hb, lane);  // h1 = W1 x + b1
+                    m1 = relu16(hb);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {  // h1 → the CF image (dW2's B operand): row 16 ob + 4q + j
+                        // (the row's swizzle (row >> 1) & 7 does not depend on ob)
+                        float *const cj = cf_tile + (4 * q + j) * kTileS + ((cf_grp ^ ((2 * q + (j >> 1)) & 7)) << 2) + cf_el;
+#pragma unroll
+                        for (int ob = 0; ob < 8; ++ob) cj[16 * ob * kTileS] = hb[ob][j];
+                    }
                     f32x4v fb[8];
 #pragma unroll
-                    for (int ob = 0; ob < 8; ++ob) {  // δh2 = W3[0]ᵀ dsdf ⊙ m2 (k_mlp_bwd3's δf = 0 case)
+                    for (int ob = 0; ob < 8; ++ob) {
+                        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
+                        fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+                    }
+                    // h2 = W2 h1 + b2, two rings of 4 output blocks (one ring over all 8 spills)
+                    gemm16<8, 4, 2>(wrs, kImgT2, hb, *reinterpret_cast<f32x4v(*)[4]>(&fb[0]), lane);
+                    gemm16<8, 4, 2>(wrs, kImgT2 + 4 * 8 * 256, hb, *reinterpret_cast<f32x4v(*)[4]>(&fb[4]), lane);
+                    const uint64_t m2 = relu16(fb);
+                    {  // W3 row 0 += Σ_n dsdf · h2 of this unit (a register accumulator
+                       // over the units would spill: summed per round into the page)
+                        f32x4v r0[8];
+#pragma unroll
+                        for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) r0[ob][j] = row_sum16(fb[ob][j] * dsdf);
+                        if (n == 0) {
+#pragma unroll
+                            for (int ob = 0; ob < 8; ++ob) {
+                                float4 *pp = reinterpret_cast<float4 *>(page3 + 16 * ob + 4 * q);
+                                const float4 o = *pp;
+                                *pp = make_float4(o.x + r0[ob][0], o.y + r0[ob][1], o.z + r0[ob][2], o.w + r0[ob][3]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int ob = 0; ob < 8; ++ob) {
+                        // δh2 = W3[0]ᵀ dsdf ⊙ [h2 > 0] (k_mlp_bwd3's δf = 0 case)
                         const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
                         fb[ob] = f32x4v{__fmul_rn(w.x, dsdf), __fmul_rn(w.y, dsdf), __fmul_rn(w.z, dsdf),
                                         __fmul_rn(w.w, dsdf)};
                     }
+                    b30p += dsdf;
                     mask16(fb, m2);
-                    lds_u_store<8>(h2set(r) + c * kUImg, wb, fb);
+                    lds_u_store<8>(h2set + c * kUImg, wb, fb);
                     zero4(fa);
-                    gemm16<8, 8, 2>(wrs, kImgC2, fb, fa, lane);  // one ring over all 8 output blocks
+                    gemm16<8, 8, 2>(wrs, kImgC2, fb, fa, lane);  // W2ᵀ δh2
                     mask16(fa, m1);  // δh1
                 }
             }
             PSVO_STAMP(1);
-            PSVO_STAMP(2);
             raw_barrier();
             PSVO_STAMP(3);
             if (r == n_rounds) {
@@ -1713,7 +1746,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                 const int64_t un = u + 4;
                 const int64_t snx = un * kU + n;
                 const bool vn = un < u1 && snx < m;
-                load_trunk_in(masks, g_sdf, feat, snx, vn, q, nin);
+                load_trunk_in(g_sdf, feat, snx, vn, q, nin);
                 if (fuse && vn) {
                     lf_n = ip.leaf[snx];
                     ro_n = ip.ray_of[snx];
@@ -1739,14 +1772,14 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                             rd3[a] = ip.rays_d[(int64_t)row * 3 + a];
                         }
                     }
-                    interp_bwd_unit(ip, lds + kT3I + c * 512, m, s, valid, n, q, ts, ro3, rd3, cen, vid0, vid1, ev,
+                    interp_bwd_unit(ip, lds + kT4I + c * 512, m, s, valid, n, q, ts, ro3, rd3, cen, vid0, vid1, ev,
                                     gf);
                     PSVO_STAMP(5);
                     if (ip.grad_emb != nullptr) {
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging is this wave's own
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        scatter_unit(ip, lds + kT3I + c * 512, u, m, lane, lf);
+                        scatter_unit(ip, lds + kT4I + c * 512, u, m, lane, lf);
                     }
                 }
             }
@@ -1755,30 +1788,24 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
             PSVO_STAMP(7);
             PSVO_STAMP_FLUSH(0);
         }
+        // b3[0]: Σ dsdf (every sample's in each of the 4 q rows: row 0's)
+        const float bs = row_sum16(b30p);
+        if (lane == 0) page3[128] = bs;
     } else {
-        // ================= gradient wave: column block d of W2, row 0 of W3 (cols of block d), biases
+        // ================= gradient wave: column block d of W2, row block d of W1, biases
         const int d = wave - 4;
         f32x16 acc2[kNB];
         zero(acc2);
-        float b2p = 0.f, r0 = 0.f, b30 = 0.f, unused0 = 0.f, unused1 = 0.f, b1p = 0.f;
-        float *const page1 = lds + kT3A + d * 1024;  // dW1 row block d accumulators
+        float b2p = 0.f, b1p = 0.f;
+        float *const page1 = lds + kT4A + d * 1024;  // dW1 row block d accumulators
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-        const __amdgpu_buffer_rsrc_t h1m = rsrc_of(act, tb), h2m = rsrc_of(act + tstride, tb);
-        float4 ring[3], h2t[8];
         for (int r = 0; r <= n_rounds; ++r) {
             PSVO_STAMP(0);
             const int64_t ubase = u0 + 4 * (int64_t)r;
-            // A (the chain's W2ᵀ GEMM): dW1 row block d += δh1(r−1) ⊗ x(r−1)
-            // (32 MFMAs beside the chain's 256); this round's h1 / h2 tiles start loading
+            // A (the chain's forward and W2ᵀ GEMMs): dW1 row block d += δh1(r−1) ⊗ x(r−1)
             if (r > 0) xgrad16(h1set, xset(r - 1), d, ubase - 4, u1, lane, page1, &b1p);
-            if (r < n_rounds) {
-#pragma unroll
-                for (int qq = 0; qq < 8; ++qq) h2t[qq] = dw_bsrc(h2m, ubase, u1, d, lane, qq);
-                ring[0] = dw_bsrc(h1m, ubase, u1, d, lane, 0);
-                ring[1] = dw_bsrc(h1m, ubase, u1, d, lane, 1);
-            }
             PSVO_STAMP(1);
             raw_barrier();
             PSVO_STAMP(3);
@@ -1786,26 +1813,13 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
                 PSVO_STAMP_FLUSH(0);
                 break;
             }
-            // B (beside the chain's interpolation backward): dW2 += δh2 ⊗ h1 of
-            // this round (its δh2 set from phase A), W3 row 0 += dsdf ⊙ h2
-            dw_job<0, 0>(ring, h2set(r), nullptr, h1m, ubase, true, h1m, ubase, false, u1, d, lane, acc2, b2p,
-                         unused0, unused1);
-#pragma unroll
-            for (int qq = 0; qq < 8; ++qq) {
-                const int up = qq >> 1, gg = qq & 1;
-                if (ubase + up < u1) {  // wave-uniform
-                    const float4 bb = h2t[qq];
-                    const float4 w = *reinterpret_cast<const float4 *>(sset + up * kU + 8 * h + 4 * gg);
-                    r0 += (bb.x * w.x + bb.y * w.y) + (bb.z * w.z + bb.w * w.w);
-                    b30 += (w.x + w.y) + (w.z + w.w);
-                }
-            }
+            // B (beside the chain's interpolation backward): dW2 += δh2 ⊗ h1 of this round
+            dw_job_lds(h2set, cf, ubase, u1, d, lane, acc2, b2p);
             PSVO_STAMP(6);
             raw_barrier();
             PSVO_STAMP(7);
             PSVO_STAMP_FLUSH(0);
         }
-        // ---- slabs: W1 row block d + b1, W2 column block d + b2, W3 row 0 + b3[0]
         float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
         if (i < 16) {
 #pragma unroll
@@ -1819,20 +1833,32 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3t(const int *__restri
         if (h == 0) store_nt(s1, 128 * 16 + 32 * d + i, bv);
         const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
         float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
-        float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
         {
             f32x16 t[kNB][1];
 #pragma unroll
             for (int k = 0; k < kNB; ++k) t[k][0] = acc2[k];
             dw_store<kNB, 1, true>(s2, 128, 0, 128, rb, cb, t, lane);
         }
-        const float v2 = b2p + __shfl_xor(b2p, 32, 64), vr0 = r0 + __shfl_xor(r0, 32, 64),
-                    v30 = b30 + __shfl_xor(b30, 32, 64);
+        const float v2 = b2p + __shfl_xor(b2p, 32, 64);
+        if (h == 0) store_nt(s2, 128 * 128 + 32 * d + i, v2);
+    }
+    // W3 row 0 (+ b3[0]): the chain waves' pages, summed in wave order
+    __syncthreads();
+    if (wave >= 4) {
+        const int d = wave - 4;
+        float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
         if (h == 0) {
-            store_nt(s2, 128 * 128 + 32 * d + i, v2);
-            store_nt(s3, 32 * d + i, vr0);  // W3 row 0 (sdf)
+            float v = 0.f;
+#pragma unroll
+            for (int cw = 0; cw < 4; ++cw) v += lds[kT4R + cw * 132 + 32 * d + i];
+            store_nt(s3, 32 * d + i, v);
         }
-        if (d == 0 && lane == 0) store_nt(s3, 129 * 128, v30);
+        if (d == 0 && lane == 0) {
+            float v = 0.f;
+#pragma unroll
+            for (int cw = 0; cw < 4; ++cw) v += lds[kT4R + cw * 132 + 128];
+            store_nt(s3, 129 * 128, v);
+        }
     }
 }
 
@@ -1927,23 +1953,6 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
 }
 
 namespace psvo {
-int mlp_fwd_trunk(hipStream_t st, int64_t m_cap, const int *m_dev, const float *feat, const float *images, float *act,
-                  uint64_t *masks, float *rgb) {
-    PSVO_REQUIRE(m_cap >= 0 && m_cap <= kMaxSamples && m_dev && images && act && masks && rgb,
-                 "mlp_fwd_trunk: bad arguments");
-    if (m_cap == 0) return PSVO_OK;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk2),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSdf2);
-        attr = true;
-    }
-    const int64_t tiles = div_up(m_cap, kF2Tile);
-    const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-    psvo::launch(k_mlp_trunk2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m_dev, feat, images, act, masks, rgb);
-    return check_launch("mlp_fwd_trunk");
-}
-
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images) {
@@ -1995,7 +2004,7 @@ extern "C" int64_t psvo_mlp_workspace_floats(int64_t m, int n_split) {
     DwGrid g;
     int slab;
     dw_grid_uniform(bwd3_grid(m), &g, &slab);
-    return m * 3 + 2 * (int64_t)slab;  // k_mlp_bwd3's slabs, then k_mlp_bwd3t's (the sparse decoder's class B)
+    return m * 3 + 2 * (int64_t)slab;  // k_mlp_bwd3's slabs, then k_mlp_trunk_fb's (the sparse decoder's class B)
 }
 
 extern "C" int64_t psvo_mlp_workspace_floats_w(int64_t m, int width, int n_split) {
@@ -2033,7 +2042,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
     DwGrid g;
     int slab_floats;
     float *gw[5] = {gw1, gw2, gw3, gw4, gw5}, *gb[5] = {gb1, gb2, gb3, gb4, gb5};
-    PSVO_REQUIRE(tb == nullptr || (gw1 != nullptr && tb->m_dev && tb->masks && tb->g_sdf && tb->feat && tb->act),
+    PSVO_REQUIRE(tb == nullptr || (gw1 != nullptr && tb->m_dev && tb->g_sdf && tb->feat),
                  "mlp_bwd: the trunk backward needs the weight-gradient path and its inputs");
     float *slabs_b = nullptr;
     auto reduce = [&](float *slabs, hipStream_t rs) {
@@ -2086,17 +2095,17 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
             return set_error(PSVO_E_LAUNCH, "mlp_bwd: memset failed");
         }
-        if (tb && m > 0) {  // the trunk backward of the sparse decoder's class B, its own slabs
+        if (tb && m > 0) {  // the sparse decoder's class B: the trunk forward + backward, its own slabs
             static bool attr_t = false;
             if (!attr_t) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_bwd3t),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd3t);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk_fb),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTrunk);
                 attr_t = true;
             }
             slabs_b = slabs + slab_floats;
-            psvo::launch(k_mlp_bwd3t, dim3(grid), dim3(kF2Threads), kLdsBwd3t, st, tb->m_dev, images, tb->masks,
-                         tb->g_sdf, tb->feat, tb->act, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{});
-            const int rc = check_launch("mlp_bwd3t");
+            psvo::launch(k_mlp_trunk_fb, dim3(grid), dim3(kF2Threads), kLdsTrunk, st, tb->m_dev, images, tb->g_sdf,
+                         tb->feat, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{});
+            const int rc = check_launch("mlp_trunk_fb");
             if (rc) return rc;
         }
         if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)

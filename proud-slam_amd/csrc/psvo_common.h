@@ -240,7 +240,8 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
 // [0, M_A), class B (only a loss term: the decoder trunk) at [cap, cap + M_B)
 // (split = false: every kept sample in class A) —, the classes' compact ray
 // offsets offa / offb [R_hit + 1] and compact copies of their features /
-// leaf / t / ray ([2 cap] arrays).  counts[0] = M_A, counts[1] = M_B (the
+// leaf / t / ray ([2 cap] arrays; split: class B's colour rows of rgb_c
+// [2 cap][3] are written 0 — their composite weights are 0).  counts[0] = M_A, counts[1] = M_B (the
 // compact decoder launches read them on the device), counts[2] |= 8 if the
 // look-back wait was abandoned (then both are 0); counts + 4: u64 running
 // sums of kept / composited samples and of launches (kSelCountInts ints,
@@ -251,7 +252,7 @@ int select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, f
                    const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_depth,
                    const float *sdf_s, const float *feat, const int *leaf, const float *t, const int *ray_of,
                    int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c, int *leaf_c, float *t_c,
-                   int *ray_of_c, int *counts, unsigned long long *desc, uint32_t tag);
+                   int *ray_of_c, float *rgb_c, int *counts, unsigned long long *desc, uint32_t tag);
 int select_rays_per_wave(int64_t r_hit);
 int64_t select_granules(int64_t r_hit);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
@@ -356,13 +357,12 @@ int interp_rays_gx(hipStream_t st, int64_t r_hit, const int *offsets, const int 
 // dfeat is not stored.  m_dev (width 128; the sparse decoder): the sample
 // count is read on the device (select_samples' counts[0] <= m; the buffers
 // are sized for m).
-// the sparse decoder's class B (k_mlp_bwd3t after k_mlp_bwd3, width 128):
-// its count on the device, the forward's masks / activations (h1, h2:
-// mlp_fwd_trunk), dL/dsdf, the features and the fused interpolation backward
+// the sparse decoder's class B (k_mlp_trunk_fb after k_mlp_bwd3, width 128:
+// the trunk's forward recomputed and its backward in one kernel): its count
+// on the device, dL/dsdf, the features and the fused interpolation backward
 struct TrunkBwd {
     const int *m_dev;
-    const uint64_t *masks;
-    const float *g_sdf, *feat, *act;
+    const float *g_sdf, *feat;
     const InterpFuse *ip;
 };
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
@@ -385,11 +385,6 @@ bool mlp_bwd_split_tail(int width);
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images);
-// the sparse decoder's class B forward (k_mlp_trunk2, width 128): h1 / h2 CF
-// tiles into act (buffers for m_cap samples), the masks, zero colours; the
-// class count read on the device
-int mlp_fwd_trunk(hipStream_t st, int64_t m_cap, const int *m_dev, const float *feat, const float *images, float *act,
-                  uint64_t *masks, float *rgb);
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,

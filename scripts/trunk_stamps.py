@@ -1,4 +1,4 @@
-"""Diagnostic: where k_mlp_bwd3t (the sparse decoder's trunk backward) spends a
+"""Diagnostic: where k_mlp_trunk_fb (the sparse decoder's class-B trunk forward + backward) spends a
 round — s_memtime stamps of the lib/diag/libpsvo_stamps.so build (`make -C
 proud-slam_amd/csrc stamps`), recorded by the last launch of a short
 bench.py run (config B).  Read the SHARES of the segments: the stamps fence
@@ -14,9 +14,9 @@ DIAG = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_stamps.so")
 os.environ["PSVO_LIB_PATH"] = DIAG
 sys.path.insert(0, ROOT)
 
-CHAIN = [("A: dh2, W2T", 0, 1), ("A: dW1 (xgrad)", 1, 2), ("bar A", 2, 3), ("B: loads, W1T", 3, 4),
+CHAIN = [("A: W1, W2, dh2, W2T", 0, 1), ("bar A", 1, 3), ("B: loads, W1T", 3, 4),
          ("B: interp", 4, 5), ("B: scatter", 5, 6), ("bar B", 6, 7)]
-GRAD = [("A: dW2", 0, 1), ("bar A", 1, 3), ("B: W3 row 0", 3, 6), ("bar B", 6, 7)]
+GRAD = [("A: dW1 (xgrad)", 0, 1), ("bar A", 1, 3), ("B: dW2", 3, 6), ("bar B", 6, 7)]
 B3 = [("P0", 0, 1), ("bar0", 1, 2), ("P1", 2, 3), ("bar1", 3, 4), ("P2", 4, 5), ("bar2", 5, 6), ("P3", 6, 7),
       ("bar3", 7, 8)]
 
@@ -28,7 +28,7 @@ def main():
     L = ctypes.CDLL(DIAG)
     buf = np.zeros((3, 256, 8, 8, 16), dtype=np.uint64)
     assert L.psvo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(buf.nbytes)) == 0
-    for kern, k, last, roles in (("bwd3t", 2, 7, (("chain", range(4), CHAIN), ("grad", range(4, 8), GRAD))),
+    for kern, k, last, roles in (("trunk_fb", 2, 7, (("chain", range(4), CHAIN), ("grad", range(4, 8), GRAD))),
                                  ("bwd3", 1, 8, (("chain", range(4), B3), ("grad", range(4, 8), B3)))):
         report(buf[k].astype(np.int64), kern, last, roles)
 
