@@ -1504,30 +1504,35 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
 // measured 57 + 110 µs at config B).  The forward is recomputed here with the
 // chain's 16 × 16 × 4 MFMAs (the sdf came from k_mlp_sdf2: the same values up
 // to the accumulation order, which only the ReLU masks' ties could see).
-// Rounds of four 16-sample units, two phases each:
-//   phase  chain wave c (unit u0 + 4r + c)                         gradient wave d
-//   A      x → LDS; h1 (W1) → LDS (CF image); h2 (W2); W3 row 0    dW1 row block d += δh1(r−1) ⊗ x(r−1)
-//          partial (registers); δh2 → LDS; δh1 = W2ᵀ δh2
-//   B      δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation          dW2 col block d += δh2(r) ⊗ h1(r)
-//          backward (dL/dx, the embedding scatter)                 (both operands from LDS)
-// plus a last phase A for the final round's dW1.  A chain wave and a
-// gradient wave share each SIMD's matrix unit: the chain's forward + W2ᵀ
-// fill phase A, the gradient waves' dW2 overlaps the chain's latency-bound
-// interpolation backward in phase B.  Writes one slab per workgroup of W1
-// (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the DwGrid layout;
-// k_mlp_dw_reduce adds these elements only).  m: the class's count on the device.
+// Rounds of four 16-sample units (unit u0 + 4r + k on chain wave k and
+// gradient wave 4 + k), two phases each:
+//   phase  chain wave c                                    gradient wave d
+//   P(r)   δh2(r) from LDS; δh1 = W2ᵀ δh2 ⊙ [h1 > 0]       dW2 col block d += δh2(r) ⊗ h1(r)
+//          → LDS                                           (both operands in LDS)
+//   Q(r)   dfeat = W1ᵀ δh1 → the interpolation backward    dW1 row block d += δh1(r) ⊗ x(r); the
+//          (dL/dx, the embedding scatter)                  forward of unit d of round r + 1: x → LDS,
+//                                                          h1 = relu(W1 x + b1) → LDS (CF tile),
+//                                                          h2 = relu(W2 h1 + b2), W3 row 0 += dsdf · h2,
+//                                                          δh2 → LDS, the h1 mask words → LDS
+// (the forward of round 0 before the loop).  A chain wave and a gradient
+// wave share each SIMD's matrix unit: in P both run 128 × 128 GEMMs (W2ᵀ,
+// dW2), in Q the gradient wave's forward overlaps the chain's latency-bound
+// interpolation backward.  (The forward on the chain waves, with W2ᵀ in one
+// phase: 42 k cycles per round, the chain alone in that phase for 62 % of
+// it — s_memtime stamps, scripts/trunk_stamps.py.)  Writes one slab per
+// workgroup of W1 (+ b1), W2 (+ b2) and W3's row 0 (+ b3[0]) in `slabs` (the
+// DwGrid layout; k_mlp_dw_reduce adds these elements only).  m: the class's
+// count on the device.
 constexpr int kT4H2 = kVecPad;                 // δh2 unit images [unit 4]
 constexpr int kT4H1 = kT4H2 + 4 * kUImg;       // δh1 unit images [unit 4]
-constexpr int kT4CF = kT4H1 + 4 * kUImg;       // h1 as CF tiles [2] (the round's units: slot up → tile up / 2, half up % 2)
+constexpr int kT4CF = kT4H1 + 4 * kUImg;       // h1 as CF tiles [2] (the round's unit k → tile k / 2, half k % 2)
 constexpr int kT4X = kT4CF + 2 * kCfTile;      // x images [round parity 2][unit 4][16 × 16]
 constexpr int kT4I = kT4X + 2 * 4 * 16 * kU;   // interpolation backward staging [chain wave 4][512]
-constexpr int kT4A = kT4I + 4 * 512;           // dW1 accumulators [gradient wave 4][4][lane 64][4]
-constexpr int kT4R = kT4A + 4 * 1024;          // W3 row 0 / b3[0] partials [chain wave 4][132]
-constexpr int kLdsTrunk = (kT4R + 4 * 132) * 4;  // 138,304 B
+constexpr int kT4R = kT4I + 4 * 512;           // W3 row 0 / b3[0] partials [gradient wave 4][132]
+constexpr int kT4M = kT4R + 4 * 132;           // h1 mask words [unit 4][lane 64] (u64)
+constexpr int kLdsTrunk = (kT4M + 4 * 64 * 2) * 4;  // 123,968 B
 static_assert(kLdsTrunk <= 160 * 1024, "trunk kernel LDS budget");
 
-// the chain's ReLU: v = max(v, 0) and the mask word mask16 reads (feature
-// 16·ob + 4q + j of the lane's sample ↔ bit 8·ob + j)
 // Σ of v over the 16 lanes of the lane's DPP row (the chain's samples n of one
 // q group), in every lane of the row: quad xor 1, xor 2, half-row mirror, row mirror
 template <int CTRL>
@@ -1596,6 +1601,91 @@ __device__ __forceinline__ void load_trunk_in(const float *__restrict__ g_sdf, c
     in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
 }
 
+template <int NOB>
+__device__ __forceinline__ void lds_u_load(const float *img, int wb, f32x4v (&v)[NOB]) {
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[ob][j] = img[wb + 256 * ob + 16 * j];
+}
+
+// gradient wave k: the trunk forward of unit k of round r (chain layout: lane
+// (n, q) holds features 16·ob + 4q + j of sample n) → x image, h1 CF tile,
+// δh2 unit image, h1 mask words; W3 row 0 / b3[0] partials into `page3`
+__device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_t wrs, const TrunkIn &in, int64_t u,
+                                               int64_t u1, int64_t m, int k, int lane, int wb, float *xl,
+                                               float *page3, float &b30p) {
+    const int n = lane & 15, q = lane >> 4;
+    const int64_t s = u * kU + n;
+    const bool active = u < u1;  // wave-uniform
+    const bool valid = active && s < m;
+    const float dsdf = valid ? in.gs : 0.0f;
+    const float4 xv = valid ? in.x : make_float4(0.f, 0.f, 0.f, 0.f);
+    xl[wb + 0] = xv.x;
+    xl[wb + 16] = xv.y;
+    xl[wb + 32] = xv.z;
+    xl[wb + 48] = xv.w;
+    if (!active) return;
+    f32x4v xin[1] = {f32x4v{xv.x, xv.y, xv.z, xv.w}};
+    f32x4v hb[8];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB1 + 16 * ob + 4 * q);
+        hb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+    }
+    gemm16<1, 4, 1>(wrs, kImgT1, xin, *reinterpret_cast<f32x4v(*)[4]>(&hb[0]), lane);  // h1 = W1 x + b1
+    gemm16<1, 4, 1>(wrs, kImgT1 + 4 * 256, xin, *reinterpret_cast<f32x4v(*)[4]>(&hb[4]), lane);
+    const uint64_t m1 = relu16(hb);
+    reinterpret_cast<uint64_t *>(lds + kT4M)[k * 64 + lane] = m1;
+    {  // h1 → the CF tile (dW2's B operand; k_mlp_fwd2's layout): row 16 ob + 4q + j,
+       // sample n at group 4 (n & 1) + 2 (k & 1) + n / 8, element (n / 2) & 3;
+       // the row's swizzle (row >> 1) & 7 does not depend on ob
+        const int grp = 4 * (n & 1) + 2 * (k & 1) + (n >> 3), el = (n >> 1) & 3;
+        float *const tile = lds + kT4CF + (k >> 1) * kCfTile;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float *const cj = tile + (4 * q + j) * kTileS + ((grp ^ ((2 * q + (j >> 1)) & 7)) << 2) + el;
+#pragma unroll
+            for (int ob = 0; ob < 8; ++ob) cj[16 * ob * kTileS] = hb[ob][j];
+        }
+    }
+    f32x4v fb[8];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
+        fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+    }
+    // h2 = W2 h1 + b2, four rings of 2 output blocks (beside the dW2 accumulators
+    // wider rings spill)
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+        gemm16<8, 2, 2>(wrs, kImgT2 + qq * 2 * 8 * 256, hb, *reinterpret_cast<f32x4v(*)[2]>(&fb[2 * qq]), lane);
+    const uint64_t m2 = relu16(fb);
+    {  // W3 row 0 += Σ_n dsdf · h2 (the unit's 16 samples by DPP row sums, into the page)
+        f32x4v r0[8];
+#pragma unroll
+        for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r0[ob][j] = row_sum16(fb[ob][j] * dsdf);
+        if (n == 0) {
+#pragma unroll
+            for (int ob = 0; ob < 8; ++ob) {
+                float4 *pp = reinterpret_cast<float4 *>(page3 + 16 * ob + 4 * q);
+                const float4 o = *pp;
+                *pp = make_float4(o.x + r0[ob][0], o.y + r0[ob][1], o.z + r0[ob][2], o.w + r0[ob][3]);
+            }
+        }
+    }
+    b30p += dsdf;
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {  // δh2 = W3[0]ᵀ dsdf ⊙ [h2 > 0] (k_mlp_bwd3's δf = 0 case)
+        const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
+        fb[ob] = f32x4v{__fmul_rn(w.x, dsdf), __fmul_rn(w.y, dsdf), __fmul_rn(w.z, dsdf), __fmul_rn(w.w, dsdf)};
+    }
+    mask16(fb, m2);
+    lds_u_store<8>(lds + kT4H2 + k * kUImg, wb, fb);
+}
+
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__restrict__ m_dev,
                                                                 const float *__restrict__ img,
                                                                 const float *__restrict__ g_sdf,
@@ -1615,40 +1705,34 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
     raw_barrier();
     const int b = blockIdx.x;
     const int i = lane & 31, h = lane >> 5;
+    const int n = lane & 15, q = lane >> 4;
+    const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot in a unit image
+    const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
+    const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
     const bool fuse = ip.gx != nullptr;  // uniform
     [[maybe_unused]] constexpr int kStampK = 2;
     PSVO_STAMP_DECL;
     if (wave < 4) {
         // ================= chain wave c
-        const __amdgpu_buffer_rsrc_t wrs = rsrc_of(img, (int64_t)kImgTotal * 4);
         const int c = wave;
-        const int n = lane & 15, q = lane >> 4;
-        const int sn = (n & 1) * 8 + (n >> 1);                     // the sample's slot in a unit image
-        const int wb = 64 * q + ((((sn >> 2) ^ q) << 2) | (sn & 3));  // + 256 ob + 16 j
-        // the sample's column in the round's CF image (k_mlp_fwd2's layout, as dw_bsrc reads it)
-        const int cf_grp = 4 * (n & 1) + 2 * (c & 1) + (n >> 3), cf_el = (n >> 1) & 3;
-        float *const cf_tile = cf + (c >> 1) * kCfTile;
-        float *const page3 = lds + kT4R + c * 132;  // W3 row 0 (+ b3[0]) partials of this wave's units
-        if (lane < 33) *reinterpret_cast<float4 *>(page3 + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
-        float b30p = 0.f;
-        TrunkIn nin;
+        f32x4v w1acc[8];  // dW1 partials of this wave's units: rows 16 t + 4 (lane >> 4) + j, column lane & 15
+        zero4(w1acc);
+        float b1p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // b1 partials: rows 16 t + (lane & 15)
         int lf_n = 0, ro_n = 0;
         float ts_n = 0.f;
         {
             const int64_t u = u0 + c;
             const int64_t s = u * kU + n;
-            load_trunk_in(g_sdf, feat, s, u < u1 && s < m, q, nin);
             if (fuse && u < u1 && s < m) {
                 lf_n = ip.leaf[s];
                 ro_n = ip.ray_of[s];
                 ts_n = ip.t[s];
             }
         }
-        for (int r = 0; r <= n_rounds; ++r) {
+        for (int r = 0; r < n_rounds; ++r) {
             PSVO_STAMP(0);
-            const int64_t ubase = u0 + 4 * (int64_t)r;
-            const int64_t u = ubase + c;
-            const bool active = r < n_rounds && u < u1;  // wave-uniform
+            const int64_t u = u0 + 4 * (int64_t)r + c;
+            const bool active = u < u1;  // wave-uniform
             const int64_t s = u * kU + n;
             const bool valid = active && s < m;
             const int lf = lf_n, ro = ro_n;
@@ -1663,91 +1747,27 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
                 for (int a = 0; a < 3; ++a) cen[a] = ip.centres[(int64_t)lf * 3 + a];
                 row = ip.rank_ray[ro];
             }
-            // ---- A: x → LDS; forward h1 → LDS, h2; δh2 → LDS; δh1 = W2ᵀ δh2 ⊙ [h1 > 0]
-            f32x4v fa[8];
-            uint64_t m1 = 0;
-            if (r < n_rounds) {
-                const TrunkIn in = nin;
-                const float dsdf = valid ? in.gs : 0.0f;
-                const float4 xv = valid ? in.x : make_float4(0.f, 0.f, 0.f, 0.f);
-                float *xl = xset(r) + c * 16 * kU;
-                xl[wb + 0] = xv.x;
-                xl[wb + 16] = xv.y;
-                xl[wb + 32] = xv.z;
-                xl[wb + 48] = xv.w;
-                if (active) {
-                    f32x4v xin[1] = {f32x4v{xv.x, xv.y, xv.z, xv.w}};
-                    f32x4v hb[8];
-#pragma unroll
-                    for (int ob = 0; ob < 8; ++ob) {
-                        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB1 + 16 * ob + 4 * q);
-                        hb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
-                    }
-                    gemm16<1, 8, 1>(wrs, kImgT1, xin, hb, lane);  // h1 = W1 x + b1
-                    m1 = relu16(hb);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {  // h1 → the CF image (dW2's B operand): row 16 ob + 4q + j
-                        // (the row's swizzle (row >> 1) & 7 does not depend on ob)
-                        float *const cj = cf_tile + (4 * q + j) * kTileS + ((cf_grp ^ ((2 * q + (j >> 1)) & 7)) << 2) + cf_el;
-#pragma unroll
-                        for (int ob = 0; ob < 8; ++ob) cj[16 * ob * kTileS] = hb[ob][j];
-                    }
-                    f32x4v fb[8];
-#pragma unroll
-                    for (int ob = 0; ob < 8; ++ob) {
-                        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
-                        fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
-                    }
-                    // h2 = W2 h1 + b2, two rings of 4 output blocks (one ring over all 8 spills)
-                    gemm16<8, 4, 2>(wrs, kImgT2, hb, *reinterpret_cast<f32x4v(*)[4]>(&fb[0]), lane);
-                    gemm16<8, 4, 2>(wrs, kImgT2 + 4 * 8 * 256, hb, *reinterpret_cast<f32x4v(*)[4]>(&fb[4]), lane);
-                    const uint64_t m2 = relu16(fb);
-                    {  // W3 row 0 += Σ_n dsdf · h2 of this unit (a register accumulator
-                       // over the units would spill: summed per round into the page)
-                        f32x4v r0[8];
-#pragma unroll
-                        for (int ob = 0; ob < 8; ++ob)
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) r0[ob][j] = row_sum16(fb[ob][j] * dsdf);
-                        if (n == 0) {
-#pragma unroll
-                            for (int ob = 0; ob < 8; ++ob) {
-                                float4 *pp = reinterpret_cast<float4 *>(page3 + 16 * ob + 4 * q);
-                                const float4 o = *pp;
-                                *pp = make_float4(o.x + r0[ob][0], o.y + r0[ob][1], o.z + r0[ob][2], o.w + r0[ob][3]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int ob = 0; ob < 8; ++ob) {
-                        // δh2 = W3[0]ᵀ dsdf ⊙ [h2 > 0] (k_mlp_bwd3's δf = 0 case)
-                        const float4 w = *reinterpret_cast<const float4 *>(lds + kOffW3r0 + 16 * ob + 4 * q);
-                        fb[ob] = f32x4v{__fmul_rn(w.x, dsdf), __fmul_rn(w.y, dsdf), __fmul_rn(w.z, dsdf),
-                                        __fmul_rn(w.w, dsdf)};
-                    }
-                    b30p += dsdf;
-                    mask16(fb, m2);
-                    lds_u_store<8>(h2set + c * kUImg, wb, fb);
-                    zero4(fa);
-                    gemm16<8, 8, 2>(wrs, kImgC2, fb, fa, lane);  // W2ᵀ δh2
-                    mask16(fa, m1);  // δh1
-                }
-            }
+            raw_barrier();  // the round's forward (gradient waves) is in LDS
             PSVO_STAMP(1);
+            // ---- P: δh1 = W2ᵀ δh2 ⊙ [h1 > 0] → LDS
+            f32x4v fa[8];
+            if (active) {
+                f32x4v fb[8];
+                lds_u_load<8>(h2set + c * kUImg, wb, fb);
+                const uint64_t m1 = reinterpret_cast<const uint64_t *>(lds + kT4M)[c * 64 + lane];
+                zero4(fa);
+                gemm16<8, 8, 2>(wrs, kImgC2, fb, fa, lane);  // one ring over all 8 output blocks
+                mask16(fa, m1);
+                lds_u_store<8>(h1set + c * kUImg, wb, fa);
+            }
+            PSVO_STAMP(2);
             raw_barrier();
             PSVO_STAMP(3);
-            if (r == n_rounds) {
-                PSVO_STAMP_FLUSH(0);
-                break;
-            }
-            // ---- B: δh1 → LDS; dfeat = W1ᵀ δh1 → the interpolation backward; the next unit's inputs
-            if (active) lds_u_store<8>(h1set + c * kUImg, wb, fa);
+            // ---- Q: dfeat = W1ᵀ δh1 → the interpolation backward; the next unit's inputs
             if (r + 1 < n_rounds) {
                 const int64_t un = u + 4;
                 const int64_t snx = un * kU + n;
-                const bool vn = un < u1 && snx < m;
-                load_trunk_in(g_sdf, feat, snx, vn, q, nin);
-                if (fuse && vn) {
+                if (fuse && un < u1 && snx < m) {
                     lf_n = ip.leaf[snx];
                     ro_n = ip.ray_of[snx];
                     ts_n = ip.t[snx];
@@ -1757,6 +1777,23 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
                 f32x4v t1[1];
                 zero4(t1);
                 gemm16<8, 1, 4>(wrs, kImgC1, fa, t1, lane);
+                // dW1 += δh1 ⊗ x of this unit (16 × 16 × 4 MFMAs over its 16 samples: lane (m, kq)
+                // feeds slots 4 kq .. 4 kq + 3 of row 16 t + m, one 16-B chunk of each image)
+                {
+                    const int mr = lane & 15, kq = lane >> 4;
+                    const float *dl = h1set + c * kUImg, *xl = xset(r) + c * 16 * kU;
+                    const float4 bx = *reinterpret_cast<const float4 *>(xl + mr * kU + ((kq ^ ((mr >> 2) & 3)) << 2));
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int rw = 16 * t + mr;
+                        const float4 a = *reinterpret_cast<const float4 *>(dl + rw * kU + ((kq ^ ((rw >> 2) & 3)) << 2));
+                        w1acc[t] = mfma16(a.x, bx.x, w1acc[t]);
+                        w1acc[t] = mfma16(a.y, bx.y, w1acc[t]);
+                        w1acc[t] = mfma16(a.z, bx.z, w1acc[t]);
+                        w1acc[t] = mfma16(a.w, bx.w, w1acc[t]);
+                        b1p[t] += (a.x + a.y) + (a.z + a.w);
+                    }
+                }
                 PSVO_STAMP(4);
                 const float4 gf = make_float4(t1[0][0], t1[0][1], t1[0][2], t1[0][3]);
                 if (fuse) {
@@ -1784,53 +1821,65 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
                 }
             }
             PSVO_STAMP(6);
+            PSVO_STAMP_FLUSH(0);
+        }
+        // this wave's dW1 / b1 partials → LDS (the CF tiles and mask words: read in P only)
+        float *const pw = lds + kT4CF + c * 2048;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pw[(16 * t + 4 * (lane >> 4) + j) * 16 + (lane & 15)] = w1acc[t][j];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            float v = b1p[t];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (lane < 16) lds[kT4M + c * 128 + 16 * t + lane] = v;
+        }
+    } else {
+        // ================= gradient wave: column block d of W2, row block d of W1, the forward of unit d
+        const int d = wave - 4;
+        f32x16 acc2[kNB];
+        zero(acc2);
+        float b2p = 0.f, b30p = 0.f;
+        float *const page3 = lds + kT4R + d * 132;   // W3 row 0 (+ b3[0]) partials of this wave's units
+        if (lane < 33) *reinterpret_cast<float4 *>(page3 + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+        TrunkIn nin;
+        auto load_in = [&](int r) {
+            const int64_t u = u0 + 4 * (int64_t)r + d;
+            const int64_t s = u * kU + n;
+            load_trunk_in(g_sdf, feat, s, u < u1 && s < m, q, nin);
+        };
+        if (n_rounds > 0) {  // the forward of round 0
+            load_in(0);
+            const TrunkIn in = nin;
+            if (n_rounds > 1) load_in(1);
+            trunk_fwd_unit(lds, wrs, in, u0 + d, u1, m, d, lane, wb, xset(0) + d * 16 * kU, page3, b30p);
+        }
+        for (int r = 0; r < n_rounds; ++r) {
+            PSVO_STAMP(0);
+            const int64_t ubase = u0 + 4 * (int64_t)r;
             raw_barrier();
-            PSVO_STAMP(7);
+            PSVO_STAMP(1);
+            // P (beside the chain's W2ᵀ): dW2 += δh2 ⊗ h1 of this round
+            dw_job_lds(h2set, cf, ubase, u1, d, lane, acc2, b2p);
+            PSVO_STAMP(2);
+            raw_barrier();
+            PSVO_STAMP(3);
+            // Q (beside the chain's interpolation backward): the next round's forward
+            PSVO_STAMP(4);
+            if (r + 1 < n_rounds) {
+                const TrunkIn in = nin;
+                if (r + 2 < n_rounds) load_in(r + 2);
+                trunk_fwd_unit(lds, wrs, in, ubase + 4 + d, u1, m, d, lane, wb, xset(r + 1) + d * 16 * kU, page3,
+                               b30p);
+            }
+            PSVO_STAMP(6);
             PSVO_STAMP_FLUSH(0);
         }
         // b3[0]: Σ dsdf (every sample's in each of the 4 q rows: row 0's)
         const float bs = row_sum16(b30p);
         if (lane == 0) page3[128] = bs;
-    } else {
-        // ================= gradient wave: column block d of W2, row block d of W1, biases
-        const int d = wave - 4;
-        f32x16 acc2[kNB];
-        zero(acc2);
-        float b2p = 0.f, b1p = 0.f;
-        float *const page1 = lds + kT4A + d * 1024;  // dW1 row block d accumulators
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *reinterpret_cast<float4 *>(page1 + (k * 64 + lane) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int r = 0; r <= n_rounds; ++r) {
-            PSVO_STAMP(0);
-            const int64_t ubase = u0 + 4 * (int64_t)r;
-            // A (the chain's forward and W2ᵀ GEMMs): dW1 row block d += δh1(r−1) ⊗ x(r−1)
-            if (r > 0) xgrad16(h1set, xset(r - 1), d, ubase - 4, u1, lane, page1, &b1p);
-            PSVO_STAMP(1);
-            raw_barrier();
-            PSVO_STAMP(3);
-            if (r == n_rounds) {
-                PSVO_STAMP_FLUSH(0);
-                break;
-            }
-            // B (beside the chain's interpolation backward): dW2 += δh2 ⊗ h1 of this round
-            dw_job_lds(h2set, cf, ubase, u1, d, lane, acc2, b2p);
-            PSVO_STAMP(6);
-            raw_barrier();
-            PSVO_STAMP(7);
-            PSVO_STAMP_FLUSH(0);
-        }
-        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
-        if (i < 16) {
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
-                const int row = 32 * d + phi(rr, h);
-                const int pos = ((rr >> 2) * 64 + lane) * 4 + (rr & 3);
-                store_nt(s1, row * 16 + i, page1[pos]);
-            }
-        }
-        const float bv = b1p + __shfl_xor(b1p, 32, 64);
-        if (h == 0) store_nt(s1, 128 * 16 + 32 * d + i, bv);
         const int rb[kNB] = {0, 1, 2, 3}, cb[1] = {d};
         float *s2 = slabs + g.slab_off[1] + (int64_t)b * g.slab_len[1];
         {
@@ -1842,21 +1891,36 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
         const float v2 = b2p + __shfl_xor(b2p, 32, 64);
         if (h == 0) store_nt(s2, 128 * 128 + 32 * d + i, v2);
     }
-    // W3 row 0 (+ b3[0]): the chain waves' pages, summed in wave order
+    // W3 row 0 (+ b3[0]): the gradient waves' pages; W1 (+ b1): the chain
+    // waves' partials — each summed in wave order
     __syncthreads();
+    {
+        float *s1 = slabs + g.slab_off[0] + (int64_t)b * g.slab_len[0];
+        for (int e = threadIdx.x; e < 128 * 16 + 128; e += kF2Threads) {
+            float v = 0.f;
+            if (e < 128 * 16) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v += lds[kT4CF + k * 2048 + e];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v += lds[kT4M + k * 128 + e - 128 * 16];
+            }
+            store_nt(s1, e, v);
+        }
+    }
     if (wave >= 4) {
         const int d = wave - 4;
         float *s3 = slabs + g.slab_off[2] + (int64_t)b * g.slab_len[2];
         if (h == 0) {
             float v = 0.f;
 #pragma unroll
-            for (int cw = 0; cw < 4; ++cw) v += lds[kT4R + cw * 132 + 32 * d + i];
+            for (int k = 0; k < 4; ++k) v += lds[kT4R + k * 132 + 32 * d + i];
             store_nt(s3, 32 * d + i, v);
         }
         if (d == 0 && lane == 0) {
             float v = 0.f;
 #pragma unroll
-            for (int cw = 0; cw < 4; ++cw) v += lds[kT4R + cw * 132 + 128];
+            for (int k = 0; k < 4; ++k) v += lds[kT4R + k * 132 + 128];
             store_nt(s3, 129 * 128, v);
         }
     }

@@ -14,9 +14,9 @@ DIAG = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_stamps.so")
 os.environ["PSVO_LIB_PATH"] = DIAG
 sys.path.insert(0, ROOT)
 
-CHAIN = [("A: W1, W2, dh2, W2T", 0, 1), ("bar A", 1, 3), ("B: loads, W1T", 3, 4),
-         ("B: interp", 4, 5), ("B: scatter", 5, 6), ("bar B", 6, 7)]
-GRAD = [("A: dW1 (xgrad)", 0, 1), ("bar A", 1, 3), ("B: dW2", 3, 6), ("bar B", 6, 7)]
+CHAIN = [("wait fwd (bar)", 0, 1), ("P: W2T", 1, 2), ("bar P", 2, 3), ("Q: W1T", 3, 4),
+         ("Q: interp", 4, 5), ("Q: scatter", 5, 6)]
+GRAD = [("bar top", 0, 1), ("P: dW2", 1, 2), ("bar P", 2, 3), ("Q: dW1 (xgrad)", 3, 4), ("Q: forward", 4, 6)]
 B3 = [("P0", 0, 1), ("bar0", 1, 2), ("P1", 2, 3), ("bar1", 3, 4), ("P2", 4, 5), ("bar2", 5, 6), ("P3", 6, 7),
       ("bar3", 7, 8)]
 
@@ -28,7 +28,7 @@ def main():
     L = ctypes.CDLL(DIAG)
     buf = np.zeros((3, 256, 8, 8, 16), dtype=np.uint64)
     assert L.psvo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(buf.nbytes)) == 0
-    for kern, k, last, roles in (("trunk_fb", 2, 7, (("chain", range(4), CHAIN), ("grad", range(4, 8), GRAD))),
+    for kern, k, last, roles in (("trunk_fb", 2, 6, (("chain", range(4), CHAIN), ("grad", range(4, 8), GRAD))),
                                  ("bwd3", 1, 8, (("chain", range(4), B3), ("grad", range(4, 8), B3)))):
         report(buf[k].astype(np.int64), kern, last, roles)
 
