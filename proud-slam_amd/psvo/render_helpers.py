@@ -520,11 +520,11 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     batched = all(getattr(kf, "uniform_pixel_sampling", False) for kf in kfs)
     cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs)  # noqa: E731
 
-    def draw(it):
+    def draw(it, out=None):
         """iteration it's pixels (dirs_cam, rgb, depth) and sampler seed, in
         the order the reference draws them (pixels, then the sampler noise)"""
         if batched:
-            d_all, c_all, z_all = sample_util.sample_frames(kfs, N_rays)
+            d_all, c_all, z_all = sample_util.sample_frames(kfs, N_rays, out=out)
         else:
             dirs, rgbs, depths = [], [], []
             for kf in kfs:
@@ -557,8 +557,24 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     ahead = lookahead and not callable(noise)
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev) if ahead and num_iterations > 1 else None
+    # the batched draws' output ring: draw j + 4 (queued on `side` at the top
+    # of iteration j + 3) overwrites draw j's buffers, which step j reads on
+    # main.  The host queues it only after step j + 2 read back its query's
+    # statistics, which the look-ahead sampler queued on main after step
+    # j + 1's backward writes — after all of step j (and the auxiliary work
+    # step j joined into main) on the device: the ring needs no event.
+    ring = []
+    if side is not None and batched:
+        nt = len(kfs) * N_rays
+        for _ in range(4):
+            r3 = (torch.empty(nt, 3, dtype=torch.float32, device=dev),
+                  torch.empty(nt, 3, dtype=torch.float32, device=dev),
+                  torch.empty(nt, dtype=torch.float32, device=dev))
+            for t in r3:
+                t.record_stream(side)  # freed at the call's end: after the side stream's draws
+            ring.append(r3)
     if side is not None:
-        side.wait_stream(main)  # the keyframes as the caller left them
+        side.wait_stream(main)  # the keyframes as the caller left them (and the ring's blocks)
     clk("side")
 
     # each next draw is queued as soon as its step is (beside the persistent
@@ -567,12 +583,20 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     def draw_ahead(it):
         if side is None:
             return draw(it), None
+        # the batched draw writes into a ring of buffers made once per call
+        # (below): no tensor of the loop is freed with record_stream(main),
+        # whose allocator event — recorded on main at the free, with the
+        # runtime's default system-scope release — put a marker packet between
+        # the step's kernels: ≈ 15 µs of idle GPU per iteration between the
+        # sampler and the interpolation, measured (rocprofv3 timeline, config B)
+        bufs = ring[it % len(ring)] if ring else None
         with torch.cuda.stream(side):
-            out = draw(it)
+            out = draw(it, bufs)
         if it == 0:
             clk("draw")
-        for t in out[:3]:
-            t.record_stream(main)  # freed blocks are reused only after the steps that read them
+        if bufs is None:
+            for t in out[:3]:
+                t.record_stream(main)  # freed blocks are reused only after the steps that read them
         if it > 0:  # later draws are ordered by the engine (next_stream), no event needed
             return out, None
         ev = torch.cuda.Event()

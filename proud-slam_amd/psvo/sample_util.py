@@ -98,12 +98,13 @@ def sample_rays(mask, num_samples, u=None, seed=None):
     return out
 
 
-def sample_frames(frames, n, seed=None, u=None):
+def sample_frames(frames, n, seed=None, u=None, out=None):
     """frame.sample_rays(n) (frame.py:83-85: uniform over the frame's
     pixels) on every frame, plus the gathers of bundle_adjust_frames
     (render_helpers.py:625-633): sets each frame's sample_mask [H, W] and
     sample_idx [n] and returns (dirs [F·n, 3], rgb [F·n, 3], depth [F·n]) in
-    torch.cat([frame.rays_d[frame.sample_mask], ...]) order."""
+    torch.cat([frame.rays_d[frame.sample_mask], ...]) order (into `out` when
+    given)."""
     frames = list(frames)
     F = len(frames)
     f0 = frames[0]
@@ -118,9 +119,15 @@ def sample_frames(frames, n, seed=None, u=None):
                 raise ValueError("sample_frames: rays_d / rgb / depth must be contiguous f32 on one device")
         m = torch.empty(H, W, dtype=torch.bool, device=dev)
         srcs.append((fr.rays_d, fr.rgb, fr.depth, m))
-    dirs = torch.empty(F * n, 3, dtype=torch.float32, device=dev)
-    rgb = torch.empty(F * n, 3, dtype=torch.float32, device=dev)
-    depth = torch.empty(F * n, dtype=torch.float32, device=dev)
+    if out is not None:  # the caller's (dirs, rgb, depth) buffers
+        dirs, rgb, depth = out
+        if not (tuple(dirs.shape) == (F * n, 3) and tuple(rgb.shape) == (F * n, 3) and tuple(depth.shape) == (F * n,)
+                and all(t.dtype == torch.float32 and t.is_contiguous() and t.device == dev for t in out)):
+            raise ValueError("sample_frames: out must be contiguous f32 [F*n, 3], [F*n, 3], [F*n] on the frames' device")
+    else:
+        dirs = torch.empty(F * n, 3, dtype=torch.float32, device=dev)
+        rgb = torch.empty(F * n, 3, dtype=torch.float32, device=dev)
+        depth = torch.empty(F * n, dtype=torch.float32, device=dev)
     idx = sample_pixels(F, H * W, int(n), dev, u=u, seed=seed, frames=srcs, out_dirs=dirs, out_rgb=rgb,
                         out_depth=depth)
     for f, fr in enumerate(frames):
