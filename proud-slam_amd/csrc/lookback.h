@@ -27,7 +27,10 @@
 // spin while a lower workgroup of another XCD is queued behind a co-running
 // kernel (e.g. the width-256 dW kernel at one workgroup per CU) — the wait
 // then lasts as long as that kernel holds the CUs.  A wait that never ends
-// (a bug) is abandoned after kLbSpinMax re-reads (≳ 65 ms): lb_scan returns
+// (a bug) is abandoned after kLbSpinMax re-reads (≳ 1 s; 2^16, ≳ 65 ms, was
+// reached once by two processes sharing one GPU in the data-parallel test —
+// the other process's kernels held the CUs a queued lower workgroup needed
+// for that long): lb_scan returns
 // false, the caller raises PSVO_STAT_FLAGS bit 3, stores no rank / offset /
 // compacted sample from the undefined prefix, and the engine reports the
 // batch as failed — the grid still drains.
@@ -36,7 +39,7 @@
 
 namespace psvo {
 
-constexpr int kLbSpinMax = 1 << 16;
+constexpr int kLbSpinMax = 1 << 20;
 constexpr int kLbFlagTimeout = 8;  // PSVO_STAT_FLAGS bit 3
 
 template <unsigned MAXMASK>

@@ -243,8 +243,14 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     __shared__ float part[kGradThreads / 64][12];
     __shared__ float tot[12];
     __shared__ float rot_s[12];  // R row-major, then t
+    __shared__ float pst[18];    // the frame's pose, Adam m, v (loaded beside the rays: no dependent
+                                 // global round trips in the serial part)
     const int f = blockIdx.x;
     const int64_t lo = f * rpf, hi = lo + rpf;
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + 18) {  // (frame_sums_direct's barriers publish them)
+        const int k = threadIdx.x - 64;
+        pst[k] = k < 6 ? poses[f * 6 + k] : (pose_m ? (k < 12 ? pose_m[f * 6 + k - 6] : pose_v[f * 6 + k - 12]) : 0.f);
+    }
     // the next rays' camera directions depend on nothing here: loaded first
     // (one thread per ray when rpf <= kGradThreads), beside the gradient rows
     const int64_t r1 = lo + threadIdx.x;
@@ -255,16 +261,17 @@ __global__ __launch_bounds__(kGradThreads) void k_pose_step_frames(
     if (threadIdx.x == 0) {
         float t[12];
         for (int i = 0; i < 12; ++i) t[i] = tot[i];
-        float *pose = poses + f * 6;
         float *g = grads + f * 8;
-        pose_chain(pose, t, g);
+        float g6[8];
+        pose_chain(pst, t, g6);
+        for (int i = 0; i < 6; ++i) g[i] = g6[i];
         float p6[6];
-        for (int i = 0; i < 6; ++i) p6[i] = pose[i];
+        for (int i = 0; i < 6; ++i) p6[i] = pst[i];
         if (a.step[f] >= 1) {  // stamp 0 / update_pose False: fixed (render_helpers.py:594-596)
             for (int i = 0; i < 6; ++i) {
-                float mi = pose_m[f * 6 + i], vi = pose_v[f * 6 + i];
-                adam_elem(p6[i], g[i], mi, vi, beta1, beta2, omb1, omb2, eps, 0.0f, a.lr_bc1[f], a.bc2_sqrt[f]);
-                pose[i] = p6[i];
+                float mi = pst[6 + i], vi = pst[12 + i];
+                adam_elem(p6[i], g6[i], mi, vi, beta1, beta2, omb1, omb2, eps, 0.0f, a.lr_bc1[f], a.bc2_sqrt[f]);
+                poses[f * 6 + i] = p6[i];
                 pose_m[f * 6 + i] = mi;
                 pose_v[f * 6 + i] = vi;
             }
