@@ -1609,6 +1609,45 @@ __device__ __forceinline__ void lds_u_load(const float *img, int wb, f32x4v (&v)
         for (int j = 0; j < 4; ++j) v[ob][j] = img[wb + 256 * ob + 16 * j];
 }
 
+// acc[ob] += W blocks (ob, kb) of the image at `img_off` · in[kb] for NOB output
+// blocks, streamed as one sequence of (output-block pair, kb) steps with the
+// A-operand ring D steps deep running across the pairs (one ring fill per
+// GEMM, not one per pair; 2 · 4 · (D + 1) ring registers)
+template <int NKB, int NOB, int D>
+__device__ __forceinline__ void gemm16_stream(__amdgpu_buffer_rsrc_t rs, int img_off, const f32x4v (&in)[NKB],
+                                              f32x4v (&acc)[NOB], int lane) {
+    static_assert(NOB % 2 == 0, "output blocks in pairs");
+    constexpr int kSteps = NOB / 2 * NKB;
+    auto ld = [&](int st, int i) {
+        const int ob = 2 * (st / NKB) + i, kb = st % NKB;
+        return bload4(rs, lane * 16, (img_off + (ob * NKB + kb) * 256) * 4);
+    };
+    float4 ring[D + 1][2];
+#pragma unroll
+    for (int st = 0; st < D; ++st)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ring[st][i] = ld(st, i);
+#pragma unroll
+    for (int st = 0; st < kSteps; ++st) {
+        const int cs = st % (D + 1), ob = 2 * (st / NKB), kb = st % NKB;
+        if (st + D < kSteps) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) ring[(st + D) % (D + 1)][i] = ld(st + D, i);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[ob + i] = mfma16(ring[cs][i].x, in[kb][0], acc[ob + i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[ob + i] = mfma16(ring[cs][i].y, in[kb][1], acc[ob + i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[ob + i] = mfma16(ring[cs][i].z, in[kb][2], acc[ob + i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[ob + i] = mfma16(ring[cs][i].w, in[kb][3], acc[ob + i]);
+        if (st + D < kSteps) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the prefetch
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                      // this step's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // gradient wave k: the trunk forward of unit k of round r (chain layout: lane
 // (n, q) holds features 16·ob + 4q + j of sample n) → x image, h1 CF tile,
 // δh2 unit image, h1 mask words; W3 row 0 / b3[0] partials into `page3`
@@ -1633,8 +1672,7 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
         const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB1 + 16 * ob + 4 * q);
         hb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
     }
-    gemm16<1, 4, 1>(wrs, kImgT1, xin, *reinterpret_cast<f32x4v(*)[4]>(&hb[0]), lane);  // h1 = W1 x + b1
-    gemm16<1, 4, 1>(wrs, kImgT1 + 4 * 256, xin, *reinterpret_cast<f32x4v(*)[4]>(&hb[4]), lane);
+    gemm16_stream<1, 8, 3>(wrs, kImgT1, xin, hb, lane);  // h1 = W1 x + b1
     const uint64_t m1 = relu16(hb);
     reinterpret_cast<uint64_t *>(lds + kT4M)[k * 64 + lane] = m1;
     {  // h1 → the CF tile (dW2's B operand; k_mlp_fwd2's layout): row 16 ob + 4q + j,
@@ -1655,11 +1693,9 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
         const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
         fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
     }
-    // h2 = W2 h1 + b2, four rings of 2 output blocks (beside the dW2 accumulators
-    // wider rings spill)
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-        gemm16<8, 2, 2>(wrs, kImgT2 + qq * 2 * 8 * 256, hb, *reinterpret_cast<f32x4v(*)[2]>(&fb[2 * qq]), lane);
+    // h2 = W2 h1 + b2: output-block pairs, one ring across them (beside the dW2
+    // accumulators a ring over all 8 output blocks spills)
+    gemm16_stream<8, 8, 3>(wrs, kImgT2, hb, fb, lane);
     const uint64_t m2 = relu16(fb);
     {  // W3 row 0 += Σ_n dsdf · h2 (the unit's 16 samples by DPP row sums, into the page)
         f32x4v r0[8];
