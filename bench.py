@@ -704,19 +704,22 @@ def main():
         kept, comp = (float(x) / world for x in t.cpu())
     # executed: the sdf trunk on every sample; the whole decoder forward and backward on the kept
     # ones — width 128 on the composited ones only, the trunk forward + backward (δ chain, dW1, dW2,
-    # the sdf row of W3) on the kept samples that only the direct sdf loss reaches (class B)
+    # the sdf row of W3) on the kept samples that only the direct sdf loss reaches (class B); width
+    # 128 reads the W2 layer's output (h2) the sdf trunk wrote instead of recomputing it
     two_class = w == 128 and kept is not None
     n_b = max(kept - comp, 0.0) if two_class else 0.0
     n_full = comp if two_class else kept
-    flops_exec = (2.0 * trunk * h_m + 3 * 2.0 * macs * n_full + 3 * 2.0 * trunk * n_b) if kept is not None \
-        else flops_mlp
-    flops_bwd = (2 * 2.0 * macs * n_full + 2 * 2.0 * trunk * n_b) if kept is not None else 2 * 2.0 * macs * h_m
+    w2 = w * w if two_class else 0  # the W2 layer, read rather than recomputed (two_class: width 128)
+    flops_exec = (2.0 * trunk * h_m + 2.0 * (3 * macs - w2) * n_full + 2.0 * (3 * trunk - w2) * n_b) \
+        if kept is not None else flops_mlp
+    flops_bwd = (2 * 2.0 * macs * n_full + 2.0 * (3 * trunk - w2) * n_b) if kept is not None \
+        else 2 * 2.0 * macs * h_m
     mlp_tf = flops_exec / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None
     m_bwd = kept if kept is not None else h_m  # the samples the backward runs on
-    if fused_ib:  # k_mlp_bwd3 (+ k_mlp_bwd3t): δ chain + weight gradients + the interpolation backward
+    if fused_ib:  # k_mlp_bwd3 (+ k_mlp_trunk_fb): δ chain + weight gradients + the interpolation backward
         b_tf = flops_bwd / (mlp_b_ms * 1e-3) / 1e12 if mlp_b_ms > 0 else None
         ib_gbs = 1664.0 * m_bwd / (mlp_b_ms * 1e-3) / 1e9 if mlp_b_ms > 0 else None
-        roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_bwd3t + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
+        roof_ib = {"kernel": "k_mlp_bwd3 + k_mlp_trunk_fb + k_mlp_dw_reduce (decoder delta chain, weight gradients, and the "
                              "interpolation backward: embedding scatter + dL/dx)",
                    "bound": "mfma", "achieved": b_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                    "frac": b_tf / MFMA_F32_PEAK_TFS if b_tf else None,
@@ -769,7 +772,8 @@ def main():
                           "flops_algorithmic_per_step": flops_mlp,
                           "achieved_basis": "executed FLOPs (sdf trunk on every sample, the whole decoder forward + "
                                             "backward on the composited samples (W=256: on every kept sample), the "
-                                            "trunk forward + backward on the other kept samples) / time",
+                                            "trunk forward + backward on the other kept samples; W=128: the W2 "
+                                            "layer's output read from the sdf trunk, not recomputed) / time",
                           "effective_algorithmic_tflops": flops_mlp / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else None,
                           "avg_launch_ms": mlp_ms,
                           "fwd_ms": mlp_f_ms, "bwd_ms": mlp_b_ms,

@@ -458,6 +458,7 @@ struct SelectArgs {
     float *t_c;
     float *rgb_c;            // [2 cap][3] (split): class B's colours, written 0 (their weights are 0;
                              // the fused trunk kernel computes no colour head)
+    int *src_c;              // [2 cap] or null: each kept sample's row in the step's sample order
     int64_t cap;             // class B's base index (the step's sample count M)
     int split;
     int *counts;             // [0] M_A, [1] M_B, [2] flags (look-back abandoned: bit 3), [3] pad, then u64
@@ -615,6 +616,7 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
                 a.leaf_c[j] = a.leaf[src];
                 a.t_c[j] = a.t[src];
                 a.ray_of_c[j] = (int)r;
+                if (a.src_c) a.src_c[j] = (int)src;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) a.feat_c[j * 4 + q] = a.feat[src * 4 + q];
                 if (in_b) {
@@ -692,8 +694,8 @@ int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncat
                          const int *offsets, const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray,
                          const float *gt_depth, const float *sdf_s, const float *feat, const int *leaf, const float *t,
                          const int *ray_of, int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c,
-                         int *leaf_c, float *t_c, int *ray_of_c, float *rgb_c, int *counts, unsigned long long *desc,
-                         uint32_t tag) {
+                         int *leaf_c, float *t_c, int *ray_of_c, float *rgb_c, int *src_c, int *counts,
+                         unsigned long long *desc, uint32_t tag) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0 && cap > 0,
                  "select_samples: bad sizes");
     PSVO_REQUIRE(!split || (offb != nullptr && rgb_c != nullptr),
@@ -703,7 +705,7 @@ int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncat
                  (long long)r_hit, kSelWaves * kSelMaxRpw * kLbMaxBlocks);
     if (r_hit == 0) return PSVO_OK;
     SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offa, offb,
-                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, rgb_c, cap, split ? 1 : 0, counts, desc, tag};
+                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, rgb_c, src_c, cap, split ? 1 : 0, counts, desc, tag};
     psvo::launch(k_select_samples, dim3(div_up(r_hit, (int64_t)kSelWaves * rpw)), dim3(64 * kSelWaves), 0, st, r_hit,
                  rpw, s_max, truncation, max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_depth, sdf_s, a);
     return check_launch("select_samples");

@@ -36,7 +36,7 @@ enum Slot {
     // the sparse decoder (select_samples): compact index, ray offsets, the kept samples' rows, counts, look-back
     kCidx, kOffB, kFeatB, kLeafB, kTB, kRayOfB, kSdfB, kSelCnt, kSelDesc,
     // its class B (the trunk only): ray offsets, activations and masks
-    kOffB2, kSlots
+    kOffB2, kH2, kSrcC, kSlots
 };
 
 struct Arena {
@@ -785,7 +785,10 @@ struct Render {
     bool z_recorded = false;  // e->z_ready marks the sample compaction on st (aux has not waited yet)
     int z_stride = 0;         // row stride of z_vals: s_max (padded copy) or the sampler's row capacity
     bool sparse = false;      // the decoder ran the sdf trunk only (sdf_s): the rest after select_samples
+    float *h2 = nullptr;      // (sparse, width 128) every sample's h2 rows [m][128] from the sdf trunk
 };
+
+constexpr int64_t kW128 = 128;  // h2 row length (the width-128 decoder)
 
 #define Q_BUF(T, name, slot, bytes)                                              \
     T *name = reinterpret_cast<T *>(arena_buf(q.a, st, slot, (bytes), &rc));    \
@@ -1065,13 +1068,19 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     const int64_t m_early = std::min<int64_t>(e->m_early, (int64_t)qset.R * max_steps);
     const bool early = rays_path && sparse && width == 128 && qset.compacted && qset.a.p[kMDev] && m_early > 0 &&
                        (early_images || prebuilt) && !(e->paths & PSVO_PATH_QUERY_SPLIT);
-    float *feat_e = nullptr, *sdf_e = nullptr;
+    float *feat_e = nullptr, *sdf_e = nullptr, *h2_e = nullptr;
+    // the sparse decoder (width 128): the sdf trunk hands every sample's h2 to
+    // the later layers (k_mlp_fwd2 / k_mlp_trunk_fb read it instead of
+    // recomputing the W2 layer)
+    const bool want_h2 = sparse && width == 128;
     if (early) {
         const int *m_dev = static_cast<const int *>(qset.a.p[kMDev]);
         ENG_BUF(float, fe, kFeat, m_early * 16 * sizeof(float));
         ENG_BUF(float, se, kSdfS, m_early * sizeof(float));
+        ENG_BUF(float, he, kH2, m_early * kW128 * sizeof(float));
         feat_e = fe;
         sdf_e = se;
+        h2_e = he;
         ENG_CALL(join_adam(e, st, who, 2000.0));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
         ENG_CALL(psvo::interp_fwd_dev(st, m_early, m_dev, d->voxel_size, static_cast<const int *>(qset.a.p[kLeafQ]),
@@ -1082,8 +1091,9 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         mark(e, st, PSVO_TIME_MLP_FWD, 0);
         if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        const psvo::H2Rows h2o{h2_e, nullptr, nullptr};
         ENG_CALL(mlp_fwd_prepared(stream, m_early, width, feat_e, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7],
-                                  W[8], W[9], images, sdf_e, nullptr, nullptr, nullptr, m_dev));
+                                  W[8], W[9], images, sdf_e, nullptr, nullptr, nullptr, m_dev, &h2o));
         // the loss normalisers need only z (the sampler's rows): aux may start
         // them after these (a marker in front of them delays the interpolation)
         if (engine_overlap(e) && need_z_event) {
@@ -1169,6 +1179,12 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     }
     ENG_BUF(float, sdf_s, kSdfS, M * sizeof(float));
     if (early_done && sdf_s != sdf_e) return set_error(PSVO_E_LAUNCH, "%s: sdf buffer moved", who);
+    float *h2_s = nullptr;
+    if (want_h2) {
+        ENG_BUF(float, hb, kH2, M * kW128 * sizeof(float));
+        if (early_done && hb != h2_e) return set_error(PSVO_E_LAUNCH, "%s: h2 buffer moved", who);
+        h2_s = hb;
+    }
     float *rgb_s = nullptr, *act = nullptr;
     uint64_t *masks = nullptr;
     // sparse: the sdf trunk (h1, h2, the sdf row: 18.6 of 53.8 k MACs per
@@ -1186,12 +1202,16 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
         masks = mbuf;
     }
     if (!early) mark(e, st, PSVO_TIME_MLP_FWD, 0);  // (the device-sized forward opened it)
+    o.h2 = nullptr;
     if (early_done) {
+        o.h2 = h2_s;
     } else if (early_images || prebuilt) {
         if (early_images && hipStreamWaitEvent(st, e->prep_done, 0) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "%s: stream wait failed", who);
+        const psvo::H2Rows h2o{h2_s, nullptr, nullptr};
         ENG_CALL(mlp_fwd_prepared(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                                  images, sdf_s, rgb_s, act, masks));
+                                  images, sdf_s, rgb_s, act, masks, nullptr, &h2o));
+        o.h2 = h2_s;
     } else {
         ENG_CALL(psvo_mlp_fwd(stream, M, width, feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
                               images, sdf_s, rgb_s, act, masks));
@@ -1419,6 +1439,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     int *cidx = nullptr, *sel_cnt = nullptr;
     const bool two_class = q.sparse && d->width == 128;
     int *offb = nullptr;
+    const int *h2_src = nullptr;  // the kept samples' rows of q.h2 (class A at [0, M), B at [M, 2 M))
     if (q.sparse && !empty) {
         const int64_t M2 = 2 * M;  // the compact rows: class A at [0, M), class B at [M, 2 M)
         ENG_BUF(int, cx, kCidx, M * sizeof(int));
@@ -1441,18 +1462,25 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             offb = ob;
         }
         ENG_BUF(float, rgb_c, kRgbS, M2 * 3 * sizeof(float));
+        int *src_c = nullptr;
+        if (q.h2) {
+            ENG_BUF(int, sc, kSrcC, M2 * sizeof(int));
+            src_c = sc;
+        }
         e->sel_tag = e->sel_tag == 0xffffffffu ? 1u : e->sel_tag + 1u;
         mark(e, st, PSVO_TIME_SELECT, 0);
         ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                       q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, M,
-                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, rgb_c, cnt, desc,
-                                      e->sel_tag));
+                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, rgb_c, src_c, cnt,
+                                      desc, e->sel_tag));
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
         ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
+        const psvo::H2Rows h2r{nullptr, q.h2, src_c};
         ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_c, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                                  q.images, sdf_b, rgb_c, act, masks, cnt));
+                                  q.images, sdf_b, rgb_c, act, masks, cnt, src_c ? &h2r : nullptr));
+        h2_src = src_c;
         mark(e, st, PSVO_TIME_MLP_FWD, 1);
         qb.offsets = offa;
         qb.leaf = leaf_c;
@@ -1605,7 +1633,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     const psvo::InterpFuse ipf_b{qb.leaf + M, qb.ray_of + M, q.rank_ray, d->vertex_idx, qb.tt + M, rays_o, rays_d,
                                  d->centres, d->emb, d->voxel_size, grad_emb, gx ? gx + 3 * M : nullptr, mark_into};
     const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, g_sdf_s + M, qb.feat + M * 16,
-                             fuse_ib ? &ipf_b : nullptr};
+                             fuse_ib ? &ipf_b : nullptr, h2_src ? q.h2 : nullptr, h2_src ? h2_src + M : nullptr};
     ENG_CALL(mlp_bwd(st, M, d->width, qb.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      qb.rgb_s, qb.act, qb.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6],
                      G[7], G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr,

@@ -229,6 +229,24 @@ __device__ __forceinline__ void store_rows(float *dst, int64_t s, bool valid, in
                 make_float4(v[b][4 * rg], v[b][4 * rg + 1], v[b][4 * rg + 2], v[b][4 * rg + 3]);
 }
 
+// load_rows' inverse: row `row` of a row-major [·][128] matrix into
+// accumulator form (zeros when !valid)
+__device__ __forceinline__ void load_rows(const float *__restrict__ src, int64_t row, bool valid, f32x16 (&v)[kNB],
+                                          int h) {
+    const float *p = src + (valid ? row : 0) * kW;
+#pragma unroll
+    for (int b = 0; b < kNB; ++b)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+            float4 q = *reinterpret_cast<const float4 *>(p + 32 * b + 8 * rg + 4 * h);
+            if (!valid) q = make_float4(0.f, 0.f, 0.f, 0.f);
+            v[b][4 * rg] = q.x;
+            v[b][4 * rg + 1] = q.y;
+            v[b][4 * rg + 2] = q.z;
+            v[b][4 * rg + 3] = q.w;
+        }
+}
+
 // Activations and δ's the weight gradients consume are stored TILE-FEATURE
 // major ("CF"): per 32-sample tile a [128 feature][32 slot] block (16 KB) in
 // which tile-local sample c sits at position p = (c&1)·16 + c/2 (the two
@@ -559,8 +577,7 @@ constexpr int kStampIters = 8, kStampWgs = 256;  // psvo_g_stamps[2][256][8][8][
 #define PSVO_STAMP(i)                                                                               \
     do {                                                                                            \
         __builtin_amdgcn_sched_barrier(0);                                                          \
-        unsigned long long t_;                                                                      \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                 \
         __builtin_amdgcn_sched_barrier(0);                                                          \
         if ((threadIdx.x & 63) == 0 && stit_ < kStampIters && blockIdx.x < kStampWgs)               \
             psvo_g_stamps[kStampK][blockIdx.x][threadIdx.x >> 6][stit_][i] = t_;                         \
@@ -660,13 +677,20 @@ __device__ __forceinline__ void stage8(float *dst, const float *img, int n_float
     for (int c = wave; c < n_floats / 256; c += kF2Waves) glds16(img + (c * 64 + lane) * 4, dst + c * 256);
 }
 
+template <bool H2>
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const float *__restrict__ feat,
                                                             const float *__restrict__ img,
                                                             float *__restrict__ sdf_out, float *__restrict__ rgb_out,
                                                             float *__restrict__ act, uint64_t *__restrict__ masks,
-                                                            const int *__restrict__ m_dev) {
+                                                            const int *__restrict__ m_dev,
+                                                            const float *__restrict__ h2_rows,
+                                                            const int *__restrict__ h2_src) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (m_dev) m = __builtin_amdgcn_readfirstlane(*m_dev);  // the sparse decoder's kept samples (<= m)
+    // h2_rows: h2 of every sample of the step (k_mlp_sdf2's, the same
+    // instructions: the same bits), sample s's row h2_src[s] — the W2 layer
+    // is read instead of recomputed (W3 / W4 stream through the buffers)
+    constexpr bool h2_given = H2;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
@@ -686,20 +710,22 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     auto buf = [&](int i) { return lds + ((i & 1) ? kF2Buf1 : kF2Buf0); };
     int seq = 0;  // staged layers so far: W(seq) sits in buf(seq)
     float xn[8];
+    int srcn = 0;
     {
         const int64_t u = u0 + wave;
         const int64_t s = u * kTileS + (lane & 31);
         load_x(feat, s, u < u1 && s < m, h, xn);
+        if (h2_given && u < u1 && s < m) srcn = h2_src[s];
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
-    stage8(buf(0), img + kImgF2, 16384, wave, lane);
+    stage8(buf(0), img + (h2_given ? kImgF3 : kImgF2), 16384, wave, lane);
     wait_vm(0);
     raw_barrier();
     [[maybe_unused]] constexpr int kStampK = 0;
     PSVO_STAMP_DECL;
     for (int it = 0; it < n_it; ++it) {
-        PSVO_STAMP(0);
+        if (!H2) PSVO_STAMP(0);  // (the h2-reading instantiation: no stamps — the diagnostic build hit a backend error there)
         const int64_t u = u0 + (int64_t)it * kF2Waves + wave;
         const bool active = u < u1;  // wave-uniform
         const int64_t s = u * kTileS + (lane & 31);
@@ -708,6 +734,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = xn[i];
+        const int src = srcn;
         const CfStore cfs(u, lane, n_tiles);
         f32x16 a[kNB], bacc[kNB];
         uint64_t m1 = 0, m2 = 0;
@@ -718,16 +745,24 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
             gemm_x(lds + kF2W1, x, a, lane);
             m1 = relu(a);
         }
-        // h2 = relu(W2 h1 + b2)
-        wait_vm(0);
-        raw_barrier();
-        stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
-        if (active) {
-            init_bias(bacc, lds + kOffB2, h);
-            gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
-            m2 = relu(bacc);
+        if (h2_given) {  // h2 read (its row of the step's h2), h1's stores
+            if (active) {
+                load_rows(h2_rows, src, valid, bacc, h);
+                if (save) cfs.store(act, tbytes, a);
+                m2 = relu(bacc);  // post-ReLU values: the same values and mask bits
+            }
+        } else {
+            // h2 = relu(W2 h1 + b2)
+            wait_vm(0);
+            raw_barrier();
+            stage8(buf(seq + 1), img + kImgF3, 16384, wave, lane);
+            if (active) {
+                init_bias(bacc, lds + kOffB2, h);
+                gemm_acc<kNB, kNB>(buf(seq), a, bacc, lane, CfQueue(cfs, act, tbytes, save, a));  // + h1 stores
+                m2 = relu(bacc);
+            }
+            ++seq;
         }
-        ++seq;
         // [sdf | f] = W3 h2 + b3
         wait_vm(0);
         raw_barrier();
@@ -742,14 +777,15 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
         wait_vm(0);
         raw_barrier();
         if (more) {
-            stage8(buf(seq + 1), img + kImgF2, 16384, wave, lane);
+            stage8(buf(seq + 1), img + (h2_given ? kImgF3 : kImgF2), 16384, wave, lane);
             const int64_t un = u + kF2Waves;
             const int64_t sn = un * kTileS + (lane & 31);
             load_x(feat, sn, un < u1 && sn < m, h, xn);
+            if (h2_given && un < u1 && sn < m) srcn = h2_src[sn];
         }
         if (!active) {
             ++seq;
-            PSVO_STAMP(8);
+            if (!H2) PSVO_STAMP(8);
             PSVO_STAMP_FLUSH(0);
             continue;
         }
@@ -789,7 +825,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
             rgb_out[s * 3 + 1] = rgb[1];
             rgb_out[s * 3 + 2] = rgb[2];
         }
-        PSVO_STAMP(8);
+        if (!H2) PSVO_STAMP(8);
         PSVO_STAMP_FLUSH(0);
     }
     wait_vm(0);
@@ -803,7 +839,8 @@ constexpr int kLdsSdf2 = (kF2Buf0 + 16384) * 4;
 
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, const float *__restrict__ feat,
                                                             const float *__restrict__ img,
-                                                            float *__restrict__ sdf_out, const int *__restrict__ m_dev) {
+                                                            float *__restrict__ sdf_out, const int *__restrict__ m_dev,
+                                                            float *__restrict__ h2_out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // m_dev: the count on the device, m_host the buffers' capacity (a larger
     // batch: nothing here, the host-sized launch after the read-back)
@@ -846,6 +883,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_sdf2(int64_t m_host, cons
         (void)relu(bacc);
         const float sdf = __fadd_rn(lds[kOffB3], row_dot(lds + kOffW3r0, bacc, h));
         if (valid && h == 0) sdf_out[s] = sdf;
+        if (h2_out) store_rows(h2_out, s, valid, kW, bacc, h);  // (the sparse decoder's later layers read it)
     }
     wait_vm(0);
 }
@@ -1593,12 +1631,15 @@ __device__ __forceinline__ void dw_job_lds(const float *dset, const float *cf, i
 struct TrunkIn {
     float gs;
     float4 x;
+    int src;  // the sample's h2 row (h2 given), else 0
 };
 __device__ __forceinline__ void load_trunk_in(const float *__restrict__ g_sdf, const float *__restrict__ feat,
-                                              int64_t s, bool valid, int q, TrunkIn &in) {
+                                              const int *__restrict__ src, int64_t s, bool valid, int q,
+                                              TrunkIn &in) {
     const int64_t sv = valid ? s : 0;
     in.gs = g_sdf[sv];
     in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
+    in.src = src && valid ? src[sv] : 0;
 }
 
 template <int NOB>
@@ -1651,9 +1692,10 @@ __device__ __forceinline__ void gemm16_stream(__amdgpu_buffer_rsrc_t rs, int img
 // gradient wave k: the trunk forward of unit k of round r (chain layout: lane
 // (n, q) holds features 16·ob + 4q + j of sample n) → x image, h1 CF tile,
 // δh2 unit image, h1 mask words; W3 row 0 / b3[0] partials into `page3`
+template <bool H2>
 __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_t wrs, const TrunkIn &in, int64_t u,
                                                int64_t u1, int64_t m, int k, int lane, int wb, float *xl,
-                                               float *page3, float &b30p) {
+                                               float *page3, float &b30p, const float *__restrict__ h2) {
     const int n = lane & 15, q = lane >> 4;
     const int64_t s = u * kU + n;
     const bool active = u < u1;  // wave-uniform
@@ -1665,6 +1707,7 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
     xl[wb + 32] = xv.z;
     xl[wb + 48] = xv.w;
     if (!active) return;
+    f32x4v fb[8];
     f32x4v xin[1] = {f32x4v{xv.x, xv.y, xv.z, xv.w}};
     f32x4v hb[8];
 #pragma unroll
@@ -1673,6 +1716,15 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
         hb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
     }
     gemm16_stream<1, 8, 3>(wrs, kImgT1, xin, hb, lane);  // h1 = W1 x + b1
+    if (H2) {  // h2 read: features 16 ob + 4q .. + 3 of the sample's row (in flight under h1's ReLU and stores)
+        const float *row = h2 + (int64_t)in.src * kW;
+#pragma unroll
+        for (int ob = 0; ob < 8; ++ob) {
+            float4 v = *reinterpret_cast<const float4 *>(row + 16 * ob + 4 * q);
+            if (!valid) v = make_float4(0.f, 0.f, 0.f, 0.f);
+            fb[ob] = f32x4v{v.x, v.y, v.z, v.w};
+        }
+    }
     const uint64_t m1 = relu16(hb);
     reinterpret_cast<uint64_t *>(lds + kT4M)[k * 64 + lane] = m1;
     {  // h1 → the CF tile (dW2's B operand; k_mlp_fwd2's layout): row 16 ob + 4q + j,
@@ -1687,15 +1739,16 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
             for (int ob = 0; ob < 8; ++ob) cj[16 * ob * kTileS] = hb[ob][j];
         }
     }
-    f32x4v fb[8];
+    if (!H2) {
 #pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-        const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
-        fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+        for (int ob = 0; ob < 8; ++ob) {
+            const float4 bb = *reinterpret_cast<const float4 *>(lds + kOffB2 + 16 * ob + 4 * q);
+            fb[ob] = f32x4v{bb.x, bb.y, bb.z, bb.w};
+        }
+        // h2 = W2 h1 + b2: output-block pairs, one ring across them (beside the dW2
+        // accumulators a ring over all 8 output blocks spills)
+        gemm16_stream<8, 8, 3>(wrs, kImgT2, hb, fb, lane);
     }
-    // h2 = W2 h1 + b2: output-block pairs, one ring across them (beside the dW2
-    // accumulators a ring over all 8 output blocks spills)
-    gemm16_stream<8, 8, 3>(wrs, kImgT2, hb, fb, lane);
     const uint64_t m2 = relu16(fb);
     {  // W3 row 0 += Σ_n dsdf · h2 (the unit's 16 samples by DPP row sums, into the page)
         f32x4v r0[8];
@@ -1722,11 +1775,14 @@ __device__ __forceinline__ void trunk_fwd_unit(float *lds, __amdgpu_buffer_rsrc_
     lds_u_store<8>(lds + kT4H2 + k * kUImg, wb, fb);
 }
 
+template <bool H2>
 __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__restrict__ m_dev,
                                                                 const float *__restrict__ img,
                                                                 const float *__restrict__ g_sdf,
                                                                 const float *__restrict__ feat, DwGrid g,
-                                                                float *__restrict__ slabs, InterpFuse ip) {
+                                                                float *__restrict__ slabs, InterpFuse ip,
+                                                                const float *__restrict__ h2,
+                                                                const int *__restrict__ h2_src) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int64_t m = __builtin_amdgcn_readfirstlane(*m_dev);
     const int lane = threadIdx.x & 63;
@@ -1884,13 +1940,13 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
         auto load_in = [&](int r) {
             const int64_t u = u0 + 4 * (int64_t)r + d;
             const int64_t s = u * kU + n;
-            load_trunk_in(g_sdf, feat, s, u < u1 && s < m, q, nin);
+            load_trunk_in(g_sdf, feat, H2 ? h2_src : nullptr, s, u < u1 && s < m, q, nin);
         };
         if (n_rounds > 0) {  // the forward of round 0
             load_in(0);
             const TrunkIn in = nin;
             if (n_rounds > 1) load_in(1);
-            trunk_fwd_unit(lds, wrs, in, u0 + d, u1, m, d, lane, wb, xset(0) + d * 16 * kU, page3, b30p);
+            trunk_fwd_unit<H2>(lds, wrs, in, u0 + d, u1, m, d, lane, wb, xset(0) + d * 16 * kU, page3, b30p, h2);
         }
         for (int r = 0; r < n_rounds; ++r) {
             PSVO_STAMP(0);
@@ -1907,8 +1963,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_trunk_fb(const int *__res
             if (r + 1 < n_rounds) {
                 const TrunkIn in = nin;
                 if (r + 2 < n_rounds) load_in(r + 2);
-                trunk_fwd_unit(lds, wrs, in, ubase + 4 + d, u1, m, d, lane, wb, xset(r + 1) + d * 16 * kU, page3,
-                               b30p);
+                trunk_fwd_unit<H2>(lds, wrs, in, ubase + 4 + d, u1, m, d, lane, wb, xset(r + 1) + d * 16 * kU,
+                                   page3, b30p, h2);
             }
             PSVO_STAMP(6);
             PSVO_STAMP_FLUSH(0);
@@ -2003,7 +2059,8 @@ extern "C" int64_t psvo_mlp_mask_words(int64_t m, int width) {
 static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                             const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                             const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                            float *act, uint64_t *masks, bool images_ready, const int *m_dev = nullptr) {
+                            float *act, uint64_t *masks, bool images_ready, const int *m_dev = nullptr,
+                            const H2Rows *h2 = nullptr) {
     if (width == 256) {
         PSVO_REQUIRE(m >= 0, "mlp_fwd: m < 0");
         PSVO_REQUIRE(images != nullptr, "mlp_fwd: images workspace required (psvo_mlp_image_floats_w floats)");
@@ -2036,19 +2093,24 @@ static int mlp_fwd_impl(void *stream, int64_t m, int width, const float *feat, c
         }
         const int64_t tiles = div_up(m, kF2Tile);
         const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-        psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf, m_dev);
+        psvo::launch(k_mlp_sdf2, dim3(grid), dim3(kF2Threads), kLdsSdf2, st, m, feat, images, sdf, m_dev,
+                     h2 ? h2->out : nullptr);
         return check_launch("mlp_fwd");
     }
     static bool attr2 = false;
     if (!attr2) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_fwd2<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsFwd2);
         attr2 = true;
     }
     const int64_t tiles = div_up(m, kF2Tile);  // ≥ 8 units per workgroup
     const int grid = (int)(tiles < device_cus() ? tiles : device_cus());
-    psvo::launch(k_mlp_fwd2, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat, images, sdf, rgb, act, masks,
-                 m_dev);
+    PSVO_REQUIRE(!h2 || !h2->rows || h2->src, "mlp_fwd: h2 rows need their source index");
+    const bool h2r = h2 && h2->rows;
+    psvo::launch(h2r ? k_mlp_fwd2<true> : k_mlp_fwd2<false>, dim3(grid), dim3(kF2Threads), kLdsFwd2, st, m, feat,
+                 images, sdf, rgb, act, masks, m_dev, h2r ? h2->rows : nullptr, h2r ? h2->src : nullptr);
     return check_launch("mlp_fwd");
 }
 
@@ -2064,9 +2126,9 @@ int mlp_images(void *stream, int width, const float *w1, const float *b1, const 
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                     float *act, uint64_t *masks, const int *m_dev) {
+                     float *act, uint64_t *masks, const int *m_dev, const H2Rows *h2) {
     return mlp_fwd_impl(stream, m, width, feat, w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, images, sdf, rgb, act, masks,
-                        true, m_dev);
+                        true, m_dev, h2);
 }
 }  // namespace psvo
 
@@ -2198,13 +2260,17 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         if (tb && m > 0) {  // the sparse decoder's class B: the trunk forward + backward, its own slabs
             static bool attr_t = false;
             if (!attr_t) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk_fb),
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk_fb<true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTrunk);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mlp_trunk_fb<false>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTrunk);
                 attr_t = true;
             }
             slabs_b = slabs + slab_floats;
-            psvo::launch(k_mlp_trunk_fb, dim3(grid), dim3(kF2Threads), kLdsTrunk, st, tb->m_dev, images, tb->g_sdf,
-                         tb->feat, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{});
+            PSVO_REQUIRE(!tb->h2 || tb->src, "mlp_bwd: the trunk's h2 rows need their source index");
+            psvo::launch(tb->h2 ? k_mlp_trunk_fb<true> : k_mlp_trunk_fb<false>, dim3(grid), dim3(kF2Threads), kLdsTrunk,
+                         st, tb->m_dev, images, tb->g_sdf, tb->feat, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{},
+                         tb->h2, tb->src);
             const int rc = check_launch("mlp_trunk_fb");
             if (rc) return rc;
         }

@@ -241,7 +241,8 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
 // (split = false: every kept sample in class A) —, the classes' compact ray
 // offsets offa / offb [R_hit + 1] and compact copies of their features /
 // leaf / t / ray ([2 cap] arrays; split: class B's colour rows of rgb_c
-// [2 cap][3] are written 0 — their composite weights are 0).  counts[0] = M_A, counts[1] = M_B (the
+// [2 cap][3] are written 0 — their composite weights are 0; src_c [2 cap],
+// if not null: each kept sample's index in the step's sample order).  counts[0] = M_A, counts[1] = M_B (the
 // compact decoder launches read them on the device), counts[2] |= 8 if the
 // look-back wait was abandoned (then both are 0); counts + 4: u64 running
 // sums of kept / composited samples and of launches (kSelCountInts ints,
@@ -252,7 +253,7 @@ int select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, f
                    const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_depth,
                    const float *sdf_s, const float *feat, const int *leaf, const float *t, const int *ray_of,
                    int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c, int *leaf_c, float *t_c,
-                   int *ray_of_c, float *rgb_c, int *counts, unsigned long long *desc, uint32_t tag);
+                   int *ray_of_c, float *rgb_c, int *src_c, int *counts, unsigned long long *desc, uint32_t tag);
 int select_rays_per_wave(int64_t r_hit);
 int64_t select_granules(int64_t r_hit);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):
@@ -364,6 +365,8 @@ struct TrunkBwd {
     const int *m_dev;
     const float *g_sdf, *feat;
     const InterpFuse *ip;
+    const float *h2 = nullptr;  // or: the step's h2 rows (H2Rows) and each class-B sample's row —
+    const int *src = nullptr;   // the W2 layer is read instead of recomputed
 };
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
             const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
@@ -385,10 +388,21 @@ bool mlp_bwd_split_tail(int width);
 int mlp_images(void *stream, int width, const float *w1, const float *b1, const float *w2, const float *b2,
                const float *w3, const float *b3, const float *w4, const float *b4, const float *w5, const float *b5,
                float *images);
+// the sparse decoder's h2 hand-over (width 128): the sdf-only forward
+// (rgb == nullptr) writes every sample's h2 as row-major rows into `out`
+// [m][128]; the full forward (k_mlp_fwd2) reads sample s's h2 from row src[s]
+// of `rows` instead of recomputing the W2 layer (the same instructions made
+// it: the same bits)
+struct H2Rows {
+    float *out = nullptr;
+    const float *rows = nullptr;
+    const int *src = nullptr;
+};
 int mlp_fwd_prepared(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1,
                      const float *w2, const float *b2, const float *w3, const float *b3, const float *w4,
                      const float *b4, const float *w5, const float *b5, float *images, float *sdf, float *rgb,
-                     float *act, uint64_t *masks, const int *m_dev = nullptr);  // m_dev: as mlp_bwd (width 128)
+                     float *act, uint64_t *masks, const int *m_dev = nullptr,
+                     const H2Rows *h2 = nullptr);  // m_dev: as mlp_bwd (width 128)
 
 }  // namespace psvo
 
