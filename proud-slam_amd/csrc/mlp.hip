@@ -739,15 +739,16 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
         f32x16 a[kNB], bacc[kNB];
         uint64_t m1 = 0, m2 = 0;
         float sdf = 0.f;
+        // h2 read (its row of the step's h2): in flight under the W1 layer
+        if (h2_given && active) load_rows(h2_rows, src, valid, bacc, h);
         // h1 = relu(W1 x + b1): resident W1
         if (active) {
             init_bias(a, lds + kOffB1, h);
             gemm_x(lds + kF2W1, x, a, lane);
             m1 = relu(a);
         }
-        if (h2_given) {  // h2 read (its row of the step's h2), h1's stores
+        if (h2_given) {  // h1's stores; h2's mask
             if (active) {
-                load_rows(h2_rows, src, valid, bacc, h);
                 if (save) cfs.store(act, tbytes, a);
                 m2 = relu(bacc);  // post-ReLU values: the same values and mask bits
             }
