@@ -63,6 +63,8 @@ struct QuerySet {
     hipEvent_t freed = nullptr;   // the consuming step finished with the buffers
     bool freed_recorded = false;
     hipStream_t freed_on = nullptr;  // the stream `freed` was recorded on (a wait on that stream is implied)
+    bool freed_lazy = false;         // released on freed_on, event not recorded yet (a consumer on
+                                     // another stream records it then: a later point of freed_on)
     bool pending = false;
     int64_t R = 0;
     const float *ro = nullptr, *rd = nullptr;
@@ -461,6 +463,7 @@ extern "C" int psvo_map_discard(psvo_engine *e) {
         if (qs && hipEventRecord(q.freed, qs) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_discard: event record failed");
         q.freed_recorded = qs != nullptr;
+        q.freed_lazy = false;
         q.freed_on = qs;
         q.pending = false;
         e->q_head ^= 1;
@@ -965,6 +968,21 @@ int take_query(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, int64_t R
 // Give back the head query set once the step's kernels are queued.
 int release_query(psvo_engine *e, hipStream_t st, QuerySet *q);
 
+// `s` waits until the set's last consumer is done with its buffers (nothing
+// when that consumer ran on `s` itself)
+int freed_wait(QuerySet &q, hipStream_t s) {
+    if (q.freed_lazy) {
+        if (q.freed_on == s) return PSVO_OK;
+        if (hipEventRecord(q.freed, q.freed_on) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "engine: event record failed");
+        q.freed_lazy = false;
+        q.freed_recorded = true;
+    }
+    if (q.freed_recorded && q.freed_on != s && hipStreamWaitEvent(s, q.freed, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine: stream ordering failed");
+    return PSVO_OK;
+}
+
 // Drops the step's query set if the step fails after take_query: without it a
 // failed batch (no hit ray, sampler overflow) would stay at the FIFO head and
 // every later step would be refused as "rays differ from the queued batch".
@@ -983,8 +1001,10 @@ struct QueryGuard {
 };
 
 int release_query(psvo_engine *e, hipStream_t st, QuerySet *q) {
-    if (hipEventRecord(q->freed, st) != hipSuccess) return set_error(PSVO_E_LAUNCH, "engine: event record failed");
-    q->freed_recorded = true;
+    // no marker packet on st now (between two kernels one costs ≈ 5 µs):
+    // a consumer on another stream records it when it needs it (freed_wait)
+    q->freed_lazy = true;
+    q->freed_recorded = false;
     q->freed_on = st;
     if (e->q_count > 0 && q == &e->qs[e->q_head]) {
         q->pending = false;
@@ -1342,8 +1362,7 @@ int frames_lookahead(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, con
     QuerySet &q = e->qs[e->q_head];
     // the set's last consumer ran on st itself: stream order suffices (no wait
     // packet between the backward and the pose step)
-    if (q.freed_recorded && q.freed_on != st && hipStreamWaitEvent(st, q.freed, 0) != hipSuccess)
-        return set_error(PSVO_E_LAUNCH, "map_step_frames: stream ordering failed");
+    ENG_CALL(freed_wait(q, st));
     ENG_BUF(float, rays_o, kRaysO, (size_t)R * 3 * sizeof(float));
     ENG_BUF(float, rays_d, kRaysD, (size_t)R * 3 * sizeof(float));
     float *pg = fr->pose_grad;
@@ -1795,9 +1814,9 @@ extern "C" int psvo_map_query(psvo_engine *e, void *stream, const psvo_map_desc 
     QuerySet &q = e->qs[(e->q_head + e->q_count) & 1];
     // the rays were produced on the caller's stream; the set's buffers may
     // still be read by the step that consumed it last
-    if (hipEventRecord(e->in_ready, st) != hipSuccess || hipStreamWaitEvent(e->side, e->in_ready, 0) != hipSuccess ||
-        (q.freed_recorded && hipStreamWaitEvent(e->side, q.freed, 0) != hipSuccess))
+    if (hipEventRecord(e->in_ready, st) != hipSuccess || hipStreamWaitEvent(e->side, e->in_ready, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "map_query: stream ordering failed");
+    ENG_CALL(freed_wait(q, e->side));
     // (a buffer that must grow syncs the side stream first, which includes that wait)
     ENG_CALL(query_enqueue(e, e->side, q, d, n_rays, rays_o, rays_d, seed, "map_query"));
     q.pending = true;
