@@ -617,8 +617,10 @@ __global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, 
                 a.t_c[j] = a.t[src];
                 a.ray_of_c[j] = (int)r;
                 if (a.src_c) a.src_c[j] = (int)src;
+                if (a.feat_c) {  // (null: the consumers read row src_c[j] of the step's features)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) a.feat_c[j * 4 + q] = a.feat[src * 4 + q];
+                    for (int q = 0; q < 4; ++q) a.feat_c[j * 4 + q] = a.feat[src * 4 + q];
+                }
                 if (in_b) {
 #pragma unroll
                     for (int k = 0; k < 3; ++k) a.rgb_c[j * 3 + k] = 0.f;

@@ -1463,7 +1463,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         const int64_t M2 = 2 * M;  // the compact rows: class A at [0, M), class B at [M, 2 M)
         ENG_BUF(int, cx, kCidx, M * sizeof(int));
         ENG_BUF(int, offa, kOffB, (size_t)(r_hit + 1) * sizeof(int));
-        ENG_BUF(float, feat_c, kFeatB, M2 * 16 * sizeof(float));
+        // the compact feature copy: width 256 only (width 128 reads the step's rows by src_c)
+        float *feat_c = nullptr;
+        if (!q.h2) {
+            ENG_BUF(float, fc, kFeatB, M2 * 16 * sizeof(float));
+            feat_c = fc;
+        }
         ENG_BUF(int, leaf_c, kLeafB, M2 * sizeof(int));
         ENG_BUF(float, t_c, kTB, M2 * sizeof(float));
         ENG_BUF(int, ray_of_c, kRayOfB, M2 * sizeof(int));
@@ -1497,15 +1502,15 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
         ENG_BUF(uint64_t, masks, kMasks, (size_t)psvo_mlp_mask_words(M, d->width) * sizeof(uint64_t));
         const psvo::H2Rows h2r{nullptr, q.h2, src_c};
-        ENG_CALL(mlp_fwd_prepared(st, M, d->width, feat_c, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9],
-                                  q.images, sdf_b, rgb_c, act, masks, cnt, src_c ? &h2r : nullptr));
+        ENG_CALL(mlp_fwd_prepared(st, M, d->width, src_c ? q.feat : feat_c, W[0], W[1], W[2], W[3], W[4], W[5], W[6],
+                                  W[7], W[8], W[9], q.images, sdf_b, rgb_c, act, masks, cnt, src_c ? &h2r : nullptr));
         h2_src = src_c;
         mark(e, st, PSVO_TIME_MLP_FWD, 1);
         qb.offsets = offa;
         qb.leaf = leaf_c;
         qb.tt = t_c;
         qb.ray_of = ray_of_c;
-        qb.feat = feat_c;
+        qb.feat = src_c ? q.feat : feat_c;  // (src_c: x of kept sample j is row src_c[j])
         qb.rgb_s = rgb_c;
         qb.act = act;
         qb.masks = masks;
@@ -1651,12 +1656,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     // the sparse decoder's class B: its rows at [M, 2 M) of the compact arrays
     const psvo::InterpFuse ipf_b{qb.leaf + M, qb.ray_of + M, q.rank_ray, d->vertex_idx, qb.tt + M, rays_o, rays_d,
                                  d->centres, d->emb, d->voxel_size, grad_emb, gx ? gx + 3 * M : nullptr, mark_into};
-    const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, g_sdf_s + M, qb.feat + M * 16,
+    const psvo::TrunkBwd tbw{sel_cnt ? sel_cnt + 1 : nullptr, g_sdf_s + M, h2_src ? qb.feat : qb.feat + M * 16,
                              fuse_ib ? &ipf_b : nullptr, h2_src ? q.h2 : nullptr, h2_src ? h2_src + M : nullptr};
     ENG_CALL(mlp_bwd(st, M, d->width, qb.feat, W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9], q.images,
                      qb.rgb_s, qb.act, qb.masks, g_sdf_s, g_rgb_s, dfeat, G[0], G[1], G[2], G[3], G[4], G[5], G[6],
                      G[7], G[8], G[9], 0, n_split, mlp_ws, overlap ? e->dfeat_ready : nullptr,
-                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt, two_class ? &tbw : nullptr));
+                     fuse_ib ? &ipf : nullptr, split ? ax : nullptr, sel_cnt, two_class ? &tbw : nullptr, h2_src));
     mark(e, st, PSVO_TIME_MLP_BWD, 1);
     if (overlap) e->bwd_recorded = true;  // mlp_bwd recorded dfeat_ready on st
     // embedding backward: after dfeat (the fused kernel), beside the weight-gradient reduce

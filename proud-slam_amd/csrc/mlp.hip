@@ -714,8 +714,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
     {
         const int64_t u = u0 + wave;
         const int64_t s = u * kTileS + (lane & 31);
-        load_x(feat, s, u < u1 && s < m, h, xn);
         if (h2_given && u < u1 && s < m) srcn = h2_src[s];
+        load_x(feat, h2_given ? (int64_t)srcn : s, u < u1 && s < m, h, xn);  // (h2 given: feat is the step's rows)
     }
     stage8(lds, img + kImgVec, kVecPad, wave, lane);
     stage8(lds + kF2W1, img + kImgF1, 2048, wave, lane);
@@ -781,8 +781,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_fwd2(int64_t m, const flo
             stage8(buf(seq + 1), img + (h2_given ? kImgF3 : kImgF2), 16384, wave, lane);
             const int64_t un = u + kF2Waves;
             const int64_t sn = un * kTileS + (lane & 31);
-            load_x(feat, sn, un < u1 && sn < m, h, xn);
             if (h2_given && un < u1 && sn < m) srcn = h2_src[sn];
+            load_x(feat, h2_given ? (int64_t)srcn : sn, un < u1 && sn < m, h, xn);
         }
         if (!active) {
             ++seq;
@@ -1025,7 +1025,7 @@ struct BwdIn16 {
 __device__ __forceinline__ void load_bwd_in16(const float *__restrict__ rgb_in, const uint64_t *__restrict__ masks,
                                               const float *__restrict__ g_sdf, const float *__restrict__ g_rgb,
                                               const float *__restrict__ feat, int64_t s, bool valid, int q,
-                                              BwdIn16 &in) {
+                                              BwdIn16 &in, const int *__restrict__ x_src = nullptr) {
     const int64_t sv = valid ? s : 0;
     const uint64_t *mk = masks + (sv * 2 + (q & 1)) * 3;
 #pragma unroll
@@ -1035,7 +1035,8 @@ __device__ __forceinline__ void load_bwd_in16(const float *__restrict__ rgb_in, 
         in.g[i] = g_rgb[sv * 3 + i];
     }
     in.gs = g_sdf[sv];
-    in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
+    const int64_t xr = x_src ? (int64_t)x_src[sv] : sv;  // x_src: the sample's feature row (no compact copy)
+    in.x = *reinterpret_cast<const float4 *>(feat + xr * kIn + 4 * q);
 }
 
 // chain wave: acc += δ rows [32c, 32c + 32) of the round's unit images ⊗ the
@@ -1194,6 +1195,7 @@ struct Bwd3Src {
     const uint64_t *masks;
     const float *act;  // CF [h1 | h2 | f | c1]
     float *dfeat;
+    const int *x_src;  // or null: sample s's x is row x_src[s] of feat
 };
 
 // W = false (frozen decoder: dfeat only, e.g. tracking): all 8 waves run the
@@ -1252,7 +1254,7 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
         {
             const int64_t u = u0 + c;
             const int64_t s = u * kU + n;
-            load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, s, u < u1 && s < m, q, nin);
+            load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, s, u < u1 && s < m, q, nin, src.x_src);
         }
         [[maybe_unused]] constexpr int kStampK = 1;
         PSVO_STAMP_DECL;
@@ -1385,7 +1387,8 @@ __global__ __launch_bounds__(kF2Threads, 1) void k_mlp_bwd3(int64_t m, const flo
             if (r + 1 < n_rounds) {
                 const int64_t un = u + kPer;
                 const int64_t snx = un * kU + n;
-                load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, snx, un < u1 && snx < m, q, nin);
+                load_bwd_in16(src.rgb, src.masks, src.g_sdf, src.g_rgb, src.feat, snx, un < u1 && snx < m, q, nin,
+                              src.x_src);
             }
             if (active) {
                 f32x4v t1[1];
@@ -1639,8 +1642,9 @@ __device__ __forceinline__ void load_trunk_in(const float *__restrict__ g_sdf, c
                                               TrunkIn &in) {
     const int64_t sv = valid ? s : 0;
     in.gs = g_sdf[sv];
-    in.x = *reinterpret_cast<const float4 *>(feat + sv * kIn + 4 * q);
     in.src = src && valid ? src[sv] : 0;
+    in.x = *reinterpret_cast<const float4 *>(feat + (src ? (int64_t)in.src : sv) * kIn + 4 * q);  // (src: feat is
+                                                                                                 // the step's rows)
 }
 
 template <int NOB>
@@ -2185,7 +2189,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip, hipStream_t reduce_stream,
-            const int *m_dev, const TrunkBwd *tb) {
+            const int *m_dev, const TrunkBwd *tb, const int *x_src) {
     PSVO_REQUIRE(ip == nullptr || ((width == 256 || width == kW) && gw1 != nullptr),
                  "mlp_bwd: the fused interpolation backward needs a fused weight-gradient path");
     if (width == 256) {
@@ -2233,7 +2237,7 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBwd3);
             attr3 = true;
         }
-        Bwd3Src src{rgb, g_sdf, g_rgb, feat, masks, act, dfeat};
+        Bwd3Src src{rgb, g_sdf, g_rgb, feat, masks, act, dfeat, x_src};
         if (!want_w) {
             if (m > 0) {
                 const int64_t rounds = div_up(div_up(m, kU), 8);

@@ -366,7 +366,8 @@ struct TrunkBwd {
     const float *g_sdf, *feat;
     const InterpFuse *ip;
     const float *h2 = nullptr;  // or: the step's h2 rows (H2Rows) and each class-B sample's row —
-    const int *src = nullptr;   // the W2 layer is read instead of recomputed
+    const int *src = nullptr;   // the W2 layer is read instead of recomputed; feat then holds the
+                                // step's rows too (x of sample s: row src[s])
 };
 int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *w1, const float *b1, const float *w2,
             const float *b2, const float *w3, const float *b3, const float *w4, const float *b4, const float *w5,
@@ -374,7 +375,8 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             const float *g_sdf, const float *g_rgb, float *dfeat, float *gw1, float *gb1, float *gw2, float *gb2,
             float *gw3, float *gb3, float *gw4, float *gb4, float *gw5, float *gb5, int accumulate, int n_split,
             float *workspace, hipEvent_t dfeat_ready, const InterpFuse *ip = nullptr,
-            hipStream_t reduce_stream = nullptr, const int *m_dev = nullptr, const TrunkBwd *tb = nullptr);
+            hipStream_t reduce_stream = nullptr, const int *m_dev = nullptr, const TrunkBwd *tb = nullptr,
+            const int *x_src = nullptr);  // x_src (width 128): sample s's x is row x_src[s] of feat
 // whether mlp_bwd can take `ip` for this width (the fused width-128 backward is built and selected)
 bool mlp_bwd_fuses_interp(int width);
 // the look-ahead's split tail (psvo_map_step_frames): the weight-gradient
@@ -392,7 +394,8 @@ int mlp_images(void *stream, int width, const float *w1, const float *b1, const 
 // (rgb == nullptr) writes every sample's h2 as row-major rows into `out`
 // [m][128]; the full forward (k_mlp_fwd2) reads sample s's h2 from row src[s]
 // of `rows` instead of recomputing the W2 layer (the same instructions made
-// it: the same bits)
+// it: the same bits) — and its x from row src[s] of `feat` (the step's
+// features, no compact copy)
 struct H2Rows {
     float *out = nullptr;
     const float *rows = nullptr;
