@@ -443,10 +443,11 @@ __global__ __launch_bounds__(256) void k_composite_loss(int64_t r_hit, int s_max
 // z_min, the masks and `first` are computed exactly as k_composite_loss
 // computes them (same expressions, same padding).
 //
-// One wave per ray (rpw rays per wave when R_hit > 16,384: the look-back's
-// 4,096 workgroups), 4 waves per workgroup; the compact ray offsets of both
+// One wave per ray (rpw rays per wave when R_hit > 32,768: the look-back's
+// 4,096 workgroups), 8 waves per workgroup (4: 15.7 µs at config B, 8: 14.6,
+// 16: 17.4 — profiles/r05b{b,d,c}_kernel_stats.csv); the compact ray offsets of both
 // classes by decoupled look-back over {A, B, composited} (lookback.h): one launch.
-constexpr int kSelWaves = 4, kSelMaxRpw = 16;
+constexpr int kSelWaves = 8, kSelMaxRpw = 16;
 struct SelectArgs {
     const float4 *feat;      // [M][16] the interpolated features (4 float4 per sample)
     const int *leaf, *ray_of;
@@ -497,7 +498,7 @@ __device__ __forceinline__ SelFlags sel_flags(float zs, float zmin, float d, flo
     return o;
 }
 
-__global__ __launch_bounds__(256) void k_select_samples(int64_t r_hit, int rpw, int s_max, float tr, float max_depth,
+__global__ __launch_bounds__(512) void k_select_samples(int64_t r_hit, int rpw, int s_max, float tr, float max_depth,
                                                         const int *__restrict__ offsets,
                                                         const int *__restrict__ ray_ns,
                                                         const float *__restrict__ z_vals, int z_stride,
