@@ -1368,6 +1368,7 @@ struct SampleTail {
     int *m_out;  // or null: the batch's sample count M, on the device (the step's device-sized forward)
 };
 constexpr int kSmpStage = 256;  // a row's first samples staged in LDS for the in-launch compaction
+constexpr int kSmpWaves = 8;    // k_sample_fused: waves (rays) per workgroup
 // ray_cnt word: valid front / sdf samples (12 bits each), then whether a
 // padded sample (z = MAX_DEPTH) is front / sdf, whether the ray's depth is valid
 __device__ __forceinline__ int pack_counts(int nf, int nsm, bool pf, bool psm, bool valid) {
@@ -1392,7 +1393,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
                                                 int *stage_i, float *stage_z);
 
-__global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+__global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
                                                       const int *__restrict__ rank_ray,
                                                       const int *__restrict__ hit_idx,
@@ -1405,15 +1406,15 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
                                                       int *__restrict__ ray_ns, const int *__restrict__ slot0,
                                                       int slot0_nch, SampleTail tl, const int *__restrict__ nv_rank,
                                                       const int *__restrict__ col0_rank) {
-    __shared__ WaveBins bins_all[4];
+    __shared__ WaveBins bins_all[kSmpWaves];
     // look-back mode (the engine's single-GPU query: row_begin 0, all rows):
     // the rows of this batch, read before any workgroup can re-zero `stats`
     // (the last one does, after every workgroup in front of it published)
     const int n_lb = tl.desc && stats[PSVO_STAT_P] > 0 ? (int)min((int64_t)stats[PSVO_STAT_R_HIT], r_hit_cap) : 0;
-    const int last_lb = n_lb > 0 ? (n_lb - 1) / 4 : 0;  // the workgroup holding the last row
+    const int last_lb = n_lb > 0 ? (n_lb - 1) / kSmpWaves : 0;  // the workgroup holding the last row
     if (tl.desc && (int)blockIdx.x > last_lb) return;
-    __shared__ int stage_i[4][kSmpStage];
-    __shared__ float stage_z[4][kSmpStage];
+    __shared__ int stage_i[kSmpWaves][kSmpStage];
+    __shared__ float stage_z[kSmpWaves][kSmpStage];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     SMP_T(0);
     const bool compact = tl.desc && tl.leaf;
@@ -1434,7 +1435,7 @@ __global__ __launch_bounds__(256) void k_sample_fused(int64_t row_begin, int64_t
         }
         return;
     }
-    __shared__ int s_ns[4], s_cw[4], s_off[4];
+    __shared__ int s_ns[kSmpWaves], s_cw[kSmpWaves], s_off[kSmpWaves];
     if (lane == 0) {
         if (count >= 0) ray_ns[il] = count;
         s_ns[w] = count;  // -1: no row
@@ -1604,7 +1605,7 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
     for (int g = 0; g < NG; ++g) agg[g] = 0;
     int before = 0;  // samples of this workgroup's rows in front of lane's row
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kSmpWaves; ++k) {
         const int c = max(s_ns[k], 0);
         before += k < lane ? c : 0;
         agg[0] += (uint32_t)c;
@@ -1622,12 +1623,12 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's flag atomics land before its descriptors
     uint32_t ex[NG];
-    const int last = n > 0 ? (n - 1) / 4 : 0;  // the workgroups past it returned without a descriptor
+    const int last = n > 0 ? (n - 1) / kSmpWaves : 0;  // the workgroups past it returned without a descriptor
     const bool ok = lb_scan<NG, 0b10u>(tl.desc, (int)blockIdx.x, last + 1, tl.tag, lane, agg, ex);
-    const int il = (int)blockIdx.x * 4 + lane;
+    const int il = (int)blockIdx.x * kSmpWaves + lane;
     // an abandoned wait (!ok: `ex` undefined) stores no offset, and the compaction skips its rows
-    if (lane < 4) s_off[lane] = ok ? (int)ex[0] + before : -1;  // the in-launch compaction's
-    if (lane < 4 && il < n && ok) tl.offsets[il] = (int)ex[0] + before;
+    if (lane < kSmpWaves) s_off[lane] = ok ? (int)ex[0] + before : -1;  // the in-launch compaction's
+    if (lane < kSmpWaves && il < n && ok) tl.offsets[il] = (int)ex[0] + before;
     if ((int)blockIdx.x != last) return;
     const int tot = (int)(ex[0] + agg[0]);
     const int smax = (int)max(ex[1], agg[1]);
@@ -2065,7 +2066,7 @@ namespace psvo {
 // dependent sc1 round trips) and is gone.
 bool query_lookback(int64_t r) { return r > 0 && r <= kLbMaxRays; }
 int64_t lookback_granules(int64_t r) {
-    return lb_granules<kLbIsGranules>(div_up(r, 4)) + lb_granules<kLbSmpGranules>(div_up(r, 4));
+    return lb_granules<kLbIsGranules>(div_up(r, kIsWaves)) + lb_granules<kLbSmpGranules>(div_up(r, kSmpWaves));
 }
 // the single-GPU sampler with the statistics read-back fused into its scan
 // (one launch less before the host can size the rest of the step)
@@ -2083,7 +2084,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     tl.seq = seq;
     if (lb_desc) {  // after the traversal's descriptors (lookback_granules)
         tl.offsets = offsets;
-        tl.desc = lb_desc + lb_granules<kLbIsGranules>(div_up(r_hit_cap, 4));
+        tl.desc = lb_desc + lb_granules<kLbIsGranules>(div_up(r_hit_cap, kIsWaves));
         tl.tag = lb_tag;
         if (leaf && t && ray_of) {
             tl.leaf = leaf;
@@ -2092,7 +2093,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
             tl.m_out = m_out;
         }
     }
-    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, -1, r_hit_cap, max_steps_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, kSmpWaves)), dim3(64 * kSmpWaves), 0, st, 0, -1, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, nullptr, 0, tl, nv_rank, col0_rank);
     if (!lb_desc)
@@ -2160,7 +2161,7 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
                 int *offsets, const int *nv_rank, const int *col0_rank) {
     if (r_hit_cap == 0) return PSVO_OK;
-    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, 0, 0, r_hit_cap, max_steps_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, kSmpWaves)), dim3(64 * kSmpWaves), 0, st, 0, 0, r_hit_cap, max_steps_cap,
                        rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, nullptr, seed, stats, s_idx, s_depth,
                        s_dist, ray_ns, table, nch, SampleTail{}, nv_rank, col0_rank);
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
@@ -2190,7 +2191,7 @@ extern "C" int psvo_sample_rays_range(void *stream, int64_t row_begin, int64_t n
     PSVO_REQUIRE(offsets != nullptr && ray_ns != nullptr, "sample_rays: ray_ns / offsets required");
     if (r_hit_cap == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, 4)), dim3(256), 0, st, row_begin, n_rows, r_hit_cap,
+    psvo::launch(k_sample_fused, dim3(div_up(r_hit_cap, kSmpWaves)), dim3(64 * kSmpWaves), 0, st, row_begin, n_rows, r_hit_cap,
                        max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats,
                        s_idx, s_depth, s_dist, ray_ns, nullptr, 0, SampleTail{}, static_cast<const int *>(nullptr),
                        static_cast<const int *>(nullptr));
