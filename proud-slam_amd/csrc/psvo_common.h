@@ -145,7 +145,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
                         const int *nv_rank = nullptr, const int *col0_rank = nullptr);  // intersect_ranked's copies
 // whether a query of r rays runs its statistics / rank pass and its sample
 // scan by look-back (up to kLbMaxRays rays), and its descriptor granules
-constexpr int64_t kLbMaxRays = 16384;  // 4 rays per workgroup, <= 64 · 64 workgroups (lookback.h)
+constexpr int64_t kLbMaxRays = 16384;  // 8 rays per workgroup: 2,048 workgroups, within lookback.h's 64 · 64
 constexpr int kLbIsGranules = 5, kLbSmpGranules = 8;
 bool query_lookback(int64_t r);
 int64_t lookback_granules(int64_t r);

@@ -233,7 +233,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // counted in stats[PSVO_STAT_SPILLS]).
 constexpr int kStk = 512;    // candidate stack entries per ray
 constexpr int kBfsL = 128;   // leaf list capacity (≤ 49 + 64 between compactions)
-constexpr int kIsWaves = 4;  // waves (rays) per block
+constexpr int kIsWaves = 8;  // waves (rays) per block
 
 // Diagnostic build only (-DPSVO_IS_STAMPS, `make is_stamps`: lib/diag/): per
 // ray, k_intersect_sorted's cycles by segment (s_memtime; scalar reads of the
@@ -437,7 +437,7 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
 // 32-B record, siblings contiguous) instead of reference node ids into the
 // two AoS rows; the same floats, the same keys, the reference ids emitted.
 template <bool PACKED>
-__global__ __launch_bounds__(256) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
+__global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
                                                           const float *__restrict__ rays_d,
                                                           const float *__restrict__ centres,
                                                           const int *__restrict__ structure,
