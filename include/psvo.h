@@ -516,7 +516,10 @@ void psvo_engine_free(psvo_engine *e);
  * then ONE all-gather of 8 words after the sampler (S_max and, when the
  * step's GT depth was known at query time and the loss value is not wanted,
  * the loss normalisers' counts); step phase: the normaliser counts (8
- * doubles summed) only when the query could not count them, the loss sums
+ * doubles summed) only when some rank's query could not count them (one
+ * decision for all ranks, from the gathered words: every rank issues the same
+ * collectives; a query that counted used the GT depths it was given, which
+ * must be the step's), the loss sums
  * (8 doubles) only when the loss value is wanted; then the caller sums
  * grad_flat over ranks (PSVO_STEP_NO_ADAM) before psvo_map_adam.  A non-NULL fn turns
  * the protocol on for any world, 1 included (the collectives are then
@@ -554,6 +557,19 @@ int psvo_engine_set_paths(psvo_engine *e, int paths);   /* with no query queued 
  * summed; reset != 0 zeroes the sums.  An abandoned look-back wait of any
  * step is reported as an error. */
 int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *out, int reset);
+
+/* Tests only: the in-launch look-back scans of the sites in `mask` (1
+ * traversal, 2 sampler, 4 sample selection) get a spin bound of spin_bound
+ * re-reads instead of the bug-trap bound (0: every workgroup with a
+ * predecessor gives up at once; -1: the default), and with delay_us > 0 every
+ * 4th workgroup (from 1) and every 64th (the tiles' last) waits that long
+ * before it starts, so that its successors compute its aggregate themselves
+ * (the path a workgroup kept off the CUs by other work takes).  mask 0: the
+ * defaults.  Process-wide; takes effect at the next launch. */
+int psvo_debug_set_lookback(int mask, int spin_bound, int delay_us);
+/* Tests only: look-back blocks helped so far ([0] traversal, [1] sampler,
+ * [2] sample selection); reset != 0 zeroes them.  Synchronises the device. */
+int psvo_debug_lb_helps(int64_t *out3, int reset);
 
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,
@@ -761,6 +777,11 @@ int64_t psvo_octree_count_leaves(void *tree);
 int psvo_octree_export(void *tree, float *voxels, float *children, int *features);
 int psvo_octree_has_voxel(void *tree, int x, int y, int z);
 double psvo_octree_try_insert(void *tree, const int *vox, int64_t n);
+/* Octree::get_leaf_voxels (octree.cpp:480-505): the integer corner of every
+ * SURFACE leaf, in the reference's depth-first child-index (0..7) order, into
+ * out f32[cap, 3]; returns the number of leaves (-1 on error), writing at
+ * most cap of them. */
+int64_t psvo_octree_leaf_voxels(void *tree, float *out, int64_t cap);
 
 #ifdef __cplusplus
 }

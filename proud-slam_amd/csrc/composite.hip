@@ -464,8 +464,11 @@ struct SelectArgs {
     int split;
     int *counts;             // [0] M_A, [1] M_B, [2] flags (look-back abandoned: bit 3), [3] pad, then u64
                              // running sums of kept / composited samples and of launches
-    unsigned long long *desc;
+    unsigned long long *desc;  // select_granules(r_hit): the ticket counter, aggregates, tile totals
     uint32_t tag;
+    LbCtl ctl;                 // lookback.h (tests: psvo_debug_set_lookback)
+    int *host_flag;            // coherent pinned word: bit 3 set by a workgroup that gave up its wait —
+                               // the engine reports it at its next host read-back
 };
 
 // the ray's z_min (k_composite_loss's first sign change of the padded sdf row)
@@ -498,6 +501,9 @@ __device__ __forceinline__ SelFlags sel_flags(float zs, float zmin, float d, flo
     return o;
 }
 
+// look-back blocks this kernel helped (lookback.h; diagnostic: psvo_debug_lb_helps)
+__device__ unsigned long long psvo_g_sel_helps;
+
 __global__ __launch_bounds__(512) void k_select_samples(int64_t r_hit, int rpw, int s_max, float tr, float max_depth,
                                                         const int *__restrict__ offsets,
                                                         const int *__restrict__ ray_ns,
@@ -510,71 +516,113 @@ __global__ __launch_bounds__(512) void k_select_samples(int64_t r_hit, int rpw, 
     __shared__ float s_zmin[kSelWaves * kSelMaxRpw];
     __shared__ int s_nc[kSelWaves], s_base[2];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t r0 = ((int64_t)blockIdx.x * kSelWaves + w) * rpw;
+    const int blk = (int)blockIdx.x;
+    lb_debug_delay(a.ctl, blk);
+    if (threadIdx.x == 0) lb_mark_started<3>(a.desc, blk, (int)gridDim.x, a.tag);
+    const int64_t r0 = ((int64_t)blk * kSelWaves + w) * rpw;
     const uint64_t below = (1ull << lane) - 1ull;
     const bool split = a.split != 0;
-    // ---- count the classes per ray
-    int nc_w = 0;
-    for (int k = 0; k < rpw; ++k) {
-        const int64_t r = r0 + k;
-        int na = 0, nb = 0;
-        float zmin = 0.f;
-        if (r < r_hit) {
-            const int off = offsets[r], ns = ray_ns[r];
-            const float *z = z_vals + r * z_stride;
-            const float d = gt_depth[rank_ray[r]];
-            zmin = sel_zmin(lane, s_max, ns, off, z, sdf_s);
-            for (int s0 = 0; s0 < ns; s0 += 64) {
-                const int s = s0 + lane;
-                SelFlags f{false, false};
-                if (s < ns) f = sel_flags(z[s], zmin, d, tr, max_depth);
-                const int nk = __popcll(__ballot(f.keep)), nc = __popcll(__ballot(f.comp && s < ns));
-                na += split ? nc : nk;
-                nb += split ? nk - nc : 0;
-                nc_w += nc;
+    // ---- count the classes per ray of block `cur` (the own block, or one
+    // whose aggregate this workgroup computes for a successor: lookback.h)
+    auto count_classes = [&](int cur) {
+        const int64_t c0 = ((int64_t)cur * kSelWaves + w) * rpw;
+        int nc_w = 0;
+        for (int k = 0; k < rpw; ++k) {
+            const int64_t r = c0 + k;
+            int na = 0, nb = 0;
+            float zmin = 0.f;
+            if (r < r_hit) {
+                const int off = offsets[r], ns = ray_ns[r];
+                const float *z = z_vals + r * z_stride;
+                const float d = gt_depth[rank_ray[r]];
+                zmin = sel_zmin(lane, s_max, ns, off, z, sdf_s);
+                for (int s0 = 0; s0 < ns; s0 += 64) {
+                    const int s = s0 + lane;
+                    SelFlags f{false, false};
+                    if (s < ns) f = sel_flags(z[s], zmin, d, tr, max_depth);
+                    const int nk = __popcll(__ballot(f.keep)), nc = __popcll(__ballot(f.comp && s < ns));
+                    na += split ? nc : nk;
+                    nb += split ? nk - nc : 0;
+                    nc_w += nc;
+                }
+            }
+            if (lane == 0) {
+                s_na[w * rpw + k] = na;
+                s_nb[w * rpw + k] = nb;
+                s_zmin[w * rpw + k] = zmin;
             }
         }
-        if (lane == 0) {
-            s_na[w * rpw + k] = na;
-            s_nb[w * rpw + k] = nb;
-            s_zmin[w * rpw + k] = zmin;
-        }
-    }
-    if (lane == 0) s_nc[w] = nc_w;
-    __syncthreads();
-    if (w == 0) {
-        const int n_r = kSelWaves * rpw;
-        int va = 0, vb = 0;
-        for (int i = lane; i < n_r; i += 64) {
-            va += s_na[i];
-            vb += s_nb[i];
-        }
-        int c = lane < kSelWaves ? s_nc[lane] : 0;
+        if (lane == 0) s_nc[w] = nc_w;
+    };
+    __shared__ int s_cmd;
+    uint32_t own_agg[3] = {0u, 0u, 0u}, own_ex[3] = {0u, 0u, 0u};
+    int rc = kLbDone, spins = 0;
+    bool helped = false;
+    for (int cur = blk;;) {  // pass loop: the own block, then any block helped
+        count_classes(cur);
+        __syncthreads();
+        if (w == 0) {
+            const int n_r = kSelWaves * rpw;
+            int va = 0, vb = 0;
+            for (int i = lane; i < n_r; i += 64) {
+                va += s_na[i];
+                vb += s_nb[i];
+            }
+            int c = lane < kSelWaves ? s_nc[lane] : 0;
 #pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            va += __shfl_xor(va, sh, 64);
-            vb += __shfl_xor(vb, sh, 64);
-            c += __shfl_xor(c, sh, 64);
-        }
-        const uint32_t agg[3] = {(uint32_t)va, (uint32_t)vb, (uint32_t)c};
-        uint32_t ex[3];
-        const bool ok = lb_scan<3, 0u>(a.desc, (int)blockIdx.x, (int)gridDim.x, a.tag, lane, agg, ex);
-        if (lane == 0) {
-            s_base[0] = ok ? (int)ex[0] : -1;
-            s_base[1] = (int)ex[1];
-            if ((int)blockIdx.x == (int)gridDim.x - 1) {
-                const uint32_t ta = ex[0] + agg[0], tb = ex[1] + agg[1], tc = ex[2] + agg[2];
-                a.offa[r_hit] = (int)ta;
-                if (split) a.offb[r_hit] = (int)tb;
-                a.counts[0] = ok ? (int)ta : 0;  // an abandoned wait: empty compact batches
-                a.counts[1] = ok ? (int)tb : 0;
-                a.counts[3] = ok ? (int)tc : 0;  // composited (the statistics; split: = counts[0])
-                unsigned long long *sums = reinterpret_cast<unsigned long long *>(a.counts + 4);
-                sums[0] += ta + tb;  // one writer per launch, launches stream-ordered
-                sums[1] += tc;
-                sums[2] += 1;
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                va += __shfl_xor(va, sh, 64);
+                vb += __shfl_xor(vb, sh, 64);
+                c += __shfl_xor(c, sh, 64);
             }
-            if (!ok) atomicOr(a.counts + 2, kLbFlagTimeout);
+            const uint32_t agg[3] = {(uint32_t)va, (uint32_t)vb, (uint32_t)c};
+            if (cur == blk) {
+#pragma unroll
+                for (int g = 0; g < 3; ++g) own_agg[g] = agg[g];
+            } else {
+                lb_publish<3>(a.desc, cur, lane, agg, a.tag);
+                if (lane == 0) atomicAdd(&psvo_g_sel_helps, 1ull);
+            }
+            uint32_t ex[3];
+            rc = lb_scan_help<3, 0u>(a.desc, blk, (int)gridDim.x, a.tag, lane, own_agg, ex, spins, a.ctl.spin_max);
+            if (rc == kLbDone) {
+#pragma unroll
+                for (int g = 0; g < 3; ++g) own_ex[g] = ex[g];
+            }
+            if (lane == 0) s_cmd = rc;
+        }
+        __syncthreads();
+        const int cmd = __builtin_amdgcn_readfirstlane(s_cmd);  // uniform (scalar addressing in the next pass)
+        if (cmd < 0) break;
+        cur = cmd;
+        helped = true;
+    }
+    if (helped) {  // the LDS counts hold a helped block's: the own block's again
+        count_classes(blk);
+        __syncthreads();
+    }
+    if (w == 0 && lane == 0) {
+        const bool ok = rc == kLbDone;
+        const uint32_t(&ex)[3] = own_ex;
+        const uint32_t(&agg)[3] = own_agg;
+        s_base[0] = ok ? (int)ex[0] : -1;
+        s_base[1] = (int)ex[1];
+        if (blk == (int)gridDim.x - 1) {
+            const uint32_t ta = ex[0] + agg[0], tb = ex[1] + agg[1], tc = ex[2] + agg[2];
+            a.offa[r_hit] = ok ? (int)ta : 0;
+            if (split) a.offb[r_hit] = ok ? (int)tb : 0;
+            a.counts[0] = ok ? (int)ta : 0;  // an abandoned wait: empty compact batches
+            a.counts[1] = ok ? (int)tb : 0;
+            a.counts[3] = ok ? (int)tc : 0;  // composited (the statistics; split: = counts[0])
+            unsigned long long *sums = reinterpret_cast<unsigned long long *>(a.counts + 4);
+            sums[0] += ta + tb;  // one writer per launch, launches stream-ordered
+            sums[1] += tc;
+            sums[2] += 1;
+        }
+        if (!ok) {
+            atomicOr(a.counts + 2, kLbFlagTimeout);
+            if (a.host_flag)
+                __hip_atomic_fetch_or(a.host_flag, kLbFlagTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     __syncthreads();
@@ -588,7 +636,20 @@ __global__ __launch_bounds__(512) void k_select_samples(int64_t r_hit, int rpw, 
         }
     }
     __syncthreads();
-    if (s_base[0] < 0) return;  // the prefix is undefined: no stores
+    if (s_base[0] < 0) {  // the prefix is undefined: the rays' samples dropped, their compact
+        // ranges empty or in bounds (the step is reported failed at the next read-back)
+        for (int k = 0; k < rpw; ++k) {
+            const int64_t r = r0 + k;
+            if (r >= r_hit) break;
+            const int off = offsets[r], ns = ray_ns[r];
+            for (int s = lane; s < ns; s += 64) a.cidx[off + s] = -1;
+            if (lane == 0) {
+                a.offa[r] = 0;
+                if (split) a.offb[r] = 0;
+            }
+        }
+        return;
+    }
     // ---- write: compact index of every sample, the kept samples' rows
     for (int k = 0; k < rpw; ++k) {
         const int64_t r = r0 + k;
@@ -698,7 +759,7 @@ int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncat
                          const float *gt_depth, const float *sdf_s, const float *feat, const int *leaf, const float *t,
                          const int *ray_of, int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c,
                          int *leaf_c, float *t_c, int *ray_of_c, float *rgb_c, int *src_c, int *counts,
-                         unsigned long long *desc, uint32_t tag) {
+                         unsigned long long *desc, uint32_t tag, int *host_flag) {
     PSVO_REQUIRE(r_hit >= 0 && s_max > 0 && truncation > 0.f && z_stride >= s_max && tag != 0 && cap > 0,
                  "select_samples: bad sizes");
     PSVO_REQUIRE(!split || (offb != nullptr && rgb_c != nullptr),
@@ -708,10 +769,22 @@ int psvo::select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncat
                  (long long)r_hit, kSelWaves * kSelMaxRpw * kLbMaxBlocks);
     if (r_hit == 0) return PSVO_OK;
     SelectArgs a{reinterpret_cast<const float4 *>(feat), leaf, ray_of, t, cidx, offa, offb,
-                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, rgb_c, src_c, cap, split ? 1 : 0, counts, desc, tag};
+                 reinterpret_cast<float4 *>(feat_c), leaf_c, ray_of_c, t_c, rgb_c, src_c, cap, split ? 1 : 0, counts, desc, tag,
+                 lb_ctl(4), host_flag};
     psvo::launch(k_select_samples, dim3(div_up(r_hit, (int64_t)kSelWaves * rpw)), dim3(64 * kSelWaves), 0, st, r_hit,
                  rpw, s_max, truncation, max_depth, offsets, ray_ns, z_vals, z_stride, rank_ray, gt_depth, sdf_s, a);
     return check_launch("select_samples");
+}
+
+int psvo::lb_helps_select(int64_t *out1, bool reset) {
+    unsigned long long h = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&h, HIP_SYMBOL(psvo_g_sel_helps), sizeof(h)) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "debug_lb_helps: copy failed");
+    *out1 = (int64_t)h;
+    const unsigned long long z = 0;
+    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(psvo_g_sel_helps), &z, sizeof(z)) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "debug_lb_helps: reset failed");
+    return PSVO_OK;
 }
 
 int psvo::select_rays_per_wave(int64_t r_hit) {

@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void k_dist_counts(const int *__restrict__ sta
                                                      const int *__restrict__ ray_ns, float tr, float max_depth,
                                                      int *__restrict__ in) {
     __shared__ int red[7];
-    if (blockIdx.x == 0 && threadIdx.x == 0) in[0] = stats[PSVO_STAT_S_MAX];
+    if (blockIdx.x == 0 && threadIdx.x == 0) in[0] = stats[PSVO_STAT_S_MAX] | (gt_depth ? 0 : kDistNotCounted);
     if (!gt_depth) return;
     if (threadIdx.x < 7) red[threadIdx.x] = 0;
     __syncthreads();

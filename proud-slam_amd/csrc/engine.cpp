@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "psvo_common.h"
+#include "lookback.h"
 
 namespace psvo {
 namespace {
@@ -42,6 +43,7 @@ enum Slot {
 struct Arena {
     void *p[kSlots] = {};
     size_t cap[kSlots] = {};
+    uint32_t gen[kSlots] = {};  // allocations made for the slot (a new buffer may reuse a freed base address)
 };
 
 // One ray batch's query: its buffers, the pinned statistics it reads back
@@ -56,7 +58,7 @@ struct QuerySet {
     int seq = 0;                  // the flag value the current statistics carry
     hipStream_t qstream = nullptr;  // the stream the query was queued on
     const int *stats_zeroed = nullptr;  // the device statistics buffer a completed read-back left zeroed
-    const void *lb_zeroed = nullptr;    // the look-back descriptor buffer, zeroed once at allocation (tags ≠ 0)
+    uint32_t lb_zero_gen = 0;           // the look-back descriptor allocation (Arena::gen) last zeroed (tags ≠ 0)
     bool compacted = false;             // the sampler compacted the samples (slots kLeafQ / kTQ / kRayOfQ)
     hipEvent_t done = nullptr;    // statistics landed (after the sampler)
     bool done_recorded = false;   // a query consumed on its own stream skips it (one packet less there)
@@ -168,7 +170,8 @@ struct psvo_engine {
     int paths = 0;                  // PSVO_PATH_* (psvo_engine_set_paths)
     int64_t m_early = 0;            // the device-sized forward's capacity (render): 1.25 × the largest M seen
     uint32_t sel_tag = 0;           // the sample selection's look-back descriptor tag
-    const void *sel_zeroed = nullptr;  // its descriptor buffer, zeroed once at allocation
+    uint32_t sel_zero_gen = 0;      // its descriptor allocation (Arena::gen) last zeroed
+    int *host_flags = nullptr;      // coherent pinned: bit 3 = a sample selection gave up its look-back wait
     bool grads_clean = false;       // embedding-gradient buffer known to be zero (Adam zeroes it)
     const float *clean_buf = nullptr;  // ... and which buffer that is
 };
@@ -204,6 +207,7 @@ void *arena_buf(Arena &a, hipStream_t st, int slot, size_t bytes, int *rc) {
         return nullptr;
     }
     a.cap[slot] = cap;
+    a.gen[slot]++;
     return a.p[slot];
 }
 
@@ -529,7 +533,13 @@ extern "C" int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *o
     out[2] = (int64_t)u[0];
     out[3] = (int64_t)u[1];
     out[4] = (int64_t)u[2];
-    PSVO_REQUIRE(!(c[2] & 8), "engine_select_stats: a sample selection's look-back wait was abandoned");
+    if (c[2] & psvo::kLbFlagTimeout) {  // reported once: the bit and the host word cleared
+        if (hipMemsetAsync(static_cast<int *>(e->a.p[kSelCnt]) + 2, 0, sizeof(int), st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "engine_select_stats: memset failed");
+        if (e->host_flags) *(volatile int *)e->host_flags = 0;
+        e->sel_zero_gen = 0;
+        return set_error(PSVO_E_LAUNCH, "engine_select_stats: a sample selection's look-back wait was abandoned");
+    }
     if (reset && hipMemsetAsync(static_cast<int *>(e->a.p[kSelCnt]) + 4, 0, 6 * sizeof(int), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine_select_stats: memset failed");
     return PSVO_OK;
@@ -663,6 +673,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
     if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
+    if (e->host_flags) (void)hipHostFree(e->host_flags);
     delete e;
 }
 
@@ -830,10 +841,12 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         const size_t lb_bytes = (size_t)psvo::lookback_granules(R) * sizeof(unsigned long long);
         lb = reinterpret_cast<unsigned long long *>(arena_buf(q.a, st, kLbDesc, lb_bytes, &rc));
         if (!lb) return rc;
-        if (q.lb_zeroed != lb) {  // fresh memory: no stale granule may carry a future tag
+        // fresh memory (or after a reported failure): no stale granule may
+        // carry a future tag, and the ticket counters start at 0 (lookback.h)
+        if (q.lb_zero_gen != q.a.gen[kLbDesc]) {
             if (hipMemsetAsync(lb, 0, q.a.cap[kLbDesc], st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
-            q.lb_zeroed = lb;
+            q.lb_zero_gen = q.a.gen[kLbDesc];
         }
         e->lb_tag = e->lb_tag == 0xffffffffu ? 1u : e->lb_tag + 1u;
         tag = e->lb_tag;
@@ -857,7 +870,8 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                              (long long)R, (long long)x.max_rays_rank);
         ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off(), nv_rank));
         ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), x.cw, st, "query layout"));
-        ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, x.cw, x.nch, stats, x.xi32 + x.table_off()));
+        ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, x.cw, x.nch, stats, x.xi32 + x.table_off(),
+                             x.xi32 + x.q2_in_off()));
     }
     mark(e, st, PSVO_TIME_INTERSECT, 1);
     const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
@@ -1039,6 +1053,21 @@ int fork_join(hipStream_t from, hipStream_t st, hipEvent_t ev) {
     return PSVO_OK;
 }
 
+// A sample selection (k_select_samples) that gave up its look-back wait set
+// bit 3 of the pinned host word: its step's loss and gradients were formed
+// without the abandoned workgroups' samples.  Reported at the engine's next
+// host read-back (the following step's statistics, or select_stats) — the
+// step itself queues everything without a host round trip — and cleared
+// once reported; the descriptors are re-zeroed before the next selection.
+int select_failed(psvo_engine *e, const char *who) {
+    if (!e->host_flags) return PSVO_OK;
+    volatile int *f = e->host_flags;
+    if (!(*f & psvo::kLbFlagTimeout)) return PSVO_OK;
+    *f = 0;
+    e->sel_zero_gen = 0;
+    return set_error(PSVO_E_LAUNCH, "%s: the previous step's sample selection abandoned a look-back wait", who);
+}
+
 // render_rays (render_helpers.py:363-556) on the device, after the query:
 // sample compaction (sized by the query's read-back), interpolation, decoder,
 // compositing.  want_act: keep the decoder activations for weight gradients
@@ -1127,7 +1156,11 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     const int *hs = qset.host_stats;
     // data-parallel: this rank's hit rays, padded to the union's S_max
     const int r_hit = dist ? hs[PSVO_STAT_R_HIT_LOCAL] : hs[PSVO_STAT_R_HIT];
-    if (hs[PSVO_STAT_FLAGS] & 8) return set_error(PSVO_E_LAUNCH, "%s: query look-back wait abandoned", who);
+    if (hs[PSVO_STAT_FLAGS] & 8) {
+        qset.lb_zero_gen = 0;  // the next query re-zeroes the descriptors and ticket counters
+        return set_error(PSVO_E_LAUNCH, "%s: query look-back wait abandoned", who);
+    }
+    ENG_CALL(select_failed(e, who));
     if (hs[PSVO_STAT_FLAGS] & 1) return set_error(PSVO_E_OVERFLOW, "%s: octree deeper than the DFS stack", who);
     if (hs[PSVO_STAT_FLAGS] & 4) return set_error(PSVO_E_OVERFLOW, "%s: union batch exceeds max_rays_global", who);
     if (hs[PSVO_STAT_R_HIT] == 0)
@@ -1475,11 +1508,17 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_BUF(int, cnt, kSelCnt, psvo::kSelCountInts * sizeof(int));
         ENG_BUF(unsigned long long, desc, kSelDesc,
                 (size_t)psvo::select_granules(r_hit) * sizeof(unsigned long long));
-        if (e->sel_zeroed != desc) {  // fresh memory: no stale granule may carry a future tag
+        if (e->sel_zero_gen != e->a.gen[kSelDesc]) {  // fresh memory: no stale granule may carry a future tag
             if (hipMemsetAsync(desc, 0, e->a.cap[kSelDesc], st) != hipSuccess ||
                 hipMemsetAsync(cnt, 0, psvo::kSelCountInts * sizeof(int), st) != hipSuccess)
                 return set_error(PSVO_E_LAUNCH, "map_step: memset failed");
-            e->sel_zeroed = desc;
+            e->sel_zero_gen = e->a.gen[kSelDesc];
+        }
+        if (!e->host_flags) {
+            if (hipHostMalloc(reinterpret_cast<void **>(&e->host_flags), sizeof(int),
+                              hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "map_step: pinned allocation failed");
+            *e->host_flags = 0;
         }
         if (two_class) {
             ENG_BUF(int, ob, kOffB2, (size_t)(r_hit + 1) * sizeof(int));
@@ -1496,7 +1535,7 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
                                       q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, M,
                                       two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, rgb_c, src_c, cnt,
-                                      desc, e->sel_tag));
+                                      desc, e->sel_tag, e->host_flags));
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
@@ -1529,8 +1568,12 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     }
     // the sampler counted the normalisers for exactly this GT (its tail wrote the coefficients)
     const bool coef_q = !dist && counts_gt && qset->counts_gt == counts_gt;
-    // data parallel: the query gathered the union's counts for exactly this GT
-    const bool sums_q = dist && counts_gt && qset->counts_gt == counts_gt;
+    // data parallel: the query gathered the union's counts — decided from the
+    // gathered words (PSVO_FLAG_UNION_UNCOUNTED), the same on every rank, so
+    // that all ranks issue the same collectives (psvo_map_query's counts_gt
+    // must hold the step's GT depths: psvo.h)
+    const bool sums_q = dist && counts_gt && qset->counts_gt != nullptr &&
+                        !(qset->host_stats[PSVO_STAT_FLAGS] & psvo::PSVO_FLAG_UNION_UNCOUNTED);
     float *coef = coef_q ? static_cast<float *>(qset->a.p[kCoefQ]) : nullptr;
     if (!coef_q) {
         ENG_BUF(float, cbuf, kCoef, 4 * sizeof(float));

@@ -184,3 +184,31 @@ extern "C" double psvo_octree_try_insert(void *tree, const int *vox, int64_t n) 
     for (uint64_t k : tmp) hit += t->keys.count(k);
     return (double)hit / (double)tmp.size();
 }
+
+// octree.cpp:480-505 get_leaf_voxel_recursive: a node that is a SURFACE leaf
+// emits its corner, any other node recurses into children 0..7 in order
+// (FEATURE leaves have no children: nothing).  Iterative, explicit stack.
+extern "C" int64_t psvo_octree_leaf_voxels(void *tree, float *out, int64_t cap) {
+    const Tree *t = static_cast<Tree *>(tree);
+    if (!t || (cap > 0 && !out)) return -1;
+    int64_t n = 0;
+    std::vector<int> stack{0};
+    while (!stack.empty()) {
+        const int nd = stack.back();
+        stack.pop_back();
+        if (t->type[nd] == kSurface) {
+            if (n < cap) {
+                out[n * 3 + 0] = (float)squeeze3(t->code[nd]);
+                out[n * 3 + 1] = (float)squeeze3(t->code[nd] >> 1);
+                out[n * 3 + 2] = (float)squeeze3(t->code[nd] >> 2);
+            }
+            ++n;
+            continue;
+        }
+        for (int k = 7; k >= 0; --k) {  // pushed 7..0: child 0 is visited first
+            const int c = t->child[(size_t)nd * 8 + k];
+            if (c >= 0) stack.push_back(c);
+        }
+    }
+    return n;
+}

@@ -79,6 +79,15 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 // CUDA_CHECK_ERRORS calls exit(-1), cuda_utils.h:37-48): the binding raises.
 int check_launch(const char *what);
 
+// the look-back controls of site 1 (traversal), 2 (sampler) or 4 (sample
+// selection): lookback.h's kLbSpinMax and no delay unless
+// psvo_debug_set_lookback set them
+struct LbCtl;
+LbCtl lb_ctl(int site);
+// look-back blocks helped (lookback.h): traversal + sampler, selection
+int lb_helps_query(int64_t *out2, bool reset);
+int lb_helps_select(int64_t *out1, bool reset);
+
 // multi-tensor Adam launch (optim.hip): per-tensor lr, optional per-tensor
 // step numbers (steps: else `step` for all), optional gradient zeroing
 int adam_launch(hipStream_t st, int n_tensors, float *const *params, const float *const *grads, float *const *exp_avg,
@@ -147,6 +156,12 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
 // scan by look-back (up to kLbMaxRays rays), and its descriptor granules
 constexpr int64_t kLbMaxRays = 16384;  // 8 rays per workgroup: 2,048 workgroups, within lookback.h's 64 · 64
 constexpr int kLbIsGranules = 5, kLbSmpGranules = 8;
+// statistics words [kStatQuery, +3): the traversal's P / R_hit / max ⌈steps⌉
+// again, for the look-back sampler — never zeroed by a read-back, so a
+// sampler workgroup that starts after the launch's last one zeroed words
+// [0, kStatQuery) still reads this batch's values (lookback.h helping)
+constexpr int kStatQuery = 13;
+static_assert(kStatQuery + 3 <= PSVO_STAT_WORDS, "statistics words");
 bool query_lookback(int64_t r);
 int64_t lookback_granules(int64_t r);
 
@@ -197,11 +212,20 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
 // rows; after the second all-gather ([S_max, 7 count words] per rank) the
 // union S_max and normaliser sums
 constexpr int kDistWordsPerRank = 8;
+// word 0 of a rank's second-gather words: its S_max, with this bit set when
+// it did not count its rows (no GT depths given to its query)
+constexpr int kDistNotCounted = 1 << 30;
+// PSVO_STAT_FLAGS bit set by k_dist_smax when some rank did not count: every
+// rank then counts in its step (one decision for all ranks, so all issue the
+// same collectives)
+constexpr int PSVO_FLAG_UNION_UNCOUNTED = 16;
 int dist_slot0_rows(int64_t max_rays_global);
 int dist_count_words(int max_rays_rank);
 int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
               const int *ray_nv, int *out, const int *nv_rank = nullptr);
-int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table);
+// (q2_in: this rank's words of the second gather, whose count words it zeroes)
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table,
+                int *q2_in);
 int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
                 const float *hit_t0, const float *hit_t1, const float *ray_dsum, float step_size, uint64_t seed,
                 int *stats, const int *table, int nch, int *s_idx, float *s_depth, float *s_dist, int *ray_ns,
@@ -210,7 +234,7 @@ int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, do
 // this rank's words of the second gather: in[0] = S_max of its rows; given
 // the GT depths, in[1..7] += n_valid, Σ front / Σ sdf-band over the valid
 // samples, and per padding class (front, band: sample_terms of the MAX_DEPTH
-// fill) the rays and their Σ ns — in[1..7] zero on entry (criterion.hip)
+// fill) the rays and their Σ ns — in[1..7] zeroed by dist_layout (criterion.hip)
 int dist_counts(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const float *gt_depth,
                 const float *z_rows, int z_stride, const int *ray_ns, float truncation, float max_depth, int *in);
 
@@ -244,7 +268,8 @@ int composite_loss_z(void *stream, int64_t r_hit, int s_max, float truncation, f
 // [2 cap][3] are written 0 — their composite weights are 0; src_c [2 cap],
 // if not null: each kept sample's index in the step's sample order).  counts[0] = M_A, counts[1] = M_B (the
 // compact decoder launches read them on the device), counts[2] |= 8 if the
-// look-back wait was abandoned (then both are 0); counts + 4: u64 running
+// look-back wait was abandoned (then both are 0; with host_flag — coherent
+// pinned memory — bit 3 is also set there for the host); counts + 4: u64 running
 // sums of kept / composited samples and of launches (kSelCountInts ints,
 // zeroed once).  desc: select_granules(r_hit) granules, zeroed once; tag
 // fresh per launch (≠ 0).
@@ -253,7 +278,8 @@ int select_samples(hipStream_t st, int64_t r_hit, int s_max, float truncation, f
                    const int *ray_ns, const float *z_vals, int z_stride, const int *rank_ray, const float *gt_depth,
                    const float *sdf_s, const float *feat, const int *leaf, const float *t, const int *ray_of,
                    int64_t cap, bool split, int *cidx, int *offa, int *offb, float *feat_c, int *leaf_c, float *t_c,
-                   int *ray_of_c, float *rgb_c, int *src_c, int *counts, unsigned long long *desc, uint32_t tag);
+                   int *ray_of_c, float *rgb_c, int *src_c, int *counts, unsigned long long *desc, uint32_t tag,
+                   int *host_flag = nullptr);
 int select_rays_per_wave(int64_t r_hit);
 int64_t select_granules(int64_t r_hit);
 // sample compaction alone, one wave per hit ray (svo_query.hip k_compact_rays):

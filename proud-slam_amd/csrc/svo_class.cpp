@@ -107,12 +107,15 @@ struct SvoOctree : torch::CustomClassHolder {
         return {v, c, f, torch::zeros({n, max_num, 4}, torch::kFloat32), torch::zeros({n, max_num, 3}, torch::kFloat32)};
     }
 
-    // the SURFACE leaves' integer corners (octree.cpp get_leaf_voxels: leaves with vertex rows)
+    // the SURFACE leaves' integer corners in the reference's depth-first
+    // child-index order (octree.cpp:480-505)
     torch::Tensor get_leaf_voxels() {
-        auto [v, c, f] = arrays();
-        (void)c;
-        torch::Tensor keep = f.select(1, 0).ge(0);
-        return v.index({keep}).narrow(1, 0, 3).contiguous();
+        check();
+        const int64_t n = psvo_octree_leaf_voxels(h, nullptr, 0);
+        TORCH_CHECK(n >= 0, "Octree.get_leaf_voxels: ", psvo_last_error());
+        torch::Tensor v = torch::empty({n, 3}, torch::kFloat32);
+        TORCH_CHECK(psvo_octree_leaf_voxels(h, v.data_ptr<float>(), n) == n, "Octree.get_leaf_voxels failed");
+        return v;
     }
 
     using State = std::tuple<int64_t, int64_t, double, std::vector<torch::Tensor>, int64_t>;

@@ -436,29 +436,28 @@ __device__ int top_start(KeyLds &S, const PackRec *__restrict__ packed, const fl
 // (tree_pack.hip: centre + side and ref id / first child / child mask in one
 // 32-B record, siblings contiguous) instead of reference node ids into the
 // two AoS rows; the same floats, the same keys, the reference ids emitted.
+// look-back blocks helped (lookback.h: a predecessor that had not started):
+// [0] traversal, [1] sampler — diagnostic, read by psvo_debug_lb_helps
+__device__ unsigned long long psvo_g_lb_helps[2];
+
+// The per-ray work of k_intersect_sorted for the rays of block `cur` (one
+// wave per ray): hit rows, ray_nv / ray_dsum, and the wave's totals in L.
+// Inlined for the workgroup's own block; the look-back's help path calls
+// trace_pass_help (not inlined: the own pass keeps its registers).
+struct IsLds {
+    int vis[kIsWaves], ov[kIsWaves], sp[kIsWaves], rd[kIsWaves], nv[kIsWaves], mc[kIsWaves], c0[kIsWaves];
+};
 template <bool PACKED>
-__global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
-                                                          const float *__restrict__ rays_d,
-                                                          const float *__restrict__ centres,
-                                                          const int *__restrict__ structure,
-                                                          const PackRec *__restrict__ packed, float voxel_size,
-                                                          float max_distance, float step_size,
-                                                          int *__restrict__ hit_idx, float *__restrict__ hit_t0,
-                                                          float *__restrict__ hit_t1, int *__restrict__ ray_nv,
-                                                          float *__restrict__ ray_dsum, int *__restrict__ stats,
-                                                          int *__restrict__ blk_out, int *__restrict__ ray_rank,
-                                                          int *__restrict__ rank_ray, unsigned long long *lb_desc,
-                                                          uint32_t lb_tag, int *__restrict__ nv_rank,
-                                                          int *__restrict__ col0_rank) {
-    // lb_desc != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
-    // runs in this launch by decoupled look-back (lookback.h): each workgroup
-    // ranks its own hit rays, the last one writes P / R_hit / max ⌈Σ/step⌉
-    __shared__ KeyLds lds_all[kIsWaves];
-    KeyLds &S = lds_all[threadIdx.x / kWave];
+__device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float *__restrict__ rays_o,
+                                           const float *__restrict__ rays_d, const float *__restrict__ centres,
+                                           const int *__restrict__ structure, const PackRec *__restrict__ packed,
+                                           float half, float max_distance, float step_size, int *__restrict__ hit_idx,
+                                           float *__restrict__ hit_t0, float *__restrict__ hit_t1,
+                                           int *__restrict__ ray_nv, float *__restrict__ ray_dsum, KeyLds &S,
+                                           IsLds &L) {
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t r = (int64_t)blockIdx.x * kIsWaves + threadIdx.x / kWave;
-    const float half = voxel_size * 0.5f;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t r = (int64_t)cur * kIsWaves + threadIdx.x / kWave;
     int visits = 0, rounds = 0;
     int w_nv = 0, w_mc = 0, w_c0 = -1;  // this wave's ray: valid hits, ⌈Σ/step⌉ (lane 0), first hit's id
     bool overflow_stack = false, spill = false;
@@ -697,33 +696,92 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
     // visits / overflow: one atomic per block (per-ray P, R_hit and max ceil
     // are reduced by k_ray_stats: thousands of same-address atomics serialise
     // at the memory side)
-    __shared__ int blk_vis[kIsWaves], blk_ov[kIsWaves], blk_sp[kIsWaves], blk_rd[kIsWaves];
-    __shared__ int blk_nv[kIsWaves], blk_mc[kIsWaves], blk_c0[kIsWaves];
     const int wvis = wave_sum(visits);
     const int wov = wave_max(overflow_stack ? 1 : 0);
     if (lane == 0) {
-        blk_vis[threadIdx.x / kWave] = wvis;
-        blk_ov[threadIdx.x / kWave] = wov;
-        blk_sp[threadIdx.x / kWave] = spill ? 1 : 0;
-        blk_rd[threadIdx.x / kWave] = rounds;  // wave-uniform
-        blk_nv[threadIdx.x / kWave] = w_nv;
-        blk_mc[threadIdx.x / kWave] = w_mc;
-        blk_c0[threadIdx.x / kWave] = w_c0;
+        L.vis[threadIdx.x / kWave] = wvis;
+        L.ov[threadIdx.x / kWave] = wov;
+        L.sp[threadIdx.x / kWave] = spill ? 1 : 0;
+        L.rd[threadIdx.x / kWave] = rounds;  // wave-uniform
+        L.nv[threadIdx.x / kWave] = w_nv;
+        L.mc[threadIdx.x / kWave] = w_mc;
+        L.c0[threadIdx.x / kWave] = w_c0;
     }
+}
+
+template <bool PACKED>
+__device__ __forceinline__ void trace_pass_help(int cur, int64_t n_rays, const float *rays_o, const float *rays_d,
+                                             const float *centres, const int *structure, const PackRec *packed,
+                                             float half, float max_distance, float step_size, int *hit_idx,
+                                             float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, KeyLds &S,
+                                             IsLds &L) {
+    trace_pass<PACKED>(cur, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance, step_size,
+                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
+}
+
+// wave 0: a block's aggregate {hit rays, P, max ⌈Σ/step⌉, AABB tests, rounds}
+__device__ __forceinline__ void trace_agg(const IsLds &L, uint32_t (&agg)[5], uint64_t &hm) {
+    const int lane = threadIdx.x & (kWave - 1);
+    hm = __ballot(lane < kIsWaves && L.nv[lane] > 0);
+    agg[0] = (uint32_t)__popcll(hm);
+    agg[1] = agg[2] = agg[3] = agg[4] = 0u;
+#pragma unroll
+    for (int w = 0; w < kIsWaves; ++w) {
+        agg[1] = max(agg[1], (uint32_t)L.nv[w]);
+        agg[2] = max(agg[2], (uint32_t)L.mc[w]);
+        agg[3] += (uint32_t)L.vis[w];
+        agg[4] += (uint32_t)L.rd[w];
+    }
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
+                                                          const float *__restrict__ rays_d,
+                                                          const float *__restrict__ centres,
+                                                          const int *__restrict__ structure,
+                                                          const PackRec *__restrict__ packed, float voxel_size,
+                                                          float max_distance, float step_size,
+                                                          int *__restrict__ hit_idx, float *__restrict__ hit_t0,
+                                                          float *__restrict__ hit_t1, int *__restrict__ ray_nv,
+                                                          float *__restrict__ ray_dsum, int *__restrict__ stats,
+                                                          int *__restrict__ blk_out, int *__restrict__ ray_rank,
+                                                          int *__restrict__ rank_ray, unsigned long long *lb_desc,
+                                                          uint32_t lb_tag, int *__restrict__ nv_rank,
+                                                          int *__restrict__ col0_rank, LbCtl ctl) {
+    // lb_desc != nullptr: the statistics / hit-rank pass (k_ray_stats_rank)
+    // runs in this launch by decoupled look-back (lookback.h): each workgroup
+    // ranks its own hit rays, the last one writes P / R_hit / max ⌈Σ/step⌉.
+    // A workgroup whose look-back finds a predecessor that has not started
+    // traces that block's rays too (their aggregate: lookback.h) — the
+    // pass loop below; `own` is the first pass.
+    __shared__ KeyLds lds_all[kIsWaves];
+    KeyLds &S = lds_all[threadIdx.x / kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int blk = (int)blockIdx.x;
+    if (lb_desc) {
+        lb_debug_delay(ctl, blk);
+        if (threadIdx.x == 0) lb_mark_started<5>(lb_desc, blk, (int)gridDim.x, lb_tag);
+    }
+    const float half = voxel_size * 0.5f;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    __shared__ IsLds L;
+    __shared__ int s_cmd;
+    trace_pass<PACKED>(blk, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance, step_size, hit_idx,
+                       hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
     __syncthreads();
     if (threadIdx.x == 0) {
         int v = 0, ov = 0, sps = 0, rd = 0;
         for (int w = 0; w < kIsWaves; ++w) {
-            v += blk_vis[w];
-            ov |= blk_ov[w];
-            sps += blk_sp[w];
-            rd += blk_rd[w];
+            v += L.vis[w];
+            ov |= L.ov[w];
+            sps += L.sp[w];
+            rd += L.rd[w];
         }
         if (lb_desc) {
             // summed by the look-back below
         } else if (blk_out) {  // summed by k_ray_stats_rank: no same-address atomics (they serialise at the memory side)
-            blk_out[2 * blockIdx.x] = v;
-            blk_out[2 * blockIdx.x + 1] = rd;
+            blk_out[2 * blk] = v;
+            blk_out[2 * blk + 1] = rd;
         } else {
             atomicAdd(stats + PSVO_STAT_VISITS, v);
             atomicAdd(stats + PSVO_STAT_ROUNDS, rd);
@@ -731,22 +789,46 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
         if (sps) atomicAdd(stats + PSVO_STAT_SPILLS, sps);
         if (ov) atomicOr(stats + 7, 1);
     }
-    if (!lb_desc || threadIdx.x >= kWave) return;
-    // wave 0: the workgroup's aggregate {hit rays, P, max ⌈Σ/step⌉, AABB
-    // tests, rounds} → its exclusive prefix → the hit ranks of its rays
-    const int nv_l = lane < kIsWaves ? blk_nv[lane] : 0;
-    const uint64_t hm = __ballot(nv_l > 0);
-    uint32_t agg[5] = {(uint32_t)__popcll(hm), 0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int w = 0; w < kIsWaves; ++w) {
-        agg[1] = max(agg[1], (uint32_t)blk_nv[w]);
-        agg[2] = max(agg[2], (uint32_t)blk_mc[w]);
-        agg[3] += (uint32_t)blk_vis[w];
-        agg[4] += (uint32_t)blk_rd[w];
+    if (!lb_desc) return;
+    // wave 0: the workgroup's aggregate → its exclusive prefix (lookback.h);
+    // a predecessor that has not started: this workgroup traces that block's
+    // rays too and publishes its aggregate (a helped block's statistics
+    // arrive through it), then resumes its own look-back
+    uint32_t own_agg[5], own_ex[5] = {0u, 0u, 0u, 0u, 0u};
+    uint64_t own_hm = 0;
+    int own_nv = 0, own_c0 = -1, lb_rc = kLbDone, spins = 0;
+    if (threadIdx.x < kWave) {
+        trace_agg(L, own_agg, own_hm);
+        own_nv = lane < kIsWaves ? L.nv[lane] : 0;
+        own_c0 = lane < kIsWaves ? L.c0[lane] : -1;
+        lb_rc = lb_scan_help<5, 0b00110u>(lb_desc, blk, (int)gridDim.x, lb_tag, lane, own_agg, own_ex, spins,
+                                           ctl.spin_max);
+        if (lane == 0) s_cmd = lb_rc;
     }
-    uint32_t ex[5];
-    const bool ok = lb_scan<5, 0b00110u>(lb_desc, (int)blockIdx.x, (int)gridDim.x, lb_tag, lane, agg, ex);
-    const int64_t rr = (int64_t)blockIdx.x * kIsWaves + lane;
+    __syncthreads();
+    for (int cmd = __builtin_amdgcn_readfirstlane(s_cmd); cmd >= 0; cmd = __builtin_amdgcn_readfirstlane(s_cmd)) {
+        trace_pass_help<PACKED>(cmd, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance,
+                                step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
+        __syncthreads();
+        if (threadIdx.x < kWave) {
+            uint32_t agg[5];
+            uint64_t hm;
+            trace_agg(L, agg, hm);
+            lb_publish<5>(lb_desc, cmd, lane, agg, lb_tag);
+            if (lane == 0) atomicAdd(&psvo_g_lb_helps[0], 1ull);
+            lb_rc = lb_scan_help<5, 0b00110u>(lb_desc, blk, (int)gridDim.x, lb_tag, lane, own_agg, own_ex, spins,
+                                               ctl.spin_max);
+            if (lane == 0) s_cmd = lb_rc;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x >= kWave) return;
+    const bool ok = lb_rc == kLbDone;
+    const uint32_t(&ex)[5] = own_ex;    // the exclusive prefix
+    const uint32_t(&agg)[5] = own_agg;  // the own aggregate
+    const int nv_l = own_nv;
+    const uint64_t hm = own_hm;
+    const int64_t rr = (int64_t)blk * kIsWaves + lane;
     if (lane < kIsWaves && rr < n_rays) {  // an abandoned wait (!ok) leaves `ex` undefined: no rank stores
         const int rk = (int)ex[0] + __popcll(hm & below);
         ray_rank[rr] = (nv_l > 0 && ok) ? rk : -1;
@@ -754,14 +836,20 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
             rank_ray[rk] = (int)rr;
             if (nv_rank) {  // by rank: the sampler's reads of other rows, one load each
                 nv_rank[rk] = nv_l;
-                col0_rank[rk] = blk_c0[lane];
+                col0_rank[rk] = own_c0;
             }
         }
     }
-    if (lane == 0 && blockIdx.x == gridDim.x - 1) {  // the stats words were zeroed by the last read-back
-        stats[PSVO_STAT_P] = (int)max(ex[1], agg[1]);
-        stats[PSVO_STAT_R_HIT] = (int)(ex[0] + agg[0]);
-        stats[PSVO_STAT_MAX_CEIL] = (int)max(ex[2], agg[2]);
+    if (lane == 0 && blk == (int)gridDim.x - 1) {  // the stats words were zeroed by the last read-back
+        // an abandoned wait: no hit ray (the sampler then does nothing; the flag reports it)
+        const int p = ok ? (int)max(ex[1], agg[1]) : 0, rh = ok ? (int)(ex[0] + agg[0]) : 0;
+        const int mc = ok ? (int)max(ex[2], agg[2]) : 0;
+        stats[PSVO_STAT_P] = p;
+        stats[PSVO_STAT_R_HIT] = rh;
+        stats[PSVO_STAT_MAX_CEIL] = mc;
+        stats[kStatQuery + PSVO_STAT_P] = p;  // the sampler's copy (never re-zeroed inside its launch)
+        stats[kStatQuery + PSVO_STAT_R_HIT] = rh;
+        stats[kStatQuery + PSVO_STAT_MAX_CEIL] = mc;
         atomicAdd(stats + PSVO_STAT_VISITS, (int)(ex[3] + agg[3]));
         atomicAdd(stats + PSVO_STAT_ROUNDS, (int)(ex[4] + agg[4]));
     }
@@ -1366,6 +1454,7 @@ struct SampleTail {
     float *t;
     int *ray_of;
     int *m_out;  // or null: the batch's sample count M, on the device (the step's device-sized forward)
+    LbCtl ctl;   // lookback.h (tests: psvo_debug_set_lookback)
 };
 constexpr int kSmpStage = 256;  // a row's first samples staged in LDS for the in-launch compaction
 constexpr int kSmpWaves = 8;    // k_sample_fused: waves (rays) per workgroup
@@ -1375,9 +1464,17 @@ __device__ __forceinline__ int pack_counts(int nf, int nsm, bool pf, bool psm, b
     return nf | (nsm << 12) | ((int)pf << 24) | ((int)psm << 25) | ((int)valid << 26);
 }
 
-template <int NG>
-__device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__restrict__ stats, const SampleTail &tl,
-                                int *s_off, int st_word, int max_steps_cap);
+// the sampler's look-back state (wave 0): the own block's aggregate {M,
+// S_max, nf, nsm, Σ_pf ns, Σ_psm ns, pf | psm << 16, valid}, its lanes'
+// in-block offsets, its exclusive prefix and the wait's state
+struct SmpLb {  // in LDS: nothing of it stays in registers across the help passes
+    uint32_t agg[kLbSmpGranules], ex[kLbSmpGranules];
+    int before[kSmpWaves], rc, spins;
+};
+__device__ int smp_lb_pass(bool own, int cur, int blk, int nb, const int *s_ns, const int *s_cw, const SampleTail &tl,
+                           SmpLb &lb);
+__device__ void smp_lb_finish(int n, const SmpLb &lb, int *__restrict__ stats, const SampleTail &tl, int *s_off,
+                              int st_word, int max_steps_cap, int blk);
 
 // one ray of k_sample_fused; returns its valid-sample count, or -1 when the
 // wave has no ray (the launch covers r_hit_cap rows)
@@ -1391,7 +1488,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 const int *__restrict__ slot0, int slot0_nch,
                                                 const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
                                                 int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                int *stage_i, float *stage_z);
+                                                int *stage_i, float *stage_z, int blk);
 
 __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
@@ -1408,11 +1505,17 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
                                                       const int *__restrict__ col0_rank) {
     __shared__ WaveBins bins_all[kSmpWaves];
     // look-back mode (the engine's single-GPU query: row_begin 0, all rows):
-    // the rows of this batch, read before any workgroup can re-zero `stats`
-    // (the last one does, after every workgroup in front of it published)
-    const int n_lb = tl.desc && stats[PSVO_STAT_P] > 0 ? (int)min((int64_t)stats[PSVO_STAT_R_HIT], r_hit_cap) : 0;
+    // the rows of this batch from the traversal's copy of its statistics
+    // (kStatQuery: never re-zeroed inside this launch)
+    const int blk = (int)blockIdx.x;
+    const int *qp = stats + kStatQuery;
+    const int n_lb = tl.desc && qp[PSVO_STAT_P] > 0 ? (int)min((int64_t)qp[PSVO_STAT_R_HIT], r_hit_cap) : 0;
     const int last_lb = n_lb > 0 ? (n_lb - 1) / kSmpWaves : 0;  // the workgroup holding the last row
-    if (tl.desc && (int)blockIdx.x > last_lb) return;
+    if (tl.desc && blk > last_lb) return;
+    if (tl.desc) {
+        lb_debug_delay(tl.ctl, blk);
+        if (threadIdx.x == 0) lb_mark_started<kLbSmpGranules>(tl.desc, blk, last_lb + 1, tl.tag);
+    }
     __shared__ int stage_i[kSmpWaves][kSmpStage];
     __shared__ float stage_z[kSmpWaves][kSmpStage];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -1423,10 +1526,10 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     // no dependent round trip after the look-back in the last workgroup
     const int st_word = tl.desc && w == 0 && lane < PSVO_STAT_WORDS ? stats[lane] : 0;
     int il = 0, cnt_word = 0;
-    const int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
-                                       ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
-                                       slot0_nch, nv_rank, col0_rank, il, bins_all[w], tl, cnt_word,
-                                       compact ? stage_i[w] : nullptr, compact ? stage_z[w] : nullptr);
+    int count = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1,
+                                 ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0, slot0_nch,
+                                 nv_rank, col0_rank, il, bins_all[w], tl, cnt_word,
+                                 compact ? stage_i[w] : nullptr, compact ? stage_z[w] : nullptr, blk);
     SMP_T(1);
     if (!tl.desc) {  // k_scan_samples reads them after the launch
         if (count >= 0 && lane == 0) {
@@ -1435,7 +1538,7 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
         }
         return;
     }
-    __shared__ int s_ns[kSmpWaves], s_cw[kSmpWaves], s_off[kSmpWaves];
+    __shared__ int s_ns[kSmpWaves], s_cw[kSmpWaves], s_off[kSmpWaves], s_cmd;
     if (lane == 0) {
         if (count >= 0) ray_ns[il] = count;
         s_ns[w] = count;  // -1: no row
@@ -1446,29 +1549,54 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     // drain in front of the look-back cost up to 7 µs at the launch's tail)
     __syncthreads();
     SMP_T(2);
+    __shared__ SmpLb lb;  // wave 0: the own block's aggregate / prefix
     if (w == 0) {
-        if (tl.c.gt_depth)
-            scan_samples_lb<8>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
-        else
-            scan_samples_lb<2>(n_lb, s_ns, s_cw, stats, tl, s_off, st_word, max_steps_cap);
+        const int rc = smp_lb_pass(true, blk, blk, last_lb + 1, s_ns, s_cw, tl, lb);
+        if (lane == 0) s_cmd = rc;
     }
+    __syncthreads();
+    // a predecessor that has not started: this workgroup samples that
+    // block's rows too and publishes their aggregate (lookback.h)
+    bool helped = false;
+    for (int cmd = __builtin_amdgcn_readfirstlane(s_cmd); cmd >= 0; cmd = __builtin_amdgcn_readfirstlane(s_cmd)) {
+        helped = true;
+        int hil = 0, hcw = 0;
+        const int hc = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0,
+                                        hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
+                                        slot0_nch, nv_rank, col0_rank, hil, bins_all[w], tl, hcw, nullptr, nullptr,
+                                        cmd);
+        if (lane == 0) {
+            if (hc >= 0) ray_ns[hil] = hc;
+            s_ns[w] = hc;
+            s_cw[w] = hcw;
+        }
+        __syncthreads();
+        if (w == 0) {
+            const int rc = smp_lb_pass(false, cmd, blk, last_lb + 1, s_ns, s_cw, tl, lb);
+            if (lane == 0) s_cmd = rc;
+        }
+        __syncthreads();
+    }
+    const int own_count = count, own_il = il;
+    if (w == 0) smp_lb_finish(n_lb, lb, stats, tl, s_off, st_word, max_steps_cap, blk);
     SMP_T(3);
     if (!compact) return;
-    // a row longer than the LDS stage is re-read below: this wave's own stores first
-    if (count > kSmpStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // a row longer than the LDS stage (or any row, after helping: the stage
+    // then holds the helped rows) is re-read below: this wave's own stores first
+    if (own_count > kSmpStage || helped) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // k_compact_rays' work: the row's valid prefix to its compacted place —
     // the first kSmpStage samples from LDS, the rest (rows longer than that)
     // read back from the row with sc1 loads (this wave's own stores, past L1)
     const int off = s_off[w];
-    if (count <= 0 || off < 0) return;
-    const int *oi = s_idx + (int64_t)il * max_steps_cap;
-    const float *od = s_depth + (int64_t)il * max_steps_cap;
-    for (int s = lane; s < count; s += kWave) {
-        const bool st = s < kSmpStage;
+    if (own_count <= 0 || off < 0) return;
+    const int *oi = s_idx + (int64_t)own_il * max_steps_cap;
+    const float *od = s_depth + (int64_t)own_il * max_steps_cap;
+    for (int s = lane; s < own_count; s += kWave) {
+        const bool st = s < kSmpStage && !helped;
         tl.leaf[off + s] = st ? stage_i[w][s] : ld_wt(oi + s);
         tl.t[off + s] = st ? stage_z[w][s] : ld_wt(od + s);
-        tl.ray_of[off + s] = il;
+        tl.ray_of[off + s] = own_il;
     }
     SMP_T(4);
 }
@@ -1483,25 +1611,30 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 const int *__restrict__ slot0, int slot0_nch,
                                                 const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
                                                 int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                int *stage_i, float *stage_z) {
-    const int P = stats[PSVO_STAT_P];
-    const int r_hit = stats[PSVO_STAT_R_HIT];
-    const int max_steps = stats[PSVO_STAT_MAX_CEIL] + P;
+                                                int *stage_i, float *stage_z, int blk) {
+    // look-back mode: P / R_hit / max ⌈steps⌉ from the traversal's copy, which
+    // no workgroup of this launch re-zeroes (a workgroup may start after the
+    // last one zeroed the statistics: lookback.h helping)
+    const int *qp = tl.desc ? stats + kStatQuery : stats;
+    const int P = qp[PSVO_STAT_P];
+    const int r_hit = qp[PSVO_STAT_R_HIT];
+    const int max_steps = qp[PSVO_STAT_MAX_CEIL] + P;
     // the engine's launches (row_begin 0, or a data-parallel rank's own rows
     // indexed locally): the ray's rank → ray read beside the statistics words
-    const int il_s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int il_s = blk * (blockDim.x / kWave) + threadIdx.x / kWave;
     const int orig_s = (nv_rank && il_s < r_hit_cap) ? rank_ray[il_s] : 0;
     if (slot0) {  // data-parallel engine: the rank's rows, local rank_ray / hit arrays
         row_begin = stats[PSVO_STAT_ROW_BEGIN];
         n_rows = stats[PSVO_STAT_R_HIT_LOCAL];
     }
     const int lane = threadIdx.x & (kWave - 1);
-    const int il = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    const int il = blk * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
     const int i = (int)row_begin + il;                                        // logical row
     il_out = il;
     const int64_t n_own = n_rows < 0 ? (int64_t)r_hit - row_begin : n_rows;
     if (i >= r_hit || il >= n_own || il >= r_hit_cap || P <= 0) return -1;
-    if (max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + PSVO_STAT_FLAGS, 2);
+    // (look-back mode: the last workgroup derives this flag; no atomics on `stats`)
+    if (!tl.desc && max_steps > max_steps_cap && lane == 0 && il == 0) atomicOr(stats + PSVO_STAT_FLAGS, 2);
     const int kp = (r_hit + kSamplerG - 1) / kSamplerG;
     const int b = i / kp;
     const int j = i - b * kp;
@@ -1509,6 +1642,9 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     const int jj = j - c * kSamplerChunk;
     const int nr = min(kSamplerChunk, kp - c * kSamplerChunk);
     const int orig = nv_rank ? orig_s : slot0 ? rank_ray[il] : rank_ray[i];
+    // look-back mode (r_hit_cap = the batch's rays): a rank outside it only
+    // after an abandoned look-back wait (flagged) — no row
+    if (tl.desc && (orig < 0 || orig >= r_hit_cap)) return -1;
     const float dsum = ray_dsum[orig];
     FusedRows rows{rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, P, r_hit, i, b * kp + c * kSamplerChunk, jj,
                    (int64_t)orig * kMaxHits, dsum};
@@ -1588,29 +1724,32 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     return wave_sum(count);
 }
 
-// k_scan_samples' work for one sampler workgroup (its 4 rows), wave 0 only:
-// the workgroup's aggregate {M, S_max, and with the normalisers nf, nsm,
-// Σ_pf ns, Σ_psm ns, pf | psm << 16, valid} → its exclusive prefix by look-
-// back → its rows' offsets; the workgroup holding row n − 1 (block 0 when
-// there is no row) writes offsets[n], the loss coefficients and the
-// statistics read-back (granules, no system-scope release), and zeroes the
-// device statistics for the next query.  Integer sums: exact, the same
-// totals as k_scan_samples.
-template <int NG>
-__device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__restrict__ stats, const SampleTail &tl,
-                                int *s_off, int st_word, int max_steps_cap) {
+// k_scan_samples' work for one sampler workgroup (its 8 rows), wave 0 only,
+// in two parts.  smp_lb_pass: the aggregate of block `cur`'s rows {M, S_max,
+// and with the normalisers nf, nsm, Σ_pf ns, Σ_psm ns, pf | psm << 16,
+// valid} — the own block's kept in `lb`, a helped block's published — then
+// the own block's look-back (lookback.h lb_scan_help: returns the next block
+// to help, or done / failed).  smp_lb_finish: its rows' offsets; the
+// workgroup holding row n − 1 (block 0 when there is no row) writes
+// offsets[n], the loss coefficients and the statistics read-back (granules,
+// no system-scope release), and zeroes the device statistics for the next
+// query.  Integer sums: exact, the same totals as k_scan_samples.
+__device__ int smp_lb_pass(bool own, int cur, int blk, int nb, const int *s_ns, const int *s_cw, const SampleTail &tl,
+                           SmpLb &lb) {
+    constexpr int NG = kLbSmpGranules;
     const int lane = threadIdx.x & (kWave - 1);
     uint32_t agg[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) agg[g] = 0;
     int before = 0;  // samples of this workgroup's rows in front of lane's row
+    const bool counting = tl.c.gt_depth != nullptr;
 #pragma unroll
     for (int k = 0; k < kSmpWaves; ++k) {
         const int c = max(s_ns[k], 0);
         before += k < lane ? c : 0;
         agg[0] += (uint32_t)c;
         agg[1] = max(agg[1], (uint32_t)c);
-        if constexpr (NG == 8) {
+        if (counting) {
             const int cw = s_ns[k] >= 0 ? s_cw[k] : 0;
             const int pf = (cw >> 24) & 1, psm = (cw >> 25) & 1;
             agg[2] += (uint32_t)(cw & 0xFFF);
@@ -1621,39 +1760,74 @@ __device__ void scan_samples_lb(int n, const int *s_ns, const int *s_cw, int *__
             agg[7] += (uint32_t)((cw >> 26) & 1);
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's flag atomics land before its descriptors
+    int spins = 0;
+    if (own) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (lane == g) lb.agg[g] = agg[g];
+        if (lane < kSmpWaves) lb.before[lane] = before;
+    } else {
+        lb_publish<NG>(tl.desc, cur, lane, agg, tl.tag);
+        if (lane == 0) atomicAdd(&psvo_g_lb_helps[1], 1ull);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) agg[g] = lb.agg[g];  // the own aggregate again
+        spins = lb.spins;
+    }
     uint32_t ex[NG];
+    const int rc = lb_scan_help<NG, 0b10u>(tl.desc, blk, nb, tl.tag, lane, agg, ex, spins, tl.ctl.spin_max);
+    if (lane == 0) {
+        lb.rc = rc;
+        lb.spins = spins;
+    }
+    if (rc == kLbDone) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (lane == g) lb.ex[g] = ex[g];
+    }
+    return rc;
+}
+
+__device__ void smp_lb_finish(int n, const SmpLb &lb, int *__restrict__ stats, const SampleTail &tl, int *s_off,
+                              int st_word, int max_steps_cap, int blk) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool ok = lb.rc == kLbDone;
+    uint32_t ex[kLbSmpGranules], agg[kLbSmpGranules];
+#pragma unroll
+    for (int g = 0; g < kLbSmpGranules; ++g) {
+        ex[g] = lb.ex[g];
+        agg[g] = lb.agg[g];
+    }
     const int last = n > 0 ? (n - 1) / kSmpWaves : 0;  // the workgroups past it returned without a descriptor
-    const bool ok = lb_scan<NG, 0b10u>(tl.desc, (int)blockIdx.x, last + 1, tl.tag, lane, agg, ex);
-    const int il = (int)blockIdx.x * kSmpWaves + lane;
-    // an abandoned wait (!ok: `ex` undefined) stores no offset, and the compaction skips its rows
+    const int il = blk * kSmpWaves + lane;
+    const int before = lane < kSmpWaves ? lb.before[lane] : 0;
+    // an abandoned wait (!ok: `ex` undefined) stores offset 0 (an in-bounds
+    // range for any reader; the batch is reported failed) and the compaction
+    // skips its rows
     if (lane < kSmpWaves) s_off[lane] = ok ? (int)ex[0] + before : -1;  // the in-launch compaction's
-    if (lane < kSmpWaves && il < n && ok) tl.offsets[il] = (int)ex[0] + before;
-    if ((int)blockIdx.x != last) return;
-    const int tot = (int)(ex[0] + agg[0]);
-    const int smax = (int)max(ex[1], agg[1]);
+    if (lane < kSmpWaves && il < n) tl.offsets[il] = ok ? (int)ex[0] + before : 0;
+    if (blk != last) return;
+    const int tot = ok ? (int)(ex[0] + agg[0]) : 0;
+    const int smax = ok ? (int)max(ex[1], agg[1]) : 0;
     if (lane == 0) {
         tl.offsets[n] = tot;
-        if (tl.m_out) *tl.m_out = ok ? tot : 0;  // an abandoned wait: no samples (the flag reports it)
+        if (tl.m_out) *tl.m_out = tot;  // an abandoned wait: no samples (the flag reports it)
     }
-    if constexpr (NG == 8) {
-        if (lane == 0) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
-            const uint32_t pp = ex[6] + agg[6];
-            const long long t_nf = ex[2] + agg[2], t_nsm = ex[3] + agg[3], t_nspf = ex[4] + agg[4],
-                            t_nspsm = ex[5] + agg[5], t_pf = pp & 0xFFFF, t_psm = pp >> 16, t_valid = ex[7] + agg[7];
-            const long long n_f = t_nf + (long long)smax * t_pf - t_nspf;
-            const long long n_s = t_nsm + (long long)smax * t_psm - t_nspsm;
-            crit_coef_from_counts((double)t_valid, (double)n_f, (double)n_s, (double)n, (double)smax, tl.c.w_rgb,
-                                  tl.c.w_depth, tl.c.w_fs, tl.c.w_sdf, tl.c.tr, tl.c.crit_flags, tl.c.coef);
-        }
+    if (tl.c.gt_depth && lane == 0) {  // the count sums over the padded [R_hit, S_max] layout (criterion.py:70-101)
+        const uint32_t pp = ex[6] + agg[6];
+        const long long t_nf = ex[2] + agg[2], t_nsm = ex[3] + agg[3], t_nspf = ex[4] + agg[4],
+                        t_nspsm = ex[5] + agg[5], t_pf = pp & 0xFFFF, t_psm = pp >> 16, t_valid = ex[7] + agg[7];
+        const long long n_f = t_nf + (long long)smax * t_pf - t_nspf;
+        const long long n_s = t_nsm + (long long)smax * t_psm - t_nspsm;
+        crit_coef_from_counts((double)t_valid, (double)n_f, (double)n_s, (double)n, (double)smax, tl.c.w_rgb,
+                              tl.c.w_depth, tl.c.w_fs, tl.c.w_sdf, tl.c.tr, tl.c.crit_flags, tl.c.coef);
     }
     // the sampler's own flag (sample_fused_ray: max_steps beyond the rows' capacity)
-    const int max_steps = __shfl(st_word, PSVO_STAT_MAX_CEIL, kWave) + __shfl(st_word, PSVO_STAT_P, kWave);
+    const int max_steps = stats[kStatQuery + PSVO_STAT_MAX_CEIL] + stats[kStatQuery + PSVO_STAT_P];
     if (lane < PSVO_STAT_WORDS) {
         int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : st_word;
         if (lane == PSVO_STAT_FLAGS && n > 0 && max_steps > max_steps_cap) v |= 2;
         if (lane == PSVO_STAT_FLAGS && !ok) v |= kLbFlagTimeout;
-        stats[lane] = 0;  // ready for the query set's next use (no memset launch)
+        if (lane < kStatQuery) stats[lane] = 0;  // ready for the query set's next use (no memset launch)
         if (tl.host) stat_to_host(tl.host, lane, v, tl.seq);
     }
 }
@@ -1918,9 +2092,13 @@ __global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats
 // (world x stride): table[b · nch + c] = hit count of logical row b·K' + c·800
 // (row 0 past the union's end)
 __global__ __launch_bounds__(256) void k_dist_layout(const int *__restrict__ all, int world, int rank, int stride,
-                                                     int nch, int *__restrict__ stats, int *__restrict__ table) {
+                                                     int nch, int *__restrict__ stats, int *__restrict__ table,
+                                                     int *__restrict__ q2_in) {
     int r_hit = 0;
     for (int r = 0; r < world; ++r) r_hit += all[r * stride];
+    // this query's count words start at zero (k_dist_counts adds into them),
+    // whatever an earlier query that failed before k_dist_smax left there
+    if (q2_in && threadIdx.x >= 1 && threadIdx.x < kDistWords) q2_in[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         int p = 0, mc = 0, begin = 0, flags = 0;
         for (int r = 0; r < world; ++r) {
@@ -1969,10 +2147,18 @@ __global__ void k_dist_smax(const int *__restrict__ all, int world, int *__restr
                             double *__restrict__ sums) {
     if (threadIdx.x != 0) return;
     int mx = 0;
-    for (int r = 0; r < world; ++r) mx = max(mx, all[r * kDistWords]);
+    bool counted = true;  // every rank counted its rows against GT depths (k_dist_counts)
+    for (int r = 0; r < world; ++r) {
+        const int w0 = all[r * kDistWords];
+        mx = max(mx, w0 & ~kDistNotCounted);
+        counted = counted && !(w0 & kDistNotCounted);
+    }
     stats[PSVO_STAT_S_MAX_LOCAL] = stats[PSVO_STAT_S_MAX];
     stats[PSVO_STAT_S_MAX] = mx;
-    if (sums) {
+    // the same on every rank: whether the step may take the union's count
+    // sums from here or must count (and all-reduce) them itself
+    if (!counted) stats[PSVO_STAT_FLAGS] |= PSVO_FLAG_UNION_UNCOUNTED;
+    if (sums && counted) {
         long long c[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int r = 0; r < world; ++r)
             for (int k = 0; k < 7; ++k) c[k] += all[r * kDistWords + 1 + k];
@@ -2032,7 +2218,7 @@ extern "C" int psvo_ray_intersect_sorted(void *stream, int64_t n_rays, const flo
     psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
                        hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr, nullptr, nullptr, 0u,
-                       nullptr, nullptr);
+                       nullptr, nullptr, LbCtl{});
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted");
 }
@@ -2050,7 +2236,7 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
                        max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
-                       nullptr, nullptr, 0u, nullptr, nullptr);
+                       nullptr, nullptr, 0u, nullptr, nullptr, LbCtl{});
     psvo::launch(k_ray_stats, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats);
     return check_launch("ray_intersect_sorted_packed");
 }
@@ -2086,6 +2272,7 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
         tl.offsets = offsets;
         tl.desc = lb_desc + lb_granules<kLbIsGranules>(div_up(r_hit_cap, kIsWaves));
         tl.tag = lb_tag;
+        tl.ctl = lb_ctl(2);
         if (leaf && t && ray_of) {
             tl.leaf = leaf;
             tl.t = t;
@@ -2126,12 +2313,12 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
         psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
-                           lb_tag, nv_rank, col0_rank);
+                           lb_tag, nv_rank, col0_rank, lb_ctl(1));
     else
         psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
                            hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
-                           lb_tag, nv_rank, col0_rank);
+                           lb_tag, nv_rank, col0_rank, lb_ctl(1));
     if (!lb_desc)
         psvo::launch(k_ray_stats_rank, dim3(1), dim3(1024), 0, st, n_rays, ray_nv, ray_dsum, step_size, stats,
                            ray_rank, rank_ray, blk_out, (int)div_up(n_rays, kIsWaves));
@@ -2151,8 +2338,9 @@ int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, 
                  hit_idx, ray_nv, out, nv_rank);
     return check_launch("dist_pack");
 }
-int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table) {
-    psvo::launch(k_dist_layout, dim3(1), dim3(256), 0, st, all, world, rank, stride, nch, stats, table);
+int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table,
+                int *q2_in) {
+    psvo::launch(k_dist_layout, dim3(1), dim3(256), 0, st, all, world, rank, stride, nch, stats, table, q2_in);
     return check_launch("dist_layout");
 }
 // the fused sampler + scan over this rank's rows (stats from dist_layout)
@@ -2167,6 +2355,18 @@ int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int 
     psvo::launch(k_scan_samples, dim3(1), dim3(1024), 0, st, 0, 0, r_hit_cap, ray_ns, offsets, stats, 1,
                        nullptr, 0, SampleCounts{});
     return check_launch("dist_sample");
+}
+// the traversal's and sampler's helped-block counters (psvo_debug_lb_helps)
+int lb_helps_query(int64_t *out2, bool reset) {
+    unsigned long long h[2] = {0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(psvo_g_lb_helps), sizeof(h)) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "debug_lb_helps: copy failed");
+    out2[0] = (int64_t)h[0];
+    out2[1] = (int64_t)h[1];
+    const unsigned long long z[2] = {0, 0};
+    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(psvo_g_lb_helps), z, sizeof(z)) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "debug_lb_helps: reset failed");
+    return PSVO_OK;
 }
 int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, double *sums) {
     psvo::launch(k_dist_smax, dim3(1), dim3(64), 0, st, all, world, stats, in, sums);

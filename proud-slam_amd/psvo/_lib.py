@@ -77,6 +77,8 @@ _SIGNATURES = {
     "psvo_engine_set_timing": (_i32, [_vp, _i32]),
     "psvo_engine_set_paths": (_i32, [_vp, _i32]),
     "psvo_engine_select_stats": (_i32, [_vp, _vp, _vp, _i32]),
+    "psvo_debug_set_lookback": (_i32, [_i32, _i32, _i32]),
+    "psvo_debug_lb_helps": (_i32, [_vp, _i32]),
     "psvo_engine_queued": (_i32, [_vp]),
     "psvo_map_discard": (_i32, [_vp]),
     "psvo_engine_exchange_words": (_i64, [_i32, _i64, _i64]),
@@ -140,6 +142,7 @@ _SIGNATURES = {
     "psvo_octree_export": (_i32, [_vp, _vp, _vp, _vp]),
     "psvo_octree_has_voxel": (_i32, [_vp, _i32, _i32, _i32]),
     "psvo_octree_try_insert": (_f64, [_vp, _vp, _i64]),
+    "psvo_octree_leaf_voxels": (_i64, [_vp, _vp, _i64]),
 }
 
 _lib = None

@@ -98,8 +98,15 @@ class Octree:
                 _zeros_view(n, self.max_num, 3))
 
     def get_leaf_voxels(self):
-        v, _, f = self.export_arrays()
-        return torch.from_numpy(v[f[:, 0] >= 0, :3].copy())
+        """SURFACE leaves' integer corners in the reference's depth-first
+        child-index order (octree.cpp:480-505)."""
+        n = L.lib().psvo_octree_leaf_voxels(self._h, None, 0)
+        if n < 0:
+            raise L.PsvoError("octree_leaf_voxels failed")
+        out = torch.empty((n, 3), dtype=torch.float32)
+        if n:
+            L.lib().psvo_octree_leaf_voxels(self._h, out.data_ptr(), n)
+        return out
 
     def close(self):
         if self._h:

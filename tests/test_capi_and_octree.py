@@ -136,3 +136,33 @@ def test_torchscript_octree_class_matches_python_octree():
     assert torch.equal(t3.get_centres_and_children()[0], got[0])
     with pytest.raises(RuntimeError, match="not initialized"):
         torch.classes.svo.Octree().count_nodes()
+
+
+def test_leaf_voxels_in_reference_dfs_order():
+    """Octree::get_leaf_voxels (octree.cpp:480-505) walks the tree depth
+    first in child-index order (cid = x-bit + 2·y-bit + 4·z-bit, octree.cpp
+    :419-439) and emits only SURFACE leaves — not in creation order, and not
+    the FEATURE corner leaves every insert adds.  Hand-built tree inserted
+    in the reverse of that order (16³: every corner inside the grid)."""
+    t = Octree()
+    t.init(16, 16, 0.2, 8)
+    t.insert(np.array([[7, 7, 7], [4, 0, 0], [0, 0, 0], [0, 4, 0]], dtype=np.int32))
+    got = t.get_leaf_voxels()
+    want = torch.tensor([[0, 0, 0], [4, 0, 0], [0, 4, 0], [7, 7, 7]], dtype=torch.float32)
+    assert torch.equal(got, want)
+    # the same order as a DFS over the exported child table, on a bigger tree
+    from psvo import synthetic as syn
+    vox = syn.surface_voxels(syn.room0(), seed=1)
+    big = Octree()
+    big.init(256, 16, 0.2, 8)
+    big.insert(vox)
+    v, c, f = big.export_arrays()
+    order, stack = [], [0]
+    while stack:
+        nd = stack.pop()
+        if f[nd, 0] >= 0:  # SURFACE rows carry their corner rows (features)
+            order.append(v[nd, :3])
+            continue
+        stack.extend(int(k) for k in c[nd][::-1] if k >= 0)
+    assert torch.equal(big.get_leaf_voxels(), torch.from_numpy(np.stack(order).astype(np.float32)))
+    assert big.get_leaf_voxels().shape[0] == big.count_leaf_nodes()
