@@ -76,6 +76,11 @@ def parse():
                          "of the default command holds only headline-mode launches)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the PMC passes (rocprofv3 FETCH_SIZE / WRITE_SIZE children) that measure roofline.traffic")
+    ap.add_argument("--train-iters", type=int, default=400,
+                    help="untimed bundle_adjust_frames iterations on the same keyframes before the headline is "
+                         "timed, so that it runs on a map in the state Mapping renders (trained: the sparse "
+                         "decoder's class mix settles); stops early once the composited fraction is stable. "
+                         "0: time the random-init map (the untrained figure is reported beside the trained one)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # PMC child: headline iterations only
     ap.add_argument("--step-size", type=float, default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
@@ -333,7 +338,8 @@ def measure_traffic(args, step_size):
             cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", c, "--output-format", "csv", "-d", d, "-o", "pmc",
                    "--", sys.executable, os.path.abspath(__file__), "--probe", "--step-size", repr(step_size),
                    "--scene", args.scene, "--frames", str(args.frames), "--rays-per-frame", str(args.rays_per_frame),
-                   "--width", str(args.width), "--steps", "8", "--warmup", "2", "--no-cpu-baseline"]
+                   "--width", str(args.width), "--steps", "8", "--warmup", "2", "--no-cpu-baseline",
+                   "--train-iters", str(args.train_iters_done)]
             env = dict(os.environ, TMPDIR=tmp)
             r = subprocess.run(cmd, env=env, capture_output=True, text=True)
             if r.returncode != 0:
@@ -349,6 +355,8 @@ def measure_traffic(args, step_size):
             for row in csv.DictReader(open(path)):
                 if row.get("Counter_Name") == c:
                     vals[_short(row["Kernel_Name"])].append(float(row["Counter_Value"]) * 1024.0)  # KB units
+            # the trained map's launches: the last quarter of each kernel's (the probe trains first)
+            vals = {k: v[len(v) - max(1, len(v) // 4):] if args.train_iters_done else v for k, v in vals.items()}
             out[c] = {k: sorted(v)[len(v) // 2] * (2.0 if c == "FETCH_SIZE" else 1.0) for k, v in vals.items()}
     kern = {}
     for k in set(out["FETCH_SIZE"]) | set(out["WRITE_SIZE"]):
@@ -497,12 +505,67 @@ def main():
             el = float(t.item())
         return el
 
-    if args.probe:  # PMC child (measure_traffic): the headline iterations only
+    def train_map(max_iters, chunk=50):
+        """Untimed bundle_adjust_frames iterations on the same keyframes (the
+        map as Mapping.spin leaves it for its next call, mapping.py:96-218):
+        chunks of `chunk` until the composited fraction moves by < 0.01 between
+        chunks (at least 2) or max_iters.  Returns [(iterations, composited
+        fraction, kept fraction)] after each chunk."""
+        trace, done, prev = [], 0, None
+        m_acc = {"m": 0, "n": 0}
+        while done < max_iters:
+            n = min(chunk, max_iters - done)
+            run_ba(n)  # the first call creates the engine
+            done += n
+            eng = head_engine()
+            eng.select_stats(reset=True)
+            eng.stats_hook = lambda st: (m_acc.__setitem__("m", m_acc["m"] + st[4]),
+                                         m_acc.__setitem__("n", m_acc["n"] + 1))
+            m_acc.update(m=0, n=0)
+            run_ba(10)  # a short measured call: the class mix of the map as it now is
+            done += 10
+            eng.stats_hook = None
+            sel = eng.select_stats(reset=True)
+            m_step = m_acc["m"] / max(m_acc["n"], 1)
+            comp = sel["composited_sum"] / max(sel["steps"], 1) / max(m_step, 1)
+            kept = sel["kept_sum"] / max(sel["steps"], 1) / max(m_step, 1)
+            trace.append((done, round(comp, 4), round(kept, 4)))
+            if prev is not None and abs(comp - prev) < 0.01 and len(trace) >= 2:
+                break
+            prev = comp
+        torch.cuda.synchronize()
+        return trace
+
+    if args.probe:  # PMC child (measure_traffic): the headline iterations only (after the same training)
+        if args.train_iters > 0:
+            run_ba(args.train_iters)
         run_ba(args.warmup + args.steps)
         torch.cuda.synchronize()
         return
     if args.path != "ba":
         raise SystemExit("bench.py: the headline is --path ba (the other paths run with --extras)")
+    # the random-init map first (rounds 1-5 timed only this), then the map
+    # trained on the same keyframes: the headline
+    untrained, train_trace = None, []
+    args.train_iters_done = 0
+    if args.train_iters > 0:
+        el_u = timed_ba(args.steps, max(1, args.warmup), record=True)
+        hs_u = dict(head_stats)
+        steps_u = sel_stats.get("steps", 0)
+        m_u = hs_u["m"] / max(hs_u["n"], 1)
+        untrained = {"value": args.frames * args.rays_per_frame * args.steps * world / el_u,
+                     "ms_per_step": 1000.0 * el_u / args.steps, "gpu_ms_per_step": pace.get("gpu_ms_per_step"),
+                     "decoder_kept_fraction": sel_stats["kept_sum"] / steps_u / m_u if steps_u and m_u else None,
+                     "composited_fraction": sel_stats["composited_sum"] / steps_u / m_u if steps_u and m_u else None,
+                     "samples_per_step": m_u}
+        log(f"untrained map: {untrained['ms_per_step']:.4f} ms/step; training (untimed, <= {args.train_iters} it)")
+        train_trace = train_map(args.train_iters)
+        args.train_iters_done = train_trace[-1][0] if train_trace else 0
+        log(f"trained {args.train_iters_done} iterations: composited / kept fraction {train_trace[-1][1:]}")
+        for k in list(head_stats):
+            head_stats[k] = 0
+        sel_stats.clear()
+        pace.clear()
     elapsed = timed_ba(args.steps, max(1, args.warmup), record=True)
     path_desc = ("bundle_adjust_frames as Mapping.do_mapping calls it (points encoder + its Adam, torch Adam "
                  "optimisers; per-iteration gumbel pixel sampling on the device, keyframe poses optimised) — "
@@ -750,8 +813,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (room0-shaped octree + Replica pinhole RGB-D keyframes, analytic GT; random-init "
-                "embeddings/decoder)",
+        "data": ("synthetic (room0-shaped octree + Replica pinhole RGB-D keyframes, analytic GT); embeddings / "
+                 "decoder / poses trained from random init by %d untimed bundle_adjust_frames iterations on the "
+                 "same keyframes before timing (map_state: %s)" % (args.train_iters_done, "trained"
+                                                                   if args.train_iters_done else "random-init")),
         "config": {"workload": f"{args.scene}: {args.frames} keyframes x {args.rays_per_frame} rays/iter per GPU, "
                                f"{tree.count_nodes()} octree nodes, decoder W={args.width}, "
                                f"{h_m / max(h_r, 1):.1f} samples/hit ray (step {step_size:.5f} m)",
@@ -761,6 +826,11 @@ def main():
                    # these) and the composited ones (a compositing weight: z < z_min + truncation)
                    "decoder_kept_fraction": kept / h_m if kept is not None and h_m else None,
                    "composited_fraction": comp / h_m if comp is not None and h_m else None,
+                   "map_state": "trained" if args.train_iters_done else "random-init",
+                   "train_iterations": args.train_iters_done,
+                   # (iterations so far, composited fraction, kept fraction) after each training chunk
+                   "train_trace": train_trace,
+                   "untrained": untrained,
                    "parallelism": f"dp{world} (ray-sharded, union-batch loss, "
                                   f"{dist.get_backend() if world > 1 else 'no'} collectives)"},
         "roofline": roof_qi,

@@ -709,14 +709,55 @@ __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float 
     }
 }
 
-template <bool PACKED>
-__device__ __forceinline__ void trace_pass_help(int cur, int64_t n_rays, const float *rays_o, const float *rays_d,
-                                             const float *centres, const int *structure, const PackRec *packed,
-                                             float half, float max_distance, float step_size, int *hit_idx,
-                                             float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, KeyLds &S,
-                                             IsLds &L) {
-    trace_pass<PACKED>(cur, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance, step_size,
-                       hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
+// A helped block's per-ray values for its aggregate (lookback.h: a
+// predecessor that has not started), one wave per ray: the hits by the
+// serial DFS (dfs_ray: the reference's emission order — the 50 smallest DFS
+// keys the wave traversal keeps), then the same stable (t_in, DFS order)
+// ranks, max_distance trim and left-to-right Σ(t_out − t_in) as trace_pass,
+// so the hit count and ⌈Σ/step⌉ are the same bits; the AABB-test count is
+// the DFS's (a statistic) and no rounds.  Nothing is written to the hit
+// rows: the block's owner writes them when it runs.  Small on purpose — a
+// second copy of the wave traversal here cost the own pass 3 µs.
+__device__ __forceinline__ void help_trace_pass(int cur, int64_t n_rays, const float *rays_o, const float *rays_d,
+                                             const float *centres, const int *structure, float half,
+                                             float max_distance, float step_size, KeyLds &S, IsLds &L) {
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int64_t r = (int64_t)cur * kIsWaves + w;
+    int nv = 0, mc = 0, visits = 0;
+    if (r < n_rays) {
+        const float o[3] = {rays_o[r * 3 + 0], rays_o[r * 3 + 1], rays_o[r * 3 + 2]};
+        const float d[3] = {rays_d[r * 3 + 0], rays_d[r * 3 + 1], rays_d[r * 3 + 2]};
+        int cnt = 0;
+        bool ov = false;
+        if (lane == 0)
+            visits = dfs_ray<1>(o, d, centres, structure, half, kMaxHits, S.dfs_node, S.dfs_mask, S.lidx, S.lt0,
+                                S.lt1, &cnt, &ov);
+        cnt = __shfl(cnt, 0, kWave);
+        visits = __shfl(visits, 0, kWave);
+        wave_lds_sync();
+        const float ti = lane < cnt ? S.lt0[lane] : 0.f;
+        int rank = 0;
+        for (int j = 0; j < cnt; ++j) {
+            const float tj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ti), j));
+            rank += (tj < ti) || (tj == ti && j < lane);
+        }
+        if (lane < cnt) S.hd[rank] = S.lt1[lane] - ti;
+        nv = wave_sum(lane < cnt && !(ti > max_distance) ? 1 : 0);
+        wave_lds_sync();
+        if (lane == 0) {
+            float dsum = 0.0f;
+            for (int l = 0; l < nv; ++l) dsum = dsum + S.hd[l];
+            mc = nv > 0 ? (int)ceilf(__fdiv_rn(dsum, step_size)) : 0;
+        }
+        mc = __shfl(mc, 0, kWave);
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        L.vis[w] = visits;
+        L.rd[w] = 0;
+        L.nv[w] = nv;
+        L.mc[w] = mc;
+    }
 }
 
 // wave 0: a block's aggregate {hit rays, P, max ⌈Σ/step⌉, AABB tests, rounds}
@@ -801,26 +842,27 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
         trace_agg(L, own_agg, own_hm);
         own_nv = lane < kIsWaves ? L.nv[lane] : 0;
         own_c0 = lane < kIsWaves ? L.c0[lane] : -1;
-        lb_rc = lb_scan_help<5, 0b00110u>(lb_desc, blk, (int)gridDim.x, lb_tag, lane, own_agg, own_ex, spins,
-                                           ctl.spin_max);
-        if (lane == 0) s_cmd = lb_rc;
     }
-    __syncthreads();
-    for (int cmd = __builtin_amdgcn_readfirstlane(s_cmd); cmd >= 0; cmd = __builtin_amdgcn_readfirstlane(s_cmd)) {
-        trace_pass_help<PACKED>(cmd, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance,
-                                step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
-        __syncthreads();
+    for (int cmd = -1;;) {  // one look-back call site; cmd ≥ 0: a block helped first
+        if (cmd >= 0) {
+            help_trace_pass(cmd, n_rays, rays_o, rays_d, centres, structure, half, max_distance, step_size, S, L);
+            __syncthreads();
+        }
         if (threadIdx.x < kWave) {
-            uint32_t agg[5];
-            uint64_t hm;
-            trace_agg(L, agg, hm);
-            lb_publish<5>(lb_desc, cmd, lane, agg, lb_tag);
-            if (lane == 0) atomicAdd(&psvo_g_lb_helps[0], 1ull);
+            if (cmd >= 0) {
+                uint32_t agg[5];
+                uint64_t hm;
+                trace_agg(L, agg, hm);
+                lb_publish<5>(lb_desc, cmd, lane, agg, lb_tag);
+                if (lane == 0) atomicAdd(&psvo_g_lb_helps[0], 1ull);
+            }
             lb_rc = lb_scan_help<5, 0b00110u>(lb_desc, blk, (int)gridDim.x, lb_tag, lane, own_agg, own_ex, spins,
                                                ctl.spin_max);
             if (lane == 0) s_cmd = lb_rc;
         }
         __syncthreads();
+        cmd = __builtin_amdgcn_readfirstlane(s_cmd);
+        if (cmd < 0) break;
     }
     if (threadIdx.x >= kWave) return;
     const bool ok = lb_rc == kLbDone;
@@ -1473,6 +1515,14 @@ struct SmpLb {  // in LDS: nothing of it stays in registers across the help pass
 };
 __device__ int smp_lb_pass(bool own, int cur, int blk, int nb, const int *s_ns, const int *s_cw, const SampleTail &tl,
                            SmpLb &lb);
+__device__ __forceinline__ int sample_fused_ray_help(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                  int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                                                  const float *hit_t0, const float *hit_t1, const float *ray_dsum,
+                                                  float step_size, const float *noise, uint64_t seed, int *stats,
+                                                  int *s_idx, float *s_depth, float *s_dist, const int *slot0,
+                                                  int slot0_nch, const int *nv_rank, const int *col0_rank,
+                                                  int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
+                                                  int blk);
 __device__ void smp_lb_finish(int n, const SmpLb &lb, int *__restrict__ stats, const SampleTail &tl, int *s_off,
                               int st_word, int max_steps_cap, int blk);
 
@@ -1550,32 +1600,32 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     __syncthreads();
     SMP_T(2);
     __shared__ SmpLb lb;  // wave 0: the own block's aggregate / prefix
-    if (w == 0) {
-        const int rc = smp_lb_pass(true, blk, blk, last_lb + 1, s_ns, s_cw, tl, lb);
-        if (lane == 0) s_cmd = rc;
-    }
-    __syncthreads();
-    // a predecessor that has not started: this workgroup samples that
-    // block's rows too and publishes their aggregate (lookback.h)
+    // one look-back call site; cmd ≥ 0: a predecessor that has not started,
+    // whose rows this workgroup samples first to publish their aggregate
+    // (lookback.h)
     bool helped = false;
-    for (int cmd = __builtin_amdgcn_readfirstlane(s_cmd); cmd >= 0; cmd = __builtin_amdgcn_readfirstlane(s_cmd)) {
-        helped = true;
-        int hil = 0, hcw = 0;
-        const int hc = sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0,
-                                        hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0,
-                                        slot0_nch, nv_rank, col0_rank, hil, bins_all[w], tl, hcw, nullptr, nullptr,
-                                        cmd);
-        if (lane == 0) {
-            if (hc >= 0) ray_ns[hil] = hc;
-            s_ns[w] = hc;
-            s_cw[w] = hcw;
+    for (int cmd = -1;;) {
+        if (cmd >= 0) {
+            helped = true;
+            int hil = 0, hcw = 0;
+            const int hc = sample_fused_ray_help(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx,
+                                                 hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx,
+                                                 s_depth, s_dist, slot0, slot0_nch, nv_rank, col0_rank, hil,
+                                                 bins_all[w], tl, hcw, cmd);
+            if (lane == 0) {
+                if (hc >= 0) ray_ns[hil] = hc;
+                s_ns[w] = hc;
+                s_cw[w] = hcw;
+            }
+            __syncthreads();
         }
-        __syncthreads();
         if (w == 0) {
-            const int rc = smp_lb_pass(false, cmd, blk, last_lb + 1, s_ns, s_cw, tl, lb);
+            const int rc = smp_lb_pass(cmd < 0, cmd < 0 ? blk : cmd, blk, last_lb + 1, s_ns, s_cw, tl, lb);
             if (lane == 0) s_cmd = rc;
         }
         __syncthreads();
+        cmd = __builtin_amdgcn_readfirstlane(s_cmd);
+        if (cmd < 0) break;
     }
     const int own_count = count, own_il = il;
     if (w == 0) smp_lb_finish(n_lb, lb, stats, tl, s_off, st_word, max_steps_cap, blk);
@@ -1722,6 +1772,20 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
         cnt_word = pack_counts(wave_sum(nf), wave_sum(nsm), pf, psm, gd > 0.01f && gd < tl.c.max_depth);
     }
     return wave_sum(count);
+}
+
+// a helped block's rows (lookback.h), out of line: the own pass keeps its registers
+__device__ __forceinline__ int sample_fused_ray_help(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
+                                                  int max_steps_cap, const int *rank_ray, const int *hit_idx,
+                                                  const float *hit_t0, const float *hit_t1, const float *ray_dsum,
+                                                  float step_size, const float *noise, uint64_t seed, int *stats,
+                                                  int *s_idx, float *s_depth, float *s_dist, const int *slot0,
+                                                  int slot0_nch, const int *nv_rank, const int *col0_rank,
+                                                  int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
+                                                  int blk) {
+    return sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
+                            step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0, slot0_nch, nv_rank,
+                            col0_rank, il_out, W, tl, cnt_word, nullptr, nullptr, blk);
 }
 
 // k_scan_samples' work for one sampler workgroup (its 8 rows), wave 0 only,

@@ -3,7 +3,7 @@ kernel trace: start / end / duration (us, relative to the iteration's
 look-ahead pose kernel: k_pose_step_frames, or k_pose_rays_frames before it
 existed) and queue of every kernel; with a HIP runtime trace beside it
 (rocprofv3 --hip-runtime-trace), also when the host issued each launch.
-Usage: ba_timeline.py run_kernel_trace.csv [iteration index]"""
+Usage: ba_timeline.py run_kernel_trace.csv [--] [iteration index; negative: from the last]"""
 import csv
 import os
 import re
@@ -11,7 +11,8 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+argv = [a for a in sys.argv[1:] if a != "--"]  # (`--` lets a negative index through: from the end)
+k = int(argv[1]) if len(argv) > 1 else 8
 api = {}
 hip = sys.argv[1].replace("kernel_trace.csv", "hip_api_trace.csv")
 if os.path.exists(hip):

@@ -25,7 +25,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic ${BENCH_ARGS:-} \
       > gpurun_out/${R}_prof_bench.json 2> gpurun_out/${R}_prof.err
   rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
-  for it in 8 12; do python3 scripts/ba_timeline.py gpurun_out/${R}_prof/run_kernel_trace.csv $it > gpurun_out/${R}_ba_timeline_$it.txt 2>&1 || true; done
+  for it in ${TL_ITERS:--30 -25}; do python3 scripts/ba_timeline.py gpurun_out/${R}_prof/run_kernel_trace.csv -- $it > gpurun_out/${R}_ba_timeline_$it.txt 2>&1 || true; done
   rm -f gpurun_out/${R}_prof/run_kernel_trace.csv.bak gpurun_out/${R}_prof/run_hip_api_trace.csv.bak
 fi
 if [ "${CONFIGS:-0}" = "1" ]; then  # C: ScanNet W=256 8x1024; E: multiroom W=256
@@ -42,5 +42,14 @@ for f in sys.argv[1:]:
     print(f, round(d["value"]), d["ms_per_step"], d["gpu_ms_per_step"], d["config"].get("decoder_kept_fraction"),
           d["roofline_mfma"]["fwd_ms"], d["roofline_mfma"]["bwd_ms"])
 PY
+fi
+
+if [ "${DIST:-0}" = "1" ]; then
+  # N>1 rehearsal: two ranks sharing the one GPU over gloo (the driver runs RCCL on 8 GPUs)
+  PSVO_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 ${DIST_ARGS:-} \
+      > gpurun_out/${R}_bench_dist2.json 2> gpurun_out/${R}_bench_dist2.err
+  rc=$?
+  echo "dist2 rc=$rc"; tail -c 600 gpurun_out/${R}_bench_dist2.json; tail -5 gpurun_out/${R}_bench_dist2.err
 fi
 echo done
