@@ -529,6 +529,10 @@ def main():
             m_step = m_acc["m"] / max(m_acc["n"], 1)
             comp = sel["composited_sum"] / max(sel["steps"], 1) / max(m_step, 1)
             kept = sel["kept_sum"] / max(sel["steps"], 1) / max(m_step, 1)
+            if world > 1:  # one decision for all ranks (each call issues collectives): the ranks' mean
+                t = torch.tensor([comp, kept], dtype=torch.float64, device=device)
+                dist.all_reduce(t)
+                comp, kept = (float(x) / world for x in t.cpu())
             trace.append((done, round(comp, 4), round(kept, 4)))
             if prev is not None and abs(comp - prev) < 0.01 and len(trace) >= 2:
                 break

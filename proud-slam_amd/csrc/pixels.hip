@@ -27,6 +27,8 @@
 // mask (1 B, optional), the weights (4 B, optional); plus the N gathered rows.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include "psvo_common.h"
 
 namespace psvo {
@@ -211,9 +213,12 @@ __device__ void px_state(const PxArgs &a, int f, int *sh_suffix, int *sh_res, ui
 // (a 16-KB LDS histogram whatever the digit: 1-KB histograms for the FAST
 // digits, co-resident with the decoder forward, measured slower — the
 // decoder loses more than the draw gains, profiles/r04px_ab_draw_lds.txt)
-template <bool FAST, int P>
+// SMALL (FAST only, PSVO_PX_SMALL_LDS=1, a measured switch): a 1-KB histogram, so the pass
+// fits beside the traversal's 2 × 76.5 KB per CU (with PSVO_BA_DRAW_AFTER_STEP=1)
+template <bool FAST, int P, bool SMALL = false>
 __global__ __launch_bounds__(kPxThreads) void k_px_hist(PxArgs a) {
-    __shared__ int h[kPxBins];
+    static_assert(!SMALL || FAST, "the 1-KB histogram holds 8-bit digits");
+    __shared__ int h[SMALL ? 256 : kPxBins];
     __shared__ int sh_suffix[kPxThreads];
     __shared__ int sh_res[2];
     constexpr int kShift = px_shift<FAST>(P);
@@ -428,9 +433,16 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     const dim3 grid(a.nb, n_frames);
     if (weights) psvo::launch(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
     if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
-        psvo::launch((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
-        psvo::launch((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
+        static const bool small = getenv("PSVO_PX_SMALL_LDS") && *getenv("PSVO_PX_SMALL_LDS") == '1';
+        if (small) {
+            psvo::launch((k_px_hist<true, 0, true>), grid, dim3(kPxThreads), 0, st, a);
+            psvo::launch((k_px_hist<true, 1, true>), grid, dim3(kPxThreads), 0, st, a);
+            psvo::launch((k_px_hist<true, 2, true>), grid, dim3(kPxThreads), 0, st, a);
+        } else {
+            psvo::launch((k_px_hist<true, 0>), grid, dim3(kPxThreads), 0, st, a);
+            psvo::launch((k_px_hist<true, 1>), grid, dim3(kPxThreads), 0, st, a);
+            psvo::launch((k_px_hist<true, 2>), grid, dim3(kPxThreads), 0, st, a);
+        }
         psvo::launch(k_px_count<true>, grid, dim3(kPxThreads), 0, st, a);
         psvo::launch(k_px_write<true>, grid, dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb, out_depth);
     } else {

@@ -580,9 +580,18 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     # each next draw is queued as soon as its step is (beside the persistent
     # decoder kernels); ordered after the previous step's decoder backward it
     # measured slower (round 4, config B: 1.000-1.059 vs 0.985-1.000 ms)
+    # PSVO_BA_DRAW_AFTER_STEP=1 (measured switch): each draw waits until the
+    # previous step's kernels on the caller's stream are done, so that it runs
+    # beside the next step's latency-bound query instead of beside the
+    # persistent decoder backward
+    after_step = os.environ.get("PSVO_BA_DRAW_AFTER_STEP") == "1"
+    step_done = [None]
+
     def draw_ahead(it):
         if side is None:
             return draw(it), None
+        if after_step and step_done[0] is not None:
+            side.wait_event(step_done[0])
         # the batched draw writes into a ring of buffers made once per call
         # (below): no tensor of the loop is freed with record_stream(main),
         # whose allocator event — recorded on main at the free, with the
@@ -660,6 +669,9 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
             eng.grad_exchange()
             eng.adam()
         pstep = [c if upd[f] else pstep[f] for f, c in enumerate(cur_steps)]
+        if after_step and side is not None:
+            step_done[0] = step_done[0] or torch.cuda.Event()
+            step_done[0].record(main)
         cur = nxt if nxt is not None else (draw(it + 1) if it + 1 < num_iterations else None)
         if it < 2 or it == num_iterations - 1:
             clk(f"step{it}")
