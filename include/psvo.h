@@ -515,7 +515,9 @@ void psvo_engine_free(psvo_engine *e);
  * the union layout and the sampler's slot-0 table follow on every rank —
  * then ONE all-gather of 8 words after the sampler (S_max and, when the
  * step's GT depth was known at query time and the loss value is not wanted,
- * the loss normalisers' counts); step phase: the normaliser counts (8
+ * the loss normalisers' counts) — issued by the consuming step once its
+ * interpolation is queued, on a stream of the engine's own (`stream` is then
+ * not the query's), and before the next query's first gather; step phase: the normaliser counts (8
  * doubles summed) only when some rank's query could not count them (one
  * decision for all ranks, from the gathered words: every rank issues the same
  * collectives; a query that counted used the GT depths it was given, which
@@ -557,6 +559,13 @@ int psvo_engine_set_paths(psvo_engine *e, int paths);   /* with no query queued 
  * summed; reset != 0 zeroes the sums.  An abandoned look-back wait of any
  * step is reported as an error. */
 int psvo_engine_select_stats(psvo_engine *e, void *stream, int64_t *out, int reset);
+
+/* `stream` waits until the last mapping step's sample selection (the sparse
+ * decoder's k_select_samples) has run — nothing if no step has.  The
+ * keyframe pixel draws of bundle_adjust_frames queue behind it, so that
+ * their latency-bound passes run beside the decoder forward / backward
+ * instead of beside the selection's look-back. */
+int psvo_engine_gate_stream(psvo_engine *e, void *stream);
 
 /* Tests only: the in-launch look-back scans of the sites in `mask` (1
  * traversal, 2 sampler, 4 sample selection) get a spin bound of spin_bound

@@ -9,6 +9,7 @@
 namespace psvo {
 
 static thread_local char g_err[512] = "";
+thread_local hipEvent_t g_stop_event = nullptr;
 
 int set_error(int code, const char *fmt, ...) {
     va_list ap;

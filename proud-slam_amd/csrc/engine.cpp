@@ -53,7 +53,9 @@ struct Arena {
 // updates), so the step that consumes it finds its sizes already on the host.
 struct QuerySet {
     Arena a;                      // slots kStats..kOffsets
-    unsigned long long *host_raw = nullptr;  // coherent pinned, PSVO_STAT_WORDS {seq, value} granules
+    // coherent pinned {seq, value} granules: PSVO_STAT_WORDS for the read-back
+    // after the sampler, PSVO_STAT_WORDS more for a data-parallel query's second
+    unsigned long long *host_raw = nullptr;
     int host_stats[PSVO_STAT_WORDS] = {};     // the values of the last statistics that landed
     int seq = 0;                  // the flag value the current statistics carry
     hipStream_t qstream = nullptr;  // the stream the query was queued on
@@ -76,6 +78,16 @@ struct QuerySet {
     const float *counts_gt = nullptr;
     uint64_t seed = 0;
     int max_steps = 0;
+    // data parallel: the query's second half — dist_counts → the all-gather of
+    // [S_max, count words] → dist_smax → the second read-back — on the
+    // engine's q2 stream, issued by the step once its interpolation and sdf
+    // trunk are queued (query_phase2), so it runs beside them instead of on
+    // the pose → traversal → sampler → interpolation chain
+    hipEvent_t p1 = nullptr;     // the first read-back's kernel done (bound to its dispatch)
+    hipEvent_t done2 = nullptr;  // the second read-back done
+    bool p2_pending = false;     // queued first half, second half not issued yet
+    const float *p2_gt = nullptr;
+    float p2_tr = 0.f, p2_max_depth = 0.f;
 };
 
 }  // namespace
@@ -141,6 +153,7 @@ struct psvo_engine {
     int q_head = 0, q_count = 0;
     uint32_t lb_tag = 0;            // the last look-back descriptor tag handed out (lookback.h)
     hipStream_t side = nullptr;     // psvo_map_query's stream
+    hipStream_t q2s = nullptr;      // data parallel: the queries' second halves (QuerySet::p2_pending)
     hipEvent_t in_ready = nullptr;  // the caller's stream position at psvo_map_query
     // the embedding backward runs on `aux` beside the decoder's weight
     // gradients (k_interp_bwd's 8-KB workgroups fit next to k_mlp_dw2's 152 KB)
@@ -161,6 +174,8 @@ struct psvo_engine {
     bool bwd_recorded = false;     // dfeat_ready holds a step's decoder backward end (psvo_map_side_wait)
     bool adam_pending = false;
     hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
+    hipEvent_t draw_gate = nullptr;   // the last step's sample selection done (psvo_engine_gate_stream)
+    bool draw_gate_recorded = false;
     EngineTimer tm;
     // the decoder images a look-ahead step built on st after its Adam step,
     // for the decoder whose W[0] it names; consumed by the next
@@ -380,23 +395,25 @@ bool stats_landed(const unsigned long long *raw, int seq, int *out) {
     memcpy(out, v, sizeof(v));
     return true;
 }
-int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who);
-int spin_wait(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) {
+int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who, int part);
+// part 0: the read-back after the sampler; 1: a data-parallel query's second
+int spin_wait(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who, int part = 0) {
     int tmp[PSVO_STAT_WORDS];
-    const bool ready = stats_landed(q.host_raw, q.seq, tmp);
+    const bool ready = stats_landed(q.host_raw + part * PSVO_STAT_WORDS, q.seq, tmp);
     const double t0 = now_ns();
-    const int rc = spin_wait_impl(q, ev, qs, who);
+    const int rc = spin_wait_impl(q, ev, qs, who, part);
     g_host_wait.ns += now_ns() - t0;
     g_host_wait.calls += 1;
     g_host_wait.spun += ready ? 0 : 1;
     return rc;
 }
-int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) {
+int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who, int part) {
     // the runtime query (error detection only) costs microseconds: at most one
     // per 0.5 ms of waiting, so the statistics are seen as soon as they land
+    const unsigned long long *raw = q.host_raw + part * PSVO_STAT_WORDS;
     double next_query = now_ns() + 5e5;
     for (unsigned it = 1;; ++it) {
-        if (stats_landed(q.host_raw, q.seq, q.host_stats)) return PSVO_OK;
+        if (stats_landed(raw, q.seq, q.host_stats)) return PSVO_OK;
         if ((it & 255) == 0 && now_ns() >= next_query) {
             next_query = now_ns() + 5e5;
             const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(qs);
@@ -405,7 +422,7 @@ int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) 
             // the event (no system-scope fence) may complete just before the
             // kernel's system-scope granule stores are visible: poll a while more
             for (unsigned k = 0; k < (1u << 22); ++k)
-                if (stats_landed(q.host_raw, q.seq, q.host_stats)) return PSVO_OK;
+                if (stats_landed(raw, q.seq, q.host_stats)) return PSVO_OK;
             return set_error(PSVO_E_LAUNCH, "%s: stats read-back: event complete, granules not tagged %d", who,
                              q.seq);
         }
@@ -414,15 +431,19 @@ int spin_wait_impl(QuerySet &q, hipEvent_t ev, hipStream_t qs, const char *who) 
 
 int query_set_init(QuerySet &s) {
     if (s.host_raw) return PSVO_OK;
-    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_raw), PSVO_STAT_WORDS * sizeof(unsigned long long),
+    if (hipHostMalloc(reinterpret_cast<void **>(&s.host_raw), 2 * PSVO_STAT_WORDS * sizeof(unsigned long long),
                       hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
         // device-side ordering only: the statistics reach the host through the
         // scan kernel's own system-scope release (k_scan_samples / k_stats_to_host)
         hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
-        hipEventCreateWithFlags(&s.freed, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+        hipEventCreateWithFlags(&s.freed, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+        // (bound to a dispatch as its stop event: a timing event)
+        hipEventCreateWithFlags(&s.p1, hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done2, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine: query set allocation failed");
-    memset(s.host_raw, 0, PSVO_STAT_WORDS * sizeof(unsigned long long));  // tag 0: no statistics yet (seq from 1)
+    // tag 0: no statistics yet (seq from 1)
+    memset(s.host_raw, 0, 2 * PSVO_STAT_WORDS * sizeof(unsigned long long));
     return PSVO_OK;
 }
 
@@ -432,6 +453,8 @@ void query_set_free(QuerySet &s) {
     if (s.host_raw) (void)hipHostFree(s.host_raw);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.freed) (void)hipEventDestroy(s.freed);
+    if (s.p1) (void)hipEventDestroy(s.p1);
+    if (s.done2) (void)hipEventDestroy(s.done2);
 }
 
 }  // namespace
@@ -514,6 +537,14 @@ extern "C" int psvo_engine_set_paths(psvo_engine *e, int paths) {
     PSVO_REQUIRE(e && (paths & ~(PSVO_PATH_QUERY_SPLIT | PSVO_PATH_PADDED | PSVO_PATH_DENSE_DECODER)) == 0, "engine_set_paths: bad arguments");
     PSVO_REQUIRE(e->q_count == 0, "engine_set_paths: queries are queued");
     e->paths = paths;
+    return PSVO_OK;
+}
+
+extern "C" int psvo_engine_gate_stream(psvo_engine *e, void *stream) {
+    PSVO_REQUIRE(e, "engine_gate_stream: null engine");
+    if (!e->draw_gate_recorded) return PSVO_OK;
+    if (hipStreamWaitEvent(as_stream(stream), e->draw_gate, 0) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "engine_gate_stream: stream wait failed");
     return PSVO_OK;
 }
 
@@ -657,6 +688,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
         if (e->a.p[s]) (void)hipFree(e->a.p[s]);
     for (auto &q : e->qs) query_set_free(q);
     if (e->side) (void)hipStreamDestroy(e->side);
+    if (e->q2s) (void)hipStreamDestroy(e->q2s);
     if (e->aux) {
         (void)hipStreamSynchronize(e->aux);  // a pending tail split's optimiser step
         (void)hipStreamDestroy(e->aux);
@@ -673,6 +705,7 @@ extern "C" void psvo_engine_free(psvo_engine *e) {
     if (e->adam_done) (void)hipEventDestroy(e->adam_done);
     if (e->next_ready) (void)hipEventDestroy(e->next_ready);
     if (e->in_ready) (void)hipEventDestroy(e->in_ready);
+    if (e->draw_gate) (void)hipEventDestroy(e->draw_gate);
     if (e->host_flags) (void)hipHostFree(e->host_flags);
     delete e;
 }
@@ -808,6 +841,50 @@ constexpr int64_t kW128 = 128;  // h2 row length (the width-128 decoder)
     T *name = reinterpret_cast<T *>(arena_buf(q.a, st, slot, (bytes), &rc));    \
     if (!name) return rc;
 
+// A data-parallel query's second half (QuerySet::p2_pending) on the q2
+// stream, forked at the first read-back: the rank's [S_max, count words]
+// (dist_counts), their all-gather on the query communicator, the union S_max
+// and normaliser sums (dist_smax), the second read-back.  Nothing on the
+// step's stream waits for it: the host does (render, before the first launch
+// sized by S_max), and aux before it reads the sums.
+int query_phase2(psvo_engine *e, QuerySet &q, const char *who) {
+    if (!q.p2_pending) return PSVO_OK;
+    q.p2_pending = false;
+    const EngineExchange &x = e->x;
+    if (!e->q2s && hipStreamCreateWithFlags(&e->q2s, hipStreamNonBlocking) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "%s: stream creation failed", who);
+    hipStream_t s2 = e->q2s;
+    int *stats = static_cast<int *>(q.a.p[kStats]);
+    int *in = x.xi32 + x.q2_in_off();
+    // (the count words start at zero, whatever a failed earlier half left)
+    if (hipStreamWaitEvent(s2, q.p1, 0) != hipSuccess ||
+        hipMemsetAsync(in + 1, 0, (kDistWordsPerRank - 1) * sizeof(int), s2) != hipSuccess)
+        return set_error(PSVO_E_LAUNCH, "%s: stream ordering failed", who);
+    ENG_CALL(dist_counts(s2, q.R, stats, static_cast<const int *>(q.a.p[kRankRay]), q.p2_gt,
+                         static_cast<const float *>(q.a.p[kSDepth]), q.max_steps,
+                         static_cast<const int *>(q.a.p[kRayNs]), q.p2_tr, q.p2_max_depth, in));
+    ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.q2_in_off(), x.q2_all_off(), kDistWordsPerRank, s2,
+                    "S_max + counts"));
+    ENG_CALL(dist_smax(s2, x.xi32 + x.q2_all_off(), x.world, stats, in,
+                       q.p2_gt ? static_cast<double *>(q.a.p[kDistSums]) : nullptr));
+    ENG_CALL(psvo::stats_to_host(s2, stats, q.host_raw + PSVO_STAT_WORDS, PSVO_STAT_WORDS, q.seq));
+    q.stats_zeroed = stats;
+    if (hipEventRecord(q.done2, s2) != hipSuccess) return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+    return PSVO_OK;
+}
+
+// every queued second half, oldest query first; `st` then follows them
+int flush_phase2(psvo_engine *e, hipStream_t st, const char *who) {
+    for (int k = 0; k < 2; ++k) {
+        QuerySet &o = e->qs[e->q_head ^ k];
+        if (!o.p2_pending) continue;
+        ENG_CALL(query_phase2(e, o, who));
+        if (hipStreamWaitEvent(st, o.done2, 0) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: stream ordering failed", who);
+    }
+    return PSVO_OK;
+}
+
 // The query half of render_rays (render_helpers.py:363-413): intersection,
 // hit ranks and sampling of one ray batch into query set `q` on stream `st`,
 // then the 32-byte statistics read-back (event q.done).  The sampler reads P,
@@ -819,6 +896,10 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
                   const float *rays_o, const float *rays_d, uint64_t seed, const char *who,
                   const float *noise = nullptr, bool record_done = true, const float *counts_gt = nullptr) {
     int rc = PSVO_OK;
+    // data parallel: an earlier query's second half first — every rank issues
+    // the collectives in query order, and this query's kernels follow that
+    // half's reads of the buffers they overwrite
+    ENG_CALL(flush_phase2(e, st, who));
     Q_BUF(int, stats, kStats, PSVO_STAT_WORDS * sizeof(int));
     if (q.stats_zeroed != stats && hipMemsetAsync(stats, 0, PSVO_STAT_WORDS * sizeof(int), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: memset failed", who);
@@ -868,10 +949,13 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         if (R > x.max_rays_rank)
             return set_error(PSVO_E_INVALID, "%s: %lld rays exceed the exchange's max_rays_rank %lld", who,
                              (long long)R, (long long)x.max_rays_rank);
-        ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off(), nv_rank));
+        // (a query without GT depths: the step counts the normalisers itself —
+        // on every rank, decided from the gathered flags)
+        ENG_CALL(dist_pack(st, R, stats, rank_ray, hit_idx, ray_nv, x.xi32 + x.in_off(), nv_rank,
+                           counts_gt ? 0 : psvo::PSVO_FLAG_UNION_UNCOUNTED));
         ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.in_off(), x.all_off(), x.cw, st, "query layout"));
         ENG_CALL(dist_layout(st, x.xi32 + x.all_off(), x.world, x.rank, x.cw, x.nch, stats, x.xi32 + x.table_off(),
-                             x.xi32 + x.q2_in_off()));
+                             nullptr));
     }
     mark(e, st, PSVO_TIME_INTERSECT, 1);
     const int max_steps = (int)ceil(kMaxHits * 1.7321 * 1.001 * (double)d->voxel_size / (double)d->step_size) +
@@ -888,18 +972,16 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         ENG_CALL(dist_sample(st, R, max_steps, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum, d->step_size, seed, stats,
                              x.xi32 + x.table_off(), x.nch, s_idx, s_depth, s_dist, ray_ns, offsets, nv_rank,
                              col0_rank));
-        // S_max of the union (every rank pads its [R_hit, S_max] blocks to it) and, given the
-        // step's GT depths, the loss normalisers' counts: ONE all-gather of 8 words
-        double *qsums = nullptr;
+        // S_max of the union (every rank pads its [R_hit, S_max] blocks to it)
+        // and, given the step's GT depths, the loss normalisers' counts: ONE
+        // all-gather of 8 words, in the query's second half (query_phase2)
         if (counts_gt) {
             Q_BUF(double, qs_, kDistSums, 8 * sizeof(double));
-            qsums = qs_;
+            (void)qs_;
         }
-        ENG_CALL(dist_counts(st, R, stats, rank_ray, counts_gt, s_depth, max_steps, ray_ns, d->truncation,
-                             d->max_depth, x.xi32 + x.q2_in_off()));
-        ENG_CALL(x.call(PSVO_XCH_GATHER_I32 | PSVO_XCH_QUERY, x.q2_in_off(), x.q2_all_off(), kDistWordsPerRank, st,
-                        "S_max + counts"));
-        ENG_CALL(dist_smax(st, x.xi32 + x.q2_all_off(), x.world, stats, x.xi32 + x.q2_in_off(), qsums));
+        q.p2_gt = counts_gt;
+        q.p2_tr = d->truncation;
+        q.p2_max_depth = d->max_depth;
     }
     q.seq = q.seq == 0x7fffffff ? 1 : q.seq + 1;
     q.counts_gt = x.on() ? counts_gt : nullptr;  // data parallel: the union's count sums in kDistSums
@@ -936,8 +1018,19 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
         q.compacted = leaf_q != nullptr;
     }
     mark(e, st, PSVO_TIME_SAMPLE, 1);
-    if (x.on()) ENG_CALL(psvo::stats_to_host(st, stats, q.host_raw, PSVO_STAT_WORDS, q.seq));
-    q.stats_zeroed = stats;
+    if (x.on()) {
+        // the first read-back (the shard's sizes and the union's R_hit / P /
+        // flags), the words kept for the second half, whose stream forks here
+        psvo::g_stop_event = q.p1;
+        const int rb = psvo::stats_to_host(st, stats, q.host_raw, PSVO_STAT_WORDS, q.seq, false);
+        const bool bound = psvo::g_stop_event == nullptr;
+        psvo::g_stop_event = nullptr;
+        ENG_CALL(rb);
+        if (!bound && hipEventRecord(q.p1, st) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "%s: event record failed", who);
+        q.p2_pending = true;
+    }
+    q.stats_zeroed = x.on() ? nullptr : stats;  // (data parallel: the second read-back zeroes them)
     q.done_recorded = record_done;
     if (record_done && hipEventRecord(q.done, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "%s: stats read-back failed", who);
@@ -1165,10 +1258,21 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     if (hs[PSVO_STAT_FLAGS] & 4) return set_error(PSVO_E_OVERFLOW, "%s: union batch exceeds max_rays_global", who);
     if (hs[PSVO_STAT_R_HIT] == 0)
         return set_error(PSVO_E_INVALID, "%s: no ray hits the octree (render_helpers.py:388)", who);
-    const int s_max = hs[PSVO_STAT_S_MAX];
     const int64_t M = hs[PSVO_STAT_M];
     if (hs[PSVO_STAT_FLAGS] & 2) return set_error(PSVO_E_OVERFLOW, "%s: sampler exceeded max_steps", who);
-    if (stats_out) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
+    // data parallel: the union S_max comes with the query's second half
+    // (query_phase2) — the mapping step waits for it only after queueing the
+    // interpolation and the sdf trunk, which do not need it; the padded
+    // paths (and an empty shard, which still joins the collectives) now
+    auto phase2 = [&]() -> int {
+        ENG_CALL(query_phase2(e, qset, who));
+        ENG_CALL(spin_wait(qset, qset.done2, e->q2s, who, 1));
+        return PSVO_OK;
+    };
+    const bool p2_late = dist && rays_path && r_hit > 0 && M > 0;
+    if (dist && !p2_late) ENG_CALL(phase2());
+    const int s_max = hs[PSVO_STAT_S_MAX];
+    if (stats_out && !p2_late) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
     o.r_hit = r_hit;
     o.m = M;
     o.s_max = s_max;
@@ -1286,6 +1390,11 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     o.rgb_s = rgb_s;
     o.act = act;
     o.masks = masks;
+    if (p2_late) {
+        ENG_CALL(phase2());
+        o.s_max = hs[PSVO_STAT_S_MAX];
+        if (stats_out) memcpy(stats_out, hs, PSVO_STAT_WORDS * sizeof(int));
+    }
     if (fused_loss) return PSVO_OK;  // compositing is part of psvo_composite_loss
     const size_t RS = (size_t)r_hit * s_max;
     ENG_BUF(float, sdf, kSdf, RS * sizeof(float));
@@ -1532,10 +1641,16 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
         }
         e->sel_tag = e->sel_tag == 0xffffffffu ? 1u : e->sel_tag + 1u;
         mark(e, st, PSVO_TIME_SELECT, 0);
-        ENG_CALL(psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns, q.z_vals,
-                                      q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf, q.tt, q.ray_of, M,
-                                      two_class, cx, offa, offb, feat_c, leaf_c, t_c, ray_of_c, rgb_c, src_c, cnt,
-                                      desc, e->sel_tag, e->host_flags));
+        if (!e->draw_gate && hipEventCreateWithFlags(&e->draw_gate, hipEventDisableSystemFence) != hipSuccess)
+            return set_error(PSVO_E_LAUNCH, "map_step: event creation failed");
+        psvo::g_stop_event = e->draw_gate;  // bound to the selection's dispatch (no marker)
+        const int sel_rc = psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns,
+                                                q.z_vals, q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf,
+                                                q.tt, q.ray_of, M, two_class, cx, offa, offb, feat_c, leaf_c, t_c,
+                                                ray_of_c, rgb_c, src_c, cnt, desc, e->sel_tag, e->host_flags);
+        e->draw_gate_recorded = e->draw_gate_recorded || psvo::g_stop_event == nullptr;  // (consumed: launched)
+        psvo::g_stop_event = nullptr;
+        ENG_CALL(sel_rc);
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));
         ENG_BUF(float, act, kAct, (size_t)psvo_mlp_act_floats(M, d->width) * sizeof(float));
@@ -1596,6 +1711,9 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
     if (dist) {
         if (sums_q) {
             sums_c = static_cast<double *>(qset->a.p[kDistSums]);
+            // (landed on the host before this launch; the wait orders it formally)
+            if (hipStreamWaitEvent(ax, qset->done2, 0) != hipSuccess)
+                return set_error(PSVO_E_LAUNCH, "map_step: stream wait failed");
         } else {
             ENG_CALL(criterion_counts(ax, empty ? 0 : r_hit, s_max, d->truncation, d->max_depth, q.rank_ray,
                                       gt_depth, q.z_vals, q.z_stride, q.z_stride == s_max ? nullptr : q.ray_ns,

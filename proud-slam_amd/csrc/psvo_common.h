@@ -44,6 +44,11 @@ struct KernelClock {
 // never attributed to it)
 extern thread_local KernelClock *g_kclock;
 
+// set by the engine around one launch: that launch's completion records this
+// event (bound to the dispatch, no marker packet), unless a kernel clock
+// needs the slot — then it is recorded right after the launch
+extern thread_local hipEvent_t g_stop_event;
+
 template <typename... KArgs, typename... A>
 inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A &&...a) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -67,7 +72,16 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hip
             c->overflow = true;
         }
     }
+    hipEvent_t late = nullptr;
+    if (g_stop_event) {
+        if (e1)
+            late = g_stop_event;
+        else
+            e1 = g_stop_event;
+        g_stop_event = nullptr;
+    }
     hipExtLaunchKernelGGL(k, grid, block, lds, st, e0, e1, 0u, static_cast<KArgs>(a)...);
+    if (late) (void)hipEventRecord(late, st);
 }
 
 // Set the thread-local error message; returns `code` for tail calls.
@@ -121,7 +135,9 @@ struct PackRec {  // 32 B, 16-B aligned
 // the query's statistics words → coherent pinned host memory as {seq, value}
 // granules (stat_to_host; zeroing them on the device): the engine's host
 // thread polls the tags instead of waiting for an event (svo_query.hip)
-int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq);
+// zero: clear the words read (the query set's next use needs no memset);
+// false for a first read-back that later kernels of the query still extend
+int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq, bool zero = true);
 // the same granules from the statistics' device copy, which stays as it is
 // The Criterion's normalisers (criterion.py:70-101: the valid-depth rays and
 // the front / sdf samples over the padded [R_hit, S_max] layout) depend only
@@ -222,8 +238,9 @@ constexpr int PSVO_FLAG_UNION_UNCOUNTED = 16;
 int dist_slot0_rows(int64_t max_rays_global);
 int dist_count_words(int max_rays_rank);
 int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
-              const int *ray_nv, int *out, const int *nv_rank = nullptr);
-// (q2_in: this rank's words of the second gather, whose count words it zeroes)
+              const int *ray_nv, int *out, const int *nv_rank = nullptr, int flags_or = 0);
+// (q2_in: this rank's words of the second gather, whose count words it
+// zeroes, or null: the caller zeroes them on the stream of dist_counts)
 int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table,
                 int *q2_in);
 int dist_sample(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, const int *rank_ray, const int *hit_idx,
@@ -234,7 +251,7 @@ int dist_smax(hipStream_t st, const int *all, int world, int *stats, int *in, do
 // this rank's words of the second gather: in[0] = S_max of its rows; given
 // the GT depths, in[1..7] += n_valid, Σ front / Σ sdf-band over the valid
 // samples, and per padding class (front, band: sample_terms of the MAX_DEPTH
-// fill) the rays and their Σ ns — in[1..7] zeroed by dist_layout (criterion.hip)
+// fill) the rays and their Σ ns — in[1..7] zeroed before (criterion.hip)
 int dist_counts(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const float *gt_depth,
                 const float *z_rows, int z_stride, const int *ray_ns, float truncation, float max_depth, int *in);
 

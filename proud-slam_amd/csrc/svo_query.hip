@@ -899,11 +899,11 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
 }
 
 // one wave, one word per lane (words <= 64)
-__global__ void k_stats_to_host(int *__restrict__ stats, unsigned long long *host, int words, int seq) {
+__global__ void k_stats_to_host(int *__restrict__ stats, unsigned long long *host, int words, int seq, int zero) {
     const int i = threadIdx.x;
     if (i < words) {
         const int v = stats[i];
-        stats[i] = 0;  // ready for the query set's next use (no memset launch)
+        if (zero) stats[i] = 0;  // ready for the query set's next use (no memset launch)
         stat_to_host(host, i, v, seq);
     }
 }
@@ -1515,19 +1515,12 @@ struct SmpLb {  // in LDS: nothing of it stays in registers across the help pass
 };
 __device__ int smp_lb_pass(bool own, int cur, int blk, int nb, const int *s_ns, const int *s_cw, const SampleTail &tl,
                            SmpLb &lb);
-__device__ __forceinline__ int sample_fused_ray_help(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
-                                                  int max_steps_cap, const int *rank_ray, const int *hit_idx,
-                                                  const float *hit_t0, const float *hit_t1, const float *ray_dsum,
-                                                  float step_size, const float *noise, uint64_t seed, int *stats,
-                                                  int *s_idx, float *s_depth, float *s_dist, const int *slot0,
-                                                  int slot0_nch, const int *nv_rank, const int *col0_rank,
-                                                  int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                  int blk);
 __device__ void smp_lb_finish(int n, const SmpLb &lb, int *__restrict__ stats, const SampleTail &tl, int *s_off,
                               int st_word, int max_steps_cap, int blk);
 
 // one ray of k_sample_fused; returns its valid-sample count, or -1 when the
 // wave has no ray (the launch covers r_hit_cap rows)
+template <bool HELP = false>
 __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                 int max_steps_cap, const int *__restrict__ rank_ray,
                                                 const int *__restrict__ hit_idx, const float *__restrict__ hit_t0,
@@ -1538,7 +1531,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 const int *__restrict__ slot0, int slot0_nch,
                                                 const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
                                                 int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                int *stage_i, float *stage_z, int blk);
+                                                int *stage_i, float *stage_z, int blk, int wrow = -1);
 
 __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                       int max_steps_cap,
@@ -1588,7 +1581,7 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
         }
         return;
     }
-    __shared__ int s_ns[kSmpWaves], s_cw[kSmpWaves], s_off[kSmpWaves], s_cmd;
+    __shared__ int s_ns[kSmpWaves], s_cw[kSmpWaves], s_off[kSmpWaves];
     if (lane == 0) {
         if (count >= 0) ray_ns[il] = count;
         s_ns[w] = count;  // -1: no row
@@ -1600,40 +1593,31 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     __syncthreads();
     SMP_T(2);
     __shared__ SmpLb lb;  // wave 0: the own block's aggregate / prefix
-    // one look-back call site; cmd ≥ 0: a predecessor that has not started,
-    // whose rows this workgroup samples first to publish their aggregate
-    // (lookback.h)
-    bool helped = false;
-    for (int cmd = -1;;) {
-        if (cmd >= 0) {
-            helped = true;
-            int hil = 0, hcw = 0;
-            const int hc = sample_fused_ray_help(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx,
-                                                 hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx,
-                                                 s_depth, s_dist, slot0, slot0_nch, nv_rank, col0_rank, hil,
-                                                 bins_all[w], tl, hcw, cmd);
-            if (lane == 0) {
-                if (hc >= 0) ray_ns[hil] = hc;
-                s_ns[w] = hc;
-                s_cw[w] = hcw;
+    if (w == 0) {
+        // a predecessor that has not started: wave 0 counts its rows (one
+        // per lane, the serial sampler) and publishes their aggregate, then
+        // resumes its own look-back (lookback.h)
+        __shared__ int s_hns[kSmpWaves], s_hcw[kSmpWaves];
+        int rc = smp_lb_pass(true, blk, blk, last_lb + 1, s_ns, s_cw, tl, lb);
+        while (rc >= 0) {
+            if (lane < kSmpWaves) {
+                int hil = 0, hcw = 0;
+                const int hc = sample_fused_ray<true>(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx,
+                                                      hit_t0, hit_t1, ray_dsum, step_size, noise, seed, stats, s_idx,
+                                                      s_depth, s_dist, slot0, slot0_nch, nv_rank, col0_rank, hil,
+                                                      bins_all[0], tl, hcw, nullptr, nullptr, rc, lane);
+                s_hns[lane] = hc;
+                s_hcw[lane] = hcw;
             }
-            __syncthreads();
+            rc = smp_lb_pass(false, rc, blk, last_lb + 1, s_hns, s_hcw, tl, lb);
         }
-        if (w == 0) {
-            const int rc = smp_lb_pass(cmd < 0, cmd < 0 ? blk : cmd, blk, last_lb + 1, s_ns, s_cw, tl, lb);
-            if (lane == 0) s_cmd = rc;
-        }
-        __syncthreads();
-        cmd = __builtin_amdgcn_readfirstlane(s_cmd);
-        if (cmd < 0) break;
     }
     const int own_count = count, own_il = il;
     if (w == 0) smp_lb_finish(n_lb, lb, stats, tl, s_off, st_word, max_steps_cap, blk);
     SMP_T(3);
     if (!compact) return;
-    // a row longer than the LDS stage (or any row, after helping: the stage
-    // then holds the helped rows) is re-read below: this wave's own stores first
-    if (own_count > kSmpStage || helped) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // a row longer than the LDS stage is re-read below: this wave's own stores first
+    if (own_count > kSmpStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // k_compact_rays' work: the row's valid prefix to its compacted place —
     // the first kSmpStage samples from LDS, the rest (rows longer than that)
@@ -1643,7 +1627,7 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     const int *oi = s_idx + (int64_t)own_il * max_steps_cap;
     const float *od = s_depth + (int64_t)own_il * max_steps_cap;
     for (int s = lane; s < own_count; s += kWave) {
-        const bool st = s < kSmpStage && !helped;
+        const bool st = s < kSmpStage;
         tl.leaf[off + s] = st ? stage_i[w][s] : ld_wt(oi + s);
         tl.t[off + s] = st ? stage_z[w][s] : ld_wt(od + s);
         tl.ray_of[off + s] = own_il;
@@ -1651,6 +1635,7 @@ __global__ __launch_bounds__(64 * kSmpWaves) void k_sample_fused(int64_t row_beg
     SMP_T(4);
 }
 
+template <bool HELP>
 __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
                                                 int max_steps_cap, const int *__restrict__ rank_ray,
                                                 const int *__restrict__ hit_idx, const float *__restrict__ hit_t0,
@@ -1661,7 +1646,7 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
                                                 const int *__restrict__ slot0, int slot0_nch,
                                                 const int *__restrict__ nv_rank, const int *__restrict__ col0_rank,
                                                 int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                int *stage_i, float *stage_z, int blk) {
+                                                int *stage_i, float *stage_z, int blk, int wrow) {
     // look-back mode: P / R_hit / max ⌈steps⌉ from the traversal's copy, which
     // no workgroup of this launch re-zeroes (a workgroup may start after the
     // last one zeroed the statistics: lookback.h helping)
@@ -1671,14 +1656,16 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     const int max_steps = qp[PSVO_STAT_MAX_CEIL] + P;
     // the engine's launches (row_begin 0, or a data-parallel rank's own rows
     // indexed locally): the ray's rank → ray read beside the statistics words
-    const int il_s = blk * (blockDim.x / kWave) + threadIdx.x / kWave;
+    // the block's row of this wave (HELP: of this lane, wrow)
+    if (wrow < 0) wrow = threadIdx.x / kWave;
+    const int il_s = blk * (blockDim.x / kWave) + wrow;
     const int orig_s = (nv_rank && il_s < r_hit_cap) ? rank_ray[il_s] : 0;
     if (slot0) {  // data-parallel engine: the rank's rows, local rank_ray / hit arrays
         row_begin = stats[PSVO_STAT_ROW_BEGIN];
         n_rows = stats[PSVO_STAT_R_HIT_LOCAL];
     }
     const int lane = threadIdx.x & (kWave - 1);
-    const int il = blk * (blockDim.x / kWave) + threadIdx.x / kWave;  // one ray per wave
+    const int il = blk * (blockDim.x / kWave) + wrow;  // one ray per wave (HELP: per lane)
     const int i = (int)row_begin + il;                                        // logical row
     il_out = il;
     const int64_t n_own = n_rows < 0 ? (int64_t)r_hit - row_begin : n_rows;
@@ -1734,13 +1721,33 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
     const float lo_t = gd - tl.c.tr, hi_t = gd + tl.c.tr;
     const bool dm = gd > 0.0f && gd < tl.c.max_depth;
     int nf = 0, nsm = 0;
+    auto noise_at = [&](int cs) {
+        if (nz) return nz[cs];
+        const float u = (float)(mix32(key + (uint64_t)cs) >> 8) * (1.0f / 16777216.0f);
+        return fminf(fmaxf(u, 0.001f), 0.999f);
+    };
+    if constexpr (HELP) {
+        // a helped row (lookback.h), one per lane: its count and count word
+        // only, by the serial loop the wave sampler restates bit for bit
+        // (sample_one) — small code; the row's owner writes it when it runs
+        sample_one(rows, steps_j, 0.0f, P, nr, jj * P, cap, noise_at, [&](int s, int v, float dep, float) {
+            if (s >= cap || v == -1) return;
+            ++count;
+            if (counting) {
+                const bool f = dep < lo_t;
+                nf += f;
+                nsm += !f && !(dep > hi_t) && dm;
+            }
+        });
+        if (counting) {
+            const bool pf = kMaxDepthFill < lo_t;
+            const bool psm = !pf && !(kMaxDepthFill > hi_t) && dm;
+            cnt_word = pack_counts(nf, nsm, pf, psm, gd > 0.01f && gd < tl.c.max_depth);
+        }
+        return count;
+    }
     const int s_end = sample_wave(
-        rows, steps_j, P, nr, jj * P,
-        [&](int cs) {
-            if (nz) return nz[cs];
-            const float u = (float)(mix32(key + (uint64_t)cs) >> 8) * (1.0f / 16777216.0f);
-            return fminf(fmaxf(u, 0.001f), 0.999f);
-        },
+        rows, steps_j, P, nr, jj * P, noise_at,
         [&](int s, int v, float dep, float dis) {
             if (s >= cap) return;
             if (nopad && v == -1) return;  // the implied padding
@@ -1772,20 +1779,6 @@ __device__ __forceinline__ int sample_fused_ray(int64_t row_begin, int64_t n_row
         cnt_word = pack_counts(wave_sum(nf), wave_sum(nsm), pf, psm, gd > 0.01f && gd < tl.c.max_depth);
     }
     return wave_sum(count);
-}
-
-// a helped block's rows (lookback.h), out of line: the own pass keeps its registers
-__device__ __forceinline__ int sample_fused_ray_help(int64_t row_begin, int64_t n_rows, int64_t r_hit_cap,
-                                                  int max_steps_cap, const int *rank_ray, const int *hit_idx,
-                                                  const float *hit_t0, const float *hit_t1, const float *ray_dsum,
-                                                  float step_size, const float *noise, uint64_t seed, int *stats,
-                                                  int *s_idx, float *s_depth, float *s_dist, const int *slot0,
-                                                  int slot0_nch, const int *nv_rank, const int *col0_rank,
-                                                  int &il_out, WaveBins &W, const SampleTail &tl, int &cnt_word,
-                                                  int blk) {
-    return sample_fused_ray(row_begin, n_rows, r_hit_cap, max_steps_cap, rank_ray, hit_idx, hit_t0, hit_t1, ray_dsum,
-                            step_size, noise, seed, stats, s_idx, s_depth, s_dist, slot0, slot0_nch, nv_rank,
-                            col0_rank, il_out, W, tl, cnt_word, nullptr, nullptr, blk);
 }
 
 // k_scan_samples' work for one sampler workgroup (its 8 rows), wave 0 only,
@@ -1886,7 +1879,9 @@ __device__ void smp_lb_finish(int n, const SmpLb &lb, int *__restrict__ stats, c
                               tl.c.w_depth, tl.c.w_fs, tl.c.w_sdf, tl.c.tr, tl.c.crit_flags, tl.c.coef);
     }
     // the sampler's own flag (sample_fused_ray: max_steps beyond the rows' capacity)
-    const int max_steps = stats[kStatQuery + PSVO_STAT_MAX_CEIL] + stats[kStatQuery + PSVO_STAT_P];
+    // (st_word: the last workgroup's load at its start — only it re-zeroes
+    // the statistics, so its words are the traversal's; no dependent load here)
+    const int max_steps = __shfl(st_word, PSVO_STAT_MAX_CEIL, kWave) + __shfl(st_word, PSVO_STAT_P, kWave);
     if (lane < PSVO_STAT_WORDS) {
         int v = lane == PSVO_STAT_S_MAX ? smax : lane == PSVO_STAT_M ? tot : st_word;
         if (lane == PSVO_STAT_FLAGS && n > 0 && max_steps > max_steps_cap) v |= 2;
@@ -2133,7 +2128,8 @@ constexpr int kDistWords = 8;  // per rank: R_hit, P, max ceil, first voxel id o
 // this rank's words: thread t packs the hit counts of its hit rows 4t..4t+3
 __global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats, const int *__restrict__ rank_ray,
                                                    const int *__restrict__ hit_idx, const int *__restrict__ ray_nv,
-                                                   int *__restrict__ out, const int *__restrict__ nv_rank) {
+                                                   int *__restrict__ out, const int *__restrict__ nv_rank,
+                                                   int flags_or) {
     const int r_hit = stats[PSVO_STAT_R_HIT];
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
@@ -2141,7 +2137,9 @@ __global__ __launch_bounds__(256) void k_dist_pack(const int *__restrict__ stats
         out[1] = stats[PSVO_STAT_P];
         out[2] = stats[PSVO_STAT_MAX_CEIL];
         out[3] = r_hit > 0 ? hit_idx[(int64_t)rank_ray[0] * kMaxHits] : -1;
-        out[4] = stats[PSVO_STAT_FLAGS];  // e.g. a DFS-stack overflow on one rank: every rank fails together
+        // e.g. a DFS-stack overflow on one rank: every rank fails together; and
+        // PSVO_FLAG_UNION_UNCOUNTED from a rank whose query had no GT depths
+        out[4] = stats[PSVO_STAT_FLAGS] | flags_or;
         for (int k = 5; k < kDistWords; ++k) out[k] = 0;
     }
     const int j0 = 4 * t;
@@ -2353,8 +2351,8 @@ int sample_rays_to_host(hipStream_t st, int64_t r_hit_cap, int max_steps_cap, co
     return check_launch("sample_rays_to_host");
 }
 
-int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq) {
-    psvo::launch(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq);
+int stats_to_host(hipStream_t st, int *stats, unsigned long long *host, int words, int seq, bool zero) {
+    psvo::launch(k_stats_to_host, dim3(1), dim3(64), 0, st, stats, host, words, seq, zero ? 1 : 0);
     return check_launch("stats_to_host");
 }
 
@@ -2397,9 +2395,9 @@ int dist_slot0_rows(int64_t max_rays_global) {
 }
 int dist_count_words(int max_rays_rank) { return kDistWords + (max_rays_rank + 3) / 4; }
 int dist_pack(hipStream_t st, int64_t R, const int *stats, const int *rank_ray, const int *hit_idx,
-              const int *ray_nv, int *out, const int *nv_rank) {
+              const int *ray_nv, int *out, const int *nv_rank, int flags_or) {
     psvo::launch(k_dist_pack, dim3((int)div_up(div_up(R, 4), 256) + (R == 0)), dim3(256), 0, st, stats, rank_ray,
-                 hit_idx, ray_nv, out, nv_rank);
+                 hit_idx, ray_nv, out, nv_rank, flags_or);
     return check_launch("dist_pack");
 }
 int dist_layout(hipStream_t st, const int *all, int world, int rank, int stride, int nch, int *stats, int *table,

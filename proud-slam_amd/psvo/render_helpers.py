@@ -20,6 +20,7 @@ octree 256× per intersection; this path syncs twice and copies nothing.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from copy import deepcopy
 
@@ -653,10 +654,20 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     if cur_ready is not None:
         main.wait_event(cur_ready)
     clk("poses")
+    # PSVO_BA_DRAW_GATE=1 (measured switch): draws run two iterations ahead,
+    # each queued after its step's sample selection (psvo_engine_gate_stream),
+    # so their passes overlap the decoder instead of the selection's look-back
+    gate = ahead and batched and os.environ.get("PSVO_BA_DRAW_GATE") == "1"
+    pending = None
+    if gate and num_iterations > 1:
+        pending = draw_ahead(1)
     for it in range(num_iterations):
         # the engine orders the look-ahead's pose step (reads nxt's dirs) after
         # the draw queued on `side` (next_stream), and with it the next step
-        nxt, _ = draw_ahead(it + 1) if ahead and it + 1 < num_iterations else (None, None)
+        if gate:
+            nxt, _ = pending if pending is not None else (None, None)
+        else:
+            nxt, _ = draw_ahead(it + 1) if ahead and it + 1 < num_iterations else (None, None)
         d_all, c_all, z_all, nz, seed = cur
         adam_step += 1
         cur_steps = [pstep[f] + 1 if upd[f] else 0 for f in range(len(kfs))]
@@ -672,6 +683,11 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
         if after_step and side is not None:
             step_done[0] = step_done[0] or torch.cuda.Event()
             step_done[0].record(main)
+        if gate:  # the draw two ahead, behind this step's selection (the ring of 4 stays safe: see above)
+            pending = None
+            if it + 2 < num_iterations:
+                L.call("psvo_engine_gate_stream", eng.handle, ctypes.c_void_p(side.cuda_stream))
+                pending = draw_ahead(it + 2)
         cur = nxt if nxt is not None else (draw(it + 1) if it + 1 < num_iterations else None)
         if it < 2 or it == num_iterations - 1:
             clk(f"step{it}")

@@ -84,8 +84,15 @@ def ba_loop(tree, emb0, scene, dev, exchange=None):
     eo = torch.optim.Adam([emb], lr=5e-3)
     mo = torch.optim.Adam(dec.parameters(), lr=5e-3)
     eng = MappingEngine(ms, dec, 0.2, STEP, truncation=0.1, max_distance=10.0, criteria=CRIT, max_depth=10.0)
+    calls = []  # (op, count, stream) of every collective the engine issued
     if exchange is not None:
         eng.set_exchange(exchange)
+        apply = exchange.apply
+
+        def logged(op, in_off, out_off, count, stream=None):
+            calls.append((int(op), int(count), int(stream or 0)))
+            return apply(op, in_off, out_off, count, stream)
+        exchange.apply = logged
     losses = []
     eng.ba_loss = True  # bundle_adjust_frames' steps return their loss (recorded below)
     eng.stats_hook = None
@@ -101,7 +108,7 @@ def ba_loop(tree, emb0, scene, dev, exchange=None):
     torch.cuda.synchronize()
     out = {"loss": losses, "emb": emb.detach().cpu(),
            "dec": [p.detach().cpu() for p in dec.parameters()],
-           "poses": [kf.pose.data.detach().cpu() for kf in kfs]}
+           "poses": [kf.pose.data.detach().cpu() for kf in kfs], "calls": calls}
     eng.close()
     return out
 

@@ -68,3 +68,13 @@ def test_engine_protocol_over_rccl(tmp_path):
             torch.testing.assert_close(x, y, rtol=0, atol=1e-5)
         for x, y in zip(got["dec"], bref["dec"]):
             adam_close(x.numpy(), y.numpy(), tight=1e-4, frac=0.99, max_abs=2.0 * 5e-3 * 3)
+        # the query's second gather ([S_max, counts]: 8 words) runs on the
+        # engine's own stream, off the stream of the first gather and the
+        # interpolation, once per step, after that step's first
+        calls = got["calls"]
+        first = [c for c in calls if c[0] == 0x101 and c[1] > 8]
+        second = [c for c in calls if c[0] == 0x101 and c[1] == 8]
+        assert len(second) == len(bref["loss"]) and len(first) in (len(second), len(second) + 1), calls
+        assert not {c[2] for c in second} & {c[2] for c in first}, calls
+        seq = [c[1] > 8 for c in calls if c[0] == 0x101]
+        assert seq[:2 * len(second)] == [True, False] * len(second) and all(seq[2 * len(second):]), seq
