@@ -579,6 +579,11 @@ int psvo_debug_set_lookback(int mask, int spin_bound, int delay_us);
 /* Tests only: look-back blocks helped so far ([0] traversal, [1] sampler,
  * [2] sample selection); reset != 0 zeroes them.  Synchronises the device. */
 int psvo_debug_lb_helps(int64_t *out3, int reset);
+/* Tests only: psvo_sample_pixels' draw for uniform weights and generated
+ * uniforms — 0: the candidate-band draw where it applies (the default), 1:
+ * always the radix passes, 2: the band forced to miss (its exact fallback).
+ * The three give the same picks.  Process-wide. */
+int psvo_debug_set_pixel_draw(int mode);
 
 /* Optional HIP-event timing of the roofline regions (on the launch stream). */
 enum { PSVO_TIME_MLP_FWD = 0, PSVO_TIME_MLP_BWD = 1, PSVO_TIME_INTERP_FWD = 2, PSVO_TIME_INTERP_BWD = 3,

@@ -25,6 +25,25 @@
 //                  gathered rows
 // HBM traffic per pixel: the key written once and read 4 times (20 B), the
 // mask (1 B, optional), the weights (4 B, optional); plus the N gathered rows.
+//
+// The keyframe sampler's case (uniform weights, generated uniforms: the
+// 24-bit integer behind u orders the scores, px_key_at FAST) draws k of
+// n_pix ≫ k, so its k-th largest key lies near 2²⁴(1 − k/n_pix).  The
+// candidate-band draw (round 6) needs one pass over the pixels, not five:
+//   k_px_cand  every pixel's key from the counter hash (no memory read);
+//              keys ≥ t0 — a band holding k + 8√k + 64 pixels on average —
+//              in pixel order into a per-block segment of kPxSeg slots;
+//              the mask zeroed
+//   k_px_pick  one short 256-thread workgroup per frame: the segments into
+//              registers (pixel order), the k-th largest key T among them by
+//              two LDS histograms over the band, then the same pick rule as
+//              k_px_write over the candidates only: idx, mask ones, the
+//              gathered rows.
+// Every key ≥ T is a candidate when the band holds ≥ k pixels, so the picks
+// are k_px_write's, bit for bit.  A band that missed (fewer than k pixels
+// in it: ≈ 8σ below the mean, p < 1e-15; or a full segment) is detected in
+// k_px_pick, which then picks over every pixel of the frame itself (slow,
+// exact: tests force it with psvo_debug_set_pixel_draw).
 #include <hip/hip_runtime.h>
 
 #include <stdlib.h>
@@ -40,6 +59,9 @@ constexpr int kPxRound = kPxPer * kPxThreads;   // pixels per block per round
 constexpr int kPxMaxBlocks = 256;               // blocks per frame
 constexpr int kPxBins = 4096;    // 12-bit digits (the last pass: 8 bits)
 constexpr int kPxMaxFrames = 32;
+constexpr int kPxSeg = 64;            // candidate slots per k_px_cand block (≈ 7 used at the bench's draw)
+constexpr int kPxPickRegs = 8;                         // k_px_pick (256 threads per frame): candidates per thread
+constexpr int kPxCandMax = kPxThreads * kPxPickRegs;    // candidates k_px_pick holds in registers
 
 struct PxFrames {
     psvo_pixel_frame f[kPxMaxFrames];
@@ -58,6 +80,9 @@ struct PxArgs {
     int *counts;                 // [F][kPxMaxBlocks][2]: keys > T, keys = T
     double *wsum;                // [F][kPxMaxBlocks] partial weight sums
     uint32_t *keys;              // [F][n_pix] orderable score keys (written by pass 0)
+    uint32_t t0;                 // candidate-band draw: the band's lowest key
+    int *cand;                   // [F][kPxMaxBlocks][kPxSeg] candidate pixels, per block in pixel order
+    int *ccount;                 // [F][kPxMaxBlocks] candidates per block (> kPxSeg: the segment overflowed)
 };
 
 __device__ __forceinline__ uint32_t px_mix32(uint64_t x) {
@@ -385,15 +410,279 @@ __global__ __launch_bounds__(kPxThreads) void k_px_write(PxArgs a, PxFrames fr, 
     }
 }
 
+// exclusive block scan of one int per thread (any block size ≤ 1024, whole
+// waves); returns the prefix, *tot = the block's sum; sh: ≥ 16 ints
+__device__ __forceinline__ int px_block_scan(int v, int *sh, int *tot) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += x;
+    }
+    if (lane == 63) sh[wave] = inc;
+    __syncthreads();
+    int before = inc - v, t = 0;
+    for (int w = 0; w < nw; ++w) {
+        before += w < wave ? sh[w] : 0;
+        t += sh[w];
+    }
+    __syncthreads();
+    *tot = t;
+    return before;
+}
+
+// the FAST key (the 24-bit integer behind the pixel's uniform)
+__device__ __forceinline__ uint32_t px_hash(const PxArgs &a, int f, int64_t i) {
+    return px_key_at<true, false>(a, f, i, 0.0f);
+}
+
+// k_px_cand: the band's pixels of block b of frame f, in pixel order; the mask zeroed
+__global__ __launch_bounds__(kPxThreads) void k_px_cand(PxArgs a, PxFrames fr) {
+    __shared__ int sh[kPxThreads / kWave];
+    const int f = blockIdx.y, b = blockIdx.x;
+    const int64_t i0 = (int64_t)b * a.chunk, i1 = min(a.n_pix, i0 + a.chunk);
+    uint8_t *const mask = fr.f[f].mask;
+    int *const seg = a.cand + ((int64_t)f * kPxMaxBlocks + b) * kPxSeg;
+    int n = 0;  // candidates of the rounds before (uniform over the block)
+    for (int64_t rr = i0; rr < i1; rr += kPxRound) {
+        const int64_t r0 = rr + kPxPer * threadIdx.x;
+        int flags = 0, c = 0;
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q) {
+            if (r0 + q < i1 && px_hash(a, f, r0 + q) >= a.t0) {
+                flags |= 1 << q;
+                ++c;
+            }
+        }
+        if (mask && r0 < i1) {
+            uint8_t *m = mask + r0;
+            if (r0 + kPxPer <= i1 && ((uintptr_t)m & 3) == 0) {
+                *reinterpret_cast<uint32_t *>(m) = 0u;
+            } else {
+                for (int q = 0; q < kPxPer && r0 + q < i1; ++q) m[q] = 0;
+            }
+        }
+        int tot;
+        int pos = n + px_block_scan(c, sh, &tot);
+#pragma unroll
+        for (int q = 0; q < kPxPer; ++q)
+            if ((flags >> q) & 1) {
+                if (pos < kPxSeg) seg[pos] = (int)(r0 + q);
+                ++pos;
+            }
+        n += tot;
+    }
+    if (threadIdx.x == 0) a.ccount[f * kPxMaxBlocks + b] = n;
+}
+
+// block sum (every thread gets it); sh: ≥ 16 ints
+__device__ __forceinline__ int px_block_sum(int v, int *sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sh[w];
+    __syncthreads();
+    return t;
+}
+
+// the k-th largest of n keys key_at(e): the largest T with #{key ≥ T} ≥ k
+template <typename KeyAt>
+__device__ uint32_t px_kth(int64_t n, int64_t k, KeyAt key_at, int *sh) {
+    uint32_t T = 0;
+    for (int bit = 23; bit >= 0; --bit) {
+        const uint32_t c = T | (1u << bit);
+        int cnt = 0;
+        for (int64_t e = threadIdx.x; e < n; e += blockDim.x) cnt += key_at(e) >= c;
+        if (px_block_sum(cnt, sh) >= k) T = c;
+    }
+    return T;
+}
+
+// pick pixel i into output row `row`: idx, the mask's one, the gathered rows
+__device__ __forceinline__ void px_emit(const PxArgs &a, const psvo_pixel_frame &F, int64_t row, int64_t i,
+                                        int64_t *__restrict__ idx, float *__restrict__ out_dirs,
+                                        float *__restrict__ out_rgb, float *__restrict__ out_depth) {
+    if (idx) idx[row] = i;
+    if (out_dirs && F.dirs)
+        for (int c = 0; c < 3; ++c) out_dirs[row * 3 + c] = F.dirs[i * 3 + c];
+    if (out_rgb && F.rgb)
+        for (int c = 0; c < 3; ++c) out_rgb[row * 3 + c] = F.rgb[i * 3 + c];
+    if (out_depth && F.depth) out_depth[row] = F.depth[i];
+    if (F.mask) F.mask[i] = 1;
+}
+
+// the picks among n elements in pixel order (element e: key key_at(e), pixel
+// pix_at(e)): key > T, or key = T and fewer than `ties` keys = T before it —
+// k_px_write's rule; idx, mask ones, gathered rows
+template <typename KeyAt, typename PixAt>
+__device__ void px_pick_pass(const PxArgs &a, const psvo_pixel_frame &F, int f, int64_t n, uint32_t T, int ties,
+                             KeyAt key_at, PixAt pix_at, int *sh, int64_t *__restrict__ idx,
+                             float *__restrict__ out_dirs, float *__restrict__ out_rgb,
+                             float *__restrict__ out_depth) {
+    int gt_run = 0, eq_run = 0;
+    for (int64_t base = 0; base < n; base += blockDim.x) {
+        const int64_t e = base + threadIdx.x;
+        uint32_t key = 0;
+        int64_t i = 0;
+        if (e < n) {
+            key = key_at(e);
+            i = pix_at(e);
+        }
+        const bool in = e < n, is_gt = in && key > T, is_eq = in && key == T;
+        int tot;
+        const int before = px_block_scan((is_gt ? 1 : 0) + (is_eq ? (1 << 16) : 0), sh, &tot);
+        const int gt_b = gt_run + (before & 0xffff), eq_b = eq_run + (before >> 16);
+        if (is_gt || (is_eq && eq_b < ties))
+            px_emit(a, F, (int64_t)f * a.k + gt_b + min(eq_b, ties), i, idx, out_dirs, out_rgb, out_depth);
+        gt_run += tot & 0xffff;
+        eq_run += tot >> 16;
+    }
+}
+
+// The bin of a histogram of 256 · BPT bins (thread t owns [BPT·t, BPT·t +
+// BPT), highest bin first) holding the rem-th largest key: bin → res[0],
+// keys still needed inside it → res[1] (every thread reads them after).
+template <int BPT>
+__device__ void px_select_fast(const int *h, int rem, int *sh, int *res) {
+    const int t = threadIdx.x;
+    int v[BPT];
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+        v[j] = h[t * BPT + j];
+        s += v[j];
+    }
+    int tot;
+    const int before = px_block_scan(s, sh, &tot);
+    const int above = tot - before - s;  // keys in the bins of threads t+1..
+    if (above < rem && rem <= above + s) {
+        int acc = above;
+        for (int j = BPT - 1; j >= 0; --j) {
+            if (acc + v[j] >= rem) {
+                res[0] = t * BPT + j;
+                res[1] = rem - acc;
+                break;
+            }
+            acc += v[j];
+        }
+    }
+    __syncthreads();
+}
+
+// One short workgroup of 256 threads per frame (a long-lived one holds a CU
+// slot a persistent decoder workgroup then waits for — measured: a one-wave
+// pick of ≈ 40 µs cost ≈ 80 µs per step): the band's candidates into
+// registers — element e = 256·r + t, pixel order — the k-th largest key T by
+// two LDS histograms over the band (≤ 1,024 bins each: the band is at most
+// 2¹⁸ keys wide, t0's eligibility), then k_px_write's pick rule in element
+// order.  A band that missed: the same rule over every pixel (slow, exact).
+__global__ __launch_bounds__(kPxThreads) void k_px_pick(PxArgs a, PxFrames fr, int64_t *__restrict__ idx,
+                                                        float *__restrict__ out_dirs, float *__restrict__ out_rgb,
+                                                        float *__restrict__ out_depth) {
+    __shared__ int s_off[kPxMaxBlocks];
+    __shared__ int s_hist[1024];
+    __shared__ int sh[kPxThreads / kWave];
+    __shared__ int s_res[2];
+    const int f = blockIdx.x, t = threadIdx.x;
+    const psvo_pixel_frame F = fr.f[f];
+    // the segments' offsets in pixel order (nb ≤ 256 = the block)
+    const int cnt = t < a.nb ? a.ccount[f * kPxMaxBlocks + t] : 0;
+    int n_cand;
+    const int off = px_block_scan(min(cnt, kPxSeg), sh, &n_cand);
+    const bool full = __syncthreads_or(cnt > kPxSeg) != 0;
+    if (t < a.nb) s_off[t] = off;
+    for (int j = t; j < 1024; j += kPxThreads) s_hist[j] = 0;
+    __syncthreads();
+    if (!full && n_cand >= a.k && n_cand <= kPxCandMax) {
+        uint32_t h[kPxPickRegs];
+        int px[kPxPickRegs];
+        // the band's width → the first histogram's shift (≤ 1,024 bins)
+        const uint32_t width = 0x1000000u - a.t0;
+        int s1 = 0;
+        while ((width - 1) >> s1 >= 1024u) ++s1;
+#pragma unroll
+        for (int r = 0; r < kPxPickRegs; ++r) {
+            const int e = r * kPxThreads + t;
+            h[r] = 0;
+            px[r] = 0;
+            if (e < n_cand) {
+                // the segment holding e: the last b with s_off[b] ≤ e (a run
+                // of empty segments shares its successor's offset)
+                int lo = 0, hi = a.nb - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_off[mid] <= e) lo = mid;
+                    else hi = mid - 1;
+                }
+                px[r] = a.cand[((int64_t)f * kPxMaxBlocks + lo) * kPxSeg + (e - s_off[lo])];
+                h[r] = px_hash(a, f, px[r]);
+                atomicAdd(&s_hist[(h[r] - a.t0) >> s1], 1);
+            }
+        }
+        __syncthreads();
+        px_select_fast<4>(s_hist, (int)a.k, sh, s_res);
+        const uint32_t b1 = (uint32_t)s_res[0];
+        const int rem1 = s_res[1];
+        for (int j = t; j < 1024; j += kPxThreads) s_hist[j] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kPxPickRegs; ++r)
+            if (r * kPxThreads + t < n_cand && ((h[r] - a.t0) >> s1) == b1)
+                atomicAdd(&s_hist[(h[r] - a.t0) & ((1u << s1) - 1u)], 1);
+        __syncthreads();
+        px_select_fast<4>(s_hist, rem1, sh, s_res);
+        const uint32_t T = a.t0 + ((b1 << s1) | (uint32_t)s_res[0]);
+        const int ties = s_res[1];  // keys = T to take, in pixel order
+        int gt_run = 0, eq_run = 0;
+#pragma unroll
+        for (int r = 0; r < kPxPickRegs; ++r) {
+            if (r * kPxThreads < n_cand) {  // (block-uniform)
+                const bool in = r * kPxThreads + t < n_cand;
+                const bool is_gt = in && h[r] > T, is_eq = in && h[r] == T;
+                int tot;
+                const int before = px_block_scan((is_gt ? 1 : 0) + (is_eq ? (1 << 16) : 0), sh, &tot);
+                const int gt_b = gt_run + (before & 0xffff), eq_b = eq_run + (before >> 16);
+                if (is_gt || (is_eq && eq_b < ties))
+                    px_emit(a, F, (int64_t)f * a.k + gt_b + min(eq_b, ties), px[r], idx, out_dirs, out_rgb,
+                            out_depth);
+                gt_run += tot & 0xffff;
+                eq_run += tot >> 16;
+            }
+        }
+        return;
+    }
+    // the band missed: every pixel of the frame (exact, slow — p < 1e-15 at
+    // the bench's draw; forced in tests)
+    auto key_at = [&](int64_t e) { return px_hash(a, f, e); };
+    const uint32_t T = px_kth(a.n_pix, a.k, key_at, sh);
+    int gt = 0;
+    for (int64_t e = t; e < a.n_pix; e += kPxThreads) gt += key_at(e) > T;
+    gt = px_block_sum(gt, sh);
+    px_pick_pass(a, F, f, a.n_pix, T, (int)a.k - gt, key_at, [](int64_t e) { return e; }, sh, idx, out_dirs,
+                 out_rgb, out_depth);
+}
+
 }  // namespace
 }  // namespace psvo
 
 using namespace psvo;
 
+// tests only: 0 = the candidate-band draw where it applies, 1 = always the
+// radix passes, 2 = the band forced to miss (k_px_pick's fallback);
+// PSVO_PX_RADIX=1 starts at 1 (a measured switch: bench A/B)
+static int g_px_draw_mode = getenv("PSVO_PX_RADIX") && *getenv("PSVO_PX_RADIX") == '1' ? 1 : 0;
+extern "C" int psvo_debug_set_pixel_draw(int mode) {
+    PSVO_REQUIRE(mode >= 0 && mode <= 2, "debug_set_pixel_draw: mode %d (0..2)", mode);
+    g_px_draw_mode = mode;
+    return PSVO_OK;
+}
+
 extern "C" int64_t psvo_sample_pixels_workspace_ints(int n_frames, int64_t n_pix) {
     return (int64_t)3 * n_frames * kPxBins + (int64_t)n_frames * 6 +
            (int64_t)n_frames * kPxMaxBlocks * 2 +
-           (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */ + (int64_t)n_frames * n_pix;
+           (int64_t)n_frames * kPxMaxBlocks * 2 /* doubles */ + 2 /* alignment */ + (int64_t)n_frames * n_pix +
+           (int64_t)n_frames * kPxMaxBlocks * (kPxSeg + 1) /* candidate segments + counts */;
 }
 
 extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int64_t k, const float *weights,
@@ -415,6 +704,7 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     a.weights = weights;
     a.u = u;
     a.seed = seed;
+    a.t0 = 0;
     a.joint_sum = joint_sum ? 1 : 0;
     a.n_frames = n_frames;
     a.hist = workspace;
@@ -424,13 +714,29 @@ extern "C" int psvo_sample_pixels(void *stream, int n_frames, int64_t n_pix, int
     wp += ((uintptr_t)wp & 7) ? 1 : 0;
     a.wsum = reinterpret_cast<double *>(wp);
     a.keys = reinterpret_cast<uint32_t *>(a.wsum + (int64_t)n_frames * kPxMaxBlocks);
+    a.cand = reinterpret_cast<int *>(a.keys + (int64_t)n_frames * n_pix);
+    a.ccount = a.cand + (int64_t)n_frames * kPxMaxBlocks * kPxSeg;
     PxFrames fr = {};
     if (frames)
         for (int f = 0; f < n_frames; ++f) fr.f[f] = frames[f];
     hipStream_t st = as_stream(stream);
+    const dim3 grid(a.nb, n_frames);
+    if (!weights && !u && g_px_draw_mode != 1) {
+        // the candidate band: k + 8√k + 64 pixels expected, ≤ 16 per block on
+        // average (kPxSeg = 64 slots), ≤ 3/4 of kPxCandMax in all
+        const double m = (double)k + 8.0 * sqrt((double)k) + 64.0;
+        const double per_block = m * (double)a.chunk / (double)n_pix;
+        const double t0 = 16777216.0 - ceil(m * 16777216.0 / (double)n_pix);
+        if (t0 >= 1.0 && per_block <= 16.0 && m <= 0.75 * kPxCandMax) {
+            a.t0 = g_px_draw_mode == 2 ? 0xffffffu : (uint32_t)t0;
+            psvo::launch(k_px_cand, grid, dim3(kPxThreads), 0, st, a, fr);
+            psvo::launch(k_px_pick, dim3(n_frames), dim3(kPxThreads), 0, st, a, fr, idx, out_dirs, out_rgb,
+                         out_depth);
+            return check_launch("sample_pixels");
+        }
+    }
     if (hipMemsetAsync(workspace, 0, sizeof(int) * (3 * n_frames * kPxBins), st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "sample_pixels: memset failed");
-    const dim3 grid(a.nb, n_frames);
     if (weights) psvo::launch(k_px_wsum, grid, dim3(kPxThreads), 0, st, a);
     if (!weights && !u) {  // uniform weights, generated uniforms: 24-bit integer keys
         static const bool small = getenv("PSVO_PX_SMALL_LDS") && *getenv("PSVO_PX_SMALL_LDS") == '1';

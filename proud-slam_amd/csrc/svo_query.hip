@@ -485,102 +485,11 @@ __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float 
             sp = 1;
         }
         wave_lds_sync();
-        while (sp > 0) {  // wave-uniform trip count
-            ++rounds;
-            IS_MARK(is_ta);
-            const int n = min(sp, kWave);
-            uint64_t key = 0;
-            int node = 0, dep = 0;
-            if (lane < n) {
-                const int e = sp - 1 - lane;
-                key = S.skey[e];
-                node = S.snode[e];
-                dep = S.sdep[e];
-            }
-            // popped keys ascend with the lane: the live lanes are a prefix
-            const bool live = lane < n && !(bounded && key > kbound);
-            const int n_eff = __popcll(__ballot(live));
-            int row[8];
-            int side = 0, first = 0, cmask = 0, ref = node;
-            float a = 0.f, b = 0.f;
-            bool hit = false;
-            if (live) {
-                if constexpr (PACKED) {
-                    const float4 pc = packed[node].c;
-                    const int4 pi = packed[node].i;
-                    side = __float_as_int(pc.w);
-                    ref = pi.x;
-                    first = pi.y;
-                    cmask = pi.z;
-                    hit = ray_aabb_nb(o, inv, pc.x, pc.y, pc.z, half * (float)side, a, b);
-                } else {
-                    const int *rw = structure + (int64_t)node * 9;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) row[u] = rw[u];
-                    side = rw[8];
-                    const float *pc = centres + (int64_t)node * 3;
-                    hit = ray_aabb_nb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
-                }
-            }
-            IS_MARK(is_tb);
-            IS_ADD(1, is_ta, is_tb);
-            const bool leaf = hit && side == 1;
-            const bool inner = hit && side != 1;
-            if (__ballot(inner && dep >= kLevels)) {  // deeper than the reference's stack
-                spill = true;
-                break;
-            }
-            int c = 0;
-            if (inner) {
-                if constexpr (PACKED) {
-                    c = __popc(cmask);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) c += row[u] > -1;
-                }
-            }
-            const int incl = wave_incl_scan16(c);
-            // a prune drops everything below the popped chunk (all keys > kbound)
-            const int floor_ = (n_eff < n) ? 0 : sp - n;
-            const bool ok = !live || floor_ + (n_eff - 1 - lane) + incl <= kStk;
-            const uint64_t bad = __ballot(!ok);
-            const int J = bad ? (int)__ffsll((unsigned long long)bad) - 1 : n_eff;  // accepted lanes [0, J)
-            if (J == 0 && n_eff > 0) {
-                spill = true;
-                break;
-            }
-            const int T = J > 0 ? __builtin_amdgcn_readlane(incl, J - 1) : 0;
-            const bool acc = lane < J;
-            wave_lds_sync();  // every lane has read its candidate before the stack is rewritten
-            if (live && !acc) {  // re-queued tail keeps its order on top of the floor
-                const int pos = floor_ + (n_eff - 1 - lane);
-                S.skey[pos] = key;
-                S.snode[pos] = node;
-                S.sdep[pos] = (uint8_t)dep;
-            }
-            const int base = floor_ + (n_eff - J);
-            if (acc && inner) {
-                int g = incl - c;  // rank of this lane's first (smallest-key) child
-                const int cd = dep + 1;
-#pragma unroll
-                for (int u = 7; u >= 0; --u) {
-                    const bool present = PACKED ? ((cmask >> u) & 1) != 0 : row[u] > -1;
-                    if (present) {
-                        const int pos = base + (T - 1 - g);
-                        S.skey[pos] = key | key_digit(u, cd);
-                        S.snode[pos] = PACKED ? first + __popc(cmask & ((1 << u) - 1)) : row[u];
-                        S.sdep[pos] = (uint8_t)cd;
-                        ++g;
-                    }
-                }
-            }
-            IS_MARK(is_ta);
-            IS_ADD(2, is_tb, is_ta);
-            visits += acc ? 1 : 0;
-            sp = base + T;
-            const bool fresh = acc && leaf;
+        // merge one group's fresh leaves (keys ascending with the lane) into
+        // the key-sorted list
+        auto merge_leaves = [&](bool fresh, uint64_t key, int ref, float a, float b) {
             const uint64_t lb = __ballot(fresh);
-            if (lb) {  // merge this round's leaves (keys ascend with the lane) into the key-sorted list
+            if (lb) {
                 const int m = __popcll(lb), q = __popcll(lb & below);
                 if (fresh) S.lkey[kWave + q] = key;  // scratch past the list (nl <= 50)
                 const bool hold = lane < nl;
@@ -622,6 +531,182 @@ __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float 
             } else {
                 wave_lds_sync();
             }
+        };
+        while (sp > 0) {  // wave-uniform trip count
+            ++rounds;
+            IS_MARK(is_ta);
+            const int n = min(sp, kWave);
+            // PACKED: a full top chunk brings the next 64 entries along (group
+            // B, one more record load in flight per lane); they are processed
+            // in this round when every entry of both chunks is live and the
+            // stack holds all their children — the heavy rays of a deep tree
+            // (config E: up to ≈ 1,500 AABB tests) then walk half the rounds.
+            // B's keys exceed A's and no B entry descends from an A entry, so
+            // A's children stay above B's on the stack (key order); otherwise
+            // B stays where it is, untouched (only read), for later rounds.
+            const int nB = PACKED ? min(max(sp - kWave, 0), kWave) : 0;
+            uint64_t key = 0, keyB = 0;
+            int node = 0, dep = 0, nodeB = 0, depB = 0;
+            if (lane < n) {
+                const int e = sp - 1 - lane;
+                key = S.skey[e];
+                node = S.snode[e];
+                dep = S.sdep[e];
+            }
+            if (lane < nB) {
+                const int e = sp - 1 - kWave - lane;
+                keyB = S.skey[e];
+                nodeB = S.snode[e];
+                depB = S.sdep[e];
+            }
+            // popped keys ascend with the lane: the live lanes are a prefix
+            const bool live = lane < n && !(bounded && key > kbound);
+            const int n_eff = __popcll(__ballot(live));
+            const bool liveB = lane < nB && !(bounded && keyB > kbound);
+            const bool two = nB > 0 && n_eff == kWave && __popcll(__ballot(liveB)) == nB;
+            int row[8];
+            int side = 0, first = 0, cmask = 0, ref = node;
+            int sideB = 0, firstB = 0, cmaskB = 0, refB = nodeB;
+            float a = 0.f, b = 0.f, aB = 0.f, bB = 0.f;
+            bool hit = false, hitB = false;
+            if (live) {
+                if constexpr (PACKED) {
+                    const float4 pc = packed[node].c;
+                    const int4 pi = packed[node].i;
+                    float4 pcB = make_float4(0.f, 0.f, 0.f, 0.f);
+                    int4 piB = make_int4(0, 0, 0, 0);
+                    if (two && liveB) {
+                        pcB = packed[nodeB].c;
+                        piB = packed[nodeB].i;
+                    }
+                    side = __float_as_int(pc.w);
+                    ref = pi.x;
+                    first = pi.y;
+                    cmask = pi.z;
+                    hit = ray_aabb_nb(o, inv, pc.x, pc.y, pc.z, half * (float)side, a, b);
+                    if (two && liveB) {
+                        sideB = __float_as_int(pcB.w);
+                        refB = piB.x;
+                        firstB = piB.y;
+                        cmaskB = piB.z;
+                        hitB = ray_aabb_nb(o, inv, pcB.x, pcB.y, pcB.z, half * (float)sideB, aB, bB);
+                    }
+                } else {
+                    const int *rw = structure + (int64_t)node * 9;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) row[u] = rw[u];
+                    side = rw[8];
+                    const float *pc = centres + (int64_t)node * 3;
+                    hit = ray_aabb_nb(o, inv, pc[0], pc[1], pc[2], half * (float)side, a, b);
+                }
+            }
+            IS_MARK(is_tb);
+            IS_ADD(1, is_ta, is_tb);
+            const bool leaf = hit && side == 1;
+            const bool inner = hit && side != 1;
+            const bool leafB = hitB && sideB == 1;
+            const bool innerB = hitB && sideB != 1;
+            if (__ballot((inner && dep >= kLevels) || (innerB && depB >= kLevels))) {  // deeper than the reference's stack
+                spill = true;
+                break;
+            }
+            int c = 0, cB = 0;
+            if (inner) {
+                if constexpr (PACKED) {
+                    c = __popc(cmask);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) c += row[u] > -1;
+                }
+            }
+            if (innerB) cB = __popc(cmaskB);
+            const int incl = wave_incl_scan16(c);
+            if (two) {
+                const int inclB = wave_incl_scan16(cB);
+                const int TA = __builtin_amdgcn_readlane(incl, kWave - 1);
+                const int TB = __builtin_amdgcn_readlane(inclB, kWave - 1);
+                const int floorB = sp - kWave - nB;
+                if (floorB + TA + TB <= kStk) {  // (wave-uniform) both chunks accepted
+                    wave_lds_sync();  // every lane has read its candidates before the stack is rewritten
+                    // B's children, then A's on top, each in reverse key order
+                    if (innerB) {
+                        int g = inclB - cB;
+                        const int cd = depB + 1;
+#pragma unroll
+                        for (int u = 7; u >= 0; --u) {
+                            if ((cmaskB >> u) & 1) {
+                                const int pos = floorB + (TB - 1 - g);
+                                S.skey[pos] = keyB | key_digit(u, cd);
+                                S.snode[pos] = firstB + __popc(cmaskB & ((1 << u) - 1));
+                                S.sdep[pos] = (uint8_t)cd;
+                                ++g;
+                            }
+                        }
+                    }
+                    if (inner) {
+                        int g = incl - c;
+                        const int cd = dep + 1;
+#pragma unroll
+                        for (int u = 7; u >= 0; --u) {
+                            if ((cmask >> u) & 1) {
+                                const int pos = floorB + TB + (TA - 1 - g);
+                                S.skey[pos] = key | key_digit(u, cd);
+                                S.snode[pos] = first + __popc(cmask & ((1 << u) - 1));
+                                S.sdep[pos] = (uint8_t)cd;
+                                ++g;
+                            }
+                        }
+                    }
+                    IS_MARK(is_ta);
+                    IS_ADD(2, is_tb, is_ta);
+                    visits += 1 + (liveB ? 1 : 0);
+                    sp = floorB + TA + TB;
+                    merge_leaves(leaf, key, ref, a, b);
+                    merge_leaves(leafB, keyB, refB, aB, bB);
+                    IS_MARK(is_tb);
+                    IS_ADD(3, is_ta, is_tb);
+                    continue;
+                }
+            }
+            // a prune drops everything below the popped chunk (all keys > kbound)
+            const int floor_ = (n_eff < n) ? 0 : sp - n;
+            const bool ok = !live || floor_ + (n_eff - 1 - lane) + incl <= kStk;
+            const uint64_t bad = __ballot(!ok);
+            const int J = bad ? (int)__ffsll((unsigned long long)bad) - 1 : n_eff;  // accepted lanes [0, J)
+            if (J == 0 && n_eff > 0) {
+                spill = true;
+                break;
+            }
+            const int T = J > 0 ? __builtin_amdgcn_readlane(incl, J - 1) : 0;
+            const bool acc = lane < J;
+            wave_lds_sync();  // every lane has read its candidate before the stack is rewritten
+            if (live && !acc) {  // re-queued tail keeps its order on top of the floor
+                const int pos = floor_ + (n_eff - 1 - lane);
+                S.skey[pos] = key;
+                S.snode[pos] = node;
+                S.sdep[pos] = (uint8_t)dep;
+            }
+            const int base = floor_ + (n_eff - J);
+            if (acc && inner) {
+                int g = incl - c;  // rank of this lane's first (smallest-key) child
+                const int cd = dep + 1;
+#pragma unroll
+                for (int u = 7; u >= 0; --u) {
+                    const bool present = PACKED ? ((cmask >> u) & 1) != 0 : row[u] > -1;
+                    if (present) {
+                        const int pos = base + (T - 1 - g);
+                        S.skey[pos] = key | key_digit(u, cd);
+                        S.snode[pos] = PACKED ? first + __popc(cmask & ((1 << u) - 1)) : row[u];
+                        S.sdep[pos] = (uint8_t)cd;
+                        ++g;
+                    }
+                }
+            }
+            IS_MARK(is_ta);
+            IS_ADD(2, is_tb, is_ta);
+            visits += acc ? 1 : 0;
+            sp = base + T;
+            merge_leaves(acc && leaf, key, ref, a, b);
             IS_MARK(is_tb);
             IS_ADD(3, is_ta, is_tb);
         }

@@ -79,6 +79,7 @@ _SIGNATURES = {
     "psvo_engine_select_stats": (_i32, [_vp, _vp, _vp, _i32]),
     "psvo_engine_gate_stream": (_i32, [_vp, _vp]),
     "psvo_debug_set_lookback": (_i32, [_i32, _i32, _i32]),
+    "psvo_debug_set_pixel_draw": (_i32, [_i32]),
     "psvo_debug_lb_helps": (_i32, [_vp, _i32]),
     "psvo_engine_queued": (_i32, [_vp]),
     "psvo_map_discard": (_i32, [_vp]),

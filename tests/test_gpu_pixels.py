@@ -121,3 +121,36 @@ def test_sample_frames_uniform_distribution():
     c = counts.view(H, W).sum(1).double().cpu()  # per image row
     mean = reps * n / H
     assert float((c - mean).abs().max()) < 6 * mean ** 0.5, (float(c.min()), float(c.max()), mean)
+
+
+@pytest.mark.parametrize("H,W,F,n", [(680, 1200, 4, 1024), (240, 320, 3, 200), (68, 120, 2, 64)])
+def test_candidate_band_draw_equals_radix_passes(H, W, F, n):
+    """The candidate-band draw (k_px_cand + k_px_pick), its exact fallback
+    (the band forced to miss) and the five radix passes give the same picks,
+    masks and gathered rows, bit for bit."""
+    from psvo import _lib as L
+    from psvo import sample_util
+    frames = [_Frame(H, W, 300 + f) for f in range(F)]
+    outs = []
+    try:
+        for mode in (0, 1, 2):
+            L.call("psvo_debug_set_pixel_draw", mode)
+            for seed in (5, 77):
+                d, c, z = sample_util.sample_frames(frames, n, seed=seed)
+                outs.append((mode, seed, d.clone(), c.clone(), z.clone(),
+                             torch.stack([fr.sample_idx for fr in frames]).clone(),
+                             torch.stack([fr.sample_mask for fr in frames]).clone()))
+    finally:
+        L.call("psvo_debug_set_pixel_draw", 0)
+    torch.cuda.synchronize()
+    by_seed = {}
+    for o in outs:
+        by_seed.setdefault(o[1], []).append(o)
+    for seed, group in by_seed.items():
+        ref = group[1]  # the radix passes
+        for o in group:
+            for a, b in zip(o[2:], ref[2:]):
+                assert torch.equal(a, b), (o[0], seed)
+        u = O.pixel_uniforms(seed, F, H * W)
+        for f in range(F):
+            _assert_same_picks(ref[5][f:f + 1].cpu().numpy(), np.ones((1, H, W), np.float32), u[f:f + 1], n)

@@ -108,11 +108,13 @@ def test_packed_records_and_traversal(name):
         assert torch.equal(a[k], b[k]), k
     # P, R_hit, max ceil, spills, flags; the AABB-test count (a diagnostic)
     # may differ: the packed walk tests the top levels in full before any
-    # prune can apply, the reference-layout one in key-ordered rounds
+    # prune can apply, the reference-layout one in key-ordered rounds, and
+    # the packed walk's two-chunk rounds test a second chunk before the first
+    # chunk's leaves can set the prune bound (config E: ≈ +2 %)
     keep = [0, 1, 2, 3, 4, 6, 7]
     assert torch.equal(a["st"][keep], b["st"][keep])
     va, vb = int(a["st"][5]), int(b["st"][5])
-    assert abs(va - vb) <= 0.02 * va, (va, vb)
+    assert abs(va - vb) <= 0.05 * va, (va, vb)
     assert int(a["st"][6]) == 0  # no serial-DFS fallback on either side
 
 
