@@ -29,7 +29,7 @@
 // for workgroups the other one's waiters kept out (r05aj: `query look-back
 // wait abandoned` after 2^16 re-reads).  Now each workgroup stores a STARTED
 // granule {tag} as its first act.  A waiter that still misses a predecessor's
-// aggregate after kLbHelpAfter re-reads checks that predecessor's started
+// aggregate after kLbHelpAfterUs of waiting checks that predecessor's started
 // granule: if it has started, its aggregate follows its own work, which
 // depends on nothing (keep waiting); if it has not, the waiter computes that
 // workgroup's aggregate itself — the same deterministic per-item work on the
@@ -47,13 +47,20 @@
 // re-reads (≳ 0.3 s); the caller raises PSVO_STAT_FLAGS bit 3, stores no
 // rank / offset / compacted sample from the undefined prefix, and the engine
 // reports the batch as failed — the grid still drains.
+// The help threshold is time, not re-reads: a predecessor that starts late
+// because the CUs are briefly full (the draw, the decoder's prep kernels on
+// other streams) is waited for — helping is the slow path (the traversal's
+// help is a serial walk per ray: config E's traversal took 64 → 140 µs per
+// launch with help after 16 re-reads, profiles/r06l_*); only a predecessor
+// kept out for 100 µs — another queue holding the CUs — is helped.
 #pragma once
 #include "psvo_common.h"
 
 namespace psvo {
 
 constexpr int kLbSpinMax = 1 << 18;
-constexpr int kLbHelpAfter = 16;   // re-reads before the started granules of the missing producers are checked
+constexpr int kLbHelpAfter = 16;   // re-reads between checks of the missing producers' started granules
+constexpr uint64_t kLbHelpAfterTicks = 10000;  // kLbHelpAfterUs = 100 µs of waiting (s_memrealtime: 100 MHz)
 constexpr int kLbFlagTimeout = 8;  // PSVO_STAT_FLAGS bit 3
 constexpr int kLbDone = -1, kLbFail = -2;  // lb_scan_help's results (≥ 0: the block to help)
 
@@ -108,14 +115,16 @@ __device__ __forceinline__ void lb_mark_started(unsigned long long *desc, int b,
 // src[lane·NG + g] tagged `tag`, then reduce them over the wave into `red`
 // (every lane).  Lane i's granules come from workgroup producer0 + i·pstride
 // (capped at nb − 1).  Returns kLbDone; the lowest producer of a missing
-// granule that has not started after kLbHelpAfter re-reads (the caller helps
-// it); or kLbFail after spin_max re-reads (the bug trap; tests: 0 = at once).
+// granule that has not started after kLbHelpAfterTicks of waiting (the
+// caller helps it); or kLbFail after spin_max re-reads (the bug trap; tests:
+// 0 = at once).
 template <int NG, unsigned MAXMASK>
 __device__ __forceinline__ int lb_gather(const unsigned long long *src, int n, uint32_t tag, int lane,
                                          uint32_t (&red)[NG], const unsigned long long *started, int producer0,
                                          int pstride, int nb, int &spins, int spin_max) {
     uint32_t v[NG];
     int rc = kLbDone;
+    uint64_t t_wait = 0;  // when this gather first missed a granule
     for (;; ++spins) {
         bool mine = true;
 #pragma unroll
@@ -138,7 +147,9 @@ __device__ __forceinline__ int lb_gather(const unsigned long long *src, int n, u
             rc = kLbFail;
             break;
         }
-        if (spins + 1 >= kLbHelpAfter && (spins & (kLbHelpAfter - 1)) == kLbHelpAfter - 1) {
+        if (t_wait == 0) t_wait = __builtin_amdgcn_s_memrealtime();
+        if ((spins & (kLbHelpAfter - 1)) == kLbHelpAfter - 1 &&
+            __builtin_amdgcn_s_memrealtime() - t_wait >= kLbHelpAfterTicks) {
             // which of the missing producers have not started
             const int p = min(producer0 + lane * pstride, nb - 1);
             bool unstarted = false;

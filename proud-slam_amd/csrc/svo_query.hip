@@ -234,6 +234,9 @@ __device__ __forceinline__ int wave_sum(int v) {
 constexpr int kStk = 512;    // candidate stack entries per ray
 constexpr int kBfsL = 128;   // leaf list capacity (≤ 49 + 64 between compactions)
 constexpr int kIsWaves = 8;  // waves (rays) per block
+#ifndef PSVO_IS_TWO_CHUNK
+#define PSVO_IS_TWO_CHUNK 1  // the packed walk's two-chunk rounds (A/B builds: 0)
+#endif
 
 // Diagnostic build only (-DPSVO_IS_STAMPS, `make is_stamps`: lib/diag/): per
 // ray, k_intersect_sorted's cycles by segment (s_memtime; scalar reads of the
@@ -544,7 +547,7 @@ __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float 
             // B's keys exceed A's and no B entry descends from an A entry, so
             // A's children stay above B's on the stack (key order); otherwise
             // B stays where it is, untouched (only read), for later rounds.
-            const int nB = PACKED ? min(max(sp - kWave, 0), kWave) : 0;
+            const int nB = (PACKED && PSVO_IS_TWO_CHUNK) ? min(max(sp - kWave, 0), kWave) : 0;
             uint64_t key = 0, keyB = 0;
             int node = 0, dep = 0, nodeB = 0, depB = 0;
             if (lane < n) {

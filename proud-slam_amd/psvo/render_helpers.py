@@ -654,10 +654,13 @@ def _bundle_adjust_engine(eng, keyframe_graph, embed_optim, model_optim, N_rays,
     if cur_ready is not None:
         main.wait_event(cur_ready)
     clk("poses")
-    # PSVO_BA_DRAW_GATE=1 (measured switch): draws run two iterations ahead,
-    # each queued after its step's sample selection (psvo_engine_gate_stream),
-    # so their passes overlap the decoder instead of the selection's look-back
-    gate = ahead and batched and os.environ.get("PSVO_BA_DRAW_GATE") == "1"
+    # batched draws run two iterations ahead, each queued after its step's
+    # sample selection (psvo_engine_gate_stream), so that they overlap the
+    # decoder instead of the latency-bound query / selection kernels:
+    # config B 0.695 vs 0.722 ms per iteration ungated (profiles/r06_ab_draw.txt);
+    # PSVO_BA_DRAW_GATE=0 queues each draw one ahead, ungated
+    gate = (ahead and batched and os.environ.get("PSVO_BA_DRAW_GATE", "1") != "0"
+            and hasattr(L.lib(), "psvo_engine_gate_stream"))  # (an older A/B build has no gate)
     pending = None
     if gate and num_iterations > 1:
         pending = draw_ahead(1)

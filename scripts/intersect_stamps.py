@@ -14,9 +14,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "proud-slam_amd"))
+os.environ["PSVO_LIB_PATH"] = os.environ.get("PSVO_DIAG_LIB") or os.path.join(ROOT, "proud-slam_amd", "lib", "diag",
+                                                                             "libpsvo_is_stamps.so")
 from psvo import _lib  # noqa: E402
-
-_lib.LIB_PATH = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_is_stamps.so")
 import bench  # noqa: E402
 
 SEG = ["pop+load+aabb", "scan+push", "leaf merge", "sort+output"]

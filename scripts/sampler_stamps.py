@@ -12,7 +12,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DIAG = os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_is_stamps.so")
+DIAG = os.environ.get("PSVO_DIAG_LIB") or os.path.join(ROOT, "proud-slam_amd", "lib", "diag", "libpsvo_is_stamps.so")
 os.environ["PSVO_LIB_PATH"] = DIAG
 sys.path.insert(0, ROOT)
 
