@@ -945,7 +945,7 @@ int query_enqueue(psvo_engine *e, hipStream_t st, QuerySet &q, const psvo_map_de
     ENG_CALL(psvo::intersect_ranked(st, R, rays_o, rays_d, d->centres, d->structure, d->voxel_size,
                                     d->max_distance, d->step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats,
                                     ray_rank, rank_ray, static_cast<const PackRec *>(d->packed), blk_out, lb, tag,
-                                    nv_rank, col0_rank));
+                                    nv_rank, col0_rank, d->n_nodes));
     if (x.on() && noise) return set_error(PSVO_E_INVALID, "%s: injected sampler noise is single-GPU only", who);
     if (x.on()) {  // union-batch layout: ONE all-gather (8 words + the hit rows' counts), then local
         if (R > x.max_rays_rank)

@@ -218,7 +218,7 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray, const PackRec *packed = nullptr, int *blk_out = nullptr,
                      unsigned long long *lb_desc = nullptr, uint32_t lb_tag = 0,
-                     int *nv_rank = nullptr, int *col0_rank = nullptr);  // look-back: by-rank hit count, first id
+                     int *nv_rank = nullptr, int *col0_rank = nullptr, int64_t n_nodes = 0);  // look-back: by-rank hit count, first id
 
 // data-parallel query (svo_query.hip): rows of the slot-0 count table for a
 // union batch of at most max_rays_global rays; the words one rank

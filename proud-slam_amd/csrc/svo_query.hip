@@ -234,9 +234,9 @@ __device__ __forceinline__ int wave_sum(int v) {
 constexpr int kStk = 512;    // candidate stack entries per ray
 constexpr int kBfsL = 128;   // leaf list capacity (≤ 49 + 64 between compactions)
 constexpr int kIsWaves = 8;  // waves (rays) per block
-#ifndef PSVO_IS_TWO_CHUNK
-#define PSVO_IS_TWO_CHUNK 1  // the packed walk's two-chunk rounds (A/B builds: 0)
-#endif
+// the packed walk's two-chunk rounds (trace_pass TWO): for deep trees only —
+// config E's traversal 73 → 67 µs, room0's +0.7 µs (profiles/r06_ab_two_chunk.txt)
+constexpr int64_t kTwoChunkNodes = 1 << 18;
 
 // Diagnostic build only (-DPSVO_IS_STAMPS, `make is_stamps`: lib/diag/): per
 // ray, k_intersect_sorted's cycles by segment (s_memtime; scalar reads of the
@@ -450,7 +450,7 @@ __device__ unsigned long long psvo_g_lb_helps[2];
 struct IsLds {
     int vis[kIsWaves], ov[kIsWaves], sp[kIsWaves], rd[kIsWaves], nv[kIsWaves], mc[kIsWaves], c0[kIsWaves];
 };
-template <bool PACKED>
+template <bool PACKED, bool TWO = false>
 __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float *__restrict__ rays_o,
                                            const float *__restrict__ rays_d, const float *__restrict__ centres,
                                            const int *__restrict__ structure, const PackRec *__restrict__ packed,
@@ -547,7 +547,7 @@ __device__ __forceinline__ void trace_pass(int cur, int64_t n_rays, const float 
             // B's keys exceed A's and no B entry descends from an A entry, so
             // A's children stay above B's on the stack (key order); otherwise
             // B stays where it is, untouched (only read), for later rounds.
-            const int nB = (PACKED && PSVO_IS_TWO_CHUNK) ? min(max(sp - kWave, 0), kWave) : 0;
+            const int nB = (PACKED && TWO) ? min(max(sp - kWave, 0), kWave) : 0;
             uint64_t key = 0, keyB = 0;
             int node = 0, dep = 0, nodeB = 0, depB = 0;
             if (lane < n) {
@@ -863,7 +863,7 @@ __device__ __forceinline__ void trace_agg(const IsLds &L, uint32_t (&agg)[5], ui
     }
 }
 
-template <bool PACKED>
+template <bool PACKED, bool TWO = false>
 __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_rays, const float *__restrict__ rays_o,
                                                           const float *__restrict__ rays_d,
                                                           const float *__restrict__ centres,
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(64 * kIsWaves) void k_intersect_sorted(int64_t n_ra
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     __shared__ IsLds L;
     __shared__ int s_cmd;
-    trace_pass<PACKED>(blk, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance, step_size, hit_idx,
+    trace_pass<PACKED, TWO>(blk, n_rays, rays_o, rays_d, centres, structure, packed, half, max_distance, step_size, hit_idx,
                        hit_t0, hit_t1, ray_nv, ray_dsum, S, L);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2383,7 +2383,8 @@ extern "C" int psvo_ray_intersect_sorted_packed(void *stream, int64_t n_rays, co
     PSVO_REQUIRE(packed && ((uintptr_t)packed & 15) == 0, "ray_intersect_sorted_packed: packed records (16-B aligned)");
     if (n_rays == 0) return PSVO_OK;
     hipStream_t st = as_stream(stream);
-    psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
+    // (the two-chunk walk: the same hits; the deep-tree parity tests run it here)
+    psvo::launch(k_intersect_sorted<true, true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                        n_rays, rays_o, rays_d, centres, structure, static_cast<const PackRec *>(packed), voxel_size,
                        max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, nullptr, nullptr,
                        nullptr, nullptr, 0u, nullptr, nullptr, LbCtl{});
@@ -2450,7 +2451,7 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
                      const int *structure, float voxel_size, float max_distance, float step_size, int *hit_idx,
                      float *hit_t0, float *hit_t1, int *ray_nv, float *ray_dsum, int *stats, int *ray_rank,
                      int *rank_ray, const PackRec *packed, int *blk_out, unsigned long long *lb_desc,
-                     uint32_t lb_tag, int *nv_rank, int *col0_rank) {
+                     uint32_t lb_tag, int *nv_rank, int *col0_rank, int64_t n_nodes) {
     PSVO_REQUIRE(n_rays >= 0, "intersect_ranked: n_rays < 0");
     PSVO_REQUIRE((nv_rank == nullptr) == (col0_rank == nullptr) && (!nv_rank || lb_desc),
                  "intersect_ranked: the by-rank copies come with the look-back pass");
@@ -2460,10 +2461,10 @@ int intersect_ranked(hipStream_t st, int64_t n_rays, const float *rays_o, const 
     // lb_desc: the statistics / rank pass inside the traversal launch (look-
     // back; the stats words are zero: memset / the last read-back)
     if (packed)
-        psvo::launch(k_intersect_sorted<true>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
-                           n_rays, rays_o, rays_d, centres, structure, packed, voxel_size, max_distance, step_size,
-                           hit_idx, hit_t0, hit_t1, ray_nv, ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc,
-                           lb_tag, nv_rank, col0_rank, lb_ctl(1));
+        psvo::launch(n_nodes >= kTwoChunkNodes ? k_intersect_sorted<true, true> : k_intersect_sorted<true, false>,
+                     dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st, n_rays, rays_o, rays_d, centres,
+                     structure, packed, voxel_size, max_distance, step_size, hit_idx, hit_t0, hit_t1, ray_nv,
+                     ray_dsum, stats, blk_out, ray_rank, rank_ray, lb_desc, lb_tag, nv_rank, col0_rank, lb_ctl(1));
     else
         psvo::launch(k_intersect_sorted<false>, dim3(div_up(n_rays, kIsWaves)), dim3(kIsWaves * kWave), 0, st,
                            n_rays, rays_o, rays_d, centres, structure, nullptr, voxel_size, max_distance, step_size,
