@@ -102,7 +102,15 @@ struct BwdPass {  // per-wave LDS: one 16-sample pass, slot-minor so a lane read
     float w[8][16];    // trilinear weights [corner][slot]
     float g[16][16];   // grad_feat [dim][slot]
     int vid[16][8];    // vertex rows of the slot's leaf
-};  // 8 KB per 4-wave workgroup: fits beside k_mlp_dw2 (152 KB) on one CU
+};  // 2 KB per wave
+// waves per k_interp_bwd workgroup: one — a 2-KB workgroup fits three times
+// into the 6.4 KB of LDS the width-256 weight-gradient kernel (k_dec256_dw,
+// 153.6 KB, one per CU) leaves free, so the embedding backward runs on every
+// CU beside it; 4-wave (8-KB) workgroups fitted none of them
+#ifndef PSVO_IB_WAVES
+#define PSVO_IB_WAVES 1
+#endif
+constexpr int kIbWaves = PSVO_IB_WAVES;
 
 // One wave per ray; 16 samples per pass, 4 lanes per sample (dims 4q..4q+3)
 // for the gathers and dL/dx.  The embedding gradient is summed per leaf RUN
@@ -114,7 +122,7 @@ struct BwdPass {  // per-wave LDS: one 16-sample pass, slot-minor so a lane read
 // (MI355X_MICROARCH.md, global float atomics).
 // EMB = false: pose-only backward (tracking, frozen embeddings): d_o / d_d only
 template <bool EMB>
-__global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
+__global__ __launch_bounds__(64 * kIbWaves) void k_interp_bwd(int64_t r_hit, float voxel_size, const int *__restrict__ offsets,
                                                     const int *__restrict__ ray_index,
                                                     const int *__restrict__ leaf, const float *__restrict__ t,
                                                     const float *__restrict__ rays_o,
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(256) void k_interp_bwd(int64_t r_hit, float voxel_s
                                                     float *__restrict__ grad_emb, float *__restrict__ grad_o,
                                                     float *__restrict__ grad_d, int chunk, int c_max,
                                                     float *__restrict__ part) {
-    __shared__ BwdPass pass_all[4];
+    __shared__ BwdPass pass_all[kIbWaves];
     BwdPass &B = pass_all[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     // unit = one ray (chunk == 0) or chunk c of ray r (chunk samples each, c < c_max):
@@ -409,12 +417,12 @@ extern "C" int psvo_interp_bwd(void *stream, int64_t r_hit, int d, float voxel_s
     PSVO_REQUIRE(grad_o != nullptr && grad_d != nullptr, "interp_bwd: grad_o / grad_d required");
     if (r_hit == 0) return PSVO_OK;
     if (grad_emb)
-        psvo::launch(k_interp_bwd<true>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+        psvo::launch(k_interp_bwd<true>, dim3(div_up(r_hit, kIbWaves)), dim3(64 * kIbWaves), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            grad_emb, grad_o, grad_d, 0, 1, nullptr);
     else
-        psvo::launch(k_interp_bwd<false>, dim3(div_up(r_hit, 4)), dim3(256), 0, as_stream(stream), r_hit,
+        psvo::launch(k_interp_bwd<false>, dim3(div_up(r_hit, kIbWaves)), dim3(64 * kIbWaves), 0, as_stream(stream), r_hit,
                            voxel_size, offsets, ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            nullptr, grad_o, grad_d, 0, 1, nullptr);
@@ -439,12 +447,12 @@ extern "C" int psvo_interp_bwd_chunked(void *stream, int64_t r_hit, int s_max, i
     const int64_t units = r_hit * c_max;
     hipStream_t st = as_stream(stream);
     if (grad_emb)
-        psvo::launch(k_interp_bwd<true>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+        psvo::launch(k_interp_bwd<true>, dim3(div_up(units, kIbWaves)), dim3(64 * kIbWaves), 0, st, r_hit, voxel_size, offsets,
                            ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            grad_emb, grad_o, grad_d, kInterpChunk, c_max, workspace);
     else
-        psvo::launch(k_interp_bwd<false>, dim3(div_up(units, 4)), dim3(256), 0, st, r_hit, voxel_size, offsets,
+        psvo::launch(k_interp_bwd<false>, dim3(div_up(units, kIbWaves)), dim3(64 * kIbWaves), 0, st, r_hit, voxel_size, offsets,
                            ray_index, leaf, t, rays_o, rays_d, centres, vertex_idx,
                            reinterpret_cast<const float4 *>(emb), reinterpret_cast<const float4 *>(grad_feat),
                            nullptr, grad_o, grad_d, kInterpChunk, c_max, workspace);
