@@ -10,6 +10,8 @@ namespace psvo {
 
 static thread_local char g_err[512] = "";
 thread_local hipEvent_t g_stop_event = nullptr;
+thread_local bool g_stop_share = false;
+thread_local hipEvent_t g_stop_bound = nullptr;
 
 int set_error(int code, const char *fmt, ...) {
     va_list ap;

@@ -175,6 +175,7 @@ struct psvo_engine {
     bool adam_pending = false;
     hipEvent_t next_ready = nullptr;  // psvo_map_frames.next_stream's position at the call
     hipEvent_t draw_gate = nullptr;   // the last step's sample selection done (psvo_engine_gate_stream)
+    hipEvent_t draw_gate_ev = nullptr;  // the event that marks it: draw_gate, or a timed step's clock event
     bool draw_gate_recorded = false;
     bool draw_gate_used = false;      // a caller gates on it: bind it to the selections from now on
     EngineTimer tm;
@@ -545,7 +546,7 @@ extern "C" int psvo_engine_gate_stream(psvo_engine *e, void *stream) {
     PSVO_REQUIRE(e, "engine_gate_stream: null engine");
     e->draw_gate_used = true;  // (binding the event costs the selection's stream ≈ 5 µs: only for a gating caller)
     if (!e->draw_gate_recorded) return PSVO_OK;
-    if (hipStreamWaitEvent(as_stream(stream), e->draw_gate, 0) != hipSuccess)
+    if (hipStreamWaitEvent(as_stream(stream), e->draw_gate_ev, 0) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "engine_gate_stream: stream wait failed");
     return PSVO_OK;
 }
@@ -1647,12 +1648,18 @@ static int map_step_impl(psvo_engine *e, hipStream_t st, const psvo_map_desc *d,
             hipEventCreateWithFlags(&e->draw_gate, hipEventDisableSystemFence) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "map_step: event creation failed");
         psvo::g_stop_event = e->draw_gate_used ? e->draw_gate : nullptr;  // bound to the selection's dispatch
+        psvo::g_stop_share = true;  // (a timed step: the clock's stop event of the selection, no marker)
+        psvo::g_stop_bound = nullptr;
         const int sel_rc = psvo::select_samples(st, r_hit, s_max, d->truncation, d->max_depth, q.offsets, q.ray_ns,
                                                 q.z_vals, q.z_stride, q.rank_ray, gt_depth, q.sdf_s, q.feat, q.leaf,
                                                 q.tt, q.ray_of, M, two_class, cx, offa, offb, feat_c, leaf_c, t_c,
                                                 ray_of_c, rgb_c, src_c, cnt, desc, e->sel_tag, e->host_flags);
-        e->draw_gate_recorded = e->draw_gate_recorded || (e->draw_gate_used && psvo::g_stop_event == nullptr);
+        if (e->draw_gate_used && psvo::g_stop_event == nullptr && psvo::g_stop_bound) {  // (consumed: launched)
+            e->draw_gate_ev = psvo::g_stop_bound;
+            e->draw_gate_recorded = true;
+        }
         psvo::g_stop_event = nullptr;
+        psvo::g_stop_share = false;
         ENG_CALL(sel_rc);
         mark(e, st, PSVO_TIME_SELECT, 1);
         ENG_BUF(float, sdf_b, kSdfB, M * sizeof(float));

@@ -46,8 +46,13 @@ extern thread_local KernelClock *g_kclock;
 
 // set by the engine around one launch: that launch's completion records this
 // event (bound to the dispatch, no marker packet), unless a kernel clock
-// needs the slot — then it is recorded right after the launch
+// needs the slot — then it is recorded right after the launch, or, with
+// g_stop_share, not at all: g_stop_bound names the clock's stop event, which
+// marks the same completion (the caller waits on that one before the clock
+// reuses it)
 extern thread_local hipEvent_t g_stop_event;
+extern thread_local bool g_stop_share;
+extern thread_local hipEvent_t g_stop_bound;
 
 template <typename... KArgs, typename... A>
 inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A &&...a) {
@@ -74,10 +79,12 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hip
     }
     hipEvent_t late = nullptr;
     if (g_stop_event) {
-        if (e1)
-            late = g_stop_event;
+        if (!e1)
+            e1 = g_stop_bound = g_stop_event;
+        else if (g_stop_share)
+            g_stop_bound = e1;
         else
-            e1 = g_stop_event;
+            late = g_stop_bound = g_stop_event;
         g_stop_event = nullptr;
     }
     hipExtLaunchKernelGGL(k, grid, block, lds, st, e0, e1, 0u, static_cast<KArgs>(a)...);
