@@ -1211,21 +1211,25 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     // A batch beyond the capacity makes them write nothing; the host then
     // runs them sized by the read-back, as without this path.
     const int64_t m_early = std::min<int64_t>(e->m_early, (int64_t)qset.R * max_steps);
-    const bool early = rays_path && sparse && width == 128 && qset.compacted && qset.a.p[kMDev] && m_early > 0 &&
+    const bool early = rays_path && sparse && qset.compacted && qset.a.p[kMDev] && m_early > 0 &&
                        (early_images || prebuilt) && !(e->paths & PSVO_PATH_QUERY_SPLIT);
     float *feat_e = nullptr, *sdf_e = nullptr, *h2_e = nullptr;
     // the sparse decoder (width 128): the sdf trunk hands every sample's h2 to
     // the later layers (k_mlp_fwd2 / k_mlp_trunk_fb read it instead of
-    // recomputing the W2 layer)
+    // recomputing the W2 layer); width 256's trunk (k_dec256_trunk) is
+    // device-sized too (round 6: C / E lost 22–37 µs per step to the host's
+    // read-back before the interpolation)
     const bool want_h2 = sparse && width == 128;
     if (early) {
         const int *m_dev = static_cast<const int *>(qset.a.p[kMDev]);
         ENG_BUF(float, fe, kFeat, m_early * 16 * sizeof(float));
         ENG_BUF(float, se, kSdfS, m_early * sizeof(float));
-        ENG_BUF(float, he, kH2, m_early * kW128 * sizeof(float));
         feat_e = fe;
         sdf_e = se;
-        h2_e = he;
+        if (want_h2) {  // (width 256: its trunk keeps no h2)
+            ENG_BUF(float, he, kH2, m_early * kW128 * sizeof(float));
+            h2_e = he;
+        }
         ENG_CALL(join_adam(e, st, who, 2000.0));
         mark(e, st, PSVO_TIME_INTERP_FWD, 0);
         ENG_CALL(psvo::interp_fwd_dev(st, m_early, m_dev, d->voxel_size, static_cast<const int *>(qset.a.p[kLeafQ]),
@@ -1283,7 +1287,7 @@ int render(psvo_engine *e, hipStream_t st, const psvo_map_desc *d, QuerySet &qse
     if (M == 0) return set_error(PSVO_E_INVALID, "%s: no valid samples", who);
     // the device-sized forward covered this batch (else: it wrote nothing, run it host-sized below)
     const bool early_done = early && M <= m_early;
-    if (rays_path && sparse && width == 128) e->m_early = std::max<int64_t>(e->m_early, M + M / 4);
+    if (rays_path && sparse) e->m_early = std::max<int64_t>(e->m_early, M + M / 4);
     ENG_BUF(int, leaf, kLeaf, M * sizeof(int));
     ENG_BUF(float, tt, kT, M * sizeof(float));
     ENG_BUF(int, ray_of, kRayOf, M * sizeof(int));

@@ -536,8 +536,16 @@ __global__ __launch_bounds__(kCThreads, 1) void k_dec256_fwd(int64_t m, int64_t 
 // block 8 of k_dec256_fwd's L3: the same sdf bits.
 __global__ __launch_bounds__(kCThreads, 1) void k_dec256_trunk(int64_t m, const float *__restrict__ feat,
                                                                const float *__restrict__ img,
-                                                               float *__restrict__ sdf) {
+                                                               float *__restrict__ sdf,
+                                                               const int *__restrict__ m_dev) {
     extern __shared__ __align__(16) float lds[];
+    // the device-sized forward (queued before the host reads the query's
+    // statistics): the sampler's M; m is then the buffers' capacity — a
+    // larger batch: nothing here, the host-sized launch after the read-back
+    if (m_dev) {
+        const int64_t md = __builtin_amdgcn_readfirstlane(*m_dev);
+        m = md > m ? 0 : md;
+    }
     float *vec = lds;  // kVecN
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int e = threadIdx.x; e < kVecN; e += kCThreads) vec[e] = img[kImgMats + e];
@@ -1089,7 +1097,6 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
     if (m == 0) return PSVO_OK;
     const int64_t n_tiles = (m + kChainTile - 1) / kChainTile;
     if (!rgb && !act && !masks) {  // sdf only: the trunk
-        PSVO_REQUIRE(m_dev == nullptr, "dec256_fwd: the sdf trunk runs host-sized");
         const int lds = (((kVecN + 63) / 64) * 64 + kRing * kChunkFloats) * 4;
         static bool tattr = false;
         if (!tattr) {
@@ -1097,7 +1104,7 @@ int dec256_fwd(hipStream_t st, int64_t m, const float *feat, const float *images
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             tattr = true;
         }
-        psvo::launch(k_dec256_trunk, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, feat, images, sdf);
+        psvo::launch(k_dec256_trunk, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, feat, images, sdf, m_dev);
         return check_launch("dec256_trunk");
     }
     const int64_t n16 = dec256_tiles16(m);
