@@ -14,6 +14,11 @@
  *   psvo_inverse_cdf_sampling     grid.inverse_cdf_sampling
  *                                 third_party/sparse_voxels/src/sample.cpp:56-95,
  *                                 sample_gpu.cu:133-239, :255-269
+ *   psvo_ball_intersect / psvo_aabb_intersect / psvo_triangle_intersect
+ *                                 grid.ball_intersect / aabb_intersect / triangle_intersect
+ *                                 intersect.cpp:15-42, :49-76, :119-146; intersect_gpu.cu:13-187, :273-362
+ *   psvo_uniform_ray_sampling     grid.uniform_ray_sampling sample.cpp:21-54, sample_gpu.cu:13-124
+ *   psvo_build_octree             grid.build_octree octree.cpp:12-164 (CPU, host memory)
  *   psvo_ray_intersect_sorted     voxel_helpers.ray_intersect_vox (voxel_helpers.py:557-595)
  *                                 + SparseVoxelOctreeRayIntersect (:110-166), fused
  *   psvo_hit_rank / psvo_sample_rays / psvo_sample_points
@@ -73,6 +78,34 @@ int psvo_inverse_cdf_sampling(void *stream, int b, int num_rays, int max_hits, i
                               float fixed_step_size, const int *pts_idx, const float *min_depth,
                               const float *max_depth, const float *uniform_noise, const float *probs,
                               const float *steps, int *sampled_idx, float *sampled_depth, float *sampled_dists);
+
+/* The `grid` functions off the render path (csrc/grid_aux.hip), reference
+ * layouts; outputs pre-filled by the caller as the reference allocates them
+ * (zeros; -1 for sampled_idx).  ball / aabb: the first n_max hits in point
+ * order, idx -1 after.  triangle: face_points f32[b,n,9]; the first n_max
+ * hits in face order sorted by depth (ties in face order); depth
+ * f32[b,m,3·n_max] = (t, -gap/2 capped, +gap/2 capped), uv f32[b,m,2·n_max];
+ * n_max <= 2048.  uniform sampling: pts_idx/min/max [b,num_rays,max_hits],
+ * noise and outputs [b,num_rays,max_steps]. */
+int psvo_ball_intersect(void *stream, int b, int n, int m, float radius, int n_max, const float *ray_start,
+                        const float *ray_dir, const float *points, int *idx, float *min_depth, float *max_depth);
+int psvo_aabb_intersect(void *stream, int b, int n, int m, float voxelsize, int n_max, const float *ray_start,
+                        const float *ray_dir, const float *points, int *idx, float *min_depth, float *max_depth);
+int psvo_triangle_intersect(void *stream, int b, int n, int m, float cagesize, float blur, int n_max,
+                            const float *ray_start, const float *ray_dir, const float *face_points, int *idx,
+                            float *depth, float *uv);
+int psvo_uniform_ray_sampling(void *stream, int b, int num_rays, int max_hits, int max_steps, float step_size,
+                              const int *pts_idx, const float *min_depth, const float *max_depth,
+                              const float *uniform_noise, int *sampled_idx, float *sampled_depth,
+                              float *sampled_dists);
+/* grid.build_octree on the host: n int64 points [n,3] under a root centred at
+ * center[3] (f32) of the given depth.  Sets *total (nodes) and *terminal
+ * (leaves = n); writes centers i32[total,3] and children i32[total,9] only
+ * when capacity >= total (call with capacity 0 first to size them).
+ * PSVO_E_INVALID for depth outside [0, 29] or two points in one leaf slot
+ * (*total = the second point's index). */
+int psvo_build_octree(const float *center, const int64_t *points, int64_t n, int depth, int64_t capacity,
+                      int *centers, int *children, int64_t *total, int64_t *terminal);
 
 /* ---- fused render path ------------------------------------------------ */
 

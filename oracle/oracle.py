@@ -51,6 +51,10 @@ def lib():
         L.oracle_svo_intersect.restype = i64
         L.oracle_svo_intersect.argtypes = [i64, vp, vp, vp, vp, f32, i32, vp, vp, vp]
         L.oracle_inverse_cdf.argtypes = [i32, i32, i32, i32, f32] + [vp] * 9
+        L.oracle_ball_intersect.argtypes = [i32, i32, i32, f32, i32] + [vp] * 6
+        L.oracle_aabb_intersect.argtypes = [i32, i32, i32, f32, i32] + [vp] * 6
+        L.oracle_triangle_intersect.argtypes = [i32, i32, i32, f32, f32, i32] + [vp] * 6
+        L.oracle_uniform_sampling.argtypes = [i32, i32, i32, i32, f32] + [vp] * 7
         _lib = L
     return _lib
 
@@ -652,3 +656,126 @@ def sample_rays(mask, n, u):
         order = np.lexsort((np.arange(s.shape[1]), -s[b].astype(np.float64)))
         out[b] = np.sort(order[:n])
     return out
+
+
+# ---------------------------------------------------------------------------
+# The `grid` functions off the render path (SURVEY.md §8b import contract).
+# Arrays in the reference layouts; outputs allocated as intersect.cpp /
+# sample.cpp allocate them.
+# ---------------------------------------------------------------------------
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def ball_intersect(ray_start, ray_dir, points, radius, n_max):
+    """intersect.cpp:15-42 + intersect_gpu.cu:13-73 → (idx, min_depth, max_depth) [b, m, n_max]."""
+    rs, rd, pts = _f32(ray_start), _f32(ray_dir), _f32(points)
+    b, m, n = rs.shape[0], rs.shape[1], pts.shape[1]
+    idx = np.zeros((b, m, n_max), np.int32)
+    lo = np.zeros((b, m, n_max), np.float32)
+    hi = np.zeros((b, m, n_max), np.float32)
+    lib().oracle_ball_intersect(b, n, m, float(radius), int(n_max), _ptr(rs), _ptr(rd), _ptr(pts), _ptr(idx),
+                                _ptr(lo), _ptr(hi))
+    return idx, lo, hi
+
+
+def aabb_intersect(ray_start, ray_dir, points, voxelsize, n_max):
+    """intersect.cpp:49-76 + intersect_gpu.cu:142-187 → (idx, min_depth, max_depth) [b, m, n_max]."""
+    rs, rd, pts = _f32(ray_start), _f32(ray_dir), _f32(points)
+    b, m, n = rs.shape[0], rs.shape[1], pts.shape[1]
+    idx = np.zeros((b, m, n_max), np.int32)
+    lo = np.zeros((b, m, n_max), np.float32)
+    hi = np.zeros((b, m, n_max), np.float32)
+    lib().oracle_aabb_intersect(b, n, m, float(voxelsize), int(n_max), _ptr(rs), _ptr(rd), _ptr(pts), _ptr(idx),
+                                _ptr(lo), _ptr(hi))
+    return idx, lo, hi
+
+
+def triangle_intersect(ray_start, ray_dir, face_points, cagesize, blur, n_max):
+    """intersect.cpp:119-146 + intersect_gpu.cu:273-369 → (idx [b,m,n_max], depth [b,m,3n_max], uv [b,m,2n_max])."""
+    rs, rd, fp = _f32(ray_start), _f32(ray_dir), _f32(face_points)
+    b, m, n = rs.shape[0], rs.shape[1], fp.shape[1]
+    idx = np.zeros((b, m, n_max), np.int32)
+    depth = np.zeros((b, m, 3 * n_max), np.float32)
+    uv = np.zeros((b, m, 2 * n_max), np.float32)
+    lib().oracle_triangle_intersect(b, n, m, float(cagesize), float(blur), int(n_max), _ptr(rs), _ptr(rd), _ptr(fp),
+                                    _ptr(idx), _ptr(depth), _ptr(uv))
+    return idx, depth, uv
+
+
+def uniform_ray_sampling(pts_idx, min_depth, max_depth, uniform_noise, step_size, max_steps):
+    """sample.cpp:21-54 + sample_gpu.cu:13-124 → (sampled_idx, depth, dists) [b, k, max_steps]."""
+    pi = np.ascontiguousarray(pts_idx, dtype=np.int32)
+    lo, hi, nz = _f32(min_depth), _f32(max_depth), _f32(uniform_noise)
+    b, k, p = lo.shape
+    s_idx = -np.ones((b, k, max_steps), np.int32)
+    s_depth = np.zeros((b, k, max_steps), np.float32)
+    s_dist = np.zeros((b, k, max_steps), np.float32)
+    lib().oracle_uniform_sampling(b, k, p, int(max_steps), float(step_size), _ptr(pi), _ptr(lo), _ptr(hi), _ptr(nz),
+                                  _ptr(s_idx), _ptr(s_depth), _ptr(s_dist))
+    return s_idx, s_depth, s_dist
+
+
+class _EasyNode:
+    __slots__ = ("center", "depth", "index", "children")
+
+    def __init__(self, center, depth, index):
+        self.center, self.depth, self.index = center, depth, index
+        self.children = [None] * 8
+
+
+def build_octree(center, points, depth):
+    """sparse_voxels/src/octree.cpp:12-164 (EasyOctree), pure Python (small
+    inputs): centre compared and advanced in f32, leaves keep their point
+    index, internal ids from total-1 down in BFS order.  Returns
+    (centers i32 [total, 3], children i32 [total, 9])."""
+    c0 = np.asarray(center, dtype=np.float32).reshape(3)
+    pts = np.asarray(points, dtype=np.int64).reshape(-1, 3)
+    root = _EasyNode(c0.copy(), int(depth), -1)
+
+    def insert(p, point, index):  # octree.cpp:71-92
+        diff = (point.astype(np.float32) > p.center).astype(np.int32)
+        i = int(diff[0] + 2 * diff[1] + 4 * diff[2])
+        if p.depth == 0:
+            p.children[i] = _EasyNode(point.copy(), -1, index)
+        else:
+            if p.children[i] is None:
+                length = 1 << (p.depth - 1)
+                p.children[i] = _EasyNode((p.center + ((2 * diff - 1) * length).astype(np.float32)).astype(np.float32),
+                                          p.depth - 1, -1)
+            insert(p.children[i], point, index)
+
+    for k in range(pts.shape[0]):
+        insert(root, pts[k], k)
+
+    def count(p):  # octree.cpp:94-111
+        total, terminal = 1, 1 if p.depth == -1 else 0
+        for c in p.children:
+            if c is not None:
+                a, t = count(c)
+                total += a
+                terminal += t
+        return total, terminal
+
+    total, terminal = count(root)
+    centers = np.zeros((total, 3), np.int32)
+    children = -np.ones((total, 9), np.int32)
+    node_idx = total - 1
+    root.index = node_idx
+    queue = [root]
+    head = 0
+    while head < len(queue):  # octree.cpp:127-145
+        node = queue[head]
+        head += 1
+        for i, c in enumerate(node.children):
+            if c is not None:
+                if c.depth > -1:
+                    node_idx -= 1
+                    c.index = node_idx
+                queue.append(c)
+                children[node.index, i] = c.index
+        children[node.index, 8] = 1 << (node.depth + 1)
+        centers[node.index] = np.trunc(np.asarray(node.center, dtype=np.float64)).astype(np.int32)
+    assert node_idx == terminal  # octree.cpp:146
+    return centers, children

@@ -385,3 +385,210 @@ void oracle_inverse_cdf(int b, int num_rays, int max_hits, int max_steps, float 
         }
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* The `grid` functions off the render path (they must exist  */
+/* for import compatibility; test_aabb.py calls aabb_intersect).  Serial     */
+/* loops in the reference's own structure, one ray at a time.                */
+/* ------------------------------------------------------------------------ */
+
+/* intersect_gpu.cu:13-73 (pow(p, 2) is the correctly rounded square p*p) */
+void oracle_ball_intersect(int b, int n, int m, float radius, int n_max, const float *ray_start,
+                           const float *ray_dir, const float *points, int *idx, float *min_depth, float *max_depth)
+{
+    const float radius2 = radius * radius;
+    for (int64_t r = 0; r < (int64_t)b * m; ++r) {
+        const float *pts = points + (r / m) * n * 3;
+        const float *o = ray_start + r * 3, *w = ray_dir + r * 3;
+        int *id = idx + r * n_max;
+        float *lo = min_depth + r * n_max, *hi = max_depth + r * n_max;
+        for (int l = 0; l < n_max; ++l) id[l] = -1;
+        for (int k = 0, cnt = 0; k < n && cnt < n_max; ++k) {
+            float x = pts[k * 3 + 0] - o[0];
+            float y = pts[k * 3 + 1] - o[1];
+            float z = pts[k * 3 + 2] - o[2];
+            float d2 = x * x + y * y + z * z;
+            float p = x * w[0] + y * w[1] + z * w[2];
+            float d2_proj = p * p;
+            float r2 = d2 - d2_proj;
+            if (r2 < radius2) {
+                id[cnt] = k;
+                float depth = sqrtf(d2_proj);
+                float blur = sqrtf(radius2 - r2);
+                lo[cnt] = depth - blur;
+                hi[cnt] = depth + blur;
+                ++cnt;
+            }
+        }
+    }
+}
+
+/* intersect_gpu.cu:142-187 over or_ray_aabb (a miss is (-1,-1); kept when t_in > -1) */
+void oracle_aabb_intersect(int b, int n, int m, float voxelsize, int n_max, const float *ray_start,
+                           const float *ray_dir, const float *points, int *idx, float *min_depth, float *max_depth)
+{
+    const float half = voxelsize * 0.5f;
+    for (int64_t r = 0; r < (int64_t)b * m; ++r) {
+        const float *pts = points + (r / m) * n * 3;
+        int *id = idx + r * n_max;
+        float *lo = min_depth + r * n_max, *hi = max_depth + r * n_max;
+        for (int l = 0; l < n_max; ++l) id[l] = -1;
+        for (int k = 0, cnt = 0; k < n && cnt < n_max; ++k) {
+            float t0 = -1.0f, t1 = -1.0f;
+            if (!or_ray_aabb(ray_start + r * 3, ray_dir + r * 3, pts + k * 3, half, &t0, &t1)) t0 = t1 = -1.0f;
+            if (t0 > -1.0f) {
+                id[cnt] = k;
+                lo[cnt] = t0;
+                hi[cnt] = t1;
+                ++cnt;
+            }
+        }
+    }
+}
+
+static void or_sub(const float a[3], const float b[3], float o[3])
+{
+    o[0] = a[0] - b[0];
+    o[1] = a[1] - b[1];
+    o[2] = a[2] - b[2];
+}
+static float or_dot(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void or_cross(const float a[3], const float b[3], float o[3]) /* cutil_math.h:424-427 */
+{
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* RayTriangleIntersection intersect_gpu.cu:273-305: returns (t, u, v), t = -1 on a miss */
+static void or_ray_triangle(const float o[3], const float d[3], const float *f, float blur, float tuv[3])
+{
+    float e1[3], e2[3], s[3], p[3], q[3];
+    or_sub(f + 3, f, e1);
+    or_sub(f + 6, f, e2);
+    or_sub(o, f, s);
+    or_cross(d, e2, p);
+    float det = 1.0f / or_dot(e1, p);
+    float u = or_dot(s, p) * det;
+    tuv[0] = -1.0f;
+    tuv[1] = tuv[2] = 0.0f;
+    if ((u < 0.0f - blur) || (u > 1.0f + blur)) return;
+    or_cross(s, e1, q);
+    float v = or_dot(d, q) * det;
+    if ((v < 0.0f - blur) || (v > 1.0f + blur)) return;
+    if (((u + v) < 0.0f - blur) || ((u + v) > 1.0f + blur)) return;
+    tuv[0] = or_dot(e2, q) * det;
+    tuv[1] = u;
+    tuv[2] = v;
+}
+
+/* intersect_gpu.cu:307-369: insertion while collecting, then the cage offsets */
+void oracle_triangle_intersect(int b, int n, int m, float cagesize, float blur, int n_max, const float *ray_start,
+                               const float *ray_dir, const float *face_points, int *idx, float *depth, float *uv)
+{
+    for (int64_t r = 0; r < (int64_t)b * m; ++r) {
+        const float *fp = face_points + (r / m) * n * 9;
+        int *id = idx + r * n_max;
+        float *dp = depth + r * n_max * 3, *uvr = uv + r * n_max * 2;
+        for (int l = 0; l < n_max; ++l) id[l] = -1;
+        int cnt = 0;
+        for (int k = 0; k < n && cnt < n_max; ++k) {
+            float tuv[3];
+            or_ray_triangle(ray_start + r * 3, ray_dir + r * 3, fp + (int64_t)k * 9, blur, tuv);
+            if (tuv[0] > 0) {
+                int ki = k;
+                float d = tuv[0], u = tuv[1], v = tuv[2], tf;
+                int ti;
+                for (int l = 0; l < cnt; l++) {
+                    if (d < dp[l * 3]) {
+                        ti = ki; ki = id[l]; id[l] = ti;
+                        tf = d; d = dp[l * 3]; dp[l * 3] = tf;
+                        tf = u; u = uvr[l * 2]; uvr[l * 2] = tf;
+                        tf = v; v = uvr[l * 2 + 1]; uvr[l * 2 + 1] = tf;
+                    }
+                }
+                id[cnt] = ki;
+                dp[cnt * 3] = d;
+                uvr[cnt * 2] = u;
+                uvr[cnt * 2 + 1] = v;
+                cnt++;
+            }
+        }
+        for (int l = 0; l < cnt; l++) {
+            dp[l * 3 + 1] = (l == 0) ? -cagesize : -fminf(cagesize, (float)(.5 * (dp[l * 3] - dp[l * 3 - 3])));
+            dp[l * 3 + 2] = (l == cnt - 1) ? cagesize : fminf(cagesize, (float)(.5 * (dp[l * 3 + 3] - dp[l * 3])));
+        }
+    }
+}
+
+/* sample_gpu.cu:13-124 for every ray of the flat [b, num_rays] layout.  Reads
+ * past a ray's row go to the neighbouring row as in the reference (-1 / 0
+ * outside the array); writes past max_steps (a cross-row race there) are
+ * dropped; the merge stops after max_steps + 2·max_hits + 3 rounds. */
+void oracle_uniform_sampling(int b, int num_rays, int max_hits, int max_steps, float step_size,
+                             const int *pts_idx, const float *min_depth, const float *max_depth,
+                             const float *uniform_noise, int *sampled_idx, float *sampled_depth, float *sampled_dists)
+{
+    const int64_t total = (int64_t)b * num_rays, n_idx = total * max_hits;
+#define OR_PIDX(at) (((at) >= 0 && (at) < n_idx) ? pts_idx[(at)] : -1)
+    for (int64_t j = 0; j < total; ++j) {
+        const int64_t H = j * max_hits, K = j * max_steps;
+        int s = 0, ucur = 0, umin = 0, umax = 0, guard = 0;
+        float last_min_depth, last_max_depth, curr_depth = 0.0f;
+        while (guard++ <= max_steps + 2 * max_hits + 2) {
+            if ((umax == max_hits) || (ucur == max_steps) || (OR_PIDX(H + umax) == -1)) break;
+            last_min_depth = (umin < max_hits) ? min_depth[H + umin] : 10000.0f;
+            last_max_depth = (umax < max_hits) ? max_depth[H + umax] : 10000.0f;
+            if (ucur < max_steps) curr_depth = min_depth[H] + ((float)ucur + uniform_noise[K + ucur]) * step_size;
+            if ((last_max_depth <= curr_depth) && (last_max_depth <= last_min_depth)) {
+                if (s < max_steps) {
+                    sampled_depth[K + s] = last_max_depth;
+                    sampled_idx[K + s] = OR_PIDX(H + umax);
+                }
+                umax++;
+                s++;
+                continue;
+            }
+            if ((curr_depth <= last_min_depth) && (curr_depth <= last_max_depth)) {
+                if (s < max_steps) {
+                    sampled_depth[K + s] = curr_depth;
+                    sampled_idx[K + s] = OR_PIDX(H + umin - 1);
+                }
+                ucur++;
+                s++;
+                continue;
+            }
+            if ((last_min_depth <= curr_depth) && (last_min_depth <= last_max_depth)) {
+                if (s < max_steps) {
+                    sampled_depth[K + s] = last_min_depth;
+                    sampled_idx[K + s] = OR_PIDX(H + umin);
+                }
+                umin++;
+                s++;
+                continue;
+            }
+        }
+        float l_depth, r_depth;
+        int step = 0;
+        for (ucur = 0, umin = 0, umax = 0; ucur < max_steps - 1; ucur++) {
+            if (sampled_idx[K + ucur + 1] == -1) break;
+            l_depth = sampled_depth[K + ucur];
+            r_depth = sampled_depth[K + ucur + 1];
+            sampled_depth[K + ucur] = (l_depth + r_depth) * .5f;
+            sampled_dists[K + ucur] = (r_depth - l_depth);
+            if ((umin < max_hits) && (sampled_depth[K + ucur] >= min_depth[H + umin]) && (pts_idx[H + umin] > -1))
+                umin++;
+            if ((umax < max_hits) && (sampled_depth[K + ucur] >= max_depth[H + umax]) && (pts_idx[H + umax] > -1))
+                umax++;
+            if ((umax == max_hits) || (pts_idx[H + umax] == -1)) break;
+            if ((umin - 1 == umax) && (sampled_dists[K + ucur] > 0)) {
+                sampled_depth[K + step] = sampled_depth[K + ucur];
+                sampled_dists[K + step] = sampled_dists[K + ucur];
+                sampled_idx[K + step] = sampled_idx[K + ucur];
+                step++;
+            }
+        }
+        for (int l = step; l < max_steps; l++) sampled_idx[K + l] = -1;
+    }
+#undef OR_PIDX
+}

@@ -1,0 +1,399 @@
+// The `grid` extension's off-path entry points on gfx950: brute-force
+// ray/ball, ray/box and ray/triangle intersection and NSVF uniform ray
+// sampling.  The render path never calls them; they
+// exist so code written against the reference's `grid` module — its own
+// src/variations/test_aabb.py among it — runs unchanged.
+//
+// Reference behaviour restated (DARYL-GWZ/Proud-SLAM, third_party/sparse_voxels):
+//   intersect_gpu.cu:13-73    ball test; first n_max hits in point order
+//   intersect_gpu.cu:75-187   slab test (f_low 0, f_high 1e5); first n_max boxes in order
+//   intersect_gpu.cu:273-362  Möller–Trumbore with blur; first n_max hits in face
+//                             order, then ordered by depth (ties keep face order),
+//                             then the cage offsets from the neighbour gaps
+//   sample_gpu.cu:13-124      merge of box boundaries with uniform steps, midpoints,
+//                             compaction of the in-box intervals
+//
+// MI355X design: the intersections give one wave per ray and test 64
+// primitives per wave-step (coalesced 768-B / 2.3-KB reads of the primitive
+// list); __ballot + mbcnt compact the hits in primitive order, so the wave
+// stops as soon as n_max hits exist — the same prefix the reference's serial
+// loop keeps.  The triangle kernel sorts its ≤ n_max hits in LDS by rank
+// (count of smaller depths, ties broken by face order), which is the order
+// the reference's insertion produces.  The uniform sampler is an in-place
+// serial merge per ray, one lane per ray, exactly as the reference's.
+//
+// Arithmetic: contraction off and IEEE division / square root, matching the
+// CPU oracle bit for bit (the reference uses __fdividef and nvcc's FMA
+// contraction; DESIGN.md "parity").  sqrtf, not __fsqrt_rn: on this
+// toolchain the latter lowers to the bare v_sqrt_f32 (1 ulp), sqrtf to the
+// correctly rounded sequence.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "psvo_common.h"
+
+namespace psvo {
+namespace {
+
+constexpr int kGaWaves = 4;           // rays (waves) per workgroup
+constexpr int kTriMaxHits = 2048;     // LDS bound of the triangle kernel's hit list
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// intersect_gpu.cu:75-140 — the same comparisons as svo_query.hip's ray_aabb
+__device__ __forceinline__ bool slab(const float o[3], const float inv[3], const float c[3], float half,
+                                     float &t_lo, float &t_hi) {
+    float lo_all = 0.0f, hi_all = 100000.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float lo = (c[a] - half - o[a]) * inv[a];
+        float hi = (c[a] + half - o[a]) * inv[a];
+        if (hi < lo) {
+            const float tmp = lo;
+            lo = hi;
+            hi = tmp;
+        }
+        if (hi < lo_all || lo > hi_all) return false;
+        lo_all = (lo > lo_all) ? lo : lo_all;
+        hi_all = (hi < hi_all) ? hi : hi_all;
+        if (lo_all > hi_all) return false;
+    }
+    t_lo = lo_all;
+    t_hi = hi_all;
+    return true;
+}
+
+// One wave per ray over [b, m] rays; `test(k, lo, hi)` decides primitive k.
+// Writes the first n_max hits in primitive order, -1 in the unused idx slots.
+template <class Test>
+__device__ __forceinline__ void first_hits(int n, int n_max, const Test &test, int *idx, float *lo_out,
+                                           float *hi_out) {
+    const int lane = threadIdx.x % kWave;
+    int cnt = 0;
+    for (int k0 = 0; k0 < n && cnt < n_max; k0 += kWave) {
+        const int k = k0 + lane;
+        float lo = 0.0f, hi = 0.0f;
+        const bool hit = k < n && test(k, lo, hi);
+        const uint64_t mask = __ballot(hit);
+        const int pos = cnt + lanes_below(mask);
+        if (hit && pos < n_max) {
+            idx[pos] = k;
+            lo_out[pos] = lo;
+            hi_out[pos] = hi;
+        }
+        cnt += __popcll(mask);
+    }
+    for (int l = min(cnt, n_max) + lane; l < n_max; l += kWave) idx[l] = -1;
+}
+
+__global__ __launch_bounds__(kGaWaves *kWave) void k_ball_intersect(int b, int n, int m, float radius, int n_max,
+                                                                     const float *__restrict__ ray_start,
+                                                                     const float *__restrict__ ray_dir,
+                                                                     const float *__restrict__ points, int *idx,
+                                                                     float *min_depth, float *max_depth) {
+    const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
+    if (ray >= (int64_t)b * m) return;
+    const int64_t bi = ray / m;
+    const float *pts = points + bi * n * 3;
+    const float o[3] = {ray_start[ray * 3], ray_start[ray * 3 + 1], ray_start[ray * 3 + 2]};
+    const float w[3] = {ray_dir[ray * 3], ray_dir[ray * 3 + 1], ray_dir[ray * 3 + 2]};
+    const float r2max = radius * radius;
+    auto test = [&](int k, float &lo, float &hi) {
+        const float x = pts[(int64_t)k * 3] - o[0];
+        const float y = pts[(int64_t)k * 3 + 1] - o[1];
+        const float z = pts[(int64_t)k * 3 + 2] - o[2];
+        const float d2 = x * x + y * y + z * z;
+        const float proj = x * w[0] + y * w[1] + z * w[2];
+        const float d2_proj = proj * proj;
+        const float r2 = d2 - d2_proj;
+        if (!(r2 < r2max)) return false;
+        const float depth = sqrtf(d2_proj);
+        const float blur = sqrtf(r2max - r2);
+        lo = depth - blur;
+        hi = depth + blur;
+        return true;
+    };
+    first_hits(n, n_max, test, idx + ray * n_max, min_depth + ray * n_max, max_depth + ray * n_max);
+}
+
+__global__ __launch_bounds__(kGaWaves *kWave) void k_aabb_intersect(int b, int n, int m, float voxelsize, int n_max,
+                                                                     const float *__restrict__ ray_start,
+                                                                     const float *__restrict__ ray_dir,
+                                                                     const float *__restrict__ points, int *idx,
+                                                                     float *min_depth, float *max_depth) {
+    const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
+    if (ray >= (int64_t)b * m) return;
+    const int64_t bi = ray / m;
+    const float *pts = points + bi * n * 3;
+    const float o[3] = {ray_start[ray * 3], ray_start[ray * 3 + 1], ray_start[ray * 3 + 2]};
+    float inv[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, ray_dir[ray * 3 + a]);
+    const float half = voxelsize * 0.5f;
+    auto test = [&](int k, float &lo, float &hi) {
+        const float c[3] = {pts[(int64_t)k * 3], pts[(int64_t)k * 3 + 1], pts[(int64_t)k * 3 + 2]};
+        // the reference keeps a box only when t_in > -1 (intersect_gpu.cu:176)
+        return slab(o, inv, c, half, lo, hi) && lo > -1.0f;
+    };
+    first_hits(n, n_max, test, idx + ray * n_max, min_depth + ray * n_max, max_depth + ray * n_max);
+}
+
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ F3 sub(F3 a, F3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ F3 cross(F3 a, F3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// intersect_gpu.cu:273-305: t (> 0 to count), u, v
+__device__ __forceinline__ bool ray_triangle(F3 o, F3 d, const float *f, float blur, float &t, float &u, float &v) {
+    const F3 v0 = {f[0], f[1], f[2]}, v1 = {f[3], f[4], f[5]}, v2 = {f[6], f[7], f[8]};
+    const F3 e1 = sub(v1, v0), e2 = sub(v2, v0), s = sub(o, v0);
+    const F3 p = cross(d, e2);
+    const float inv_det = __fdiv_rn(1.0f, dot(e1, p));
+    u = dot(s, p) * inv_det;
+    if ((u < 0.0f - blur) || (u > 1.0f + blur)) return false;
+    const F3 q = cross(s, e1);
+    v = dot(d, q) * inv_det;
+    if ((v < 0.0f - blur) || (v > 1.0f + blur)) return false;
+    if (((u + v) < 0.0f - blur) || ((u + v) > 1.0f + blur)) return false;
+    t = dot(e2, q) * inv_det;
+    return t > 0.0f;
+}
+
+// One wave per ray; the ≤ n_max hits live in LDS (dynamic, 20 B per slot).
+__global__ __launch_bounds__(kWave) void k_triangle_intersect(int b, int n, int m, float cagesize, float blur,
+                                                              int n_max, const float *__restrict__ ray_start,
+                                                              const float *__restrict__ ray_dir,
+                                                              const float *__restrict__ faces, int *idx_out,
+                                                              float *depth_out, float *uv_out) {
+    extern __shared__ float tri_lds[];
+    int *h_k = reinterpret_cast<int *>(tri_lds);
+    float *h_t = tri_lds + n_max;
+    float *h_u = h_t + n_max;
+    float *h_v = h_u + n_max;
+    float *s_t = h_v + n_max;  // depths in sorted order
+    const int lane = threadIdx.x;
+    const int64_t ray = blockIdx.x;
+    const int64_t bi = ray / m;
+    const float *fp = faces + bi * n * 9;
+    const F3 o = {ray_start[ray * 3], ray_start[ray * 3 + 1], ray_start[ray * 3 + 2]};
+    const F3 d = {ray_dir[ray * 3], ray_dir[ray * 3 + 1], ray_dir[ray * 3 + 2]};
+    int cnt = 0;
+    for (int k0 = 0; k0 < n && cnt < n_max; k0 += kWave) {
+        const int k = k0 + lane;
+        float t = 0.0f, u = 0.0f, v = 0.0f;
+        const bool hit = k < n && ray_triangle(o, d, fp + (int64_t)k * 9, blur, t, u, v);
+        const uint64_t mask = __ballot(hit);
+        const int pos = cnt + lanes_below(mask);
+        if (hit && pos < n_max) {
+            h_k[pos] = k;
+            h_t[pos] = t;
+            h_u[pos] = u;
+            h_v[pos] = v;
+        }
+        cnt += __popcll(mask);
+    }
+    cnt = min(cnt, n_max);
+    __syncthreads();
+    int *idx = idx_out + ray * n_max;
+    float *depth = depth_out + ray * n_max * 3;
+    float *uv = uv_out + ray * n_max * 2;
+    // Order of the reference's insertion (intersect_gpu.cu:339-353, strict <):
+    // a hit goes before the first strictly deeper entry and the entry it
+    // displaces is carried on, which moves the head of every later run of
+    // equal depths to that run's end.  So a hit's slot is #(strictly
+    // shallower hits); within a run of equal depths v the order is a queue
+    // fed in face order — a hit of depth v appends, a shallower hit rotates
+    // the queue by one.  Distinct depths (the usual case) place themselves;
+    // the first hit of a tied run replays its queue, using the run's output
+    // slots as the ring.
+    for (int i = lane; i < cnt; i += kWave) {
+        const float ti = h_t[i];
+        int less = 0, eq_before = 0, eq = 0;
+        for (int j = 0; j < cnt; ++j) {
+            const float tj = h_t[j];
+            less += tj < ti;
+            eq += tj == ti;
+            eq_before += (tj == ti) && (j < i);
+        }
+        if (eq == 1) {
+            idx[less] = h_k[i];
+            depth[less * 3] = ti;
+            uv[less * 2] = h_u[i];
+            uv[less * 2 + 1] = h_v[i];
+            s_t[less] = ti;
+        } else if (eq_before == 0) {
+            int *ring = idx + less;  // hit numbers, later replaced by face ids
+            int head = 0, len = 0;
+            for (int j = i; j < cnt; ++j) {
+                const float tj = h_t[j];
+                if (tj == ti) {
+                    ring[(head + len) % eq] = j;
+                    ++len;
+                } else if (tj < ti && len > 0) {
+                    if (len < eq) ring[(head + len) % eq] = ring[head];
+                    head = (head + 1) % eq;
+                }
+            }
+            // slot q takes ring[(head + q) % eq]: park the hit numbers in the
+            // min-cage words (rewritten below) so the ring can be overwritten
+            for (int q = 0; q < eq; ++q) depth[(less + q) * 3 + 1] = __int_as_float(ring[(head + q) % eq]);
+            for (int q = 0; q < eq; ++q) {
+                const int hq = __float_as_int(depth[(less + q) * 3 + 1]);
+                idx[less + q] = h_k[hq];
+                depth[(less + q) * 3] = ti;
+                uv[(less + q) * 2] = h_u[hq];
+                uv[(less + q) * 2 + 1] = h_v[hq];
+                s_t[less + q] = ti;
+            }
+        }
+    }
+    __syncthreads();
+    // intersect_gpu.cu:354-368: half the gap to each neighbour, capped at cagesize
+    for (int l = lane; l < cnt; l += kWave) {
+        depth[l * 3 + 1] = (l == 0) ? -cagesize : -fminf(cagesize, 0.5f * (s_t[l] - s_t[l - 1]));
+        depth[l * 3 + 2] = (l == cnt - 1) ? cagesize : fminf(cagesize, 0.5f * (s_t[l + 1] - s_t[l]));
+    }
+    for (int l = cnt + lane; l < n_max; l += kWave) idx[l] = -1;
+}
+
+// sample_gpu.cu:13-124, one lane per ray, in place in the output rows like
+// the reference.  Two places where the reference leaves its own row are
+// pinned here: reads past the row (pts_idx[H + umin - 1] at umin = 0, and
+// umin past max_hits) read the neighbouring row of the flat array as the
+// reference does (-1 outside the array), and writes past max_steps — the
+// reference's write into the next ray's row, a race between lanes — are
+// dropped.  The merge is bounded by its event count so NaN depths cannot
+// spin it forever.
+__global__ __launch_bounds__(256) void k_uniform_sampling(int b, int num_rays, int max_hits, int max_steps,
+                                                          float step_size, const int *__restrict__ pts_idx,
+                                                          const float *__restrict__ min_depth,
+                                                          const float *__restrict__ max_depth,
+                                                          const float *__restrict__ uniform_noise,
+                                                          int *sampled_idx, float *sampled_depth,
+                                                          float *sampled_dists) {
+    const int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)b * num_rays;
+    if (ray >= total) return;
+    const int64_t n_idx = total * max_hits;
+    const int64_t H = ray * max_hits, K = ray * max_steps;
+    auto pidx = [&](int64_t at) { return (at >= 0 && at < n_idx) ? pts_idx[at] : -1; };
+    auto mind = [&](int64_t at) { return (at >= 0 && at < n_idx) ? min_depth[at] : 0.0f; };
+    int s = 0, ucur = 0, umin = 0, umax = 0;
+    float curr_depth = 0.0f;
+    const float d0 = min_depth[H];
+    for (int guard = 0; guard <= max_steps + 2 * max_hits + 2; ++guard) {
+        if (umax == max_hits || ucur == max_steps || pidx(H + umax) == -1) break;
+        const float last_min = (umin < max_hits) ? min_depth[H + umin] : 10000.0f;
+        const float last_max = (umax < max_hits) ? max_depth[H + umax] : 10000.0f;
+        curr_depth = d0 + ((float)ucur + uniform_noise[K + ucur]) * step_size;
+        float dep;
+        int id;
+        if (last_max <= curr_depth && last_max <= last_min) {
+            dep = last_max;
+            id = pidx(H + umax);
+            ++umax;
+        } else if (curr_depth <= last_min && curr_depth <= last_max) {
+            dep = curr_depth;
+            id = pidx(H + umin - 1);
+            ++ucur;
+        } else if (last_min <= curr_depth && last_min <= last_max) {
+            dep = last_min;
+            id = pidx(H + umin);
+            ++umin;
+        } else {
+            continue;
+        }
+        if (s < max_steps) {
+            sampled_depth[K + s] = dep;
+            sampled_idx[K + s] = id;
+        }
+        ++s;
+    }
+    int step = 0;
+    umin = 0;
+    umax = 0;
+    for (ucur = 0; ucur < max_steps - 1; ++ucur) {
+        if (sampled_idx[K + ucur + 1] == -1) break;
+        const float l_depth = sampled_depth[K + ucur];
+        const float r_depth = sampled_depth[K + ucur + 1];
+        const float mid = (l_depth + r_depth) * 0.5f;
+        const float dist = r_depth - l_depth;
+        sampled_depth[K + ucur] = mid;
+        sampled_dists[K + ucur] = dist;
+        if (umin < max_hits && mid >= mind(H + umin) && pidx(H + umin) > -1) ++umin;
+        if (umax < max_hits && mid >= max_depth[H + umax] && pidx(H + umax) > -1) ++umax;
+        if (umax == max_hits || pidx(H + umax) == -1) break;
+        if (umin - 1 == umax && dist > 0.0f) {
+            sampled_depth[K + step] = mid;
+            sampled_dists[K + step] = dist;
+            sampled_idx[K + step] = sampled_idx[K + ucur];
+            ++step;
+        }
+    }
+    for (int l = step; l < max_steps; ++l) sampled_idx[K + l] = -1;
+}
+
+}  // namespace
+}  // namespace psvo
+
+using namespace psvo;
+
+extern "C" int psvo_ball_intersect(void *stream, int b, int n, int m, float radius, int n_max,
+                                   const float *ray_start, const float *ray_dir, const float *points, int *idx,
+                                   float *min_depth, float *max_depth) {
+    PSVO_REQUIRE(b >= 0 && n >= 0 && m >= 0 && n_max > 0, "ball_intersect: bad sizes b=%d n=%d m=%d n_max=%d", b, n,
+                 m, n_max);
+    const int64_t total = (int64_t)b * m;
+    if (total == 0) return PSVO_OK;
+    psvo::launch(k_ball_intersect, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
+                 n, m, radius, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    return check_launch("ball_intersect");
+}
+
+extern "C" int psvo_aabb_intersect(void *stream, int b, int n, int m, float voxelsize, int n_max,
+                                   const float *ray_start, const float *ray_dir, const float *points, int *idx,
+                                   float *min_depth, float *max_depth) {
+    PSVO_REQUIRE(b >= 0 && n >= 0 && m >= 0 && n_max > 0, "aabb_intersect: bad sizes b=%d n=%d m=%d n_max=%d", b, n,
+                 m, n_max);
+    const int64_t total = (int64_t)b * m;
+    if (total == 0) return PSVO_OK;
+    psvo::launch(k_aabb_intersect, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
+                 n, m, voxelsize, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    return check_launch("aabb_intersect");
+}
+
+extern "C" int psvo_triangle_intersect(void *stream, int b, int n, int m, float cagesize, float blur, int n_max,
+                                       const float *ray_start, const float *ray_dir, const float *face_points,
+                                       int *idx, float *depth, float *uv) {
+    PSVO_REQUIRE(b >= 0 && n >= 0 && m >= 0 && n_max > 0, "triangle_intersect: bad sizes b=%d n=%d m=%d n_max=%d",
+                 b, n, m, n_max);
+    PSVO_REQUIRE(n_max <= kTriMaxHits, "triangle_intersect: n_max=%d exceeds %d", n_max, kTriMaxHits);
+    const int64_t total = (int64_t)b * m;
+    if (total == 0) return PSVO_OK;
+    PSVO_REQUIRE(total <= 0x7fffffff, "triangle_intersect: %lld rays exceed the grid", (long long)total);
+    psvo::launch(k_triangle_intersect, dim3((unsigned)total), dim3(kWave), (size_t)n_max * 5 * sizeof(float),
+                 as_stream(stream), b, n, m, cagesize, blur, n_max, ray_start, ray_dir, face_points, idx, depth, uv);
+    return check_launch("triangle_intersect");
+}
+
+extern "C" int psvo_uniform_ray_sampling(void *stream, int b, int num_rays, int max_hits, int max_steps,
+                                         float step_size, const int *pts_idx, const float *min_depth,
+                                         const float *max_depth, const float *uniform_noise, int *sampled_idx,
+                                         float *sampled_depth, float *sampled_dists) {
+    PSVO_REQUIRE(b >= 0 && num_rays >= 0 && max_hits > 0 && max_steps > 0,
+                 "uniform_ray_sampling: bad sizes b=%d num_rays=%d max_hits=%d max_steps=%d", b, num_rays, max_hits,
+                 max_steps);
+    const int64_t total = (int64_t)b * num_rays;
+    if (total == 0) return PSVO_OK;
+    psvo::launch(k_uniform_sampling, dim3(div_up(total, 256)), dim3(256), 0, as_stream(stream), b, num_rays,
+                 max_hits, max_steps, step_size, pts_idx, min_depth, max_depth, uniform_noise, sampled_idx,
+                 sampled_depth, sampled_dists);
+    return check_launch("uniform_ray_sampling");
+}

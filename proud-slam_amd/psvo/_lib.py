@@ -25,6 +25,10 @@ _SIGNATURES = {
     "psvo_version": (ctypes.c_char_p, []),
     "psvo_svo_intersect": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32] + [_vp] * 7),
     "psvo_inverse_cdf_sampling": (_i32, [_vp, _i32, _i32, _i32, _i32, _f32] + [_vp] * 9),
+    "psvo_ball_intersect": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32] + [_vp] * 6),
+    "psvo_aabb_intersect": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32] + [_vp] * 6),
+    "psvo_triangle_intersect": (_i32, [_vp, _i32, _i32, _i32, _f32, _f32, _i32] + [_vp] * 6),
+    "psvo_uniform_ray_sampling": (_i32, [_vp, _i32, _i32, _i32, _i32, _f32] + [_vp] * 7),
     "psvo_ray_intersect_sorted": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32] + [_vp] * 6),
     "psvo_hit_rank": (_i32, [_vp, _i64, _vp, _vp, _vp]),
     "psvo_sample_rays": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _u64, _vp, _vp, _vp, _vp,
@@ -142,6 +146,7 @@ _SIGNATURES = {
     "psvo_octree_count": (_i64, [_vp]),
     "psvo_octree_count_leaves": (_i64, [_vp]),
     "psvo_octree_export": (_i32, [_vp, _vp, _vp, _vp]),
+    "psvo_build_octree": (_i32, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp]),
     "psvo_octree_has_voxel": (_i32, [_vp, _i32, _i32, _i32]),
     "psvo_octree_try_insert": (_f64, [_vp, _vp, _i64]),
     "psvo_octree_leaf_voxels": (_i64, [_vp, _vp, _i64]),

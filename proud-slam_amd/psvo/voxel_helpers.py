@@ -1,6 +1,8 @@
-"""Drop-in mirror of the reference's src/variations/voxel_helpers.py render-path
-API (SparseVoxelOctreeRayIntersect, InverseCDFRaySampling, ray_intersect_vox,
-ray_sample), running on libpsvo's HIP kernels.
+"""Drop-in mirror of the reference's src/variations/voxel_helpers.py API on
+libpsvo's HIP kernels: the render path (SparseVoxelOctreeRayIntersect,
+InverseCDFRaySampling, ray_intersect_vox, ray_sample) and the helpers off it
+(Ball/AABB/TriangleRayIntersect, UniformRaySampling, discretize_points,
+build_easy_octree, ray_intersect_vox_AABB).
 
 Differences from the reference that do not change results:
   * no G-fold replication of the octree before the DFS kernel
@@ -103,6 +105,159 @@ class InverseCDFRaySampling(Function):
 
 
 inverse_cdf_sampling = InverseCDFRaySampling.apply
+
+
+class BallRayIntersect(Function):
+    """voxel_helpers.py:27-46: (radius, n_max, points [S,n,3], ray_start, ray_dir [S,N,3])
+    → (idx, min_depth, max_depth) [S, N, n_max], non-differentiable."""
+
+    @staticmethod
+    def forward(ctx, radius, n_max, points, ray_start, ray_dir):
+        idx, lo, hi = _ext.ball_intersect(ray_start.float().contiguous(), ray_dir.float().contiguous(),
+                                          points.float().contiguous(), radius, n_max)
+        lo, hi = lo.type_as(ray_start), hi.type_as(ray_start)
+        ctx.mark_non_differentiable(idx, lo, hi)
+        return idx, lo, hi
+
+    @staticmethod
+    def backward(ctx, a, b, c):
+        return None, None, None, None, None
+
+
+ball_ray_intersect = BallRayIntersect.apply
+
+
+class AABBRayIntersect(Function):
+    """voxel_helpers.py:49-101: (voxelsize, n_max, points [n,3], ray_start, ray_dir [S,N,3])
+    → (idx, min_depth, max_depth) [S, N, n_max].  One box list serves every
+    ray (the reference copies it up to 2048 times, :55-74); its debug prints
+    are not reproduced."""
+
+    @staticmethod
+    def forward(ctx, voxelsize, n_max, points, ray_start, ray_dir):
+        S, N = ray_start.shape[:2]
+        rs = ray_start.reshape(1, S * N, 3).float().contiguous()
+        rd = ray_dir.reshape(1, S * N, 3).float().contiguous()
+        idx, lo, hi = _ext.aabb_intersect(rs, rd, points.reshape(1, -1, 3).float().contiguous(), voxelsize, n_max)
+        idx, lo, hi = idx.reshape(S, N, -1), lo.reshape(S, N, -1).type_as(ray_start), hi.reshape(S, N, -1).type_as(ray_start)
+        ctx.mark_non_differentiable(idx, lo, hi)
+        return idx, lo, hi
+
+    @staticmethod
+    def backward(ctx, a, b, c):
+        return None, None, None, None, None
+
+
+aabb_ray_intersect = AABBRayIntersect.apply
+
+
+class TriangleRayIntersect(Function):
+    """voxel_helpers.py:169-217: (cagesize, blur_ratio, n_max, points, faces, ray_start, ray_dir)
+    → (idx [S,N,n_max], depth [S,N,n_max,3], uv [S,N,2·n_max])."""
+
+    @staticmethod
+    def forward(ctx, cagesize, blur_ratio, n_max, points, faces, ray_start, ray_dir):
+        S, N = ray_start.shape[:2]
+        rs = ray_start.reshape(1, S * N, 3).float().contiguous()
+        rd = ray_dir.reshape(1, S * N, 3).float().contiguous()
+        face_points = torch.nn.functional.embedding(faces.reshape(-1, 3), points.reshape(-1, 3))
+        fp = face_points.reshape(1, -1, 9).float().contiguous()
+        idx, depth, uv = _ext.triangle_intersect(rs, rd, fp, cagesize, blur_ratio, n_max)
+        idx = idx.reshape(S, N, -1)
+        depth = depth.type_as(ray_start).reshape(S, N, -1, 3)
+        uv = uv.type_as(ray_start).reshape(S, N, -1)
+        ctx.mark_non_differentiable(idx, depth, uv)
+        return idx, depth, uv
+
+    @staticmethod
+    def backward(ctx, a, b, c):
+        return None, None, None, None, None, None, None
+
+
+triangle_ray_intersect = TriangleRayIntersect.apply
+
+
+class UniformRaySampling(Function):
+    """voxel_helpers.py:220-285: [256, K', P] layout with first-rows padding,
+    max_steps = int(max_ray_length / step_size) + 2P, noise U[0,1) (0.5 when
+    deterministic), trimmed to the longest valid row."""
+
+    @staticmethod
+    def forward(ctx, pts_idx, min_depth, max_depth, step_size, max_ray_length, deterministic=False, noise=None):
+        G, N, P = 256, pts_idx.size(0), pts_idx.size(1)
+        H = int(math.ceil(N / G)) * G
+        if H > N:
+            pts_idx = torch.cat([pts_idx, pts_idx[:H - N]], 0)
+            min_depth = torch.cat([min_depth, min_depth[:H - N]], 0)
+            max_depth = torch.cat([max_depth, max_depth[:H - N]], 0)
+        pts_idx = pts_idx.reshape(G, -1, P)
+        min_depth = min_depth.reshape(G, -1, P)
+        max_depth = max_depth.reshape(G, -1, P)
+        max_steps = int(max_ray_length / step_size) + min_depth.size(-1) * 2
+        if noise is None:
+            noise = min_depth.new_zeros(*min_depth.size()[:-1], max_steps)
+            if deterministic:
+                noise += 0.5
+            else:
+                noise = noise.uniform_()
+        s_idx, s_dep, s_dis = _ext.uniform_ray_sampling(pts_idx.int().contiguous(), min_depth.float().contiguous(),
+                                                        max_depth.float().contiguous(),
+                                                        noise.float().reshape(G, -1, max_steps).contiguous(),
+                                                        step_size, max_steps)
+        s_dep, s_dis = s_dep.type_as(min_depth), s_dis.type_as(min_depth)
+        s_idx, s_dep, s_dis = s_idx.reshape(H, -1)[:N], s_dep.reshape(H, -1)[:N], s_dis.reshape(H, -1)[:N]
+        max_len = int(s_idx.ne(-1).sum(-1).max())
+        s_idx, s_dep, s_dis = s_idx[:, :max_len], s_dep[:, :max_len], s_dis[:, :max_len]
+        ctx.mark_non_differentiable(s_idx, s_dep, s_dis)
+        return s_idx, s_dep, s_dis
+
+    @staticmethod
+    def backward(ctx, a, b, c):
+        return None, None, None, None, None, None, None
+
+
+uniform_ray_sampling = UniformRaySampling.apply
+
+
+def discretize_points(voxel_points, voxel_size):
+    """voxel_helpers.py:481-491: integer voxel indices from the minimum, and the mean residual."""
+    minimal_voxel_point = voxel_points.min(dim=0, keepdim=True)[0]
+    voxel_indices = ((voxel_points - minimal_voxel_point) / voxel_size).round_().long()
+    residual = (voxel_points - voxel_indices.type_as(voxel_points) * voxel_size).mean(0, keepdim=True)
+    return voxel_indices, residual
+
+
+def build_easy_octree(points, half_voxel):
+    """voxel_helpers.py:494-501: EasyOctree (grid.build_octree) over the discretised points."""
+    coords, residual = discretize_points(points, half_voxel)
+    ranges = coords.max(0)[0] - coords.min(0)[0]
+    depths = torch.log2(ranges.max().float()).ceil_().long() - 1
+    center = (coords.max(0)[0] + coords.min(0)[0]) / 2
+    centers, children = _ext.build_octree(center, coords, int(depths))
+    centers = centers.float() * half_voxel + residual
+    return centers, children
+
+
+@torch.no_grad()
+def ray_intersect_vox_AABB(ray_start, ray_dir, flatten_centers, voxel_size, max_hits, max_distance=10.0):
+    """voxel_helpers.py:598-634 (brute-force boxes, used by test_aabb.py):
+    50 first hits in box order, sorted by t_in (stable here; the reference's
+    torch.sort leaves ties unspecified), max_distance trim."""
+    pts_idx, min_depth, max_depth = aabb_ray_intersect(voxel_size, N_MAX_HITS, flatten_centers, ray_start, ray_dir)
+    min_depth.masked_fill_(pts_idx.eq(-1), max_distance)
+    max_depth.masked_fill_(pts_idx.eq(-1), max_distance)
+    min_depth, sorted_idx = min_depth.sort(dim=-1, stable=True)
+    max_depth = max_depth.gather(-1, sorted_idx)
+    pts_idx = pts_idx.gather(-1, sorted_idx)
+    pts_idx[min_depth > max_distance] = -1
+    min_depth.masked_fill_(pts_idx.eq(-1), max_distance)
+    max_depth.masked_fill_(pts_idx.eq(-1), max_distance)
+    max_hits = torch.max(pts_idx.ne(-1).sum(-1))
+    min_depth = min_depth[..., :max_hits]
+    max_depth = max_depth[..., :max_hits]
+    pts_idx = pts_idx[..., :max_hits]
+    hits = pts_idx.ne(-1).any(-1)
+    return {"min_depth": min_depth, "max_depth": max_depth, "intersected_voxel_idx": pts_idx}, hits
 
 
 def _intersect_sorted(rays_o, rays_d, centres, structure, voxel_size, max_distance, step_size=1.0):

@@ -89,7 +89,7 @@ def test_grid_module_rejects_host_tensors():
         grid.svo_intersect(x, x, torch.zeros(1, 2, 3), torch.zeros(1, 2, 9, dtype=torch.int32), 0.2, 50)
     with pytest.raises(RuntimeError, match="contiguous"):
         grid.svo_intersect(x.transpose(1, 2), x, x, x, 0.2, 50)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="CUDA"):
         grid.ball_intersect(x, x, x, 0.1, 4)
 
 
