@@ -271,7 +271,7 @@ __global__ __launch_bounds__(kWave) void k_triangle_intersect(int b, int n, int 
 // reference's write into the next ray's row, a race between lanes — are
 // dropped.  The merge is bounded by its event count so NaN depths cannot
 // spin it forever.
-__global__ __launch_bounds__(256) void k_uniform_sampling(int b, int num_rays, int max_hits, int max_steps,
+__global__ __launch_bounds__(kWave) void k_uniform_sampling(int b, int num_rays, int max_hits, int max_steps,
                                                           float step_size, const int *__restrict__ pts_idx,
                                                           const float *__restrict__ min_depth,
                                                           const float *__restrict__ max_depth,
@@ -392,7 +392,8 @@ extern "C" int psvo_uniform_ray_sampling(void *stream, int b, int num_rays, int 
                  max_steps);
     const int64_t total = (int64_t)b * num_rays;
     if (total == 0) return PSVO_OK;
-    psvo::launch(k_uniform_sampling, dim3(div_up(total, 256)), dim3(256), 0, as_stream(stream), b, num_rays,
+    // one wave per workgroup: a few thousand serial rays spread over all CUs
+    psvo::launch(k_uniform_sampling, dim3(div_up(total, kWave)), dim3(kWave), 0, as_stream(stream), b, num_rays,
                  max_hits, max_steps, step_size, pts_idx, min_depth, max_depth, uniform_noise, sampled_idx,
                  sampled_depth, sampled_dists);
     return check_launch("uniform_ray_sampling");
