@@ -36,7 +36,8 @@
 namespace psvo {
 namespace {
 
-constexpr int kGaWaves = 4;           // rays (waves) per workgroup
+constexpr int kGaWaves = 8;           // rays (waves) per workgroup of the point kernels
+constexpr int kGaTile = 512;          // points per LDS tile (6 KB)
 constexpr int kTriMaxHits = 2048;     // LDS bound of the triangle kernel's hit list
 
 __device__ __forceinline__ int lanes_below(uint64_t m) {
@@ -66,25 +67,55 @@ __device__ __forceinline__ bool slab(const float o[3], const float inv[3], const
     return true;
 }
 
-// One wave per ray over [b, m] rays; `test(k, lo, hi)` decides primitive k.
-// Writes the first n_max hits in primitive order, -1 in the unused idx slots.
+// Point primitives (ball centres, box centres) for the rays of one
+// workgroup: kGaWaves rays, one per wave.  When the workgroup's rays share a
+// batch (the usual case: a batch holds many rays) the primitive list streams
+// once per workgroup through an LDS tile of kGaTile points instead of once
+// per wave — the waves' L2 traffic, which bounds the brute-force scan, drops
+// kGaWaves-fold.  `test(p, lo, hi)` decides the point at p[0..2].  Writes the
+// first n_max hits in point order and -1 in the unused idx slots.
 template <class Test>
-__device__ __forceinline__ void first_hits(int n, int n_max, const Test &test, int *idx, float *lo_out,
-                                           float *hi_out) {
+__device__ __forceinline__ void point_hits(int64_t ray, int64_t total, int m, int n, int n_max,
+                                           const float *__restrict__ points, const Test &test, int *idx_out,
+                                           float *lo_out, float *hi_out) {
+    __shared__ float tile[kGaTile * 3];
     const int lane = threadIdx.x % kWave;
+    const int64_t ray0 = (int64_t)blockIdx.x * kGaWaves;
+    const int64_t last = min(ray0 + kGaWaves, total) - 1;
+    const bool active = ray < total;
+    int *idx = idx_out + ray * n_max;
+    float *lo_o = lo_out + ray * n_max, *hi_o = hi_out + ray * n_max;
     int cnt = 0;
-    for (int k0 = 0; k0 < n && cnt < n_max; k0 += kWave) {
-        const int k = k0 + lane;
+    auto step = [&](const float *p, int k) {  // one wave-step over points k..k+63 (this lane: k)
         float lo = 0.0f, hi = 0.0f;
-        const bool hit = k < n && test(k, lo, hi);
+        const bool hit = k < n && test(p, lo, hi);
         const uint64_t mask = __ballot(hit);
         const int pos = cnt + lanes_below(mask);
         if (hit && pos < n_max) {
             idx[pos] = k;
-            lo_out[pos] = lo;
-            hi_out[pos] = hi;
+            lo_o[pos] = lo;
+            hi_o[pos] = hi;
         }
         cnt += __popcll(mask);
+    };
+    if (ray0 / m != last / m) {  // workgroup spans batches (block-uniform): direct loads
+        if (!active) return;
+        const float *pts = points + (ray / m) * n * 3;
+        for (int k0 = 0; k0 < n && cnt < n_max; k0 += kWave) {
+            const int k = min(k0 + lane, n - 1);
+            step(pts + (int64_t)k * 3, k0 + lane);
+        }
+    } else {
+        const float *pts = points + (ray0 / m) * n * 3;
+        for (int t0 = 0; t0 < n; t0 += kGaTile) {
+            if (!__syncthreads_or(active && cnt < n_max)) break;  // also orders the tile rewrite
+            const int span = min(kGaTile, n - t0) * 3;
+            for (int e = threadIdx.x; e < span; e += blockDim.x) tile[e] = pts[(int64_t)t0 * 3 + e];
+            __syncthreads();
+            if (active)
+                for (int c = 0; c < kGaTile && t0 + c < n && cnt < n_max; c += kWave) step(tile + (c + lane) * 3, t0 + c + lane);
+        }
+        if (!active) return;
     }
     for (int l = min(cnt, n_max) + lane; l < n_max; l += kWave) idx[l] = -1;
 }
@@ -94,17 +125,16 @@ __global__ __launch_bounds__(kGaWaves *kWave) void k_ball_intersect(int b, int n
                                                                      const float *__restrict__ ray_dir,
                                                                      const float *__restrict__ points, int *idx,
                                                                      float *min_depth, float *max_depth) {
+    const int64_t total = (int64_t)b * m;
     const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
-    if (ray >= (int64_t)b * m) return;
-    const int64_t bi = ray / m;
-    const float *pts = points + bi * n * 3;
-    const float o[3] = {ray_start[ray * 3], ray_start[ray * 3 + 1], ray_start[ray * 3 + 2]};
-    const float w[3] = {ray_dir[ray * 3], ray_dir[ray * 3 + 1], ray_dir[ray * 3 + 2]};
+    const int64_t r = min(ray, total - 1);
+    const float o[3] = {ray_start[r * 3], ray_start[r * 3 + 1], ray_start[r * 3 + 2]};
+    const float w[3] = {ray_dir[r * 3], ray_dir[r * 3 + 1], ray_dir[r * 3 + 2]};
     const float r2max = radius * radius;
-    auto test = [&](int k, float &lo, float &hi) {
-        const float x = pts[(int64_t)k * 3] - o[0];
-        const float y = pts[(int64_t)k * 3 + 1] - o[1];
-        const float z = pts[(int64_t)k * 3 + 2] - o[2];
+    auto test = [&](const float *p, float &lo, float &hi) {
+        const float x = p[0] - o[0];
+        const float y = p[1] - o[1];
+        const float z = p[2] - o[2];
         const float d2 = x * x + y * y + z * z;
         const float proj = x * w[0] + y * w[1] + z * w[2];
         const float d2_proj = proj * proj;
@@ -116,7 +146,7 @@ __global__ __launch_bounds__(kGaWaves *kWave) void k_ball_intersect(int b, int n
         hi = depth + blur;
         return true;
     };
-    first_hits(n, n_max, test, idx + ray * n_max, min_depth + ray * n_max, max_depth + ray * n_max);
+    point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
 }
 
 __global__ __launch_bounds__(kGaWaves *kWave) void k_aabb_intersect(int b, int n, int m, float voxelsize, int n_max,
@@ -124,21 +154,19 @@ __global__ __launch_bounds__(kGaWaves *kWave) void k_aabb_intersect(int b, int n
                                                                      const float *__restrict__ ray_dir,
                                                                      const float *__restrict__ points, int *idx,
                                                                      float *min_depth, float *max_depth) {
+    const int64_t total = (int64_t)b * m;
     const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
-    if (ray >= (int64_t)b * m) return;
-    const int64_t bi = ray / m;
-    const float *pts = points + bi * n * 3;
-    const float o[3] = {ray_start[ray * 3], ray_start[ray * 3 + 1], ray_start[ray * 3 + 2]};
+    const int64_t r = min(ray, total - 1);
+    const float o[3] = {ray_start[r * 3], ray_start[r * 3 + 1], ray_start[r * 3 + 2]};
     float inv[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, ray_dir[ray * 3 + a]);
+    for (int a = 0; a < 3; ++a) inv[a] = __fdiv_rn(1.0f, ray_dir[r * 3 + a]);
     const float half = voxelsize * 0.5f;
-    auto test = [&](int k, float &lo, float &hi) {
-        const float c[3] = {pts[(int64_t)k * 3], pts[(int64_t)k * 3 + 1], pts[(int64_t)k * 3 + 2]};
+    auto test = [&](const float *p, float &lo, float &hi) {
         // the reference keeps a box only when t_in > -1 (intersect_gpu.cu:176)
-        return slab(o, inv, c, half, lo, hi) && lo > -1.0f;
+        return slab(o, inv, p, half, lo, hi) && lo > -1.0f;
     };
-    first_hits(n, n_max, test, idx + ray * n_max, min_depth + ray * n_max, max_depth + ray * n_max);
+    point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
 }
 
 struct F3 {
