@@ -38,33 +38,36 @@ namespace {
 
 constexpr int kGaWaves = 8;           // rays (waves) per workgroup of the point kernels
 constexpr int kGaTile = 512;          // points per LDS tile (6 KB)
+constexpr int kGaSegs = 4;            // split mode: waves (point segments) per ray
+constexpr int kGaSplitHits = 128;     // split mode: per-segment hit list in LDS (n_max bound)
+constexpr int kGaSplitMinN = 1024;    // split mode: shortest point list worth splitting
 constexpr int kTriMaxHits = 2048;     // LDS bound of the triangle kernel's hit list
 
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// intersect_gpu.cu:75-140 — the same comparisons as svo_query.hip's ray_aabb
+// intersect_gpu.cu:75-140 — the comparisons of svo_query.hip's ray_aabb_nb:
+// the reference's early-exit tests in order, the verdict accumulated so the
+// wave runs one basic block per box instead of three divergent exits
 __device__ __forceinline__ bool slab(const float o[3], const float inv[3], const float c[3], float half,
                                      float &t_lo, float &t_hi) {
     float lo_all = 0.0f, hi_all = 100000.0f;
+    bool miss = false;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        float lo = (c[a] - half - o[a]) * inv[a];
-        float hi = (c[a] + half - o[a]) * inv[a];
-        if (hi < lo) {
-            const float tmp = lo;
-            lo = hi;
-            hi = tmp;
-        }
-        if (hi < lo_all || lo > hi_all) return false;
-        lo_all = (lo > lo_all) ? lo : lo_all;
-        hi_all = (hi < hi_all) ? hi : hi_all;
-        if (lo_all > hi_all) return false;
+        const float lo = (c[a] - half - o[a]) * inv[a];
+        const float hi = (c[a] + half - o[a]) * inv[a];
+        const bool sw = hi < lo;
+        const float l2 = sw ? hi : lo, h2 = sw ? lo : hi;
+        miss = miss | (h2 < lo_all) | (l2 > hi_all);
+        lo_all = (l2 > lo_all) ? l2 : lo_all;
+        hi_all = (h2 < hi_all) ? h2 : hi_all;
+        miss = miss | (lo_all > hi_all);
     }
     t_lo = lo_all;
     t_hi = hi_all;
-    return true;
+    return !miss;
 }
 
 // Point primitives (ball centres, box centres) for the rays of one
@@ -120,13 +123,70 @@ __device__ __forceinline__ void point_hits(int64_t ray, int64_t total, int m, in
     for (int l = min(cnt, n_max) + lane; l < n_max; l += kWave) idx[l] = -1;
 }
 
+// Split mode (n_max <= kGaSplitHits, long lists): each ray gets kGaSegs
+// waves, each scanning one contiguous segment of the point list into its
+// own LDS hit list (capped at n_max); the segment-0 wave then concatenates
+// the lists in segment order and truncates at n_max — the first n_max hits
+// in point order, as the serial loop keeps.  A few thousand rays are 4 waves
+// per SIMD in the one-wave-per-ray layout; this gives each SIMD kGaSegs×
+// as many waves to hide the per-step latency with.
+template <class Test>
+__device__ __forceinline__ void point_hits_split(int64_t ray, int64_t total, int m, int n, int n_max,
+                                                 const float *__restrict__ points, const Test &test,
+                                                 int *idx_out, float *lo_out, float *hi_out) {
+    __shared__ int s_cnt[kGaWaves];
+    __shared__ int s_k[kGaWaves * kGaSplitHits];
+    __shared__ float s_lo[kGaWaves * kGaSplitHits], s_hi[kGaWaves * kGaSplitHits];
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int seg = wave % kGaSegs, grp = wave - seg;
+    const bool active = ray < total;
+    if (active) {
+        const int seg_len = ((n + kGaSegs - 1) / kGaSegs + kWave - 1) / kWave * kWave;
+        const int k_begin = seg * seg_len, k_end = min(n, k_begin + seg_len);
+        const float *pts = points + (ray / m) * n * 3;
+        int cnt = 0;
+        for (int k0 = k_begin; k0 < k_end && cnt < n_max; k0 += kWave) {
+            const int k = k0 + lane;
+            float lo = 0.0f, hi = 0.0f;
+            const bool hit = k < k_end && test(pts + (int64_t)k * 3, lo, hi);
+            const uint64_t mask = __ballot(hit);
+            const int pos = cnt + lanes_below(mask);
+            if (hit && pos < n_max) {
+                s_k[wave * kGaSplitHits + pos] = k;
+                s_lo[wave * kGaSplitHits + pos] = lo;
+                s_hi[wave * kGaSplitHits + pos] = hi;
+            }
+            cnt += __popcll(mask);
+        }
+        if (lane == 0) s_cnt[wave] = min(cnt, n_max);
+    }
+    __syncthreads();
+    if (!active || seg != 0) return;
+    int *idx = idx_out + ray * n_max;
+    float *lo_o = lo_out + ray * n_max, *hi_o = hi_out + ray * n_max;
+    int base = 0;
+    for (int sgi = 0; sgi < kGaSegs && base < n_max; ++sgi) {
+        const int src = (grp + sgi) * kGaSplitHits;
+        const int take = min(s_cnt[grp + sgi], n_max - base);
+        for (int q = lane; q < take; q += kWave) {
+            idx[base + q] = s_k[src + q];
+            lo_o[base + q] = s_lo[src + q];
+            hi_o[base + q] = s_hi[src + q];
+        }
+        base += take;
+    }
+    for (int l = base + lane; l < n_max; l += kWave) idx[l] = -1;
+}
+
+template <bool SPLIT>
 __global__ __launch_bounds__(kGaWaves *kWave) void k_ball_intersect(int b, int n, int m, float radius, int n_max,
                                                                      const float *__restrict__ ray_start,
                                                                      const float *__restrict__ ray_dir,
                                                                      const float *__restrict__ points, int *idx,
                                                                      float *min_depth, float *max_depth) {
     const int64_t total = (int64_t)b * m;
-    const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
+    const int64_t ray = SPLIT ? (int64_t)blockIdx.x * (kGaWaves / kGaSegs) + threadIdx.x / (kWave * kGaSegs)
+                              : (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
     const int64_t r = min(ray, total - 1);
     const float o[3] = {ray_start[r * 3], ray_start[r * 3 + 1], ray_start[r * 3 + 2]};
     const float w[3] = {ray_dir[r * 3], ray_dir[r * 3 + 1], ray_dir[r * 3 + 2]};
@@ -146,16 +206,21 @@ __global__ __launch_bounds__(kGaWaves *kWave) void k_ball_intersect(int b, int n
         hi = depth + blur;
         return true;
     };
-    point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
+    if constexpr (SPLIT)
+        point_hits_split(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
+    else
+        point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(kGaWaves *kWave) void k_aabb_intersect(int b, int n, int m, float voxelsize, int n_max,
                                                                      const float *__restrict__ ray_start,
                                                                      const float *__restrict__ ray_dir,
                                                                      const float *__restrict__ points, int *idx,
                                                                      float *min_depth, float *max_depth) {
     const int64_t total = (int64_t)b * m;
-    const int64_t ray = (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
+    const int64_t ray = SPLIT ? (int64_t)blockIdx.x * (kGaWaves / kGaSegs) + threadIdx.x / (kWave * kGaSegs)
+                              : (int64_t)blockIdx.x * kGaWaves + threadIdx.x / kWave;
     const int64_t r = min(ray, total - 1);
     const float o[3] = {ray_start[r * 3], ray_start[r * 3 + 1], ray_start[r * 3 + 2]};
     float inv[3];
@@ -166,7 +231,10 @@ __global__ __launch_bounds__(kGaWaves *kWave) void k_aabb_intersect(int b, int n
         // the reference keeps a box only when t_in > -1 (intersect_gpu.cu:176)
         return slab(o, inv, p, half, lo, hi) && lo > -1.0f;
     };
-    point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
+    if constexpr (SPLIT)
+        point_hits_split(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
+    else
+        point_hits(ray, total, m, n, n_max, points, test, idx, min_depth, max_depth);
 }
 
 struct F3 {
@@ -380,8 +448,12 @@ extern "C" int psvo_ball_intersect(void *stream, int b, int n, int m, float radi
                  m, n_max);
     const int64_t total = (int64_t)b * m;
     if (total == 0) return PSVO_OK;
-    psvo::launch(k_ball_intersect, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
-                 n, m, radius, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    if (n_max <= kGaSplitHits && n >= kGaSplitMinN)
+        psvo::launch(k_ball_intersect<true>, dim3(div_up(total, kGaWaves / kGaSegs)), dim3(kGaWaves * kWave), 0,
+                     as_stream(stream), b, n, m, radius, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    else
+        psvo::launch(k_ball_intersect<false>, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
+                     n, m, radius, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
     return check_launch("ball_intersect");
 }
 
@@ -392,8 +464,12 @@ extern "C" int psvo_aabb_intersect(void *stream, int b, int n, int m, float voxe
                  m, n_max);
     const int64_t total = (int64_t)b * m;
     if (total == 0) return PSVO_OK;
-    psvo::launch(k_aabb_intersect, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
-                 n, m, voxelsize, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    if (n_max <= kGaSplitHits && n >= kGaSplitMinN)
+        psvo::launch(k_aabb_intersect<true>, dim3(div_up(total, kGaWaves / kGaSegs)), dim3(kGaWaves * kWave), 0,
+                     as_stream(stream), b, n, m, voxelsize, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
+    else
+        psvo::launch(k_aabb_intersect<false>, dim3(div_up(total, kGaWaves)), dim3(kGaWaves * kWave), 0, as_stream(stream), b,
+                     n, m, voxelsize, n_max, ray_start, ray_dir, points, idx, min_depth, max_depth);
     return check_launch("aabb_intersect");
 }
 

@@ -34,7 +34,10 @@ def _gpu(*arrays):
     (1, 1, 1, 1, 0.5, 0),
     (2, 301, 1000, 10, 0.4, 1),     # n_max saturates: first hits in point order only
     (3, 130, 333, 100, 0.25, 2),    # n not a multiple of the wave
-    (1, 64, 5000, 50, 0.1, 3),
+    (1, 64, 5000, 50, 0.1, 3),      # >= 1024 points, n_max <= 128: four segment waves per ray
+    (2, 150, 3000, 10, 0.5, 5),     # split mode, saturating inside the first segments
+    (1, 97, 4097, 128, 0.3, 6),     # split mode at its n_max bound, ragged last segment
+    (1, 50, 2000, 129, 0.3, 7),     # n_max past the split bound: one wave per ray
     (2, 17, 0, 4, 0.2, 4),          # no primitives: every idx -1
 ])
 def test_point_intersect_matches_oracle(fn, b, m, n, n_max, size, seed):
