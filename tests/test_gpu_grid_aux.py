@@ -111,6 +111,7 @@ def _boxes(rng, b, k, p, frac_hit=0.8):
     (4, 50, 6, 0.05, 212, 1),     # int(10 / 0.05) + 2P: the reference's sizing
     (2, 77, 12, 0.02, 524, 2),
     (2, 40, 8, 0.05, 30, 3),      # too few steps: the merge stops at max_steps
+    (1, 37, 4, 0.01, 1000, 4),    # rows too long for the LDS staging: merged in place in HBM
 ])
 def test_uniform_sampling_matches_oracle(b, k, p, step, max_steps, seed):
     import grid
