@@ -1136,8 +1136,9 @@ int ensure_aux(psvo_engine *e) {
         return set_error(PSVO_E_LAUNCH, "engine: aux stream creation failed");
     // stream-ordering events on one device: no system-scope fence (its L2
     // write-back, ≈ dirty bytes ÷ 6 TB/s, would sit between the kernels)
-    for (hipEvent_t *ev : evs)
-        if (hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+    for (hipEvent_t *ev : evs)  // (dfeat_ready may be bound to a dispatch as its stop event, like q.p1)
+        if (hipEventCreateWithFlags(ev, (ev == &e->dfeat_ready ? 0 : hipEventDisableTiming) |
+                                            hipEventDisableSystemFence) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "engine: event creation failed");
     return PSVO_OK;
 }

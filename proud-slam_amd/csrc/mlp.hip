@@ -2254,9 +2254,29 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
         const int grid = bwd3_grid(m);
         dw_grid_uniform(grid, &g, &slab_floats);
         float *slabs = workspace + m * 3;
+        // dfeat_ready marks the last kernel's completion through its dispatch
+        // (psvo::launch's stop event): no marker packet between the decoder's
+        // backward and the per-ray sums that follow it on st
+        static const bool bind_env = [] {
+            const char *v = getenv("PSVO_BIND_DFEAT");
+            return !(v && v[0] == '0');
+        }();
+        const bool trunk_last = tb && m > 0;
+        bool bound = false;
+        auto bind = [&](bool last) {
+            if (last && bind_env && dfeat_ready) psvo::g_stop_event = dfeat_ready;
+        };
+        auto taken = [&](bool last) {
+            if (last && bind_env && dfeat_ready) {
+                bound = psvo::g_stop_event == nullptr;
+                psvo::g_stop_event = nullptr;
+            }
+        };
         if (m > 0) {
+            bind(!trunk_last);
             psvo::launch(k_mlp_bwd3<true>, dim3(grid), dim3(kF2Threads), kLdsBwd3, st, m, images, src, g, slabs,
                          ip ? *ip : InterpFuse{}, m_dev);
+            taken(!trunk_last);
             const int rc = check_launch("mlp_bwd3");
             if (rc) return rc;
         } else if (hipMemsetAsync(slabs, 0, (size_t)slab_floats * sizeof(float), st) != hipSuccess) {
@@ -2273,13 +2293,15 @@ int mlp_bwd(void *stream, int64_t m, int width, const float *feat, const float *
             }
             slabs_b = slabs + slab_floats;
             PSVO_REQUIRE(!tb->h2 || tb->src, "mlp_bwd: the trunk's h2 rows need their source index");
+            bind(true);
             psvo::launch(tb->h2 ? k_mlp_trunk_fb<true> : k_mlp_trunk_fb<false>, dim3(grid), dim3(kF2Threads), kLdsTrunk,
                          st, tb->m_dev, images, tb->g_sdf, tb->feat, g, slabs_b, tb->ip ? *tb->ip : InterpFuse{},
                          tb->h2, tb->src);
+            taken(true);
             const int rc = check_launch("mlp_trunk_fb");
             if (rc) return rc;
         }
-        if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
+        if (dfeat_ready && !bound && hipEventRecord(dfeat_ready, st) != hipSuccess)
             return set_error(PSVO_E_LAUNCH, "mlp_bwd: event record failed");
         if (reduce_stream && reduce_stream != st) {  // the slab sum beside the caller's next work on st
             PSVO_REQUIRE(dfeat_ready != nullptr, "mlp_bwd: a separate reduce stream needs the dfeat_ready event");

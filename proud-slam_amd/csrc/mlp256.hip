@@ -1155,6 +1155,7 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
     } else {
         ws += n16 * 16 * (256 + 256 + 144 + 256 + 16);
     }
+    bool bound = false;
     if (m > 0) {
         const int lds = (kRing * kChunkFloats + kCWaves * 512) * 4;  // ring + per-wave scatter staging
         static bool attr = false;
@@ -1163,12 +1164,21 @@ int dec256_bwd(hipStream_t st, int64_t m, const float *feat, const float *images
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             attr = true;
         }
+        // dfeat_ready through the dispatch's stop event (no marker packet
+        // between the backward and the weight-gradient kernel on st)
+        static const bool bind_env = [] {
+            const char *v = getenv("PSVO_BIND_DFEAT");
+            return !(v && v[0] == '0');
+        }();
+        if (bind_env && dfeat_ready) psvo::g_stop_event = dfeat_ready;
         psvo::launch(k_dec256_bwd, dim3(grid_for(n_tiles)), dim3(kCThreads), lds, st, m, n_tiles, images, rgb,
                      g_sdf, g_rgb, a, d, dfeat, ip ? *ip : InterpFuse{}, m_dev);
+        bound = bind_env && dfeat_ready && psvo::g_stop_event == nullptr;
+        psvo::g_stop_event = nullptr;
         const int rc = check_launch("dec256_bwd");
         if (rc) return rc;
     }
-    if (dfeat_ready && hipEventRecord(dfeat_ready, st) != hipSuccess)
+    if (dfeat_ready && !bound && hipEventRecord(dfeat_ready, st) != hipSuccess)
         return set_error(PSVO_E_LAUNCH, "dec256_bwd: event record failed");
     if (!want_w) return PSVO_OK;
     DwPlan pl;
